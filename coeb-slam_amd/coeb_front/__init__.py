@@ -1,0 +1,344 @@
+"""Python mirror of the reference's front-end interface over the C-ABI (include/coeb_front.h).
+
+  ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+      include/ORBextractor.h:50-51; __call__ mirrors operator() (ORBextractor.h:73-75,
+      src/ORBextractor.cc:1088-1342) and returns (keypoints, descriptors) instead of filling
+      output arguments.  Accessors GetLevels/GetScaleFactor/... as ORBextractor.h:77-99.
+  ORBmatcher(nnratio=0.6, checkOri=True).SearchByProjection(CurrentFrame, LastFrame, th, bMono)
+      include/ORBmatcher.h:41,52, src/ORBmatcher.cc:1329-1471; mutates
+      CurrentFrame.mvpMapPoints (slot index of the LastFrame MapPoint, -1 = NULL) and returns
+      nmatches.
+  ORBmatcher.DescriptorDistance(a, b)  src/ORBmatcher.cc:1648-1664
+
+All compute runs in libcoeb_front.so (hand-written gfx950 HIP kernels).  There is no CPU
+fallback: importing works anywhere, but constructing an extractor without the built library
+or without a gfx950 device raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libcoeb_front.so")
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 28
+MAX_LEVELS = 16
+
+# exported symbols of include/coeb_front.h (checked by tests/test_capi_symbols.py)
+ABI_SYMBOLS = [
+    "coeb_create", "coeb_destroy", "coeb_last_error", "coeb_orb_tables_get", "coeb_max_keypoints",
+    "coeb_extract", "coeb_extract_batch_device", "coeb_batch_results", "coeb_match_batch_device",
+    "coeb_batch_match_results", "coeb_match_lastframe", "coeb_blur_flags", "coeb_stereo_from_rgbd",
+    "coeb_rgbd_preprocess", "coeb_descriptor_distance", "coeb_profile_enable", "coeb_profile_read",
+    "coeb_profile_reset", "coeb_synchronize", "coeb_device_count", "coeb_debug_read",
+]
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+class OrbTables(C.Structure):
+    _fields_ = [("nlevels", C.c_int32), ("scale_factor", C.c_float),
+                ("scale", C.c_float * MAX_LEVELS), ("inv_scale", C.c_float * MAX_LEVELS),
+                ("sigma2", C.c_float * MAX_LEVELS), ("inv_sigma2", C.c_float * MAX_LEVELS),
+                ("features_per_level", C.c_int32 * MAX_LEVELS), ("umax", C.c_int32 * 16)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
+                ("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float)]
+
+
+class LastFrameC(C.Structure):
+    _fields_ = [("n", C.c_int32), ("has_mappoint", C.c_void_p), ("outlier", C.c_void_p), ("world_pos", C.c_void_p),
+                ("mp_descriptor", C.c_void_p), ("mp_observations", C.c_void_p), ("keys_un", C.c_void_p)]
+
+
+class CurFrameC(C.Structure):
+    _fields_ = [("n", C.c_int32), ("keys_un", C.c_void_p), ("descriptors", C.c_void_p), ("u_right", C.c_void_p)]
+
+
+class CoebError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libcoeb_front.so (in-tree build); raise if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise CoebError("libcoeb_front.so not built (run __graft_entry__.build() or make -C coeb-slam_amd/csrc)")
+        L = C.CDLL(LIB_PATH)
+        L.coeb_create.restype = C.c_void_p
+        L.coeb_create.argtypes = [C.POINTER(OrbParams), C.c_int, C.c_int, C.c_int, C.c_int]
+        L.coeb_destroy.argtypes = [C.c_void_p]
+        L.coeb_last_error.restype = C.c_char_p
+        L.coeb_last_error.argtypes = [C.c_void_p]
+        L.coeb_orb_tables_get.argtypes = [C.c_void_p, C.POINTER(OrbTables)]
+        L.coeb_max_keypoints.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.coeb_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_int,
+                                   C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                   C.POINTER(C.c_int)]
+        L.coeb_extract_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.coeb_batch_results.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                         C.POINTER(C.c_void_p), C.POINTER(C.c_int)]
+        L.coeb_match_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(Camera),
+                                              C.c_void_p, C.c_float, C.c_int32]
+        L.coeb_batch_match_results.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.coeb_match_lastframe.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(CurFrameC),
+                                           C.POINTER(LastFrameC), C.c_void_p, C.c_void_p, C.c_float, C.c_int,
+                                           C.c_int, C.c_void_p, C.POINTER(C.c_int)]
+        L.coeb_blur_flags.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_int,
+                                      C.c_void_p]
+        L.coeb_stereo_from_rgbd.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                            C.c_size_t, C.c_float, C.c_void_p, C.c_void_p]
+        L.coeb_rgbd_preprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_size_t,
+                                           C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.coeb_descriptor_distance.argtypes = [C.c_void_p, C.c_void_p]
+        L.coeb_profile_enable.argtypes = [C.c_void_p, C.c_int]
+        L.coeb_profile_reset.argtypes = [C.c_void_p]
+        L.coeb_profile_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                        C.POINTER(C.c_int)]
+        L.coeb_synchronize.argtypes = [C.c_void_p]
+        L.coeb_debug_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_size_t,
+                                      C.POINTER(C.c_size_t)]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+class Context:
+    """One coeb_ctx: device buffers + HIP stream of one host thread (not reentrant)."""
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, device=0,
+                 max_width=1280, max_height=960, max_batch=1):
+        L = lib()
+        self.params = OrbParams(nfeatures, scale_factor, nlevels, ini_th, min_th)
+        h = L.coeb_create(C.byref(self.params), device, max_width, max_height, max_batch)
+        if not h:
+            raise CoebError(L.coeb_last_error(None).decode())
+        self.h = C.c_void_p(h)
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().coeb_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc):
+        if rc != 0:
+            raise CoebError("coeb rc=%d: %s" % (rc, lib().coeb_last_error(self.h).decode()))
+        return rc
+
+    def tables(self):
+        t = OrbTables()
+        self.check(lib().coeb_orb_tables_get(self.h, C.byref(t)))
+        return t
+
+    def max_keypoints(self, w, h):
+        r = lib().coeb_max_keypoints(self.h, w, h)
+        if r < 0:
+            self.check(r)
+        return r
+
+    # ---- single frame (host buffers) ----
+    def extract(self, gray, boxes=None, tm=None, blur=None):
+        gray = np.ascontiguousarray(gray, np.uint8)
+        if gray.size == 0:
+            return np.zeros(0, KEYPOINT_DTYPE), None
+        h, w = gray.shape
+        boxes = np.zeros((0, 4), np.float32) if boxes is None else np.ascontiguousarray(boxes, np.float32)
+        tm = np.zeros((0, 2), np.float32) if tm is None else np.ascontiguousarray(tm, np.float32)
+        blur = np.zeros(0, np.int32) if blur is None else np.ascontiguousarray(blur, np.int32)
+        cap = self.max_keypoints(w, h)
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int()
+        self.check(lib().coeb_extract(self.h, _p(gray), w, h, w, _p(boxes) if len(boxes) else None, len(boxes),
+                                      _p(tm) if len(tm) else None, len(tm), _p(blur) if len(blur) else None,
+                                      len(blur), _p(kps), _p(desc), cap, C.byref(n)))
+        n = n.value
+        return kps[:n].copy(), (desc[:n].copy() if n else None)
+
+    # ---- device-resident batch ----
+    def extract_batch_device(self, d_gray_ptr, nframes, w, h, boxes=None, box_off=None, tm=None, tm_off=None,
+                             blur=None):
+        args = []
+        keep = []
+        for a, dt in ((boxes, np.float32), (box_off, np.int32), (tm, np.float32), (tm_off, np.int32),
+                      (blur, np.int32)):
+            if a is None:
+                args.append(None)
+            else:
+                a = np.ascontiguousarray(a, dt)
+                keep.append(a)
+                args.append(_p(a))
+        self.check(lib().coeb_extract_batch_device(self.h, C.c_void_p(d_gray_ptr), nframes, w, h, *args))
+
+    def batch_results(self):
+        k, d, n = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        cap = C.c_int()
+        self.check(lib().coeb_batch_results(self.h, C.byref(k), C.byref(d), C.byref(n), C.byref(cap)))
+        return k.value, d.value, n.value, cap.value
+
+    def match_batch_device(self, d_depth_ptr, nframes, w, h, cam, Tcw, th=15.0, nobs=2):
+        Tcw = np.ascontiguousarray(Tcw, np.float32)
+        self.check(lib().coeb_match_batch_device(self.h, C.c_void_p(d_depth_ptr), nframes, w, h, C.byref(cam),
+                                                 _p(Tcw), th, nobs))
+
+    def batch_match_results(self):
+        m, n = C.c_void_p(), C.c_void_p()
+        self.check(lib().coeb_batch_match_results(self.h, C.byref(m), C.byref(n)))
+        return m.value, n.value
+
+    def synchronize(self):
+        self.check(lib().coeb_synchronize(self.h))
+
+    def debug_read(self, what, f=0):
+        size = C.c_size_t()
+        self.check(lib().coeb_debug_read(self.h, what.encode(), f, None, 0, C.byref(size)))
+        buf = np.zeros(size.value, np.uint8)
+        self.check(lib().coeb_debug_read(self.h, what.encode(), f, _p(buf), size.value, C.byref(size)))
+        return buf
+
+    # ---- profiling (HIP events on the context stream) ----
+    def profile(self, enable=True):
+        self.check(lib().coeb_profile_enable(self.h, int(enable)))
+
+    def profile_reset(self):
+        self.check(lib().coeb_profile_reset(self.h))
+
+    def profile_read(self):
+        names = C.create_string_buffer(4096)
+        ms = np.zeros(64, np.float64)
+        cnt = np.zeros(64, np.int64)
+        nk = C.c_int()
+        self.check(lib().coeb_profile_read(self.h, names, 4096, _p(ms), _p(cnt), 64, C.byref(nk)))
+        nm = names.value.decode().split(",") if nk.value else []
+        return {nm[i]: (float(ms[i]), int(cnt[i])) for i in range(nk.value)}
+
+
+class ORBextractor:
+    """Drop-in mirror of ORB_SLAM2::ORBextractor (include/ORBextractor.h:44-128)."""
+
+    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device=0, max_width=1280,
+                 max_height=960):
+        self.ctx = Context(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device, max_width, max_height, 1)
+        t = self.ctx.tables()
+        self.nlevels = nlevels
+        self.scaleFactor = scaleFactor
+        self.mvScaleFactor = list(t.scale[:nlevels])
+        self.mvInvScaleFactor = list(t.inv_scale[:nlevels])
+        self.mvLevelSigma2 = list(t.sigma2[:nlevels])
+        self.mvInvLevelSigma2 = list(t.inv_sigma2[:nlevels])
+        self.mnFeaturesPerLevel = list(t.features_per_level[:nlevels])
+        self.umax = list(t.umax)
+
+    def __call__(self, image, mask=None, img=None, imD=None, box=None, T_M=None, mask_result=None, blur_flag=None):
+        """operator()(image, mask, img, imD, keypoints, descriptors, box, T_M, mask_result, blur_flag).
+        mask, img, imD and mask_result are accepted and ignored, as in the reference."""
+        image = np.asarray(image)
+        if image.size == 0:
+            return np.zeros(0, KEYPOINT_DTYPE), None
+        assert image.dtype == np.uint8 and image.ndim == 2, "image.type() == CV_8UC1 (ORBextractor.cc:1099)"
+        boxes = None if not box else np.asarray(box, np.float32).reshape(-1, 4)
+        tm = None if T_M is None or len(T_M) == 0 else np.asarray(T_M, np.float32).reshape(-1, 2)
+        bf = None if blur_flag is None or len(blur_flag) == 0 else np.asarray(blur_flag, np.int32)
+        return self.ctx.extract(image, boxes, tm, bf)
+
+    def GetLevels(self):
+        return self.nlevels
+
+    def GetScaleFactor(self):
+        return self.scaleFactor
+
+    def GetScaleFactors(self):
+        return list(self.mvScaleFactor)
+
+    def GetInverseScaleFactors(self):
+        return list(self.mvInvScaleFactor)
+
+    def GetScaleSigmaSquares(self):
+        return list(self.mvLevelSigma2)
+
+    def GetInverseScaleSigmaSquares(self):
+        return list(self.mvInvLevelSigma2)
+
+
+class Frame:
+    """The Frame fields SearchByProjection reads (src/Frame.cc / include/Frame.h)."""
+
+    def __init__(self, keys_un, descriptors, u_right=None, Tcw=None, map_points=None, outlier=None):
+        self.mvKeysUn = np.ascontiguousarray(keys_un)
+        self.N = len(self.mvKeysUn)
+        self.mDescriptors = np.ascontiguousarray(descriptors, np.uint8).reshape(self.N, 32) if self.N else \
+            np.zeros((0, 32), np.uint8)
+        self.mvuRight = np.full(self.N, -1, np.float32) if u_right is None else np.ascontiguousarray(u_right, np.float32)
+        self.mTcw = np.eye(4, dtype=np.float32) if Tcw is None else np.ascontiguousarray(Tcw, np.float32)
+        # map_points: dict(world_pos [N,3] f32, descriptor [N,32] u8, observations [N] i32, valid [N] u8)
+        self.map_points = map_points
+        self.mvbOutlier = np.zeros(self.N, np.uint8) if outlier is None else np.ascontiguousarray(outlier, np.uint8)
+        self.mvpMapPoints = np.full(self.N, -1, np.int32)
+
+
+class ORBmatcher:
+    """Mirror of ORB_SLAM2::ORBmatcher for the tracking projection search."""
+    TH_HIGH = 100
+    TH_LOW = 50
+    HISTO_LENGTH = 30
+
+    def __init__(self, nnratio=0.6, checkOri=True, ctx=None):
+        self.mfNNratio = nnratio
+        self.mbCheckOrientation = checkOri
+        self.ctx = ctx
+
+    @staticmethod
+    def DescriptorDistance(a, b):
+        a = np.ascontiguousarray(a, np.uint8)
+        b = np.ascontiguousarray(b, np.uint8)
+        return lib().coeb_descriptor_distance(_p(a), _p(b))
+
+    def SearchByProjection(self, CurrentFrame, LastFrame, th, bMono, camera):
+        if self.ctx is None:
+            self.ctx = Context()
+        mp = LastFrame.map_points
+        n = LastFrame.N
+        lf_arrays = dict(has=np.ascontiguousarray(mp["valid"], np.uint8),
+                         out=np.ascontiguousarray(LastFrame.mvbOutlier, np.uint8),
+                         xw=np.ascontiguousarray(mp["world_pos"], np.float32),
+                         desc=np.ascontiguousarray(mp["descriptor"], np.uint8),
+                         nobs=np.ascontiguousarray(mp["observations"], np.int32),
+                         keys=np.ascontiguousarray(LastFrame.mvKeysUn))
+        lf = LastFrameC(n, *[C.c_void_p(lf_arrays[k].ctypes.data) for k in ("has", "out", "xw", "desc", "nobs", "keys")])
+        cf = CurFrameC(CurrentFrame.N, C.c_void_p(CurrentFrame.mvKeysUn.ctypes.data),
+                       C.c_void_p(CurrentFrame.mDescriptors.ctypes.data), C.c_void_p(CurrentFrame.mvuRight.ctypes.data))
+        out = np.full(max(CurrentFrame.N, 1), -1, np.int32)
+        nm = C.c_int()
+        self.ctx.check(lib().coeb_match_lastframe(self.ctx.h, C.byref(camera), C.byref(cf), C.byref(lf),
+                                                  _p(CurrentFrame.mTcw), _p(LastFrame.mTcw), th, int(bMono),
+                                                  int(self.mbCheckOrientation), _p(out), C.byref(nm)))
+        CurrentFrame.mvpMapPoints = out[:CurrentFrame.N].copy()
+        return nm.value
+
+
+def make_camera(fx, fy, cx, cy, bf, w, h):
+    """Camera + Frame::ComputeImageBounds for an undistorted image (src/Frame.cc:635-641)."""
+    return Camera(fx, fy, cx, cy, bf, 0.0, float(w), 0.0, float(h))

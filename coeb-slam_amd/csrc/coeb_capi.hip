@@ -1,0 +1,918 @@
+// coeb_capi.hip -- context, host-side geometry plan and the C-ABI of include/coeb_front.h.
+//
+// Host work here is O(levels + cells) per image size (cached), plus the per-call argument
+// marshalling.  All per-pixel / per-keypoint work runs in the kernels of coeb_extract.hip and
+// coeb_match.hip.  There is no CPU fallback: without a usable gfx950 device coeb_create fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/coeb_front.h"
+#include "coeb_internal.hpp"
+
+static const int8_t kPattern[1024] = {
+#include "../../data/orb_bit_pattern_31.inc"
+};
+
+static std::string g_last_error;
+
+namespace {
+
+enum { PATCH_SIZE = 31, HALF_PATCH_SIZE = 15, EDGE_THRESHOLD = 19 };
+constexpr int kRoiMax = 64;
+constexpr int kOctLMax = 1024;
+constexpr int kCurMax = 4096;
+
+inline int cv_round(float v) { return (int)lrintf(v); }
+inline int cv_round_d(double v) { return (int)lrint(v); }
+inline int cv_floor(float v) { int i = (int)v; return i - (i > v); }
+inline int cv_ceil_d(double v) { int i = (int)v; return i + (i < v); }
+inline int64_t align256(int64_t v) { return (v + 255) & ~int64_t(255); }
+
+struct Tables {
+    int nfeatures;
+    double scale_factor;   // ORBextractor.h:114 `double scaleFactor`
+    int nlevels;
+    float scale[COEB_MAXL], inv_scale[COEB_MAXL], sigma2[COEB_MAXL], inv_sigma2[COEB_MAXL];
+    int nfeat[COEB_MAXL];
+    int umax[16];
+};
+
+// ORBextractor::ORBextractor (src/ORBextractor.cc:418-477)
+bool make_tables(const coeb_orb_params& prm, Tables& t)
+{
+    if (prm.nlevels < 1 || prm.nlevels > COEB_MAXL || prm.nfeatures < 0 || !(prm.scale_factor > 0)) return false;
+    memset(&t, 0, sizeof(t));
+    t.nfeatures = prm.nfeatures;
+    t.scale_factor = prm.scale_factor;
+    t.nlevels = prm.nlevels;
+    t.scale[0] = 1.0f;
+    t.sigma2[0] = 1.0f;
+    for (int i = 1; i < t.nlevels; i++) {
+        t.scale[i] = (float)((double)t.scale[i - 1] * t.scale_factor);
+        t.sigma2[i] = t.scale[i] * t.scale[i];
+    }
+    for (int i = 0; i < t.nlevels; i++) {
+        t.inv_scale[i] = 1.0f / t.scale[i];
+        t.inv_sigma2[i] = 1.0f / t.sigma2[i];
+    }
+    const float factor = (float)(1.0f / t.scale_factor);
+    float ndesired = t.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)t.nlevels));
+    int sum = 0;
+    for (int l = 0; l < t.nlevels - 1; l++) {
+        t.nfeat[l] = cv_round(ndesired);
+        sum += t.nfeat[l];
+        ndesired *= factor;
+    }
+    t.nfeat[t.nlevels - 1] = std::max(t.nfeatures - sum, 0);
+    int v, v0;
+    const int vmax = cv_floor(HALF_PATCH_SIZE * sqrtf(2.f) / 2 + 1);
+    const int vmin = cv_ceil_d(HALF_PATCH_SIZE * sqrtf(2.f) / 2);
+    const double hp2 = HALF_PATCH_SIZE * HALF_PATCH_SIZE;
+    for (v = 0; v <= vmax; ++v) t.umax[v] = cv_round_d(std::sqrt(hp2 - v * v));
+    for (v = HALF_PATCH_SIZE, v0 = 0; v >= vmin; --v) {
+        while (t.umax[v0] == t.umax[v0 + 1]) ++v0;
+        t.umax[v] = v0;
+        ++v0;
+    }
+    return true;
+}
+
+// Gaussian 7-tap sigma 2, Q8 error-diffused
+void gauss_kernel7(int k[7])
+{
+    const int n = 7, n2 = 3;
+    const double scale2X = -0.125 / (2.0 * 2.0);
+    double values[3], sum = 0.0;
+    for (int i = 0, x = 1 - n; i < n2; i++, x += 2) {
+        const double t = std::exp((double)(x * x) * scale2X);
+        values[i] = t;
+        sum += t;
+    }
+    sum = sum * 2.0 + 1.0;
+    const double mul1 = 1.0 / sum;
+    double err = 0.0;
+    int64_t s = 0;
+    for (int i = 0; i < n2; i++) {
+        const double adj = values[i] * mul1 * 256.0 + err;
+        const int64_t q = cv_round_d(adj);
+        err = adj - (double)q;
+        k[i] = k[n - 1 - i] = (int)q;
+        s += q;
+    }
+    k[n2] = (int)(256 - 2 * s);
+}
+
+// cv::resize INTER_LINEAR coefficient tables (imgproc resize.cpp, 8U fixed point)
+int resize_tables(int sw, int sh, int dw, int dh, std::vector<int>& tab)
+{
+    const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+    const size_t base = tab.size();
+    tab.resize(base + 2 * dw + 2 * dh);
+    int* xofs = tab.data() + base;
+    int* alpha = xofs + dw;
+    int* yofs = alpha + dw;
+    int* beta = yofs + dh;
+    int xmax = dw;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw) {
+            xmax = std::min(xmax, dx);
+            if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        }
+        xofs[dx] = sx;
+        const int a0 = std::max(-32768, std::min(32767, cv_round((1.f - fx) * 2048)));
+        const int a1 = std::max(-32768, std::min(32767, cv_round(fx * 2048)));
+        alpha[dx] = (a0 & 0xFFFF) | (a1 << 16);
+    }
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        const int sy = cv_floor(fy);
+        fy -= sy;
+        yofs[dy] = sy;
+        const int b0 = std::max(-32768, std::min(32767, cv_round((1.f - fy) * 2048)));
+        const int b1 = std::max(-32768, std::min(32767, cv_round(fy * 2048)));
+        beta[dy] = (b0 & 0xFFFF) | (b1 << 16);
+    }
+    return xmax;
+}
+
+bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, std::vector<CellDesc>& cells,
+               std::string& err)
+{
+    memset(&P, 0, sizeof(P));
+    P.W = W; P.H = H; P.L = t.nlevels;
+    rtab.clear();
+    cells.clear();
+    if (W > 4096 || H > 4096) { err = "image larger than 4096 px is not supported (12-bit key packing)"; return false; }
+    int64_t pyr = 0, blur = 0, node = 0;
+    int kcap_total = 0, out_total = 0, cell_cap = 1;
+    for (int l = 0; l < t.nlevels; l++) {
+        LevelGeom& g = P.lv[l];
+        g.w = cv_round((float)W * t.inv_scale[l]);     // ComputePyramid :1349
+        g.h = cv_round((float)H * t.inv_scale[l]);
+        g.scale = t.scale[l];
+        g.size_i = (int)(PATCH_SIZE * t.scale[l]);
+        if (l == 0) g.pyr_off = -1;
+        else { g.pyr_off = pyr; pyr = align256(pyr + (int64_t)g.w * g.h); }
+        g.blur_off = blur;
+        blur = align256(blur + (int64_t)g.w * g.h);
+        if (l > 0) {
+            g.rtab_off = (int)rtab.size();
+            g.xmax = resize_tables(P.lv[l - 1].w, P.lv[l - 1].h, g.w, g.h, rtab);
+        }
+        // FAST cells (ComputeKeyPointsOctTree :795-829)
+        const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+        const int maxBorderX = g.w - EDGE_THRESHOLD + 3, maxBorderY = g.h - EDGE_THRESHOLD + 3;
+        const float width = (float)(maxBorderX - minBorderX), height = (float)(maxBorderY - minBorderY);
+        const float Wc = 30;
+        g.ncols = (int)(width / Wc);
+        g.nrows = (int)(height / Wc);
+        if (g.ncols <= 0 || g.nrows <= 0) { err = "pyramid level too small for the 30-px FAST grid"; return false; }
+        g.wcell = (int)ceilf(width / g.ncols);
+        g.hcell = (int)ceilf(height / g.nrows);
+        g.cell0 = (int)cells.size();
+        for (int i = 0; i < g.nrows; i++) {
+            const float iniY = (float)(minBorderY + i * g.hcell);
+            float maxY = iniY + g.hcell + 6;
+            if (iniY >= maxBorderY - 3) continue;
+            if (maxY > maxBorderY) maxY = (float)maxBorderY;
+            for (int j = 0; j < g.ncols; j++) {
+                const float iniX = (float)(minBorderX + j * g.wcell);
+                float maxX = iniX + g.wcell + 6;
+                if (iniX >= maxBorderX - 6) continue;
+                if (maxX > maxBorderX) maxX = (float)maxBorderX;
+                CellDesc c;
+                c.level = (int16_t)l; c.pad = 0;
+                c.x0 = (int16_t)(int)iniX; c.y0 = (int16_t)(int)iniY;
+                c.rw = (int16_t)((int)maxX - (int)iniX); c.rh = (int16_t)((int)maxY - (int)iniY);
+                c.i = (int16_t)i; c.j = (int16_t)j;
+                if (c.rw > kRoiMax || c.rh > kRoiMax) { err = "FAST cell ROI exceeds 64 px"; return false; }
+                const int ww = std::max(0, c.rw - 6), wh = std::max(0, c.rh - 6);
+                cell_cap = std::max(cell_cap, ((ww + 1) / 2) * ((wh + 1) / 2));
+                P.max_roi_w = std::max(P.max_roi_w, (int)c.rw);
+                P.max_roi_h = std::max(P.max_roi_h, (int)c.rh);
+                cells.push_back(c);
+            }
+        }
+        g.ncells = (int)cells.size() - g.cell0;
+        // DistributeOctTree constants (:549-552, :866-875)
+        g.nfeat = t.nfeat[l];
+        g.nfeat_area = (int)((double)t.nfeat[l] * 0.7);
+        g.maxX = maxBorderX - minBorderX;
+        g.maxY = maxBorderY - minBorderY;
+        g.nini = (int)roundf((float)g.maxX / g.maxY);
+        if (g.nini < 1 || g.nini > 4) { err = "aspect ratio gives an unsupported number of initial octree nodes"; return false; }
+        g.hx = (float)g.maxX / g.nini;
+        int b = 0;
+        for (int i = 0; i <= g.nini; i++) {
+            while (b <= g.maxX + 1 && (int)((float)b / g.hx) < i) b++;
+            g.ini_bound[i] = b;
+        }
+        g.ini_bound[g.nini] = 1 << 20;
+        if (g.nfeat + 8 > kOctLMax) { err = "features per level exceed the octree work-list capacity (1016)"; return false; }
+        g.out_cap = std::max(g.nfeat + 3, 4 * g.nini) + 5;
+        g.ncap = 5 * (g.nfeat + 4) + 4 * g.nini + 16;
+        g.ncap = std::max(g.ncap, g.out_cap);
+        g.node_off = node;
+        node += 2 * 8 * (int64_t)g.ncap;
+        g.out_off = out_total;
+        out_total += g.out_cap;
+    }
+    P.ncells = (int)cells.size();
+    P.cell_cap = cell_cap;
+    for (int l = 0; l < t.nlevels; l++) {
+        P.lv[l].kcap_off = kcap_total;
+        P.lv[l].kcap = P.lv[l].ncells * cell_cap;
+        kcap_total += P.lv[l].kcap;
+    }
+    P.pyr_stride = std::max<int64_t>(pyr, 256);
+    P.blur_stride = blur;
+    P.kbuf_stride = kcap_total;
+    P.node_stride = node;
+    P.lvl_stride = out_total;
+    P.kcap = out_total;
+    P.rtab_ints = (int)rtab.size();
+    memcpy(P.umax, t.umax, sizeof(P.umax));
+    gauss_kernel7(P.gauss);
+    return true;
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+};
+
+struct ProfImpl {
+    bool enabled = false;
+    std::vector<std::string> names;
+    std::vector<double> ms;
+    std::vector<int64_t> launches;
+    std::vector<hipEvent_t> pool;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    int cur_name = -1;
+    hipEvent_t cur_start = nullptr;
+    hipEvent_t get()
+    {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    void drain()
+    {
+        for (auto& pe : pending) {
+            float t = 0.f;
+            (void)hipEventSynchronize(pe.second.second);
+            (void)hipEventElapsedTime(&t, pe.second.first, pe.second.second);
+            ms[pe.first] += t;
+            launches[pe.first] += 1;
+            pool.push_back(pe.second.first);
+            pool.push_back(pe.second.second);
+        }
+        pending.clear();
+    }
+};
+
+}  // namespace
+
+void prof_begin(ProfileHook* p, const char* name, hipStream_t s)
+{
+    if (!p || !p->impl) return;
+    ProfImpl* pi = static_cast<ProfImpl*>(p->impl);
+    if (!pi->enabled) return;
+    int id = -1;
+    for (size_t i = 0; i < pi->names.size(); i++)
+        if (pi->names[i] == name) id = (int)i;
+    if (id < 0) {
+        id = (int)pi->names.size();
+        pi->names.push_back(name);
+        pi->ms.push_back(0.0);
+        pi->launches.push_back(0);
+    }
+    pi->cur_name = id;
+    pi->cur_start = pi->get();
+    (void)hipEventRecord(pi->cur_start, s);
+}
+
+void prof_end(ProfileHook* p, hipStream_t s)
+{
+    if (!p || !p->impl) return;
+    ProfImpl* pi = static_cast<ProfImpl*>(p->impl);
+    if (!pi->enabled || pi->cur_name < 0) return;
+    hipEvent_t e = pi->get();
+    (void)hipEventRecord(e, s);
+    pi->pending.push_back({pi->cur_name, {pi->cur_start, e}});
+    pi->cur_name = -1;
+    if (pi->pending.size() > 4096) pi->drain();
+}
+
+struct coeb_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    coeb_orb_params params{};
+    Tables tab{};
+    int max_w = 0, max_h = 0, max_batch = 0;
+    bool has_plan = false;
+    Plan plan{};
+    std::vector<int> rtab;
+    std::vector<CellDesc> cells;
+    std::map<std::string, DevBuf> bufs;
+    std::string err;
+    ProfImpl prof;
+    ProfileHook hook;
+    int batch_frames = 0;      // frames of the last extracted batch
+    const uint8_t* batch_gray = nullptr;
+};
+
+namespace {
+
+int set_err(coeb_ctx* c, int code, const std::string& msg)
+{
+    if (c) c->err = msg;
+    g_last_error = msg;
+    return code;
+}
+
+int hip_err(coeb_ctx* c, hipError_t e, const char* where)
+{
+    return set_err(c, COEB_EDEVICE, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(ctx, expr)                                          \
+    do {                                                            \
+        hipError_t _e = (expr);                                     \
+        if (_e != hipSuccess) return hip_err((ctx), _e, #expr);     \
+    } while (0)
+
+template <typename T>
+int ensure(coeb_ctx* c, const char* name, size_t count, T** out)
+{
+    DevBuf& b = c->bufs[name];
+    const size_t bytes = std::max<size_t>(count * sizeof(T), 256);
+    if (b.n < bytes) {
+        if (b.p) (void)hipFree(b.p);
+        b.p = nullptr;
+        b.n = 0;
+        hipError_t e = hipMalloc(&b.p, bytes);
+        if (e != hipSuccess) return set_err(c, COEB_ENOMEM, std::string("hipMalloc ") + name + ": " + hipGetErrorString(e));
+        b.n = bytes;
+    }
+    *out = static_cast<T*>(b.p);
+    return 0;
+}
+
+int ensure_plan(coeb_ctx* c, int W, int H)
+{
+    if (c->has_plan && c->plan.W == W && c->plan.H == H) return 0;
+    if (W <= 0 || H <= 0 || W > c->max_w || H > c->max_h)
+        return set_err(c, COEB_EINVAL, "image size outside the context limits");
+    std::string err;
+    Plan P;
+    if (!make_plan(c->tab, W, H, P, c->rtab, c->cells, err)) return set_err(c, COEB_EINVAL, err);
+    c->plan = P;
+    Plan* dplan;
+    int* drtab;
+    CellDesc* dcells;
+    int8_t* dpat;
+    int rc;
+    if ((rc = ensure(c, "plan", 1, &dplan))) return rc;
+    if ((rc = ensure(c, "rtab", std::max<size_t>(c->rtab.size(), 1), &drtab))) return rc;
+    if ((rc = ensure(c, "cells", c->cells.size(), &dcells))) return rc;
+    if ((rc = ensure(c, "pattern", 1024, &dpat))) return rc;
+    HIP_TRY(c, hipMemcpy(dplan, &c->plan, sizeof(Plan), hipMemcpyHostToDevice));
+    if (!c->rtab.empty()) HIP_TRY(c, hipMemcpy(drtab, c->rtab.data(), c->rtab.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(dcells, c->cells.data(), c->cells.size() * sizeof(CellDesc), hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(dpat, kPattern, 1024, hipMemcpyHostToDevice));
+    c->has_plan = true;
+    return 0;
+}
+
+// Allocate per-frame buffers for F frames and fill ExtractBufs.
+int extract_bufs(coeb_ctx* c, int F, ExtractBufs& b)
+{
+    const Plan& P = c->plan;
+    memset(&b, 0, sizeof(b));
+    int rc;
+    uint8_t *pyr, *blur, *nodes, *desc;
+    int *cand_n, *lvl_n, *counts, *err;
+    uint32_t *cand, *keys, *lvl_kp;
+    coeb_keypoint* kps;
+    DynMask* dyn;
+    if ((rc = ensure(c, "pyr", (size_t)F * P.pyr_stride, &pyr))) return rc;
+    if ((rc = ensure(c, "blur", (size_t)F * P.blur_stride, &blur))) return rc;
+    if ((rc = ensure(c, "cand_n", (size_t)F * P.ncells, &cand_n))) return rc;
+    if ((rc = ensure(c, "cand", (size_t)F * P.ncells * P.cell_cap, &cand))) return rc;
+    if ((rc = ensure(c, "keys", (size_t)F * 2 * P.kbuf_stride, &keys))) return rc;
+    if ((rc = ensure(c, "nodes", (size_t)F * P.node_stride * 4, &nodes))) return rc;
+    if ((rc = ensure(c, "lvl_n", (size_t)F * P.L, &lvl_n))) return rc;
+    if ((rc = ensure(c, "lvl_kp", (size_t)F * P.lvl_stride, &lvl_kp))) return rc;
+    if ((rc = ensure(c, "kps", (size_t)F * P.kcap, &kps))) return rc;
+    if ((rc = ensure(c, "desc", (size_t)F * P.kcap * 32, &desc))) return rc;
+    if ((rc = ensure(c, "counts", (size_t)F, &counts))) return rc;
+    if ((rc = ensure(c, "dyn", (size_t)F, &dyn))) return rc;
+    if ((rc = ensure(c, "err", 4, &err))) return rc;
+    b.pyr = pyr; b.blur = blur; b.cand_n = cand_n; b.cand = cand; b.keys = keys; b.nodes = nodes;
+    b.lvl_n = lvl_n; b.lvl_kp = lvl_kp; b.kps = kps; b.desc = desc; b.counts = counts; b.dyn = dyn; b.err = err;
+    b.rtab = static_cast<const int*>(c->bufs["rtab"].p);
+    b.cells = static_cast<const CellDesc*>(c->bufs["cells"].p);
+    b.pattern = static_cast<const int8_t*>(c->bufs["pattern"].p);
+    return 0;
+}
+
+// Upload per-frame boxes / T_M / blur flags (host arrays, offset layout) for F frames.
+int upload_dyn(coeb_ctx* c, int F, const coeb_box* boxes, const int32_t* box_off, const float* tm_xy,
+               const int32_t* tm_off, const int32_t* blur_flag, ExtractBufs& b)
+{
+    const int nbox = (box_off && boxes) ? box_off[F] : 0;
+    const int ntm = (tm_off && tm_xy) ? tm_off[F] : 0;
+    int rc;
+    float *dbox, *dtm;
+    int32_t *dboff, *dtoff, *dblur;
+    if (nbox > 0) {
+        for (int f = 0; f < F; f++)
+            if (box_off[f + 1] - box_off[f] > COEB_MAXBOX) return set_err(c, COEB_EINVAL, "more than 16 boxes in a frame");
+        if ((rc = ensure(c, "boxes", (size_t)nbox * 4, &dbox))) return rc;
+        if ((rc = ensure(c, "box_off", (size_t)F + 1, &dboff))) return rc;
+        if ((rc = ensure(c, "blurf", (size_t)nbox, &dblur))) return rc;
+        HIP_TRY(c, hipMemcpyAsync(dbox, boxes, (size_t)nbox * 16, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(dboff, box_off, (size_t)(F + 1) * 4, hipMemcpyHostToDevice, c->stream));
+        if (blur_flag) {
+            HIP_TRY(c, hipMemcpyAsync(dblur, blur_flag, (size_t)nbox * 4, hipMemcpyHostToDevice, c->stream));
+        } else {
+            HIP_TRY(c, hipMemsetAsync(dblur, 0, (size_t)nbox * 4, c->stream));
+        }
+        b.boxes = dbox; b.box_off = dboff; b.blurf = dblur;
+    }
+    if (ntm > 0) {
+        if ((rc = ensure(c, "tm", (size_t)ntm * 2, &dtm))) return rc;
+        if ((rc = ensure(c, "tm_off", (size_t)F + 1, &dtoff))) return rc;
+        HIP_TRY(c, hipMemcpyAsync(dtm, tm_xy, (size_t)ntm * 8, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(dtoff, tm_off, (size_t)(F + 1) * 4, hipMemcpyHostToDevice, c->stream));
+        b.tm = dtm; b.tm_off = dtoff;
+    }
+    return 0;
+}
+
+int check_err_word(coeb_ctx* c)
+{
+    int* derr = static_cast<int*>(c->bufs["err"].p);
+    if (!derr) return 0;
+    int h = 0;
+    HIP_TRY(c, hipMemcpyAsync(&h, derr, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (h) {
+        char msg[160];
+        snprintf(msg, sizeof msg, "internal capacity exceeded (device error bits 0x%x)", h);
+        HIP_TRY(c, hipMemsetAsync(derr, 0, 4, c->stream));
+        return set_err(c, COEB_ERANGE, msg);
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int coeb_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+coeb_ctx* coeb_create(const coeb_orb_params* params, int device, int max_width, int max_height, int max_batch)
+{
+    if (!params || max_width <= 0 || max_height <= 0 || max_batch <= 0) {
+        g_last_error = "coeb_create: invalid arguments";
+        return nullptr;
+    }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) {
+        g_last_error = "coeb_create: no usable HIP device (the HIP path has no CPU fallback)";
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        g_last_error = std::string("coeb_create: device is not gfx950 (") + prop.gcnArchName + ")";
+        return nullptr;
+    }
+    coeb_ctx* c = new coeb_ctx();
+    c->device = device;
+    c->params = *params;
+    if (!make_tables(*params, c->tab)) {
+        g_last_error = "coeb_create: invalid ORB parameters";
+        delete c;
+        return nullptr;
+    }
+    c->max_w = max_width;
+    c->max_h = max_height;
+    c->max_batch = max_batch;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        g_last_error = "coeb_create: stream creation failed";
+        delete c;
+        return nullptr;
+    }
+    c->hook.impl = &c->prof;
+    int* err;
+    if (ensure(c, "err", 4, &err) || hipMemset(err, 0, 16) != hipSuccess) {
+        g_last_error = "coeb_create: device allocation failed";
+        coeb_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void coeb_destroy(coeb_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& kv : c->bufs)
+        if (kv.second.p) (void)hipFree(kv.second.p);
+    c->prof.drain();
+    for (auto e : c->prof.pool) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* coeb_last_error(const coeb_ctx* c)
+{
+    if (c && !c->err.empty()) return c->err.c_str();
+    return g_last_error.c_str();
+}
+
+int coeb_orb_tables_get(const coeb_ctx* c, coeb_orb_tables* out)
+{
+    if (!c || !out) return COEB_EINVAL;
+    memset(out, 0, sizeof(*out));
+    out->nlevels = c->tab.nlevels;
+    out->scale_factor = (float)c->tab.scale_factor;
+    for (int l = 0; l < c->tab.nlevels; l++) {
+        out->scale[l] = c->tab.scale[l];
+        out->inv_scale[l] = c->tab.inv_scale[l];
+        out->sigma2[l] = c->tab.sigma2[l];
+        out->inv_sigma2[l] = c->tab.inv_sigma2[l];
+        out->features_per_level[l] = c->tab.nfeat[l];
+    }
+    memcpy(out->umax, c->tab.umax, sizeof(out->umax));
+    return COEB_OK;
+}
+
+int coeb_max_keypoints(const coeb_ctx* cc, int width, int height)
+{
+    coeb_ctx* c = const_cast<coeb_ctx*>(cc);
+    if (!c) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    int rc = ensure_plan(c, width, height);
+    if (rc) return rc;
+    return c->plan.kcap;
+}
+
+int coeb_extract_batch_device(coeb_ctx* c, const uint8_t* d_gray, int F, int W, int H, const coeb_box* boxes,
+                              const int32_t* box_off, const float* tm_xy, const int32_t* tm_off,
+                              const int32_t* blur_flag)
+{
+    if (!c || !d_gray || F <= 0) return set_err(c, COEB_EINVAL, "coeb_extract_batch_device: invalid arguments");
+    if (F > c->max_batch) return set_err(c, COEB_EINVAL, "batch larger than max_batch");
+    (void)hipSetDevice(c->device);
+    int rc;
+    if ((rc = ensure_plan(c, W, H))) return rc;
+    ExtractBufs b;
+    if ((rc = extract_bufs(c, F, b))) return rc;
+    if ((rc = upload_dyn(c, F, boxes, box_off, tm_xy, tm_off, blur_flag, b))) return rc;
+    b.gray = d_gray;
+    if (launch_extract(c->plan, static_cast<const Plan*>(c->bufs["plan"].p), b, F, c->stream, &c->hook))
+        return hip_err(c, hipGetLastError(), "launch_extract");
+    c->batch_frames = F;
+    c->batch_gray = d_gray;
+    return COEB_OK;
+}
+
+int coeb_batch_results(coeb_ctx* c, const coeb_keypoint** d_kps, const uint8_t** d_desc, const int32_t** d_counts,
+                       int* kcap)
+{
+    if (!c || !c->has_plan) return set_err(c, COEB_EINVAL, "no batch extracted yet");
+    if (d_kps) *d_kps = static_cast<const coeb_keypoint*>(c->bufs["kps"].p);
+    if (d_desc) *d_desc = static_cast<const uint8_t*>(c->bufs["desc"].p);
+    if (d_counts) *d_counts = static_cast<const int32_t*>(c->bufs["counts"].p);
+    if (kcap) *kcap = c->plan.kcap;
+    return COEB_OK;
+}
+
+int coeb_extract(coeb_ctx* c, const uint8_t* gray, int W, int H, size_t stride, const coeb_box* boxes, int nbox,
+                 const float* tm_xy, int ntm, const int32_t* blur_flag, int nblur, coeb_keypoint* kp_out,
+                 uint8_t* desc_out, int cap, int* n_out)
+{
+    if (!c || !n_out) return set_err(c, COEB_EINVAL, "coeb_extract: invalid arguments");
+    *n_out = 0;
+    if (!gray || W <= 0 || H <= 0) return COEB_OK;          // _image.empty() -> return (:1096-1097)
+    if (stride < (size_t)W) return set_err(c, COEB_EINVAL, "stride < width");
+    if (nbox < 0 || nbox > COEB_MAXBOX || ntm < 0 || nblur < 0) return set_err(c, COEB_EINVAL, "bad box/T_M counts");
+    (void)hipSetDevice(c->device);
+    int rc;
+    if ((rc = ensure_plan(c, W, H))) return rc;
+    uint8_t* dgray;
+    if ((rc = ensure(c, "gray_stage", (size_t)W * H, &dgray))) return rc;
+    HIP_TRY(c, hipMemcpy2DAsync(dgray, W, gray, stride, W, H, hipMemcpyHostToDevice, c->stream));
+    int32_t box_off[2] = {0, nbox}, tm_off[2] = {0, ntm};
+    std::vector<int32_t> blur(nbox, 0);
+    for (int i = 0; i < nbox && i < nblur; i++) blur[i] = blur_flag[i];   // missing flags read as 0
+    ExtractBufs b;
+    if ((rc = extract_bufs(c, 1, b))) return rc;
+    if ((rc = upload_dyn(c, 1, nbox ? boxes : nullptr, box_off, ntm ? tm_xy : nullptr, tm_off,
+                         nbox ? blur.data() : nullptr, b)))
+        return rc;
+    b.gray = dgray;
+    if (launch_extract(c->plan, static_cast<const Plan*>(c->bufs["plan"].p), b, 1, c->stream, &c->hook))
+        return hip_err(c, hipGetLastError(), "launch_extract");
+    c->batch_frames = 1;
+    c->batch_gray = dgray;
+    int n = 0;
+    HIP_TRY(c, hipMemcpyAsync(&n, b.counts, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if ((rc = check_err_word(c))) return rc;
+    *n_out = n;
+    const int m = std::min(n, cap);
+    if (m > 0 && kp_out)
+        HIP_TRY(c, hipMemcpyAsync(kp_out, b.kps, (size_t)m * sizeof(coeb_keypoint), hipMemcpyDeviceToHost, c->stream));
+    if (m > 0 && desc_out) HIP_TRY(c, hipMemcpyAsync(desc_out, b.desc, (size_t)m * 32, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (n > cap) return set_err(c, COEB_ERANGE, "keypoint output capacity too small");
+    return COEB_OK;
+}
+
+static MatchCam make_cam(const coeb_ctx* c, const coeb_camera* cam)
+{
+    MatchCam m;
+    memset(&m, 0, sizeof(m));
+    m.fx = cam->fx; m.fy = cam->fy; m.cx = cam->cx; m.cy = cam->cy; m.bf = cam->bf;
+    m.mb = cam->bf / cam->fx;                                       // Frame.cc:246
+    m.min_x = cam->min_x; m.max_x = cam->max_x; m.min_y = cam->min_y; m.max_y = cam->max_y;
+    m.grid_inv_w = (float)COEB_GRID_COLS / (cam->max_x - cam->min_x);   // Frame.cc:233-234
+    m.grid_inv_h = (float)COEB_GRID_ROWS / (cam->max_y - cam->min_y);
+    for (int l = 0; l < c->tab.nlevels; l++) m.scale[l] = c->tab.scale[l];
+    return m;
+}
+
+int coeb_match_lastframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curframe* cur, const coeb_lastframe* last,
+                         const float Tcw_cur[16], const float Tcw_last[16], float th, int bmono, int check_ori,
+                         int32_t* match_out, int* nmatches)
+{
+    if (!c || !cam || !cur || !last || !Tcw_cur || !Tcw_last || !nmatches)
+        return set_err(c, COEB_EINVAL, "coeb_match_lastframe: invalid arguments");
+    *nmatches = 0;
+    if (cur->n < 0 || last->n < 0) return set_err(c, COEB_EINVAL, "negative frame size");
+    if (cur->n > kCurMax) return set_err(c, COEB_EINVAL, "more than 4096 current keypoints");
+    (void)hipSetDevice(c->device);
+    const int n = cur->n, nl = last->n;
+    const int cs = std::max(n, 1), ls = std::max(nl, 1);
+    int rc;
+    coeb_keypoint *dck, *dlk;
+    uint8_t *dcd, *dld, *dhas, *dout;
+    float *dur, *dxw, *dT;
+    int32_t *dcn, *dnobs, *dmatch, *dnm, *dscr, *derr;
+    if ((rc = ensure(c, "m_ck", cs, &dck)) || (rc = ensure(c, "m_lk", ls, &dlk)) || (rc = ensure(c, "m_cd", (size_t)cs * 32, &dcd)) ||
+        (rc = ensure(c, "m_ld", (size_t)ls * 32, &dld)) || (rc = ensure(c, "m_has", ls, &dhas)) ||
+        (rc = ensure(c, "m_out", ls, &dout)) || (rc = ensure(c, "m_ur", cs, &dur)) ||
+        (rc = ensure(c, "m_xw", (size_t)ls * 3, &dxw)) || (rc = ensure(c, "m_T", 32, &dT)) ||
+        (rc = ensure(c, "m_cn", 2, &dcn)) || (rc = ensure(c, "m_nobs", ls, &dnobs)) ||
+        (rc = ensure(c, "m_match", cs, &dmatch)) || (rc = ensure(c, "m_nm", 1, &dnm)) ||
+        (rc = ensure(c, "m_scr", (size_t)2 * ls + 2, &dscr)) || (rc = ensure(c, "err", 4, &derr)))
+        return rc;
+    hipStream_t s = c->stream;
+    int32_t cnts[2] = {n, nl};
+    HIP_TRY(c, hipMemcpyAsync(dcn, cnts, 8, hipMemcpyHostToDevice, s));
+    if (n) {
+        HIP_TRY(c, hipMemcpyAsync(dck, cur->keys_un, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dcd, cur->descriptors, (size_t)n * 32, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dur, cur->u_right, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    }
+    if (nl) {
+        HIP_TRY(c, hipMemcpyAsync(dlk, last->keys_un, (size_t)nl * sizeof(coeb_keypoint), hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dld, last->mp_descriptor, (size_t)nl * 32, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dhas, last->has_mappoint, (size_t)nl, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dout, last->outlier, (size_t)nl, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dxw, last->world_pos, (size_t)nl * 12, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dnobs, last->mp_observations, (size_t)nl * 4, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(c, hipMemcpyAsync(dT, Tcw_cur, 64, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(dT + 16, Tcw_last, 64, hipMemcpyHostToDevice, s));
+    MatchBufs mb;
+    memset(&mb, 0, sizeof(mb));
+    mb.cur_kps = dck; mb.cur_desc = dcd; mb.cur_n = dcn; mb.cur_ur = dur; mb.cur_stride = cs;
+    mb.last_kps = dlk; mb.last_desc = dld; mb.last_n = dcn + 1; mb.last_has = dhas; mb.last_out = dout;
+    mb.last_xw = dxw; mb.last_nobs = dnobs; mb.last_stride = ls;
+    mb.Tcw_cur = dT; mb.Tcw_last = dT + 16;
+    mb.match = dmatch; mb.nmatch = dnm; mb.scratch = dscr; mb.scratch_stride = 2 * ls + 2; mb.err = derr;
+    if (launch_match(make_cam(c, cam), mb, 1, th, bmono, check_ori, 0, s, &c->hook))
+        return hip_err(c, hipGetLastError(), "launch_match");
+    int nm = 0;
+    HIP_TRY(c, hipMemcpyAsync(&nm, dnm, 4, hipMemcpyDeviceToHost, s));
+    if (n && match_out) HIP_TRY(c, hipMemcpyAsync(match_out, dmatch, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if ((rc = check_err_word(c))) return rc;
+    *nmatches = nm;
+    return COEB_OK;
+}
+
+int coeb_match_batch_device(coeb_ctx* c, const float* d_depth, int F, int W, int H, const coeb_camera* cam,
+                            const float* Tcw, float th, int32_t nobs)
+{
+    if (!c || !d_depth || !cam || !Tcw || F <= 0) return set_err(c, COEB_EINVAL, "coeb_match_batch_device: invalid arguments");
+    if (!c->has_plan || c->batch_frames != F || c->plan.W != W || c->plan.H != H)
+        return set_err(c, COEB_EINVAL, "coeb_match_batch_device: must follow coeb_extract_batch_device on the same batch");
+    (void)hipSetDevice(c->device);
+    const int K = c->plan.kcap;
+    if (K > kCurMax) return set_err(c, COEB_EINVAL, "keypoint capacity exceeds the matcher limit (4096)");
+    int rc;
+    float *ur, *dep, *xw, *dT;
+    uint8_t *has, *outl;
+    int32_t *nobsb, *match, *nm, *scr, *derr;
+    if ((rc = ensure(c, "b_ur", (size_t)F * K, &ur)) || (rc = ensure(c, "b_dep", (size_t)F * K, &dep)) ||
+        (rc = ensure(c, "b_xw", (size_t)F * K * 3, &xw)) || (rc = ensure(c, "b_has", (size_t)F * K, &has)) ||
+        (rc = ensure(c, "b_outl", (size_t)F * K, &outl)) || (rc = ensure(c, "b_nobs", (size_t)F * K, &nobsb)) ||
+        (rc = ensure(c, "b_match", (size_t)F * K, &match)) || (rc = ensure(c, "b_nm", (size_t)F, &nm)) ||
+        (rc = ensure(c, "b_T", (size_t)F * 32, &dT)) || (rc = ensure(c, "b_scr", (size_t)F * (2 * K + 2), &scr)) ||
+        (rc = ensure(c, "err", 4, &derr)))
+        return rc;
+    const coeb_keypoint* kps = static_cast<const coeb_keypoint*>(c->bufs["kps"].p);
+    const uint8_t* desc = static_cast<const uint8_t*>(c->bufs["desc"].p);
+    const int32_t* counts = static_cast<const int32_t*>(c->bufs["counts"].p);
+    PrepBufs pb;
+    memset(&pb, 0, sizeof(pb));
+    pb.kps = kps; pb.n = counts; pb.stride = K; pb.depth = d_depth; pb.W = W; pb.H = H;
+    pb.bf = cam->bf; pb.fx = cam->fx; pb.fy = cam->fy; pb.cx = cam->cx; pb.cy = cam->cy;
+    pb.ur = ur; pb.dep = dep; pb.has = has; pb.outl = outl; pb.xw = xw; pb.nobs = nobsb; pb.nobs_value = nobs;
+    if (launch_prep(pb, F, c->stream, &c->hook)) return hip_err(c, hipGetLastError(), "launch_prep");
+    if (F < 2) return COEB_OK;
+    // pair p: current = frame p+1, last = frame p (Tcw_last = I, Tcw_cur = Tcw[p+1])
+    std::vector<float> T((size_t)(F - 1) * 32);
+    static const float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    for (int p = 0; p < F - 1; p++) {
+        memcpy(&T[(size_t)p * 16], Tcw + (size_t)(p + 1) * 16, 64);
+        memcpy(&T[(size_t)(F - 1) * 16 + (size_t)p * 16], I, 64);
+    }
+    HIP_TRY(c, hipMemcpyAsync(dT, T.data(), T.size() * 4, hipMemcpyHostToDevice, c->stream));
+    MatchBufs mb;
+    memset(&mb, 0, sizeof(mb));
+    mb.cur_kps = kps + K; mb.cur_desc = desc + (size_t)K * 32; mb.cur_n = counts + 1; mb.cur_ur = ur + K; mb.cur_stride = K;
+    mb.last_kps = kps; mb.last_desc = desc; mb.last_n = counts; mb.last_has = has; mb.last_out = outl;
+    mb.last_xw = xw; mb.last_nobs = nobsb; mb.last_stride = K;
+    mb.Tcw_cur = dT; mb.Tcw_last = dT + (size_t)(F - 1) * 16;
+    mb.match = match + K; mb.nmatch = nm + 1; mb.scratch = scr; mb.scratch_stride = 2 * K + 2; mb.err = derr;
+    if (launch_match(make_cam(c, cam), mb, F - 1, th, 0, 1, 20, c->stream, &c->hook))
+        return hip_err(c, hipGetLastError(), "launch_match");
+    return COEB_OK;
+}
+
+int coeb_batch_match_results(coeb_ctx* c, const int32_t** d_match, const int32_t** d_nmatches)
+{
+    if (!c) return COEB_EINVAL;
+    if (d_match) *d_match = static_cast<const int32_t*>(c->bufs["b_match"].p);
+    if (d_nmatches) *d_nmatches = static_cast<const int32_t*>(c->bufs["b_nm"].p);
+    return COEB_OK;
+}
+
+int coeb_stereo_from_rgbd(coeb_ctx* c, const coeb_keypoint* kps, int n, const float* depth, int W, int H,
+                          size_t dstride, float bf, float* ur_out, float* dep_out)
+{
+    if (!c || (n > 0 && (!kps || !depth || !ur_out || !dep_out)) || n < 0 || dstride < (size_t)W)
+        return set_err(c, COEB_EINVAL, "coeb_stereo_from_rgbd: invalid arguments");
+    if (n == 0) return COEB_OK;
+    (void)hipSetDevice(c->device);
+    int rc;
+    coeb_keypoint* dk;
+    float *dd, *dur, *ddep;
+    int32_t* dn;
+    if ((rc = ensure(c, "s_k", n, &dk)) || (rc = ensure(c, "s_d", (size_t)W * H, &dd)) || (rc = ensure(c, "s_ur", n, &dur)) ||
+        (rc = ensure(c, "s_dep", n, &ddep)) || (rc = ensure(c, "s_n", 1, &dn)))
+        return rc;
+    HIP_TRY(c, hipMemcpyAsync(dk, kps, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpy2DAsync(dd, (size_t)W * 4, depth, dstride * 4, (size_t)W * 4, H, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(dn, &n, 4, hipMemcpyHostToDevice, c->stream));
+    PrepBufs pb;
+    memset(&pb, 0, sizeof(pb));
+    pb.kps = dk; pb.n = dn; pb.stride = n; pb.depth = dd; pb.W = W; pb.H = H; pb.bf = bf; pb.fx = 1; pb.fy = 1;
+    pb.ur = dur; pb.dep = ddep;
+    if (launch_prep(pb, 1, c->stream, &c->hook)) return hip_err(c, hipGetLastError(), "launch_prep");
+    HIP_TRY(c, hipMemcpyAsync(ur_out, dur, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(dep_out, ddep, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return COEB_OK;
+}
+
+int coeb_descriptor_distance(const uint8_t* a, const uint8_t* b)
+{
+    // ORBmatcher::DescriptorDistance (ORBmatcher.cc:1648-1664): 8 x 32-bit XOR + popcount.
+    // Kept on the CPU: it is also called one pair at a time from MapPoint/Frame code.
+    int d = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t x, y;
+        memcpy(&x, a + 4 * i, 4);
+        memcpy(&y, b + 4 * i, 4);
+        d += __builtin_popcount(x ^ y);
+    }
+    return d;
+}
+
+int coeb_profile_enable(coeb_ctx* c, int enable)
+{
+    if (!c) return COEB_EINVAL;
+    c->prof.enabled = enable != 0;
+    return COEB_OK;
+}
+
+int coeb_profile_reset(coeb_ctx* c)
+{
+    if (!c) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    c->prof.drain();
+    std::fill(c->prof.ms.begin(), c->prof.ms.end(), 0.0);
+    std::fill(c->prof.launches.begin(), c->prof.launches.end(), 0);
+    return COEB_OK;
+}
+
+int coeb_profile_read(coeb_ctx* c, char* names, int cap, double* total_ms, int64_t* launches, int max_k, int* nk)
+{
+    if (!c) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    c->prof.drain();
+    std::string s;
+    const int k = std::min<int>(max_k, (int)c->prof.names.size());
+    for (int i = 0; i < k; i++) {
+        if (i) s += ",";
+        s += c->prof.names[i];
+        if (total_ms) total_ms[i] = c->prof.ms[i];
+        if (launches) launches[i] = c->prof.launches[i];
+    }
+    if (names && cap > 0) {
+        strncpy(names, s.c_str(), cap - 1);
+        names[cap - 1] = 0;
+    }
+    if (nk) *nk = k;
+    return COEB_OK;
+}
+
+int coeb_internal_stream(coeb_ctx* c, hipStream_t* s, int* device)
+{
+    if (!c) return COEB_EINVAL;
+    *s = c->stream;
+    *device = c->device;
+    return COEB_OK;
+}
+
+int coeb_internal_scratch(coeb_ctx* c, const char* name, size_t bytes, void** p)
+{
+    uint8_t* q;
+    int rc = ensure(c, name, bytes, &q);
+    *p = q;
+    return rc;
+}
+
+int coeb_internal_error(coeb_ctx* c, int code, const char* msg) { return set_err(c, code, msg); }
+
+/* Debug readback of intermediate buffers of frame f of the last batch (test support):
+ * what = "pyr" | "blur" | "cand_n" | "lvl_n" | "lvl_kp" | "dyn"; copies min(bytes, size). */
+int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t bytes, size_t* size_out)
+{
+    if (!c || !what || !c->has_plan || f < 0 || f >= c->batch_frames) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    const Plan& P = c->plan;
+    const uint8_t* src = nullptr;
+    size_t n = 0;
+    std::string w(what);
+    if (w == "pyr") { src = (const uint8_t*)c->bufs["pyr"].p + (size_t)f * P.pyr_stride; n = P.pyr_stride; }
+    else if (w == "blur") { src = (const uint8_t*)c->bufs["blur"].p + (size_t)f * P.blur_stride; n = P.blur_stride; }
+    else if (w == "cand_n") { src = (const uint8_t*)c->bufs["cand_n"].p + (size_t)f * P.ncells * 4; n = (size_t)P.ncells * 4; }
+    else if (w == "lvl_n") { src = (const uint8_t*)c->bufs["lvl_n"].p + (size_t)f * P.L * 4; n = (size_t)P.L * 4; }
+    else if (w == "lvl_kp") { src = (const uint8_t*)c->bufs["lvl_kp"].p + (size_t)f * P.lvl_stride * 4; n = (size_t)P.lvl_stride * 4; }
+    else if (w == "dyn") { src = (const uint8_t*)c->bufs["dyn"].p + (size_t)f * sizeof(DynMask); n = sizeof(DynMask); }
+    else if (w == "plan") { if (size_out) *size_out = sizeof(Plan); if (host) memcpy(host, &P, std::min(bytes, sizeof(Plan))); return COEB_OK; }
+    else return COEB_EINVAL;
+    if (size_out) *size_out = n;
+    if (host && bytes) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, hipMemcpy(host, src, std::min(bytes, n), hipMemcpyDeviceToHost));
+    }
+    return COEB_OK;
+}
+
+int coeb_synchronize(coeb_ctx* c)
+{
+    if (!c) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return check_err_word(c);
+}
+
+}  // extern "C"

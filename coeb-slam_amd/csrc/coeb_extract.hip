@@ -1,0 +1,993 @@
+// coeb_extract.hip -- CDNA4 (gfx950) kernels for ORBextractor::operator()
+// (src/ORBextractor.cc:1088-1342).  Integer/bitwise work: no MFMA.  Built with
+// -ffp-contract=off; every fused multiply-add is an explicit __builtin_fmaf placed where the
+// reference binary fused (SURVEY.md s7 hard part 3).
+//
+// Pipeline for F frames (one launch each, all on the context stream):
+//   k_dynmask    dynamic-object rectangles + area flag           (ORBextractor.cc:1101-1195)
+//   k_pyr_level  cascaded INTER_LINEAR pyramid, level l from l-1  (:1344-1367)
+//   k_blur       7x7 sigma-2 Gaussian of every level, LDS tiled   (:1317-1318)
+//   k_fast       per 30-px cell FAST-9/16 + NMS + iniTh/minTh     (:811-850)
+//   k_octree     per (frame, level) DistributeOctTree emulation   (:546-769, 852-890, 1204-1207)
+//   k_describe   IC_Angle + rBRIEF + output assembly              (:80-156, 902-903, 1291-1337)
+#include <hip/hip_runtime.h>
+
+#include "coeb_internal.hpp"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kRoiMax = 64;          // max FAST ROI side (host plan asserts)
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+__device__ __forceinline__ int wave_sum(int v)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Exclusive block scan of one int per thread (256 threads).  Returns prefix; *total = sum.
+// All threads must call it.  sbuf: >= kWaves+1 ints of LDS.
+__device__ __forceinline__ int block_scan_excl(int v, int* total, int* sbuf)
+{
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sbuf[w] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int i = 0; i < kWaves; i++) {
+        int t = sbuf[i];
+        if (i < w) base += t;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+// Exclusive block scan for a 0/1 predicate via ballots (cheaper).
+__device__ __forceinline__ int block_scan_flag(bool pred, int* total, int* sbuf)
+{
+    const int w = threadIdx.x >> 6;
+    uint64_t m = __ballot(pred);
+    int pre = __popcll(m & lanemask_lt());
+    if (lane_id() == 0) sbuf[w] = __popcll(m);
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int i = 0; i < kWaves; i++) {
+        int t = sbuf[i];
+        if (i < w) base += t;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + pre;
+}
+
+__device__ __forceinline__ const uint8_t* level_ptr(const Plan* P, const ExtractBufs& b, int f, int l)
+{
+    if (l == 0) return b.gray + (int64_t)f * P->W * P->H;
+    return b.pyr + (int64_t)f * P->pyr_stride + P->lv[l].pyr_off;
+}
+
+// CheckMovingKeyPoints / _finall mask lookup (ORBextractor.cc:1391-1397, 1426-1440)
+__device__ __forceinline__ bool masked_out(const DynMask& m, float px, float py, float scale, int W, int H)
+{
+    float sx = px * scale, sy = py * scale;
+    if (sx >= (float)(W - 1)) sx = (float)(W - 1);
+    if (sy >= (float)(H - 1)) sy = (float)(H - 1);
+    const int ix = (int)sx, iy = (int)sy;
+    for (int r = 0; r < m.nrect; r++)
+        if (ix >= m.rect[r][0] && ix < m.rect[r][2] && iy >= m.rect[r][1] && iy < m.rect[r][3]) return true;
+    return false;
+}
+
+// ================================ k_dynmask ================================
+// One thread per frame: the literal box-layer loop (tiny, <= 16 boxes x |T_M| points).
+__global__ void k_dynmask(ExtractBufs b, int F, int W, int H)
+{
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    DynMask m;
+    m.area_flag = 0;
+    m.nrect = 0;
+    float area = 0.f;
+    const int b0 = b.box_off ? b.box_off[f] : 0, b1 = b.box_off ? b.box_off[f + 1] : 0;
+    const int t0 = b.tm_off ? b.tm_off[f] : 0, t1 = b.tm_off ? b.tm_off[f + 1] : 0;
+    for (int bi = b0; bi < b1; bi++) {
+        const float xmin = b.boxes[4 * bi + 0], ymin = b.boxes[4 * bi + 1];
+        const float xmax = b.boxes[4 * bi + 2], ymax = b.boxes[4 * bi + 3];
+        const int rx = (int)xmin, ry = (int)ymin, rw = (int)(xmax - xmin), rh = (int)(ymax - ymin);
+        const float area_box = (xmax - xmin) * (ymax - ymin);
+        bool mark = false;
+        unsigned long long nin = 0;
+        for (int t = t0; t < t1; t++) {
+            const int px = (int)b.tm[2 * t], py = (int)b.tm[2 * t + 1];
+            const bool in = px >= 0 && px < W && py >= 0 && py < H && px >= rx && px < rx + rw &&
+                            py >= ry && py < ry + rh;
+            if (in) nin++;
+            if ((float)(nin * 10000ull) > area_box) { mark = true; break; }   // layer 1 (:1145)
+        }
+        const int bf = b.blurf ? b.blurf[bi] : 0;
+        if (mark || (bf == 1 && nin > 0)) {                                       // layer 2 (:1168)
+            area = area + area_box;
+            const int x0 = max((int)xmin, 0), x1 = min((int)xmax, W);
+            const int y0 = max((int)ymin, 0), y1 = min((int)ymax, H);
+            if (x1 > x0 && y1 > y0) {
+                if (m.nrect < COEB_MAXBOX) {
+                    m.rect[m.nrect][0] = x0; m.rect[m.nrect][1] = y0;
+                    m.rect[m.nrect][2] = x1; m.rect[m.nrect][3] = y1;
+                    m.nrect++;
+                } else {
+                    atomicOr(b.err, 1);
+                }
+            }
+        }
+    }
+    m.area_flag = area > 200000.f ? 1 : 0;                                      // :1192
+    b.dyn[f] = m;
+}
+
+// ================================ k_pyr_level ================================
+// cv::resize INTER_LINEAR 8U, canonical rounding.  One output pixel per
+// thread, 64 x 4 pixels per workgroup; the source rows are read through L1/L2.
+__global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restrict__ src, int64_t src_fs,
+                                                        int sw, int sh, uint8_t* __restrict__ dst,
+                                                        int64_t dst_fs, int dw, int dh,
+                                                        const int* __restrict__ tab, int xmax)
+{
+    const int f = blockIdx.z;
+    const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (dx >= dw || dy >= dh) return;
+    const int* xofs = tab;
+    const int* alpha = tab + dw;
+    const int* yofs = tab + 2 * dw;
+    const int* beta = tab + 2 * dw + dh;
+    const uint8_t* S = src + (int64_t)f * src_fs;
+    const int sy0 = yofs[dy];
+    const int r0 = sy0 >= 0 ? (sy0 < sh ? sy0 : sh - 1) : 0;
+    const int r1 = sy0 + 1 >= 0 ? (sy0 + 1 < sh ? sy0 + 1 : sh - 1) : 0;
+    const uint8_t* S0 = S + (int64_t)r0 * sw;
+    const uint8_t* S1 = S + (int64_t)r1 * sw;
+    const int sx = xofs[dx];
+    int h0, h1;
+    if (dx < xmax) {
+        const int a = alpha[dx];
+        const int a0 = (int)(short)(a & 0xFFFF), a1 = a >> 16;
+        h0 = S0[sx] * a0 + S0[sx + 1] * a1;
+        h1 = S1[sx] * a0 + S1[sx + 1] * a1;
+    } else {
+        h0 = S0[sx] * 2048;
+        h1 = S1[sx] * 2048;
+    }
+    const int bb = beta[dy];
+    const int b0 = (int)(short)(bb & 0xFFFF), b1 = bb >> 16;
+    int v0 = min(h0 >> 4, 32767), v1 = min(h1 >> 4, 32767);
+    int m0 = (v0 * b0) >> 16, m1 = (v1 * b1) >> 16;       // _mm_mulhi_epi16
+    int s = max(min(m0 + m1, 32767), -32768);              // _mm_adds_epi16
+    s = max(min(s + 2, 32767), -32768) >> 2;
+    dst[(int64_t)f * dst_fs + (int64_t)dy * dw + dx] = (uint8_t)max(0, min(s, 255));
+}
+
+// ================================ k_blur ================================
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), Q8 kernel, Q16 vertical accumulation
+// (DESIGN.md s3.3).  Tile 64 x 16 outputs; (64+6) x (16+6) input staged in LDS.
+constexpr int BT_W = 64, BT_H = 16, BT_IW = BT_W + 6, BT_IH = BT_H + 6;
+
+__device__ __forceinline__ int reflect101(int p, int len)
+{
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
+    return p;
+}
+
+struct BlurTiles {
+    int L;
+    int tiles_x[COEB_MAXL];
+    int tile_off[COEB_MAXL + 1];
+};
+
+__global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, ExtractBufs b, BlurTiles bt)
+{
+    __shared__ uint8_t sin_[BT_IH][BT_IW + 2];
+    __shared__ uint16_t sh_[BT_IH][BT_W];
+    const int f = blockIdx.y;
+    int l = 0;
+    while (l + 1 < bt.L && (int)blockIdx.x >= bt.tile_off[l + 1]) l++;
+    const int t = blockIdx.x - bt.tile_off[l];
+    const int tx = t % bt.tiles_x[l], ty = t / bt.tiles_x[l];
+    const LevelGeom& g = P->lv[l];
+    const int w = g.w, h = g.h;
+    const uint8_t* src = level_ptr(P, b, f, l);
+    uint8_t* dst = b.blur + (int64_t)f * P->blur_stride + g.blur_off;
+    const int ox = tx * BT_W, oy = ty * BT_H;
+    int k[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) k[i] = P->gauss[i];
+    for (int i = threadIdx.x; i < BT_IH * BT_IW; i += kThreads) {
+        const int yy = i / BT_IW, xx = i - yy * BT_IW;
+        const int sy = reflect101(oy + yy - 3, h), sx = reflect101(ox + xx - 3, w);
+        sin_[yy][xx] = src[(int64_t)sy * w + sx];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < BT_IH * BT_W; i += kThreads) {
+        const int yy = i / BT_W, xx = i - yy * BT_W;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int q = 0; q < 7; q++) acc += (uint32_t)k[q] * sin_[yy][xx + q];
+        sh_[yy][xx] = (uint16_t)acc;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < BT_H * BT_W; i += kThreads) {
+        const int yy = i / BT_W, xx = i - yy * BT_W;
+        const int gx = ox + xx, gy = oy + yy;
+        if (gx >= w || gy >= h) continue;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int q = 0; q < 7; q++) acc += (uint32_t)k[q] * sh_[yy + q][xx];
+        const uint32_t o = (acc + (1u << 15)) >> 16;
+        dst[(int64_t)gy * w + gx] = (uint8_t)(o > 255u ? 255u : o);
+    }
+}
+
+// ================================ k_fast ================================
+// One workgroup per (FAST cell, frame).  The cell ROI (<= 64 x 64) is staged in LDS; each
+// detection pixel gets its corner strength M = max over the 16 nine-pixel arcs of
+// min(|v - ring|) taken with the arc's sign.  For threshold t: corner <=> M > t, and
+// OpenCV's cornerScore<16> = M - 1 (derivation: DESIGN.md s4.2).  Per-cell NMS then
+// compares against neighbours' scores (0 outside the detection window), exactly as
+// FAST_t's 3-row buffers do; an empty cell at iniThFAST is redone at minThFAST (:834-838).
+__device__ __forceinline__ int ring_strength(const uint8_t* c, int st, int tmin)
+{
+    const int v = c[0];
+    int p[16];
+    p[0] = c[3 * st];      p[1] = c[3 * st + 1];  p[2] = c[2 * st + 2];  p[3] = c[st + 3];
+    p[4] = c[3];           p[5] = c[-st + 3];     p[6] = c[-2 * st + 2]; p[7] = c[-3 * st + 1];
+    p[8] = c[-3 * st];     p[9] = c[-3 * st - 1]; p[10] = c[-2 * st - 2]; p[11] = c[-st - 3];
+    p[12] = c[-3];         p[13] = c[st - 3];     p[14] = c[2 * st - 2]; p[15] = c[3 * st - 1];
+    // quick reject at the smaller threshold (a corner at tmin must pass OpenCV's pre-test)
+    auto cls = [&](int x) { int d = x - v; return d < -tmin ? 1 : (d > tmin ? 2 : 0); };
+    int d = cls(p[0]) | cls(p[8]);
+    d &= cls(p[2]) | cls(p[10]);
+    d &= cls(p[4]) | cls(p[12]);
+    d &= cls(p[6]) | cls(p[14]);
+    if (d == 0) return 0;
+    int dd[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) dd[i] = v - p[i];
+    int A = -1000, B = -1000;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        int mn = dd[k], mx = dd[k];
+#pragma unroll
+        for (int j = 1; j < 9; j++) {
+            const int x = dd[(k + j) & 15];
+            mn = min(mn, x);
+            mx = max(mx, x);
+        }
+        A = max(A, mn);
+        B = max(B, -mx);
+    }
+    const int M = max(A, B);
+    return M > 0 ? M : 0;
+}
+
+__global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, ExtractBufs b)
+{
+    __shared__ uint8_t roi[kRoiMax * kRoiMax];
+    __shared__ uint8_t Ms[kRoiMax * kRoiMax];
+    __shared__ int sbuf[kWaves + 2];
+    const int cidx = blockIdx.x, f = blockIdx.y;
+    const CellDesc c = b.cells[cidx];
+    const int l = c.level;
+    const LevelGeom& g = P->lv[l];
+    const int area = b.dyn[f].area_flag;
+    const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
+    const uint8_t* img = level_ptr(P, b, f, l);
+    const int rw = c.rw, rh = c.rh;
+    for (int i = threadIdx.x; i < rw * rh; i += kThreads) {
+        const int yy = i / rw, xx = i - yy * rw;
+        roi[yy * kRoiMax + xx] = img[(int64_t)(c.y0 + yy) * g.w + c.x0 + xx];
+        Ms[yy * kRoiMax + xx] = 0;
+    }
+    __syncthreads();
+    const int ww = rw - 6, wh = rh - 6;
+    const int npix = ww > 0 && wh > 0 ? ww * wh : 0;
+    for (int p = threadIdx.x; p < npix; p += kThreads) {
+        const int yy = p / ww + 3, xx = p - (p / ww) * ww + 3;
+        Ms[yy * kRoiMax + xx] = (uint8_t)ring_strength(&roi[yy * kRoiMax + xx], kRoiMax, th_min);
+    }
+    __syncthreads();
+    uint32_t* out = b.cand + ((int64_t)f * P->ncells + cidx) * P->cell_cap;
+    int nkept = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        const int t = pass == 0 ? th_ini : th_min;
+        int running = 0;
+        for (int base = 0; base < npix; base += kThreads) {
+            const int p = base + threadIdx.x;
+            bool kept = false;
+            int yy = 0, xx = 0, s = 0;
+            if (p < npix) {
+                yy = p / ww + 3;
+                xx = p - (p / ww) * ww + 3;
+                const int M = Ms[yy * kRoiMax + xx];
+                if (M > t) {
+                    s = M - 1;
+                    kept = true;
+#pragma unroll
+                    for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; dx++) {
+                            if (dx == 0 && dy == 0) continue;
+                            const int Mn = Ms[(yy + dy) * kRoiMax + xx + dx];
+                            const int ns = Mn > t ? Mn - 1 : 0;
+                            kept = kept && (s > ns);
+                        }
+                }
+            }
+            int tot;
+            const int pre = block_scan_flag(kept, &tot, sbuf);
+            if (kept) {
+                const int o = running + pre;
+                if (o < P->cell_cap)
+                    out[o] = pack_key(xx + c.j * g.wcell, yy + c.i * g.hcell, s);
+                else
+                    atomicOr(b.err, 2);
+            }
+            running += tot;
+        }
+        nkept = running;
+        if (nkept > 0) break;
+    }
+    if (threadIdx.x == 0) b.cand_n[(int64_t)f * P->ncells + cidx] = min(nkept, P->cell_cap);
+}
+
+// ================================ k_octree ================================
+// One workgroup per (level, frame): gathers the level's FAST candidates in the reference
+// order (cell row-major, then FAST row-major), applies the pre-octree cull when area_flag,
+// and emulates DistributeOctTree's std::list exactly (push_front order, erase, the sorted
+// final phase with size ties broken by allocation order = monotonic allocator), then
+// retains the best response per node (first wins ties), adds the border, and applies
+// CheckMovingKeyPoints_finall when !area_flag.  Keys live in two global ping-pong buffers
+// (L2-resident); a node's keys are a contiguous range and DivideNode is a stable 4-way
+// partition of it done by one wave with ballots.  Node records live in two global sets and
+// are compacted into list order after every pass.
+struct NodeRef {
+    int* start; int* cnt; int* alloc; int* buf; int4* rect;
+};
+
+__device__ __forceinline__ NodeRef node_set(uint8_t* nodes_f, const LevelGeom& g, int set)
+{
+    int* base = reinterpret_cast<int*>(nodes_f) + g.node_off + (int64_t)set * 8 * g.ncap;
+    NodeRef r;
+    r.start = base;
+    r.cnt = base + g.ncap;
+    r.alloc = base + 2 * g.ncap;
+    r.buf = base + 3 * g.ncap;
+    r.rect = reinterpret_cast<int4*>(base + 4 * g.ncap);
+    return r;
+}
+
+__device__ __forceinline__ int quadrant(uint32_t k, int sx, int sy)
+{
+    const int x = key_x(k), y = key_y(k);
+    return x < sx ? (y < sy ? 0 : 2) : (y < sy ? 1 : 3);
+}
+
+// Count keys per quadrant of node range [s, s+n) (one wave).
+__device__ __forceinline__ int4 wave_count_quadrants(const uint32_t* src, int s, int n, int sx, int sy)
+{
+    int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    const int lane = lane_id();
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + lane;
+        const bool v = i < n;
+        const int q = v ? quadrant(src[s + i], sx, sy) : -1;
+        c0 += __popcll(__ballot(q == 0));
+        c1 += __popcll(__ballot(q == 1));
+        c2 += __popcll(__ballot(q == 2));
+        c3 += __popcll(__ballot(q == 3));
+    }
+    return make_int4(c0, c1, c2, c3);
+}
+
+// Stable scatter of node range [s, s+n) from src into dst at [s, s+n), quadrant order.
+__device__ __forceinline__ void wave_scatter_quadrants(const uint32_t* src, uint32_t* dst, int s, int n,
+                                                       int sx, int sy, int4 c)
+{
+    int r0 = s, r1 = s + c.x, r2 = s + c.x + c.y, r3 = s + c.x + c.y + c.z;
+    const int lane = lane_id();
+    const uint64_t lt = lanemask_lt();
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + lane;
+        const bool v = i < n;
+        const uint32_t k = v ? src[s + i] : 0u;
+        const int q = v ? quadrant(k, sx, sy) : -1;
+        const uint64_t m0 = __ballot(q == 0), m1 = __ballot(q == 1), m2 = __ballot(q == 2), m3 = __ballot(q == 3);
+        if (v) {
+            const uint64_t mq = q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
+            const int rq = q == 0 ? r0 : q == 1 ? r1 : q == 2 ? r2 : r3;
+            dst[rq + __popcll(mq & lt)] = k;
+        }
+        r0 += __popcll(m0); r1 += __popcll(m1); r2 += __popcll(m2); r3 += __popcll(m3);
+    }
+}
+
+__device__ __forceinline__ void child_rect(const int4 p, int q, int4* out, int* sx, int* sy)
+{
+    const int hx = (int)ceilf((float)(p.z - p.x) / 2);   // ExtractorNode::DivideNode :491-492
+    const int hy = (int)ceilf((float)(p.w - p.y) / 2);
+    const int mx = p.x + hx, my = p.y + hy;
+    *sx = mx; *sy = my;
+    if (q == 0) *out = make_int4(p.x, p.y, mx, my);
+    else if (q == 1) *out = make_int4(mx, p.y, p.z, my);
+    else if (q == 2) *out = make_int4(p.x, my, mx, p.w);
+    else *out = make_int4(mx, my, p.z, p.w);
+}
+
+constexpr int OCT_LMAX = 1024;   // max live list / work items per phase (host plan asserts)
+
+__global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P, ExtractBufs b)
+{
+    __shared__ int sbuf[kWaves + 2];
+    __shared__ int s_work[OCT_LMAX];      // slot ids of nodes divided this phase (processing order)
+    __shared__ int4 s_cnt[OCT_LMAX];      // their quadrant counts
+    __shared__ int s_base[OCT_LMAX];      // exclusive prefix of nonempty children (push order)
+    __shared__ int s_rank[OCT_LMAX];      // final phase: processing rank of vPrev entry
+    __shared__ int s_push[OCT_LMAX];      // final phase: push-order base per rank
+    __shared__ uint8_t s_dead[OCT_LMAX];  // final phase: slot erased this round
+
+    const int l = blockIdx.x, f = blockIdx.y;
+    const LevelGeom& g = P->lv[l];
+    const int tid = threadIdx.x, wv = tid >> 6, lane = lane_id();
+    const DynMask dm = b.dyn[f];
+    const int area = dm.area_flag;
+    const int N = area ? g.nfeat_area : g.nfeat;
+    uint32_t* KB[2];
+    KB[0] = b.keys + (int64_t)f * 2 * P->kbuf_stride + g.kcap_off;
+    KB[1] = KB[0] + P->kbuf_stride;
+    uint8_t* nodes_f = b.nodes + (int64_t)f * P->node_stride * 4;
+
+    // ---- 1. gather candidates in reference order ----
+    const int* cn = b.cand_n + (int64_t)f * P->ncells + g.cell0;
+    const uint32_t* cand = b.cand + ((int64_t)f * P->ncells + g.cell0) * P->cell_cap;
+    int K = 0;
+    {
+        int carry = 0;
+        for (int base = 0; base < g.ncells; base += kThreads) {
+            const int ci = base + tid;
+            const int v = ci < g.ncells ? cn[ci] : 0;
+            int tot;
+            const int pre = block_scan_excl(v, &tot, sbuf);
+            // copy: each thread copies its own cell (cells are small)
+            if (ci < g.ncells) {
+                const uint32_t* src = cand + (int64_t)ci * P->cell_cap;
+                uint32_t* dst = KB[0] + carry + pre;
+                for (int q = 0; q < v; q++) dst[q] = src[q];
+            }
+            carry += tot;
+        }
+        K = carry;
+    }
+    __syncthreads();
+    int kb = 0;   // buffer currently holding the candidates
+    // ---- pre-octree cull (ORBextractor.cc:854-858; coordinates still relative, reference quirk)
+    if (area) {
+        const float scale = (l != 0) ? g.scale : 1.0f;
+        int carry = 0;
+        for (int base = 0; base < K; base += kThreads) {
+            const int i = base + tid;
+            uint32_t k = 0;
+            bool keep = false;
+            if (i < K) {
+                k = KB[0][i];
+                keep = !masked_out(dm, (float)key_x(k), (float)key_y(k), scale, P->W, P->H);
+            }
+            int tot;
+            const int pre = block_scan_flag(keep, &tot, sbuf);
+            if (keep) KB[1][carry + pre] = k;
+            carry += tot;
+        }
+        K = carry;
+        kb = 1;
+        __syncthreads();
+    }
+
+    // ---- 2. initial nodes (:549-592) ----
+    int n = 0;             // live list length (list order == slot order in set `cs`)
+    int cs = 0;            // current node set
+    int alloc_ctr = g.nini;
+    {
+        NodeRef S = node_set(nodes_f, g, 0);
+        if (g.nini == 1) {
+            if (K > 0 && tid == 0) {
+                S.start[0] = 0; S.cnt[0] = K; S.alloc[0] = 0; S.buf[0] = kb;
+                S.rect[0] = make_int4((int)(g.hx * 0.f), 0, (int)(g.hx * 1.f), g.maxY);
+            }
+            n = K > 0 ? 1 : 0;
+        } else {
+            // stable multiway distribution by (int)(x / hX) into the other buffer
+            int carry = 0;
+            for (int i = 0; i < g.nini; i++) {
+                const int lo = g.ini_bound[i], hi = g.ini_bound[i + 1];
+                const int start = carry;
+                for (int base = 0; base < K; base += kThreads) {
+                    const int idx = base + tid;
+                    uint32_t k = 0;
+                    bool in = false;
+                    if (idx < K) {
+                        k = KB[kb][idx];
+                        in = key_x(k) >= lo && key_x(k) < hi;
+                    }
+                    int tot;
+                    const int pre = block_scan_flag(in, &tot, sbuf);
+                    if (in) KB[kb ^ 1][carry + pre] = k;
+                    carry += tot;
+                }
+                if (carry > start) {
+                    if (tid == 0) {
+                        S.start[n] = start; S.cnt[n] = carry - start; S.alloc[n] = i; S.buf[n] = kb ^ 1;
+                        S.rect[n] = make_int4((int)(g.hx * (float)i), 0, (int)(g.hx * (float)(i + 1)), g.maxY);
+                    }
+                    n++;
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- 3. main loop (:601-745) ----
+    bool finish = false;
+    bool final_phase = false;
+    while (!finish) {
+        const int prevSize = n;
+        if (n > OCT_LMAX || n > g.ncap) { if (tid == 0) atomicOr(b.err, 4); finish = true; break; }
+        NodeRef S = node_set(nodes_f, g, cs), D = node_set(nodes_f, g, cs ^ 1);
+        // divided nodes = cnt > 1, in list order
+        int nd = 0;
+        for (int base = 0; base < n; base += kThreads) {
+            const int k = base + tid;
+            const bool dv = k < n && S.cnt[k] > 1;
+            int tot;
+            const int pre = block_scan_flag(dv, &tot, sbuf);
+            if (dv) s_work[nd + pre] = k;
+            nd += tot;
+        }
+        __syncthreads();
+        // partition: one wave per divided node
+        for (int j = wv; j < nd; j += kWaves) {
+            const int k = s_work[j];
+            const int s = S.start[k], c = S.cnt[k], bf = S.buf[k];
+            const int4 r = S.rect[k];
+            int4 tmp; int sx, sy;
+            child_rect(r, 0, &tmp, &sx, &sy);
+            const int4 qc = wave_count_quadrants(KB[bf], s, c, sx, sy);
+            wave_scatter_quadrants(KB[bf], KB[bf ^ 1], s, c, sx, sy, qc);
+            if (lane == 0) s_cnt[j] = qc;
+        }
+        __syncthreads();
+        // children alloc order = divided nodes in list order, n1..n4 nonempty
+        int T = 0, nexp = 0;
+        for (int base = 0; base < nd; base += kThreads) {
+            const int j = base + tid;
+            int e = 0, x = 0;
+            if (j < nd) {
+                const int4 q = s_cnt[j];
+                e = (q.x > 0) + (q.y > 0) + (q.z > 0) + (q.w > 0);
+                x = (q.x > 1) + (q.y > 1) + (q.z > 1) + (q.w > 1);
+            }
+            int tot, tot2;
+            const int pre = block_scan_excl(e, &tot, sbuf);
+            block_scan_excl(x, &tot2, sbuf);
+            if (j < nd) s_base[j] = T + pre;
+            T += tot;
+            nexp += tot2;
+        }
+        __syncthreads();
+        const int nnew = T + (n - nd);
+        if (nnew > g.ncap) { if (tid == 0) atomicOr(b.err, 4); finish = true; break; }
+        // write children (reverse push order at the front)
+        for (int j = tid; j < nd; j += kThreads) {
+            const int k = s_work[j];
+            const int4 q = s_cnt[j];
+            const int s = S.start[k], bf = S.buf[k];
+            const int4 r = S.rect[k];
+            int a = s_base[j];
+            int off = s;
+            const int qq[4] = {q.x, q.y, q.z, q.w};
+            for (int c4 = 0; c4 < 4; c4++) {
+                if (qq[c4] > 0) {
+                    const int pos = T - 1 - a;
+                    int4 cr; int sx, sy;
+                    child_rect(r, c4, &cr, &sx, &sy);
+                    D.start[pos] = off; D.cnt[pos] = qq[c4]; D.alloc[pos] = alloc_ctr + a;
+                    D.buf[pos] = bf ^ 1; D.rect[pos] = cr;
+                    a++;
+                }
+                off += qq[c4];
+            }
+        }
+        // non-divided nodes keep their relative order after the children
+        {
+            int carry = 0;
+            for (int base = 0; base < n; base += kThreads) {
+                const int k = base + tid;
+                const bool keep = k < n && S.cnt[k] <= 1;
+                int tot;
+                const int pre = block_scan_flag(keep, &tot, sbuf);
+                if (keep) {
+                    const int pos = T + carry + pre;
+                    D.start[pos] = S.start[k]; D.cnt[pos] = S.cnt[k]; D.alloc[pos] = S.alloc[k];
+                    D.buf[pos] = S.buf[k]; D.rect[pos] = S.rect[k];
+                }
+                carry += tot;
+            }
+        }
+        __syncthreads();
+        alloc_ctr += T;
+        n = nnew;
+        cs ^= 1;
+        if (n >= N || n == prevSize) { finish = true; break; }
+        if (n + nexp * 3 > N) { final_phase = true; break; }
+    }
+
+    // ---- 3b. final phase (:683-743) ----
+    while (final_phase && !finish) {
+        const int prevSize = n;
+        if (n > OCT_LMAX) { if (tid == 0) atomicOr(b.err, 4); break; }
+        NodeRef S = node_set(nodes_f, g, cs), D = node_set(nodes_f, g, cs ^ 1);
+        // vPrev = list nodes with cnt > 1, i.e. vSizeAndPointerToNode of the previous round
+        int m = 0;
+        for (int base = 0; base < n; base += kThreads) {
+            const int k = base + tid;
+            const bool dv = k < n && S.cnt[k] > 1;
+            int tot;
+            const int pre = block_scan_flag(dv, &tot, sbuf);
+            if (dv) s_work[m + pre] = k;
+            m += tot;
+        }
+        for (int k = tid; k < n; k += kThreads) s_dead[k] = 0;
+        __syncthreads();
+        // quadrant counts of every vPrev node (one wave per node)
+        for (int j = wv; j < m; j += kWaves) {
+            const int k = s_work[j];
+            int4 tmp; int sx, sy;
+            child_rect(S.rect[k], 0, &tmp, &sx, &sy);
+            const int4 qc = wave_count_quadrants(KB[S.buf[k]], S.start[k], S.cnt[k], sx, sy);
+            if (lane == 0) s_cnt[j] = qc;
+        }
+        // sort(vPrev) by (size, node) ascending and walk from the back: rank 0 = largest size,
+        // ties -> later allocation first (pointer order of a monotonic allocator)
+        for (int j = tid; j < m; j += kThreads) {
+            const int k = s_work[j];
+            const int cj = S.cnt[k], aj = S.alloc[k];
+            int rank = 0;
+            for (int i = 0; i < m; i++) {
+                const int ki = s_work[i];
+                const int ci = S.cnt[ki], ai = S.alloc[ki];
+                rank += (ci > cj) || (ci == cj && ai > aj);
+            }
+            s_rank[j] = rank;
+        }
+        __syncthreads();
+        for (int j = tid; j < m; j += kThreads) s_base[s_rank[j]] = j;
+        __syncthreads();
+        // list size after processing rank r is n + sum_{r'<=r}(e-1); the first r reaching N breaks
+        int nproc = m;
+        {
+            int carry = 0, found = 0x7fffffff;
+            for (int base = 0; base < m; base += kThreads) {
+                const int r = base + tid;
+                int d = 0;
+                if (r < m) {
+                    const int4 q = s_cnt[s_base[r]];
+                    d = (q.x > 0) + (q.y > 0) + (q.z > 0) + (q.w > 0) - 1;
+                }
+                int tot;
+                const int pre = block_scan_excl(d, &tot, sbuf);
+                if (r < m && n + carry + pre + d >= N) found = min(found, r);
+                carry += tot;
+            }
+            int fr = found;
+            for (int o = 32; o > 0; o >>= 1) fr = min(fr, __shfl_xor(fr, o, 64));
+            if (lane == 0) sbuf[wv] = fr;
+            __syncthreads();
+            int mn = 0x7fffffff;
+            for (int i = 0; i < kWaves; i++) mn = min(mn, sbuf[i]);
+            __syncthreads();
+            if (mn != 0x7fffffff) nproc = mn + 1;
+        }
+        // push order = processing order, children n1..n4 nonempty
+        int T = 0;
+        for (int base = 0; base < nproc; base += kThreads) {
+            const int r = base + tid;
+            int e = 0;
+            if (r < nproc) {
+                const int4 q = s_cnt[s_base[r]];
+                e = (q.x > 0) + (q.y > 0) + (q.z > 0) + (q.w > 0);
+            }
+            int tot;
+            const int pre = block_scan_excl(e, &tot, sbuf);
+            if (r < nproc) s_push[r] = T + pre;
+            T += tot;
+        }
+        for (int j = tid; j < m; j += kThreads)
+            if (s_rank[j] < nproc) s_dead[s_work[j]] = 1;
+        __syncthreads();
+        const int nnew = T + n - nproc;
+        if (nnew > g.ncap) { if (tid == 0) atomicOr(b.err, 4); break; }
+        // DivideNode of the processed nodes + push_front of their children
+        for (int r = wv; r < nproc; r += kWaves) {
+            const int j = s_base[r];
+            const int k = s_work[j];
+            const int s = S.start[k], c = S.cnt[k], bf = S.buf[k];
+            const int4 pr = S.rect[k];
+            int4 tmp; int sx, sy;
+            child_rect(pr, 0, &tmp, &sx, &sy);
+            const int4 qc = s_cnt[j];
+            wave_scatter_quadrants(KB[bf], KB[bf ^ 1], s, c, sx, sy, qc);
+            if (lane == 0) {
+                int a = s_push[r];
+                int off = s;
+                const int qq[4] = {qc.x, qc.y, qc.z, qc.w};
+                for (int c4 = 0; c4 < 4; c4++) {
+                    if (qq[c4] > 0) {
+                        const int pos = T - 1 - a;
+                        int4 cr; int ssx, ssy;
+                        child_rect(pr, c4, &cr, &ssx, &ssy);
+                        D.start[pos] = off; D.cnt[pos] = qq[c4]; D.alloc[pos] = alloc_ctr + a;
+                        D.buf[pos] = bf ^ 1; D.rect[pos] = cr;
+                        a++;
+                    }
+                    off += qq[c4];
+                }
+            }
+        }
+        // erase processed nodes, keep the rest in list order behind the children
+        {
+            int carry = 0;
+            for (int base = 0; base < n; base += kThreads) {
+                const int k = base + tid;
+                const bool keep = k < n && !s_dead[k];
+                int tot;
+                const int pre = block_scan_flag(keep, &tot, sbuf);
+                if (keep) {
+                    const int pos = T + carry + pre;
+                    D.start[pos] = S.start[k]; D.cnt[pos] = S.cnt[k]; D.alloc[pos] = S.alloc[k];
+                    D.buf[pos] = S.buf[k]; D.rect[pos] = S.rect[k];
+                }
+                carry += tot;
+            }
+        }
+        __syncthreads();
+        alloc_ctr += T;
+        n = nnew;
+        cs ^= 1;
+        if (n >= N || n == prevSize) finish = true;
+    }
+
+    // ---- 4. retain the best response per node (:747-766), border, final cull ----
+    NodeRef S = node_set(nodes_f, g, cs);
+    uint32_t* out = b.lvl_kp + (int64_t)f * P->lvl_stride + g.out_off;
+    const bool cull = !area && l < 8;                  // CheckMovingKeyPoints_finall loops 8 levels
+    const float scale = (l != 0) ? g.scale : 1.0f;
+    int carry = 0;
+    for (int base = 0; base < n; base += kThreads) {
+        const int k = base + tid;
+        uint32_t best = 0;
+        bool keep = false;
+        if (k < n) {
+            const uint32_t* src = KB[S.buf[k]] + S.start[k];
+            const int c = S.cnt[k];
+            best = src[0];
+            int maxr = key_s(best);
+            for (int q = 1; q < c; q++) {
+                const uint32_t kk = src[q];
+                if (key_s(kk) > maxr) { best = kk; maxr = key_s(kk); }
+            }
+            const int x = key_x(best) + 16, y = key_y(best) + 16;   // :886-887 (minBorderX/Y)
+            best = pack_key(x, y, key_s(best));
+            keep = !(cull && masked_out(dm, (float)x, (float)y, scale, P->W, P->H));
+        }
+        int tot;
+        const int pre = block_scan_flag(keep, &tot, sbuf);
+        if (keep) {
+            if (carry + pre < g.out_cap) out[carry + pre] = best;
+            else atomicOr(b.err, 8);
+        }
+        carry += tot;
+    }
+    if (tid == 0) b.lvl_n[(int64_t)f * P->L + l] = min(carry, g.out_cap);
+}
+
+// ================================ k_describe ================================
+// One wave per keypoint: IC_Angle on the unblurred level (lanes over patch columns, two
+// row halves), fastAtan2, canonical sincosf, 256 rBRIEF tests (4 per lane) on the blurred
+// level, output in cv::KeyPoint layout.
+__device__ float fast_atan2_dev(float y, float x)
+{
+    const float p1 = 0.9997878412794807f * (float)(180 / 3.1415926535897932384626433832795);
+    const float p3 = -0.3258083974640975f * (float)(180 / 3.1415926535897932384626433832795);
+    const float p5 = 0.1555786518463281f * (float)(180 / 3.1415926535897932384626433832795);
+    const float p7 = -0.04432655554792128f * (float)(180 / 3.1415926535897932384626433832795);
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)2.2204460492503131e-16);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)2.2204460492503131e-16);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// canonical sincosf, identical operation sequence to the oracle
+__device__ void sincos_canon(float af, float* s, float* c)
+{
+    const double two_over_pi = 6.36619772367581382433e-01;
+    const double pio2_1 = 1.57079632673412561417e+00;
+    const double pio2_1t = 6.07710050650619224932e-11;
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double x = (double)af;
+    const double kd = rint(x * two_over_pi);
+    double r = __builtin_fma(-kd, pio2_1, x);
+    r = __builtin_fma(-kd, pio2_1t, r);
+    const double z = r * r;
+    const double v = z * r;
+    const double sr = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    const double sn = r + v * (S1 + z * sr);
+    const double cr = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double cs = w + (((1.0 - w) - hz) + z * cr);
+    const int q = ((int)kd) & 3;
+    double so, co;
+    if (q == 0) { so = sn; co = cs; }
+    else if (q == 1) { so = cs; co = -sn; }
+    else if (q == 2) { so = -sn; co = -cs; }
+    else { so = -cs; co = sn; }
+    *s = (float)so;
+    *c = (float)co;
+}
+
+struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
+
+__global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ P, ExtractBufs b)
+{
+    __shared__ int off[COEB_MAXL + 1];
+    const int f = blockIdx.y;
+    const int L = P->L;
+    if (threadIdx.x == 0) {
+        int s = 0;
+        for (int l = 0; l < L; l++) { off[l] = s; s += b.lvl_n[(int64_t)f * L + l]; }
+        off[L] = s;
+        if (blockIdx.x == 0) b.counts[f] = s;
+    }
+    __syncthreads();
+    const int total = off[L];
+    const int wv = threadIdx.x >> 6, lane = lane_id();
+    for (int sidx = 0; sidx < 4; sidx++) {
+        const int idx = blockIdx.x * 16 + wv * 4 + sidx;
+        if (idx >= total) break;
+        int l = 0;
+        while (l + 1 < L && idx >= off[l + 1]) l++;
+        const LevelGeom& g = P->lv[l];
+        const uint32_t key = b.lvl_kp[(int64_t)f * P->lvl_stride + g.out_off + (idx - off[l])];
+        const int x = key_x(key), y = key_y(key), sc = key_s(key);
+        const int st = g.w;
+        // IC_Angle (ORBextractor.cc:80-107)
+        const uint8_t* img = level_ptr(P, b, f, l);
+        const uint8_t* center = img + (int64_t)y * st + x;
+        const int h = lane >> 5;
+        const int u = (lane & 31) - 15;
+        const bool uv = (lane & 31) < 31;
+        int m10 = 0, m01 = 0;
+        if (h == 0 && uv) m10 += u * center[u];
+        const int v0 = h == 0 ? 1 : 9, v1 = h == 0 ? 8 : 15;
+        for (int v = v0; v <= v1; v++) {
+            const int d = P->umax[v];
+            if (uv && u >= -d && u <= d) {
+                const int vp = center[u + v * st], vm = center[u - v * st];
+                m01 += v * (vp - vm);
+                m10 += u * (vp + vm);
+            }
+        }
+        m10 = wave_sum(m10);
+        m01 = wave_sum(m01);
+        const float angle = fast_atan2_dev((float)m01, (float)m10);
+        // descriptor (ORBextractor.cc:109-156), fused rotation forms of the reference binary
+        const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
+        float bs, ac;
+        sincos_canon(angle * factorPI, &bs, &ac);
+        const uint8_t* bl = b.blur + (int64_t)f * P->blur_stride + g.blur_off + (int64_t)y * st + x;
+        int nib = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int test = 4 * lane + t;
+            const float px0 = (float)b.pattern[4 * test + 0], py0 = (float)b.pattern[4 * test + 1];
+            const float px1 = (float)b.pattern[4 * test + 2], py1 = (float)b.pattern[4 * test + 3];
+            const int r0 = (int)rintf(__builtin_fmaf(px0, bs, py0 * ac));
+            const int c0 = (int)rintf(__builtin_fmaf(px0, ac, -(py0 * bs)));
+            const int r1 = (int)rintf(__builtin_fmaf(px1, bs, py1 * ac));
+            const int c1 = (int)rintf(__builtin_fmaf(px1, ac, -(py1 * bs)));
+            const int t0 = bl[r0 * st + c0], t1 = bl[r1 * st + c1];
+            nib |= (t0 < t1) << t;
+        }
+        const int other = __shfl_xor(nib, 1, 64);
+        uint8_t* dd = b.desc + ((int64_t)f * P->kcap + idx) * 32;
+        if ((lane & 1) == 0) dd[lane >> 1] = (uint8_t)(nib | (other << 4));
+        if (lane == 0) {
+            KeyPointOut o;
+            o.x = (float)x;
+            o.y = (float)y;
+            if (l != 0) { o.x *= g.scale; o.y *= g.scale; }          // :1327-1334
+            o.size = (float)g.size_i;
+            o.angle = angle;
+            o.response = (float)sc;
+            o.octave = l;
+            o.class_id = -1;
+            reinterpret_cast<KeyPointOut*>(b.kps)[(int64_t)f * P->kcap + idx] = o;
+        }
+    }
+}
+
+}  // namespace
+
+int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, int F, hipStream_t s,
+                   ProfileHook* prof)
+{
+    prof_begin(prof, "k_dynmask", s);
+    hipLaunchKernelGGL(k_dynmask, dim3((F + 63) / 64), dim3(64), 0, s, b, F, plan.W, plan.H);
+    prof_end(prof, s);
+    for (int l = 1; l < plan.L; l++) {
+        const LevelGeom& g = plan.lv[l];
+        const LevelGeom& gp = plan.lv[l - 1];
+        const uint8_t* src = l == 1 ? b.gray : b.pyr + gp.pyr_off;
+        const int64_t src_fs = l == 1 ? (int64_t)plan.W * plan.H : plan.pyr_stride;
+        prof_begin(prof, "k_pyr_level", s);
+        hipLaunchKernelGGL(k_pyr_level, dim3((g.w + 63) / 64, (g.h + 3) / 4, F), dim3(kThreads), 0, s, src, src_fs,
+                           gp.w, gp.h, b.pyr + g.pyr_off, plan.pyr_stride, g.w, g.h, b.rtab + g.rtab_off, g.xmax);
+        prof_end(prof, s);
+    }
+    BlurTiles bt;
+    bt.L = plan.L;
+    int tiles = 0;
+    for (int l = 0; l < plan.L; l++) {
+        bt.tiles_x[l] = (plan.lv[l].w + BT_W - 1) / BT_W;
+        bt.tile_off[l] = tiles;
+        tiles += bt.tiles_x[l] * ((plan.lv[l].h + BT_H - 1) / BT_H);
+    }
+    bt.tile_off[plan.L] = tiles;
+    prof_begin(prof, "k_blur", s);
+    hipLaunchKernelGGL(k_blur, dim3(tiles, F), dim3(kThreads), 0, s, d_plan, b, bt);
+    prof_end(prof, s);
+    prof_begin(prof, "k_fast", s);
+    hipLaunchKernelGGL(k_fast, dim3(plan.ncells, F), dim3(kThreads), 0, s, d_plan, b);
+    prof_end(prof, s);
+    prof_begin(prof, "k_octree", s);
+    hipLaunchKernelGGL(k_octree, dim3(plan.L, F), dim3(kThreads), 0, s, d_plan, b);
+    prof_end(prof, s);
+    prof_begin(prof, "k_describe", s);
+    hipLaunchKernelGGL(k_describe, dim3((plan.kcap + 15) / 16, F), dim3(kThreads), 0, s, d_plan, b);
+    prof_end(prof, s);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

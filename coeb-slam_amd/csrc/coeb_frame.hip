@@ -1,0 +1,146 @@
+// coeb_frame.hip -- per-frame pre-filter kernels around the extractor:
+//   Frame blur flag: crop -> Laplacian(CV_16U, ksize 1) -> mean < 4.2   src/Frame.cc:171-202, 905-913
+//   Tracking::GrabImageRGBD: cvtColor RGB2GRAY (8U, 14-bit fixed point), depth 16U -> 32F x scale
+//                                                                       src/Tracking.cc:207-228
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/coeb_front.h"
+#include "coeb_internal.hpp"
+
+namespace {
+
+__device__ __forceinline__ int reflect101(int p, int len)
+{
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
+    return p;
+}
+
+// one workgroup per box: Laplacian [0 1 0; 1 -4 1; 0 1 0] on the cloned crop (REFLECT_101 at
+// the crop edge), negatives saturate to 0 (saturate_cast<ushort>), exact integer sum,
+// cv::mean = sum * (1./count).
+__global__ __launch_bounds__(256) void k_blur_flags(const uint8_t* __restrict__ img, int W, int H, int stride,
+                                                    const float* __restrict__ boxes, int* __restrict__ out,
+                                                    double* __restrict__ mean_out)
+{
+    __shared__ unsigned long long s_part[4];
+    const int bi = blockIdx.x;
+    const float x0f = boxes[4 * bi], y0f = boxes[4 * bi + 1], x1f = boxes[4 * bi + 2], y1f = boxes[4 * bi + 3];
+    const int rx = (int)x0f, ry = (int)y0f, rw = (int)(x1f - x0f), rh = (int)(y1f - y0f);
+    if (rx < 0 || ry < 0 || rw <= 0 || rh <= 0 || rx + rw > W || ry + rh > H) {
+        if (threadIdx.x == 0) { out[bi] = 0; if (mean_out) mean_out[bi] = -1.0; }
+        return;
+    }
+    const uint8_t* c = img + (int64_t)ry * stride + rx;
+    unsigned long long acc = 0;
+    for (int i = threadIdx.x; i < rw * rh; i += 256) {
+        const int y = i / rw, x = i - y * rw;
+        const int ym = reflect101(y - 1, rh), yp = reflect101(y + 1, rh);
+        const int xm = reflect101(x - 1, rw), xp = reflect101(x + 1, rw);
+        const int lap = c[(int64_t)ym * stride + x] + c[(int64_t)yp * stride + x] + c[(int64_t)y * stride + xm] +
+                        c[(int64_t)y * stride + xp] - 4 * c[(int64_t)y * stride + x];
+        acc += lap > 0 ? (unsigned)lap : 0u;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (__lane_id() == 0) s_part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long S = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+        const double mean = (double)S * (1. / (double)((long long)rw * rh));
+        out[bi] = mean < 4.2 ? 1 : 0;
+        if (mean_out) mean_out[bi] = mean;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_rgbd(const uint8_t* __restrict__ rgb, int rgb_stride, int rgb_order,
+                                              const uint16_t* __restrict__ d16, int dstride, float dscale, int W,
+                                              int H, uint8_t* __restrict__ gray, float* __restrict__ depth)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= W || y >= H) return;
+    if (rgb) {
+        const uint8_t* s = rgb + (int64_t)y * rgb_stride + 3 * x;
+        const int R2Y = 4899, G2Y = 9617, B2Y = 1868;
+        const int v = rgb_order ? (s[0] * R2Y + s[1] * G2Y + s[2] * B2Y) : (s[0] * B2Y + s[1] * G2Y + s[2] * R2Y);
+        gray[(int64_t)y * W + x] = (uint8_t)((v + (1 << 13)) >> 14);
+    }
+    if (d16) depth[(int64_t)y * W + x] = (float)d16[(int64_t)y * dstride + x] * dscale;
+}
+
+}  // namespace
+
+// host entry points (C-ABI); context internals are reached through small accessors in
+// coeb_capi.hip
+extern "C" int coeb_internal_stream(coeb_ctx* c, hipStream_t* s, int* device);
+extern "C" int coeb_internal_scratch(coeb_ctx* c, const char* name, size_t bytes, void** p);
+extern "C" int coeb_internal_error(coeb_ctx* c, int code, const char* msg);
+
+#define FR_TRY(c, expr)                                                                         \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess) return coeb_internal_error((c), COEB_EDEVICE, hipGetErrorString(_e)); \
+    } while (0)
+
+extern "C" int coeb_blur_flags(coeb_ctx* c, const uint8_t* gray, int W, int H, size_t stride, const coeb_box* boxes,
+                               int nbox, int32_t* flags_out)
+{
+    if (!c || nbox < 0 || (nbox > 0 && (!gray || !boxes || !flags_out)) || stride < (size_t)W)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_blur_flags: invalid arguments");
+    if (nbox == 0) return COEB_OK;
+    hipStream_t s;
+    int dev;
+    if (coeb_internal_stream(c, &s, &dev)) return COEB_EINVAL;
+    (void)hipSetDevice(dev);
+    void *dimg, *dbox, *dout;
+    int rc;
+    if ((rc = coeb_internal_scratch(c, "bf_img", (size_t)W * H, &dimg)) ||
+        (rc = coeb_internal_scratch(c, "bf_box", (size_t)nbox * 16, &dbox)) ||
+        (rc = coeb_internal_scratch(c, "bf_out", (size_t)nbox * 4, &dout)))
+        return rc;
+    FR_TRY(c, hipMemcpy2DAsync(dimg, W, gray, stride, W, H, hipMemcpyHostToDevice, s));
+    FR_TRY(c, hipMemcpyAsync(dbox, boxes, (size_t)nbox * 16, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_blur_flags, dim3(nbox), dim3(256), 0, s, (const uint8_t*)dimg, W, H, W, (const float*)dbox,
+                       (int*)dout, (double*)nullptr);
+    FR_TRY(c, hipGetLastError());
+    FR_TRY(c, hipMemcpyAsync(flags_out, dout, (size_t)nbox * 4, hipMemcpyDeviceToHost, s));
+    FR_TRY(c, hipStreamSynchronize(s));
+    return COEB_OK;
+}
+
+extern "C" int coeb_rgbd_preprocess(coeb_ctx* c, const uint8_t* rgb, size_t rgb_stride, int rgb_order,
+                                    const uint16_t* depth16, size_t depth_stride, float depth_scale, int W, int H,
+                                    uint8_t* gray_out, float* depth_out)
+{
+    if (!c || W <= 0 || H <= 0 || (rgb && (!gray_out || rgb_stride < (size_t)3 * W)) ||
+        (depth16 && (!depth_out || depth_stride < (size_t)W)))
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_rgbd_preprocess: invalid arguments");
+    hipStream_t s;
+    int dev;
+    if (coeb_internal_stream(c, &s, &dev)) return COEB_EINVAL;
+    (void)hipSetDevice(dev);
+    void *drgb = nullptr, *dgray = nullptr, *dd16 = nullptr, *ddep = nullptr;
+    int rc;
+    if (rgb) {
+        if ((rc = coeb_internal_scratch(c, "pp_rgb", (size_t)W * H * 3, &drgb)) ||
+            (rc = coeb_internal_scratch(c, "pp_gray", (size_t)W * H, &dgray)))
+            return rc;
+        FR_TRY(c, hipMemcpy2DAsync(drgb, (size_t)3 * W, rgb, rgb_stride, (size_t)3 * W, H, hipMemcpyHostToDevice, s));
+    }
+    if (depth16) {
+        if ((rc = coeb_internal_scratch(c, "pp_d16", (size_t)W * H * 2, &dd16)) ||
+            (rc = coeb_internal_scratch(c, "pp_dep", (size_t)W * H * 4, &ddep)))
+            return rc;
+        FR_TRY(c, hipMemcpy2DAsync(dd16, (size_t)2 * W, depth16, depth_stride * 2, (size_t)2 * W, H,
+                                   hipMemcpyHostToDevice, s));
+    }
+    hipLaunchKernelGGL(k_rgbd, dim3((W + 63) / 64, (H + 3) / 4), dim3(256), 0, s, (const uint8_t*)drgb, 3 * W, rgb_order,
+                       (const uint16_t*)dd16, W, depth_scale, W, H, (uint8_t*)dgray, (float*)ddep);
+    FR_TRY(c, hipGetLastError());
+    if (rgb) FR_TRY(c, hipMemcpyAsync(gray_out, dgray, (size_t)W * H, hipMemcpyDeviceToHost, s));
+    if (depth16) FR_TRY(c, hipMemcpyAsync(depth_out, ddep, (size_t)W * H * 4, hipMemcpyDeviceToHost, s));
+    FR_TRY(c, hipStreamSynchronize(s));
+    return COEB_OK;
+}

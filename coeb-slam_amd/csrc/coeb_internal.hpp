@@ -1,0 +1,176 @@
+// coeb_internal.hpp -- shared host/device definitions of the MI355X ORB front end.
+//
+// HBM layout (per frame slot f of a context, all packed, byte offsets 256-aligned):
+//   gray      [f][H][W]                 u8   level 0 (caller's device buffer or ctx staging)
+//   pyr       [f][pyr_stride]           u8   levels 1..L-1, level l at pyr_off[l], row stride W_l
+//   blur      [f][blur_stride]          u8   7x7 Gaussian of levels 0..L-1 (descriptor input)
+//   cand_n    [f][ncells]               i32  FAST corners kept per cell
+//   cand      [f][ncells][cell_cap]     u32  packed (x_rel | y_rel<<12 | score<<24), row-major
+//   keys      [f][2][kbuf_stride]       u32  octree key ping-pong buffers (per level kcap_off)
+//   nodes     [f][L][2][NCAP] records        octree node scratch (start,cnt,rect,alloc)
+//   lvl_n     [f][L]                    i32  keypoints per level after culls
+//   lvl_kp    [f][lvl_stride]           u32  packed level keypoints in output order
+//   kps       [f][kcap]                 28B  coeb_keypoint (== cv::KeyPoint)
+//   desc      [f][kcap][32]             u8
+//   dyn       [f]                       DynMask (area flag + zeroed rectangles)
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+#define COEB_MAXL 16
+#define COEB_MAXBOX 16
+#define COEB_GRID_COLS 64
+#define COEB_GRID_ROWS 48
+#define COEB_GRID_CELLS (COEB_GRID_COLS * COEB_GRID_ROWS)
+
+// Per-level geometry and offsets, computed on the host once per (W, H) and copied to the
+// device as one POD block (kernel argument).
+struct LevelGeom {
+    int w, h;
+    int64_t pyr_off;       // into pyr frame block (-1 for level 0)
+    int64_t blur_off;      // into blur frame block
+    int rtab_off;          // into resize table (ints): xofs[w], alpha[w], yofs[h], beta[h]
+    int xmax;              // resize: columns >= xmax use S[sx]*2048
+    int ncols, nrows, wcell, hcell;
+    int cell0, ncells;     // range in the cell table (row-major over non-skipped cells)
+    int kcap_off, kcap;    // octree key buffers: offset / capacity (u32 entries)
+    int nfeat, nfeat_area; // DistributeOctTree N: mnFeaturesPerLevel[l], (int)(N*0.7)
+    int nini;              // initial octree nodes
+    float hx;              // (maxX-minX)/nIni
+    int ini_bound[5];      // initial node i holds x_rel in [ini_bound[i], ini_bound[i+1])
+    int ncap;              // node record capacity per set
+    int64_t node_off;      // into node scratch (records) per frame
+    int out_cap, out_off;  // level keypoint capacity / offset into lvl_kp frame block
+    float scale;           // mvScaleFactor[l]
+    int size_i;            // (int)(PATCH_SIZE * scale)
+    int maxX, maxY;        // octree box: maxBorderX - minBorderX, maxBorderY - minBorderY
+};
+
+struct Plan {
+    int W, H, L;
+    LevelGeom lv[COEB_MAXL];
+    int ncells;            // all levels
+    int cell_cap;          // u32 entries per cell slot
+    int max_roi_w, max_roi_h;
+    int64_t pyr_stride, blur_stride;
+    int64_t kbuf_stride;   // u32 entries per key buffer (x2 per frame)
+    int64_t node_stride;   // node records per frame (all levels, both sets)
+    int lvl_stride;        // u32 entries per frame in lvl_kp
+    int kcap;              // output keypoints per frame (sum of out_cap)
+    int rtab_ints;
+    int umax[16];
+    int gauss[7];
+};
+
+// FAST cell descriptor (ORBextractor.cc:811-829): ROI in level coordinates
+struct CellDesc {
+    int16_t level, pad;
+    int16_t x0, y0;        // iniX, iniY
+    int16_t rw, rh;        // maxX-iniX, maxY-iniY (ROI; detection window = inset 3)
+    int16_t i, j;          // cell row / column (for x_rel/y_rel offsets)
+};
+
+// Dynamic-object mask of one frame (ORBextractor.cc:1101-1195): the mask is the complement of
+// the union of these rectangles (x in [x0,x1), y in [y0,y1)), so the W x H byte mask never
+// needs to be materialised.
+struct DynMask {
+    int area_flag;
+    int nrect;
+    int rect[COEB_MAXBOX][4];
+};
+
+struct NodeSet {           // SoA node records (one set of a level)
+    int* start;
+    int* cnt;
+    int4* rect;            // x0, y0, x1, y1 (relative coordinates)
+    int* alloc;
+    int* buf;
+};
+
+static inline __host__ __device__ uint32_t pack_key(int x, int y, int s)
+{
+    return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)s << 24);
+}
+static inline __host__ __device__ int key_x(uint32_t k) { return (int)(k & 0xFFFu); }
+static inline __host__ __device__ int key_y(uint32_t k) { return (int)((k >> 12) & 0xFFFu); }
+static inline __host__ __device__ int key_s(uint32_t k) { return (int)(k >> 24); }
+
+// ---- launch wrappers (coeb_extract.hip / coeb_match.hip) ----
+struct ExtractBufs {
+    const uint8_t* gray;   // [F][H][W]
+    uint8_t* pyr;
+    uint8_t* blur;
+    int* cand_n;
+    uint32_t* cand;
+    uint32_t* keys;
+    uint8_t* nodes;        // raw node scratch
+    int* lvl_n;
+    uint32_t* lvl_kp;
+    void* kps;             // coeb_keypoint
+    uint8_t* desc;
+    int* counts;
+    DynMask* dyn;
+    const int* rtab;
+    const CellDesc* cells;
+    const int8_t* pattern; // 512 x (x, y)
+    // dynamic-mask inputs
+    const float* boxes;    // [nbox_total][4]
+    const int* box_off;    // [F+1]
+    const float* tm;       // [ntm_total][2]
+    const int* tm_off;     // [F+1]
+    const int* blurf;      // [nbox_total]
+    int* err;              // device error word (capacity overflows)
+};
+
+struct ProfileHook {
+    void* impl = nullptr;   // owned by the context (coeb_capi.hip)
+};
+void prof_begin(ProfileHook* p, const char* name, hipStream_t s);
+void prof_end(ProfileHook* p, hipStream_t s);
+
+int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, int F, hipStream_t s,
+                   ProfileHook* prof);
+
+struct MatchCam {
+    float fx, fy, cx, cy, bf, mb;
+    float min_x, max_x, min_y, max_y;
+    float grid_inv_w, grid_inv_h;
+    float scale[COEB_MAXL];
+};
+struct MatchBufs {
+    // current frames
+    const void* cur_kps;       // coeb_keypoint [P][cur_stride]
+    const uint8_t* cur_desc;   // [P][cur_stride][32]
+    const int* cur_n;          // [P]
+    const float* cur_ur;       // [P][cur_stride] (may be computed by prep)
+    int cur_stride;
+    // last frames
+    const void* last_kps;      // coeb_keypoint [P][last_stride]
+    const uint8_t* last_desc;  // [P][last_stride][32] MapPoint descriptors
+    const int* last_n;         // [P]
+    const uint8_t* last_has;   // [P][last_stride]
+    const uint8_t* last_out;   // [P][last_stride]
+    const float* last_xw;      // [P][last_stride][3]
+    const int* last_nobs;      // [P][last_stride]
+    int last_stride;
+    const float* Tcw_cur;      // [P][16]
+    const float* Tcw_last;     // [P][16]
+    int* match;                // [P][cur_stride]
+    int* nmatch;               // [P]
+    int* scratch;              // [P][scratch_stride]
+    int scratch_stride;
+    int* err;
+};
+int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int bmono, int check_ori,
+                 int retry_below, hipStream_t s, ProfileHook* prof);
+
+// frame preparation for batch matching: u_right/depth per keypoint + LastFrame map snapshot
+struct PrepBufs {
+    const void* kps; const int* n; int stride;
+    const float* depth; int W, H;
+    float bf, fx, fy, cx, cy;
+    float* ur; float* dep;
+    uint8_t* has; uint8_t* outl; float* xw; int* nobs; int nobs_value;
+    const float* Twc;          // [F][16] inverse poses for UnprojectStereo (may be NULL = I)
+};
+int launch_prep(const PrepBufs& b, int F, hipStream_t s, ProfileHook* prof);

@@ -1,0 +1,196 @@
+/*
+ * coeb_front.h -- C-ABI of the MI355X-native COEB-SLAM per-frame ORB front end.
+ *
+ * Plain C: pointers, sizes and POD structs only (no OpenCV, no torch types).  Every entry
+ * point names the reference interface it replaces (paths are into biscuitzb/COEB-SLAM):
+ *
+ *   coeb_create / coeb_orb_tables   <- ORBextractor::ORBextractor(nfeatures, scaleFactor,
+ *                                      nlevels, iniThFAST, minThFAST)  include/ORBextractor.h:50-51,
+ *                                      src/ORBextractor.cc:418-477, accessors ORBextractor.h:77-99
+ *   coeb_extract                    <- ORBextractor::operator()(image, mask, img, imD, keypoints,
+ *                                      descriptors, box, T_M, mask_result, blur_flag)
+ *                                      include/ORBextractor.h:73-75, src/ORBextractor.cc:1088-1342
+ *   coeb_extract_batch_device       <- the same, for a device-resident batch of frames
+ *   coeb_blur_flags                 <- Frame RGB-D ctor blur-flag loop + Frame::detect_laplacian
+ *                                      src/Frame.cc:171-202, 905-913
+ *   coeb_rgbd_preprocess            <- Tracking::GrabImageRGBD cvtColor / depth convertTo
+ *                                      src/Tracking.cc:207-228
+ *   coeb_stereo_from_rgbd           <- Frame::ComputeStereoFromRGBD  src/Frame.cc:820-842
+ *   coeb_match_lastframe            <- ORBmatcher::SearchByProjection(Frame&, const Frame&,
+ *                                      const float th, const bool bMono)
+ *                                      include/ORBmatcher.h:52, src/ORBmatcher.cc:1329-1471
+ *                                      (with Frame::GetFeaturesInArea / AssignFeaturesToGrid,
+ *                                      src/Frame.cc:396-411, 503-568)
+ *   coeb_descriptor_distance        <- ORBmatcher::DescriptorDistance  src/ORBmatcher.cc:1648-1664
+ *
+ * Conventions: 0 on success, negative COEB_E* code on failure (the reference has no error
+ * returns: it asserts or is UB).  The caller owns host buffers; the context
+ * owns device buffers and streams.  One context per host thread; calls are not reentrant.
+ */
+#ifndef COEB_FRONT_H
+#define COEB_FRONT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define COEB_OK 0
+#define COEB_EINVAL (-22)    /* bad argument / shape outside the context limits */
+#define COEB_ENOMEM (-12)    /* device allocation failed */
+#define COEB_EDEVICE (-5)    /* HIP runtime error (see coeb_last_error) */
+#define COEB_ERANGE (-34)    /* an internal capacity was exceeded (see coeb_last_error) */
+#define COEB_ENODEV (-19)    /* no usable gfx950 device */
+
+#define COEB_MAX_LEVELS 16
+#define COEB_MAX_BOXES 16
+
+typedef struct coeb_ctx coeb_ctx;
+
+/* ORBextractor ctor arguments.  iniThFAST/minThFAST are accepted but, as in the reference,
+ * overridden per frame to 20/7 (30/10 when the dynamic area exceeds 200000 px)
+ * (src/ORBextractor.cc:775-784). */
+typedef struct {
+    int32_t nfeatures;
+    float scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+} coeb_orb_params;
+
+/* layout-identical to cv::KeyPoint {Point2f pt; float size, angle, response; int octave, class_id;} */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} coeb_keypoint;
+
+/* YOLO person box, xyxy, as std::vector<float>{xmin,ymin,xmax,ymax} (ros_rgbd.cc:106-115) */
+typedef struct {
+    float xmin, ymin, xmax, ymax;
+} coeb_box;
+
+/* ORBextractor accessors (include/ORBextractor.h:77-99) and derived per-level constants */
+typedef struct {
+    int32_t nlevels;
+    float scale_factor;
+    float scale[COEB_MAX_LEVELS];          /* GetScaleFactors() */
+    float inv_scale[COEB_MAX_LEVELS];      /* GetInverseScaleFactors() */
+    float sigma2[COEB_MAX_LEVELS];         /* GetScaleSigmaSquares() */
+    float inv_sigma2[COEB_MAX_LEVELS];     /* GetInverseScaleSigmaSquares() */
+    int32_t features_per_level[COEB_MAX_LEVELS];
+    int32_t umax[16];
+} coeb_orb_tables;
+
+/* Camera + Frame constants used by the matcher (Frame.cc:231-246, ComputeImageBounds :611-641) */
+typedef struct {
+    float fx, fy, cx, cy;
+    float bf;                   /* mbf */
+    float min_x, max_x, min_y, max_y;
+} coeb_camera;
+
+/* Snapshot of the previous Frame taken by the caller (MapPoint accessors under their mutexes):
+ * ORBmatcher.cc:1352-1396 reads exactly these. */
+typedef struct {
+    int32_t n;                        /* LastFrame.N */
+    const uint8_t* has_mappoint;      /* LastFrame.mvpMapPoints[i] != NULL */
+    const uint8_t* outlier;           /* LastFrame.mvbOutlier[i] */
+    const float* world_pos;           /* n x 3, MapPoint::GetWorldPos() */
+    const uint8_t* mp_descriptor;     /* n x 32, MapPoint::GetDescriptor() */
+    const int32_t* mp_observations;   /* MapPoint::Observations() */
+    const coeb_keypoint* keys_un;     /* LastFrame.mvKeysUn (octave, angle) */
+} coeb_lastframe;
+
+/* The current Frame (after ExtractORB + ComputeStereoFromRGBD) */
+typedef struct {
+    int32_t n;                        /* CurrentFrame.N */
+    const coeb_keypoint* keys_un;     /* CurrentFrame.mvKeysUn */
+    const uint8_t* descriptors;       /* n x 32 */
+    const float* u_right;             /* CurrentFrame.mvuRight */
+} coeb_curframe;
+
+/* ---- context ---- */
+coeb_ctx* coeb_create(const coeb_orb_params* params, int device, int max_width, int max_height,
+                      int max_batch);
+void coeb_destroy(coeb_ctx* ctx);
+const char* coeb_last_error(const coeb_ctx* ctx);   /* also valid with ctx == NULL */
+int coeb_orb_tables_get(const coeb_ctx* ctx, coeb_orb_tables* out);
+/* keypoint capacity per frame needed by coeb_extract for a w x h image */
+int coeb_max_keypoints(const coeb_ctx* ctx, int width, int height);
+
+/* ---- ORBextractor::operator() on one host frame ----
+ * gray: 8UC1 (stride in bytes).  boxes/T_M/blur_flag as passed by Frame::ExtractORB.
+ * Writes up to `cap` keypoints and their 32-byte descriptors; *n_out = keypoint count.
+ * An empty image (width or height 0) returns COEB_OK with *n_out = 0 (:1096-1097). */
+int coeb_extract(coeb_ctx* ctx, const uint8_t* gray, int width, int height, size_t stride,
+                 const coeb_box* boxes, int nbox, const float* tm_xy, int ntm,
+                 const int32_t* blur_flag, int nblur,
+                 coeb_keypoint* kp_out, uint8_t* desc_out, int cap, int* n_out);
+
+/* ---- device-resident batch (the throughput path) ----
+ * d_gray: device pointer, nframes x height x width bytes, packed.  boxes/T_M/blur flags are
+ * host arrays: per frame f, boxes[box_off[f] .. box_off[f+1]) etc. (offset arrays of length
+ * nframes+1; all may be NULL for "no boxes").  Results stay on the device; fetch them with
+ * coeb_batch_results.  Enqueued on the context stream; returns without synchronising. */
+int coeb_extract_batch_device(coeb_ctx* ctx, const uint8_t* d_gray, int nframes, int width, int height,
+                              const coeb_box* boxes, const int32_t* box_off,
+                              const float* tm_xy, const int32_t* tm_off,
+                              const int32_t* blur_flag);
+/* Device pointers to the batch outputs: keypoints [nframes][kcap], descriptors
+ * [nframes][kcap][32], counts [nframes]. */
+int coeb_batch_results(coeb_ctx* ctx, const coeb_keypoint** d_kps, const uint8_t** d_desc,
+                       const int32_t** d_counts, int* kcap);
+
+/* Batch TrackWithMotionModel matching (Tracking.cc:933-958 call pattern): for f = 1..nframes-1
+ * frame f is matched to frame f-1 of the last extracted batch: LastFrame map points are the
+ * keypoints of f-1 with depth > 0 unprojected with Tcw_prev (Frame::UnprojectStereo,
+ * Frame.cc:844-858), observations = nobs; SearchByProjection(th) and, if < 20 matches,
+ * again with 2*th.  d_depth: nframes x height x width float (device).  Tcw: nframes x 16 host
+ * floats (row-major 4x4).  Results: coeb_batch_match_results. */
+int coeb_match_batch_device(coeb_ctx* ctx, const float* d_depth, int nframes, int width, int height,
+                            const coeb_camera* cam, const float* Tcw, float th, int32_t nobs);
+int coeb_batch_match_results(coeb_ctx* ctx, const int32_t** d_match, const int32_t** d_nmatches);
+
+/* ---- ORBmatcher::SearchByProjection(CurrentFrame, LastFrame, th, bMono) ----
+ * match_out[i2] (length cur->n) = index of the LastFrame slot whose MapPoint was assigned to
+ * current keypoint i2 (CurrentFrame.mvpMapPoints[i2]), or -1; *nmatches = the return value.
+ * CurrentFrame.mvpMapPoints is taken as all-NULL on entry (Tracking.cc:943). */
+int coeb_match_lastframe(coeb_ctx* ctx, const coeb_camera* cam, const coeb_curframe* cur,
+                         const coeb_lastframe* last, const float Tcw_cur[16], const float Tcw_last[16],
+                         float th, int bmono, int check_orientation, int32_t* match_out, int* nmatches);
+
+/* ---- Frame helpers ---- */
+int coeb_blur_flags(coeb_ctx* ctx, const uint8_t* gray, int width, int height, size_t stride,
+                    const coeb_box* boxes, int nbox, int32_t* flags_out);
+int coeb_stereo_from_rgbd(coeb_ctx* ctx, const coeb_keypoint* kps, int n, const float* depth,
+                          int width, int height, size_t depth_stride_floats, float bf,
+                          float* u_right_out, float* depth_out);
+/* rgb: 8UC3 (rgb_order=1: RGB as Camera.RGB=1; 0: BGR); depth16: 16UC1 scaled by depth_scale
+ * (= 1/DepthMapFactor) to float.  Either input may be NULL. */
+int coeb_rgbd_preprocess(coeb_ctx* ctx, const uint8_t* rgb, size_t rgb_stride, int rgb_order,
+                         const uint16_t* depth16, size_t depth_stride, float depth_scale,
+                         int width, int height, uint8_t* gray_out, float* depth_out);
+
+int coeb_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* ---- measurement ---- */
+/* Per-kernel device time accumulated with HIP events on the context stream while profiling
+ * is enabled.  names: comma-separated list written to `names` (cap bytes). */
+int coeb_profile_enable(coeb_ctx* ctx, int enable);
+int coeb_profile_read(coeb_ctx* ctx, char* names, int cap, double* total_ms, int64_t* launches,
+                      int max_kernels, int* nkernels);
+int coeb_profile_reset(coeb_ctx* ctx);
+int coeb_synchronize(coeb_ctx* ctx);
+int coeb_device_count(void);
+
+/* Test support: copy an intermediate buffer of frame `frame` of the last batch to the host.
+ * what: "pyr" (levels 1..L-1, packed), "blur" (levels 0..L-1), "cand_n" (FAST corners per
+ * cell), "lvl_n" (keypoints per level), "lvl_kp" (packed level keypoints), "dyn" (mask
+ * rectangles), "plan".  Copies min(bytes, size); *size_out = full size. */
+int coeb_debug_read(coeb_ctx* ctx, const char* what, int frame, void* host, size_t bytes, size_t* size_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

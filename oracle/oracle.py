@@ -1,0 +1,223 @@
+"""ctypes binding of oracle/liborb_oracle.so.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker / timed CPU baseline.  The product never imports it.
+Parity vs the original reference binary: UNPINNED (see orb_oracle.h).
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liborb_oracle.so")
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+MAX_LEVELS = 16
+
+
+class Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_double), ("nlevels", C.c_int),
+                ("ini_th", C.c_int), ("min_th", C.c_int),
+                ("scale", C.c_float * MAX_LEVELS), ("inv_scale", C.c_float * MAX_LEVELS),
+                ("sigma2", C.c_float * MAX_LEVELS), ("inv_sigma2", C.c_float * MAX_LEVELS),
+                ("nfeat", C.c_int * MAX_LEVELS), ("umax", C.c_int * 16),
+                ("pattern", (C.c_int * 2) * 512)]
+
+
+class Debug(C.Structure):
+    _fields_ = [("pyramid", C.c_void_p), ("level_off", C.c_int64 * (MAX_LEVELS + 1)),
+                ("ncand", C.c_int * MAX_LEVELS), ("nkept", C.c_int * MAX_LEVELS),
+                ("area_flag", C.c_int)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("bf", C.c_float), ("mb", C.c_float),
+                ("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float),
+                ("grid_inv_w", C.c_float), ("grid_inv_h", C.c_float),
+                ("scale", C.c_float * MAX_LEVELS), ("nlevels", C.c_int)]
+
+
+class LastFrame(C.Structure):
+    _fields_ = [("n", C.c_int), ("has_mp", C.c_void_p), ("outlier", C.c_void_p), ("xw", C.c_void_p),
+                ("mp_desc", C.c_void_p), ("mp_nobs", C.c_void_p), ("keys_un", C.c_void_p)]
+
+
+class CurFrame(C.Structure):
+    _fields_ = [("n", C.c_int), ("keys_un", C.c_void_p), ("desc", C.c_void_p), ("uright", C.c_void_p)]
+
+
+class Grid(C.Structure):
+    _fields_ = [("cell_start", C.c_void_p), ("cell_idx", C.c_void_p)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = C.CDLL(LIB)
+        _lib.oc_fast_atan2.restype = C.c_float
+        _lib.oc_fast_atan2.argtypes = [C.c_float, C.c_float]
+        _lib.oc_sincos.argtypes = [C.c_float, C.c_void_p, C.c_void_p]
+    return _lib
+
+
+def ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class Extractor:
+    """ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST) on the CPU oracle."""
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7):
+        self.p = Params()
+        rc = lib().oc_init(C.byref(self.p), nfeatures, C.c_float(scale_factor), nlevels, ini_th, min_th)
+        assert rc == 0
+
+    @property
+    def nlevels(self):
+        return self.p.nlevels
+
+    def level_sizes(self, w, h):
+        out = []
+        for l in range(self.p.nlevels):
+            lw, lh = C.c_int(), C.c_int()
+            lib().oc_level_size(C.byref(self.p), w, h, l, C.byref(lw), C.byref(lh))
+            out.append((lw.value, lh.value))
+        return out
+
+    def extract(self, gray, boxes=None, tm=None, blur=None, debug=False):
+        gray = np.ascontiguousarray(gray, dtype=np.uint8)
+        h, w = gray.shape
+        boxes = np.zeros((0, 4), np.float32) if boxes is None else np.ascontiguousarray(boxes, np.float32)
+        tm = np.zeros((0, 2), np.float32) if tm is None else np.ascontiguousarray(tm, np.float32)
+        blur = np.zeros(0, np.int32) if blur is None else np.ascontiguousarray(blur, np.int32)
+        cap = 8 * self.p.nfeatures + 256
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int()
+        dbg = Debug()
+        pyr = None
+        if debug:
+            total = sum(a * b for a, b in self.level_sizes(w, h))
+            pyr = np.zeros(total, np.uint8)
+            dbg.pyramid = pyr.ctypes.data
+        rc = lib().oc_extract(C.byref(self.p), ptr(gray), w, h, w, ptr(boxes), len(boxes), ptr(tm), len(tm),
+                              ptr(blur), len(blur), ptr(kps), ptr(desc), cap, C.byref(n), C.byref(dbg))
+        if rc != 0:
+            raise RuntimeError("oc_extract rc=%d" % rc)
+        n = n.value
+        res = dict(kps=kps[:n].copy(), desc=desc[:n].copy())
+        if debug:
+            res["pyramid"] = pyr
+            res["level_off"] = list(dbg.level_off[: self.p.nlevels + 1])
+            res["ncand"] = list(dbg.ncand[: self.p.nlevels])
+            res["nkept"] = list(dbg.nkept[: self.p.nlevels])
+            res["area_flag"] = dbg.area_flag
+        return res
+
+
+def camera(ex, w, h, fx, fy, cx, cy, bf):
+    c = Camera()
+    lib().oc_camera_init(C.byref(c), C.c_float(fx), C.c_float(fy), C.c_float(cx), C.c_float(cy),
+                         C.c_float(bf), w, h, C.byref(ex.p))
+    return c
+
+
+def stereo_from_rgbd(kps, depth, bf):
+    n = len(kps)
+    ur = np.zeros(n, np.float32)
+    dep = np.zeros(n, np.float32)
+    depth = np.ascontiguousarray(depth, np.float32)
+    lib().oc_stereo_from_rgbd(ptr(kps), n, ptr(depth), depth.shape[1], depth.shape[1], C.c_float(bf),
+                              ptr(ur), ptr(dep))
+    return ur, dep
+
+
+def search_by_projection(cam, cur_kps, cur_desc, cur_ur, last, Tcw_cur, Tcw_last, th=15.0, bmono=False,
+                         check_ori=True):
+    """last: dict(has_mp u8[n], outlier u8[n], xw f32[n,3], mp_desc u8[n,32], mp_nobs i32[n], keys_un KP[n])"""
+    cur_kps = np.ascontiguousarray(cur_kps)
+    cur_desc = np.ascontiguousarray(cur_desc, np.uint8)
+    cur_ur = np.ascontiguousarray(cur_ur, np.float32)
+    cf = CurFrame(len(cur_kps), cur_kps.ctypes.data, cur_desc.ctypes.data, cur_ur.ctypes.data)
+    arrs = {k: np.ascontiguousarray(v) for k, v in last.items()}
+    lf = LastFrame(len(arrs["has_mp"]), arrs["has_mp"].ctypes.data, arrs["outlier"].ctypes.data,
+                   arrs["xw"].ctypes.data, arrs["mp_desc"].ctypes.data, arrs["mp_nobs"].ctypes.data,
+                   arrs["keys_un"].ctypes.data)
+    out = np.zeros(max(len(cur_kps), 1), np.int32)
+    Tc = np.ascontiguousarray(Tcw_cur, np.float32)
+    Tl = np.ascontiguousarray(Tcw_last, np.float32)
+    nm = lib().oc_search_by_projection(C.byref(cam), C.byref(cf), C.byref(lf), ptr(Tc), ptr(Tl),
+                                       C.c_float(th), int(bmono), int(check_ori), ptr(out))
+    return nm, out[: len(cur_kps)]
+
+
+def blur_flags(gray, boxes):
+    gray = np.ascontiguousarray(gray, np.uint8)
+    boxes = np.ascontiguousarray(boxes, np.float32)
+    out = np.zeros(len(boxes), np.int32)
+    mean = np.zeros(len(boxes), np.float64)
+    h, w = gray.shape
+    lib().oc_blur_flags(ptr(gray), w, h, w, ptr(boxes), len(boxes), ptr(out), ptr(mean))
+    return out, mean
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().oc_descriptor_distance(ptr(a), ptr(b))
+
+
+def fast_atan2(y, x):
+    return lib().oc_fast_atan2(C.c_float(y), C.c_float(x))
+
+
+def sincos(a):
+    s, c = C.c_float(), C.c_float()
+    lib().oc_sincos(C.c_float(a), C.byref(s), C.byref(c))
+    return s.value, c.value
+
+
+def gauss_kernel7():
+    k = (C.c_int * 7)()
+    lib().oc_gauss_kernel7(k)
+    return list(k)
+
+
+def rgb2gray(rgb, rgb_order=1):
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    h, w, _ = rgb.shape
+    out = np.zeros((h, w), np.uint8)
+    lib().oc_rgb2gray(ptr(rgb), w, h, 3 * w, rgb_order, ptr(out))
+    return out
+
+
+def mapframe_from_extraction(kps, desc, depth, cam_fx, cam_fy, cam_cx, cam_cy, bf, nobs=2):
+    """LastFrame snapshot from an extracted frame with Tcw = I: MapPoint = UnprojectStereo(i)
+    (src/Frame.cc:844-858) for every keypoint with depth > 0, descriptor = its own."""
+    ur, dep = stereo_from_rgbd(kps, depth, bf)
+    n = len(kps)
+    has = (dep > 0).astype(np.uint8)
+    z = dep.astype(np.float32)
+    invfx = np.float32(1.0) / np.float32(cam_fx)
+    invfy = np.float32(1.0) / np.float32(cam_fy)
+    u = kps["x"].astype(np.float32)
+    v = kps["y"].astype(np.float32)
+    x = ((u - np.float32(cam_cx)) * z) * invfx
+    y = ((v - np.float32(cam_cy)) * z) * invfy
+    xw = np.stack([x, y, z], axis=1).astype(np.float32)
+    return dict(has_mp=has, outlier=np.zeros(n, np.uint8), xw=np.ascontiguousarray(xw),
+                mp_desc=np.ascontiguousarray(desc, np.uint8), mp_nobs=np.full(n, nobs, np.int32),
+                keys_un=np.ascontiguousarray(kps))

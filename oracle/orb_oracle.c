@@ -1,0 +1,1157 @@
+/*
+ * orb_oracle.c -- literal, single-threaded CPU restatement of COEB-SLAM's ORB front end.
+ *
+ * TEST INFRASTRUCTURE ONLY (see orb_oracle.h): the checker for the HIP path and the
+ * timed CPU baseline ("port").  Parity vs the original binary is UNPINNED (OpenCV 3.4
+ * absent, no reference tests); the canonical OpenCV-primitive definitions are DESIGN.md s3.
+ *
+ * Build: gcc -O3 -march=native -ffp-contract=off -shared -fPIC (oracle/Makefile).
+ * -ffp-contract=off matters: every fused multiply-add below is an explicit fma()/fmaf()
+ * placed where the reference binary fused (SURVEY.md s7 hard part 3); all else is unfused.
+ */
+#include "orb_oracle.h"
+
+#include <math.h>
+
+#define OC_PI 3.1415926535897932384626433832795   /* CV_PI */
+#include <stdlib.h>
+#include <string.h>
+
+static const int PATTERN_31[1024] = {
+#include "../data/orb_bit_pattern_31.inc"
+};
+
+enum { PATCH_SIZE = 31, HALF_PATCH_SIZE = 15, EDGE_THRESHOLD = 19 };
+
+/* ---- OpenCV 3.4 scalar helpers (core/fast_math.hpp) ---- */
+static inline int cv_round(float v) { return (int)lrintf(v); }     /* half to even */
+static inline int cv_round_d(double v) { return (int)lrint(v); }
+static inline int cv_floor(float v) { int i = (int)v; return i - (i > v); }
+static inline int cv_floor_d(double v) { int i = (int)v; return i - (i > v); }
+static inline int cv_ceil_d(double v) { int i = (int)v; return i + (i < v); }
+static inline int imin(int a, int b) { return a < b ? a : b; }
+static inline int imax(int a, int b) { return a > b ? a : b; }
+static inline short sat_short(int v) { return (short)(v < -32768 ? -32768 : v > 32767 ? 32767 : v); }
+static inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+/* ================= ORBextractor ctor: src/ORBextractor.cc:418-477 ================= */
+int oc_init(oc_params* p, int nfeatures, float scale_factor, int nlevels, int ini_th, int min_th)
+{
+    if (nlevels < 1 || nlevels > OC_MAX_LEVELS) return -1;
+    memset(p, 0, sizeof(*p));
+    p->nfeatures = nfeatures;
+    p->scale_factor = scale_factor;                 /* float -> double member */
+    p->nlevels = nlevels;
+    p->ini_th = ini_th;
+    p->min_th = min_th;
+    p->scale[0] = 1.0f;
+    p->sigma2[0] = 1.0f;
+    for (int i = 1; i < nlevels; i++) {               /* :426-430, float * double -> float */
+        p->scale[i] = (float)((double)p->scale[i - 1] * p->scale_factor);
+        p->sigma2[i] = p->scale[i] * p->scale[i];
+    }
+    for (int i = 0; i < nlevels; i++) {               /* :434-438 */
+        p->inv_scale[i] = 1.0f / p->scale[i];
+        p->inv_sigma2[i] = 1.0f / p->sigma2[i];
+    }
+    float factor = (float)(1.0f / p->scale_factor);  /* :443 */
+    float ndesired = nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)nlevels));
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; l++) {           /* :447-453 */
+        p->nfeat[l] = cv_round(ndesired);
+        sum += p->nfeat[l];
+        ndesired *= factor;
+    }
+    p->nfeat[nlevels - 1] = imax(nfeatures - sum, 0);
+    for (int i = 0; i < 512; i++) {                   /* :455-457 */
+        p->pattern[i][0] = PATTERN_31[2 * i];
+        p->pattern[i][1] = PATTERN_31[2 * i + 1];
+    }
+    /* umax :461-476 */
+    int v, v0;
+    int vmax = cv_floor(HALF_PATCH_SIZE * sqrtf(2.f) / 2 + 1);
+    int vmin = cv_ceil_d(HALF_PATCH_SIZE * sqrtf(2.f) / 2);
+    const double hp2 = HALF_PATCH_SIZE * HALF_PATCH_SIZE;
+    for (v = 0; v <= vmax; ++v) p->umax[v] = cv_round_d(sqrt(hp2 - v * v));
+    for (v = HALF_PATCH_SIZE, v0 = 0; v >= vmin; --v) {
+        while (p->umax[v0] == p->umax[v0 + 1]) ++v0;
+        p->umax[v] = v0;
+        ++v0;
+    }
+    return 0;
+}
+
+/* ComputePyramid level size (src/ORBextractor.cc:1348-1349) */
+void oc_level_size(const oc_params* p, int w, int h, int level, int* lw, int* lh)
+{
+    float s = p->inv_scale[level];
+    *lw = cv_round((float)w * s);
+    *lh = cv_round((float)h * s);
+}
+
+/* ============ cv::resize INTER_LINEAR, CV_8U (imgproc resize.cpp, OpenCV 3.4) ============
+ * Coefficients: 11-bit fixed point, computed exactly as resize()'s table setup.
+ * Horizontal pass: exact int (HResizeLinear).  Vertical pass: the SIMD rounding
+ * (VResizeLinearVec_32s8u: ((S0>>4)*b0>>16) + ((S1>>4)*b1>>16), +2 >> 2), applied to
+ * every column -- canonical definition, DESIGN.md s3.1. */
+void oc_resize_linear(const uint8_t* src, int sw, int sh, int sstride,
+                      uint8_t* dst, int dw, int dh, int dstride)
+{
+    if (sw == dw && sh == dh) {                       /* resize(): same size -> copy */
+        for (int y = 0; y < dh; y++) memcpy(dst + (size_t)y * dstride, src + (size_t)y * sstride, dw);
+        return;
+    }
+    double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
+    double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+    int* xofs = (int*)malloc(sizeof(int) * dw);
+    short* ialpha = (short*)malloc(sizeof(short) * 2 * dw);
+    int* yofs = (int*)malloc(sizeof(int) * dh);
+    short* ibeta = (short*)malloc(sizeof(short) * 2 * dh);
+    int xmax = dw;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw) {
+            xmax = imin(xmax, dx);
+            if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        }
+        xofs[dx] = sx;
+        float c0 = 1.f - fx, c1 = fx;
+        ialpha[2 * dx] = sat_short(cv_round(c0 * 2048));
+        ialpha[2 * dx + 1] = sat_short(cv_round(c1 * 2048));
+    }
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floor(fy);
+        fy -= sy;
+        yofs[dy] = sy;
+        float c0 = 1.f - fy, c1 = fy;
+        ibeta[2 * dy] = sat_short(cv_round(c0 * 2048));
+        ibeta[2 * dy + 1] = sat_short(cv_round(c1 * 2048));
+    }
+    int* h0 = (int*)malloc(sizeof(int) * dw);
+    int* h1 = (int*)malloc(sizeof(int) * dw);
+    for (int dy = 0; dy < dh; dy++) {
+        int sy0 = yofs[dy];
+        int r0 = sy0 >= 0 ? (sy0 < sh ? sy0 : sh - 1) : 0;          /* clip(sy, 0, sh) */
+        int r1 = sy0 + 1 >= 0 ? (sy0 + 1 < sh ? sy0 + 1 : sh - 1) : 0;
+        const uint8_t* S0 = src + (size_t)r0 * sstride;
+        const uint8_t* S1 = src + (size_t)r1 * sstride;
+        for (int dx = 0; dx < dw; dx++) {
+            int sx = xofs[dx];
+            if (dx < xmax) {
+                int a0 = ialpha[2 * dx], a1 = ialpha[2 * dx + 1];
+                h0[dx] = S0[sx] * a0 + S0[sx + 1] * a1;
+                h1[dx] = S1[sx] * a0 + S1[sx + 1] * a1;
+            } else {
+                h0[dx] = S0[sx] * 2048;
+                h1[dx] = S1[sx] * 2048;
+            }
+        }
+        int b0 = ibeta[2 * dy], b1 = ibeta[2 * dy + 1];
+        uint8_t* D = dst + (size_t)dy * dstride;
+        for (int dx = 0; dx < dw; dx++) {
+            int v0 = sat_short(h0[dx] >> 4), v1 = sat_short(h1[dx] >> 4);
+            int m0 = (v0 * b0) >> 16, m1 = (v1 * b1) >> 16;   /* _mm_mulhi_epi16 */
+            int s = sat_short(m0 + m1);                         /* _mm_adds_epi16 */
+            s = sat_short(s + 2) >> 2;
+            D[dx] = sat_u8(s);
+        }
+    }
+    free(h0); free(h1); free(xofs); free(ialpha); free(yofs); free(ibeta);
+}
+
+/* ComputePyramid (src/ORBextractor.cc:1344-1367): cascaded level l from level l-1. The
+ * 19-px REFLECT_101 border frame is not materialised: no output-affecting read touches it
+ * on the RGB-D path. */
+int oc_pyramid(const oc_params* p, const uint8_t* gray, int w, int h, int stride,
+               uint8_t* out, int64_t* level_off)
+{
+    int64_t off = 0;
+    for (int l = 0; l < p->nlevels; l++) {
+        int lw, lh;
+        oc_level_size(p, w, h, l, &lw, &lh);
+        level_off[l] = off;
+        uint8_t* dst = out + off;
+        if (l == 0) {
+            for (int y = 0; y < h; y++) memcpy(dst + (size_t)y * lw, gray + (size_t)y * stride, w);
+        } else {
+            int pw, ph;
+            oc_level_size(p, w, h, l - 1, &pw, &ph);
+            oc_resize_linear(out + level_off[l - 1], pw, ph, pw, dst, lw, lh, lw);
+        }
+        off += (int64_t)lw * lh;
+    }
+    level_off[p->nlevels] = off;
+    return 0;
+}
+
+/* ======================= FAST-9/16 (OpenCV 3.4 features2d/fast.cpp) ======================= */
+static void fast_offsets(int pixel[25], int step)
+{
+    static const int offsets16[16][2] = {
+        {0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+        {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+    int k = 0;
+    for (; k < 16; k++) pixel[k] = offsets16[k][0] + offsets16[k][1] * step;
+    for (; k < 25; k++) pixel[k] = pixel[k - 16];
+}
+
+/* cornerScore<16> (fast_score.cpp), scalar form */
+static int corner_score16(const uint8_t* ptr, const int pixel[25], int threshold)
+{
+    const int K = 8, N = K * 3 + 1;
+    int k, v = ptr[0];
+    short d[25];
+    for (k = 0; k < N; k++) d[k] = (short)(v - ptr[pixel[k]]);
+    int a0 = threshold;
+    for (k = 0; k < 16; k += 2) {
+        int a = imin(d[k + 1], d[k + 2]);
+        a = imin(a, d[k + 3]);
+        if (a <= a0) continue;
+        a = imin(a, d[k + 4]);
+        a = imin(a, d[k + 5]);
+        a = imin(a, d[k + 6]);
+        a = imin(a, d[k + 7]);
+        a = imin(a, d[k + 8]);
+        a0 = imax(a0, imin(a, d[k]));
+        a0 = imax(a0, imin(a, d[k + 9]));
+    }
+    int b0 = -a0;
+    for (k = 0; k < 16; k += 2) {
+        int b = imax(d[k + 1], d[k + 2]);
+        b = imax(b, d[k + 3]);
+        b = imax(b, d[k + 4]);
+        b = imax(b, d[k + 5]);
+        if (b >= b0) continue;
+        b = imax(b, d[k + 6]);
+        b = imax(b, d[k + 7]);
+        b = imax(b, d[k + 8]);
+        b0 = imin(b0, imax(b, d[k]));
+        b0 = imin(b0, imax(b, d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+/* FAST_t<16>(img, kps, threshold, nonmax_suppression=true) on an ROI */
+int oc_fast_roi(const uint8_t* img, int stride, int rows, int cols, int threshold,
+                int* xs, int* ys, int* score, int cap)
+{
+    const int K = 8, N = 25;
+    int pixel[25];
+    fast_offsets(pixel, stride);
+    threshold = imin(imax(threshold, 0), 255);
+    uint8_t tabbuf[512];
+    for (int i = -255; i <= 255; i++) tabbuf[i + 255] = (uint8_t)(i < -threshold ? 1 : i > threshold ? 2 : 0);
+    uint8_t* buf[3];
+    int* cpbuf[3];
+    uint8_t* sbuf = (uint8_t*)calloc((size_t)cols * 3 + 16, 1);
+    int* cbuf = (int*)calloc((size_t)(cols + 1) * 3 + 4, sizeof(int));
+    buf[0] = sbuf; buf[1] = sbuf + cols; buf[2] = sbuf + 2 * cols;
+    cpbuf[0] = cbuf + 1; cpbuf[1] = cpbuf[0] + cols + 1; cpbuf[2] = cpbuf[1] + cols + 1;
+    int nout = 0;
+    for (int i = 3; i < rows - 2; i++) {
+        const uint8_t* ptr = img + (size_t)i * stride + 3;
+        uint8_t* curr = buf[(i - 3) % 3];
+        int* cornerpos = cpbuf[(i - 3) % 3];
+        memset(curr, 0, cols);
+        int ncorners = 0;
+        if (i < rows - 3) {
+            for (int j = 3; j < cols - 3; j++, ptr++) {
+                int v = ptr[0];
+                const uint8_t* tab = tabbuf - v + 255;
+                int d = tab[ptr[pixel[0]]] | tab[ptr[pixel[8]]];
+                if (d == 0) continue;
+                d &= tab[ptr[pixel[2]]] | tab[ptr[pixel[10]]];
+                d &= tab[ptr[pixel[4]]] | tab[ptr[pixel[12]]];
+                d &= tab[ptr[pixel[6]]] | tab[ptr[pixel[14]]];
+                if (d == 0) continue;
+                d &= tab[ptr[pixel[1]]] | tab[ptr[pixel[9]]];
+                d &= tab[ptr[pixel[3]]] | tab[ptr[pixel[11]]];
+                d &= tab[ptr[pixel[5]]] | tab[ptr[pixel[13]]];
+                d &= tab[ptr[pixel[7]]] | tab[ptr[pixel[15]]];
+                if (d & 1) {
+                    int vt = v - threshold, count = 0;
+                    for (int k = 0; k < N; k++) {
+                        int x = ptr[pixel[k]];
+                        if (x < vt) {
+                            if (++count > K) {
+                                cornerpos[ncorners++] = j;
+                                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                                break;
+                            }
+                        } else
+                            count = 0;
+                    }
+                }
+                if (d & 2) {
+                    int vt = v + threshold, count = 0;
+                    for (int k = 0; k < N; k++) {
+                        int x = ptr[pixel[k]];
+                        if (x > vt) {
+                            if (++count > K) {
+                                cornerpos[ncorners++] = j;
+                                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                                break;
+                            }
+                        } else
+                            count = 0;
+                    }
+                }
+            }
+        }
+        cornerpos[-1] = ncorners;
+        if (i == 3) continue;
+        const uint8_t* prev = buf[(i - 4 + 3) % 3];
+        const uint8_t* pprev = buf[(i - 5 + 3) % 3];
+        cornerpos = cpbuf[(i - 4 + 3) % 3];
+        ncorners = cornerpos[-1];
+        for (int k = 0; k < ncorners; k++) {
+            int j = cornerpos[k];
+            int s = prev[j];
+            if (s > prev[j + 1] && s > prev[j - 1] && s > pprev[j - 1] && s > pprev[j] &&
+                s > pprev[j + 1] && s > curr[j - 1] && s > curr[j] && s > curr[j + 1]) {
+                if (nout < cap) { xs[nout] = j; ys[nout] = i - 1; score[nout] = s; }
+                nout++;
+            }
+        }
+    }
+    free(sbuf);
+    free(cbuf);
+    return nout;
+}
+
+/* FAST stage of ComputeKeyPointsOctTree (src/ORBextractor.cc:793-850), one level */
+int oc_level_candidates(const uint8_t* lvl, int lw, int lh, int stride, int ini_th, int min_th,
+                        int* xs, int* ys, int* score, int cap)
+{
+    const float W = 30;
+    const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+    const int maxBorderX = lw - EDGE_THRESHOLD + 3, maxBorderY = lh - EDGE_THRESHOLD + 3;
+    const float width = (float)(maxBorderX - minBorderX);
+    const float height = (float)(maxBorderY - minBorderY);
+    const int nCols = (int)(width / W), nRows = (int)(height / W);
+    if (nCols <= 0 || nRows <= 0) return -1;          /* reference: division by zero (UB) */
+    const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+    int n = 0;
+    int tmpcap = (wCell + 7) * (hCell + 7);
+    int* tx = (int*)malloc(sizeof(int) * tmpcap * 3);
+    int *ty = tx + tmpcap, *ts = ty + tmpcap;
+    for (int i = 0; i < nRows; i++) {
+        const float iniY = (float)(minBorderY + i * hCell);
+        float maxY = iniY + hCell + 6;
+        if (iniY >= maxBorderY - 3) continue;
+        if (maxY > maxBorderY) maxY = (float)maxBorderY;
+        for (int j = 0; j < nCols; j++) {
+            const float iniX = (float)(minBorderX + j * wCell);
+            float maxX = iniX + wCell + 6;
+            if (iniX >= maxBorderX - 6) continue;
+            if (maxX > maxBorderX) maxX = (float)maxBorderX;
+            int r0 = (int)iniY, r1 = (int)maxY, c0 = (int)iniX, c1 = (int)maxX;
+            const uint8_t* roi = lvl + (size_t)r0 * stride + c0;
+            int k = oc_fast_roi(roi, stride, r1 - r0, c1 - c0, ini_th, tx, ty, ts, tmpcap);
+            if (k == 0) k = oc_fast_roi(roi, stride, r1 - r0, c1 - c0, min_th, tx, ty, ts, tmpcap);
+            for (int q = 0; q < k; q++) {
+                if (n < cap) {
+                    xs[n] = tx[q] + j * wCell;   /* :844-845, relative to (16,16) */
+                    ys[n] = ty[q] + i * hCell;
+                    score[n] = ts[q];
+                }
+                n++;
+            }
+        }
+    }
+    free(tx);
+    return n;
+}
+
+/* ================= DistributeOctTree (src/ORBextractor.cc:489-769) ================= */
+typedef struct OcNode {
+    int* keys; int nkeys;
+    int ulx, uly, urx, ury, blx, bly, brx, bry;
+    int no_more;
+    long seq;                         /* allocation order == canonical pointer order */
+    struct OcNode *prev, *next;
+} OcNode;
+
+typedef struct { OcNode* head; OcNode* tail; int size; long seq; } OcList;
+
+static OcNode* node_new(OcList* L, const OcNode* src)
+{
+    OcNode* n = (OcNode*)malloc(sizeof(OcNode));
+    *n = *src;
+    n->seq = L->seq++;
+    n->prev = n->next = NULL;
+    return n;
+}
+static void list_push_front(OcList* L, OcNode* n)
+{
+    n->prev = NULL; n->next = L->head;
+    if (L->head) L->head->prev = n; else L->tail = n;
+    L->head = n; L->size++;
+}
+static void list_push_back(OcList* L, OcNode* n)
+{
+    n->next = NULL; n->prev = L->tail;
+    if (L->tail) L->tail->next = n; else L->head = n;
+    L->tail = n; L->size++;
+}
+static OcNode* list_erase(OcList* L, OcNode* n)
+{
+    OcNode* nx = n->next;
+    if (n->prev) n->prev->next = n->next; else L->head = n->next;
+    if (n->next) n->next->prev = n->prev; else L->tail = n->prev;
+    L->size--;
+    free(n->keys);
+    free(n);
+    return nx;
+}
+
+/* ExtractorNode::DivideNode (:489-544); children get fresh key arrays */
+static void divide_node(const OcNode* p, const int* xs, const int* ys, OcNode c[4])
+{
+    const int halfX = (int)ceilf((float)(p->urx - p->ulx) / 2);
+    const int halfY = (int)ceilf((float)(p->bry - p->uly) / 2);
+    memset(c, 0, sizeof(OcNode) * 4);
+    c[0].ulx = p->ulx;          c[0].uly = p->uly;
+    c[0].urx = p->ulx + halfX;  c[0].ury = p->uly;
+    c[0].blx = p->ulx;          c[0].bly = p->uly + halfY;
+    c[0].brx = p->ulx + halfX;  c[0].bry = p->uly + halfY;
+    c[1].ulx = c[0].urx;        c[1].uly = c[0].ury;
+    c[1].urx = p->urx;          c[1].ury = p->ury;
+    c[1].blx = c[0].brx;        c[1].bly = c[0].bry;
+    c[1].brx = p->urx;          c[1].bry = p->uly + halfY;
+    c[2].ulx = c[0].blx;        c[2].uly = c[0].bly;
+    c[2].urx = c[0].brx;        c[2].ury = c[0].bry;
+    c[2].blx = p->blx;          c[2].bly = p->bly;
+    c[2].brx = c[0].brx;        c[2].bry = p->bly;
+    c[3].ulx = c[2].urx;        c[3].uly = c[2].ury;
+    c[3].urx = c[1].brx;        c[3].ury = c[1].bry;
+    c[3].blx = c[2].brx;        c[3].bly = c[2].bry;
+    c[3].brx = p->brx;          c[3].bry = p->bry;
+    for (int q = 0; q < 4; q++) c[q].keys = (int*)malloc(sizeof(int) * (p->nkeys > 0 ? p->nkeys : 1));
+    for (int i = 0; i < p->nkeys; i++) {
+        int k = p->keys[i];
+        int q;
+        if (xs[k] < c[0].urx) q = (ys[k] < c[0].bry) ? 0 : 2;
+        else q = (ys[k] < c[0].bry) ? 1 : 3;
+        c[q].keys[c[q].nkeys++] = k;
+    }
+    for (int q = 0; q < 4; q++) c[q].no_more = (c[q].nkeys == 1);
+}
+
+typedef struct { int size; OcNode* node; } SizeNode;
+static int cmp_size_node(const void* a, const void* b)
+{
+    const SizeNode* x = (const SizeNode*)a;
+    const SizeNode* y = (const SizeNode*)b;
+    if (x->size != y->size) return x->size < y->size ? -1 : 1;
+    return x->node->seq < y->node->seq ? -1 : (x->node->seq > y->node->seq ? 1 : 0);
+}
+
+int oc_distribute_octree(const int* xs, const int* ys, const int* score, int n,
+                         int minX, int maxX, int minY, int maxY, int N,
+                         int* out_idx, int cap)
+{
+    const int nIni = (int)roundf((float)(maxX - minX) / (maxY - minY));
+    const float hX = (float)(maxX - minX) / nIni;
+    OcList L = {NULL, NULL, 0, 0};
+    OcNode** ini = (OcNode**)malloc(sizeof(OcNode*) * (nIni > 0 ? nIni : 1));
+    for (int i = 0; i < nIni; i++) {
+        OcNode t;
+        memset(&t, 0, sizeof(t));
+        t.ulx = (int)(hX * (float)i);       t.uly = 0;
+        t.urx = (int)(hX * (float)(i + 1)); t.ury = 0;
+        t.blx = t.ulx; t.bly = maxY - minY;
+        t.brx = t.urx; t.bry = maxY - minY;
+        t.keys = (int*)malloc(sizeof(int) * (n > 0 ? n : 1));
+        OcNode* nn = node_new(&L, &t);
+        list_push_back(&L, nn);
+        ini[i] = nn;
+    }
+    for (int i = 0; i < n; i++) {                   /* :573-577 */
+        int b = (int)((float)xs[i] / hX);
+        ini[b]->keys[ini[b]->nkeys++] = i;
+    }
+    free(ini);
+    for (OcNode* it = L.head; it;) {                /* :579-592 */
+        if (it->nkeys == 1) { it->no_more = 1; it = it->next; }
+        else if (it->nkeys == 0) it = list_erase(&L, it);
+        else it = it->next;
+    }
+    int bFinish = 0;
+    SizeNode* vsz = (SizeNode*)malloc(sizeof(SizeNode) * (4 * (size_t)L.size + 16));
+    size_t vsz_cap = 4 * (size_t)L.size + 16;
+    int nvsz = 0;
+#define VSZ_PUSH(S, ND) do { if ((size_t)nvsz >= vsz_cap) { vsz_cap *= 2; vsz = (SizeNode*)realloc(vsz, sizeof(SizeNode) * vsz_cap); } vsz[nvsz].size = (S); vsz[nvsz].node = (ND); nvsz++; } while (0)
+    while (!bFinish) {                                /* :601-745 */
+        int prevSize = L.size;
+        int nToExpand = 0;
+        nvsz = 0;
+        OcNode* it = L.head;
+        while (it) {
+            if (it->no_more) { it = it->next; continue; }
+            OcNode c[4];
+            divide_node(it, xs, ys, c);
+            for (int q = 0; q < 4; q++) {
+                if (c[q].nkeys > 0) {
+                    OcNode* nn = node_new(&L, &c[q]);
+                    list_push_front(&L, nn);
+                    if (c[q].nkeys > 1) { nToExpand++; VSZ_PUSH(c[q].nkeys, nn); }
+                } else
+                    free(c[q].keys);
+            }
+            it = list_erase(&L, it);
+        }
+        if (L.size >= N || L.size == prevSize) {
+            bFinish = 1;
+        } else if (L.size + nToExpand * 3 > N) {
+            while (!bFinish) {                        /* :683-743 */
+                prevSize = L.size;
+                int nprev = nvsz;
+                SizeNode* vprev = (SizeNode*)malloc(sizeof(SizeNode) * (nprev > 0 ? nprev : 1));
+                memcpy(vprev, vsz, sizeof(SizeNode) * nprev);
+                nvsz = 0;
+                qsort(vprev, nprev, sizeof(SizeNode), cmp_size_node);
+                for (int j = nprev - 1; j >= 0; j--) {
+                    OcNode c[4];
+                    divide_node(vprev[j].node, xs, ys, c);
+                    for (int q = 0; q < 4; q++) {
+                        if (c[q].nkeys > 0) {
+                            OcNode* nn = node_new(&L, &c[q]);
+                            list_push_front(&L, nn);
+                            if (c[q].nkeys > 1) VSZ_PUSH(c[q].nkeys, nn);
+                        } else
+                            free(c[q].keys);
+                    }
+                    list_erase(&L, vprev[j].node);
+                    if (L.size >= N) break;
+                }
+                free(vprev);
+                if (L.size >= N || L.size == prevSize) bFinish = 1;
+            }
+        }
+    }
+#undef VSZ_PUSH
+    free(vsz);
+    int nout = 0;                                     /* :747-766 retain best */
+    for (OcNode* it = L.head; it; it = it->next) {
+        int best = it->keys[0];
+        int maxr = score[best];
+        for (int k = 1; k < it->nkeys; k++) {
+            if (score[it->keys[k]] > maxr) { best = it->keys[k]; maxr = score[best]; }
+        }
+        if (nout < cap) out_idx[nout] = best;
+        nout++;
+    }
+    while (L.head) list_erase(&L, L.head);
+    return nout;
+}
+
+/* ============================ orientation / descriptor ============================ */
+/* IC_Angle moments (src/ORBextractor.cc:80-104) */
+int oc_ic_angle_moments(const uint8_t* img, int stride, int x, int y, const int* umax,
+                        int* m01_out, int* m10_out)
+{
+    int m_01 = 0, m_10 = 0;
+    const uint8_t* center = img + (size_t)y * stride + x;
+    for (int u = -HALF_PATCH_SIZE; u <= HALF_PATCH_SIZE; ++u) m_10 += u * center[u];
+    for (int v = 1; v <= HALF_PATCH_SIZE; ++v) {
+        int v_sum = 0;
+        int d = umax[v];
+        for (int u = -d; u <= d; ++u) {
+            int val_plus = center[u + v * stride], val_minus = center[u - v * stride];
+            v_sum += (val_plus - val_minus);
+            m_10 += u * (val_plus + val_minus);
+        }
+        m_01 += v * v_sum;
+    }
+    *m01_out = m_01;
+    *m10_out = m_10;
+    return 0;
+}
+
+/* cv::fastAtan2 (OpenCV 3.4 core mathfuncs_core: atan_f32), degrees, no FMA */
+float oc_fast_atan2(float y, float x)
+{
+    static const float p1 = 0.9997878412794807f * (float)(180 / OC_PI);
+    static const float p3 = -0.3258083974640975f * (float)(180 / OC_PI);
+    static const float p5 = 0.1555786518463281f * (float)(180 / OC_PI);
+    static const float p7 = -0.04432655554792128f * (float)(180 / OC_PI);
+    float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)2.2204460492503131e-16);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)2.2204460492503131e-16);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+/* Canonical sincosf: double evaluation with fdlibm kernels, explicit fma in
+ * the Cody-Waite reduction, rounded once to float.  Bit-identical to the HIP device version. */
+void oc_sincos(float a, float* s, float* c)
+{
+    const double two_over_pi = 6.36619772367581382433e-01;
+    const double pio2_1 = 1.57079632673412561417e+00;
+    const double pio2_1t = 6.07710050650619224932e-11;
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    double x = (double)a;
+    double kd = rint(x * two_over_pi);
+    double r = fma(-kd, pio2_1, x);
+    r = fma(-kd, pio2_1t, r);
+    double z = r * r;
+    double v = z * r;
+    double sr = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    double sn = r + v * (S1 + z * sr);
+    double cr = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    double hz = 0.5 * z;
+    double w = 1.0 - hz;
+    double cs = w + (((1.0 - w) - hz) + z * cr);
+    int q = ((int)kd) & 3;
+    double so, co;
+    switch (q) {
+    case 0: so = sn; co = cs; break;
+    case 1: so = cs; co = -sn; break;
+    case 2: so = -sn; co = -cs; break;
+    default: so = -cs; co = sn; break;
+    }
+    *s = (float)so;
+    *c = (float)co;
+}
+
+/* Gaussian 7-tap, sigma 2, Q8 (OpenCV 3.4.8+/4.x getGaussianKernelBitExact +
+ * getGaussianKernelFixedPoint_ED) */
+void oc_gauss_kernel7(int k[7])
+{
+    const int n = 7, n2 = 3;
+    const double sigma = 2.0;
+    double scale2X = -0.125 / (sigma * sigma);
+    double values[3], sum = 0.0;
+    for (int i = 0, x = 1 - n; i < n2; i++, x += 2) {
+        double t = exp((double)(x * x) * scale2X);
+        values[i] = t;
+        sum += t;
+    }
+    sum *= 2.0;
+    sum += 1.0;
+    double mul1 = 1.0 / sum;
+    double res[7];
+    for (int i = 0; i < n2; i++) { res[i] = res[n - 1 - i] = values[i] * mul1; }
+    res[n2] = 1.0 * mul1;
+    double err = 0.0;
+    int64_t s = 0;
+    for (int i = 0; i < n2; i++) {
+        double adj = res[i] * 256.0 + err;
+        int64_t v0 = cv_round_d(adj);
+        err = adj - (double)v0;
+        k[i] = k[n - 1 - i] = (int)v0;
+        s += v0;
+    }
+    s *= 2;
+    k[n2] = (int)(256 - s);
+}
+
+static inline int reflect101(int p, int len)
+{
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) {
+        if (p < 0) p = -p;
+        else p = 2 * len - p - 2;
+    }
+    return p;
+}
+
+/* GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101) on a cloned level (src/ORBextractor.cc:1317-1318):
+ * fixedSmoothInvoker<uint8_t, ufixedpoint16>: horizontal u8 x Q8 -> Q8 sums, vertical
+ * Q8 x Q8 -> Q16, out = (v + 2^15) >> 16. */
+void oc_gaussian_blur7(const uint8_t* src, int w, int h, int sstride, uint8_t* dst, int dstride)
+{
+    int k[7];
+    oc_gauss_kernel7(k);
+    uint32_t* hbuf = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)w * h);
+    for (int y = 0; y < h; y++) {
+        const uint8_t* S = src + (size_t)y * sstride;
+        for (int x = 0; x < w; x++) {
+            uint32_t acc = 0;
+            for (int t = 0; t < 7; t++) acc += (uint32_t)k[t] * S[reflect101(x + t - 3, w)];
+            hbuf[(size_t)y * w + x] = acc;
+        }
+    }
+    for (int y = 0; y < h; y++) {
+        for (int x = 0; x < w; x++) {
+            uint32_t acc = 0;
+            for (int t = 0; t < 7; t++) acc += (uint32_t)k[t] * hbuf[(size_t)reflect101(y + t - 3, h) * w + x];
+            uint32_t o = (acc + (1u << 15)) >> 16;
+            dst[(size_t)y * dstride + x] = (uint8_t)(o > 255 ? 255 : o);
+        }
+    }
+    free(hbuf);
+}
+
+/* computeOrbDescriptor (src/ORBextractor.cc:109-156); rotation in the fused forms of the
+ * reference binary: row = cvRound(fmaf(x, b, y*a)), col = cvRound(fmaf(x, a, -(y*b))) */
+void oc_orb_descriptor(const uint8_t* img, int stride, int x, int y, float angle,
+                       const int (*pattern)[2], uint8_t desc[32])
+{
+    const float factorPI = (float)(OC_PI / 180.f);
+    float ang = angle * factorPI;
+    float b, a;
+    oc_sincos(ang, &b, &a);
+    const uint8_t* center = img + (size_t)y * stride + x;
+    for (int i = 0; i < 32; ++i) {
+        int val = 0;
+        for (int t = 0; t < 8; t++) {
+            const int* p0 = pattern[16 * i + 2 * t];
+            const int* p1 = pattern[16 * i + 2 * t + 1];
+            float px0 = (float)p0[0], py0 = (float)p0[1];
+            float px1 = (float)p1[0], py1 = (float)p1[1];
+            int r0 = cv_round(fmaf(px0, b, py0 * a)), c0 = cv_round(fmaf(px0, a, -(py0 * b)));
+            int r1 = cv_round(fmaf(px1, b, py1 * a)), c1 = cv_round(fmaf(px1, a, -(py1 * b)));
+            int t0 = center[r0 * stride + c0];
+            int t1 = center[r1 * stride + c1];
+            val |= (t0 < t1) << t;
+        }
+        desc[i] = (uint8_t)val;
+    }
+}
+
+/* ======================== dynamic mask: src/ORBextractor.cc:1101-1195 ======================== */
+int oc_dynamic_mask(const oc_box* boxes, int nbox, const float* tm_xy, int ntm,
+                    const int32_t* blur_flag, int nblur, int w, int h,
+                    uint8_t* mask, float* area_out)
+{
+    memset(mask, 1, (size_t)w * h);
+    float area = 0;
+    for (int b = 0; b < nbox; b++) {
+        float xmin = boxes[b].xmin, ymin = boxes[b].ymin, xmax = boxes[b].xmax, ymax = boxes[b].ymax;
+        /* mask_mark(Rect(int(xmin), int(ymin), int(xmax - xmin), int(ymax - ymin))) = 0 */
+        int rx = (int)xmin, ry = (int)ymin, rw = (int)(xmax - xmin), rh = (int)(ymax - ymin);
+        float area_box = (xmax - xmin) * (ymax - ymin);
+        int mark_box = 0;
+        size_t nin = 0;
+        for (int t = 0; t < ntm; t++) {
+            int px = (int)tm_xy[2 * t], py = (int)tm_xy[2 * t + 1];
+            int in = px >= 0 && px < w && py >= 0 && py < h &&
+                     px >= rx && px < rx + rw && py >= ry && py < ry + rh;
+            if (in) nin++;
+            if ((float)(nin * 10000) > area_box) {   /* layer 1, :1145 */
+                mark_box = 1;
+                area = area + area_box;
+                for (int i = imax((int)xmin, 0); i < imin((int)xmax, w); i++)
+                    for (int j = imax((int)ymin, 0); j < imin((int)ymax, h); j++) mask[(size_t)j * w + i] = 0;
+                break;
+            }
+        }
+        if (mark_box) continue;
+        int bf = b < nblur ? blur_flag[b] : 0;
+        if (bf == 1 && nin > 0) {                  /* layer 2, :1168 */
+            for (int i = imax((int)xmin, 0); i < imin((int)xmax, w); i++)
+                for (int j = imax((int)ymin, 0); j < imin((int)ymax, h); j++) mask[(size_t)j * w + i] = 0;
+            area = area + area_box;
+            continue;
+        }
+    }
+    if (area_out) *area_out = area;
+    return area > 200000 ? 1 : 0;                   /* :1192 */
+}
+
+/* CheckMovingKeyPoints / _finall lookup (src/ORBextractor.cc:1391-1397, 1426-1440) */
+static int masked_out(const uint8_t* mask, int w, int h, float px, float py, float scale)
+{
+    float sx = px * scale, sy = py * scale;
+    if (sx >= (float)(w - 1)) sx = (float)(w - 1);
+    if (sy >= (float)(h - 1)) sy = (float)(h - 1);
+    int ix = (int)sx, iy = (int)sy;
+    return mask[(size_t)iy * w + ix] == 0;
+}
+
+/* ============================ operator(): src/ORBextractor.cc:1088-1342 ============================ */
+int oc_extract(const oc_params* p, const uint8_t* gray, int w, int h, int stride,
+               const oc_box* boxes, int nbox, const float* tm_xy, int ntm,
+               const int32_t* blur_flag, int nblur,
+               oc_kp* kp_out, uint8_t* desc_out, int cap, int* n_out, oc_debug* dbg)
+{
+    *n_out = 0;
+    if (!gray || w <= 0 || h <= 0) return 0;          /* _image.empty() -> return */
+    const int L = p->nlevels;
+    if (L < 1 || L > OC_MAX_LEVELS) return -1;
+    uint8_t* mask = (uint8_t*)malloc((size_t)w * h);
+    float area;
+    int area_flag = oc_dynamic_mask(boxes, nbox, tm_xy, ntm, blur_flag, nblur, w, h, mask, &area);
+    int64_t off[OC_MAX_LEVELS + 1];
+    int64_t total = 0;
+    int lw[OC_MAX_LEVELS], lh[OC_MAX_LEVELS];
+    for (int l = 0; l < L; l++) { oc_level_size(p, w, h, l, &lw[l], &lh[l]); total += (int64_t)lw[l] * lh[l]; }
+    uint8_t* pyr = (uint8_t*)malloc((size_t)total);
+    oc_pyramid(p, gray, w, h, stride, pyr, off);
+    const int ini_th = area_flag ? 30 : 20, min_th = area_flag ? 10 : 7;   /* :775-784 */
+
+    int* lvl_n = (int*)calloc((size_t)L, sizeof(int));
+    int** lvl_x = (int**)calloc((size_t)L, sizeof(int*));
+    int** lvl_y = (int**)calloc((size_t)L, sizeof(int*));
+    int** lvl_s = (int**)calloc((size_t)L, sizeof(int*));
+    int rc = 0;
+    for (int l = 0; l < L; l++) {
+        const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+        const int maxBorderX = lw[l] - EDGE_THRESHOLD + 3, maxBorderY = lh[l] - EDGE_THRESHOLD + 3;
+        int capc = lw[l] * lh[l] / 2 + 16;
+        int* cx = (int*)malloc(sizeof(int) * capc * 3);
+        int *cy = cx + capc, *cs = cy + capc;
+        int nc = oc_level_candidates(pyr + off[l], lw[l], lh[l], lw[l], ini_th, min_th, cx, cy, cs, capc);
+        if (nc < 0) { free(cx); rc = -2; break; }
+        if (dbg) dbg->ncand[l] = nc;
+        if (area_flag) {                                                  /* :854-858 */
+            float scale = (l != 0) ? p->scale[l] : 1.0f;
+            int m = 0;
+            for (int k = 0; k < nc; k++) {
+                if (!masked_out(mask, w, h, (float)cx[k], (float)cy[k], scale)) {
+                    cx[m] = cx[k]; cy[m] = cy[k]; cs[m] = cs[k]; m++;
+                }
+            }
+            nc = m;
+        }
+        int N = area_flag ? (int)((double)p->nfeat[l] * 0.7) : p->nfeat[l];   /* :866-875 */
+        int ocap = nc + 8;
+        int* oidx = (int*)malloc(sizeof(int) * ocap);
+        int nk = oc_distribute_octree(cx, cy, cs, nc, minBorderX, maxBorderX, minBorderY, maxBorderY, N, oidx, ocap);
+        lvl_x[l] = (int*)malloc(sizeof(int) * (nk + 1));
+        lvl_y[l] = (int*)malloc(sizeof(int) * (nk + 1));
+        lvl_s[l] = (int*)malloc(sizeof(int) * (nk + 1));
+        for (int k = 0; k < nk; k++) {                                    /* :884-890 */
+            lvl_x[l][k] = cx[oidx[k]] + minBorderX;
+            lvl_y[l][k] = cy[oidx[k]] + minBorderY;
+            lvl_s[l][k] = cs[oidx[k]];
+        }
+        lvl_n[l] = nk;
+        free(oidx);
+        free(cx);
+    }
+    if (rc == 0 && !area_flag) {                                          /* :1204-1207 */
+        for (int l = 0; l < L && l < 8; l++) {
+            float scale = (l != 0) ? p->scale[l] : 1.0f;
+            int m = 0;
+            for (int k = 0; k < lvl_n[l]; k++) {
+                if (!masked_out(mask, w, h, (float)lvl_x[l][k], (float)lvl_y[l][k], scale)) {
+                    lvl_x[l][m] = lvl_x[l][k]; lvl_y[l][m] = lvl_y[l][k]; lvl_s[l][m] = lvl_s[l][k]; m++;
+                }
+            }
+            lvl_n[l] = m;
+        }
+    }
+    int n = 0;
+    if (rc == 0) {
+        uint8_t* blur = (uint8_t*)malloc((size_t)lw[0] * lh[0]);
+        for (int l = 0; l < L; l++) {
+            if (dbg) dbg->nkept[l] = lvl_n[l];
+            if (lvl_n[l] == 0) continue;
+            const uint8_t* lvl = pyr + off[l];
+            oc_gaussian_blur7(lvl, lw[l], lh[l], lw[l], blur, lw[l]);   /* :1317-1318 */
+            const int scaledPatchSize = (int)(PATCH_SIZE * p->scale[l]);   /* :877 */
+            for (int k = 0; k < lvl_n[l]; k++) {
+                int x = lvl_x[l][k], y = lvl_y[l][k];
+                int m01, m10;
+                oc_ic_angle_moments(lvl, lw[l], x, y, p->umax, &m01, &m10);
+                float angle = oc_fast_atan2((float)m01, (float)m10);
+                if (n < cap) {
+                    oc_kp* kp = &kp_out[n];
+                    kp->x = (float)x; kp->y = (float)y;
+                    kp->size = (float)scaledPatchSize;
+                    kp->angle = angle;
+                    kp->response = (float)lvl_s[l][k];
+                    kp->octave = l;
+                    kp->class_id = -1;
+                    if (desc_out)
+                        oc_orb_descriptor(blur, lw[l], x, y, angle, (const int (*)[2])p->pattern, desc_out + (size_t)n * 32);
+                    if (l != 0) { kp->x *= p->scale[l]; kp->y *= p->scale[l]; }   /* :1327-1334 */
+                }
+                n++;
+            }
+        }
+        free(blur);
+    }
+    if (dbg) {
+        dbg->area_flag = area_flag;
+        for (int l = 0; l <= L; l++) dbg->level_off[l] = off[l];
+        if (dbg->pyramid) memcpy(dbg->pyramid, pyr, (size_t)total);
+    }
+    for (int l = 0; l < L; l++) { free(lvl_x[l]); free(lvl_y[l]); free(lvl_s[l]); }
+    free(lvl_x); free(lvl_y); free(lvl_s); free(lvl_n);
+    free(pyr);
+    free(mask);
+    *n_out = n;
+    return rc;
+}
+
+/* ===================== Frame blur flag: src/Frame.cc:171-202, 905-913 ===================== */
+int oc_blur_flags(const uint8_t* gray, int w, int h, int stride,
+                  const oc_box* boxes, int nbox, int32_t* out, double* mean_out)
+{
+    for (int b = 0; b < nbox; b++) {
+        int rx = (int)boxes[b].xmin, ry = (int)boxes[b].ymin;
+        int rw = (int)(boxes[b].xmax - boxes[b].xmin), rh = (int)(boxes[b].ymax - boxes[b].ymin);
+        if (rx < 0 || ry < 0 || rw <= 0 || rh <= 0 || rx + rw > w || ry + rh > h) {
+            out[b] = 0;                   /* reference: cv::Rect assertion; documented as 0 */
+            if (mean_out) mean_out[b] = -1.0;
+            continue;
+        }
+        int64_t S = 0;
+        for (int y = 0; y < rh; y++) {
+            for (int x = 0; x < rw; x++) {
+                const uint8_t* c = gray + (size_t)(ry) * stride + rx;
+                int ym = reflect101(y - 1, rh), yp = reflect101(y + 1, rh);
+                int xm = reflect101(x - 1, rw), xp = reflect101(x + 1, rw);
+                int lap = c[(size_t)ym * stride + x] + c[(size_t)yp * stride + x] +
+                          c[(size_t)y * stride + xm] + c[(size_t)y * stride + xp] - 4 * c[(size_t)y * stride + x];
+                S += lap < 0 ? 0 : lap;   /* saturate_cast<ushort> */
+            }
+        }
+        double mean = (double)S * (1. / (double)((int64_t)rw * rh));   /* cv::mean: s*(1./nz) */
+        if (mean_out) mean_out[b] = mean;
+        out[b] = mean < 4.2 ? 1 : 0;
+    }
+    return 0;
+}
+
+/* cvtColor RGB2GRAY / BGR2GRAY 8U, 14-bit fixed point (imgproc color.cpp RGB2Gray<uchar>) */
+void oc_rgb2gray(const uint8_t* rgb, int w, int h, int stride, int rgb_order, uint8_t* out)
+{
+    const int R2Y = 4899, G2Y = 9617, B2Y = 1868;
+    for (int y = 0; y < h; y++) {
+        const uint8_t* s = rgb + (size_t)y * stride;
+        for (int x = 0; x < w; x++) {
+            int c0 = s[3 * x], c1 = s[3 * x + 1], c2 = s[3 * x + 2];
+            int v = rgb_order ? (c0 * R2Y + c1 * G2Y + c2 * B2Y) : (c0 * B2Y + c1 * G2Y + c2 * R2Y);
+            out[(size_t)y * w + x] = (uint8_t)((v + (1 << 13)) >> 14);
+        }
+    }
+}
+
+/* ================================= matcher side ================================= */
+void oc_camera_init(oc_camera* c, float fx, float fy, float cx, float cy, float bf,
+                    int w, int h, const oc_params* p)
+{
+    memset(c, 0, sizeof(*c));
+    c->fx = fx; c->fy = fy; c->cx = cx; c->cy = cy; c->bf = bf;
+    c->mb = bf / fx;                                                  /* Frame.cc:246 */
+    c->min_x = 0.0f; c->max_x = (float)w; c->min_y = 0.0f; c->max_y = (float)h;   /* :635-641 */
+    c->grid_inv_w = (float)OC_GRID_COLS / (c->max_x - c->min_x);       /* :233-234 */
+    c->grid_inv_h = (float)OC_GRID_ROWS / (c->max_y - c->min_y);
+    c->nlevels = p->nlevels;
+    for (int l = 0; l < p->nlevels; l++) c->scale[l] = p->scale[l];
+}
+
+void oc_stereo_from_rgbd(const oc_kp* kps, int n, const float* depth, int w, int dstride,
+                         float bf, float* uright, float* dep)
+{
+    (void)w;
+    for (int i = 0; i < n; i++) {
+        uright[i] = -1; dep[i] = -1;
+        const float v = kps[i].y, u = kps[i].x;
+        const float d = depth[(size_t)(int)v * dstride + (int)u];      /* at<float>(v,u) */
+        if (d > 0) { dep[i] = d; uright[i] = kps[i].x - bf / d; }
+    }
+}
+
+void oc_assign_grid(const oc_camera* c, const oc_kp* kps, int n, oc_grid* g)
+{
+    const int NC = OC_GRID_COLS * OC_GRID_ROWS;
+    int* cell = (int*)malloc(sizeof(int) * (n > 0 ? n : 1));
+    memset(g->cell_start, 0, sizeof(int) * (NC + 1));
+    for (int i = 0; i < n; i++) {
+        int px = (int)roundf((kps[i].x - c->min_x) * c->grid_inv_w);   /* PosInGrid :560-561 */
+        int py = (int)roundf((kps[i].y - c->min_y) * c->grid_inv_h);
+        if (px < 0 || px >= OC_GRID_COLS || py < 0 || py >= OC_GRID_ROWS) { cell[i] = -1; continue; }
+        cell[i] = px * OC_GRID_ROWS + py;
+        g->cell_start[cell[i] + 1]++;
+    }
+    for (int k = 0; k < NC; k++) g->cell_start[k + 1] += g->cell_start[k];
+    int* fill = (int*)malloc(sizeof(int) * NC);
+    memcpy(fill, g->cell_start, sizeof(int) * NC);
+    for (int i = 0; i < n; i++)
+        if (cell[i] >= 0) g->cell_idx[fill[cell[i]]++] = i;
+    free(fill);
+    free(cell);
+}
+
+int oc_features_in_area(const oc_camera* c, const oc_kp* kps, const oc_grid* g,
+                        float x, float y, float r, int minLevel, int maxLevel,
+                        int* out, int cap)
+{
+    int n = 0;
+    const int nMinCellX = imax(0, (int)floorf((x - c->min_x - r) * c->grid_inv_w));
+    if (nMinCellX >= OC_GRID_COLS) return 0;
+    const int nMaxCellX = imin(OC_GRID_COLS - 1, (int)ceilf((x - c->min_x + r) * c->grid_inv_w));
+    if (nMaxCellX < 0) return 0;
+    const int nMinCellY = imax(0, (int)floorf((y - c->min_y - r) * c->grid_inv_h));
+    if (nMinCellY >= OC_GRID_ROWS) return 0;
+    const int nMaxCellY = imin(OC_GRID_ROWS - 1, (int)ceilf((y - c->min_y + r) * c->grid_inv_h));
+    if (nMaxCellY < 0) return 0;
+    const int bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+            int cidx = ix * OC_GRID_ROWS + iy;
+            for (int j = g->cell_start[cidx]; j < g->cell_start[cidx + 1]; j++) {
+                const oc_kp* kp = &kps[g->cell_idx[j]];
+                if (bCheckLevels) {
+                    if (kp->octave < minLevel) continue;
+                    if (maxLevel >= 0 && kp->octave > maxLevel) continue;
+                }
+                const float distx = kp->x - x, disty = kp->y - y;
+                if (fabsf(distx) < r && fabsf(disty) < r) {
+                    if (n < cap) out[n] = g->cell_idx[j];
+                    n++;
+                }
+            }
+        }
+    }
+    return n;
+}
+
+int oc_descriptor_distance(const uint8_t* a, const uint8_t* b)
+{
+    int dist = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t pa, pb;
+        memcpy(&pa, a + 4 * i, 4);
+        memcpy(&pb, b + 4 * i, 4);
+        unsigned int v = pa ^ pb;
+        v = v - ((v >> 1) & 0x55555555);
+        v = (v & 0x33333333) + ((v >> 2) & 0x33333333);
+        dist += (((v + (v >> 4)) & 0xF0F0F0F) * 0x1010101) >> 24;
+    }
+    return dist;
+}
+
+/* ORBmatcher::ComputeThreeMaxima (src/ORBmatcher.cc:1602-1643) */
+static void three_maxima(const int* hist, int L, int* i1, int* i2, int* i3)
+{
+    int max1 = 0, max2 = 0, max3 = 0;
+    *i1 = *i2 = *i3 = -1;
+    for (int i = 0; i < L; i++) {
+        const int s = hist[i];
+        if (s > max1) { max3 = max2; max2 = max1; max1 = s; *i3 = *i2; *i2 = *i1; *i1 = i; }
+        else if (s > max2) { max3 = max2; max2 = s; *i3 = *i2; *i2 = i; }
+        else if (s > max3) { max3 = s; *i3 = i; }
+    }
+    if (max2 < 0.1f * (float)max1) { *i2 = -1; *i3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { *i3 = -1; }
+}
+
+int oc_search_by_projection(const oc_camera* cam, const oc_curframe* cur, const oc_lastframe* last,
+                            const float Tcw_cur[16], const float Tcw_last[16],
+                            float th, int bMono, int check_ori, int32_t* match_out)
+{
+    enum { HISTO_LENGTH = 30, TH_HIGH = 100 };
+    int nmatches = 0;
+    const float factor = 1.0f / HISTO_LENGTH;
+    const float* T = Tcw_cur;
+    const float* Tl = Tcw_last;
+    /* twc = -Rcw.t()*tcw (GEMM_1_T: generic path, double accumulation) */
+    float twc[3], tlc[3];
+    for (int k = 0; k < 3; k++) {
+        double s = (double)T[0 * 4 + k] * T[3] + (double)T[1 * 4 + k] * T[7];
+        s = s + (double)T[2 * 4 + k] * T[11];
+        twc[k] = (float)(s * -1.0);
+    }
+    /* tlc = Rlw*twc + tlw (small-matrix float path) */
+    for (int k = 0; k < 3; k++) {
+        float t = Tl[k * 4 + 0] * twc[0] + Tl[k * 4 + 1] * twc[1];
+        t = t + Tl[k * 4 + 2] * twc[2];
+        tlc[k] = (float)((double)t + (double)Tl[k * 4 + 3]);
+    }
+    const int bForward = tlc[2] > cam->mb && !bMono;
+    const int bBackward = -tlc[2] > cam->mb && !bMono;
+
+    oc_grid g;
+    g.cell_start = (int*)malloc(sizeof(int) * (OC_GRID_COLS * OC_GRID_ROWS + 1));
+    g.cell_idx = (int*)malloc(sizeof(int) * (cur->n > 0 ? cur->n : 1));
+    oc_assign_grid(cam, cur->keys_un, cur->n, &g);
+
+    int* owner = match_out;                       /* CurrentFrame.mvpMapPoints as slot ids */
+    for (int i = 0; i < cur->n; i++) owner[i] = -1;
+    int* hist_items = (int*)malloc(sizeof(int) * (last->n > 0 ? last->n : 1) * 2);
+    int* hist_bin = hist_items + (last->n > 0 ? last->n : 1);
+    int nhist = 0;
+    int* cand = (int*)malloc(sizeof(int) * (cur->n > 0 ? cur->n : 1));
+
+    for (int i = 0; i < last->n; i++) {
+        if (!last->has_mp[i] || last->outlier[i]) continue;
+        const float* X = &last->xw[3 * i];
+        float p3[3];
+        for (int k = 0; k < 3; k++) {             /* x3Dc = Rcw*x3Dw+tcw (small-matrix path) */
+            float t = T[k * 4 + 0] * X[0] + T[k * 4 + 1] * X[1];
+            t = t + T[k * 4 + 2] * X[2];
+            p3[k] = (float)((double)t + (double)T[k * 4 + 3]);
+        }
+        const float xc = p3[0], yc = p3[1];
+        const float invzc = (float)(1.0 / (double)p3[2]);
+        if (invzc < 0) continue;
+        float u = fmaf(cam->fx * xc, invzc, cam->cx);   /* fused in the reference binary */
+        float v = fmaf(cam->fy * yc, invzc, cam->cy);
+        if (u < cam->min_x || u > cam->max_x) continue;
+        if (v < cam->min_y || v > cam->max_y) continue;
+        int nLastOctave = last->keys_un[i].octave;
+        float radius = th * cam->scale[nLastOctave];
+        int nc;
+        if (bForward) nc = oc_features_in_area(cam, cur->keys_un, &g, u, v, radius, nLastOctave, -1, cand, cur->n);
+        else if (bBackward) nc = oc_features_in_area(cam, cur->keys_un, &g, u, v, radius, 0, nLastOctave, cand, cur->n);
+        else nc = oc_features_in_area(cam, cur->keys_un, &g, u, v, radius, nLastOctave - 1, nLastOctave + 1, cand, cur->n);
+        if (nc == 0) continue;
+        const uint8_t* dMP = &last->mp_desc[32 * i];
+        int bestDist = 256, bestIdx2 = -1;
+        for (int c = 0; c < nc; c++) {
+            const int i2 = cand[c];
+            if (owner[i2] >= 0 && last->mp_nobs[owner[i2]] > 0) continue;
+            if (cur->uright[i2] > 0) {
+                const float ur = fmaf(-cam->bf, invzc, u);   /* u - mbf*invzc, fused */
+                const float er = fabsf(ur - cur->uright[i2]);
+                if (er > radius) continue;
+            }
+            const int dist = oc_descriptor_distance(dMP, &cur->desc[32 * i2]);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = i2; }
+        }
+        if (bestDist <= TH_HIGH) {
+            owner[bestIdx2] = i;
+            nmatches++;
+            if (check_ori) {
+                float rot = last->keys_un[i].angle - cur->keys_un[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == HISTO_LENGTH) bin = 0;
+                hist_items[nhist] = bestIdx2;
+                hist_bin[nhist] = bin;
+                nhist++;
+            }
+        }
+    }
+    if (check_ori) {
+        int hist[HISTO_LENGTH] = {0};
+        for (int k = 0; k < nhist; k++) hist[hist_bin[k]]++;
+        int i1, i2, i3;
+        three_maxima(hist, HISTO_LENGTH, &i1, &i2, &i3);
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b == i1 || b == i2 || b == i3) continue;
+            for (int k = 0; k < nhist; k++)
+                if (hist_bin[k] == b) { owner[hist_items[k]] = -1; nmatches--; }
+        }
+    }
+    free(cand);
+    free(hist_items);
+    free(g.cell_start);
+    free(g.cell_idx);
+    return nmatches;
+}

@@ -1,0 +1,150 @@
+/*
+ * orb_oracle.h -- CPU restatement of COEB-SLAM's per-frame ORB front end.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the timed CPU
+ * baseline.  The product (coeb-slam_amd/, libcoeb_front.so) never links or calls it.
+ *
+ * PARITY STATUS: "parity unpinned" against the original reference binary.  The reference
+ * (src/ORBextractor.cc, src/ORBmatcher.cc, src/Frame.cc) needs OpenCV 3.4, which is absent
+ * from this image, and it ships no tests or golden vectors.  This
+ * restatement is pinned by the reference's own tables (bit_pattern_31_, umax, level sizes,
+ * features per level, DescriptorDistance) and restates the OpenCV 3.4 primitives with the
+ * canonical definitions documented in DESIGN.md s3 (resize, FAST, GaussianBlur, fastAtan2,
+ * sincosf, Laplacian, cvtColor).
+ *
+ * Every function cites the reference file:line it follows.
+ */
+#ifndef ORB_ORACLE_H
+#define ORB_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OC_MAX_LEVELS 16
+
+/* layout-identical to cv::KeyPoint (28 B) */
+typedef struct { float x, y, size, angle, response; int32_t octave, class_id; } oc_kp;
+typedef struct { float xmin, ymin, xmax, ymax; } oc_box;
+
+/* ORBextractor::ORBextractor tables (src/ORBextractor.cc:418-477) */
+typedef struct {
+    int nfeatures;
+    double scale_factor;           /* `double scaleFactor` member (ORBextractor.h:114) */
+    int nlevels;
+    int ini_th, min_th;            /* overridden to 20/7 or 30/10 (ORBextractor.cc:775-784) */
+    float scale[OC_MAX_LEVELS], inv_scale[OC_MAX_LEVELS];
+    float sigma2[OC_MAX_LEVELS], inv_sigma2[OC_MAX_LEVELS];
+    int nfeat[OC_MAX_LEVELS];
+    int umax[16];
+    int pattern[512][2];
+} oc_params;
+
+int oc_init(oc_params* p, int nfeatures, float scale_factor, int nlevels, int ini_th, int min_th);
+void oc_level_size(const oc_params* p, int w, int h, int level, int* lw, int* lh);
+
+/* cv::resize INTER_LINEAR 8U (canonical) used by ComputePyramid :1356 */
+void oc_resize_linear(const uint8_t* src, int sw, int sh, int sstride,
+                      uint8_t* dst, int dw, int dh, int dstride);
+/* ComputePyramid (src/ORBextractor.cc:1344-1367); levels packed, level l stride = lw */
+int oc_pyramid(const oc_params* p, const uint8_t* gray, int w, int h, int stride,
+               uint8_t* out, int64_t* level_off);
+
+/* cv::FAST(roi, kps, th, nonmax=true) on an ROI (OpenCV FAST_t<16>); xs/ys/score out */
+int oc_fast_roi(const uint8_t* img, int stride, int rows, int cols, int threshold,
+                int* xs, int* ys, int* score, int cap);
+/* FAST stage of ComputeKeyPointsOctTree (src/ORBextractor.cc:786-850) for one level:
+ * candidates relative to (16,16), canonical order. */
+int oc_level_candidates(const uint8_t* lvl, int lw, int lh, int stride, int ini_th, int min_th,
+                        int* xs, int* ys, int* score, int cap);
+/* DistributeOctTree (src/ORBextractor.cc:546-769), pointer tie-break = allocation order */
+int oc_distribute_octree(const int* xs, const int* ys, const int* score, int n,
+                         int minX, int maxX, int minY, int maxY, int N,
+                         int* out_idx, int cap);
+
+int oc_ic_angle_moments(const uint8_t* img, int stride, int x, int y, const int* umax,
+                        int* m01, int* m10);
+float oc_fast_atan2(float y, float x);
+void oc_sincos(float a, float* s, float* c);
+void oc_gauss_kernel7(int k[7]);
+void oc_gaussian_blur7(const uint8_t* src, int w, int h, int sstride, uint8_t* dst, int dstride);
+void oc_orb_descriptor(const uint8_t* blurred, int stride, int x, int y, float angle,
+                       const int (*pattern)[2], uint8_t desc[32]);
+
+/* mask layers of operator() (src/ORBextractor.cc:1101-1195); mask is w x h */
+int oc_dynamic_mask(const oc_box* boxes, int nbox, const float* tm_xy, int ntm,
+                    const int32_t* blur_flag, int nblur, int w, int h,
+                    uint8_t* mask, float* area_out);
+
+typedef struct {
+    uint8_t* pyramid;              /* optional: packed levels (oc_pyramid layout) */
+    int64_t level_off[OC_MAX_LEVELS + 1];
+    int ncand[OC_MAX_LEVELS];      /* FAST candidates per level (before any cull) */
+    int nkept[OC_MAX_LEVELS];      /* keypoints per level in the output */
+    int area_flag;
+} oc_debug;
+
+/* ORBextractor::operator() (src/ORBextractor.cc:1088-1342), debug imshow block excluded */
+int oc_extract(const oc_params* p, const uint8_t* gray, int w, int h, int stride,
+               const oc_box* boxes, int nbox, const float* tm_xy, int ntm,
+               const int32_t* blur_flag, int nblur,
+               oc_kp* kp_out, uint8_t* desc_out, int cap, int* n_out, oc_debug* dbg);
+
+/* Frame blur flag (src/Frame.cc:171-202, 905-913) */
+int oc_blur_flags(const uint8_t* gray, int w, int h, int stride,
+                  const oc_box* boxes, int nbox, int32_t* out, double* mean_out);
+/* Tracking::GrabImageRGBD cvtColor RGB->GRAY 8U (src/Tracking.cc:212-225) */
+void oc_rgb2gray(const uint8_t* rgb, int w, int h, int stride, int rgb_order, uint8_t* out);
+
+/* ---- matcher side ---- */
+typedef struct {
+    float fx, fy, cx, cy, bf, mb;
+    float min_x, max_x, min_y, max_y;
+    float grid_inv_w, grid_inv_h;
+    float scale[OC_MAX_LEVELS];
+    int nlevels;
+} oc_camera;
+void oc_camera_init(oc_camera* c, float fx, float fy, float cx, float cy, float bf,
+                    int w, int h, const oc_params* p);
+
+/* Frame::ComputeStereoFromRGBD (src/Frame.cc:820-842) */
+void oc_stereo_from_rgbd(const oc_kp* kps, int n, const float* depth, int w, int dstride,
+                         float bf, float* uright, float* dep);
+
+#define OC_GRID_COLS 64
+#define OC_GRID_ROWS 48
+typedef struct {
+    int* cell_start;   /* [GRID_COLS*GRID_ROWS+1], cell index ix*GRID_ROWS+iy */
+    int* cell_idx;     /* [n] keypoint indices in insertion order */
+} oc_grid;
+/* Frame::AssignFeaturesToGrid / PosInGrid (src/Frame.cc:396-411, 558-568) */
+void oc_assign_grid(const oc_camera* c, const oc_kp* kps, int n, oc_grid* g);
+/* Frame::GetFeaturesInArea (src/Frame.cc:503-556) */
+int oc_features_in_area(const oc_camera* c, const oc_kp* kps, const oc_grid* g,
+                        float x, float y, float r, int minLevel, int maxLevel,
+                        int* out, int cap);
+
+int oc_descriptor_distance(const uint8_t* a, const uint8_t* b);  /* ORBmatcher.cc:1648 */
+
+typedef struct {
+    int n;
+    const uint8_t* has_mp; const uint8_t* outlier;
+    const float* xw; const uint8_t* mp_desc; const int32_t* mp_nobs;
+    const oc_kp* keys_un;
+} oc_lastframe;
+typedef struct {
+    int n; const oc_kp* keys_un; const uint8_t* desc; const float* uright;
+} oc_curframe;
+
+/* ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) (ORBmatcher.cc:1329-1471)
+ * match_out[i2] = index of the LastFrame slot whose MapPoint was assigned, or -1 */
+int oc_search_by_projection(const oc_camera* cam, const oc_curframe* cur, const oc_lastframe* last,
+                            const float Tcw_cur[16], const float Tcw_last[16],
+                            float th, int bMono, int check_ori, int32_t* match_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
