@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Benchmark: frames/s of the ORB front end (extract + Hamming match to the previous frame)
+on synthetic 640x480 input, 8 levels, 1000 keypoints (BASELINE.json configs[1]).
+
+A step = one pass of the hot path over one batch of B frames already resident in HBM:
+extraction of B+1 frames (frame 0 is the halo that gives frame 1 its LastFrame) and B
+SearchByProjection calls (th = 15, retried at 30 below 20 matches, Tracking.cc:947-958).
+Only the B matched frames are counted.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one
+process per GPU, each with its own batch (frames are independent; no data-path collective,
+scaling "weak").  torch.distributed (gloo) is used only for the barrier and the max-over-
+ranks of the timed interval; the GPU work is libcoeb_front.so's (torch.cuda is never
+initialised: the torch wheel bundles its own HIP runtime).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "coeb-slam_amd"))
+
+import numpy as np  # noqa: E402
+
+METRIC = "frames/sec ORB extract+match @640x480/1000 kp; 1/2/4/8 GPU + %HBM roofline"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
+CONFIGS = {
+    "A": dict(w=640, h=480, nfeatures=1000, workload="640x480, 8-level pyramid, 1000 kp, extract + Hamming match to prev frame (BASELINE configs[1])"),
+    "B": dict(w=1280, h=960, nfeatures=2000, workload="1280x960, 8-level pyramid, 2000 kp, extract + match (BASELINE configs[3] shape)"),
+}
+
+
+def level_pixels(w, h, nlevels=8, scale=1.2):
+    s, tot = 1.0, 0
+    for l in range(nlevels):
+        if l:
+            s = float(np.float32(np.float64(np.float32(s)) * np.float64(np.float32(scale))))
+        inv = np.float32(1.0) / np.float32(s)
+        tot += int(np.rint(np.float32(w) * inv)) * int(np.rint(np.float32(h) * inv))
+    return tot
+
+
+def kernel_bytes(name, w, h, nkp, nprev, npx, ncand):
+    """Algorithmic (compulsory) HBM bytes of one launch per frame, DESIGN.md s5."""
+    if name == "k_fast":        # read every pyramid level once, write candidate keys
+        return npx + 4 * ncand
+    if name == "k_blur":        # read + write every level
+        return 2 * npx
+    if name == "k_pyr_level":   # 7 launches: read level l-1, write level l (sum over launches / 7)
+        return 2 * (npx - w * h) / 7.0 + w * h / 7.0
+    if name == "k_octree":      # read candidates, write level keypoints
+        return 4 * ncand + 4 * nkp
+    if name == "k_describe":    # 31x31 + 37x37 patches are cache reads; compulsory: keypoints+descs out
+        return 4 * nkp + 60 * nkp
+    if name == "k_match":       # read current kps+descs and LastFrame snapshot, write matches
+        return 60 * nkp + (32 + 28 + 12 + 4) * nprev + 4 * nkp
+    if name == "k_prep":
+        return 28 * nkp + 4 * nkp + 25 * nkp
+    return 0
+
+
+def cpu_baseline(cfg, seconds=12.0, min_frames=30):
+    """Oracle ('port') timed single-threaded on this host: extract + ComputeStereoFromRGBD +
+    SearchByProjection (retry at 2*th) per frame, on consecutive synthetic frames."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"])
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes as C
+    import oracle as O
+    from coeb_front import synth
+    O.LIB = os.path.join(ROOT, "oracle", "liborb_oracle_native.so")
+    O._lib = None
+    w, h = cfg["w"], cfg["h"]
+    ex = O.Extractor(cfg["nfeatures"], 1.2, 8, 20, 7)
+    cam = O.camera(ex, w, h, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    depth = synth.make_depth(w, h)
+    nfr = 64
+    frames = synth.make_frames(w, h, nfr, seed=5151)
+    Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
+    prev = ex.extract(frames[0])
+    for i in range(1, 4):          # warm-up
+        prev = ex.extract(frames[i])
+    times = []
+    t_end = time.perf_counter() + seconds
+    i = 4
+    while (time.perf_counter() < t_end or len(times) < min_frames) and len(times) < 400:
+        f = frames[i % nfr]
+        last = O.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX, synth.TUM_FY,
+                                          synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)   # map snapshot (untimed)
+        t0 = time.perf_counter()
+        r = ex.extract(f)
+        ur, _ = O.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
+        nm, _ = O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 15.0)
+        if nm < 20:
+            O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 30.0)
+        times.append(time.perf_counter() - t0)
+        prev = r
+        i += 1
+    med = float(np.median(times))
+    return dict(value=round(1.0 / med, 3), unit="frames/s", cores=1, kind="port",
+                sample="%d consecutive %dx%d synthetic frames, oracle (-O3 -march=native) single thread: "
+                       "extract + ComputeStereoFromRGBD + SearchByProjection(th 15, retry 30); median %.2f ms/frame"
+                       % (len(times), w, h, med * 1e3))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="matched frames per step per GPU")
+    ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip HIP-event kernel timing")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from coeb_front import synth
+    from coeb_front.pipeline import BatchPipeline
+    cfg = CONFIGS[args.config]
+    w, h = cfg["w"], cfg["h"]
+    F = args.batch + 1
+    frames = synth.make_frames(w, h, F, seed=1000 + 17 * rank)
+    Tcw = np.stack([synth.motion_pose()] * F)
+    bp = BatchPipeline(w, h, F, nfeatures=cfg["nfeatures"], device=local_rank)
+    bp.load(frames, Tcw=Tcw)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        bp.run()
+    bp.synchronize()
+    out, matches, nms = bp.results()
+    nkp = float(np.mean([len(o[0]) for o in out[1:]]))
+    nmatch = float(np.mean(nms[1:]))
+    ncand = int(bp.ctx.debug_read("cand_n", 1).view(np.int32).sum())
+    if not args.no_profile:
+        bp.ctx.profile(True)
+        bp.ctx.profile_reset()
+
+    barrier()
+    bp.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        bp.run()
+    bp.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = bp.ctx.profile_read() if not args.no_profile else {}
+
+    frames_total = args.batch * args.steps * world
+    value = frames_total / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        npx = level_pixels(w, h)
+        roof = None
+        if prof:
+            dom = max(prof.items(), key=lambda kv: kv[1][0])
+            name, (tot_ms, launches) = dom
+            avg_s = tot_ms / launches / 1e3
+            frames_per_launch = F if name != "k_match" else F - 1
+            if name == "k_pyr_level":
+                frames_per_launch = F
+            bpl = kernel_bytes(name, w, h, nkp, nkp, npx, ncand) * frames_per_launch
+            achieved = bpl / avg_s / 1e9
+            roof = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None, kernel=name,
+                        avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=int(bpl))
+        pipeline_bytes = w * h + 60 * nkp + 36 * nkp     # B = W*H + 60 N_kp + 36 N_prev
+        line = dict(metric=METRIC, value=round(value, 2), unit="frames/s", n_gpus=world, steps=args.steps,
+                    warmup=args.warmup, ms_per_step=round(ms_per_step, 4), higher_is_better=True,
+                    scaling="weak", vs_baseline=None, dtype="u8",
+                    data="synthetic (TUM-like rectangles + noise, (+2,+1) px/frame, Z=2 m)",
+                    config=dict(workload=cfg["workload"], width=w, height=h, nfeatures=cfg["nfeatures"],
+                                nlevels=8, frames_per_step_per_gpu=args.batch, halo_frames_per_step=1,
+                                parallelism="frame-sharded x%d (no collectives)" % world),
+                    roofline=roof,
+                    pipeline_roofline=dict(bytes_per_frame=int(pipeline_bytes),
+                                           achieved_GBps=round(value * pipeline_bytes / 1e9, 3),
+                                           frac=round(value * pipeline_bytes / 1e9 / HBM_PEAK_GBS, 6)),
+                    kernels_ms_per_step={k: round(v[0] / max(1, args.steps), 4) for k, v in prof.items()},
+                    keypoints_per_frame=round(nkp, 1), matches_per_frame=round(nmatch, 1))
+        if not args.no_cpu_baseline and world == 1:
+            cb = cpu_baseline(cfg)
+            line["cpu_baseline"] = cb
+            line["speedup_vs_cpu_baseline"] = round(value / cb["value"], 1)
+        print(json.dumps(line), flush=True)
+    bp.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

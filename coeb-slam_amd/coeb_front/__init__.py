@@ -34,6 +34,7 @@ ABI_SYMBOLS = [
     "coeb_batch_match_results", "coeb_match_lastframe", "coeb_blur_flags", "coeb_stereo_from_rgbd",
     "coeb_rgbd_preprocess", "coeb_descriptor_distance", "coeb_profile_enable", "coeb_profile_read",
     "coeb_profile_reset", "coeb_synchronize", "coeb_device_count", "coeb_debug_read",
+    "coeb_device_alloc", "coeb_device_free", "coeb_memcpy_h2d", "coeb_memcpy_d2h",
 ]
 
 
@@ -109,6 +110,10 @@ def lib():
         L.coeb_profile_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                         C.POINTER(C.c_int)]
         L.coeb_synchronize.argtypes = [C.c_void_p]
+        L.coeb_device_alloc.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]
+        L.coeb_device_free.argtypes = [C.c_void_p, C.c_void_p]
+        L.coeb_memcpy_h2d.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        L.coeb_memcpy_d2h.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
         L.coeb_debug_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_size_t,
                                       C.POINTER(C.c_size_t)]
         _lib = L
@@ -219,6 +224,22 @@ class Context:
         self.check(lib().coeb_debug_read(self.h, what.encode(), f, _p(buf), size.value, C.byref(size)))
         return buf
 
+    # ---- caller-owned device buffers ----
+    def alloc(self, nbytes):
+        return DeviceBuffer(self, nbytes)
+
+    def upload(self, arr):
+        arr = np.ascontiguousarray(arr)
+        buf = DeviceBuffer(self, arr.nbytes)
+        buf.write(arr)
+        return buf
+
+    def download(self, dptr, nbytes, dtype=np.uint8):
+        out = np.empty(nbytes // np.dtype(dtype).itemsize, dtype)
+        if nbytes:
+            self.check(lib().coeb_memcpy_d2h(self.h, _p(out), C.c_void_p(dptr), nbytes))
+        return out
+
     # ---- profiling (HIP events on the context stream) ----
     def profile(self, enable=True):
         self.check(lib().coeb_profile_enable(self.h, int(enable)))
@@ -234,6 +255,40 @@ class Context:
         self.check(lib().coeb_profile_read(self.h, names, 4096, _p(ms), _p(cnt), 64, C.byref(nk)))
         nm = names.value.decode().split(",") if nk.value else []
         return {nm[i]: (float(ms[i]), int(cnt[i])) for i in range(nk.value)}
+
+
+class DeviceBuffer:
+    """hipMalloc'ed buffer on the context's device (torch.cuda is not used in-process: the
+    torch wheel bundles its own HIP/HSA runtime, which cannot share a process with the
+    system ROCm runtime libcoeb_front.so links)."""
+
+    def __init__(self, ctx, nbytes):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        ctx.check(lib().coeb_device_alloc(ctx.h, self.nbytes, C.byref(p)))
+        self.ptr = p.value
+
+    def write(self, arr, offset=0):
+        arr = np.ascontiguousarray(arr)
+        assert offset + arr.nbytes <= self.nbytes
+        self.ctx.check(lib().coeb_memcpy_h2d(self.ctx.h, C.c_void_p(self.ptr + offset), _p(arr), arr.nbytes))
+
+    def read(self, dtype=np.uint8, count=None, offset=0):
+        dt = np.dtype(dtype)
+        count = (self.nbytes - offset) // dt.itemsize if count is None else count
+        return self.ctx.download(self.ptr + offset, count * dt.itemsize, dt)
+
+    def free(self):
+        if self.ptr is not None and self.ctx.h is not None:
+            lib().coeb_device_free(self.ctx.h, C.c_void_p(self.ptr))
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class ORBextractor:

@@ -863,6 +863,42 @@ int coeb_profile_read(coeb_ctx* c, char* names, int cap, double* total_ms, int64
     return COEB_OK;
 }
 
+int coeb_device_alloc(coeb_ctx* c, size_t bytes, void** dptr)
+{
+    if (!c || !dptr) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    hipError_t e = hipMalloc(dptr, std::max<size_t>(bytes, 1));
+    if (e != hipSuccess) return set_err(c, COEB_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return COEB_OK;
+}
+
+int coeb_device_free(coeb_ctx* c, void* dptr)
+{
+    if (!c) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (dptr) HIP_TRY(c, hipFree(dptr));
+    return COEB_OK;
+}
+
+int coeb_memcpy_h2d(coeb_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c || (bytes && (!dst || !src))) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return COEB_OK;
+}
+
+int coeb_memcpy_d2h(coeb_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c || (bytes && (!dst || !src))) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return COEB_OK;
+}
+
 int coeb_internal_stream(coeb_ctx* c, hipStream_t* s, int* device)
 {
     if (!c) return COEB_EINVAL;

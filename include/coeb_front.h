@@ -174,6 +174,14 @@ int coeb_rgbd_preprocess(coeb_ctx* ctx, const uint8_t* rgb, size_t rgb_stride, i
 
 int coeb_descriptor_distance(const uint8_t* a, const uint8_t* b);
 
+/* ---- device memory owned by the caller (for the device-resident batch entry points) ----
+ * Plain hipMalloc'ed buffers on the context's device.  Copies are synchronous w.r.t. the
+ * context stream (they are enqueued on it and waited for). */
+int coeb_device_alloc(coeb_ctx* ctx, size_t bytes, void** dptr);
+int coeb_device_free(coeb_ctx* ctx, void* dptr);
+int coeb_memcpy_h2d(coeb_ctx* ctx, void* dst, const void* src, size_t bytes);
+int coeb_memcpy_d2h(coeb_ctx* ctx, void* dst, const void* src, size_t bytes);
+
 /* ---- measurement ---- */
 /* Per-kernel device time accumulated with HIP events on the context stream while profiling
  * is enabled.  names: comma-separated list written to `names` (cap bytes). */

@@ -1,0 +1,283 @@
+"""HIP path (through the C-ABI) vs the CPU oracle, bit-exact (MI355X only).
+
+Tolerances (BASELINE.json north_star): keypoint coordinates/octave/size/response and the
+256-bit descriptors bit-exact; angles within 1e-4 degrees -- and this build also asserts
+they are bit-identical (descriptors depend on the angle bits through sincosf).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from coeb_front import KEYPOINT_DTYPE, synth
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+ANGLE_TOL = 1e-4
+
+
+def assert_same(kps, desc, ref_kps, ref_desc, tag=""):
+    assert len(kps) == len(ref_kps), (tag, len(kps), len(ref_kps))
+    for f in KEYPOINT_DTYPE.names:
+        if f == "angle":
+            assert np.all(np.abs(kps[f] - ref_kps[f]) <= ANGLE_TOL), tag
+        bad = np.nonzero(kps[f] != ref_kps[f])[0]
+        assert len(bad) == 0, (tag, f, len(bad), kps[bad[:3]], ref_kps[bad[:3]])
+    if len(kps):
+        assert np.array_equal(desc, ref_desc), (tag, int((desc != ref_desc).any(axis=1).sum()))
+
+
+def run_both(ctx, ex, gray, boxes=None, tm=None, blur=None, tag=""):
+    r = ex.extract(gray, boxes, tm, blur)
+    k, d = ctx.extract(gray, boxes, tm, blur)
+    assert_same(k, d, r["kps"], r["desc"], tag)
+    return k, d
+
+
+@pytest.fixture(scope="module")
+def ex(oracle_mod):
+    return oracle_mod.Extractor()
+
+
+def test_golden_extract(ctx):
+    g = np.load(os.path.join(HERE, "golden", "extract_A.npz"))
+    for name in ("plain", "dyn", "area"):
+        args = () if name == "plain" else (g[name + "_boxes"], g[name + "_tm"], g[name + "_blur"])
+        k, d = ctx.extract(g["frame"], *args)
+        assert_same(k, d, g[name + "_kps"], g[name + "_desc"], name)
+
+
+@pytest.mark.parametrize("seed", [1000, 1001, 1002, 7])
+def test_extract_A_frames(ctx, ex, seed):
+    fr = synth.make_frames(640, 480, 3, seed=seed)
+    for i in range(3):
+        run_both(ctx, ex, fr[i], tag="seed%d f%d" % (seed, i))
+
+
+def test_extract_B_1280x960(ctx, oracle_mod):
+    ex2 = oracle_mod.Extractor(2000, 1.2, 8, 20, 7)
+    from coeb_front import Context
+    c2 = Context(2000, 1.2, 8, 20, 7, max_width=1280, max_height=960)
+    try:
+        fr = synth.make_frames(1280, 960, 1, seed=2000)
+        run_both(c2, ex2, fr[0], tag="B")
+        b, t, bl = synth.dynamic_inputs(1280, 960)
+        run_both(c2, ex2, fr[0], b, t, bl, tag="B dyn")
+    finally:
+        c2.close()
+
+
+@pytest.mark.parametrize("w,h", [(641, 479), (320, 240), (800, 600), (1024, 768), (720, 405)])
+def test_extract_ragged_sizes(ctx, ex, w, h):
+    fr = synth.make_frames(w, h, 1, seed=w * 7 + h)
+    run_both(ctx, ex, fr[0], tag="%dx%d" % (w, h))
+
+
+@pytest.mark.parametrize("nfeat,scale,nlev", [(500, 1.2, 8), (2000, 1.2, 8), (1000, 1.3, 6), (1000, 1.2, 4),
+                                              (1000, 1.1, 10)])
+def test_extract_params(oracle_mod, nfeat, scale, nlev):
+    """nlevels = 10 exercises CheckMovingKeyPoints_finall's hard-coded 8-level loop."""
+    from coeb_front import Context
+    ex2 = oracle_mod.Extractor(nfeat, scale, nlev, 20, 7)
+    c2 = Context(nfeat, scale, nlev, 20, 7, max_width=640, max_height=480)
+    try:
+        fr = synth.make_frames(640, 480, 1, seed=nfeat + nlev)
+        run_both(c2, ex2, fr[0], tag="params")
+        b, t, bl = synth.dynamic_inputs(640, 480)
+        run_both(c2, ex2, fr[0], b, t, bl, tag="params dyn")
+    finally:
+        c2.close()
+
+
+def test_extract_edge_images(ctx, ex):
+    # constant: no corners at all; near-constant: only minThFAST fallback corners
+    run_both(ctx, ex, np.full((480, 640), 128, np.uint8), tag="const")
+    rng = np.random.default_rng(5)
+    run_both(ctx, ex, np.clip(128 + rng.integers(-5, 6, (480, 640)), 0, 255).astype(np.uint8), tag="low")
+    # high texture: thousands of candidates per level (octree final phase, size ties)
+    run_both(ctx, ex, rng.integers(0, 256, (480, 640), dtype=np.uint8), tag="noise")
+    chk = ((np.indices((480, 640)).sum(axis=0) // 3) % 2 * 255).astype(np.uint8)
+    run_both(ctx, ex, chk, tag="checker")
+    k, d = ctx.extract(np.zeros((0, 0), np.uint8))
+    assert len(k) == 0 and d is None
+
+
+def test_extract_dynamic_masks(ctx, ex):
+    fr = synth.make_frames(640, 480, 1, seed=1234)[0]
+    b, t, bl = synth.dynamic_inputs(640, 480, seed=3)
+    run_both(ctx, ex, fr, b, t, bl, tag="dyn")
+    run_both(ctx, ex, fr, b, t, None, tag="no blur flags (missing -> 0)")
+    run_both(ctx, ex, fr, b, t[:0], np.array([1, 1], np.int32), tag="no T_M")
+    b2, t2, bl2 = synth.dynamic_inputs(640, 480, seed=4, area_flag=True)
+    run_both(ctx, ex, fr, b2, t2, bl2, tag="area")
+    # fractional boxes: Rect(int(x), int(y), int(w), int(h)) vs fill loop (int)xmin..(int)xmax
+    b3 = np.array([[100.7, 50.2, 300.4, 420.9], [0.0, 0.0, 639.0, 479.0]], np.float32)
+    t3 = np.array([[150.5, 60.5], [299.9, 419.9], [10, 10]], np.float32)
+    run_both(ctx, ex, fr, b3, t3, np.array([1, 0], np.int32), tag="fractional")
+
+
+def test_blur_flags(ctx, oracle_mod):
+    from coeb_front import lib
+    import ctypes as C
+    fr = synth.make_frames(640, 480, 1, seed=9)[0]
+    sm = fr.copy()
+    sm[100:300, 200:320] = 90           # flat region -> blurred -> flag 1
+    boxes = np.array([[200, 100, 320, 300], [10.5, 20.5, 200.2, 400.7], [630, 470, 640, 480], [0, 0, 1, 1],
+                      [-5, 0, 10, 10]], np.float32)
+    ref, _ = oracle_mod.blur_flags(sm, boxes)
+    out = np.zeros(len(boxes), np.int32)
+    ctx.check(lib().coeb_blur_flags(ctx.h, sm.ctypes.data_as(C.c_void_p), 640, 480, 640,
+                                    boxes.ctypes.data_as(C.c_void_p), len(boxes), out.ctypes.data_as(C.c_void_p)))
+    assert np.array_equal(out, ref) and ref[0] == 1
+
+
+def test_rgbd_preprocess_and_stereo(ctx, oracle_mod):
+    from coeb_front import lib
+    import ctypes as C
+    rng = np.random.default_rng(3)
+    rgb = rng.integers(0, 256, (480, 640, 3), dtype=np.uint8)
+    d16 = rng.integers(0, 6000, (480, 640), dtype=np.uint16)
+    gray = np.zeros((480, 640), np.uint8)
+    dep = np.zeros((480, 640), np.float32)
+    ctx.check(lib().coeb_rgbd_preprocess(ctx.h, rgb.ctypes.data_as(C.c_void_p), 640 * 3, 1,
+                                         d16.ctypes.data_as(C.c_void_p), 640, C.c_float(1 / 5000.0), 640, 480,
+                                         gray.ctypes.data_as(C.c_void_p), dep.ctypes.data_as(C.c_void_p)))
+    assert np.array_equal(gray, oracle_mod.rgb2gray(rgb, 1))
+    assert np.array_equal(dep, d16.astype(np.float32) * np.float32(1 / 5000.0))
+    k, d = ctx.extract(gray)
+    ur_ref, dep_ref = oracle_mod.stereo_from_rgbd(k, dep, synth.TUM_BF)
+    ur = np.zeros(len(k), np.float32)
+    dd = np.zeros(len(k), np.float32)
+    ctx.check(lib().coeb_stereo_from_rgbd(ctx.h, k.ctypes.data_as(C.c_void_p), len(k), dep.ctypes.data_as(C.c_void_p),
+                                          640, 480, 640, C.c_float(synth.TUM_BF), ur.ctypes.data_as(C.c_void_p),
+                                          dd.ctypes.data_as(C.c_void_p)))
+    assert np.array_equal(ur, ur_ref) and np.array_equal(dd, dep_ref)
+
+
+# ------------------------------------------------------------------ matcher
+def match_both(ctx, oracle_mod, ex, cur_k, cur_d, cur_ur, last, Tc, Tl, th=15.0, bmono=False, check_ori=True):
+    import coeb_front
+    cam_o = oracle_mod.camera(ex, 640, 480, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    nm_ref, m_ref = oracle_mod.search_by_projection(cam_o, cur_k, cur_d, cur_ur, last, Tc, Tl, th, bmono, check_ori)
+    cam = coeb_front.make_camera(synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF, 640, 480)
+    cur = coeb_front.Frame(cur_k, cur_d, cur_ur, Tcw=Tc)
+    lf = coeb_front.Frame(last["keys_un"], last["mp_desc"], Tcw=Tl, outlier=last["outlier"],
+                          map_points=dict(world_pos=last["xw"], descriptor=last["mp_desc"],
+                                          observations=last["mp_nobs"], valid=last["has_mp"]))
+    m = coeb_front.ORBmatcher(0.9, check_ori, ctx=ctx)
+    nm = m.SearchByProjection(cur, lf, th, bmono, cam)
+    assert nm == nm_ref and np.array_equal(cur.mvpMapPoints, m_ref), (nm, nm_ref)
+    return nm
+
+
+def test_golden_match(ctx, oracle_mod, ex):
+    g = np.load(os.path.join(HERE, "golden", "match_A.npz"))
+    last = {k[5:]: g[k] for k in g.files if k.startswith("last_")}
+    nm = match_both(ctx, oracle_mod, ex, g["cur_kps"], g["cur_desc"], g["cur_ur"], last, g["Tcw_cur"], g["Tcw_last"])
+    assert nm == int(g["nmatches"])
+
+
+@pytest.fixture(scope="module")
+def pair(oracle_mod, ex):
+    fr = synth.make_frames(640, 480, 2, seed=77)
+    r0, r1 = ex.extract(fr[0]), ex.extract(fr[1])
+    depth = synth.make_depth(640, 480)
+    last = oracle_mod.mapframe_from_extraction(r0["kps"], r0["desc"], depth, synth.TUM_FX, synth.TUM_FY,
+                                               synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    ur1, _ = oracle_mod.stereo_from_rgbd(r1["kps"], depth, synth.TUM_BF)
+    return r1, ur1, last
+
+
+def test_match_variants(ctx, oracle_mod, ex, pair):
+    r1, ur1, last = pair
+    Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
+    rng = np.random.default_rng(11)
+    n = len(last["has_mp"])
+    v = dict(last)
+    v["mp_nobs"] = np.where(rng.random(n) < 0.3, 0, 2).astype(np.int32)   # claim-overwrite path
+    match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, v, Tc, Tl)
+    v = dict(last)
+    v["outlier"] = (rng.random(n) < 0.2).astype(np.uint8)
+    v["has_mp"] = (last["has_mp"] & (rng.random(n) < 0.8)).astype(np.uint8)
+    match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, v, Tc, Tl)
+    match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, last, Tc, Tl, check_ori=False)
+    match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, last, Tc, Tl, bmono=True)
+    match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, last, Tc, Tl, th=30.0)
+    match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], np.full(len(ur1), -1, np.float32), last, Tc, Tl)
+    for tz in (0.5, -0.5):            # bForward / bBackward level windows
+        T = Tc.copy()
+        T[2, 3] = tz
+        match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, last, T, Tl)
+    # empty frames
+    e = {k: val[:0] for k, val in last.items()}
+    assert match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, e, Tc, Tl) == 0
+
+
+# ------------------------------------------------------------------ batch (device-resident) path
+def test_batch_pipeline_matches_oracle(oracle_mod, ex):
+    from coeb_front.pipeline import BatchPipeline
+    F = 6
+    fr = synth.make_frames(640, 480, F, seed=4242)
+    Tcw = np.stack([synth.motion_pose()] * F)
+    bp = BatchPipeline(640, 480, F)
+    try:
+        dyn = [synth.dynamic_inputs(640, 480, seed=f) if f % 2 else (None, None, None) for f in range(F)]
+        bp.load(fr, Tcw=Tcw, dyn=dyn)
+        bp.run()
+        bp.synchronize()
+        out, matches, nms = bp.results()
+        depth = synth.make_depth(640, 480)
+        cam_o = oracle_mod.camera(ex, 640, 480, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+        prev = None
+        for f in range(F):
+            b, t, bl = dyn[f]
+            r = ex.extract(fr[f], b, t, bl)
+            assert_same(out[f][0], out[f][1], r["kps"], r["desc"], "batch f%d" % f)
+            if prev is not None:
+                last = oracle_mod.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX,
+                                                           synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+                ur, _ = oracle_mod.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
+                I4 = np.eye(4, dtype=np.float32)
+                nm, m = oracle_mod.search_by_projection(cam_o, r["kps"], r["desc"], ur, last, Tcw[f], I4, 15.0)
+                if nm < 20:                                      # Tracking.cc:954-958
+                    nm, m = oracle_mod.search_by_projection(cam_o, r["kps"], r["desc"], ur, last, Tcw[f], I4, 30.0)
+                assert nms[f] == nm and np.array_equal(matches[f], m), (f, nms[f], nm)
+            prev = r
+        # idempotence: a second run gives identical outputs
+        bp.run()
+        bp.synchronize()
+        out2, matches2, nms2 = bp.results()
+        assert all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(out, out2))
+        assert nms == nms2
+    finally:
+        bp.close()
+
+
+def test_batch_B_full_size_properties(oracle_mod):
+    """Config B at full size: 1280x960, 2000 kp, batch of 16 -- properties for every frame,
+    exact oracle parity on two of them."""
+    from coeb_front.pipeline import BatchPipeline
+    F = 16
+    fr = synth.make_frames(1280, 960, F, seed=99)
+    bp = BatchPipeline(1280, 960, F, nfeatures=2000)
+    try:
+        bp.load(fr, Tcw=np.stack([synth.motion_pose()] * F))
+        bp.run()
+        bp.synchronize()
+        out, matches, nms = bp.results()
+        ex2 = oracle_mod.Extractor(2000, 1.2, 8, 20, 7)
+        for f in (0, F - 1):
+            r = ex2.extract(fr[f])
+            assert_same(out[f][0], out[f][1], r["kps"], r["desc"], "B batch f%d" % f)
+        for f in range(F):
+            k = out[f][0]
+            assert 0 < len(k) <= 2000 + 8 * 8
+            assert (k["x"] >= 0).all() and (k["x"] < 1280).all() and (k["y"] >= 0).all() and (k["y"] < 960).all()
+            assert set(np.unique(k["octave"])) <= set(range(8))
+            assert (k["class_id"] == -1).all()
+            if f:
+                m = matches[f]
+                assert (m >= -1).all() and (m < len(out[f - 1][0])).all()
+                assert nms[f] == int((m >= 0).sum()) and nms[f] > 0.5 * len(k)
+    finally:
+        bp.close()

@@ -1,0 +1,174 @@
+"""Known-answer tests of the CPU oracle against the reference's own tables and definitions.
+
+The reference ships no tests or golden vectors.  What it does hold are
+constant tables and closed-form derived values; these pin the oracle:
+  * bit_pattern_31_ (src/ORBextractor.cc:158-416), sha256 of the 1024 ints
+  * umax (:461-476), features per level (:443-453), scale factors (:426-438)
+  * pyramid level sizes (:1348-1349), SURVEY.md s8 level table
+  * DescriptorDistance (src/ORBmatcher.cc:1648-1664) == popcount(a ^ b)
+plus property checks of the OpenCV primitives the oracle restates.
+"""
+import hashlib
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PATTERN_SHA = "88df8ca875cc8db56799edd57bb914edad8acb2d48c202b7a464a575b55dbdb8"
+
+
+def inc_ints():
+    txt = open(os.path.join(ROOT, "data", "orb_bit_pattern_31.inc")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return [int(v) for v in re.findall(r"-?\d+", txt)]
+
+
+def test_pattern_table_pinned():
+    vals = inc_ints()
+    assert len(vals) == 1024
+    assert hashlib.sha256(",".join(map(str, vals)).encode()).hexdigest() == PATTERN_SHA
+    assert min(vals) >= -13 and max(vals) <= 12
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/src/ORBextractor.cc"), reason="reference not mounted")
+def test_pattern_table_matches_reference_source():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from gen_pattern import extract
+    assert extract() == inc_ints()
+
+
+def test_oracle_pattern_loaded(oracle_mod):
+    ex = oracle_mod.Extractor()
+    pat = np.array(ex.p.pattern)
+    assert pat.reshape(-1).tolist() == inc_ints()
+
+
+def test_ctor_tables(oracle_mod):
+    ex = oracle_mod.Extractor(1000, 1.2, 8, 20, 7)
+    p = ex.p
+    assert list(p.umax) == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+    assert list(p.nfeat[:8]) == [217, 181, 151, 126, 105, 87, 73, 60]
+    # mvScaleFactor[i] = (float)(mvScaleFactor[i-1] * (double)1.2f)
+    s = [np.float32(1.0)]
+    for i in range(1, 8):
+        s.append(np.float32(np.float64(s[-1]) * np.float64(np.float32(1.2))))
+    assert np.array_equal(np.array(p.scale[:8], np.float32), np.array(s, np.float32))
+    B = oracle_mod.Extractor(2000, 1.2, 8, 20, 7)
+    assert list(B.p.nfeat[:8]) == [434, 362, 302, 251, 209, 175, 145, 122]
+
+
+def test_level_sizes_survey_table(oracle_mod):
+    ex = oracle_mod.Extractor()
+    assert ex.level_sizes(640, 480) == [(640, 480), (533, 400), (444, 333), (370, 278), (309, 231),
+                                        (257, 193), (214, 161), (179, 134)]
+    assert ex.level_sizes(1280, 960) == [(1280, 960), (1067, 800), (889, 667), (741, 556), (617, 463),
+                                         (514, 386), (429, 322), (357, 268)]
+
+
+def test_descriptor_distance_kat(oracle_mod):
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        a = rng.integers(0, 256, 32, dtype=np.uint8)
+        b = rng.integers(0, 256, 32, dtype=np.uint8)
+        want = int(np.unpackbits(a ^ b).sum())
+        assert oracle_mod.descriptor_distance(a, b) == want
+    z = np.zeros(32, np.uint8)
+    assert oracle_mod.descriptor_distance(z, np.full(32, 255, np.uint8)) == 256
+    assert oracle_mod.descriptor_distance(z, z) == 0
+
+
+def test_gauss_kernel_q8(oracle_mod):
+    k = oracle_mod.gauss_kernel7()
+    assert k == [18, 34, 48, 56, 48, 34, 18] and sum(k) == 256
+    # exact float Gaussian, sigma 2, for reference: 0.07016, 0.13107, 0.19071, 0.21611
+    g = np.exp(-np.arange(-3, 4) ** 2 / 8.0)
+    g /= g.sum()
+    assert np.abs(np.array(k) / 256.0 - g).max() < 2.5 / 256
+
+
+def test_fast_atan2_properties(oracle_mod):
+    f = oracle_mod.fast_atan2
+    assert f(0.0, 0.0) == 0.0
+    for deg in np.linspace(0, 359, 361):
+        y, x = math.sin(math.radians(deg)), math.cos(math.radians(deg))
+        a = f(y * 1000, x * 1000)
+        d = (a - deg + 180) % 360 - 180
+        assert abs(d) < 0.02, (deg, a)
+        assert 0.0 <= a < 360.0 + 1e-4
+
+
+def test_sincos_canonical_vs_libm(oracle_mod):
+    """The canonical sincosf is the double-evaluated value rounded once to float: it must be
+    within 1 ulp of the host libm sinf/cosf everywhere on [0, 2pi) and equal on >99.9%."""
+    rng = np.random.default_rng(1)
+    a = np.concatenate([rng.uniform(0, 2 * np.pi, 20000), np.linspace(0, 2 * np.pi, 5000)]).astype(np.float32)
+    same = 0
+    for v in a:
+        s, c = oracle_mod.sincos(float(v))
+        rs, rc = np.float32(math.sin(float(v))), np.float32(math.cos(float(v)))
+        assert abs(int(np.float32(s).view(np.int32)) - int(rs.view(np.int32))) <= 1
+        assert abs(int(np.float32(c).view(np.int32)) - int(rc.view(np.int32))) <= 1
+        same += (np.float32(s) == rs) and (np.float32(c) == rc)
+    assert same >= 0.999 * len(a)
+
+
+def _corner_strength(patch):
+    """Closed form used by the HIP k_fast: M = max over the 16 nine-pixel arcs of the
+    arc's min of (v - ring) (dark) or (ring - v) (bright); corner at t <=> M > t and
+    OpenCV cornerScore<16> = M - 1."""
+    off = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3), (-2, -2),
+           (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+    v = int(patch[3, 3])
+    d = [v - int(patch[3 + dy, 3 + dx]) for dx, dy in off]
+    A = max(min(d[(k + j) % 16] for j in range(9)) for k in range(16))
+    B = max(min(-d[(k + j) % 16] for j in range(9)) for k in range(16))
+    return max(A, B)
+
+
+def test_fast_closed_form_matches_opencv_literal(oracle_mod):
+    """cv::FAST (literal restatement in the oracle) on a single-pixel ROI agrees with the
+    closed form the GPU kernel evaluates, for many random and structured patches."""
+    import ctypes as C
+    L = oracle_mod.lib()
+    rng = np.random.default_rng(2)
+    xs = np.zeros(4, np.int32)
+    ys = np.zeros(4, np.int32)
+    sc = np.zeros(4, np.int32)
+    checked = 0
+    for it in range(6000):
+        if it % 3 == 0:
+            patch = rng.integers(0, 256, (7, 7)).astype(np.uint8)
+        else:
+            base = rng.integers(0, 256)
+            patch = np.clip(base + rng.integers(-40, 41, (7, 7)), 0, 255).astype(np.uint8)
+            if it % 3 == 2:
+                patch[3, 3] = np.clip(int(patch[3, 3]) + rng.choice([-60, 60]), 0, 255)
+        # embed in a 9x9 ROI so the centre pixel is the only detection candidate and NMS
+        # neighbours are outside the detection window (score 0)
+        roi = np.zeros((9, 9), np.uint8)
+        roi[1:8, 1:8] = patch
+        roi = np.ascontiguousarray(roi[1:8, 1:8])
+        M = _corner_strength(roi)
+        for t in (7, 10, 20, 30):
+            n = L.oc_fast_roi(roi.ctypes.data_as(C.c_void_p), 7, 7, 7, t, xs.ctypes.data_as(C.c_void_p),
+                              ys.ctypes.data_as(C.c_void_p), sc.ctypes.data_as(C.c_void_p), 4)
+            if M > t:
+                assert n == 1 and sc[0] == M - 1, (t, M, n, sc[0])
+                checked += 1
+            else:
+                assert n == 0
+    assert checked > 500
+
+
+def test_resize_and_blur_constant_images(oracle_mod):
+    """resize / blur of a constant image stay constant (fixed-point weights sum to 1)."""
+    ex = oracle_mod.Extractor()
+    for v in (0, 1, 77, 128, 254, 255):
+        img = np.full((480, 640), v, np.uint8)
+        r = ex.extract(img, debug=True)
+        assert (r["pyramid"] == v).all()
+        assert len(r["kps"]) == 0
