@@ -27,7 +27,8 @@ namespace {
 enum { PATCH_SIZE = 31, HALF_PATCH_SIZE = 15, EDGE_THRESHOLD = 19 };
 constexpr int kRoiMax = 64;
 constexpr int kOctLMax = 1024;
-constexpr int kCurMax = 4096;
+constexpr int kCurMax = 4095;
+constexpr int kMatchCQ = 64;   // candidate list entries per LastFrame point (coeb_match.hip kCQ)
 
 inline int cv_round(float v) { return (int)lrintf(v); }
 inline int cv_round_d(double v) { return (int)lrint(v); }
@@ -672,7 +673,7 @@ int coeb_match_lastframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curfram
         return set_err(c, COEB_EINVAL, "coeb_match_lastframe: invalid arguments");
     *nmatches = 0;
     if (cur->n < 0 || last->n < 0) return set_err(c, COEB_EINVAL, "negative frame size");
-    if (cur->n > kCurMax) return set_err(c, COEB_EINVAL, "more than 4096 current keypoints");
+    if (cur->n > kCurMax) return set_err(c, COEB_EINVAL, "more than 4095 current keypoints");
     (void)hipSetDevice(c->device);
     const int n = cur->n, nl = last->n;
     const int cs = std::max(n, 1), ls = std::max(nl, 1);
@@ -687,7 +688,7 @@ int coeb_match_lastframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curfram
         (rc = ensure(c, "m_xw", (size_t)ls * 3, &dxw)) || (rc = ensure(c, "m_T", 32, &dT)) ||
         (rc = ensure(c, "m_cn", 2, &dcn)) || (rc = ensure(c, "m_nobs", ls, &dnobs)) ||
         (rc = ensure(c, "m_match", cs, &dmatch)) || (rc = ensure(c, "m_nm", 1, &dnm)) ||
-        (rc = ensure(c, "m_scr", (size_t)2 * ls + 2, &dscr)) || (rc = ensure(c, "err", 4, &derr)))
+        (rc = ensure(c, "m_scr", (size_t)ls * kMatchCQ, &dscr)) || (rc = ensure(c, "err", 4, &derr)))
         return rc;
     hipStream_t s = c->stream;
     int32_t cnts[2] = {n, nl};
@@ -713,7 +714,7 @@ int coeb_match_lastframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curfram
     mb.last_kps = dlk; mb.last_desc = dld; mb.last_n = dcn + 1; mb.last_has = dhas; mb.last_out = dout;
     mb.last_xw = dxw; mb.last_nobs = dnobs; mb.last_stride = ls;
     mb.Tcw_cur = dT; mb.Tcw_last = dT + 16;
-    mb.match = dmatch; mb.nmatch = dnm; mb.scratch = dscr; mb.scratch_stride = 2 * ls + 2; mb.err = derr;
+    mb.match = dmatch; mb.nmatch = dnm; mb.scratch = dscr; mb.scratch_stride = ls * kMatchCQ; mb.err = derr;
     if (launch_match(make_cam(c, cam), mb, 1, th, bmono, check_ori, 0, s, &c->hook))
         return hip_err(c, hipGetLastError(), "launch_match");
     int nm = 0;
@@ -733,7 +734,7 @@ int coeb_match_batch_device(coeb_ctx* c, const float* d_depth, int F, int W, int
         return set_err(c, COEB_EINVAL, "coeb_match_batch_device: must follow coeb_extract_batch_device on the same batch");
     (void)hipSetDevice(c->device);
     const int K = c->plan.kcap;
-    if (K > kCurMax) return set_err(c, COEB_EINVAL, "keypoint capacity exceeds the matcher limit (4096)");
+    if (K > kCurMax) return set_err(c, COEB_EINVAL, "keypoint capacity exceeds the matcher limit (4095)");
     int rc;
     float *ur, *dep, *xw, *dT;
     uint8_t *has, *outl;
@@ -742,7 +743,7 @@ int coeb_match_batch_device(coeb_ctx* c, const float* d_depth, int F, int W, int
         (rc = ensure(c, "b_xw", (size_t)F * K * 3, &xw)) || (rc = ensure(c, "b_has", (size_t)F * K, &has)) ||
         (rc = ensure(c, "b_outl", (size_t)F * K, &outl)) || (rc = ensure(c, "b_nobs", (size_t)F * K, &nobsb)) ||
         (rc = ensure(c, "b_match", (size_t)F * K, &match)) || (rc = ensure(c, "b_nm", (size_t)F, &nm)) ||
-        (rc = ensure(c, "b_T", (size_t)F * 32, &dT)) || (rc = ensure(c, "b_scr", (size_t)F * (2 * K + 2), &scr)) ||
+        (rc = ensure(c, "b_T", (size_t)F * 32, &dT)) || (rc = ensure(c, "b_scr", (size_t)F * K * kMatchCQ, &scr)) ||
         (rc = ensure(c, "err", 4, &derr)))
         return rc;
     const coeb_keypoint* kps = static_cast<const coeb_keypoint*>(c->bufs["kps"].p);
@@ -769,7 +770,7 @@ int coeb_match_batch_device(coeb_ctx* c, const float* d_depth, int F, int W, int
     mb.last_kps = kps; mb.last_desc = desc; mb.last_n = counts; mb.last_has = has; mb.last_out = outl;
     mb.last_xw = xw; mb.last_nobs = nobsb; mb.last_stride = K;
     mb.Tcw_cur = dT; mb.Tcw_last = dT + (size_t)(F - 1) * 16;
-    mb.match = match + K; mb.nmatch = nm + 1; mb.scratch = scr; mb.scratch_stride = 2 * K + 2; mb.err = derr;
+    mb.match = match + K; mb.nmatch = nm + 1; mb.scratch = scr; mb.scratch_stride = K * kMatchCQ; mb.err = derr;
     if (launch_match(make_cam(c, cam), mb, F - 1, th, 0, 1, 20, c->stream, &c->hook))
         return hip_err(c, hipGetLastError(), "launch_match");
     return COEB_OK;

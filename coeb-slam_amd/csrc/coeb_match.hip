@@ -14,13 +14,13 @@
 // minimum with one wave min.  Phase 2 applies the rotation-histogram top-3 filter.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "coeb_internal.hpp"
 
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kCurMax = 4096;          // current keypoints per frame (host checks)
-constexpr int kCellIdxBits = 13;
 constexpr int HISTO_LENGTH = 30;
 constexpr int TH_HIGH = 100;
 
@@ -32,15 +32,6 @@ __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b)
 #pragma unroll
     for (int i = 0; i < 8; i++) d += __popc(a[i] ^ b[i]);
     return d;
-}
-
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
-{
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long y = __shfl_xor(v, o, 64);
-        v = y < v ? y : v;
-    }
-    return v;
 }
 
 // ================================ k_prep ================================
@@ -75,16 +66,193 @@ __global__ __launch_bounds__(kThreads) void k_prep(PrepBufs b)
 }
 
 // ================================ k_match ================================
-__global__ __launch_bounds__(kThreads) void k_match(MatchCam cam, MatchBufs b, float th0, int bmono,
-                                                     int check_ori, int retry_below)
+// One workgroup (1024 threads) per frame pair.
+//   phase 0  stage CurrentFrame (x, y, uR, octave, descriptor) in LDS; build the 64 x 48
+//            grid as a CSR by a bitonic sort of (cell << 12 | index): a cell column ix over
+//            rows [iy0, iy1] is one contiguous range, so range order == the reference's
+//            (ix outer, iy inner, insertion order) enumeration.
+//   phase 1  one thread per LastFrame point: projection, window, level / window / stereo
+//            filters and Hamming distance; the candidates with dist <= TH_HIGH are kept in
+//            enumeration order (only they can ever be chosen).
+//   phase 2  claims.  Sequentially, point q takes the first strict minimum (dist, order) among
+//            its candidates not claimed by an earlier point p < q whose MapPoint has
+//            Observations() > 0 (ORBmatcher.cc:1401-1429).  With res_q = F_q(res_{<q}) this is
+//            a triangular system; Jacobi iteration (all q in parallel, owner[c] = min p with
+//            res_p = c, nobs_p > 0) reaches its unique fixpoint -- the sequential result --
+//            and stops when an iteration changes nothing.
+//   phase 3  CurrentFrame.mvpMapPoints[c] = last claimer of c; rotation histogram
+//            (round(rot/30)), ComputeThreeMaxima, drop the rest (ORBmatcher.cc:1432-1468).
+//   retry    nmatches < retry_below -> again with 2*th (Tracking.cc:954-958).
+// A pair whose candidate list overflows kCQ, or that does not converge in kMaxIter
+// iterations, runs the literal sequential loop instead (exact, slower).
+constexpr int kMThreads = 1024;
+constexpr int kCQ = 64;
+constexpr int kMaxIter = 64;
+constexpr int kIdxBits = 12;
+
+struct QueryWin {
+    bool ok, chk;
+    float u, v, radius, ur_q;
+    int minL, maxL, x0, x1, y0, y1;
+};
+
+__device__ __forceinline__ QueryWin query_window(const MatchCam& cam, const float* T, const float* X, int octave,
+                                                 float th, bool fwd, bool bwd)
 {
-    __shared__ uint32_t s_sort[kCurMax];
-    __shared__ int s_cell[COEB_GRID_CELLS + 1];
-    __shared__ int s_owner[kCurMax];
+    QueryWin w;
+    w.ok = false;
+    float p3[3];
+    for (int k = 0; k < 3; k++) {                  // x3Dc = Rcw*x3Dw + tcw (cv::Mat small gemm)
+        float t = T[k * 4 + 0] * X[0] + T[k * 4 + 1] * X[1];
+        t = t + T[k * 4 + 2] * X[2];
+        p3[k] = (float)((double)t + (double)T[k * 4 + 3]);
+    }
+    const float invzc = (float)(1.0 / (double)p3[2]);
+    if (invzc < 0) return w;
+    w.u = __builtin_fmaf(cam.fx * p3[0], invzc, cam.cx);   // fused in the reference binary
+    w.v = __builtin_fmaf(cam.fy * p3[1], invzc, cam.cy);
+    if (w.u < cam.min_x || w.u > cam.max_x) return w;
+    if (w.v < cam.min_y || w.v > cam.max_y) return w;
+    w.radius = th * cam.scale[octave];
+    if (fwd) { w.minL = octave; w.maxL = -1; }
+    else if (bwd) { w.minL = 0; w.maxL = octave; }
+    else { w.minL = octave - 1; w.maxL = octave + 1; }
+    w.x0 = max(0, (int)floorf(((w.u - cam.min_x) - w.radius) * cam.grid_inv_w));
+    if (w.x0 >= COEB_GRID_COLS) return w;
+    w.x1 = min(COEB_GRID_COLS - 1, (int)ceilf(((w.u - cam.min_x) + w.radius) * cam.grid_inv_w));
+    if (w.x1 < 0) return w;
+    w.y0 = max(0, (int)floorf(((w.v - cam.min_y) - w.radius) * cam.grid_inv_h));
+    if (w.y0 >= COEB_GRID_ROWS) return w;
+    w.y1 = min(COEB_GRID_ROWS - 1, (int)ceilf(((w.v - cam.min_y) + w.radius) * cam.grid_inv_h));
+    if (w.y1 < 0) return w;
+    w.chk = (w.minL > 0) || (w.maxL >= 0);
+    w.ur_q = __builtin_fmaf(-cam.bf, invzc, w.u);     // u - mbf*invzc (fused)
+    w.ok = true;
+    return w;
+}
+
+template <bool kLds>
+struct CurView {
+    const float4* kp;         // LDS: (x, y, uR, octave bits)
+    const uint32_t* desc;     // LDS: 8 words per keypoint
+    const Kp* gkp;            // global fallbacks
+    const float* gur;
+    const uint8_t* gdesc;
+    __device__ __forceinline__ void get(int i, float& x, float& y, float& ur, int& oct) const
+    {
+        if (kLds) {
+            const float4 k = kp[i];
+            x = k.x; y = k.y; ur = k.z; oct = __float_as_int(k.w);
+        } else {
+            x = gkp[i].x; y = gkp[i].y; oct = gkp[i].octave; ur = gur[i];
+        }
+    }
+    __device__ __forceinline__ int dist(int i, const uint32_t* q) const
+    {
+        const uint32_t* d = kLds ? desc + 8 * i : reinterpret_cast<const uint32_t*>(gdesc + 32 * i);
+        return hamming32(q, d);
+    }
+};
+
+// Candidates of one query passing the level / window / stereo filters, in enumeration order.
+template <bool kLds, class Fn>
+__device__ __forceinline__ void for_candidates(const QueryWin& w, const int* s_cell, const uint32_t* s_sort,
+                                               const CurView<kLds>& cv, Fn&& fn)
+{
+    for (int ix = w.x0; ix <= w.x1; ix++) {
+        const int c0 = s_cell[ix * COEB_GRID_ROWS + w.y0];
+        const int c1 = s_cell[ix * COEB_GRID_ROWS + w.y1 + 1];
+        for (int q = c0; q < c1; q++) {
+            const int i2 = (int)(s_sort[q] & ((1u << kIdxBits) - 1));
+            float x, y, ur;
+            int oct;
+            cv.get(i2, x, y, ur, oct);
+            if (w.chk) {
+                if (oct < w.minL) continue;
+                if (w.maxL >= 0 && oct > w.maxL) continue;
+            }
+            const float distx = x - w.u, disty = y - w.v;
+            if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) continue;
+            if (ur > 0) {
+                const float er = fabsf(w.ur_q - ur);
+                if (er > w.radius) continue;
+            }
+            if (!fn(i2)) return;
+        }
+    }
+}
+
+__device__ __forceinline__ int rot_bin(float a_last, float a_cur)
+{
+    float rot = a_last - a_cur;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
+    if (bin == HISTO_LENGTH) bin = 0;
+    return bin;
+}
+
+__device__ __forceinline__ void three_maxima(const int* hist, int& ind1, int& ind2, int& ind3)
+{
+    int max1 = 0, max2 = 0, max3 = 0;
+    ind1 = ind2 = ind3 = -1;
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        const int s = hist[i];
+        if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+        else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+        else if (s > max3) { max3 = s; ind3 = i; }
+    }
+    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+}
+
+struct MatchLds {
+    int* cell; uint32_t* sort; int* owner; int* res; int* qn; float4* kp; uint32_t* desc;
+};
+
+__host__ __device__ inline int next_pow2(int n)
+{
+    int p = 64;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+__host__ __device__ inline size_t match_lds_bytes(int nmax, int qmax, bool lds_cur, size_t* offs)
+{
+    const size_t n4 = (size_t)((nmax + 3) & ~3), q4 = (size_t)((qmax + 3) & ~3);
+    size_t o = 0;
+    size_t off[7];
+    off[0] = o; o += ((COEB_GRID_CELLS + 1) * 4 + 15) & ~(size_t)15;
+    off[1] = o; o += (size_t)next_pow2(nmax) * 4;
+    off[2] = o; o += n4 * 4;
+    off[3] = o; o += q4 * 4;
+    off[4] = o; o += q4 * 4;
+    off[5] = o; if (lds_cur) o += n4 * 16;
+    off[6] = o; if (lds_cur) o += n4 * 32;
+    if (offs) for (int i = 0; i < 7; i++) offs[i] = off[i];
+    return o;
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, float th0, int bmono, int check_ori,
+                                                     int retry_below, int force_seq)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int s_hist[HISTO_LENGTH];
+    __shared__ int s_flag[8];
     const int p = blockIdx.x;
-    const int tid = threadIdx.x, lane = __lane_id(), wv = tid >> 6;
+    const int tid = threadIdx.x;
     const int n = b.cur_n[p];
     const int nl = b.last_n[p];
+    size_t off[7];
+    match_lds_bytes(b.cur_stride, b.last_stride, kLds, off);
+    MatchLds L;
+    L.cell = reinterpret_cast<int*>(smem + off[0]);
+    L.sort = reinterpret_cast<uint32_t*>(smem + off[1]);
+    L.owner = reinterpret_cast<int*>(smem + off[2]);
+    L.res = reinterpret_cast<int*>(smem + off[3]);
+    L.qn = reinterpret_cast<int*>(smem + off[4]);
+    L.kp = reinterpret_cast<float4*>(smem + off[5]);
+    L.desc = reinterpret_cast<uint32_t*>(smem + off[6]);
     const Kp* cur = reinterpret_cast<const Kp*>(b.cur_kps) + (int64_t)p * b.cur_stride;
     const uint8_t* cdesc = b.cur_desc + (int64_t)p * b.cur_stride * 32;
     const float* cur_ur = b.cur_ur + (int64_t)p * b.cur_stride;
@@ -94,62 +262,71 @@ __global__ __launch_bounds__(kThreads) void k_match(MatchCam cam, MatchBufs b, f
     const uint8_t* lout = b.last_out + (int64_t)p * b.last_stride;
     const float* lxw = b.last_xw + (int64_t)p * b.last_stride * 3;
     const int* lnobs = b.last_nobs + (int64_t)p * b.last_stride;
-    int* hist_i2 = b.scratch + (int64_t)p * b.scratch_stride;
-    int* hist_bin = hist_i2 + b.scratch_stride / 2;
-    if (n > kCurMax) {
+    uint32_t* lists = reinterpret_cast<uint32_t*>(b.scratch) + (int64_t)p * b.scratch_stride;
+    if (n > b.cur_stride || nl > b.last_stride || n >= (1 << kIdxBits)) {
         if (tid == 0) { atomicOr(b.err, 16); b.nmatch[p] = 0; }
         return;
     }
+    CurView<kLds> cv;
+    cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = cur_ur; cv.gdesc = cdesc;
 
-    // ---- phase 0: grid CSR (AssignFeaturesToGrid / PosInGrid) ----
-    int np2 = 64;
-    while (np2 < n) np2 <<= 1;
-    for (int c = tid; c <= COEB_GRID_CELLS; c += kThreads) s_cell[c] = 0;
+    // ---- phase 0 ----
+    const int np2 = next_pow2(n);
+    for (int c = tid; c <= COEB_GRID_CELLS; c += kMThreads) L.cell[c] = 0;
     __syncthreads();
-    for (int i = tid; i < np2; i += kThreads) {
+    for (int i = tid; i < np2; i += kMThreads) {
         uint32_t key = 0xFFFFFFFFu;
         if (i < n) {
-            const int px = (int)roundf((cur[i].x - cam.min_x) * cam.grid_inv_w);
-            const int py = (int)roundf((cur[i].y - cam.min_y) * cam.grid_inv_h);
+            const Kp k = cur[i];
+            if (kLds) {
+                L.kp[i] = make_float4(k.x, k.y, cur_ur[i], __int_as_float(k.octave));
+                const uint4* d = reinterpret_cast<const uint4*>(cdesc + 32 * i);
+                const uint4 d0 = d[0], d1 = d[1];
+                uint32_t* o = L.desc + 8 * i;
+                o[0] = d0.x; o[1] = d0.y; o[2] = d0.z; o[3] = d0.w;
+                o[4] = d1.x; o[5] = d1.y; o[6] = d1.z; o[7] = d1.w;
+            }
+            const int px = (int)roundf((k.x - cam.min_x) * cam.grid_inv_w);   // PosInGrid (Frame.cc:560)
+            const int py = (int)roundf((k.y - cam.min_y) * cam.grid_inv_h);
             if (px >= 0 && px < COEB_GRID_COLS && py >= 0 && py < COEB_GRID_ROWS) {
                 const int cell = px * COEB_GRID_ROWS + py;
-                key = ((uint32_t)cell << kCellIdxBits) | (uint32_t)i;
-                atomicAdd(&s_cell[cell + 1], 1);
+                key = ((uint32_t)cell << kIdxBits) | (uint32_t)i;
+                atomicAdd(&L.cell[cell + 1], 1);
             }
         }
-        s_sort[i] = key;
+        L.sort[i] = key;
     }
     __syncthreads();
     for (int k = 2; k <= np2; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < np2; i += kThreads) {
+            for (int i = tid; i < np2; i += kMThreads) {
                 const int ixj = i ^ j;
                 if (ixj > i) {
-                    const uint32_t a = s_sort[i], c = s_sort[ixj];
+                    const uint32_t a = L.sort[i], c = L.sort[ixj];
                     const bool up = (i & k) == 0;
-                    if ((a > c) == up) { s_sort[i] = c; s_sort[ixj] = a; }
+                    if ((a > c) == up) { L.sort[i] = c; L.sort[ixj] = a; }
                 }
             }
             __syncthreads();
         }
     }
-    // inclusive scan of counts -> cell_start (single wave; 3072 cells)
-    if (wv == 0) {
+    if (tid < 64) {
+        const int lane = tid;
         int carry = 0;
         for (int base = 1; base <= COEB_GRID_CELLS; base += 64) {
             const int c = base + lane;
-            int v = c <= COEB_GRID_CELLS ? s_cell[c] : 0;
+            int v = c <= COEB_GRID_CELLS ? L.cell[c] : 0;
             for (int o = 1; o < 64; o <<= 1) {
                 const int y = __shfl_up(v, o, 64);
                 if (lane >= o) v += y;
             }
-            if (c <= COEB_GRID_CELLS) s_cell[c] = carry + v;
+            if (c <= COEB_GRID_CELLS) L.cell[c] = carry + v;
             carry += __shfl(v, 63, 64);
         }
     }
     __syncthreads();
 
-    // ---- pose algebra (ORBmatcher.cc:1339-1350) ----
+    // pose algebra (ORBmatcher.cc:1339-1350): twc = -Rcw^T tcw (double accumulation), tlc
     const float* T = b.Tcw_cur + (int64_t)p * 16;
     const float* Tl = b.Tcw_last + (int64_t)p * 16;
     float twc[3], tlc[3];
@@ -163,143 +340,157 @@ __global__ __launch_bounds__(kThreads) void k_match(MatchCam cam, MatchBufs b, f
         t = t + Tl[k * 4 + 2] * twc[2];
         tlc[k] = (float)((double)t + (double)Tl[k * 4 + 3]);
     }
-    const bool bForward = tlc[2] > cam.mb && !bmono;
-    const bool bBackward = -tlc[2] > cam.mb && !bmono;
-
-    if (wv != 0) return;   // phases 1-2: one wave (sequential claim dependency)
+    const bool fwd = tlc[2] > cam.mb && !bmono;
+    const bool bwd = -tlc[2] > cam.mb && !bmono;
 
     float th = th0;
     int nmatches = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
-        for (int i = lane; i < n; i += 64) s_owner[i] = -1;
-        __builtin_amdgcn_wave_barrier();
-        nmatches = 0;
-        int nhist = 0;
-        for (int i = 0; i < nl; i++) {
-            if (!lhas[i] || lout[i]) continue;
-            const float X0 = lxw[3 * i], X1 = lxw[3 * i + 1], X2 = lxw[3 * i + 2];
-            float p3[3];
-            for (int k = 0; k < 3; k++) {
-                float t = T[k * 4 + 0] * X0 + T[k * 4 + 1] * X1;
-                t = t + T[k * 4 + 2] * X2;
-                p3[k] = (float)((double)t + (double)T[k * 4 + 3]);
-            }
-            const float invzc = (float)(1.0 / (double)p3[2]);
-            if (invzc < 0) continue;
-            const float u = __builtin_fmaf(cam.fx * p3[0], invzc, cam.cx);
-            const float v = __builtin_fmaf(cam.fy * p3[1], invzc, cam.cy);
-            if (u < cam.min_x || u > cam.max_x) continue;
-            if (v < cam.min_y || v > cam.max_y) continue;
-            const int nLastOctave = last[i].octave;
-            const float radius = th * cam.scale[nLastOctave];
-            int minLevel, maxLevel;
-            if (bForward) { minLevel = nLastOctave; maxLevel = -1; }
-            else if (bBackward) { minLevel = 0; maxLevel = nLastOctave; }
-            else { minLevel = nLastOctave - 1; maxLevel = nLastOctave + 1; }
-            // GetFeaturesInArea cell window (Frame.cc:508-522)
-            const int nMinCellX = max(0, (int)floorf(((u - cam.min_x) - radius) * cam.grid_inv_w));
-            if (nMinCellX >= COEB_GRID_COLS) continue;
-            const int nMaxCellX = min(COEB_GRID_COLS - 1, (int)ceilf(((u - cam.min_x) + radius) * cam.grid_inv_w));
-            if (nMaxCellX < 0) continue;
-            const int nMinCellY = max(0, (int)floorf(((v - cam.min_y) - radius) * cam.grid_inv_h));
-            if (nMinCellY >= COEB_GRID_ROWS) continue;
-            const int nMaxCellY = min(COEB_GRID_ROWS - 1, (int)ceilf(((v - cam.min_y) + radius) * cam.grid_inv_h));
-            if (nMaxCellY < 0) continue;
-            const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
-            uint32_t qd[8];
-#pragma unroll
-            for (int w = 0; w < 8; w++) qd[w] = reinterpret_cast<const uint32_t*>(ldesc + 32 * i)[w];
-            const float ur_q = __builtin_fmaf(-cam.bf, invzc, u);     // u - mbf*invzc (fused)
-            unsigned long long best = ~0ull;
-            int pos = 0;
-            for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
-                const int c0 = s_cell[ix * COEB_GRID_ROWS + nMinCellY];
-                const int c1 = s_cell[ix * COEB_GRID_ROWS + nMaxCellY + 1];
-                for (int base = c0; base < c1; base += 64) {
-                    const int q = base + lane;
-                    unsigned long long cand = ~0ull;
-                    if (q < c1) {
-                        const int i2 = (int)(s_sort[q] & ((1u << kCellIdxBits) - 1));
-                        const Kp kp = cur[i2];
-                        bool ok = true;
-                        if (bCheckLevels) {
-                            if (kp.octave < minLevel) ok = false;
-                            if (maxLevel >= 0 && kp.octave > maxLevel) ok = false;
+        // ---- phase 1: candidate lists (static filters) ----
+        if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; s_flag[2] = 0; s_flag[3] = 0; }
+        __syncthreads();
+        for (int q = tid; q < nl; q += kMThreads) {
+            int cnt = -1;
+            if (lhas[q] && !lout[q]) {
+                const QueryWin w = query_window(cam, T, lxw + 3 * q, last[q].octave, th, fwd, bwd);
+                if (w.ok) {
+                    uint32_t qd[8];
+                    const uint4* d = reinterpret_cast<const uint4*>(ldesc + 32 * q);
+                    const uint4 d0 = d[0], d1 = d[1];
+                    qd[0] = d0.x; qd[1] = d0.y; qd[2] = d0.z; qd[3] = d0.w;
+                    qd[4] = d1.x; qd[5] = d1.y; qd[6] = d1.z; qd[7] = d1.w;
+                    cnt = 0;
+                    uint32_t* lst = lists + (int64_t)q * kCQ;
+                    for_candidates<kLds>(w, L.cell, L.sort, cv, [&](int i2) {
+                        const int dist = cv.dist(i2, qd);
+                        if (dist <= TH_HIGH) {
+                            if (cnt < kCQ) lst[cnt] = ((uint32_t)dist << kIdxBits) | (uint32_t)i2;
+                            cnt++;
                         }
-                        const float distx = kp.x - u, disty = kp.y - v;
-                        ok = ok && fabsf(distx) < radius && fabsf(disty) < radius;
-                        if (ok) {
-                            const int own = __hip_atomic_load(&s_owner[i2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            if (own >= 0 && lnobs[own] > 0) ok = false;
-                        }
-                        if (ok && cur_ur[i2] > 0) {
-                            const float er = fabsf(ur_q - cur_ur[i2]);
-                            if (er > radius) ok = false;
-                        }
-                        if (ok) {
-                            const int dist = hamming32(qd, reinterpret_cast<const uint32_t*>(cdesc + 32 * i2));
-                            if (dist < 256)
-                                cand = ((unsigned long long)dist << 40) | ((unsigned long long)(pos + q - base) << 16) |
-                                       (unsigned long long)i2;
-                        }
-                    }
-                    cand = wave_min_u64(cand);
-                    best = cand < best ? cand : best;
+                        return true;
+                    });
+                    if (cnt > kCQ) s_flag[0] = 1;      // overflow -> sequential path
                 }
-                pos += c1 - c0;
             }
-            if (best != ~0ull) {
-                const int bestDist = (int)(best >> 40);
-                const int bestIdx2 = (int)(best & 0xFFFF);
-                if (bestDist <= TH_HIGH) {
-                    if (lane == 0)
-                        __hip_atomic_store(&s_owner[bestIdx2], i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __builtin_amdgcn_wave_barrier();
-                    nmatches++;
-                    if (check_ori) {
-                        float rot = last[i].angle - cur[bestIdx2].angle;
-                        if (rot < 0.0) rot += 360.0f;
-                        int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
-                        if (bin == HISTO_LENGTH) bin = 0;
-                        if (lane == 0) { hist_i2[nhist] = bestIdx2; hist_bin[nhist] = bin; }
-                        nhist++;
+            L.qn[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | (lnobs[q] > 0 ? 0x10000 : 0));
+        }
+        __syncthreads();
+        bool seq = force_seq || s_flag[0];
+        // ---- phase 2: claims by fixpoint iteration ----
+        if (!seq) {
+            for (int it = 0;; it++) {
+                for (int c = tid; c < n; c += kMThreads) L.owner[c] = 0x7fffffff;
+                if (tid == 0) s_flag[1] = 0;
+                __syncthreads();
+                if (it > 0) {
+                    for (int q = tid; q < nl; q += kMThreads) {
+                        const int r = L.res[q];
+                        if (r >= 0 && (L.qn[q] & 0x10000)) atomicMin(&L.owner[r], q);
                     }
+                    __syncthreads();
+                }
+                for (int q = tid; q < nl; q += kMThreads) {
+                    const int qn = L.qn[q];
+                    int best = -1;
+                    if (qn >= 0) {
+                        const int m = qn & 0xFFFF;
+                        const uint32_t* lst = lists + (int64_t)q * kCQ;
+                        uint32_t bk = 0xFFFFFFFFu;
+                        for (int e = 0; e < m; e++) {
+                            const uint32_t v = lst[e];
+                            const int i2 = (int)(v & ((1u << kIdxBits) - 1));
+                            if (L.owner[i2] < q) continue;            // claimed by an earlier point
+                            const uint32_t key = ((v >> kIdxBits) << 16) | (uint32_t)e;
+                            if (key < bk) { bk = key; best = i2; }
+                        }
+                    }
+                    if (it == 0 || best != L.res[q]) s_flag[1] = 1;
+                    L.res[q] = best;
+                }
+                __syncthreads();
+                if (!s_flag[1]) break;
+                if (it >= kMaxIter) { seq = true; break; }
+                __syncthreads();
+            }
+        }
+        // ---- sequential path (overflow / no convergence / forced): literal loop, one thread ----
+        if (seq) {
+            for (int c = tid; c < n; c += kMThreads) L.owner[c] = -1;
+            __syncthreads();
+            if (tid == 0) {
+                for (int q = 0; q < nl; q++) {
+                    int best = -1;
+                    if (L.qn[q] >= 0) {
+                        const QueryWin w = query_window(cam, T, lxw + 3 * q, last[q].octave, th, fwd, bwd);
+                        if (w.ok) {
+                            uint32_t qd[8];
+                            for (int k = 0; k < 8; k++) qd[k] = reinterpret_cast<const uint32_t*>(ldesc + 32 * q)[k];
+                            int bestDist = 256;
+                            for_candidates<kLds>(w, L.cell, L.sort, cv, [&](int i2) {
+                                const int own = L.owner[i2];
+                                if (own >= 0 && lnobs[own] > 0) return true;
+                                const int dist = cv.dist(i2, qd);
+                                if (dist < bestDist) { bestDist = dist; best = i2; }
+                                return true;
+                            });
+                            if (bestDist > TH_HIGH) best = -1;
+                            if (best >= 0) L.owner[best] = q;
+                        }
+                    }
+                    L.res[q] = best;
+                }
+            }
+            __syncthreads();
+        }
+        // ---- phase 3: mvpMapPoints, rotation consistency ----
+        for (int c = tid; c < n; c += kMThreads) L.owner[c] = -1;
+        if (tid < HISTO_LENGTH) s_hist[tid] = 0;
+        __syncthreads();
+        int mine = 0;
+        for (int q = tid; q < nl; q += kMThreads) {
+            const int r = L.res[q];
+            if (r >= 0) {
+                atomicMax(&L.owner[r], q);
+                mine++;
+                if (check_ori) {
+                    const int bin = rot_bin(last[q].angle, cur[r].angle);
+                    L.qn[q] = bin;
+                    atomicAdd(&s_hist[bin], 1);
                 }
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if (mine) atomicAdd(&s_flag[2], mine);
+        __syncthreads();
         if (check_ori) {
-            // ComputeThreeMaxima (ORBmatcher.cc:1602-1643)
-            int cnt = 0;
-            if (lane < HISTO_LENGTH)
-                for (int e = 0; e < nhist; e++) cnt += hist_bin[e] == lane;
-            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-            for (int bi = 0; bi < HISTO_LENGTH; bi++) {
-                const int s = __shfl(cnt, bi, 64);
-                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = bi; }
-                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = bi; }
-                else if (s > max3) { max3 = s; ind3 = bi; }
+            if (tid == 0) {
+                int i1, i2, i3;
+                three_maxima(s_hist, i1, i2, i3);
+                s_flag[4] = i1; s_flag[5] = i2; s_flag[6] = i3;
             }
-            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
-            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-            int removed = 0;
-            for (int e = lane; e < nhist; e += 64) {
-                const int bn = hist_bin[e];
-                if (bn != ind1 && bn != ind2 && bn != ind3) {
-                    __hip_atomic_store(&s_owner[hist_i2[e]], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    removed++;
+            __syncthreads();
+            const int i1 = s_flag[4], i2 = s_flag[5], i3 = s_flag[6];
+            int rem = 0;
+            for (int q = tid; q < nl; q += kMThreads) {
+                const int r = L.res[q];
+                if (r >= 0) {
+                    const int bin = L.qn[q];
+                    if (bin != i1 && bin != i2 && bin != i3) {
+                        L.owner[r] = -1;
+                        rem++;
+                    }
                 }
             }
-            for (int o = 32; o > 0; o >>= 1) removed += __shfl_xor(removed, o, 64);
-            nmatches -= removed;
+            if (rem) atomicAdd(&s_flag[3], rem);
+            __syncthreads();
         }
-        __builtin_amdgcn_wave_barrier();
+        nmatches = s_flag[2] - s_flag[3];
+        __syncthreads();
         if (nmatches >= retry_below) break;
-        th = 2 * th0;                  // Tracking.cc:954-958
+        th = 2 * th0;                                  // Tracking.cc:954-958
     }
     int* mo = b.match + (int64_t)p * b.cur_stride;
-    for (int i = lane; i < n; i += 64) mo[i] = s_owner[i];
-    if (lane == 0) b.nmatch[p] = nmatches;
+    for (int i = tid; i < n; i += kMThreads) mo[i] = L.owner[i];
+    if (tid == 0) b.nmatch[p] = nmatches;
 }
 
 }  // namespace
@@ -316,8 +507,22 @@ int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int b
                  int retry_below, hipStream_t s, ProfileHook* prof)
 {
     if (P <= 0) return 0;
+    const int force_seq = getenv("COEB_MATCH_SEQUENTIAL") ? 1 : 0;   // test knob: exact literal path
+    const size_t lds_full = match_lds_bytes(b.cur_stride, b.last_stride, true, nullptr) + 256;
+    const size_t lds_min = match_lds_bytes(b.cur_stride, b.last_stride, false, nullptr) + 256;
     prof_begin(prof, "k_match", s);
-    hipLaunchKernelGGL(k_match, dim3(P), dim3(kThreads), 0, s, cam, b, th, bmono, check_ori, retry_below);
+    if (lds_full <= 160 * 1024) {
+        (void)hipFuncSetAttribute((const void*)k_match<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_full);
+        hipLaunchKernelGGL(k_match<true>, dim3(P), dim3(kMThreads), lds_full - 256, s, cam, b, th, bmono, check_ori,
+                           retry_below, force_seq);
+    } else if (lds_min <= 160 * 1024) {
+        (void)hipFuncSetAttribute((const void*)k_match<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_min);
+        hipLaunchKernelGGL(k_match<false>, dim3(P), dim3(kMThreads), lds_min - 256, s, cam, b, th, bmono, check_ori,
+                           retry_below, force_seq);
+    } else {
+        prof_end(prof, s);
+        return -2;
+    }
     prof_end(prof, s);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

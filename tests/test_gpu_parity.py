@@ -213,6 +213,40 @@ def test_match_variants(ctx, oracle_mod, ex, pair):
     assert match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, e, Tc, Tl) == 0
 
 
+def test_match_paths_agree(ctx, oracle_mod, ex, pair, monkeypatch):
+    """The parallel fixpoint claim resolution and the literal sequential loop (forced with
+    COEB_MATCH_SEQUENTIAL) both equal the oracle."""
+    r1, ur1, last = pair
+    Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
+    rng = np.random.default_rng(12)
+    v = dict(last)
+    v["mp_nobs"] = np.where(rng.random(len(last["has_mp"])) < 0.5, 0, 2).astype(np.int32)
+    for seq in (False, True):
+        if seq:
+            monkeypatch.setenv("COEB_MATCH_SEQUENTIAL", "1")
+        match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, v, Tc, Tl)
+        match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, last, Tc, Tl, th=30.0)
+    monkeypatch.delenv("COEB_MATCH_SEQUENTIAL")
+
+
+def test_match_repetitive_texture(ctx, oracle_mod, ex):
+    """Repetitive structure -> many near-identical descriptors per window: exercises long
+    candidate lists (and the sequential fallback when a list overflows)."""
+    yy, xx = np.indices((480, 640))
+    base = (((yy // 12) + (xx // 12)) % 2 * 200 + 30).astype(np.int16)
+    rng = np.random.default_rng(8)
+    f0 = np.clip(base + rng.integers(-6, 7, base.shape), 0, 255).astype(np.uint8)
+    f1 = np.clip(np.roll(base, (1, 2), axis=(0, 1)) + rng.integers(-6, 7, base.shape), 0, 255).astype(np.uint8)
+    r0, r1 = ex.extract(f0), ex.extract(f1)
+    depth = synth.make_depth(640, 480)
+    last = oracle_mod.mapframe_from_extraction(r0["kps"], r0["desc"], depth, synth.TUM_FX, synth.TUM_FY,
+                                               synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    ur1, _ = oracle_mod.stereo_from_rgbd(r1["kps"], depth, synth.TUM_BF)
+    for th in (15.0, 30.0, 60.0):
+        match_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, last, synth.motion_pose(),
+                   np.eye(4, dtype=np.float32), th=th)
+
+
 # ------------------------------------------------------------------ batch (device-resident) path
 def test_batch_pipeline_matches_oracle(oracle_mod, ex):
     from coeb_front.pipeline import BatchPipeline
