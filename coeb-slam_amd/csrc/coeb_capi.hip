@@ -163,11 +163,14 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
         g.h = cv_round((float)H * t.inv_scale[l]);
         g.scale = t.scale[l];
         g.size_i = (int)(PATCH_SIZE * t.scale[l]);
+        g.pitch = l == 0 ? W : (g.w + 63) & ~63;
+        g.bpitch = (g.w + 63) & ~63;
         if (l == 0) g.pyr_off = -1;
-        else { g.pyr_off = pyr; pyr = align256(pyr + (int64_t)g.w * g.h); }
+        else { g.pyr_off = pyr; pyr = align256(pyr + (int64_t)g.pitch * g.h); }
         g.blur_off = blur;
-        blur = align256(blur + (int64_t)g.w * g.h);
+        blur = align256(blur + (int64_t)g.bpitch * g.h);
         if (l > 0) {
+            while (rtab.size() % 4) rtab.push_back(0);     // 16-byte aligned table rows
             g.rtab_off = (int)rtab.size();
             g.xmax = resize_tables(P.lv[l - 1].w, P.lv[l - 1].h, g.w, g.h, rtab);
         }

@@ -137,17 +137,32 @@ __global__ void k_dynmask(ExtractBufs b, int F, int W, int H)
 }
 
 // ================================ k_pyr_level ================================
-// cv::resize INTER_LINEAR 8U, canonical rounding.  One output pixel per
-// thread, 64 x 4 pixels per workgroup; the source rows are read through L1/L2.
-__global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restrict__ src, int64_t src_fs,
-                                                        int sw, int sh, uint8_t* __restrict__ dst,
-                                                        int64_t dst_fs, int dw, int dh,
-                                                        const int* __restrict__ tab, int xmax)
+// cv::resize INTER_LINEAR 8U, canonical rounding.  Four consecutive output
+// pixels per thread (one 32-bit store); the <= 12 source bytes they need from each of the
+// two source rows come from three aligned 32-bit loads.  64 x 4 threads cover 256 x 4 outputs.
+__device__ __forceinline__ int byte_of(uint32_t w0, uint32_t w1, uint32_t w2, int o)
+{
+    const uint32_t w = o < 4 ? w0 : (o < 8 ? w1 : w2);
+    return (int)((w >> ((o & 3) * 8)) & 0xFFu);
+}
+
+__device__ __forceinline__ int vresize(int h0, int h1, int b0, int b1)
+{
+    const int v0 = min(h0 >> 4, 32767), v1 = min(h1 >> 4, 32767);
+    const int m0 = (v0 * b0) >> 16, m1 = (v1 * b1) >> 16;       // _mm_mulhi_epi16
+    int s = max(min(m0 + m1, 32767), -32768);                    // _mm_adds_epi16
+    s = max(min(s + 2, 32767), -32768) >> 2;                     // rounding shift, pack
+    return max(0, min(s, 255));
+}
+
+__global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
+                                                        int sw, int sh, uint8_t* __restrict__ dst, int64_t dst_fs,
+                                                        int dp, int dw, int dh, const int* __restrict__ tab, int xmax)
 {
     const int f = blockIdx.z;
-    const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int dx0 = blockIdx.x * 256 + (threadIdx.x & 63) * 4;
     const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (dx >= dw || dy >= dh) return;
+    if (dx0 >= dw || dy >= dh) return;
     const int* xofs = tab;
     const int* alpha = tab + dw;
     const int* yofs = tab + 2 * dw;
@@ -156,32 +171,61 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
     const int sy0 = yofs[dy];
     const int r0 = sy0 >= 0 ? (sy0 < sh ? sy0 : sh - 1) : 0;
     const int r1 = sy0 + 1 >= 0 ? (sy0 + 1 < sh ? sy0 + 1 : sh - 1) : 0;
-    const uint8_t* S0 = S + (int64_t)r0 * sw;
-    const uint8_t* S1 = S + (int64_t)r1 * sw;
-    const int sx = xofs[dx];
-    int h0, h1;
-    if (dx < xmax) {
-        const int a = alpha[dx];
-        const int a0 = (int)(short)(a & 0xFFFF), a1 = a >> 16;
-        h0 = S0[sx] * a0 + S0[sx + 1] * a1;
-        h1 = S1[sx] * a0 + S1[sx + 1] * a1;
-    } else {
-        h0 = S0[sx] * 2048;
-        h1 = S1[sx] * 2048;
-    }
+    const uint8_t* S0 = S + (int64_t)r0 * sp;
+    const uint8_t* S1 = S + (int64_t)r1 * sp;
     const int bb = beta[dy];
     const int b0 = (int)(short)(bb & 0xFFFF), b1 = bb >> 16;
-    int v0 = min(h0 >> 4, 32767), v1 = min(h1 >> 4, 32767);
-    int m0 = (v0 * b0) >> 16, m1 = (v1 * b1) >> 16;       // _mm_mulhi_epi16
-    int s = max(min(m0 + m1, 32767), -32768);              // _mm_adds_epi16
-    s = max(min(s + 2, 32767), -32768) >> 2;
-    dst[(int64_t)f * dst_fs + (int64_t)dy * dw + dx] = (uint8_t)max(0, min(s, 255));
+    const int nk = min(4, dw - dx0);
+    int sx[4], a0[4], a1[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int d = min(dx0 + k, dw - 1);
+        sx[k] = xofs[d];
+        const int a = alpha[d];
+        a0[k] = (int)(short)(a & 0xFFFF);
+        a1[k] = a >> 16;
+        if (d >= xmax) { a0[k] = 2048; a1[k] = 0; }      // HResizeLinear tail: S[sx]*ONE
+    }
+    const int base = sx[0] & ~3;
+    const bool fast = ((sp & 3) == 0) && (sx[nk - 1] + 1 - base < 12) && (base + 12 <= sw);
+    int out[4];
+    if (fast) {
+        const uint32_t* q0 = reinterpret_cast<const uint32_t*>(S0 + base);
+        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(S1 + base);
+        const uint32_t u0 = q0[0], u1 = q0[1], u2 = q0[2];
+        const uint32_t v0 = q1[0], v1 = q1[1], v2 = q1[2];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int o = sx[k] - base;
+            const int h0 = byte_of(u0, u1, u2, o) * a0[k] + byte_of(u0, u1, u2, o + 1) * a1[k];
+            const int h1 = byte_of(v0, v1, v2, o) * a0[k] + byte_of(v0, v1, v2, o + 1) * a1[k];
+            out[k] = vresize(h0, h1, b0, b1);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int s1 = min(sx[k] + 1, sw - 1);      // a1 == 0 whenever sx + 1 == sw
+            const int h0 = S0[sx[k]] * a0[k] + S0[s1] * a1[k];
+            const int h1 = S1[sx[k]] * a0[k] + S1[s1] * a1[k];
+            out[k] = vresize(h0, h1, b0, b1);
+        }
+    }
+    uint8_t* D = dst + (int64_t)f * dst_fs + (int64_t)dy * dp + dx0;
+    if (nk == 4 && (dp & 3) == 0) {
+        *reinterpret_cast<uint32_t*>(D) = (uint32_t)out[0] | ((uint32_t)out[1] << 8) | ((uint32_t)out[2] << 16) |
+                                          ((uint32_t)out[3] << 24);
+    } else {
+        for (int k = 0; k < nk; k++) D[k] = (uint8_t)out[k];
+    }
 }
 
 // ================================ k_blur ================================
 // GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), Q8 kernel, Q16 vertical accumulation
-// (DESIGN.md s3.3).  Tile 64 x 16 outputs; (64+6) x (16+6) input staged in LDS.
-constexpr int BT_W = 64, BT_H = 16, BT_IW = BT_W + 6, BT_IH = BT_H + 6;
+// (DESIGN.md s3.3).  Each thread owns 4 adjacent columns x 16 rows: the 7 horizontally
+// filtered rows the vertical tap needs slide through registers, so every source row is
+// fetched once per thread (three aligned 32-bit loads) and every output is one 32-bit store.
+// A wave covers 256 columns; a workgroup 256 x 64 outputs.
+constexpr int BT_W = 256, BT_H = 64, BT_ROWS = 16;
 
 __device__ __forceinline__ int reflect101(int p, int len)
 {
@@ -198,44 +242,71 @@ struct BlurTiles {
 
 __global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, ExtractBufs b, BlurTiles bt)
 {
-    __shared__ uint8_t sin_[BT_IH][BT_IW + 2];
-    __shared__ uint16_t sh_[BT_IH][BT_W];
     const int f = blockIdx.y;
     int l = 0;
     while (l + 1 < bt.L && (int)blockIdx.x >= bt.tile_off[l + 1]) l++;
     const int t = blockIdx.x - bt.tile_off[l];
     const int tx = t % bt.tiles_x[l], ty = t / bt.tiles_x[l];
     const LevelGeom& g = P->lv[l];
-    const int w = g.w, h = g.h;
+    const int w = g.w, h = g.h, sp = g.pitch, dp = g.bpitch;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int x0 = tx * BT_W + lane * 4;
+    const int y0 = ty * BT_H + wv * BT_ROWS;
+    if (x0 >= w || y0 >= h) return;
+    const int rows = min(BT_ROWS, h - y0);
     const uint8_t* src = level_ptr(P, b, f, l);
     uint8_t* dst = b.blur + (int64_t)f * P->blur_stride + g.blur_off;
-    const int ox = tx * BT_W, oy = ty * BT_H;
     int k[7];
 #pragma unroll
     for (int i = 0; i < 7; i++) k[i] = P->gauss[i];
-    for (int i = threadIdx.x; i < BT_IH * BT_IW; i += kThreads) {
-        const int yy = i / BT_IW, xx = i - yy * BT_IW;
-        const int sy = reflect101(oy + yy - 3, h), sx = reflect101(ox + xx - 3, w);
-        sin_[yy][xx] = src[(int64_t)sy * w + sx];
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < BT_IH * BT_W; i += kThreads) {
-        const int yy = i / BT_W, xx = i - yy * BT_W;
-        uint32_t acc = 0;
+    const bool interior = (x0 >= 4) && (x0 + 8 <= w) && ((sp & 3) == 0);
+    uint32_t ring[7][4];
 #pragma unroll
-        for (int q = 0; q < 7; q++) acc += (uint32_t)k[q] * sin_[yy][xx + q];
-        sh_[yy][xx] = (uint16_t)acc;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < BT_H * BT_W; i += kThreads) {
-        const int yy = i / BT_W, xx = i - yy * BT_W;
-        const int gx = ox + xx, gy = oy + yy;
-        if (gx >= w || gy >= h) continue;
-        uint32_t acc = 0;
+    for (int i = 0; i < 7; i++)
 #pragma unroll
-        for (int q = 0; q < 7; q++) acc += (uint32_t)k[q] * sh_[yy + q][xx];
-        const uint32_t o = (acc + (1u << 15)) >> 16;
-        dst[(int64_t)gy * w + gx] = (uint8_t)(o > 255u ? 255u : o);
+        for (int q = 0; q < 4; q++) ring[i][q] = 0;
+    for (int r = y0 - 3; r < y0 + rows + 3; r++) {
+        const uint8_t* row = src + (int64_t)reflect101(r, h) * sp;
+        int px[12];
+        if (interior) {
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(row + x0 - 4);
+            const uint32_t u0 = q[0], u1 = q[1], u2 = q[2];
+#pragma unroll
+            for (int i = 0; i < 12; i++) px[i] = byte_of(u0, u1, u2, i);
+        } else {
+#pragma unroll
+            for (int i = 1; i < 11; i++) px[i] = row[reflect101(x0 - 4 + i, w)];
+            px[0] = px[11] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) ring[i][q] = ring[i + 1][q];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int tp = 0; tp < 7; tp++) acc += (uint32_t)k[tp] * (uint32_t)px[q + tp + 1];
+            ring[6][q] = acc;
+        }
+        const int y = r - 3;
+        if (y >= y0) {
+            uint32_t o[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int tp = 0; tp < 7; tp++) acc += (uint32_t)k[tp] * ring[tp][q];
+                const uint32_t v = (acc + (1u << 15)) >> 16;
+                o[q] = v > 255u ? 255u : v;
+            }
+            uint8_t* D = dst + (int64_t)y * dp + x0;
+            if (x0 + 4 <= w) {
+                *reinterpret_cast<uint32_t*>(D) = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
+            } else {
+                for (int q = 0; q < w - x0; q++) D[q] = (uint8_t)o[q];
+            }
+        }
     }
 }
 
@@ -296,7 +367,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
     const int rw = c.rw, rh = c.rh;
     for (int i = threadIdx.x; i < rw * rh; i += kThreads) {
         const int yy = i / rw, xx = i - yy * rw;
-        roi[yy * kRoiMax + xx] = img[(int64_t)(c.y0 + yy) * g.w + c.x0 + xx];
+        roi[yy * kRoiMax + xx] = img[(int64_t)(c.y0 + yy) * g.pitch + c.x0 + xx];
         Ms[yy * kRoiMax + xx] = 0;
     }
     __syncthreads();
@@ -893,7 +964,7 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         const LevelGeom& g = P->lv[l];
         const uint32_t key = b.lvl_kp[(int64_t)f * P->lvl_stride + g.out_off + (idx - off[l])];
         const int x = key_x(key), y = key_y(key), sc = key_s(key);
-        const int st = g.w;
+        const int st = g.pitch, bst = g.bpitch;
         // IC_Angle (ORBextractor.cc:80-107)
         const uint8_t* img = level_ptr(P, b, f, l);
         const uint8_t* center = img + (int64_t)y * st + x;
@@ -918,7 +989,7 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
         float bs, ac;
         sincos_canon(angle * factorPI, &bs, &ac);
-        const uint8_t* bl = b.blur + (int64_t)f * P->blur_stride + g.blur_off + (int64_t)y * st + x;
+        const uint8_t* bl = b.blur + (int64_t)f * P->blur_stride + g.blur_off + (int64_t)y * bst + x;
         int nib = 0;
 #pragma unroll
         for (int t = 0; t < 4; t++) {
@@ -929,7 +1000,7 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
             const int c0 = (int)rintf(__builtin_fmaf(px0, ac, -(py0 * bs)));
             const int r1 = (int)rintf(__builtin_fmaf(px1, bs, py1 * ac));
             const int c1 = (int)rintf(__builtin_fmaf(px1, ac, -(py1 * bs)));
-            const int t0 = bl[r0 * st + c0], t1 = bl[r1 * st + c1];
+            const int t0 = bl[r0 * bst + c0], t1 = bl[r1 * bst + c1];
             nib |= (t0 < t1) << t;
         }
         const int other = __shfl_xor(nib, 1, 64);
@@ -964,8 +1035,9 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         const uint8_t* src = l == 1 ? b.gray : b.pyr + gp.pyr_off;
         const int64_t src_fs = l == 1 ? (int64_t)plan.W * plan.H : plan.pyr_stride;
         prof_begin(prof, "k_pyr_level", s);
-        hipLaunchKernelGGL(k_pyr_level, dim3((g.w + 63) / 64, (g.h + 3) / 4, F), dim3(kThreads), 0, s, src, src_fs,
-                           gp.w, gp.h, b.pyr + g.pyr_off, plan.pyr_stride, g.w, g.h, b.rtab + g.rtab_off, g.xmax);
+        hipLaunchKernelGGL(k_pyr_level, dim3((g.w + 255) / 256, (g.h + 3) / 4, F), dim3(kThreads), 0, s, src, src_fs,
+                           gp.pitch, gp.w, gp.h, b.pyr + g.pyr_off, plan.pyr_stride, g.pitch, g.w, g.h,
+                           b.rtab + g.rtab_off, g.xmax);
         prof_end(prof, s);
     }
     BlurTiles bt;

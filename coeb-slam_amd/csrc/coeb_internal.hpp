@@ -27,6 +27,8 @@
 // device as one POD block (kernel argument).
 struct LevelGeom {
     int w, h;
+    int pitch;             // row pitch of the level image (level 0: W; levels >= 1: 64-byte multiple)
+    int bpitch;            // row pitch of the blurred level (64-byte multiple)
     int64_t pyr_off;       // into pyr frame block (-1 for level 0)
     int64_t blur_off;      // into blur frame block
     int rtab_off;          // into resize table (ints): xofs[w], alpha[w], yofs[h], beta[h]

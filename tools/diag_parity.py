@@ -30,11 +30,12 @@ def cmp_extract(ctx, ex, gray, boxes=None, tm=None, blur=None, tag=""):
     pyr_bad = []
     for l in range(1, len(sizes)):
         lw, lh = sizes[l]
+        pitch = (lw + 63) // 64 * 64
         o0 = r["level_off"][l]
-        ref = r["pyramid"][o0:o0 + lw * lh]
-        got = plan_pyr[off:off + lw * lh]
+        ref = r["pyramid"][o0:o0 + lw * lh].reshape(lh, lw)
+        got = plan_pyr[off:off + pitch * lh].reshape(lh, pitch)[:, :lw]
         pyr_bad.append(int((ref != got).sum()))
-        off = (off + lw * lh + 255) // 256 * 256
+        off = (off + pitch * lh + 255) // 256 * 256
     lvl_n = ctx.debug_read("lvl_n").view(np.int32)
     print("[%s] area_flag=%d n_ref=%d n_gpu=%d" % (tag, r["area_flag"], len(r["kps"]), len(kps)))
     print("   pyr mismatches per level:", pyr_bad)
