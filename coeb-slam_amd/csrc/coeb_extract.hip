@@ -352,12 +352,21 @@ __device__ __forceinline__ int ring_strength(const uint8_t* c, int st, int tmin)
     return M > 0 ? M : 0;
 }
 
+// One wave per cell, four cells per workgroup, no workgroup barriers: the wave stages its
+// cell ROI in its own LDS slab with aligned 32-bit loads (the slab row starts at the ROI's
+// x0 & 3, so words are stored unshifted), computes M for every detection pixel, then walks
+// the detection window in row-major order 64 pixels at a time: NMS flag, ballot prefix,
+// ordered store of the kept keys.
+constexpr int kFastRowBytes = 72;          // >= 3 + 64 + 3 rounded to a word multiple
+constexpr int kFastSlab = kFastRowBytes * kRoiMax;
+
 __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, ExtractBufs b)
 {
-    __shared__ uint8_t roi[kRoiMax * kRoiMax];
-    __shared__ uint8_t Ms[kRoiMax * kRoiMax];
-    __shared__ int sbuf[kWaves + 2];
-    const int cidx = blockIdx.x, f = blockIdx.y;
+    __shared__ __attribute__((aligned(16))) uint8_t s_roi[kWaves][kFastSlab];
+    __shared__ __attribute__((aligned(16))) uint8_t s_M[kWaves][kFastSlab];
+    const int wv = threadIdx.x >> 6, lane = lane_id();
+    const int cidx = blockIdx.x * kWaves + wv, f = blockIdx.y;
+    if (cidx >= P->ncells) return;
     const CellDesc c = b.cells[cidx];
     const int l = c.level;
     const LevelGeom& g = P->lv[l];
@@ -365,61 +374,83 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
     const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
     const uint8_t* img = level_ptr(P, b, f, l);
     const int rw = c.rw, rh = c.rh;
-    for (int i = threadIdx.x; i < rw * rh; i += kThreads) {
-        const int yy = i / rw, xx = i - yy * rw;
-        roi[yy * kRoiMax + xx] = img[(int64_t)(c.y0 + yy) * g.pitch + c.x0 + xx];
-        Ms[yy * kRoiMax + xx] = 0;
+    uint8_t* roi = s_roi[wv];
+    uint8_t* Ms = s_M[wv];
+    const int sh = c.x0 & 3;                        // ROI column xx lives at slab byte sh + xx
+    // ---- stage the ROI (rows c.y0 .. c.y0+rh-1, bytes [x0 & ~3, x0 + rw) rounded up to words)
+    const int nwords = (sh + rw + 3) >> 2;
+    if ((g.pitch & 3) == 0) {
+        const uint8_t* base = img + (int64_t)c.y0 * g.pitch + (c.x0 & ~3);
+        for (int i = lane; i < nwords * rh; i += 64) {
+            const int yy = i / nwords, k = i - yy * nwords;
+            *reinterpret_cast<uint32_t*>(roi + yy * kFastRowBytes + 4 * k) =
+                *reinterpret_cast<const uint32_t*>(base + (int64_t)yy * g.pitch + 4 * k);
+        }
+    } else {
+        for (int i = lane; i < rw * rh; i += 64) {
+            const int yy = i / rw, xx = i - yy * rw;
+            roi[yy * kFastRowBytes + sh + xx] = img[(int64_t)(c.y0 + yy) * g.pitch + c.x0 + xx];
+        }
     }
-    __syncthreads();
+    for (int i = lane; i < kFastRowBytes * rh / 4; i += 64) reinterpret_cast<uint32_t*>(Ms)[i] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- corner strength of every detection pixel (window = ROI inset by 3)
     const int ww = rw - 6, wh = rh - 6;
     const int npix = ww > 0 && wh > 0 ? ww * wh : 0;
-    for (int p = threadIdx.x; p < npix; p += kThreads) {
+    for (int p = lane; p < npix; p += 64) {
         const int yy = p / ww + 3, xx = p - (p / ww) * ww + 3;
-        Ms[yy * kRoiMax + xx] = (uint8_t)ring_strength(&roi[yy * kRoiMax + xx], kRoiMax, th_min);
+        const int o = yy * kFastRowBytes + sh + xx;
+        Ms[o] = (uint8_t)ring_strength(&roi[o], kFastRowBytes, th_min);
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- per-cell NMS at iniThFAST, fallback to minThFAST when empty; ordered compaction
     uint32_t* out = b.cand + ((int64_t)f * P->ncells + cidx) * P->cell_cap;
+    const uint64_t lt = lanemask_lt();
     int nkept = 0;
     for (int pass = 0; pass < 2; pass++) {
         const int t = pass == 0 ? th_ini : th_min;
         int running = 0;
-        for (int base = 0; base < npix; base += kThreads) {
-            const int p = base + threadIdx.x;
+        for (int base = 0; base < npix; base += 64) {
+            const int p = base + lane;
             bool kept = false;
-            int yy = 0, xx = 0, s = 0;
+            int yy = 0, xx = 0, sc = 0;
             if (p < npix) {
                 yy = p / ww + 3;
                 xx = p - (p / ww) * ww + 3;
-                const int M = Ms[yy * kRoiMax + xx];
+                const int o = yy * kFastRowBytes + sh + xx;
+                const int M = Ms[o];
                 if (M > t) {
-                    s = M - 1;
+                    sc = M - 1;
                     kept = true;
 #pragma unroll
                     for (int dy = -1; dy <= 1; dy++)
 #pragma unroll
                         for (int dx = -1; dx <= 1; dx++) {
                             if (dx == 0 && dy == 0) continue;
-                            const int Mn = Ms[(yy + dy) * kRoiMax + xx + dx];
+                            const int Mn = Ms[o + dy * kFastRowBytes + dx];
                             const int ns = Mn > t ? Mn - 1 : 0;
-                            kept = kept && (s > ns);
+                            kept = kept && (sc > ns);
                         }
                 }
             }
-            int tot;
-            const int pre = block_scan_flag(kept, &tot, sbuf);
+            const uint64_t m = __ballot(kept);
             if (kept) {
-                const int o = running + pre;
-                if (o < P->cell_cap)
-                    out[o] = pack_key(xx + c.j * g.wcell, yy + c.i * g.hcell, s);
+                const int oo = running + __popcll(m & lt);
+                if (oo < P->cell_cap)
+                    out[oo] = pack_key(xx + c.j * g.wcell, yy + c.i * g.hcell, sc);
                 else
                     atomicOr(b.err, 2);
             }
-            running += tot;
+            running += __popcll(m);
         }
         nkept = running;
         if (nkept > 0) break;
     }
-    if (threadIdx.x == 0) b.cand_n[(int64_t)f * P->ncells + cidx] = min(nkept, P->cell_cap);
+    if (lane == 0) b.cand_n[(int64_t)f * P->ncells + cidx] = min(nkept, P->cell_cap);
 }
 
 // ================================ k_octree ================================
@@ -1053,7 +1084,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     hipLaunchKernelGGL(k_blur, dim3(tiles, F), dim3(kThreads), 0, s, d_plan, b, bt);
     prof_end(prof, s);
     prof_begin(prof, "k_fast", s);
-    hipLaunchKernelGGL(k_fast, dim3(plan.ncells, F), dim3(kThreads), 0, s, d_plan, b);
+    hipLaunchKernelGGL(k_fast, dim3((plan.ncells + kWaves - 1) / kWaves, F), dim3(kThreads), 0, s, d_plan, b);
     prof_end(prof, s);
     prof_begin(prof, "k_octree", s);
     hipLaunchKernelGGL(k_octree, dim3(plan.L, F), dim3(kThreads), 0, s, d_plan, b);

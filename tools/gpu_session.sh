@@ -23,7 +23,7 @@ for step in "$@"; do
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
         benchB) run benchB 600 python bench.py --config B --batch 64 --no-cpu-baseline ;;
-        prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 5 --no-cpu-baseline ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 10 --no-cpu-baseline ;;
         diag) run diag 600 python tools/diag_parity.py ;;
         *) echo "unknown step $step" ;;
     esac
