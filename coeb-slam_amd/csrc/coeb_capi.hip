@@ -26,7 +26,6 @@ namespace {
 
 enum { PATCH_SIZE = 31, HALF_PATCH_SIZE = 15, EDGE_THRESHOLD = 19 };
 constexpr int kRoiMax = 64;
-constexpr int kOctLMax = 1024;
 constexpr int kCurMax = 4095;
 constexpr int kMatchCQ = 64;   // candidate list entries per LastFrame point (coeb_match.hip kCQ)
 
@@ -223,10 +222,9 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
             g.ini_bound[i] = b;
         }
         g.ini_bound[g.nini] = 1 << 20;
-        if (g.nfeat + 8 > kOctLMax) { err = "features per level exceed the octree work-list capacity (1016)"; return false; }
+        // list size never exceeds max(N + 2, 4 * nIni)
         g.out_cap = std::max(g.nfeat + 3, 4 * g.nini) + 5;
-        g.ncap = 5 * (g.nfeat + 4) + 4 * g.nini + 16;
-        g.ncap = std::max(g.ncap, g.out_cap);
+        g.ncap = g.out_cap + 8;
         g.node_off = node;
         node += 2 * 8 * (int64_t)g.ncap;
         g.out_off = out_total;
@@ -246,6 +244,12 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
     P.lvl_stride = out_total;
     P.kcap = out_total;
     P.rtab_ints = (int)rtab.size();
+    P.oct_w = 0;
+    for (int l = 0; l < t.nlevels; l++) P.oct_w = std::max(P.oct_w, P.lv[l].ncap);
+    P.oct_w = (P.oct_w + 15) & ~15;
+    P.oct_kl = 2048;
+    P.oct_lds = P.oct_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * P.oct_kl;
+    if (P.oct_lds > 150 * 1024) { err = "octree LDS budget exceeded (features per level too large)"; return false; }
     memcpy(P.umax, t.umax, sizeof(P.umax));
     gauss_kernel7(P.gauss);
     return true;

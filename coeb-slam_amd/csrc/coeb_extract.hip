@@ -317,53 +317,85 @@ __global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, E
 // OpenCV's cornerScore<16> = M - 1 (derivation: DESIGN.md s4.2).  Per-cell NMS then
 // compares against neighbours' scores (0 outside the detection window), exactly as
 // FAST_t's 3-row buffers do; an empty cell at iniThFAST is redone at minThFAST (:834-838).
-__device__ __forceinline__ int ring_strength(const uint8_t* c, int st, int tmin)
+__device__ __forceinline__ void ring16(const uint8_t* c, int st, int p[16])
 {
-    const int v = c[0];
-    int p[16];
     p[0] = c[3 * st];      p[1] = c[3 * st + 1];  p[2] = c[2 * st + 2];  p[3] = c[st + 3];
     p[4] = c[3];           p[5] = c[-st + 3];     p[6] = c[-2 * st + 2]; p[7] = c[-3 * st + 1];
     p[8] = c[-3 * st];     p[9] = c[-3 * st - 1]; p[10] = c[-2 * st - 2]; p[11] = c[-st - 3];
     p[12] = c[-3];         p[13] = c[st - 3];     p[14] = c[2 * st - 2]; p[15] = c[3 * st - 1];
-    // quick reject at the smaller threshold (a corner at tmin must pass OpenCV's pre-test)
-    auto cls = [&](int x) { int d = x - v; return d < -tmin ? 1 : (d > tmin ? 2 : 0); };
-    int d = cls(p[0]) | cls(p[8]);
-    d &= cls(p[2]) | cls(p[10]);
-    d &= cls(p[4]) | cls(p[12]);
-    d &= cls(p[6]) | cls(p[14]);
-    if (d == 0) return 0;
-    int dd[16];
+}
+
+// FAST-9/16 test at threshold t: >= 9 contiguous ring pixels all < v - t or all > v + t
+// (FAST_t's count loop), evaluated on 16-bit dark/bright masks by shift-and doubling.
+__device__ __forceinline__ bool fast_corner(const uint8_t* c, int st, int t)
+{
+    int p[16];
+    ring16(c, st, p);
+    const int v = c[0];
+    uint32_t dk = 0, br = 0;
 #pragma unroll
-    for (int i = 0; i < 16; i++) dd[i] = v - p[i];
+    for (int k = 0; k < 16; k++) {
+        dk |= (uint32_t)(p[k] < v - t) << k;
+        br |= (uint32_t)(p[k] > v + t) << k;
+    }
+    uint32_t a = dk | (dk << 16), bb = br | (br << 16);
+    uint32_t ra = a & (a >> 1), rb = bb & (bb >> 1);
+    ra &= ra >> 2; rb &= rb >> 2;
+    ra &= ra >> 4; rb &= rb >> 4;
+    ra &= a >> 8; rb &= bb >> 8;
+    return ((ra | rb) & 0xFFFFu) != 0;
+}
+
+// Exact corner strength M = max over the 16 nine-pixel arcs of min(v - ring) (dark) or
+// min(ring - v) (bright); OpenCV cornerScore<16> = M - 1 for a corner.
+// Arc minima by doubling: m2 -> m4 -> m8 -> m9.
+__device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
+{
+    int p[16];
+    ring16(c, st, p);
+    const int v = c[0];
+    int d[16], m[16], n[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = v - p[k];
+#pragma unroll
+    for (int k = 0; k < 16; k++) { m[k] = min(d[k], d[(k + 1) & 15]); n[k] = max(d[k], d[(k + 1) & 15]); }
+    int m4[16], n4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) { m4[k] = min(m[k], m[(k + 2) & 15]); n4[k] = max(n[k], n[(k + 2) & 15]); }
     int A = -1000, B = -1000;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        int mn = dd[k], mx = dd[k];
-#pragma unroll
-        for (int j = 1; j < 9; j++) {
-            const int x = dd[(k + j) & 15];
-            mn = min(mn, x);
-            mx = max(mx, x);
-        }
-        A = max(A, mn);
-        B = max(B, -mx);
+        const int m8 = min(m4[k], m4[(k + 4) & 15]), n8 = max(n4[k], n4[(k + 4) & 15]);
+        A = max(A, min(m8, d[(k + 8) & 15]));
+        B = max(B, -max(n8, d[(k + 8) & 15]));
     }
-    const int M = max(A, B);
-    return M > 0 ? M : 0;
+    return max(A, B);
 }
 
-// One wave per cell, four cells per workgroup, no workgroup barriers: the wave stages its
-// cell ROI in its own LDS slab with aligned 32-bit loads (the slab row starts at the ROI's
-// x0 & 3, so words are stored unshifted), computes M for every detection pixel, then walks
-// the detection window in row-major order 64 pixels at a time: NMS flag, ballot prefix,
-// ordered store of the kept keys.
+// One wave per cell, four cells per workgroup, no workgroup barriers.
+//  1. stage the cell ROI in the wave's LDS slab with aligned 32-bit loads (slab row starts at
+//     the ROI's x0 & 3, so words are stored unshifted);
+//  2. FAST test at minThFAST on every detection pixel; corners are compacted (ballot) into a
+//     small per-wave list and get their exact strength M (everything else has M = 0: it is not
+//     a corner at minThFAST, hence at no threshold the reference uses);
+//  3. walk the window row-major 64 pixels at a time: NMS at iniThFAST (fallback minThFAST if
+//     the cell came out empty, :834-838), ordered store of the kept keys.
 constexpr int kFastRowBytes = 72;          // >= 3 + 64 + 3 rounded to a word multiple
 constexpr int kFastSlab = kFastRowBytes * kRoiMax;
+constexpr int kFastList = 256;
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, ExtractBufs b)
 {
     __shared__ __attribute__((aligned(16))) uint8_t s_roi[kWaves][kFastSlab];
     __shared__ __attribute__((aligned(16))) uint8_t s_M[kWaves][kFastSlab];
+    __shared__ uint16_t s_list[kWaves][kFastList];
     const int wv = threadIdx.x >> 6, lane = lane_id();
     const int cidx = blockIdx.x * kWaves + wv, f = blockIdx.y;
     if (cidx >= P->ncells) return;
@@ -376,8 +408,8 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
     const int rw = c.rw, rh = c.rh;
     uint8_t* roi = s_roi[wv];
     uint8_t* Ms = s_M[wv];
-    const int sh = c.x0 & 3;                        // ROI column xx lives at slab byte sh + xx
-    // ---- stage the ROI (rows c.y0 .. c.y0+rh-1, bytes [x0 & ~3, x0 + rw) rounded up to words)
+    uint16_t* lst = s_list[wv];
+    const int sh = c.x0 & 3;
     const int nwords = (sh + rw + 3) >> 2;
     if ((g.pitch & 3) == 0) {
         const uint8_t* base = img + (int64_t)c.y0 * g.pitch + (c.x0 & ~3);
@@ -393,35 +425,48 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
         }
     }
     for (int i = lane; i < kFastRowBytes * rh / 4; i += 64) reinterpret_cast<uint32_t*>(Ms)[i] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- corner strength of every detection pixel (window = ROI inset by 3)
+    wave_sync_lds();
     const int ww = rw - 6, wh = rh - 6;
     const int npix = ww > 0 && wh > 0 ? ww * wh : 0;
-    for (int p = lane; p < npix; p += 64) {
-        const int yy = p / ww + 3, xx = p - (p / ww) * ww + 3;
-        const int o = yy * kFastRowBytes + sh + xx;
-        Ms[o] = (uint8_t)ring_strength(&roi[o], kFastRowBytes, th_min);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- per-cell NMS at iniThFAST, fallback to minThFAST when empty; ordered compaction
-    uint32_t* out = b.cand + ((int64_t)f * P->ncells + cidx) * P->cell_cap;
     const uint64_t lt = lanemask_lt();
+    // ---- 2. corners at minThFAST, exact strength for the corners only
+    int nl = 0;
+    int row0 = 0, col0 = 0;                 // (row, col) of pixel `base` in the window
+    for (int base = 0; base < npix; base += 64) {
+        int col = col0 + lane, row = row0;
+        while (col >= ww) { col -= ww; row++; }
+        const int o = (row + 3) * kFastRowBytes + sh + col + 3;
+        const bool corner = base + lane < npix && fast_corner(&roi[o], kFastRowBytes, th_min);
+        const uint64_t m = __ballot(corner);
+        if (corner) lst[nl + __popcll(m & lt)] = (uint16_t)o;
+        nl += __popcll(m);
+        col0 += 64;
+        while (col0 >= ww) { col0 -= ww; row0++; }
+        if (nl > kFastList - 64 || base + 64 >= npix) {
+            wave_sync_lds();
+            for (int e = lane; e < nl; e += 64) {
+                const int oo = lst[e];
+                Ms[oo] = (uint8_t)max(0, corner_strength(&roi[oo], kFastRowBytes));
+            }
+            wave_sync_lds();
+            nl = 0;
+        }
+    }
+    // ---- 3. NMS + ordered compaction
+    uint32_t* out = b.cand + ((int64_t)f * P->ncells + cidx) * P->cell_cap;
     int nkept = 0;
     for (int pass = 0; pass < 2; pass++) {
         const int t = pass == 0 ? th_ini : th_min;
         int running = 0;
+        row0 = 0;
+        col0 = 0;
         for (int base = 0; base < npix; base += 64) {
-            const int p = base + lane;
+            int col = col0 + lane, row = row0;
+            while (col >= ww) { col -= ww; row++; }
             bool kept = false;
-            int yy = 0, xx = 0, sc = 0;
-            if (p < npix) {
-                yy = p / ww + 3;
-                xx = p - (p / ww) * ww + 3;
-                const int o = yy * kFastRowBytes + sh + xx;
+            int sc = 0;
+            const int o = (row + 3) * kFastRowBytes + sh + col + 3;
+            if (base + lane < npix) {
                 const int M = Ms[o];
                 if (M > t) {
                     sc = M - 1;
@@ -441,11 +486,13 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
             if (kept) {
                 const int oo = running + __popcll(m & lt);
                 if (oo < P->cell_cap)
-                    out[oo] = pack_key(xx + c.j * g.wcell, yy + c.i * g.hcell, sc);
+                    out[oo] = pack_key(col + 3 + c.j * g.wcell, row + 3 + c.i * g.hcell, sc);
                 else
                     atomicOr(b.err, 2);
             }
             running += __popcll(m);
+            col0 += 64;
+            while (col0 >= ww) { col0 -= ww; row0++; }
         }
         nkept = running;
         if (nkept > 0) break;
@@ -467,16 +514,34 @@ struct NodeRef {
     int* start; int* cnt; int* alloc; int* buf; int4* rect;
 };
 
-__device__ __forceinline__ NodeRef node_set(uint8_t* nodes_f, const LevelGeom& g, int set)
+// k_octree dynamic LDS: work arrays (W entries), two node-record sets (W records), and two
+// key buffers of oct_kl entries used when the level has at most that many candidates.
+struct OctLds {
+    int* work; int4* cnt; int* base; int* rank; int* push; uint8_t* dead;
+    NodeRef set[2];
+    uint32_t* keys[2];
+};
+
+__device__ __forceinline__ OctLds oct_lds(uint8_t* smem, int W, int KL)
 {
-    int* base = reinterpret_cast<int*>(nodes_f) + g.node_off + (int64_t)set * 8 * g.ncap;
-    NodeRef r;
-    r.start = base;
-    r.cnt = base + g.ncap;
-    r.alloc = base + 2 * g.ncap;
-    r.buf = base + 3 * g.ncap;
-    r.rect = reinterpret_cast<int4*>(base + 4 * g.ncap);
-    return r;
+    OctLds o;
+    size_t off = 0;
+    o.cnt = reinterpret_cast<int4*>(smem + off); off += (size_t)W * 16;
+    o.work = reinterpret_cast<int*>(smem + off); off += (size_t)W * 4;
+    o.base = reinterpret_cast<int*>(smem + off); off += (size_t)W * 4;
+    o.rank = reinterpret_cast<int*>(smem + off); off += (size_t)W * 4;
+    o.push = reinterpret_cast<int*>(smem + off); off += (size_t)W * 4;
+    for (int s = 0; s < 2; s++) {
+        o.set[s].rect = reinterpret_cast<int4*>(smem + off); off += (size_t)W * 16;
+        o.set[s].start = reinterpret_cast<int*>(smem + off); off += (size_t)W * 4;
+        o.set[s].cnt = reinterpret_cast<int*>(smem + off); off += (size_t)W * 4;
+        o.set[s].alloc = reinterpret_cast<int*>(smem + off); off += (size_t)W * 4;
+        o.set[s].buf = reinterpret_cast<int*>(smem + off); off += (size_t)W * 4;
+    }
+    o.keys[0] = reinterpret_cast<uint32_t*>(smem + off); off += (size_t)KL * 4;
+    o.keys[1] = reinterpret_cast<uint32_t*>(smem + off); off += (size_t)KL * 4;
+    o.dead = smem + off;
+    return o;
 }
 
 __device__ __forceinline__ int quadrant(uint32_t k, int sx, int sy)
@@ -536,17 +601,18 @@ __device__ __forceinline__ void child_rect(const int4 p, int q, int4* out, int* 
     else *out = make_int4(mx, my, p.z, p.w);
 }
 
-constexpr int OCT_LMAX = 1024;   // max live list / work items per phase (host plan asserts)
-
 __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P, ExtractBufs b)
 {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int sbuf[kWaves + 2];
-    __shared__ int s_work[OCT_LMAX];      // slot ids of nodes divided this phase (processing order)
-    __shared__ int4 s_cnt[OCT_LMAX];      // their quadrant counts
-    __shared__ int s_base[OCT_LMAX];      // exclusive prefix of nonempty children (push order)
-    __shared__ int s_rank[OCT_LMAX];      // final phase: processing rank of vPrev entry
-    __shared__ int s_push[OCT_LMAX];      // final phase: push-order base per rank
-    __shared__ uint8_t s_dead[OCT_LMAX];  // final phase: slot erased this round
+    const OctLds O = oct_lds(smem, P->oct_w, P->oct_kl);
+    int* const s_work = O.work;      // slot ids of nodes divided this phase (processing order)
+    int4* const s_cnt = O.cnt;       // their quadrant counts
+    int* const s_base = O.base;      // exclusive prefix of nonempty children (push order)
+    int* const s_rank = O.rank;      // final phase: processing rank of vPrev entry
+    int* const s_push = O.push;      // final phase: push-order base per rank
+    uint8_t* const s_dead = O.dead;  // final phase: slot erased this round
+    const int OCT_LMAX = P->oct_w;
 
     const int l = blockIdx.x, f = blockIdx.y;
     const LevelGeom& g = P->lv[l];
@@ -554,15 +620,26 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     const DynMask dm = b.dyn[f];
     const int area = dm.area_flag;
     const int N = area ? g.nfeat_area : g.nfeat;
-    uint32_t* KB[2];
-    KB[0] = b.keys + (int64_t)f * 2 * P->kbuf_stride + g.kcap_off;
-    KB[1] = KB[0] + P->kbuf_stride;
-    uint8_t* nodes_f = b.nodes + (int64_t)f * P->node_stride * 4;
-
     // ---- 1. gather candidates in reference order ----
     const int* cn = b.cand_n + (int64_t)f * P->ncells + g.cell0;
     const uint32_t* cand = b.cand + ((int64_t)f * P->ncells + g.cell0) * P->cell_cap;
     int K = 0;
+    {
+        int part = 0;
+        for (int ci = tid; ci < g.ncells; ci += kThreads) part += cn[ci];
+        int tot;
+        block_scan_excl(part, &tot, sbuf);
+        K = tot;
+    }
+    // keys in LDS when they fit, else in the level's global ping-pong buffers (L2-resident)
+    uint32_t* KB[2];
+    if (K <= P->oct_kl) {
+        KB[0] = O.keys[0];
+        KB[1] = O.keys[1];
+    } else {
+        KB[0] = b.keys + (int64_t)f * 2 * P->kbuf_stride + g.kcap_off;
+        KB[1] = KB[0] + P->kbuf_stride;
+    }
     {
         int carry = 0;
         for (int base = 0; base < g.ncells; base += kThreads) {
@@ -609,7 +686,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     int cs = 0;            // current node set
     int alloc_ctr = g.nini;
     {
-        NodeRef S = node_set(nodes_f, g, 0);
+        NodeRef S = O.set[0];
         if (g.nini == 1) {
             if (K > 0 && tid == 0) {
                 S.start[0] = 0; S.cnt[0] = K; S.alloc[0] = 0; S.buf[0] = kb;
@@ -653,7 +730,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     while (!finish) {
         const int prevSize = n;
         if (n > OCT_LMAX || n > g.ncap) { if (tid == 0) atomicOr(b.err, 4); finish = true; break; }
-        NodeRef S = node_set(nodes_f, g, cs), D = node_set(nodes_f, g, cs ^ 1);
+        NodeRef S = O.set[cs], D = O.set[cs ^ 1];
         // divided nodes = cnt > 1, in list order
         int nd = 0;
         for (int base = 0; base < n; base += kThreads) {
@@ -746,7 +823,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     while (final_phase && !finish) {
         const int prevSize = n;
         if (n > OCT_LMAX) { if (tid == 0) atomicOr(b.err, 4); break; }
-        NodeRef S = node_set(nodes_f, g, cs), D = node_set(nodes_f, g, cs ^ 1);
+        NodeRef S = O.set[cs], D = O.set[cs ^ 1];
         // vPrev = list nodes with cnt > 1, i.e. vSizeAndPointerToNode of the previous round
         int m = 0;
         for (int base = 0; base < n; base += kThreads) {
@@ -878,7 +955,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     }
 
     // ---- 4. retain the best response per node (:747-766), border, final cull ----
-    NodeRef S = node_set(nodes_f, g, cs);
+    NodeRef S = O.set[cs];
     uint32_t* out = b.lvl_kp + (int64_t)f * P->lvl_stride + g.out_off;
     const bool cull = !area && l < 8;                  // CheckMovingKeyPoints_finall loops 8 levels
     const float scale = (l != 0) ? g.scale : 1.0f;
@@ -987,9 +1064,9 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
     __syncthreads();
     const int total = off[L];
     const int wv = threadIdx.x >> 6, lane = lane_id();
-    for (int sidx = 0; sidx < 4; sidx++) {
-        const int idx = blockIdx.x * 16 + wv * 4 + sidx;
-        if (idx >= total) break;
+    {
+        const int idx = blockIdx.x * kWaves + wv;
+        if (idx >= total) return;
         int l = 0;
         while (l + 1 < L && idx >= off[l + 1]) l++;
         const LevelGeom& g = P->lv[l];
@@ -1087,10 +1164,11 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     hipLaunchKernelGGL(k_fast, dim3((plan.ncells + kWaves - 1) / kWaves, F), dim3(kThreads), 0, s, d_plan, b);
     prof_end(prof, s);
     prof_begin(prof, "k_octree", s);
-    hipLaunchKernelGGL(k_octree, dim3(plan.L, F), dim3(kThreads), 0, s, d_plan, b);
+    (void)hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);
+    hipLaunchKernelGGL(k_octree, dim3(plan.L, F), dim3(kThreads), plan.oct_lds, s, d_plan, b);
     prof_end(prof, s);
     prof_begin(prof, "k_describe", s);
-    hipLaunchKernelGGL(k_describe, dim3((plan.kcap + 15) / 16, F), dim3(kThreads), 0, s, d_plan, b);
+    hipLaunchKernelGGL(k_describe, dim3((plan.kcap + kWaves - 1) / kWaves, F), dim3(kThreads), 0, s, d_plan, b);
     prof_end(prof, s);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

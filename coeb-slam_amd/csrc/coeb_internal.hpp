@@ -62,6 +62,9 @@ struct Plan {
     int rtab_ints;
     int umax[16];
     int gauss[7];
+    int oct_w;             // k_octree: node records per set / work-list entries (max ncap)
+    int oct_kl;            // k_octree: keys kept in LDS when a level has <= oct_kl candidates
+    int oct_lds;           // k_octree dynamic LDS bytes
 };
 
 // FAST cell descriptor (ORBextractor.cc:811-829): ROI in level coordinates
