@@ -325,27 +325,6 @@ __device__ __forceinline__ void ring16(const uint8_t* c, int st, int p[16])
     p[12] = c[-3];         p[13] = c[st - 3];     p[14] = c[2 * st - 2]; p[15] = c[3 * st - 1];
 }
 
-// FAST-9/16 test at threshold t: >= 9 contiguous ring pixels all < v - t or all > v + t
-// (FAST_t's count loop), evaluated on 16-bit dark/bright masks by shift-and doubling.
-__device__ __forceinline__ bool fast_corner(const uint8_t* c, int st, int t)
-{
-    int p[16];
-    ring16(c, st, p);
-    const int v = c[0];
-    uint32_t dk = 0, br = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        dk |= (uint32_t)(p[k] < v - t) << k;
-        br |= (uint32_t)(p[k] > v + t) << k;
-    }
-    uint32_t a = dk | (dk << 16), bb = br | (br << 16);
-    uint32_t ra = a & (a >> 1), rb = bb & (bb >> 1);
-    ra &= ra >> 2; rb &= rb >> 2;
-    ra &= ra >> 4; rb &= rb >> 4;
-    ra &= a >> 8; rb &= bb >> 8;
-    return ((ra | rb) & 0xFFFFu) != 0;
-}
-
 // Exact corner strength M = max over the 16 nine-pixel arcs of min(v - ring) (dark) or
 // min(ring - v) (bright); OpenCV cornerScore<16> = M - 1 for a corner.
 // Arc minima by doubling: m2 -> m4 -> m8 -> m9.
@@ -375,14 +354,19 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
 // One wave per cell, four cells per workgroup, no workgroup barriers.
 //  1. stage the cell ROI in the wave's LDS slab with aligned 32-bit loads (slab row starts at
 //     the ROI's x0 & 3, so words are stored unshifted);
-//  2. FAST test at minThFAST on every detection pixel; corners are compacted (ballot) into a
-//     small per-wave list and get their exact strength M (everything else has M = 0: it is not
-//     a corner at minThFAST, hence at no threshold the reference uses);
-//  3. walk the window row-major 64 pixels at a time: NMS at iniThFAST (fallback minThFAST if
-//     the cell came out empty, :834-838), ordered store of the kept keys.
+//  2. OpenCV's pre-test at minThFAST (ring pairs 0/8, 2/10, 4/12, 6/14 -- a necessary
+//     condition of a corner) on every detection pixel; survivors (a few %) are compacted
+//     (ballot) into a per-wave list, keeping row-major order;
+//  3. exact strength M of the survivors; M > minThFAST <=> corner at minThFAST.  Corners go to
+//     Ms (all other pixels keep M = 0: not a corner at any threshold the reference uses) and,
+//     still in row-major order, to the corner list;
+//  4. NMS over the corner list at iniThFAST (fallback minThFAST if the cell came out empty,
+//     :834-838) with ordered (ballot) stores of the kept keys.  A cell with more corners than
+//     the list holds walks the whole window instead.
 constexpr int kFastRowBytes = 72;          // >= 3 + 64 + 3 rounded to a word multiple
 constexpr int kFastSlab = kFastRowBytes * kRoiMax;
-constexpr int kFastList = 256;
+constexpr int kFastSurv = 128;             // survivor list (flushed when nearly full)
+constexpr int kFastCorners = 512;          // corner list
 
 __device__ __forceinline__ void wave_sync_lds()
 {
@@ -391,11 +375,45 @@ __device__ __forceinline__ void wave_sync_lds()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// FAST_t's first rejection stage (features2d/fast.cpp): d = tab[p0]|tab[p8]; d &= tab[p2]|tab[p10];
+// d &= tab[p4]|tab[p12]; d &= tab[p6]|tab[p14]; with tab = 1 (darker than v-t) / 2 (brighter).
+__device__ __forceinline__ bool fast_pretest(const uint8_t* c, int st, int t)
+{
+    const int v = c[0];
+    const int lo = v - t, hi = v + t;
+    auto cls = [&](int x) { return (x < lo ? 1 : 0) | (x > hi ? 2 : 0); };
+    int d = cls(c[3 * st]) | cls(c[-3 * st]);                 // p0 | p8
+    d &= cls(c[2 * st + 2]) | cls(c[-2 * st - 2]);             // p2 | p10
+    d &= cls(c[3]) | cls(c[-3]);                               // p4 | p12
+    d &= cls(c[-2 * st + 2]) | cls(c[2 * st - 2]);             // p6 | p14
+    return d != 0;
+}
+
+__device__ __forceinline__ int nms_keep(const uint8_t* Ms, int o, int t, int* sc_out)
+{
+    const int M = Ms[o];
+    if (M <= t) return 0;
+    const int sc = M - 1;
+    bool kept = true;
+#pragma unroll
+    for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+        for (int dx = -1; dx <= 1; dx++) {
+            if (dx == 0 && dy == 0) continue;
+            const int Mn = Ms[o + dy * kFastRowBytes + dx];
+            const int ns = Mn > t ? Mn - 1 : 0;
+            kept = kept && (sc > ns);
+        }
+    *sc_out = sc;
+    return kept ? 1 : 0;
+}
+
 __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, ExtractBufs b)
 {
     __shared__ __attribute__((aligned(16))) uint8_t s_roi[kWaves][kFastSlab];
     __shared__ __attribute__((aligned(16))) uint8_t s_M[kWaves][kFastSlab];
-    __shared__ uint16_t s_list[kWaves][kFastList];
+    __shared__ uint16_t s_surv[kWaves][kFastSurv];
+    __shared__ uint16_t s_corn[kWaves][kFastCorners];
     const int wv = threadIdx.x >> 6, lane = lane_id();
     const int cidx = blockIdx.x * kWaves + wv, f = blockIdx.y;
     if (cidx >= P->ncells) return;
@@ -408,7 +426,8 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
     const int rw = c.rw, rh = c.rh;
     uint8_t* roi = s_roi[wv];
     uint8_t* Ms = s_M[wv];
-    uint16_t* lst = s_list[wv];
+    uint16_t* surv = s_surv[wv];
+    uint16_t* corn = s_corn[wv];
     const int sh = c.x0 & 3;
     const int nwords = (sh + rw + 3) >> 2;
     if ((g.pitch & 3) == 0) {
@@ -429,70 +448,83 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
     const int ww = rw - 6, wh = rh - 6;
     const int npix = ww > 0 && wh > 0 ? ww * wh : 0;
     const uint64_t lt = lanemask_lt();
-    // ---- 2. corners at minThFAST, exact strength for the corners only
-    int nl = 0;
-    int row0 = 0, col0 = 0;                 // (row, col) of pixel `base` in the window
+    // ---- 2 + 3: pre-test, survivors -> exact strength -> corners (row-major throughout)
+    int ns = 0, nc = 0;
+    int row0 = 0, col0 = 0;
     for (int base = 0; base < npix; base += 64) {
         int col = col0 + lane, row = row0;
         while (col >= ww) { col -= ww; row++; }
         const int o = (row + 3) * kFastRowBytes + sh + col + 3;
-        const bool corner = base + lane < npix && fast_corner(&roi[o], kFastRowBytes, th_min);
-        const uint64_t m = __ballot(corner);
-        if (corner) lst[nl + __popcll(m & lt)] = (uint16_t)o;
-        nl += __popcll(m);
+        const bool sv = base + lane < npix && fast_pretest(&roi[o], kFastRowBytes, th_min);
+        const uint64_t m = __ballot(sv);
+        if (sv) surv[ns + __popcll(m & lt)] = (uint16_t)o;
+        ns += __popcll(m);
         col0 += 64;
         while (col0 >= ww) { col0 -= ww; row0++; }
-        if (nl > kFastList - 64 || base + 64 >= npix) {
+        if (ns > kFastSurv - 64 || base + 64 >= npix) {
             wave_sync_lds();
-            for (int e = lane; e < nl; e += 64) {
-                const int oo = lst[e];
-                Ms[oo] = (uint8_t)max(0, corner_strength(&roi[oo], kFastRowBytes));
+            for (int e0 = 0; e0 < ns; e0 += 64) {
+                const int e = e0 + lane;
+                int oo = 0, M = 0;
+                if (e < ns) {
+                    oo = surv[e];
+                    M = corner_strength(&roi[oo], kFastRowBytes);
+                }
+                const bool isc = e < ns && M > th_min;
+                if (isc) Ms[oo] = (uint8_t)M;
+                const uint64_t mc = __ballot(isc);
+                if (isc) {
+                    const int q = nc + __popcll(mc & lt);
+                    if (q < kFastCorners) corn[q] = (uint16_t)oo;
+                }
+                nc += __popcll(mc);
             }
             wave_sync_lds();
-            nl = 0;
+            ns = 0;
         }
     }
-    // ---- 3. NMS + ordered compaction
+    // ---- 4: NMS + ordered compaction
     uint32_t* out = b.cand + ((int64_t)f * P->ncells + cidx) * P->cell_cap;
     int nkept = 0;
     for (int pass = 0; pass < 2; pass++) {
         const int t = pass == 0 ? th_ini : th_min;
         int running = 0;
-        row0 = 0;
-        col0 = 0;
-        for (int base = 0; base < npix; base += 64) {
-            int col = col0 + lane, row = row0;
-            while (col >= ww) { col -= ww; row++; }
-            bool kept = false;
-            int sc = 0;
-            const int o = (row + 3) * kFastRowBytes + sh + col + 3;
-            if (base + lane < npix) {
-                const int M = Ms[o];
-                if (M > t) {
-                    sc = M - 1;
-                    kept = true;
-#pragma unroll
-                    for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-                        for (int dx = -1; dx <= 1; dx++) {
-                            if (dx == 0 && dy == 0) continue;
-                            const int Mn = Ms[o + dy * kFastRowBytes + dx];
-                            const int ns = Mn > t ? Mn - 1 : 0;
-                            kept = kept && (sc > ns);
-                        }
+        if (nc <= kFastCorners) {
+            for (int e0 = 0; e0 < nc; e0 += 64) {
+                const int e = e0 + lane;
+                int oo = 0, sc = 0, kept = 0;
+                if (e < nc) {
+                    oo = corn[e];
+                    kept = nms_keep(Ms, oo, t, &sc);
                 }
+                const uint64_t m = __ballot(kept);
+                if (kept) {
+                    const int q = running + __popcll(m & lt);
+                    const int yy = oo / kFastRowBytes, xx = oo - yy * kFastRowBytes - sh;
+                    if (q < P->cell_cap) out[q] = pack_key(xx + c.j * g.wcell, yy + c.i * g.hcell, sc);
+                    else atomicOr(b.err, 2);
+                }
+                running += __popcll(m);
             }
-            const uint64_t m = __ballot(kept);
-            if (kept) {
-                const int oo = running + __popcll(m & lt);
-                if (oo < P->cell_cap)
-                    out[oo] = pack_key(col + 3 + c.j * g.wcell, row + 3 + c.i * g.hcell, sc);
-                else
-                    atomicOr(b.err, 2);
+        } else {
+            row0 = 0;
+            col0 = 0;
+            for (int base = 0; base < npix; base += 64) {
+                int col = col0 + lane, row = row0;
+                while (col >= ww) { col -= ww; row++; }
+                const int o = (row + 3) * kFastRowBytes + sh + col + 3;
+                int sc = 0, kept = 0;
+                if (base + lane < npix) kept = nms_keep(Ms, o, t, &sc);
+                const uint64_t m = __ballot(kept);
+                if (kept) {
+                    const int q = running + __popcll(m & lt);
+                    if (q < P->cell_cap) out[q] = pack_key(col + 3 + c.j * g.wcell, row + 3 + c.i * g.hcell, sc);
+                    else atomicOr(b.err, 2);
+                }
+                running += __popcll(m);
+                col0 += 64;
+                while (col0 >= ww) { col0 -= ww; row0++; }
             }
-            running += __popcll(m);
-            col0 += 64;
-            while (col0 >= ww) { col0 -= ww; row0++; }
         }
         nkept = running;
         if (nkept > 0) break;

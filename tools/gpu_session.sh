@@ -25,6 +25,13 @@ for step in "$@"; do
         benchB) run benchB 600 python bench.py --config B --batch 64 --no-cpu-baseline ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 10 --no-cpu-baseline ;;
         diag) run diag 600 python tools/diag_parity.py ;;
+        pmc)
+            B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --batch 64"
+            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- $B
+            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- $B
+            run pmc_sq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace --output-format csv -d gpurun_out/pmc_sq -o run -- $B
+            run pmc_sq2 600 rocprofv3 --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_sq2 -o run -- $B
+            ;;
         *) echo "unknown step $step" ;;
     esac
 done
