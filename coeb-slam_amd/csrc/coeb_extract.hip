@@ -364,7 +364,6 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
 //     :834-838) with ordered (ballot) stores of the kept keys.  A cell with more corners than
 //     the list holds walks the whole window instead.
 constexpr int kFastRowBytes = 72;          // >= 3 + 64 + 3 rounded to a word multiple
-constexpr int kFastSlab = kFastRowBytes * kRoiMax;
 constexpr int kFastSurv = 128;             // survivor list (flushed when nearly full)
 constexpr int kFastCorners = 512;          // corner list
 
@@ -410,11 +409,10 @@ __device__ __forceinline__ int nms_keep(const uint8_t* Ms, int o, int t, int* sc
 
 __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, ExtractBufs b)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t s_roi[kWaves][kFastSlab];
-    __shared__ __attribute__((aligned(16))) uint8_t s_M[kWaves][kFastSlab];
-    __shared__ uint16_t s_surv[kWaves][kFastSurv];
-    __shared__ uint16_t s_corn[kWaves][kFastCorners];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wv = threadIdx.x >> 6, lane = lane_id();
+    const int slab = kFastRowBytes * P->max_roi_h;          // per-wave LDS: roi, M, lists
+    uint8_t* wbase = smem + (size_t)wv * (2 * slab + 2 * (kFastSurv + kFastCorners));
     const int cidx = blockIdx.x * kWaves + wv, f = blockIdx.y;
     if (cidx >= P->ncells) return;
     const CellDesc c = b.cells[cidx];
@@ -424,10 +422,10 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
     const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
     const uint8_t* img = level_ptr(P, b, f, l);
     const int rw = c.rw, rh = c.rh;
-    uint8_t* roi = s_roi[wv];
-    uint8_t* Ms = s_M[wv];
-    uint16_t* surv = s_surv[wv];
-    uint16_t* corn = s_corn[wv];
+    uint8_t* roi = wbase;
+    uint8_t* Ms = wbase + slab;
+    uint16_t* surv = reinterpret_cast<uint16_t*>(wbase + 2 * slab);
+    uint16_t* corn = surv + kFastSurv;
     const int sh = c.x0 & 3;
     const int nwords = (sh + rw + 3) >> 2;
     if ((g.pitch & 3) == 0) {
@@ -1193,7 +1191,8 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     hipLaunchKernelGGL(k_blur, dim3(tiles, F), dim3(kThreads), 0, s, d_plan, b, bt);
     prof_end(prof, s);
     prof_begin(prof, "k_fast", s);
-    hipLaunchKernelGGL(k_fast, dim3((plan.ncells + kWaves - 1) / kWaves, F), dim3(kThreads), 0, s, d_plan, b);
+    const int fast_lds = kWaves * (2 * kFastRowBytes * plan.max_roi_h + 2 * (kFastSurv + kFastCorners));
+    hipLaunchKernelGGL(k_fast, dim3((plan.ncells + kWaves - 1) / kWaves, F), dim3(kThreads), fast_lds, s, d_plan, b);
     prof_end(prof, s);
     prof_begin(prof, "k_octree", s);
     (void)hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);
