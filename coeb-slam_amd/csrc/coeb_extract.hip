@@ -18,7 +18,6 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr int kRoiMax = 64;          // max FAST ROI side (host plan asserts)
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
@@ -155,77 +154,87 @@ __device__ __forceinline__ int vresize(int h0, int h1, int b0, int b1)
     return max(0, min(s, 255));
 }
 
+// Output tile 128 x 32 per workgroup; the source rows/columns it touches (<= 32*scale+2 rows,
+// <= 128*scale+2 columns) are staged in LDS with aligned 32-bit loads, then each thread
+// produces 4 x 4 outputs (one 32-bit store per output row).
+constexpr int PT_W = 128, PT_H = 32, PT_SW = 264, PT_SH = 72;   // LDS source tile (scale <= 2)
+
 __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
                                                         int sw, int sh, uint8_t* __restrict__ dst, int64_t dst_fs,
                                                         int dp, int dw, int dh, const int* __restrict__ tab, int xmax)
 {
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[PT_SH * PT_SW];
     const int f = blockIdx.z;
-    const int dx0 = blockIdx.x * 256 + (threadIdx.x & 63) * 4;
-    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (dx0 >= dw || dy >= dh) return;
+    const int ox = blockIdx.x * PT_W, oy = blockIdx.y * PT_H;
     const int* xofs = tab;
     const int* alpha = tab + dw;
     const int* yofs = tab + 2 * dw;
     const int* beta = tab + 2 * dw + dh;
+    const int ex = min(ox + PT_W, dw) - 1, ey = min(oy + PT_H, dh) - 1;
+    const int sx0 = xofs[ox] & ~3, sx1 = min(xofs[ex] + 1, sw - 1);
+    const int sy0 = max(yofs[oy], 0), sy1 = min(max(yofs[ey] + 1, 0), sh - 1);
+    const int nwords = (sx1 - sx0) / 4 + 1, nrows = sy1 - sy0 + 1;
     const uint8_t* S = src + (int64_t)f * src_fs;
-    const int sy0 = yofs[dy];
-    const int r0 = sy0 >= 0 ? (sy0 < sh ? sy0 : sh - 1) : 0;
-    const int r1 = sy0 + 1 >= 0 ? (sy0 + 1 < sh ? sy0 + 1 : sh - 1) : 0;
-    const uint8_t* S0 = S + (int64_t)r0 * sp;
-    const uint8_t* S1 = S + (int64_t)r1 * sp;
-    const int bb = beta[dy];
-    const int b0 = (int)(short)(bb & 0xFFFF), b1 = bb >> 16;
-    const int nk = min(4, dw - dx0);
-    int sx[4], a0[4], a1[4];
+    if ((sp & 3) == 0) {
+        for (int i = threadIdx.x; i < nwords * nrows; i += kThreads) {
+            const int r = i / nwords, k = i - r * nwords;
+            *reinterpret_cast<uint32_t*>(s_src + r * PT_SW + 4 * k) =
+                *reinterpret_cast<const uint32_t*>(S + (int64_t)(sy0 + r) * sp + sx0 + 4 * k);
+        }
+    } else {
+        const int nb = sx1 - sx0 + 1;
+        for (int i = threadIdx.x; i < nb * nrows; i += kThreads) {
+            const int r = i / nb, k = i - r * nb;
+            s_src[r * PT_SW + k] = S[(int64_t)(sy0 + r) * sp + sx0 + k];
+        }
+    }
+    __syncthreads();
+    const int cx = ox + (threadIdx.x & 31) * 4, cy = oy + (threadIdx.x >> 5) * 4;
+    if (cx >= dw) return;
+    const int nk = min(4, dw - cx);
+    int lx[4], a0[4], a1[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int d = min(dx0 + k, dw - 1);
-        sx[k] = xofs[d];
+        const int d = min(cx + k, dw - 1);
+        const int sx = xofs[d];
         const int a = alpha[d];
         a0[k] = (int)(short)(a & 0xFFFF);
         a1[k] = a >> 16;
-        if (d >= xmax) { a0[k] = 2048; a1[k] = 0; }      // HResizeLinear tail: S[sx]*ONE
+        if (d >= xmax) { a0[k] = 2048; a1[k] = 0; }        // HResizeLinear tail: S[sx]*ONE
+        lx[k] = sx - sx0;
     }
-    const int base = sx[0] & ~3;
-    const bool fast = ((sp & 3) == 0) && (sx[nk - 1] + 1 - base < 12) && (base + 12 <= sw);
-    int out[4];
-    if (fast) {
-        const uint32_t* q0 = reinterpret_cast<const uint32_t*>(S0 + base);
-        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(S1 + base);
-        const uint32_t u0 = q0[0], u1 = q0[1], u2 = q0[2];
-        const uint32_t v0 = q1[0], v1 = q1[1], v2 = q1[2];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int dy = cy + r;
+        if (dy >= dh) break;
+        const int q0 = yofs[dy];
+        const int r0 = (q0 >= 0 ? (q0 < sh ? q0 : sh - 1) : 0) - sy0;
+        const int r1 = (q0 + 1 >= 0 ? (q0 + 1 < sh ? q0 + 1 : sh - 1) : 0) - sy0;
+        const int bb = beta[dy];
+        const int b0 = (int)(short)(bb & 0xFFFF), b1 = bb >> 16;
+        const uint8_t* R0 = s_src + r0 * PT_SW;
+        const uint8_t* R1 = s_src + r1 * PT_SW;
+        uint32_t word = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const int o = sx[k] - base;
-            const int h0 = byte_of(u0, u1, u2, o) * a0[k] + byte_of(u0, u1, u2, o + 1) * a1[k];
-            const int h1 = byte_of(v0, v1, v2, o) * a0[k] + byte_of(v0, v1, v2, o + 1) * a1[k];
-            out[k] = vresize(h0, h1, b0, b1);
+            const int h0 = R0[lx[k]] * a0[k] + R0[lx[k] + 1] * a1[k];
+            const int h1 = R1[lx[k]] * a0[k] + R1[lx[k] + 1] * a1[k];
+            word |= (uint32_t)vresize(h0, h1, b0, b1) << (8 * k);
         }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int s1 = min(sx[k] + 1, sw - 1);      // a1 == 0 whenever sx + 1 == sw
-            const int h0 = S0[sx[k]] * a0[k] + S0[s1] * a1[k];
-            const int h1 = S1[sx[k]] * a0[k] + S1[s1] * a1[k];
-            out[k] = vresize(h0, h1, b0, b1);
-        }
-    }
-    uint8_t* D = dst + (int64_t)f * dst_fs + (int64_t)dy * dp + dx0;
-    if (nk == 4 && (dp & 3) == 0) {
-        *reinterpret_cast<uint32_t*>(D) = (uint32_t)out[0] | ((uint32_t)out[1] << 8) | ((uint32_t)out[2] << 16) |
-                                          ((uint32_t)out[3] << 24);
-    } else {
-        for (int k = 0; k < nk; k++) D[k] = (uint8_t)out[k];
+        uint8_t* D = dst + (int64_t)f * dst_fs + (int64_t)dy * dp + cx;
+        if (nk == 4 && (dp & 3) == 0) *reinterpret_cast<uint32_t*>(D) = word;
+        else for (int k = 0; k < nk; k++) D[k] = (uint8_t)(word >> (8 * k));
     }
 }
 
 // ================================ k_blur ================================
-// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), Q8 kernel, Q16 vertical accumulation
-// (DESIGN.md s3.3).  Each thread owns 4 adjacent columns x 16 rows: the 7 horizontally
-// filtered rows the vertical tap needs slide through registers, so every source row is
-// fetched once per thread (three aligned 32-bit loads) and every output is one 32-bit store.
-// A wave covers 256 columns; a workgroup 256 x 64 outputs.
-constexpr int BT_W = 256, BT_H = 64, BT_ROWS = 16;
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), Q8 kernel [18 34 48 56 48 34 18] (sum 256),
+// Q16 vertical accumulation.  A lane owns 8 adjacent columns x 8 rows:
+// every source row it needs (14) is fetched once with four aligned 32-bit loads, filtered
+// horizontally with the symmetric taps, and the vertical taps run over a fully unrolled
+// window (static register indices, no ring moves).  Two 8-row strips per wave, 32 column
+// groups per strip: a workgroup covers 256 x 64 outputs.
+constexpr int BT_W = 256, BT_H = 64;
 
 __device__ __forceinline__ int reflect101(int p, int len)
 {
@@ -250,61 +259,58 @@ __global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, E
     const LevelGeom& g = P->lv[l];
     const int w = g.w, h = g.h, sp = g.pitch, dp = g.bpitch;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int x0 = tx * BT_W + lane * 4;
-    const int y0 = ty * BT_H + wv * BT_ROWS;
+    const int x0 = tx * BT_W + (lane & 31) * 8;
+    const int y0 = ty * BT_H + wv * 16 + (lane >> 5) * 8;
     if (x0 >= w || y0 >= h) return;
-    const int rows = min(BT_ROWS, h - y0);
     const uint8_t* src = level_ptr(P, b, f, l);
     uint8_t* dst = b.blur + (int64_t)f * P->blur_stride + g.blur_off;
-    int k[7];
+    const int k0 = P->gauss[0], k1 = P->gauss[1], k2 = P->gauss[2], k3 = P->gauss[3];
+    const bool interior = (x0 >= 4) && (x0 + 11 <= w) && ((sp & 3) == 0);
+    uint32_t hr[14][8];
 #pragma unroll
-    for (int i = 0; i < 7; i++) k[i] = P->gauss[i];
-    const bool interior = (x0 >= 4) && (x0 + 8 <= w) && ((sp & 3) == 0);
-    uint32_t ring[7][4];
-#pragma unroll
-    for (int i = 0; i < 7; i++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) ring[i][q] = 0;
-    for (int r = y0 - 3; r < y0 + rows + 3; r++) {
+    for (int rr = 0; rr < 14; rr++) {
+        const int r = y0 - 3 + rr;
         const uint8_t* row = src + (int64_t)reflect101(r, h) * sp;
-        int px[12];
+        uint32_t px[16];
         if (interior) {
             const uint32_t* q = reinterpret_cast<const uint32_t*>(row + x0 - 4);
-            const uint32_t u0 = q[0], u1 = q[1], u2 = q[2];
+            const uint32_t u0 = q[0], u1 = q[1], u2 = q[2], u3 = q[3];
 #pragma unroll
-            for (int i = 0; i < 12; i++) px[i] = byte_of(u0, u1, u2, i);
+            for (int i = 0; i < 4; i++) {
+                px[i] = (u0 >> (8 * i)) & 0xFFu;
+                px[4 + i] = (u1 >> (8 * i)) & 0xFFu;
+                px[8 + i] = (u2 >> (8 * i)) & 0xFFu;
+                px[12 + i] = (u3 >> (8 * i)) & 0xFFu;
+            }
         } else {
 #pragma unroll
-            for (int i = 1; i < 11; i++) px[i] = row[reflect101(x0 - 4 + i, w)];
-            px[0] = px[11] = 0;
+            for (int i = 1; i < 15; i++) px[i] = row[reflect101(x0 - 4 + i, w)];
+            px[0] = px[15] = 0;
         }
+        // output column x0+q uses pixels x0+q-3 .. x0+q+3 = px[q+1 .. q+7]
 #pragma unroll
-        for (int i = 0; i < 6; i++)
+        for (int q = 0; q < 8; q++)
+            hr[rr][q] = k0 * (px[q + 1] + px[q + 7]) + k1 * (px[q + 2] + px[q + 6]) + k2 * (px[q + 3] + px[q + 5]) +
+                        k3 * px[q + 4];
+        // vertical taps as soon as the 7-row window of output row rr-6 is complete
+        if (rr >= 6) {
+            const int yy = rr - 6;
+            const int y = y0 + yy;
+            if (y < h) {
+                uint32_t o[8];
 #pragma unroll
-            for (int q = 0; q < 4; q++) ring[i][q] = ring[i + 1][q];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int tp = 0; tp < 7; tp++) acc += (uint32_t)k[tp] * (uint32_t)px[q + tp + 1];
-            ring[6][q] = acc;
-        }
-        const int y = r - 3;
-        if (y >= y0) {
-            uint32_t o[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                uint32_t acc = 0;
-#pragma unroll
-                for (int tp = 0; tp < 7; tp++) acc += (uint32_t)k[tp] * ring[tp][q];
-                const uint32_t v = (acc + (1u << 15)) >> 16;
-                o[q] = v > 255u ? 255u : v;
-            }
-            uint8_t* D = dst + (int64_t)y * dp + x0;
-            if (x0 + 4 <= w) {
-                *reinterpret_cast<uint32_t*>(D) = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
-            } else {
-                for (int q = 0; q < w - x0; q++) D[q] = (uint8_t)o[q];
+                for (int q = 0; q < 8; q++) {
+                    const uint32_t acc = k0 * (hr[yy][q] + hr[yy + 6][q]) + k1 * (hr[yy + 1][q] + hr[yy + 5][q]) +
+                                         k2 * (hr[yy + 2][q] + hr[yy + 4][q]) + k3 * hr[yy + 3][q];
+                    o[q] = (acc + (1u << 15)) >> 16;       // <= 255: taps sum to 256
+                }
+                uint8_t* D = dst + (int64_t)y * dp + x0;
+                if (x0 + 8 <= w) {
+                    *reinterpret_cast<uint2*>(D) = make_uint2(o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24),
+                                                              o[4] | (o[5] << 8) | (o[6] << 16) | (o[7] << 24));
+                } else {
+                    for (int q = 0; q < w - x0; q++) D[q] = (uint8_t)o[q];
+                }
             }
         }
     }
@@ -1173,7 +1179,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         const uint8_t* src = l == 1 ? b.gray : b.pyr + gp.pyr_off;
         const int64_t src_fs = l == 1 ? (int64_t)plan.W * plan.H : plan.pyr_stride;
         prof_begin(prof, "k_pyr_level", s);
-        hipLaunchKernelGGL(k_pyr_level, dim3((g.w + 255) / 256, (g.h + 3) / 4, F), dim3(kThreads), 0, s, src, src_fs,
+        hipLaunchKernelGGL(k_pyr_level, dim3((g.w + PT_W - 1) / PT_W, (g.h + PT_H - 1) / PT_H, F), dim3(kThreads), 0, s, src, src_fs,
                            gp.pitch, gp.w, gp.h, b.pyr + g.pyr_off, plan.pyr_stride, g.pitch, g.w, g.h,
                            b.rtab + g.rtab_off, g.xmax);
         prof_end(prof, s);
