@@ -228,13 +228,12 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
 }
 
 // ================================ k_blur ================================
-// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), Q8 kernel [18 34 48 56 48 34 18] (sum 256),
-// Q16 vertical accumulation.  A lane owns 8 adjacent columns x 8 rows:
-// every source row it needs (14) is fetched once with four aligned 32-bit loads, filtered
-// horizontally with the symmetric taps, and the vertical taps run over a fully unrolled
-// window (static register indices, no ring moves).  Two 8-row strips per wave, 32 column
-// groups per strip: a workgroup covers 256 x 64 outputs.
-constexpr int BT_W = 256, BT_H = 64;
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), Q8 kernel, Q16 vertical accumulation
+// (DESIGN.md s3.3).  Each thread owns 4 adjacent columns x 16 rows: the 7 horizontally
+// filtered rows the vertical tap needs slide through registers, so every source row is
+// fetched once per thread (three aligned 32-bit loads) and every output is one 32-bit store.
+// A wave covers 256 columns; a workgroup 256 x 64 outputs.
+constexpr int BT_W = 256, BT_H = 64, BT_ROWS = 16;
 
 __device__ __forceinline__ int reflect101(int p, int len)
 {
@@ -259,58 +258,61 @@ __global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, E
     const LevelGeom& g = P->lv[l];
     const int w = g.w, h = g.h, sp = g.pitch, dp = g.bpitch;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int x0 = tx * BT_W + (lane & 31) * 8;
-    const int y0 = ty * BT_H + wv * 16 + (lane >> 5) * 8;
+    const int x0 = tx * BT_W + lane * 4;
+    const int y0 = ty * BT_H + wv * BT_ROWS;
     if (x0 >= w || y0 >= h) return;
+    const int rows = min(BT_ROWS, h - y0);
     const uint8_t* src = level_ptr(P, b, f, l);
     uint8_t* dst = b.blur + (int64_t)f * P->blur_stride + g.blur_off;
-    const int k0 = P->gauss[0], k1 = P->gauss[1], k2 = P->gauss[2], k3 = P->gauss[3];
-    const bool interior = (x0 >= 4) && (x0 + 11 <= w) && ((sp & 3) == 0);
-    uint32_t hr[14][8];
+    int k[7];
 #pragma unroll
-    for (int rr = 0; rr < 14; rr++) {
-        const int r = y0 - 3 + rr;
+    for (int i = 0; i < 7; i++) k[i] = P->gauss[i];
+    const bool interior = (x0 >= 4) && (x0 + 8 <= w) && ((sp & 3) == 0);
+    uint32_t ring[7][4];
+#pragma unroll
+    for (int i = 0; i < 7; i++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) ring[i][q] = 0;
+    for (int r = y0 - 3; r < y0 + rows + 3; r++) {
         const uint8_t* row = src + (int64_t)reflect101(r, h) * sp;
-        uint32_t px[16];
+        int px[12];
         if (interior) {
             const uint32_t* q = reinterpret_cast<const uint32_t*>(row + x0 - 4);
-            const uint32_t u0 = q[0], u1 = q[1], u2 = q[2], u3 = q[3];
+            const uint32_t u0 = q[0], u1 = q[1], u2 = q[2];
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                px[i] = (u0 >> (8 * i)) & 0xFFu;
-                px[4 + i] = (u1 >> (8 * i)) & 0xFFu;
-                px[8 + i] = (u2 >> (8 * i)) & 0xFFu;
-                px[12 + i] = (u3 >> (8 * i)) & 0xFFu;
-            }
+            for (int i = 0; i < 12; i++) px[i] = byte_of(u0, u1, u2, i);
         } else {
 #pragma unroll
-            for (int i = 1; i < 15; i++) px[i] = row[reflect101(x0 - 4 + i, w)];
-            px[0] = px[15] = 0;
+            for (int i = 1; i < 11; i++) px[i] = row[reflect101(x0 - 4 + i, w)];
+            px[0] = px[11] = 0;
         }
-        // output column x0+q uses pixels x0+q-3 .. x0+q+3 = px[q+1 .. q+7]
 #pragma unroll
-        for (int q = 0; q < 8; q++)
-            hr[rr][q] = k0 * (px[q + 1] + px[q + 7]) + k1 * (px[q + 2] + px[q + 6]) + k2 * (px[q + 3] + px[q + 5]) +
-                        k3 * px[q + 4];
-        // vertical taps as soon as the 7-row window of output row rr-6 is complete
-        if (rr >= 6) {
-            const int yy = rr - 6;
-            const int y = y0 + yy;
-            if (y < h) {
-                uint32_t o[8];
+        for (int i = 0; i < 6; i++)
 #pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const uint32_t acc = k0 * (hr[yy][q] + hr[yy + 6][q]) + k1 * (hr[yy + 1][q] + hr[yy + 5][q]) +
-                                         k2 * (hr[yy + 2][q] + hr[yy + 4][q]) + k3 * hr[yy + 3][q];
-                    o[q] = (acc + (1u << 15)) >> 16;       // <= 255: taps sum to 256
-                }
-                uint8_t* D = dst + (int64_t)y * dp + x0;
-                if (x0 + 8 <= w) {
-                    *reinterpret_cast<uint2*>(D) = make_uint2(o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24),
-                                                              o[4] | (o[5] << 8) | (o[6] << 16) | (o[7] << 24));
-                } else {
-                    for (int q = 0; q < w - x0; q++) D[q] = (uint8_t)o[q];
-                }
+            for (int q = 0; q < 4; q++) ring[i][q] = ring[i + 1][q];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int tp = 0; tp < 7; tp++) acc += (uint32_t)k[tp] * (uint32_t)px[q + tp + 1];
+            ring[6][q] = acc;
+        }
+        const int y = r - 3;
+        if (y >= y0) {
+            uint32_t o[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int tp = 0; tp < 7; tp++) acc += (uint32_t)k[tp] * ring[tp][q];
+                const uint32_t v = (acc + (1u << 15)) >> 16;
+                o[q] = v > 255u ? 255u : v;
+            }
+            uint8_t* D = dst + (int64_t)y * dp + x0;
+            if (x0 + 4 <= w) {
+                *reinterpret_cast<uint32_t*>(D) = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
+            } else {
+                for (int q = 0; q < w - x0; q++) D[q] = (uint8_t)o[q];
             }
         }
     }
