@@ -105,6 +105,47 @@ def cpu_baseline(cfg, seconds=12.0, min_frames=30):
                        % (len(times), w, h, med * 1e3))
 
 
+class DryRunPipeline:
+    """CPU stand-in with the BatchPipeline surface, for testing bench's multi-rank plumbing."""
+
+    class _Ctx:
+        def __init__(self):
+            self._on = False
+
+        def profile(self, on=True):
+            self._on = on
+
+        def profile_reset(self):
+            pass
+
+        def profile_read(self):
+            return {"k_fast": (1.0, 1)} if self._on else {}
+
+        def debug_read(self, what, f=0):
+            return np.zeros(4, np.uint8)
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.ctx = self._Ctx()
+
+    def load(self, frames, **kw):
+        self.F = len(frames)
+
+    def run(self):
+        time.sleep(0.002 * (1 + self.rank))   # ranks finish at different times: max must win
+
+    def synchronize(self):
+        pass
+
+    def results(self):
+        from coeb_front import KEYPOINT_DTYPE
+        out = [(np.zeros(1000, KEYPOINT_DTYPE), np.zeros((1000, 32), np.uint8))] * self.F
+        return out, None, [None] + [750] * (self.F - 1)
+
+    def close(self):
+        pass
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,30 +155,29 @@ def main():
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip HIP-event kernel timing")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: exercise the rank/timing/JSON plumbing with a stand-in pipeline (tests)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    from coeb_front.dist import Ranks
+    ranks = Ranks()
+    world, rank, local_rank = ranks.world, ranks.rank, ranks.local_rank
 
     from coeb_front import synth
-    from coeb_front.pipeline import BatchPipeline
     cfg = CONFIGS[args.config]
     w, h = cfg["w"], cfg["h"]
     F = args.batch + 1
     frames = synth.make_frames(w, h, F, seed=1000 + 17 * rank)
     Tcw = np.stack([synth.motion_pose()] * F)
-    bp = BatchPipeline(w, h, F, nfeatures=cfg["nfeatures"], device=local_rank)
+    if args.dry_run:
+        bp = DryRunPipeline(rank)
+    else:
+        from coeb_front.pipeline import BatchPipeline
+        bp = BatchPipeline(w, h, F, nfeatures=cfg["nfeatures"], device=local_rank)
     bp.load(frames, Tcw=Tcw)
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        ranks.barrier()
 
     for _ in range(args.warmup):
         bp.run()
@@ -158,12 +198,7 @@ def main():
     bp.synchronize()
     t1 = time.perf_counter()
     barrier()
-    elapsed = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = ranks.max(t1 - t0)
     prof = bp.ctx.profile_read() if not args.no_profile else {}
 
     frames_total = args.batch * args.steps * world
@@ -199,14 +234,13 @@ def main():
                                            frac=round(value * pipeline_bytes / 1e9 / HBM_PEAK_GBS, 6)),
                     kernels_ms_per_step={k: round(v[0] / max(1, args.steps), 4) for k, v in prof.items()},
                     keypoints_per_frame=round(nkp, 1), matches_per_frame=round(nmatch, 1))
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and not args.dry_run:
             cb = cpu_baseline(cfg)
             line["cpu_baseline"] = cb
             line["speedup_vs_cpu_baseline"] = round(value / cb["value"], 1)
         print(json.dumps(line), flush=True)
     bp.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    ranks.close()
 
 
 if __name__ == "__main__":

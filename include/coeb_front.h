@@ -143,11 +143,13 @@ int coeb_batch_results(coeb_ctx* ctx, const coeb_keypoint** d_kps, const uint8_t
                        const int32_t** d_counts, int* kcap);
 
 /* Batch TrackWithMotionModel matching (Tracking.cc:933-958 call pattern): for f = 1..nframes-1
- * frame f is matched to frame f-1 of the last extracted batch: LastFrame map points are the
- * keypoints of f-1 with depth > 0 unprojected with Tcw_prev (Frame::UnprojectStereo,
- * Frame.cc:844-858), observations = nobs; SearchByProjection(th) and, if < 20 matches,
- * again with 2*th.  d_depth: nframes x height x width float (device).  Tcw: nframes x 16 host
- * floats (row-major 4x4).  Results: coeb_batch_match_results. */
+ * frame f is matched to frame f-1 of the last extracted batch.  Frame f-1 is the LastFrame and
+ * defines the world frame (its Tcw = I): its map points are its keypoints with depth > 0
+ * unprojected with Twc = I (Frame::UnprojectStereo, Frame.cc:844-858), Observations() = nobs.
+ * Tcw[f] (row-major 4x4, host, nframes x 16 floats; entry 0 unused) is the pose of frame f
+ * relative to frame f-1 (the motion-model prediction mVelocity*mLastFrame.mTcw,
+ * Tracking.cc:937).  SearchByProjection(th) and, if < 20 matches, again with 2*th.
+ * d_depth: nframes x height x width float (device).  Results: coeb_batch_match_results. */
 int coeb_match_batch_device(coeb_ctx* ctx, const float* d_depth, int nframes, int width, int height,
                             const coeb_camera* cam, const float* Tcw, float th, int32_t nobs);
 int coeb_batch_match_results(coeb_ctx* ctx, const int32_t** d_match, const int32_t** d_nmatches);

@@ -1,0 +1,33 @@
+// Compile check of the drop-in adapters against reference-shaped Frame/MapPoint types
+// (include/Frame.h:142-215, include/MapPoint.h:46-75 member names and types).
+#include "ORBextractor.h"
+#include "ORBmatcher_coeb.h"
+
+struct MapPoint {
+    cv::Mat GetWorldPos() { return cv::Mat(); }
+    cv::Mat GetDescriptor() { return cv::Mat(); }
+    int Observations() { return 2; }
+};
+struct Frame {
+    static float fx, fy, cx, cy, mnMinX, mnMaxX, mnMinY, mnMaxY;
+    float mbf = 0, mb = 0;
+    int N = 0;
+    std::vector<cv::KeyPoint> mvKeysUn;
+    std::vector<float> mvuRight;
+    std::vector<MapPoint*> mvpMapPoints;
+    std::vector<bool> mvbOutlier;
+    cv::Mat mDescriptors, mTcw;
+};
+float Frame::fx, Frame::fy, Frame::cx, Frame::cy, Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY, Frame::mnMaxY;
+
+int use_adapters(Frame& cur, const Frame& last, cv::Mat& im)
+{
+    ORB_SLAM2::ORBextractor ex(1000, 1.2f, 8, 20, 7);
+    std::vector<cv::KeyPoint> kps;
+    cv::Mat desc, mask_result;
+    std::vector<std::vector<float>> box;
+    std::vector<cv::Point2f> tm;
+    std::vector<int> blur;
+    ex(im, cv::Mat(), im, im, kps, desc, box, tm, mask_result, blur);
+    return coeb::SearchByProjectionLastFrame(cur, last, 15.0f, false, 0.9f, true) + ex.GetLevels();
+}
