@@ -105,6 +105,20 @@ def cpu_baseline(cfg, seconds=12.0, min_frames=30):
                        % (len(times), w, h, med * 1e3))
 
 
+def pmc_traffic(kernel, frames_per_launch):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py --json from separate
+    FETCH_SIZE / WRITE_SIZE passes of this bench), scaled to this run's frames per launch."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        k = d["kernels"][kernel]
+        return int(k["traffic_bytes"] * frames_per_launch / d["frames_per_launch"]), d.get("command", "")
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None, None
+
+
 class DryRunPipeline:
     """CPU stand-in with the BatchPipeline surface, for testing bench's multi-rank plumbing."""
 
@@ -155,6 +169,7 @@ def main():
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip HIP-event kernel timing")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the rank/timing/JSON plumbing with a stand-in pipeline (tests)")
     args = ap.parse_args()
@@ -201,6 +216,23 @@ def main():
     elapsed = ranks.max(t1 - t0)
     prof = bp.ctx.profile_read() if not args.no_profile else {}
 
+    e2e = None
+    if not args.no_e2e and not args.dry_run:
+        # host buffers in and out (synchronous copies, no overlap): reported, never `value`
+        e2e_steps = max(2, min(5, args.steps))
+        st = bp.run_host(frames)
+        bp.synchronize()
+        barrier()
+        te0 = time.perf_counter()
+        for _ in range(e2e_steps):
+            st = bp.run_host(frames, st)
+        bp.synchronize()
+        te = ranks.max(time.perf_counter() - te0)
+        e2e = dict(value=round(args.batch * e2e_steps * world / te, 2), unit="frames/s",
+                   ms_per_step=round(te / e2e_steps * 1e3, 4), steps=e2e_steps,
+                   note="host gray frames uploaded and keypoints/descriptors/matches downloaded each step "
+                        "(synchronous hipMemcpy on the context stream, pageable host memory)")
+
     frames_total = args.batch * args.steps * world
     value = frames_total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -217,9 +249,12 @@ def main():
                 frames_per_launch = F
             bpl = kernel_bytes(name, w, h, nkp, nkp, npx, ncand) * frames_per_launch
             achieved = bpl / avg_s / 1e9
+            traffic, tsrc = pmc_traffic(name, frames_per_launch)
             roof = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None, kernel=name,
+                        frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, kernel=name,
                         avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=int(bpl))
+            if traffic is not None:
+                roof["traffic_source"] = "profiles/pmc_traffic.json (%s)" % tsrc
         pipeline_bytes = w * h + 60 * nkp + 36 * nkp     # B = W*H + 60 N_kp + 36 N_prev
         line = dict(metric=METRIC, value=round(value, 2), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(ms_per_step, 4), higher_is_better=True,
@@ -233,7 +268,8 @@ def main():
                                            achieved_GBps=round(value * pipeline_bytes / 1e9, 3),
                                            frac=round(value * pipeline_bytes / 1e9 / HBM_PEAK_GBS, 6)),
                     kernels_ms_per_step={k: round(v[0] / max(1, args.steps), 4) for k, v in prof.items()},
-                    keypoints_per_frame=round(nkp, 1), matches_per_frame=round(nmatch, 1))
+                    keypoints_per_frame=round(nkp, 1), matches_per_frame=round(nmatch, 1),
+                    pcie_inclusive=e2e)
         if not args.no_cpu_baseline and world == 1 and not args.dry_run:
             cb = cpu_baseline(cfg)
             line["cpu_baseline"] = cb

@@ -240,6 +240,13 @@ class Context:
             self.check(lib().coeb_memcpy_d2h(self.h, _p(out), C.c_void_p(dptr), nbytes))
         return out
 
+    def download_into(self, dptr, out):
+        """Copy out.nbytes bytes from device pointer dptr into the contiguous array out."""
+        assert out.flags["C_CONTIGUOUS"]
+        if out.nbytes:
+            self.check(lib().coeb_memcpy_d2h(self.h, _p(out), C.c_void_p(dptr), out.nbytes))
+        return out
+
     # ---- profiling (HIP events on the context stream) ----
     def profile(self, enable=True):
         self.check(lib().coeb_profile_enable(self.h, int(enable)))

@@ -64,6 +64,27 @@ class BatchPipeline:
     def synchronize(self):
         self.ctx.synchronize()
 
+    def run_host(self, frames, staging=None):
+        """One step with host buffers at both ends (the PCIe-inclusive rate):
+        upload `frames` (F, H, W) u8, extract + match, copy keypoints, descriptors, counts and
+        match indices back.  Copies are synchronous on the context stream (not overlapped).
+        Returns the staging dict of host arrays (reused across calls)."""
+        kp_ptr, desc_ptr, cnt_ptr, kcap = self.ctx.batch_results()
+        if staging is None:
+            staging = dict(kps=np.empty(28 * kcap * self.F, np.uint8), desc=np.empty(32 * kcap * self.F, np.uint8),
+                           counts=np.empty(self.F, np.int32), match=np.empty(kcap * self.F, np.int32),
+                           nmatch=np.empty(self.F, np.int32))
+        self.gray.write(frames)
+        self.run()
+        kp_ptr, desc_ptr, cnt_ptr, kcap = self.ctx.batch_results()
+        m_ptr, n_ptr = self.ctx.batch_match_results()
+        self.ctx.download_into(cnt_ptr, staging["counts"])
+        self.ctx.download_into(kp_ptr, staging["kps"])
+        self.ctx.download_into(desc_ptr, staging["desc"])
+        self.ctx.download_into(m_ptr, staging["match"])
+        self.ctx.download_into(n_ptr, staging["nmatch"])
+        return staging
+
     def results(self):
         """Host copies: list of (keypoints, descriptors) per frame, match arrays, nmatches."""
         kp_ptr, desc_ptr, cnt_ptr, kcap = self.ctx.batch_results()

@@ -313,5 +313,7 @@ def test_batch_B_full_size_properties(oracle_mod):
                 m = matches[f]
                 assert (m >= -1).all() and (m < len(out[f - 1][0])).all()
                 assert nms[f] == int((m >= 0).sum()) and nms[f] > 0.5 * len(k)
+                used = m[m >= 0]
+                assert len(np.unique(used)) == len(used)     # a LastFrame point matches at most once
     finally:
         bp.close()

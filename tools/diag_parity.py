@@ -100,46 +100,30 @@ def main():
     print("[match] nmatches ref=%d gpu=%d, array equal=%s" % (nm_ref, nm, np.array_equal(cur.mvpMapPoints, m_ref)))
     allok &= mok
 
-    # batch device path vs single-frame path
-    import torch
+    # batch device path vs single-frame path (library-owned device memory; no torch.cuda)
+    from coeb_front.pipeline import BatchPipeline
     F = 4
     fr = synth.make_frames(640, 480, F, seed=1000)
-    d = torch.from_numpy(fr).cuda()
-    torch.cuda.synchronize()
-    ctx.extract_batch_device(d.data_ptr(), F, 640, 480)
-    ctx.synchronize()
-    kp_ptr, desc_ptr, cnt_ptr, kcap = ctx.batch_results()
-    import ctypes as C
-    counts = np.zeros(F, np.int32)
-    hip = C.CDLL("libamdhip64.so")
-    hip.hipMemcpy(C.c_void_p(counts.ctypes.data), C.c_void_p(cnt_ptr), C.c_size_t(4 * F), 2)
+    bp = BatchPipeline(640, 480, F)
+    bp.load(fr, Tcw=np.stack([synth.motion_pose()] * F))
+    bp.run()
+    bp.synchronize()
+    out, matches, nms = bp.results()
     bok = True
     for f in range(F):
         ref = ex.extract(fr[f])
-        kb = np.zeros(kcap, KEYPOINT_DTYPE)
-        hip.hipMemcpy(C.c_void_p(kb.ctypes.data), C.c_void_p(kp_ptr + f * kcap * 28), C.c_size_t(kcap * 28), 2)
-        kb = kb[:counts[f]]
-        e = len(kb) == len(ref["kps"]) and all(np.array_equal(kb[n], ref["kps"][n]) for n in KEYPOINT_DTYPE.names)
-        bok &= e
-    print("[batch] counts", list(counts), "parity", bok)
+        kb = out[f][0]
+        bok &= len(kb) == len(ref["kps"]) and all(np.array_equal(kb[n], ref["kps"][n]) for n in KEYPOINT_DTYPE.names)
+    print("[batch] counts", [len(o[0]) for o in out], "parity", bok, "nmatches", nms[1:])
     allok &= bok
-    dd = torch.from_numpy(np.stack([depth] * F)).cuda()
-    Tcw = np.stack([synth.motion_pose()] * F)
-    torch.cuda.synchronize()
-    ctx.match_batch_device(dd.data_ptr(), F, 640, 480, cam, Tcw, 15.0, 2)
-    ctx.synchronize()
-    mptr, nptr = ctx.batch_match_results()
-    nms = np.zeros(F, np.int32)
-    hip.hipMemcpy(C.c_void_p(nms.ctypes.data), C.c_void_p(nptr), C.c_size_t(4 * F), 2)
-    print("[batch match] nmatches", list(nms[1:]))
-    # timing
-    ctx.profile(True)
+    bp.ctx.profile(True)
     t = time.time()
     for _ in range(5):
-        ctx.extract_batch_device(d.data_ptr(), F, 640, 480)
-    ctx.synchronize()
+        bp.run()
+    bp.synchronize()
     print("[time] 5 x batch4: %.3f ms/batch" % ((time.time() - t) / 5 * 1e3))
-    print(ctx.profile_read())
+    print(bp.ctx.profile_read())
+    bp.close()
     print("ALL", "OK" if allok else "FAIL")
 
 

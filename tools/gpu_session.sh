@@ -23,12 +23,14 @@ for step in "$@"; do
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
         benchB) run benchB 600 python bench.py --config B --batch 64 --no-cpu-baseline ;;
-        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 10 --no-cpu-baseline ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-e2e ;;
         diag) run diag 600 python tools/diag_parity.py ;;
         pmc)
-            B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --batch 64"
+            B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-e2e"
             run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- $B
             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- $B
+            python tools/pmc_summary.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv \
+                --json gpurun_out/pmc_traffic.json --frames 257 --command "$B" > gpurun_out/pmc_traffic.log 2>&1
             run pmc_sq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace --output-format csv -d gpurun_out/pmc_sq -o run -- $B
             run pmc_sq2 600 rocprofv3 --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_sq2 -o run -- $B
             ;;

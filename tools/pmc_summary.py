@@ -21,12 +21,38 @@ def load(path):
     return {k: ({c: v / len(disp[k]) for c, v in agg[k].items()}, len(disp[k]), grid[k]) for k in agg}
 
 
+def traffic_json(merged, nd, frames, command):
+    """Per kernel, HBM bytes per launch: 2 x FETCH_SIZE (gfx950 under-count of streaming reads,
+    MI355X_MICROARCH.md s HBM) + WRITE_SIZE, both reported by rocprofv3 in KB."""
+    out = dict(frames_per_launch=frames, command=command,
+               correction="bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch, mean over dispatches",
+               kernels={})
+    for k, cv in sorted(merged.items()):
+        if "FETCH_SIZE" not in cv or "WRITE_SIZE" not in cv:
+            continue
+        out["kernels"][k] = dict(fetch_kb=round(cv["FETCH_SIZE"], 3), write_kb=round(cv["WRITE_SIZE"], 3),
+                                 traffic_bytes=int((2 * cv["FETCH_SIZE"] + cv["WRITE_SIZE"]) * 1024),
+                                 dispatches=nd[k])
+    return out
+
+
 if __name__ == "__main__":
+    import argparse
+    import json
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv", nargs="+")
+    ap.add_argument("--json", help="write per-kernel HBM traffic per launch (for bench.py roofline.traffic)")
+    ap.add_argument("--frames", type=int, default=0, help="frames per launch of the profiled command")
+    ap.add_argument("--command", default="")
+    a = ap.parse_args()
     merged = collections.defaultdict(dict)
     nd = {}
-    for p in sys.argv[1:]:
+    for p in a.csv:
         for k, (cv, n, g) in load(p).items():
             merged[k].update(cv)
             nd[k] = n
     for k, cv in sorted(merged.items()):
         print("%-16s n=%-3d %s" % (k, nd[k], " ".join("%s=%.4g" % (c, v) for c, v in sorted(cv.items()))))
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(traffic_json(merged, nd, a.frames, a.command), f, indent=1)
