@@ -228,12 +228,18 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
 }
 
 // ================================ k_blur ================================
-// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), Q8 kernel, Q16 vertical accumulation
-// (DESIGN.md s3.3).  Each thread owns 4 adjacent columns x 16 rows: the 7 horizontally
-// filtered rows the vertical tap needs slide through registers, so every source row is
-// fetched once per thread (three aligned 32-bit loads) and every output is one 32-bit store.
-// A wave covers 256 columns; a workgroup 256 x 64 outputs.
-constexpr int BT_W = 256, BT_H = 64, BT_ROWS = 16;
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), Q8 kernel k (symmetric, sum 256), result
+// (sum_ij k_i k_j p_ij + 2^15) >> 16.  OpenCV's horizontal-then-vertical
+// order has no intermediate rounding, so the same integer is computed vertical-first:
+//   * vertical 7-tap on packed u16 column pairs (sums <= 255*256 fit 16 bits): 7 v_pk ops
+//     per 2 columns, the 7 source rows slide through registers (row loop unrolled by 7, so
+//     the ring never moves);
+//   * horizontal 7-tap as four v_dot2_u32_u16 per output on the packed vertical sums, the
+//     3-column halo coming from the neighbouring lanes by DPP row shifts;
+//   * the rounded result is byte 2 of the 24-bit accumulator: v_perm packs 4 outputs.
+// Work item = one wave: 4 row groups of 16 lanes; a group covers 64 source columns (4 per
+// lane) of which lanes 1..14 produce (56 output columns), and one band of rows.
+constexpr int kBlurCols = 56;
 
 __device__ __forceinline__ int reflect101(int p, int len)
 {
@@ -242,77 +248,121 @@ __device__ __forceinline__ int reflect101(int p, int len)
     return p;
 }
 
-struct BlurTiles {
+struct BlurWork {
     int L;
-    int tiles_x[COEB_MAXL];
-    int tile_off[COEB_MAXL + 1];
+    int item_off[COEB_MAXL + 1];   // wave items per level (prefix)
+    int nstrips[COEB_MAXL];        // 56-column strips
+    int bh[COEB_MAXL];             // rows per band (4 bands per item)
 };
 
-__global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, ExtractBufs b, BlurTiles bt)
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us2, v); }
+__device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ us2 pk2(int lo, int hi) { us2 r; r.x = (unsigned short)lo; r.y = (unsigned short)hi; return r; }
+
+__device__ __forceinline__ uint32_t dpp_shr1(uint32_t v)   // lane i <- lane i-1 (16-lane rows)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_shl1(uint32_t v)   // lane i <- lane i+1 (16-lane rows)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xf, 0xf, false);
+}
+
+__global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, ExtractBufs b, BlurWork bw)
 {
     const int f = blockIdx.y;
+    const int item = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (item >= bw.item_off[bw.L]) return;
     int l = 0;
-    while (l + 1 < bt.L && (int)blockIdx.x >= bt.tile_off[l + 1]) l++;
-    const int t = blockIdx.x - bt.tile_off[l];
-    const int tx = t % bt.tiles_x[l], ty = t / bt.tiles_x[l];
+    while (l + 1 < bw.L && item >= bw.item_off[l + 1]) l++;
+    const int it = item - bw.item_off[l];
+    const int strip = it % bw.nstrips[l], bq = it / bw.nstrips[l];
     const LevelGeom& g = P->lv[l];
     const int w = g.w, h = g.h, sp = g.pitch, dp = g.bpitch;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int x0 = tx * BT_W + lane * 4;
-    const int y0 = ty * BT_H + wv * BT_ROWS;
-    if (x0 >= w || y0 >= h) return;
-    const int rows = min(BT_ROWS, h - y0);
+    const int lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
+    const int bh = bw.bh[l];
+    const int y0 = (bq * 4 + grp) * bh;
+    const int y1 = min(h, y0 + bh);
+    const int x = strip * kBlurCols - 4 + gl * 4;
     const uint8_t* src = level_ptr(P, b, f, l);
     uint8_t* dst = b.blur + (int64_t)f * P->blur_stride + g.blur_off;
-    int k[7];
+    const bool produce = gl >= 1 && gl <= 14 && x < w && y0 < y1;
+    const bool edge = x < 0 || x + 3 >= w || (sp & 3) != 0;
+    int cx[4];
 #pragma unroll
-    for (int i = 0; i < 7; i++) k[i] = P->gauss[i];
-    const bool interior = (x0 >= 4) && (x0 + 8 <= w) && ((sp & 3) == 0);
-    uint32_t ring[7][4];
+    for (int q = 0; q < 4; q++) cx[q] = reflect101(min(x + q, w + 2), w);
+    const int k0 = P->gauss[0], k1 = P->gauss[1], k2 = P->gauss[2], k3 = P->gauss[3];
+    const us2 K0 = pk2(k0, k0), K1 = pk2(k1, k1), K2 = pk2(k2, k2), K3 = pk2(k3, k3);
+    // horizontal weights per (output column, source pair), DESIGN.md s4
+    const us2 W_l01_0 = pk2(0, k0), W_l23_0 = pk2(k1, k2), W_c01_0 = pk2(k3, k2), W_c23_0 = pk2(k1, k0);
+    const us2 W_l23_1 = pk2(k0, k1), W_c01_1 = pk2(k2, k3), W_c23_1 = pk2(k2, k1), W_r01_1 = pk2(k0, 0);
+    const us2 W_l23_2 = pk2(0, k0), W_c01_2 = pk2(k1, k2), W_c23_2 = pk2(k3, k2), W_r01_2 = pk2(k1, k0);
+    const us2 W_c01_3 = pk2(k0, k1), W_c23_3 = pk2(k2, k3), W_r01_3 = pk2(k2, k1), W_r23_3 = pk2(k0, 0);
+    const uint32_t rnd = 1u << 15;
+    const int n_iter = bh + 6;
+    const int hm = 2 * h - 2;
+    uint32_t R0[7], R1[7];
+    for (int i0 = 0; i0 < n_iter; i0 += 7) {
+        // issue the block's 7 row loads up front (latency hiding), then filter
+        uint32_t raw[7];
 #pragma unroll
-    for (int i = 0; i < 7; i++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) ring[i][q] = 0;
-    for (int r = y0 - 3; r < y0 + rows + 3; r++) {
-        const uint8_t* row = src + (int64_t)reflect101(r, h) * sp;
-        int px[12];
-        if (interior) {
-            const uint32_t* q = reinterpret_cast<const uint32_t*>(row + x0 - 4);
-            const uint32_t u0 = q[0], u1 = q[1], u2 = q[2];
-#pragma unroll
-            for (int i = 0; i < 12; i++) px[i] = byte_of(u0, u1, u2, i);
-        } else {
-#pragma unroll
-            for (int i = 1; i < 11; i++) px[i] = row[reflect101(x0 - 4 + i, w)];
-            px[0] = px[11] = 0;
-        }
-#pragma unroll
-        for (int i = 0; i < 6; i++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) ring[i][q] = ring[i + 1][q];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int tp = 0; tp < 7; tp++) acc += (uint32_t)k[tp] * (uint32_t)px[q + tp + 1];
-            ring[6][q] = acc;
-        }
-        const int y = r - 3;
-        if (y >= y0) {
-            uint32_t o[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                uint32_t acc = 0;
-#pragma unroll
-                for (int tp = 0; tp < 7; tp++) acc += (uint32_t)k[tp] * ring[tp][q];
-                const uint32_t v = (acc + (1u << 15)) >> 16;
-                o[q] = v > 255u ? 255u : v;
-            }
-            uint8_t* D = dst + (int64_t)y * dp + x0;
-            if (x0 + 4 <= w) {
-                *reinterpret_cast<uint32_t*>(D) = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
+        for (int ph = 0; ph < 7; ph++) {
+            // source row y0 - 3 + i, REFLECT_101 (|r| <= 3 outside the level), clamped for
+            // idle bands and for the rows past the end of the last block
+            const int r = y0 - 3 + i0 + ph;
+            int rr = r < 0 ? -r : r;
+            rr = min(rr, hm - rr);
+            rr = max(0, min(rr, h - 1));
+            const uint8_t* row = src + (int64_t)rr * sp;
+            if (!edge) {
+                raw[ph] = *reinterpret_cast<const uint32_t*>(row + x);
             } else {
-                for (int q = 0; q < w - x0; q++) D[q] = (uint8_t)o[q];
+                raw[ph] = (uint32_t)row[cx[0]] | ((uint32_t)row[cx[1]] << 8) | ((uint32_t)row[cx[2]] << 16) |
+                          ((uint32_t)row[cx[3]] << 24);
+            }
+        }
+#pragma unroll
+        for (int ph = 0; ph < 7; ph++) {
+            const int i = i0 + ph;
+            if (i >= n_iter) break;
+            const int r = y0 - 3 + i;
+            R0[ph] = __builtin_amdgcn_perm(0u, raw[ph], 0x0c010c00u);
+            R1[ph] = __builtin_amdgcn_perm(0u, raw[ph], 0x0c030c02u);
+            if (i < 6) continue;
+            // rows i-6 .. i are ring slots ph+1 .. ph (mod 7); centre = slot ph+4
+            const int s0 = (ph + 1) % 7, s1 = (ph + 2) % 7, s2 = (ph + 3) % 7, s3 = (ph + 4) % 7,
+                      s4 = (ph + 5) % 7, s5 = (ph + 6) % 7, s6 = ph;
+            const us2 v01 = K3 * as_us2(R0[s3]) + K2 * (as_us2(R0[s2]) + as_us2(R0[s4])) +
+                            K1 * (as_us2(R0[s1]) + as_us2(R0[s5])) + K0 * (as_us2(R0[s0]) + as_us2(R0[s6]));
+            const us2 v23 = K3 * as_us2(R1[s3]) + K2 * (as_us2(R1[s2]) + as_us2(R1[s4])) +
+                            K1 * (as_us2(R1[s1]) + as_us2(R1[s5])) + K0 * (as_us2(R1[s0]) + as_us2(R1[s6]));
+            const uint32_t V01 = as_u32(v01), V23 = as_u32(v23);
+            const us2 L01 = as_us2(dpp_shr1(V01)), L23 = as_us2(dpp_shr1(V23));
+            const us2 R01 = as_us2(dpp_shl1(V01)), R23 = as_us2(dpp_shl1(V23));
+            uint32_t a0 = __builtin_amdgcn_udot2(L01, W_l01_0, rnd, false);
+            a0 = __builtin_amdgcn_udot2(L23, W_l23_0, a0, false);
+            a0 = __builtin_amdgcn_udot2(v01, W_c01_0, a0, false);
+            a0 = __builtin_amdgcn_udot2(v23, W_c23_0, a0, false);
+            uint32_t a1 = __builtin_amdgcn_udot2(L23, W_l23_1, rnd, false);
+            a1 = __builtin_amdgcn_udot2(v01, W_c01_1, a1, false);
+            a1 = __builtin_amdgcn_udot2(v23, W_c23_1, a1, false);
+            a1 = __builtin_amdgcn_udot2(R01, W_r01_1, a1, false);
+            uint32_t a2 = __builtin_amdgcn_udot2(L23, W_l23_2, rnd, false);
+            a2 = __builtin_amdgcn_udot2(v01, W_c01_2, a2, false);
+            a2 = __builtin_amdgcn_udot2(v23, W_c23_2, a2, false);
+            a2 = __builtin_amdgcn_udot2(R01, W_r01_2, a2, false);
+            uint32_t a3 = __builtin_amdgcn_udot2(v01, W_c01_3, rnd, false);
+            a3 = __builtin_amdgcn_udot2(v23, W_c23_3, a3, false);
+            a3 = __builtin_amdgcn_udot2(R01, W_r01_3, a3, false);
+            a3 = __builtin_amdgcn_udot2(R23, W_r23_3, a3, false);
+            const int y = r - 3;
+            if (produce && y < y1) {
+                // byte 2 of each accumulator = (acc + 2^15) >> 16 (acc + 2^15 < 2^24)
+                const uint32_t p01 = __builtin_amdgcn_perm(a1, a0, 0x0c0c0602u);
+                const uint32_t p23 = __builtin_amdgcn_perm(a3, a2, 0x06020c0cu);
+                *reinterpret_cast<uint32_t*>(dst + (int64_t)y * dp + x) = p01 | p23;
             }
         }
     }
@@ -1186,17 +1236,20 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
                            b.rtab + g.rtab_off, g.xmax);
         prof_end(prof, s);
     }
-    BlurTiles bt;
-    bt.L = plan.L;
-    int tiles = 0;
+    BlurWork bw;
+    bw.L = plan.L;
+    int items = 0;
     for (int l = 0; l < plan.L; l++) {
-        bt.tiles_x[l] = (plan.lv[l].w + BT_W - 1) / BT_W;
-        bt.tile_off[l] = tiles;
-        tiles += bt.tiles_x[l] * ((plan.lv[l].h + BT_H - 1) / BT_H);
+        const LevelGeom& g = plan.lv[l];
+        bw.nstrips[l] = (g.w + kBlurCols - 1) / kBlurCols;
+        const int nbands = 4 * ((g.h + 63) / 64);
+        bw.bh[l] = (g.h + nbands - 1) / nbands;
+        bw.item_off[l] = items;
+        items += bw.nstrips[l] * (nbands / 4);
     }
-    bt.tile_off[plan.L] = tiles;
+    bw.item_off[plan.L] = items;
     prof_begin(prof, "k_blur", s);
-    hipLaunchKernelGGL(k_blur, dim3(tiles, F), dim3(kThreads), 0, s, d_plan, b, bt);
+    hipLaunchKernelGGL(k_blur, dim3((items + kWaves - 1) / kWaves, F), dim3(kThreads), 0, s, d_plan, b, bw);
     prof_end(prof, s);
     prof_begin(prof, "k_fast", s);
     const int fast_lds = kWaves * (2 * kFastRowBytes * plan.max_roi_h + 2 * (kFastSurv + kFastCorners));
