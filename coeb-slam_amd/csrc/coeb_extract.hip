@@ -421,8 +421,9 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
 //  4. NMS over the corner list at iniThFAST (fallback minThFAST if the cell came out empty,
 //     :834-838) with ordered (ballot) stores of the kept keys.  A cell with more corners than
 //     the list holds walks the whole window instead.
-constexpr int kFastRowBytes = 72;          // >= 3 + 64 + 3 rounded to a word multiple
-constexpr int kFastSurv = 128;             // survivor list (flushed when nearly full)
+constexpr int kRoiMax = 64;                // FAST cell ROI limit (make_plan)
+constexpr int kFastRowBytes = 72;          // >= 1 + 64 + 7 (slab byte = ROI column + 1)
+constexpr int kFastSurv = 512;             // survivor list (flushed when one more pass could overflow it)
 constexpr int kFastCorners = 512;          // corner list
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -444,6 +445,59 @@ __device__ __forceinline__ bool fast_pretest(const uint8_t* c, int st, int t)
     d &= cls(c[3]) | cls(c[-3]);                               // p4 | p12
     d &= cls(c[-2 * st + 2]) | cls(c[2 * st - 2]);             // p6 | p14
     return d != 0;
+}
+
+// The same pre-test for 4 adjacent detection pixels at once (one lane): c points at the first
+// of them, 4-byte aligned in the slab.  Ring bytes are gathered by v_perm straight into
+// packed u16 pairs; per pair, with d = min/max of the opposite ring pixels,
+//   dark  survives <=> max over pairs of min(a, b) <  v - t   (some of each pair darker)
+//   bright survives <=> min over pairs of max(a, b) >  v + t
+// Returns a 4-bit survivor mask (bit q = pixel q).
+__device__ __forceinline__ uint32_t win_lo(uint32_t a, uint32_t b, int s)   // bytes s, s+1 of a:b as u16 pair
+{
+    return __builtin_amdgcn_perm(b, a, 0x0c000c00u | (uint32_t)s | ((uint32_t)(s + 1) << 16));
+}
+__device__ __forceinline__ uint32_t win_hi(uint32_t a, uint32_t b, int s)   // bytes s+2, s+3
+{
+    return __builtin_amdgcn_perm(b, a, 0x0c000c00u | (uint32_t)(s + 2) | ((uint32_t)(s + 3) << 16));
+}
+
+__device__ __forceinline__ us2 pk_min(us2 a, us2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ us2 pk_max(us2 a, us2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ us2 pk_subs(us2 a, us2 b) { return __builtin_elementwise_sub_sat(a, b); }
+
+__device__ __forceinline__ uint32_t pretest_half(us2 v, us2 p0, us2 p8, us2 p2, us2 p10, us2 p4, us2 p12, us2 p6,
+                                                 us2 p14, us2 T)
+{
+    const us2 lo = pk_subs(v, T), hi = v + T;
+    const us2 md = pk_max(pk_max(pk_min(p0, p8), pk_min(p2, p10)), pk_max(pk_min(p4, p12), pk_min(p6, p14)));
+    const us2 mb = pk_min(pk_min(pk_max(p0, p8), pk_max(p2, p10)), pk_min(pk_max(p4, p12), pk_max(p6, p14)));
+    return as_u32(pk_subs(lo, md)) | as_u32(pk_subs(mb, hi));
+}
+
+__device__ __forceinline__ uint32_t fast_pretest4(const uint8_t* c, int t)
+{
+    constexpr int st = kFastRowBytes;
+    const uint32_t* r0 = reinterpret_cast<const uint32_t*>(c);
+    const uint32_t* rp2 = reinterpret_cast<const uint32_t*>(c + 2 * st);
+    const uint32_t* rm2 = reinterpret_cast<const uint32_t*>(c - 2 * st);
+    const uint32_t a0 = r0[-1], b0 = r0[0], c0 = r0[1];
+    const uint32_t ap = rp2[-1], bp = rp2[0], cp = rp2[1];
+    const uint32_t am = rm2[-1], bm = rm2[0], cm = rm2[1];
+    const uint32_t u3 = *reinterpret_cast<const uint32_t*>(c + 3 * st);
+    const uint32_t d3 = *reinterpret_cast<const uint32_t*>(c - 3 * st);
+    const us2 T = pk2(t, t);
+    // low pair = pixels 0,1; high pair = pixels 2,3
+    const uint32_t sl = __builtin_amdgcn_perm(0u, b0, 0x0c010c00u), sh2 = __builtin_amdgcn_perm(0u, b0, 0x0c030c02u);
+    const uint32_t lo = pretest_half(
+        as_us2(sl), as_us2(__builtin_amdgcn_perm(0u, u3, 0x0c010c00u)), as_us2(__builtin_amdgcn_perm(0u, d3, 0x0c010c00u)),
+        as_us2(win_lo(bp, cp, 2)), as_us2(win_lo(am, bm, 2)), as_us2(win_lo(b0, c0, 3)), as_us2(win_lo(a0, b0, 1)),
+        as_us2(win_lo(bm, cm, 2)), as_us2(win_lo(ap, bp, 2)), T);
+    const uint32_t hi = pretest_half(
+        as_us2(sh2), as_us2(__builtin_amdgcn_perm(0u, u3, 0x0c030c02u)), as_us2(__builtin_amdgcn_perm(0u, d3, 0x0c030c02u)),
+        as_us2(win_hi(bp, cp, 2)), as_us2(win_hi(am, bm, 2)), as_us2(win_hi(b0, c0, 3)), as_us2(win_hi(a0, b0, 1)),
+        as_us2(win_hi(bm, cm, 2)), as_us2(win_hi(ap, bp, 2)), T);
+    return ((lo & 0xffffu) ? 1u : 0u) | ((lo >> 16) ? 2u : 0u) | ((hi & 0xffffu) ? 4u : 0u) | ((hi >> 16) ? 8u : 0u);
 }
 
 __device__ __forceinline__ int nms_keep(const uint8_t* Ms, int o, int t, int* sc_out)
@@ -484,40 +538,76 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
     uint8_t* Ms = wbase + slab;
     uint16_t* surv = reinterpret_cast<uint16_t*>(wbase + 2 * slab);
     uint16_t* corn = surv + kFastSurv;
-    const int sh = c.x0 & 3;
+    // slab byte = ROI column + 1, so detection column 0 (ROI column 3) is 4-byte aligned
+    constexpr int sh = 1;
     const int nwords = (sh + rw + 3) >> 2;
-    if ((g.pitch & 3) == 0) {
-        const uint8_t* base = img + (int64_t)c.y0 * g.pitch + (c.x0 & ~3);
-        for (int i = lane; i < nwords * rh; i += 64) {
-            const int yy = i / nwords, k = i - yy * nwords;
-            *reinterpret_cast<uint32_t*>(roi + yy * kFastRowBytes + 4 * k) =
-                *reinterpret_cast<const uint32_t*>(base + (int64_t)yy * g.pitch + 4 * k);
+    if ((g.pitch & 3) == 0 && nwords <= 16) {
+        // slab word k holds ROI columns 4k-1 .. 4k+2: an unaligned global word (x0 >= 16).
+        // All loads are issued before the first LDS store (one latency, not one per row);
+        // rows past the ROI are clamped loads whose stores are skipped.
+        const int gx = c.x0 - 1;
+        const int al = gx & 3;
+        const int k = min(lane & 15, nwords - 1);
+        const uint32_t* base = reinterpret_cast<const uint32_t*>(img + (int64_t)c.y0 * g.pitch + (gx & ~3)) + k;
+        const int pw = g.pitch >> 2;
+        uint32_t q0[kRoiMax / 4], q1[kRoiMax / 4];
+#pragma unroll
+        for (int i = 0; i < kRoiMax / 4; i++) {
+            const int yy = min((lane >> 4) + 4 * i, rh - 1);
+            q0[i] = base[yy * pw];
+            q1[i] = base[yy * pw + 1];
         }
+#pragma unroll
+        for (int i = 0; i < kRoiMax / 4; i++) {
+            const int yy = (lane >> 4) + 4 * i;
+            if (yy < rh && (lane & 15) < nwords)
+                *reinterpret_cast<uint32_t*>(roi + yy * kFastRowBytes + 4 * (lane & 15)) =
+                    __builtin_amdgcn_alignbyte(q1[i], q0[i], (uint32_t)al);
+        }
+    } else if ((g.pitch & 3) == 0) {
+        const int gx = c.x0 - 1;
+        const int al = gx & 3;
+        const uint8_t* base = img + (int64_t)c.y0 * g.pitch + (gx & ~3);
+        for (int yy = lane >> 4; yy < rh; yy += 4)
+            for (int k = lane & 15; k < nwords; k += 16) {
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(base + (int64_t)yy * g.pitch) + k;
+                *reinterpret_cast<uint32_t*>(roi + yy * kFastRowBytes + 4 * k) =
+                    __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)al);
+            }
     } else {
-        for (int i = lane; i < rw * rh; i += 64) {
-            const int yy = i / rw, xx = i - yy * rw;
-            roi[yy * kFastRowBytes + sh + xx] = img[(int64_t)(c.y0 + yy) * g.pitch + c.x0 + xx];
-        }
+        for (int yy = lane >> 4; yy < rh; yy += 4)
+            for (int xx = lane & 15; xx < rw; xx += 16)
+                roi[yy * kFastRowBytes + sh + xx] = img[(int64_t)(c.y0 + yy) * g.pitch + c.x0 + xx];
     }
     for (int i = lane; i < kFastRowBytes * rh / 4; i += 64) reinterpret_cast<uint32_t*>(Ms)[i] = 0u;
     wave_sync_lds();
     const int ww = rw - 6, wh = rh - 6;
     const int npix = ww > 0 && wh > 0 ? ww * wh : 0;
     const uint64_t lt = lanemask_lt();
-    // ---- 2 + 3: pre-test, survivors -> exact strength -> corners (row-major throughout)
+    // ---- 2 + 3: pre-test 4 pixels per lane (8 or 16 lanes per row), survivors in row-major
+    //      order -> exact strength -> corners
     int ns = 0, nc = 0;
-    int row0 = 0, col0 = 0;
-    for (int base = 0; base < npix; base += 64) {
-        int col = col0 + lane, row = row0;
-        while (col >= ww) { col -= ww; row++; }
-        const int o = (row + 3) * kFastRowBytes + sh + col + 3;
-        const bool sv = base + lane < npix && fast_pretest(&roi[o], kFastRowBytes, th_min);
-        const uint64_t m = __ballot(sv);
-        if (sv) surv[ns + __popcll(m & lt)] = (uint16_t)o;
-        ns += __popcll(m);
-        col0 += 64;
-        while (col0 >= ww) { col0 -= ww; row0++; }
-        if (ns > kFastSurv - 64 || base + 64 >= npix) {
+    const int ngrp = (ww + 3) >> 2;
+    const int lpr_log = ngrp > 8 ? 4 : 3;
+    const int cg = lane & ((1 << lpr_log) - 1), rsub = lane >> lpr_log;
+    const int rpi = 64 >> lpr_log;
+    for (int r0 = 0; npix > 0 && r0 < wh; r0 += rpi) {
+        const int row = r0 + rsub;
+        const int o = (row + 3) * kFastRowBytes + 4 + 4 * cg;
+        uint32_t sm = 0;
+        if (row < wh && cg < ngrp) {
+            sm = fast_pretest4(&roi[o], th_min);
+            const int left = ww - 4 * cg;            // pixels of this group inside the window
+            if (left < 4) sm &= (1u << left) - 1u;
+        }
+        const uint64_t m0 = __ballot(sm & 1u), m1 = __ballot(sm & 2u), m2 = __ballot(sm & 4u), m3 = __ballot(sm & 8u);
+        int q = ns + __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
+        if (sm & 1u) surv[q++] = (uint16_t)o;
+        if (sm & 2u) surv[q++] = (uint16_t)(o + 1);
+        if (sm & 4u) surv[q++] = (uint16_t)(o + 2);
+        if (sm & 8u) surv[q++] = (uint16_t)(o + 3);
+        ns += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+        if (ns > kFastSurv - 256 || r0 + rpi >= wh) {
             wave_sync_lds();
             for (int e0 = 0; e0 < ns; e0 += 64) {
                 const int e = e0 + lane;
@@ -530,8 +620,8 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
                 if (isc) Ms[oo] = (uint8_t)M;
                 const uint64_t mc = __ballot(isc);
                 if (isc) {
-                    const int q = nc + __popcll(mc & lt);
-                    if (q < kFastCorners) corn[q] = (uint16_t)oo;
+                    const int qq = nc + __popcll(mc & lt);
+                    if (qq < kFastCorners) corn[qq] = (uint16_t)oo;
                 }
                 nc += __popcll(mc);
             }
@@ -563,12 +653,11 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
                 running += __popcll(m);
             }
         } else {
-            row0 = 0;
-            col0 = 0;
+            int row0 = 0, col0 = 0;
             for (int base = 0; base < npix; base += 64) {
                 int col = col0 + lane, row = row0;
                 while (col >= ww) { col -= ww; row++; }
-                const int o = (row + 3) * kFastRowBytes + sh + col + 3;
+                const int o = (row + 3) * kFastRowBytes + sh + col + 3;   // == + 4 + col
                 int sc = 0, kept = 0;
                 if (base + lane < npix) kept = nms_keep(Ms, o, t, &sc);
                 const uint64_t m = __ballot(kept);
@@ -1169,13 +1258,24 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         const bool uv = (lane & 31) < 31;
         int m10 = 0, m01 = 0;
         if (h == 0 && uv) m10 += u * center[u];
+        // rows 1..8 (h = 0) or 9..15 (h = 1); fully unrolled so the 16 row loads of a lane
+        // are in flight together (keypoints are >= 19 px from the level edge: rows +-16 and
+        // column +16 stay inside the level)
         const int v0 = h == 0 ? 1 : 9, v1 = h == 0 ? 8 : 15;
-        for (int v = v0; v <= v1; v++) {
-            const int d = P->umax[v];
-            if (uv && u >= -d && u <= d) {
-                const int vp = center[u + v * st], vm = center[u - v * st];
-                m01 += v * (vp - vm);
-                m10 += u * (vp + vm);
+        int vps[8], vms[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int v = v0 + j;
+            vps[j] = center[u + v * st];
+            vms[j] = center[u - v * st];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int v = v0 + j;
+            const int d = P->umax[min(v, 15)];
+            if (uv && v <= v1 && u >= -d && u <= d) {
+                m01 += v * (vps[j] - vms[j]);
+                m10 += u * (vps[j] + vms[j]);
             }
         }
         m10 = wave_sum(m10);
@@ -1187,11 +1287,12 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         sincos_canon(angle * factorPI, &bs, &ac);
         const uint8_t* bl = b.blur + (int64_t)f * P->blur_stride + g.blur_off + (int64_t)y * bst + x;
         int nib = 0;
+        const int4 pat = reinterpret_cast<const int4*>(b.pattern)[lane];   // 4 tests x (x0,y0,x1,y1) int8
 #pragma unroll
         for (int t = 0; t < 4; t++) {
-            const int test = 4 * lane + t;
-            const float px0 = (float)b.pattern[4 * test + 0], py0 = (float)b.pattern[4 * test + 1];
-            const float px1 = (float)b.pattern[4 * test + 2], py1 = (float)b.pattern[4 * test + 3];
+            const int pw = t == 0 ? pat.x : t == 1 ? pat.y : t == 2 ? pat.z : pat.w;
+            const float px0 = (float)(int8_t)(pw & 0xff), py0 = (float)(int8_t)((pw >> 8) & 0xff);
+            const float px1 = (float)(int8_t)((pw >> 16) & 0xff), py1 = (float)(int8_t)(pw >> 24);
             const int r0 = (int)rintf(__builtin_fmaf(px0, bs, py0 * ac));
             const int c0 = (int)rintf(__builtin_fmaf(px0, ac, -(py0 * bs)));
             const int r1 = (int)rintf(__builtin_fmaf(px1, bs, py1 * ac));
