@@ -145,13 +145,14 @@ __device__ __forceinline__ int byte_of(uint32_t w0, uint32_t w1, uint32_t w2, in
     return (int)((w >> ((o & 3) * 8)) & 0xFFu);
 }
 
+// VResizeLinearVec_32s8u: ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2.
+// Coefficients are in [0, 2048] and h <= 255 * 2048, so h >> 4 <= 32640 (the 16-bit
+// saturations of the SIMD code never trigger) and every product fits 26 bits: full-rate
+// 24-bit multiplies instead of the quarter-rate v_mul_lo_u32.
 __device__ __forceinline__ int vresize(int h0, int h1, int b0, int b1)
 {
-    const int v0 = min(h0 >> 4, 32767), v1 = min(h1 >> 4, 32767);
-    const int m0 = (v0 * b0) >> 16, m1 = (v1 * b1) >> 16;       // _mm_mulhi_epi16
-    int s = max(min(m0 + m1, 32767), -32768);                    // _mm_adds_epi16
-    s = max(min(s + 2, 32767), -32768) >> 2;                     // rounding shift, pack
-    return max(0, min(s, 255));
+    const int m0 = __mul24(h0 >> 4, b0) >> 16, m1 = __mul24(h1 >> 4, b1) >> 16;
+    return max(0, min((m0 + m1 + 2) >> 2, 255));
 }
 
 // Output tile 128 x 32 per workgroup; the source rows/columns it touches (<= 32*scale+2 rows,
@@ -175,7 +176,22 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
     const int sy0 = max(yofs[oy], 0), sy1 = min(max(yofs[ey] + 1, 0), sh - 1);
     const int nwords = (sx1 - sx0) / 4 + 1, nrows = sy1 - sy0 + 1;
     const uint8_t* S = src + (int64_t)f * src_fs;
-    if ((sp & 3) == 0) {
+    if ((sp & 3) == 0 && nwords <= 64) {
+        // wave w stages rows w, w+4, ...; lane = source word.  All loads of a thread are
+        // issued before its first LDS store (clamped rows / words, stores guarded).
+        constexpr int kPass = PT_SH / kWaves;
+        const int wv = threadIdx.x >> 6, k = threadIdx.x & 63;
+        const uint32_t* base = reinterpret_cast<const uint32_t*>(S + (int64_t)sy0 * sp + sx0) + min(k, nwords - 1);
+        const int pw = sp >> 2;
+        uint32_t q[kPass];
+#pragma unroll
+        for (int i = 0; i < kPass; i++) q[i] = base[min(wv + kWaves * i, nrows - 1) * pw];
+#pragma unroll
+        for (int i = 0; i < kPass; i++) {
+            const int r = wv + kWaves * i;
+            if (r < nrows && k < nwords) *reinterpret_cast<uint32_t*>(s_src + r * PT_SW + 4 * k) = q[i];
+        }
+    } else if ((sp & 3) == 0) {
         for (int i = threadIdx.x; i < nwords * nrows; i += kThreads) {
             const int r = i / nwords, k = i - r * nwords;
             *reinterpret_cast<uint32_t*>(s_src + r * PT_SW + 4 * k) =
@@ -217,8 +233,8 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
         uint32_t word = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const int h0 = R0[lx[k]] * a0[k] + R0[lx[k] + 1] * a1[k];
-            const int h1 = R1[lx[k]] * a0[k] + R1[lx[k] + 1] * a1[k];
+            const int h0 = __mul24((int)R0[lx[k]], a0[k]) + __mul24((int)R0[lx[k] + 1], a1[k]);
+            const int h1 = __mul24((int)R1[lx[k]], a0[k]) + __mul24((int)R1[lx[k] + 1], a1[k]);
             word |= (uint32_t)vresize(h0, h1, b0, b1) << (8 * k);
         }
         uint8_t* D = dst + (int64_t)f * dst_fs + (int64_t)dy * dp + cx;
