@@ -713,6 +713,7 @@ struct OctLds {
     int* work; int4* cnt; int* base; int* rank; int* push; uint8_t* dead;
     NodeRef set[2];
     uint32_t* keys[2];
+    size_t set_stride;     // bytes between set[0] and set[1] fields
 };
 
 __device__ __forceinline__ OctLds oct_lds(uint8_t* smem, int W, int KL)
@@ -731,10 +732,24 @@ __device__ __forceinline__ OctLds oct_lds(uint8_t* smem, int W, int KL)
         o.set[s].alloc = reinterpret_cast<int*>(smem + off); off += (size_t)W * 4;
         o.set[s].buf = reinterpret_cast<int*>(smem + off); off += (size_t)W * 4;
     }
+    o.set_stride = (size_t)W * 32;
     o.keys[0] = reinterpret_cast<uint32_t*>(smem + off); off += (size_t)KL * 4;
     o.keys[1] = reinterpret_cast<uint32_t*>(smem + off); off += (size_t)KL * 4;
     o.dead = smem + off;
     return o;
+}
+
+// set[s] without a dynamically indexed local array (which the compiler puts in scratch)
+__device__ __forceinline__ NodeRef nref(const OctLds& O, int s)
+{
+    NodeRef r = O.set[0];
+    const size_t d = s ? O.set_stride : 0;
+    r.rect = reinterpret_cast<int4*>(reinterpret_cast<uint8_t*>(r.rect) + d);
+    r.start = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(r.start) + d);
+    r.cnt = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(r.cnt) + d);
+    r.alloc = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(r.alloc) + d);
+    r.buf = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(r.buf) + d);
+    return r;
 }
 
 __device__ __forceinline__ int quadrant(uint32_t k, int sx, int sy)
@@ -810,7 +825,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     const int l = blockIdx.x, f = blockIdx.y;
     const LevelGeom& g = P->lv[l];
     const int tid = threadIdx.x, wv = tid >> 6, lane = lane_id();
-    const DynMask dm = b.dyn[f];
+    const DynMask& dm = b.dyn[f];      // by reference: a local copy is indexed dynamically (scratch)
     const int area = dm.area_flag;
     const int N = area ? g.nfeat_area : g.nfeat;
     // ---- 1. gather candidates in reference order ----
@@ -825,14 +840,16 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
         K = tot;
     }
     // keys in LDS when they fit, else in the level's global ping-pong buffers (L2-resident)
-    uint32_t* KB[2];
+    uint32_t* KB0;
+    int64_t kdelta;
     if (K <= P->oct_kl) {
-        KB[0] = O.keys[0];
-        KB[1] = O.keys[1];
+        KB0 = O.keys[0];
+        kdelta = O.keys[1] - O.keys[0];
     } else {
-        KB[0] = b.keys + (int64_t)f * 2 * P->kbuf_stride + g.kcap_off;
-        KB[1] = KB[0] + P->kbuf_stride;
+        KB0 = b.keys + (int64_t)f * 2 * P->kbuf_stride + g.kcap_off;
+        kdelta = P->kbuf_stride;
     }
+    auto KB = [&](int i) -> uint32_t* { return KB0 + (i ? kdelta : 0); };
     {
         int carry = 0;
         for (int base = 0; base < g.ncells; base += kThreads) {
@@ -843,7 +860,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
             // copy: each thread copies its own cell (cells are small)
             if (ci < g.ncells) {
                 const uint32_t* src = cand + (int64_t)ci * P->cell_cap;
-                uint32_t* dst = KB[0] + carry + pre;
+                uint32_t* dst = KB(0) + carry + pre;
                 for (int q = 0; q < v; q++) dst[q] = src[q];
             }
             carry += tot;
@@ -861,12 +878,12 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
             uint32_t k = 0;
             bool keep = false;
             if (i < K) {
-                k = KB[0][i];
+                k = KB(0)[i];
                 keep = !masked_out(dm, (float)key_x(k), (float)key_y(k), scale, P->W, P->H);
             }
             int tot;
             const int pre = block_scan_flag(keep, &tot, sbuf);
-            if (keep) KB[1][carry + pre] = k;
+            if (keep) KB(1)[carry + pre] = k;
             carry += tot;
         }
         K = carry;
@@ -897,12 +914,12 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
                     uint32_t k = 0;
                     bool in = false;
                     if (idx < K) {
-                        k = KB[kb][idx];
+                        k = KB(kb)[idx];
                         in = key_x(k) >= lo && key_x(k) < hi;
                     }
                     int tot;
                     const int pre = block_scan_flag(in, &tot, sbuf);
-                    if (in) KB[kb ^ 1][carry + pre] = k;
+                    if (in) KB(kb ^ 1)[carry + pre] = k;
                     carry += tot;
                 }
                 if (carry > start) {
@@ -923,7 +940,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     while (!finish) {
         const int prevSize = n;
         if (n > OCT_LMAX || n > g.ncap) { if (tid == 0) atomicOr(b.err, 4); finish = true; break; }
-        NodeRef S = O.set[cs], D = O.set[cs ^ 1];
+        NodeRef S = nref(O, cs), D = nref(O, cs ^ 1);
         // divided nodes = cnt > 1, in list order
         int nd = 0;
         for (int base = 0; base < n; base += kThreads) {
@@ -942,8 +959,8 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
             const int4 r = S.rect[k];
             int4 tmp; int sx, sy;
             child_rect(r, 0, &tmp, &sx, &sy);
-            const int4 qc = wave_count_quadrants(KB[bf], s, c, sx, sy);
-            wave_scatter_quadrants(KB[bf], KB[bf ^ 1], s, c, sx, sy, qc);
+            const int4 qc = wave_count_quadrants(KB(bf), s, c, sx, sy);
+            wave_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
             if (lane == 0) s_cnt[j] = qc;
         }
         __syncthreads();
@@ -1016,7 +1033,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     while (final_phase && !finish) {
         const int prevSize = n;
         if (n > OCT_LMAX) { if (tid == 0) atomicOr(b.err, 4); break; }
-        NodeRef S = O.set[cs], D = O.set[cs ^ 1];
+        NodeRef S = nref(O, cs), D = nref(O, cs ^ 1);
         // vPrev = list nodes with cnt > 1, i.e. vSizeAndPointerToNode of the previous round
         int m = 0;
         for (int base = 0; base < n; base += kThreads) {
@@ -1034,7 +1051,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
             const int k = s_work[j];
             int4 tmp; int sx, sy;
             child_rect(S.rect[k], 0, &tmp, &sx, &sy);
-            const int4 qc = wave_count_quadrants(KB[S.buf[k]], S.start[k], S.cnt[k], sx, sy);
+            const int4 qc = wave_count_quadrants(KB(S.buf[k]), S.start[k], S.cnt[k], sx, sy);
             if (lane == 0) s_cnt[j] = qc;
         }
         // sort(vPrev) by (size, node) ascending and walk from the back: rank 0 = largest size,
@@ -1106,7 +1123,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
             int4 tmp; int sx, sy;
             child_rect(pr, 0, &tmp, &sx, &sy);
             const int4 qc = s_cnt[j];
-            wave_scatter_quadrants(KB[bf], KB[bf ^ 1], s, c, sx, sy, qc);
+            wave_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
             if (lane == 0) {
                 int a = s_push[r];
                 int off = s;
@@ -1148,7 +1165,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     }
 
     // ---- 4. retain the best response per node (:747-766), border, final cull ----
-    NodeRef S = O.set[cs];
+    NodeRef S = nref(O, cs);
     uint32_t* out = b.lvl_kp + (int64_t)f * P->lvl_stride + g.out_off;
     const bool cull = !area && l < 8;                  // CheckMovingKeyPoints_finall loops 8 levels
     const float scale = (l != 0) ? g.scale : 1.0f;
@@ -1158,7 +1175,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
         uint32_t best = 0;
         bool keep = false;
         if (k < n) {
-            const uint32_t* src = KB[S.buf[k]] + S.start[k];
+            const uint32_t* src = KB(S.buf[k]) + S.start[k];
             const int c = S.cnt[k];
             best = src[0];
             int maxr = key_s(best);
