@@ -20,7 +20,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libcoeb_front.so")
+# COEB_LIB_PATH: an alternative build of the same library (kernel experiments); never a fallback
+LIB_PATH = os.environ.get("COEB_LIB_PATH") or os.path.join(os.path.dirname(HERE), "lib", "libcoeb_front.so")
 
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])

@@ -407,22 +407,22 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
     int p[16];
     ring16(c, st, p);
     const int v = c[0];
-    int d[16], m[16], n[16];
+    int d[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) d[k] = v - p[k];
+    // 9-arc minima (dark) and maxima (bright) from 3-arcs: arc9(k) = arc3(k), arc3(k+3), arc3(k+6)
+    int t[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) { m[k] = min(d[k], d[(k + 1) & 15]); n[k] = max(d[k], d[(k + 1) & 15]); }
-    int m4[16], n4[16];
+    for (int k = 0; k < 16; k++) t[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+    int A = -1000;
 #pragma unroll
-    for (int k = 0; k < 16; k++) { m4[k] = min(m[k], m[(k + 2) & 15]); n4[k] = max(n[k], n[(k + 2) & 15]); }
-    int A = -1000, B = -1000;
+    for (int k = 0; k < 16; k++) A = max(A, min(min(t[k], t[(k + 3) & 15]), t[(k + 6) & 15]));
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int m8 = min(m4[k], m4[(k + 4) & 15]), n8 = max(n4[k], n4[(k + 4) & 15]);
-        A = max(A, min(m8, d[(k + 8) & 15]));
-        B = max(B, -max(n8, d[(k + 8) & 15]));
-    }
-    return max(A, B);
+    for (int k = 0; k < 16; k++) t[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+    int Bm = 1000;
+#pragma unroll
+    for (int k = 0; k < 16; k++) Bm = min(Bm, max(max(t[k], t[(k + 3) & 15]), t[(k + 6) & 15]));
+    return max(A, -Bm);
 }
 
 // One wave per cell, four cells per workgroup, no workgroup barriers.
@@ -535,71 +535,97 @@ __device__ __forceinline__ int nms_keep(const uint8_t* Ms, int o, int t, int* sc
     return kept ? 1 : 0;
 }
 
-__global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, ExtractBufs b)
+// Count of set bits of a wave mask below this lane (v_mbcnt_lo/hi).
+__device__ __forceinline__ int mbcnt(uint64_t m)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int wv = threadIdx.x >> 6, lane = lane_id();
-    const int slab = kFastRowBytes * P->max_roi_h;          // per-wave LDS: roi, M, lists
-    uint8_t* wbase = smem + (size_t)wv * (2 * slab + 2 * (kFastSurv + kFastCorners));
-    const int cidx = blockIdx.x * kWaves + wv, f = blockIdx.y;
-    if (cidx >= P->ncells) return;
-    const CellDesc c = b.cells[cidx];
-    const int l = c.level;
-    const LevelGeom& g = P->lv[l];
-    const int area = b.dyn[f].area_flag;
-    const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
-    const uint8_t* img = level_ptr(P, b, f, l);
-    const int rw = c.rw, rh = c.rh;
-    uint8_t* roi = wbase;
-    uint8_t* Ms = wbase + slab;
-    uint16_t* surv = reinterpret_cast<uint16_t*>(wbase + 2 * slab);
-    uint16_t* corn = surv + kFastSurv;
-    // slab byte = ROI column + 1, so detection column 0 (ROI column 3) is 4-byte aligned
-    constexpr int sh = 1;
-    const int nwords = (sh + rw + 3) >> 2;
-    if ((g.pitch & 3) == 0 && nwords <= 16) {
-        // slab word k holds ROI columns 4k-1 .. 4k+2: an unaligned global word (x0 >= 16).
-        // All loads are issued before the first LDS store (one latency, not one per row);
-        // rows past the ROI are clamped loads whose stores are skipped.
-        const int gx = c.x0 - 1;
-        const int al = gx & 3;
-        const int k = min(lane & 15, nwords - 1);
-        const uint32_t* base = reinterpret_cast<const uint32_t*>(img + (int64_t)c.y0 * g.pitch + (gx & ~3)) + k;
-        const int pw = g.pitch >> 2;
-        uint32_t q0[kRoiMax / 4], q1[kRoiMax / 4];
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+constexpr int kFastCellsPerWave = 2;
+constexpr int kFastPass = 12;            // prefetched ROI rows / 4 (cells up to 48 rows)
+
+// Staging of a cell ROI into the wave's slab (slab byte = ROI column + 1, so detection
+// column 0 = ROI column 3 is 4-byte aligned).  The word path keeps the loads in registers
+// (q0) so the next cell's loads can be issued before the current cell is processed.
+struct FastCellGeom {
+    const uint8_t* img;
+    int pitch, x0, y0, rw, rh, nwords;
+    bool words;                        // pitch % 4 == 0 and the row fits 15 words
+};
+
+__device__ __forceinline__ FastCellGeom fast_geom(const Plan* P, const ExtractBufs& b, int f, const CellDesc& c)
+{
+    FastCellGeom G;
+    const LevelGeom& g = P->lv[c.level];
+    G.img = level_ptr(P, b, f, c.level);
+    G.pitch = g.pitch;
+    G.x0 = c.x0; G.y0 = c.y0; G.rw = c.rw; G.rh = c.rh;
+    G.nwords = (1 + c.rw + 3) >> 2;
+    G.words = (g.pitch & 3) == 0 && G.nwords <= 15 && c.rh <= 4 * kFastPass;
+    return G;
+}
+
+__device__ __forceinline__ void fast_prefetch(const FastCellGeom& G, uint32_t q0[kFastPass])
+{
+    if (!G.words) return;
+    const int lane = lane_id();
+    const int gx = G.x0 - 1;
+    const int k = min(lane & 15, G.nwords);
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(G.img + (int64_t)G.y0 * G.pitch + (gx & ~3)) + k;
+    const int pw = G.pitch >> 2;
+    const int npass = (G.rh + 3) >> 2;
 #pragma unroll
-        for (int i = 0; i < kRoiMax / 4; i++) {
-            const int yy = min((lane >> 4) + 4 * i, rh - 1);
-            q0[i] = base[yy * pw];
-            q1[i] = base[yy * pw + 1];
-        }
+    for (int i = 0; i < kFastPass; i++)
+        if (i < npass) q0[i] = base[min((lane >> 4) + 4 * i, G.rh - 1) * pw];
+}
+
+__device__ __forceinline__ void fast_stage(const FastCellGeom& G, const uint32_t q0[kFastPass], uint8_t* roi)
+{
+    const int lane = lane_id();
+    if (G.words) {
+        // word k of slab row = ROI columns 4k-1 .. 4k+2 = this lane's aligned word joined
+        // with the next lane's (DPP row shift; one slab row = one 16-lane DPP row)
+        const int al = (G.x0 - 1) & 3;
+        const int npass = (G.rh + 3) >> 2;
 #pragma unroll
-        for (int i = 0; i < kRoiMax / 4; i++) {
-            const int yy = (lane >> 4) + 4 * i;
-            if (yy < rh && (lane & 15) < nwords)
-                *reinterpret_cast<uint32_t*>(roi + yy * kFastRowBytes + 4 * (lane & 15)) =
-                    __builtin_amdgcn_alignbyte(q1[i], q0[i], (uint32_t)al);
+        for (int i = 0; i < kFastPass; i++) {
+            if (i < npass) {
+                const uint32_t q1 = dpp_shl1(q0[i]);
+                const int yy = (lane >> 4) + 4 * i;
+                if (yy < G.rh && (lane & 15) < G.nwords)
+                    *reinterpret_cast<uint32_t*>(roi + yy * kFastRowBytes + 4 * (lane & 15)) =
+                        __builtin_amdgcn_alignbyte(q1, q0[i], (uint32_t)al);
+            }
         }
-    } else if ((g.pitch & 3) == 0) {
-        const int gx = c.x0 - 1;
+    } else if ((G.pitch & 3) == 0) {
+        const int gx = G.x0 - 1;
         const int al = gx & 3;
-        const uint8_t* base = img + (int64_t)c.y0 * g.pitch + (gx & ~3);
-        for (int yy = lane >> 4; yy < rh; yy += 4)
-            for (int k = lane & 15; k < nwords; k += 16) {
-                const uint32_t* q = reinterpret_cast<const uint32_t*>(base + (int64_t)yy * g.pitch) + k;
+        const uint8_t* base = G.img + (int64_t)G.y0 * G.pitch + (gx & ~3);
+        for (int yy = lane >> 4; yy < G.rh; yy += 4)
+            for (int k = lane & 15; k < G.nwords; k += 16) {
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(base + (int64_t)yy * G.pitch) + k;
                 *reinterpret_cast<uint32_t*>(roi + yy * kFastRowBytes + 4 * k) =
                     __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)al);
             }
     } else {
-        for (int yy = lane >> 4; yy < rh; yy += 4)
-            for (int xx = lane & 15; xx < rw; xx += 16)
-                roi[yy * kFastRowBytes + sh + xx] = img[(int64_t)(c.y0 + yy) * g.pitch + c.x0 + xx];
+        for (int yy = lane >> 4; yy < G.rh; yy += 4)
+            for (int xx = lane & 15; xx < G.rw; xx += 16)
+                roi[yy * kFastRowBytes + 1 + xx] = G.img[(int64_t)(G.y0 + yy) * G.pitch + G.x0 + xx];
     }
-    for (int i = lane; i < kFastRowBytes * rh / 4; i += 64) reinterpret_cast<uint32_t*>(Ms)[i] = 0u;
-    wave_sync_lds();
+}
+
+// Pre-test, exact strength, NMS and ordered output of one staged cell.
+__device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, int f, int cidx, const CellDesc& c,
+                                          int th_ini, int th_min, const uint8_t* roi, uint8_t* Ms, uint16_t* surv,
+                                          uint16_t* corn)
+{
+    constexpr int sh = 1;
+    const int lane = lane_id();
+    const LevelGeom& g = P->lv[c.level];
+    const int rw = c.rw, rh = c.rh;
     const int ww = rw - 6, wh = rh - 6;
     const int npix = ww > 0 && wh > 0 ? ww * wh : 0;
-    const uint64_t lt = lanemask_lt();
     // ---- 2 + 3: pre-test 4 pixels per lane (8 or 16 lanes per row), survivors in row-major
     //      order -> exact strength -> corners
     int ns = 0, nc = 0;
@@ -617,12 +643,14 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
             if (left < 4) sm &= (1u << left) - 1u;
         }
         const uint64_t m0 = __ballot(sm & 1u), m1 = __ballot(sm & 2u), m2 = __ballot(sm & 4u), m3 = __ballot(sm & 8u);
-        int q = ns + __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
-        if (sm & 1u) surv[q++] = (uint16_t)o;
-        if (sm & 2u) surv[q++] = (uint16_t)(o + 1);
-        if (sm & 4u) surv[q++] = (uint16_t)(o + 2);
-        if (sm & 8u) surv[q++] = (uint16_t)(o + 3);
-        ns += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+        if (sm) {
+            int q = ns + mbcnt(m0) + mbcnt(m1) + mbcnt(m2) + mbcnt(m3);
+            if (sm & 1u) surv[q++] = (uint16_t)o;
+            if (sm & 2u) surv[q++] = (uint16_t)(o + 1);
+            if (sm & 4u) surv[q++] = (uint16_t)(o + 2);
+            if (sm & 8u) surv[q] = (uint16_t)(o + 3);
+        }
+        ns = uniform(ns + __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
         if (ns > kFastSurv - 256 || r0 + rpi >= wh) {
             wave_sync_lds();
             for (int e0 = 0; e0 < ns; e0 += 64) {
@@ -636,10 +664,10 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
                 if (isc) Ms[oo] = (uint8_t)M;
                 const uint64_t mc = __ballot(isc);
                 if (isc) {
-                    const int qq = nc + __popcll(mc & lt);
+                    const int qq = nc + mbcnt(mc);
                     if (qq < kFastCorners) corn[qq] = (uint16_t)oo;
                 }
-                nc += __popcll(mc);
+                nc = uniform(nc + __popcll(mc));
             }
             wave_sync_lds();
             ns = 0;
@@ -661,12 +689,12 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
                 }
                 const uint64_t m = __ballot(kept);
                 if (kept) {
-                    const int q = running + __popcll(m & lt);
+                    const int q = running + mbcnt(m);
                     const int yy = oo / kFastRowBytes, xx = oo - yy * kFastRowBytes - sh;
                     if (q < P->cell_cap) out[q] = pack_key(xx + c.j * g.wcell, yy + c.i * g.hcell, sc);
                     else atomicOr(b.err, 2);
                 }
-                running += __popcll(m);
+                running = uniform(running + __popcll(m));
             }
         } else {
             int row0 = 0, col0 = 0;
@@ -678,11 +706,11 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
                 if (base + lane < npix) kept = nms_keep(Ms, o, t, &sc);
                 const uint64_t m = __ballot(kept);
                 if (kept) {
-                    const int q = running + __popcll(m & lt);
+                    const int q = running + mbcnt(m);
                     if (q < P->cell_cap) out[q] = pack_key(col + 3 + c.j * g.wcell, row + 3 + c.i * g.hcell, sc);
                     else atomicOr(b.err, 2);
                 }
-                running += __popcll(m);
+                running = uniform(running + __popcll(m));
                 col0 += 64;
                 while (col0 >= ww) { col0 -= ww; row0++; }
             }
@@ -691,6 +719,44 @@ __global__ __launch_bounds__(kThreads) void k_fast(const Plan* __restrict__ P, E
         if (nkept > 0) break;
     }
     if (lane == 0) b.cand_n[(int64_t)f * P->ncells + cidx] = min(nkept, P->cell_cap);
+}
+
+// One wave per kFastCellsPerWave consecutive cells, four waves per workgroup, no workgroup
+// barriers.  The next cell's ROI loads are issued before the current cell is processed.
+__global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P, ExtractBufs b)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wv = threadIdx.x >> 6, lane = lane_id();
+    const int slab = kFastRowBytes * P->max_roi_h;          // per-wave LDS: roi, M, lists
+    uint8_t* wbase = smem + (size_t)wv * (2 * slab + 2 * (kFastSurv + kFastCorners));
+    uint8_t* roi = wbase;
+    uint8_t* Ms = wbase + slab;
+    uint16_t* surv = reinterpret_cast<uint16_t*>(wbase + 2 * slab);
+    uint16_t* corn = surv + kFastSurv;
+    const int f = blockIdx.y;
+    int cidx = (blockIdx.x * kWaves + wv) * kFastCellsPerWave;
+    if (cidx >= P->ncells) return;
+    const int area = b.dyn[f].area_flag;
+    const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
+    CellDesc c = b.cells[cidx];
+    FastCellGeom G = fast_geom(P, b, f, c);
+    uint32_t q0[kFastPass];
+    fast_prefetch(G, q0);
+    for (int t = 0; t < kFastCellsPerWave; t++, cidx++) {
+        fast_stage(G, q0, roi);
+        for (int i = lane; i < (kFastRowBytes * c.rh + 15) / 16; i += 64) reinterpret_cast<uint4*>(Ms)[i] = make_uint4(0, 0, 0, 0);
+        wave_sync_lds();
+        const CellDesc cur = c;
+        const bool more = t + 1 < kFastCellsPerWave && cidx + 1 < P->ncells;
+        if (more) {
+            c = b.cells[cidx + 1];
+            G = fast_geom(P, b, f, c);
+            fast_prefetch(G, q0);
+        }
+        fast_cell(P, b, f, cidx, cur, th_ini, th_min, roi, Ms, surv, corn);
+        if (!more) break;
+        wave_sync_lds();
+    }
 }
 
 // ================================ k_octree ================================
@@ -850,14 +916,36 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
         kdelta = P->kbuf_stride;
     }
     auto KB = [&](int i) -> uint32_t* { return KB0 + (i ? kdelta : 0); };
-    {
+    if (g.ncells < P->oct_kl) {
+        // per-cell offsets in LDS (keys[1] is free until the pre-octree cull), then every
+        // thread copies keys, finding its cell by binary search: all loads independent
+        int* s_coff = reinterpret_cast<int*>(O.keys[1]);
         int carry = 0;
         for (int base = 0; base < g.ncells; base += kThreads) {
             const int ci = base + tid;
             const int v = ci < g.ncells ? cn[ci] : 0;
             int tot;
             const int pre = block_scan_excl(v, &tot, sbuf);
-            // copy: each thread copies its own cell (cells are small)
+            if (ci < g.ncells) s_coff[ci] = carry + pre;
+            carry += tot;
+        }
+        K = carry;
+        __syncthreads();
+        for (int i = tid; i < K; i += kThreads) {
+            int lo = 0, hi = g.ncells - 1;            // last cell with offset <= i
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_coff[mid] <= i) lo = mid; else hi = mid - 1;
+            }
+            KB(0)[i] = cand[(int64_t)lo * P->cell_cap + (i - s_coff[lo])];
+        }
+    } else {
+        int carry = 0;
+        for (int base = 0; base < g.ncells; base += kThreads) {
+            const int ci = base + tid;
+            const int v = ci < g.ncells ? cn[ci] : 0;
+            int tot;
+            const int pre = block_scan_excl(v, &tot, sbuf);
             if (ci < g.ncells) {
                 const uint32_t* src = cand + (int64_t)ci * P->cell_cap;
                 uint32_t* dst = KB(0) + carry + pre;
@@ -1056,16 +1144,33 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
         }
         // sort(vPrev) by (size, node) ascending and walk from the back: rank 0 = largest size,
         // ties -> later allocation first (pointer order of a monotonic allocator)
+        // (cnt, alloc) packed as cnt << 16 | alloc (alloc < 2^16, cnt < 2^15) in s_push,
+        // which is free until the push order is written
         for (int j = tid; j < m; j += kThreads) {
             const int k = s_work[j];
-            const int cj = S.cnt[k], aj = S.alloc[k];
-            int rank = 0;
-            for (int i = 0; i < m; i++) {
-                const int ki = s_work[i];
-                const int ci = S.cnt[ki], ai = S.alloc[ki];
-                rank += (ci > cj) || (ci == cj && ai > aj);
+            s_push[j] = (int)(((uint32_t)S.cnt[k] << 16) | (uint32_t)S.alloc[k]);   // used when K < 2^15
+        }
+        __syncthreads();
+        if (K < 32768 && alloc_ctr < 65536) {
+            for (int j = tid; j < m; j += kThreads) {
+                const int kj = s_push[j];
+                int rank = 0;
+#pragma unroll 8
+                for (int i = 0; i < m; i++) rank += s_push[i] > kj;
+                s_rank[j] = rank;
             }
-            s_rank[j] = rank;
+        } else {
+            for (int j = tid; j < m; j += kThreads) {
+                const int k = s_work[j];
+                const int cj = S.cnt[k], aj = S.alloc[k];
+                int rank = 0;
+                for (int i = 0; i < m; i++) {
+                    const int ki = s_work[i];
+                    const int ci = S.cnt[ki], ai = S.alloc[ki];
+                    rank += (ci > cj) || (ci == cj && ai > aj);
+                }
+                s_rank[j] = rank;
+            }
         }
         __syncthreads();
         for (int j = tid; j < m; j += kThreads) s_base[s_rank[j]] = j;
@@ -1199,9 +1304,8 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
 }
 
 // ================================ k_describe ================================
-// One wave per keypoint: IC_Angle on the unblurred level (lanes over patch columns, two
-// row halves), fastAtan2, canonical sincosf, 256 rBRIEF tests (4 per lane) on the blurred
-// level, output in cv::KeyPoint layout.
+// IC_Angle on the unblurred level, fastAtan2, canonical sincosf, 256 rBRIEF tests on the
+// blurred level, output in cv::KeyPoint layout.
 __device__ float fast_atan2_dev(float y, float x)
 {
     const float p1 = 0.9997878412794807f * (float)(180 / 3.1415926535897932384626433832795);
@@ -1260,6 +1364,8 @@ __device__ void sincos_canon(float af, float* s, float* c)
 
 struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
 
+// Two keypoints per wave (one per 32-lane half) so each lane has 31 patch loads in flight
+// and every lane produces exactly one descriptor byte (8 tests).
 __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ P, ExtractBufs b)
 {
     __shared__ int off[COEB_MAXL + 1];
@@ -1273,81 +1379,73 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
     }
     __syncthreads();
     const int total = off[L];
-    const int wv = threadIdx.x >> 6, lane = lane_id();
-    {
-        const int idx = blockIdx.x * kWaves + wv;
-        if (idx >= total) return;
-        int l = 0;
-        while (l + 1 < L && idx >= off[l + 1]) l++;
-        const LevelGeom& g = P->lv[l];
-        const uint32_t key = b.lvl_kp[(int64_t)f * P->lvl_stride + g.out_off + (idx - off[l])];
-        const int x = key_x(key), y = key_y(key), sc = key_s(key);
-        const int st = g.pitch, bst = g.bpitch;
-        // IC_Angle (ORBextractor.cc:80-107)
-        const uint8_t* img = level_ptr(P, b, f, l);
-        const uint8_t* center = img + (int64_t)y * st + x;
-        const int h = lane >> 5;
-        const int u = (lane & 31) - 15;
-        const bool uv = (lane & 31) < 31;
-        int m10 = 0, m01 = 0;
-        if (h == 0 && uv) m10 += u * center[u];
-        // rows 1..8 (h = 0) or 9..15 (h = 1); fully unrolled so the 16 row loads of a lane
-        // are in flight together (keypoints are >= 19 px from the level edge: rows +-16 and
-        // column +16 stay inside the level)
-        const int v0 = h == 0 ? 1 : 9, v1 = h == 0 ? 8 : 15;
-        int vps[8], vms[8];
+    const int lane = lane_id(), hl = lane & 31;
+    const int idx = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+    if (idx >= total) return;          // whole 32-lane halves only: the shuffles stay in-half
+    int l = 0;
+    while (l + 1 < L && idx >= off[l + 1]) l++;
+    const LevelGeom& g = P->lv[l];
+    const uint32_t key = b.lvl_kp[(int64_t)f * P->lvl_stride + g.out_off + (idx - off[l])];
+    const int x = key_x(key), y = key_y(key), sc = key_s(key);
+    const int st = g.pitch, bst = g.bpitch;
+    // IC_Angle (ORBextractor.cc:80-107): lane = patch column u in [-15, 15] (lane 31 idle);
+    // row v is inside the disc iff |u| <= umax[|v|]
+    const uint8_t* img = level_ptr(P, b, f, l);
+    const uint8_t* col = img + (int64_t)y * st + x + (hl - 15);
+    const int u = hl - 15;
+    const int au = u < 0 ? -u : u;
+    int pv[31];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int v = v0 + j;
-            vps[j] = center[u + v * st];
-            vms[j] = center[u - v * st];
-        }
+    for (int j = 0; j < 31; j++) pv[j] = col[(j - 15) * st];
+    int m10 = 0, m01 = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int v = v0 + j;
-            const int d = P->umax[min(v, 15)];
-            if (uv && v <= v1 && u >= -d && u <= d) {
-                m01 += v * (vps[j] - vms[j]);
-                m10 += u * (vps[j] + vms[j]);
-            }
+    for (int j = 0; j < 31; j++) {
+        const int v = j - 15;
+        const int av = v < 0 ? -v : v;
+        if (hl < 31 && au <= P->umax[av]) {
+            m10 += u * pv[j];
+            m01 += v * pv[j];
         }
-        m10 = wave_sum(m10);
-        m01 = wave_sum(m01);
-        const float angle = fast_atan2_dev((float)m01, (float)m10);
-        // descriptor (ORBextractor.cc:109-156), fused rotation forms of the reference binary
-        const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
-        float bs, ac;
-        sincos_canon(angle * factorPI, &bs, &ac);
-        const uint8_t* bl = b.blur + (int64_t)f * P->blur_stride + g.blur_off + (int64_t)y * bst + x;
-        int nib = 0;
-        const int4 pat = reinterpret_cast<const int4*>(b.pattern)[lane];   // 4 tests x (x0,y0,x1,y1) int8
+    }
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int pw = t == 0 ? pat.x : t == 1 ? pat.y : t == 2 ? pat.z : pat.w;
-            const float px0 = (float)(int8_t)(pw & 0xff), py0 = (float)(int8_t)((pw >> 8) & 0xff);
-            const float px1 = (float)(int8_t)((pw >> 16) & 0xff), py1 = (float)(int8_t)(pw >> 24);
-            const int r0 = (int)rintf(__builtin_fmaf(px0, bs, py0 * ac));
-            const int c0 = (int)rintf(__builtin_fmaf(px0, ac, -(py0 * bs)));
-            const int r1 = (int)rintf(__builtin_fmaf(px1, bs, py1 * ac));
-            const int c1 = (int)rintf(__builtin_fmaf(px1, ac, -(py1 * bs)));
-            const int t0 = bl[r0 * bst + c0], t1 = bl[r1 * bst + c1];
-            nib |= (t0 < t1) << t;
-        }
-        const int other = __shfl_xor(nib, 1, 64);
-        uint8_t* dd = b.desc + ((int64_t)f * P->kcap + idx) * 32;
-        if ((lane & 1) == 0) dd[lane >> 1] = (uint8_t)(nib | (other << 4));
-        if (lane == 0) {
-            KeyPointOut o;
-            o.x = (float)x;
-            o.y = (float)y;
-            if (l != 0) { o.x *= g.scale; o.y *= g.scale; }          // :1327-1334
-            o.size = (float)g.size_i;
-            o.angle = angle;
-            o.response = (float)sc;
-            o.octave = l;
-            o.class_id = -1;
-            reinterpret_cast<KeyPointOut*>(b.kps)[(int64_t)f * P->kcap + idx] = o;
-        }
+    for (int o = 16; o > 0; o >>= 1) {
+        m10 += __shfl_xor(m10, o, 64);
+        m01 += __shfl_xor(m01, o, 64);
+    }
+    const float angle = fast_atan2_dev((float)m01, (float)m10);
+    // descriptor (ORBextractor.cc:109-156), fused rotation forms of the reference binary
+    const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
+    float bs, ac;
+    sincos_canon(angle * factorPI, &bs, &ac);
+    const uint8_t* bl = b.blur + (int64_t)f * P->blur_stride + g.blur_off + (int64_t)y * bst + x;
+    const int4* pat = reinterpret_cast<const int4*>(b.pattern) + 2 * hl;   // tests 8*hl .. 8*hl+7
+    const int4 pa = pat[0], pb = pat[1];
+    int byte = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const int pw = t == 0 ? pa.x : t == 1 ? pa.y : t == 2 ? pa.z : t == 3 ? pa.w
+                     : t == 4 ? pb.x : t == 5 ? pb.y : t == 6 ? pb.z : pb.w;
+        const float px0 = (float)(int8_t)(pw & 0xff), py0 = (float)(int8_t)((pw >> 8) & 0xff);
+        const float px1 = (float)(int8_t)((pw >> 16) & 0xff), py1 = (float)(int8_t)(pw >> 24);
+        const int r0 = (int)rintf(__builtin_fmaf(px0, bs, py0 * ac));
+        const int c0 = (int)rintf(__builtin_fmaf(px0, ac, -(py0 * bs)));
+        const int r1 = (int)rintf(__builtin_fmaf(px1, bs, py1 * ac));
+        const int c1 = (int)rintf(__builtin_fmaf(px1, ac, -(py1 * bs)));
+        const int t0 = bl[r0 * bst + c0], t1 = bl[r1 * bst + c1];
+        byte |= (t0 < t1) << t;
+    }
+    b.desc[((int64_t)f * P->kcap + idx) * 32 + hl] = (uint8_t)byte;
+    if (hl == 0) {
+        KeyPointOut o;
+        o.x = (float)x;
+        o.y = (float)y;
+        if (l != 0) { o.x *= g.scale; o.y *= g.scale; }          // :1327-1334
+        o.size = (float)g.size_i;
+        o.angle = angle;
+        o.response = (float)sc;
+        o.octave = l;
+        o.class_id = -1;
+        reinterpret_cast<KeyPointOut*>(b.kps)[(int64_t)f * P->kcap + idx] = o;
     }
 }
 
@@ -1387,14 +1485,14 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     prof_end(prof, s);
     prof_begin(prof, "k_fast", s);
     const int fast_lds = kWaves * (2 * kFastRowBytes * plan.max_roi_h + 2 * (kFastSurv + kFastCorners));
-    hipLaunchKernelGGL(k_fast, dim3((plan.ncells + kWaves - 1) / kWaves, F), dim3(kThreads), fast_lds, s, d_plan, b);
+    hipLaunchKernelGGL(k_fast, dim3((plan.ncells + kWaves * kFastCellsPerWave - 1) / (kWaves * kFastCellsPerWave), F), dim3(kThreads), fast_lds, s, d_plan, b);
     prof_end(prof, s);
     prof_begin(prof, "k_octree", s);
     (void)hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);
     hipLaunchKernelGGL(k_octree, dim3(plan.L, F), dim3(kThreads), plan.oct_lds, s, d_plan, b);
     prof_end(prof, s);
     prof_begin(prof, "k_describe", s);
-    hipLaunchKernelGGL(k_describe, dim3((plan.kcap + kWaves - 1) / kWaves, F), dim3(kThreads), 0, s, d_plan, b);
+    hipLaunchKernelGGL(k_describe, dim3((plan.kcap + 2 * kWaves - 1) / (2 * kWaves), F), dim3(kThreads), 0, s, d_plan, b);
     prof_end(prof, s);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
