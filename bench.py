@@ -43,18 +43,32 @@ def level_pixels(w, h, nlevels=8, scale=1.2):
     return tot
 
 
+def fast_roi_pixels(w, h, nlevels=8, scale=1.2):
+    """Pixels of the union of the FAST cell ROIs, [16, W_l-13) x [16, H_l-13) per level
+    (ORBextractor.cc:795-798: minBorder = 16, maxBorder = W_l - 16 + 3)."""
+    s, tot = 1.0, 0
+    for l in range(nlevels):
+        if l:
+            s = float(np.float32(np.float64(np.float32(s)) * np.float64(np.float32(scale))))
+        inv = np.float32(1.0) / np.float32(s)
+        lw, lh = int(np.rint(np.float32(w) * inv)), int(np.rint(np.float32(h) * inv))
+        tot += max(0, lw - 29) * max(0, lh - 29)
+    return tot
+
+
 def kernel_bytes(name, w, h, nkp, nprev, npx, ncand):
-    """Algorithmic (compulsory) HBM bytes of one launch per frame, DESIGN.md s5."""
-    if name == "k_fast":        # read every pyramid level once, write candidate keys
-        return npx + 4 * ncand
+    """Algorithmic bytes of one launch per frame (each byte the algorithm must read or write,
+    touched once), DESIGN.md s4."""
+    if name == "k_fast":        # read the FAST ROIs of every level, write candidate keys
+        return fast_roi_pixels(w, h) + 4 * ncand
     if name == "k_blur":        # read + write every level
         return 2 * npx
     if name == "k_pyr_level":   # 7 launches: read level l-1, write level l (sum over launches / 7)
         return 2 * (npx - w * h) / 7.0 + w * h / 7.0
     if name == "k_octree":      # read candidates, write level keypoints
         return 4 * ncand + 4 * nkp
-    if name == "k_describe":    # 31x31 + 37x37 patches are cache reads; compulsory: keypoints+descs out
-        return 4 * nkp + 60 * nkp
+    if name == "k_describe":    # per keypoint: 749-px IC_Angle disc + 512 blurred samples in,
+        return (749 + 512 + 4 + 60) * nkp   # key in, 28-B record + 32-B descriptor out
     if name == "k_match":       # read current kps+descs and LastFrame snapshot, write matches
         return 60 * nkp + (32 + 28 + 12 + 4) * nprev + 4 * nkp
     if name == "k_prep":

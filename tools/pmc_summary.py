@@ -21,17 +21,21 @@ def load(path):
     return {k: ({c: v / len(disp[k]) for c, v in agg[k].items()}, len(disp[k]), grid[k]) for k in agg}
 
 
-def traffic_json(merged, nd, frames, command):
-    """Per kernel, HBM bytes per launch: 2 x FETCH_SIZE (gfx950 under-count of streaming reads,
-    MI355X_MICROARCH.md s HBM) + WRITE_SIZE, both reported by rocprofv3 in KB."""
-    out = dict(frames_per_launch=frames, command=command,
-               correction="bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch, mean over dispatches",
+def traffic_json(merged, nd, frames, command, fetch_scale):
+    """Per kernel, HBM bytes per launch: fetch_scale x FETCH_SIZE + WRITE_SIZE (rocprofv3 KB).
+    MI355X_MICROARCH.md s HBM: FETCH_SIZE reads 1/2 of the bytes of 16-B-per-lane streaming
+    reads (fetch_scale 2 there); other widths are uncalibrated and must be calibrated on a known
+    byte count.  Every kernel here loads <= 4 B per lane; k_blur (each level byte read once plus
+    the 6-row vertical halo, each written once) is the calibration: raw FETCH_SIZE ~ its known
+    read bytes, so fetch_scale = 1."""
+    out = dict(frames_per_launch=frames, command=command, fetch_scale=fetch_scale,
+               correction="bytes = (%g * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch, mean over dispatches" % fetch_scale,
                kernels={})
     for k, cv in sorted(merged.items()):
         if "FETCH_SIZE" not in cv or "WRITE_SIZE" not in cv:
             continue
         out["kernels"][k] = dict(fetch_kb=round(cv["FETCH_SIZE"], 3), write_kb=round(cv["WRITE_SIZE"], 3),
-                                 traffic_bytes=int((2 * cv["FETCH_SIZE"] + cv["WRITE_SIZE"]) * 1024),
+                                 traffic_bytes=int((fetch_scale * cv["FETCH_SIZE"] + cv["WRITE_SIZE"]) * 1024),
                                  dispatches=nd[k])
     return out
 
@@ -44,6 +48,7 @@ if __name__ == "__main__":
     ap.add_argument("--json", help="write per-kernel HBM traffic per launch (for bench.py roofline.traffic)")
     ap.add_argument("--frames", type=int, default=0, help="frames per launch of the profiled command")
     ap.add_argument("--command", default="")
+    ap.add_argument("--fetch-scale", type=float, default=1.0)
     a = ap.parse_args()
     merged = collections.defaultdict(dict)
     nd = {}
@@ -55,4 +60,4 @@ if __name__ == "__main__":
         print("%-16s n=%-3d %s" % (k, nd[k], " ".join("%s=%.4g" % (c, v) for c, v in sorted(cv.items()))))
     if a.json:
         with open(a.json, "w") as f:
-            json.dump(traffic_json(merged, nd, a.frames, a.command), f, indent=1)
+            json.dump(traffic_json(merged, nd, a.frames, a.command, a.fetch_scale), f, indent=1)
