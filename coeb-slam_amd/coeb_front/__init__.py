@@ -32,6 +32,7 @@ MAX_LEVELS = 16
 ABI_SYMBOLS = [
     "coeb_create", "coeb_destroy", "coeb_last_error", "coeb_orb_tables_get", "coeb_max_keypoints",
     "coeb_extract", "coeb_extract_batch_device", "coeb_batch_results", "coeb_match_batch_device",
+    "coeb_match_batch_device_tcw",
     "coeb_batch_match_results", "coeb_match_lastframe", "coeb_blur_flags", "coeb_stereo_from_rgbd",
     "coeb_rgbd_preprocess", "coeb_descriptor_distance", "coeb_profile_enable", "coeb_profile_read",
     "coeb_profile_reset", "coeb_synchronize", "coeb_device_count", "coeb_debug_read",
@@ -95,6 +96,8 @@ def lib():
                                          C.POINTER(C.c_void_p), C.POINTER(C.c_int)]
         L.coeb_match_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(Camera),
                                               C.c_void_p, C.c_float, C.c_int32]
+        L.coeb_match_batch_device_tcw.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                                  C.POINTER(Camera), C.c_void_p, C.c_float, C.c_int32]
         L.coeb_batch_match_results.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
         L.coeb_match_lastframe.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(CurFrameC),
                                            C.POINTER(LastFrameC), C.c_void_p, C.c_void_p, C.c_float, C.c_int,
@@ -209,6 +212,11 @@ class Context:
         Tcw = np.ascontiguousarray(Tcw, np.float32)
         self.check(lib().coeb_match_batch_device(self.h, C.c_void_p(d_depth_ptr), nframes, w, h, C.byref(cam),
                                                  _p(Tcw), th, nobs))
+
+    def match_batch_device_tcw(self, d_depth_ptr, nframes, w, h, cam, d_tcw_ptr, th=15.0, nobs=2):
+        """As match_batch_device, with the (nframes, 4, 4) poses already in device memory."""
+        self.check(lib().coeb_match_batch_device_tcw(self.h, C.c_void_p(d_depth_ptr), nframes, w, h, C.byref(cam),
+                                                     C.c_void_p(d_tcw_ptr), th, nobs))
 
     def batch_match_results(self):
         m, n = C.c_void_p(), C.c_void_p()

@@ -19,6 +19,7 @@ class BatchPipeline:
                                          width, height)
         self.gray = None
         self.depth = None
+        self.dTcw = None
         self.Tcw = np.stack([np.eye(4, dtype=np.float32)] * nframes)
         self.dyn = None
 
@@ -33,6 +34,7 @@ class BatchPipeline:
         self.depth = self.ctx.upload(np.ascontiguousarray(depth, np.float32))
         if Tcw is not None:
             self.Tcw = np.ascontiguousarray(Tcw, np.float32)
+        self.dTcw = self.ctx.upload(self.Tcw.reshape(self.F, 16))     # poses resident like the frames
         if dyn is not None:
             boxes, tms, blurs = [], [], []
             box_off, tm_off = [0], [0]
@@ -59,7 +61,7 @@ class BatchPipeline:
         else:
             self.ctx.extract_batch_device(self.gray.ptr, self.F, self.W, self.H)
         if match:
-            self.ctx.match_batch_device(self.depth.ptr, self.F, self.W, self.H, self.cam, self.Tcw, th, nobs)
+            self.ctx.match_batch_device_tcw(self.depth.ptr, self.F, self.W, self.H, self.cam, self.dTcw.ptr, th, nobs)
 
     def synchronize(self):
         self.ctx.synchronize()
@@ -102,7 +104,7 @@ class BatchPipeline:
         return out, matches, nm
 
     def close(self):
-        for b in (self.gray, self.depth):
+        for b in (self.gray, self.depth, self.dTcw):
             if b is not None:
                 b.free()
         self.ctx.close()

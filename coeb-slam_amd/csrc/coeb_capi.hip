@@ -340,6 +340,7 @@ struct coeb_ctx {
     ProfileHook hook;
     int batch_frames = 0;      // frames of the last extracted batch
     const uint8_t* batch_gray = nullptr;
+    int ident_frames = 0;      // identity poses initialised in "b_I"
 };
 
 namespace {
@@ -733,26 +734,34 @@ int coeb_match_lastframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curfram
     return COEB_OK;
 }
 
-int coeb_match_batch_device(coeb_ctx* c, const float* d_depth, int F, int W, int H, const coeb_camera* cam,
-                            const float* Tcw, float th, int32_t nobs)
+namespace {
+
+// Common body of the batch matchers.  dT_cur: device poses, pair p (current frame p+1) at
+// dT_cur + 16 p; LastFrame poses are identities (frame p is the world frame of its pair).
+int match_batch_impl(coeb_ctx* c, const float* d_depth, int F, int W, int H, const coeb_camera* cam,
+                     const float* dT_cur, float th, int32_t nobs)
 {
-    if (!c || !d_depth || !cam || !Tcw || F <= 0) return set_err(c, COEB_EINVAL, "coeb_match_batch_device: invalid arguments");
-    if (!c->has_plan || c->batch_frames != F || c->plan.W != W || c->plan.H != H)
-        return set_err(c, COEB_EINVAL, "coeb_match_batch_device: must follow coeb_extract_batch_device on the same batch");
-    (void)hipSetDevice(c->device);
     const int K = c->plan.kcap;
     if (K > kCurMax) return set_err(c, COEB_EINVAL, "keypoint capacity exceeds the matcher limit (4095)");
     int rc;
-    float *ur, *dep, *xw, *dT;
+    float *ur, *dep, *xw, *dI;
     uint8_t *has, *outl;
     int32_t *nobsb, *match, *nm, *scr, *derr;
     if ((rc = ensure(c, "b_ur", (size_t)F * K, &ur)) || (rc = ensure(c, "b_dep", (size_t)F * K, &dep)) ||
         (rc = ensure(c, "b_xw", (size_t)F * K * 3, &xw)) || (rc = ensure(c, "b_has", (size_t)F * K, &has)) ||
         (rc = ensure(c, "b_outl", (size_t)F * K, &outl)) || (rc = ensure(c, "b_nobs", (size_t)F * K, &nobsb)) ||
         (rc = ensure(c, "b_match", (size_t)F * K, &match)) || (rc = ensure(c, "b_nm", (size_t)F, &nm)) ||
-        (rc = ensure(c, "b_T", (size_t)F * 32, &dT)) || (rc = ensure(c, "b_scr", (size_t)F * K * kMatchCQ, &scr)) ||
-        (rc = ensure(c, "err", 4, &derr)))
+        (rc = ensure(c, "b_scr", (size_t)F * K * kMatchCQ, &scr)) || (rc = ensure(c, "err", 4, &derr)))
         return rc;
+    if (c->ident_frames < F || !c->bufs.count("b_I")) {
+        const int n = std::max(F, c->max_batch);
+        if ((rc = ensure(c, "b_I", (size_t)n * 16, &dI))) return rc;
+        std::vector<float> I((size_t)n * 16, 0.f);
+        for (int p = 0; p < n; p++) I[(size_t)p * 16 + 0] = I[(size_t)p * 16 + 5] = I[(size_t)p * 16 + 10] = I[(size_t)p * 16 + 15] = 1.f;
+        HIP_TRY(c, hipMemcpy(dI, I.data(), I.size() * 4, hipMemcpyHostToDevice));
+        c->ident_frames = n;
+    }
+    dI = static_cast<float*>(c->bufs["b_I"].p);
     const coeb_keypoint* kps = static_cast<const coeb_keypoint*>(c->bufs["kps"].p);
     const uint8_t* desc = static_cast<const uint8_t*>(c->bufs["desc"].p);
     const int32_t* counts = static_cast<const int32_t*>(c->bufs["counts"].p);
@@ -763,24 +772,47 @@ int coeb_match_batch_device(coeb_ctx* c, const float* d_depth, int F, int W, int
     pb.ur = ur; pb.dep = dep; pb.has = has; pb.outl = outl; pb.xw = xw; pb.nobs = nobsb; pb.nobs_value = nobs;
     if (launch_prep(pb, F, c->stream, &c->hook)) return hip_err(c, hipGetLastError(), "launch_prep");
     if (F < 2) return COEB_OK;
-    // pair p: current = frame p+1, last = frame p (Tcw_last = I, Tcw_cur = Tcw[p+1])
-    std::vector<float> T((size_t)(F - 1) * 32);
-    static const float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-    for (int p = 0; p < F - 1; p++) {
-        memcpy(&T[(size_t)p * 16], Tcw + (size_t)(p + 1) * 16, 64);
-        memcpy(&T[(size_t)(F - 1) * 16 + (size_t)p * 16], I, 64);
-    }
-    HIP_TRY(c, hipMemcpyAsync(dT, T.data(), T.size() * 4, hipMemcpyHostToDevice, c->stream));
     MatchBufs mb;
     memset(&mb, 0, sizeof(mb));
     mb.cur_kps = kps + K; mb.cur_desc = desc + (size_t)K * 32; mb.cur_n = counts + 1; mb.cur_ur = ur + K; mb.cur_stride = K;
     mb.last_kps = kps; mb.last_desc = desc; mb.last_n = counts; mb.last_has = has; mb.last_out = outl;
     mb.last_xw = xw; mb.last_nobs = nobsb; mb.last_stride = K;
-    mb.Tcw_cur = dT; mb.Tcw_last = dT + (size_t)(F - 1) * 16;
+    mb.Tcw_cur = dT_cur; mb.Tcw_last = dI;
     mb.match = match + K; mb.nmatch = nm + 1; mb.scratch = scr; mb.scratch_stride = K * kMatchCQ; mb.err = derr;
     if (launch_match(make_cam(c, cam), mb, F - 1, th, 0, 1, 20, c->stream, &c->hook))
         return hip_err(c, hipGetLastError(), "launch_match");
     return COEB_OK;
+}
+
+int match_batch_check(coeb_ctx* c, const float* d_depth, int F, int W, int H, const coeb_camera* cam, const float* T)
+{
+    if (!c || !d_depth || !cam || !T || F <= 0) return set_err(c, COEB_EINVAL, "coeb_match_batch_device: invalid arguments");
+    if (!c->has_plan || c->batch_frames != F || c->plan.W != W || c->plan.H != H)
+        return set_err(c, COEB_EINVAL, "coeb_match_batch_device: must follow coeb_extract_batch_device on the same batch");
+    return COEB_OK;
+}
+
+}  // namespace
+
+int coeb_match_batch_device(coeb_ctx* c, const float* d_depth, int F, int W, int H, const coeb_camera* cam,
+                            const float* Tcw, float th, int32_t nobs)
+{
+    int rc;
+    if ((rc = match_batch_check(c, d_depth, F, W, H, cam, Tcw))) return rc;
+    (void)hipSetDevice(c->device);
+    float* dT;
+    if ((rc = ensure(c, "b_T", (size_t)F * 16, &dT))) return rc;
+    HIP_TRY(c, hipMemcpyAsync(dT, Tcw, (size_t)F * 64, hipMemcpyHostToDevice, c->stream));
+    return match_batch_impl(c, d_depth, F, W, H, cam, dT + 16, th, nobs);
+}
+
+int coeb_match_batch_device_tcw(coeb_ctx* c, const float* d_depth, int F, int W, int H, const coeb_camera* cam,
+                                const float* d_Tcw, float th, int32_t nobs)
+{
+    int rc;
+    if ((rc = match_batch_check(c, d_depth, F, W, H, cam, d_Tcw))) return rc;
+    (void)hipSetDevice(c->device);
+    return match_batch_impl(c, d_depth, F, W, H, cam, d_Tcw + 16, th, nobs);
 }
 
 int coeb_batch_match_results(coeb_ctx* c, const int32_t** d_match, const int32_t** d_nmatches)

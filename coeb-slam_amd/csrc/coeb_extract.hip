@@ -516,6 +516,29 @@ __device__ __forceinline__ uint32_t fast_pretest4(const uint8_t* c, int t)
     return ((lo & 0xffffu) ? 1u : 0u) | ((lo >> 16) ? 2u : 0u) | ((hi & 0xffffu) ? 4u : 0u) | ((hi >> 16) ? 8u : 0u);
 }
 
+// Same test, raw packed results: pixel q survives iff 16-bit half q of (lo, hi) is nonzero.
+__device__ __forceinline__ void fast_pretest4_raw(const uint8_t* c, int t, uint32_t& lo, uint32_t& hi)
+{
+    constexpr int st = kFastRowBytes;
+    const uint32_t* r0 = reinterpret_cast<const uint32_t*>(c);
+    const uint32_t* rp2 = reinterpret_cast<const uint32_t*>(c + 2 * st);
+    const uint32_t* rm2 = reinterpret_cast<const uint32_t*>(c - 2 * st);
+    const uint32_t a0 = r0[-1], b0 = r0[0], c0 = r0[1];
+    const uint32_t ap = rp2[-1], bp = rp2[0], cp = rp2[1];
+    const uint32_t am = rm2[-1], bm = rm2[0], cm = rm2[1];
+    const uint32_t u3 = *reinterpret_cast<const uint32_t*>(c + 3 * st);
+    const uint32_t d3 = *reinterpret_cast<const uint32_t*>(c - 3 * st);
+    const us2 T = pk2(t, t);
+    lo = pretest_half(
+        as_us2(__builtin_amdgcn_perm(0u, b0, 0x0c010c00u)), as_us2(__builtin_amdgcn_perm(0u, u3, 0x0c010c00u)),
+        as_us2(__builtin_amdgcn_perm(0u, d3, 0x0c010c00u)), as_us2(win_lo(bp, cp, 2)), as_us2(win_lo(am, bm, 2)),
+        as_us2(win_lo(b0, c0, 3)), as_us2(win_lo(a0, b0, 1)), as_us2(win_lo(bm, cm, 2)), as_us2(win_lo(ap, bp, 2)), T);
+    hi = pretest_half(
+        as_us2(__builtin_amdgcn_perm(0u, b0, 0x0c030c02u)), as_us2(__builtin_amdgcn_perm(0u, u3, 0x0c030c02u)),
+        as_us2(__builtin_amdgcn_perm(0u, d3, 0x0c030c02u)), as_us2(win_hi(bp, cp, 2)), as_us2(win_hi(am, bm, 2)),
+        as_us2(win_hi(b0, c0, 3)), as_us2(win_hi(a0, b0, 1)), as_us2(win_hi(bm, cm, 2)), as_us2(win_hi(ap, bp, 2)), T);
+}
+
 __device__ __forceinline__ int nms_keep(const uint8_t* Ms, int o, int t, int* sc_out)
 {
     const int M = Ms[o];
@@ -633,22 +656,25 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
     const int lpr_log = ngrp > 8 ? 4 : 3;
     const int cg = lane & ((1 << lpr_log) - 1), rsub = lane >> lpr_log;
     const int rpi = 64 >> lpr_log;
-    for (int r0 = 0; npix > 0 && r0 < wh; r0 += rpi) {
-        const int row = r0 + rsub;
-        const int o = (row + 3) * kFastRowBytes + 4 + 4 * cg;
-        uint32_t sm = 0;
-        if (row < wh && cg < ngrp) {
-            sm = fast_pretest4(&roi[o], th_min);
-            const int left = ww - 4 * cg;            // pixels of this group inside the window
-            if (left < 4) sm &= (1u << left) - 1u;
-        }
-        const uint64_t m0 = __ballot(sm & 1u), m1 = __ballot(sm & 2u), m2 = __ballot(sm & 4u), m3 = __ballot(sm & 8u);
-        if (sm) {
+    // lanes' pixel columns inside the window (fixed for the cell): one wave mask per pixel slot
+    const uint64_t vm0 = __ballot(cg < ngrp && 4 * cg + 0 < ww), vm1 = __ballot(cg < ngrp && 4 * cg + 1 < ww);
+    const uint64_t vm2 = __ballot(cg < ngrp && 4 * cg + 2 < ww), vm3 = __ballot(cg < ngrp && 4 * cg + 3 < ww);
+    int o = (rsub + 3) * kFastRowBytes + 4 + 4 * cg;
+    for (int r0 = 0; npix > 0 && r0 < wh; r0 += rpi, o += rpi * kFastRowBytes) {
+        // every lane runs the test (rows past the window read slab bytes that are masked off)
+        uint32_t lo, hi;
+        fast_pretest4_raw(&roi[o], th_min, lo, hi);
+        const uint64_t rm = __ballot(r0 + rsub < wh);
+        const uint64_t m0 = __ballot((lo & 0xffffu) != 0u) & vm0 & rm, m1 = __ballot((lo >> 16) != 0u) & vm1 & rm;
+        const uint64_t m2 = __ballot((hi & 0xffffu) != 0u) & vm2 & rm, m3 = __ballot((hi >> 16) != 0u) & vm3 & rm;
+        const uint64_t any = m0 | m1 | m2 | m3;
+        if ((any >> lane) & 1u) {
+            const uint64_t me = 1ull << lane;
             int q = ns + mbcnt(m0) + mbcnt(m1) + mbcnt(m2) + mbcnt(m3);
-            if (sm & 1u) surv[q++] = (uint16_t)o;
-            if (sm & 2u) surv[q++] = (uint16_t)(o + 1);
-            if (sm & 4u) surv[q++] = (uint16_t)(o + 2);
-            if (sm & 8u) surv[q] = (uint16_t)(o + 3);
+            if (m0 & me) surv[q++] = (uint16_t)o;
+            if (m1 & me) surv[q++] = (uint16_t)(o + 1);
+            if (m2 & me) surv[q++] = (uint16_t)(o + 2);
+            if (m3 & me) surv[q] = (uint16_t)(o + 3);
         }
         ns = uniform(ns + __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
         if (ns > kFastSurv - 256 || r0 + rpi >= wh) {

@@ -152,6 +152,9 @@ int coeb_batch_results(coeb_ctx* ctx, const coeb_keypoint** d_kps, const uint8_t
  * d_depth: nframes x height x width float (device).  Results: coeb_batch_match_results. */
 int coeb_match_batch_device(coeb_ctx* ctx, const float* d_depth, int nframes, int width, int height,
                             const coeb_camera* cam, const float* Tcw, float th, int32_t nobs);
+/* The same with the poses already in device memory (d_Tcw: nframes x 16 floats). */
+int coeb_match_batch_device_tcw(coeb_ctx* ctx, const float* d_depth, int nframes, int width, int height,
+                                const coeb_camera* cam, const float* d_Tcw, float th, int32_t nobs);
 int coeb_batch_match_results(coeb_ctx* ctx, const int32_t** d_match, const int32_t** d_nmatches);
 
 /* ---- ORBmatcher::SearchByProjection(CurrentFrame, LastFrame, th, bMono) ----

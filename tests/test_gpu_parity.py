@@ -283,6 +283,11 @@ def test_batch_pipeline_matches_oracle(oracle_mod, ex):
         out2, matches2, nms2 = bp.results()
         assert all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(out, out2))
         assert nms == nms2
+        # host-pose entry point (coeb_match_batch_device) == device-pose one
+        bp.ctx.match_batch_device(bp.depth.ptr, F, 640, 480, bp.cam, Tcw)
+        bp.synchronize()
+        _, matches3, nms3 = bp.results()
+        assert nms3 == nms and all(np.array_equal(a, b) for a, b in zip(matches[1:], matches3[1:]))
     finally:
         bp.close()
 
