@@ -565,7 +565,7 @@ __device__ __forceinline__ int mbcnt(uint64_t m)
 }
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-constexpr int kFastCellsPerWave = 2;
+constexpr int kFastCellsPerWave = 1;
 constexpr int kFastPass = 12;            // prefetched ROI rows / 4 (cells up to 48 rows)
 
 // Staging of a cell ROI into the wave's slab (slab byte = ROI column + 1, so detection
