@@ -270,47 +270,30 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
     CurView<kLds> cv;
     cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = cur_ur; cv.gdesc = cdesc;
 
-    // ---- phase 0 ----
-    const int np2 = next_pow2(n);
+    // ---- phase 0: stage CurrentFrame, grid CSR by a stable counting sort ----
     for (int c = tid; c <= COEB_GRID_CELLS; c += kMThreads) L.cell[c] = 0;
     __syncthreads();
-    for (int i = tid; i < np2; i += kMThreads) {
-        uint32_t key = 0xFFFFFFFFu;
-        if (i < n) {
-            const Kp k = cur[i];
-            if (kLds) {
-                L.kp[i] = make_float4(k.x, k.y, cur_ur[i], __int_as_float(k.octave));
-                const uint4* d = reinterpret_cast<const uint4*>(cdesc + 32 * i);
-                const uint4 d0 = d[0], d1 = d[1];
-                uint32_t* o = L.desc + 8 * i;
-                o[0] = d0.x; o[1] = d0.y; o[2] = d0.z; o[3] = d0.w;
-                o[4] = d1.x; o[5] = d1.y; o[6] = d1.z; o[7] = d1.w;
-            }
-            const int px = (int)roundf((k.x - cam.min_x) * cam.grid_inv_w);   // PosInGrid (Frame.cc:560)
-            const int py = (int)roundf((k.y - cam.min_y) * cam.grid_inv_h);
-            if (px >= 0 && px < COEB_GRID_COLS && py >= 0 && py < COEB_GRID_ROWS) {
-                const int cell = px * COEB_GRID_ROWS + py;
-                key = ((uint32_t)cell << kIdxBits) | (uint32_t)i;
-                atomicAdd(&L.cell[cell + 1], 1);
-            }
+    for (int i = tid; i < n; i += kMThreads) {
+        const Kp k = cur[i];
+        if (kLds) {
+            L.kp[i] = make_float4(k.x, k.y, cur_ur[i], __int_as_float(k.octave));
+            const uint4* d = reinterpret_cast<const uint4*>(cdesc + 32 * i);
+            const uint4 d0 = d[0], d1 = d[1];
+            uint32_t* o = L.desc + 8 * i;
+            o[0] = d0.x; o[1] = d0.y; o[2] = d0.z; o[3] = d0.w;
+            o[4] = d1.x; o[5] = d1.y; o[6] = d1.z; o[7] = d1.w;
         }
-        L.sort[i] = key;
+        const int px = (int)roundf((k.x - cam.min_x) * cam.grid_inv_w);   // PosInGrid (Frame.cc:560)
+        const int py = (int)roundf((k.y - cam.min_y) * cam.grid_inv_h);
+        int cell = -1;
+        if (px >= 0 && px < COEB_GRID_COLS && py >= 0 && py < COEB_GRID_ROWS) {
+            cell = px * COEB_GRID_ROWS + py;
+            atomicAdd(&L.cell[cell + 1], 1);
+        }
+        L.owner[i] = cell;                 // scratch until phase 2
     }
     __syncthreads();
-    for (int k = 2; k <= np2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < np2; i += kMThreads) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const uint32_t a = L.sort[i], c = L.sort[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((a > c) == up) { L.sort[i] = c; L.sort[ixj] = a; }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    if (tid < 64) {
+    if (tid < 64) {                        // exclusive prefix: L.cell[c] = start of cell c
         const int lane = tid;
         int carry = 0;
         for (int base = 1; base <= COEB_GRID_CELLS; base += 64) {
@@ -322,6 +305,44 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
             }
             if (c <= COEB_GRID_CELLS) L.cell[c] = carry + v;
             carry += __shfl(v, 63, 64);
+        }
+    }
+    __syncthreads();
+    // scatter with a per-cell cursor (L.cell[c] advances to the end of cell c = start of c+1) ...
+    for (int i = tid; i < n; i += kMThreads) {
+        const int cell = L.owner[i];
+        if (cell >= 0) {
+            const int pos = atomicAdd(&L.cell[cell], 1);
+            L.sort[pos] = ((uint32_t)cell << kIdxBits) | (uint32_t)i;
+        }
+    }
+    __syncthreads();
+    // ... so shift the cursors back by one cell to get the starts again
+    {
+        int v[(COEB_GRID_CELLS + kMThreads) / kMThreads];
+#pragma unroll
+        for (int k = 0; k < (COEB_GRID_CELLS + kMThreads) / kMThreads; k++) {
+            const int c = tid + k * kMThreads;
+            v[k] = (c >= 1 && c <= COEB_GRID_CELLS) ? L.cell[c - 1] : 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < (COEB_GRID_CELLS + kMThreads) / kMThreads; k++) {
+            const int c = tid + k * kMThreads;
+            if (c >= 1 && c <= COEB_GRID_CELLS) L.cell[c] = v[k];
+        }
+        if (tid == 0) L.cell[0] = 0;
+    }
+    __syncthreads();
+    // insertion order inside a cell = keypoint index order (Frame.cc:403-410): sort each
+    // (short) cell range by index
+    for (int c = tid; c < COEB_GRID_CELLS; c += kMThreads) {
+        const int a = L.cell[c], e = L.cell[c + 1];
+        for (int x = a + 1; x < e; x++) {
+            const uint32_t key = L.sort[x];
+            int y = x - 1;
+            while (y >= a && L.sort[y] > key) { L.sort[y + 1] = L.sort[y]; y--; }
+            L.sort[y + 1] = key;
         }
     }
     __syncthreads();
@@ -349,10 +370,16 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
         // ---- phase 1: candidate lists (static filters) ----
         if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; s_flag[2] = 0; s_flag[3] = 0; }
         __syncthreads();
-        for (int q = tid; q < nl; q += kMThreads) {
-            int cnt = -1;
-            if (lhas[q] && !lout[q]) {
-                const QueryWin w = query_window(cam, T, lxw + 3 * q, last[q].octave, th, fwd, bwd);
+        // one 16-lane group per query; lanes take the candidates of a grid column range 16 at a
+        // time and ballot-compact them, so each list stays in enumeration order
+        {
+            const int grp = tid >> 4, gl = tid & 15, gsh = (tid & 63) & ~15;
+            for (int q0 = 0; q0 < nl; q0 += kMThreads / 16) {
+                const int q = q0 + grp;
+                int cnt = -1;
+                QueryWin w;
+                w.ok = false;
+                if (q < nl && lhas[q] && !lout[q]) w = query_window(cam, T, lxw + 3 * q, last[q].octave, th, fwd, bwd);
                 if (w.ok) {
                     uint32_t qd[8];
                     const uint4* d = reinterpret_cast<const uint4*>(ldesc + 32 * q);
@@ -361,18 +388,44 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
                     qd[4] = d1.x; qd[5] = d1.y; qd[6] = d1.z; qd[7] = d1.w;
                     cnt = 0;
                     uint32_t* lst = lists + (int64_t)q * kCQ;
-                    for_candidates<kLds>(w, L.cell, L.sort, cv, [&](int i2) {
-                        const int dist = cv.dist(i2, qd);
-                        if (dist <= TH_HIGH) {
-                            if (cnt < kCQ) lst[cnt] = ((uint32_t)dist << kIdxBits) | (uint32_t)i2;
-                            cnt++;
+                    for (int ix = w.x0; ix <= w.x1; ix++) {
+                        const int c0 = L.cell[ix * COEB_GRID_ROWS + w.y0];
+                        const int c1 = L.cell[ix * COEB_GRID_ROWS + w.y1 + 1];
+                        for (int base = c0; base < c1; base += 16) {
+                            const int e = base + gl;
+                            bool ok = false;
+                            uint32_t ent = 0;
+                            if (e < c1) {
+                                const int i2 = (int)(L.sort[e] & ((1u << kIdxBits) - 1));
+                                float x, y, ur;
+                                int oct;
+                                cv.get(i2, x, y, ur, oct);
+                                ok = true;
+                                if (w.chk) {
+                                    if (oct < w.minL) ok = false;
+                                    if (w.maxL >= 0 && oct > w.maxL) ok = false;
+                                }
+                                const float distx = x - w.u, disty = y - w.v;
+                                if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) ok = false;
+                                if (ur > 0 && fabsf(w.ur_q - ur) > w.radius) ok = false;
+                                if (ok) {
+                                    const int dist = cv.dist(i2, qd);
+                                    ok = dist <= TH_HIGH;
+                                    ent = ((uint32_t)dist << kIdxBits) | (uint32_t)i2;
+                                }
+                            }
+                            const uint32_t gb = (uint32_t)(__ballot(ok) >> gsh) & 0xFFFFu;
+                            if (ok) {
+                                const int pos = cnt + __popc(gb & ((1u << gl) - 1u));
+                                if (pos < kCQ) lst[pos] = ent;
+                            }
+                            cnt += __popc(gb);
                         }
-                        return true;
-                    });
+                    }
                     if (cnt > kCQ) s_flag[0] = 1;      // overflow -> sequential path
                 }
+                if (q < nl && gl == 0) L.qn[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | (lnobs[q] > 0 ? 0x10000 : 0));
             }
-            L.qn[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | (lnobs[q] > 0 ? 0x10000 : 0));
         }
         __syncthreads();
         bool seq = force_seq || s_flag[0];
