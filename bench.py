@@ -152,6 +152,9 @@ class DryRunPipeline:
         def debug_read(self, what, f=0):
             return np.zeros(4, np.uint8)
 
+        def set_batch_streams(self, n):
+            pass
+
     def __init__(self, rank):
         self.rank = rank
         self.ctx = self._Ctx()
@@ -181,6 +184,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="matched frames per step per GPU")
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
+    ap.add_argument("--streams", type=int, default=1,
+                    help="HIP streams the batch is chunked over (kernels of different chunks overlap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip HIP-event kernel timing")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
@@ -203,6 +208,7 @@ def main():
     else:
         from coeb_front.pipeline import BatchPipeline
         bp = BatchPipeline(w, h, F, nfeatures=cfg["nfeatures"], device=local_rank)
+    bp.ctx.set_batch_streams(args.streams)
     bp.load(frames, Tcw=Tcw)
 
     def barrier():
@@ -227,11 +233,13 @@ def main():
     barrier()
     elapsed = ranks.max(t1 - t0)
 
-    # per-kernel device time: a separate pass with HIP events on the context stream
+    # per-kernel device time: a separate pass with HIP events, kernels serialised on one
+    # stream so each event pair brackets exactly one launch
     prof = {}
     prof_steps = 0
     if not args.no_profile:
         prof_steps = max(1, min(args.steps, 10))
+        bp.ctx.set_batch_streams(1)
         bp.ctx.profile(True)
         bp.ctx.profile_reset()
         for _ in range(prof_steps):
@@ -239,6 +247,7 @@ def main():
         bp.synchronize()
         prof = bp.ctx.profile_read()
         bp.ctx.profile(False)
+        bp.ctx.set_batch_streams(args.streams)
 
     e2e = None
     if not args.no_e2e and not args.dry_run:
@@ -286,6 +295,7 @@ def main():
                     data="synthetic (TUM-like rectangles + noise, (+2,+1) px/frame, Z=2 m)",
                     config=dict(workload=cfg["workload"], width=w, height=h, nfeatures=cfg["nfeatures"],
                                 nlevels=8, frames_per_step_per_gpu=args.batch, halo_frames_per_step=1,
+                                streams_per_gpu=args.streams,
                                 parallelism="frame-sharded x%d (no collectives)" % world),
                     roofline=roof,
                     pipeline_roofline=dict(bytes_per_frame=int(pipeline_bytes),

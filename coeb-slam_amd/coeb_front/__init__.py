@@ -36,7 +36,7 @@ ABI_SYMBOLS = [
     "coeb_batch_match_results", "coeb_match_lastframe", "coeb_blur_flags", "coeb_stereo_from_rgbd",
     "coeb_rgbd_preprocess", "coeb_descriptor_distance", "coeb_profile_enable", "coeb_profile_read",
     "coeb_profile_reset", "coeb_synchronize", "coeb_device_count", "coeb_debug_read",
-    "coeb_device_alloc", "coeb_device_free", "coeb_memcpy_h2d", "coeb_memcpy_d2h",
+    "coeb_device_alloc", "coeb_device_free", "coeb_memcpy_h2d", "coeb_memcpy_d2h", "coeb_set_batch_streams",
 ]
 
 
@@ -114,6 +114,7 @@ def lib():
         L.coeb_profile_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                         C.POINTER(C.c_int)]
         L.coeb_synchronize.argtypes = [C.c_void_p]
+        L.coeb_set_batch_streams.argtypes = [C.c_void_p, C.c_int]
         L.coeb_device_alloc.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]
         L.coeb_device_free.argtypes = [C.c_void_p, C.c_void_p]
         L.coeb_memcpy_h2d.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
@@ -225,6 +226,10 @@ class Context:
 
     def synchronize(self):
         self.check(lib().coeb_synchronize(self.h))
+
+    def set_batch_streams(self, n):
+        """HIP streams a batch is chunked over (1 = serial on the context stream)."""
+        self.check(lib().coeb_set_batch_streams(self.h, int(n)))
 
     def debug_read(self, what, f=0):
         size = C.c_size_t()

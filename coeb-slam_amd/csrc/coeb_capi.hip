@@ -251,7 +251,11 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
     P.oct_lds = P.oct_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * P.oct_kl;
     if (P.oct_lds > 150 * 1024) { err = "octree LDS budget exceeded (features per level too large)"; return false; }
     memcpy(P.umax, t.umax, sizeof(P.umax));
+    // k_describe folds the IC_Angle disc (umax for HALF_PATCH_SIZE 15) into constants
+    static const int kUmaxDisc[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+    if (memcmp(t.umax, kUmaxDisc, sizeof(kUmaxDisc)) != 0) { err = "unexpected IC_Angle disc (umax)"; return false; }
     gauss_kernel7(P.gauss);
+
     return true;
 }
 
@@ -341,6 +345,18 @@ struct coeb_ctx {
     int batch_frames = 0;      // frames of the last extracted batch
     const uint8_t* batch_gray = nullptr;
     int ident_frames = 0;      // identity poses initialised in "b_I"
+    // Batch chunking over several HIP streams (coeb_set_batch_streams): chunk k = frames
+    // [chunk[k], chunk[k+1]) runs extract -> prep -> match on subs[k]; match of chunk k's first
+    // frame waits for chunk k-1's prep (its LastFrame).  The context stream joins the chunk
+    // streams lazily, before anything else is enqueued on it (main_stream()).
+    int nstreams = 1;
+    std::vector<hipStream_t> subs;
+    std::vector<int> chunk;                      // chunk boundaries of the last batch
+    std::vector<hipEvent_t> ev_prep, ev_mdone;   // per chunk: prep done / match done
+    bool mdone_valid = false;                    // ev_mdone holds the previous batch's matches
+    bool pending_join = false;
+    bool extract_chunked = false;                // the last batch extract ran on the chunk streams
+    hipEvent_t ev_main = nullptr, ev_join = nullptr;
 };
 
 namespace {
@@ -472,17 +488,76 @@ int upload_dyn(coeb_ctx* c, int F, const coeb_box* boxes, const int32_t* box_off
     return 0;
 }
 
+// The context stream, after it has been made to wait for every chunk stream of the last
+// batch (so work enqueued on it sees the batch's results).
+hipStream_t main_stream(coeb_ctx* c)
+{
+    if (c->pending_join) {
+        for (hipStream_t s : c->subs) {
+            (void)hipEventRecord(c->ev_join, s);
+            (void)hipStreamWaitEvent(c->stream, c->ev_join, 0);
+        }
+        c->pending_join = false;
+    }
+    return c->stream;
+}
+
+// Chunk boundaries for F frames over the context's batch streams (>= 16 frames per chunk).
+int make_chunks(coeb_ctx* c, int F)
+{
+    int n = std::max(1, std::min(c->nstreams, F / 16));
+    if (n > 1 && (int)c->subs.size() < n) {
+        while ((int)c->subs.size() < n) {
+            hipStream_t s;
+            hipEvent_t a, b;
+            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) break;
+            (void)hipEventCreateWithFlags(&a, hipEventDisableTiming);
+            (void)hipEventCreateWithFlags(&b, hipEventDisableTiming);
+            c->subs.push_back(s);
+            c->ev_prep.push_back(a);
+            c->ev_mdone.push_back(b);
+        }
+        n = std::min<int>(n, (int)c->subs.size());
+    }
+    c->chunk.assign(n + 1, 0);
+    for (int k = 0; k <= n; k++) c->chunk[k] = (int)((int64_t)F * k / n);
+    return n;
+}
+
+// Per-frame buffers of frames [f0, ...): every per-frame array advanced by f0 frames.
+ExtractBufs offset_bufs(const Plan& P, const ExtractBufs& b, int f0)
+{
+    ExtractBufs o = b;
+    o.gray = b.gray + (int64_t)f0 * P.W * P.H;
+    o.pyr = b.pyr + (int64_t)f0 * P.pyr_stride;
+    o.blur = b.blur + (int64_t)f0 * P.blur_stride;
+    o.cand_n = b.cand_n + (int64_t)f0 * P.ncells;
+    o.cand = b.cand + (int64_t)f0 * P.ncells * P.cell_cap;
+    o.keys = b.keys + (int64_t)f0 * 2 * P.kbuf_stride;
+    o.nodes = b.nodes + (int64_t)f0 * P.node_stride * 4;
+    o.lvl_n = b.lvl_n + (int64_t)f0 * P.L;
+    o.lvl_kp = b.lvl_kp + (int64_t)f0 * P.lvl_stride;
+    o.kps = static_cast<coeb_keypoint*>(b.kps) + (int64_t)f0 * P.kcap;
+    o.desc = b.desc + (int64_t)f0 * P.kcap * 32;
+    o.counts = b.counts + f0;
+    o.dyn = b.dyn + f0;
+    if (b.box_off) o.box_off = b.box_off + f0;   // offsets index the shared box / T_M arrays
+    if (b.tm_off) o.tm_off = b.tm_off + f0;
+    return o;
+}
+
 int check_err_word(coeb_ctx* c)
 {
+    main_stream(c);
     int* derr = static_cast<int*>(c->bufs["err"].p);
     if (!derr) return 0;
     int h = 0;
-    HIP_TRY(c, hipMemcpyAsync(&h, derr, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpyAsync(&h, derr, 4, hipMemcpyDeviceToHost, main_stream(c)));
+    HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
     if (h) {
         char msg[160];
         snprintf(msg, sizeof msg, "internal capacity exceeded (device error bits 0x%x)", h);
-        HIP_TRY(c, hipMemsetAsync(derr, 0, 4, c->stream));
+        HIP_TRY(c, hipMemsetAsync(derr, 0, 4, main_stream(c)));
         return set_err(c, COEB_ERANGE, msg);
     }
     return 0;
@@ -532,6 +607,12 @@ coeb_ctx* coeb_create(const coeb_orb_params* params, int device, int max_width, 
         return nullptr;
     }
     c->hook.impl = &c->prof;
+    if (hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        g_last_error = "coeb_create: event creation failed";
+        coeb_destroy(c);
+        return nullptr;
+    }
     int* err;
     if (ensure(c, "err", 4, &err) || hipMemset(err, 0, 16) != hipSuccess) {
         g_last_error = "coeb_create: device allocation failed";
@@ -545,11 +626,18 @@ void coeb_destroy(coeb_ctx* c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamSynchronize(main_stream(c));
     for (auto& kv : c->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     c->prof.drain();
     for (auto e : c->prof.pool) (void)hipEventDestroy(e);
+    for (size_t k = 0; k < c->subs.size(); k++) {
+        (void)hipStreamDestroy(c->subs[k]);
+        (void)hipEventDestroy(c->ev_prep[k]);
+        (void)hipEventDestroy(c->ev_mdone[k]);
+    }
+    if (c->ev_main) (void)hipEventDestroy(c->ev_main);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -597,13 +685,48 @@ int coeb_extract_batch_device(coeb_ctx* c, const uint8_t* d_gray, int F, int W, 
     int rc;
     if ((rc = ensure_plan(c, W, H))) return rc;
     ExtractBufs b;
+    const std::vector<int> prev_chunk = c->chunk;
+    const bool prev_mdone = c->mdone_valid;
+    const int n = make_chunks(c, F);
+    const bool has_dyn = (boxes && box_off) || (tm_xy && tm_off);
+    // per-frame buffers may be reallocated and the box / T_M staging rewritten: let every
+    // outstanding batch finish first in those cases
+    const bool serial = n == 1 || has_dyn || (c->batch_frames != F);
+    if (serial) main_stream(c);
     if ((rc = extract_bufs(c, F, b))) return rc;
     if ((rc = upload_dyn(c, F, boxes, box_off, tm_xy, tm_off, blur_flag, b))) return rc;
     b.gray = d_gray;
-    if (launch_extract(c->plan, static_cast<const Plan*>(c->bufs["plan"].p), b, F, c->stream, &c->hook))
-        return hip_err(c, hipGetLastError(), "launch_extract");
+    const Plan* dplan = static_cast<const Plan*>(c->bufs["plan"].p);
+    c->mdone_valid = false;
+    c->extract_chunked = n > 1;
+    if (n == 1) {
+        if (launch_extract(c->plan, dplan, b, F, main_stream(c), &c->hook)) return hip_err(c, hipGetLastError(), "launch_extract");
+    } else {
+        HIP_TRY(c, hipEventRecord(c->ev_main, c->stream));   // no join: steps overlap
+        const bool cross = !serial && prev_mdone && prev_chunk == c->chunk;
+        for (int k = 0; k < n; k++) {
+            hipStream_t s = c->subs[k];
+            HIP_TRY(c, hipStreamWaitEvent(s, c->ev_main, 0));
+            // the previous batch's matcher of chunk k+1 reads chunk k's last frame
+            if (cross && k + 1 < n) HIP_TRY(c, hipStreamWaitEvent(s, c->ev_mdone[k + 1], 0));
+            const int f0 = c->chunk[k], f1 = c->chunk[k + 1];
+            if (launch_extract(c->plan, dplan, offset_bufs(c->plan, b, f0), f1 - f0, s, &c->hook))
+                return hip_err(c, hipGetLastError(), "launch_extract");
+        }
+        c->pending_join = true;
+    }
     c->batch_frames = F;
     c->batch_gray = d_gray;
+    return COEB_OK;
+}
+
+int coeb_set_batch_streams(coeb_ctx* c, int nstreams)
+{
+    if (!c || nstreams < 1 || nstreams > 16) return set_err(c, COEB_EINVAL, "coeb_set_batch_streams: 1..16 streams");
+    (void)hipSetDevice(c->device);
+    main_stream(c);
+    c->nstreams = nstreams;
+    c->mdone_valid = false;
     return COEB_OK;
 }
 
@@ -632,7 +755,7 @@ int coeb_extract(coeb_ctx* c, const uint8_t* gray, int W, int H, size_t stride, 
     if ((rc = ensure_plan(c, W, H))) return rc;
     uint8_t* dgray;
     if ((rc = ensure(c, "gray_stage", (size_t)W * H, &dgray))) return rc;
-    HIP_TRY(c, hipMemcpy2DAsync(dgray, W, gray, stride, W, H, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpy2DAsync(dgray, W, gray, stride, W, H, hipMemcpyHostToDevice, main_stream(c)));
     int32_t box_off[2] = {0, nbox}, tm_off[2] = {0, ntm};
     std::vector<int32_t> blur(nbox, 0);
     for (int i = 0; i < nbox && i < nblur; i++) blur[i] = blur_flag[i];   // missing flags read as 0
@@ -642,20 +765,20 @@ int coeb_extract(coeb_ctx* c, const uint8_t* gray, int W, int H, size_t stride, 
                          nbox ? blur.data() : nullptr, b)))
         return rc;
     b.gray = dgray;
-    if (launch_extract(c->plan, static_cast<const Plan*>(c->bufs["plan"].p), b, 1, c->stream, &c->hook))
+    if (launch_extract(c->plan, static_cast<const Plan*>(c->bufs["plan"].p), b, 1, main_stream(c), &c->hook))
         return hip_err(c, hipGetLastError(), "launch_extract");
     c->batch_frames = 1;
     c->batch_gray = dgray;
     int n = 0;
-    HIP_TRY(c, hipMemcpyAsync(&n, b.counts, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpyAsync(&n, b.counts, 4, hipMemcpyDeviceToHost, main_stream(c)));
+    HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
     if ((rc = check_err_word(c))) return rc;
     *n_out = n;
     const int m = std::min(n, cap);
     if (m > 0 && kp_out)
-        HIP_TRY(c, hipMemcpyAsync(kp_out, b.kps, (size_t)m * sizeof(coeb_keypoint), hipMemcpyDeviceToHost, c->stream));
-    if (m > 0 && desc_out) HIP_TRY(c, hipMemcpyAsync(desc_out, b.desc, (size_t)m * 32, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, hipMemcpyAsync(kp_out, b.kps, (size_t)m * sizeof(coeb_keypoint), hipMemcpyDeviceToHost, main_stream(c)));
+    if (m > 0 && desc_out) HIP_TRY(c, hipMemcpyAsync(desc_out, b.desc, (size_t)m * 32, hipMemcpyDeviceToHost, main_stream(c)));
+    HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
     if (n > cap) return set_err(c, COEB_ERANGE, "keypoint output capacity too small");
     return COEB_OK;
 }
@@ -698,7 +821,7 @@ int coeb_match_lastframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curfram
         (rc = ensure(c, "m_match", cs, &dmatch)) || (rc = ensure(c, "m_nm", 1, &dnm)) ||
         (rc = ensure(c, "m_scr", (size_t)ls * kMatchCQ, &dscr)) || (rc = ensure(c, "err", 4, &derr)))
         return rc;
-    hipStream_t s = c->stream;
+    hipStream_t s = main_stream(c);
     int32_t cnts[2] = {n, nl};
     HIP_TRY(c, hipMemcpyAsync(dcn, cnts, 8, hipMemcpyHostToDevice, s));
     if (n) {
@@ -739,7 +862,7 @@ namespace {
 // Common body of the batch matchers.  dT_cur: device poses, pair p (current frame p+1) at
 // dT_cur + 16 p; LastFrame poses are identities (frame p is the world frame of its pair).
 int match_batch_impl(coeb_ctx* c, const float* d_depth, int F, int W, int H, const coeb_camera* cam,
-                     const float* dT_cur, float th, int32_t nobs)
+                     const float* dT_cur, float th, int32_t nobs, bool wait_main)
 {
     const int K = c->plan.kcap;
     if (K > kCurMax) return set_err(c, COEB_EINVAL, "keypoint capacity exceeds the matcher limit (4095)");
@@ -755,6 +878,7 @@ int match_batch_impl(coeb_ctx* c, const float* d_depth, int F, int W, int H, con
         return rc;
     if (c->ident_frames < F || !c->bufs.count("b_I")) {
         const int n = std::max(F, c->max_batch);
+        HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
         if ((rc = ensure(c, "b_I", (size_t)n * 16, &dI))) return rc;
         std::vector<float> I((size_t)n * 16, 0.f);
         for (int p = 0; p < n; p++) I[(size_t)p * 16 + 0] = I[(size_t)p * 16 + 5] = I[(size_t)p * 16 + 10] = I[(size_t)p * 16 + 15] = 1.f;
@@ -765,22 +889,47 @@ int match_batch_impl(coeb_ctx* c, const float* d_depth, int F, int W, int H, con
     const coeb_keypoint* kps = static_cast<const coeb_keypoint*>(c->bufs["kps"].p);
     const uint8_t* desc = static_cast<const uint8_t*>(c->bufs["desc"].p);
     const int32_t* counts = static_cast<const int32_t*>(c->bufs["counts"].p);
-    PrepBufs pb;
-    memset(&pb, 0, sizeof(pb));
-    pb.kps = kps; pb.n = counts; pb.stride = K; pb.depth = d_depth; pb.W = W; pb.H = H;
-    pb.bf = cam->bf; pb.fx = cam->fx; pb.fy = cam->fy; pb.cx = cam->cx; pb.cy = cam->cy;
-    pb.ur = ur; pb.dep = dep; pb.has = has; pb.outl = outl; pb.xw = xw; pb.nobs = nobsb; pb.nobs_value = nobs;
-    if (launch_prep(pb, F, c->stream, &c->hook)) return hip_err(c, hipGetLastError(), "launch_prep");
-    if (F < 2) return COEB_OK;
-    MatchBufs mb;
-    memset(&mb, 0, sizeof(mb));
-    mb.cur_kps = kps + K; mb.cur_desc = desc + (size_t)K * 32; mb.cur_n = counts + 1; mb.cur_ur = ur + K; mb.cur_stride = K;
-    mb.last_kps = kps; mb.last_desc = desc; mb.last_n = counts; mb.last_has = has; mb.last_out = outl;
-    mb.last_xw = xw; mb.last_nobs = nobsb; mb.last_stride = K;
-    mb.Tcw_cur = dT_cur; mb.Tcw_last = dI;
-    mb.match = match + K; mb.nmatch = nm + 1; mb.scratch = scr; mb.scratch_stride = K * kMatchCQ; mb.err = derr;
-    if (launch_match(make_cam(c, cam), mb, F - 1, th, 0, 1, 20, c->stream, &c->hook))
-        return hip_err(c, hipGetLastError(), "launch_match");
+    const MatchCam mcam = make_cam(c, cam);
+    // chunk k (frames [f0, f1)) on its stream: prep, then the pairs whose current frame is in
+    // the chunk; the first of them needs chunk k-1's last frame prepared
+    const bool chunked = c->extract_chunked && (int)c->chunk.size() > 2 && c->chunk.back() == F;
+    const int n = chunked ? (int)c->chunk.size() - 1 : 1;
+    if (!chunked) main_stream(c);
+    else if (wait_main) HIP_TRY(c, hipEventRecord(c->ev_main, c->stream));
+    for (int k = 0; k < n; k++) {
+        const int f0 = chunked ? c->chunk[k] : 0, f1 = chunked ? c->chunk[k + 1] : F;
+        hipStream_t s = chunked ? c->subs[k] : main_stream(c);
+        if (chunked && wait_main) HIP_TRY(c, hipStreamWaitEvent(s, c->ev_main, 0));
+        PrepBufs pb;
+        memset(&pb, 0, sizeof(pb));
+        const int64_t o = (int64_t)f0 * K;
+        pb.kps = kps + o; pb.n = counts + f0; pb.stride = K; pb.depth = d_depth + (int64_t)f0 * W * H; pb.W = W; pb.H = H;
+        pb.bf = cam->bf; pb.fx = cam->fx; pb.fy = cam->fy; pb.cx = cam->cx; pb.cy = cam->cy;
+        pb.ur = ur + o; pb.dep = dep + o; pb.has = has + o; pb.outl = outl + o; pb.xw = xw + 3 * o;
+        pb.nobs = nobsb + o; pb.nobs_value = nobs;
+        if (launch_prep(pb, f1 - f0, s, &c->hook)) return hip_err(c, hipGetLastError(), "launch_prep");
+        if (chunked) {
+            HIP_TRY(c, hipEventRecord(c->ev_prep[k], s));
+            if (k > 0) HIP_TRY(c, hipStreamWaitEvent(s, c->ev_prep[k - 1], 0));
+        }
+        const int p0 = std::max(f0, 1) - 1, np = f1 - std::max(f0, 1);   // pair p: current p+1, last p
+        if (np > 0) {
+            const int64_t q = (int64_t)p0 * K;
+            MatchBufs mb;
+            memset(&mb, 0, sizeof(mb));
+            mb.cur_kps = kps + q + K; mb.cur_desc = desc + (q + K) * 32; mb.cur_n = counts + p0 + 1; mb.cur_ur = ur + q + K;
+            mb.cur_stride = K;
+            mb.last_kps = kps + q; mb.last_desc = desc + q * 32; mb.last_n = counts + p0; mb.last_has = has + q;
+            mb.last_out = outl + q; mb.last_xw = xw + 3 * q; mb.last_nobs = nobsb + q; mb.last_stride = K;
+            mb.Tcw_cur = dT_cur + 16 * p0; mb.Tcw_last = dI + 16 * p0;
+            mb.match = match + q + K; mb.nmatch = nm + p0 + 1; mb.scratch = scr + q * kMatchCQ;
+            mb.scratch_stride = K * kMatchCQ; mb.err = derr;
+            if (launch_match(mcam, mb, np, th, 0, 1, 20, s, &c->hook)) return hip_err(c, hipGetLastError(), "launch_match");
+        }
+        if (chunked) HIP_TRY(c, hipEventRecord(c->ev_mdone[k], s));
+    }
+    c->mdone_valid = chunked;
+    if (chunked) c->pending_join = true;
     return COEB_OK;
 }
 
@@ -802,8 +951,9 @@ int coeb_match_batch_device(coeb_ctx* c, const float* d_depth, int F, int W, int
     (void)hipSetDevice(c->device);
     float* dT;
     if ((rc = ensure(c, "b_T", (size_t)F * 16, &dT))) return rc;
-    HIP_TRY(c, hipMemcpyAsync(dT, Tcw, (size_t)F * 64, hipMemcpyHostToDevice, c->stream));
-    return match_batch_impl(c, d_depth, F, W, H, cam, dT + 16, th, nobs);
+    // the previous batch's matchers may still read b_T: join them before overwriting it
+    HIP_TRY(c, hipMemcpyAsync(dT, Tcw, (size_t)F * 64, hipMemcpyHostToDevice, main_stream(c)));
+    return match_batch_impl(c, d_depth, F, W, H, cam, dT + 16, th, nobs, true);
 }
 
 int coeb_match_batch_device_tcw(coeb_ctx* c, const float* d_depth, int F, int W, int H, const coeb_camera* cam,
@@ -812,7 +962,7 @@ int coeb_match_batch_device_tcw(coeb_ctx* c, const float* d_depth, int F, int W,
     int rc;
     if ((rc = match_batch_check(c, d_depth, F, W, H, cam, d_Tcw))) return rc;
     (void)hipSetDevice(c->device);
-    return match_batch_impl(c, d_depth, F, W, H, cam, d_Tcw + 16, th, nobs);
+    return match_batch_impl(c, d_depth, F, W, H, cam, d_Tcw + 16, th, nobs, false);
 }
 
 int coeb_batch_match_results(coeb_ctx* c, const int32_t** d_match, const int32_t** d_nmatches)
@@ -837,17 +987,17 @@ int coeb_stereo_from_rgbd(coeb_ctx* c, const coeb_keypoint* kps, int n, const fl
     if ((rc = ensure(c, "s_k", n, &dk)) || (rc = ensure(c, "s_d", (size_t)W * H, &dd)) || (rc = ensure(c, "s_ur", n, &dur)) ||
         (rc = ensure(c, "s_dep", n, &ddep)) || (rc = ensure(c, "s_n", 1, &dn)))
         return rc;
-    HIP_TRY(c, hipMemcpyAsync(dk, kps, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipMemcpy2DAsync(dd, (size_t)W * 4, depth, dstride * 4, (size_t)W * 4, H, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(dn, &n, 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(dk, kps, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, main_stream(c)));
+    HIP_TRY(c, hipMemcpy2DAsync(dd, (size_t)W * 4, depth, dstride * 4, (size_t)W * 4, H, hipMemcpyHostToDevice, main_stream(c)));
+    HIP_TRY(c, hipMemcpyAsync(dn, &n, 4, hipMemcpyHostToDevice, main_stream(c)));
     PrepBufs pb;
     memset(&pb, 0, sizeof(pb));
     pb.kps = dk; pb.n = dn; pb.stride = n; pb.depth = dd; pb.W = W; pb.H = H; pb.bf = bf; pb.fx = 1; pb.fy = 1;
     pb.ur = dur; pb.dep = ddep;
-    if (launch_prep(pb, 1, c->stream, &c->hook)) return hip_err(c, hipGetLastError(), "launch_prep");
-    HIP_TRY(c, hipMemcpyAsync(ur_out, dur, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(dep_out, ddep, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (launch_prep(pb, 1, main_stream(c), &c->hook)) return hip_err(c, hipGetLastError(), "launch_prep");
+    HIP_TRY(c, hipMemcpyAsync(ur_out, dur, (size_t)n * 4, hipMemcpyDeviceToHost, main_stream(c)));
+    HIP_TRY(c, hipMemcpyAsync(dep_out, ddep, (size_t)n * 4, hipMemcpyDeviceToHost, main_stream(c)));
+    HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
     return COEB_OK;
 }
 
@@ -916,7 +1066,7 @@ int coeb_device_free(coeb_ctx* c, void* dptr)
 {
     if (!c) return COEB_EINVAL;
     (void)hipSetDevice(c->device);
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
     if (dptr) HIP_TRY(c, hipFree(dptr));
     return COEB_OK;
 }
@@ -925,8 +1075,8 @@ int coeb_memcpy_h2d(coeb_ctx* c, void* dst, const void* src, size_t bytes)
 {
     if (!c || (bytes && (!dst || !src))) return COEB_EINVAL;
     (void)hipSetDevice(c->device);
-    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, main_stream(c)));
+    HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
     return COEB_OK;
 }
 
@@ -934,15 +1084,15 @@ int coeb_memcpy_d2h(coeb_ctx* c, void* dst, const void* src, size_t bytes)
 {
     if (!c || (bytes && (!dst || !src))) return COEB_EINVAL;
     (void)hipSetDevice(c->device);
-    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, main_stream(c)));
+    HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
     return COEB_OK;
 }
 
 int coeb_internal_stream(coeb_ctx* c, hipStream_t* s, int* device)
 {
     if (!c) return COEB_EINVAL;
-    *s = c->stream;
+    *s = main_stream(c);
     *device = c->device;
     return COEB_OK;
 }
@@ -977,7 +1127,7 @@ int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t byt
     else return COEB_EINVAL;
     if (size_out) *size_out = n;
     if (host && bytes) {
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
         HIP_TRY(c, hipMemcpy(host, src, std::min(bytes, n), hipMemcpyDeviceToHost));
     }
     return COEB_OK;
@@ -987,7 +1137,7 @@ int coeb_synchronize(coeb_ctx* c)
 {
     if (!c) return COEB_EINVAL;
     (void)hipSetDevice(c->device);
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
     return check_err_word(c);
 }
 

@@ -437,7 +437,6 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
 //  4. NMS over the corner list at iniThFAST (fallback minThFAST if the cell came out empty,
 //     :834-838) with ordered (ballot) stores of the kept keys.  A cell with more corners than
 //     the list holds walks the whole window instead.
-constexpr int kRoiMax = 64;                // FAST cell ROI limit (make_plan)
 constexpr int kFastRowBytes = 72;          // >= 1 + 64 + 7 (slab byte = ROI column + 1)
 constexpr int kFastSurv = 512;             // survivor list (flushed when one more pass could overflow it)
 constexpr int kFastCorners = 512;          // corner list
@@ -1390,89 +1389,263 @@ __device__ void sincos_canon(float af, float* s, float* c)
 
 struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
 
-// Two keypoints per wave (one per 32-lane half) so each lane has 31 patch loads in flight
-// and every lane produces exactly one descriptor byte (8 tests).
+// kDescKp (32) keypoints of one frame per wave, in three phases:
+//   A  lanes k and k+32 = keypoint k: IC_Angle from 16-byte row loads of the unblurred level,
+//      the two halves taking rows -|v| and +|v| (the disc weights depend on |v| only, so they
+//      are compile-time constants for both), realigned in registers so byte j of a row is
+//      patch column j-15; each 4-pixel group costs two v_dot4_u32_u8.  fastAtan2 and the
+//      canonical sincosf run once per keypoint; the cv::KeyPoint record is written here.
+//   B  kDescGroup keypoints per step: their 37 x 64 B blurred patches are staged in the wave's
+//      LDS slab (the next group's are loaded into registers meanwhile); lane = 4 of the 256
+//      tests of each; the nibbles are OR-combined by DPP into the descriptor dwords (LDS).
+//   C  the wave's descriptors (32 x 32 B) are written out with 16-byte stores.
+// Few wide loads per keypoint: with one byte per lane per load (lane = patch column) the
+// texture-address path, not the VALU, bounded this kernel.
+// The rotated pattern offsets are cvRound of |(px, py)| <= 13*sqrt(2), so |offset| <= 18.
+constexpr int kBlRow = 64, kBlRows = 37, kBlChunks = kBlRows * 4;   // 148 16-byte chunks
+constexpr int kDescKp = 32;                                          // keypoints per wave
+constexpr int kDescGroup = 2;                                        // patches staged per step
+constexpr int kDescSlab = kBlRow * kBlRows * kDescGroup + 32 * kDescKp;   // 5760 B per wave
+constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};   // ORBextractor.cc:461-476
+
+// Weights of aligned row dword d (patch columns j = 4d..4d+3, u = j - 15) in row |v| = av:
+// W1 = bytes (j * in), W0 = bytes (in), in = |u| <= umax[av].
+__device__ __forceinline__ constexpr uint32_t ic_w(int av, int d, bool with_j)
+{
+    uint32_t w = 0;
+    for (int i = 0; i < 4; i++) {
+        const int j = 4 * d + i, u = j - 15;
+        const bool in = (u < 0 ? -u : u) <= kUmax[av];
+        w |= (uint32_t)(in ? (with_j ? j : 1) : 0) << (8 * i);
+    }
+    return w;
+}
+
+__device__ __forceinline__ uint32_t dpp_or_xor1(uint32_t v)   // quad_perm [1,0,3,2]
+{
+    return v | (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_or_xor2(uint32_t v)   // quad_perm [2,3,0,1]
+{
+    return v | (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_or_shl4(uint32_t v)   // lane i |= lane i+4 (row_shl:4)
+{
+    return v | (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xf, 0xf, false);
+}
+
+// One IC row: 48 bytes from 16-byte aligned `rp` (kVec) or byte loads.
+template <bool kVec>
+__device__ __forceinline__ void ic_row_load(const uint8_t* rp, uint4& c0, uint4& c1, uint4& c2)
+{
+    if (kVec) {
+        c0 = reinterpret_cast<const uint4*>(rp)[0];
+        c1 = reinterpret_cast<const uint4*>(rp)[1];
+        c2 = reinterpret_cast<const uint4*>(rp)[2];
+    } else {
+        uint32_t q[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++)
+            q[k] = (uint32_t)rp[4 * k] | ((uint32_t)rp[4 * k + 1] << 8) | ((uint32_t)rp[4 * k + 2] << 16) |
+                   ((uint32_t)rp[4 * k + 3] << 24);
+        c0 = make_uint4(q[0], q[1], q[2], q[3]);
+        c1 = make_uint4(q[4], q[5], q[6], q[7]);
+        c2 = make_uint4(q[8], q[9], q[10], q[11]);
+    }
+}
+
+// Disc sums of row |v| = av from its 48-byte window (byte a = patch column 0): A += sum j*p,
+// returns the row sum.
+template <int av>
+__device__ __forceinline__ uint32_t ic_row_acc(uint4 c0, uint4 c1, uint4 c2, int a, uint32_t m8, uint32_t m4, uint32_t& A)
+{
+    const uint32_t q[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+    // realign by a: bit selects (ternaries become a scratch-indexed array), then alignbyte
+    uint32_t r1[10], r2[9];
+#pragma unroll
+    for (int k = 0; k < 10; k++) r1[k] = (m8 & q[k + 2]) | (~m8 & q[k]);
+#pragma unroll
+    for (int k = 0; k < 9; k++) r2[k] = (m4 & r1[k + 1]) | (~m4 & r1[k]);
+    uint32_t rs = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+        const uint32_t w1 = ic_w(av, d, true), w0 = ic_w(av, d, false);
+        if (w0 == 0) continue;
+        const uint32_t o = __builtin_amdgcn_alignbyte(r2[d + 1], r2[d], (uint32_t)(a & 3));
+        A = __builtin_amdgcn_udot4(o, w1, A, false);
+        rs = __builtin_amdgcn_udot4(o, w0, rs, false);
+    }
+    return rs;
+}
+
+// Rows |v| = av0 .. av0+3 at row offsets sgn*|v| from `rowp` (4 rows of loads in flight).
+template <bool kVec, int av0>
+__device__ __forceinline__ void ic_rows4(const uint8_t* rowp, int64_t spitch, int a, uint32_t m8, uint32_t m4,
+                                         uint32_t& A, uint32_t& S, int& m01, uint32_t& A0, uint32_t& S0)
+{
+    uint4 c[4][3];
+#pragma unroll
+    for (int r = 0; r < 4; r++) ic_row_load<kVec>(rowp + (av0 + r) * spitch, c[r][0], c[r][1], c[r][2]);
+#define COEB_IC_ACC(r)                                                                   \
+    {                                                                                    \
+        constexpr int av = av0 + r;                                                      \
+        if constexpr (av == 0) {                                                         \
+            S0 += ic_row_acc<0>(c[r][0], c[r][1], c[r][2], a, m8, m4, A0);               \
+        } else {                                                                         \
+            const uint32_t rs = ic_row_acc<av>(c[r][0], c[r][1], c[r][2], a, m8, m4, A); \
+            S += rs;                                                                     \
+            m01 += av * (int)rs;                                                         \
+        }                                                                                \
+    }
+    COEB_IC_ACC(0) COEB_IC_ACC(1) COEB_IC_ACC(2) COEB_IC_ACC(3)
+#undef COEB_IC_ACC
+}
+
+template <bool kVec0>
 __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ P, ExtractBufs b)
 {
-    __shared__ int off[COEB_MAXL + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_slab[kWaves][kDescSlab];
     const int f = blockIdx.y;
     const int L = P->L;
-    if (threadIdx.x == 0) {
-        int s = 0;
-        for (int l = 0; l < L; l++) { off[l] = s; s += b.lvl_n[(int64_t)f * L + l]; }
-        off[L] = s;
-        if (blockIdx.x == 0) b.counts[f] = s;
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    // per-level keypoint offsets (wave prefix over lanes 0..L-1)
+    const int nl = lane < L ? b.lvl_n[(int64_t)f * L + lane] : 0;
+    int incl = nl;
+    for (int o = 1; o < COEB_MAXL; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
     }
-    __syncthreads();
-    const int total = off[L];
-    const int lane = lane_id(), hl = lane & 31;
-    const int idx = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * 2 + (lane >> 5);
-    if (idx >= total) return;          // whole 32-lane halves only: the shuffles stay in-half
-    int l = 0;
-    while (l + 1 < L && idx >= off[l + 1]) l++;
+    const int total = __builtin_amdgcn_readlane(incl, L - 1);
+    if (blockIdx.x == 0 && threadIdx.x == 0) b.counts[f] = total;
+    const int idx0 = (blockIdx.x * kWaves + wv) * kDescKp;
+    if (idx0 >= total) return;
+    const int nk = min(kDescKp, total - idx0);
+    // ---- phase A: lanes k, k+32 = keypoint idx0 + k (excess repeat the last one, no writes)
+    const int kq = lane & 31, half = lane >> 5;
+    const int id = idx0 + min(kq, nk - 1);
+    int l = 0, start = 0;
+    for (int q = 0; q < L - 1; q++) {
+        const int e = __builtin_amdgcn_readlane(incl, q);      // end of level q
+        if (id >= e) { l = q + 1; start = e; }
+    }
     const LevelGeom& g = P->lv[l];
-    const uint32_t key = b.lvl_kp[(int64_t)f * P->lvl_stride + g.out_off + (idx - off[l])];
+    const uint32_t key = b.lvl_kp[(int64_t)f * P->lvl_stride + g.out_off + (id - start)];
     const int x = key_x(key), y = key_y(key), sc = key_s(key);
-    const int st = g.pitch, bst = g.bpitch;
-    // IC_Angle (ORBextractor.cc:80-107): lane = patch column u in [-15, 15] (lane 31 idle);
-    // row v is inside the disc iff |u| <= umax[|v|]
     const uint8_t* img = level_ptr(P, b, f, l);
-    const uint8_t* col = img + (int64_t)y * st + x + (hl - 15);
-    const int u = hl - 15;
-    const int au = u < 0 ? -u : u;
-    int pv[31];
-#pragma unroll
-    for (int j = 0; j < 31; j++) pv[j] = col[(j - 15) * st];
-    int m10 = 0, m01 = 0;
-#pragma unroll
-    for (int j = 0; j < 31; j++) {
-        const int v = j - 15;
-        const int av = v < 0 ? -v : v;
-        if (hl < 31 && au <= P->umax[av]) {
-            m10 += u * pv[j];
-            m01 += v * pv[j];
-        }
+    // IC_Angle (ORBextractor.cc:80-107): A = sum j*p, S = sum p over the disc, m01 = sum v*rowsum
+    uint32_t A = 0, S = 0, A0 = 0, S0 = 0;
+    int m01 = 0;
+    const int a = (x - 15) & 15;
+    const uint32_t m8 = (a & 8) ? 0xFFFFFFFFu : 0u, m4 = (a & 4) ? 0xFFFFFFFFu : 0u;
+    const uint8_t* rowp = img + (int64_t)y * g.pitch + (x - 15 - a);         // row v = 0
+    const int64_t spitch = half ? (int64_t)g.pitch : -(int64_t)g.pitch;      // rows +|v| / -|v|
+    if (kVec0 || l != 0) {
+        ic_rows4<true, 0>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
+        ic_rows4<true, 4>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
+        ic_rows4<true, 8>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
+        ic_rows4<true, 12>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
+    } else {
+        ic_rows4<false, 0>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
+        ic_rows4<false, 4>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
+        ic_rows4<false, 8>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
+        ic_rows4<false, 12>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
     }
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-        m10 += __shfl_xor(m10, o, 64);
-        m01 += __shfl_xor(m01, o, 64);
+    if (half == 0) {                   // lower half: rows -|v| (and row 0, counted once)
+        m01 = -m01;
+        A += A0;
+        S += S0;
     }
+    A += __shfl_xor(A, 32, 64);
+    S += __shfl_xor(S, 32, 64);
+    m01 += __shfl_xor(m01, 32, 64);
+    const int m10 = (int)A - 15 * (int)S;
     const float angle = fast_atan2_dev((float)m01, (float)m10);
-    // descriptor (ORBextractor.cc:109-156), fused rotation forms of the reference binary
     const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
     float bs, ac;
     sincos_canon(angle * factorPI, &bs, &ac);
-    const uint8_t* bl = b.blur + (int64_t)f * P->blur_stride + g.blur_off + (int64_t)y * bst + x;
-    const int4* pat = reinterpret_cast<const int4*>(b.pattern) + 2 * hl;   // tests 8*hl .. 8*hl+7
-    const int4 pa = pat[0], pb = pat[1];
-    int byte = 0;
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        const int pw = t == 0 ? pa.x : t == 1 ? pa.y : t == 2 ? pa.z : t == 3 ? pa.w
-                     : t == 4 ? pb.x : t == 5 ? pb.y : t == 6 ? pb.z : pb.w;
-        const float px0 = (float)(int8_t)(pw & 0xff), py0 = (float)(int8_t)((pw >> 8) & 0xff);
-        const float px1 = (float)(int8_t)((pw >> 16) & 0xff), py1 = (float)(int8_t)(pw >> 24);
-        const int r0 = (int)rintf(__builtin_fmaf(px0, bs, py0 * ac));
-        const int c0 = (int)rintf(__builtin_fmaf(px0, ac, -(py0 * bs)));
-        const int r1 = (int)rintf(__builtin_fmaf(px1, bs, py1 * ac));
-        const int c1 = (int)rintf(__builtin_fmaf(px1, ac, -(py1 * bs)));
-        const int t0 = bl[r0 * bst + c0], t1 = bl[r1 * bst + c1];
-        byte |= (t0 < t1) << t;
-    }
-    b.desc[((int64_t)f * P->kcap + idx) * 32 + hl] = (uint8_t)byte;
-    if (hl == 0) {
+    if (half == 0 && kq < nk) {        // cv::KeyPoint {x, y, size, angle, response, octave, class_id}
+        float fx = (float)x, fy = (float)y;
+        if (l != 0) { fx *= g.scale; fy *= g.scale; }          // :1327-1334
         KeyPointOut o;
-        o.x = (float)x;
-        o.y = (float)y;
-        if (l != 0) { o.x *= g.scale; o.y *= g.scale; }          // :1327-1334
-        o.size = (float)g.size_i;
-        o.angle = angle;
-        o.response = (float)sc;
-        o.octave = l;
-        o.class_id = -1;
-        reinterpret_cast<KeyPointOut*>(b.kps)[(int64_t)f * P->kcap + idx] = o;
+        o.x = fx; o.y = fy; o.size = (float)g.size_i; o.angle = angle; o.response = (float)sc;
+        o.octave = l; o.class_id = -1;
+        reinterpret_cast<KeyPointOut*>(b.kps)[(int64_t)f * P->kcap + idx0 + kq] = o;
     }
+    // ---- phase B: descriptors (ORBextractor.cc:109-156), kDescGroup keypoints per step
+    const int4 pa = reinterpret_cast<const int4*>(b.pattern)[lane];   // tests 4*lane .. 4*lane+3
+    float px0[4], py0[4], px1[4], py1[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int pw = t == 0 ? pa.x : t == 1 ? pa.y : t == 2 ? pa.z : pa.w;
+        px0[t] = (float)(int8_t)(pw & 0xff); py0[t] = (float)(int8_t)((pw >> 8) & 0xff);
+        px1[t] = (float)(int8_t)((pw >> 16) & 0xff); py1[t] = (float)(int8_t)(pw >> 24);
+    }
+    uint8_t* slab = s_slab[wv];
+    uint32_t* dsl = reinterpret_cast<uint32_t*>(slab + kBlRow * kBlRows * kDescGroup);
+    // per keypoint: blurred patch origin (16-aligned) relative to the frame's blur block
+    const int porg = (int)g.blur_off + (y - 18) * g.bpitch + ((x - 18) & ~15);
+    const int xoff = x - ((x - 18) & ~15);        // patch column of the keypoint
+    const uint8_t* blur_f = b.blur + (int64_t)f * P->blur_stride;
+    const int bpitch = g.bpitch;
+    static_assert(kDescGroup == 2, "staging below is written for 2 patches per step");
+    uint4 qa0, qa1, qa2, qb0, qb1, qb2;
+    const int e0 = lane, e1 = lane + 64, e2 = min(lane + 128, kBlChunks - 1);
+    const int eo0 = (e0 >> 2), eo1 = (e1 >> 2), eo2 = (e2 >> 2);
+    const int ec0 = 16 * (e0 & 3), ec1 = 16 * (e1 & 3), ec2 = 16 * (e2 & 3);
+#define COEB_LOAD_PATCH(t, q0, q1, q2)                                                          \
+    {                                                                                           \
+        const int tt_ = min((t), nk - 1);                                                       \
+        const uint8_t* o_ = blur_f + __builtin_amdgcn_readlane(porg, tt_);                      \
+        const int bpt_ = __builtin_amdgcn_readlane(bpitch, tt_);                                \
+        q0 = *reinterpret_cast<const uint4*>(o_ + eo0 * bpt_ + ec0);                            \
+        q1 = *reinterpret_cast<const uint4*>(o_ + eo1 * bpt_ + ec1);                            \
+        q2 = *reinterpret_cast<const uint4*>(o_ + eo2 * bpt_ + ec2);                            \
+    }
+    COEB_LOAD_PATCH(0, qa0, qa1, qa2)
+    COEB_LOAD_PATCH(1, qb0, qb1, qb2)
+    for (int t0 = 0; t0 < nk; t0 += kDescGroup) {
+        {
+            uint4* pd = reinterpret_cast<uint4*>(slab);
+            pd[lane] = qa0;
+            pd[lane + 64] = qa1;
+            if (lane + 128 < kBlChunks) pd[lane + 128] = qa2;
+            pd += kBlRow * kBlRows / 16;
+            pd[lane] = qb0;
+            pd[lane + 64] = qb1;
+            if (lane + 128 < kBlChunks) pd[lane + 128] = qb2;
+        }
+        wave_sync_lds();
+        if (t0 + kDescGroup < nk) {
+            COEB_LOAD_PATCH(t0 + 2, qa0, qa1, qa2)
+            COEB_LOAD_PATCH(t0 + 3, qb0, qb1, qb2)
+        }
+#pragma unroll
+        for (int k = 0; k < kDescGroup; k++) {
+            const int t = t0 + k;
+            if (t >= nk) break;
+            const float tb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bs), t));
+            const float ta = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ac), t));
+            const uint8_t* bc = slab + k * kBlRow * kBlRows + 18 * kBlRow + __builtin_amdgcn_readlane(xoff, t);
+            uint32_t nib = 0;
+#pragma unroll
+            for (int tt = 0; tt < 4; tt++) {
+                const int r0 = (int)rintf(__builtin_fmaf(px0[tt], tb, py0[tt] * ta));
+                const int c0 = (int)rintf(__builtin_fmaf(px0[tt], ta, -(py0[tt] * tb)));
+                const int r1 = (int)rintf(__builtin_fmaf(px1[tt], tb, py1[tt] * ta));
+                const int c1 = (int)rintf(__builtin_fmaf(px1[tt], ta, -(py1[tt] * tb)));
+                nib |= (uint32_t)(bc[r0 * kBlRow + c0] < bc[r1 * kBlRow + c1]) << tt;
+            }
+            // bit k of byte i = test 8i+k: dword d = nibbles of lanes 8d .. 8d+7
+            uint32_t dw = nib << (4 * (lane & 7));
+            dw = dpp_or_shl4(dpp_or_xor2(dpp_or_xor1(dw)));
+            if ((lane & 7) == 0) dsl[8 * t + (lane >> 3)] = dw;
+        }
+        wave_sync_lds();                         // patch reads done before the next staging
+    }
+#undef COEB_LOAD_PATCH
+    // ---- phase C: descriptors out
+    uint4* gd = reinterpret_cast<uint4*>(b.desc + ((int64_t)f * P->kcap + idx0) * 32);
+    if (lane < 2 * nk) gd[lane] = reinterpret_cast<const uint4*>(dsl)[lane];
 }
 
 }  // namespace
@@ -1518,7 +1691,8 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     hipLaunchKernelGGL(k_octree, dim3(plan.L, F), dim3(kThreads), plan.oct_lds, s, d_plan, b);
     prof_end(prof, s);
     prof_begin(prof, "k_describe", s);
-    hipLaunchKernelGGL(k_describe, dim3((plan.kcap + 2 * kWaves - 1) / (2 * kWaves), F), dim3(kThreads), 0, s, d_plan, b);
+    const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
+    hipLaunchKernelGGL(vec0 ? k_describe<true> : k_describe<false>, dim3((plan.kcap + kWaves * kDescKp - 1) / (kWaves * kDescKp), F), dim3(kThreads), 0, s, d_plan, b);
     prof_end(prof, s);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

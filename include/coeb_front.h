@@ -132,7 +132,9 @@ int coeb_extract(coeb_ctx* ctx, const uint8_t* gray, int width, int height, size
  * d_gray: device pointer, nframes x height x width bytes, packed.  boxes/T_M/blur flags are
  * host arrays: per frame f, boxes[box_off[f] .. box_off[f+1]) etc. (offset arrays of length
  * nframes+1; all may be NULL for "no boxes").  Results stay on the device; fetch them with
- * coeb_batch_results.  Enqueued on the context stream; returns without synchronising. */
+ * coeb_batch_results.  Returns without synchronising: the frames are split into contiguous
+ * chunks, one per batch stream (coeb_set_batch_streams), so the kernels of different chunks
+ * overlap on the device; every other call on the context waits for them. */
 int coeb_extract_batch_device(coeb_ctx* ctx, const uint8_t* d_gray, int nframes, int width, int height,
                               const coeb_box* boxes, const int32_t* box_off,
                               const float* tm_xy, const int32_t* tm_off,
@@ -141,6 +143,9 @@ int coeb_extract_batch_device(coeb_ctx* ctx, const uint8_t* d_gray, int nframes,
  * [nframes][kcap][32], counts [nframes]. */
 int coeb_batch_results(coeb_ctx* ctx, const coeb_keypoint** d_kps, const uint8_t** d_desc,
                        const int32_t** d_counts, int* kcap);
+/* Number of HIP streams a batch is spread over (1..16, default 1; chunks of >= 16 frames).
+ * 1 = every kernel of the batch on the context stream, one after another. */
+int coeb_set_batch_streams(coeb_ctx* ctx, int nstreams);
 
 /* Batch TrackWithMotionModel matching (Tracking.cc:933-958 call pattern): for f = 1..nframes-1
  * frame f is matched to frame f-1 of the last extracted batch.  Frame f-1 is the LastFrame and

@@ -322,3 +322,46 @@ def test_batch_B_full_size_properties(oracle_mod):
                 assert len(np.unique(used)) == len(used)     # a LastFrame point matches at most once
     finally:
         bp.close()
+
+
+def test_batch_streams_agree(oracle_mod, ex):
+    """The batch chunked over 4 HIP streams (kernels of different chunks overlapping, several
+    steps enqueued back to back) gives the same bits as the serial single-stream batch, and the
+    frames on either side of each chunk boundary match the oracle."""
+    from coeb_front.pipeline import BatchPipeline
+    F = 65
+    fr = synth.make_frames(640, 480, F, seed=777)
+    bp = BatchPipeline(640, 480, F)
+    try:
+        bp.load(fr, Tcw=np.stack([synth.motion_pose()] * F))
+        res = {}
+        for ns in (1, 4, 3, 1):
+            bp.ctx.set_batch_streams(ns)
+            for _ in range(3):
+                bp.run()
+            bp.synchronize()
+            res.setdefault(ns, []).append(bp.results())
+        out1, m1, n1 = res[1][0]
+        for ns, runs in res.items():
+            for out, m, n in runs:
+                assert n == n1, ns
+                for f in range(F):
+                    assert np.array_equal(out[f][0], out1[f][0]) and np.array_equal(out[f][1], out1[f][1]), (ns, f)
+                    if f:
+                        assert np.array_equal(m[f], m1[f]), (ns, f)
+        depth = synth.make_depth(640, 480)
+        cam_o = oracle_mod.camera(ex, 640, 480, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+        I4 = np.eye(4, dtype=np.float32)
+        for f in (16, 32, 48):       # 4-chunk boundaries: frame f is the first of its chunk
+            rp, r = ex.extract(fr[f - 1]), ex.extract(fr[f])
+            assert_same(out1[f][0], out1[f][1], r["kps"], r["desc"], "f%d" % f)
+            last = oracle_mod.mapframe_from_extraction(rp["kps"], rp["desc"], depth, synth.TUM_FX, synth.TUM_FY,
+                                                       synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+            ur, _ = oracle_mod.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
+            nm, mm = oracle_mod.search_by_projection(cam_o, r["kps"], r["desc"], ur, last, synth.motion_pose(), I4, 15.0)
+            if nm < 20:
+                nm, mm = oracle_mod.search_by_projection(cam_o, r["kps"], r["desc"], ur, last, synth.motion_pose(), I4,
+                                                         30.0)
+            assert n1[f] == nm and np.array_equal(m1[f], mm), f
+    finally:
+        bp.close()
