@@ -573,7 +573,15 @@ constexpr int kFastPass = 12;            // prefetched ROI rows / 4 (cells up to
 struct FastCellGeom {
     const uint8_t* img;
     int pitch, x0, y0, rw, rh, nwords;
+    bool vec;                          // 16-byte aligned rows, row fits 12 words, <= 48 rows
     bool words;                        // pitch % 4 == 0 and the row fits 15 words
+};
+
+// ROI prefetch registers: 16-byte path (lane = row (lane >> 2) + 16 i, chunk lane & 3) or
+// word path (lane = row (lane >> 4) + 4 i, word lane & 15).
+struct FastRegs {
+    uint4 v0, v1, v2;
+    uint32_t q0[kFastPass];
 };
 
 __device__ __forceinline__ FastCellGeom fast_geom(const Plan* P, const ExtractBufs& b, int f, const CellDesc& c)
@@ -584,14 +592,24 @@ __device__ __forceinline__ FastCellGeom fast_geom(const Plan* P, const ExtractBu
     G.pitch = g.pitch;
     G.x0 = c.x0; G.y0 = c.y0; G.rw = c.rw; G.rh = c.rh;
     G.nwords = (1 + c.rw + 3) >> 2;
+    G.vec = ((g.pitch | (int)reinterpret_cast<uintptr_t>(G.img)) & 15) == 0 && G.nwords <= 12 && c.rh <= 48;
     G.words = (g.pitch & 3) == 0 && G.nwords <= 15 && c.rh <= 4 * kFastPass;
     return G;
 }
 
-__device__ __forceinline__ void fast_prefetch(const FastCellGeom& G, uint32_t q0[kFastPass])
+__device__ __forceinline__ void fast_prefetch(const FastCellGeom& G, FastRegs& R)
 {
-    if (!G.words) return;
     const int lane = lane_id();
+    if (G.vec) {
+        // three 16-byte loads per lane cover 48 rows x 64 bytes from (x0 - 1) & ~15
+        const uint8_t* base = G.img + (int64_t)G.y0 * G.pitch + ((G.x0 - 1) & ~15) + 16 * (lane & 3);
+        const int r = lane >> 2;
+        R.v0 = *reinterpret_cast<const uint4*>(base + (int64_t)min(r, G.rh - 1) * G.pitch);
+        R.v1 = *reinterpret_cast<const uint4*>(base + (int64_t)min(r + 16, G.rh - 1) * G.pitch);
+        R.v2 = *reinterpret_cast<const uint4*>(base + (int64_t)min(r + 32, G.rh - 1) * G.pitch);
+        return;
+    }
+    if (!G.words) return;
     const int gx = G.x0 - 1;
     const int k = min(lane & 15, G.nwords);
     const uint32_t* base = reinterpret_cast<const uint32_t*>(G.img + (int64_t)G.y0 * G.pitch + (gx & ~3)) + k;
@@ -599,13 +617,42 @@ __device__ __forceinline__ void fast_prefetch(const FastCellGeom& G, uint32_t q0
     const int npass = (G.rh + 3) >> 2;
 #pragma unroll
     for (int i = 0; i < kFastPass; i++)
-        if (i < npass) q0[i] = base[min((lane >> 4) + 4 * i, G.rh - 1) * pw];
+        if (i < npass) R.q0[i] = base[min((lane >> 4) + 4 * i, G.rh - 1) * pw];
 }
 
-__device__ __forceinline__ void fast_stage(const FastCellGeom& G, const uint32_t q0[kFastPass], uint8_t* roi)
+// One 16-byte chunk of the vec path realigned by sh = (x0 - 1) & 15 (wave-uniform): slab
+// dwords 4c .. 4c+3 of the lane's row = source bytes sh + 16c .. sh + 16c + 15, taken from this
+// lane's chunk and the next lane's (DPP; chunk 3 is never stored, so its neighbour is moot).
+__device__ __forceinline__ void fast_stage_chunk(uint4 q, uint32_t m2, uint32_t m1, uint32_t bsh, uint8_t* dst,
+                                                 bool store)
+{
+    const uint32_t w[8] = {q.x, q.y, q.z, q.w, dpp_shl1(q.x), dpp_shl1(q.y), dpp_shl1(q.z), dpp_shl1(q.w)};
+    uint32_t w2[6], w1[5];
+#pragma unroll
+    for (int k = 0; k < 6; k++) w2[k] = (m2 & w[k + 2]) | (~m2 & w[k]);
+#pragma unroll
+    for (int k = 0; k < 5; k++) w1[k] = (m1 & w2[k + 1]) | (~m1 & w2[k]);
+    if (store) {
+        uint2* d = reinterpret_cast<uint2*>(dst);
+        d[0] = make_uint2(__builtin_amdgcn_alignbyte(w1[1], w1[0], bsh), __builtin_amdgcn_alignbyte(w1[2], w1[1], bsh));
+        d[1] = make_uint2(__builtin_amdgcn_alignbyte(w1[3], w1[2], bsh), __builtin_amdgcn_alignbyte(w1[4], w1[3], bsh));
+    }
+}
+
+__device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs& R, uint8_t* roi)
 {
     const int lane = lane_id();
-    if (G.words) {
+    if (G.vec) {
+        const int sh = (G.x0 - 1) & 15;
+        const uint32_t m2 = (sh & 8) ? 0xFFFFFFFFu : 0u, m1 = (sh & 4) ? 0xFFFFFFFFu : 0u;
+        const uint32_t bsh = (uint32_t)(sh & 3);
+        const int r = lane >> 2, c = lane & 3;
+        uint8_t* d = roi + r * kFastRowBytes + 16 * c;
+        fast_stage_chunk(R.v0, m2, m1, bsh, d, c < 3 && r < G.rh);
+        fast_stage_chunk(R.v1, m2, m1, bsh, d + 16 * kFastRowBytes, c < 3 && r + 16 < G.rh);
+        fast_stage_chunk(R.v2, m2, m1, bsh, d + 32 * kFastRowBytes, c < 3 && r + 32 < G.rh);
+    } else if (G.words) {
+        const uint32_t* q0 = R.q0;
         // word k of slab row = ROI columns 4k-1 .. 4k+2 = this lane's aligned word joined
         // with the next lane's (DPP row shift; one slab row = one 16-lane DPP row)
         const int al = (G.x0 - 1) & 3;
@@ -636,6 +683,9 @@ __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const uint32_t
                 roi[yy * kFastRowBytes + 1 + xx] = G.img[(int64_t)(G.y0 + yy) * G.pitch + G.x0 + xx];
     }
 }
+
+// Bytes of one per-wave ROI (or M) slab: 16-byte multiple so every slab starts 16-aligned.
+__host__ __device__ inline int fast_slab(const Plan& P) { return (kFastRowBytes * P.max_roi_h + 15) & ~15; }
 
 // Pre-test, exact strength, NMS and ordered output of one staged cell.
 __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, int f, int cidx, const CellDesc& c,
@@ -752,7 +802,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wv = threadIdx.x >> 6, lane = lane_id();
-    const int slab = kFastRowBytes * P->max_roi_h;          // per-wave LDS: roi, M, lists
+    const int slab = fast_slab(*P);                          // per-wave LDS: roi, M, lists
     uint8_t* wbase = smem + (size_t)wv * (2 * slab + 2 * (kFastSurv + kFastCorners));
     uint8_t* roi = wbase;
     uint8_t* Ms = wbase + slab;
@@ -765,10 +815,10 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
     const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
     CellDesc c = b.cells[cidx];
     FastCellGeom G = fast_geom(P, b, f, c);
-    uint32_t q0[kFastPass];
-    fast_prefetch(G, q0);
+    FastRegs R;
+    fast_prefetch(G, R);
     for (int t = 0; t < kFastCellsPerWave; t++, cidx++) {
-        fast_stage(G, q0, roi);
+        fast_stage(G, R, roi);
         for (int i = lane; i < (kFastRowBytes * c.rh + 15) / 16; i += 64) reinterpret_cast<uint4*>(Ms)[i] = make_uint4(0, 0, 0, 0);
         wave_sync_lds();
         const CellDesc cur = c;
@@ -776,7 +826,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
         if (more) {
             c = b.cells[cidx + 1];
             G = fast_geom(P, b, f, c);
-            fast_prefetch(G, q0);
+            fast_prefetch(G, R);
         }
         fast_cell(P, b, f, cidx, cur, th_ini, th_min, roi, Ms, surv, corn);
         if (!more) break;
@@ -1683,7 +1733,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     hipLaunchKernelGGL(k_blur, dim3((items + kWaves - 1) / kWaves, F), dim3(kThreads), 0, s, d_plan, b, bw);
     prof_end(prof, s);
     prof_begin(prof, "k_fast", s);
-    const int fast_lds = kWaves * (2 * kFastRowBytes * plan.max_roi_h + 2 * (kFastSurv + kFastCorners));
+    const int fast_lds = kWaves * (2 * fast_slab(plan) + 2 * (kFastSurv + kFastCorners));
     hipLaunchKernelGGL(k_fast, dim3((plan.ncells + kWaves * kFastCellsPerWave - 1) / (kWaves * kFastCellsPerWave), F), dim3(kThreads), fast_lds, s, d_plan, b);
     prof_end(prof, s);
     prof_begin(prof, "k_octree", s);
