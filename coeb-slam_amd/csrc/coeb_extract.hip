@@ -156,9 +156,10 @@ __device__ __forceinline__ int vresize(int h0, int h1, int b0, int b1)
 }
 
 // Output tile 128 x 32 per workgroup; the source rows/columns it touches (<= 32*scale+2 rows,
-// <= 128*scale+2 columns) are staged in LDS with aligned 32-bit loads, then each thread
-// produces 4 x 4 outputs (one 32-bit store per output row).
-constexpr int PT_W = 128, PT_H = 32, PT_SW = 264, PT_SH = 72;   // LDS source tile (scale <= 2)
+// <= 128*scale+2 columns) are staged in LDS -- 16-byte loads, each thread issuing all of its
+// loads before its first LDS store -- then each thread produces 4 x 4 outputs (one 32-bit
+// store per output row).
+constexpr int PT_W = 128, PT_H = 32, PT_SW = 288, PT_SH = 72;   // LDS source tile (scale <= 2)
 
 __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
                                                         int sw, int sh, uint8_t* __restrict__ dst, int64_t dst_fs,
@@ -172,34 +173,42 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
     const int* yofs = tab + 2 * dw;
     const int* beta = tab + 2 * dw + dh;
     const int ex = min(ox + PT_W, dw) - 1, ey = min(oy + PT_H, dh) - 1;
-    const int sx0 = xofs[ox] & ~3, sx1 = min(xofs[ex] + 1, sw - 1);
+    const int sx1 = min(xofs[ex] + 1, sw - 1);
     const int sy0 = max(yofs[oy], 0), sy1 = min(max(yofs[ey] + 1, 0), sh - 1);
-    const int nwords = (sx1 - sx0) / 4 + 1, nrows = sy1 - sy0 + 1;
+    const int nrows = sy1 - sy0 + 1;
     const uint8_t* S = src + (int64_t)f * src_fs;
-    if ((sp & 3) == 0 && nwords <= 64) {
-        // wave w stages rows w, w+4, ...; lane = source word.  All loads of a thread are
-        // issued before its first LDS store (clamped rows / words, stores guarded).
-        constexpr int kPass = PT_SH / kWaves;
-        const int wv = threadIdx.x >> 6, k = threadIdx.x & 63;
-        const uint32_t* base = reinterpret_cast<const uint32_t*>(S + (int64_t)sy0 * sp + sx0) + min(k, nwords - 1);
-        const int pw = sp >> 2;
-        uint32_t q[kPass];
-#pragma unroll
-        for (int i = 0; i < kPass; i++) q[i] = base[min(wv + kWaves * i, nrows - 1) * pw];
-#pragma unroll
-        for (int i = 0; i < kPass; i++) {
-            const int r = wv + kWaves * i;
-            if (r < nrows && k < nwords) *reinterpret_cast<uint32_t*>(s_src + r * PT_SW + 4 * k) = q[i];
+    const int tid = threadIdx.x;
+    int sx0;                                      // source column of LDS tile column 0
+    const bool vec = ((sp | (int)reinterpret_cast<uintptr_t>(S)) & 15) == 0;
+    if (vec && ((sx1 - (xofs[ox] & ~15)) >> 4) + 1 <= PT_SW / 16 && nrows <= PT_SH) {
+        sx0 = xofs[ox] & ~15;
+        const int nch = ((sx1 - sx0) >> 4) + 1;   // 16-byte chunks per row
+        const int rstep = kThreads / nch;         // rows per pass; thread = (row, chunk)
+        const int r = tid / nch, k = tid - r * nch;
+        if (r < rstep) {
+            const uint4* base = reinterpret_cast<const uint4*>(S + (int64_t)sy0 * sp + sx0) + k;
+            const int pw = sp >> 4;
+            uint4 q0 = base[min(r, nrows - 1) * pw];
+            uint4 q1 = base[min(r + rstep, nrows - 1) * pw];
+            uint4 q2 = base[min(r + 2 * rstep, nrows - 1) * pw];
+            if (r < nrows) *reinterpret_cast<uint4*>(s_src + r * PT_SW + 16 * k) = q0;
+            if (r + rstep < nrows) *reinterpret_cast<uint4*>(s_src + (r + rstep) * PT_SW + 16 * k) = q1;
+            if (r + 2 * rstep < nrows) *reinterpret_cast<uint4*>(s_src + (r + 2 * rstep) * PT_SW + 16 * k) = q2;
+            for (int rr = r + 3 * rstep; rr < nrows; rr += rstep)     // tall tiles (scale > 1.5)
+                *reinterpret_cast<uint4*>(s_src + rr * PT_SW + 16 * k) = base[rr * pw];
         }
     } else if ((sp & 3) == 0) {
-        for (int i = threadIdx.x; i < nwords * nrows; i += kThreads) {
+        sx0 = xofs[ox] & ~3;
+        const int nwords = (sx1 - sx0) / 4 + 1;
+        for (int i = tid; i < nwords * nrows; i += kThreads) {
             const int r = i / nwords, k = i - r * nwords;
             *reinterpret_cast<uint32_t*>(s_src + r * PT_SW + 4 * k) =
                 *reinterpret_cast<const uint32_t*>(S + (int64_t)(sy0 + r) * sp + sx0 + 4 * k);
         }
     } else {
+        sx0 = xofs[ox];
         const int nb = sx1 - sx0 + 1;
-        for (int i = threadIdx.x; i < nb * nrows; i += kThreads) {
+        for (int i = tid; i < nb * nrows; i += kThreads) {
             const int r = i / nb, k = i - r * nb;
             s_src[r * PT_SW + k] = S[(int64_t)(sy0 + r) * sp + sx0 + k];
         }
