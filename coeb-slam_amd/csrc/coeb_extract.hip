@@ -972,7 +972,9 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     uint8_t* const s_dead = O.dead;  // final phase: slot erased this round
     const int OCT_LMAX = P->oct_w;
 
-    const int l = blockIdx.x, f = blockIdx.y;
+    // frame-fastest grid: every frame's level-0 list (the longest) is dispatched in the first
+    // wave of workgroups, the cheap upper levels fill in behind them
+    const int f = blockIdx.x, l = blockIdx.y;
     const LevelGeom& g = P->lv[l];
     const int tid = threadIdx.x, wv = tid >> 6, lane = lane_id();
     const DynMask& dm = b.dyn[f];      // by reference: a local copy is indexed dynamically (scratch)
@@ -1461,10 +1463,13 @@ struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
 // Few wide loads per keypoint: with one byte per lane per load (lane = patch column) the
 // texture-address path, not the VALU, bounded this kernel.
 // The rotated pattern offsets are cvRound of |(px, py)| <= 13*sqrt(2), so |offset| <= 18.
-constexpr int kBlRow = 64, kBlRows = 37, kBlChunks = kBlRows * 4;   // 148 16-byte chunks
+// Patch rows are 64 source bytes at an LDS pitch of 72 (18 dwords): consecutive rows land on
+// different banks, so the 64 lanes' scattered test samples rarely conflict (a 64-byte pitch put
+// every other row on the same 16 banks).
+constexpr int kBlRow = 72, kBlRows = 37, kBlChunks = kBlRows * 4;   // 148 16-byte chunks
 constexpr int kDescKp = 32;                                          // keypoints per wave
 constexpr int kDescGroup = 2;                                        // patches staged per step
-constexpr int kDescSlab = kBlRow * kBlRows * kDescGroup + 32 * kDescKp;   // 5760 B per wave
+constexpr int kDescSlab = kBlRow * kBlRows * kDescGroup + 32 * kDescKp;   // 6352 B per wave
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};   // ORBextractor.cc:461-476
 
 // Weights of aligned row dword d (patch columns j = 4d..4d+3, u = j - 15) in row |v| = av:
@@ -1664,14 +1669,19 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
     COEB_LOAD_PATCH(1, qb0, qb1, qb2)
     for (int t0 = 0; t0 < nk; t0 += kDescGroup) {
         {
-            uint4* pd = reinterpret_cast<uint4*>(slab);
-            pd[lane] = qa0;
-            pd[lane + 64] = qa1;
-            if (lane + 128 < kBlChunks) pd[lane + 128] = qa2;
-            pd += kBlRow * kBlRows / 16;
-            pd[lane] = qb0;
-            pd[lane + 64] = qb1;
-            if (lane + 128 < kBlChunks) pd[lane + 128] = qb2;
+            // chunk e -> row e >> 2, bytes 16 (e & 3) .. +15 (two 8-byte stores: the pitch is 8-aligned)
+            auto put = [&](uint8_t* base, int e, uint4 v) {
+                uint2* d = reinterpret_cast<uint2*>(base + (e >> 2) * kBlRow + 16 * (e & 3));
+                d[0] = make_uint2(v.x, v.y);
+                d[1] = make_uint2(v.z, v.w);
+            };
+            uint8_t* pb = slab + kBlRow * kBlRows;
+            put(slab, lane, qa0);
+            put(slab, lane + 64, qa1);
+            if (lane + 128 < kBlChunks) put(slab, lane + 128, qa2);
+            put(pb, lane, qb0);
+            put(pb, lane + 64, qb1);
+            if (lane + 128 < kBlChunks) put(pb, lane + 128, qb2);
         }
         wave_sync_lds();
         if (t0 + kDescGroup < nk) {
@@ -1732,7 +1742,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     for (int l = 0; l < plan.L; l++) {
         const LevelGeom& g = plan.lv[l];
         bw.nstrips[l] = (g.w + kBlurCols - 1) / kBlurCols;
-        const int nbands = 4 * ((g.h + 63) / 64);
+        const int nbands = 4 * ((g.h + 63) / 64);     // 256- and 128-row bands measured slower
         bw.bh[l] = (g.h + nbands - 1) / nbands;
         bw.item_off[l] = items;
         items += bw.nstrips[l] * (nbands / 4);
@@ -1747,7 +1757,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     prof_end(prof, s);
     prof_begin(prof, "k_octree", s);
     (void)hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);
-    hipLaunchKernelGGL(k_octree, dim3(plan.L, F), dim3(kThreads), plan.oct_lds, s, d_plan, b);
+    hipLaunchKernelGGL(k_octree, dim3(F, plan.L), dim3(kThreads), plan.oct_lds, s, d_plan, b);
     prof_end(prof, s);
     prof_begin(prof, "k_describe", s);
     const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
