@@ -31,6 +31,7 @@ __device__ __forceinline__ int wave_sum(int v)
 
 // Exclusive block scan of one int per thread (256 threads).  Returns prefix; *total = sum.
 // All threads must call it.  sbuf: >= kWaves+1 ints of LDS.
+template <int NW = kWaves>
 __device__ __forceinline__ int block_scan_excl(int v, int* total, int* sbuf)
 {
     const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -42,7 +43,7 @@ __device__ __forceinline__ int block_scan_excl(int v, int* total, int* sbuf)
     if (lane == 63) sbuf[w] = x;
     __syncthreads();
     int base = 0, tot = 0;
-    for (int i = 0; i < kWaves; i++) {
+    for (int i = 0; i < NW; i++) {
         int t = sbuf[i];
         if (i < w) base += t;
         tot += t;
@@ -53,6 +54,7 @@ __device__ __forceinline__ int block_scan_excl(int v, int* total, int* sbuf)
 }
 
 // Exclusive block scan for a 0/1 predicate via ballots (cheaper).
+template <int NW = kWaves>
 __device__ __forceinline__ int block_scan_flag(bool pred, int* total, int* sbuf)
 {
     const int w = threadIdx.x >> 6;
@@ -61,7 +63,7 @@ __device__ __forceinline__ int block_scan_flag(bool pred, int* total, int* sbuf)
     if (lane_id() == 0) sbuf[w] = __popcll(m);
     __syncthreads();
     int base = 0, tot = 0;
-    for (int i = 0; i < kWaves; i++) {
+    for (int i = 0; i < NW; i++) {
         int t = sbuf[i];
         if (i < w) base += t;
         tot += t;
@@ -947,6 +949,30 @@ __device__ __forceinline__ void wave_scatter_quadrants(const uint32_t* src, uint
     }
 }
 
+// The same two steps for one node by one lane (the final phase and the late passes divide
+// many nodes of a few keys each: a wave per node would idle most of its lanes).
+__device__ __forceinline__ int4 lane_count_quadrants(const uint32_t* src, int s, int n, int sx, int sy)
+{
+    int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    for (int i = 0; i < n; i++) {
+        const int q = quadrant(src[s + i], sx, sy);
+        c0 += q == 0; c1 += q == 1; c2 += q == 2; c3 += q == 3;
+    }
+    return make_int4(c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ void lane_scatter_quadrants(const uint32_t* src, uint32_t* dst, int s, int n, int sx,
+                                                       int sy, int4 c)
+{
+    int r0 = s, r1 = s + c.x, r2 = s + c.x + c.y, r3 = s + c.x + c.y + c.z;
+    for (int i = 0; i < n; i++) {
+        const uint32_t k = src[s + i];
+        const int q = quadrant(k, sx, sy);
+        const int r = q == 0 ? r0++ : q == 1 ? r1++ : q == 2 ? r2++ : r3++;
+        dst[r] = k;
+    }
+}
+
 __device__ __forceinline__ void child_rect(const int4 p, int q, int4* out, int* sx, int* sy)
 {
     const int hx = (int)ceilf((float)(p.z - p.x) / 2);   // ExtractorNode::DivideNode :491-492
@@ -959,10 +985,12 @@ __device__ __forceinline__ void child_rect(const int4 p, int q, int4* out, int* 
     else *out = make_int4(mx, my, p.z, p.w);
 }
 
-__global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P, ExtractBufs b)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, ExtractBufs b)
 {
+    constexpr int NW = NT / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ int sbuf[kWaves + 2];
+    __shared__ int sbuf[(NW + 2 + 3) & ~3];   // 16-byte multiple: keeps the dynamic LDS base aligned
     const OctLds O = oct_lds(smem, P->oct_w, P->oct_kl);
     int* const s_work = O.work;      // slot ids of nodes divided this phase (processing order)
     int4* const s_cnt = O.cnt;       // their quadrant counts
@@ -986,9 +1014,9 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     int K = 0;
     {
         int part = 0;
-        for (int ci = tid; ci < g.ncells; ci += kThreads) part += cn[ci];
+        for (int ci = tid; ci < g.ncells; ci += NT) part += cn[ci];
         int tot;
-        block_scan_excl(part, &tot, sbuf);
+        block_scan_excl<NW>(part, &tot, sbuf);
         K = tot;
     }
     // keys in LDS when they fit, else in the level's global ping-pong buffers (L2-resident)
@@ -1007,17 +1035,17 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
         // thread copies keys, finding its cell by binary search: all loads independent
         int* s_coff = reinterpret_cast<int*>(O.keys[1]);
         int carry = 0;
-        for (int base = 0; base < g.ncells; base += kThreads) {
+        for (int base = 0; base < g.ncells; base += NT) {
             const int ci = base + tid;
             const int v = ci < g.ncells ? cn[ci] : 0;
             int tot;
-            const int pre = block_scan_excl(v, &tot, sbuf);
+            const int pre = block_scan_excl<NW>(v, &tot, sbuf);
             if (ci < g.ncells) s_coff[ci] = carry + pre;
             carry += tot;
         }
         K = carry;
         __syncthreads();
-        for (int i = tid; i < K; i += kThreads) {
+        for (int i = tid; i < K; i += NT) {
             int lo = 0, hi = g.ncells - 1;            // last cell with offset <= i
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
@@ -1027,11 +1055,11 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
         }
     } else {
         int carry = 0;
-        for (int base = 0; base < g.ncells; base += kThreads) {
+        for (int base = 0; base < g.ncells; base += NT) {
             const int ci = base + tid;
             const int v = ci < g.ncells ? cn[ci] : 0;
             int tot;
-            const int pre = block_scan_excl(v, &tot, sbuf);
+            const int pre = block_scan_excl<NW>(v, &tot, sbuf);
             if (ci < g.ncells) {
                 const uint32_t* src = cand + (int64_t)ci * P->cell_cap;
                 uint32_t* dst = KB(0) + carry + pre;
@@ -1047,7 +1075,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     if (area) {
         const float scale = (l != 0) ? g.scale : 1.0f;
         int carry = 0;
-        for (int base = 0; base < K; base += kThreads) {
+        for (int base = 0; base < K; base += NT) {
             const int i = base + tid;
             uint32_t k = 0;
             bool keep = false;
@@ -1056,7 +1084,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
                 keep = !masked_out(dm, (float)key_x(k), (float)key_y(k), scale, P->W, P->H);
             }
             int tot;
-            const int pre = block_scan_flag(keep, &tot, sbuf);
+            const int pre = block_scan_flag<NW>(keep, &tot, sbuf);
             if (keep) KB(1)[carry + pre] = k;
             carry += tot;
         }
@@ -1083,7 +1111,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
             for (int i = 0; i < g.nini; i++) {
                 const int lo = g.ini_bound[i], hi = g.ini_bound[i + 1];
                 const int start = carry;
-                for (int base = 0; base < K; base += kThreads) {
+                for (int base = 0; base < K; base += NT) {
                     const int idx = base + tid;
                     uint32_t k = 0;
                     bool in = false;
@@ -1092,7 +1120,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
                         in = key_x(k) >= lo && key_x(k) < hi;
                     }
                     int tot;
-                    const int pre = block_scan_flag(in, &tot, sbuf);
+                    const int pre = block_scan_flag<NW>(in, &tot, sbuf);
                     if (in) KB(kb ^ 1)[carry + pre] = k;
                     carry += tot;
                 }
@@ -1117,30 +1145,43 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
         NodeRef S = nref(O, cs), D = nref(O, cs ^ 1);
         // divided nodes = cnt > 1, in list order
         int nd = 0;
-        for (int base = 0; base < n; base += kThreads) {
+        for (int base = 0; base < n; base += NT) {
             const int k = base + tid;
             const bool dv = k < n && S.cnt[k] > 1;
             int tot;
-            const int pre = block_scan_flag(dv, &tot, sbuf);
+            const int pre = block_scan_flag<NW>(dv, &tot, sbuf);
             if (dv) s_work[nd + pre] = k;
             nd += tot;
         }
         __syncthreads();
-        // partition: one wave per divided node
-        for (int j = wv; j < nd; j += kWaves) {
-            const int k = s_work[j];
-            const int s = S.start[k], c = S.cnt[k], bf = S.buf[k];
-            const int4 r = S.rect[k];
-            int4 tmp; int sx, sy;
-            child_rect(r, 0, &tmp, &sx, &sy);
-            const int4 qc = wave_count_quadrants(KB(bf), s, c, sx, sy);
-            wave_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
-            if (lane == 0) s_cnt[j] = qc;
+        // partition: one wave per divided node while the nodes are few and large, one lane per
+        // node once there are many (then each holds a few keys)
+        if (nd < 2 * NW) {
+            for (int j = wv; j < nd; j += NW) {
+                const int k = s_work[j];
+                const int s = S.start[k], c = S.cnt[k], bf = S.buf[k];
+                const int4 r = S.rect[k];
+                int4 tmp; int sx, sy;
+                child_rect(r, 0, &tmp, &sx, &sy);
+                const int4 qc = wave_count_quadrants(KB(bf), s, c, sx, sy);
+                wave_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
+                if (lane == 0) s_cnt[j] = qc;
+            }
+        } else {
+            for (int j = tid; j < nd; j += NT) {
+                const int k = s_work[j];
+                const int s = S.start[k], c = S.cnt[k], bf = S.buf[k];
+                int4 tmp; int sx, sy;
+                child_rect(S.rect[k], 0, &tmp, &sx, &sy);
+                const int4 qc = lane_count_quadrants(KB(bf), s, c, sx, sy);
+                lane_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
+                s_cnt[j] = qc;
+            }
         }
         __syncthreads();
         // children alloc order = divided nodes in list order, n1..n4 nonempty
         int T = 0, nexp = 0;
-        for (int base = 0; base < nd; base += kThreads) {
+        for (int base = 0; base < nd; base += NT) {
             const int j = base + tid;
             int e = 0, x = 0;
             if (j < nd) {
@@ -1149,8 +1190,8 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
                 x = (q.x > 1) + (q.y > 1) + (q.z > 1) + (q.w > 1);
             }
             int tot, tot2;
-            const int pre = block_scan_excl(e, &tot, sbuf);
-            block_scan_excl(x, &tot2, sbuf);
+            const int pre = block_scan_excl<NW>(e, &tot, sbuf);
+            block_scan_excl<NW>(x, &tot2, sbuf);
             if (j < nd) s_base[j] = T + pre;
             T += tot;
             nexp += tot2;
@@ -1159,7 +1200,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
         const int nnew = T + (n - nd);
         if (nnew > g.ncap) { if (tid == 0) atomicOr(b.err, 4); finish = true; break; }
         // write children (reverse push order at the front)
-        for (int j = tid; j < nd; j += kThreads) {
+        for (int j = tid; j < nd; j += NT) {
             const int k = s_work[j];
             const int4 q = s_cnt[j];
             const int s = S.start[k], bf = S.buf[k];
@@ -1182,11 +1223,11 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
         // non-divided nodes keep their relative order after the children
         {
             int carry = 0;
-            for (int base = 0; base < n; base += kThreads) {
+            for (int base = 0; base < n; base += NT) {
                 const int k = base + tid;
                 const bool keep = k < n && S.cnt[k] <= 1;
                 int tot;
-                const int pre = block_scan_flag(keep, &tot, sbuf);
+                const int pre = block_scan_flag<NW>(keep, &tot, sbuf);
                 if (keep) {
                     const int pos = T + carry + pre;
                     D.start[pos] = S.start[k]; D.cnt[pos] = S.cnt[k]; D.alloc[pos] = S.alloc[k];
@@ -1210,35 +1251,34 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
         NodeRef S = nref(O, cs), D = nref(O, cs ^ 1);
         // vPrev = list nodes with cnt > 1, i.e. vSizeAndPointerToNode of the previous round
         int m = 0;
-        for (int base = 0; base < n; base += kThreads) {
+        for (int base = 0; base < n; base += NT) {
             const int k = base + tid;
             const bool dv = k < n && S.cnt[k] > 1;
             int tot;
-            const int pre = block_scan_flag(dv, &tot, sbuf);
+            const int pre = block_scan_flag<NW>(dv, &tot, sbuf);
             if (dv) s_work[m + pre] = k;
             m += tot;
         }
-        for (int k = tid; k < n; k += kThreads) s_dead[k] = 0;
+        for (int k = tid; k < n; k += NT) s_dead[k] = 0;
         __syncthreads();
-        // quadrant counts of every vPrev node (one wave per node)
-        for (int j = wv; j < m; j += kWaves) {
+        // quadrant counts of every vPrev node (one lane per node)
+        for (int j = tid; j < m; j += NT) {
             const int k = s_work[j];
             int4 tmp; int sx, sy;
             child_rect(S.rect[k], 0, &tmp, &sx, &sy);
-            const int4 qc = wave_count_quadrants(KB(S.buf[k]), S.start[k], S.cnt[k], sx, sy);
-            if (lane == 0) s_cnt[j] = qc;
+            s_cnt[j] = lane_count_quadrants(KB(S.buf[k]), S.start[k], S.cnt[k], sx, sy);
         }
         // sort(vPrev) by (size, node) ascending and walk from the back: rank 0 = largest size,
         // ties -> later allocation first (pointer order of a monotonic allocator)
         // (cnt, alloc) packed as cnt << 16 | alloc (alloc < 2^16, cnt < 2^15) in s_push,
         // which is free until the push order is written
-        for (int j = tid; j < m; j += kThreads) {
+        for (int j = tid; j < m; j += NT) {
             const int k = s_work[j];
             s_push[j] = (int)(((uint32_t)S.cnt[k] << 16) | (uint32_t)S.alloc[k]);   // used when K < 2^15
         }
         __syncthreads();
         if (K < 32768 && alloc_ctr < 65536) {
-            for (int j = tid; j < m; j += kThreads) {
+            for (int j = tid; j < m; j += NT) {
                 const int kj = s_push[j];
                 int rank = 0;
 #pragma unroll 8
@@ -1246,7 +1286,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
                 s_rank[j] = rank;
             }
         } else {
-            for (int j = tid; j < m; j += kThreads) {
+            for (int j = tid; j < m; j += NT) {
                 const int k = s_work[j];
                 const int cj = S.cnt[k], aj = S.alloc[k];
                 int rank = 0;
@@ -1259,13 +1299,13 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
             }
         }
         __syncthreads();
-        for (int j = tid; j < m; j += kThreads) s_base[s_rank[j]] = j;
+        for (int j = tid; j < m; j += NT) s_base[s_rank[j]] = j;
         __syncthreads();
         // list size after processing rank r is n + sum_{r'<=r}(e-1); the first r reaching N breaks
         int nproc = m;
         {
             int carry = 0, found = 0x7fffffff;
-            for (int base = 0; base < m; base += kThreads) {
+            for (int base = 0; base < m; base += NT) {
                 const int r = base + tid;
                 int d = 0;
                 if (r < m) {
@@ -1273,7 +1313,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
                     d = (q.x > 0) + (q.y > 0) + (q.z > 0) + (q.w > 0) - 1;
                 }
                 int tot;
-                const int pre = block_scan_excl(d, &tot, sbuf);
+                const int pre = block_scan_excl<NW>(d, &tot, sbuf);
                 if (r < m && n + carry + pre + d >= N) found = min(found, r);
                 carry += tot;
             }
@@ -1282,13 +1322,13 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
             if (lane == 0) sbuf[wv] = fr;
             __syncthreads();
             int mn = 0x7fffffff;
-            for (int i = 0; i < kWaves; i++) mn = min(mn, sbuf[i]);
+            for (int i = 0; i < NW; i++) mn = min(mn, sbuf[i]);
             __syncthreads();
             if (mn != 0x7fffffff) nproc = mn + 1;
         }
         // push order = processing order, children n1..n4 nonempty
         int T = 0;
-        for (int base = 0; base < nproc; base += kThreads) {
+        for (int base = 0; base < nproc; base += NT) {
             const int r = base + tid;
             int e = 0;
             if (r < nproc) {
@@ -1296,17 +1336,17 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
                 e = (q.x > 0) + (q.y > 0) + (q.z > 0) + (q.w > 0);
             }
             int tot;
-            const int pre = block_scan_excl(e, &tot, sbuf);
+            const int pre = block_scan_excl<NW>(e, &tot, sbuf);
             if (r < nproc) s_push[r] = T + pre;
             T += tot;
         }
-        for (int j = tid; j < m; j += kThreads)
+        for (int j = tid; j < m; j += NT)
             if (s_rank[j] < nproc) s_dead[s_work[j]] = 1;
         __syncthreads();
         const int nnew = T + n - nproc;
         if (nnew > g.ncap) { if (tid == 0) atomicOr(b.err, 4); break; }
-        // DivideNode of the processed nodes + push_front of their children
-        for (int r = wv; r < nproc; r += kWaves) {
+        // DivideNode of the processed nodes + push_front of their children (one lane per node)
+        for (int r = tid; r < nproc; r += NT) {
             const int j = s_base[r];
             const int k = s_work[j];
             const int s = S.start[k], c = S.cnt[k], bf = S.buf[k];
@@ -1314,8 +1354,8 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
             int4 tmp; int sx, sy;
             child_rect(pr, 0, &tmp, &sx, &sy);
             const int4 qc = s_cnt[j];
-            wave_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
-            if (lane == 0) {
+            lane_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
+            {
                 int a = s_push[r];
                 int off = s;
                 const int qq[4] = {qc.x, qc.y, qc.z, qc.w};
@@ -1335,11 +1375,11 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
         // erase processed nodes, keep the rest in list order behind the children
         {
             int carry = 0;
-            for (int base = 0; base < n; base += kThreads) {
+            for (int base = 0; base < n; base += NT) {
                 const int k = base + tid;
                 const bool keep = k < n && !s_dead[k];
                 int tot;
-                const int pre = block_scan_flag(keep, &tot, sbuf);
+                const int pre = block_scan_flag<NW>(keep, &tot, sbuf);
                 if (keep) {
                     const int pos = T + carry + pre;
                     D.start[pos] = S.start[k]; D.cnt[pos] = S.cnt[k]; D.alloc[pos] = S.alloc[k];
@@ -1361,7 +1401,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
     const bool cull = !area && l < 8;                  // CheckMovingKeyPoints_finall loops 8 levels
     const float scale = (l != 0) ? g.scale : 1.0f;
     int carry = 0;
-    for (int base = 0; base < n; base += kThreads) {
+    for (int base = 0; base < n; base += NT) {
         const int k = base + tid;
         uint32_t best = 0;
         bool keep = false;
@@ -1379,7 +1419,7 @@ __global__ __launch_bounds__(kThreads) void k_octree(const Plan* __restrict__ P,
             keep = !(cull && masked_out(dm, (float)x, (float)y, scale, P->W, P->H));
         }
         int tot;
-        const int pre = block_scan_flag(keep, &tot, sbuf);
+        const int pre = block_scan_flag<NW>(keep, &tot, sbuf);
         if (keep) {
             if (carry + pre < g.out_cap) out[carry + pre] = best;
             else atomicOr(b.err, 8);
@@ -1756,8 +1796,9 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     hipLaunchKernelGGL(k_fast, dim3((plan.ncells + kWaves * kFastCellsPerWave - 1) / (kWaves * kFastCellsPerWave), F), dim3(kThreads), fast_lds, s, d_plan, b);
     prof_end(prof, s);
     prof_begin(prof, "k_octree", s);
-    (void)hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);
-    hipLaunchKernelGGL(k_octree, dim3(F, plan.L), dim3(kThreads), plan.oct_lds, s, d_plan, b);
+    constexpr int kOctThreads = 256;       // 512 / 1024 measured slower
+    (void)hipFuncSetAttribute((const void*)k_octree<kOctThreads>, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);
+    hipLaunchKernelGGL(k_octree<kOctThreads>, dim3(F, plan.L), dim3(kOctThreads), plan.oct_lds, s, d_plan, b);
     prof_end(prof, s);
     prof_begin(prof, "k_describe", s);
     const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
