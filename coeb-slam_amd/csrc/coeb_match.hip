@@ -89,6 +89,9 @@ constexpr int kMThreads = 1024;
 constexpr int kCQ = 64;
 constexpr int kMaxIter = 64;
 constexpr int kIdxBits = 12;
+// Lanes per LastFrame query in the candidate phase: a grid column range holds a few
+// candidates (10-px cells), so 8 lanes waste fewer than 16 (measured 0.171 -> 0.147 ms/step)
+constexpr int kQL = 8;
 
 struct QueryWin {
     bool ok, chk;
@@ -370,11 +373,11 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
         // ---- phase 1: candidate lists (static filters) ----
         if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; s_flag[2] = 0; s_flag[3] = 0; }
         __syncthreads();
-        // one 16-lane group per query; lanes take the candidates of a grid column range 16 at a
+        // one kQL-lane group per query; lanes take the candidates of a grid column range kQL at a
         // time and ballot-compact them, so each list stays in enumeration order
         {
-            const int grp = tid >> 4, gl = tid & 15, gsh = (tid & 63) & ~15;
-            for (int q0 = 0; q0 < nl; q0 += kMThreads / 16) {
+            const int grp = tid / kQL, gl = tid % kQL, gsh = (tid & 63) & ~(kQL - 1);
+            for (int q0 = 0; q0 < nl; q0 += kMThreads / kQL) {
                 const int q = q0 + grp;
                 int cnt = -1;
                 QueryWin w;
@@ -391,7 +394,7 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
                     for (int ix = w.x0; ix <= w.x1; ix++) {
                         const int c0 = L.cell[ix * COEB_GRID_ROWS + w.y0];
                         const int c1 = L.cell[ix * COEB_GRID_ROWS + w.y1 + 1];
-                        for (int base = c0; base < c1; base += 16) {
+                        for (int base = c0; base < c1; base += kQL) {
                             const int e = base + gl;
                             bool ok = false;
                             uint32_t ent = 0;
@@ -414,7 +417,7 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
                                     ent = ((uint32_t)dist << kIdxBits) | (uint32_t)i2;
                                 }
                             }
-                            const uint32_t gb = (uint32_t)(__ballot(ok) >> gsh) & 0xFFFFu;
+                            const uint32_t gb = (uint32_t)(__ballot(ok) >> gsh) & ((1u << kQL) - 1u);
                             if (ok) {
                                 const int pos = cnt + __popc(gb & ((1u << gl) - 1u));
                                 if (pos < kCQ) lst[pos] = ent;
