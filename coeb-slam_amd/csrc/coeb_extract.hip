@@ -20,6 +20,10 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+// Wave index in the workgroup as a wave-uniform (scalar) value: derived from threadIdx the
+// compiler treats it as divergent, and everything indexed by it (cell descriptors, level
+// geometry) becomes per-lane vector loads and VGPR arithmetic.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
@@ -300,7 +304,7 @@ __device__ __forceinline__ uint32_t dpp_shl1(uint32_t v)   // lane i <- lane i+1
 __global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, ExtractBufs b, BlurWork bw)
 {
     const int f = blockIdx.y;
-    const int item = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    const int item = blockIdx.x * kWaves + wave_id();
     if (item >= bw.item_off[bw.L]) return;
     int l = 0;
     while (l + 1 < bw.L && item >= bw.item_off[l + 1]) l++;
@@ -807,11 +811,27 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
     if (lane == 0) b.cand_n[(int64_t)f * P->ncells + cidx] = min(nkept, P->cell_cap);
 }
 
+// Cell descriptor as one 16-byte scalar load (16-bit fields would become vector loads).
+__device__ __forceinline__ CellDesc load_cell(const CellDesc* __restrict__ cells, int i)
+{
+    const int4 r = reinterpret_cast<const int4*>(cells)[i];
+    CellDesc c;
+    c.level = (int16_t)(r.x & 0xFFFF); c.pad = 0;
+    c.x0 = (int16_t)(r.y & 0xFFFF); c.y0 = (int16_t)(r.y >> 16);
+    c.rw = (int16_t)(r.z & 0xFFFF); c.rh = (int16_t)(r.z >> 16);
+    c.i = (int16_t)(r.w & 0xFFFF); c.j = (int16_t)(r.w >> 16);
+    return c;
+}
+
 // One wave per kFastCellsPerWave consecutive cells, four waves per workgroup, no workgroup
 // barriers.  The next cell's ROI loads are issued before the current cell is processed.
-__global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P, ExtractBufs b)
+__global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P, ExtractBufs b,
+                                                       const CellDesc* __restrict__ cells)   // read-only: scalar loads
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // a per-lane wave index here (unlike the other kernels): with the cell geometry in SGPRs the
+    // compiler moves the per-cell bookkeeping onto the shared scalar unit and the kernel ran
+    // 5 % slower (0.320 vs 0.335 ms/step)
     const int wv = threadIdx.x >> 6, lane = lane_id();
     const int slab = fast_slab(*P);                          // per-wave LDS: roi, M, lists
     uint8_t* wbase = smem + (size_t)wv * (2 * slab + 2 * (kFastSurv + kFastCorners));
@@ -824,7 +844,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
     if (cidx >= P->ncells) return;
     const int area = b.dyn[f].area_flag;
     const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
-    CellDesc c = b.cells[cidx];
+    CellDesc c = load_cell(cells, cidx);
     FastCellGeom G = fast_geom(P, b, f, c);
     FastRegs R;
     fast_prefetch(G, R);
@@ -835,7 +855,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
         const CellDesc cur = c;
         const bool more = t + 1 < kFastCellsPerWave && cidx + 1 < P->ncells;
         if (more) {
-            c = b.cells[cidx + 1];
+            c = load_cell(cells, cidx + 1);
             G = fast_geom(P, b, f, c);
             fast_prefetch(G, R);
         }
@@ -1004,7 +1024,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
     // wave of workgroups, the cheap upper levels fill in behind them
     const int f = blockIdx.x, l = blockIdx.y;
     const LevelGeom& g = P->lv[l];
-    const int tid = threadIdx.x, wv = tid >> 6, lane = lane_id();
+    const int tid = threadIdx.x, wv = wave_id(), lane = lane_id();
     const DynMask& dm = b.dyn[f];      // by reference: a local copy is indexed dynamically (scratch)
     const int area = dm.area_flag;
     const int N = area ? g.nfeat_area : g.nfeat;
@@ -1611,7 +1631,7 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
     __shared__ __attribute__((aligned(16))) uint8_t s_slab[kWaves][kDescSlab];
     const int f = blockIdx.y;
     const int L = P->L;
-    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const int lane = lane_id(), wv = wave_id();
     // per-level keypoint offsets (wave prefix over lanes 0..L-1)
     const int nl = lane < L ? b.lvl_n[(int64_t)f * L + lane] : 0;
     int incl = nl;
@@ -1793,7 +1813,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     prof_end(prof, s);
     prof_begin(prof, "k_fast", s);
     const int fast_lds = kWaves * (2 * fast_slab(plan) + 2 * (kFastSurv + kFastCorners));
-    hipLaunchKernelGGL(k_fast, dim3((plan.ncells + kWaves * kFastCellsPerWave - 1) / (kWaves * kFastCellsPerWave), F), dim3(kThreads), fast_lds, s, d_plan, b);
+    hipLaunchKernelGGL(k_fast, dim3((plan.ncells + kWaves * kFastCellsPerWave - 1) / (kWaves * kFastCellsPerWave), F), dim3(kThreads), fast_lds, s, d_plan, b, b.cells);
     prof_end(prof, s);
     prof_begin(prof, "k_octree", s);
     constexpr int kOctThreads = 256;       // 512 / 1024 measured slower
