@@ -287,6 +287,7 @@ struct BlurWork {
 };
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us2, v); }
 __device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -1755,14 +1756,19 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
             const float tb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bs), t));
             const float ta = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ac), t));
             const uint8_t* bc = slab + k * kBlRow * kBlRows + 18 * kBlRow + __builtin_amdgcn_readlane(xoff, t);
+            // (row, col) = (fma(px, b, py*a), fma(px, a, -(py*b))) as packed-f32 pairs: the same
+            // two roundings per component as the reference's fused forms, half the instructions
+            const f32x2 AB = {ta, tb}, BA = {tb, ta};
             uint32_t nib = 0;
 #pragma unroll
             for (int tt = 0; tt < 4; tt++) {
-                const int r0 = (int)rintf(__builtin_fmaf(px0[tt], tb, py0[tt] * ta));
-                const int c0 = (int)rintf(__builtin_fmaf(px0[tt], ta, -(py0[tt] * tb)));
-                const int r1 = (int)rintf(__builtin_fmaf(px1[tt], tb, py1[tt] * ta));
-                const int c1 = (int)rintf(__builtin_fmaf(px1[tt], ta, -(py1[tt] * tb)));
-                nib |= (uint32_t)(bc[r0 * kBlRow + c0] < bc[r1 * kBlRow + c1]) << tt;
+                const f32x2 t0 = f32x2{py0[tt], py0[tt]} * AB, t1 = f32x2{py1[tt], py1[tt]} * AB;
+                const f32x2 rc0 = __builtin_elementwise_fma(f32x2{px0[tt], px0[tt]}, BA, f32x2{t0.x, -t0.y});
+                const f32x2 rc1 = __builtin_elementwise_fma(f32x2{px1[tt], px1[tt]}, BA, f32x2{t1.x, -t1.y});
+                // cvRound, then row * pitch + col exactly in f32 (|row|, |col| <= 18)
+                const int o0 = (int)__builtin_fmaf(rintf(rc0.x), (float)kBlRow, rintf(rc0.y));
+                const int o1 = (int)__builtin_fmaf(rintf(rc1.x), (float)kBlRow, rintf(rc1.y));
+                nib |= (uint32_t)(bc[o0] < bc[o1]) << tt;
             }
             // bit k of byte i = test 8i+k: dword d = nibbles of lanes 8d .. 8d+7
             uint32_t dw = nib << (4 * (lane & 7));
