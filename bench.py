@@ -133,6 +133,19 @@ def pmc_traffic(kernel, frames_per_launch):
         return None, None
 
 
+def pmc_valu(kernel):
+    """VALU issue utilisation of `kernel` from the committed PMC summary (profiles/pmc_valu.json,
+    tools/pmc_summary.py --valu-json: SQ_INSTS_VALU / (256 CUs x busy cycles))."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_valu.json")) as f:
+            d = json.load(f)
+        k = d["kernels"][kernel]
+        return dict(valu_issue_frac=k["valu_issue_frac"], valu_insts_per_launch=k["valu_insts"],
+                    source="profiles/pmc_valu.json (%s)" % d.get("command", ""))
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 class DryRunPipeline:
     """CPU stand-in with the BatchPipeline surface, for testing bench's multi-rank plumbing."""
 
@@ -288,6 +301,11 @@ def main():
                         avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=int(bpl))
             if traffic is not None:
                 roof["traffic_source"] = "profiles/pmc_traffic.json (%s)" % tsrc
+            # the path is integer-VALU bound, not HBM bound: the PMC VALU issue fraction of the
+            # same kernel says how close it runs to the chip's one-VALU-op-per-CU-cycle ceiling
+            valu = pmc_valu(name)
+            if valu is not None:
+                roof["valu"] = valu
         pipeline_bytes = w * h + 60 * nkp + 36 * nkp     # B = W*H + 60 N_kp + 36 N_prev
         line = dict(metric=METRIC, value=round(value, 2), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(ms_per_step, 4), higher_is_better=True,

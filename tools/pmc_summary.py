@@ -40,6 +40,22 @@ def traffic_json(merged, nd, frames, command, fetch_scale):
     return out
 
 
+def valu_json(merged, nd, frames, command, n_cu=256, n_xcd=8):
+    """Per kernel, VALU wave-instructions per launch and the fraction of the chip's VALU issue
+    rate they fill: a CU issues at most one wave64 VALU instruction per cycle (4 SIMDs x one
+    every 4 cycles), and GRBM_GUI_ACTIVE sums the busy cycles of the 8 XCDs."""
+    out = dict(frames_per_launch=frames, command=command,
+               definition="valu_issue_frac = SQ_INSTS_VALU / (%d CUs * GRBM_GUI_ACTIVE / %d XCDs), per dispatch"
+                          % (n_cu, n_xcd), kernels={})
+    for k, cv in sorted(merged.items()):
+        if "SQ_INSTS_VALU" not in cv or not cv.get("GRBM_GUI_ACTIVE"):
+            continue
+        cycles = cv["GRBM_GUI_ACTIVE"] / n_xcd
+        out["kernels"][k] = dict(valu_insts=int(cv["SQ_INSTS_VALU"]), busy_cycles=int(cycles),
+                                 valu_issue_frac=round(cv["SQ_INSTS_VALU"] / (n_cu * cycles), 4), dispatches=nd[k])
+    return out
+
+
 if __name__ == "__main__":
     import argparse
     import json
@@ -49,6 +65,7 @@ if __name__ == "__main__":
     ap.add_argument("--frames", type=int, default=0, help="frames per launch of the profiled command")
     ap.add_argument("--command", default="")
     ap.add_argument("--fetch-scale", type=float, default=1.0)
+    ap.add_argument("--valu-json", help="write per-kernel VALU issue utilisation (SQ_INSTS_VALU, GRBM_GUI_ACTIVE)")
     a = ap.parse_args()
     merged = collections.defaultdict(dict)
     nd = {}
@@ -61,3 +78,6 @@ if __name__ == "__main__":
     if a.json:
         with open(a.json, "w") as f:
             json.dump(traffic_json(merged, nd, a.frames, a.command, a.fetch_scale), f, indent=1)
+    if a.valu_json:
+        with open(a.valu_json, "w") as f:
+            json.dump(valu_json(merged, nd, a.frames, a.command), f, indent=1)
