@@ -8,6 +8,9 @@
       include/ORBmatcher.h:41,52, src/ORBmatcher.cc:1329-1471; mutates
       CurrentFrame.mvpMapPoints (slot index of the LastFrame MapPoint, -1 = NULL) and returns
       nmatches.
+  ORBmatcher(nnratio).SearchByProjection(F, LocalMap, th=3)
+      include/ORBmatcher.h:46, src/ORBmatcher.cc:44-129 (the Tracking::SearchLocalPoints call,
+      src/Tracking.cc:1222-1271); assigns F.mvpMapPoints[i] = local-map index and returns nmatches.
   ORBmatcher.DescriptorDistance(a, b)  src/ORBmatcher.cc:1648-1664
 
 All compute runs in libcoeb_front.so (hand-written gfx950 HIP kernels).  There is no CPU
@@ -37,6 +40,7 @@ ABI_SYMBOLS = [
     "coeb_rgbd_preprocess", "coeb_descriptor_distance", "coeb_profile_enable", "coeb_profile_read",
     "coeb_profile_reset", "coeb_synchronize", "coeb_device_count", "coeb_debug_read",
     "coeb_device_alloc", "coeb_device_free", "coeb_memcpy_h2d", "coeb_memcpy_d2h", "coeb_set_batch_streams",
+    "coeb_match_localmap",
 ]
 
 
@@ -64,6 +68,12 @@ class LastFrameC(C.Structure):
 
 class CurFrameC(C.Structure):
     _fields_ = [("n", C.c_int32), ("keys_un", C.c_void_p), ("descriptors", C.c_void_p), ("u_right", C.c_void_p)]
+
+
+class LocalMapC(C.Structure):
+    _fields_ = [("n", C.c_int32), ("in_view", C.c_void_p), ("proj_x", C.c_void_p), ("proj_y", C.c_void_p),
+                ("proj_xr", C.c_void_p), ("level", C.c_void_p), ("view_cos", C.c_void_p), ("descriptor", C.c_void_p),
+                ("observations", C.c_void_p)]
 
 
 class CoebError(RuntimeError):
@@ -102,6 +112,8 @@ def lib():
         L.coeb_match_lastframe.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(CurFrameC),
                                            C.POINTER(LastFrameC), C.c_void_p, C.c_void_p, C.c_float, C.c_int,
                                            C.c_int, C.c_void_p, C.POINTER(C.c_int)]
+        L.coeb_match_localmap.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(CurFrameC), C.c_void_p,
+                                          C.POINTER(LocalMapC), C.c_float, C.c_float, C.c_void_p, C.POINTER(C.c_int)]
         L.coeb_blur_flags.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_int,
                                       C.c_void_p]
         L.coeb_stereo_from_rgbd.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
@@ -373,6 +385,34 @@ class Frame:
         self.map_points = map_points
         self.mvbOutlier = np.zeros(self.N, np.uint8) if outlier is None else np.ascontiguousarray(outlier, np.uint8)
         self.mvpMapPoints = np.full(self.N, -1, np.int32)
+        # Observations() of the MapPoint in mvpMapPoints[i] (-1 = NULL); read by the local-map search
+        self.mvpMapPointObs = np.full(self.N, -1, np.int32)
+
+
+class LocalMap:
+    """vpLocalMapPoints after Tracking::SearchLocalPoints ran Frame::isInFrustum on them
+    (src/Tracking.cc:1244-1259, src/Frame.cc:445-501): the fields ORBmatcher::SearchByProjection(F, vpMapPoints, th) reads (ORBmatcher.cc:50-80)."""
+
+    def __init__(self, in_view, proj_x, proj_y, proj_xr, level, view_cos, descriptor, observations):
+        self.mbTrackInView = np.ascontiguousarray(in_view, np.uint8)
+        self.N = len(self.mbTrackInView)
+        self.mTrackProjX = np.ascontiguousarray(proj_x, np.float32)
+        self.mTrackProjY = np.ascontiguousarray(proj_y, np.float32)
+        self.mTrackProjXR = np.ascontiguousarray(proj_xr, np.float32)
+        self.mnTrackScaleLevel = np.ascontiguousarray(level, np.int32)
+        self.mTrackViewCos = np.ascontiguousarray(view_cos, np.float32)
+        self.mDescriptor = np.ascontiguousarray(descriptor, np.uint8).reshape(self.N, 32) if self.N else \
+            np.zeros((0, 32), np.uint8)
+        self.nObs = np.ascontiguousarray(observations, np.int32)
+        for a in (self.mTrackProjX, self.mTrackProjY, self.mTrackProjXR, self.mnTrackScaleLevel, self.mTrackViewCos,
+                  self.nObs):
+            if len(a) != self.N:
+                raise ValueError("LocalMap arrays differ in length")
+
+    def c_struct(self):
+        return LocalMapC(self.N, *[C.c_void_p(a.ctypes.data) for a in (
+            self.mbTrackInView, self.mTrackProjX, self.mTrackProjY, self.mTrackProjXR, self.mnTrackScaleLevel,
+            self.mTrackViewCos, self.mDescriptor, self.nObs)])
 
 
 class ORBmatcher:
@@ -392,9 +432,13 @@ class ORBmatcher:
         b = np.ascontiguousarray(b, np.uint8)
         return lib().coeb_descriptor_distance(_p(a), _p(b))
 
-    def SearchByProjection(self, CurrentFrame, LastFrame, th, bMono, camera):
+    def SearchByProjection(self, CurrentFrame, LastFrame, th=3.0, bMono=None, camera=None):
+        """(CurrentFrame, LastFrame, th, bMono, camera): ORBmatcher.cc:1329-1471;
+        (F, LocalMap, th=3, camera=...): ORBmatcher.cc:44-129."""
         if self.ctx is None:
             self.ctx = Context()
+        if isinstance(LastFrame, LocalMap):
+            return self._search_local_map(CurrentFrame, LastFrame, th, camera if camera is not None else bMono)
         mp = LastFrame.map_points
         n = LastFrame.N
         lf_arrays = dict(has=np.ascontiguousarray(mp["valid"], np.uint8),
@@ -412,6 +456,25 @@ class ORBmatcher:
                                                   _p(CurrentFrame.mTcw), _p(LastFrame.mTcw), th, int(bMono),
                                                   int(self.mbCheckOrientation), _p(out), C.byref(nm)))
         CurrentFrame.mvpMapPoints = out[:CurrentFrame.N].copy()
+        return nm.value
+
+
+    def _search_local_map(self, F, local_map, th, camera):
+        if camera is None:
+            raise ValueError("SearchByProjection(F, LocalMap, th): camera is required")
+        cf = CurFrameC(F.N, C.c_void_p(F.mvKeysUn.ctypes.data), C.c_void_p(F.mDescriptors.ctypes.data),
+                       C.c_void_p(F.mvuRight.ctypes.data))
+        cobs = np.ascontiguousarray(F.mvpMapPointObs, np.int32)
+        lm = local_map.c_struct()
+        out = np.full(max(F.N, 1), -1, np.int32)
+        nm = C.c_int()
+        self.ctx.check(lib().coeb_match_localmap(self.ctx.h, C.byref(camera), C.byref(cf), _p(cobs), C.byref(lm),
+                                                 th, self.mfNNratio, _p(out), C.byref(nm)))
+        got = out[:F.N]
+        hit = got >= 0
+        F.mvpMapPoints = np.where(hit, got, F.mvpMapPoints).astype(np.int32)
+        if hit.any():
+            F.mvpMapPointObs = np.where(hit, local_map.nObs[np.maximum(got, 0)], F.mvpMapPointObs).astype(np.int32)
         return nm.value
 
 

@@ -88,3 +88,57 @@ def dynamic_inputs(w, h, seed=7, area_flag=False):
     tm = np.array(pts, dtype=np.float32)
     blur = np.array([0, 1, 1][:len(boxes)], dtype=np.int32)
     return boxes, tm, blur
+
+
+def make_local_map(xw, desc, octave, Tcw, w, h, fx=TUM_FX, fy=TUM_FY, cx=TUM_CX, cy=TUM_CY, bf=TUM_BF,
+                   nlevels=8, seed=0, dup_frac=0.3, n_distract=300, jitter=1.0):
+    """A synthetic vpLocalMapPoints snapshot after Frame::isInFrustum (Frame.cc:445-501) for the
+    local-map projection search: the map points xw [n,3] projected with Tcw (+ Gaussian jitter
+    in px), predicted level = octave +- 1, view cosines on both sides of 0.998
+    (RadiusByViewingCos), plus near-duplicates (a few descriptor bits flipped: ratio-test and
+    claim conflicts) and random distractors, shuffled.  Returns a dict of the coeb_localmap
+    arrays (in_view, proj_x, proj_y, proj_xr, level, view_cos, descriptor, observations)."""
+    rng = np.random.default_rng(seed)
+    xw = np.asarray(xw, np.float32).reshape(-1, 3)
+    desc = np.asarray(desc, np.uint8).reshape(-1, 32)
+    octave = np.asarray(octave, np.int32)
+    R, t = np.asarray(Tcw, np.float32)[:3, :3], np.asarray(Tcw, np.float32)[:3, 3]
+    pc = xw @ R.T + t
+    z = pc[:, 2]
+    ok = z > 0
+    invz = np.where(ok, 1.0 / np.where(ok, z, 1), 0).astype(np.float32)
+    u = (fx * pc[:, 0] * invz + cx).astype(np.float32)
+    v = (fy * pc[:, 1] * invz + cy).astype(np.float32)
+    n = len(xw)
+    lvl = np.clip(octave + rng.integers(-1, 2, n), 0, nlevels - 1).astype(np.int32)
+    pts = [dict(u=u, v=v, ur=(u - bf * invz).astype(np.float32), lvl=lvl, desc=desc, ok=ok)]
+    nd = int(n * dup_frac)
+    if nd:
+        pick = rng.choice(n, nd, replace=True)
+        d = desc[pick].copy()
+        for k in range(nd):                 # flip 0..12 random bits
+            for b in rng.integers(0, 256, rng.integers(0, 13)):
+                d[k, b >> 3] ^= np.uint8(1 << (b & 7))
+        pts.append(dict(u=u[pick] + rng.normal(0, 2, nd).astype(np.float32),
+                        v=v[pick] + rng.normal(0, 2, nd).astype(np.float32),
+                        ur=(u[pick] - bf * invz[pick]).astype(np.float32), lvl=lvl[pick], desc=d, ok=ok[pick]))
+    if n_distract:
+        pts.append(dict(u=rng.uniform(-20, w + 20, n_distract).astype(np.float32),
+                        v=rng.uniform(-20, h + 20, n_distract).astype(np.float32),
+                        ur=rng.uniform(-50, w, n_distract).astype(np.float32),
+                        lvl=rng.integers(0, nlevels, n_distract).astype(np.int32),
+                        desc=rng.integers(0, 256, (n_distract, 32)).astype(np.uint8),
+                        ok=np.ones(n_distract, bool)))
+    cat = {k: np.concatenate([p[k] for p in pts]) for k in pts[0]}
+    m = len(cat["u"])
+    order = rng.permutation(m)
+    ju = rng.normal(0, jitter, m).astype(np.float32)
+    jv = rng.normal(0, jitter, m).astype(np.float32)
+    px = (cat["u"] + ju)[order].astype(np.float32)
+    py = (cat["v"] + jv)[order].astype(np.float32)
+    in_view = (cat["ok"][order] & (px >= 0) & (px < w) & (py >= 0) & (py < h)).astype(np.uint8)
+    cos = np.where(rng.random(m) < 0.5, rng.uniform(0.9981, 1.0, m), rng.uniform(0.5, 0.998, m)).astype(np.float32)
+    return dict(in_view=in_view, proj_x=px, proj_y=py, proj_xr=(cat["ur"] + ju)[order].astype(np.float32),
+                level=np.where(in_view > 0, cat["lvl"][order], -1).astype(np.int32), view_cos=cos,
+                descriptor=np.ascontiguousarray(cat["desc"][order]),
+                observations=rng.choice(np.array([0, 1, 2, 3], np.int32), m, p=[0.3, 0.2, 0.3, 0.2]).astype(np.int32))

@@ -857,6 +857,74 @@ int coeb_match_lastframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curfram
     return COEB_OK;
 }
 
+int coeb_match_localmap(coeb_ctx* c, const coeb_camera* cam, const coeb_curframe* cur, const int32_t* cur_obs,
+                        const coeb_localmap* mp, float th, float nnratio, int32_t* match_out, int* nmatches)
+{
+    if (!c || !cam || !cur || !mp || !nmatches) return set_err(c, COEB_EINVAL, "coeb_match_localmap: invalid arguments");
+    *nmatches = 0;
+    if (cur->n < 0 || mp->n < 0) return set_err(c, COEB_EINVAL, "negative frame / local map size");
+    if (cur->n > kCurMax) return set_err(c, COEB_EINVAL, "more than 4095 current keypoints");
+    const int n = cur->n, nq = mp->n;
+    if (n && (!cur->keys_un || !cur->descriptors || !cur->u_right))
+        return set_err(c, COEB_EINVAL, "coeb_match_localmap: missing current-frame arrays");
+    if (nq && (!mp->in_view || !mp->proj_x || !mp->proj_y || !mp->proj_xr || !mp->level || !mp->view_cos ||
+               !mp->descriptor || !mp->observations))
+        return set_err(c, COEB_EINVAL, "coeb_match_localmap: missing local-map arrays");
+    // the kernel indexes mvScaleFactors[level] for every point in view
+    for (int q = 0; q < nq; q++)
+        if (mp->in_view[q] && (mp->level[q] < 0 || mp->level[q] >= c->tab.nlevels))
+            return set_err(c, COEB_EINVAL, "coeb_match_localmap: predicted level outside the pyramid");
+    (void)hipSetDevice(c->device);
+    const int cs = std::max(n, 1), qs = std::max(nq, 1);
+    int rc;
+    coeb_keypoint* dck;
+    uint8_t *dcd, *dview, *dqd;
+    float *dur, *dpx, *dpy, *dpxr, *dcos;
+    int32_t *dcobs, *dlvl, *dnobs, *dmatch, *dnm, *derr, *dpath;
+    uint32_t* dlist;
+    if ((rc = ensure(c, "m_ck", cs, &dck)) || (rc = ensure(c, "m_cd", (size_t)cs * 32, &dcd)) ||
+        (rc = ensure(c, "m_ur", cs, &dur)) || (rc = ensure(c, "l_cobs", cs, &dcobs)) ||
+        (rc = ensure(c, "l_view", qs, &dview)) || (rc = ensure(c, "l_px", qs, &dpx)) || (rc = ensure(c, "l_py", qs, &dpy)) ||
+        (rc = ensure(c, "l_pxr", qs, &dpxr)) || (rc = ensure(c, "l_lvl", qs, &dlvl)) || (rc = ensure(c, "l_cos", qs, &dcos)) ||
+        (rc = ensure(c, "l_qd", (size_t)qs * 32, &dqd)) || (rc = ensure(c, "l_nobs", qs, &dnobs)) ||
+        (rc = ensure(c, "m_match", cs, &dmatch)) || (rc = ensure(c, "m_nm", 1, &dnm)) ||
+        (rc = ensure(c, "l_list", (size_t)qs * match_list_cap(), &dlist)) || (rc = ensure(c, "err", 4, &derr)) ||
+        (rc = ensure(c, "l_path", 2, &dpath)))
+        return rc;
+    hipStream_t s = main_stream(c);
+    if (n) {
+        HIP_TRY(c, hipMemcpyAsync(dck, cur->keys_un, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dcd, cur->descriptors, (size_t)n * 32, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dur, cur->u_right, (size_t)n * 4, hipMemcpyHostToDevice, s));
+        if (cur_obs) HIP_TRY(c, hipMemcpyAsync(dcobs, cur_obs, (size_t)n * 4, hipMemcpyHostToDevice, s));
+        else HIP_TRY(c, hipMemsetAsync(dcobs, 0xff, (size_t)n * 4, s));   // -1: all NULL
+    }
+    if (nq) {
+        HIP_TRY(c, hipMemcpyAsync(dview, mp->in_view, (size_t)nq, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dpx, mp->proj_x, (size_t)nq * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dpy, mp->proj_y, (size_t)nq * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dpxr, mp->proj_xr, (size_t)nq * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dlvl, mp->level, (size_t)nq * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dcos, mp->view_cos, (size_t)nq * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dqd, mp->descriptor, (size_t)nq * 32, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dnobs, mp->observations, (size_t)nq * 4, hipMemcpyHostToDevice, s));
+    }
+    LocalBufsHost b;
+    b.cur_kps = dck; b.cur_desc = dcd; b.cur_ur = dur; b.cur_obs = dcobs; b.cur_n = n;
+    b.in_view = dview; b.proj_x = dpx; b.proj_y = dpy; b.proj_xr = dpxr; b.level = dlvl; b.view_cos = dcos;
+    b.desc = dqd; b.nobs = dnobs; b.mp_n = nq; b.match = dmatch; b.nmatch = dnm; b.lists = dlist; b.err = derr; b.path = dpath;
+    rc = launch_match_local(make_cam(c, cam), b, th, nnratio, s, &c->hook);
+    if (rc == -2) return set_err(c, COEB_ERANGE, "coeb_match_localmap: frame and local map exceed the LDS budget");
+    if (rc) return hip_err(c, hipGetLastError(), "launch_match_local");
+    int nm = 0;
+    HIP_TRY(c, hipMemcpyAsync(&nm, dnm, 4, hipMemcpyDeviceToHost, s));
+    if (n && match_out) HIP_TRY(c, hipMemcpyAsync(match_out, dmatch, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if ((rc = check_err_word(c))) return rc;
+    *nmatches = nm;
+    return COEB_OK;
+}
+
 namespace {
 
 // Common body of the batch matchers.  dT_cur: device poses, pair p (current frame p+1) at
@@ -1111,6 +1179,15 @@ int coeb_internal_error(coeb_ctx* c, int code, const char* msg) { return set_err
  * what = "pyr" | "blur" | "cand_n" | "lvl_n" | "lvl_kp" | "dyn"; copies min(bytes, size). */
 int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t bytes, size_t* size_out)
 {
+    if (c && what && std::string(what) == "localmap_path") {   // {path, iterations} of the last coeb_match_localmap
+        if (!c->bufs.count("l_path")) return COEB_EINVAL;
+        if (size_out) *size_out = 8;
+        if (host && bytes) {
+            HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
+            HIP_TRY(c, hipMemcpy(host, c->bufs["l_path"].p, std::min(bytes, (size_t)8), hipMemcpyDeviceToHost));
+        }
+        return COEB_OK;
+    }
     if (!c || !what || !c->has_plan || f < 0 || f >= c->batch_frames) return COEB_EINVAL;
     (void)hipSetDevice(c->device);
     const Plan& P = c->plan;

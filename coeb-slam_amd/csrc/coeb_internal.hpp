@@ -169,6 +169,18 @@ struct MatchBufs {
 int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int bmono, int check_ori,
                  int retry_below, hipStream_t s, ProfileHook* prof);
 
+// local-map projection search (ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th))
+struct LocalBufsHost {
+    const void* cur_kps; const uint8_t* cur_desc; const float* cur_ur; const int* cur_obs; int cur_n;
+    const uint8_t* in_view; const float* proj_x; const float* proj_y; const float* proj_xr;
+    const int* level; const float* view_cos; const uint8_t* desc; const int* nobs; int mp_n;
+    int* match; int* nmatch; uint32_t* lists; int* err;
+    int* path;   // [0]: 0 parallel claims, 1 forced sequential, 2 list overflow, 3 no convergence; [1]: iterations
+};
+int launch_match_local(const MatchCam& cam, const LocalBufsHost& b, float th, float nnratio, hipStream_t s,
+                       ProfileHook* prof);
+int match_list_cap();   // candidate-list entries per query (kCQ)
+
 // frame preparation for batch matching: u_right/depth per keypoint + LastFrame map snapshot
 struct PrepBufs {
     const void* kps; const int* n; int stride;

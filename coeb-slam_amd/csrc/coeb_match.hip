@@ -1,19 +1,21 @@
-// coeb_match.hip -- CDNA4 kernels for the tracking-time projection matcher:
-//   ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)  src/ORBmatcher.cc:1329-1471
+// coeb_match.hip -- CDNA4 kernels for the tracking-time projection searches:
+//   ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)  src/ORBmatcher.cc:1329-1471  (k_match)
+//   ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th)     src/ORBmatcher.cc:44-129     (k_match_local)
 //   Frame::AssignFeaturesToGrid / GetFeaturesInArea                   src/Frame.cc:396-411, 503-568
-//   Frame::ComputeStereoFromRGBD                                      src/Frame.cc:820-842
+//   Frame::ComputeStereoFromRGBD                                      src/Frame.cc:820-842         (k_prep)
 //   ORBmatcher::DescriptorDistance                                    src/ORBmatcher.cc:1648-1664
 //
-// One workgroup per (current, last) frame pair.  Phase 0 (whole workgroup) builds the
-// 64 x 48 keypoint grid as a CSR: keys (cell << 13 | index) are bitonic-sorted in LDS, so a
-// cell column ix over rows [iy0, iy1] is ONE contiguous range and the reference's
-// enumeration order (ix outer, iy inner, in-cell insertion order) is range order.  Phase 1
-// walks the LastFrame points in index order (the claim dependency of :1404-1406/1429 is
-// sequential); each query's candidates are evaluated 64 at a time by one wave (window,
-// level, claim, stereo check, 256-bit Hamming via popcount) and reduced to the first strict
-// minimum with one wave min.  Phase 2 applies the rotation-histogram top-3 filter.
+// One 1024-thread workgroup per frame (pair).  Phase 0 (stage_grid) stages the current frame
+// in LDS and builds the 64 x 48 keypoint grid as a CSR by a stable counting sort, so a cell
+// column ix over rows [iy0, iy1] is ONE contiguous range in the reference's enumeration order
+// (ix outer, iy inner, in-cell insertion order).  Phase 1: kQL lanes per query walk its
+// window (level, window, stereo checks, 256-bit Hamming via popcount) and write its candidate
+// list in that order.  Phase 2 resolves the sequential claim dependency (:1404-1406 / :86-88)
+// as a Jacobi fixpoint, with the literal loop as fallback.  Phase 3 assigns (last writer
+// wins) and, for k_match, applies the rotation-histogram top-3 filter.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "coeb_internal.hpp"
@@ -99,6 +101,22 @@ struct QueryWin {
     int minL, maxL, x0, x1, y0, y1;
 };
 
+// Grid cell range of GetFeaturesInArea(u, v, radius, minL, maxL) (Frame.cc:507-522); false when
+// the window misses the grid.
+__device__ __forceinline__ bool window_cells(const MatchCam& cam, QueryWin& w)
+{
+    w.x0 = max(0, (int)floorf(((w.u - cam.min_x) - w.radius) * cam.grid_inv_w));
+    if (w.x0 >= COEB_GRID_COLS) return false;
+    w.x1 = min(COEB_GRID_COLS - 1, (int)ceilf(((w.u - cam.min_x) + w.radius) * cam.grid_inv_w));
+    if (w.x1 < 0) return false;
+    w.y0 = max(0, (int)floorf(((w.v - cam.min_y) - w.radius) * cam.grid_inv_h));
+    if (w.y0 >= COEB_GRID_ROWS) return false;
+    w.y1 = min(COEB_GRID_ROWS - 1, (int)ceilf(((w.v - cam.min_y) + w.radius) * cam.grid_inv_h));
+    if (w.y1 < 0) return false;
+    w.chk = (w.minL > 0) || (w.maxL >= 0);
+    return true;
+}
+
 __device__ __forceinline__ QueryWin query_window(const MatchCam& cam, const float* T, const float* X, int octave,
                                                  float th, bool fwd, bool bwd)
 {
@@ -120,17 +138,8 @@ __device__ __forceinline__ QueryWin query_window(const MatchCam& cam, const floa
     if (fwd) { w.minL = octave; w.maxL = -1; }
     else if (bwd) { w.minL = 0; w.maxL = octave; }
     else { w.minL = octave - 1; w.maxL = octave + 1; }
-    w.x0 = max(0, (int)floorf(((w.u - cam.min_x) - w.radius) * cam.grid_inv_w));
-    if (w.x0 >= COEB_GRID_COLS) return w;
-    w.x1 = min(COEB_GRID_COLS - 1, (int)ceilf(((w.u - cam.min_x) + w.radius) * cam.grid_inv_w));
-    if (w.x1 < 0) return w;
-    w.y0 = max(0, (int)floorf(((w.v - cam.min_y) - w.radius) * cam.grid_inv_h));
-    if (w.y0 >= COEB_GRID_ROWS) return w;
-    w.y1 = min(COEB_GRID_ROWS - 1, (int)ceilf(((w.v - cam.min_y) + w.radius) * cam.grid_inv_h));
-    if (w.y1 < 0) return w;
-    w.chk = (w.minL > 0) || (w.maxL >= 0);
     w.ur_q = __builtin_fmaf(-cam.bf, invzc, w.u);     // u - mbf*invzc (fused)
-    w.ok = true;
+    w.ok = window_cells(cam, w);
     return w;
 }
 
@@ -235,45 +244,15 @@ __host__ __device__ inline size_t match_lds_bytes(int nmax, int qmax, bool lds_c
     return o;
 }
 
+// Phase 0 of both matchers: stage the CurrentFrame (x, y, uR, octave, descriptor) in LDS and
+// build its 64 x 48 grid (Frame::AssignFeaturesToGrid, Frame.cc:396-411) as a CSR by a stable
+// counting sort: L.cell[c] = start of cell c in L.sort, L.sort = (cell << kIdxBits | index) in
+// cell order, index order inside a cell.  L.owner is scratch here.
 template <bool kLds>
-__global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, float th0, int bmono, int check_ori,
-                                                     int retry_below, int force_seq)
+__device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, const float* cur_ur, const uint8_t* cdesc,
+                                           int n, const MatchLds& L)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ int s_hist[HISTO_LENGTH];
-    __shared__ int s_flag[8];
-    const int p = blockIdx.x;
     const int tid = threadIdx.x;
-    const int n = b.cur_n[p];
-    const int nl = b.last_n[p];
-    size_t off[7];
-    match_lds_bytes(b.cur_stride, b.last_stride, kLds, off);
-    MatchLds L;
-    L.cell = reinterpret_cast<int*>(smem + off[0]);
-    L.sort = reinterpret_cast<uint32_t*>(smem + off[1]);
-    L.owner = reinterpret_cast<int*>(smem + off[2]);
-    L.res = reinterpret_cast<int*>(smem + off[3]);
-    L.qn = reinterpret_cast<int*>(smem + off[4]);
-    L.kp = reinterpret_cast<float4*>(smem + off[5]);
-    L.desc = reinterpret_cast<uint32_t*>(smem + off[6]);
-    const Kp* cur = reinterpret_cast<const Kp*>(b.cur_kps) + (int64_t)p * b.cur_stride;
-    const uint8_t* cdesc = b.cur_desc + (int64_t)p * b.cur_stride * 32;
-    const float* cur_ur = b.cur_ur + (int64_t)p * b.cur_stride;
-    const Kp* last = reinterpret_cast<const Kp*>(b.last_kps) + (int64_t)p * b.last_stride;
-    const uint8_t* ldesc = b.last_desc + (int64_t)p * b.last_stride * 32;
-    const uint8_t* lhas = b.last_has + (int64_t)p * b.last_stride;
-    const uint8_t* lout = b.last_out + (int64_t)p * b.last_stride;
-    const float* lxw = b.last_xw + (int64_t)p * b.last_stride * 3;
-    const int* lnobs = b.last_nobs + (int64_t)p * b.last_stride;
-    uint32_t* lists = reinterpret_cast<uint32_t*>(b.scratch) + (int64_t)p * b.scratch_stride;
-    if (n > b.cur_stride || nl > b.last_stride || n >= (1 << kIdxBits)) {
-        if (tid == 0) { atomicOr(b.err, 16); b.nmatch[p] = 0; }
-        return;
-    }
-    CurView<kLds> cv;
-    cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = cur_ur; cv.gdesc = cdesc;
-
-    // ---- phase 0: stage CurrentFrame, grid CSR by a stable counting sort ----
     for (int c = tid; c <= COEB_GRID_CELLS; c += kMThreads) L.cell[c] = 0;
     __syncthreads();
     for (int i = tid; i < n; i += kMThreads) {
@@ -349,6 +328,49 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
         }
     }
     __syncthreads();
+
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, float th0, int bmono, int check_ori,
+                                                     int retry_below, int force_seq)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int s_hist[HISTO_LENGTH];
+    __shared__ int s_flag[8];
+    const int p = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int n = b.cur_n[p];
+    const int nl = b.last_n[p];
+    size_t off[7];
+    match_lds_bytes(b.cur_stride, b.last_stride, kLds, off);
+    MatchLds L;
+    L.cell = reinterpret_cast<int*>(smem + off[0]);
+    L.sort = reinterpret_cast<uint32_t*>(smem + off[1]);
+    L.owner = reinterpret_cast<int*>(smem + off[2]);
+    L.res = reinterpret_cast<int*>(smem + off[3]);
+    L.qn = reinterpret_cast<int*>(smem + off[4]);
+    L.kp = reinterpret_cast<float4*>(smem + off[5]);
+    L.desc = reinterpret_cast<uint32_t*>(smem + off[6]);
+    const Kp* cur = reinterpret_cast<const Kp*>(b.cur_kps) + (int64_t)p * b.cur_stride;
+    const uint8_t* cdesc = b.cur_desc + (int64_t)p * b.cur_stride * 32;
+    const float* cur_ur = b.cur_ur + (int64_t)p * b.cur_stride;
+    const Kp* last = reinterpret_cast<const Kp*>(b.last_kps) + (int64_t)p * b.last_stride;
+    const uint8_t* ldesc = b.last_desc + (int64_t)p * b.last_stride * 32;
+    const uint8_t* lhas = b.last_has + (int64_t)p * b.last_stride;
+    const uint8_t* lout = b.last_out + (int64_t)p * b.last_stride;
+    const float* lxw = b.last_xw + (int64_t)p * b.last_stride * 3;
+    const int* lnobs = b.last_nobs + (int64_t)p * b.last_stride;
+    uint32_t* lists = reinterpret_cast<uint32_t*>(b.scratch) + (int64_t)p * b.scratch_stride;
+    if (n > b.cur_stride || nl > b.last_stride || n >= (1 << kIdxBits)) {
+        if (tid == 0) { atomicOr(b.err, 16); b.nmatch[p] = 0; }
+        return;
+    }
+    CurView<kLds> cv;
+    cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = cur_ur; cv.gdesc = cdesc;
+
+    // ---- phase 0: stage CurrentFrame, grid CSR by a stable counting sort ----
+    stage_grid<kLds>(cam, cur, cur_ur, cdesc, n, L);
 
     // pose algebra (ORBmatcher.cc:1339-1350): twc = -Rcw^T tcw (double accumulation), tlc
     const float* T = b.Tcw_cur + (int64_t)p * 16;
@@ -549,6 +571,233 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
     if (tid == 0) b.nmatch[p] = nmatches;
 }
 
+
+// ================================ k_match_local ================================
+// ORBmatcher::SearchByProjection(Frame &F, const vector<MapPoint*> &vpMapPoints, th)
+// (src/ORBmatcher.cc:44-129) for one frame, one 1024-thread workgroup.  The local-map points
+// arrive as Frame::isInFrustum left them (projection, predicted level, viewing cosine).
+//   phase 0  stage CurrentFrame + grid CSR (stage_grid)
+//   phase 1  per point (kQL lanes): window r = RadiusByViewingCos(cos) * th * scale[level],
+//            levels [level-1, level], keypoints whose entry MapPoint has Observations() > 0
+//            dropped, stereo check; EVERY candidate kept with its distance and octave (the
+//            second best feeds the ratio test, whatever its distance)
+//   phase 2  claims: point q skips keypoints taken by an earlier point p < q with
+//            Observations() > 0; best / second best / ratio test on what is left.  Same
+//            Jacobi fixpoint as k_match (owner[c] = min such p), reaching the sequential answer
+//   phase 3  the last point assigned to a keypoint wins (F.mvpMapPoints[bestIdx] = pMP)
+// Overflowing lists or no convergence run the literal loop instead.
+struct LocalBufs {
+    const void* cur_kps; const uint8_t* cur_desc; const float* cur_ur; const int* cur_obs; int cur_n;
+    const uint8_t* in_view; const float* proj_x; const float* proj_y; const float* proj_xr;
+    const int* level; const float* view_cos; const uint8_t* desc; const int* nobs; int mp_n;
+    int* match; int* nmatch; uint32_t* lists; int* err; int* path;
+};
+
+__device__ __forceinline__ float radius_by_viewing_cos(float c) { return c > 0.998f ? 2.5f : 4.0f; }   // ORBmatcher.cc:131-137
+
+// window of point q (r = RadiusByViewingCos * th (if th != 1) * mvScaleFactors[level])
+__device__ __forceinline__ QueryWin local_window(const MatchCam& cam, const LocalBufs& b, int q, float th)
+{
+    QueryWin w;
+    const int level = b.level[q];
+    float r = radius_by_viewing_cos(b.view_cos[q]);
+    if (th != 1.0f) r *= th;
+    w.u = b.proj_x[q];
+    w.v = b.proj_y[q];
+    w.radius = r * cam.scale[level];
+    w.minL = level - 1;
+    w.maxL = level;
+    w.ur_q = b.proj_xr[q];
+    w.ok = b.in_view[q] && window_cells(cam, w);
+    return w;
+}
+
+constexpr int kLocKeyDist = 16, kLocKeyOct = 12;    // list entry: dist << 16 | octave << 12 | index
+
+template <bool kLds>
+__global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBufs b, float th, float nnratio,
+                                                           int force_seq)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int s_flag[8];
+    const int tid = threadIdx.x;
+    const int n = b.cur_n, nq = b.mp_n;
+    size_t off[7];
+    match_lds_bytes(n, nq, kLds, off);
+    MatchLds L;
+    L.cell = reinterpret_cast<int*>(smem + off[0]);
+    L.sort = reinterpret_cast<uint32_t*>(smem + off[1]);
+    L.owner = reinterpret_cast<int*>(smem + off[2]);
+    L.res = reinterpret_cast<int*>(smem + off[3]);
+    L.qn = reinterpret_cast<int*>(smem + off[4]);
+    L.kp = reinterpret_cast<float4*>(smem + off[5]);
+    L.desc = reinterpret_cast<uint32_t*>(smem + off[6]);
+    const Kp* cur = reinterpret_cast<const Kp*>(b.cur_kps);
+    if (n >= (1 << kIdxBits)) {
+        if (tid == 0) { atomicOr(b.err, 16); *b.nmatch = 0; }
+        return;
+    }
+    CurView<kLds> cv;
+    cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = b.cur_ur; cv.gdesc = b.cur_desc;
+    stage_grid<kLds>(cam, cur, b.cur_ur, b.cur_desc, n, L);
+    if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; s_flag[2] = 0; }
+    __syncthreads();
+
+    // ---- phase 1: candidate lists ----
+    {
+        const int grp = tid / kQL, gl = tid % kQL, gsh = (tid & 63) & ~(kQL - 1);
+        for (int q0 = 0; q0 < nq; q0 += kMThreads / kQL) {
+            const int q = q0 + grp;
+            int cnt = -1;
+            QueryWin w;
+            w.ok = false;
+            if (q < nq) w = local_window(cam, b, q, th);
+            if (w.ok) {
+                uint32_t qd[8];
+                const uint4* d = reinterpret_cast<const uint4*>(b.desc + 32 * q);
+                const uint4 d0 = d[0], d1 = d[1];
+                qd[0] = d0.x; qd[1] = d0.y; qd[2] = d0.z; qd[3] = d0.w;
+                qd[4] = d1.x; qd[5] = d1.y; qd[6] = d1.z; qd[7] = d1.w;
+                cnt = 0;
+                uint32_t* lst = b.lists + (int64_t)q * kCQ;
+                for (int ix = w.x0; ix <= w.x1; ix++) {
+                    const int c0 = L.cell[ix * COEB_GRID_ROWS + w.y0];
+                    const int c1 = L.cell[ix * COEB_GRID_ROWS + w.y1 + 1];
+                    for (int base = c0; base < c1; base += kQL) {
+                        const int e = base + gl;
+                        bool ok = false;
+                        uint32_t ent = 0;
+                        if (e < c1) {
+                            const int i2 = (int)(L.sort[e] & ((1u << kIdxBits) - 1));
+                            float x, y, ur;
+                            int oct;
+                            cv.get(i2, x, y, ur, oct);
+                            ok = !(oct < w.minL || oct > w.maxL);              // chk is always set here
+                            const float distx = x - w.u, disty = y - w.v;
+                            if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) ok = false;
+                            if (b.cur_obs[i2] > 0) ok = false;                    // :86-88, entry holder
+                            if (ur > 0 && fabsf(w.ur_q - ur) > w.radius) ok = false;   // :90-95
+                            if (ok) {
+                                const int dist = cv.dist(i2, qd);
+                                ent = ((uint32_t)dist << kLocKeyDist) | ((uint32_t)oct << kLocKeyOct) | (uint32_t)i2;
+                            }
+                        }
+                        const uint32_t gb = (uint32_t)(__ballot(ok) >> gsh) & ((1u << kQL) - 1u);
+                        if (ok) {
+                            const int pos = cnt + __popc(gb & ((1u << gl) - 1u));
+                            if (pos < kCQ) lst[pos] = ent;
+                        }
+                        cnt += __popc(gb);
+                    }
+                }
+                if (cnt > kCQ) s_flag[0] = 1;
+            }
+            if (q < nq && gl == 0) L.qn[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | (b.nobs[q] > 0 ? 0x10000 : 0));
+        }
+    }
+    __syncthreads();
+    bool seq = force_seq || s_flag[0];
+    int iters = 0;
+    // ---- phase 2: claims by fixpoint iteration ----
+    if (!seq) {
+        for (int it = 0;; it++) {
+            iters = it + 1;
+            for (int c = tid; c < n; c += kMThreads) L.owner[c] = 0x7fffffff;
+            if (tid == 0) s_flag[1] = 0;
+            __syncthreads();
+            if (it > 0) {
+                for (int q = tid; q < nq; q += kMThreads) {
+                    const int r = L.res[q];
+                    if (r >= 0 && (L.qn[q] & 0x10000)) atomicMin(&L.owner[r], q);
+                }
+                __syncthreads();
+            }
+            for (int q = tid; q < nq; q += kMThreads) {
+                const int qn = L.qn[q];
+                int res = -1;
+                if (qn >= 0) {
+                    const int m = qn & 0xFFFF;
+                    const uint32_t* lst = b.lists + (int64_t)q * kCQ;
+                    int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+                    for (int e = 0; e < m; e++) {
+                        const uint32_t v = lst[e];
+                        const int i2 = (int)(v & ((1u << kIdxBits) - 1));
+                        if (L.owner[i2] < q) continue;             // taken by an earlier point
+                        const int dist = (int)(v >> kLocKeyDist), oct = (int)((v >> kLocKeyOct) & 0xF);
+                        if (dist < bestDist) {
+                            bestDist2 = bestDist; bestDist = dist;
+                            bestLevel2 = bestLevel; bestLevel = oct; bestIdx = i2;
+                        } else if (dist < bestDist2) {
+                            bestLevel2 = oct; bestDist2 = dist;
+                        }
+                    }
+                    if (bestDist <= TH_HIGH && !(bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2))
+                        res = bestIdx;
+                }
+                if (it == 0 || res != L.res[q]) s_flag[1] = 1;
+                L.res[q] = res;
+            }
+            __syncthreads();
+            if (!s_flag[1]) break;
+            if (it >= kMaxIter) { seq = true; break; }
+            __syncthreads();
+        }
+    }
+    if (seq) {
+        // literal loop (ORBmatcher.cc:48-126), one thread; L.owner = Observations() of each
+        // keypoint's holder
+        for (int c = tid; c < n; c += kMThreads) { L.owner[c] = b.cur_obs[c]; }
+        __syncthreads();
+        if (tid == 0) {
+            b.path[0] = force_seq ? 1 : s_flag[0] ? 2 : 3;   // forced / list overflow / no convergence
+            b.path[1] = iters;
+            int nm = 0;
+            for (int c = 0; c < n; c++) b.match[c] = -1;
+            for (int q = 0; q < nq; q++) {
+                QueryWin w = local_window(cam, b, q, th);
+                if (!w.ok) continue;
+                uint32_t qd[8];
+                for (int k = 0; k < 8; k++) qd[k] = reinterpret_cast<const uint32_t*>(b.desc + 32 * q)[k];
+                int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+                for_candidates<kLds>(w, L.cell, L.sort, cv, [&](int i2) {
+                    if (L.owner[i2] > 0) return true;
+                    const int dist = cv.dist(i2, qd);
+                    float x, y, ur;
+                    int oct;
+                    cv.get(i2, x, y, ur, oct);
+                    if (dist < bestDist) {
+                        bestDist2 = bestDist; bestDist = dist;
+                        bestLevel2 = bestLevel; bestLevel = oct; bestIdx = i2;
+                    } else if (dist < bestDist2) {
+                        bestLevel2 = oct; bestDist2 = dist;
+                    }
+                    return true;
+                });
+                if (bestDist <= TH_HIGH) {
+                    if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
+                    b.match[bestIdx] = q;
+                    L.owner[bestIdx] = b.nobs[q];
+                    nm++;
+                }
+            }
+            *b.nmatch = nm;
+        }
+        return;
+    }
+    // ---- phase 3: the last assignment to a keypoint wins ----
+    for (int c = tid; c < n; c += kMThreads) L.owner[c] = -1;
+    __syncthreads();
+    int mine = 0;
+    for (int q = tid; q < nq; q += kMThreads) {
+        const int r = L.res[q];
+        if (r >= 0) { atomicMax(&L.owner[r], q); mine++; }
+    }
+    if (mine) atomicAdd(&s_flag[2], mine);
+    __syncthreads();
+    for (int c = tid; c < n; c += kMThreads) b.match[c] = L.owner[c];
+    if (tid == 0) { *b.nmatch = s_flag[2]; b.path[0] = 0; b.path[1] = iters; }
+}
+
 }  // namespace
 
 int launch_prep(const PrepBufs& b, int F, hipStream_t s, ProfileHook* prof)
@@ -582,3 +831,31 @@ int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int b
     prof_end(prof, s);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+int launch_match_local(const MatchCam& cam, const LocalBufsHost& h, float th, float nnratio, hipStream_t s, ProfileHook* prof)
+{
+    LocalBufs b;
+    b.cur_kps = h.cur_kps; b.cur_desc = h.cur_desc; b.cur_ur = h.cur_ur; b.cur_obs = h.cur_obs; b.cur_n = h.cur_n;
+    b.in_view = h.in_view; b.proj_x = h.proj_x; b.proj_y = h.proj_y; b.proj_xr = h.proj_xr; b.level = h.level;
+    b.view_cos = h.view_cos; b.desc = h.desc; b.nobs = h.nobs; b.mp_n = h.mp_n;
+    b.match = h.match; b.nmatch = h.nmatch; b.lists = h.lists; b.err = h.err; b.path = h.path;
+    const int force_seq = getenv("COEB_MATCH_SEQUENTIAL") ? 1 : 0;
+    const int cs = std::max(h.cur_n, 1), qs = std::max(h.mp_n, 1);
+    const size_t lds_full = match_lds_bytes(cs, qs, true, nullptr) + 256;
+    const size_t lds_min = match_lds_bytes(cs, qs, false, nullptr) + 256;
+    prof_begin(prof, "k_match_local", s);
+    if (lds_full <= 160 * 1024) {
+        (void)hipFuncSetAttribute((const void*)k_match_local<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_full);
+        hipLaunchKernelGGL(k_match_local<true>, dim3(1), dim3(kMThreads), lds_full - 256, s, cam, b, th, nnratio, force_seq);
+    } else if (lds_min <= 160 * 1024) {
+        (void)hipFuncSetAttribute((const void*)k_match_local<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_min);
+        hipLaunchKernelGGL(k_match_local<false>, dim3(1), dim3(kMThreads), lds_min - 256, s, cam, b, th, nnratio, force_seq);
+    } else {
+        prof_end(prof, s);
+        return -2;
+    }
+    prof_end(prof, s);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int match_list_cap() { return kCQ; }

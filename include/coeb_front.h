@@ -21,6 +21,10 @@
  *                                      include/ORBmatcher.h:52, src/ORBmatcher.cc:1329-1471
  *                                      (with Frame::GetFeaturesInArea / AssignFeaturesToGrid,
  *                                      src/Frame.cc:396-411, 503-568)
+ *   coeb_match_localmap             <- ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&,
+ *                                      const float th)  include/ORBmatcher.h:46,
+ *                                      src/ORBmatcher.cc:44-129 (RadiusByViewingCos :131-137),
+ *                                      the call in Tracking::SearchLocalPoints  src/Tracking.cc:1222-1271
  *   coeb_descriptor_distance        <- ORBmatcher::DescriptorDistance  src/ORBmatcher.cc:1648-1664
  *
  * Conventions: 0 on success, negative COEB_E* code on failure (the reference has no error
@@ -170,6 +174,31 @@ int coeb_match_lastframe(coeb_ctx* ctx, const coeb_camera* cam, const coeb_curfr
                          const coeb_lastframe* last, const float Tcw_cur[16], const float Tcw_last[16],
                          float th, int bmono, int check_orientation, int32_t* match_out, int* nmatches);
 
+/* Local-map points as Frame::isInFrustum left them (Frame.cc:445-501 writes mbTrackInView,
+ * mTrackProjX/Y/XR, mnTrackScaleLevel, mTrackViewCos); ORBmatcher.cc:50-80 reads exactly these. */
+typedef struct {
+    int32_t n;                        /* vpMapPoints.size() */
+    const uint8_t* in_view;           /* mbTrackInView && !isBad() */
+    const float* proj_x;              /* mTrackProjX */
+    const float* proj_y;              /* mTrackProjY */
+    const float* proj_xr;             /* mTrackProjXR */
+    const int32_t* level;             /* mnTrackScaleLevel (0 .. nlevels-1 where in_view) */
+    const float* view_cos;            /* mTrackViewCos */
+    const uint8_t* descriptor;        /* n x 32, GetDescriptor() */
+    const int32_t* observations;      /* Observations() */
+} coeb_localmap;
+
+/* ---- ORBmatcher::SearchByProjection(CurrentFrame, vpLocalMapPoints, th) ----
+ * cur_observations[i] (length cur->n, may be NULL = all NULL): Observations() of the MapPoint
+ * already in CurrentFrame.mvpMapPoints[i], or -1 for NULL; keypoints whose holder has
+ * Observations() > 0 are skipped (ORBmatcher.cc:86-88), as are keypoints given on the way to a
+ * point with Observations() > 0.  match_out[i] (length cur->n) = index of the local-map point
+ * assigned to keypoint i by this call (the last one when several were), or -1; *nmatches = the
+ * return value (every assignment counts, as in the reference).  nnratio = mfNNratio. */
+int coeb_match_localmap(coeb_ctx* ctx, const coeb_camera* cam, const coeb_curframe* cur,
+                        const int32_t* cur_observations, const coeb_localmap* mp, float th,
+                        float nnratio, int32_t* match_out, int* nmatches);
+
 /* ---- Frame helpers ---- */
 int coeb_blur_flags(coeb_ctx* ctx, const uint8_t* gray, int width, int height, size_t stride,
                     const coeb_box* boxes, int nbox, int32_t* flags_out);
@@ -205,7 +234,9 @@ int coeb_device_count(void);
 /* Test support: copy an intermediate buffer of frame `frame` of the last batch to the host.
  * what: "pyr" (levels 1..L-1, packed), "blur" (levels 0..L-1), "cand_n" (FAST corners per
  * cell), "lvl_n" (keypoints per level), "lvl_kp" (packed level keypoints), "dyn" (mask
- * rectangles), "plan".  Copies min(bytes, size); *size_out = full size. */
+ * rectangles), "plan", "localmap_path" (int32 {path, iterations} of the last
+ * coeb_match_localmap: 0 parallel claims, 1 forced sequential, 2 candidate-list overflow, 3 no
+ * convergence; frame ignored).  Copies min(bytes, size); *size_out = full size. */
 int coeb_debug_read(coeb_ctx* ctx, const char* what, int frame, void* host, size_t bytes, size_t* size_out);
 
 #ifdef __cplusplus

@@ -50,6 +50,12 @@ class CurFrame(C.Structure):
     _fields_ = [("n", C.c_int), ("keys_un", C.c_void_p), ("desc", C.c_void_p), ("uright", C.c_void_p)]
 
 
+class LocalMap(C.Structure):
+    _fields_ = [("n", C.c_int), ("in_view", C.c_void_p), ("proj_x", C.c_void_p), ("proj_y", C.c_void_p),
+                ("proj_xr", C.c_void_p), ("level", C.c_void_p), ("view_cos", C.c_void_p), ("desc", C.c_void_p),
+                ("nobs", C.c_void_p)]
+
+
 class Grid(C.Structure):
     _fields_ = [("cell_start", C.c_void_p), ("cell_idx", C.c_void_p)]
 
@@ -161,6 +167,27 @@ def search_by_projection(cam, cur_kps, cur_desc, cur_ur, last, Tcw_cur, Tcw_last
     Tl = np.ascontiguousarray(Tcw_last, np.float32)
     nm = lib().oc_search_by_projection(C.byref(cam), C.byref(cf), C.byref(lf), ptr(Tc), ptr(Tl),
                                        C.c_float(th), int(bmono), int(check_ori), ptr(out))
+    return nm, out[: len(cur_kps)]
+
+
+LOCALMAP_FIELDS = (("in_view", np.uint8), ("proj_x", np.float32), ("proj_y", np.float32), ("proj_xr", np.float32),
+                   ("level", np.int32), ("view_cos", np.float32), ("descriptor", np.uint8), ("observations", np.int32))
+
+
+def search_local_map(cam, cur_kps, cur_desc, cur_ur, cur_obs, mp, th=3.0, nnratio=0.8):
+    """ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) (ORBmatcher.cc:44-129).
+    cur_obs: i32[n] Observations() of the MapPoint already on each current keypoint (-1: none).
+    mp: dict of LOCALMAP_FIELDS arrays.  Returns (nmatches, match[n]: local-map index or -1)."""
+    cur_kps = np.ascontiguousarray(cur_kps)
+    cur_desc = np.ascontiguousarray(cur_desc, np.uint8)
+    cur_ur = np.ascontiguousarray(cur_ur, np.float32)
+    cur_obs = np.ascontiguousarray(cur_obs, np.int32)
+    cf = CurFrame(len(cur_kps), cur_kps.ctypes.data, cur_desc.ctypes.data, cur_ur.ctypes.data)
+    arrs = {k: np.ascontiguousarray(mp[k], dt) for k, dt in LOCALMAP_FIELDS}
+    lm = LocalMap(len(arrs["in_view"]), *[arrs[k].ctypes.data for k, _ in LOCALMAP_FIELDS])
+    out = np.zeros(max(len(cur_kps), 1), np.int32)
+    nm = lib().oc_search_local_map(C.byref(cam), C.byref(cf), ptr(cur_obs), C.byref(lm), C.c_float(th),
+                                   C.c_float(nnratio), ptr(out))
     return nm, out[: len(cur_kps)]
 
 

@@ -1155,3 +1155,66 @@ int oc_search_by_projection(const oc_camera* cam, const oc_curframe* cur, const 
     free(g.cell_idx);
     return nmatches;
 }
+
+/* ORBmatcher::RadiusByViewingCos (src/ORBmatcher.cc:131-137) */
+static float radius_by_viewing_cos(float viewCos) { return viewCos > 0.998f ? 2.5f : 4.0f; }
+
+/* ORBmatcher::SearchByProjection(Frame &F, const vector<MapPoint*> &vpMapPoints, const float th)
+ * (src/ORBmatcher.cc:44-129).  The MapPoint* written into F.mvpMapPoints is tracked as the
+ * local-map index (match_out) plus the Observations() of whoever holds each keypoint. */
+int oc_search_local_map(const oc_camera* cam, const oc_curframe* cur, const int32_t* cur_obs,
+                        const oc_localmap* mp, float th, float nnratio, int32_t* match_out)
+{
+    enum { TH_HIGH = 100 };
+    int nmatches = 0;
+    const int bFactor = th != 1.0f;
+    oc_grid g;
+    g.cell_start = (int*)malloc(sizeof(int) * (OC_GRID_COLS * OC_GRID_ROWS + 1));
+    g.cell_idx = (int*)malloc(sizeof(int) * (cur->n > 0 ? cur->n : 1));
+    oc_assign_grid(cam, cur->keys_un, cur->n, &g);
+    int* holder_obs = (int*)malloc(sizeof(int) * (cur->n > 0 ? cur->n : 1));   /* Observations() of F.mvpMapPoints[i], -1 = NULL */
+    for (int i = 0; i < cur->n; i++) { holder_obs[i] = cur_obs ? cur_obs[i] : -1; match_out[i] = -1; }
+    int* cand = (int*)malloc(sizeof(int) * (cur->n > 0 ? cur->n : 1));
+    for (int q = 0; q < mp->n; q++) {
+        if (!mp->in_view[q]) continue;                            /* :53-57 */
+        const int nPredictedLevel = mp->level[q];
+        float r = radius_by_viewing_cos(mp->view_cos[q]);         /* :62 */
+        if (bFactor) r *= th;
+        const float rs = r * cam->scale[nPredictedLevel];
+        const int nc = oc_features_in_area(cam, cur->keys_un, &g, mp->proj_x[q], mp->proj_y[q], rs,
+                                           nPredictedLevel - 1, nPredictedLevel, cand, cur->n);
+        if (nc == 0) continue;
+        const uint8_t* dMP = &mp->desc[32 * q];
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (int c = 0; c < nc; c++) {
+            const int idx = cand[c];
+            if (holder_obs[idx] > 0) continue;                   /* :86-88 */
+            if (cur->uright[idx] > 0) {                          /* :90-95 */
+                const float er = fabsf(mp->proj_xr[q] - cur->uright[idx]);
+                if (er > r * cam->scale[nPredictedLevel]) continue;
+            }
+            const int dist = oc_descriptor_distance(dMP, &cur->desc[32 * idx]);
+            if (dist < bestDist) {                               /* :101-113 */
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = cur->keys_un[idx].octave;
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = cur->keys_un[idx].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_HIGH) {                               /* :117-125 */
+            if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
+            match_out[bestIdx] = q;
+            holder_obs[bestIdx] = mp->nobs[q];
+            nmatches++;
+        }
+    }
+    free(cand);
+    free(holder_obs);
+    free(g.cell_start);
+    free(g.cell_idx);
+    return nmatches;
+}

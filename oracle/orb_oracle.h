@@ -144,6 +144,27 @@ int oc_search_by_projection(const oc_camera* cam, const oc_curframe* cur, const 
                             const float Tcw_cur[16], const float Tcw_last[16],
                             float th, int bMono, int check_ori, int32_t* match_out);
 
+/* Local-map points as Frame::isInFrustum left them (Frame.cc:463-501): the inputs of
+ * ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th) */
+typedef struct {
+    int n;
+    const uint8_t* in_view;        /* mbTrackInView && !isBad() */
+    const float* proj_x;           /* mTrackProjX */
+    const float* proj_y;           /* mTrackProjY */
+    const float* proj_xr;          /* mTrackProjXR */
+    const int32_t* level;          /* mnTrackScaleLevel */
+    const float* view_cos;         /* mTrackViewCos */
+    const uint8_t* desc;           /* GetDescriptor(), n x 32 */
+    const int32_t* nobs;           /* Observations() */
+} oc_localmap;
+
+/* ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th) (ORBmatcher.cc:44-129)
+ * with RadiusByViewingCos (:131-137).  cur_obs[i2] = Observations() of the MapPoint already in
+ * CurrentFrame.mvpMapPoints[i2] at entry (< 0: none).  match_out[i2] = index of the local-map
+ * point assigned to keypoint i2 by this call (the last one), or -1 (entry unchanged). */
+int oc_search_local_map(const oc_camera* cam, const oc_curframe* cur, const int32_t* cur_obs,
+                        const oc_localmap* mp, float th, float nnratio, int32_t* match_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,11 +7,18 @@ struct MapPoint {
     cv::Mat GetWorldPos() { return cv::Mat(); }
     cv::Mat GetDescriptor() { return cv::Mat(); }
     int Observations() { return 2; }
+    bool isBad() { return false; }
+    bool mbTrackInView = false;
+    float mTrackProjX = 0, mTrackProjY = 0, mTrackProjXR = 0;
+    int mnTrackScaleLevel = 0;
+    float mTrackViewCos = 0;
 };
 struct Frame {
     static float fx, fy, cx, cy, mnMinX, mnMaxX, mnMinY, mnMaxY;
     float mbf = 0, mb = 0;
     int N = 0;
+    int mnScaleLevels = 8;
+    float mfScaleFactor = 1.2f;
     std::vector<cv::KeyPoint> mvKeysUn;
     std::vector<float> mvuRight;
     std::vector<MapPoint*> mvpMapPoints;
@@ -29,5 +36,7 @@ int use_adapters(Frame& cur, const Frame& last, cv::Mat& im)
     std::vector<cv::Point2f> tm;
     std::vector<int> blur;
     ex(im, cv::Mat(), im, im, kps, desc, box, tm, mask_result, blur);
-    return coeb::SearchByProjectionLastFrame(cur, last, 15.0f, false, 0.9f, true) + ex.GetLevels();
+    std::vector<MapPoint*> local;
+    return coeb::SearchByProjectionLastFrame(cur, last, 15.0f, false, 0.9f, true) + ex.GetLevels() +
+           coeb::SearchByProjectionLocalMap(cur, local, 3.0f, 0.8f);
 }

@@ -365,3 +365,114 @@ def test_batch_streams_agree(oracle_mod, ex):
             assert n1[f] == nm and np.array_equal(m1[f], mm), f
     finally:
         bp.close()
+
+
+# ------------------------------------------------------------------ local-map projection search
+def localmap_both(ctx, oracle_mod, ex, cur_k, cur_d, cur_ur, cur_obs, mp, th=3.0, nnratio=0.8):
+    """coeb_match_localmap vs oracle.search_local_map (ORBmatcher.cc:44-129), bit-exact."""
+    import coeb_front
+    cam_o = oracle_mod.camera(ex, 640, 480, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    obs = np.full(len(cur_k), -1, np.int32) if cur_obs is None else cur_obs
+    nm_ref, m_ref = oracle_mod.search_local_map(cam_o, cur_k, cur_d, cur_ur, obs, mp, th, nnratio)
+    cam = coeb_front.make_camera(synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF, 640, 480)
+    F = coeb_front.Frame(cur_k, cur_d, cur_ur)
+    if cur_obs is not None:
+        F.mvpMapPointObs = cur_obs.copy()
+    lm = coeb_front.LocalMap(mp["in_view"], mp["proj_x"], mp["proj_y"], mp["proj_xr"], mp["level"], mp["view_cos"],
+                             mp["descriptor"], mp["observations"])
+    nm = coeb_front.ORBmatcher(nnratio, ctx=ctx).SearchByProjection(F, lm, th, camera=cam)
+    got = F.mvpMapPoints
+    assert nm == nm_ref, (nm, nm_ref)
+    assert np.array_equal(got, m_ref), int(np.sum(got != m_ref))
+    return nm
+
+
+def localmap_path(ctx):
+    """(path, iterations) of the last coeb_match_localmap: 0 parallel claims, 1 forced
+    sequential, 2 candidate-list overflow, 3 no convergence."""
+    p = ctx.debug_read("localmap_path").view(np.int32)
+    return int(p[0]), int(p[1])
+
+
+@pytest.fixture(scope="module")
+def local_scene(oracle_mod, ex, pair):
+    r1, ur1, last = pair
+    Tc = synth.motion_pose()
+    return r1, ur1, last, Tc
+
+
+@pytest.mark.parametrize("seed,th,nnratio", [(0, 3.0, 0.8), (1, 1.0, 0.8), (2, 5.0, 0.8), (3, 3.0, 1.0),
+                                             (4, 3.0, 0.6)])
+def test_localmap_matches_oracle(ctx, oracle_mod, ex, local_scene, seed, th, nnratio):
+    r1, ur1, last, Tc = local_scene
+    mp = synth.make_local_map(last["xw"], last["mp_desc"], last["keys_un"]["octave"], Tc, 640, 480, seed=seed)
+    rng = np.random.default_rng(100 + seed)
+    nm = localmap_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, None, mp, th, nnratio)
+    assert nm > 50
+    assert localmap_path(ctx)[0] == 0          # the parallel claim resolution produced this
+    # keypoints already holding MapPoints (Observations() -1 / 0 / >0, ORBmatcher.cc:86-88)
+    obs = rng.choice(np.array([-1, -1, 0, 2], np.int32), len(r1["kps"])).astype(np.int32)
+    localmap_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, obs, mp, th, nnratio)
+    # monocular current frame (mvuRight < 0 everywhere)
+    localmap_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], np.full(len(ur1), -1, np.float32), obs, mp, th, nnratio)
+
+
+def test_localmap_paths_agree(ctx, oracle_mod, ex, local_scene, monkeypatch):
+    """Parallel claim fixpoint and the literal sequential loop (COEB_MATCH_SEQUENTIAL) agree."""
+    r1, ur1, last, Tc = local_scene
+    mp = synth.make_local_map(last["xw"], last["mp_desc"], last["keys_un"]["octave"], Tc, 640, 480, seed=9,
+                              dup_frac=0.8)
+    obs = np.random.default_rng(9).choice(np.array([-1, 0, 3], np.int32), len(r1["kps"])).astype(np.int32)
+    for seq in (False, True):
+        if seq:
+            monkeypatch.setenv("COEB_MATCH_SEQUENTIAL", "1")
+        localmap_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, obs, mp, 3.0, 0.8)
+        assert localmap_path(ctx)[0] == (1 if seq else 0)
+        localmap_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, None, mp, 5.0, 0.9)
+        assert localmap_path(ctx)[0] == (1 if seq else 0)
+    monkeypatch.delenv("COEB_MATCH_SEQUENTIAL")
+
+
+def test_localmap_edge_cases(ctx, oracle_mod, ex, local_scene):
+    import coeb_front
+    r1, ur1, last, Tc = local_scene
+    mp = synth.make_local_map(last["xw"], last["mp_desc"], last["keys_un"]["octave"], Tc, 640, 480, seed=5)
+    empty = {k: v[:0] for k, v in mp.items()}
+    assert localmap_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, None, empty) == 0
+    k0 = r1["kps"][:0]
+    assert localmap_both(ctx, oracle_mod, ex, k0, r1["desc"][:0], ur1[:0], None, mp) == 0
+    off = dict(mp)
+    off["in_view"] = np.zeros_like(mp["in_view"])
+    assert localmap_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, None, off) == 0
+    # every point predicted at level 0 (window levels [-1, 0]) or at the top level
+    for lv in (0, 7):
+        v = dict(mp)
+        v["level"] = np.where(mp["in_view"] > 0, lv, -1).astype(np.int32)
+        localmap_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, None, v, 5.0)
+    # a level outside the pyramid on a point in view is rejected, not read out of bounds
+    bad = dict(mp)
+    bad["level"] = mp["level"].copy()
+    bad["level"][np.argmax(mp["in_view"])] = 8
+    with pytest.raises(coeb_front.CoebError):
+        localmap_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, None, bad)
+
+
+def test_localmap_crowded_windows(ctx, oracle_mod, ex):
+    """Repetitive texture + a wide window: candidate lists overflow (sequential fallback)."""
+    yy, xx = np.indices((480, 640))
+    base = (((yy // 12) + (xx // 12)) % 2 * 200 + 30).astype(np.int16)
+    rng = np.random.default_rng(8)
+    f0 = np.clip(base + rng.integers(-6, 7, base.shape), 0, 255).astype(np.uint8)
+    f1 = np.clip(np.roll(base, (1, 2), axis=(0, 1)) + rng.integers(-6, 7, base.shape), 0, 255).astype(np.uint8)
+    r0, r1 = ex.extract(f0), ex.extract(f1)
+    depth = synth.make_depth(640, 480)
+    last = oracle_mod.mapframe_from_extraction(r0["kps"], r0["desc"], depth, synth.TUM_FX, synth.TUM_FY,
+                                               synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    ur1, _ = oracle_mod.stereo_from_rgbd(r1["kps"], depth, synth.TUM_BF)
+    mp = synth.make_local_map(last["xw"], last["mp_desc"], last["keys_un"]["octave"], synth.motion_pose(), 640, 480,
+                              seed=3)
+    paths = []
+    for th in (3.0, 12.0):
+        localmap_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, None, mp, th)
+        paths.append(localmap_path(ctx)[0])
+    assert paths == [0, 2], paths

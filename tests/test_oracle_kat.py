@@ -172,3 +172,108 @@ def test_resize_and_blur_constant_images(oracle_mod):
         r = ex.extract(img, debug=True)
         assert (r["pyramid"] == v).all()
         assert len(r["kps"]) == 0
+
+
+# ---- local-map SearchByProjection: C oracle vs a literal Python loop (ORBmatcher.cc:44-129) ----
+def _py_search_local_map(cam, kps, desc, ur, cur_obs, mp, th, nnratio):
+    """Pure-Python restatement, small sizes only: AssignFeaturesToGrid (Frame.cc:396-411,
+    PosInGrid :553-568), GetFeaturesInArea (:503-551), the search loop (ORBmatcher.cc:44-129)."""
+    f32 = np.float32
+    cols, rows = 64, 48
+    grid = [[[] for _ in range(rows)] for _ in range(cols)]
+    for i, k in enumerate(kps):
+        px = math.floor(abs(float((f32(k["x"]) - cam.min_x) * f32(cam.grid_inv_w))) + 0.5)
+        py = math.floor(abs(float((f32(k["y"]) - cam.min_y) * f32(cam.grid_inv_h))) + 0.5)
+        if (f32(k["x"]) - cam.min_x) < 0:
+            px = -px
+        if (f32(k["y"]) - cam.min_y) < 0:
+            py = -py
+        if 0 <= px < cols and 0 <= py < rows:
+            grid[px][py].append(i)
+
+    def in_area(x, y, r, minL, maxL):
+        out = []
+        x0 = max(0, math.floor(float((f32(x) - f32(cam.min_x) - f32(r)) * f32(cam.grid_inv_w))))
+        if x0 >= cols:
+            return out
+        x1 = min(cols - 1, math.ceil(float((f32(x) - f32(cam.min_x) + f32(r)) * f32(cam.grid_inv_w))))
+        if x1 < 0:
+            return out
+        y0 = max(0, math.floor(float((f32(y) - f32(cam.min_y) - f32(r)) * f32(cam.grid_inv_h))))
+        if y0 >= rows:
+            return out
+        y1 = min(rows - 1, math.ceil(float((f32(y) - f32(cam.min_y) + f32(r)) * f32(cam.grid_inv_h))))
+        if y1 < 0:
+            return out
+        chk = minL > 0 or maxL >= 0
+        for ix in range(x0, x1 + 1):
+            for iy in range(y0, y1 + 1):
+                for j in grid[ix][iy]:
+                    if chk and (kps[j]["octave"] < minL or (maxL >= 0 and kps[j]["octave"] > maxL)):
+                        continue
+                    if abs(f32(kps[j]["x"]) - f32(x)) < f32(r) and abs(f32(kps[j]["y"]) - f32(y)) < f32(r):
+                        out.append(j)
+        return out
+
+    holder = list(cur_obs)
+    match = [-1] * len(kps)
+    nm = 0
+    for q in range(len(mp["in_view"])):
+        if not mp["in_view"][q]:
+            continue
+        lvl = int(mp["level"][q])
+        r = f32(2.5) if f32(mp["view_cos"][q]) > f32(0.998) else f32(4.0)
+        if th != 1.0:
+            r = f32(r * f32(th))
+        rs = f32(r * f32(cam.scale[lvl]))
+        best, bl, best2, bl2, bi = 256, -1, 256, -1, -1
+        for idx in in_area(mp["proj_x"][q], mp["proj_y"][q], rs, lvl - 1, lvl):
+            if holder[idx] > 0:
+                continue
+            if ur[idx] > 0 and abs(f32(mp["proj_xr"][q]) - f32(ur[idx])) > rs:
+                continue
+            d = sum(bin(int(a) ^ int(b)).count("1") for a, b in zip(mp["descriptor"][q], desc[idx]))
+            if d < best:
+                best2, bl2, best, bl, bi = best, bl, d, int(kps[idx]["octave"]), idx
+            elif d < best2:
+                bl2, best2 = int(kps[idx]["octave"]), d
+        if best <= 100:
+            if bl == bl2 and f32(best) > f32(nnratio) * f32(best2):
+                continue
+            match[bi] = q
+            holder[bi] = int(mp["observations"][q])
+            nm += 1
+    return nm, np.array(match, np.int32)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_search_local_map_oracle_vs_python(oracle_mod, seed):
+    rng = np.random.default_rng(seed)
+    ex = oracle_mod.Extractor()
+    cam = oracle_mod.camera(ex, 640, 480, 535.4, 539.2, 320.1, 247.6, 40.0)
+    n, m = 300, 260
+    kps = np.zeros(n, oracle_mod.KP_DTYPE)
+    kps["x"] = rng.uniform(0, 640, n)
+    kps["y"] = rng.uniform(0, 480, n)
+    kps["octave"] = rng.integers(0, 8, n)
+    desc = rng.integers(0, 256, (n, 32)).astype(np.uint8)
+    ur = np.where(rng.random(n) < 0.7, kps["x"] - rng.uniform(5, 30, n), -1).astype(np.float32)
+    cur_obs = rng.choice(np.array([-1, -1, 0, 2], np.int32), n).astype(np.int32)
+    src = rng.integers(0, n, m)
+    d = desc[src].copy()
+    flip = rng.integers(0, 256, (m, 30))
+    for q in range(m):                       # 0..30 flipped bits: near and far descriptors
+        for b in flip[q, : rng.integers(0, 31)]:
+            d[q, b >> 3] ^= np.uint8(1 << (b & 7))
+    px = (kps["x"][src] + rng.normal(0, 3, m)).astype(np.float32)
+    mp = dict(in_view=(rng.random(m) < 0.9).astype(np.uint8), proj_x=px,
+              proj_y=(kps["y"][src] + rng.normal(0, 3, m)).astype(np.float32),
+              proj_xr=(px - rng.uniform(5, 30, m)).astype(np.float32),
+              level=np.clip(kps["octave"][src] + rng.integers(-1, 2, m), 0, 7).astype(np.int32),
+              view_cos=rng.uniform(0.99, 1.0, m).astype(np.float32), descriptor=d,
+              observations=rng.choice(np.array([0, 1, 2], np.int32), m).astype(np.int32))
+    for th, ratio in ((3.0, 0.8), (1.0, 1.0), (6.0, 0.6)):
+        nm, mt = oracle_mod.search_local_map(cam, kps, desc, ur, cur_obs, mp, th, ratio)
+        nm_py, mt_py = _py_search_local_map(cam, kps, desc, ur, cur_obs, mp, th, ratio)
+        assert nm == nm_py and np.array_equal(mt, mt_py)
+        assert nm > 0
