@@ -293,6 +293,28 @@ __device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us
 __device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ us2 pk2(int lo, int hi) { us2 r; r.x = (unsigned short)lo; r.y = (unsigned short)hi; return r; }
 
+#ifndef COEB_XCD_REMAP
+#define COEB_XCD_REMAP 1
+#endif
+// Logical (x, y) block of a 2-D grid with each XCD given a contiguous run of logical blocks.
+// Blocks are observed to be dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, Workgroup
+// dispatch & XCD placement): physical block p lands on XCD p % 8.  Mapping XCD x's k-th block
+// to logical block x*q + min(x, r) + k (q, r = n / 8, n % 8) keeps the blocks of one frame
+// (y) on one L2, so the patches / ROIs they share are fetched into one L2 instead of eight.
+// Performance only: any placement gives the same results.  Measured (256 frames): k_describe
+// 0.227 -> 0.215 ms, k_blur 0.178 -> 0.169 ms; k_fast 0.320 -> 0.324 ms, so k_fast keeps the
+// round-robin order (its cells share only 3-px borders).
+template <bool kRemap = true>
+__device__ __forceinline__ int2 block_xy()
+{
+    const int gx = gridDim.x;
+    if (!COEB_XCD_REMAP || !kRemap) return make_int2(blockIdx.x, blockIdx.y);
+    const int n = gx * gridDim.y, p = blockIdx.x + gx * blockIdx.y;
+    const int q = n >> 3, r = n & 7, x = p & 7, k = p >> 3;
+    const int lg = x * q + min(x, r) + k;
+    return make_int2(lg % gx, lg / gx);
+}
+
 __device__ __forceinline__ uint32_t dpp_shr1(uint32_t v)   // lane i <- lane i-1 (16-lane rows)
 {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, false);
@@ -304,8 +326,9 @@ __device__ __forceinline__ uint32_t dpp_shl1(uint32_t v)   // lane i <- lane i+1
 
 __global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, ExtractBufs b, BlurWork bw)
 {
-    const int f = blockIdx.y;
-    const int item = blockIdx.x * kWaves + wave_id();
+    const int2 bxy = block_xy();
+    const int f = bxy.y;
+    const int item = bxy.x * kWaves + wave_id();
     if (item >= bw.item_off[bw.L]) return;
     int l = 0;
     while (l + 1 < bw.L && item >= bw.item_off[l + 1]) l++;
@@ -840,8 +863,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
     uint8_t* Ms = wbase + slab;
     uint16_t* surv = reinterpret_cast<uint16_t*>(wbase + 2 * slab);
     uint16_t* corn = surv + kFastSurv;
-    const int f = blockIdx.y;
-    int cidx = (blockIdx.x * kWaves + wv) * kFastCellsPerWave;
+    const int2 bxy = block_xy<false>();
+    const int f = bxy.y;
+    int cidx = (bxy.x * kWaves + wv) * kFastCellsPerWave;
     if (cidx >= P->ncells) return;
     const int area = b.dyn[f].area_flag;
     const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
@@ -1630,7 +1654,8 @@ template <bool kVec0>
 __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ P, ExtractBufs b)
 {
     __shared__ __attribute__((aligned(16))) uint8_t s_slab[kWaves][kDescSlab];
-    const int f = blockIdx.y;
+    const int2 bxy = block_xy();
+    const int f = bxy.y;
     const int L = P->L;
     const int lane = lane_id(), wv = wave_id();
     // per-level keypoint offsets (wave prefix over lanes 0..L-1)
@@ -1641,8 +1666,8 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         if (lane >= o) incl += y;
     }
     const int total = __builtin_amdgcn_readlane(incl, L - 1);
-    if (blockIdx.x == 0 && threadIdx.x == 0) b.counts[f] = total;
-    const int idx0 = (blockIdx.x * kWaves + wv) * kDescKp;
+    if (bxy.x == 0 && threadIdx.x == 0) b.counts[f] = total;
+    const int idx0 = (bxy.x * kWaves + wv) * kDescKp;
     if (idx0 >= total) return;
     const int nk = min(kDescKp, total - idx0);
     // ---- phase A: lanes k, k+32 = keypoint idx0 + k (excess repeat the last one, no writes)

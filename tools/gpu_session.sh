@@ -18,8 +18,8 @@ run() {
 }
 for step in "$@"; do
     case "$step" in
-        pytest) run pytest_gpu 900 python -m pytest tests -q -m gpu -x ;;
-        pytestall) run pytest_gpu 900 python -m pytest tests -q -m gpu ;;
+        pytest) run pytest_gpu 900 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread ;;
+        pytestall) run pytest_gpu 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
         benchB) run benchB 600 python bench.py --config B --batch 64 --no-cpu-baseline ;;

@@ -21,21 +21,28 @@ def load(path):
     return {k: ({c: v / len(disp[k]) for c, v in agg[k].items()}, len(disp[k]), grid[k]) for k in agg}
 
 
-def traffic_json(merged, nd, frames, command, fetch_scale):
-    """Per kernel, HBM bytes per launch: fetch_scale x FETCH_SIZE + WRITE_SIZE (rocprofv3 KB).
-    MI355X_MICROARCH.md s HBM: FETCH_SIZE reads 1/2 of the bytes of 16-B-per-lane streaming
-    reads (fetch_scale 2 there); other widths are uncalibrated and must be calibrated on a known
-    byte count.  Every kernel here loads <= 4 B per lane; k_blur (each level byte read once plus
-    the 6-row vertical halo, each written once) is the calibration: raw FETCH_SIZE ~ its known
-    read bytes, so fetch_scale = 1."""
-    out = dict(frames_per_launch=frames, command=command, fetch_scale=fetch_scale,
-               correction="bytes = (%g * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch, mean over dispatches" % fetch_scale,
+# kernels whose HBM reads are 16-byte-per-lane loads (uint4): k_pyr_level tile staging,
+# k_fast ROI staging, k_describe patch rows
+WIDE16 = ("k_pyr_level", "k_fast", "k_describe")
+
+
+def traffic_json(merged, nd, frames, command, fetch_scale, wide_scale=2.0, wide=WIDE16):
+    """Per kernel, HBM bytes per launch: scale x FETCH_SIZE + WRITE_SIZE (rocprofv3 KB).
+    MI355X_MICROARCH.md s HBM: on gfx950 FETCH_SIZE reports 1/2 of the bytes of 16-B-per-lane
+    reads, so kernels in `wide` get wide_scale = 2.  The kernels loading <= 4 B per lane are
+    calibrated on k_blur (each level byte read once plus the 6-row vertical halo, each written
+    once): raw FETCH_SIZE ~ its known read bytes, so fetch_scale = 1 for them."""
+    out = dict(frames_per_launch=frames, command=command, fetch_scale=fetch_scale, wide_kernels=list(wide),
+               wide_scale=wide_scale,
+               correction="bytes = (s * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch, mean over dispatches; "
+                          "s = %g for the 16-B-load kernels (wide_kernels), %g otherwise" % (wide_scale, fetch_scale),
                kernels={})
     for k, cv in sorted(merged.items()):
         if "FETCH_SIZE" not in cv or "WRITE_SIZE" not in cv:
             continue
+        sc = wide_scale if k in wide else fetch_scale
         out["kernels"][k] = dict(fetch_kb=round(cv["FETCH_SIZE"], 3), write_kb=round(cv["WRITE_SIZE"], 3),
-                                 traffic_bytes=int((fetch_scale * cv["FETCH_SIZE"] + cv["WRITE_SIZE"]) * 1024),
+                                 fetch_scale=sc, traffic_bytes=int((sc * cv["FETCH_SIZE"] + cv["WRITE_SIZE"]) * 1024),
                                  dispatches=nd[k])
     return out
 
