@@ -2,6 +2,8 @@
  * ORBmatcher_coeb.h -- MI355X bodies for two ORBmatcher::SearchByProjection overloads:
  *   (Frame&, const Frame&, float th, bool bMono)  include/ORBmatcher.h:52, src/ORBmatcher.cc:1329-1471
  *   (Frame&, const vector<MapPoint*>&, float th)  include/ORBmatcher.h:46, src/ORBmatcher.cc:44-129
+ *   (Frame&, KeyFrame*, const set<MapPoint*>&, float th, int ORBdist)
+ *                                                 include/ORBmatcher.h:55, src/ORBmatcher.cc:1473-1600
  *
  * Included from the reference's src/ORBmatcher.cc (which already includes Frame.h and
  * MapPoint.h); the method body becomes
@@ -30,13 +32,25 @@
  * Observations() of F.mvpMapPoints[i] (-1 for NULL), then writes F.mvpMapPoints[i] =
  * vpMapPoints[match[i]] for the keypoints the call assigned.
  *
- * Both use a matcher context built with the frame's own pyramid (F.mnScaleLevels,
+ * The relocalisation overload body becomes
+ *
+ *     return coeb::SearchByProjectionKeyFrame(CurrentFrame, pKF, sAlreadyFound, th, ORBdist,
+ *                                             mbCheckOrientation);
+ *
+ * It snapshots pKF->GetMapPointMatches() as :1489-1530 reads it (valid = pMP && !isBad() &&
+ * !sAlreadyFound.count(pMP), GetWorldPos(), GetDescriptor(), the distance-invariance range and
+ * pKF->mvKeysUn[i].angle) and which keypoints of CurrentFrame already hold a MapPoint.
+ * MapPoint::PredictScale reads the protected mfMaxDistance, so the integration adds two locked
+ * getters to MapPoint (GetMaxDistance / GetMinDistance).
+ *
+ * All use a matcher context built with the frame's own pyramid (F.mnScaleLevels,
  * F.mfScaleFactor), so mvScaleFactors on the device are the frame's.
  */
 #ifndef COEB_ADAPTER_ORBMATCHER_H
 #define COEB_ADAPTER_ORBMATCHER_H
 
 #include <cstring>
+#include <set>
 #include <stdexcept>
 #include <vector>
 
@@ -149,6 +163,49 @@ inline int SearchByProjectionLocalMap(FrameT& F, const std::vector<MapPointT*>& 
     if (rc != COEB_OK) throw std::runtime_error(coeb_last_error(ctx));
     for (int i = 0; i < F.N; ++i)
         if (match[i] >= 0) F.mvpMapPoints[i] = vpMapPoints[match[i]];
+    return nmatches;
+}
+
+template <class FrameT, class KeyFrameT, class MapPointT>
+inline int SearchByProjectionKeyFrame(FrameT& CurrentFrame, KeyFrameT* pKF, const std::set<MapPointT*>& sAlreadyFound,
+                                      float th, int ORBdist, bool mbCheckOrientation, coeb_ctx* ctx = nullptr)
+{
+    if (!ctx) ctx = matcher_ctx(CurrentFrame.mnScaleLevels, CurrentFrame.mfScaleFactor);
+    const std::vector<MapPointT*> vpMPs = pKF->GetMapPointMatches();
+    const int nq = (int)vpMPs.size();
+    std::vector<uint8_t> valid(nq), desc((size_t)nq * 32), has((size_t)CurrentFrame.N);
+    std::vector<float> xw((size_t)nq * 3), maxd(nq), mind(nq), ang(nq);
+    for (int i = 0; i < nq; ++i) {
+        MapPointT* pMP = vpMPs[i];
+        valid[i] = pMP && !pMP->isBad() && !sAlreadyFound.count(pMP);
+        if (!valid[i]) continue;
+        cv::Mat x3D = pMP->GetWorldPos();
+        xw[3 * i + 0] = x3D.at<float>(0);
+        xw[3 * i + 1] = x3D.at<float>(1);
+        xw[3 * i + 2] = x3D.at<float>(2);
+        cv::Mat d = pMP->GetDescriptor();
+        std::memcpy(&desc[32 * (size_t)i], d.ptr<uint8_t>(0), 32);
+        maxd[i] = pMP->GetMaxDistance();
+        mind[i] = pMP->GetMinDistance();
+        ang[i] = pKF->mvKeysUn[i].angle;
+    }
+    for (int i = 0; i < CurrentFrame.N; ++i) has[i] = CurrentFrame.mvpMapPoints[i] != nullptr;
+    coeb_keyframe_points kf{nq, valid.data(), xw.data(), desc.data(), maxd.data(), mind.data(), ang.data()};
+    cv::Mat curDesc = CurrentFrame.mDescriptors.isContinuous() ? CurrentFrame.mDescriptors
+                                                               : CurrentFrame.mDescriptors.clone();
+    coeb_curframe cur{CurrentFrame.N, reinterpret_cast<const coeb_keypoint*>(CurrentFrame.mvKeysUn.data()),
+                      curDesc.empty() ? nullptr : curDesc.ptr<uint8_t>(0), nullptr};
+    const coeb_camera cam = frame_camera(CurrentFrame);
+    float T[16];
+    for (int r = 0; r < 4; ++r)
+        for (int k = 0; k < 4; ++k) T[4 * r + k] = CurrentFrame.mTcw.template at<float>(r, k);
+    std::vector<int32_t> match((size_t)CurrentFrame.N);
+    int nmatches = 0;
+    const int rc = coeb_match_keyframe(ctx, &cam, &cur, has.data(), &kf, T, th, ORBdist, mbCheckOrientation ? 1 : 0,
+                                       match.data(), &nmatches);
+    if (rc != COEB_OK) throw std::runtime_error(coeb_last_error(ctx));
+    for (int i = 0; i < CurrentFrame.N; ++i)
+        if (match[i] >= 0) CurrentFrame.mvpMapPoints[i] = vpMPs[match[i]];
     return nmatches;
 }
 

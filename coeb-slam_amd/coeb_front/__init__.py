@@ -11,6 +11,9 @@
   ORBmatcher(nnratio).SearchByProjection(F, LocalMap, th=3)
       include/ORBmatcher.h:46, src/ORBmatcher.cc:44-129 (the Tracking::SearchLocalPoints call,
       src/Tracking.cc:1222-1271); assigns F.mvpMapPoints[i] = local-map index and returns nmatches.
+  ORBmatcher(nnratio, checkOri).SearchByProjection(F, KeyFramePoints, sAlreadyFound, th, ORBdist)
+      include/ORBmatcher.h:55, src/ORBmatcher.cc:1473-1600 (Tracking::Relocalization,
+      src/Tracking.cc:1531,1545); assigns F.mvpMapPoints[i] = KeyFrame point index.
   ORBmatcher.DescriptorDistance(a, b)  src/ORBmatcher.cc:1648-1664
 
 All compute runs in libcoeb_front.so (hand-written gfx950 HIP kernels).  There is no CPU
@@ -40,7 +43,7 @@ ABI_SYMBOLS = [
     "coeb_rgbd_preprocess", "coeb_descriptor_distance", "coeb_profile_enable", "coeb_profile_read",
     "coeb_profile_reset", "coeb_synchronize", "coeb_device_count", "coeb_debug_read",
     "coeb_device_alloc", "coeb_device_free", "coeb_memcpy_h2d", "coeb_memcpy_d2h", "coeb_set_batch_streams",
-    "coeb_match_localmap",
+    "coeb_match_localmap", "coeb_match_keyframe",
 ]
 
 
@@ -74,6 +77,11 @@ class LocalMapC(C.Structure):
     _fields_ = [("n", C.c_int32), ("in_view", C.c_void_p), ("proj_x", C.c_void_p), ("proj_y", C.c_void_p),
                 ("proj_xr", C.c_void_p), ("level", C.c_void_p), ("view_cos", C.c_void_p), ("descriptor", C.c_void_p),
                 ("observations", C.c_void_p)]
+
+
+class KeyFramePointsC(C.Structure):
+    _fields_ = [("n", C.c_int32), ("valid", C.c_void_p), ("world_pos", C.c_void_p), ("descriptor", C.c_void_p),
+                ("max_distance", C.c_void_p), ("min_distance", C.c_void_p), ("angle", C.c_void_p)]
 
 
 class CoebError(RuntimeError):
@@ -114,6 +122,9 @@ def lib():
                                            C.c_int, C.c_void_p, C.POINTER(C.c_int)]
         L.coeb_match_localmap.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(CurFrameC), C.c_void_p,
                                           C.POINTER(LocalMapC), C.c_float, C.c_float, C.c_void_p, C.POINTER(C.c_int)]
+        L.coeb_match_keyframe.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(CurFrameC), C.c_void_p,
+                                          C.POINTER(KeyFramePointsC), C.c_void_p, C.c_float, C.c_int, C.c_int,
+                                          C.c_void_p, C.POINTER(C.c_int)]
         L.coeb_blur_flags.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_int,
                                       C.c_void_p]
         L.coeb_stereo_from_rgbd.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
@@ -415,6 +426,26 @@ class LocalMap:
             self.mTrackViewCos, self.mDescriptor, self.nObs)])
 
 
+class KeyFramePoints:
+    """pKF->GetMapPointMatches() snapshot for the relocalisation search (ORBmatcher.cc:1487-1530):
+    per slot i, valid (pMP && !isBad()), GetWorldPos(), GetDescriptor(), mfMaxDistance,
+    mfMinDistance and pKF->mvKeysUn[i].angle.  sAlreadyFound is passed to SearchByProjection as
+    a set of slot indices."""
+
+    def __init__(self, valid, world_pos, descriptor, max_distance, min_distance, angle):
+        self.valid = np.ascontiguousarray(valid, np.uint8)
+        self.N = len(self.valid)
+        self.world_pos = np.ascontiguousarray(world_pos, np.float32).reshape(self.N, 3)
+        self.descriptor = np.ascontiguousarray(descriptor, np.uint8).reshape(self.N, 32) if self.N else \
+            np.zeros((0, 32), np.uint8)
+        self.max_distance = np.ascontiguousarray(max_distance, np.float32)
+        self.min_distance = np.ascontiguousarray(min_distance, np.float32)
+        self.angle = np.ascontiguousarray(angle, np.float32)
+        for a in (self.max_distance, self.min_distance, self.angle):
+            if len(a) != self.N:
+                raise ValueError("KeyFramePoints arrays differ in length")
+
+
 class ORBmatcher:
     """Mirror of ORB_SLAM2::ORBmatcher for the tracking projection search."""
     TH_HIGH = 100
@@ -432,13 +463,20 @@ class ORBmatcher:
         b = np.ascontiguousarray(b, np.uint8)
         return lib().coeb_descriptor_distance(_p(a), _p(b))
 
-    def SearchByProjection(self, CurrentFrame, LastFrame, th=3.0, bMono=None, camera=None):
-        """(CurrentFrame, LastFrame, th, bMono, camera): ORBmatcher.cc:1329-1471;
-        (F, LocalMap, th=3, camera=...): ORBmatcher.cc:44-129."""
+    def SearchByProjection(self, CurrentFrame, second, *args, **kw):
+        """The reference's overloads, by the type of the second argument:
+          (CurrentFrame, LastFrame: Frame, th, bMono, camera)        ORBmatcher.cc:1329-1471
+          (F, vpMapPoints: LocalMap, th=3, camera=...)                 ORBmatcher.cc:44-129
+          (F, pKF: KeyFramePoints, sAlreadyFound, th, ORBdist, camera) ORBmatcher.cc:1473-1600"""
         if self.ctx is None:
             self.ctx = Context()
-        if isinstance(LastFrame, LocalMap):
-            return self._search_local_map(CurrentFrame, LastFrame, th, camera if camera is not None else bMono)
+        if isinstance(second, LocalMap):
+            return self._search_local_map(CurrentFrame, second, *args, **kw)
+        if isinstance(second, KeyFramePoints):
+            return self._search_keyframe(CurrentFrame, second, *args, **kw)
+        return self._search_last_frame(CurrentFrame, second, *args, **kw)
+
+    def _search_last_frame(self, CurrentFrame, LastFrame, th, bMono, camera):
         mp = LastFrame.map_points
         n = LastFrame.N
         lf_arrays = dict(has=np.ascontiguousarray(mp["valid"], np.uint8),
@@ -459,7 +497,26 @@ class ORBmatcher:
         return nm.value
 
 
-    def _search_local_map(self, F, local_map, th, camera):
+    def _search_keyframe(self, F, kf, sAlreadyFound=(), th=10.0, ORBdist=100, camera=None):
+        if camera is None:
+            raise ValueError("SearchByProjection(F, pKF, sAlreadyFound, th, ORBdist): camera is required")
+        valid = kf.valid.copy()
+        for i in sAlreadyFound:
+            valid[i] = 0
+        cf = CurFrameC(F.N, C.c_void_p(F.mvKeysUn.ctypes.data), C.c_void_p(F.mDescriptors.ctypes.data), None)
+        has = np.ascontiguousarray(F.mvpMapPoints >= 0, np.uint8)
+        kc = KeyFramePointsC(kf.N, *[C.c_void_p(a.ctypes.data) for a in (
+            valid, kf.world_pos, kf.descriptor, kf.max_distance, kf.min_distance, kf.angle)])
+        out = np.full(max(F.N, 1), -1, np.int32)
+        nm = C.c_int()
+        self.ctx.check(lib().coeb_match_keyframe(self.ctx.h, C.byref(camera), C.byref(cf), _p(has), C.byref(kc),
+                                                 _p(np.ascontiguousarray(F.mTcw, np.float32)), th, int(ORBdist),
+                                                 int(self.mbCheckOrientation), _p(out), C.byref(nm)))
+        got = out[:F.N]
+        F.mvpMapPoints = np.where(got >= 0, got, F.mvpMapPoints).astype(np.int32)
+        return nm.value
+
+    def _search_local_map(self, F, local_map, th=3.0, camera=None):
         if camera is None:
             raise ValueError("SearchByProjection(F, LocalMap, th): camera is required")
         cf = CurFrameC(F.N, C.c_void_p(F.mvKeysUn.ctypes.data), C.c_void_p(F.mDescriptors.ctypes.data),

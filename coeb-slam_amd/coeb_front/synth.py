@@ -142,3 +142,48 @@ def make_local_map(xw, desc, octave, Tcw, w, h, fx=TUM_FX, fy=TUM_FY, cx=TUM_CX,
                 level=np.where(in_view > 0, cat["lvl"][order], -1).astype(np.int32), view_cos=cos,
                 descriptor=np.ascontiguousarray(cat["desc"][order]),
                 observations=rng.choice(np.array([0, 1, 2, 3], np.int32), m, p=[0.3, 0.2, 0.3, 0.2]).astype(np.int32))
+
+
+def make_keyframe_points(xw, desc, octave, angle, scale_factor=1.2, nlevels=8, seed=0, n_distract=200,
+                         invalid_frac=0.1, far_frac=0.05):
+    """A synthetic pKF->GetMapPointMatches() snapshot for the relocalisation search: the map
+    points xw [n,3] of a KeyFrame at Twc = I, with mfMaxDistance = |x| * scale[octave] and
+    mfMinDistance = mfMaxDistance / scale[nlevels-1] (MapPoint::UpdateNormalAndDepth,
+    MapPoint.cc:352-369) jittered by +-10 % (a few pushed out of the invariance range), a
+    fraction invalid (NULL / bad), plus random distractors.  Returns a dict of the
+    coeb_keyframe_points arrays (valid, world_pos, descriptor, max_distance, min_distance, angle)."""
+    rng = np.random.default_rng(seed)
+    xw = np.asarray(xw, np.float32).reshape(-1, 3)
+    n = len(xw)
+    sc = np.float32(scale_factor) ** np.arange(nlevels, dtype=np.float32)
+    dist = np.sqrt((xw.astype(np.float64) ** 2).sum(1)).astype(np.float32)
+    maxd = (dist * sc[np.clip(octave, 0, nlevels - 1)] * rng.uniform(0.9, 1.1, n)).astype(np.float32)
+    far = rng.random(n) < far_frac
+    maxd[far] *= np.float32(0.3)                     # outside [0.8 min, 1.2 max]
+    mind = (maxd / sc[-1]).astype(np.float32)
+    dx = rng.uniform(-1.5, 1.5, (n_distract, 3)).astype(np.float32)
+    dx[:, 2] = rng.uniform(1.0, 4.0, n_distract)
+    dd = np.sqrt((dx.astype(np.float64) ** 2).sum(1)).astype(np.float32)
+    dmax = (dd * sc[rng.integers(0, nlevels, n_distract)]).astype(np.float32)
+    return dict(valid=np.concatenate([(rng.random(n) >= invalid_frac), np.ones(n_distract, bool)]).astype(np.uint8),
+                world_pos=np.ascontiguousarray(np.concatenate([xw, dx]), np.float32),
+                descriptor=np.ascontiguousarray(np.concatenate([np.asarray(desc, np.uint8).reshape(-1, 32),
+                                                                rng.integers(0, 256, (n_distract, 32)).astype(np.uint8)])),
+                max_distance=np.concatenate([maxd, dmax]).astype(np.float32),
+                min_distance=np.concatenate([mind, (dmax / sc[-1])]).astype(np.float32),
+                angle=np.concatenate([np.asarray(angle, np.float32),
+                                      rng.uniform(0, 360, n_distract).astype(np.float32)]).astype(np.float32))
+
+
+def rotated_pose(deg, axis=1, t=(0.02, -0.01, 0.03)):
+    """Tcw with a rotation of `deg` degrees about one axis plus a translation (relocalisation
+    poses that are not pure translations)."""
+    a = np.deg2rad(deg)
+    c, s = np.cos(a), np.sin(a)
+    R = np.eye(3)
+    i, j = [(1, 2), (0, 2), (0, 1)][axis]
+    R[i, i] = c; R[j, j] = c; R[i, j] = -s; R[j, i] = s
+    T = np.eye(4, dtype=np.float32)
+    T[:3, :3] = R.astype(np.float32)
+    T[:3, 3] = np.asarray(t, np.float32)
+    return T

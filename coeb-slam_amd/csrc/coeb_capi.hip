@@ -793,6 +793,9 @@ static MatchCam make_cam(const coeb_ctx* c, const coeb_camera* cam)
     m.grid_inv_w = (float)COEB_GRID_COLS / (cam->max_x - cam->min_x);   // Frame.cc:233-234
     m.grid_inv_h = (float)COEB_GRID_ROWS / (cam->max_y - cam->min_y);
     for (int l = 0; l < c->tab.nlevels; l++) m.scale[l] = c->tab.scale[l];
+    m.nlevels = c->tab.nlevels;
+    // mfLogScaleFactor = log(mfScaleFactor): std::log(float), canonical correctly rounded
+    m.log_sf = (float)std::log((double)(float)c->tab.scale_factor);
     return m;
 }
 
@@ -916,6 +919,66 @@ int coeb_match_localmap(coeb_ctx* c, const coeb_camera* cam, const coeb_curframe
     rc = launch_match_local(make_cam(c, cam), b, th, nnratio, s, &c->hook);
     if (rc == -2) return set_err(c, COEB_ERANGE, "coeb_match_localmap: frame and local map exceed the LDS budget");
     if (rc) return hip_err(c, hipGetLastError(), "launch_match_local");
+    int nm = 0;
+    HIP_TRY(c, hipMemcpyAsync(&nm, dnm, 4, hipMemcpyDeviceToHost, s));
+    if (n && match_out) HIP_TRY(c, hipMemcpyAsync(match_out, dmatch, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if ((rc = check_err_word(c))) return rc;
+    *nmatches = nm;
+    return COEB_OK;
+}
+
+int coeb_match_keyframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curframe* cur, const uint8_t* cur_has,
+                        const coeb_keyframe_points* kf, const float Tcw[16], float th, int orb_dist, int check_ori,
+                        int32_t* match_out, int* nmatches)
+{
+    if (!c || !cam || !cur || !kf || !Tcw || !nmatches) return set_err(c, COEB_EINVAL, "coeb_match_keyframe: invalid arguments");
+    *nmatches = 0;
+    if (cur->n < 0 || kf->n < 0) return set_err(c, COEB_EINVAL, "negative frame / keyframe size");
+    if (cur->n > kCurMax) return set_err(c, COEB_EINVAL, "more than 4095 current keypoints");
+    const int n = cur->n, nq = kf->n;
+    if (n && (!cur->keys_un || !cur->descriptors)) return set_err(c, COEB_EINVAL, "coeb_match_keyframe: missing current-frame arrays");
+    if (nq && (!kf->valid || !kf->world_pos || !kf->descriptor || !kf->max_distance || !kf->min_distance || !kf->angle))
+        return set_err(c, COEB_EINVAL, "coeb_match_keyframe: missing keyframe arrays");
+    (void)hipSetDevice(c->device);
+    const int cs = std::max(n, 1), qs = std::max(nq, 1);
+    int rc;
+    coeb_keypoint* dck;
+    uint8_t *dcd, *dhas, *dvalid, *dqd;
+    float *dxw, *dmax, *dmin, *dang, *dT;
+    int32_t *dmatch, *dnm, *derr, *dpath;
+    uint32_t* dlist;
+    if ((rc = ensure(c, "m_ck", cs, &dck)) || (rc = ensure(c, "m_cd", (size_t)cs * 32, &dcd)) ||
+        (rc = ensure(c, "k_has", cs, &dhas)) || (rc = ensure(c, "k_valid", qs, &dvalid)) ||
+        (rc = ensure(c, "k_xw", (size_t)qs * 3, &dxw)) || (rc = ensure(c, "k_qd", (size_t)qs * 32, &dqd)) ||
+        (rc = ensure(c, "k_max", qs, &dmax)) || (rc = ensure(c, "k_min", qs, &dmin)) || (rc = ensure(c, "k_ang", qs, &dang)) ||
+        (rc = ensure(c, "m_T", 32, &dT)) || (rc = ensure(c, "m_match", cs, &dmatch)) || (rc = ensure(c, "m_nm", 1, &dnm)) ||
+        (rc = ensure(c, "l_list", (size_t)qs * match_list_cap(), &dlist)) || (rc = ensure(c, "err", 4, &derr)) ||
+        (rc = ensure(c, "l_path", 2, &dpath)))
+        return rc;
+    hipStream_t s = main_stream(c);
+    if (n) {
+        HIP_TRY(c, hipMemcpyAsync(dck, cur->keys_un, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dcd, cur->descriptors, (size_t)n * 32, hipMemcpyHostToDevice, s));
+        if (cur_has) HIP_TRY(c, hipMemcpyAsync(dhas, cur_has, (size_t)n, hipMemcpyHostToDevice, s));
+        else HIP_TRY(c, hipMemsetAsync(dhas, 0, (size_t)n, s));
+    }
+    if (nq) {
+        HIP_TRY(c, hipMemcpyAsync(dvalid, kf->valid, (size_t)nq, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dxw, kf->world_pos, (size_t)nq * 12, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dqd, kf->descriptor, (size_t)nq * 32, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dmax, kf->max_distance, (size_t)nq * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dmin, kf->min_distance, (size_t)nq * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dang, kf->angle, (size_t)nq * 4, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(c, hipMemcpyAsync(dT, Tcw, 64, hipMemcpyHostToDevice, s));
+    KfBufsHost b;
+    b.cur_kps = dck; b.cur_desc = dcd; b.cur_has = dhas; b.cur_n = n;
+    b.valid = dvalid; b.xw = dxw; b.desc = dqd; b.maxd = dmax; b.mind = dmin; b.angle = dang; b.kf_n = nq; b.Tcw = dT;
+    b.match = dmatch; b.nmatch = dnm; b.lists = dlist; b.err = derr; b.path = dpath;
+    rc = launch_match_kf(make_cam(c, cam), b, th, orb_dist, check_ori ? 1 : 0, s, &c->hook);
+    if (rc == -2) return set_err(c, COEB_ERANGE, "coeb_match_keyframe: frame and keyframe exceed the LDS budget");
+    if (rc) return hip_err(c, hipGetLastError(), "launch_match_kf");
     int nm = 0;
     HIP_TRY(c, hipMemcpyAsync(&nm, dnm, 4, hipMemcpyDeviceToHost, s));
     if (n && match_out) HIP_TRY(c, hipMemcpyAsync(match_out, dmatch, (size_t)n * 4, hipMemcpyDeviceToHost, s));
@@ -1179,7 +1242,8 @@ int coeb_internal_error(coeb_ctx* c, int code, const char* msg) { return set_err
  * what = "pyr" | "blur" | "cand_n" | "lvl_n" | "lvl_kp" | "dyn"; copies min(bytes, size). */
 int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t bytes, size_t* size_out)
 {
-    if (c && what && std::string(what) == "localmap_path") {   // {path, iterations} of the last coeb_match_localmap
+    if (c && what && (std::string(what) == "search_path" || std::string(what) == "localmap_path")) {
+        // {path, iterations} of the last coeb_match_localmap / coeb_match_keyframe
         if (!c->bufs.count("l_path")) return COEB_EINVAL;
         if (size_out) *size_out = 8;
         if (host && bytes) {

@@ -141,6 +141,8 @@ struct MatchCam {
     float min_x, max_x, min_y, max_y;
     float grid_inv_w, grid_inv_h;
     float scale[COEB_MAXL];
+    int nlevels;       // mnScaleLevels
+    float log_sf;      // mfLogScaleFactor = log(mfScaleFactor) (Frame.cc:85), correctly rounded
 };
 struct MatchBufs {
     // current frames
@@ -180,6 +182,18 @@ struct LocalBufsHost {
 int launch_match_local(const MatchCam& cam, const LocalBufsHost& b, float th, float nnratio, hipStream_t s,
                        ProfileHook* prof);
 int match_list_cap();   // candidate-list entries per query (kCQ)
+
+// relocalisation projection search (ORBmatcher::SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist))
+struct KfBufsHost {
+    const void* cur_kps; const uint8_t* cur_desc; const uint8_t* cur_has; int cur_n;
+    const uint8_t* valid; const float* xw; const uint8_t* desc; const float* maxd; const float* mind;
+    const float* angle; int kf_n;
+    const float* Tcw;   // device, 16 floats row-major
+    int* match; int* nmatch; uint32_t* lists; int* err;
+    int* path;          // as LocalBufsHost::path
+};
+int launch_match_kf(const MatchCam& cam, const KfBufsHost& b, float th, int orb_dist, int check_ori, hipStream_t s,
+                    ProfileHook* prof);
 
 // frame preparation for batch matching: u_right/depth per keypoint + LastFrame map snapshot
 struct PrepBufs {

@@ -97,6 +97,7 @@ constexpr int kQL = 8;
 
 struct QueryWin {
     bool ok, chk;
+    bool st = true;            // stereo (uR) check applies
     float u, v, radius, ur_q;
     int minL, maxL, x0, x1, y0, y1;
 };
@@ -156,7 +157,7 @@ struct CurView {
             const float4 k = kp[i];
             x = k.x; y = k.y; ur = k.z; oct = __float_as_int(k.w);
         } else {
-            x = gkp[i].x; y = gkp[i].y; oct = gkp[i].octave; ur = gur[i];
+            x = gkp[i].x; y = gkp[i].y; oct = gkp[i].octave; ur = gur ? gur[i] : -1.f;
         }
     }
     __device__ __forceinline__ int dist(int i, const uint32_t* q) const
@@ -185,7 +186,7 @@ __device__ __forceinline__ void for_candidates(const QueryWin& w, const int* s_c
             }
             const float distx = x - w.u, disty = y - w.v;
             if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) continue;
-            if (ur > 0) {
+            if (w.st && ur > 0) {
                 const float er = fabsf(w.ur_q - ur);
                 if (er > w.radius) continue;
             }
@@ -258,7 +259,7 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
     for (int i = tid; i < n; i += kMThreads) {
         const Kp k = cur[i];
         if (kLds) {
-            L.kp[i] = make_float4(k.x, k.y, cur_ur[i], __int_as_float(k.octave));
+            L.kp[i] = make_float4(k.x, k.y, cur_ur ? cur_ur[i] : -1.f, __int_as_float(k.octave));
             const uint4* d = reinterpret_cast<const uint4*>(cdesc + 32 * i);
             const uint4 d0 = d[0], d1 = d[1];
             uint32_t* o = L.desc + 8 * i;
@@ -329,6 +330,104 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
     }
     __syncthreads();
 
+}
+
+// Phase 2 of the first-minimum matchers (k_match, k_match_kf).  lists + q * stride: query q's
+// candidates (dist << kIdxBits | index) in enumeration order; L.qn[q] = count (-1: none), with
+// 0x10000 set when q's assignment blocks later queries.  res_q = first minimum of q's list over
+// keypoints not claimed by a blocking p < q, solved as a Jacobi fixpoint (iteration k fixes
+// queries 0..k-1, so it reaches the sequential answer).  L.res = the result.  Returns true when
+// kMaxIter rounds did not converge (the caller then runs its literal loop).  Block-uniform.
+__device__ bool claims_first_min(const MatchLds& L, const uint32_t* lists, int stride, int n, int nq, int* s_flag)
+{
+    const int tid = threadIdx.x;
+    for (int it = 0;; it++) {
+        for (int c = tid; c < n; c += kMThreads) L.owner[c] = 0x7fffffff;
+        if (tid == 0) s_flag[1] = 0;
+        __syncthreads();
+        if (it > 0) {
+            for (int q = tid; q < nq; q += kMThreads) {
+                const int r = L.res[q];
+                if (r >= 0 && (L.qn[q] & 0x10000)) atomicMin(&L.owner[r], q);
+            }
+            __syncthreads();
+        }
+        for (int q = tid; q < nq; q += kMThreads) {
+            const int qn = L.qn[q];
+            int best = -1;
+            if (qn >= 0) {
+                const int m = qn & 0xFFFF;
+                const uint32_t* lst = lists + (int64_t)q * stride;
+                uint32_t bk = 0xFFFFFFFFu;
+                for (int e = 0; e < m; e++) {
+                    const uint32_t v = lst[e];
+                    const int i2 = (int)(v & ((1u << kIdxBits) - 1));
+                    if (L.owner[i2] < q) continue;            // claimed by an earlier point
+                    const uint32_t key = ((v >> kIdxBits) << 16) | (uint32_t)e;
+                    if (key < bk) { bk = key; best = i2; }
+                }
+            }
+            if (it == 0 || best != L.res[q]) s_flag[1] = 1;
+            L.res[q] = best;
+        }
+        __syncthreads();
+        if (!s_flag[1]) return false;
+        if (it >= kMaxIter) return true;
+        __syncthreads();
+    }
+}
+
+// Phase 3 of the first-minimum matchers: CurrentFrame.mvpMapPoints[res_q] = q (the last q
+// wins), then the rotation-histogram filter (ORBmatcher.cc:1446-1466 / :1580-1597) over
+// rot = angle(q) - cur[res_q].angle when check_ori.  Leaves L.owner[c] = assigned query or -1
+// and returns nmatches (assignments minus the ones the filter removed).  Block-uniform.
+template <class AngleFn>
+__device__ int assign_rotation(const MatchLds& L, int n, int nq, const Kp* cur, int check_ori, AngleFn qangle,
+                               int* s_hist, int* s_flag)
+{
+    const int tid = threadIdx.x;
+    for (int c = tid; c < n; c += kMThreads) L.owner[c] = -1;
+    if (tid < HISTO_LENGTH) s_hist[tid] = 0;
+    if (tid == 0) { s_flag[2] = 0; s_flag[3] = 0; }
+    __syncthreads();
+    int mine = 0;
+    for (int q = tid; q < nq; q += kMThreads) {
+        const int r = L.res[q];
+        if (r >= 0) {
+            atomicMax(&L.owner[r], q);
+            mine++;
+            if (check_ori) {
+                const int bin = rot_bin(qangle(q), cur[r].angle);
+                L.qn[q] = bin;
+                atomicAdd(&s_hist[bin], 1);
+            }
+        }
+    }
+    if (mine) atomicAdd(&s_flag[2], mine);
+    __syncthreads();
+    if (check_ori) {
+        if (tid == 0) {
+            int i1, i2, i3;
+            three_maxima(s_hist, i1, i2, i3);
+            s_flag[4] = i1; s_flag[5] = i2; s_flag[6] = i3;
+        }
+        __syncthreads();
+        const int i1 = s_flag[4], i2 = s_flag[5], i3 = s_flag[6];
+        int rem = 0;
+        for (int q = tid; q < nq; q += kMThreads) {
+            const int r = L.res[q];
+            if (r >= 0) {
+                const int bin = L.qn[q];
+                if (bin != i1 && bin != i2 && bin != i3) {
+                    L.owner[r] = -1;
+                    rem++;
+                }
+            }
+        }
+        if (rem) atomicAdd(&s_flag[3], rem);
+        __syncthreads();
+    }
+    return s_flag[2] - s_flag[3];
 }
 
 template <bool kLds>
@@ -455,42 +554,7 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
         __syncthreads();
         bool seq = force_seq || s_flag[0];
         // ---- phase 2: claims by fixpoint iteration ----
-        if (!seq) {
-            for (int it = 0;; it++) {
-                for (int c = tid; c < n; c += kMThreads) L.owner[c] = 0x7fffffff;
-                if (tid == 0) s_flag[1] = 0;
-                __syncthreads();
-                if (it > 0) {
-                    for (int q = tid; q < nl; q += kMThreads) {
-                        const int r = L.res[q];
-                        if (r >= 0 && (L.qn[q] & 0x10000)) atomicMin(&L.owner[r], q);
-                    }
-                    __syncthreads();
-                }
-                for (int q = tid; q < nl; q += kMThreads) {
-                    const int qn = L.qn[q];
-                    int best = -1;
-                    if (qn >= 0) {
-                        const int m = qn & 0xFFFF;
-                        const uint32_t* lst = lists + (int64_t)q * kCQ;
-                        uint32_t bk = 0xFFFFFFFFu;
-                        for (int e = 0; e < m; e++) {
-                            const uint32_t v = lst[e];
-                            const int i2 = (int)(v & ((1u << kIdxBits) - 1));
-                            if (L.owner[i2] < q) continue;            // claimed by an earlier point
-                            const uint32_t key = ((v >> kIdxBits) << 16) | (uint32_t)e;
-                            if (key < bk) { bk = key; best = i2; }
-                        }
-                    }
-                    if (it == 0 || best != L.res[q]) s_flag[1] = 1;
-                    L.res[q] = best;
-                }
-                __syncthreads();
-                if (!s_flag[1]) break;
-                if (it >= kMaxIter) { seq = true; break; }
-                __syncthreads();
-            }
-        }
+        if (!seq) seq = claims_first_min(L, lists, kCQ, n, nl, s_flag);
         // ---- sequential path (overflow / no convergence / forced): literal loop, one thread ----
         if (seq) {
             for (int c = tid; c < n; c += kMThreads) L.owner[c] = -1;
@@ -521,47 +585,7 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
             __syncthreads();
         }
         // ---- phase 3: mvpMapPoints, rotation consistency ----
-        for (int c = tid; c < n; c += kMThreads) L.owner[c] = -1;
-        if (tid < HISTO_LENGTH) s_hist[tid] = 0;
-        __syncthreads();
-        int mine = 0;
-        for (int q = tid; q < nl; q += kMThreads) {
-            const int r = L.res[q];
-            if (r >= 0) {
-                atomicMax(&L.owner[r], q);
-                mine++;
-                if (check_ori) {
-                    const int bin = rot_bin(last[q].angle, cur[r].angle);
-                    L.qn[q] = bin;
-                    atomicAdd(&s_hist[bin], 1);
-                }
-            }
-        }
-        if (mine) atomicAdd(&s_flag[2], mine);
-        __syncthreads();
-        if (check_ori) {
-            if (tid == 0) {
-                int i1, i2, i3;
-                three_maxima(s_hist, i1, i2, i3);
-                s_flag[4] = i1; s_flag[5] = i2; s_flag[6] = i3;
-            }
-            __syncthreads();
-            const int i1 = s_flag[4], i2 = s_flag[5], i3 = s_flag[6];
-            int rem = 0;
-            for (int q = tid; q < nl; q += kMThreads) {
-                const int r = L.res[q];
-                if (r >= 0) {
-                    const int bin = L.qn[q];
-                    if (bin != i1 && bin != i2 && bin != i3) {
-                        L.owner[r] = -1;
-                        rem++;
-                    }
-                }
-            }
-            if (rem) atomicAdd(&s_flag[3], rem);
-            __syncthreads();
-        }
-        nmatches = s_flag[2] - s_flag[3];
+        nmatches = assign_rotation(L, n, nl, cur, check_ori, [&](int q) { return last[q].angle; }, s_hist, s_flag);
         __syncthreads();
         if (nmatches >= retry_below) break;
         th = 2 * th0;                                  // Tracking.cc:954-958
@@ -798,6 +822,200 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
     if (tid == 0) { *b.nmatch = s_flag[2]; b.path[0] = 0; b.path[1] = iters; }
 }
 
+
+// ================================ k_match_kf ================================
+// ORBmatcher::SearchByProjection(Frame &CurrentFrame, KeyFrame *pKF, const set<MapPoint*>
+// &sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:1473-1600), the relocalisation search
+// (calls Tracking.cc:1531, 1545), for one frame, one 1024-thread workgroup.  Per KeyFrame map
+// point: project with CurrentFrame.mTcw (no depth-sign test in the reference), bounds, the
+// distance-invariance range, MapPoint::PredictScale, window th * scale[level] over levels
+// [level-1, level+1], no stereo check.  A keypoint holding any MapPoint (at entry or given
+// earlier in this call) is skipped (:1545-1546), so every assignment blocks later points: the
+// same fixpoint as k_match with every query blocking.  Then the rotation histogram.
+struct KfBufs {
+    const void* cur_kps; const uint8_t* cur_desc; const uint8_t* cur_has; int cur_n;
+    const uint8_t* valid; const float* xw; const uint8_t* desc; const float* maxd; const float* mind;
+    const float* angle; int kf_n;
+    const float* Tcw;
+    int* match; int* nmatch; uint32_t* lists; int* err; int* path;
+};
+
+// MapPoint::PredictScale(dist, Frame*) (MapPoint.cc:402-417); log canonical as in the oracle
+__device__ __forceinline__ int predict_scale(const MatchCam& cam, float max_dist, float dist)
+{
+    const float ratio = max_dist / dist;
+    int s = (int)ceilf((float)log((double)ratio) / cam.log_sf);
+    if (s < 0) s = 0;
+    else if (s >= cam.nlevels) s = cam.nlevels - 1;
+    return s;
+}
+
+__device__ __forceinline__ QueryWin kf_window(const MatchCam& cam, const float* T, const float* Ow, const KfBufs& b,
+                                              int q, float th)
+{
+    QueryWin w;
+    w.ok = false;
+    w.st = false;
+    w.ur_q = 0.f;
+    if (!b.valid[q]) return w;
+    const float* X = b.xw + 3 * q;
+    float p3[3];
+    for (int k = 0; k < 3; k++) {                  // x3Dc = Rcw*x3Dw + tcw (as query_window)
+        float t = T[k * 4 + 0] * X[0] + T[k * 4 + 1] * X[1];
+        t = t + T[k * 4 + 2] * X[2];
+        p3[k] = (float)((double)t + (double)T[k * 4 + 3]);
+    }
+    const float invzc = (float)(1.0 / (double)p3[2]);
+    w.u = __builtin_fmaf(cam.fx * p3[0], invzc, cam.cx);
+    w.v = __builtin_fmaf(cam.fy * p3[1], invzc, cam.cy);
+    if (w.u < cam.min_x || w.u > cam.max_x) return w;
+    if (w.v < cam.min_y || w.v > cam.max_y) return w;
+    // dist3D = cv::norm(x3Dw - Ow): float differences, squares summed in double (normL2_32f)
+    const float d0 = X[0] - Ow[0], d1 = X[1] - Ow[1], d2 = X[2] - Ow[2];
+    double ss = 0.0;
+    ss += (double)d0 * (double)d0;
+    ss += (double)d1 * (double)d1;
+    ss += (double)d2 * (double)d2;
+    const float dist3D = (float)sqrt(ss);
+    const float maxd = b.maxd[q], mind = b.mind[q];
+    if (dist3D < 0.8f * mind || dist3D > 1.2f * maxd) return w;   // Get{Min,Max}DistanceInvariance
+    const int lvl = predict_scale(cam, maxd, dist3D);
+    w.radius = th * cam.scale[lvl];
+    w.minL = lvl - 1;
+    w.maxL = lvl + 1;
+    w.ok = window_cells(cam, w);
+    return w;
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kMThreads) void k_match_kf(MatchCam cam, KfBufs b, float th, int orb_dist, int check_ori,
+                                                        int force_seq)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int s_hist[HISTO_LENGTH];
+    __shared__ int s_flag[8];
+    const int tid = threadIdx.x;
+    const int n = b.cur_n, nq = b.kf_n;
+    size_t off[7];
+    match_lds_bytes(n, nq, kLds, off);
+    MatchLds L;
+    L.cell = reinterpret_cast<int*>(smem + off[0]);
+    L.sort = reinterpret_cast<uint32_t*>(smem + off[1]);
+    L.owner = reinterpret_cast<int*>(smem + off[2]);
+    L.res = reinterpret_cast<int*>(smem + off[3]);
+    L.qn = reinterpret_cast<int*>(smem + off[4]);
+    L.kp = reinterpret_cast<float4*>(smem + off[5]);
+    L.desc = reinterpret_cast<uint32_t*>(smem + off[6]);
+    const Kp* cur = reinterpret_cast<const Kp*>(b.cur_kps);
+    if (n >= (1 << kIdxBits)) {
+        if (tid == 0) { atomicOr(b.err, 16); *b.nmatch = 0; }
+        return;
+    }
+    // no uR is read here: the CSR staging takes the keypoint records only
+    CurView<kLds> cv;
+    cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = nullptr; cv.gdesc = b.cur_desc;
+    stage_grid<kLds>(cam, cur, nullptr, b.cur_desc, n, L);
+    const float* T = b.Tcw;
+    float Ow[3];
+    for (int k = 0; k < 3; k++) {                 // Ow = -Rcw^T tcw (double accumulation)
+        double s = (double)T[0 * 4 + k] * T[3] + (double)T[1 * 4 + k] * T[7];
+        s = s + (double)T[2 * 4 + k] * T[11];
+        Ow[k] = (float)(s * -1.0);
+    }
+    if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; }
+    __syncthreads();
+    // ---- phase 1: candidate lists (window, levels, entry holders, dist <= ORBdist) ----
+    {
+        const int grp = tid / kQL, gl = tid % kQL, gsh = (tid & 63) & ~(kQL - 1);
+        for (int q0 = 0; q0 < nq; q0 += kMThreads / kQL) {
+            const int q = q0 + grp;
+            int cnt = -1;
+            QueryWin w;
+            w.ok = false;
+            if (q < nq) w = kf_window(cam, T, Ow, b, q, th);
+            if (w.ok) {
+                uint32_t qd[8];
+                const uint4* d = reinterpret_cast<const uint4*>(b.desc + 32 * q);
+                const uint4 d0 = d[0], d1 = d[1];
+                qd[0] = d0.x; qd[1] = d0.y; qd[2] = d0.z; qd[3] = d0.w;
+                qd[4] = d1.x; qd[5] = d1.y; qd[6] = d1.z; qd[7] = d1.w;
+                cnt = 0;
+                uint32_t* lst = b.lists + (int64_t)q * kCQ;
+                for (int ix = w.x0; ix <= w.x1; ix++) {
+                    const int c0 = L.cell[ix * COEB_GRID_ROWS + w.y0];
+                    const int c1 = L.cell[ix * COEB_GRID_ROWS + w.y1 + 1];
+                    for (int base = c0; base < c1; base += kQL) {
+                        const int e = base + gl;
+                        bool ok = false;
+                        uint32_t ent = 0;
+                        if (e < c1) {
+                            const int i2 = (int)(L.sort[e] & ((1u << kIdxBits) - 1));
+                            float x, y, ur;
+                            int oct;
+                            cv.get(i2, x, y, ur, oct);
+                            ok = !(oct < w.minL || oct > w.maxL);            // chk always set (maxL >= 0)
+                            const float distx = x - w.u, disty = y - w.v;
+                            if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) ok = false;
+                            if (b.cur_has[i2]) ok = false;                     // :1545-1546, entry holder
+                            if (ok) {
+                                const int dist = cv.dist(i2, qd);
+                                ok = dist <= orb_dist;
+                                ent = ((uint32_t)dist << kIdxBits) | (uint32_t)i2;
+                            }
+                        }
+                        const uint32_t gb = (uint32_t)(__ballot(ok) >> gsh) & ((1u << kQL) - 1u);
+                        if (ok) {
+                            const int pos = cnt + __popc(gb & ((1u << gl) - 1u));
+                            if (pos < kCQ) lst[pos] = ent;
+                        }
+                        cnt += __popc(gb);
+                    }
+                }
+                if (cnt > kCQ) s_flag[0] = 1;
+            }
+            if (q < nq && gl == 0) L.qn[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | 0x10000);
+        }
+    }
+    __syncthreads();
+    const bool overflow = s_flag[0] != 0;
+    bool seq = force_seq || overflow;
+    if (!seq) seq = claims_first_min(L, b.lists, kCQ, n, nq, s_flag);
+    if (seq) {
+        // literal loop (ORBmatcher.cc:1489-1578), one thread; L.owner[c] >= 0: c holds a MapPoint
+        const int path = force_seq ? 1 : overflow ? 2 : 3;
+        for (int c = tid; c < n; c += kMThreads) L.owner[c] = b.cur_has[c] ? nq : -1;
+        __syncthreads();
+        if (tid == 0) {
+            b.path[0] = path;
+            for (int q = 0; q < nq; q++) {
+                int best = -1;
+                const QueryWin w = kf_window(cam, T, Ow, b, q, th);
+                if (w.ok) {
+                    uint32_t qd[8];
+                    for (int k = 0; k < 8; k++) qd[k] = reinterpret_cast<const uint32_t*>(b.desc + 32 * q)[k];
+                    int bestDist = 256;
+                    for_candidates<kLds>(w, L.cell, L.sort, cv, [&](int i2) {
+                        if (L.owner[i2] >= 0) return true;
+                        const int dist = cv.dist(i2, qd);
+                        if (dist < bestDist) { bestDist = dist; best = i2; }
+                        return true;
+                    });
+                    if (bestDist > orb_dist) best = -1;
+                    if (best >= 0) L.owner[best] = q;
+                }
+                L.res[q] = best;
+            }
+        }
+        __syncthreads();
+    } else if (tid == 0) {
+        b.path[0] = 0;
+    }
+    // ---- phase 3: assignments (unique here), rotation consistency ----
+    const int nm = assign_rotation(L, n, nq, cur, check_ori, [&](int q) { return b.angle[q]; }, s_hist, s_flag);
+    for (int c = tid; c < n; c += kMThreads) b.match[c] = L.owner[c];
+    if (tid == 0) *b.nmatch = nm;
+}
+
 }  // namespace
 
 int launch_prep(const PrepBufs& b, int F, hipStream_t s, ProfileHook* prof)
@@ -859,3 +1077,32 @@ int launch_match_local(const MatchCam& cam, const LocalBufsHost& h, float th, fl
 }
 
 int match_list_cap() { return kCQ; }
+
+int launch_match_kf(const MatchCam& cam, const KfBufsHost& h, float th, int orb_dist, int check_ori, hipStream_t s,
+                    ProfileHook* prof)
+{
+    KfBufs b;
+    b.cur_kps = h.cur_kps; b.cur_desc = h.cur_desc; b.cur_has = h.cur_has; b.cur_n = h.cur_n;
+    b.valid = h.valid; b.xw = h.xw; b.desc = h.desc; b.maxd = h.maxd; b.mind = h.mind; b.angle = h.angle;
+    b.kf_n = h.kf_n; b.Tcw = h.Tcw; b.match = h.match; b.nmatch = h.nmatch; b.lists = h.lists; b.err = h.err;
+    b.path = h.path;
+    const int force_seq = getenv("COEB_MATCH_SEQUENTIAL") ? 1 : 0;
+    const int cs = std::max(h.cur_n, 1), qs = std::max(h.kf_n, 1);
+    const size_t lds_full = match_lds_bytes(cs, qs, true, nullptr) + 256;
+    const size_t lds_min = match_lds_bytes(cs, qs, false, nullptr) + 256;
+    prof_begin(prof, "k_match_kf", s);
+    if (lds_full <= 160 * 1024) {
+        (void)hipFuncSetAttribute((const void*)k_match_kf<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_full);
+        hipLaunchKernelGGL(k_match_kf<true>, dim3(1), dim3(kMThreads), lds_full - 256, s, cam, b, th, orb_dist, check_ori,
+                           force_seq);
+    } else if (lds_min <= 160 * 1024) {
+        (void)hipFuncSetAttribute((const void*)k_match_kf<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_min);
+        hipLaunchKernelGGL(k_match_kf<false>, dim3(1), dim3(kMThreads), lds_min - 256, s, cam, b, th, orb_dist, check_ori,
+                           force_seq);
+    } else {
+        prof_end(prof, s);
+        return -2;
+    }
+    prof_end(prof, s);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -25,6 +25,11 @@
  *                                      const float th)  include/ORBmatcher.h:46,
  *                                      src/ORBmatcher.cc:44-129 (RadiusByViewingCos :131-137),
  *                                      the call in Tracking::SearchLocalPoints  src/Tracking.cc:1222-1271
+ *   coeb_match_keyframe             <- ORBmatcher::SearchByProjection(Frame&, KeyFrame*,
+ *                                      const set<MapPoint*>&, const float th, const int ORBdist)
+ *                                      include/ORBmatcher.h:55, src/ORBmatcher.cc:1473-1600
+ *                                      (MapPoint::PredictScale  src/MapPoint.cc:402-417), the
+ *                                      calls in Tracking::Relocalization  src/Tracking.cc:1531,1545
  *   coeb_descriptor_distance        <- ORBmatcher::DescriptorDistance  src/ORBmatcher.cc:1648-1664
  *
  * Conventions: 0 on success, negative COEB_E* code on failure (the reference has no error
@@ -199,6 +204,29 @@ int coeb_match_localmap(coeb_ctx* ctx, const coeb_camera* cam, const coeb_curfra
                         const int32_t* cur_observations, const coeb_localmap* mp, float th,
                         float nnratio, int32_t* match_out, int* nmatches);
 
+/* Map points of a KeyFrame as ORBmatcher.cc:1487-1530 reads them (pKF->GetMapPointMatches()). */
+typedef struct {
+    int32_t n;                        /* vpMPs.size() */
+    const uint8_t* valid;             /* pMP && !pMP->isBad() && !sAlreadyFound.count(pMP) */
+    const float* world_pos;           /* n x 3, GetWorldPos() */
+    const uint8_t* descriptor;        /* n x 32, GetDescriptor() */
+    const float* max_distance;        /* mfMaxDistance (GetMaxDistanceInvariance() = 1.2f * it) */
+    const float* min_distance;        /* mfMinDistance (GetMinDistanceInvariance() = 0.8f * it) */
+    const float* angle;               /* pKF->mvKeysUn[i].angle */
+} coeb_keyframe_points;
+
+/* ---- ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) ----
+ * cur_has_mappoint[i] (length cur->n, may be NULL = all NULL): CurrentFrame.mvpMapPoints[i] !=
+ * NULL on entry; such keypoints are skipped, as are keypoints given earlier in the call.
+ * Tcw: CurrentFrame.mTcw (row-major 4x4).  The scale pyramid is the context's (mnScaleLevels,
+ * mvScaleFactors, mfLogScaleFactor).  match_out[i] = index of the KeyFrame point assigned to
+ * keypoint i, or -1; *nmatches = the return value (after the rotation filter when
+ * check_orientation = mbCheckOrientation).  cur->u_right is not read (may be NULL). */
+int coeb_match_keyframe(coeb_ctx* ctx, const coeb_camera* cam, const coeb_curframe* cur,
+                        const uint8_t* cur_has_mappoint, const coeb_keyframe_points* kf,
+                        const float Tcw[16], float th, int orb_dist, int check_orientation,
+                        int32_t* match_out, int* nmatches);
+
 /* ---- Frame helpers ---- */
 int coeb_blur_flags(coeb_ctx* ctx, const uint8_t* gray, int width, int height, size_t stride,
                     const coeb_box* boxes, int nbox, int32_t* flags_out);
@@ -234,9 +262,9 @@ int coeb_device_count(void);
 /* Test support: copy an intermediate buffer of frame `frame` of the last batch to the host.
  * what: "pyr" (levels 1..L-1, packed), "blur" (levels 0..L-1), "cand_n" (FAST corners per
  * cell), "lvl_n" (keypoints per level), "lvl_kp" (packed level keypoints), "dyn" (mask
- * rectangles), "plan", "localmap_path" (int32 {path, iterations} of the last
- * coeb_match_localmap: 0 parallel claims, 1 forced sequential, 2 candidate-list overflow, 3 no
- * convergence; frame ignored).  Copies min(bytes, size); *size_out = full size. */
+ * rectangles), "plan", "search_path" (int32 {path, iterations} of the last
+ * coeb_match_localmap / coeb_match_keyframe: 0 parallel claims, 1 forced sequential,
+ * 2 candidate-list overflow, 3 no convergence; frame ignored; alias "localmap_path").  Copies min(bytes, size); *size_out = full size. */
 int coeb_debug_read(coeb_ctx* ctx, const char* what, int frame, void* host, size_t bytes, size_t* size_out);
 
 #ifdef __cplusplus

@@ -56,6 +56,15 @@ class LocalMap(C.Structure):
                 ("nobs", C.c_void_p)]
 
 
+class KfPoints(C.Structure):
+    _fields_ = [("n", C.c_int), ("valid", C.c_void_p), ("xw", C.c_void_p), ("desc", C.c_void_p),
+                ("max_dist", C.c_void_p), ("min_dist", C.c_void_p), ("angle", C.c_void_p)]
+
+
+KFPOINT_FIELDS = (("valid", np.uint8), ("world_pos", np.float32), ("descriptor", np.uint8),
+                  ("max_distance", np.float32), ("min_distance", np.float32), ("angle", np.float32))
+
+
 class Grid(C.Structure):
     _fields_ = [("cell_start", C.c_void_p), ("cell_idx", C.c_void_p)]
 
@@ -189,6 +198,25 @@ def search_local_map(cam, cur_kps, cur_desc, cur_ur, cur_obs, mp, th=3.0, nnrati
     nm = lib().oc_search_local_map(C.byref(cam), C.byref(cf), ptr(cur_obs), C.byref(lm), C.c_float(th),
                                    C.c_float(nnratio), ptr(out))
     return nm, out[: len(cur_kps)]
+
+
+def search_keyframe(cam, cur_kps, cur_desc, cur_has, kf, Tcw, th=10.0, orb_dist=100, check_ori=True):
+    """ORBmatcher::SearchByProjection(Frame&, KeyFrame*, set<MapPoint*>, th, ORBdist)
+    (ORBmatcher.cc:1473-1560).  cur_has: u8[n], CurrentFrame.mvpMapPoints[i] != NULL at entry.
+    kf: dict of KFPOINT_FIELDS arrays.  Returns (nmatches, match[n]: KeyFrame point index or -1)."""
+    cur_kps = np.ascontiguousarray(cur_kps)
+    cur_desc = np.ascontiguousarray(cur_desc, np.uint8)
+    n = len(cur_kps)
+    cur_has = np.zeros(n, np.uint8) if cur_has is None else np.ascontiguousarray(cur_has, np.uint8)
+    dummy_ur = np.full(max(n, 1), -1, np.float32)
+    cf = CurFrame(n, cur_kps.ctypes.data, cur_desc.ctypes.data, dummy_ur.ctypes.data)
+    arrs = {k: np.ascontiguousarray(kf[k], dt) for k, dt in KFPOINT_FIELDS}
+    kp = KfPoints(len(arrs["valid"]), *[arrs[k].ctypes.data for k, _ in KFPOINT_FIELDS])
+    T = np.ascontiguousarray(Tcw, np.float32)
+    out = np.zeros(max(n, 1), np.int32)
+    nm = lib().oc_search_keyframe(C.byref(cam), C.byref(cf), ptr(cur_has), C.byref(kp), ptr(T), C.c_float(th),
+                                  int(orb_dist), int(bool(check_ori)), ptr(out))
+    return nm, out[:n]
 
 
 def blur_flags(gray, boxes):

@@ -1218,3 +1218,114 @@ int oc_search_local_map(const oc_camera* cam, const oc_curframe* cur, const int3
     free(g.cell_idx);
     return nmatches;
 }
+
+/* MapPoint::PredictScale(currentDist, Frame*) (MapPoint.cc:402-417): ratio = mfMaxDistance /
+ * currentDist; nScale = ceil(log(ratio) / mfLogScaleFactor), clamped to the pyramid.  log is
+ * std::log(float); canonical: correctly rounded, as (float)log((double)x). */
+static float canon_logf(float x) { return (float)log((double)x); }
+
+static int predict_scale(float max_dist, float dist, float log_sf, int nlevels)
+{
+    const float ratio = max_dist / dist;
+    int s = (int)ceilf(canon_logf(ratio) / log_sf);
+    if (s < 0) s = 0;
+    else if (s >= nlevels) s = nlevels - 1;
+    return s;
+}
+
+int oc_search_keyframe(const oc_camera* cam, const oc_curframe* cur, const uint8_t* cur_has,
+                       const oc_kfpoints* kf, const float Tcw[16], float th, int orb_dist, int check_ori,
+                       int32_t* match_out)
+{
+    enum { HISTO_LENGTH = 30 };
+    int nmatches = 0;
+    const float factor = 1.0f / HISTO_LENGTH;
+    const float* T = Tcw;
+    const float log_sf = cam->nlevels > 1 ? canon_logf(cam->scale[1]) : 1.0f;   /* Frame.cc:85 */
+    /* Ow = -Rcw.t()*tcw (GEMM_1_T, double accumulation) */
+    float Ow[3];
+    for (int k = 0; k < 3; k++) {
+        double s = (double)T[0 * 4 + k] * T[3] + (double)T[1 * 4 + k] * T[7];
+        s = s + (double)T[2 * 4 + k] * T[11];
+        Ow[k] = (float)(s * -1.0);
+    }
+    oc_grid g;
+    g.cell_start = (int*)malloc(sizeof(int) * (OC_GRID_COLS * OC_GRID_ROWS + 1));
+    g.cell_idx = (int*)malloc(sizeof(int) * (cur->n > 0 ? cur->n : 1));
+    oc_assign_grid(cam, cur->keys_un, cur->n, &g);
+    /* taken[i2]: CurrentFrame.mvpMapPoints[i2] != NULL (entry holders and this call's) */
+    uint8_t* taken = (uint8_t*)malloc(cur->n > 0 ? cur->n : 1);
+    for (int i = 0; i < cur->n; i++) { taken[i] = cur_has ? cur_has[i] != 0 : 0; match_out[i] = -1; }
+    int* hist_items = (int*)malloc(sizeof(int) * (kf->n > 0 ? kf->n : 1) * 2);
+    int* hist_bin = hist_items + (kf->n > 0 ? kf->n : 1);
+    int nhist = 0;
+    int* cand = (int*)malloc(sizeof(int) * (cur->n > 0 ? cur->n : 1));
+    for (int i = 0; i < kf->n; i++) {
+        if (!kf->valid[i]) continue;                                    /* :1493-1495 */
+        const float* X = &kf->xw[3 * i];
+        float p3[3];
+        for (int k = 0; k < 3; k++) {                                   /* x3Dc = Rcw*x3Dw+tcw */
+            float t = T[k * 4 + 0] * X[0] + T[k * 4 + 1] * X[1];
+            t = t + T[k * 4 + 2] * X[2];
+            p3[k] = (float)((double)t + (double)T[k * 4 + 3]);
+        }
+        const float invzc = (float)(1.0 / (double)p3[2]);
+        const float u = fmaf(cam->fx * p3[0], invzc, cam->cx);
+        const float v = fmaf(cam->fy * p3[1], invzc, cam->cy);
+        if (u < cam->min_x || u > cam->max_x) continue;                 /* :1509-1512 */
+        if (v < cam->min_y || v > cam->max_y) continue;
+        /* dist3D = cv::norm(x3Dw - Ow): float differences, squares summed in double */
+        const float d0 = X[0] - Ow[0], d1 = X[1] - Ow[1], d2 = X[2] - Ow[2];
+        double ss = 0.0;
+        ss += (double)d0 * (double)d0;
+        ss += (double)d1 * (double)d1;
+        ss += (double)d2 * (double)d2;
+        const float dist3D = (float)sqrt(ss);
+        const float maxDistance = 1.2f * kf->max_dist[i];                /* MapPoint.cc:373-383 */
+        const float minDistance = 0.8f * kf->min_dist[i];
+        if (dist3D < minDistance || dist3D > maxDistance) continue;     /* :1522-1523 */
+        const int lvl = predict_scale(kf->max_dist[i], dist3D, log_sf, cam->nlevels);
+        const float radius = th * cam->scale[lvl];
+        const int nc = oc_features_in_area(cam, cur->keys_un, &g, u, v, radius, lvl - 1, lvl + 1, cand, cur->n);
+        if (nc == 0) continue;
+        const uint8_t* dMP = &kf->desc[32 * i];
+        int bestDist = 256, bestIdx2 = -1;
+        for (int c = 0; c < nc; c++) {
+            const int i2 = cand[c];
+            if (taken[i2]) continue;                                    /* :1545-1546 */
+            const int dist = oc_descriptor_distance(dMP, &cur->desc[32 * i2]);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = i2; }
+        }
+        if (bestDist <= orb_dist) {                                     /* :1556-1574 */
+            taken[bestIdx2] = 1;
+            match_out[bestIdx2] = i;
+            nmatches++;
+            if (check_ori) {
+                float rot = kf->angle[i] - cur->keys_un[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == HISTO_LENGTH) bin = 0;
+                hist_items[nhist] = bestIdx2;
+                hist_bin[nhist] = bin;
+                nhist++;
+            }
+        }
+    }
+    if (check_ori) {                                                    /* :1580-1597 */
+        int hist[HISTO_LENGTH] = {0};
+        for (int k = 0; k < nhist; k++) hist[hist_bin[k]]++;
+        int i1, i2, i3;
+        three_maxima(hist, HISTO_LENGTH, &i1, &i2, &i3);
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b == i1 || b == i2 || b == i3) continue;
+            for (int k = 0; k < nhist; k++)
+                if (hist_bin[k] == b) { match_out[hist_items[k]] = -1; nmatches--; }
+        }
+    }
+    free(cand);
+    free(hist_items);
+    free(taken);
+    free(g.cell_start);
+    free(g.cell_idx);
+    return nmatches;
+}

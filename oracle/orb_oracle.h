@@ -165,6 +165,26 @@ typedef struct {
 int oc_search_local_map(const oc_camera* cam, const oc_curframe* cur, const int32_t* cur_obs,
                         const oc_localmap* mp, float th, float nnratio, int32_t* match_out);
 
+/* Map points of a KeyFrame for the relocalisation search: pKF->GetMapPointMatches() snapshot
+ * (ORBmatcher.cc:1487-1530 reads exactly these). */
+typedef struct {
+    int n;
+    const uint8_t* valid;          /* pMP && !pMP->isBad() && !sAlreadyFound.count(pMP) */
+    const float* xw;               /* n x 3 GetWorldPos() */
+    const uint8_t* desc;           /* n x 32 GetDescriptor() */
+    const float* max_dist;         /* mfMaxDistance */
+    const float* min_dist;         /* mfMinDistance */
+    const float* angle;            /* pKF->mvKeysUn[i].angle */
+} oc_kfpoints;
+
+/* ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
+ * (ORBmatcher.cc:1473-1560) with MapPoint::PredictScale (MapPoint.cc:402-417).
+ * cur_has[i2] = CurrentFrame.mvpMapPoints[i2] != NULL at entry.  match_out[i2] = index of the
+ * KeyFrame point assigned to keypoint i2 by this call, or -1. */
+int oc_search_keyframe(const oc_camera* cam, const oc_curframe* cur, const uint8_t* cur_has,
+                       const oc_kfpoints* kf, const float Tcw[16], float th, int orb_dist, int check_ori,
+                       int32_t* match_out);
+
 #ifdef __cplusplus
 }
 #endif

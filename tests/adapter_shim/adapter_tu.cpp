@@ -12,6 +12,12 @@ struct MapPoint {
     float mTrackProjX = 0, mTrackProjY = 0, mTrackProjXR = 0;
     int mnTrackScaleLevel = 0;
     float mTrackViewCos = 0;
+    float GetMaxDistance() { return 0; }   // the two getters INTEGRATION.md s3 adds
+    float GetMinDistance() { return 0; }
+};
+struct KeyFrame {
+    std::vector<MapPoint*> GetMapPointMatches() { return {}; }
+    std::vector<cv::KeyPoint> mvKeysUn;
 };
 struct Frame {
     static float fx, fy, cx, cy, mnMinX, mnMaxX, mnMinY, mnMaxY;
@@ -38,5 +44,6 @@ int use_adapters(Frame& cur, const Frame& last, cv::Mat& im)
     ex(im, cv::Mat(), im, im, kps, desc, box, tm, mask_result, blur);
     std::vector<MapPoint*> local;
     return coeb::SearchByProjectionLastFrame(cur, last, 15.0f, false, 0.9f, true) + ex.GetLevels() +
-           coeb::SearchByProjectionLocalMap(cur, local, 3.0f, 0.8f);
+           coeb::SearchByProjectionLocalMap(cur, local, 3.0f, 0.8f) +
+           coeb::SearchByProjectionKeyFrame(cur, (KeyFrame*)nullptr, std::set<MapPoint*>(), 10.0f, 100, true);
 }

@@ -476,3 +476,85 @@ def test_localmap_crowded_windows(ctx, oracle_mod, ex):
         localmap_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], ur1, None, mp, th)
         paths.append(localmap_path(ctx)[0])
     assert paths == [0, 2], paths
+
+
+# ------------------------------------------------------------------ relocalisation projection search
+def keyframe_both(ctx, oracle_mod, ex, cur_k, cur_d, cur_has, kf, Tcw, th=10.0, orb_dist=100, check_ori=True,
+                  already=()):
+    """coeb_match_keyframe vs oracle.search_keyframe (ORBmatcher.cc:1473-1600), bit-exact."""
+    import coeb_front
+    cam_o = oracle_mod.camera(ex, 640, 480, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    kv = dict(kf)
+    kv["valid"] = kf["valid"].copy()
+    for i in already:
+        kv["valid"][i] = 0
+    has = np.zeros(len(cur_k), np.uint8) if cur_has is None else cur_has
+    nm_ref, m_ref = oracle_mod.search_keyframe(cam_o, cur_k, cur_d, has, kv, Tcw, th, orb_dist, check_ori)
+    cam = coeb_front.make_camera(synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF, 640, 480)
+    F = coeb_front.Frame(cur_k, cur_d, Tcw=Tcw)
+    if cur_has is not None:
+        F.mvpMapPoints = np.where(cur_has > 0, 10 ** 6, -1).astype(np.int32)    # a MapPoint from elsewhere
+    kp = coeb_front.KeyFramePoints(kf["valid"], kf["world_pos"], kf["descriptor"], kf["max_distance"],
+                                   kf["min_distance"], kf["angle"])
+    nm = coeb_front.ORBmatcher(0.75, check_ori, ctx=ctx).SearchByProjection(F, kp, set(already), th, orb_dist, cam)
+    got = np.where(F.mvpMapPoints == 10 ** 6, -1, F.mvpMapPoints)
+    assert nm == nm_ref, (nm, nm_ref)
+    assert np.array_equal(got, m_ref), int(np.sum(got != m_ref))
+    return nm
+
+
+def search_path(ctx):
+    p = ctx.debug_read("search_path").view(np.int32)
+    return int(p[0]), int(p[1])
+
+
+@pytest.mark.parametrize("seed,th,orb_dist", [(0, 10.0, 100), (1, 3.0, 64), (2, 10.0, 50), (3, 25.0, 100)])
+def test_keyframe_matches_oracle(ctx, oracle_mod, ex, pair, seed, th, orb_dist):
+    r1, ur1, last = pair
+    kf = synth.make_keyframe_points(last["xw"], last["mp_desc"], last["keys_un"]["octave"], last["keys_un"]["angle"],
+                                    seed=seed)
+    kf["valid"] &= last_has(last, kf)
+    rng = np.random.default_rng(200 + seed)
+    for T in (synth.motion_pose(), synth.rotated_pose(1.5, axis=seed % 3)):
+        nm = keyframe_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], None, kf, T, th, orb_dist)
+        assert search_path(ctx)[0] == 0
+        has = (rng.random(len(r1["kps"])) < 0.3).astype(np.uint8)
+        keyframe_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], has, kf, T, th, orb_dist,
+                      already=rng.choice(len(kf["valid"]), 50, replace=False))
+        keyframe_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], None, kf, T, th, orb_dist, check_ori=False)
+    assert nm > 20
+
+
+def last_has(last, kf):
+    """Valid only where the LastFrame keypoint had a MapPoint (depth > 0); distractors stay."""
+    v = np.ones(len(kf["valid"]), np.uint8)
+    v[:len(last["has_mp"])] = last["has_mp"]
+    return v
+
+
+def test_keyframe_paths_and_edges(ctx, oracle_mod, ex, pair, monkeypatch):
+    import coeb_front
+    r1, ur1, last = pair
+    kf = synth.make_keyframe_points(last["xw"], last["mp_desc"], last["keys_un"]["octave"], last["keys_un"]["angle"],
+                                    seed=7)
+    kf["valid"] &= last_has(last, kf)
+    T = synth.motion_pose()
+    monkeypatch.setenv("COEB_MATCH_SEQUENTIAL", "1")
+    keyframe_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], None, kf, T)
+    assert search_path(ctx)[0] == 1
+    monkeypatch.delenv("COEB_MATCH_SEQUENTIAL")
+    # wide window on repetitive descriptors: list overflow -> literal loop
+    dup = dict(kf)
+    dup["descriptor"] = np.repeat(kf["descriptor"][:1], len(kf["valid"]), axis=0)
+    keyframe_both(ctx, oracle_mod, ex, r1["kps"], np.repeat(kf["descriptor"][:1], len(r1["kps"]), axis=0), None,
+                  dup, T, th=200.0)
+    assert search_path(ctx)[0] == 2
+    # empty keyframe / empty frame / every point behind or outside
+    empty = {k: v[:0] for k, v in kf.items()}
+    assert keyframe_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], None, empty, T) == 0
+    assert keyframe_both(ctx, oracle_mod, ex, r1["kps"][:0], r1["desc"][:0], None, kf, T) == 0
+    away = synth.rotated_pose(180.0, axis=1, t=(0, 0, 0))
+    keyframe_both(ctx, oracle_mod, ex, r1["kps"], r1["desc"], None, kf, away)
+    with pytest.raises(ValueError):
+        coeb_front.KeyFramePoints(kf["valid"], kf["world_pos"], kf["descriptor"], kf["max_distance"],
+                                  kf["min_distance"], kf["angle"][:-1])

@@ -277,3 +277,138 @@ def test_search_local_map_oracle_vs_python(oracle_mod, seed):
         nm_py, mt_py = _py_search_local_map(cam, kps, desc, ur, cur_obs, mp, th, ratio)
         assert nm == nm_py and np.array_equal(mt, mt_py)
         assert nm > 0
+
+
+# ---- relocalisation SearchByProjection: C oracle vs a literal Python loop (ORBmatcher.cc:1473-1600) ----
+def _py_search_keyframe(cam, kps, desc, cur_has, kf, T, th, orb_dist, check_ori):
+    f32, f64 = np.float32, np.float64
+    cols, rows = 64, 48
+    grid = [[[] for _ in range(rows)] for _ in range(cols)]
+    for i, k in enumerate(kps):
+        gx = float((f32(k["x"]) - f32(cam.min_x)) * f32(cam.grid_inv_w))
+        gy = float((f32(k["y"]) - f32(cam.min_y)) * f32(cam.grid_inv_h))
+        px = int(math.copysign(math.floor(abs(gx) + 0.5), gx))
+        py = int(math.copysign(math.floor(abs(gy) + 0.5), gy))
+        if 0 <= px < cols and 0 <= py < rows:
+            grid[px][py].append(i)
+    T = np.asarray(T, f32)
+    Ow = [f32(-(f64(T[0, k]) * f64(T[0, 3]) + f64(T[1, k]) * f64(T[1, 3]) + f64(T[2, k]) * f64(T[2, 3])))
+          for k in range(3)]
+    log_sf = f32(math.log(f64(f32(cam.scale[1]))))
+    taken = [bool(h) for h in cur_has]
+    match = [-1] * len(kps)
+    hist = []
+    nm = 0
+    for q in range(len(kf["valid"])):
+        if not kf["valid"][q]:
+            continue
+        X = kf["world_pos"][q].astype(f32)
+        p3 = []
+        for k in range(3):
+            t = f32(T[k, 0] * X[0]) + f32(T[k, 1] * X[1])
+            t = f32(t + f32(T[k, 2] * X[2]))
+            p3.append(f32(f64(t) + f64(T[k, 3])))
+        invz = f32(1.0 / f64(p3[2]))
+        u = f32(f64(f32(f32(cam.fx) * p3[0])) * f64(invz) + f64(f32(cam.cx)))    # fmaf, exact in double
+        v = f32(f64(f32(f32(cam.fy) * p3[1])) * f64(invz) + f64(f32(cam.cy)))
+        if u < f32(cam.min_x) or u > f32(cam.max_x) or v < f32(cam.min_y) or v > f32(cam.max_y):
+            continue
+        d = [f32(X[k] - Ow[k]) for k in range(3)]
+        ss = 0.0
+        for k in range(3):
+            ss += f64(d[k]) * f64(d[k])
+        dist3 = f32(math.sqrt(ss))
+        if dist3 < f32(f32(0.8) * f32(kf["min_distance"][q])) or dist3 > f32(f32(1.2) * f32(kf["max_distance"][q])):
+            continue
+        ratio = f32(f32(kf["max_distance"][q]) / dist3)
+        lvl = int(math.ceil(f32(f32(math.log(f64(ratio))) / log_sf)))
+        lvl = min(max(lvl, 0), cam.nlevels - 1)
+        r = f32(f32(th) * f32(cam.scale[lvl]))
+        x0 = max(0, math.floor(f32(f32(u - f32(cam.min_x)) - r) * f32(cam.grid_inv_w)))
+        x1 = min(cols - 1, math.ceil(f32(f32(u - f32(cam.min_x)) + r) * f32(cam.grid_inv_w)))
+        y0 = max(0, math.floor(f32(f32(v - f32(cam.min_y)) - r) * f32(cam.grid_inv_h)))
+        y1 = min(rows - 1, math.ceil(f32(f32(v - f32(cam.min_y)) + r) * f32(cam.grid_inv_h)))
+        if x0 >= cols or x1 < 0 or y0 >= rows or y1 < 0:
+            continue
+        best, bi = 256, -1
+        for ix in range(x0, x1 + 1):
+            for iy in range(y0, y1 + 1):
+                for j in grid[ix][iy]:
+                    o = int(kps[j]["octave"])
+                    if o < lvl - 1 or o > lvl + 1:
+                        continue
+                    if not (abs(f32(kps[j]["x"]) - u) < r and abs(f32(kps[j]["y"]) - v) < r):
+                        continue
+                    if taken[j]:
+                        continue
+                    dd = sum(bin(int(a) ^ int(b)).count("1") for a, b in zip(kf["descriptor"][q], desc[j]))
+                    if dd < best:
+                        best, bi = dd, j
+        if best <= orb_dist:
+            taken[bi] = True
+            match[bi] = q
+            nm += 1
+            if check_ori:
+                rot = f32(f32(kf["angle"][q]) - f32(kps[bi]["angle"]))
+                if rot < 0:
+                    rot = f32(rot + f32(360.0))
+                x = float(f32(rot * f32(1.0 / 30)))
+                b = int(math.floor(x + 0.5))
+                hist.append((bi, 0 if b == 30 else b))
+    if check_ori:
+        h = [0] * 30
+        for _, b in hist:
+            h[b] += 1
+        m1 = m2 = m3 = 0
+        i1 = i2 = i3 = -1
+        for i in range(30):
+            if h[i] > m1:
+                m3, m2, m1, i3, i2, i1 = m2, m1, h[i], i2, i1, i
+            elif h[i] > m2:
+                m3, m2, i3, i2 = m2, h[i], i2, i
+            elif h[i] > m3:
+                m3, i3 = h[i], i
+        if m2 < f32(0.1) * f32(m1):
+            i2 = i3 = -1
+        elif m3 < f32(0.1) * f32(m1):
+            i3 = -1
+        for bi, b in hist:
+            if b not in (i1, i2, i3):
+                match[bi] = -1
+                nm -= 1
+    return nm, np.array(match, np.int32)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_search_keyframe_oracle_vs_python(oracle_mod, seed):
+    rng = np.random.default_rng(seed)
+    ex = oracle_mod.Extractor()
+    cam = oracle_mod.camera(ex, 640, 480, 535.4, 539.2, 320.1, 247.6, 40.0)
+    n, m = 300, 260
+    kps = np.zeros(n, oracle_mod.KP_DTYPE)
+    kps["x"] = rng.uniform(0, 640, n)
+    kps["y"] = rng.uniform(0, 480, n)
+    kps["octave"] = rng.integers(0, 8, n)
+    kps["angle"] = rng.uniform(0, 360, n)
+    desc = rng.integers(0, 256, (n, 32)).astype(np.uint8)
+    src = rng.integers(0, n, m)
+    z = rng.uniform(1.0, 4.0, m).astype(np.float32)
+    xw = np.stack([((kps["x"][src] + rng.normal(0, 2, m) - 320.1) * z / 535.4),
+                   ((kps["y"][src] + rng.normal(0, 2, m) - 247.6) * z / 539.2), z], 1).astype(np.float32)
+    d = desc[src].copy()
+    for q in range(m):
+        for b in rng.integers(0, 256, rng.integers(0, 40)):
+            d[q, b >> 3] ^= np.uint8(1 << (b & 7))
+    dist = np.sqrt((xw.astype(np.float64) ** 2).sum(1)).astype(np.float32)
+    maxd = (dist * np.float32(1.2) ** kps["octave"][src].astype(np.float32) * rng.uniform(0.9, 1.1, m)).astype(np.float32)
+    kf = dict(valid=(rng.random(m) < 0.9).astype(np.uint8), world_pos=xw, descriptor=d, max_distance=maxd,
+              min_distance=(maxd / np.float32(1.2) ** 7).astype(np.float32),
+              angle=(kps["angle"][src] + rng.normal(0, 5, m)).astype(np.float32) % 360)
+    T = np.eye(4, dtype=np.float32)
+    T[:3, 3] = [0.01, -0.02, 0.015]
+    has = (rng.random(n) < 0.2).astype(np.uint8)
+    for th, od, ori in ((10.0, 100, True), (3.0, 64, True), (15.0, 80, False)):
+        nm, mt = oracle_mod.search_keyframe(cam, kps, desc, has, kf, T, th, od, ori)
+        nm_py, mt_py = _py_search_keyframe(cam, kps, desc, has, kf, T, th, od, ori)
+        assert nm == nm_py and np.array_equal(mt, mt_py), (nm, nm_py)
+        assert nm > 0
