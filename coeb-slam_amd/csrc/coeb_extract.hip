@@ -153,12 +153,16 @@ __device__ __forceinline__ int byte_of(uint32_t w0, uint32_t w1, uint32_t w2, in
 
 // VResizeLinearVec_32s8u: ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2.
 // Coefficients are in [0, 2048] and h <= 255 * 2048, so h >> 4 <= 32640 (the 16-bit
-// saturations of the SIMD code never trigger) and every product fits 26 bits: full-rate
-// 24-bit multiplies instead of the quarter-rate v_mul_lo_u32.
-__device__ __forceinline__ int vresize(int h0, int h1, int b0, int b1)
+// saturations of the SIMD code never trigger).  The horizontal pass produces g = h << 4 (its
+// coefficients pre-shifted; g < 2^24), so ((h >> 4) * b) >> 16 = mul_hi_u24(g & ~0xFF, b << 8):
+// one AND and one full-rate 24-bit multiply-high per term.  Each term is <= (32656 * b) >> 16
+// and b0 + b1 <= 2049 (coefficients rounded separately), so the sum is <= 1021 and the result
+// <= 255: the final saturate_cast never clips.
+__device__ __forceinline__ uint32_t vresize_g(uint32_t g0, uint32_t g1, uint32_t b0s, uint32_t b1s)
 {
-    const int m0 = __mul24(h0 >> 4, b0) >> 16, m1 = __mul24(h1 >> 4, b1) >> 16;
-    return max(0, min((m0 + m1 + 2) >> 2, 255));
+    const uint32_t m0 = __umulhi(g0 & 0xFFFF00u, b0s & 0xFFFFFFu);   // v_mul_hi_u32_u24
+    const uint32_t m1 = __umulhi(g1 & 0xFFFF00u, b1s & 0xFFFFFFu);
+    return (m0 + m1 + 2u) >> 2;
 }
 
 // Output tile 128 x 32 per workgroup; the source rows/columns it touches (<= 32*scale+2 rows,
@@ -223,15 +227,15 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
     const int cx = ox + (threadIdx.x & 31) * 4, cy = oy + (threadIdx.x >> 5) * 4;
     if (cx >= dw) return;
     const int nk = min(4, dw - cx);
-    int lx[4], a0[4], a1[4];
+    int lx[4], a0[4], a1[4];                      // horizontal coefficients << 4 (pass gives g = h << 4)
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int d = min(cx + k, dw - 1);
         const int sx = xofs[d];
         const int a = alpha[d];
-        a0[k] = (int)(short)(a & 0xFFFF);
-        a1[k] = a >> 16;
-        if (d >= xmax) { a0[k] = 2048; a1[k] = 0; }        // HResizeLinear tail: S[sx]*ONE
+        a0[k] = ((int)(short)(a & 0xFFFF)) << 4;
+        a1[k] = (a >> 16) << 4;
+        if (d >= xmax) { a0[k] = 2048 << 4; a1[k] = 0; }   // HResizeLinear tail: S[sx]*ONE
         lx[k] = sx - sx0;
     }
 #pragma unroll
@@ -242,15 +246,15 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
         const int r0 = (q0 >= 0 ? (q0 < sh ? q0 : sh - 1) : 0) - sy0;
         const int r1 = (q0 + 1 >= 0 ? (q0 + 1 < sh ? q0 + 1 : sh - 1) : 0) - sy0;
         const int bb = beta[dy];
-        const int b0 = (int)(short)(bb & 0xFFFF), b1 = bb >> 16;
-        const uint8_t* R0 = s_src + r0 * PT_SW;
-        const uint8_t* R1 = s_src + r1 * PT_SW;
+        const uint32_t b0s = (uint32_t)((int)(short)(bb & 0xFFFF)) << 8, b1s = (uint32_t)(bb >> 16) << 8;
+        const uint8_t* R0 = s_src + __mul24(r0, PT_SW);
+        const uint8_t* R1 = s_src + __mul24(r1, PT_SW);
         uint32_t word = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const int h0 = __mul24((int)R0[lx[k]], a0[k]) + __mul24((int)R0[lx[k] + 1], a1[k]);
-            const int h1 = __mul24((int)R1[lx[k]], a0[k]) + __mul24((int)R1[lx[k] + 1], a1[k]);
-            word |= (uint32_t)vresize(h0, h1, b0, b1) << (8 * k);
+            const int g0 = __mul24((int)R0[lx[k]], a0[k]) + __mul24((int)R0[lx[k] + 1], a1[k]);
+            const int g1 = __mul24((int)R1[lx[k]], a0[k]) + __mul24((int)R1[lx[k] + 1], a1[k]);
+            word |= vresize_g((uint32_t)g0, (uint32_t)g1, b0s, b1s) << (8 * k);
         }
         uint8_t* D = dst + (int64_t)f * dst_fs + (int64_t)dy * dp + cx;
         if (nk == 4 && (dp & 3) == 0) *reinterpret_cast<uint32_t*>(D) = word;
@@ -855,7 +859,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // a per-lane wave index here (unlike the other kernels): with the cell geometry in SGPRs the
     // compiler moves the per-cell bookkeeping onto the shared scalar unit and the kernel ran
-    // 5 % slower (0.320 vs 0.335 ms/step)
+    // 5 % slower (0.320 vs 0.335 ms/step).  A u16-pixel slab (ring operands as aligned u16
+    // pairs, no byte gathers; 11 ds_read_b64 per 4-pixel group) cut VALU 7 % but ran 5 % slower
+    // (twice the staging stores): the byte slab stays.
     const int wv = threadIdx.x >> 6, lane = lane_id();
     const int slab = fast_slab(*P);                          // per-wave LDS: roi, M, lists
     uint8_t* wbase = smem + (size_t)wv * (2 * slab + 2 * (kFastSurv + kFastCorners));
