@@ -15,6 +15,8 @@
       include/ORBmatcher.h:55, src/ORBmatcher.cc:1473-1600 (Tracking::Relocalization,
       src/Tracking.cc:1531,1545); assigns F.mvpMapPoints[i] = KeyFrame point index.
   ORBmatcher.DescriptorDistance(a, b)  src/ORBmatcher.cc:1648-1664
+  Optimizer.PoseOptimization(F, camera)  include/Optimizer.h:47, src/Optimizer.cc:239-451; reads
+      F.mvpMapPoints (>= 0: has a MapPoint) and F.mvMapPointPos, sets F.mTcw and F.mvbOutlier.
 
 All compute runs in libcoeb_front.so (hand-written gfx950 HIP kernels).  There is no CPU
 fallback: importing works anywhere, but constructing an extractor without the built library
@@ -43,7 +45,7 @@ ABI_SYMBOLS = [
     "coeb_rgbd_preprocess", "coeb_descriptor_distance", "coeb_profile_enable", "coeb_profile_read",
     "coeb_profile_reset", "coeb_synchronize", "coeb_device_count", "coeb_debug_read",
     "coeb_device_alloc", "coeb_device_free", "coeb_memcpy_h2d", "coeb_memcpy_d2h", "coeb_set_batch_streams",
-    "coeb_match_localmap", "coeb_match_keyframe",
+    "coeb_match_localmap", "coeb_match_keyframe", "coeb_pose_optimization",
 ]
 
 
@@ -82,6 +84,11 @@ class LocalMapC(C.Structure):
 class KeyFramePointsC(C.Structure):
     _fields_ = [("n", C.c_int32), ("valid", C.c_void_p), ("world_pos", C.c_void_p), ("descriptor", C.c_void_p),
                 ("max_distance", C.c_void_p), ("min_distance", C.c_void_p), ("angle", C.c_void_p)]
+
+
+class PoseFrameC(C.Structure):
+    _fields_ = [("n", C.c_int32), ("has_mappoint", C.c_void_p), ("world_pos", C.c_void_p), ("keys_un", C.c_void_p),
+                ("u_right", C.c_void_p)]
 
 
 class CoebError(RuntimeError):
@@ -125,6 +132,8 @@ def lib():
         L.coeb_match_keyframe.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(CurFrameC), C.c_void_p,
                                           C.POINTER(KeyFramePointsC), C.c_void_p, C.c_float, C.c_int, C.c_int,
                                           C.c_void_p, C.POINTER(C.c_int)]
+        L.coeb_pose_optimization.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(PoseFrameC), C.c_void_p,
+                                             C.c_void_p, C.POINTER(C.c_int)]
         L.coeb_blur_flags.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_int,
                                       C.c_void_p]
         L.coeb_stereo_from_rgbd.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
@@ -398,6 +407,8 @@ class Frame:
         self.mvpMapPoints = np.full(self.N, -1, np.int32)
         # Observations() of the MapPoint in mvpMapPoints[i] (-1 = NULL); read by the local-map search
         self.mvpMapPointObs = np.full(self.N, -1, np.int32)
+        # GetWorldPos() of the MapPoint in mvpMapPoints[i]; read by Optimizer.PoseOptimization
+        self.mvMapPointPos = np.zeros((self.N, 3), np.float32)
 
 
 class LocalMap:
@@ -533,6 +544,25 @@ class ORBmatcher:
         if hit.any():
             F.mvpMapPointObs = np.where(hit, local_map.nObs[np.maximum(got, 0)], F.mvpMapPointObs).astype(np.int32)
         return nm.value
+
+
+class Optimizer:
+    """Mirror of ORB_SLAM2::Optimizer for the tracking pose refinement."""
+
+    @staticmethod
+    def PoseOptimization(pFrame, camera, ctx):
+        F = pFrame
+        has = np.ascontiguousarray(F.mvpMapPoints >= 0, np.uint8)
+        xw = np.ascontiguousarray(F.mvMapPointPos, np.float32).reshape(F.N, 3) if F.N else np.zeros((1, 3), np.float32)
+        fr = PoseFrameC(F.N, C.c_void_p(has.ctypes.data), C.c_void_p(xw.ctypes.data), C.c_void_p(F.mvKeysUn.ctypes.data),
+                        C.c_void_p(F.mvuRight.ctypes.data))
+        T = np.ascontiguousarray(F.mTcw, np.float32).copy()
+        out = np.ascontiguousarray(F.mvbOutlier, np.uint8).copy() if len(F.mvbOutlier) else np.zeros(1, np.uint8)
+        nin = C.c_int()
+        ctx.check(lib().coeb_pose_optimization(ctx.h, C.byref(camera), C.byref(fr), _p(T), _p(out), C.byref(nin)))
+        F.mTcw = T.reshape(4, 4)
+        F.mvbOutlier = out[:F.N]
+        return nin.value
 
 
 def make_camera(fx, fy, cx, cy, bf, w, h):

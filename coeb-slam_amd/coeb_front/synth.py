@@ -187,3 +187,46 @@ def rotated_pose(deg, axis=1, t=(0.02, -0.01, 0.03)):
     T[:3, :3] = R.astype(np.float32)
     T[:3, 3] = np.asarray(t, np.float32)
     return T
+
+
+def make_pose_problem(n=600, seed=0, outlier_frac=0.2, mono_frac=0.3, noise=0.7, nlevels=8, scale_factor=1.2,
+                      w=640, h=480, fx=TUM_FX, fy=TUM_FY, cx=TUM_CX, cy=TUM_CY, bf=TUM_BF, init_err=(0.02, 0.03)):
+    """A synthetic Optimizer::PoseOptimization input: n keypoints of which most hold a MapPoint
+    seen from a true pose (rotation ~3 deg, translation ~0.1 m) with Gaussian pixel noise at
+    their octave's scale, a fraction of gross outliers (wrong 3-D points), a fraction without
+    depth (mvuRight = -1, monocular edges), and an initial pose perturbed by init_err
+    (rad, m).  Returns dict(kps, has_mp, xw, ur, Tcw_init, Tcw_true)."""
+    rng = np.random.default_rng(seed)
+
+    def pose(rv, t):
+        th = np.linalg.norm(rv)
+        K = np.array([[0, -rv[2], rv[1]], [rv[2], 0, -rv[0]], [-rv[1], rv[0], 0]])
+        R = np.eye(3) if th == 0 else np.eye(3) + np.sin(th) / th * K + (1 - np.cos(th)) / th ** 2 * K @ K
+        T = np.eye(4)
+        T[:3, :3] = R
+        T[:3, 3] = t
+        return T
+
+    Ttrue = pose(rng.normal(0, 0.03, 3), rng.normal(0, 0.1, 3))
+    Tinit = pose(rng.normal(0, init_err[0], 3), rng.normal(0, init_err[1], 3)) @ Ttrue
+    z = rng.uniform(1.0, 6.0, n)
+    u = rng.uniform(20, w - 20, n)
+    v = rng.uniform(20, h - 20, n)
+    pc = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
+    Rt, tt = Ttrue[:3, :3], Ttrue[:3, 3]
+    xw = (pc - tt) @ Rt                                        # Xw = R^T (Xc - t)
+    octave = rng.integers(0, nlevels, n).astype(np.int32)
+    sig = np.float64(scale_factor) ** octave
+    kps = np.zeros(n, np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                                ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")]))
+    kps["x"] = u + rng.normal(0, noise, n) * sig
+    kps["y"] = v + rng.normal(0, noise, n) * sig
+    kps["octave"] = octave
+    kps["class_id"] = -1
+    ur = (kps["x"] - bf / z + rng.normal(0, noise, n) * sig).astype(np.float32)
+    ur[rng.random(n) < mono_frac] = -1.0
+    out = rng.random(n) < outlier_frac
+    xw[out] += rng.normal(0, 0.5, (out.sum(), 3))
+    has = (rng.random(n) < 0.9).astype(np.uint8)
+    return dict(kps=kps, has_mp=has, xw=xw.astype(np.float32), ur=ur, Tcw_init=Tinit.astype(np.float32),
+                Tcw_true=Ttrue.astype(np.float32), gross=out)

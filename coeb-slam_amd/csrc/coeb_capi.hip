@@ -988,6 +988,63 @@ int coeb_match_keyframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curframe
     return COEB_OK;
 }
 
+int coeb_pose_optimization(coeb_ctx* c, const coeb_camera* cam, const coeb_pose_frame* fr, float Tcw[16],
+                           uint8_t* outlier_out, int* ninliers)
+{
+    if (!c || !cam || !fr || !Tcw || !ninliers) return set_err(c, COEB_EINVAL, "coeb_pose_optimization: invalid arguments");
+    *ninliers = 0;
+    const int n = fr->n;
+    if (n < 0) return set_err(c, COEB_EINVAL, "negative frame size");
+    if (n && (!fr->has_mappoint || !fr->world_pos || !fr->keys_un || !fr->u_right))
+        return set_err(c, COEB_EINVAL, "coeb_pose_optimization: missing frame arrays");
+    for (int i = 0; i < n; i++)
+        if (fr->has_mappoint[i] && (fr->keys_un[i].octave < 0 || fr->keys_un[i].octave >= c->tab.nlevels))
+            return set_err(c, COEB_EINVAL, "coeb_pose_optimization: keypoint octave outside the pyramid");
+    (void)hipSetDevice(c->device);
+    const int cs = std::max(n, 1);
+    int rc;
+    int32_t *dn, *dres;
+    uint8_t *dhas, *dout, *dact;
+    float *dxw, *dur, *dT, *dis;
+    coeb_keypoint* dk;
+    PoseEdgeRec* dedge;
+    double* dchi;
+    if ((rc = ensure(c, "p_n", 1, &dn)) || (rc = ensure(c, "p_res", 1, &dres)) || (rc = ensure(c, "p_has", cs, &dhas)) ||
+        (rc = ensure(c, "p_out", cs, &dout)) || (rc = ensure(c, "p_act", cs, &dact)) ||
+        (rc = ensure(c, "p_xw", (size_t)cs * 3, &dxw)) || (rc = ensure(c, "p_ur", cs, &dur)) ||
+        (rc = ensure(c, "p_T", 16, &dT)) || (rc = ensure(c, "p_is", COEB_MAXL, &dis)) || (rc = ensure(c, "p_k", cs, &dk)) ||
+        (rc = ensure(c, "p_edge", cs, &dedge)) || (rc = ensure(c, "p_chi", cs, &dchi)))
+        return rc;
+    hipStream_t s = main_stream(c);
+    HIP_TRY(c, hipMemcpyAsync(dn, &fr->n, 4, hipMemcpyHostToDevice, s));
+    if (n) {
+        HIP_TRY(c, hipMemcpyAsync(dhas, fr->has_mappoint, (size_t)n, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dxw, fr->world_pos, (size_t)n * 12, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dk, fr->keys_un, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dur, fr->u_right, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(c, hipMemcpyAsync(dT, Tcw, 64, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(dis, c->tab.inv_sigma2, sizeof(float) * COEB_MAXL, hipMemcpyHostToDevice, s));
+    PoseBufs b;
+    b.n = dn; b.has_mp = dhas; b.xw = dxw; b.kps = dk; b.ur = dur; b.inv_sigma2 = dis; b.Tcw = dT; b.outlier = dout;
+    b.result = dres; b.edges = dedge; b.active = dact; b.chi2 = dchi; b.stride = cs;
+    if (launch_pose(b, 1, cam->fx, cam->fy, cam->cx, cam->cy, cam->bf, s, &c->hook))
+        return hip_err(c, hipGetLastError(), "launch_pose");
+    int res = 0;
+    HIP_TRY(c, hipMemcpyAsync(&res, dres, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(Tcw, dT, 64, hipMemcpyDeviceToHost, s));
+    if (n && outlier_out) {
+        std::vector<uint8_t> o((size_t)n);
+        HIP_TRY(c, hipMemcpyAsync(o.data(), dout, (size_t)n, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipStreamSynchronize(s));
+        for (int i = 0; i < n; i++)
+            if (fr->has_mappoint[i]) outlier_out[i] = o[i];
+    }
+    HIP_TRY(c, hipStreamSynchronize(s));
+    *ninliers = res;
+    return COEB_OK;
+}
+
 namespace {
 
 // Common body of the batch matchers.  dT_cur: device poses, pair p (current frame p+1) at

@@ -183,6 +183,26 @@ int launch_match_local(const MatchCam& cam, const LocalBufsHost& b, float th, fl
                        ProfileHook* prof);
 int match_list_cap();   // candidate-list entries per query (kCQ)
 
+// Optimizer::PoseOptimization (coeb_pose.hip): per frame f, keypoints [f][stride]
+struct PoseEdgeRec { float x, y, z, u, v, ur, w; int stereo, kp; };
+struct PoseBufs {
+    const int* n;                 // [F] keypoints
+    const uint8_t* has_mp;        // [F][stride]
+    const float* xw;              // [F][stride][3]
+    const void* kps;              // [F][stride] coeb_keypoint
+    const float* ur;              // [F][stride]
+    const float* inv_sigma2;      // [COEB_MAXL] mvInvLevelSigma2
+    float* Tcw;                   // [F][16] in/out
+    uint8_t* outlier;             // [F][stride] out (mvbOutlier, where has_mp)
+    int* result;                  // [F] nInitialCorrespondences - nBad
+    PoseEdgeRec* edges;           // scratch [F][stride]
+    uint8_t* active;              // scratch [F][stride]
+    double* chi2;                 // scratch [F][stride]
+    int stride;
+};
+int launch_pose(const PoseBufs& b, int F, double fx, double fy, double cx, double cy, double bf, hipStream_t s,
+                ProfileHook* prof);
+
 // relocalisation projection search (ORBmatcher::SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist))
 struct KfBufsHost {
     const void* cur_kps; const uint8_t* cur_desc; const uint8_t* cur_has; int cur_n;

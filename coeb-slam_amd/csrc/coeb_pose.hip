@@ -1,0 +1,500 @@
+// coeb_pose.hip -- Optimizer::PoseOptimization(Frame*) (src/Optimizer.cc:239-451) on the device:
+// g2o's Levenberg-Marquardt (OptimizationAlgorithmLevenberg, BlockSolver_6_3 with one SE3
+// vertex, LinearSolverDense) over the frame's EdgeSE3ProjectXYZOnlyPose /
+// EdgeStereoSE3ProjectXYZOnlyPose edges with the Huber kernel, 4 rounds x 10 iterations with
+// chi2 outlier classification.  g2o is not vendored in the reference (Thirdparty/g2o absent):
+// this follows its published 2012 algorithm as restated in oracle/orb_oracle.c
+// (oc_pose_optimization), operation for operation, in double precision.
+//
+// One 256-thread workgroup per frame.  Edge i lives with thread i % 256; per-edge sums (the
+// 21 Hessian terms, 6 gradient terms, robust chi2) are reduced in the canonical order
+// (per-thread sequential, xor butterfly inside each wave, (w0 + w1) + (w2 + w3)) so the
+// result is bit-identical to the oracle.  The 6x6 solve, the SE3 exponential and the LM
+// bookkeeping run on thread 0 and are broadcast through LDS.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "coeb_internal.hpp"
+
+namespace {
+
+constexpr int kPT = 256;
+
+struct Se3 { double w, x, y, z, t[3]; };
+struct KpRec { float x, y, size, angle, response; int octave, class_id; };   // coeb_keypoint
+struct PEdge { double X[3], obs[3], w; int stereo; };
+
+__device__ void pq_from_R(const double R[9], Se3& s)
+{
+    double t = (R[0] + R[4]) + R[8];
+    double q[4];
+    if (t > 0.0) {
+        t = sqrt(t + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (R[7] - R[5]) * t;
+        q[1] = (R[2] - R[6]) * t;
+        q[2] = (R[3] - R[1]) * t;
+    } else {
+        int i = 0;
+        if (R[4] > R[0]) i = 1;
+        if (R[8] > R[i * 4]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(((R[i * 4] - R[j * 4]) - R[k * 4]) + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (R[k * 3 + j] - R[j * 3 + k]) * t;
+        q[j] = (R[j * 3 + i] + R[i * 3 + j]) * t;
+        q[k] = (R[k * 3 + i] + R[i * 3 + k]) * t;
+    }
+    s.x = q[0]; s.y = q[1]; s.z = q[2]; s.w = q[3];
+}
+
+__device__ void pq_normalize(Se3& s)
+{
+    if (s.w < 0) { s.w = -s.w; s.x = -s.x; s.y = -s.y; s.z = -s.z; }
+    const double n = sqrt(((s.x * s.x + s.y * s.y) + s.z * s.z) + s.w * s.w);
+    s.x = s.x / n; s.y = s.y / n; s.z = s.z / n; s.w = s.w / n;
+}
+
+__device__ __forceinline__ void pq_rotate(const Se3& s, const double v[3], double o[3])
+{
+    double uv[3] = {s.y * v[2] - s.z * v[1], s.z * v[0] - s.x * v[2], s.x * v[1] - s.y * v[0]};
+    uv[0] = uv[0] + uv[0]; uv[1] = uv[1] + uv[1]; uv[2] = uv[2] + uv[2];
+    const double c[3] = {s.y * uv[2] - s.z * uv[1], s.z * uv[0] - s.x * uv[2], s.x * uv[1] - s.y * uv[0]};
+    for (int k = 0; k < 3; k++) o[k] = (v[k] + s.w * uv[k]) + c[k];
+}
+
+__device__ Se3 pq_mul(const Se3& a, const Se3& b)
+{
+    Se3 r;
+    double bt[3];
+    pq_rotate(a, b.t, bt);
+    for (int k = 0; k < 3; k++) r.t[k] = a.t[k] + bt[k];
+    r.w = ((a.w * b.w - a.x * b.x) - a.y * b.y) - a.z * b.z;
+    r.x = ((a.w * b.x + a.x * b.w) + a.y * b.z) - a.z * b.y;
+    r.y = ((a.w * b.y + a.y * b.w) + a.z * b.x) - a.x * b.z;
+    r.z = ((a.w * b.z + a.z * b.w) + a.x * b.y) - a.y * b.x;
+    pq_normalize(r);
+    return r;
+}
+
+// canonical sin/cos (the oracle's table)
+__constant__ double kPqSin[14] = {0x1.0000000000000p+0, -0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13,
+                                  0x1.71de3a556c734p-19, -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41,
+                                  0x1.952c77030ad4ap-49, -0x1.2f49b46814157p-57, 0x1.71b8ef6dcf572p-66, -0x1.761b413163819p-75,
+                                  0x1.3f3ccdd165fa9p-84, -0x1.d1ab1c2dccea3p-94};
+__constant__ double kPqCos[14] = {0x1.0000000000000p+0, -0x1.0000000000000p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10,
+                                  0x1.a01a01a01a01ap-16, -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37,
+                                  0x1.ae7f3e733b81fp-45, -0x1.6827863b97d97p-53, 0x1.e542ba4020225p-62, -0x1.0ce396db7f853p-70,
+                                  0x1.f2cf01972f578p-80, -0x1.88e85fc6a4e59p-89};
+
+__device__ void pq_sincos(double x, double& sn, double& cs)
+{
+    const double k = floor(x * 0.63661977236758134308 + 0.5);
+    const double r = (x - k * 1.57079632673412561417e+00) - k * 6.07710050650619224932e-11;
+    const double r2 = r * r;
+    double ps = kPqSin[13], pc = kPqCos[13];
+    for (int n = 12; n >= 0; n--) {
+        ps = ps * r2 + kPqSin[n];
+        pc = pc * r2 + kPqCos[n];
+    }
+    const double s0 = r * ps, c0 = pc;
+    const int q = ((int)(long)k) & 3;
+    if (q == 0) { sn = s0; cs = c0; }
+    else if (q == 1) { sn = c0; cs = -s0; }
+    else if (q == 2) { sn = -s0; cs = -c0; }
+    else { sn = -c0; cs = s0; }
+}
+
+// SE3Quat::exp(update)
+__device__ Se3 pq_exp(const double u[6])
+{
+    const double o0 = u[0], o1 = u[1], o2 = u[2];
+    const double theta = sqrt((o0 * o0 + o1 * o1) + o2 * o2);
+    const double Om[9] = {0.0, -o2, o1, o2, 0.0, -o0, -o1, o0, 0.0};
+    double Om2[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            Om2[i * 3 + j] = (Om[i * 3] * Om[j] + Om[i * 3 + 1] * Om[3 + j]) + Om[i * 3 + 2] * Om[6 + j];
+    double R[9], V[9];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) R[i] = ((i % 4 == 0 ? 1.0 : 0.0) + Om[i]) + Om2[i];
+        for (int i = 0; i < 9; i++) V[i] = R[i];
+    } else {
+        double sn, cs;
+        pq_sincos(theta, sn, cs);
+        const double th2 = theta * theta;
+        const double A = sn / theta, B = (1.0 - cs) / th2, Cc = (theta - sn) / (th2 * theta);
+        for (int i = 0; i < 9; i++) {
+            const double I = i % 4 == 0 ? 1.0 : 0.0;
+            R[i] = (I + A * Om[i]) + B * Om2[i];
+            V[i] = (I + B * Om[i]) + Cc * Om2[i];
+        }
+    }
+    Se3 s;
+    pq_from_R(R, s);
+    for (int i = 0; i < 3; i++) s.t[i] = (V[i * 3] * u[3] + V[i * 3 + 1] * u[4]) + V[i * 3 + 2] * u[5];
+    pq_normalize(s);
+    return s;
+}
+
+__device__ Se3 pq_from_Tcw(const float* T)
+{
+    double R[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) R[i * 3 + j] = (double)T[i * 4 + j];
+    Se3 s;
+    pq_from_R(R, s);
+    for (int i = 0; i < 3; i++) s.t[i] = (double)T[i * 4 + 3];
+    pq_normalize(s);
+    return s;
+}
+
+__device__ void pq_to_Tcw(const Se3& s, float* T)
+{
+    const double tx = 2.0 * s.x, ty = 2.0 * s.y, tz = 2.0 * s.z;
+    const double twx = tx * s.w, twy = ty * s.w, twz = tz * s.w;
+    const double txx = tx * s.x, txy = ty * s.x, txz = tz * s.x;
+    const double tyy = ty * s.y, tyz = tz * s.y, tzz = tz * s.z;
+    const double R[9] = {1.0 - (tyy + tzz), txy - twz, txz + twy,
+                         txy + twz, 1.0 - (txx + tzz), tyz - twx,
+                         txz - twy, tyz + twx, 1.0 - (txx + tyy)};
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) T[i * 4 + j] = (float)R[i * 3 + j];
+        T[i * 4 + 3] = (float)s.t[i];
+    }
+    T[12] = 0.f; T[13] = 0.f; T[14] = 0.f; T[15] = 1.f;
+}
+
+struct PoseCam { double fx, fy, cx, cy, bf; };
+
+// error, raw chi2 and (J != nullptr) the error Jacobian of one edge at pose s
+__device__ __forceinline__ double pq_edge_eval(const PoseCam& cm, const Se3& s, const PEdge& E, double e[3], double* J)
+{
+    double p[3];
+    pq_rotate(s, E.X, p);
+    for (int k = 0; k < 3; k++) p[k] = p[k] + s.t[k];
+    if (!E.stereo) {
+        const double u = (p[0] / p[2]) * cm.fx + cm.cx, v = (p[1] / p[2]) * cm.fy + cm.cy;
+        e[0] = E.obs[0] - u; e[1] = E.obs[1] - v; e[2] = 0.0;
+    } else {
+        const float invzf = 1.0f / (float)p[2];
+        const double u = (p[0] * (double)invzf) * cm.fx + cm.cx, v = (p[1] * (double)invzf) * cm.fy + cm.cy;
+        const double ur = u - cm.bf * (double)invzf;
+        e[0] = E.obs[0] - u; e[1] = E.obs[1] - v; e[2] = E.obs[2] - ur;
+    }
+    if (J) {
+        const double x = p[0], y = p[1], invz = 1.0 / p[2], invz_2 = invz * invz;
+        J[0] = ((x * y) * invz_2) * cm.fx;
+        J[1] = -(1.0 + ((x * x) * invz_2)) * cm.fx;
+        J[2] = (y * invz) * cm.fx;
+        J[3] = -invz * cm.fx;
+        J[4] = 0.0;
+        J[5] = (x * invz_2) * cm.fx;
+        J[6] = (1.0 + ((y * y) * invz_2)) * cm.fy;
+        J[7] = -((x * y) * invz_2) * cm.fy;
+        J[8] = -(x * invz) * cm.fy;
+        J[9] = 0.0;
+        J[10] = -invz * cm.fy;
+        J[11] = (y * invz_2) * cm.fy;
+        if (E.stereo) {
+            J[12] = J[0] - (cm.bf * y) * invz_2;
+            J[13] = J[1] + (cm.bf * x) * invz_2;
+            J[14] = J[2];
+            J[15] = J[3];
+            J[16] = 0.0;
+            J[17] = J[5] - cm.bf * invz_2;
+        }
+    }
+    double c = e[0] * (E.w * e[0]) + e[1] * (E.w * e[1]);
+    if (E.stereo) c = c + e[2] * (E.w * e[2]);
+    return c;
+}
+
+__device__ __forceinline__ void pq_huber(double e2, double delta, double& r0, double& r1)
+{
+    const double dsqr = delta * delta;
+    if (e2 <= dsqr) { r0 = e2; r1 = 1.0; }
+    else {
+        const double sq = sqrt(e2);
+        r0 = (2.0 * sq) * delta - dsqr;
+        r1 = delta / sq;
+    }
+}
+
+__device__ bool pq_solve6(const double H[36], const double b[6], double x[6])
+{
+    double L[36], d[6], y[6];
+    for (int i = 0; i < 36; i++) L[i] = 0.0;
+    for (int j = 0; j < 6; j++) {
+        double v = H[j * 6 + j];
+        for (int k = 0; k < j; k++) v = v - (L[j * 6 + k] * L[j * 6 + k]) * d[k];
+        if (!(v > 0.0)) return false;
+        d[j] = v;
+        for (int i = j + 1; i < 6; i++) {
+            double w = H[i * 6 + j];
+            for (int k = 0; k < j; k++) w = w - (L[i * 6 + k] * L[j * 6 + k]) * d[k];
+            L[i * 6 + j] = w / d[j];
+        }
+    }
+    for (int i = 0; i < 6; i++) {
+        double v = b[i];
+        for (int k = 0; k < i; k++) v = v - L[i * 6 + k] * y[k];
+        y[i] = v;
+    }
+    for (int i = 0; i < 6; i++) y[i] = y[i] / d[i];
+    for (int i = 5; i >= 0; i--) {
+        double v = y[i];
+        for (int k = i + 1; k < 6; k++) v = v - L[k * 6 + i] * x[k];
+        x[i] = v;
+    }
+    return true;
+}
+
+__device__ __forceinline__ double wave_sum(double v)    // xor butterfly 32 .. 1
+{
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+struct PoseLds {
+    Se3 s;                 // current estimate (broadcast)
+    double red[4][28];     // per-wave sums
+    double out[28];        // reduced
+    double rho;
+    int qmax, ok, nbad[4];
+};
+
+// block-wide canonical reduction of nv per-thread partials (uniform call)
+__device__ void block_reduce(PoseLds& L, double* v, int nv)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int k = 0; k < nv; k++) {
+        const double t = wave_sum(v[k]);
+        if (lane == 0) L.red[wv][k] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < nv) {
+        const int k = threadIdx.x;
+        L.out[k] = (L.red[0][k] + L.red[1][k]) + (L.red[2][k] + L.red[3][k]);
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ PEdge load_edge(const PoseBufs& b, int f, int e)
+{
+    const PoseEdgeRec r = b.edges[(int64_t)f * b.stride + e];
+    PEdge E;
+    E.X[0] = (double)r.x; E.X[1] = (double)r.y; E.X[2] = (double)r.z;
+    E.obs[0] = (double)r.u; E.obs[1] = (double)r.v; E.obs[2] = r.stereo ? (double)r.ur : 0.0;
+    E.w = (double)r.w;
+    E.stereo = r.stereo;
+    return E;
+}
+
+// computeActiveErrors + activeRobustChi2 at L.s; raw chi2 of active edges -> chi2_last
+__device__ double active_chi2(PoseLds& L, const PoseBufs& b, const PoseCam& cm, int f, int ne, bool robust,
+                              const double delta[2])
+{
+    const Se3 s = L.s;
+    double acc = 0.0;
+    for (int e = threadIdx.x; e < ne; e += kPT) {
+        if (!b.active[(int64_t)f * b.stride + e]) continue;
+        const PEdge E = load_edge(b, f, e);
+        double er[3];
+        const double c = pq_edge_eval(cm, s, E, er, nullptr);
+        b.chi2[(int64_t)f * b.stride + e] = c;
+        double r = c, r1;
+        if (robust) pq_huber(c, delta[E.stereo], r, r1);
+        acc += r;
+    }
+    double v[1] = {acc};
+    block_reduce(L, v, 1);
+    return L.out[0];
+}
+
+__global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
+{
+    __shared__ PoseLds L;
+    __shared__ int s_ne, s_cnt[4];
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n = b.n[f];
+    const int64_t base = (int64_t)f * b.stride;
+    // ---- edges: keypoints with a MapPoint, in keypoint order (block-ordered compaction) ----
+    if (tid == 0) s_ne = 0;
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += kPT) {
+        const int i = i0 + tid;
+        const bool has = i < n && b.has_mp[base + i];
+        const uint64_t m = __ballot(has);
+        if (lane == 0) s_cnt[wv] = __popcll(m);
+        __syncthreads();
+        int pre = s_ne;
+        for (int w = 0; w < wv; w++) pre += s_cnt[w];
+        if (has) {
+            const int e = pre + __popcll(m & ((1ull << lane) - 1ull));
+            const KpRec k = reinterpret_cast<const KpRec*>(b.kps)[base + i];
+            PoseEdgeRec r;
+            r.x = b.xw[(base + i) * 3 + 0]; r.y = b.xw[(base + i) * 3 + 1]; r.z = b.xw[(base + i) * 3 + 2];
+            r.u = k.x; r.v = k.y;
+            const float ur = b.ur[base + i];
+            r.stereo = !(ur < 0);                                  // Optimizer.cc:287
+            r.ur = ur;
+            r.w = b.inv_sigma2[k.octave];
+            r.kp = i;
+            b.edges[base + e] = r;
+            b.active[base + e] = 1;
+            b.outlier[base + i] = 0;
+        }
+        __syncthreads();
+        if (tid == 0) s_ne += s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        __syncthreads();
+    }
+    const int ne = s_ne;
+    float* Tcw = b.Tcw + (int64_t)f * 16;
+    if (ne < 3) {                                                  // :361-362
+        if (tid == 0) b.result[f] = 0;
+        return;
+    }
+    const double delta[2] = {(double)(float)sqrt(5.991), (double)(float)sqrt(7.815)};
+    const double chi2th[2] = {(double)5.991f, (double)7.815f};
+    Se3 s0;
+    if (tid == 0) s0 = pq_from_Tcw(Tcw);
+    int nBad = 0;
+    for (int it = 0; it < 4; it++) {
+        if (tid == 0) L.s = s0;                                    // setEstimate(toSE3Quat(mTcw))
+        __syncthreads();
+        const bool robust = it < 3;
+        // ---- optimize(10): OptimizationAlgorithmLevenberg::solve per iteration ----
+        double lambda = 0.0, ni = 2.0;                             // thread 0's copies
+        for (int iter = 0; iter < 10; iter++) {
+            double currentChi = active_chi2(L, b, cm, f, ne, robust, delta);
+            // buildSystem
+            double acc[27];
+            for (int k = 0; k < 27; k++) acc[k] = 0.0;
+            {
+                const Se3 s = L.s;
+                for (int e = tid; e < ne; e += kPT) {
+                    if (!b.active[base + e]) continue;
+                    const PEdge E = load_edge(b, f, e);
+                    double er[3], J[18];
+                    const double c = pq_edge_eval(cm, s, E, er, J);
+                    double r0, rho1 = 1.0;
+                    if (robust) pq_huber(c, delta[E.stereo], r0, rho1);
+                    const double wgt = rho1 * E.w;
+                    int k = 0;
+                    for (int a = 0; a < 6; a++)
+                        for (int bb = a; bb < 6; bb++) {
+                            double c2 = J[a] * J[bb] + J[6 + a] * J[6 + bb];
+                            if (E.stereo) c2 = c2 + J[12 + a] * J[12 + bb];
+                            acc[k++] += wgt * c2;
+                        }
+                    for (int a = 0; a < 6; a++) {
+                        double c1 = J[a] * er[0] + J[6 + a] * er[1];
+                        if (E.stereo) c1 = c1 + J[12 + a] * er[2];
+                        acc[21 + a] += -(wgt * c1);
+                    }
+                }
+            }
+            block_reduce(L, acc, 27);
+            double H[36], bv[6];
+            if (tid == 0) {
+                int k = 0;
+                for (int a = 0; a < 6; a++)
+                    for (int bb = a; bb < 6; bb++) { H[a * 6 + bb] = L.out[k]; H[bb * 6 + a] = L.out[k]; k++; }
+                for (int a = 0; a < 6; a++) bv[a] = L.out[21 + a];
+                if (iter == 0) {
+                    double m = 0.0;
+                    for (int j = 0; j < 6; j++) m = fmax(fabs(H[j * 6 + j]), m);
+                    lambda = 1e-5 * m;
+                    ni = 2.0;
+                }
+                L.qmax = 0;
+            }
+            __syncthreads();
+            Se3 saved;
+            double x[6];
+            int ok2 = 0;
+            for (;;) {
+                if (tid == 0) {
+                    saved = L.s;
+                    double Hl[36];
+                    for (int q = 0; q < 36; q++) Hl[q] = H[q];
+                    for (int j = 0; j < 6; j++) Hl[j * 6 + j] = Hl[j * 6 + j] + lambda;
+                    for (int j = 0; j < 6; j++) x[j] = 0.0;
+                    ok2 = pq_solve6(Hl, bv, x) ? 1 : 0;
+                    if (!ok2) for (int j = 0; j < 6; j++) x[j] = 0.0;
+                    const Se3 up = pq_exp(x);
+                    L.s = pq_mul(up, saved);
+                }
+                __syncthreads();
+                double tempChi = active_chi2(L, b, cm, f, ne, robust, delta);
+                if (tid == 0) {
+                    if (!ok2) tempChi = DBL_MAX;
+                    double scale = 0.0;
+                    for (int j = 0; j < 6; j++) scale = scale + x[j] * (lambda * x[j] + bv[j]);
+                    const double rho = (currentChi - tempChi) / scale;
+                    if (rho > 0 && isfinite(tempChi)) {
+                        const double t2 = 2.0 * rho - 1.0;
+                        double alpha = 1.0 - (t2 * t2) * t2;
+                        alpha = fmin(alpha, 2.0 / 3.0);
+                        const double sf = fmax(1.0 / 3.0, alpha);
+                        lambda = lambda * sf;
+                        ni = 2.0;
+                        currentChi = tempChi;
+                    } else {
+                        lambda = lambda * ni;
+                        ni = ni * 2.0;
+                        L.s = saved;
+                    }
+                    L.qmax = L.qmax + 1;
+                    L.rho = rho;
+                }
+                __syncthreads();
+                const double rho = L.rho;
+                const int qmax = L.qmax;
+                __syncthreads();
+                if (!(rho < 0 && qmax < 10)) break;
+            }
+            const double rho = L.rho;
+            const int qmax = L.qmax;
+            __syncthreads();
+            if (qmax == 10 || rho == 0) break;                     // Terminate
+        }
+        // ---- classification (Optimizer.cc:381-437) ----
+        const Se3 s = L.s;
+        int bad = 0;
+        for (int e = tid; e < ne; e += kPT) {
+            double c = b.chi2[base + e];
+            const PEdge E = load_edge(b, f, e);
+            if (!b.active[base + e]) { double er[3]; c = pq_edge_eval(cm, s, E, er, nullptr); b.chi2[base + e] = c; }
+            const int kp = b.edges[base + e].kp;
+            if (c > chi2th[E.stereo]) { b.outlier[base + kp] = 1; b.active[base + e] = 0; bad++; }
+            else { b.outlier[base + kp] = 0; b.active[base + e] = 1; }
+        }
+        for (int off = 32; off >= 1; off >>= 1) bad += __shfl_xor(bad, off, 64);
+        if (lane == 0) L.nbad[wv] = bad;
+        __syncthreads();
+        nBad = (L.nbad[0] + L.nbad[1]) + (L.nbad[2] + L.nbad[3]);
+        __syncthreads();
+        if (ne < 10) break;                                        // optimizer.edges().size() < 10
+    }
+    if (tid == 0) {
+        pq_to_Tcw(L.s, Tcw);
+        b.result[f] = ne - nBad;
+    }
+}
+
+}  // namespace
+
+int launch_pose(const PoseBufs& b, int F, double fx, double fy, double cx, double cy, double bf, hipStream_t s,
+                ProfileHook* prof)
+{
+    PoseCam cm{fx, fy, cx, cy, bf};
+    prof_begin(prof, "k_pose", s);
+    hipLaunchKernelGGL(k_pose, dim3(F), dim3(kPT), 0, s, b, cm);
+    prof_end(prof, s);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -30,6 +30,9 @@
  *                                      include/ORBmatcher.h:55, src/ORBmatcher.cc:1473-1600
  *                                      (MapPoint::PredictScale  src/MapPoint.cc:402-417), the
  *                                      calls in Tracking::Relocalization  src/Tracking.cc:1531,1545
+ *   coeb_pose_optimization          <- Optimizer::PoseOptimization(Frame*)  include/Optimizer.h:47,
+ *                                      src/Optimizer.cc:239-451 (g2o LM; g2o itself is not vendored,
+ *                                      parity UNPINNED); calls Tracking.cc:841,964,1006
  *   coeb_descriptor_distance        <- ORBmatcher::DescriptorDistance  src/ORBmatcher.cc:1648-1664
  *
  * Conventions: 0 on success, negative COEB_E* code on failure (the reference has no error
@@ -226,6 +229,23 @@ int coeb_match_keyframe(coeb_ctx* ctx, const coeb_camera* cam, const coeb_curfra
                         const uint8_t* cur_has_mappoint, const coeb_keyframe_points* kf,
                         const float Tcw[16], float th, int orb_dist, int check_orientation,
                         int32_t* match_out, int* nmatches);
+
+/* The Frame fields Optimizer::PoseOptimization reads (Optimizer.cc:276-357). */
+typedef struct {
+    int32_t n;                        /* pFrame->N */
+    const uint8_t* has_mappoint;      /* mvpMapPoints[i] != NULL */
+    const float* world_pos;           /* n x 3, GetWorldPos() (read where has_mappoint) */
+    const coeb_keypoint* keys_un;     /* mvKeysUn (pt, octave) */
+    const float* u_right;             /* mvuRight (< 0: monocular edge) */
+} coeb_pose_frame;
+
+/* ---- Optimizer::PoseOptimization(pFrame) ----
+ * Tcw: pFrame->mTcw on entry (row-major 4x4), the optimised pose on return (SetPose).
+ * outlier_out[i] (length n) = mvbOutlier[i], written where has_mappoint[i].  *ninliers = the
+ * return value (nInitialCorrespondences - nBad; 0 and Tcw untouched with < 3 edges).  The
+ * information matrices use the context's mvInvLevelSigma2; cam supplies fx, fy, cx, cy, mbf. */
+int coeb_pose_optimization(coeb_ctx* ctx, const coeb_camera* cam, const coeb_pose_frame* frame, float Tcw[16],
+                           uint8_t* outlier_out, int* ninliers);
 
 /* ---- Frame helpers ---- */
 int coeb_blur_flags(coeb_ctx* ctx, const uint8_t* gray, int width, int height, size_t stride,

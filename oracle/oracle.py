@@ -219,6 +219,29 @@ def search_keyframe(cam, cur_kps, cur_desc, cur_has, kf, Tcw, th=10.0, orb_dist=
     return nm, out[:n]
 
 
+class PoseFrame(C.Structure):
+    _fields_ = [("n", C.c_int), ("has_mp", C.c_void_p), ("xw", C.c_void_p), ("keys_un", C.c_void_p),
+                ("uright", C.c_void_p), ("inv_sigma2", C.c_void_p),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float)]
+
+
+def pose_optimization(kps, has_mp, xw, uright, inv_sigma2, fx, fy, cx, cy, bf, Tcw):
+    """Optimizer::PoseOptimization(Frame*) (Optimizer.cc:239-451), canonical g2o LM.
+    Returns (ninliers, Tcw_out[4,4] f32, outlier[n] u8 (0 where no MapPoint))."""
+    kps = np.ascontiguousarray(kps)
+    n = len(kps)
+    has = np.ascontiguousarray(has_mp, np.uint8)
+    xw = np.ascontiguousarray(xw, np.float32).reshape(n, 3) if n else np.zeros((1, 3), np.float32)
+    ur = np.ascontiguousarray(uright, np.float32)
+    isg = np.ascontiguousarray(inv_sigma2, np.float32)
+    fr = PoseFrame(n, has.ctypes.data, xw.ctypes.data, kps.ctypes.data, ur.ctypes.data, isg.ctypes.data,
+                   fx, fy, cx, cy, bf)
+    T = np.ascontiguousarray(Tcw, np.float32).copy()
+    out = np.zeros(max(n, 1), np.uint8)
+    nin = lib().oc_pose_optimization(C.byref(fr), ptr(T), ptr(out))
+    return nin, T.reshape(4, 4), out[:n]
+
+
 def blur_flags(gray, boxes):
     gray = np.ascontiguousarray(gray, np.uint8)
     boxes = np.ascontiguousarray(boxes, np.float32)

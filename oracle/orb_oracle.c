@@ -11,6 +11,7 @@
  */
 #include "orb_oracle.h"
 
+#include <float.h>
 #include <math.h>
 
 #define OC_PI 3.1415926535897932384626433832795   /* CV_PI */
@@ -1328,4 +1329,413 @@ int oc_search_keyframe(const oc_camera* cam, const oc_curframe* cur, const uint8
     free(g.cell_start);
     free(g.cell_idx);
     return nmatches;
+}
+
+/* ======================= Optimizer::PoseOptimization (canonical g2o) ======================= */
+/* SE3Quat as g2o holds it: unit quaternion (w, x, y, z) and translation, doubles.  Every
+ * operation below has a fixed evaluation order; the HIP kernel (csrc/coeb_pose.hip) performs
+ * the same operations in the same order. */
+typedef struct { double w, x, y, z, t[3]; } oc_se3;
+
+/* Quaterniond(const Matrix3d&) (Eigen quaternionbase_assign_impl) */
+static void pq_from_R(const double R[9], oc_se3* s)
+{
+    double t = (R[0] + R[4]) + R[8];
+    double q[4];                     /* x, y, z, w */
+    if (t > 0.0) {
+        t = sqrt(t + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (R[7] - R[5]) * t;
+        q[1] = (R[2] - R[6]) * t;
+        q[2] = (R[3] - R[1]) * t;
+    } else {
+        int i = 0;
+        if (R[4] > R[0]) i = 1;
+        if (R[8] > R[i * 4]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(((R[i * 4] - R[j * 4]) - R[k * 4]) + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (R[k * 3 + j] - R[j * 3 + k]) * t;
+        q[j] = (R[j * 3 + i] + R[i * 3 + j]) * t;
+        q[k] = (R[k * 3 + i] + R[i * 3 + k]) * t;
+    }
+    s->x = q[0]; s->y = q[1]; s->z = q[2]; s->w = q[3];
+}
+
+/* SE3Quat::normalizeRotation: w >= 0, unit norm */
+static void pq_normalize(oc_se3* s)
+{
+    if (s->w < 0) { s->w = -s->w; s->x = -s->x; s->y = -s->y; s->z = -s->z; }
+    const double n = sqrt(((s->x * s->x + s->y * s->y) + s->z * s->z) + s->w * s->w);
+    s->x = s->x / n; s->y = s->y / n; s->z = s->z / n; s->w = s->w / n;
+}
+
+/* q * v (Eigen _transformVector: uv = 2 q.vec x v; v + w uv + q.vec x uv) */
+static void pq_rotate(const oc_se3* s, const double v[3], double o[3])
+{
+    double uv[3] = {s->y * v[2] - s->z * v[1], s->z * v[0] - s->x * v[2], s->x * v[1] - s->y * v[0]};
+    uv[0] = uv[0] + uv[0]; uv[1] = uv[1] + uv[1]; uv[2] = uv[2] + uv[2];
+    const double c[3] = {s->y * uv[2] - s->z * uv[1], s->z * uv[0] - s->x * uv[2], s->x * uv[1] - s->y * uv[0]};
+    for (int k = 0; k < 3; k++) o[k] = (v[k] + s->w * uv[k]) + c[k];
+}
+
+static void pq_map(const oc_se3* s, const double X[3], double o[3])
+{
+    pq_rotate(s, X, o);
+    for (int k = 0; k < 3; k++) o[k] = o[k] + s->t[k];
+}
+
+/* a * b (SE3Quat::operator*: t = a.t + a.q b.t, q = a.q b.q, normalise) */
+static oc_se3 pq_mul(const oc_se3* a, const oc_se3* b)
+{
+    oc_se3 r;
+    double bt[3];
+    pq_rotate(a, b->t, bt);
+    for (int k = 0; k < 3; k++) r.t[k] = a->t[k] + bt[k];
+    r.w = ((a->w * b->w - a->x * b->x) - a->y * b->y) - a->z * b->z;
+    r.x = ((a->w * b->x + a->x * b->w) + a->y * b->z) - a->z * b->y;
+    r.y = ((a->w * b->y + a->y * b->w) + a->z * b->x) - a->x * b->z;
+    r.z = ((a->w * b->z + a->z * b->w) + a->x * b->y) - a->y * b->x;
+    pq_normalize(&r);
+    return r;
+}
+
+/* canonical sin/cos: Cody-Waite pi/2 reduction, Taylor series to r^27 on
+ * |r| <= pi/4 by Horner; coefficients (-1)^n / (2n+1)! and (-1)^n / (2n)! as double
+ * products of the integers, rounded once (hex literals shared with the HIP twin). */
+static const double kPqSin[14] = {0x1.0000000000000p+0, -0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19, -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49, -0x1.2f49b46814157p-57, 0x1.71b8ef6dcf572p-66, -0x1.761b413163819p-75, 0x1.3f3ccdd165fa9p-84, -0x1.d1ab1c2dccea3p-94};
+static const double kPqCos[14] = {0x1.0000000000000p+0, -0x1.0000000000000p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16, -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45, -0x1.6827863b97d97p-53, 0x1.e542ba4020225p-62, -0x1.0ce396db7f853p-70, 0x1.f2cf01972f578p-80, -0x1.88e85fc6a4e59p-89};
+static void pq_sincos(double x, double* sn, double* cs)
+{
+    const double k = floor(x * 0.63661977236758134308 + 0.5);
+    const double r = (x - k * 1.57079632673412561417e+00) - k * 6.07710050650619224932e-11;
+    const double r2 = r * r;
+    double ps = kPqSin[13], pc = kPqCos[13];
+    for (int n = 12; n >= 0; n--) {
+        ps = ps * r2 + kPqSin[n];
+        pc = pc * r2 + kPqCos[n];
+    }
+    const double s0 = r * ps, c0 = pc;
+    const int q = ((int)(long)k) & 3;
+    if (q == 0) { *sn = s0; *cs = c0; }
+    else if (q == 1) { *sn = c0; *cs = -s0; }
+    else if (q == 2) { *sn = -s0; *cs = -c0; }
+    else { *sn = -c0; *cs = s0; }
+}
+
+/* SE3Quat::exp(update), update = (omega, upsilon) */
+static oc_se3 pq_exp(const double u[6])
+{
+    const double o0 = u[0], o1 = u[1], o2 = u[2];
+    const double theta = sqrt((o0 * o0 + o1 * o1) + o2 * o2);
+    const double Om[9] = {0.0, -o2, o1, o2, 0.0, -o0, -o1, o0, 0.0};
+    double Om2[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            Om2[i * 3 + j] = (Om[i * 3] * Om[j] + Om[i * 3 + 1] * Om[3 + j]) + Om[i * 3 + 2] * Om[6 + j];
+    double R[9], V[9];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) R[i] = ((i % 4 == 0 ? 1.0 : 0.0) + Om[i]) + Om2[i];
+        for (int i = 0; i < 9; i++) V[i] = R[i];
+    } else {
+        double sn, cs;
+        pq_sincos(theta, &sn, &cs);
+        const double th2 = theta * theta;
+        const double A = sn / theta, B = (1.0 - cs) / th2, Cc = (theta - sn) / (th2 * theta);
+        for (int i = 0; i < 9; i++) {
+            const double I = i % 4 == 0 ? 1.0 : 0.0;
+            R[i] = (I + A * Om[i]) + B * Om2[i];
+            V[i] = (I + B * Om[i]) + Cc * Om2[i];
+        }
+    }
+    oc_se3 s;
+    pq_from_R(R, &s);
+    for (int i = 0; i < 3; i++) s.t[i] = (V[i * 3] * u[3] + V[i * 3 + 1] * u[4]) + V[i * 3 + 2] * u[5];
+    pq_normalize(&s);
+    return s;
+}
+
+/* Converter::toSE3Quat(cv::Mat float) */
+static oc_se3 pq_from_Tcw(const float T[16])
+{
+    double R[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) R[i * 3 + j] = (double)T[i * 4 + j];
+    oc_se3 s;
+    pq_from_R(R, &s);
+    for (int i = 0; i < 3; i++) s.t[i] = (double)T[i * 4 + 3];
+    pq_normalize(&s);
+    return s;
+}
+
+/* Converter::toCvMat(SE3Quat): to_homogeneous_matrix (Eigen toRotationMatrix), cast to float */
+static void pq_to_Tcw(const oc_se3* s, float T[16])
+{
+    const double tx = 2.0 * s->x, ty = 2.0 * s->y, tz = 2.0 * s->z;
+    const double twx = tx * s->w, twy = ty * s->w, twz = tz * s->w;
+    const double txx = tx * s->x, txy = ty * s->x, txz = tz * s->x;
+    const double tyy = ty * s->y, tyz = tz * s->y, tzz = tz * s->z;
+    const double R[9] = {1.0 - (tyy + tzz), txy - twz, txz + twy,
+                         txy + twz, 1.0 - (txx + tzz), tyz - twx,
+                         txz - twy, tyz + twx, 1.0 - (txx + tyy)};
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) T[i * 4 + j] = (float)R[i * 3 + j];
+        T[i * 4 + 3] = (float)s->t[i];
+    }
+    T[12] = 0.f; T[13] = 0.f; T[14] = 0.f; T[15] = 1.f;
+}
+
+/* One edge at pose s: error e (2 or 3), raw chi2 = e' Omega e (EdgeSE3ProjectXYZOnlyPose /
+ * EdgeStereoSE3ProjectXYZOnlyPose::computeError, ORB-SLAM2 types_six_dof_expmap.cpp); J (the
+ * error Jacobian linearizeOplus, rows 6 wide) when J != NULL. */
+typedef struct { double X[3], obs[3], w; int stereo; } pq_edge;
+
+static double pq_edge_eval(const oc_pose_frame* fr, const oc_se3* s, const pq_edge* E, double e[3], double* J)
+{
+    double p[3];
+    pq_map(s, E->X, p);
+    const double fx = fr->fx, fy = fr->fy, cx = fr->cx, cy = fr->cy, bf = fr->bf;
+    if (!E->stereo) {
+        const double u = (p[0] / p[2]) * fx + cx, v = (p[1] / p[2]) * fy + cy;   /* project2d, cam_project */
+        e[0] = E->obs[0] - u; e[1] = E->obs[1] - v; e[2] = 0.0;
+    } else {
+        const float invzf = 1.0f / (float)p[2];                  /* const float invz = 1.0f/z */
+        const double u = (p[0] * (double)invzf) * fx + cx, v = (p[1] * (double)invzf) * fy + cy;
+        const double ur = u - bf * (double)invzf;
+        e[0] = E->obs[0] - u; e[1] = E->obs[1] - v; e[2] = E->obs[2] - ur;
+    }
+    if (J) {
+        const double x = p[0], y = p[1], invz = 1.0 / p[2], invz_2 = invz * invz;
+        J[0] = ((x * y) * invz_2) * fx;
+        J[1] = -(1.0 + ((x * x) * invz_2)) * fx;
+        J[2] = (y * invz) * fx;
+        J[3] = -invz * fx;
+        J[4] = 0.0;
+        J[5] = (x * invz_2) * fx;
+        J[6] = (1.0 + ((y * y) * invz_2)) * fy;
+        J[7] = -((x * y) * invz_2) * fy;
+        J[8] = -(x * invz) * fy;
+        J[9] = 0.0;
+        J[10] = -invz * fy;
+        J[11] = (y * invz_2) * fy;
+        if (E->stereo) {
+            J[12] = J[0] - (bf * y) * invz_2;
+            J[13] = J[1] + (bf * x) * invz_2;
+            J[14] = J[2];
+            J[15] = J[3];
+            J[16] = 0.0;
+            J[17] = J[5] - bf * invz_2;
+        }
+    }
+    double c = e[0] * (E->w * e[0]) + e[1] * (E->w * e[1]);
+    if (E->stereo) c = c + e[2] * (E->w * e[2]);
+    return c;
+}
+
+/* RobustKernelHuber::robustify */
+static void pq_huber(double e2, double delta, double rho[2])
+{
+    const double dsqr = delta * delta;
+    if (e2 <= dsqr) { rho[0] = e2; rho[1] = 1.0; }
+    else {
+        const double sq = sqrt(e2);
+        rho[0] = (2.0 * sq) * delta - dsqr;
+        rho[1] = delta / sq;
+    }
+}
+
+/* The fixed reduction of per-edge terms: edge i -> lane i % 256 (sequential in i), then
+ * within each 64-lane wave a xor butterfly (32, 16, .., 1), then (w0 + w1) + (w2 + w3). */
+enum { PQ_LANES = 256, PQ_NV = 28 };
+static void pq_reduce(double lanes[PQ_LANES][PQ_NV], int nv, double out[PQ_NV])
+{
+    static double tmp[PQ_LANES][PQ_NV];
+    for (int off = 32; off >= 1; off >>= 1) {
+        for (int l = 0; l < PQ_LANES; l++)
+            for (int k = 0; k < nv; k++) tmp[l][k] = lanes[l][k] + lanes[(l & ~63) | ((l & 63) ^ off)][k];
+        for (int l = 0; l < PQ_LANES; l++)
+            for (int k = 0; k < nv; k++) lanes[l][k] = tmp[l][k];
+    }
+    for (int k = 0; k < nv; k++) out[k] = (lanes[0][k] + lanes[64][k]) + (lanes[128][k] + lanes[192][k]);
+}
+
+/* LDL' of the 6x6 (no pivoting; fails unless every pivot > 0), then solve */
+static int pq_solve6(const double H[36], const double b[6], double x[6])
+{
+    double L[36] = {0}, d[6], y[6];
+    for (int j = 0; j < 6; j++) {
+        double v = H[j * 6 + j];
+        for (int k = 0; k < j; k++) v = v - (L[j * 6 + k] * L[j * 6 + k]) * d[k];
+        if (!(v > 0.0)) return 0;
+        d[j] = v;
+        for (int i = j + 1; i < 6; i++) {
+            double w = H[i * 6 + j];
+            for (int k = 0; k < j; k++) w = w - (L[i * 6 + k] * L[j * 6 + k]) * d[k];
+            L[i * 6 + j] = w / d[j];
+        }
+    }
+    for (int i = 0; i < 6; i++) {
+        double v = b[i];
+        for (int k = 0; k < i; k++) v = v - L[i * 6 + k] * y[k];
+        y[i] = v;
+    }
+    for (int i = 0; i < 6; i++) y[i] = y[i] / d[i];
+    for (int i = 5; i >= 0; i--) {
+        double v = y[i];
+        for (int k = i + 1; k < 6; k++) v = v - L[k * 6 + i] * x[k];
+        x[i] = v;
+    }
+    return 1;
+}
+
+/* robust chi2 of the active edges at s (SparseOptimizer::computeActiveErrors +
+ * activeRobustChi2); stores every active edge's raw chi2 in chi2_last */
+static double pq_active_chi2(const oc_pose_frame* fr, const oc_se3* s, const pq_edge* E, int ne, const uint8_t* active,
+                             int robust, const double* delta, double* chi2_last)
+{
+    static double lanes[PQ_LANES][PQ_NV];
+    memset(lanes, 0, sizeof(lanes));
+    for (int i = 0; i < ne; i++) {
+        if (!active[i]) continue;
+        double e[3];
+        const double c = pq_edge_eval(fr, s, &E[i], e, NULL);
+        chi2_last[i] = c;
+        double r = c;
+        if (robust) { double rho[2]; pq_huber(c, delta[E[i].stereo], rho); r = rho[0]; }
+        lanes[i % PQ_LANES][0] += r;
+    }
+    double out[PQ_NV];
+    pq_reduce(lanes, 1, out);
+    return out[0];
+}
+
+/* one SparseOptimizer::optimize(10) with OptimizationAlgorithmLevenberg (g2o 2012) */
+static void pq_optimize(const oc_pose_frame* fr, oc_se3* s, const pq_edge* E, int ne, const uint8_t* active, int robust,
+                        const double* delta, double* chi2_last, int iterations)
+{
+    static double lanes[PQ_LANES][PQ_NV];
+    double lambda = 0.0, ni = 2.0;
+    for (int it = 0; it < iterations; it++) {
+        /* computeActiveErrors, activeRobustChi2, buildSystem (H = sum J' w rho1 J, b = -sum J' w rho1 e) */
+        double currentChi = pq_active_chi2(fr, s, E, ne, active, robust, delta, chi2_last);
+        memset(lanes, 0, sizeof(lanes));
+        for (int i = 0; i < ne; i++) {
+            if (!active[i]) continue;
+            double e[3], J[18];
+            const double c = pq_edge_eval(fr, s, &E[i], e, J);
+            double rho1 = 1.0;
+            if (robust) { double rho[2]; pq_huber(c, delta[E[i].stereo], rho); rho1 = rho[1]; }
+            const double wgt = rho1 * E[i].w;
+            const int nr = E[i].stereo ? 3 : 2;
+            double* L = lanes[i % PQ_LANES];
+            int k = 0;
+            for (int a = 0; a < 6; a++)
+                for (int bb = a; bb < 6; bb++) {
+                    double c2 = J[a] * J[bb] + J[6 + a] * J[6 + bb];
+                    if (nr == 3) c2 = c2 + J[12 + a] * J[12 + bb];
+                    L[k++] += wgt * c2;
+                }
+            for (int a = 0; a < 6; a++) {
+                double c1 = J[a] * e[0] + J[6 + a] * e[1];
+                if (nr == 3) c1 = c1 + J[12 + a] * e[2];
+                L[21 + a] += -(wgt * c1);
+            }
+        }
+        double red[PQ_NV];
+        pq_reduce(lanes, 27, red);
+        double H[36], b[6];
+        {
+            int k = 0;
+            for (int a = 0; a < 6; a++)
+                for (int bb = a; bb < 6; bb++) { H[a * 6 + bb] = red[k]; H[bb * 6 + a] = red[k]; k++; }
+            for (int a = 0; a < 6; a++) b[a] = red[21 + a];
+        }
+        if (it == 0) {                                   /* computeLambdaInit: tau * max |H_jj| */
+            double m = 0.0;
+            for (int j = 0; j < 6; j++) m = fmax(fabs(H[j * 6 + j]), m);
+            lambda = 1e-5 * m;
+            ni = 2.0;
+        }
+        double rho = 0.0;
+        int qmax = 0;
+        do {
+            const oc_se3 saved = *s;                     /* push */
+            double Hl[36], x[6] = {0, 0, 0, 0, 0, 0};
+            memcpy(Hl, H, sizeof(Hl));
+            for (int j = 0; j < 6; j++) Hl[j * 6 + j] = Hl[j * 6 + j] + lambda;
+            const int ok2 = pq_solve6(Hl, b, x);
+            if (!ok2) for (int j = 0; j < 6; j++) x[j] = 0.0;
+            const oc_se3 up = pq_exp(x);                 /* VertexSE3Expmap::oplusImpl */
+            *s = pq_mul(&up, s);
+            double tempChi = pq_active_chi2(fr, s, E, ne, active, robust, delta, chi2_last);
+            if (!ok2) tempChi = DBL_MAX;
+            double scale = 0.0;                          /* computeScale */
+            for (int j = 0; j < 6; j++) scale = scale + x[j] * (lambda * x[j] + b[j]);
+            rho = (currentChi - tempChi) / scale;
+            if (rho > 0 && isfinite(tempChi)) {
+                const double t2 = 2.0 * rho - 1.0;
+                double alpha = 1.0 - (t2 * t2) * t2;
+                alpha = fmin(alpha, 2.0 / 3.0);
+                const double sf = fmax(1.0 / 3.0, alpha);
+                lambda = lambda * sf;
+                ni = 2.0;
+                currentChi = tempChi;
+            } else {
+                lambda = lambda * ni;
+                ni = ni * 2.0;
+                *s = saved;                              /* pop */
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10);
+        if (qmax == 10 || rho == 0) break;               /* Terminate */
+    }
+}
+
+int oc_pose_optimization(const oc_pose_frame* fr, float Tcw[16], uint8_t* outlier)
+{
+    const int n = fr->n;
+    pq_edge* E = (pq_edge*)malloc(sizeof(pq_edge) * (n > 0 ? n : 1));
+    int* idx = (int*)malloc(sizeof(int) * (n > 0 ? n : 1));
+    int ne = 0;
+    for (int i = 0; i < n; i++) {
+        if (!fr->has_mp[i]) continue;
+        pq_edge* e = &E[ne];
+        for (int k = 0; k < 3; k++) e->X[k] = (double)fr->xw[3 * i + k];
+        e->obs[0] = (double)fr->keys_un[i].x;
+        e->obs[1] = (double)fr->keys_un[i].y;
+        e->stereo = !(fr->uright[i] < 0);                /* Optimizer.cc:287 */
+        e->obs[2] = e->stereo ? (double)fr->uright[i] : 0.0;
+        e->w = (double)fr->inv_sigma2[fr->keys_un[i].octave];
+        outlier[i] = 0;
+        idx[ne++] = i;
+    }
+    if (ne < 3) { free(E); free(idx); return 0; }
+    const float deltaMono = (float)sqrt(5.991), deltaStereo = (float)sqrt(7.815);
+    const double delta[2] = {(double)deltaMono, (double)deltaStereo};
+    const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
+    uint8_t* active = (uint8_t*)malloc(ne);
+    double* chi2_last = (double*)malloc(sizeof(double) * ne);
+    for (int i = 0; i < ne; i++) { active[i] = 1; chi2_last[i] = 0.0; }
+    const oc_se3 s0 = pq_from_Tcw(Tcw);
+    oc_se3 s = s0;
+    int nBad = 0;
+    for (int it = 0; it < 4; it++) {
+        s = s0;                                          /* setEstimate(toSE3Quat(pFrame->mTcw)) */
+        const int robust = it < 3;                       /* setRobustKernel(0) after round 2 */
+        pq_optimize(fr, &s, E, ne, active, robust, delta, chi2_last, 10);
+        nBad = 0;
+        for (int i = 0; i < ne; i++) {
+            double c = chi2_last[i];
+            if (!active[i]) { double e[3]; c = pq_edge_eval(fr, &s, &E[i], e, NULL); chi2_last[i] = c; }
+            const double th = E[i].stereo ? (double)chi2Stereo : (double)chi2Mono;
+            if (c > th) { outlier[idx[i]] = 1; active[i] = 0; nBad++; }
+            else { outlier[idx[i]] = 0; active[i] = 1; }
+        }
+        if (ne < 10) break;                              /* optimizer.edges().size() < 10 */
+    }
+    pq_to_Tcw(&s, Tcw);
+    free(active); free(chi2_last); free(E); free(idx);
+    return ne - nBad;
 }

@@ -185,6 +185,25 @@ int oc_search_keyframe(const oc_camera* cam, const oc_curframe* cur, const uint8
                        const oc_kfpoints* kf, const float Tcw[16], float th, int orb_dist, int check_ori,
                        int32_t* match_out);
 
+/* Optimizer::PoseOptimization(Frame*) (Optimizer.cc:239-451): the frame's matched keypoints
+ * and their map points.  fx..bf are the Frame's intrinsics. */
+typedef struct {
+    int n;
+    const uint8_t* has_mp;         /* mvpMapPoints[i] != NULL */
+    const float* xw;               /* n x 3 GetWorldPos() */
+    const oc_kp* keys_un;          /* mvKeysUn (pt, octave) */
+    const float* uright;           /* mvuRight (< 0: monocular edge) */
+    const float* inv_sigma2;       /* mvInvLevelSigma2 */
+    float fx, fy, cx, cy, bf;
+} oc_pose_frame;
+
+/* Returns nInitialCorrespondences - nBad (0 with < 3 correspondences, pose untouched);
+ * Tcw (row-major 4x4) is replaced by the optimised pose; outlier[i] = mvbOutlier[i]
+ * (written only where has_mp[i]).  Canonical restatement of g2o's Levenberg-Marquardt
+ * (OptimizationAlgorithmLevenberg, 2012 release vendored by ORB-SLAM2) with the per-edge
+ * sums reduced over 256 lanes in a fixed tree: parity vs g2o UNPINNED. */
+int oc_pose_optimization(const oc_pose_frame* fr, float Tcw[16], uint8_t* outlier);
+
 #ifdef __cplusplus
 }
 #endif

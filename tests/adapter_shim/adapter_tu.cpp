@@ -2,6 +2,7 @@
 // (include/Frame.h:142-215, include/MapPoint.h:46-75 member names and types).
 #include "ORBextractor.h"
 #include "ORBmatcher_coeb.h"
+#include "Optimizer_coeb.h"
 
 struct MapPoint {
     cv::Mat GetWorldPos() { return cv::Mat(); }
@@ -14,7 +15,9 @@ struct MapPoint {
     float mTrackViewCos = 0;
     float GetMaxDistance() { return 0; }   // the two getters INTEGRATION.md s3 adds
     float GetMinDistance() { return 0; }
+    static std::mutex mGlobalMutex;
 };
+std::mutex MapPoint::mGlobalMutex;
 struct KeyFrame {
     std::vector<MapPoint*> GetMapPointMatches() { return {}; }
     std::vector<cv::KeyPoint> mvKeysUn;
@@ -30,6 +33,7 @@ struct Frame {
     std::vector<MapPoint*> mvpMapPoints;
     std::vector<bool> mvbOutlier;
     cv::Mat mDescriptors, mTcw;
+    void SetPose(cv::Mat Tcw) { mTcw = Tcw; }
 };
 float Frame::fx, Frame::fy, Frame::cx, Frame::cy, Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY, Frame::mnMaxY;
 
@@ -45,5 +49,6 @@ int use_adapters(Frame& cur, const Frame& last, cv::Mat& im)
     std::vector<MapPoint*> local;
     return coeb::SearchByProjectionLastFrame(cur, last, 15.0f, false, 0.9f, true) + ex.GetLevels() +
            coeb::SearchByProjectionLocalMap(cur, local, 3.0f, 0.8f) +
-           coeb::SearchByProjectionKeyFrame(cur, (KeyFrame*)nullptr, std::set<MapPoint*>(), 10.0f, 100, true);
+           coeb::SearchByProjectionKeyFrame(cur, (KeyFrame*)nullptr, std::set<MapPoint*>(), 10.0f, 100, true) +
+           coeb::PoseOptimization(&cur);
 }

@@ -7,6 +7,7 @@
 #include <vector>
 #define CV_8U 0
 #define CV_8UC1 0
+#define CV_32F 5
 namespace cv {
 struct Point2f { float x, y; };
 struct Point2i { int x, y; };
@@ -25,6 +26,7 @@ struct Mat {
     void copyTo(const Mat&) const {}
     template <class T> T& at(int) { return *reinterpret_cast<T*>(data); }
     template <class T> const T& at(int, int) const { return *reinterpret_cast<const T*>(data); }
+    template <class T> T& at(int, int) { return *reinterpret_cast<T*>(data); }
     template <class T> T* ptr(int) { return reinterpret_cast<T*>(data); }
     template <class T> const T* ptr(int) const { return reinterpret_cast<const T*>(data); }
 };

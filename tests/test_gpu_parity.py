@@ -558,3 +558,41 @@ def test_keyframe_paths_and_edges(ctx, oracle_mod, ex, pair, monkeypatch):
     with pytest.raises(ValueError):
         coeb_front.KeyFramePoints(kf["valid"], kf["world_pos"], kf["descriptor"], kf["max_distance"],
                                   kf["min_distance"], kf["angle"][:-1])
+
+
+# ------------------------------------------------------------------ Optimizer::PoseOptimization
+def pose_both(ctx, oracle_mod, P, cam=None):
+    """coeb_pose_optimization vs oracle.pose_optimization: pose bits, outlier flags and the
+    inlier count identical (same canonical operations and reduction order)."""
+    import coeb_front
+    isg = np.array(ctx.tables().inv_sigma2[:8], np.float32)
+    nin_ref, T_ref, out_ref = oracle_mod.pose_optimization(P["kps"], P["has_mp"], P["xw"], P["ur"], isg,
+                                                           synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY,
+                                                           synth.TUM_BF, P["Tcw_init"])
+    cam = cam or coeb_front.make_camera(synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF, 640, 480)
+    F = coeb_front.Frame(P["kps"], np.zeros((len(P["kps"]), 32), np.uint8), P["ur"], Tcw=P["Tcw_init"])
+    F.mvpMapPoints = np.where(P["has_mp"] > 0, 0, -1).astype(np.int32)
+    F.mvMapPointPos = P["xw"]
+    nin = coeb_front.Optimizer.PoseOptimization(F, cam, ctx)
+    assert nin == nin_ref, (nin, nin_ref)
+    assert np.array_equal(F.mTcw.view(np.uint32), T_ref.view(np.uint32)), (F.mTcw, T_ref)
+    has = P["has_mp"] > 0
+    assert np.array_equal(F.mvbOutlier[has], out_ref[has])
+    return nin
+
+
+@pytest.mark.parametrize("seed,kw", [(0, {}), (1, {"outlier_frac": 0.4}), (2, {"mono_frac": 1.0}),
+                                     (3, {"mono_frac": 0.0, "n": 1500}), (4, {"noise": 3.0}),
+                                     (5, {"init_err": (0.15, 0.3)})])
+def test_pose_optimization_matches_oracle(ctx, oracle_mod, seed, kw):
+    P = synth.make_pose_problem(seed=seed, **kw)
+    assert pose_both(ctx, oracle_mod, P) > 0
+
+
+def test_pose_optimization_edges(ctx, oracle_mod):
+    P = synth.make_pose_problem(n=40, seed=9)
+    for k in (0, 2, 5, 9, 12):                       # < 3 (untouched), < 10 (one round), >= 10
+        Q = dict(P)
+        Q["has_mp"] = np.zeros_like(P["has_mp"])
+        Q["has_mp"][:k] = 1
+        pose_both(ctx, oracle_mod, Q)

@@ -412,3 +412,42 @@ def test_search_keyframe_oracle_vs_python(oracle_mod, seed):
         nm_py, mt_py = _py_search_keyframe(cam, kps, desc, has, kf, T, th, od, ori)
         assert nm == nm_py and np.array_equal(mt, mt_py), (nm, nm_py)
         assert nm > 0
+
+
+# ---- Optimizer::PoseOptimization oracle: properties (g2o absent: parity vs g2o unpinned) ----
+def _inv_sigma2(nlevels=8, sf=1.2):
+    s = [np.float32(1.0)]
+    for _ in range(1, nlevels):
+        s.append(np.float32(np.float64(s[-1]) * sf))
+    return np.array([np.float32(1.0) / np.float32(x * x) for x in s], np.float32)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_pose_optimization_oracle_recovers_pose(oracle_mod, seed):
+    from coeb_front import synth
+    P = synth.make_pose_problem(seed=seed)
+    nin, T, outl = oracle_mod.pose_optimization(P["kps"], P["has_mp"], P["xw"], P["ur"], _inv_sigma2(),
+                                                535.4, 539.2, 320.1, 247.6, 40.0, P["Tcw_init"])
+    Tt = P["Tcw_true"].astype(np.float64)
+    dR = T[:3, :3].astype(np.float64) @ Tt[:3, :3].T
+    ang = np.arccos(np.clip((np.trace(dR) - 1) / 2, -1, 1))
+    assert ang < 2e-3 and np.linalg.norm(T[:3, 3] - Tt[:3, 3]) < 5e-3, (ang, T[:3, 3], Tt[:3, 3])
+    has = P["has_mp"] > 0
+    gross = P["gross"] & has
+    assert outl[gross].mean() > 0.9                 # gross outliers classified
+    assert outl[has & ~P["gross"]].mean() < 0.1     # inliers kept
+    assert nin == int(has.sum() - outl[has].sum())
+
+
+def test_pose_optimization_oracle_edge_cases(oracle_mod):
+    from coeb_front import synth
+    P = synth.make_pose_problem(n=40, seed=5)
+    has = np.zeros_like(P["has_mp"])
+    has[:2] = 1                                     # < 3 correspondences: pose untouched, 0
+    nin, T, outl = oracle_mod.pose_optimization(P["kps"], has, P["xw"], P["ur"], _inv_sigma2(),
+                                                535.4, 539.2, 320.1, 247.6, 40.0, P["Tcw_init"])
+    assert nin == 0 and np.array_equal(T, P["Tcw_init"])
+    has[:8] = 1                                     # < 10 edges: a single round
+    nin, T, outl = oracle_mod.pose_optimization(P["kps"], has, P["xw"], P["ur"], _inv_sigma2(),
+                                                535.4, 539.2, 320.1, 247.6, 40.0, P["Tcw_init"])
+    assert 0 < nin <= 8
