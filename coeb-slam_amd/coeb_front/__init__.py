@@ -45,7 +45,8 @@ ABI_SYMBOLS = [
     "coeb_rgbd_preprocess", "coeb_descriptor_distance", "coeb_profile_enable", "coeb_profile_read",
     "coeb_profile_reset", "coeb_synchronize", "coeb_device_count", "coeb_debug_read",
     "coeb_device_alloc", "coeb_device_free", "coeb_memcpy_h2d", "coeb_memcpy_d2h", "coeb_set_batch_streams",
-    "coeb_match_localmap", "coeb_match_keyframe", "coeb_pose_optimization",
+    "coeb_match_localmap", "coeb_match_keyframe", "coeb_pose_optimization", "coeb_undistort_keypoints",
+    "coeb_boxes_from_int64",
 ]
 
 
@@ -134,6 +135,9 @@ def lib():
                                           C.c_void_p, C.POINTER(C.c_int)]
         L.coeb_pose_optimization.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(PoseFrameC), C.c_void_p,
                                              C.c_void_p, C.POINTER(C.c_int)]
+        L.coeb_undistort_keypoints.argtypes = [C.c_void_p, C.POINTER(Camera), C.c_void_p, C.c_void_p, C.c_int,
+                                               C.c_void_p]
+        L.coeb_boxes_from_int64.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         L.coeb_blur_flags.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_int,
                                       C.c_void_p]
         L.coeb_stereo_from_rgbd.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
@@ -342,6 +346,27 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+def UndistortKeyPoints(ctx, keys, camera, dist):
+    """Frame::UndistortKeyPoints (Frame.cc:579-609): mvKeysUn from mvKeys; dist = mDistCoef
+    (k1, k2, p1, p2[, k3])."""
+    keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    d = np.zeros(5, np.float32)
+    d[:len(dist)] = np.asarray(dist, np.float32)
+    out = keys.copy()
+    ctx.check(lib().coeb_undistort_keypoints(ctx.h, C.byref(camera), _p(d), _p(keys), len(keys), _p(out)))
+    return out
+
+
+def boxes_from_ros(xyxy):
+    """yolov5_ros_msgs/BoundingBoxes (int64 xmin, ymin, xmax, ymax rows) -> float32 [n, 4] as
+    ros_rgbd.cc:106-115 builds them."""
+    a = np.ascontiguousarray(np.asarray(xyxy, np.int64).reshape(-1, 4))
+    out = np.zeros((len(a), 4), np.float32)
+    if len(a) and lib().coeb_boxes_from_int64(_p(a), len(a), _p(out)) != 0:
+        raise CoebError("coeb_boxes_from_int64 failed")
+    return out
 
 
 class ORBextractor:

@@ -4,6 +4,8 @@
 //                                                                       src/Tracking.cc:207-228
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include <string>
 #include <vector>
 
@@ -68,6 +70,35 @@ __global__ __launch_bounds__(256) void k_rgbd(const uint8_t* __restrict__ rgb, i
         gray[(int64_t)y * W + x] = (uint8_t)((v + (1 << 13)) >> 14);
     }
     if (d16) depth[(int64_t)y * W + x] = (float)d16[(int64_t)y * dstride + x] * dscale;
+}
+
+// Frame::UndistortKeyPoints (Frame.cc:579-609): cv::undistortPoints(.., mK, mDistCoef, Mat(), mK)
+// of OpenCV 3.4 (cvUndistortPointsInternal, 5 fixed iterations), one thread per keypoint, in
+// double with the oracle's operation order.  k = (k1, k2, p1, p2, k3); the remaining rational /
+// thin-prism terms of the 14-coefficient model are zero and kept so the sums match.
+struct KpRec { float x, y, size, angle, response; int octave, class_id; };
+struct DistK { double k[12]; double fx, fy, cx, cy; };
+
+__global__ __launch_bounds__(256) void k_undistort(const KpRec* __restrict__ in, int n, DistK d, KpRec* __restrict__ out)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    KpRec kp = in[i];
+    const double* k = d.k;
+    const double ifx = 1. / d.fx, ify = 1. / d.fy;
+    double x = ((double)kp.x - d.cx) * ifx, y = ((double)kp.y - d.cy) * ify;
+    const double x0 = x, y0 = y;
+    for (int j = 0; j < 5; j++) {
+        const double r2 = x * x + y * y;
+        const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+        const double deltaX = ((((2 * k[2]) * x) * y + k[3] * (r2 + (2 * x) * x)) + k[8] * r2) + (k[9] * r2) * r2;
+        const double deltaY = ((k[2] * (r2 + (2 * y) * y) + ((2 * k[3]) * x) * y) + k[10] * r2) + (k[11] * r2) * r2;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    kp.x = (float)(d.fx * x + d.cx);
+    kp.y = (float)(d.fy * y + d.cy);
+    out[i] = kp;
 }
 
 }  // namespace
@@ -142,5 +173,49 @@ extern "C" int coeb_rgbd_preprocess(coeb_ctx* c, const uint8_t* rgb, size_t rgb_
     if (rgb) FR_TRY(c, hipMemcpyAsync(gray_out, dgray, (size_t)W * H, hipMemcpyDeviceToHost, s));
     if (depth16) FR_TRY(c, hipMemcpyAsync(depth_out, ddep, (size_t)W * H * 4, hipMemcpyDeviceToHost, s));
     FR_TRY(c, hipStreamSynchronize(s));
+    return COEB_OK;
+}
+
+extern "C" int coeb_undistort_keypoints(coeb_ctx* c, const coeb_camera* cam, const float dist[5], const coeb_keypoint* kps,
+                                        int n, coeb_keypoint* out)
+{
+    if (!c || !cam || !dist || n < 0 || (n > 0 && (!kps || !out)))
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_undistort_keypoints: invalid arguments");
+    if (n == 0) return COEB_OK;
+    if (dist[0] == 0.0f) {                                           // Frame.cc:581-585
+        if (out != kps) memmove(out, kps, (size_t)n * sizeof(coeb_keypoint));
+        return COEB_OK;
+    }
+    hipStream_t s;
+    int dev;
+    if (coeb_internal_stream(c, &s, &dev)) return COEB_EINVAL;
+    (void)hipSetDevice(dev);
+    void *din, *dout;
+    int rc;
+    if ((rc = coeb_internal_scratch(c, "ud_in", (size_t)n * sizeof(coeb_keypoint), &din)) ||
+        (rc = coeb_internal_scratch(c, "ud_out", (size_t)n * sizeof(coeb_keypoint), &dout)))
+        return rc;
+    DistK d;
+    for (int q = 0; q < 12; q++) d.k[q] = q < 5 ? (double)dist[q] : 0.0;
+    d.fx = cam->fx; d.fy = cam->fy; d.cx = cam->cx; d.cy = cam->cy;
+    FR_TRY(c, hipMemcpyAsync(din, kps, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_undistort, dim3((n + 255) / 256), dim3(256), 0, s, (const KpRec*)din, n, d, (KpRec*)dout);
+    FR_TRY(c, hipGetLastError());
+    FR_TRY(c, hipMemcpyAsync(out, dout, (size_t)n * sizeof(coeb_keypoint), hipMemcpyDeviceToHost, s));
+    FR_TRY(c, hipStreamSynchronize(s));
+    return COEB_OK;
+}
+
+// yolov5_ros_msgs/BoundingBox int64 xmin, ymin, xmax, ymax -> the float boxes GrabRGBD builds
+// (ros_rgbd.cc:106-115: push_back of int64 into std::vector<float>, i.e. static_cast<float>)
+extern "C" int coeb_boxes_from_int64(const int64_t* xyxy, int nbox, coeb_box* out)
+{
+    if (nbox < 0 || (nbox > 0 && (!xyxy || !out))) return COEB_EINVAL;
+    for (int i = 0; i < nbox; i++) {
+        out[i].xmin = (float)xyxy[4 * i + 0];
+        out[i].ymin = (float)xyxy[4 * i + 1];
+        out[i].xmax = (float)xyxy[4 * i + 2];
+        out[i].ymax = (float)xyxy[4 * i + 3];
+    }
     return COEB_OK;
 }

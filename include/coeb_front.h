@@ -15,6 +15,9 @@
  *                                      src/Frame.cc:171-202, 905-913
  *   coeb_rgbd_preprocess            <- Tracking::GrabImageRGBD cvtColor / depth convertTo
  *                                      src/Tracking.cc:207-228
+ *   coeb_undistort_keypoints        <- Frame::UndistortKeyPoints  src/Frame.cc:579-609
+ *   coeb_boxes_from_int64           <- ImageGrabber::GrabRGBD box copy
+ *                                      Examples/ROS/ORB-SLAM2/src/ros_rgbd.cc:106-115
  *   coeb_stereo_from_rgbd           <- Frame::ComputeStereoFromRGBD  src/Frame.cc:820-842
  *   coeb_match_lastframe            <- ORBmatcher::SearchByProjection(Frame&, const Frame&,
  *                                      const float th, const bool bMono)
@@ -258,6 +261,14 @@ int coeb_stereo_from_rgbd(coeb_ctx* ctx, const coeb_keypoint* kps, int n, const 
 int coeb_rgbd_preprocess(coeb_ctx* ctx, const uint8_t* rgb, size_t rgb_stride, int rgb_order,
                          const uint16_t* depth16, size_t depth_stride, float depth_scale,
                          int width, int height, uint8_t* gray_out, float* depth_out);
+
+/* mvKeysUn from mvKeys: cv::undistortPoints(.., mK, mDistCoef, Mat(), mK) (OpenCV 3.4, 5
+ * iterations) with dist = (k1, k2, p1, p2, k3) (k3 = 0 for a 4-coefficient mDistCoef);
+ * dist[0] == 0 copies (Frame.cc:581-585).  out may equal kps. */
+int coeb_undistort_keypoints(coeb_ctx* ctx, const coeb_camera* cam, const float dist[5], const coeb_keypoint* kps,
+                             int n, coeb_keypoint* out);
+/* yolov5_ros_msgs/BoundingBox (int64 xmin, ymin, xmax, ymax) -> coeb_box, as GrabRGBD converts */
+int coeb_boxes_from_int64(const int64_t* xyxy, int nbox, coeb_box* out);
 
 int coeb_descriptor_distance(const uint8_t* a, const uint8_t* b);
 

@@ -242,6 +242,16 @@ def pose_optimization(kps, has_mp, xw, uright, inv_sigma2, fx, fy, cx, cy, bf, T
     return nin, T.reshape(4, 4), out[:n]
 
 
+def undistort_keypoints(kps, fx, fy, cx, cy, dist):
+    """Frame::UndistortKeyPoints (Frame.cc:579-609); dist = (k1, k2, p1, p2, k3)."""
+    kps = np.ascontiguousarray(kps)
+    out = kps.copy()
+    d = np.ascontiguousarray(np.asarray(dist, np.float32).reshape(5))
+    lib().oc_undistort_keypoints(kps.ctypes.data_as(C.c_void_p), len(kps), C.c_float(fx), C.c_float(fy), C.c_float(cx),
+                                 C.c_float(cy), ptr(d), out.ctypes.data_as(C.c_void_p))
+    return out
+
+
 def blur_flags(gray, boxes):
     gray = np.ascontiguousarray(gray, np.uint8)
     boxes = np.ascontiguousarray(boxes, np.float32)

@@ -1739,3 +1739,32 @@ int oc_pose_optimization(const oc_pose_frame* fr, float Tcw[16], uint8_t* outlie
     free(active); free(chi2_last); free(E); free(idx);
     return ne - nBad;
 }
+
+/* ======================= Frame::UndistortKeyPoints ======================= */
+void oc_undistort_keypoints(const oc_kp* in, int n, float fx_f, float fy_f, float cx_f, float cy_f, const float dist[5],
+                            oc_kp* out)
+{
+    for (int i = 0; i < n; i++) out[i] = in[i];
+    if (dist[0] == 0.0f) return;                                   /* mDistCoef.at<float>(0) == 0.0 */
+    double k[12] = {0};
+    for (int q = 0; q < 5; q++) k[q] = (double)dist[q];
+    const double fx = fx_f, fy = fy_f, cx = cx_f, cy = cy_f;
+    const double ifx = 1. / fx, ify = 1. / fy;
+    for (int i = 0; i < n; i++) {
+        double x = (double)in[i].x, y = (double)in[i].y;
+        x = (x - cx) * ifx;
+        y = (y - cy) * ify;
+        const double x0 = x, y0 = y;
+        for (int j = 0; j < 5; j++) {                                /* TermCriteria(COUNT, 5, 0.01) */
+            const double r2 = x * x + y * y;
+            const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+            const double deltaX = ((((2 * k[2]) * x) * y + k[3] * (r2 + (2 * x) * x)) + k[8] * r2) + (k[9] * r2) * r2;
+            const double deltaY = ((k[2] * (r2 + (2 * y) * y) + ((2 * k[3]) * x) * y) + k[10] * r2) + (k[11] * r2) * r2;
+            x = (x0 - deltaX) * icdist;
+            y = (y0 - deltaY) * icdist;
+        }
+        /* P = mK, R = I: xx = fx x + cx, yy = fy y + cy, ww = 1 */
+        out[i].x = (float)(fx * x + cx);
+        out[i].y = (float)(fy * y + cy);
+    }
+}

@@ -204,6 +204,12 @@ typedef struct {
  * sums reduced over 256 lanes in a fixed tree: parity vs g2o UNPINNED. */
 int oc_pose_optimization(const oc_pose_frame* fr, float Tcw[16], uint8_t* outlier);
 
+/* Frame::UndistortKeyPoints (Frame.cc:579-609): cv::undistortPoints(mat, mat, mK, mDistCoef,
+ * Mat(), mK) of OpenCV 3.4 (cvUndistortPointsInternal, 5 fixed iterations) in double,
+ * dist = (k1, k2, p1, p2, k3); k1 == 0 copies the keypoints (:581-585). */
+void oc_undistort_keypoints(const oc_kp* in, int n, float fx, float fy, float cx, float cy, const float dist[5],
+                            oc_kp* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -53,3 +53,13 @@ def test_no_gpu_fails_loudly(lib):
     import coeb_front
     with pytest.raises(coeb_front.CoebError):
         coeb_front.Context()
+
+
+def test_boxes_from_int64_host_only():
+    """coeb_boxes_from_int64 (ros_rgbd.cc:106-115 int64 -> float) is host code: no GPU needed."""
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "coeb-slam_amd"))
+    import coeb_front
+    b = np.array([[10, 20, 300, 400], [-5, 0, 2 ** 40, 7]], np.int64)
+    assert np.array_equal(coeb_front.boxes_from_ros(b), b.astype(np.float32))

@@ -596,3 +596,18 @@ def test_pose_optimization_edges(ctx, oracle_mod):
         Q["has_mp"] = np.zeros_like(P["has_mp"])
         Q["has_mp"][:k] = 1
         pose_both(ctx, oracle_mod, Q)
+
+
+# ------------------------------------------------------------------ Frame ingest helpers
+def test_undistort_keypoints(ctx, oracle_mod, ex, pair):
+    import coeb_front
+    r1, _, _ = pair
+    k = r1["kps"]
+    cam = coeb_front.make_camera(517.306408, 516.469215, 318.643040, 255.313989, synth.TUM_BF, 640, 480)
+    for dist in ((0.262383, -0.953104, -0.005358, 0.002628, 1.163314), (0.2312, -0.7849, -0.0033, -0.0001, 0.0),
+                 (0.0, 0.5, 0.1, 0.1, 0.1)):
+        got = coeb_front.UndistortKeyPoints(ctx, k, cam, dist)
+        ref = oracle_mod.undistort_keypoints(k, 517.306408, 516.469215, 318.643040, 255.313989, dist)
+        assert got.tobytes() == ref.tobytes(), dist
+    assert len(coeb_front.UndistortKeyPoints(ctx, k[:0], cam, (0.1, 0, 0, 0, 0))) == 0
+

@@ -451,3 +451,42 @@ def test_pose_optimization_oracle_edge_cases(oracle_mod):
     nin, T, outl = oracle_mod.pose_optimization(P["kps"], has, P["xw"], P["ur"], _inv_sigma2(),
                                                 535.4, 539.2, 320.1, 247.6, 40.0, P["Tcw_init"])
     assert 0 < nin <= 8
+
+
+# ---- Frame::UndistortKeyPoints oracle: distort -> undistort round trip ----
+TUM1_DIST = (0.262383, -0.953104, -0.005358, 0.002628, 1.163314)   # Examples/RGB-D/TUM1.yaml
+
+
+def test_undistort_oracle_round_trip(oracle_mod):
+    rng = np.random.default_rng(3)
+    fx, fy, cx, cy = 517.306408, 516.469215, 318.643040, 255.313989
+    k1, k2, p1, p2, k3 = TUM1_DIST
+    n = 500
+    xn = rng.uniform(-0.35, 0.35, n)
+    yn = rng.uniform(-0.3, 0.3, n)
+    r2 = xn * xn + yn * yn
+    rad = 1 + k1 * r2 + k2 * r2 * r2 + k3 * r2 ** 3
+    xd = xn * rad + 2 * p1 * xn * yn + p2 * (r2 + 2 * xn * xn)
+    yd = yn * rad + p1 * (r2 + 2 * yn * yn) + 2 * p2 * xn * yn
+    kps = np.zeros(n, oracle_mod.KP_DTYPE)
+    kps["x"] = fx * xd + cx
+    kps["y"] = fy * yd + cy
+    kps["octave"] = rng.integers(0, 8, n)
+    un = oracle_mod.undistort_keypoints(kps, fx, fy, cx, cy, TUM1_DIST)
+    err = np.hypot(un["x"] - (fx * xn + cx), un["y"] - (fy * yn + cy))
+    assert np.median(err) < 0.01 and err.max() < 0.5, (np.median(err), err.max())
+    assert np.array_equal(un["octave"], kps["octave"])
+    same = oracle_mod.undistort_keypoints(kps, fx, fy, cx, cy, (0.0, 0.1, 0.1, 0.1, 0.1))   # k1 == 0: copy
+    assert np.array_equal(same, kps)
+
+
+def test_tum_association_golden():
+    """coeb_front.tum vs the reference associate.py's own output (tests/golden/make_tum_golden.py)."""
+    import json
+    from coeb_front import tum
+    cases = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tum_assoc.json")))
+    for c in cases:
+        got = tum.associate(tum.read_file_list(c["rgb"]), tum.read_file_list(c["depth"]), c["offset"],
+                            c["max_difference"])
+        assert [list(x) for x in got] == c["matches"]
+        assert len(got) > 20
