@@ -1112,6 +1112,11 @@ int match_batch_impl(coeb_ctx* c, const float* d_depth, int F, int W, int H, con
             mb.Tcw_cur = dT_cur + 16 * p0; mb.Tcw_last = dI + 16 * p0;
             mb.match = match + q + K; mb.nmatch = nm + p0 + 1; mb.scratch = scr + q * kMatchCQ;
             mb.scratch_stride = K * kMatchCQ; mb.err = derr;
+            if (getenv("COEB_MATCH_TIMING")) {
+                long long* tmb;
+                if ((rc = ensure(c, "m_timing", (size_t)F * 16, &tmb))) return rc;
+                mb.timing = tmb + (int64_t)p0 * 16;
+            }
             if (launch_match(mcam, mb, np, th, 0, 1, 20, s, &c->hook)) return hip_err(c, hipGetLastError(), "launch_match");
         }
         if (chunked) HIP_TRY(c, hipEventRecord(c->ev_mdone[k], s));
@@ -1299,6 +1304,16 @@ int coeb_internal_error(coeb_ctx* c, int code, const char* msg) { return set_err
  * what = "pyr" | "blur" | "cand_n" | "lvl_n" | "lvl_kp" | "dyn"; copies min(bytes, size). */
 int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t bytes, size_t* size_out)
 {
+    if (c && what && std::string(what) == "match_timing") {     // [F][16] k_match phase clocks (COEB_MATCH_TIMING)
+        if (!c->bufs.count("m_timing")) return COEB_EINVAL;
+        const size_t nb = c->bufs["m_timing"].n;
+        if (size_out) *size_out = nb;
+        if (host && bytes) {
+            HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
+            HIP_TRY(c, hipMemcpy(host, c->bufs["m_timing"].p, std::min(bytes, nb), hipMemcpyDeviceToHost));
+        }
+        return COEB_OK;
+    }
     if (c && what && (std::string(what) == "search_path" || std::string(what) == "localmap_path")) {
         // {path, iterations} of the last coeb_match_localmap / coeb_match_keyframe
         if (!c->bufs.count("l_path")) return COEB_EINVAL;

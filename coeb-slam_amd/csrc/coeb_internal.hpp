@@ -166,6 +166,7 @@ struct MatchBufs {
     int* nmatch;               // [P]
     int* scratch;              // [P][scratch_stride]
     int scratch_stride;
+    long long* timing;         // optional [P][16] phase clocks (COEB_MATCH_TIMING), else nullptr
     int* err;
 };
 int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int bmono, int check_ori,

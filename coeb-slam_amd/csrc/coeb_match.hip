@@ -93,7 +93,14 @@ constexpr int kMaxIter = 64;
 constexpr int kIdxBits = 12;
 // Lanes per LastFrame query in the candidate phase: a grid column range holds a few
 // candidates (10-px cells), so 8 lanes waste fewer than 16 (measured 0.171 -> 0.147 ms/step)
-constexpr int kQL = 8;
+#ifndef COEB_MATCH_QL
+#define COEB_MATCH_QL 8
+#endif
+constexpr int kQL = COEB_MATCH_QL;
+#ifndef COEB_MATCH_REGLIST
+#define COEB_MATCH_REGLIST 16
+#endif
+constexpr int kRegList = COEB_MATCH_REGLIST;        // list head kept in registers by the claim fixpoint
 
 struct QueryWin {
     bool ok, chk;
@@ -338,9 +345,30 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
 // keypoints not claimed by a blocking p < q, solved as a Jacobi fixpoint (iteration k fixes
 // queries 0..k-1, so it reaches the sequential answer).  L.res = the result.  Returns true when
 // kMaxIter rounds did not converge (the caller then runs its literal loop).  Block-uniform.
+__device__ __forceinline__ void first_min_step(const MatchLds& L, uint32_t v, int e, int q, uint32_t& bk, int& best)
+{
+    const int i2 = (int)(v & ((1u << kIdxBits) - 1));
+    if (L.owner[i2] < q) return;                          // claimed by an earlier point
+    const uint32_t key = ((v >> kIdxBits) << 16) | (uint32_t)e;
+    if (key < bk) { bk = key; best = i2; }
+}
+
 __device__ bool claims_first_min(const MatchLds& L, const uint32_t* lists, int stride, int n, int nq, int* s_flag)
 {
     const int tid = threadIdx.x;
+    // the thread's first query keeps the head of its list in registers across iterations
+    // (global list reads per iteration were most of this phase's time)
+    uint32_t rl[kRegList];
+    int rm = -1;
+    if (tid < nq) {
+        const int qn = L.qn[tid];
+        if (qn >= 0) {
+            rm = qn & 0xFFFF;
+            const uint32_t* lst = lists + (int64_t)tid * stride;
+#pragma unroll
+            for (int e = 0; e < kRegList; e++) rl[e] = e < rm ? lst[e] : 0u;
+        }
+    }
     for (int it = 0;; it++) {
         for (int c = tid; c < n; c += kMThreads) L.owner[c] = 0x7fffffff;
         if (tid == 0) s_flag[1] = 0;
@@ -353,24 +381,29 @@ __device__ bool claims_first_min(const MatchLds& L, const uint32_t* lists, int s
             __syncthreads();
         }
         for (int q = tid; q < nq; q += kMThreads) {
-            const int qn = L.qn[q];
             int best = -1;
-            if (qn >= 0) {
-                const int m = qn & 0xFFFF;
-                const uint32_t* lst = lists + (int64_t)q * stride;
-                uint32_t bk = 0xFFFFFFFFu;
-                for (int e = 0; e < m; e++) {
-                    const uint32_t v = lst[e];
-                    const int i2 = (int)(v & ((1u << kIdxBits) - 1));
-                    if (L.owner[i2] < q) continue;            // claimed by an earlier point
-                    const uint32_t key = ((v >> kIdxBits) << 16) | (uint32_t)e;
-                    if (key < bk) { bk = key; best = i2; }
+            uint32_t bk = 0xFFFFFFFFu;
+            if (q == tid) {
+                if (rm >= 0) {
+#pragma unroll
+                    for (int e = 0; e < kRegList; e++)
+                        if (e < rm) first_min_step(L, rl[e], e, q, bk, best);
+                    const uint32_t* lst = lists + (int64_t)q * stride;
+                    for (int e = kRegList; e < rm; e++) first_min_step(L, lst[e], e, q, bk, best);
+                }
+            } else {
+                const int qn = L.qn[q];
+                if (qn >= 0) {
+                    const int m = qn & 0xFFFF;
+                    const uint32_t* lst = lists + (int64_t)q * stride;
+                    for (int e = 0; e < m; e++) first_min_step(L, lst[e], e, q, bk, best);
                 }
             }
             if (it == 0 || best != L.res[q]) s_flag[1] = 1;
             L.res[q] = best;
         }
         __syncthreads();
+        if (threadIdx.x == 0) s_flag[7] = it + 1;
         if (!s_flag[1]) return false;
         if (it >= kMaxIter) return true;
         __syncthreads();
@@ -469,7 +502,10 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
     cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = cur_ur; cv.gdesc = cdesc;
 
     // ---- phase 0: stage CurrentFrame, grid CSR by a stable counting sort ----
+    long long* tm = b.timing ? b.timing + (int64_t)p * 16 : nullptr;   // phase clocks (COEB_MATCH_TIMING)
+    if (tm && tid == 0) tm[0] = clock64();
     stage_grid<kLds>(cam, cur, cur_ur, cdesc, n, L);
+    if (tm && tid == 0) tm[1] = clock64();
 
     // pose algebra (ORBmatcher.cc:1339-1350): twc = -Rcw^T tcw (double accumulation), tlc
     const float* T = b.Tcw_cur + (int64_t)p * 16;
@@ -554,7 +590,9 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
         __syncthreads();
         bool seq = force_seq || s_flag[0];
         // ---- phase 2: claims by fixpoint iteration ----
+        if (tm && tid == 0) tm[2 + 4 * attempt] = clock64();
         if (!seq) seq = claims_first_min(L, lists, kCQ, n, nl, s_flag);
+        if (tm && tid == 0) { tm[3 + 4 * attempt] = clock64(); tm[12 + attempt] = s_flag[7]; }
         // ---- sequential path (overflow / no convergence / forced): literal loop, one thread ----
         if (seq) {
             for (int c = tid; c < n; c += kMThreads) L.owner[c] = -1;
@@ -585,7 +623,9 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
             __syncthreads();
         }
         // ---- phase 3: mvpMapPoints, rotation consistency ----
+        if (tm && tid == 0) tm[4 + 4 * attempt] = clock64();
         nmatches = assign_rotation(L, n, nl, cur, check_ori, [&](int q) { return last[q].angle; }, s_hist, s_flag);
+        if (tm && tid == 0) tm[5 + 4 * attempt] = clock64();
         __syncthreads();
         if (nmatches >= retry_below) break;
         th = 2 * th0;                                  // Tracking.cc:954-958
@@ -593,6 +633,7 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
     int* mo = b.match + (int64_t)p * b.cur_stride;
     for (int i = tid; i < n; i += kMThreads) mo[i] = L.owner[i];
     if (tid == 0) b.nmatch[p] = nmatches;
+    if (tm && tid == 0) tm[10] = clock64();
 }
 
 

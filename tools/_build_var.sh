@@ -6,7 +6,7 @@ name=$1; defs=${2:-}
 out=build/var_$name; mkdir -p $out
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function"
 objs=""
-for s in coeb_extract coeb_match coeb_frame coeb_capi; do
+for s in $(sed -n "s/^SRCS = //p" Makefile | sed "s/\.hip//g"); do
   /opt/rocm/bin/hipcc $FLAGS $defs -c $s.hip -o $out/$s.o &
   objs="$objs $out/$s.o"
 done

@@ -1,0 +1,30 @@
+"""k_match phase clocks over one bench-shaped batch (COEB_MATCH_TIMING=1): median cycles per
+phase across the 256 pairs.  Diagnostic only."""
+import os
+import sys
+
+import numpy as np
+
+os.environ["COEB_MATCH_TIMING"] = "1"
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "coeb-slam_amd"))
+from coeb_front import synth  # noqa: E402
+from coeb_front.pipeline import BatchPipeline  # noqa: E402
+
+F = 257
+fr = synth.make_frames(640, 480, F, seed=1)
+bp = BatchPipeline(640, 480, F)
+bp.load(fr, Tcw=np.stack([synth.motion_pose()] * F))
+for _ in range(3):
+    bp.run()
+bp.ctx.synchronize()
+t = bp.ctx.debug_read("match_timing").view(np.int64).reshape(-1, 16)[:256]
+names = ["grid", "lists0", "claims0", "gap0", "assign0", "lists1", "claims1", "gap1", "assign1"]
+d = np.stack([t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2], t[:, 4] - t[:, 3], t[:, 5] - t[:, 4],
+              np.where(t[:, 6] > 0, t[:, 6] - t[:, 5], 0), np.where(t[:, 7] > 0, t[:, 7] - t[:, 6], 0),
+              np.where(t[:, 8] > 0, t[:, 8] - t[:, 7], 0), np.where(t[:, 9] > 0, t[:, 9] - t[:, 8], 0)], 1)
+tot = t[:, 10] - t[:, 0]
+print("total cycles median %d max %d" % (np.median(tot), tot.max()))
+for i, nme in enumerate(names):
+    print("%-8s median %8d  max %8d" % (nme, np.median(d[:, i]), d[:, i].max()))
+print("fixpoint iterations attempt0 median %d max %d; retried pairs %d" % (np.median(t[:, 12]), t[:, 12].max(),
+                                                                         int((t[:, 6] > 0).sum())))
