@@ -283,19 +283,26 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
         L.owner[i] = cell;                 // scratch until phase 2
     }
     __syncthreads();
-    if (tid < 64) {                        // exclusive prefix: L.cell[c] = start of cell c
-        const int lane = tid;
-        int carry = 0;
-        for (int base = 1; base <= COEB_GRID_CELLS; base += 64) {
-            const int c = base + lane;
-            int v = c <= COEB_GRID_CELLS ? L.cell[c] : 0;
-            for (int o = 1; o < 64; o <<= 1) {
-                const int y = __shfl_up(v, o, 64);
-                if (lane >= o) v += y;
-            }
-            if (c <= COEB_GRID_CELLS) L.cell[c] = carry + v;
-            carry += __shfl(v, 63, 64);
+    {                                      // prefix: L.cell[c + 1] = end of cell c (block scan)
+        static_assert(COEB_GRID_CELLS == 3 * kMThreads, "three cells per thread");
+        __shared__ int s_wsum[kMThreads / 64];
+        const int lane = tid & 63, wv = tid >> 6;
+        const int c0 = 1 + 3 * tid;
+        const int a0 = L.cell[c0], a1 = L.cell[c0 + 1], a2 = L.cell[c0 + 2];
+        int v = a0 + a1 + a2;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(v, o, 64);
+            if (lane >= o) v += y;
         }
+        if (lane == 63) s_wsum[wv] = v;
+        __syncthreads();
+        int off = 0;
+        for (int w = 0; w < wv; w++) off += s_wsum[w];
+        const int end2 = off + v;                           // inclusive prefix through cell c0 + 2
+        L.cell[c0 + 2] = end2;
+        L.cell[c0 + 1] = end2 - a2;
+        L.cell[c0] = end2 - a2 - a1;
+        if (tid == 0) L.cell[0] = 0;
     }
     __syncthreads();
     // scatter with a per-cell cursor (L.cell[c] advances to the end of cell c = start of c+1) ...
