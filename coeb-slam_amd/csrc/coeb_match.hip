@@ -151,25 +151,29 @@ __device__ __forceinline__ QueryWin query_window(const MatchCam& cam, const floa
     return w;
 }
 
+// The current frame's keypoints as candidates.  In LDS mode they are staged in CSR (grid)
+// order, so candidate e of a cell range is read at position e with no indirection through
+// L.sort (one LDS round trip per candidate step instead of three); the global fallback reads
+// keypoint i.
 template <bool kLds>
 struct CurView {
-    const float4* kp;         // LDS: (x, y, uR, octave bits)
-    const uint32_t* desc;     // LDS: 8 words per keypoint
-    const Kp* gkp;            // global fallbacks
+    const float4* kp;         // LDS, CSR order: (x, y, uR, octave bits)
+    const uint32_t* desc;     // LDS, CSR order: 8 words per keypoint
+    const Kp* gkp;            // global fallbacks, keypoint order
     const float* gur;
     const uint8_t* gdesc;
-    __device__ __forceinline__ void get(int i, float& x, float& y, float& ur, int& oct) const
+    __device__ __forceinline__ void get(int e, int i, float& x, float& y, float& ur, int& oct) const
     {
         if (kLds) {
-            const float4 k = kp[i];
+            const float4 k = kp[e];
             x = k.x; y = k.y; ur = k.z; oct = __float_as_int(k.w);
         } else {
             x = gkp[i].x; y = gkp[i].y; oct = gkp[i].octave; ur = gur ? gur[i] : -1.f;
         }
     }
-    __device__ __forceinline__ int dist(int i, const uint32_t* q) const
+    __device__ __forceinline__ int dist(int e, int i, const uint32_t* q) const
     {
-        const uint32_t* d = kLds ? desc + 8 * i : reinterpret_cast<const uint32_t*>(gdesc + 32 * i);
+        const uint32_t* d = kLds ? desc + 8 * e : reinterpret_cast<const uint32_t*>(gdesc + 32 * i);
         return hamming32(q, d);
     }
 };
@@ -186,7 +190,7 @@ __device__ __forceinline__ void for_candidates(const QueryWin& w, const int* s_c
             const int i2 = (int)(s_sort[q] & ((1u << kIdxBits) - 1));
             float x, y, ur;
             int oct;
-            cv.get(i2, x, y, ur, oct);
+            cv.get(q, i2, x, y, ur, oct);
             if (w.chk) {
                 if (oct < w.minL) continue;
                 if (w.maxL >= 0 && oct > w.maxL) continue;
@@ -197,7 +201,7 @@ __device__ __forceinline__ void for_candidates(const QueryWin& w, const int* s_c
                 const float er = fabsf(w.ur_q - ur);
                 if (er > w.radius) continue;
             }
-            if (!fn(i2)) return;
+            if (!fn(q, i2)) return;
         }
     }
 }
@@ -265,14 +269,6 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
     __syncthreads();
     for (int i = tid; i < n; i += kMThreads) {
         const Kp k = cur[i];
-        if (kLds) {
-            L.kp[i] = make_float4(k.x, k.y, cur_ur ? cur_ur[i] : -1.f, __int_as_float(k.octave));
-            const uint4* d = reinterpret_cast<const uint4*>(cdesc + 32 * i);
-            const uint4 d0 = d[0], d1 = d[1];
-            uint32_t* o = L.desc + 8 * i;
-            o[0] = d0.x; o[1] = d0.y; o[2] = d0.z; o[3] = d0.w;
-            o[4] = d1.x; o[5] = d1.y; o[6] = d1.z; o[7] = d1.w;
-        }
         const int px = (int)roundf((k.x - cam.min_x) * cam.grid_inv_w);   // PosInGrid (Frame.cc:560)
         const int py = (int)roundf((k.y - cam.min_y) * cam.grid_inv_h);
         int cell = -1;
@@ -343,7 +339,20 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
         }
     }
     __syncthreads();
-
+    if (kLds) {                            // candidates in CSR order (CurView)
+        const int ng = L.cell[COEB_GRID_CELLS];
+        for (int e = tid; e < ng; e += kMThreads) {
+            const int i = (int)(L.sort[e] & ((1u << kIdxBits) - 1));
+            const Kp k = cur[i];
+            L.kp[e] = make_float4(k.x, k.y, cur_ur ? cur_ur[i] : -1.f, __int_as_float(k.octave));
+            const uint4* d = reinterpret_cast<const uint4*>(cdesc + 32 * i);
+            const uint4 d0 = d[0], d1 = d[1];
+            uint4* o = reinterpret_cast<uint4*>(L.desc + 8 * e);
+            o[0] = d0;
+            o[1] = d1;
+        }
+        __syncthreads();
+    }
 }
 
 // Phase 2 of the first-minimum matchers (k_match, k_match_kf).  lists + q * stride: query q's
@@ -510,7 +519,7 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
 
     // ---- phase 0: stage CurrentFrame, grid CSR by a stable counting sort ----
     long long* tm = b.timing ? b.timing + (int64_t)p * 16 : nullptr;   // phase clocks (COEB_MATCH_TIMING)
-    if (tm && tid == 0) tm[0] = clock64();
+    if (tm && tid == 0) { tm[0] = clock64(); tm[13] = 0; tm[14] = 0x7fffffffffffffffll; tm[15] = 0; }
     stage_grid<kLds>(cam, cur, cur_ur, cdesc, n, L);
     if (tm && tid == 0) tm[1] = clock64();
 
@@ -541,18 +550,33 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
         // time and ballot-compact them, so each list stays in enumeration order
         {
             const int grp = tid / kQL, gl = tid % kQL, gsh = (tid & 63) & ~(kQL - 1);
+            // a query's inputs (flags, world point, octave, descriptor) are loaded one pass ahead
+            struct QIn { int act, oct; float X[3]; uint4 d0, d1; };
+            auto load_qin = [&](int q, QIn& r) {
+                r.act = 0;
+                if (q < nl) {
+                    r.act = lhas[q] && !lout[q];
+                    r.oct = last[q].octave;
+                    r.X[0] = lxw[3 * q]; r.X[1] = lxw[3 * q + 1]; r.X[2] = lxw[3 * q + 2];
+                    const uint4* d = reinterpret_cast<const uint4*>(ldesc + 32 * q);
+                    r.d0 = d[0]; r.d1 = d[1];
+                }
+            };
+            QIn nx;
+            load_qin(grp, nx);
+            const long long tw0 = tm ? clock64() : 0;
             for (int q0 = 0; q0 < nl; q0 += kMThreads / kQL) {
                 const int q = q0 + grp;
+                const QIn qi = nx;
+                load_qin(q + kMThreads / kQL, nx);
                 int cnt = -1;
                 QueryWin w;
                 w.ok = false;
-                if (q < nl && lhas[q] && !lout[q]) w = query_window(cam, T, lxw + 3 * q, last[q].octave, th, fwd, bwd);
+                if (qi.act) w = query_window(cam, T, qi.X, qi.oct, th, fwd, bwd);
                 if (w.ok) {
                     uint32_t qd[8];
-                    const uint4* d = reinterpret_cast<const uint4*>(ldesc + 32 * q);
-                    const uint4 d0 = d[0], d1 = d[1];
-                    qd[0] = d0.x; qd[1] = d0.y; qd[2] = d0.z; qd[3] = d0.w;
-                    qd[4] = d1.x; qd[5] = d1.y; qd[6] = d1.z; qd[7] = d1.w;
+                    qd[0] = qi.d0.x; qd[1] = qi.d0.y; qd[2] = qi.d0.z; qd[3] = qi.d0.w;
+                    qd[4] = qi.d1.x; qd[5] = qi.d1.y; qd[6] = qi.d1.z; qd[7] = qi.d1.w;
                     cnt = 0;
                     uint32_t* lst = lists + (int64_t)q * kCQ;
                     for (int ix = w.x0; ix <= w.x1; ix++) {
@@ -566,7 +590,7 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
                                 const int i2 = (int)(L.sort[e] & ((1u << kIdxBits) - 1));
                                 float x, y, ur;
                                 int oct;
-                                cv.get(i2, x, y, ur, oct);
+                                cv.get(e, i2, x, y, ur, oct);
                                 ok = true;
                                 if (w.chk) {
                                     if (oct < w.minL) ok = false;
@@ -576,7 +600,7 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
                                 if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) ok = false;
                                 if (ur > 0 && fabsf(w.ur_q - ur) > w.radius) ok = false;
                                 if (ok) {
-                                    const int dist = cv.dist(i2, qd);
+                                    const int dist = cv.dist(e, i2, qd);
                                     ok = dist <= TH_HIGH;
                                     ent = ((uint32_t)dist << kIdxBits) | (uint32_t)i2;
                                 }
@@ -592,6 +616,12 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
                     if (cnt > kCQ) s_flag[0] = 1;      // overflow -> sequential path
                 }
                 if (q < nl && gl == 0) L.qn[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | (lnobs[q] > 0 ? 0x10000 : 0));
+                if (tm && tid == 0) tm[15] += 1;
+            }
+            if (tm && (tid & 63) == 0) {           // per-wave loop time: slowest / fastest wave
+                const long long dt = clock64() - tw0;
+                atomicMax((unsigned long long*)&tm[13], (unsigned long long)dt);
+                atomicMin((unsigned long long*)&tm[14], (unsigned long long)dt);
             }
         }
         __syncthreads();
@@ -613,10 +643,10 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
                             uint32_t qd[8];
                             for (int k = 0; k < 8; k++) qd[k] = reinterpret_cast<const uint32_t*>(ldesc + 32 * q)[k];
                             int bestDist = 256;
-                            for_candidates<kLds>(w, L.cell, L.sort, cv, [&](int i2) {
+                            for_candidates<kLds>(w, L.cell, L.sort, cv, [&](int e, int i2) {
                                 const int own = L.owner[i2];
                                 if (own >= 0 && lnobs[own] > 0) return true;
-                                const int dist = cv.dist(i2, qd);
+                                const int dist = cv.dist(e, i2, qd);
                                 if (dist < bestDist) { bestDist = dist; best = i2; }
                                 return true;
                             });
@@ -743,14 +773,14 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
                             const int i2 = (int)(L.sort[e] & ((1u << kIdxBits) - 1));
                             float x, y, ur;
                             int oct;
-                            cv.get(i2, x, y, ur, oct);
+                            cv.get(e, i2, x, y, ur, oct);
                             ok = !(oct < w.minL || oct > w.maxL);              // chk is always set here
                             const float distx = x - w.u, disty = y - w.v;
                             if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) ok = false;
                             if (b.cur_obs[i2] > 0) ok = false;                    // :86-88, entry holder
                             if (ur > 0 && fabsf(w.ur_q - ur) > w.radius) ok = false;   // :90-95
                             if (ok) {
-                                const int dist = cv.dist(i2, qd);
+                                const int dist = cv.dist(e, i2, qd);
                                 ent = ((uint32_t)dist << kLocKeyDist) | ((uint32_t)oct << kLocKeyOct) | (uint32_t)i2;
                             }
                         }
@@ -831,12 +861,12 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
                 uint32_t qd[8];
                 for (int k = 0; k < 8; k++) qd[k] = reinterpret_cast<const uint32_t*>(b.desc + 32 * q)[k];
                 int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
-                for_candidates<kLds>(w, L.cell, L.sort, cv, [&](int i2) {
+                for_candidates<kLds>(w, L.cell, L.sort, cv, [&](int e, int i2) {
                     if (L.owner[i2] > 0) return true;
-                    const int dist = cv.dist(i2, qd);
+                    const int dist = cv.dist(e, i2, qd);
                     float x, y, ur;
                     int oct;
-                    cv.get(i2, x, y, ur, oct);
+                    cv.get(e, i2, x, y, ur, oct);
                     if (dist < bestDist) {
                         bestDist2 = bestDist; bestDist = dist;
                         bestLevel2 = bestLevel; bestLevel = oct; bestIdx = i2;
@@ -1000,13 +1030,13 @@ __global__ __launch_bounds__(kMThreads) void k_match_kf(MatchCam cam, KfBufs b, 
                             const int i2 = (int)(L.sort[e] & ((1u << kIdxBits) - 1));
                             float x, y, ur;
                             int oct;
-                            cv.get(i2, x, y, ur, oct);
+                            cv.get(e, i2, x, y, ur, oct);
                             ok = !(oct < w.minL || oct > w.maxL);            // chk always set (maxL >= 0)
                             const float distx = x - w.u, disty = y - w.v;
                             if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) ok = false;
                             if (b.cur_has[i2]) ok = false;                     // :1545-1546, entry holder
                             if (ok) {
-                                const int dist = cv.dist(i2, qd);
+                                const int dist = cv.dist(e, i2, qd);
                                 ok = dist <= orb_dist;
                                 ent = ((uint32_t)dist << kIdxBits) | (uint32_t)i2;
                             }
@@ -1042,9 +1072,9 @@ __global__ __launch_bounds__(kMThreads) void k_match_kf(MatchCam cam, KfBufs b, 
                     uint32_t qd[8];
                     for (int k = 0; k < 8; k++) qd[k] = reinterpret_cast<const uint32_t*>(b.desc + 32 * q)[k];
                     int bestDist = 256;
-                    for_candidates<kLds>(w, L.cell, L.sort, cv, [&](int i2) {
+                    for_candidates<kLds>(w, L.cell, L.sort, cv, [&](int e, int i2) {
                         if (L.owner[i2] >= 0) return true;
-                        const int dist = cv.dist(i2, qd);
+                        const int dist = cv.dist(e, i2, qd);
                         if (dist < bestDist) { bestDist = dist; best = i2; }
                         return true;
                     });

@@ -28,3 +28,5 @@ for i, nme in enumerate(names):
     print("%-8s median %8d  max %8d" % (nme, np.median(d[:, i]), d[:, i].max()))
 print("fixpoint iterations attempt0 median %d max %d; retried pairs %d" % (np.median(t[:, 12]), t[:, 12].max(),
                                                                          int((t[:, 6] > 0).sum())))
+print("lists phase per-wave loop time: slowest %d, fastest %d cycles (median over pairs), %d passes" %
+      (np.median(t[:, 13]), np.median(t[:, 14]), np.median(t[:, 15])))
