@@ -119,6 +119,44 @@ def cpu_baseline(cfg, seconds=12.0, min_frames=30):
                        % (len(times), w, h, med * 1e3))
 
 
+def cpu_extras(out, w, h, reps=5):
+    """The oracle ('port', single thread) on the same extras calls as extras_timing: ms per
+    call, for comparison with the device entry points (cpu_baseline leg only)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from coeb_front import synth
+    kp0, d0 = out[0][0], out[0][1]
+    kp1, d1 = out[1][0], out[1][1]
+    z = np.float32(synth.DEPTH_Z)
+    xw = np.stack([(kp0["x"] - np.float32(synth.TUM_CX)) * z / np.float32(synth.TUM_FX),
+                   (kp0["y"] - np.float32(synth.TUM_CY)) * z / np.float32(synth.TUM_FY),
+                   np.full(len(kp0), z, np.float32)], 1).astype(np.float32)
+    ur1 = (kp1["x"] - np.float32(synth.TUM_BF) / z).astype(np.float32)
+    ex = O.Extractor()
+    cam = O.camera(ex, w, h, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    T = synth.motion_pose()
+    res = {}
+
+    def timed(name, fn):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        res[name] = round((time.perf_counter() - t0) / reps * 1e3, 4)
+
+    mp = synth.make_local_map(xw, d0, kp0["octave"], T, w, h, seed=1)
+    timed("localmap_search_ms", lambda: O.search_local_map(cam, kp1, d1, ur1, np.full(len(kp1), -1, np.int32), mp,
+                                                           3.0, 0.8))
+    kf = synth.make_keyframe_points(xw, d0, kp0["octave"], kp0["angle"], seed=1)
+    timed("relocalisation_search_ms", lambda: O.search_keyframe(cam, kp1, d1, None, kf, T, 10.0, 100, True))
+    P = synth.make_pose_problem(n=len(kp1), seed=1)
+    isg = np.array([1.0 / (1.2 ** (2 * l)) for l in range(8)], np.float32)
+    timed("pose_optimization_ms", lambda: O.pose_optimization(P["kps"], P["has_mp"], P["xw"], P["ur"], isg,
+                                                              synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY,
+                                                              synth.TUM_BF, P["Tcw_init"]))
+    return res
+
+
 def pmc_traffic(kernel, frames_per_launch):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by tools/pmc_summary.py --json from separate
@@ -190,6 +228,59 @@ class DryRunPipeline:
         pass
 
 
+def extras_timing(ctx, out, w, h, reps=20):
+    """Per-call wall time of the host-buffer entry points beyond the headline path (SURVEY.md
+    s8(f) rows 2-4), on inputs built from the batch's own extraction of frames 0 and 1: mean
+    ms per call including the PCIe copies and the synchronisation each call performs."""
+    import coeb_front as cf
+    from coeb_front import synth
+    kp0, d0 = out[0][0], out[0][1]
+    kp1, d1 = out[1][0], out[1][1]
+    z = np.float32(synth.DEPTH_Z)
+    xw = np.stack([(kp0["x"] - np.float32(synth.TUM_CX)) * z / np.float32(synth.TUM_FX),
+                   (kp0["y"] - np.float32(synth.TUM_CY)) * z / np.float32(synth.TUM_FY),
+                   np.full(len(kp0), z, np.float32)], 1).astype(np.float32)
+    ur1 = (kp1["x"] - np.float32(synth.TUM_BF) / z).astype(np.float32)
+    cam = cf.make_camera(synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF, w, h)
+    T = synth.motion_pose()
+    res = {}
+
+    def timed(name, fn, note):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = fn()
+        res[name] = dict(ms_per_call=round((time.perf_counter() - t0) / reps * 1e3, 4), result=int(r), note=note)
+
+    mp = synth.make_local_map(xw, d0, kp0["octave"], T, w, h, seed=1)
+    lm = cf.LocalMap(mp["in_view"], mp["proj_x"], mp["proj_y"], mp["proj_xr"], mp["level"], mp["view_cos"],
+                     mp["descriptor"], mp["observations"])
+    F1 = cf.Frame(kp1, d1, ur1)
+    m = cf.ORBmatcher(0.8, ctx=ctx)
+    timed("localmap_search", lambda: m.SearchByProjection(cf.Frame(kp1, d1, ur1), lm, 3.0, camera=cam),
+          "SearchByProjection(F, %d local-map points, th 3), %d keypoints" % (lm.N, F1.N))
+    kf = synth.make_keyframe_points(xw, d0, kp0["octave"], kp0["angle"], seed=1)
+    kfp = cf.KeyFramePoints(kf["valid"], kf["world_pos"], kf["descriptor"], kf["max_distance"], kf["min_distance"],
+                            kf["angle"])
+    mk = cf.ORBmatcher(0.75, True, ctx=ctx)
+    timed("relocalisation_search",
+          lambda: mk.SearchByProjection(cf.Frame(kp1, d1, ur1, Tcw=T), kfp, set(), 10.0, 100, cam),
+          "SearchByProjection(F, KeyFrame of %d points, th 10, ORBdist 100)" % kfp.N)
+    P = synth.make_pose_problem(n=len(kp1), seed=1)
+
+    def pose():
+        Fp = cf.Frame(P["kps"], np.zeros((len(P["kps"]), 32), np.uint8), P["ur"], Tcw=P["Tcw_init"])
+        Fp.mvpMapPoints = np.where(P["has_mp"] > 0, 0, -1).astype(np.int32)
+        Fp.mvMapPointPos = P["xw"]
+        return cf.Optimizer.PoseOptimization(Fp, cam, ctx)
+    timed("pose_optimization", pose, "PoseOptimization, %d edges (20 %% gross outliers), 4 x 10 LM iterations"
+          % int(P["has_mp"].sum()))
+    dist = (0.262383, -0.953104, -0.005358, 0.002628, 1.163314)
+    timed("undistort_keypoints", lambda: len(cf.UndistortKeyPoints(ctx, kp1, cam, dist)),
+          "UndistortKeyPoints, %d keypoints, TUM1 distortion" % len(kp1))
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -202,6 +293,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip HIP-event kernel timing")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the per-call timing of the other entry points (local map, relocalisation, pose)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the rank/timing/JSON plumbing with a stand-in pipeline (tests)")
     args = ap.parse_args()
@@ -323,8 +416,12 @@ def main():
                     kernels_profiled_steps=prof_steps,
                     keypoints_per_frame=round(nkp, 1), matches_per_frame=round(nmatch, 1),
                     pcie_inclusive=e2e)
+        if not args.no_extras and world == 1 and not args.dry_run:
+            line["extras"] = extras_timing(bp.ctx, out, w, h)
         if not args.no_cpu_baseline and world == 1 and not args.dry_run:
             cb = cpu_baseline(cfg)
+            if "extras" in line:
+                cb["extras_ms_per_call"] = cpu_extras(out, w, h)
             line["cpu_baseline"] = cb
             line["speedup_vs_cpu_baseline"] = round(value / cb["value"], 1)
         print(json.dumps(line), flush=True)
