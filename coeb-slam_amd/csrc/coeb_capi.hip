@@ -357,6 +357,10 @@ struct coeb_ctx {
     bool pending_join = false;
     bool extract_chunked = false;                // the last batch extract ran on the chunk streams
     hipEvent_t ev_main = nullptr, ev_join = nullptr;
+    // pinned host staging of the host-buffer entry points: their inputs are packed here and
+    // moved in one copy (a dozen small pageable copies cost more than the kernels)
+    uint8_t* pin = nullptr;
+    size_t pin_n = 0;
 };
 
 namespace {
@@ -393,6 +397,55 @@ int ensure(coeb_ctx* c, const char* name, size_t count, T** out)
         b.n = bytes;
     }
     *out = static_cast<T*>(b.p);
+    return 0;
+}
+
+// Inputs of one call packed at 16-byte aligned offsets of the pinned staging buffer, moved to
+// the device in one copy; fill() parts are constant bytes (absent optional arrays).
+struct Pack {
+    struct Part { const void* p; size_t n; int fill; };
+    std::vector<Part> parts;
+    size_t total = 0;
+    size_t add(const void* p, size_t n) { return put(Part{p, n, -1}); }
+    size_t fill(int byte, size_t n) { return put(Part{nullptr, n, byte}); }
+    size_t put(Part q)
+    {
+        const size_t off = total;
+        parts.push_back(q);
+        total = (total + q.n + 15) & ~(size_t)15;
+        return off;
+    }
+};
+
+int pinned(coeb_ctx* c, size_t bytes)
+{
+    if (c->pin_n >= bytes) return 0;
+    if (c->pin) (void)hipHostFree(c->pin);
+    c->pin = nullptr;
+    c->pin_n = 0;
+    const size_t n = std::max<size_t>(bytes, (size_t)1 << 20);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&c->pin), n, hipHostMallocDefault);
+    if (e != hipSuccess) return set_err(c, COEB_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    c->pin_n = n;
+    return 0;
+}
+
+// pack -> pinned -> one H2D copy into the "stage" device buffer; *dbase = its device address.
+// The previous call's copies have completed: every host-buffer entry point synchronises.
+int stage_in(coeb_ctx* c, const Pack& pk, uint8_t** dbase, hipStream_t s)
+{
+    int rc;
+    const size_t total = std::max<size_t>(pk.total, 16);
+    if ((rc = pinned(c, total)) || (rc = ensure(c, "stage", total, dbase))) return rc;
+    size_t off = 0;
+    for (const Pack::Part& q : pk.parts) {
+        if (q.n) {
+            if (q.p) memcpy(c->pin + off, q.p, q.n);
+            else memset(c->pin + off, q.fill, q.n);
+        }
+        off = (off + q.n + 15) & ~(size_t)15;
+    }
+    HIP_TRY(c, hipMemcpyAsync(*dbase, c->pin, total, hipMemcpyHostToDevice, s));
     return 0;
 }
 
@@ -638,6 +691,7 @@ void coeb_destroy(coeb_ctx* c)
     }
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->pin) (void)hipHostFree(c->pin);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -880,51 +934,38 @@ int coeb_match_localmap(coeb_ctx* c, const coeb_camera* cam, const coeb_curframe
     (void)hipSetDevice(c->device);
     const int cs = std::max(n, 1), qs = std::max(nq, 1);
     int rc;
-    coeb_keypoint* dck;
-    uint8_t *dcd, *dview, *dqd;
-    float *dur, *dpx, *dpy, *dpxr, *dcos;
-    int32_t *dcobs, *dlvl, *dnobs, *dmatch, *dnm, *derr, *dpath;
+    int32_t *dout, *derr, *dpath;
     uint32_t* dlist;
-    if ((rc = ensure(c, "m_ck", cs, &dck)) || (rc = ensure(c, "m_cd", (size_t)cs * 32, &dcd)) ||
-        (rc = ensure(c, "m_ur", cs, &dur)) || (rc = ensure(c, "l_cobs", cs, &dcobs)) ||
-        (rc = ensure(c, "l_view", qs, &dview)) || (rc = ensure(c, "l_px", qs, &dpx)) || (rc = ensure(c, "l_py", qs, &dpy)) ||
-        (rc = ensure(c, "l_pxr", qs, &dpxr)) || (rc = ensure(c, "l_lvl", qs, &dlvl)) || (rc = ensure(c, "l_cos", qs, &dcos)) ||
-        (rc = ensure(c, "l_qd", (size_t)qs * 32, &dqd)) || (rc = ensure(c, "l_nobs", qs, &dnobs)) ||
-        (rc = ensure(c, "m_match", cs, &dmatch)) || (rc = ensure(c, "m_nm", 1, &dnm)) ||
-        (rc = ensure(c, "l_list", (size_t)qs * match_list_cap(), &dlist)) || (rc = ensure(c, "err", 4, &derr)) ||
-        (rc = ensure(c, "l_path", 2, &dpath)))
+    uint8_t* dbase;
+    if ((rc = ensure(c, "l_out", (size_t)cs + 1, &dout)) || (rc = ensure(c, "l_list", (size_t)qs * match_list_cap(), &dlist)) ||
+        (rc = ensure(c, "err", 4, &derr)) || (rc = ensure(c, "l_path", 2, &dpath)))
         return rc;
     hipStream_t s = main_stream(c);
-    if (n) {
-        HIP_TRY(c, hipMemcpyAsync(dck, cur->keys_un, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dcd, cur->descriptors, (size_t)n * 32, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dur, cur->u_right, (size_t)n * 4, hipMemcpyHostToDevice, s));
-        if (cur_obs) HIP_TRY(c, hipMemcpyAsync(dcobs, cur_obs, (size_t)n * 4, hipMemcpyHostToDevice, s));
-        else HIP_TRY(c, hipMemsetAsync(dcobs, 0xff, (size_t)n * 4, s));   // -1: all NULL
-    }
-    if (nq) {
-        HIP_TRY(c, hipMemcpyAsync(dview, mp->in_view, (size_t)nq, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dpx, mp->proj_x, (size_t)nq * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dpy, mp->proj_y, (size_t)nq * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dpxr, mp->proj_xr, (size_t)nq * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dlvl, mp->level, (size_t)nq * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dcos, mp->view_cos, (size_t)nq * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dqd, mp->descriptor, (size_t)nq * 32, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dnobs, mp->observations, (size_t)nq * 4, hipMemcpyHostToDevice, s));
-    }
+    Pack pk;
+    const size_t o_k = pk.add(cur->keys_un, (size_t)n * sizeof(coeb_keypoint)), o_d = pk.add(cur->descriptors, (size_t)n * 32);
+    const size_t o_ur = pk.add(cur->u_right, (size_t)n * 4);
+    const size_t o_co = cur_obs ? pk.add(cur_obs, (size_t)n * 4) : pk.fill(0xff, (size_t)n * 4);   // -1: all NULL
+    const size_t o_v = pk.add(mp->in_view, (size_t)nq), o_px = pk.add(mp->proj_x, (size_t)nq * 4);
+    const size_t o_py = pk.add(mp->proj_y, (size_t)nq * 4), o_pxr = pk.add(mp->proj_xr, (size_t)nq * 4);
+    const size_t o_l = pk.add(mp->level, (size_t)nq * 4), o_c = pk.add(mp->view_cos, (size_t)nq * 4);
+    const size_t o_qd = pk.add(mp->descriptor, (size_t)nq * 32), o_no = pk.add(mp->observations, (size_t)nq * 4);
+    if ((rc = stage_in(c, pk, &dbase, s))) return rc;
     LocalBufsHost b;
-    b.cur_kps = dck; b.cur_desc = dcd; b.cur_ur = dur; b.cur_obs = dcobs; b.cur_n = n;
-    b.in_view = dview; b.proj_x = dpx; b.proj_y = dpy; b.proj_xr = dpxr; b.level = dlvl; b.view_cos = dcos;
-    b.desc = dqd; b.nobs = dnobs; b.mp_n = nq; b.match = dmatch; b.nmatch = dnm; b.lists = dlist; b.err = derr; b.path = dpath;
+    b.cur_kps = dbase + o_k; b.cur_desc = dbase + o_d; b.cur_ur = (const float*)(dbase + o_ur);
+    b.cur_obs = (const int*)(dbase + o_co); b.cur_n = n;
+    b.in_view = dbase + o_v; b.proj_x = (const float*)(dbase + o_px); b.proj_y = (const float*)(dbase + o_py);
+    b.proj_xr = (const float*)(dbase + o_pxr); b.level = (const int*)(dbase + o_l); b.view_cos = (const float*)(dbase + o_c);
+    b.desc = dbase + o_qd; b.nobs = (const int*)(dbase + o_no); b.mp_n = nq;
+    b.match = dout; b.nmatch = dout + cs; b.lists = dlist; b.err = derr; b.path = dpath;
     rc = launch_match_local(make_cam(c, cam), b, th, nnratio, s, &c->hook);
     if (rc == -2) return set_err(c, COEB_ERANGE, "coeb_match_localmap: frame and local map exceed the LDS budget");
     if (rc) return hip_err(c, hipGetLastError(), "launch_match_local");
-    int nm = 0;
-    HIP_TRY(c, hipMemcpyAsync(&nm, dnm, 4, hipMemcpyDeviceToHost, s));
-    if (n && match_out) HIP_TRY(c, hipMemcpyAsync(match_out, dmatch, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    int32_t* hout = reinterpret_cast<int32_t*>(c->pin);          // one copy back: match[cs], nmatch
+    HIP_TRY(c, hipMemcpyAsync(hout, dout, ((size_t)cs + 1) * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
     if ((rc = check_err_word(c))) return rc;
-    *nmatches = nm;
+    if (n && match_out) memcpy(match_out, hout, (size_t)n * 4);
+    *nmatches = hout[cs];
     return COEB_OK;
 }
 
@@ -943,48 +984,36 @@ int coeb_match_keyframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curframe
     (void)hipSetDevice(c->device);
     const int cs = std::max(n, 1), qs = std::max(nq, 1);
     int rc;
-    coeb_keypoint* dck;
-    uint8_t *dcd, *dhas, *dvalid, *dqd;
-    float *dxw, *dmax, *dmin, *dang, *dT;
-    int32_t *dmatch, *dnm, *derr, *dpath;
+    int32_t *dout, *derr, *dpath;
     uint32_t* dlist;
-    if ((rc = ensure(c, "m_ck", cs, &dck)) || (rc = ensure(c, "m_cd", (size_t)cs * 32, &dcd)) ||
-        (rc = ensure(c, "k_has", cs, &dhas)) || (rc = ensure(c, "k_valid", qs, &dvalid)) ||
-        (rc = ensure(c, "k_xw", (size_t)qs * 3, &dxw)) || (rc = ensure(c, "k_qd", (size_t)qs * 32, &dqd)) ||
-        (rc = ensure(c, "k_max", qs, &dmax)) || (rc = ensure(c, "k_min", qs, &dmin)) || (rc = ensure(c, "k_ang", qs, &dang)) ||
-        (rc = ensure(c, "m_T", 32, &dT)) || (rc = ensure(c, "m_match", cs, &dmatch)) || (rc = ensure(c, "m_nm", 1, &dnm)) ||
-        (rc = ensure(c, "l_list", (size_t)qs * match_list_cap(), &dlist)) || (rc = ensure(c, "err", 4, &derr)) ||
-        (rc = ensure(c, "l_path", 2, &dpath)))
+    uint8_t* dbase;
+    if ((rc = ensure(c, "l_out", (size_t)cs + 1, &dout)) || (rc = ensure(c, "l_list", (size_t)qs * match_list_cap(), &dlist)) ||
+        (rc = ensure(c, "err", 4, &derr)) || (rc = ensure(c, "l_path", 2, &dpath)))
         return rc;
     hipStream_t s = main_stream(c);
-    if (n) {
-        HIP_TRY(c, hipMemcpyAsync(dck, cur->keys_un, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dcd, cur->descriptors, (size_t)n * 32, hipMemcpyHostToDevice, s));
-        if (cur_has) HIP_TRY(c, hipMemcpyAsync(dhas, cur_has, (size_t)n, hipMemcpyHostToDevice, s));
-        else HIP_TRY(c, hipMemsetAsync(dhas, 0, (size_t)n, s));
-    }
-    if (nq) {
-        HIP_TRY(c, hipMemcpyAsync(dvalid, kf->valid, (size_t)nq, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dxw, kf->world_pos, (size_t)nq * 12, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dqd, kf->descriptor, (size_t)nq * 32, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dmax, kf->max_distance, (size_t)nq * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dmin, kf->min_distance, (size_t)nq * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dang, kf->angle, (size_t)nq * 4, hipMemcpyHostToDevice, s));
-    }
-    HIP_TRY(c, hipMemcpyAsync(dT, Tcw, 64, hipMemcpyHostToDevice, s));
+    Pack pk;
+    const size_t o_k = pk.add(cur->keys_un, (size_t)n * sizeof(coeb_keypoint)), o_d = pk.add(cur->descriptors, (size_t)n * 32);
+    const size_t o_h = cur_has ? pk.add(cur_has, (size_t)n) : pk.fill(0, (size_t)n);
+    const size_t o_v = pk.add(kf->valid, (size_t)nq), o_x = pk.add(kf->world_pos, (size_t)nq * 12);
+    const size_t o_qd = pk.add(kf->descriptor, (size_t)nq * 32), o_mx = pk.add(kf->max_distance, (size_t)nq * 4);
+    const size_t o_mn = pk.add(kf->min_distance, (size_t)nq * 4), o_a = pk.add(kf->angle, (size_t)nq * 4);
+    const size_t o_T = pk.add(Tcw, 64);
+    if ((rc = stage_in(c, pk, &dbase, s))) return rc;
     KfBufsHost b;
-    b.cur_kps = dck; b.cur_desc = dcd; b.cur_has = dhas; b.cur_n = n;
-    b.valid = dvalid; b.xw = dxw; b.desc = dqd; b.maxd = dmax; b.mind = dmin; b.angle = dang; b.kf_n = nq; b.Tcw = dT;
-    b.match = dmatch; b.nmatch = dnm; b.lists = dlist; b.err = derr; b.path = dpath;
+    b.cur_kps = dbase + o_k; b.cur_desc = dbase + o_d; b.cur_has = dbase + o_h; b.cur_n = n;
+    b.valid = dbase + o_v; b.xw = (const float*)(dbase + o_x); b.desc = dbase + o_qd;
+    b.maxd = (const float*)(dbase + o_mx); b.mind = (const float*)(dbase + o_mn); b.angle = (const float*)(dbase + o_a);
+    b.kf_n = nq; b.Tcw = (const float*)(dbase + o_T);
+    b.match = dout; b.nmatch = dout + cs; b.lists = dlist; b.err = derr; b.path = dpath;
     rc = launch_match_kf(make_cam(c, cam), b, th, orb_dist, check_ori ? 1 : 0, s, &c->hook);
     if (rc == -2) return set_err(c, COEB_ERANGE, "coeb_match_keyframe: frame and keyframe exceed the LDS budget");
     if (rc) return hip_err(c, hipGetLastError(), "launch_match_kf");
-    int nm = 0;
-    HIP_TRY(c, hipMemcpyAsync(&nm, dnm, 4, hipMemcpyDeviceToHost, s));
-    if (n && match_out) HIP_TRY(c, hipMemcpyAsync(match_out, dmatch, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    int32_t* hout = reinterpret_cast<int32_t*>(c->pin);          // one copy back: match[cs], nmatch
+    HIP_TRY(c, hipMemcpyAsync(hout, dout, ((size_t)cs + 1) * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
     if ((rc = check_err_word(c))) return rc;
-    *nmatches = nm;
+    if (n && match_out) memcpy(match_out, hout, (size_t)n * 4);
+    *nmatches = hout[cs];
     return COEB_OK;
 }
 
@@ -1003,44 +1032,35 @@ int coeb_pose_optimization(coeb_ctx* c, const coeb_camera* cam, const coeb_pose_
     (void)hipSetDevice(c->device);
     const int cs = std::max(n, 1);
     int rc;
-    int32_t *dn, *dres;
-    uint8_t *dhas, *dout, *dact;
-    float *dxw, *dur, *dT, *dis;
-    coeb_keypoint* dk;
+    uint8_t *dact, *dbase;
     PoseEdgeRec* dedge;
     double* dchi;
-    if ((rc = ensure(c, "p_n", 1, &dn)) || (rc = ensure(c, "p_res", 1, &dres)) || (rc = ensure(c, "p_has", cs, &dhas)) ||
-        (rc = ensure(c, "p_out", cs, &dout)) || (rc = ensure(c, "p_act", cs, &dact)) ||
-        (rc = ensure(c, "p_xw", (size_t)cs * 3, &dxw)) || (rc = ensure(c, "p_ur", cs, &dur)) ||
-        (rc = ensure(c, "p_T", 16, &dT)) || (rc = ensure(c, "p_is", COEB_MAXL, &dis)) || (rc = ensure(c, "p_k", cs, &dk)) ||
-        (rc = ensure(c, "p_edge", cs, &dedge)) || (rc = ensure(c, "p_chi", cs, &dchi)))
+    if ((rc = ensure(c, "p_act", cs, &dact)) || (rc = ensure(c, "p_edge", cs, &dedge)) || (rc = ensure(c, "p_chi", cs, &dchi)))
         return rc;
     hipStream_t s = main_stream(c);
-    HIP_TRY(c, hipMemcpyAsync(dn, &fr->n, 4, hipMemcpyHostToDevice, s));
-    if (n) {
-        HIP_TRY(c, hipMemcpyAsync(dhas, fr->has_mappoint, (size_t)n, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dxw, fr->world_pos, (size_t)n * 12, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dk, fr->keys_un, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dur, fr->u_right, (size_t)n * 4, hipMemcpyHostToDevice, s));
-    }
-    HIP_TRY(c, hipMemcpyAsync(dT, Tcw, 64, hipMemcpyHostToDevice, s));
-    HIP_TRY(c, hipMemcpyAsync(dis, c->tab.inv_sigma2, sizeof(float) * COEB_MAXL, hipMemcpyHostToDevice, s));
+    // one staged region: outputs first (result, pose, outlier flags; copied back in one go), then inputs
+    Pack pk;
+    const size_t o_n = pk.add(&fr->n, 4), o_res = pk.fill(0, 4), o_T = pk.add(Tcw, 64), o_out = pk.fill(0, (size_t)cs);
+    const size_t head = o_out + (size_t)cs;
+    const size_t o_h = pk.add(fr->has_mappoint, (size_t)n), o_x = pk.add(fr->world_pos, (size_t)n * 12);
+    const size_t o_k = pk.add(fr->keys_un, (size_t)n * sizeof(coeb_keypoint)), o_ur = pk.add(fr->u_right, (size_t)n * 4);
+    const size_t o_is = pk.add(c->tab.inv_sigma2, sizeof(float) * COEB_MAXL);
+    if ((rc = stage_in(c, pk, &dbase, s))) return rc;
     PoseBufs b;
-    b.n = dn; b.has_mp = dhas; b.xw = dxw; b.kps = dk; b.ur = dur; b.inv_sigma2 = dis; b.Tcw = dT; b.outlier = dout;
-    b.result = dres; b.edges = dedge; b.active = dact; b.chi2 = dchi; b.stride = cs;
+    b.n = (const int*)(dbase + o_n); b.has_mp = dbase + o_h; b.xw = (const float*)(dbase + o_x); b.kps = dbase + o_k;
+    b.ur = (const float*)(dbase + o_ur); b.inv_sigma2 = (const float*)(dbase + o_is); b.Tcw = (float*)(dbase + o_T);
+    b.outlier = dbase + o_out; b.result = (int*)(dbase + o_res); b.edges = dedge; b.active = dact; b.chi2 = dchi;
+    b.stride = cs;
     if (launch_pose(b, 1, cam->fx, cam->fy, cam->cx, cam->cy, cam->bf, s, &c->hook))
         return hip_err(c, hipGetLastError(), "launch_pose");
-    int res = 0;
-    HIP_TRY(c, hipMemcpyAsync(&res, dres, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipMemcpyAsync(Tcw, dT, 64, hipMemcpyDeviceToHost, s));
-    if (n && outlier_out) {
-        std::vector<uint8_t> o((size_t)n);
-        HIP_TRY(c, hipMemcpyAsync(o.data(), dout, (size_t)n, hipMemcpyDeviceToHost, s));
-        HIP_TRY(c, hipStreamSynchronize(s));
-        for (int i = 0; i < n; i++)
-            if (fr->has_mappoint[i]) outlier_out[i] = o[i];
-    }
+    HIP_TRY(c, hipMemcpyAsync(c->pin, dbase, head, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
+    int res;
+    memcpy(&res, c->pin + o_res, 4);
+    memcpy(Tcw, c->pin + o_T, 64);
+    if (n && outlier_out)
+        for (int i = 0; i < n; i++)
+            if (fr->has_mappoint[i]) outlier_out[i] = c->pin[o_out + i];
     *ninliers = res;
     return COEB_OK;
 }
