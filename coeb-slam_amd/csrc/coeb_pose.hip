@@ -8,7 +8,7 @@
 //
 // One 256-thread workgroup per frame.  Edge i lives with thread i % 256; per-edge sums (the
 // 21 Hessian terms, 6 gradient terms, robust chi2) are reduced in the canonical order
-// (per-thread sequential, xor butterfly inside each wave, (w0 + w1) + (w2 + w3)) so the
+// (per-thread sequential, 32-thread runs in thread order, the 8 runs in order) so the
 // result is bit-identical to the oracle.  The 6x6 solve, the SE3 exponential and the LM
 // bookkeeping run on thread 0 and are broadcast through LDS.
 #include <hip/hip_runtime.h>
@@ -253,32 +253,33 @@ __device__ bool pq_solve6(const double H[36], const double b[6], double x[6])
     return true;
 }
 
-__device__ __forceinline__ double wave_sum(double v)    // xor butterfly 32 .. 1
-{
-    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
-    return v;
-}
-
 struct PoseLds {
     Se3 s;                 // current estimate (broadcast)
-    double red[4][28];     // per-wave sums
+    double part[28][kPT];  // per-thread partials
+    double run[28][8];     // 32-lane run sums
     double out[28];        // reduced
     double rho;
     int qmax, ok, nbad[4];
 };
 
-// block-wide canonical reduction of nv per-thread partials (uniform call)
+// block-wide canonical reduction of nv per-thread partials (uniform call): each run of 32
+// threads summed in thread order, then the 8 run sums in order (the oracle's pq_reduce)
 __device__ void block_reduce(PoseLds& L, double* v, int nv)
 {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int k = 0; k < nv; k++) {
-        const double t = wave_sum(v[k]);
-        if (lane == 0) L.red[wv][k] = t;
+    const int tid = threadIdx.x;
+    for (int k = 0; k < nv; k++) L.part[k][tid] = v[k];
+    __syncthreads();
+    if (tid < nv * 8) {
+        const int k = tid >> 3, c = tid & 7;
+        double p = 0.0;
+        for (int l = 32 * c; l < 32 * c + 32; l++) p = p + L.part[k][l];
+        L.run[k][c] = p;
     }
     __syncthreads();
-    if (threadIdx.x < nv) {
-        const int k = threadIdx.x;
-        L.out[k] = (L.red[0][k] + L.red[1][k]) + (L.red[2][k] + L.red[3][k]);
+    if (tid < nv) {
+        double t = L.run[tid][0];
+        for (int c = 1; c < 8; c++) t = t + L.run[tid][c];
+        L.out[tid] = t;
     }
     __syncthreads();
 }

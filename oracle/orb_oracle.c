@@ -1546,19 +1546,22 @@ static void pq_huber(double e2, double delta, double rho[2])
     }
 }
 
-/* The fixed reduction of per-edge terms: edge i -> lane i % 256 (sequential in i), then
- * within each 64-lane wave a xor butterfly (32, 16, .., 1), then (w0 + w1) + (w2 + w3). */
+/* The fixed reduction of per-edge terms: edge i -> lane i % 256 (sequential in i, from 0.0);
+ * each run of 32 lanes summed in lane order from 0.0; the 8 run sums added in order. */
 enum { PQ_LANES = 256, PQ_NV = 28 };
 static void pq_reduce(double lanes[PQ_LANES][PQ_NV], int nv, double out[PQ_NV])
 {
-    static double tmp[PQ_LANES][PQ_NV];
-    for (int off = 32; off >= 1; off >>= 1) {
-        for (int l = 0; l < PQ_LANES; l++)
-            for (int k = 0; k < nv; k++) tmp[l][k] = lanes[l][k] + lanes[(l & ~63) | ((l & 63) ^ off)][k];
-        for (int l = 0; l < PQ_LANES; l++)
-            for (int k = 0; k < nv; k++) lanes[l][k] = tmp[l][k];
+    for (int k = 0; k < nv; k++) {
+        double run[8];
+        for (int c = 0; c < 8; c++) {
+            double p = 0.0;
+            for (int l = 32 * c; l < 32 * c + 32; l++) p = p + lanes[l][k];
+            run[c] = p;
+        }
+        double t = run[0];
+        for (int c = 1; c < 8; c++) t = t + run[c];
+        out[k] = t;
     }
-    for (int k = 0; k < nv; k++) out[k] = (lanes[0][k] + lanes[64][k]) + (lanes[128][k] + lanes[192][k]);
 }
 
 /* LDL' of the 6x6 (no pivoting; fails unless every pivot > 0), then solve */
