@@ -230,3 +230,45 @@ def make_pose_problem(n=600, seed=0, outlier_frac=0.2, mono_frac=0.3, noise=0.7,
     has = (rng.random(n) < 0.9).astype(np.uint8)
     return dict(kps=kps, has_mp=has, xw=xw.astype(np.float32), ur=ur, Tcw_init=Tinit.astype(np.float32),
                 Tcw_true=Ttrue.astype(np.float32), gross=out)
+
+
+def _texture(rng, w, h, density=400):
+    tex = np.full((h, w), int(rng.integers(60, 200)), np.int16)
+    for _ in range(max(1, w * h // density)):
+        s = int(rng.integers(4, 11))
+        x0, y0 = int(rng.integers(0, w - s)), int(rng.integers(0, h - s))
+        tex[y0:y0 + s, x0:x0 + s] = int(rng.integers(0, 256))
+    return tex
+
+
+def moving_object_pair(w, h, seed=0, n_small=600, obj=(200, 120, 160, 200), obj_shift=(-5, 4), noise=True):
+    """A frame pair for Frame::ProcessMovingObject (Frame.cc:311-393).  A sideways camera
+    translation gives every static point a flow parallel to SHIFT whose length depends on its
+    depth: a far textured background (make_canvas plus n_small 4-12 px squares) moves by SHIFT,
+    three nearer textured panels by 2x and 3x SHIFT, and an object rectangle obj = (x, y, w, h)
+    moves by obj_shift, off the epipolar direction.  Returns (prev, cur, object box
+    (xmin, ymin, xmax, ymax) in cur)."""
+    rng = np.random.default_rng(seed + 31337)
+    canvas = make_canvas(w, h, seed).astype(np.int16)
+    for _ in range(n_small):
+        s = int(rng.integers(4, 13))
+        x0, y0 = int(rng.integers(0, w - s)), int(rng.integers(0, h - s))
+        canvas[y0:y0 + s, x0:x0 + s] = int(rng.integers(0, 256))
+    layers = []
+    for m, (px, py) in zip((2, 3, 2), ((40, 40), (420, 60), (380, 300))):
+        pw, ph = int(rng.integers(120, 180)), int(rng.integers(100, 150))
+        layers.append((_texture(rng, pw, ph), px, py, (m * SHIFT[0], m * SHIFT[1])))
+    ox, oy, ow, oh = obj
+    layers.append((_texture(rng, ow, oh), ox, oy, obj_shift))
+    frames = []
+    for k in range(2):
+        img = np.roll(canvas, (k * SHIFT[1], k * SHIFT[0]), axis=(0, 1)).copy()
+        for tex, px, py, sh in layers:
+            x, y = px + k * sh[0], py + k * sh[1]
+            th, tw = tex.shape
+            img[y:y + th, x:x + tw] = tex
+        if noise:
+            img = img + np.random.default_rng(seed * 7919 + k + 1).integers(-3, 4, size=(h, w), dtype=np.int16)
+        frames.append(np.clip(img, 0, 255).astype(np.uint8))
+    x, y = ox + obj_shift[0], oy + obj_shift[1]
+    return frames[0], frames[1], (x, y, x + ow, y + oh)

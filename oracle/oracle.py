@@ -309,3 +309,101 @@ def mapframe_from_extraction(kps, desc, depth, cam_fx, cam_fy, cam_cx, cam_cy, b
     return dict(has_mp=has, outlier=np.zeros(n, np.uint8), xw=np.ascontiguousarray(xw),
                 mp_desc=np.ascontiguousarray(desc, np.uint8), mp_nobs=np.full(n, nobs, np.int32),
                 keys_un=np.ascontiguousarray(kps))
+
+
+# ---- Frame::ProcessMovingObject (Frame.cc:311-393) ----
+def _gray(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    return img, img.shape[1], img.shape[0]
+
+
+def good_features(img, max_corners=1000, quality=0.01, min_distance=8.0, k=0.04, max_cand=1 << 30):
+    """cv::goodFeaturesToTrack(img, .., maxCorners, quality, minDistance, Mat(), 3, true, k): (n, 2) f32."""
+    img, w, h = _gray(img)
+    out = np.zeros((max(max_corners, 1), 2), np.float32)
+    n = lib().oc_good_features_harris(ptr(img), w, h, w, max_corners, C.c_double(quality), C.c_double(min_distance),
+                                      C.c_double(k), ptr(out), len(out), max_cand)
+    if n < 0:
+        raise RuntimeError("goodFeaturesToTrack oracle: candidate cap exceeded")
+    return out[:min(n, len(out))].copy()
+
+
+def corner_subpix(img, xy, win=10, max_iter=20, eps=0.03):
+    """cv::cornerSubPix(img, xy, Size(win, win), Size(-1,-1), TermCriteria(ITER|EPS, max_iter, eps))."""
+    img, w, h = _gray(img)
+    xy = np.ascontiguousarray(xy, dtype=np.float32).copy()
+    lib().oc_corner_subpix(ptr(img), w, h, w, ptr(xy), len(xy), win, max_iter, C.c_double(eps))
+    return xy
+
+
+def lk_pyr(prev, nxt, xy, win=22, max_level=5, max_count=20, eps=0.01):
+    """cv::calcOpticalFlowPyrLK(prev, next, xy, ..., Size(win, win), max_level, (ITER|EPS, max_count, eps)):
+    (next_xy (n,2) f32, status (n,) u8)."""
+    prev, w, h = _gray(prev)
+    nxt = np.ascontiguousarray(nxt, dtype=np.uint8)
+    xy = np.ascontiguousarray(xy, dtype=np.float32)
+    out = np.zeros_like(xy)
+    st = np.zeros(len(xy), np.uint8)
+    lib().oc_lk_pyr(ptr(prev), ptr(nxt), w, h, w, ptr(xy), len(xy), win, max_level, max_count, C.c_double(eps),
+                    ptr(out), ptr(st))
+    return out, st
+
+
+def pyr_down(img):
+    img, w, h = _gray(img)
+    out = np.zeros(((h + 1) // 2, (w + 1) // 2), np.uint8)
+    lib().oc_pyr_down(ptr(img), w, h, ptr(out))
+    return out
+
+
+def find_fundamental(m1, m2, thr=0.1, conf=0.99):
+    """cv::findFundamentalMat(m1, m2, mask, FM_RANSAC, thr, conf): 3x3 f64 or None (empty Mat)."""
+    m1 = np.ascontiguousarray(m1, dtype=np.float32)
+    m2 = np.ascontiguousarray(m2, dtype=np.float32)
+    F = np.zeros(9, np.float64)
+    ok = lib().oc_find_fundamental(ptr(m1), ptr(m2), len(m1), C.c_double(thr), C.c_double(conf), ptr(F))
+    return F.reshape(3, 3) if ok else None
+
+
+def moving_tail(prev, cur, pxy, nxy, state, edge=5, limit=2120.0):
+    """SAD check + findFundamentalMat + epipolar distance (Frame.cc:337-384) on tracked pairs:
+    (T_M (m,2) f32 or None when F is empty, state after the SAD check, F or None, |F_ sets|)."""
+    prev, w, h = _gray(prev)
+    cur = np.ascontiguousarray(cur, dtype=np.uint8)
+    pxy = np.ascontiguousarray(pxy, dtype=np.float32)
+    nxy = np.ascontiguousarray(nxy, dtype=np.float32)
+    st = np.ascontiguousarray(state, dtype=np.uint8).copy()
+    tm = np.zeros((max(len(pxy), 1), 2), np.float32)
+    F = np.zeros(9, np.float64)
+    nf = C.c_int(0)
+    nt = lib().oc_moving_tail(ptr(prev), ptr(cur), w, h, w, ptr(pxy), ptr(nxy), ptr(st), len(pxy), edge,
+                              C.c_double(limit), ptr(tm), len(tm), ptr(F), C.byref(nf))
+    if nt < 0:
+        return None, st, None, nf.value
+    return tm[:nt].copy(), st, F.reshape(3, 3), nf.value
+
+
+def process_moving_object(prev, cur):
+    """Frame::ProcessMovingObject(imgray, box) with imGrayPre = prev: T_M (m,2) f32, or None
+    when findFundamentalMat returns an empty Mat."""
+    prev, w, h = _gray(prev)
+    cur = np.ascontiguousarray(cur, dtype=np.uint8)
+    tm = np.zeros((1000, 2), np.float32)
+    nc = C.c_int(0)
+    nt = lib().oc_process_moving_object(ptr(prev), ptr(cur), w, h, w, ptr(tm), len(tm), C.byref(nc))
+    return None if nt < 0 else tm[:nt].copy()
+
+
+def fd_math(name, x):
+    """canonical double acos / log / exp / cos"""
+    f = getattr(lib(), "oc_fd_" + name)
+    f.restype = C.c_double
+    f.argtypes = [C.c_double]
+    return f(x)
+
+
+def solve_cubic(c):
+    c = np.ascontiguousarray(c, dtype=np.float64)
+    r = np.zeros(3, np.float64)
+    n = lib().oc_solve_cubic(ptr(c), ptr(r))
+    return n, r

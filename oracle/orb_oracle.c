@@ -1771,3 +1771,900 @@ void oc_undistort_keypoints(const oc_kp* in, int n, float fx_f, float fy_f, floa
         out[i].y = (float)(fy * y + cy);
     }
 }
+
+/* ======================= goodFeaturesToTrack (Harris) ======================= */
+static int gf_reflect(int p, int n)                 /* BORDER_REFLECT_101 */
+{
+    if (n == 1) return 0;
+    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - p - 2;
+    return p;
+}
+
+/* Harris response at (x, y): Sobel 3x3 scaled by 1/(4 * 3 * 255) (cornerEigenValsVecs),
+ * cov = (dx*dx, dx*dy, dy*dy), unnormalised 3x3 box (row sums, then column sum),
+ * R = a*c - b*b - k*(a+c)^2 with k double (calcHarris). */
+static float gf_response(const uint8_t* img, int w, int h, int stride, int x, int y, double k)
+{
+    const double scale = 1.0 / (4.0 * 3.0 * 255.0);
+    float A[3][3], B[3][3], C[3][3];
+    for (int j = 0; j < 3; j++) {
+        const int yy = gf_reflect(y + j - 1, h);
+        for (int i = 0; i < 3; i++) {
+            const int xx = gf_reflect(x + i - 1, w);
+            int p[3][3];
+            for (int b = 0; b < 3; b++)
+                for (int a = 0; a < 3; a++)
+                    p[b][a] = img[(size_t)gf_reflect(yy + b - 1, h) * stride + gf_reflect(xx + a - 1, w)];
+            const int gx = (p[0][2] - p[0][0]) + 2 * (p[1][2] - p[1][0]) + (p[2][2] - p[2][0]);
+            const int gy = (p[2][0] - p[0][0]) + 2 * (p[2][1] - p[0][1]) + (p[2][2] - p[0][2]);
+            const float dx = (float)((double)gx * scale), dy = (float)((double)gy * scale);
+            A[j][i] = dx * dx; B[j][i] = dx * dy; C[j][i] = dy * dy;
+        }
+    }
+    float sa[3], sb[3], sc[3];
+    for (int j = 0; j < 3; j++) {
+        sa[j] = (A[j][0] + A[j][1]) + A[j][2];
+        sb[j] = (B[j][0] + B[j][1]) + B[j][2];
+        sc[j] = (C[j][0] + C[j][1]) + C[j][2];
+    }
+    const float a = (sa[0] + sa[1]) + sa[2], b = (sb[0] + sb[1]) + sb[2], c = (sc[0] + sc[1]) + sc[2];
+    const float ac = a * c - b * b, apc = a + c;
+    return (float)((double)ac - (k * (double)apc) * (double)apc);
+}
+
+typedef struct { float v; int idx; } gf_cand;
+
+static int gf_cmp(const void* pa, const void* pb)     /* greaterThanPtr: value desc, address desc */
+{
+    const gf_cand* a = (const gf_cand*)pa;
+    const gf_cand* b = (const gf_cand*)pb;
+    if (a->v > b->v) return -1;
+    if (a->v < b->v) return 1;
+    return a->idx > b->idx ? -1 : (a->idx < b->idx ? 1 : 0);
+}
+
+int oc_good_features_harris(const uint8_t* img, int w, int h, int stride, int max_corners, double quality,
+                            double min_distance, double k, float* out_xy, int cap, int max_cand)
+{
+    if (w <= 0 || h <= 0) return 0;
+    float* eig = (float*)malloc(sizeof(float) * (size_t)w * h);
+    float maxv = -FLT_MAX;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const float r = gf_response(img, w, h, stride, x, y, k);
+            eig[(size_t)y * w + x] = r;
+            if (r > maxv) maxv = r;
+        }
+    const float thr = (float)((double)maxv * quality);             /* threshold TOZERO */
+    for (size_t i = 0; i < (size_t)w * h; i++)
+        if (!(eig[i] > thr)) eig[i] = 0.f;
+    gf_cand* cand = (gf_cand*)malloc(sizeof(gf_cand) * (size_t)w * h);
+    int nc = 0;
+    for (int y = 1; y < h - 1; y++)
+        for (int x = 1; x < w - 1; x++) {
+            const float v = eig[(size_t)y * w + x];
+            if (v == 0.f) continue;
+            float m = v;                                              /* dilate 3x3 */
+            for (int dy = -1; dy <= 1; dy++)
+                for (int dx = -1; dx <= 1; dx++) {
+                    const float u = eig[(size_t)(y + dy) * w + x + dx];
+                    if (u > m) m = u;
+                }
+            if (v == m) { cand[nc].v = v; cand[nc].idx = y * w + x; nc++; }
+        }
+    free(eig);
+    if (nc > max_cand) { free(cand); return -1; }
+    qsort(cand, (size_t)nc, sizeof(gf_cand), gf_cmp);
+    const int cell = (int)lrint(min_distance);                       /* cvRound */
+    const int gw = (w + cell - 1) / cell, gh = (h + cell - 1) / cell;
+    const double md2 = min_distance * min_distance;
+    int* gcnt = (int*)calloc((size_t)gw * gh, sizeof(int));
+    float* gpt = (float*)malloc(sizeof(float) * 2 * 16 * (size_t)gw * gh);   /* <= 16 per cell */
+    int n = 0;
+    for (int i = 0; i < nc && (max_corners <= 0 || n < max_corners); i++) {
+        const int y = cand[i].idx / w, x = cand[i].idx - y * w;
+        const int xc = x / cell, yc = y / cell;
+        int good = 1;
+        for (int yy = (yc - 1 > 0 ? yc - 1 : 0); good && yy <= (yc + 1 < gh - 1 ? yc + 1 : gh - 1); yy++)
+            for (int xx = (xc - 1 > 0 ? xc - 1 : 0); good && xx <= (xc + 1 < gw - 1 ? xc + 1 : gw - 1); xx++) {
+                const int g = yy * gw + xx;
+                for (int j = 0; j < gcnt[g]; j++) {
+                    const float ddx = (float)x - gpt[(g * 16 + j) * 2], ddy = (float)y - gpt[(g * 16 + j) * 2 + 1];
+                    if ((double)(ddx * ddx + ddy * ddy) < md2) { good = 0; break; }
+                }
+            }
+        if (good) {
+            const int g = yc * gw + xc;
+            gpt[(g * 16 + gcnt[g]) * 2] = (float)x;
+            gpt[(g * 16 + gcnt[g]) * 2 + 1] = (float)y;
+            gcnt[g]++;
+            if (n < cap) { out_xy[2 * n] = (float)x; out_xy[2 * n + 1] = (float)y; }
+            n++;
+        }
+    }
+    free(gcnt); free(gpt); free(cand);
+    return n;
+}
+
+/* ======================= cornerSubPix (cornersubpix.cpp, OpenCV 3.4) ======================= */
+static int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+
+/* getRectSubPix(src 8U, Size(ww, wh), center, dst 32F): samplers.cpp getRectSubPix_8u32f when
+ * the window (plus one column/row) is inside the image, else getRectSubPix_Cn_ (replicated
+ * edges through adjustRect: clamped rows, 2-term edge columns). */
+void oc_rect_subpix_8u32f(const uint8_t* img, int w, int h, int stride, int ww, int wh, float cx, float cy,
+                          float* dst)
+{
+    const float ctrx = cx - (float)(ww - 1) * 0.5f, ctry = cy - (float)(wh - 1) * 0.5f;
+    const int ipx = cv_floor(ctrx), ipy = cv_floor(ctry);
+    if (ipx >= 0 && ipx + ww < w && ipy >= 0 && ipy + wh < h) {
+        float a = ctrx - (float)ipx;
+        const float b = ctry - (float)ipy;
+        a = a < 0.0001f ? 0.0001f : a;
+        const float a12 = a * (1.f - b), a22 = a * b, b1 = 1.f - b, b2 = b;
+        const double s = (1. - (double)a) / (double)a;
+        for (int r = 0; r < wh; r++) {
+            const uint8_t* src = img + (size_t)(ipy + r) * stride + ipx;
+            float prev = (1.f - a) * (b1 * (float)src[0] + b2 * (float)src[stride]);
+            for (int j = 0; j < ww; j++) {
+                const float t = a12 * (float)src[j + 1] + a22 * (float)src[j + 1 + stride];
+                dst[r * ww + j] = prev + t;
+                prev = (float)((double)t * s);
+            }
+        }
+        return;
+    }
+    const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
+    const float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
+    const float b1 = 1.f - b, b2 = b;
+    for (int r = 0; r < wh; r++) {
+        const uint8_t* r0 = img + (size_t)clampi(ipy + r, 0, h - 1) * stride;
+        const uint8_t* r1 = img + (size_t)clampi(ipy + r + 1, 0, h - 1) * stride;
+        for (int j = 0; j < ww; j++) {
+            const int c = ipx + j;
+            float v;
+            if (c < 0) v = (float)r0[0] * b1 + (float)r1[0] * b2;
+            else if (c >= w - 1) v = (float)r0[w - 1] * b1 + (float)r1[w - 1] * b2;
+            else v = (float)r0[c] * a11 + (float)r0[c + 1] * a12 + (float)r1[c] * a21 + (float)r1[c + 1] * a22;
+            dst[r * ww + j] = v;
+        }
+    }
+}
+
+/* The cornerSubPix weight window: mask[i][j] = vy * expf(-x*x), vy = expf(-y*y),
+ * y = (float)(i - win)/win (float division), as cornersubpix.cpp builds it. */
+void oc_subpix_mask(int win, float* mask)
+{
+    const int n = 2 * win + 1;
+    for (int i = 0; i < n; i++) {
+        const float y = (float)(i - win) / (float)win;
+        const float vy = expf(-y * y);
+        for (int j = 0; j < n; j++) {
+            const float x = (float)(j - win) / (float)win;
+            mask[i * n + j] = vy * expf(-x * x);
+        }
+    }
+}
+
+/* cv::cornerSubPix(img, corners, Size(win, win), Size(-1,-1), TermCriteria(ITER|EPS, max_iter,
+ * eps)) (Frame.cc:334), in place.  Sums in double in the reference's row-major order. */
+void oc_corner_subpix(const uint8_t* img, int w, int h, int stride, float* xy, int n, int win, int max_iter,
+                      double eps)
+{
+    const int ww = 2 * win + 1;
+    float* mask = (float*)malloc(sizeof(float) * ww * ww);
+    float* buf = (float*)malloc(sizeof(float) * (ww + 2) * (ww + 2));
+    oc_subpix_mask(win, mask);
+    const int iters = max_iter < 1 ? 1 : max_iter > 100 ? 100 : max_iter;
+    const double eps2 = (eps > 0 ? eps : 0.) * (eps > 0 ? eps : 0.);
+    for (int p = 0; p < n; p++) {
+        const float tx = xy[2 * p], ty = xy[2 * p + 1];
+        float cx = tx, cy = ty;
+        int it = 0;
+        double err = 0;
+        do {
+            double a = 0, b = 0, c = 0, bb1 = 0, bb2 = 0;
+            oc_rect_subpix_8u32f(img, w, h, stride, ww + 2, ww + 2, cx, cy, buf);
+            for (int i = 0, k = 0; i < ww; i++) {
+                const float* sp = buf + (i + 1) * (ww + 2) + 1;
+                const double py = i - win;
+                for (int j = 0; j < ww; j++, k++) {
+                    const double m = mask[k];
+                    const double tgx = (double)(sp[j + 1] - sp[j - 1]);
+                    const double tgy = (double)(sp[j + ww + 2] - sp[j - ww - 2]);
+                    const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
+                    const double px = j - win;
+                    a += gxx; b += gxy; c += gyy;
+                    bb1 += gxx * px + gxy * py;
+                    bb2 += gxy * px + gyy * py;
+                }
+            }
+            const double det = a * c - b * b;
+            if (fabs(det) <= DBL_EPSILON * DBL_EPSILON) break;
+            const double scale = 1.0 / det;
+            const float nx = (float)((double)cx + c * scale * bb1 - b * scale * bb2);
+            const float ny = (float)((double)cy - b * scale * bb1 + a * scale * bb2);
+            err = (double)((nx - cx) * (nx - cx) + (ny - cy) * (ny - cy));
+            cx = nx; cy = ny;
+            if (cx < 0 || cx >= (float)w || cy < 0 || cy >= (float)h) break;
+        } while (++it < iters && err > eps2);
+        if (fabsf(cx - tx) > (float)win || fabsf(cy - ty) > (float)win) { cx = tx; cy = ty; }
+        xy[2 * p] = cx; xy[2 * p + 1] = cy;
+    }
+    free(mask); free(buf);
+}
+
+/* ======================= calcOpticalFlowPyrLK (lkpyramid.cpp, OpenCV 3.4) ======================= */
+/* pyrDown 8U: 5x5 [1 4 6 4 1]^2, (sum + 128) >> 8, REFLECT_101; dst ((sw+1)/2, (sh+1)/2) */
+void oc_pyr_down(const uint8_t* src, int sw, int sh, uint8_t* dst)
+{
+    const int dw = (sw + 1) / 2, dh = (sh + 1) / 2;
+    static const int k[5] = {1, 4, 6, 4, 1};
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++) {
+            int acc = 0;
+            for (int i = 0; i < 5; i++) {
+                const uint8_t* row = src + (size_t)gf_reflect(2 * y + i - 2, sh) * sw;
+                int hs = 0;
+                for (int j = 0; j < 5; j++) hs += k[j] * row[gf_reflect(2 * x + j - 2, sw)];
+                acc += k[i] * hs;
+            }
+            dst[(size_t)y * dw + x] = (uint8_t)((acc + 128) >> 8);
+        }
+}
+
+/* buildOpticalFlowPyramid(img, pyr, winSize, maxLevel, false): number of levels kept */
+int oc_lk_levels(int w, int h, int win, int max_level)
+{
+    for (int level = 0; level <= max_level; level++) {
+        w = (w + 1) / 2; h = (h + 1) / 2;
+        if (w <= win || h <= win) return level + 1;
+    }
+    return max_level + 1;
+}
+
+/* calcSharrDeriv: interleaved (dx, dy) int16, REFLECT_101 */
+static void lk_sharr(const uint8_t* img, int w, int h, int16_t* d)
+{
+    int* t0 = (int*)malloc(sizeof(int) * (w + 2));
+    int* t1 = (int*)malloc(sizeof(int) * (w + 2));
+    for (int y = 0; y < h; y++) {
+        const uint8_t* s0 = img + (size_t)(y > 0 ? y - 1 : (h > 1 ? 1 : 0)) * w;
+        const uint8_t* s1 = img + (size_t)y * w;
+        const uint8_t* s2 = img + (size_t)(y < h - 1 ? y + 1 : (h > 1 ? h - 2 : 0)) * w;
+        for (int x = 0; x < w; x++) {
+            t0[x + 1] = (s0[x] + s2[x]) * 3 + s1[x] * 10;
+            t1[x + 1] = s2[x] - s0[x];
+        }
+        const int x0 = w > 1 ? 1 : 0, x1 = w > 1 ? w - 2 : 0;
+        t0[0] = t0[x0 + 1]; t0[w + 1] = t0[x1 + 1];
+        t1[0] = t1[x0 + 1]; t1[w + 1] = t1[x1 + 1];
+        for (int x = 0; x < w; x++) {
+            d[((size_t)y * w + x) * 2] = (int16_t)(t0[x + 2] - t0[x]);
+            d[((size_t)y * w + x) * 2 + 1] = (int16_t)((t1[x + 2] + t1[x]) * 3 + t1[x + 1] * 10);
+        }
+    }
+    free(t0); free(t1);
+}
+
+#define LK_DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
+
+typedef struct { const uint8_t* img; int w, h; } lk_plane;
+static inline int lk_px(const lk_plane* p, int x, int y)   /* copyMakeBorder REFLECT_101 frame */
+{
+    return p->img[(size_t)gf_reflect(y, p->h) * p->w + gf_reflect(x, p->w)];
+}
+static inline int lk_dv(const int16_t* d, int w, int h, int x, int y, int c)  /* BORDER_CONSTANT 0 */
+{
+    return (x < 0 || y < 0 || x >= w || y >= h) ? 0 : d[((size_t)y * w + x) * 2 + c];
+}
+
+/* cv::calcOpticalFlowPyrLK(prev, next, prevPts, nextPts, status, err, Size(win, win), max_level,
+ * TermCriteria(ITER|EPS, max_count, eps)) (Frame.cc:335), flags 0, minEigThreshold 1e-4.
+ * The window sums are exact (int64); OpenCV 3.4 accumulates them in float. */
+int oc_lk_pyr(const uint8_t* prev, const uint8_t* next, int w, int h, int stride, const float* pxy, int n, int win,
+              int max_level, int max_count, double eps, float* nxy, uint8_t* status)
+{
+    const int L = oc_lk_levels(w, h, win, max_level);
+    uint8_t* P[16]; uint8_t* N[16]; int16_t* D[16]; int lw[16], lh[16];
+    lw[0] = w; lh[0] = h;
+    P[0] = (uint8_t*)malloc((size_t)w * h); N[0] = (uint8_t*)malloc((size_t)w * h);
+    for (int y = 0; y < h; y++) {
+        memcpy(P[0] + (size_t)y * w, prev + (size_t)y * stride, w);
+        memcpy(N[0] + (size_t)y * w, next + (size_t)y * stride, w);
+    }
+    for (int l = 1; l < L; l++) {
+        lw[l] = (lw[l - 1] + 1) / 2; lh[l] = (lh[l - 1] + 1) / 2;
+        P[l] = (uint8_t*)malloc((size_t)lw[l] * lh[l]); N[l] = (uint8_t*)malloc((size_t)lw[l] * lh[l]);
+        oc_pyr_down(P[l - 1], lw[l - 1], lh[l - 1], P[l]);
+        oc_pyr_down(N[l - 1], lw[l - 1], lh[l - 1], N[l]);
+    }
+    for (int l = 0; l < L; l++) {
+        D[l] = (int16_t*)malloc(sizeof(int16_t) * 2 * (size_t)lw[l] * lh[l]);
+        lk_sharr(P[l], lw[l], lh[l], D[l]);
+    }
+    const double eps2 = eps * eps;
+    const float hw = (float)(win - 1) * 0.5f;
+    const float FLT_SCALE = 1.f / (1 << 20);
+    int16_t* Iw = (int16_t*)malloc(sizeof(int16_t) * 3 * win * win);
+    for (int p = 0; p < n; p++) {
+        status[p] = 1;
+        float nx = 0, ny = 0;
+        for (int level = L - 1; level >= 0; level--) {
+            const lk_plane I = {P[level], lw[level], lh[level]}, J = {N[level], lw[level], lh[level]};
+            const float sc = (float)(1. / (1 << level));
+            float px = pxy[2 * p] * sc, py = pxy[2 * p + 1] * sc;
+            if (level == L - 1) { nx = px; ny = py; }
+            else { nx = nx * 2.f; ny = ny * 2.f; }
+            px -= hw; py -= hw;
+            const int ipx = cv_floor(px), ipy = cv_floor(py);
+            if (ipx < -win || ipx >= lw[level] || ipy < -win || ipy >= lh[level]) {
+                if (level == 0) status[p] = 0;
+                continue;
+            }
+            float a = px - (float)ipx, b = py - (float)ipy;
+            int iw00 = cv_round((1.f - a) * (1.f - b) * 16384.f);
+            int iw01 = cv_round(a * (1.f - b) * 16384.f);
+            int iw10 = cv_round((1.f - a) * b * 16384.f);
+            int iw11 = 16384 - iw00 - iw01 - iw10;
+            int64_t iA11 = 0, iA12 = 0, iA22 = 0;
+            for (int y = 0; y < win; y++)
+                for (int x = 0; x < win; x++) {
+                    const int X = ipx + x, Y = ipy + y;
+                    const int ival = LK_DESCALE(lk_px(&I, X, Y) * iw00 + lk_px(&I, X + 1, Y) * iw01 +
+                                                lk_px(&I, X, Y + 1) * iw10 + lk_px(&I, X + 1, Y + 1) * iw11, 9);
+                    int g[2];
+                    for (int c = 0; c < 2; c++)
+                        g[c] = LK_DESCALE(lk_dv(D[level], lw[level], lh[level], X, Y, c) * iw00 +
+                                          lk_dv(D[level], lw[level], lh[level], X + 1, Y, c) * iw01 +
+                                          lk_dv(D[level], lw[level], lh[level], X, Y + 1, c) * iw10 +
+                                          lk_dv(D[level], lw[level], lh[level], X + 1, Y + 1, c) * iw11, 14);
+                    Iw[3 * (y * win + x)] = (int16_t)ival;
+                    Iw[3 * (y * win + x) + 1] = (int16_t)g[0];
+                    Iw[3 * (y * win + x) + 2] = (int16_t)g[1];
+                    iA11 += (int64_t)g[0] * g[0];
+                    iA12 += (int64_t)g[0] * g[1];
+                    iA22 += (int64_t)g[1] * g[1];
+                }
+            const float A11 = (float)iA11 * FLT_SCALE, A12 = (float)iA12 * FLT_SCALE, A22 = (float)iA22 * FLT_SCALE;
+            float D2 = A11 * A22 - A12 * A12;
+            const float minEig = ((A22 + A11) - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
+                                 (float)(2 * win * win);
+            if (minEig < 1e-4f || D2 < FLT_EPSILON) {
+                if (level == 0) status[p] = 0;
+                continue;
+            }
+            D2 = 1.f / D2;
+            float lx = nx - hw, ly = ny - hw;         /* nextPt -= halfWin; nx, ny = nextPts[ptidx] */
+            float pdx = 0, pdy = 0;
+            for (int j = 0; j < max_count; j++) {
+                const int inx = cv_floor(lx), iny = cv_floor(ly);
+                if (inx < -win || inx >= lw[level] || iny < -win || iny >= lh[level]) {
+                    if (level == 0) status[p] = 0;
+                    break;
+                }
+                a = lx - (float)inx; b = ly - (float)iny;
+                iw00 = cv_round((1.f - a) * (1.f - b) * 16384.f);
+                iw01 = cv_round(a * (1.f - b) * 16384.f);
+                iw10 = cv_round((1.f - a) * b * 16384.f);
+                iw11 = 16384 - iw00 - iw01 - iw10;
+                int64_t ib1 = 0, ib2 = 0;
+                for (int y = 0; y < win; y++)
+                    for (int x = 0; x < win; x++) {
+                        const int X = inx + x, Y = iny + y;
+                        const int diff = LK_DESCALE(lk_px(&J, X, Y) * iw00 + lk_px(&J, X + 1, Y) * iw01 +
+                                                    lk_px(&J, X, Y + 1) * iw10 + lk_px(&J, X + 1, Y + 1) * iw11, 9) -
+                                         Iw[3 * (y * win + x)];
+                        ib1 += (int64_t)diff * Iw[3 * (y * win + x) + 1];
+                        ib2 += (int64_t)diff * Iw[3 * (y * win + x) + 2];
+                    }
+                const float b1 = (float)ib1 * FLT_SCALE, b2 = (float)ib2 * FLT_SCALE;
+                const float dx = (A12 * b2 - A22 * b1) * D2, dy = (A12 * b1 - A11 * b2) * D2;
+                lx += dx; ly += dy;
+                nx = lx + hw; ny = ly + hw;           /* nextPts[ptidx] = nextPt + halfWin */
+                if ((double)dx * dx + (double)dy * dy <= eps2) break;
+                if (j > 0 && fabsf(dx + pdx) < 0.01 && fabsf(dy + pdy) < 0.01) {
+                    nx -= dx * 0.5f; ny -= dy * 0.5f;
+                    break;
+                }
+                pdx = dx; pdy = dy;
+            }
+            if (level == 0 && status[p]) {            /* the err pass's bounds check */
+                const float ex = nx - hw, ey = ny - hw;
+                const int iex = cv_floor(ex), iey = cv_floor(ey);
+                if (iex < -win || iex >= lw[0] || iey < -win || iey >= lh[0]) status[p] = 0;
+            }
+        }
+        nxy[2 * p] = nx; nxy[2 * p + 1] = ny;
+    }
+    free(Iw);
+    for (int l = 0; l < L; l++) { free(P[l]); free(N[l]); free(D[l]); }
+    return L;
+}
+
+/* ======================= findFundamentalMat (fundam.cpp / ptsetreg.cpp, OpenCV 3.4) ======================= */
+/* Canonical double acos / log / exp: the fdlibm algorithms (e_acos.c, e_log.c, e_exp.c), pure
+ * IEEE arithmetic so the HIP twin is bit-identical; cos through pq_sincos.  pow(x, y) (solveCubic)
+ * = exp(y * log(x)), x > 0; 0 for x == 0. */
+static inline uint32_t fd_hi(double x) { uint64_t u; memcpy(&u, &x, 8); return (uint32_t)(u >> 32); }
+static inline uint32_t fd_lo(double x) { uint64_t u; memcpy(&u, &x, 8); return (uint32_t)u; }
+static inline double fd_make(uint32_t hi, uint32_t lo) { uint64_t u = ((uint64_t)hi << 32) | lo; double d; memcpy(&d, &u, 8); return d; }
+
+double oc_fd_acos(double x)
+{
+    const double pi = 0x1.921fb54442d18p+1, pio2_hi = 0x1.921fb54442d18p+0, pio2_lo = 0x1.1a62633145c07p-54;
+    const double pS0 = 0x1.5555555555555p-3, pS1 = -0x1.4d61203eb6f7dp-2, pS2 = 0x1.9c1550e884455p-3,
+                 pS3 = -0x1.48228b5688f3bp-5, pS4 = 0x1.9efe07501b288p-11, pS5 = 0x1.23de10dfdf709p-15;
+    const double qS1 = -0x1.33a271c8a2d4bp+1, qS2 = 0x1.02ae59c598ac8p+1, qS3 = -0x1.6066c1b8d0159p-1,
+                 qS4 = 0x1.3b8c5b12e9282p-4;
+    const int32_t hx = (int32_t)fd_hi(x), ix = hx & 0x7fffffff;
+    if (ix >= 0x3ff00000) {
+        if (((ix - 0x3ff00000) | fd_lo(x)) == 0) return hx > 0 ? 0.0 : pi + 2.0 * pio2_lo;
+        return NAN;
+    }
+    if (ix < 0x3fe00000) {
+        if (ix <= 0x3c600000) return pio2_hi + pio2_lo;
+        const double z = x * x;
+        const double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        const double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        const double r = p / q;
+        return pio2_hi - (x - (pio2_lo - x * r));
+    } else if (hx < 0) {
+        const double z = (1.0 + x) * 0.5;
+        const double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        const double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        const double s = sqrt(z);
+        const double r = p / q;
+        const double w = r * s - pio2_lo;
+        return pi - 2.0 * (s + w);
+    } else {
+        const double z = (1.0 - x) * 0.5;
+        const double s = sqrt(z);
+        const double df = fd_make(fd_hi(s), 0);
+        const double c = (z - df * df) / (s + df);
+        const double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        const double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        const double r = p / q;
+        const double w = r * s + c;
+        return 2.0 * (df + w);
+    }
+}
+
+double oc_fd_log(double x)
+{
+    const double ln2_hi = 0x1.62e42fee00000p-1, ln2_lo = 0x1.a39ef35793c76p-33, two54 = 0x1p54;
+    const double Lg1 = 0x1.5555555555593p-1, Lg2 = 0x1.999999997fa04p-2, Lg3 = 0x1.2492494229359p-2,
+                 Lg4 = 0x1.c71c51d8e78afp-3, Lg5 = 0x1.7466496cb03dep-3, Lg6 = 0x1.39a09d078c69fp-3,
+                 Lg7 = 0x1.2f112df3e5244p-3;
+    int32_t hx = (int32_t)fd_hi(x);
+    const uint32_t lx = fd_lo(x);
+    int32_t k = 0;
+    if (hx < 0x00100000) {
+        if (((hx & 0x7fffffff) | lx) == 0) return -INFINITY;
+        if (hx < 0) return NAN;
+        k -= 54; x *= two54;
+        hx = (int32_t)fd_hi(x);
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    const int32_t i0 = (hx + 0x95f64) & 0x100000;
+    x = fd_make((uint32_t)(hx | (i0 ^ 0x3ff00000)), fd_lo(x));
+    k += (i0 >> 20);
+    const double f = x - 1.0;
+    if ((0x000fffff & (2 + hx)) < 3) {
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            const double dk = (double)k;
+            return dk * ln2_hi + dk * ln2_lo;
+        }
+        const double R = f * f * (0.5 - 0.33333333333333333 * f);
+        if (k == 0) return f - R;
+        const double dk = (double)k;
+        return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    const double s = f / (2.0 + f);
+    const double dk = (double)k;
+    const double z = s * s;
+    int32_t i = hx - 0x6147a;
+    const double w = z * z;
+    const int32_t j = 0x6b851 - hx;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i |= j;
+    const double R = t2 + t1;
+    if (i > 0) {
+        const double hfsq = 0.5 * f * f;
+        if (k == 0) return f - (hfsq - s * (hfsq + R));
+        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    if (k == 0) return f - s * (f - R);
+    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+double oc_fd_exp(double x)
+{
+    const double ln2HI = 0x1.62e42fee00000p-1, ln2LO = 0x1.a39ef35793c76p-33, invln2 = 0x1.71547652b82fep+0;
+    const double P1 = 0x1.555555555553ep-3, P2 = -0x1.6c16c16bebd93p-9, P3 = 0x1.1566aaf25de2cp-14,
+                 P4 = -0x1.bbd41c5d26bf1p-20, P5 = 0x1.6376972bea4d0p-25;
+    const double o_threshold = 0x1.62e42fefa39efp+9, u_threshold = -0x1.74910d52d3051p+9;
+    uint32_t hx = fd_hi(x);
+    const int xsb = (hx >> 31) & 1;
+    hx &= 0x7fffffff;
+    if (hx >= 0x40862E42) {
+        if (hx >= 0x7ff00000) {
+            if (((hx & 0xfffff) | fd_lo(x)) != 0) return x + x;
+            return xsb == 0 ? x : 0.0;
+        }
+        if (x > o_threshold) return INFINITY;
+        if (x < u_threshold) return 0.0;
+    }
+    double hi = 0, lo = 0;
+    int k = 0;
+    if (hx > 0x3fd62e42) {
+        if (hx < 0x3FF0A2B2) {
+            hi = x - (xsb ? -ln2HI : ln2HI); lo = xsb ? -ln2LO : ln2LO; k = 1 - xsb - xsb;
+        } else {
+            k = (int)(invln2 * x + (xsb ? -0.5 : 0.5));
+            const double t = k;
+            hi = x - t * ln2HI;
+            lo = t * ln2LO;
+        }
+        x = hi - lo;
+    } else if (hx < 0x3e300000) {
+        return 1.0 + x;
+    } else k = 0;
+    const double t = x * x;
+    const double c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
+    double y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
+    if (k >= -1021) return fd_make(fd_hi(y) + ((uint32_t)k << 20), fd_lo(y));
+    y = fd_make(fd_hi(y) + ((uint32_t)(k + 1000) << 20), fd_lo(y));
+    return y * 0x1p-1000;
+}
+
+double oc_fd_cos(double x) { double s, c; pq_sincos(x, &s, &c); return c; }
+
+static double fd_pow_pos(double x, double y) { return x == 0.0 ? 0.0 : oc_fd_exp(y * oc_fd_log(x)); }
+
+/* cv::solveCubic for coeffs c[0..3] (c[0] x^3 + ...): roots and their count */
+int oc_solve_cubic(const double c[4], double r[3])
+{
+    double a0 = c[0], a1 = c[1], a2 = c[2], a3 = c[3], x0 = 0, x1 = 0, x2 = 0;
+    int n = 0;
+    if (a0 == 0) {
+        if (a1 == 0) {
+            if (a2 == 0) n = a3 == 0 ? -1 : 0;
+            else { x0 = -a3 / a2; n = 1; }
+        } else {
+            double d = a2 * a2 - 4 * a1 * a3;
+            if (d >= 0) {
+                d = sqrt(d);
+                const double q1 = (-a2 + d) * 0.5, q2 = (a2 + d) * -0.5;
+                if (fabs(q1) > fabs(q2)) { x0 = q1 / a1; x1 = a3 / q1; }
+                else { x0 = q2 / a1; x1 = a3 / q2; }
+                n = d > 0 ? 2 : 1;
+            }
+        }
+    } else {
+        a0 = 1. / a0;
+        a1 *= a0; a2 *= a0; a3 *= a0;
+        const double Q = (a1 * a1 - 3 * a2) * (1. / 9);
+        const double R = (2 * a1 * a1 * a1 - 9 * a1 * a2 + 27 * a3) * (1. / 54);
+        const double Qcubed = Q * Q * Q;
+        double d = Qcubed - R * R;
+        if (d > 0) {
+            const double theta = oc_fd_acos(R / sqrt(Qcubed));
+            const double sqrtQ = sqrt(Q);
+            const double t0 = -2 * sqrtQ, t1 = theta * (1. / 3), t2 = a1 * (1. / 3);
+            x0 = t0 * oc_fd_cos(t1) - t2;
+            x1 = t0 * oc_fd_cos(t1 + (2. * 3.1415926535897932384626433832795 / 3)) - t2;
+            x2 = t0 * oc_fd_cos(t1 + (4. * 3.1415926535897932384626433832795 / 3)) - t2;
+            n = 3;
+        } else if (d == 0) {
+            if (R >= 0) { x0 = -2 * fd_pow_pos(R, 1. / 3) - a1 / 3; x1 = fd_pow_pos(R, 1. / 3) - a1 / 3; }
+            else { x0 = 2 * fd_pow_pos(-R, 1. / 3) - a1 / 3; x1 = -fd_pow_pos(-R, 1. / 3) - a1 / 3; }
+            x2 = 0;
+            n = x0 == x1 ? 1 : 2;
+            x1 = x0 == x1 ? 0 : x1;
+        } else {
+            d = sqrt(-d);
+            double e = fd_pow_pos(d + fabs(R), 0.333333333333);
+            if (R > 0) e = -e;
+            x0 = (e + Q / e) - a1 * (1. / 3);
+            n = 1;
+        }
+    }
+    r[0] = x0; r[1] = x1; r[2] = x2;
+    return n;
+}
+
+/* run7Point (fundam.cpp): up to 3 models F[9k..9k+8], returns their count.  The null space of
+ * the 7x9 system comes from Gauss-Jordan elimination with complete pivoting (the first largest
+ * |a| in row-major order over the remaining block) instead of OpenCV's JacobiSVD: the same
+ * two-dimensional space in another basis; every model is scaled to F33 = 1, so the models
+ * agree up to rounding. */
+int oc_run7point(const float* m1, const float* m2, double* F)
+{
+    double A[7][9];
+    int perm[9];
+    for (int i = 0; i < 7; i++) {
+        const double x0 = m1[2 * i], y0 = m1[2 * i + 1], x1 = m2[2 * i], y1 = m2[2 * i + 1];
+        A[i][0] = x1 * x0; A[i][1] = x1 * y0; A[i][2] = x1;
+        A[i][3] = y1 * x0; A[i][4] = y1 * y0; A[i][5] = y1;
+        A[i][6] = x0; A[i][7] = y0; A[i][8] = 1;
+    }
+    for (int j = 0; j < 9; j++) perm[j] = j;
+    for (int r = 0; r < 7; r++) {
+        int pi = r, pj = r;
+        double best = -1.0;
+        for (int i = r; i < 7; i++)
+            for (int j = r; j < 9; j++)
+                if (fabs(A[i][j]) > best) { best = fabs(A[i][j]); pi = i; pj = j; }
+        if (!(best > 0.0)) return 0;
+        if (pi != r)
+            for (int j = 0; j < 9; j++) { const double t = A[r][j]; A[r][j] = A[pi][j]; A[pi][j] = t; }
+        if (pj != r) {
+            for (int i = 0; i < 7; i++) { const double t = A[i][r]; A[i][r] = A[i][pj]; A[i][pj] = t; }
+            const int t = perm[r]; perm[r] = perm[pj]; perm[pj] = t;
+        }
+        for (int i = 0; i < 7; i++) {
+            if (i == r) continue;
+            const double f = A[i][r] / A[r][r];
+            for (int j = r; j < 9; j++) A[i][j] = A[i][j] - f * A[r][j];
+        }
+    }
+    double f1[9], f2[9];
+    for (int q = 0; q < 2; q++) {
+        double* v = q == 0 ? f1 : f2;
+        const int col = 7 + q;
+        v[perm[7]] = q == 0 ? 1.0 : 0.0;
+        v[perm[8]] = q == 0 ? 0.0 : 1.0;
+        for (int i = 0; i < 7; i++) v[perm[i]] = -A[i][col] / A[i][i];
+    }
+    for (int i = 0; i < 9; i++) f1[i] -= f2[i];
+    double c[4], r[3];
+    double t0 = f2[4] * f2[8] - f2[5] * f2[7];
+    double t1 = f2[3] * f2[8] - f2[5] * f2[6];
+    double t2 = f2[3] * f2[7] - f2[4] * f2[6];
+    c[3] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2;
+    c[2] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2 - f1[3] * (f2[1] * f2[8] - f2[2] * f2[7]) +
+           f1[4] * (f2[0] * f2[8] - f2[2] * f2[6]) - f1[5] * (f2[0] * f2[7] - f2[1] * f2[6]) +
+           f1[6] * (f2[1] * f2[5] - f2[2] * f2[4]) - f1[7] * (f2[0] * f2[5] - f2[2] * f2[3]) +
+           f1[8] * (f2[0] * f2[4] - f2[1] * f2[3]);
+    t0 = f1[4] * f1[8] - f1[5] * f1[7];
+    t1 = f1[3] * f1[8] - f1[5] * f1[6];
+    t2 = f1[3] * f1[7] - f1[4] * f1[6];
+    c[1] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2 - f2[3] * (f1[1] * f1[8] - f1[2] * f1[7]) +
+           f2[4] * (f1[0] * f1[8] - f1[2] * f1[6]) - f2[5] * (f1[0] * f1[7] - f1[1] * f1[6]) +
+           f2[6] * (f1[1] * f1[5] - f1[2] * f1[4]) - f2[7] * (f1[0] * f1[5] - f1[2] * f1[3]) +
+           f2[8] * (f1[0] * f1[4] - f1[1] * f1[3]);
+    c[0] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2;
+    const int n = oc_solve_cubic(c, r);
+    if (n < 1 || n > 3) return n;
+    for (int k = 0; k < n; k++) {
+        double* fm = F + 9 * k;
+        double lambda = r[k], mu = 1.;
+        const double s = f1[8] * r[k] + f2[8];
+        if (fabs(s) > DBL_EPSILON) { mu = 1. / s; lambda *= mu; fm[8] = 1.; }
+        else fm[8] = 0.;
+        for (int i = 0; i < 8; i++) fm[i] = f1[i] * lambda + f2[i] * mu;
+    }
+    return n;
+}
+
+/* FMEstimatorCallback::computeError */
+static float fm_error(const double* F, float x1, float y1, float x2, float y2)
+{
+    double a = F[0] * x1 + F[1] * y1 + F[2];
+    double b = F[3] * x1 + F[4] * y1 + F[5];
+    double c = F[6] * x1 + F[7] * y1 + F[8];
+    const double s2 = 1. / (a * a + b * b);
+    const double d2 = x2 * a + y2 * b + c;
+    a = F[0] * x2 + F[3] * y2 + F[6];
+    b = F[1] * x2 + F[4] * y2 + F[7];
+    c = F[2] * x2 + F[5] * y2 + F[8];
+    const double s1 = 1. / (a * a + b * b);
+    const double d1 = x1 * a + y1 * b + c;
+    const double e1 = d1 * d1 * s1, e2 = d2 * d2 * s2;
+    return (float)(e1 < e2 ? e2 : e1);
+}
+
+/* haveCollinearPoints(m, 7): triples that include the last point only (as OpenCV checks) */
+static int fm_collinear(const float* m)
+{
+    const int i = 6;
+    for (int j = 0; j < i; j++) {
+        const double dx1 = (double)(m[2 * j] - m[2 * i]), dy1 = (double)(m[2 * j + 1] - m[2 * i + 1]);
+        for (int k = 0; k < j; k++) {
+            const double dx2 = (double)(m[2 * k] - m[2 * i]), dy2 = (double)(m[2 * k + 1] - m[2 * i + 1]);
+            if (fabs(dx2 * dy1 - dy2 * dx1) <= FLT_EPSILON * (fabs(dx1) + fabs(dy1) + fabs(dx2) + fabs(dy2)))
+                return 1;
+        }
+    }
+    return 0;
+}
+
+static inline unsigned rng_next(uint64_t* st)
+{
+    *st = (uint64_t)(unsigned)*st * 4164903690U + (unsigned)(*st >> 32);
+    return (unsigned)*st;
+}
+
+/* getSubset(m1, m2, ms1, ms2, rng, maxAttempts), checkPartialSubsets = false, checkSubset =
+ * !collinear(ms1) && !collinear(ms2): 1 when a subset was drawn */
+static int fm_subset(const float* m1, const float* m2, int count, uint64_t* rng, int max_attempts, int idx[7],
+                     float s1[14], float s2[14])
+{
+    int iters = 0, i = 0;
+    for (; iters < max_attempts; iters++) {
+        for (i = 0; i < 7 && iters < max_attempts;) {
+            int id;
+            for (;;) {
+                id = idx[i] = (int)(rng_next(rng) % (unsigned)count);
+                int j;
+                for (j = 0; j < i; j++)
+                    if (id == idx[j]) break;
+                if (j == i) break;
+            }
+            s1[2 * i] = m1[2 * id]; s1[2 * i + 1] = m1[2 * id + 1];
+            s2[2 * i] = m2[2 * id]; s2[2 * i + 1] = m2[2 * id + 1];
+            i++;
+        }
+        if (i == 7 && (fm_collinear(s1) || fm_collinear(s2))) continue;
+        break;
+    }
+    return i == 7 && iters < max_attempts;
+}
+
+/* RANSACUpdateNumIters(p, ep, 7, maxIters) */
+int oc_ransac_update_iters(double p, double ep, int max_iters)
+{
+    p = p > 0. ? p : 0.; p = p < 1. ? p : 1.;
+    ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
+    double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
+    double denom = 1. - pow(1. - ep, 7);
+    if (denom < DBL_MIN) return 0;
+    num = log(num);
+    denom = log(denom);
+    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)lrint(num / denom);
+}
+
+/* cv::findFundamentalMat(m1, m2, mask, FM_RANSAC, thr, conf) (Frame.cc:373): returns 1 and F
+ * (row-major 3x3 double; the first model when several are stacked) or 0 for an empty result.
+ * n < 7: empty; n == 7: run7Point; 8..14: LMeDS; >= 15: RANSAC (maxIters 1000). */
+int oc_find_fundamental(const float* m1, const float* m2, int n, double thr, double conf, double F[9])
+{
+    double models[27];
+    if (n < 7) return 0;
+    if (n == 7) {
+        const int k = oc_run7point(m1, m2, models);
+        if (k <= 0) return 0;
+        memcpy(F, models, sizeof(double) * 9);
+        return 1;
+    }
+    uint64_t rng = ~(uint64_t)0;
+    int idx[7];
+    float s1[14], s2[14];
+    if (n >= 15) {
+        int niters = 1000, max_good = 0, have = 0;
+        const float t = (float)(thr * thr);
+        for (int iter = 0; iter < niters; iter++) {
+            if (!fm_subset(m1, m2, n, &rng, 10000, idx, s1, s2)) {
+                if (iter == 0) return 0;
+                break;
+            }
+            const int nm = oc_run7point(s1, s2, models);
+            if (nm <= 0) continue;
+            for (int m = 0; m < nm; m++) {
+                int good = 0;
+                for (int i = 0; i < n; i++)
+                    good += fm_error(models + 9 * m, m1[2 * i], m1[2 * i + 1], m2[2 * i], m2[2 * i + 1]) <= t;
+                if (good > (max_good > 6 ? max_good : 6)) {
+                    memcpy(F, models + 9 * m, sizeof(double) * 9);
+                    max_good = good; have = 1;
+                    niters = oc_ransac_update_iters(conf, (double)(n - good) / n, niters);
+                }
+            }
+        }
+        return have && max_good > 0;
+    }
+    int niters = oc_ransac_update_iters(conf, 0.45, 1000);
+    niters = niters > 3 ? niters : 3;
+    double min_median = DBL_MAX;
+    float err[16];
+    for (int iter = 0; iter < niters; iter++) {
+        if (!fm_subset(m1, m2, n, &rng, 1000, idx, s1, s2)) {
+            if (iter == 0) return 0;
+            break;
+        }
+        const int nm = oc_run7point(s1, s2, models);
+        if (nm <= 0) continue;
+        for (int m = 0; m < nm; m++) {
+            for (int i = 0; i < n; i++) err[i] = fm_error(models + 9 * m, m1[2 * i], m1[2 * i + 1], m2[2 * i], m2[2 * i + 1]);
+            for (int a = 1; a < n; a++) {                     /* nth_element: the value is unique */
+                const float v = err[a];
+                int b = a - 1;
+                while (b >= 0 && err[b] > v) { err[b + 1] = err[b]; b--; }
+                err[b + 1] = v;
+            }
+            const double median = err[n / 2];
+            if (median < min_median) { min_median = median; memcpy(F, models + 9 * m, sizeof(double) * 9); }
+        }
+    }
+    if (!(min_median < DBL_MAX)) return 0;
+    double sigma = 2.5 * 1.4826 * (1 + 5. / (n - 7)) * sqrt(min_median);
+    sigma = sigma > 0.001 ? sigma : 0.001;
+    const float t = (float)(sigma * sigma);
+    int good = 0;
+    for (int i = 0; i < n; i++) good += fm_error(F, m1[2 * i], m1[2 * i + 1], m2[2 * i], m2[2 * i + 1]) <= t;
+    return good >= 7;
+}
+
+/* The SAD consistency check and the epipolar test of Frame::ProcessMovingObject
+ * (Frame.cc:337-384) given the tracked pairs: fills the F_ sets in order, F, and T_M.
+ * Returns |T_M| (written up to tm_cap), or -1 when findFundamentalMat is empty (the reference
+ * then reads an empty Mat: undefined). */
+int oc_moving_tail(const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, const float* pxy,
+                   const float* nxy, uint8_t* state, int n, int edge, double limit, float* tm_xy, int tm_cap,
+                   double F_out[9], int* nf_out)
+{
+    static const int dx[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1}, dy[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
+    float* m1 = (float*)malloc(sizeof(float) * 2 * (n > 0 ? n : 1));
+    float* m2 = (float*)malloc(sizeof(float) * 2 * (n > 0 ? n : 1));
+    int nf = 0;
+    for (int i = 0; i < n; i++) {
+        if (!state[i]) continue;
+        const int x1 = (int)pxy[2 * i], y1 = (int)pxy[2 * i + 1], x2 = (int)nxy[2 * i], y2 = (int)nxy[2 * i + 1];
+        if (x1 < edge || x1 >= w - edge || x2 < edge || x2 >= w - edge || y1 < edge || y1 >= h - edge ||
+            y2 < edge || y2 >= h - edge) {
+            state[i] = 0;
+            continue;
+        }
+        double sum = 0;
+        for (int j = 0; j < 9; j++)
+            sum += abs((int)prev[(size_t)(y1 + dy[j]) * stride + x1 + dx[j]] - (int)cur[(size_t)(y2 + dy[j]) * stride + x2 + dx[j]]);
+        if (sum > limit) state[i] = 0;
+        if (state[i]) {
+            m1[2 * nf] = pxy[2 * i]; m1[2 * nf + 1] = pxy[2 * i + 1];
+            m2[2 * nf] = nxy[2 * i]; m2[2 * nf + 1] = nxy[2 * i + 1];
+            nf++;
+        }
+    }
+    if (nf_out) *nf_out = nf;
+    double F[9];
+    const int ok = oc_find_fundamental(m1, m2, nf, 0.1, 0.99, F);
+    free(m1); free(m2);
+    if (!ok) return -1;
+    if (F_out) memcpy(F_out, F, sizeof(F));
+    int nt = 0;
+    for (int i = 0; i < n; i++) {
+        if (!state[i]) continue;
+        const double px = pxy[2 * i], py = pxy[2 * i + 1];
+        const double A = F[0] * px + F[1] * py + F[2];
+        const double B = F[3] * px + F[4] * py + F[5];
+        const double Cc = F[6] * px + F[7] * py + F[8];
+        const double dd = fabs(A * nxy[2 * i] + B * nxy[2 * i + 1] + Cc) / sqrt(A * A + B * B);
+        if (dd <= 1) continue;
+        if (nt < tm_cap) { tm_xy[2 * nt] = nxy[2 * i]; tm_xy[2 * nt + 1] = nxy[2 * i + 1]; }
+        nt++;
+    }
+    return nt;
+}
+
+/* Frame::ProcessMovingObject (Frame.cc:311-393): T_M from the previous and current gray frames. */
+int oc_process_moving_object(const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, float* tm_xy,
+                             int tm_cap, int* ncorners_out)
+{
+    float* pts = (float*)malloc(sizeof(float) * 2 * 1000);
+    float* nxt = (float*)malloc(sizeof(float) * 2 * 1000);
+    uint8_t* st = (uint8_t*)malloc(1000);
+    int n = oc_good_features_harris(prev, w, h, stride, 1000, 0.01, 8, 0.04, pts, 1000, 1 << 30);
+    if (n > 1000) n = 1000;
+    if (ncorners_out) *ncorners_out = n;
+    oc_corner_subpix(prev, w, h, stride, pts, n, 10, 20, 0.03);
+    oc_lk_pyr(prev, cur, w, h, stride, pts, n, 22, 5, 20, 0.01, nxt, st);
+    const int nt = oc_moving_tail(prev, cur, w, h, stride, pts, nxt, st, n, 5, 2120.0, tm_xy, tm_cap, NULL, NULL);
+    free(pts); free(nxt); free(st);
+    return nt;
+}

@@ -210,6 +210,39 @@ int oc_pose_optimization(const oc_pose_frame* fr, float Tcw[16], uint8_t* outlie
 void oc_undistort_keypoints(const oc_kp* in, int n, float fx, float fy, float cx, float cy, const float dist[5],
                             oc_kp* out);
 
+/* cv::goodFeaturesToTrack(img, corners, maxCorners, qualityLevel, minDistance, Mat(), 3, true, k)
+ * as Frame::ProcessMovingObject calls it (Frame.cc:333): OpenCV 3.4 featureselect.cpp with
+ * cornerHarris (corner.cpp, blockSize 3, Sobel 3x3, BORDER_REFLECT_101) in the canonical forms
+ * of DESIGN.md s2.1.  Writes up to cap (x, y) pairs; returns the corner count, or -1 when more
+ * than max_cand local maxima pass the quality threshold. */
+int oc_good_features_harris(const uint8_t* img, int w, int h, int stride, int max_corners, double quality,
+                            double min_distance, double k, float* out_xy, int cap, int max_cand);
+
+
+/* ---- the rest of Frame::ProcessMovingObject (Frame.cc:334-384), DESIGN.md s4.10 ---- */
+void oc_rect_subpix_8u32f(const uint8_t* img, int w, int h, int stride, int ww, int wh, float cx, float cy,
+                          float* dst);
+void oc_subpix_mask(int win, float* mask);
+void oc_corner_subpix(const uint8_t* img, int w, int h, int stride, float* xy, int n, int win, int max_iter,
+                      double eps);
+void oc_pyr_down(const uint8_t* src, int sw, int sh, uint8_t* dst);
+int oc_lk_levels(int w, int h, int win, int max_level);
+int oc_lk_pyr(const uint8_t* prev, const uint8_t* next, int w, int h, int stride, const float* pxy, int n, int win,
+              int max_level, int max_count, double eps, float* nxy, uint8_t* status);
+double oc_fd_acos(double x);
+double oc_fd_log(double x);
+double oc_fd_exp(double x);
+double oc_fd_cos(double x);
+int oc_solve_cubic(const double c[4], double r[3]);
+int oc_run7point(const float* m1, const float* m2, double* F);
+int oc_ransac_update_iters(double p, double ep, int max_iters);
+int oc_find_fundamental(const float* m1, const float* m2, int n, double thr, double conf, double F[9]);
+int oc_moving_tail(const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, const float* pxy,
+                   const float* nxy, uint8_t* state, int n, int edge, double limit, float* tm_xy, int tm_cap,
+                   double F_out[9], int* nf_out);
+int oc_process_moving_object(const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, float* tm_xy,
+                             int tm_cap, int* ncorners_out);
+
 #ifdef __cplusplus
 }
 #endif
