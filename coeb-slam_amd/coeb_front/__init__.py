@@ -46,7 +46,8 @@ ABI_SYMBOLS = [
     "coeb_profile_reset", "coeb_synchronize", "coeb_device_count", "coeb_debug_read",
     "coeb_device_alloc", "coeb_device_free", "coeb_memcpy_h2d", "coeb_memcpy_d2h", "coeb_set_batch_streams",
     "coeb_match_localmap", "coeb_match_keyframe", "coeb_pose_optimization", "coeb_undistort_keypoints",
-    "coeb_boxes_from_int64",
+    "coeb_boxes_from_int64", "coeb_good_features", "coeb_corner_subpix", "coeb_optical_flow_pyr_lk",
+    "coeb_moving_tail", "coeb_moving_object_points", "coeb_moving_object_points_device",
 ]
 
 
@@ -138,6 +139,21 @@ def lib():
         L.coeb_undistort_keypoints.argtypes = [C.c_void_p, C.POINTER(Camera), C.c_void_p, C.c_void_p, C.c_int,
                                                C.c_void_p]
         L.coeb_boxes_from_int64.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.coeb_good_features.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_int, C.c_double,
+                                         C.c_double, C.c_double, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+        L.coeb_corner_subpix.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_int,
+                                         C.c_int, C.c_int, C.c_double]
+        L.coeb_optical_flow_pyr_lk.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t,
+                                               C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
+                                               C.c_void_p, C.c_void_p]
+        L.coeb_moving_tail.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p,
+                                       C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int),
+                                       C.c_void_p, C.POINTER(C.c_int)]
+        L.coeb_moving_object_points.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t,
+                                                C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_void_p]
+        L.coeb_moving_object_points_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                                       C.c_size_t, C.c_void_p, C.c_int, C.POINTER(C.c_int),
+                                                       C.c_void_p]
         L.coeb_blur_flags.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_int,
                                       C.c_void_p]
         L.coeb_stereo_from_rgbd.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
@@ -593,3 +609,97 @@ class Optimizer:
 def make_camera(fx, fy, cx, cy, bf, w, h):
     """Camera + Frame::ComputeImageBounds for an undistorted image (src/Frame.cc:635-641)."""
     return Camera(fx, fy, cx, cy, bf, 0.0, float(w), 0.0, float(h))
+
+
+# ---- Frame::ProcessMovingObject (src/Frame.cc:311-393) ----
+class FlowDebug(C.Structure):
+    _fields_ = [("corners_raw", C.c_void_p), ("corners", C.c_void_p), ("ncorners", C.c_void_p),
+                ("next_pts", C.c_void_p), ("status", C.c_void_p), ("state", C.c_void_p), ("F", C.c_void_p),
+                ("nf", C.c_void_p)]
+
+
+def _gray(img):
+    img = np.ascontiguousarray(img, np.uint8)
+    if img.ndim != 2:
+        raise ValueError("8UC1 image expected")
+    return img, img.shape[1], img.shape[0]
+
+
+def GoodFeaturesToTrack(ctx, img, max_corners=1000, quality=0.01, min_distance=8.0, k=0.04):
+    """cv::goodFeaturesToTrack(img, corners, maxCorners, quality, minDistance, Mat(), 3, true, k)
+    as Frame.cc:333 calls it: (n, 2) float32."""
+    img, w, h = _gray(img)
+    out = np.zeros((max_corners, 2), np.float32)
+    n = C.c_int(0)
+    ctx.check(lib().coeb_good_features(ctx.h, _p(img), w, h, w, max_corners, quality, min_distance, k, _p(out),
+                                       max_corners, C.byref(n)))
+    return out[:n.value].copy()
+
+
+def CornerSubPix(ctx, img, xy, win=10, max_iter=20, eps=0.03):
+    """cv::cornerSubPix(img, xy, Size(win, win), Size(-1,-1), TermCriteria(ITER|EPS, max_iter, eps))
+    (Frame.cc:334); returns the refined copy."""
+    img, w, h = _gray(img)
+    xy = np.ascontiguousarray(xy, np.float32).copy()
+    ctx.check(lib().coeb_corner_subpix(ctx.h, _p(img), w, h, w, _p(xy), len(xy), win, max_iter, eps))
+    return xy
+
+
+def CalcOpticalFlowPyrLK(ctx, prev, nxt, xy, win=22, max_level=5, max_count=20, eps=0.01):
+    """cv::calcOpticalFlowPyrLK(prev, next, xy, next_xy, status, err, Size(win, win), max_level,
+    TermCriteria(ITER|EPS, max_count, eps)) (Frame.cc:335): (next_xy, status)."""
+    prev, w, h = _gray(prev)
+    nxt = np.ascontiguousarray(nxt, np.uint8)
+    xy = np.ascontiguousarray(xy, np.float32)
+    out = np.zeros_like(xy)
+    st = np.zeros(len(xy), np.uint8)
+    ctx.check(lib().coeb_optical_flow_pyr_lk(ctx.h, _p(prev), _p(nxt), w, h, w, _p(xy), len(xy), win, max_level,
+                                             max_count, eps, _p(out), _p(st)))
+    return out, st
+
+
+def MovingTail(ctx, prev, cur, pxy, nxy, state):
+    """SAD check + cv::findFundamentalMat(FM_RANSAC, 0.1, 0.99) + epipolar test (Frame.cc:337-384):
+    (T_M or None when F is empty, state after the SAD check, F or None, |F_prepoint|)."""
+    prev, w, h = _gray(prev)
+    cur = np.ascontiguousarray(cur, np.uint8)
+    pxy = np.ascontiguousarray(pxy, np.float32)
+    nxy = np.ascontiguousarray(nxy, np.float32)
+    st = np.ascontiguousarray(state, np.uint8).copy()
+    tm = np.zeros((max(len(pxy), 1), 2), np.float32)
+    F = np.zeros(9, np.float64)
+    nt, nf = C.c_int(0), C.c_int(0)
+    ctx.check(lib().coeb_moving_tail(ctx.h, _p(prev), _p(cur), w, h, w, _p(pxy), _p(nxy), _p(st), len(pxy), _p(tm),
+                                     len(tm), C.byref(nt), _p(F), C.byref(nf)))
+    if nt.value < 0:
+        return None, st, None, nf.value
+    return tm[:nt.value].copy(), st, F.reshape(3, 3), nf.value
+
+
+def ProcessMovingObject(ctx, prev, cur, debug=False):
+    """Frame::ProcessMovingObject(imgray, box) with imGrayPre = prev (Frame.cc:311-393): T_M as
+    (m, 2) float32, or None when findFundamentalMat returns an empty Mat.  debug=True also
+    returns the stage outputs (dict)."""
+    prev, w, h = _gray(prev)
+    cur = np.ascontiguousarray(cur, np.uint8)
+    tm = np.zeros((1024, 2), np.float32)
+    nt = C.c_int(0)
+    dbg, arrays = None, None
+    if debug:
+        arrays = dict(corners_raw=np.zeros((1000, 2), np.float32), corners=np.zeros((1000, 2), np.float32),
+                      ncorners=np.zeros(1, np.int32), next_pts=np.zeros((1000, 2), np.float32),
+                      status=np.zeros(1000, np.uint8), state=np.zeros(1000, np.uint8), F=np.zeros(9, np.float64),
+                      nf=np.zeros(1, np.int32))
+        dbg = FlowDebug(**{k: _p(v) for k, v in arrays.items()})
+    ctx.check(lib().coeb_moving_object_points(ctx.h, _p(prev), _p(cur), w, h, w, _p(tm), len(tm), C.byref(nt),
+                                              C.byref(dbg) if dbg is not None else None))
+    res = None if nt.value < 0 else tm[:nt.value].copy()
+    if not debug:
+        return res
+    n = int(arrays["ncorners"][0])
+    arrays["ncorners"] = n
+    arrays["nf"] = int(arrays["nf"][0])
+    for k in ("corners_raw", "corners", "next_pts", "status", "state"):
+        arrays[k] = arrays[k][:n]
+    arrays["F"] = arrays["F"].reshape(3, 3)
+    return res, arrays

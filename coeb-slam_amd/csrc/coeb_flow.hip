@@ -1,32 +1,62 @@
 // coeb_flow.hip -- Frame::ProcessMovingObject (src/Frame.cc:311-393), the T_M generation of the
-// dynamic filter.  Built so far: the corner detector it starts with,
-//   cv::goodFeaturesToTrack(imGrayPre, prepoint, 1000, 0.01, 8, Mat(), 3, true, 0.04)  (:333)
-// as OpenCV 3.4 computes it (featureselect.cpp; cornerHarris in corner.cpp), in the canonical
-// forms the oracle restates (oc_good_features_harris):
-//   k_gf_response  per pixel: Sobel 3x3 (REFLECT_101) scaled by 1/3060, cov products, the
-//                  unnormalised 3x3 box (row sums then column sum), Harris R in float with the
-//                  k term in double; the image maximum by an ordered-int atomicMax
-//   k_gf_candidates per pixel: threshold TOZERO at (float)(max * quality), 3x3 dilation, local
-//                  maxima appended as (ordered value, index) keys
-//   k_gf_select    one workgroup: bitonic sort of the keys (value desc, index desc =
-//                  greaterThanPtr), then the greedy minDistance selection over an 8-px cell grid
-//                  in LDS, one candidate at a time (the reference's order is sequential)
+// dynamic filter, as OpenCV 3.4 computes each call, in the canonical
+// forms the oracle restates (oracle/orb_oracle.c):
+//
+//   goodFeaturesToTrack(imGrayPre, prepoint, 1000, 0.01, 8, Mat(), 3, true, 0.04)     (:333)
+//     k_gf_response    per pixel: Sobel 3x3 (REFLECT_101) / 3060, cov products, unnormalised 3x3
+//                      box, Harris R (k term in double); image max by ordered-int atomicMax
+//     k_gf_candidates  per pixel: TOZERO at (float)(max*quality), 3x3 dilation, local maxima as
+//                      (ordered value, index) keys
+//     k_gf_select      one workgroup: bitonic sort of the keys in LDS (value desc, index desc =
+//                      greaterThanPtr), then the greedy minDistance selection solved as a
+//                      fixpoint (candidate accepted <=> no accepted earlier candidate closer than
+//                      minDistance), which equals the sequential loop; the first maxCorners kept
+//   cornerSubPix(imGrayPre, prepoint, Size(10,10), Size(-1,-1), (ITER|EPS, 20, 0.03))   (:334)
+//     k_subpix         one wave per corner: getRectSubPix 23x23 (8u32f) into LDS in parallel,
+//                      the five gradient sums in double in the reference's order (one lane each)
+//   calcOpticalFlowPyrLK(imGrayPre, imgray, .., Size(22,22), 5, (ITER|EPS, 20, 0.01))   (:335)
+//     k_pyr_down       pyrDown 5x5 [1 4 6 4 1]^2 per level, both frames in one launch
+//     k_sharr          calcSharrDeriv of every level of the previous frame in one launch
+//     k_lk             one wave per point, levels coarse to fine; 484-pixel window sums exact in
+//                      int64 (8 pixels per lane, wave reduction)
+//   SAD check (:337-365), findFundamentalMat(.., FM_RANSAC, 0.1, 0.99) (:373), epipolar
+//   distance > 1 -> T_M (:375-384)
+//     k_fm             one workgroup: SAD filter + ordered compaction into LDS, RANSAC in
+//                      chunks of 32 hypotheses (RNG draws on lane 0, 7-point solves on 32
+//                      lanes, inlier counts one wave per model, the reference's sequential
+//                      best-model / niters scan on lane 0), LMeDS for 8..14 pairs, the
+//                      epipolar test and ordered T_M compaction
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <cmath>
+#include <cstring>
 
+#include "../../include/coeb_front.h"
 #include "coeb_internal.hpp"
+
+extern "C" int coeb_internal_stream(coeb_ctx* c, hipStream_t* s, int* device);
+extern "C" int coeb_internal_scratch(coeb_ctx* c, const char* name, size_t bytes, void** p);
+extern "C" int coeb_internal_error(coeb_ctx* c, int code, const char* msg);
 
 namespace {
 
-__device__ __forceinline__ int gf_reflect(int p, int n)
+constexpr int kMaxPts = 1024;        // corners / tracked points per call (reference: 1000)
+constexpr int kGfThreads = 1024;
+constexpr int kGfSortMax = 16384;    // local maxima sorted in LDS (128 KB)
+constexpr int kGfCellCap = 64;       // an 8x8 cell holds at most 64 maxima
+constexpr int kLkMaxLevels = 8;
+constexpr int kFmThreads = 1024;
+constexpr int kFmChunk = 32;         // RANSAC hypotheses per chunk
+
+__device__ __forceinline__ int reflect101(int p, int n)
 {
     if (n == 1) return 0;
     while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - p - 2;
     return p;
 }
 
-// float -> uint order-preserving (for atomicMax and descending sorts)
+// float -> uint order-preserving (atomicMax, descending sorts)
 __device__ __forceinline__ uint32_t f2ord(float f)
 {
     const uint32_t u = __float_as_uint(f);
@@ -37,6 +67,13 @@ __device__ __forceinline__ float ord2f(uint32_t o)
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
+__device__ __forceinline__ int cv_floor(float v)
+{
+    const int i = (int)v;
+    return i - (i > v);
+}
+
+// ============================== goodFeaturesToTrack ==============================
 __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__ img, int w, int h, int stride, double k,
                                                      float* __restrict__ R, uint32_t* __restrict__ rmax)
 {
@@ -46,13 +83,13 @@ __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__
         const double scale = 1.0 / (4.0 * 3.0 * 255.0);
         float A[3][3], B[3][3], C[3][3];
         for (int j = 0; j < 3; j++) {
-            const int yy = gf_reflect(y + j - 1, h);
+            const int yy = reflect101(y + j - 1, h);
             for (int i = 0; i < 3; i++) {
-                const int xx = gf_reflect(x + i - 1, w);
+                const int xx = reflect101(x + i - 1, w);
                 int p[3][3];
                 for (int b = 0; b < 3; b++)
                     for (int a = 0; a < 3; a++)
-                        p[b][a] = img[(size_t)gf_reflect(yy + b - 1, h) * stride + gf_reflect(xx + a - 1, w)];
+                        p[b][a] = img[(size_t)reflect101(yy + b - 1, h) * stride + reflect101(xx + a - 1, w)];
                 const int gx = (p[0][2] - p[0][0]) + 2 * (p[1][2] - p[1][0]) + (p[2][2] - p[2][0]);
                 const int gy = (p[2][0] - p[0][0]) + 2 * (p[2][1] - p[0][1]) + (p[2][2] - p[0][2]);
                 const float dx = (float)((double)gx * scale), dy = (float)((double)gy * scale);
@@ -70,7 +107,6 @@ __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__
         r = (float)((double)ac - (k * (double)apc) * (double)apc);
         R[(size_t)y * w + x] = r;
     }
-    // block max, then one atomic per block
     __shared__ uint32_t s_m[4];
     uint32_t o = f2ord(r);
     for (int off = 32; off >= 1; off >>= 1) o = max(o, (uint32_t)__shfl_xor((int)o, off, 64));
@@ -100,15 +136,35 @@ __global__ __launch_bounds__(256) void k_gf_candidates(const float* __restrict__
     if (pos < cap) keys[pos] = ((uint64_t)f2ord(v) << 32) | (uint32_t)(y * w + x);   // larger = earlier
 }
 
-constexpr int kGfThreads = 1024;
-constexpr int kGfSortMax = 16384;          // keys sorted in LDS (128 KB)
+// block-wide exclusive prefix of one flag per thread (1024 threads); returns the total
+__device__ int block_scan_1024(int flag, int* s_w, int& excl)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t b = __ballot(flag);
+    const int before = __popcll(b & ((1ull << lane) - 1ull));
+    __syncthreads();
+    if (lane == 0) s_w[wv] = __popcll(b);
+    __syncthreads();
+    int base = 0, total = 0;
+    for (int i = 0; i < 16; i++) {
+        base += i < wv ? s_w[i] : 0;
+        total += s_w[i];
+    }
+    excl = base + before;
+    return total;
+}
 
+// K[i] after the sort: low 32 bits pixel index; the selection reuses the high word as the state
+// (0 undecided, 1 accepted, 2 rejected).
 __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __restrict__ keys, const int* __restrict__ nkeys,
-                                                         int w, int h, int max_corners, float min_distance, int cell,
-                                                         float* __restrict__ out_xy, int* __restrict__ nout, int cap)
+                                                         int w, int h, int max_corners, float md2, int cell,
+                                                         uint16_t* __restrict__ cell_list, float* __restrict__ out_xy,
+                                                         int* __restrict__ nout, int cap)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t* K = reinterpret_cast<uint64_t*>(smem);
+    __shared__ int s_w[16];
+    __shared__ int s_changed, s_undecided;
     const int tid = threadIdx.x;
     const int n = *nkeys;
     if (n > kGfSortMax) {
@@ -118,8 +174,10 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
     int np = 1;
     while (np < n) np <<= 1;
     for (int i = tid; i < np; i += kGfThreads) K[i] = i < n ? keys[i] : 0ull;
+    const int gw = (w + cell - 1) / cell, gh = (h + cell - 1) / cell;
+    uint32_t* gcnt = reinterpret_cast<uint32_t*>(K + (np > 1 ? np : 2));
+    for (int g = tid; g < gw * gh; g += kGfThreads) gcnt[g] = 0;
     __syncthreads();
-    // bitonic sort, descending
     for (int size = 2; size <= np; size <<= 1)
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
             for (int i = tid; i < np; i += kGfThreads) {
@@ -132,74 +190,1307 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
             }
             __syncthreads();
         }
-    // greedy selection (featureselect.cpp minDistance loop): wave 0, lanes 0..8 test the 3x3 cells
-    const int gw = (w + cell - 1) / cell, gh = (h + cell - 1) / cell;
-    constexpr int kSlots = 16;
-    uint32_t* gcnt = reinterpret_cast<uint32_t*>(K + np);               // [gw*gh]
-    float2* gpt = reinterpret_cast<float2*>(gcnt + ((gw * gh + 3) & ~3)); // [gw*gh][kSlots]
-    for (int g = tid; g < gw * gh; g += kGfThreads) gcnt[g] = 0;
-    __syncthreads();
-    if (tid >= 64) return;
-    const float md2 = min_distance * min_distance;
-    int cnt = 0;
-    for (int i = 0; i < n; i++) {
-        if (max_corners > 0 && cnt >= max_corners) break;
-        const int idx = (int)(uint32_t)(K[i] & 0xffffffffu);
+    // cell lists of ranks (order inside a list is irrelevant: ranks are compared)
+    for (int i = tid; i < n; i += kGfThreads) {
+        const int idx = (int)(uint32_t)K[i];
         const int y = idx / w, x = idx - y * w;
-        const int xc = x / cell, yc = y / cell;
-        bool bad = false;
-        if (tid < 9) {
-            const int xx = xc - 1 + tid % 3, yy = yc - 1 + tid / 3;
-            if (xx >= 0 && yy >= 0 && xx < gw && yy < gh) {
-                const int g = yy * gw + xx;
-                const int m = (int)gcnt[g];
-                for (int j = 0; j < m; j++) {
-                    const float2 p = gpt[g * kSlots + j];
-                    const float ddx = (float)x - p.x, ddy = (float)y - p.y;
-                    if (ddx * ddx + ddy * ddy < md2) bad = true;
+        const int g = (y / cell) * gw + x / cell;
+        const uint32_t pos = atomicAdd(&gcnt[g], 1u);
+        if (pos < (uint32_t)kGfCellCap) cell_list[(size_t)g * kGfCellCap + pos] = (uint16_t)i;
+        K[i] = (uint64_t)(uint32_t)idx;
+    }
+    __syncthreads();
+    // fixpoint: accept when every earlier conflicting candidate is rejected, reject when one is
+    // accepted; the lowest undecided rank is decided in every round
+    for (;;) {
+        if (tid == 0) { s_changed = 0; s_undecided = 0; }
+        __syncthreads();
+        for (int i = tid; i < n; i += kGfThreads) {
+            const uint64_t ki = K[i];
+            if ((ki >> 32) != 0) continue;
+            const int idx = (int)(uint32_t)ki;
+            const int y = idx / w, x = idx - y * w;
+            const int xc = x / cell, yc = y / cell;
+            bool pending = false, hit = false;
+            for (int yy = max(yc - 1, 0); yy <= min(yc + 1, gh - 1) && !hit; yy++)
+                for (int xx = max(xc - 1, 0); xx <= min(xc + 1, gw - 1) && !hit; xx++) {
+                    const int g = yy * gw + xx;
+                    const int m = min((int)gcnt[g], kGfCellCap);
+                    for (int q = 0; q < m; q++) {
+                        const int j = cell_list[(size_t)g * kGfCellCap + q];
+                        if (j >= i) continue;
+                        const uint64_t kj = K[j];
+                        const uint32_t st = (uint32_t)(kj >> 32);
+                        if (st == 2) continue;
+                        const int jdx = (int)(uint32_t)kj;
+                        const int jy = jdx / w, jx = jdx - jy * w;
+                        const float ddx = (float)x - (float)jx, ddy = (float)y - (float)jy;
+                        if (!(ddx * ddx + ddy * ddy < md2)) continue;
+                        if (st == 1) { hit = true; break; }
+                        pending = true;
+                    }
                 }
+            if (hit) { K[i] = ki | (2ull << 32); s_changed = 1; }
+            else if (!pending) { K[i] = ki | (1ull << 32); s_changed = 1; }
+            else s_undecided = 1;
+        }
+        __syncthreads();
+        const bool again = s_changed && s_undecided;
+        const bool stuck = !s_changed && s_undecided;
+        __syncthreads();
+        if (stuck) {                   // cannot happen (see above); fail loudly rather than spin
+            if (tid == 0) *nout = -2;
+            return;
+        }
+        if (!again) break;
+    }
+    // accepted candidates in rank order, the first max_corners
+    int base = 0;
+    for (int c0 = 0; c0 < n; c0 += kGfThreads) {
+        const int i = c0 + tid;
+        const int acc = i < n && (uint32_t)(K[i] >> 32) == 1u;
+        int excl;
+        const int tot = block_scan_1024(acc, s_w, excl);
+        if (acc) {
+            const int pos = base + excl;
+            if ((max_corners <= 0 || pos < max_corners) && pos < cap) {
+                const int idx = (int)(uint32_t)K[i];
+                const int y = idx / w, x = idx - y * w;
+                out_xy[2 * pos] = (float)x;
+                out_xy[2 * pos + 1] = (float)y;
             }
         }
-        if (__ballot(bad) == 0) {
-            if (tid == 0) {
-                const int g = yc * gw + xc;
-                const int m = (int)gcnt[g];
-                if (m < kSlots) gpt[g * kSlots + m] = make_float2((float)x, (float)y);
-                gcnt[g] = m + 1;
-                if (cnt < cap) { out_xy[2 * cnt] = (float)x; out_xy[2 * cnt + 1] = (float)y; }
+        base += tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        int cnt = max_corners > 0 ? min(base, max_corners) : base;
+        bool overflow = false;
+        for (int g = 0; g < gw * gh; g++) overflow |= gcnt[g] > (uint32_t)kGfCellCap;
+        *nout = overflow ? -3 : min(cnt, cap);
+    }
+}
+
+// ============================== cornerSubPix ==============================
+// one wave per corner; LDS per wave: the 23x23 sub-pixel window and the five addend arrays
+template <int WIN>
+__global__ __launch_bounds__(256) void k_subpix(const uint8_t* __restrict__ img, int w, int h, int stride,
+                                                float* __restrict__ xy, const int* __restrict__ d_n, int nmax,
+                                                const float* __restrict__ mask, int iters, double eps2)
+{
+    constexpr int WW = 2 * WIN + 1, BW = WW + 2, NB = BW * BW, NK = WW * WW;
+    __shared__ float s_buf[4][NB];
+    __shared__ double s_t[4][5][NK];
+    __shared__ double s_sum[4][5];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int p = blockIdx.x * 4 + wv;
+    int n = *d_n;
+    n = n < nmax ? n : nmax;
+    if (p >= n) return;
+    float* buf = s_buf[wv];
+    const float tx = xy[2 * p], ty = xy[2 * p + 1];
+    float cx = tx, cy = ty;
+    int it = 0;
+    double err = 0;
+    do {
+        // getRectSubPix(src, Size(BW, BW), (cx, cy), 32F)
+        const float ctrx = cx - (float)(BW - 1) * 0.5f, ctry = cy - (float)(BW - 1) * 0.5f;
+        const int ipx = cv_floor(ctrx), ipy = cv_floor(ctry);
+        if (ipx >= 0 && ipx + BW < w && ipy >= 0 && ipy + BW < h) {
+            float a = ctrx - (float)ipx;
+            const float b = ctry - (float)ipy;
+            a = a < 0.0001f ? 0.0001f : a;
+            const float a12 = a * (1.f - b), a22 = a * b, b1 = 1.f - b, b2 = b;
+            const double s = (1. - (double)a) / (double)a;
+            for (int e = lane; e < NB; e += 64) {
+                const int r = e / BW, j = e - r * BW;
+                const uint8_t* src = img + (size_t)(ipy + r) * stride + ipx;
+                const float t = a12 * (float)src[j + 1] + a22 * (float)src[j + 1 + stride];
+                float prev;
+                if (j == 0) prev = (1.f - a) * (b1 * (float)src[0] + b2 * (float)src[stride]);
+                else {
+                    const float tp = a12 * (float)src[j] + a22 * (float)src[j + stride];
+                    prev = (float)((double)tp * s);
+                }
+                buf[e] = prev + t;
             }
-            cnt++;
+        } else {
+            const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
+            const float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
+            const float b1 = 1.f - b, b2 = b;
+            for (int e = lane; e < NB; e += 64) {
+                const int r = e / BW, j = e - r * BW;
+                const int y0 = min(max(ipy + r, 0), h - 1), y1 = min(max(ipy + r + 1, 0), h - 1);
+                const uint8_t* r0 = img + (size_t)y0 * stride;
+                const uint8_t* r1 = img + (size_t)y1 * stride;
+                const int c = ipx + j;
+                float v;
+                if (c < 0) v = (float)r0[0] * b1 + (float)r1[0] * b2;
+                else if (c >= w - 1) v = (float)r0[w - 1] * b1 + (float)r1[w - 1] * b2;
+                else v = (float)r0[c] * a11 + (float)r0[c + 1] * a12 + (float)r1[c] * a21 + (float)r1[c + 1] * a22;
+                buf[e] = v;
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int k = lane; k < NK; k += 64) {
+            const int i = k / WW, j = k - i * WW;
+            const float* sp = buf + (i + 1) * BW + 1;
+            const double m = mask[k];
+            const double tgx = (double)(sp[j + 1] - sp[j - 1]);
+            const double tgy = (double)(sp[j + BW] - sp[j - BW]);
+            const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
+            const double px = j - WIN, py = i - WIN;
+            s_t[wv][0][k] = gxx;
+            s_t[wv][1][k] = gxy;
+            s_t[wv][2][k] = gyy;
+            s_t[wv][3][k] = gxx * px + gxy * py;
+            s_t[wv][4][k] = gxy * px + gyy * py;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (lane < 5) {
+            const double* t = s_t[wv][lane];
+            double acc = 0;
+            for (int k = 0; k < NK; k++) acc += t[k];
+            s_sum[wv][lane] = acc;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const double sa = s_sum[wv][0], sb = s_sum[wv][1], sc = s_sum[wv][2], bb1 = s_sum[wv][3], bb2 = s_sum[wv][4];
+        const double det = sa * sc - sb * sb;
+        if (fabs(det) <= DBL_EPSILON * DBL_EPSILON) break;
+        const double scale = 1.0 / det;
+        const float nx = (float)((double)cx + sc * scale * bb1 - sb * scale * bb2);
+        const float ny = (float)((double)cy - sb * scale * bb1 + sa * scale * bb2);
+        err = (double)((nx - cx) * (nx - cx) + (ny - cy) * (ny - cy));
+        cx = nx; cy = ny;
+        if (cx < 0 || cx >= (float)w || cy < 0 || cy >= (float)h) break;
+    } while (++it < iters && err > eps2);
+    if (fabsf(cx - tx) > (float)WIN || fabsf(cy - ty) > (float)WIN) { cx = tx; cy = ty; }
+    if (lane == 0) { xy[2 * p] = cx; xy[2 * p + 1] = cy; }
+}
+
+// ============================== pyramidal Lucas-Kanade ==============================
+struct LkPyr {
+    const uint8_t* P[kLkMaxLevels];   // previous frame levels (level 0 = the input, pitch stride)
+    const uint8_t* N[kLkMaxLevels];   // next frame levels
+    const short2* D[kLkMaxLevels];    // Scharr (dx, dy) of the previous frame levels
+    int pitch[kLkMaxLevels];          // image pitch per level
+    int w[kLkMaxLevels], h[kLkMaxLevels];
+    int L;
+};
+
+struct PyrDownArgs {
+    const uint8_t* src[2];
+    uint8_t* dst[2];
+    int sw, sh, spitch, dw, dh;
+};
+
+// pyrDown 8U (5x5 [1 4 6 4 1]^2, (sum + 128) >> 8, REFLECT_101); blockIdx.z = frame
+__global__ __launch_bounds__(256) void k_pyr_down(PyrDownArgs a)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= a.dw || y >= a.dh) return;
+    const uint8_t* src = a.src[blockIdx.z];
+    int cols[5];
+    for (int j = 0; j < 5; j++) cols[j] = reflect101(2 * x + j - 2, a.sw);
+    const int k[5] = {1, 4, 6, 4, 1};
+    int acc = 0;
+    for (int i = 0; i < 5; i++) {
+        const uint8_t* row = src + (size_t)reflect101(2 * y + i - 2, a.sh) * a.spitch;
+        int hs = 0;
+        for (int j = 0; j < 5; j++) hs += k[j] * row[cols[j]];
+        acc += k[i] * hs;
     }
-    if (tid == 0) *nout = cnt;
+    a.dst[blockIdx.z][(size_t)y * a.dw + x] = (uint8_t)((acc + 128) >> 8);
+}
+
+// calcSharrDeriv of every previous-frame level; blockIdx.y = level, grid-stride over pixels
+__global__ __launch_bounds__(256) void k_sharr(LkPyr pyr)
+{
+    const int l = blockIdx.y;
+    const int w = pyr.w[l], h = pyr.h[l], pitch = pyr.pitch[l];
+    const uint8_t* img = pyr.P[l];
+    short2* d = const_cast<short2*>(pyr.D[l]);
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < w * h; e += gridDim.x * 256) {
+        const int y = e / w, x = e - y * w;
+        const uint8_t* s0 = img + (size_t)(y > 0 ? y - 1 : (h > 1 ? 1 : 0)) * pitch;
+        const uint8_t* s1 = img + (size_t)y * pitch;
+        const uint8_t* s2 = img + (size_t)(y < h - 1 ? y + 1 : (h > 1 ? h - 2 : 0)) * pitch;
+        auto col = [&](int c) {             // trow border: trow[-1] = trow[1], trow[w] = trow[w-2]
+            if (c < 0) return w > 1 ? 1 : 0;
+            if (c >= w) return w > 1 ? w - 2 : 0;
+            return c;
+        };
+        const int xl = col(x - 1), xr = col(x + 1);
+        const int t0l = (s0[xl] + s2[xl]) * 3 + s1[xl] * 10, t0r = (s0[xr] + s2[xr]) * 3 + s1[xr] * 10;
+        const int t1l = s2[xl] - s0[xl], t1r = s2[xr] - s0[xr], t1c = s2[x] - s0[x];
+        d[e] = make_short2((short)(t0r - t0l), (short)((t1r + t1l) * 3 + t1c * 10));
+    }
+}
+
+__device__ __forceinline__ int64_t wave_sum64(int64_t v)
+{
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ __forceinline__ int refl1(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
+
+// one wave per point; every lane carries up to 8 window pixels (win*win <= 512)
+__global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__ pxy, const int* __restrict__ d_n, int nmax,
+                                            float* __restrict__ nxy, uint8_t* __restrict__ status, int win, int max_count,
+                                            double eps2)
+{
+    constexpr int PPL = 8;
+    const int lane = threadIdx.x & 63;
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    int n = *d_n;
+    n = n < nmax ? n : nmax;
+    if (p >= n) return;
+    const int npx = win * win;
+    const float hw = (float)(win - 1) * 0.5f;
+    const float FLT_SCALE = 1.f / (1 << 20);
+    int st = 1;
+    float nx = 0.f, ny = 0.f;
+    const float px0 = pxy[2 * p], py0 = pxy[2 * p + 1];
+    int iv[PPL], gxv[PPL], gyv[PPL];
+    for (int level = pyr.L - 1; level >= 0; level--) {
+        const int lw = pyr.w[level], lh = pyr.h[level], pitch = pyr.pitch[level];
+        const uint8_t* I = pyr.P[level];
+        const uint8_t* J = pyr.N[level];
+        const short2* D = pyr.D[level];
+        const float sc = (float)(1. / (1 << level));
+        float px = px0 * sc, py = py0 * sc;
+        if (level == pyr.L - 1) { nx = px; ny = py; }
+        else { nx = nx * 2.f; ny = ny * 2.f; }
+        px -= hw; py -= hw;
+        const int ipx = cv_floor(px), ipy = cv_floor(py);
+        if (ipx < -win || ipx >= lw || ipy < -win || ipy >= lh) {
+            if (level == 0) st = 0;
+            continue;
+        }
+        float a = px - (float)ipx, b = py - (float)ipy;
+        int iw00 = (int)rintf((1.f - a) * (1.f - b) * 16384.f);
+        int iw01 = (int)rintf(a * (1.f - b) * 16384.f);
+        int iw10 = (int)rintf((1.f - a) * b * 16384.f);
+        int iw11 = 16384 - iw00 - iw01 - iw10;
+        int64_t sA11 = 0, sA12 = 0, sA22 = 0;
+#pragma unroll
+        for (int q = 0; q < PPL; q++) {
+            const int e = lane + 64 * q;
+            iv[q] = 0; gxv[q] = 0; gyv[q] = 0;
+            if (e < npx) {
+                const int yy = e / win, xx = e - yy * win;
+                const int X = ipx + xx, Y = ipy + yy;
+                const int x0 = refl1(X, lw), x1 = refl1(X + 1, lw);
+                const uint8_t* r0 = I + (size_t)refl1(Y, lh) * pitch;
+                const uint8_t* r1 = I + (size_t)refl1(Y + 1, lh) * pitch;
+                iv[q] = (r0[x0] * iw00 + r0[x1] * iw01 + r1[x0] * iw10 + r1[x1] * iw11 + (1 << 8)) >> 9;
+                auto dv = [&](int xq, int yq) {
+                    return (xq < 0 || yq < 0 || xq >= lw || yq >= lh) ? make_short2(0, 0) : D[(size_t)yq * lw + xq];
+                };
+                const short2 d00 = dv(X, Y), d01 = dv(X + 1, Y), d10 = dv(X, Y + 1), d11 = dv(X + 1, Y + 1);
+                gxv[q] = (d00.x * iw00 + d01.x * iw01 + d10.x * iw10 + d11.x * iw11 + (1 << 13)) >> 14;
+                gyv[q] = (d00.y * iw00 + d01.y * iw01 + d10.y * iw10 + d11.y * iw11 + (1 << 13)) >> 14;
+                sA11 += (int64_t)gxv[q] * gxv[q];
+                sA12 += (int64_t)gxv[q] * gyv[q];
+                sA22 += (int64_t)gyv[q] * gyv[q];
+            }
+        }
+        sA11 = wave_sum64(sA11); sA12 = wave_sum64(sA12); sA22 = wave_sum64(sA22);
+        const float A11 = (float)sA11 * FLT_SCALE, A12 = (float)sA12 * FLT_SCALE, A22 = (float)sA22 * FLT_SCALE;
+        float D2 = A11 * A22 - A12 * A12;
+        const float minEig = ((A22 + A11) - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
+        if (minEig < 1e-4f || D2 < FLT_EPSILON) {
+            if (level == 0) st = 0;
+            continue;
+        }
+        D2 = 1.f / D2;
+        float lx = nx - hw, ly = ny - hw;
+        float pdx = 0.f, pdy = 0.f;
+        for (int j = 0; j < max_count; j++) {
+            const int inx = cv_floor(lx), iny = cv_floor(ly);
+            if (inx < -win || inx >= lw || iny < -win || iny >= lh) {
+                if (level == 0) st = 0;
+                break;
+            }
+            a = lx - (float)inx; b = ly - (float)iny;
+            iw00 = (int)rintf((1.f - a) * (1.f - b) * 16384.f);
+            iw01 = (int)rintf(a * (1.f - b) * 16384.f);
+            iw10 = (int)rintf((1.f - a) * b * 16384.f);
+            iw11 = 16384 - iw00 - iw01 - iw10;
+            int64_t ib1 = 0, ib2 = 0;
+#pragma unroll
+            for (int q = 0; q < PPL; q++) {
+                const int e = lane + 64 * q;
+                if (e < npx) {
+                    const int yy = e / win, xx = e - yy * win;
+                    const int X = inx + xx, Y = iny + yy;
+                    const int x0 = refl1(X, lw), x1 = refl1(X + 1, lw);
+                    const uint8_t* r0 = J + (size_t)refl1(Y, lh) * pitch;
+                    const uint8_t* r1 = J + (size_t)refl1(Y + 1, lh) * pitch;
+                    const int diff = ((r0[x0] * iw00 + r0[x1] * iw01 + r1[x0] * iw10 + r1[x1] * iw11 + (1 << 8)) >> 9) - iv[q];
+                    ib1 += (int64_t)diff * gxv[q];
+                    ib2 += (int64_t)diff * gyv[q];
+                }
+            }
+            ib1 = wave_sum64(ib1); ib2 = wave_sum64(ib2);
+            const float b1 = (float)ib1 * FLT_SCALE, b2 = (float)ib2 * FLT_SCALE;
+            const float dx = (A12 * b2 - A22 * b1) * D2, dy = (A12 * b1 - A11 * b2) * D2;
+            lx += dx; ly += dy;
+            nx = lx + hw; ny = ly + hw;
+            if ((double)dx * dx + (double)dy * dy <= eps2) break;
+            if (j > 0 && fabsf(dx + pdx) < 0.01 && fabsf(dy + pdy) < 0.01) {
+                nx -= dx * 0.5f; ny -= dy * 0.5f;
+                break;
+            }
+            pdx = dx; pdy = dy;
+        }
+        if (level == 0 && st) {
+            const float ex = nx - hw, ey = ny - hw;
+            const int iex = cv_floor(ex), iey = cv_floor(ey);
+            if (iex < -win || iex >= lw || iey < -win || iey >= lh) st = 0;
+        }
+    }
+    if (lane == 0) {
+        nxy[2 * p] = nx;
+        nxy[2 * p + 1] = ny;
+        status[p] = (uint8_t)st;
+    }
+}
+
+// ============================== findFundamentalMat + T_M ==============================
+// canonical double acos / log / exp (fdlibm) and cos (the pose kernel's Cody-Waite series)
+__constant__ double kFlSin[14] = {0x1.0000000000000p+0, -0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13,
+                                  0x1.71de3a556c734p-19, -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41,
+                                  0x1.952c77030ad4ap-49, -0x1.2f49b46814157p-57, 0x1.71b8ef6dcf572p-66, -0x1.761b413163819p-75,
+                                  0x1.3f3ccdd165fa9p-84, -0x1.d1ab1c2dccea3p-94};
+__constant__ double kFlCos[14] = {0x1.0000000000000p+0, -0x1.0000000000000p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10,
+                                  0x1.a01a01a01a01ap-16, -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37,
+                                  0x1.ae7f3e733b81fp-45, -0x1.6827863b97d97p-53, 0x1.e542ba4020225p-62, -0x1.0ce396db7f853p-70,
+                                  0x1.f2cf01972f578p-80, -0x1.88e85fc6a4e59p-89};
+
+__device__ double fl_cos(double x)
+{
+    const double k = floor(x * 0.63661977236758134308 + 0.5);
+    const double r = (x - k * 1.57079632673412561417e+00) - k * 6.07710050650619224932e-11;
+    const double r2 = r * r;
+    double ps = kFlSin[13], pc = kFlCos[13];
+    for (int n = 12; n >= 0; n--) {
+        ps = ps * r2 + kFlSin[n];
+        pc = pc * r2 + kFlCos[n];
+    }
+    const double s0 = r * ps, c0 = pc;
+    const int q = ((int)(long)k) & 3;
+    return q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
+}
+
+__device__ __forceinline__ uint32_t fd_hi(double x) { return (uint32_t)((uint64_t)__double_as_longlong(x) >> 32); }
+__device__ __forceinline__ uint32_t fd_lo(double x) { return (uint32_t)(uint64_t)__double_as_longlong(x); }
+__device__ __forceinline__ double fd_make(uint32_t hi, uint32_t lo)
+{
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ double fd_acos(double x)
+{
+    const double pi = 0x1.921fb54442d18p+1, pio2_hi = 0x1.921fb54442d18p+0, pio2_lo = 0x1.1a62633145c07p-54;
+    const double pS0 = 0x1.5555555555555p-3, pS1 = -0x1.4d61203eb6f7dp-2, pS2 = 0x1.9c1550e884455p-3,
+                 pS3 = -0x1.48228b5688f3bp-5, pS4 = 0x1.9efe07501b288p-11, pS5 = 0x1.23de10dfdf709p-15;
+    const double qS1 = -0x1.33a271c8a2d4bp+1, qS2 = 0x1.02ae59c598ac8p+1, qS3 = -0x1.6066c1b8d0159p-1,
+                 qS4 = 0x1.3b8c5b12e9282p-4;
+    const int32_t hx = (int32_t)fd_hi(x), ix = hx & 0x7fffffff;
+    if (ix >= 0x3ff00000) {
+        if (((ix - 0x3ff00000) | fd_lo(x)) == 0) return hx > 0 ? 0.0 : pi + 2.0 * pio2_lo;
+        return __builtin_nan("");
+    }
+    if (ix < 0x3fe00000) {
+        if (ix <= 0x3c600000) return pio2_hi + pio2_lo;
+        const double z = x * x;
+        const double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        const double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        const double r = p / q;
+        return pio2_hi - (x - (pio2_lo - x * r));
+    } else if (hx < 0) {
+        const double z = (1.0 + x) * 0.5;
+        const double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        const double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        const double s = sqrt(z);
+        const double r = p / q;
+        const double w = r * s - pio2_lo;
+        return pi - 2.0 * (s + w);
+    }
+    const double z = (1.0 - x) * 0.5;
+    const double s = sqrt(z);
+    const double df = fd_make(fd_hi(s), 0);
+    const double c = (z - df * df) / (s + df);
+    const double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const double r = p / q;
+    const double w = r * s + c;
+    return 2.0 * (df + w);
+}
+
+__device__ double fd_log(double x)
+{
+    const double ln2_hi = 0x1.62e42fee00000p-1, ln2_lo = 0x1.a39ef35793c76p-33, two54 = 0x1p54;
+    const double Lg1 = 0x1.5555555555593p-1, Lg2 = 0x1.999999997fa04p-2, Lg3 = 0x1.2492494229359p-2,
+                 Lg4 = 0x1.c71c51d8e78afp-3, Lg5 = 0x1.7466496cb03dep-3, Lg6 = 0x1.39a09d078c69fp-3,
+                 Lg7 = 0x1.2f112df3e5244p-3;
+    int32_t hx = (int32_t)fd_hi(x);
+    const uint32_t lx = fd_lo(x);
+    int32_t k = 0;
+    if (hx < 0x00100000) {
+        if (((hx & 0x7fffffff) | lx) == 0) return -__builtin_inf();
+        if (hx < 0) return __builtin_nan("");
+        k -= 54; x *= two54;
+        hx = (int32_t)fd_hi(x);
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    const int32_t i0 = (hx + 0x95f64) & 0x100000;
+    x = fd_make((uint32_t)(hx | (i0 ^ 0x3ff00000)), fd_lo(x));
+    k += (i0 >> 20);
+    const double f = x - 1.0;
+    if ((0x000fffff & (2 + hx)) < 3) {
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            const double dk = (double)k;
+            return dk * ln2_hi + dk * ln2_lo;
+        }
+        const double R = f * f * (0.5 - 0.33333333333333333 * f);
+        if (k == 0) return f - R;
+        const double dk = (double)k;
+        return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    const double s = f / (2.0 + f);
+    const double dk = (double)k;
+    const double z = s * s;
+    int32_t i = hx - 0x6147a;
+    const double w = z * z;
+    const int32_t j = 0x6b851 - hx;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i |= j;
+    const double R = t2 + t1;
+    if (i > 0) {
+        const double hfsq = 0.5 * f * f;
+        if (k == 0) return f - (hfsq - s * (hfsq + R));
+        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    if (k == 0) return f - s * (f - R);
+    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+__device__ double fd_exp(double x)
+{
+    const double ln2HI = 0x1.62e42fee00000p-1, ln2LO = 0x1.a39ef35793c76p-33, invln2 = 0x1.71547652b82fep+0;
+    const double P1 = 0x1.555555555553ep-3, P2 = -0x1.6c16c16bebd93p-9, P3 = 0x1.1566aaf25de2cp-14,
+                 P4 = -0x1.bbd41c5d26bf1p-20, P5 = 0x1.6376972bea4d0p-25;
+    const double o_threshold = 0x1.62e42fefa39efp+9, u_threshold = -0x1.74910d52d3051p+9;
+    uint32_t hx = fd_hi(x);
+    const int xsb = (hx >> 31) & 1;
+    hx &= 0x7fffffff;
+    if (hx >= 0x40862E42) {
+        if (hx >= 0x7ff00000) {
+            if (((hx & 0xfffff) | fd_lo(x)) != 0) return x + x;
+            return xsb == 0 ? x : 0.0;
+        }
+        if (x > o_threshold) return __builtin_inf();
+        if (x < u_threshold) return 0.0;
+    }
+    double hi = 0, lo = 0;
+    int k = 0;
+    if (hx > 0x3fd62e42) {
+        if (hx < 0x3FF0A2B2) {
+            hi = x - (xsb ? -ln2HI : ln2HI); lo = xsb ? -ln2LO : ln2LO; k = 1 - xsb - xsb;
+        } else {
+            k = (int)(invln2 * x + (xsb ? -0.5 : 0.5));
+            const double t = k;
+            hi = x - t * ln2HI;
+            lo = t * ln2LO;
+        }
+        x = hi - lo;
+    } else if (hx < 0x3e300000) {
+        return 1.0 + x;
+    } else k = 0;
+    const double t = x * x;
+    const double c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
+    double y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
+    if (k >= -1021) return fd_make(fd_hi(y) + ((uint32_t)k << 20), fd_lo(y));
+    y = fd_make(fd_hi(y) + ((uint32_t)(k + 1000) << 20), fd_lo(y));
+    return y * 0x1p-1000;
+}
+
+__device__ __forceinline__ double fd_pow_pos(double x, double y) { return x == 0.0 ? 0.0 : fd_exp(y * fd_log(x)); }
+
+__device__ int solve_cubic(const double c[4], double r[3])
+{
+    double a0 = c[0], a1 = c[1], a2 = c[2], a3 = c[3], x0 = 0, x1 = 0, x2 = 0;
+    int n = 0;
+    if (a0 == 0) {
+        if (a1 == 0) {
+            if (a2 == 0) n = a3 == 0 ? -1 : 0;
+            else { x0 = -a3 / a2; n = 1; }
+        } else {
+            double d = a2 * a2 - 4 * a1 * a3;
+            if (d >= 0) {
+                d = sqrt(d);
+                const double q1 = (-a2 + d) * 0.5, q2 = (a2 + d) * -0.5;
+                if (fabs(q1) > fabs(q2)) { x0 = q1 / a1; x1 = a3 / q1; }
+                else { x0 = q2 / a1; x1 = a3 / q2; }
+                n = d > 0 ? 2 : 1;
+            }
+        }
+    } else {
+        a0 = 1. / a0;
+        a1 *= a0; a2 *= a0; a3 *= a0;
+        const double Q = (a1 * a1 - 3 * a2) * (1. / 9);
+        const double R = (2 * a1 * a1 * a1 - 9 * a1 * a2 + 27 * a3) * (1. / 54);
+        const double Qcubed = Q * Q * Q;
+        double d = Qcubed - R * R;
+        if (d > 0) {
+            const double theta = fd_acos(R / sqrt(Qcubed));
+            const double sqrtQ = sqrt(Q);
+            const double t0 = -2 * sqrtQ, t1 = theta * (1. / 3), t2 = a1 * (1. / 3);
+            x0 = t0 * fl_cos(t1) - t2;
+            x1 = t0 * fl_cos(t1 + (2. * 3.1415926535897932384626433832795 / 3)) - t2;
+            x2 = t0 * fl_cos(t1 + (4. * 3.1415926535897932384626433832795 / 3)) - t2;
+            n = 3;
+        } else if (d == 0) {
+            if (R >= 0) { x0 = -2 * fd_pow_pos(R, 1. / 3) - a1 / 3; x1 = fd_pow_pos(R, 1. / 3) - a1 / 3; }
+            else { x0 = 2 * fd_pow_pos(-R, 1. / 3) - a1 / 3; x1 = -fd_pow_pos(-R, 1. / 3) - a1 / 3; }
+            x2 = 0;
+            n = x0 == x1 ? 1 : 2;
+            x1 = x0 == x1 ? 0 : x1;
+        } else {
+            d = sqrt(-d);
+            double e = fd_pow_pos(d + fabs(R), 0.333333333333);
+            if (R > 0) e = -e;
+            x0 = (e + Q / e) - a1 * (1. / 3);
+            n = 1;
+        }
+    }
+    r[0] = x0; r[1] = x1; r[2] = x2;
+    return n;
+}
+
+// run7Point with the null space from complete-pivoting Gauss-Jordan (oracle oc_run7point); A is
+// this thread's 7x9 scratch (LDS)
+__device__ int run7point(const float2* s1, const float2* s2, double* A, int* perm, double* F)
+{
+    for (int i = 0; i < 7; i++) {
+        const double x0 = s1[i].x, y0 = s1[i].y, x1 = s2[i].x, y1 = s2[i].y;
+        double* a = A + 9 * i;
+        a[0] = x1 * x0; a[1] = x1 * y0; a[2] = x1;
+        a[3] = y1 * x0; a[4] = y1 * y0; a[5] = y1;
+        a[6] = x0; a[7] = y0; a[8] = 1;
+    }
+    for (int j = 0; j < 9; j++) perm[j] = j;
+    for (int r = 0; r < 7; r++) {
+        int pi = r, pj = r;
+        double best = -1.0;
+        for (int i = r; i < 7; i++)
+            for (int j = r; j < 9; j++)
+                if (fabs(A[9 * i + j]) > best) { best = fabs(A[9 * i + j]); pi = i; pj = j; }
+        if (!(best > 0.0)) return 0;
+        if (pi != r)
+            for (int j = 0; j < 9; j++) { const double t = A[9 * r + j]; A[9 * r + j] = A[9 * pi + j]; A[9 * pi + j] = t; }
+        if (pj != r) {
+            for (int i = 0; i < 7; i++) { const double t = A[9 * i + r]; A[9 * i + r] = A[9 * i + pj]; A[9 * i + pj] = t; }
+            const int t = perm[r]; perm[r] = perm[pj]; perm[pj] = t;
+        }
+        const double piv = A[9 * r + r];
+        for (int i = 0; i < 7; i++) {
+            if (i == r) continue;
+            const double f = A[9 * i + r] / piv;
+            for (int j = r; j < 9; j++) A[9 * i + j] = A[9 * i + j] - f * A[9 * r + j];
+        }
+    }
+    double f1[9], f2[9];
+    // v[perm[i]] = -A[i][col] / A[i][i] (i < 7), v[perm[7]], v[perm[8]] = unit (a gather over the
+    // inverse permutation keeps f1/f2 in registers)
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+        double v1 = 0, v2 = 0;
+        for (int i = 0; i < 9; i++) {
+            if (perm[i] != q) continue;
+            if (i < 7) { v1 = -A[9 * i + 7] / A[9 * i + i]; v2 = -A[9 * i + 8] / A[9 * i + i]; }
+            else if (i == 7) { v1 = 1.0; v2 = 0.0; }
+            else { v1 = 0.0; v2 = 1.0; }
+        }
+        f1[q] = v1; f2[q] = v2;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) f1[i] -= f2[i];
+    double c[4], rr[3];
+    double t0 = f2[4] * f2[8] - f2[5] * f2[7];
+    double t1 = f2[3] * f2[8] - f2[5] * f2[6];
+    double t2 = f2[3] * f2[7] - f2[4] * f2[6];
+    c[3] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2;
+    c[2] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2 - f1[3] * (f2[1] * f2[8] - f2[2] * f2[7]) +
+           f1[4] * (f2[0] * f2[8] - f2[2] * f2[6]) - f1[5] * (f2[0] * f2[7] - f2[1] * f2[6]) +
+           f1[6] * (f2[1] * f2[5] - f2[2] * f2[4]) - f1[7] * (f2[0] * f2[5] - f2[2] * f2[3]) +
+           f1[8] * (f2[0] * f2[4] - f2[1] * f2[3]);
+    t0 = f1[4] * f1[8] - f1[5] * f1[7];
+    t1 = f1[3] * f1[8] - f1[5] * f1[6];
+    t2 = f1[3] * f1[7] - f1[4] * f1[6];
+    c[1] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2 - f2[3] * (f1[1] * f1[8] - f1[2] * f1[7]) +
+           f2[4] * (f1[0] * f1[8] - f1[2] * f1[6]) - f2[5] * (f1[0] * f1[7] - f1[1] * f1[6]) +
+           f2[6] * (f1[1] * f1[5] - f1[2] * f1[4]) - f2[7] * (f1[0] * f1[5] - f1[2] * f1[3]) +
+           f2[8] * (f1[0] * f1[4] - f1[1] * f1[3]);
+    c[0] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2;
+    const int n = solve_cubic(c, rr);
+    if (n < 1 || n > 3) return n;
+    for (int k = 0; k < n; k++) {
+        double* fm = F + 9 * k;
+        const double rk = k == 0 ? rr[0] : k == 1 ? rr[1] : rr[2];
+        double lambda = rk, mu = 1.;
+        const double s = f1[8] * rk + f2[8];
+        if (fabs(s) > DBL_EPSILON) { mu = 1. / s; lambda *= mu; fm[8] = 1.; }
+        else fm[8] = 0.;
+#pragma unroll
+        for (int i = 0; i < 8; i++) fm[i] = f1[i] * lambda + f2[i] * mu;
+    }
+    return n;
+}
+
+__device__ __forceinline__ float fm_error(const double* F, float x1, float y1, float x2, float y2)
+{
+    double a = F[0] * x1 + F[1] * y1 + F[2];
+    double b = F[3] * x1 + F[4] * y1 + F[5];
+    double c = F[6] * x1 + F[7] * y1 + F[8];
+    const double s2 = 1. / (a * a + b * b);
+    const double d2 = x2 * a + y2 * b + c;
+    a = F[0] * x2 + F[3] * y2 + F[6];
+    b = F[1] * x2 + F[4] * y2 + F[7];
+    c = F[2] * x2 + F[5] * y2 + F[8];
+    const double s1 = 1. / (a * a + b * b);
+    const double d1 = x1 * a + y1 * b + c;
+    const double e1 = d1 * d1 * s1, e2 = d2 * d2 * s2;
+    return (float)(e1 < e2 ? e2 : e1);
+}
+
+__device__ bool fm_collinear(const float2* m)
+{
+    const int i = 6;
+    for (int j = 0; j < i; j++) {
+        const double dx1 = (double)(m[j].x - m[i].x), dy1 = (double)(m[j].y - m[i].y);
+        for (int k = 0; k < j; k++) {
+            const double dx2 = (double)(m[k].x - m[i].x), dy2 = (double)(m[k].y - m[i].y);
+            if (fabs(dx2 * dy1 - dy2 * dx1) <= FLT_EPSILON * (fabs(dx1) + fabs(dy1) + fabs(dx2) + fabs(dy2)))
+                return true;
+        }
+    }
+    return false;
+}
+
+__device__ __forceinline__ unsigned rng_next(uint64_t& st)
+{
+    st = (uint64_t)(unsigned)st * 4164903690U + (unsigned)(st >> 32);
+    return (unsigned)st;
+}
+
+// RANSACUpdateNumIters(p, ep, 7, maxIters) in the canonical forms (oracle oc_ransac_update_iters)
+__device__ int ransac_update_iters(double p, double ep, int max_iters)
+{
+    p = p > 0. ? p : 0.; p = p < 1. ? p : 1.;
+    ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
+    double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
+    const double b = 1. - ep;
+    double denom = 1. - b * b * b * b * b * b * b;
+    if (denom < DBL_MIN) return 0;
+    num = fd_log(num);
+    denom = fd_log(denom);
+    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
+}
+
+struct FmOut {
+    float* tm;          // T_M (x, y) pairs
+    int* ntm;           // |T_M|, -1 when F is empty
+    uint8_t* state;     // state after the SAD check (optional)
+    double* F;          // 9 (optional)
+    int* nf;            // |F_prepoint| (optional)
+    int tm_cap;
+};
+
+__global__ __launch_bounds__(kFmThreads) void k_fm(const uint8_t* __restrict__ prev, const uint8_t* __restrict__ cur,
+                                                  int w, int h, int stride, const float* __restrict__ pxy,
+                                                  const float* __restrict__ nxy, const uint8_t* __restrict__ status,
+                                                  const int* __restrict__ d_n, int nmax, int edge, double limit,
+                                                  double thr, double conf, FmOut out)
+{
+    __shared__ float2 s_m1[kMaxPts], s_m2[kMaxPts];
+    __shared__ uint16_t s_map[kMaxPts];
+    __shared__ int s_w[16];
+    __shared__ double s_A[kFmChunk][63];
+    __shared__ int s_perm[kFmChunk][9];
+    __shared__ double s_models[kFmChunk][27];
+    __shared__ int s_nm[kFmChunk];
+    __shared__ float2 s_sub1[kFmChunk][7], s_sub2[kFmChunk][7];
+    __shared__ int s_found[kFmChunk];
+    __shared__ int s_good[kFmChunk * 3];
+    __shared__ float s_med[kFmChunk * 3];
+    __shared__ double s_F[9];
+    __shared__ int s_ok, s_done, s_niters, s_base;
+    __shared__ uint64_t s_rng;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int n = *d_n;
+    n = n < nmax ? n : nmax;
+    n = n < kMaxPts ? n : kMaxPts;
+    // ---- SAD check (Frame.cc:337-365) and the ordered F_ sets ----
+    int keep = 0;
+    float2 p1 = make_float2(0.f, 0.f), p2 = p1;
+    if (tid < n) {
+        uint8_t st = status[tid];
+        p1 = make_float2(pxy[2 * tid], pxy[2 * tid + 1]);
+        p2 = make_float2(nxy[2 * tid], nxy[2 * tid + 1]);
+        if (st) {
+            const int x1 = (int)p1.x, y1 = (int)p1.y, x2 = (int)p2.x, y2 = (int)p2.y;
+            if (x1 < edge || x1 >= w - edge || x2 < edge || x2 >= w - edge || y1 < edge || y1 >= h - edge ||
+                y2 < edge || y2 >= h - edge) {
+                st = 0;
+            } else {
+                double sum = 0;
+                for (int j = 0; j < 9; j++) {
+                    const int dx = j % 3 - 1, dy = j / 3 - 1;
+                    sum += (double)abs((int)prev[(size_t)(y1 + dy) * stride + x1 + dx] -
+                                       (int)cur[(size_t)(y2 + dy) * stride + x2 + dx]);
+                }
+                if (sum > limit) st = 0;
+            }
+        }
+        keep = st != 0;
+        if (out.state) out.state[tid] = (uint8_t)keep;
+    }
+    int pos;
+    const int nf = block_scan_1024(keep, s_w, pos);
+    if (keep) { s_m1[pos] = p1; s_m2[pos] = p2; s_map[pos] = (uint16_t)tid; }
+    if (tid == 0) {
+        s_ok = 0; s_done = 0; s_base = 0; s_rng = ~0ull;
+        if (out.nf) *out.nf = nf;
+    }
+    __syncthreads();
+    // ---- findFundamentalMat ----
+    if (nf == 7) {
+        if (tid == 0) {
+            const int k = run7point(s_m1, s_m2, s_A[0], s_perm[0], s_models[0]);
+            if (k > 0) {
+                for (int q = 0; q < 9; q++) s_F[q] = s_models[0][q];
+                s_ok = 1;
+            }
+        }
+    } else if (nf >= 8) {
+        const bool ransac = nf >= 15;
+        const int max_attempts = ransac ? 10000 : 1000;
+        const float t = (float)(thr * thr);
+        int max_good = 0;           // lane 0 state
+        double min_median = DBL_MAX;
+        if (tid == 0) {
+            if (ransac) s_niters = 1000;
+            else {
+                const int ni = ransac_update_iters(conf, 0.45, 1000);
+                s_niters = ni > 3 ? ni : 3;
+            }
+        }
+        __syncthreads();
+        for (;;) {
+            const int base = s_base, niters = s_niters;
+            if (s_done || base >= niters) break;
+            // draws for iterations base .. base + kFmChunk - 1 (getSubset, checkPartialSubsets = false)
+            if (tid == 0) {
+                uint64_t rng = s_rng;
+                for (int hh = 0; hh < kFmChunk; hh++) {
+                    int idx[7];
+                    int iters = 0, i = 0;
+                    for (; iters < max_attempts; iters++) {
+                        for (i = 0; i < 7 && iters < max_attempts;) {
+                            int id;
+                            for (;;) {
+                                id = (int)(rng_next(rng) % (unsigned)nf);
+                                int j;
+                                for (j = 0; j < i; j++)
+                                    if (id == idx[j]) break;
+                                if (j == i) break;
+                            }
+                            idx[i] = id;
+                            s_sub1[hh][i] = s_m1[id];
+                            s_sub2[hh][i] = s_m2[id];
+                            i++;
+                        }
+                        if (i == 7 && (fm_collinear(s_sub1[hh]) || fm_collinear(s_sub2[hh]))) continue;
+                        break;
+                    }
+                    s_found[hh] = i == 7 && iters < max_attempts;
+                }
+                s_rng = rng;
+            }
+            __syncthreads();
+            if (tid < kFmChunk) s_nm[tid] = s_found[tid] ? run7point(s_sub1[tid], s_sub2[tid], s_A[tid], s_perm[tid], s_models[tid]) : 0;
+            __syncthreads();
+            // score every (hypothesis, model): one wave each
+            for (int pr = wv; pr < kFmChunk * 3; pr += kFmThreads / 64) {
+                const int hh = pr / 3, m = pr - hh * 3;
+                if (m >= s_nm[hh]) continue;
+                const double* F = s_models[hh] + 9 * m;
+                if (ransac) {
+                    int good = 0;
+                    for (int i = lane; i < nf; i += 64)
+                        good += fm_error(F, s_m1[i].x, s_m1[i].y, s_m2[i].x, s_m2[i].y) <= t;
+                    for (int off = 32; off >= 1; off >>= 1) good += __shfl_xor(good, off, 64);
+                    if (lane == 0) s_good[pr] = good;
+                } else if (lane == 0) {
+                    float e[16];
+                    for (int i = 0; i < nf; i++) e[i] = fm_error(F, s_m1[i].x, s_m1[i].y, s_m2[i].x, s_m2[i].y);
+                    for (int a = 1; a < nf; a++) {
+                        const float v = e[a];
+                        int b = a - 1;
+                        while (b >= 0 && e[b] > v) { e[b + 1] = e[b]; b--; }
+                        e[b + 1] = v;
+                    }
+                    s_med[pr] = e[nf / 2];
+                }
+            }
+            __syncthreads();
+            // the reference's sequential scan (ptsetreg.cpp run loops)
+            if (tid == 0) {
+                int ni = niters;
+                for (int hh = 0; hh < kFmChunk; hh++) {
+                    const int iter = base + hh;
+                    if (iter >= ni) { s_done = 1; break; }
+                    if (!s_found[hh]) {
+                        if (iter == 0) s_ok = -1;
+                        s_done = 1;
+                        break;
+                    }
+                    for (int m = 0; m < s_nm[hh]; m++) {
+                        if (ransac) {
+                            const int good = s_good[hh * 3 + m];
+                            if (good > (max_good > 6 ? max_good : 6)) {
+                                for (int q = 0; q < 9; q++) s_F[q] = s_models[hh][9 * m + q];
+                                max_good = good;
+                                s_ok = 1;
+                                ni = ransac_update_iters(conf, (double)(nf - good) / nf, ni);
+                            }
+                        } else {
+                            const double med = s_med[hh * 3 + m];
+                            if (med < min_median) {
+                                min_median = med;
+                                for (int q = 0; q < 9; q++) s_F[q] = s_models[hh][9 * m + q];
+                            }
+                        }
+                    }
+                }
+                s_niters = ni;
+                s_base = base + kFmChunk;
+                if (!ransac && !s_done && s_base >= ni) s_done = 1;
+                if (!ransac && s_done && s_ok != -1) {
+                    if (min_median < DBL_MAX) {
+                        double sigma = 2.5 * 1.4826 * (1 + 5. / (nf - 7)) * sqrt(min_median);
+                        sigma = sigma > 0.001 ? sigma : 0.001;
+                        const float tt = (float)(sigma * sigma);
+                        int good = 0;
+                        for (int i = 0; i < nf; i++) good += fm_error(s_F, s_m1[i].x, s_m1[i].y, s_m2[i].x, s_m2[i].y) <= tt;
+                        s_ok = good >= 7 ? 1 : 0;
+                    } else s_ok = 0;
+                }
+                if (ransac && s_ok == 1 && max_good <= 0) s_ok = 0;
+            }
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    // ---- epipolar distance > 1 -> T_M (Frame.cc:375-384), in point order ----
+    if (s_ok != 1) {
+        if (tid == 0) *out.ntm = -1;
+        return;
+    }
+    if (tid < 9 && out.F) out.F[tid] = s_F[tid];
+    int flag = 0;
+    float2 q2 = make_float2(0.f, 0.f);
+    if (tid < nf) {
+        const float2 q1 = s_m1[tid];
+        q2 = s_m2[tid];
+        const double px = q1.x, py = q1.y;
+        const double A = s_F[0] * px + s_F[1] * py + s_F[2];
+        const double B = s_F[3] * px + s_F[4] * py + s_F[5];
+        const double Cc = s_F[6] * px + s_F[7] * py + s_F[8];
+        const double dd = fabs(A * q2.x + B * q2.y + Cc) / sqrt(A * A + B * B);
+        flag = !(dd <= 1);
+    }
+    int tpos;
+    const int nt = block_scan_1024(flag, s_w, tpos);
+    if (flag && tpos < out.tm_cap) {
+        out.tm[2 * tpos] = q2.x;
+        out.tm[2 * tpos + 1] = q2.y;
+    }
+    if (tid == 0) *out.ntm = nt;
+}
+
+// ============================== host side ==============================
+struct FlowDev {
+    uint8_t *prev, *cur;                // packed (pitch w) copies of the two frames
+    float* R;
+    uint32_t* rmax;
+    int* nkeys;
+    uint64_t* keys;
+    uint16_t* cells;
+    float *pts, *nxt;
+    int* npts;
+    uint8_t *status, *state;
+    float* mask;
+    uint8_t* pyr;                       // levels 1.. of both frames
+    short2* der;                        // Scharr of every previous-frame level
+    float* tm;
+    int* ntm;
+    double* F;
+    int* nf;
+};
+
+int lk_levels(int w, int h, int win, int max_level)
+{
+    for (int level = 0; level <= max_level; level++) {
+        w = (w + 1) / 2; h = (h + 1) / 2;
+        if (w <= win || h <= win) return level + 1;
+    }
+    return max_level + 1;
+}
+
+size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d)
+{
+    const int gw = (w + 7) / 8, gh = (h + 7) / 8;
+    size_t pyr_bytes = 0, der_px = 0;
+    {
+        int lw = w, lh = h;
+        der_px += (size_t)lw * lh;
+        for (int l = 1; l < kLkMaxLevels; l++) {
+            lw = (lw + 1) / 2; lh = (lh + 1) / 2;
+            pyr_bytes += 2 * align256((size_t)lw * lh);
+            der_px += (size_t)lw * lh;
+        }
+    }
+    const size_t sizes[] = {align256((size_t)w * h), align256((size_t)w * h), align256((size_t)w * h * 4), 256, 256,
+                            align256((size_t)kGfSortMax * 8), align256((size_t)gw * gh * kGfCellCap * 2),
+                            align256((size_t)kMaxPts * 8), align256((size_t)kMaxPts * 8), 256, align256(kMaxPts),
+                            align256(kMaxPts), align256(sizeof(float) * 23 * 23), align256(pyr_bytes),
+                            align256(der_px * 4 + 64 * kLkMaxLevels), align256((size_t)kMaxPts * 8), 256, 256, 256};
+    size_t total = 0;
+    for (size_t s : sizes) total += s;
+    void* base;
+    const int rc = coeb_internal_scratch(c, "flow", total, &base);
+    if (rc) return rc;
+    uint8_t* p = (uint8_t*)base;
+    size_t o = 0;
+    auto take = [&](int i) { void* r = p + o; o += sizes[i]; return r; };
+    d->prev = (uint8_t*)take(0); d->cur = (uint8_t*)take(1); d->R = (float*)take(2);
+    d->rmax = (uint32_t*)take(3); d->nkeys = (int*)take(4); d->keys = (uint64_t*)take(5);
+    d->cells = (uint16_t*)take(6); d->pts = (float*)take(7); d->nxt = (float*)take(8); d->npts = (int*)take(9);
+    d->status = (uint8_t*)take(10); d->state = (uint8_t*)take(11); d->mask = (float*)take(12);
+    d->pyr = (uint8_t*)take(13); d->der = (short2*)take(14); d->tm = (float*)take(15); d->ntm = (int*)take(16);
+    d->F = (double*)take(17); d->nf = (int*)take(18);
+    return COEB_OK;
+}
+
+size_t gf_select_lds(int w, int h, int cell, int np)
+{
+    const int gw = (w + cell - 1) / cell, gh = (h + cell - 1) / cell;
+    return (size_t)(np > 1 ? np : 2) * 8 + (size_t)gw * gh * 4;
+}
+
+// goodFeaturesToTrack into d->pts / d->npts (device count: -1 sort capacity, -3 cell capacity)
+int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, int max_corners, double quality,
+              double min_distance, double k, hipStream_t s)
+{
+    const int cell = (int)lrint(min_distance);
+    if (cell < 1) return -2;
+    const size_t lds = gf_select_lds(w, h, cell, kGfSortMax);
+    if (lds > 160 * 1024) return -2;
+    (void)hipMemsetAsync(d->rmax, 0, 4, s);
+    (void)hipMemsetAsync(d->nkeys, 0, 4, s);
+    const dim3 grid((w + 15) / 16, (h + 15) / 16);
+    hipLaunchKernelGGL(k_gf_response, grid, dim3(256), 0, s, img, w, h, stride, k, d->R, d->rmax);
+    hipLaunchKernelGGL(k_gf_candidates, grid, dim3(256), 0, s, d->R, w, h, quality, d->rmax, d->keys, d->nkeys,
+                       kGfSortMax);
+    (void)hipFuncSetAttribute((const void*)k_gf_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_gf_select, dim3(1), dim3(kGfThreads), lds, s, d->keys, d->nkeys, w, h, max_corners,
+                       (float)(min_distance * min_distance), cell, d->cells, d->pts, d->npts, kMaxPts);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+void subpix_mask(int win, float* mask)
+{
+    const int n = 2 * win + 1;
+    for (int i = 0; i < n; i++) {
+        const float y = (float)(i - win) / (float)win;
+        const float vy = expf(-y * y);
+        for (int j = 0; j < n; j++) {
+            const float x = (float)(j - win) / (float)win;
+            mask[i * n + j] = vy * expf(-x * x);
+        }
+    }
+}
+
+int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride, int max_iter, double eps,
+                  hipStream_t s)
+{
+    const int iters = max_iter < 1 ? 1 : max_iter > 100 ? 100 : max_iter;
+    const double e = eps > 0 ? eps : 0.;
+    hipLaunchKernelGGL(k_subpix<10>, dim3((kMaxPts + 3) / 4), dim3(256), 0, s, img, w, h, stride, d->pts, d->npts,
+                       kMaxPts, d->mask, iters, e * e);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, int win,
+              int max_level, int max_count, double eps, hipStream_t s)
+{
+    LkPyr pyr;
+    memset(&pyr, 0, sizeof(pyr));
+    const int L = lk_levels(w, h, win, max_level);
+    if (L > kLkMaxLevels) return -2;
+    pyr.L = L;
+    pyr.P[0] = prev; pyr.N[0] = cur; pyr.w[0] = w; pyr.h[0] = h; pyr.pitch[0] = stride;
+    uint8_t* q = d->pyr;
+    short2* dq = d->der;
+    pyr.D[0] = dq;
+    dq += (size_t)w * h;
+    for (int l = 1; l < L; l++) {
+        pyr.w[l] = (pyr.w[l - 1] + 1) / 2; pyr.h[l] = (pyr.h[l - 1] + 1) / 2; pyr.pitch[l] = pyr.w[l];
+        const size_t sz = (size_t)pyr.w[l] * pyr.h[l];
+        pyr.P[l] = q; q += align256(sz);
+        pyr.N[l] = q; q += align256(sz);
+        pyr.D[l] = dq; dq += sz;
+        PyrDownArgs a;
+        a.src[0] = pyr.P[l - 1]; a.src[1] = pyr.N[l - 1];
+        a.dst[0] = const_cast<uint8_t*>(pyr.P[l]); a.dst[1] = const_cast<uint8_t*>(pyr.N[l]);
+        a.sw = pyr.w[l - 1]; a.sh = pyr.h[l - 1]; a.spitch = pyr.pitch[l - 1]; a.dw = pyr.w[l]; a.dh = pyr.h[l];
+        hipLaunchKernelGGL(k_pyr_down, dim3((a.dw + 63) / 64, (a.dh + 3) / 4, 2), dim3(256), 0, s, a);
+    }
+    hipLaunchKernelGGL(k_sharr, dim3(64, L), dim3(256), 0, s, pyr);
+    hipLaunchKernelGGL(k_lk, dim3((kMaxPts + 3) / 4), dim3(256), 0, s, pyr, d->pts, d->npts, kMaxPts, d->nxt,
+                       d->status, win, max_count, eps * eps);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_fm(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, int edge, double limit,
+              hipStream_t s, int tm_cap)
+{
+    FmOut o;
+    o.tm = d->tm; o.ntm = d->ntm; o.state = d->state; o.F = d->F; o.nf = d->nf; o.tm_cap = tm_cap;
+    hipLaunchKernelGGL(k_fm, dim3(1), dim3(kFmThreads), 0, s, prev, cur, w, h, stride, d->pts, d->nxt, d->status,
+                       d->npts, kMaxPts, edge, limit, 0.1, 0.99, o);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+#define FL_TRY(c, x)                                                                          \
+    do {                                                                                      \
+        const hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) return coeb_internal_error(c, COEB_EDEVICE, hipGetErrorString(e_)); \
+    } while (0)
+
+struct FlowCall {
+    hipStream_t s;
+    FlowDev d;
+};
+
+int flow_begin(coeb_ctx* c, int w, int h, FlowCall* fc, const char* who)
+{
+    int dev;
+    if (coeb_internal_stream(c, &fc->s, &dev)) return coeb_internal_error(c, COEB_EINVAL, who);
+    (void)hipSetDevice(dev);
+    if (w < 32 || h < 32 || (size_t)w * h > (size_t)1 << 26) return coeb_internal_error(c, COEB_EINVAL, who);
+    return flow_alloc(c, w, h, &fc->d);
+}
+
+int upload_gray(coeb_ctx* c, hipStream_t s, uint8_t* dst, const uint8_t* src, int w, int h, size_t stride)
+{
+    FL_TRY(c, hipMemcpy2DAsync(dst, (size_t)w, src, stride, (size_t)w, h, hipMemcpyHostToDevice, s));
+    return COEB_OK;
 }
 
 }  // namespace
 
-size_t gf_select_lds(int w, int h, int cell)
+extern "C" int coeb_good_features(coeb_ctx* c, const uint8_t* img, int w, int h, size_t stride, int max_corners,
+                                  double quality, double min_distance, double k, float* xy_out, int cap, int* n_out)
 {
-    const int gw = (w + cell - 1) / cell, gh = (h + cell - 1) / cell;
-    return (size_t)kGfSortMax * 8 + (size_t)((gw * gh + 3) & ~3) * 4 + (size_t)gw * gh * 16 * 8;
+    if (!c || !img || !n_out || (cap > 0 && !xy_out) || stride < (size_t)w || quality <= 0 || min_distance < 1)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_good_features: invalid arguments");
+    if (max_corners <= 0 || max_corners > kMaxPts)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_good_features: max_corners must be in 1..1024");
+    FlowCall fc;
+    int rc = flow_begin(c, w, h, &fc, "coeb_good_features: invalid arguments");
+    if (rc) return rc;
+    if ((rc = upload_gray(c, fc.s, fc.d.prev, img, w, h, stride))) return rc;
+    if (launch_gf(&fc.d, fc.d.prev, w, h, w, max_corners, quality, min_distance, k, fc.s))
+        return coeb_internal_error(c, COEB_EDEVICE, "coeb_good_features: launch failed");
+    int n = 0;
+    FL_TRY(c, hipMemcpyAsync(&n, fc.d.npts, 4, hipMemcpyDeviceToHost, fc.s));
+    FL_TRY(c, hipStreamSynchronize(fc.s));
+    if (n < 0) return coeb_internal_error(c, COEB_ERANGE, "coeb_good_features: more than 16384 local maxima");
+    if (n > 0 && cap > 0) {
+        FL_TRY(c, hipMemcpyAsync(xy_out, fc.d.pts, (size_t)(n < cap ? n : cap) * 8, hipMemcpyDeviceToHost, fc.s));
+        FL_TRY(c, hipStreamSynchronize(fc.s));
+    }
+    *n_out = n;
+    return COEB_OK;
 }
 
-int launch_good_features(const uint8_t* d_img, int w, int h, int stride, int max_corners, double quality,
-                         double min_distance, double k, float* d_R, uint32_t* d_max, uint64_t* d_keys, int* d_nkeys,
-                         int key_cap, float* d_out, int* d_nout, int out_cap, hipStream_t s)
+extern "C" int coeb_corner_subpix(coeb_ctx* c, const uint8_t* img, int w, int h, size_t stride, float* xy, int n,
+                                  int win, int max_iter, double eps)
 {
-    const int cell = (int)lrint(min_distance);
-    if (cell < 1) return -2;
-    const size_t lds = gf_select_lds(w, h, cell);
-    if (lds > 160 * 1024) return -2;
-    (void)hipMemsetAsync(d_max, 0, 4, s);
-    (void)hipMemsetAsync(d_nkeys, 0, 4, s);
-    const dim3 grid((w + 15) / 16, (h + 15) / 16);
-    hipLaunchKernelGGL(k_gf_response, grid, dim3(256), 0, s, d_img, w, h, stride, k, d_R, d_max);
-    hipLaunchKernelGGL(k_gf_candidates, grid, dim3(256), 0, s, d_R, w, h, quality, d_max, d_keys, d_nkeys, key_cap);
-    (void)hipFuncSetAttribute((const void*)k_gf_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_gf_select, dim3(1), dim3(kGfThreads), lds, s, d_keys, d_nkeys, w, h, max_corners,
-                       (float)min_distance, cell, d_out, d_nout, out_cap);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    if (!c || !img || n < 0 || n > kMaxPts || (n > 0 && !xy) || stride < (size_t)w)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_corner_subpix: invalid arguments");
+    if (win != 10) return coeb_internal_error(c, COEB_EINVAL, "coeb_corner_subpix: window 10 only (Frame.cc:334)");
+    if (n == 0) return COEB_OK;
+    FlowCall fc;
+    int rc = flow_begin(c, w, h, &fc, "coeb_corner_subpix: invalid arguments");
+    if (rc) return rc;
+    float mask[21 * 21];
+    subpix_mask(win, mask);
+    if ((rc = upload_gray(c, fc.s, fc.d.prev, img, w, h, stride))) return rc;
+    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
+    FL_TRY(c, hipMemcpyAsync(fc.d.pts, xy, (size_t)n * 8, hipMemcpyHostToDevice, fc.s));
+    FL_TRY(c, hipMemcpyAsync(fc.d.npts, &n, 4, hipMemcpyHostToDevice, fc.s));
+    if (launch_subpix(&fc.d, fc.d.prev, w, h, w, max_iter, eps, fc.s))
+        return coeb_internal_error(c, COEB_EDEVICE, "coeb_corner_subpix: launch failed");
+    FL_TRY(c, hipMemcpyAsync(xy, fc.d.pts, (size_t)n * 8, hipMemcpyDeviceToHost, fc.s));
+    FL_TRY(c, hipStreamSynchronize(fc.s));
+    return COEB_OK;
+}
+
+extern "C" int coeb_optical_flow_pyr_lk(coeb_ctx* c, const uint8_t* prev, const uint8_t* next, int w, int h,
+                                        size_t stride, const float* prev_xy, int n, int win, int max_level,
+                                        int max_count, double eps, float* next_xy, uint8_t* status)
+{
+    if (!c || !prev || !next || n < 0 || n > kMaxPts || (n > 0 && (!prev_xy || !next_xy || !status)) ||
+        stride < (size_t)w || max_level < 0 || max_count < 1)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_optical_flow_pyr_lk: invalid arguments");
+    if (win < 3 || win * win > 512)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_optical_flow_pyr_lk: window must be 3..22");
+    if (n == 0) return COEB_OK;
+    FlowCall fc;
+    int rc = flow_begin(c, w, h, &fc, "coeb_optical_flow_pyr_lk: invalid arguments");
+    if (rc) return rc;
+    if (lk_levels(w, h, win, max_level) > kLkMaxLevels)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_optical_flow_pyr_lk: more than 8 pyramid levels");
+    if ((rc = upload_gray(c, fc.s, fc.d.prev, prev, w, h, stride)) || (rc = upload_gray(c, fc.s, fc.d.cur, next, w, h, stride)))
+        return rc;
+    FL_TRY(c, hipMemcpyAsync(fc.d.pts, prev_xy, (size_t)n * 8, hipMemcpyHostToDevice, fc.s));
+    FL_TRY(c, hipMemcpyAsync(fc.d.npts, &n, 4, hipMemcpyHostToDevice, fc.s));
+    if (launch_lk(&fc.d, fc.d.prev, fc.d.cur, w, h, w, win, max_level, max_count, eps, fc.s))
+        return coeb_internal_error(c, COEB_EDEVICE, "coeb_optical_flow_pyr_lk: launch failed");
+    FL_TRY(c, hipMemcpyAsync(next_xy, fc.d.nxt, (size_t)n * 8, hipMemcpyDeviceToHost, fc.s));
+    FL_TRY(c, hipMemcpyAsync(status, fc.d.status, (size_t)n, hipMemcpyDeviceToHost, fc.s));
+    FL_TRY(c, hipStreamSynchronize(fc.s));
+    return COEB_OK;
+}
+
+extern "C" int coeb_moving_tail(coeb_ctx* c, const uint8_t* prev, const uint8_t* cur, int w, int h, size_t stride,
+                                const float* prev_xy, const float* next_xy, uint8_t* state, int n, float* tm_xy,
+                                int tm_cap, int* n_tm, double F_out[9], int* nf_out)
+{
+    if (!c || !prev || !cur || n < 0 || n > kMaxPts || (n > 0 && (!prev_xy || !next_xy || !state)) || !n_tm ||
+        (tm_cap > 0 && !tm_xy) || stride < (size_t)w)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_moving_tail: invalid arguments");
+    FlowCall fc;
+    int rc = flow_begin(c, w, h, &fc, "coeb_moving_tail: invalid arguments");
+    if (rc) return rc;
+    if ((rc = upload_gray(c, fc.s, fc.d.prev, prev, w, h, stride)) || (rc = upload_gray(c, fc.s, fc.d.cur, cur, w, h, stride)))
+        return rc;
+    if (n > 0) {
+        FL_TRY(c, hipMemcpyAsync(fc.d.pts, prev_xy, (size_t)n * 8, hipMemcpyHostToDevice, fc.s));
+        FL_TRY(c, hipMemcpyAsync(fc.d.nxt, next_xy, (size_t)n * 8, hipMemcpyHostToDevice, fc.s));
+        FL_TRY(c, hipMemcpyAsync(fc.d.status, state, (size_t)n, hipMemcpyHostToDevice, fc.s));
+    }
+    FL_TRY(c, hipMemcpyAsync(fc.d.npts, &n, 4, hipMemcpyHostToDevice, fc.s));
+    if (launch_fm(&fc.d, fc.d.prev, fc.d.cur, w, h, w, 5, 2120.0, fc.s, kMaxPts))
+        return coeb_internal_error(c, COEB_EDEVICE, "coeb_moving_tail: launch failed");
+    int nt = 0, nf = 0;
+    double F[9];
+    FL_TRY(c, hipMemcpyAsync(&nt, fc.d.ntm, 4, hipMemcpyDeviceToHost, fc.s));
+    FL_TRY(c, hipMemcpyAsync(&nf, fc.d.nf, 4, hipMemcpyDeviceToHost, fc.s));
+    FL_TRY(c, hipMemcpyAsync(F, fc.d.F, sizeof(F), hipMemcpyDeviceToHost, fc.s));
+    if (n > 0) FL_TRY(c, hipMemcpyAsync(state, fc.d.state, (size_t)n, hipMemcpyDeviceToHost, fc.s));
+    FL_TRY(c, hipStreamSynchronize(fc.s));
+    if (nt > 0 && tm_cap > 0) {
+        FL_TRY(c, hipMemcpyAsync(tm_xy, fc.d.tm, (size_t)(nt < tm_cap ? nt : tm_cap) * 8, hipMemcpyDeviceToHost, fc.s));
+        FL_TRY(c, hipStreamSynchronize(fc.s));
+    }
+    *n_tm = nt;
+    if (nf_out) *nf_out = nf;
+    if (F_out && nt >= 0) memcpy(F_out, F, sizeof(F));
+    return COEB_OK;
+}
+
+extern "C" int coeb_moving_object_points(coeb_ctx* c, const uint8_t* prev, const uint8_t* cur, int w, int h,
+                                         size_t stride, float* tm_xy, int tm_cap, int* n_tm, coeb_flow_debug* dbg)
+{
+    if (!c || !prev || !cur || !n_tm || (tm_cap > 0 && !tm_xy) || stride < (size_t)w)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_moving_object_points: invalid arguments");
+    FlowCall fc;
+    int rc = flow_begin(c, w, h, &fc, "coeb_moving_object_points: invalid arguments");
+    if (rc) return rc;
+    if (lk_levels(w, h, 22, 5) > kLkMaxLevels)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_moving_object_points: image too large");
+    float mask[21 * 21];
+    subpix_mask(10, mask);
+    if ((rc = upload_gray(c, fc.s, fc.d.prev, prev, w, h, stride)) || (rc = upload_gray(c, fc.s, fc.d.cur, cur, w, h, stride)))
+        return rc;
+    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
+    return coeb_moving_object_points_device(c, fc.d.prev, fc.d.cur, w, h, w, tm_xy, tm_cap, n_tm, dbg);
+}
+
+// device-resident frames (pitch `stride`); the subpix weight table is uploaded on first use
+extern "C" int coeb_moving_object_points_device(coeb_ctx* c, const uint8_t* d_prev, const uint8_t* d_cur, int w, int h,
+                                                size_t stride, float* tm_xy, int tm_cap, int* n_tm,
+                                                coeb_flow_debug* dbg)
+{
+    if (!c || !d_prev || !d_cur || !n_tm || (tm_cap > 0 && !tm_xy) || stride < (size_t)w)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_moving_object_points_device: invalid arguments");
+    FlowCall fc;
+    int rc = flow_begin(c, w, h, &fc, "coeb_moving_object_points_device: invalid arguments");
+    if (rc) return rc;
+    if (lk_levels(w, h, 22, 5) > kLkMaxLevels)
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_moving_object_points_device: image too large");
+    float mask[21 * 21];
+    subpix_mask(10, mask);
+    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
+    const int sp = (int)stride;
+    if (launch_gf(&fc.d, d_prev, w, h, sp, 1000, 0.01, 8.0, 0.04, fc.s))
+        return coeb_internal_error(c, COEB_EDEVICE, "coeb_moving_object_points: goodFeaturesToTrack launch failed");
+    if (dbg && dbg->corners_raw) {
+        FL_TRY(c, hipMemcpyAsync(dbg->corners_raw, fc.d.pts, (size_t)1000 * 8, hipMemcpyDeviceToHost, fc.s));
+    }
+    if (launch_subpix(&fc.d, d_prev, w, h, sp, 20, 0.03, fc.s) ||
+        launch_lk(&fc.d, d_prev, d_cur, w, h, sp, 22, 5, 20, 0.01, fc.s) ||
+        launch_fm(&fc.d, d_prev, d_cur, w, h, sp, 5, 2120.0, fc.s, kMaxPts))
+        return coeb_internal_error(c, COEB_EDEVICE, "coeb_moving_object_points: launch failed");
+    int nt = 0, nc = 0;
+    FL_TRY(c, hipMemcpyAsync(&nt, fc.d.ntm, 4, hipMemcpyDeviceToHost, fc.s));
+    FL_TRY(c, hipMemcpyAsync(&nc, fc.d.npts, 4, hipMemcpyDeviceToHost, fc.s));
+    if (dbg) {
+        if (dbg->corners) FL_TRY(c, hipMemcpyAsync(dbg->corners, fc.d.pts, (size_t)1000 * 8, hipMemcpyDeviceToHost, fc.s));
+        if (dbg->next_pts) FL_TRY(c, hipMemcpyAsync(dbg->next_pts, fc.d.nxt, (size_t)1000 * 8, hipMemcpyDeviceToHost, fc.s));
+        if (dbg->status) FL_TRY(c, hipMemcpyAsync(dbg->status, fc.d.status, 1000, hipMemcpyDeviceToHost, fc.s));
+        if (dbg->state) FL_TRY(c, hipMemcpyAsync(dbg->state, fc.d.state, 1000, hipMemcpyDeviceToHost, fc.s));
+        if (dbg->F) FL_TRY(c, hipMemcpyAsync(dbg->F, fc.d.F, 72, hipMemcpyDeviceToHost, fc.s));
+        if (dbg->nf) FL_TRY(c, hipMemcpyAsync(dbg->nf, fc.d.nf, 4, hipMemcpyDeviceToHost, fc.s));
+    }
+    FL_TRY(c, hipStreamSynchronize(fc.s));
+    if (nc < 0) return coeb_internal_error(c, COEB_ERANGE, "coeb_moving_object_points: more than 16384 local maxima");
+    if (dbg && dbg->ncorners) *dbg->ncorners = nc;
+    if (nt > 0 && tm_cap > 0) {
+        FL_TRY(c, hipMemcpyAsync(tm_xy, fc.d.tm, (size_t)(nt < tm_cap ? nt : tm_cap) * 8, hipMemcpyDeviceToHost, fc.s));
+        FL_TRY(c, hipStreamSynchronize(fc.s));
+    }
+    *n_tm = nt;
+    return COEB_OK;
 }

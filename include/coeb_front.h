@@ -36,6 +36,10 @@
  *   coeb_pose_optimization          <- Optimizer::PoseOptimization(Frame*)  include/Optimizer.h:47,
  *                                      src/Optimizer.cc:239-451 (g2o LM; g2o itself is not vendored,
  *                                      parity UNPINNED); calls Tracking.cc:841,964,1006
+ *   coeb_good_features, coeb_corner_subpix, coeb_optical_flow_pyr_lk, coeb_moving_tail,
+ *   coeb_moving_object_points[_device]  <- Frame::ProcessMovingObject  src/Frame.cc:311-393
+ *                                      (OpenCV goodFeaturesToTrack / cornerSubPix / calcOpticalFlowPyrLK /
+ *                                      findFundamentalMat as called there)
  *   coeb_descriptor_distance        <- ORBmatcher::DescriptorDistance  src/ORBmatcher.cc:1648-1664
  *
  * Conventions: 0 on success, negative COEB_E* code on failure (the reference has no error
@@ -269,6 +273,48 @@ int coeb_undistort_keypoints(coeb_ctx* ctx, const coeb_camera* cam, const float 
                              int n, coeb_keypoint* out);
 /* yolov5_ros_msgs/BoundingBox (int64 xmin, ymin, xmax, ymax) -> coeb_box, as GrabRGBD converts */
 int coeb_boxes_from_int64(const int64_t* xyxy, int nbox, coeb_box* out);
+
+/* ---- Frame::ProcessMovingObject (src/Frame.cc:311-393): T_M from imGrayPre and imgray ----
+ * Each stage replaces the OpenCV 3.4 call Frame.cc makes, in the canonical forms of DESIGN.md
+ * s2.1 / s4.10 (parity against the oracle; OpenCV itself is absent, parity vs it UNPINNED):
+ *   coeb_good_features        <- cv::goodFeaturesToTrack(img, pts, 1000, 0.01, 8, Mat(), 3, true, 0.04)  :333
+ *                                (*n_out = corner count; COEB_ERANGE past 16384 local maxima)
+ *   coeb_corner_subpix        <- cv::cornerSubPix(img, pts, Size(10,10), Size(-1,-1), (ITER|EPS, 20, 0.03))  :334
+ *                                (in place; win must be 10)
+ *   coeb_optical_flow_pyr_lk  <- cv::calcOpticalFlowPyrLK(prev, next, pts, next_pts, status, err,
+ *                                Size(22,22), 5, (ITER|EPS, 20, 0.01))  :335  (win <= 22)
+ *   coeb_moving_tail          <- the SAD check (:337-365), cv::findFundamentalMat(.., FM_RANSAC, 0.1, 0.99)
+ *                                (:373) and the epipolar distance test (:375-384); state in/out
+ *   coeb_moving_object_points <- the whole of ProcessMovingObject; *n_tm = |T_M|, or -1 when
+ *                                findFundamentalMat returns an empty Mat (the reference then reads
+ *                                an empty Mat: undefined behaviour)
+ * At most 1024 points per call (the reference asks for 1000 corners). */
+typedef struct {
+    float* corners_raw;   /* 1000 x 2: goodFeaturesToTrack output (optional) */
+    float* corners;       /* 1000 x 2: after cornerSubPix (optional) */
+    int* ncorners;
+    float* next_pts;      /* 1000 x 2: calcOpticalFlowPyrLK output */
+    uint8_t* status;      /* 1000: LK status */
+    uint8_t* state;       /* 1000: state after the SAD check */
+    double* F;            /* 9: the fundamental matrix */
+    int* nf;              /* |F_prepoint| */
+} coeb_flow_debug;
+int coeb_good_features(coeb_ctx* ctx, const uint8_t* img, int width, int height, size_t stride, int max_corners,
+                       double quality, double min_distance, double k, float* xy_out, int cap, int* n_out);
+int coeb_corner_subpix(coeb_ctx* ctx, const uint8_t* img, int width, int height, size_t stride, float* xy, int n,
+                       int win, int max_iter, double eps);
+int coeb_optical_flow_pyr_lk(coeb_ctx* ctx, const uint8_t* prev, const uint8_t* next, int width, int height,
+                             size_t stride, const float* prev_xy, int n, int win, int max_level, int max_count,
+                             double eps, float* next_xy, uint8_t* status);
+int coeb_moving_tail(coeb_ctx* ctx, const uint8_t* prev, const uint8_t* cur, int width, int height, size_t stride,
+                     const float* prev_xy, const float* next_xy, uint8_t* state, int n, float* tm_xy, int tm_cap,
+                     int* n_tm, double F_out[9], int* nf_out);
+int coeb_moving_object_points(coeb_ctx* ctx, const uint8_t* prev, const uint8_t* cur, int width, int height,
+                              size_t stride, float* tm_xy, int tm_cap, int* n_tm, coeb_flow_debug* dbg);
+/* the same on device-resident frames (pitch stride) */
+int coeb_moving_object_points_device(coeb_ctx* ctx, const uint8_t* d_prev, const uint8_t* d_cur, int width,
+                                     int height, size_t stride, float* tm_xy, int tm_cap, int* n_tm,
+                                     coeb_flow_debug* dbg);
 
 int coeb_descriptor_distance(const uint8_t* a, const uint8_t* b);
 

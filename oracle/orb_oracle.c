@@ -2517,16 +2517,18 @@ static int fm_subset(const float* m1, const float* m2, int count, uint64_t* rng,
     return i == 7 && iters < max_attempts;
 }
 
-/* RANSACUpdateNumIters(p, ep, 7, maxIters) */
+/* RANSACUpdateNumIters(p, ep, 7, maxIters); std::log -> the canonical fdlibm log, std::pow(x, 7)
+ * -> x*x*x*x*x*x*x left to right */
 int oc_ransac_update_iters(double p, double ep, int max_iters)
 {
     p = p > 0. ? p : 0.; p = p < 1. ? p : 1.;
     ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
     double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
-    double denom = 1. - pow(1. - ep, 7);
+    const double b = 1. - ep;
+    double denom = 1. - b * b * b * b * b * b * b;
     if (denom < DBL_MIN) return 0;
-    num = log(num);
-    denom = log(denom);
+    num = oc_fd_log(num);
+    denom = oc_fd_log(denom);
     return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)lrint(num / denom);
 }
 

@@ -1,0 +1,152 @@
+"""Frame::ProcessMovingObject (src/Frame.cc:311-393) on the HIP path vs the CPU oracle, stage by
+stage and end to end (MI355X only).  Every comparison is bit-exact: corner and flow coordinates
+are float32 and F is float64, produced by the same canonical arithmetic;
+OpenCV itself is absent, so parity against it is unpinned."""
+import numpy as np
+import pytest
+
+import coeb_front as cf
+from coeb_front import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def pairs():
+    out = []
+    for seed in range(3):
+        prev, cur, _ = synth.moving_object_pair(640, 480, seed)
+        out.append(("obj%d" % seed, prev, cur))
+    fr = synth.make_frames(640, 480, 2, seed=1003)
+    out.append(("tum", fr[0], fr[1]))
+    return out
+
+
+PAIRS = pairs()
+
+
+def eq(a, b, tag):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (tag, a.shape, b.shape)
+    bad = np.nonzero((a != b).reshape(len(a), -1).any(axis=1))[0] if len(a) else []
+    assert len(bad) == 0, (tag, len(bad), a[bad[:3]], b[bad[:3]])
+
+
+@pytest.mark.parametrize("tag,prev,cur", PAIRS, ids=[p[0] for p in PAIRS])
+def test_good_features(ctx, oracle_mod, tag, prev, cur):
+    got = cf.GoodFeaturesToTrack(ctx, prev)
+    ref = oracle_mod.good_features(prev)
+    assert len(ref) > 50
+    eq(got, ref, tag)
+
+
+def test_good_features_edges(ctx, oracle_mod):
+    flat = np.full((96, 128), 77, np.uint8)
+    assert len(cf.GoodFeaturesToTrack(ctx, flat)) == 0
+    assert len(oracle_mod.good_features(flat)) == 0
+    small = synth.moving_object_pair(640, 480, 5)[0][100:164, 200:296].copy()
+    eq(cf.GoodFeaturesToTrack(ctx, small), oracle_mod.good_features(small), "small")
+    for mc in (1, 17, 250):                            # maxCorners cut of the greedy order
+        eq(cf.GoodFeaturesToTrack(ctx, PAIRS[0][1], max_corners=mc), oracle_mod.good_features(PAIRS[0][1], mc), mc)
+    # equal responses: a regular grid of identical corners exercises the index tie-break
+    grid = np.zeros((120, 160), np.uint8)
+    for y in range(10, 110, 20):
+        for x in range(10, 150, 20):
+            grid[y:y + 10, x:x + 10] = 200
+    eq(cf.GoodFeaturesToTrack(ctx, grid), oracle_mod.good_features(grid), "grid")
+
+
+@pytest.mark.parametrize("tag,prev,cur", PAIRS, ids=[p[0] for p in PAIRS])
+def test_corner_subpix(ctx, oracle_mod, tag, prev, cur):
+    pts = oracle_mod.good_features(prev)
+    eq(cf.CornerSubPix(ctx, prev, pts), oracle_mod.corner_subpix(prev, pts), tag)
+
+
+def test_corner_subpix_border(ctx, oracle_mod):
+    prev = PAIRS[0][1]
+    h, w = prev.shape
+    pts = np.array([[1, 1], [w - 2, h - 2], [0.5, 3.25], [w - 1.5, 40.75], [11.2, 11.9], [320.4, 2.0],
+                    [630.1, 470.2], [5, h - 1]], np.float32)
+    eq(cf.CornerSubPix(ctx, prev, pts), oracle_mod.corner_subpix(prev, pts), "border")
+
+
+@pytest.mark.parametrize("tag,prev,cur", PAIRS, ids=[p[0] for p in PAIRS])
+def test_lk(ctx, oracle_mod, tag, prev, cur):
+    pts = oracle_mod.corner_subpix(prev, oracle_mod.good_features(prev))
+    nx, st = cf.CalcOpticalFlowPyrLK(ctx, prev, cur, pts)
+    rnx, rst = oracle_mod.lk_pyr(prev, cur, pts)
+    eq(st, rst, tag + " status")
+    eq(nx, rnx, tag + " next")
+
+
+def test_lk_edges(ctx, oracle_mod):
+    prev, cur = PAIRS[1][1], PAIRS[1][2]
+    h, w = prev.shape
+    pts = np.array([[0, 0], [w - 1, h - 1], [-3, 10], [w + 40, 20], [2.5, h - 1.5], [320, 240], [11, 470]],
+                   np.float32)
+    nx, st = cf.CalcOpticalFlowPyrLK(ctx, prev, cur, pts)
+    rnx, rst = oracle_mod.lk_pyr(prev, cur, pts)
+    eq(st, rst, "status")
+    eq(nx[rst == 1], rnx[rst == 1], "next")
+    # a flat pair: every point fails the minimum-eigenvalue test
+    flat = np.full((120, 160), 90, np.uint8)
+    _, st = cf.CalcOpticalFlowPyrLK(ctx, flat, flat, np.array([[80, 60], [20, 30]], np.float32))
+    assert not st.any()
+
+
+@pytest.mark.parametrize("tag,prev,cur", PAIRS, ids=[p[0] for p in PAIRS])
+def test_moving_tail(ctx, oracle_mod, tag, prev, cur):
+    pts = oracle_mod.corner_subpix(prev, oracle_mod.good_features(prev))
+    nx, st = oracle_mod.lk_pyr(prev, cur, pts)
+    tm, st2, F, nf = cf.MovingTail(ctx, prev, cur, pts, nx, st)
+    rtm, rst2, rF, rnf = oracle_mod.moving_tail(prev, cur, pts, nx, st)
+    eq(st2, rst2, tag + " state")
+    assert nf == rnf
+    assert (F is None) == (rF is None)
+    if F is not None:
+        assert np.array_equal(F, rF), (F, rF)
+        eq(tm, rtm, tag + " T_M")
+
+
+@pytest.mark.parametrize("npts", [0, 5, 7, 9, 12, 14, 15, 40])
+def test_moving_tail_small_sets(ctx, oracle_mod, npts):
+    """n < 7 (empty F), n == 7 (run7Point), 8..14 (LMeDS), >= 15 (RANSAC)"""
+    prev, cur = PAIRS[2][1], PAIRS[2][2]
+    pts = oracle_mod.corner_subpix(prev, oracle_mod.good_features(prev))
+    nx, st = oracle_mod.lk_pyr(prev, cur, pts)
+    keep = np.nonzero(st)[0][:npts]
+    p, q, s = pts[keep], nx[keep], st[keep]
+    tm, st2, F, nf = cf.MovingTail(ctx, prev, cur, p, q, s)
+    rtm, rst2, rF, rnf = oracle_mod.moving_tail(prev, cur, p, q, s)
+    assert nf == rnf
+    eq(st2, rst2, "state")
+    assert (F is None) == (rF is None)
+    if npts < 7:
+        assert F is None
+    if F is not None:
+        assert np.array_equal(F, rF)
+        eq(tm, rtm, "T_M")
+
+
+@pytest.mark.parametrize("tag,prev,cur", PAIRS, ids=[p[0] for p in PAIRS])
+def test_process_moving_object(ctx, oracle_mod, tag, prev, cur):
+    tm, d = cf.ProcessMovingObject(ctx, prev, cur, debug=True)
+    ref = oracle_mod.process_moving_object(prev, cur)
+    assert (tm is None) == (ref is None)
+    if ref is not None:
+        eq(tm, ref, tag)
+    pts = oracle_mod.good_features(prev)
+    eq(d["corners_raw"], pts, "gf")
+    sp = oracle_mod.corner_subpix(prev, pts)
+    eq(d["corners"], sp, "subpix")
+    rnx, rst = oracle_mod.lk_pyr(prev, cur, sp)
+    eq(d["status"], rst, "lk status")
+
+
+def test_process_moving_object_flags_object(ctx):
+    """size-independent property: T_M of the layered scene lies on the moving object"""
+    for seed in range(3):
+        prev, cur, (x0, y0, x1, y1) = synth.moving_object_pair(640, 480, seed)
+        tm = cf.ProcessMovingObject(ctx, prev, cur)
+        assert tm is not None and len(tm) >= 20
+        inb = (tm[:, 0] >= x0 - 2) & (tm[:, 0] < x1 + 2) & (tm[:, 1] >= y0 - 2) & (tm[:, 1] < y1 + 2)
+        assert inb.mean() > 0.8, (seed, inb.mean())
