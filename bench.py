@@ -154,6 +154,8 @@ def cpu_extras(out, w, h, reps=5):
     timed("pose_optimization_ms", lambda: O.pose_optimization(P["kps"], P["has_mp"], P["xw"], P["ur"], isg,
                                                               synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY,
                                                               synth.TUM_BF, P["Tcw_init"]))
+    prev, cur, _ = synth.moving_object_pair(640, 480, 0)
+    timed("process_moving_object_ms", lambda: O.process_moving_object(prev, cur))
     return res
 
 
@@ -278,6 +280,10 @@ def extras_timing(ctx, out, w, h, reps=20):
     dist = (0.262383, -0.953104, -0.005358, 0.002628, 1.163314)
     timed("undistort_keypoints", lambda: len(cf.UndistortKeyPoints(ctx, kp1, cam, dist)),
           "UndistortKeyPoints, %d keypoints, TUM1 distortion" % len(kp1))
+    prev, cur, _ = synth.moving_object_pair(640, 480, 0)
+    timed("process_moving_object", lambda: len(cf.ProcessMovingObject(ctx, prev, cur)),
+          "ProcessMovingObject 640x480 (goodFeaturesToTrack 1000, cornerSubPix, 5-level LK, RANSAC F), "
+          "result = |T_M|")
     return res
 
 

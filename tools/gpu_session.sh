@@ -25,6 +25,8 @@ for step in "$@"; do
         benchB) run benchB 600 python bench.py --config B --batch 64 --no-cpu-baseline ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-e2e ;;
         diag) run diag 600 python tools/diag_parity.py ;;
+        flow) run flow 300 python tools/flow_bench.py ;;
+        flowprof) run flowprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/flowprof -o run -- python tools/flow_bench.py ;;
         pmc)
             B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-e2e"
             run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- $B
