@@ -3,6 +3,7 @@
 #include "ORBextractor.h"
 #include "ORBmatcher_coeb.h"
 #include "Optimizer_coeb.h"
+#include "Frame_coeb.h"
 
 struct MapPoint {
     cv::Mat GetWorldPos() { return cv::Mat(); }
@@ -37,6 +38,13 @@ struct Frame {
 };
 float Frame::fx, Frame::fy, Frame::cx, Frame::cy, Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY, Frame::mnMaxY;
 
+int moving_points(const cv::Mat& im)
+{
+    std::vector<cv::Point2f> T_M;
+    coeb::ProcessMovingObject(im, im, T_M);
+    return (int)T_M.size();
+}
+
 int use_adapters(Frame& cur, const Frame& last, cv::Mat& im)
 {
     ORB_SLAM2::ORBextractor ex(1000, 1.2f, 8, 20, 7);
@@ -50,5 +58,5 @@ int use_adapters(Frame& cur, const Frame& last, cv::Mat& im)
     return coeb::SearchByProjectionLastFrame(cur, last, 15.0f, false, 0.9f, true) + ex.GetLevels() +
            coeb::SearchByProjectionLocalMap(cur, local, 3.0f, 0.8f) +
            coeb::SearchByProjectionKeyFrame(cur, (KeyFrame*)nullptr, std::set<MapPoint*>(), 10.0f, 100, true) +
-           coeb::PoseOptimization(&cur);
+           coeb::PoseOptimization(&cur) + moving_points(im);
 }
