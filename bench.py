@@ -30,7 +30,20 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
 CONFIGS = {
     "A": dict(w=640, h=480, nfeatures=1000, workload="640x480, 8-level pyramid, 1000 kp, extract + Hamming match to prev frame (BASELINE configs[1])"),
     "B": dict(w=1280, h=960, nfeatures=2000, workload="1280x960, 8-level pyramid, 2000 kp, extract + match (BASELINE configs[3] shape)"),
+    "C": dict(w=640, h=480, nfeatures=1000, dyn=True,
+              workload="640x480, 1000 kp, YOLO-bbox dynamic mask (2 boxes, 60 T_M points, blur_flag [0,1]) + "
+                       "depth association (ComputeStereoFromRGBD) + match to prev frame (BASELINE configs[2])"),
+    "D": dict(w=640, h=480, nfeatures=1000, pose=True,
+              workload="640x480, 1000 kp, TrackWithMotionModel step: extract + match to prev frame + "
+                       "Optimizer::PoseOptimization (4 x 10 LM iterations) per frame (BASELINE configs[4])"),
 }
+
+
+def dyn_batch(w, h, F, seed0=0):
+    """Per-frame (boxes, T_M, blur_flag) of config 3: two boxes, 30 T_M points
+    inside them and 30 outside, a fresh T_M draw per frame."""
+    from coeb_front import synth
+    return [synth.dynamic_inputs(w, h, seed=seed0 + f) for f in range(F)]
 
 
 def level_pixels(w, h, nlevels=8, scale=1.2):
@@ -215,7 +228,7 @@ class DryRunPipeline:
     def load(self, frames, **kw):
         self.F = len(frames)
 
-    def run(self):
+    def run(self, pose=False):
         time.sleep(0.002 * (1 + self.rank))   # ranks finish at different times: max must win
 
     def synchronize(self):
@@ -287,6 +300,41 @@ def extras_timing(ctx, out, w, h, reps=20):
     return res
 
 
+def config5_timing(bp, batch, steps=10):
+    """BASELINE configs[4] on the same batch: extract + match + TrackWithMotionModel's
+    PoseOptimization for every matched frame, device-resident like `value`."""
+    bp.run(pose=True)
+    bp.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        bp.run(pose=True)
+    bp.synchronize()
+    dt = time.perf_counter() - t0
+    _, nin, _ = bp.pose_results()
+    return dict(value=round(batch * steps / dt, 2), unit="frames/s", ms_per_step=round(dt / steps * 1e3, 4),
+                steps=steps, tracked_frames=int(sum(1 for x in nin[1:] if x > 0)),
+                inliers_per_frame=round(float(np.mean(nin[1:])), 1),
+                note="extract + SearchByProjection + PoseOptimization per frame (bench.py --config D for the full line)")
+
+
+def config3_timing(bp, frames, Tcw, w, h, batch, steps=10):
+    """BASELINE configs[2] on the same batch: extract with the dynamic mask (boxes, T_M,
+    blur_flag per frame) + depth association + match, device-resident like `value`."""
+    bp.load(frames, Tcw=Tcw, dyn=dyn_batch(w, h, batch + 1))
+    bp.run()
+    bp.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        bp.run()
+    bp.synchronize()
+    dt = time.perf_counter() - t0
+    out, _, nms = bp.results()
+    return dict(value=round(batch * steps / dt, 2), unit="frames/s", ms_per_step=round(dt / steps * 1e3, 4),
+                steps=steps, keypoints_per_frame=round(float(np.mean([len(o[0]) for o in out[1:]])), 1),
+                matches_per_frame=round(float(np.mean(nms[1:])), 1),
+                note="640x480, 2 boxes + 60 T_M points + blur_flag [0,1] per frame (bench.py --config C for the full line)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -321,13 +369,15 @@ def main():
         from coeb_front.pipeline import BatchPipeline
         bp = BatchPipeline(w, h, F, nfeatures=cfg["nfeatures"], device=local_rank)
     bp.ctx.set_batch_streams(args.streams)
-    bp.load(frames, Tcw=Tcw)
+    dyn = dyn_batch(w, h, F, 17 * rank) if cfg.get("dyn") else None
+    bp.load(frames, Tcw=Tcw, dyn=dyn)
 
     def barrier():
         ranks.barrier()
 
+    pose = bool(cfg.get("pose"))
     for _ in range(args.warmup):
-        bp.run()
+        bp.run(pose=pose)
     bp.synchronize()
     out, matches, nms = bp.results()
     nkp = float(np.mean([len(o[0]) for o in out[1:]]))
@@ -339,7 +389,7 @@ def main():
     bp.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        bp.run()
+        bp.run(pose=pose)
     bp.synchronize()
     t1 = time.perf_counter()
     barrier()
@@ -355,7 +405,7 @@ def main():
         bp.ctx.profile(True)
         bp.ctx.profile_reset()
         for _ in range(prof_steps):
-            bp.run()
+            bp.run(pose=pose)
         bp.synchronize()
         prof = bp.ctx.profile_read()
         bp.ctx.profile(False)
@@ -424,6 +474,9 @@ def main():
                     pcie_inclusive=e2e)
         if not args.no_extras and world == 1 and not args.dry_run:
             line["extras"] = extras_timing(bp.ctx, out, w, h)
+            if not cfg.get("dyn") and not cfg.get("pose"):
+                line["extras"]["config5_tracking"] = config5_timing(bp, args.batch)
+                line["extras"]["config3_dynamic_mask"] = config3_timing(bp, frames, Tcw, w, h, args.batch)
         if not args.no_cpu_baseline and world == 1 and not args.dry_run:
             cb = cpu_baseline(cfg)
             if "extras" in line:

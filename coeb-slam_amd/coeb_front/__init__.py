@@ -48,6 +48,7 @@ ABI_SYMBOLS = [
     "coeb_match_localmap", "coeb_match_keyframe", "coeb_pose_optimization", "coeb_undistort_keypoints",
     "coeb_boxes_from_int64", "coeb_good_features", "coeb_corner_subpix", "coeb_optical_flow_pyr_lk",
     "coeb_moving_tail", "coeb_moving_object_points", "coeb_moving_object_points_device",
+    "coeb_pose_batch_device", "coeb_batch_pose_results",
 ]
 
 
@@ -126,6 +127,9 @@ def lib():
         L.coeb_match_batch_device_tcw.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                   C.POINTER(Camera), C.c_void_p, C.c_float, C.c_int32]
         L.coeb_batch_match_results.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.coeb_pose_batch_device.argtypes = [C.c_void_p, C.POINTER(Camera), C.c_int, C.c_void_p, C.c_int32]
+        L.coeb_batch_pose_results.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                              C.POINTER(C.c_void_p)]
         L.coeb_match_lastframe.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(CurFrameC),
                                            C.POINTER(LastFrameC), C.c_void_p, C.c_void_p, C.c_float, C.c_int,
                                            C.c_int, C.c_void_p, C.POINTER(C.c_int)]
@@ -275,6 +279,15 @@ class Context:
         m, n = C.c_void_p(), C.c_void_p()
         self.check(lib().coeb_batch_match_results(self.h, C.byref(m), C.byref(n)))
         return m.value, n.value
+
+    def pose_batch_device(self, cam, nframes, d_tcw_ptr, min_matches=20):
+        """TrackWithMotionModel's PoseOptimization over the batch matched last (Tracking.cc:947-964)."""
+        self.check(lib().coeb_pose_batch_device(self.h, C.byref(cam), nframes, C.c_void_p(d_tcw_ptr), min_matches))
+
+    def batch_pose_results(self):
+        t, n, o = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self.check(lib().coeb_batch_pose_results(self.h, C.byref(t), C.byref(n), C.byref(o)))
+        return t.value, n.value, o.value
 
     def synchronize(self):
         self.check(lib().coeb_synchronize(self.h))

@@ -53,8 +53,9 @@ class BatchPipeline:
                         np.asarray(tm_off, np.int32), np.concatenate(blurs))
         self.ctx.synchronize()
 
-    def run(self, match=True, th=15.0, nobs=2):
-        """Enqueue one step (extraction of F frames + F-1 matches); does not synchronise."""
+    def run(self, match=True, th=15.0, nobs=2, pose=False):
+        """Enqueue one step (extraction of F frames + F-1 matches, and with pose=True the
+        motion-model PoseOptimization of every matched frame); does not synchronise."""
         if self.dyn is not None:
             b, bo, t, to, bl = self.dyn
             self.ctx.extract_batch_device(self.gray.ptr, self.F, self.W, self.H, b, bo, t, to, bl)
@@ -62,6 +63,8 @@ class BatchPipeline:
             self.ctx.extract_batch_device(self.gray.ptr, self.F, self.W, self.H)
         if match:
             self.ctx.match_batch_device_tcw(self.depth.ptr, self.F, self.W, self.H, self.cam, self.dTcw.ptr, th, nobs)
+            if pose:
+                self.ctx.pose_batch_device(self.cam, self.F, self.dTcw.ptr)
 
     def synchronize(self):
         self.ctx.synchronize()
@@ -102,6 +105,17 @@ class BatchPipeline:
             matches = [None] + [mm[f, :counts[f]].copy() for f in range(1, self.F)]
             nm = [None] + [int(x) for x in nm[1:]]
         return out, matches, nm
+
+    def pose_results(self):
+        """Host copies after run(pose=True): Tcw (F, 4, 4) (frame 0 unused), inliers per frame
+        (0: not tracked), outlier flags per frame (frame 0: None)."""
+        kp_ptr, _, cnt_ptr, kcap = self.ctx.batch_results()
+        counts = self.ctx.download(cnt_ptr, 4 * self.F, np.int32)
+        t_ptr, n_ptr, o_ptr = self.ctx.batch_pose_results()
+        T = self.ctx.download(t_ptr, 64 * self.F, np.float32).reshape(self.F, 4, 4)
+        nin = self.ctx.download(n_ptr, 4 * self.F, np.int32)
+        outl = self.ctx.download(o_ptr, kcap * self.F, np.uint8).reshape(self.F, kcap)
+        return T, [int(x) for x in nin], [None] + [outl[f, :counts[f]].copy() for f in range(1, self.F)]
 
     def close(self):
         for b in (self.gray, self.depth, self.dTcw):

@@ -1186,6 +1186,62 @@ int coeb_batch_match_results(coeb_ctx* c, const int32_t** d_match, const int32_t
     return COEB_OK;
 }
 
+int coeb_pose_batch_device(coeb_ctx* c, const coeb_camera* cam, int F, const float* d_Tcw, int32_t min_matches)
+{
+    if (!c || !cam || !d_Tcw || F <= 0) return set_err(c, COEB_EINVAL, "coeb_pose_batch_device: invalid arguments");
+    if (!c->has_plan || c->batch_frames != F || !c->bufs.count("b_match") || !c->bufs.count("b_xw"))
+        return set_err(c, COEB_EINVAL, "coeb_pose_batch_device: must follow coeb_match_batch_device on the same batch");
+    (void)hipSetDevice(c->device);
+    const int K = c->plan.kcap;
+    int rc;
+    float *tout, *txw, *isg;
+    uint8_t *thas, *toutl, *tact;
+    int32_t *tn, *tres;
+    PoseEdgeRec* tedge;
+    double* tchi;
+    if ((rc = ensure(c, "t_T", (size_t)F * 16, &tout)) || (rc = ensure(c, "t_xw", (size_t)F * K * 3, &txw)) ||
+        (rc = ensure(c, "t_isg", COEB_MAXL, &isg)) || (rc = ensure(c, "t_has", (size_t)F * K, &thas)) ||
+        (rc = ensure(c, "t_outl", (size_t)F * K, &toutl)) || (rc = ensure(c, "t_act", (size_t)F * K, &tact)) ||
+        (rc = ensure(c, "t_n", (size_t)F, &tn)) || (rc = ensure(c, "t_res", (size_t)F, &tres)) ||
+        (rc = ensure(c, "t_edge", (size_t)F * K, &tedge)) || (rc = ensure(c, "t_chi", (size_t)F * K, &tchi)))
+        return rc;
+    hipStream_t s = main_stream(c);                 // joins the matchers' chunk streams
+    HIP_TRY(c, hipMemsetAsync(thas, 0, (size_t)F * K, s));
+    HIP_TRY(c, hipMemsetAsync(toutl, 0, (size_t)F * K, s));
+    HIP_TRY(c, hipMemsetAsync(tres, 0, (size_t)F * 4, s));
+    TrackPrepBufs t;
+    memset(&t, 0, sizeof(t));
+    t.match = static_cast<const int32_t*>(c->bufs["b_match"].p);
+    t.nmatch = static_cast<const int32_t*>(c->bufs["b_nm"].p);
+    t.counts = static_cast<const int32_t*>(c->bufs["counts"].p);
+    t.last_xw = static_cast<const float*>(c->bufs["b_xw"].p);
+    t.Tin = d_Tcw; t.Tout = tout; t.has = thas; t.xw = txw; t.n = tn; t.isg_out = isg;
+    for (int l = 0; l < COEB_MAXL; l++) t.isg[l] = l < c->tab.nlevels ? c->tab.inv_sigma2[l] : 0.f;
+    t.stride = K;
+    t.min_matches = min_matches;
+    if (launch_track_prep(t, F, s, &c->hook)) return hip_err(c, hipGetLastError(), "launch_track_prep");
+    if (F < 2) return COEB_OK;
+    const int64_t o = K;                            // frame 1 = current frame of pair 0
+    PoseBufs b;
+    b.n = tn + 1; b.has_mp = thas + o; b.xw = txw + 3 * o;
+    b.kps = static_cast<const coeb_keypoint*>(c->bufs["kps"].p) + o;
+    b.ur = static_cast<const float*>(c->bufs["b_ur"].p) + o;
+    b.inv_sigma2 = isg; b.Tcw = tout + 16; b.outlier = toutl + o; b.result = tres + 1;
+    b.edges = tedge + o; b.active = tact + o; b.chi2 = tchi + o; b.stride = K;
+    if (launch_pose(b, F - 1, cam->fx, cam->fy, cam->cx, cam->cy, cam->bf, s, &c->hook))
+        return hip_err(c, hipGetLastError(), "launch_pose");
+    return COEB_OK;
+}
+
+int coeb_batch_pose_results(coeb_ctx* c, const float** d_Tcw, const int32_t** d_ninliers, const uint8_t** d_outlier)
+{
+    if (!c || !c->bufs.count("t_T")) return set_err(c, COEB_EINVAL, "coeb_batch_pose_results: no batch pose yet");
+    if (d_Tcw) *d_Tcw = static_cast<const float*>(c->bufs["t_T"].p);
+    if (d_ninliers) *d_ninliers = static_cast<const int32_t*>(c->bufs["t_res"].p);
+    if (d_outlier) *d_outlier = static_cast<const uint8_t*>(c->bufs["t_outl"].p);
+    return COEB_OK;
+}
+
 int coeb_stereo_from_rgbd(coeb_ctx* c, const coeb_keypoint* kps, int n, const float* depth, int W, int H,
                           size_t dstride, float bf, float* ur_out, float* dep_out)
 {

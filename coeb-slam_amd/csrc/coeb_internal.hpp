@@ -204,6 +204,24 @@ struct PoseBufs {
 int launch_pose(const PoseBufs& b, int F, double fx, double fy, double cx, double cy, double bf, hipStream_t s,
                 ProfileHook* prof);
 
+// TrackWithMotionModel tail on a device batch (coeb_pose.hip): pair p = (frame p, frame p+1).
+// All arrays are indexed from frame 0 ([F][stride]); frame 0 (the halo) is never written.
+struct TrackPrepBufs {
+    const int32_t* match;         // [F][stride] LastFrame index per current keypoint, or -1
+    const int32_t* nmatch;        // [F] SearchByProjection result (after the 2*th retry)
+    const int32_t* counts;        // [F] keypoints
+    const float* last_xw;         // [F][stride][3] LastFrame MapPoint positions (k_prep)
+    const float* Tin;             // [F][16] motion-model prediction
+    float* Tout;                  // [F][16] <- Tin, then PoseOptimization's result
+    uint8_t* has;                 // [F][stride] CurrentFrame.mvpMapPoints[i] != NULL
+    float* xw;                    // [F][stride][3] position of that MapPoint
+    int32_t* n;                   // [F] keypoints handed to the optimiser (0: not tracked)
+    float* isg_out;               // [COEB_MAXL] device copy of isg
+    float isg[COEB_MAXL];         // mvInvLevelSigma2
+    int stride, min_matches;
+};
+int launch_track_prep(const TrackPrepBufs& t, int F, hipStream_t s, ProfileHook* prof);
+
 // relocalisation projection search (ORBmatcher::SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist))
 struct KfBufsHost {
     const void* cur_kps; const uint8_t* cur_desc; const uint8_t* cur_has; int cur_n;

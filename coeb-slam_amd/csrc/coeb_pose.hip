@@ -488,7 +488,45 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
     }
 }
 
+// ================================ k_track_prep ================================
+// Tracking::TrackWithMotionModel between SearchByProjection and PoseOptimization
+// (src/Tracking.cc:947-964): CurrentFrame.mvpMapPoints[i] = the LastFrame MapPoint the
+// matcher assigned to keypoint i (its position: the LastFrame snapshot k_prep wrote), and
+// `if (nmatches < 20) return false` (:954-958) -- such a frame reaches the optimiser with no
+// keypoints, so k_pose leaves its pose at the prediction and reports 0.
+__global__ __launch_bounds__(kPT) void k_track_prep(TrackPrepBufs t)
+{
+    const int f = blockIdx.y + 1;
+    const int i = blockIdx.x * kPT + threadIdx.x;
+    const bool go = t.nmatch[f] >= t.min_matches;
+    const int n = t.counts[f];
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 16) t.Tout[(int64_t)f * 16 + threadIdx.x] = t.Tin[(int64_t)f * 16 + threadIdx.x];
+        if (threadIdx.x == 16) t.n[f] = go ? n : 0;
+        if (f == 1 && threadIdx.x >= 32 && threadIdx.x < 32 + COEB_MAXL) t.isg_out[threadIdx.x - 32] = t.isg[threadIdx.x - 32];
+    }
+    if (!go || i >= n) return;
+    const int64_t o = (int64_t)f * t.stride + i;
+    const int m = t.match[o];
+    t.has[o] = m >= 0 ? 1 : 0;
+    if (m >= 0) {
+        const int64_t q = ((int64_t)(f - 1) * t.stride + m) * 3;
+        t.xw[3 * o + 0] = t.last_xw[q + 0];
+        t.xw[3 * o + 1] = t.last_xw[q + 1];
+        t.xw[3 * o + 2] = t.last_xw[q + 2];
+    }
+}
+
 }  // namespace
+
+int launch_track_prep(const TrackPrepBufs& t, int F, hipStream_t s, ProfileHook* prof)
+{
+    if (F < 2) return 0;
+    prof_begin(prof, "k_track_prep", s);
+    hipLaunchKernelGGL(k_track_prep, dim3((t.stride + kPT - 1) / kPT, F - 1), dim3(kPT), 0, s, t);
+    prof_end(prof, s);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_pose(const PoseBufs& b, int F, double fx, double fy, double cx, double cy, double bf, hipStream_t s,
                 ProfileHook* prof)

@@ -36,6 +36,9 @@
  *   coeb_pose_optimization          <- Optimizer::PoseOptimization(Frame*)  include/Optimizer.h:47,
  *                                      src/Optimizer.cc:239-451 (g2o LM; g2o itself is not vendored,
  *                                      parity UNPINNED); calls Tracking.cc:841,964,1006
+ *   coeb_pose_batch_device          <- Tracking::TrackWithMotionModel after the projection search
+ *                                      src/Tracking.cc:947-964 (mvpMapPoints from the matches,
+ *                                      nmatches < 20 -> not tracked, PoseOptimization :964)
  *   coeb_good_features, coeb_corner_subpix, coeb_optical_flow_pyr_lk, coeb_moving_tail,
  *   coeb_moving_object_points[_device]  <- Frame::ProcessMovingObject  src/Frame.cc:311-393
  *                                      (OpenCV goodFeaturesToTrack / cornerSubPix / calcOpticalFlowPyrLK /
@@ -180,6 +183,18 @@ int coeb_match_batch_device(coeb_ctx* ctx, const float* d_depth, int nframes, in
 int coeb_match_batch_device_tcw(coeb_ctx* ctx, const float* d_depth, int nframes, int width, int height,
                                 const coeb_camera* cam, const float* d_Tcw, float th, int32_t nobs);
 int coeb_batch_match_results(coeb_ctx* ctx, const int32_t** d_match, const int32_t** d_nmatches);
+
+/* ---- Tracking::TrackWithMotionModel tail on the batch (Tracking.cc:947-964) ----
+ * After coeb_match_batch_device*: for every pair, CurrentFrame.mvpMapPoints = the matcher's
+ * assignments (positions from the LastFrame snapshot), then, if nmatches >= min_matches (20 in
+ * the reference, :954-958), Optimizer::PoseOptimization (as coeb_pose_optimization) from the
+ * prediction d_Tcw (the same nframes x 16 device array the matcher used).  Results (device,
+ * frame 0 = halo): coeb_batch_pose_results -> Tcw nframes x 16 (the prediction where the frame
+ * was not optimised), ninliers per frame (0: not tracked), outlier flags nframes x capacity. */
+int coeb_pose_batch_device(coeb_ctx* ctx, const coeb_camera* cam, int nframes, const float* d_Tcw,
+                           int32_t min_matches);
+int coeb_batch_pose_results(coeb_ctx* ctx, const float** d_Tcw, const int32_t** d_ninliers,
+                            const uint8_t** d_outlier);
 
 /* ---- ORBmatcher::SearchByProjection(CurrentFrame, LastFrame, th, bMono) ----
  * match_out[i2] (length cur->n) = index of the LastFrame slot whose MapPoint was assigned to

@@ -292,6 +292,57 @@ def test_batch_pipeline_matches_oracle(oracle_mod, ex):
         bp.close()
 
 
+def test_batch_track_pose_matches_oracle(oracle_mod, ex):
+    """BASELINE configs[4] slice on the device batch: extract + SearchByProjection + the
+    TrackWithMotionModel PoseOptimization (Tracking.cc:947-964) for every pair, against the
+    oracle run frame by frame (extract -> search with retry -> pose_optimization).  Frame 3
+    gets a prediction 180 degrees off: < 20 matches, so it must stay untracked (pose = the
+    prediction, 0 inliers)."""
+    from coeb_front.pipeline import BatchPipeline
+    F = 6
+    fr = synth.make_frames(640, 480, F, seed=777)
+    Tcw = np.stack([synth.motion_pose()] * F)
+    Tcw[3] = synth.rotated_pose(180.0, axis=1, t=(0, 0, 0))
+    bp = BatchPipeline(640, 480, F)
+    try:
+        bp.load(fr, Tcw=Tcw)
+        bp.run(pose=True)
+        bp.synchronize()
+        out, matches, nms = bp.results()
+        T_dev, nin_dev, outl_dev = bp.pose_results()
+        depth = synth.make_depth(640, 480)
+        cam_o = oracle_mod.camera(ex, 640, 480, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+        isg = np.array(bp.ctx.tables().inv_sigma2[:8], np.float32)
+        I4 = np.eye(4, dtype=np.float32)
+        prev = ex.extract(fr[0])
+        tracked = 0
+        for f in range(1, F):
+            r = ex.extract(fr[f])
+            last = oracle_mod.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX, synth.TUM_FY,
+                                                       synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+            ur, _ = oracle_mod.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
+            nm, m = oracle_mod.search_by_projection(cam_o, r["kps"], r["desc"], ur, last, Tcw[f], I4, 15.0)
+            if nm < 20:
+                nm, m = oracle_mod.search_by_projection(cam_o, r["kps"], r["desc"], ur, last, Tcw[f], I4, 30.0)
+            assert nms[f] == nm and np.array_equal(matches[f], m), f
+            if nm < 20:                                          # Tracking.cc:954-958: not tracked
+                assert nin_dev[f] == 0 and np.array_equal(T_dev[f].view(np.uint32), Tcw[f].view(np.uint32)), f
+            else:
+                has = (m >= 0).astype(np.uint8)
+                xw = np.zeros((len(m), 3), np.float32)
+                xw[m >= 0] = last["xw"][m[m >= 0]]
+                nin, T_ref, o_ref = oracle_mod.pose_optimization(r["kps"], has, xw, ur, isg, synth.TUM_FX, synth.TUM_FY,
+                                                                 synth.TUM_CX, synth.TUM_CY, synth.TUM_BF, Tcw[f])
+                assert nin_dev[f] == nin and nin > 0, (f, nin_dev[f], nin)
+                assert np.array_equal(T_dev[f].view(np.uint32), T_ref.view(np.uint32)), f
+                assert np.array_equal(outl_dev[f][has > 0], o_ref[has > 0]), f
+                tracked += 1
+            prev = r
+        assert tracked == F - 2 and nin_dev[3] == 0
+    finally:
+        bp.close()
+
+
 def test_batch_B_full_size_properties(oracle_mod):
     """Config B at full size: 1280x960, 2000 kp, batch of 16 -- properties for every frame,
     exact oracle parity on two of them."""

@@ -23,6 +23,8 @@ for step in "$@"; do
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
         benchB) run benchB 600 python bench.py --config B --batch 64 --no-cpu-baseline ;;
+        benchC) run benchC 600 python bench.py --config C --no-cpu-baseline --no-extras ;;
+        benchD) run benchD 600 python bench.py --config D --no-cpu-baseline --no-extras ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-e2e ;;
         diag) run diag 600 python tools/diag_parity.py ;;
         flow) run flow 300 python tools/flow_bench.py ;;
