@@ -357,6 +357,14 @@ struct coeb_ctx {
     bool pending_join = false;
     bool extract_chunked = false;                // the last batch extract ran on the chunk streams
     hipEvent_t ev_main = nullptr, ev_join = nullptr;
+    // coeb_pose_batch_device runs k_pose on its own stream, so the optimiser of batch k overlaps
+    // the extraction and matching of batch k+1 (k_pose is latency bound, one workgroup per frame;
+    // the extraction kernels are VALU bound).  k_track_prep copies everything k_pose reads into
+    // t_* buffers; the next coeb_pose_batch_device, coeb_batch_pose_results, coeb_memcpy_d2h,
+    // coeb_synchronize and coeb_destroy join it (join_pose()).
+    hipStream_t pose_stream = nullptr;
+    hipEvent_t ev_tprep = nullptr, ev_pose = nullptr;
+    bool pose_pending = false;
     // pinned host staging of the host-buffer entry points: their inputs are packed here and
     // moved in one copy (a dozen small pageable copies cost more than the kernels)
     uint8_t* pin = nullptr;
@@ -543,6 +551,15 @@ int upload_dyn(coeb_ctx* c, int F, const coeb_box* boxes, const int32_t* box_off
 
 // The context stream, after it has been made to wait for every chunk stream of the last
 // batch (so work enqueued on it sees the batch's results).
+// The context stream waits for the last batch pose (k_pose on pose_stream).
+void join_pose(coeb_ctx* c)
+{
+    if (c->pose_pending) {
+        (void)hipStreamWaitEvent(c->stream, c->ev_pose, 0);
+        c->pose_pending = false;
+    }
+}
+
 hipStream_t main_stream(coeb_ctx* c)
 {
     if (c->pending_join) {
@@ -680,6 +697,12 @@ void coeb_destroy(coeb_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(main_stream(c));
+    if (c->pose_stream) {
+        (void)hipStreamSynchronize(c->pose_stream);
+        (void)hipStreamDestroy(c->pose_stream);
+        (void)hipEventDestroy(c->ev_tprep);
+        (void)hipEventDestroy(c->ev_pose);
+    }
     for (auto& kv : c->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     c->prof.drain();
@@ -1194,7 +1217,8 @@ int coeb_pose_batch_device(coeb_ctx* c, const coeb_camera* cam, int F, const flo
     (void)hipSetDevice(c->device);
     const int K = c->plan.kcap;
     int rc;
-    float *tout, *txw, *isg;
+    float *tout, *txw, *isg, *tur;
+    coeb_keypoint* tkp;
     uint8_t *thas, *toutl, *tact;
     int32_t *tn, *tres;
     PoseEdgeRec* tedge;
@@ -1203,9 +1227,16 @@ int coeb_pose_batch_device(coeb_ctx* c, const coeb_camera* cam, int F, const flo
         (rc = ensure(c, "t_isg", COEB_MAXL, &isg)) || (rc = ensure(c, "t_has", (size_t)F * K, &thas)) ||
         (rc = ensure(c, "t_outl", (size_t)F * K, &toutl)) || (rc = ensure(c, "t_act", (size_t)F * K, &tact)) ||
         (rc = ensure(c, "t_n", (size_t)F, &tn)) || (rc = ensure(c, "t_res", (size_t)F, &tres)) ||
-        (rc = ensure(c, "t_edge", (size_t)F * K, &tedge)) || (rc = ensure(c, "t_chi", (size_t)F * K, &tchi)))
+        (rc = ensure(c, "t_edge", (size_t)F * K, &tedge)) || (rc = ensure(c, "t_chi", (size_t)F * K, &tchi)) ||
+        (rc = ensure(c, "t_kp", (size_t)F * K, &tkp)) || (rc = ensure(c, "t_ur", (size_t)F * K, &tur)))
         return rc;
     hipStream_t s = main_stream(c);                 // joins the matchers' chunk streams
+    if (!c->pose_stream) {
+        HIP_TRY(c, hipStreamCreateWithFlags(&c->pose_stream, hipStreamNonBlocking));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_tprep, hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_pose, hipEventDisableTiming));
+    }
+    join_pose(c);                                   // the previous batch's k_pose still reads t_*
     HIP_TRY(c, hipMemsetAsync(thas, 0, (size_t)F * K, s));
     HIP_TRY(c, hipMemsetAsync(toutl, 0, (size_t)F * K, s));
     HIP_TRY(c, hipMemsetAsync(tres, 0, (size_t)F * 4, s));
@@ -1215,6 +1246,8 @@ int coeb_pose_batch_device(coeb_ctx* c, const coeb_camera* cam, int F, const flo
     t.nmatch = static_cast<const int32_t*>(c->bufs["b_nm"].p);
     t.counts = static_cast<const int32_t*>(c->bufs["counts"].p);
     t.last_xw = static_cast<const float*>(c->bufs["b_xw"].p);
+    t.kps_in = c->bufs["kps"].p; t.ur_in = static_cast<const float*>(c->bufs["b_ur"].p);
+    t.kps_out = tkp; t.ur_out = tur;
     t.Tin = d_Tcw; t.Tout = tout; t.has = thas; t.xw = txw; t.n = tn; t.isg_out = isg;
     for (int l = 0; l < COEB_MAXL; l++) t.isg[l] = l < c->tab.nlevels ? c->tab.inv_sigma2[l] : 0.f;
     t.stride = K;
@@ -1224,18 +1257,22 @@ int coeb_pose_batch_device(coeb_ctx* c, const coeb_camera* cam, int F, const flo
     const int64_t o = K;                            // frame 1 = current frame of pair 0
     PoseBufs b;
     b.n = tn + 1; b.has_mp = thas + o; b.xw = txw + 3 * o;
-    b.kps = static_cast<const coeb_keypoint*>(c->bufs["kps"].p) + o;
-    b.ur = static_cast<const float*>(c->bufs["b_ur"].p) + o;
+    b.kps = tkp + o; b.ur = tur + o;
     b.inv_sigma2 = isg; b.Tcw = tout + 16; b.outlier = toutl + o; b.result = tres + 1;
     b.edges = tedge + o; b.active = tact + o; b.chi2 = tchi + o; b.stride = K;
-    if (launch_pose(b, F - 1, cam->fx, cam->fy, cam->cx, cam->cy, cam->bf, s, &c->hook))
+    HIP_TRY(c, hipEventRecord(c->ev_tprep, s));
+    HIP_TRY(c, hipStreamWaitEvent(c->pose_stream, c->ev_tprep, 0));
+    if (launch_pose(b, F - 1, cam->fx, cam->fy, cam->cx, cam->cy, cam->bf, c->pose_stream, &c->hook))
         return hip_err(c, hipGetLastError(), "launch_pose");
+    HIP_TRY(c, hipEventRecord(c->ev_pose, c->pose_stream));
+    c->pose_pending = true;
     return COEB_OK;
 }
 
 int coeb_batch_pose_results(coeb_ctx* c, const float** d_Tcw, const int32_t** d_ninliers, const uint8_t** d_outlier)
 {
     if (!c || !c->bufs.count("t_T")) return set_err(c, COEB_EINVAL, "coeb_batch_pose_results: no batch pose yet");
+    join_pose(c);
     if (d_Tcw) *d_Tcw = static_cast<const float*>(c->bufs["t_T"].p);
     if (d_ninliers) *d_ninliers = static_cast<const int32_t*>(c->bufs["t_res"].p);
     if (d_outlier) *d_outlier = static_cast<const uint8_t*>(c->bufs["t_outl"].p);
@@ -1353,6 +1390,7 @@ int coeb_memcpy_d2h(coeb_ctx* c, void* dst, const void* src, size_t bytes)
 {
     if (!c || (bytes && (!dst || !src))) return COEB_EINVAL;
     (void)hipSetDevice(c->device);
+    join_pose(c);
     HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, main_stream(c)));
     HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
     return COEB_OK;
@@ -1380,6 +1418,7 @@ int coeb_internal_error(coeb_ctx* c, int code, const char* msg) { return set_err
  * what = "pyr" | "blur" | "cand_n" | "lvl_n" | "lvl_kp" | "dyn"; copies min(bytes, size). */
 int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t bytes, size_t* size_out)
 {
+    if (c) join_pose(c);
     if (c && what && std::string(what) == "match_timing") {     // [F][16] k_match phase clocks (COEB_MATCH_TIMING)
         if (!c->bufs.count("m_timing")) return COEB_EINVAL;
         const size_t nb = c->bufs["m_timing"].n;
@@ -1426,6 +1465,7 @@ int coeb_synchronize(coeb_ctx* c)
 {
     if (!c) return COEB_EINVAL;
     (void)hipSetDevice(c->device);
+    join_pose(c);
     HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
     return check_err_word(c);
 }

@@ -211,6 +211,10 @@ struct TrackPrepBufs {
     const int32_t* nmatch;        // [F] SearchByProjection result (after the 2*th retry)
     const int32_t* counts;        // [F] keypoints
     const float* last_xw;         // [F][stride][3] LastFrame MapPoint positions (k_prep)
+    const void* kps_in;           // [F][stride] coeb_keypoint (batch output) -> kps_out
+    const float* ur_in;           // [F][stride] mvuRight (k_prep) -> ur_out
+    void* kps_out;
+    float* ur_out;
     const float* Tin;             // [F][16] motion-model prediction
     float* Tout;                  // [F][16] <- Tin, then PoseOptimization's result
     uint8_t* has;                 // [F][stride] CurrentFrame.mvpMapPoints[i] != NULL

@@ -253,9 +253,16 @@ __device__ bool pq_solve6(const double H[36], const double b[6], double x[6])
     return true;
 }
 
+// Partials of thread t live at slot t + t / 32 of a 264-double row: in block_reduce lane
+// (k, c) walks run c of value k, and without the skew all 64 lanes of a wave would read the
+// same LDS bank (runs 256 B apart, rows 2 KB apart).  With it, runs are 33 doubles apart and
+// rows 264 (≡ 8 mod 32): at most two lanes of a wave share a bank.
+constexpr int kPartRow = 264;
+__device__ __forceinline__ int part_slot(int t) { return t + (t >> 5); }
+
 struct PoseLds {
     Se3 s;                 // current estimate (broadcast)
-    double part[28][kPT];  // per-thread partials
+    double part[28][kPartRow];  // per-thread partials, skewed (part_slot)
     double run[28][8];     // 32-lane run sums
     double out[28];        // reduced
     double rho;
@@ -267,12 +274,12 @@ struct PoseLds {
 __device__ void block_reduce(PoseLds& L, double* v, int nv)
 {
     const int tid = threadIdx.x;
-    for (int k = 0; k < nv; k++) L.part[k][tid] = v[k];
+    for (int k = 0; k < nv; k++) L.part[k][part_slot(tid)] = v[k];
     __syncthreads();
     if (tid < nv * 8) {
         const int k = tid >> 3, c = tid & 7;
         double p = 0.0;
-        for (int l = 32 * c; l < 32 * c + 32; l++) p = p + L.part[k][l];
+        for (int l = 33 * c; l < 33 * c + 32; l++) p = p + L.part[k][l];   // threads 32c .. 32c+31 in order
         L.run[k][c] = p;
     }
     __syncthreads();
@@ -284,9 +291,20 @@ __device__ void block_reduce(PoseLds& L, double* v, int nv)
     __syncthreads();
 }
 
-__device__ __forceinline__ PEdge load_edge(const PoseBufs& b, int f, int e)
+// Edge storage of one thread: edges e = tid + kPT * j.  EPT > 0 keeps them in registers
+// (records, chi2, active bits; every pass then runs without global loads), EPT == 0 reads the
+// global scratch arrays (frames with more than kPT * EPT keypoints).  Both visit a thread's
+// edges in increasing e, so the per-thread partial sums -- and the results -- are the same.
+template <int EPT>
+struct EdgeSet {
+    static constexpr int R = EPT > 0 ? EPT : 1;
+    PoseEdgeRec rec[R];
+    double chi[R];
+    uint32_t act;
+};
+
+__device__ __forceinline__ PEdge edge_of(const PoseEdgeRec& r)
 {
-    const PoseEdgeRec r = b.edges[(int64_t)f * b.stride + e];
     PEdge E;
     E.X[0] = (double)r.x; E.X[1] = (double)r.y; E.X[2] = (double)r.z;
     E.obs[0] = (double)r.u; E.obs[1] = (double)r.v; E.obs[2] = r.stereo ? (double)r.ur : 0.0;
@@ -295,29 +313,60 @@ __device__ __forceinline__ PEdge load_edge(const PoseBufs& b, int f, int e)
     return E;
 }
 
-// computeActiveErrors + activeRobustChi2 at L.s; raw chi2 of active edges -> chi2_last
+// Runs the body over this thread's edges in increasing e with `rec` (the edge record), `act`
+// (its active flag; the body may change it) and `chi` (a reference to its chi2) in scope.
+#define COEB_FOR_EDGES(ES, ...)                                                                   \
+    if constexpr (EPT > 0) {                                                                        \
+        _Pragma("unroll") for (int j_ = 0; j_ < EPT; j_++) {                                        \
+            const int e = threadIdx.x + j_ * kPT;                                                   \
+            if (e < ne) {                                                                           \
+                const PoseEdgeRec& rec = ES.rec[j_];                                                \
+                bool act = (ES.act >> j_) & 1u;                                                     \
+                double& chi = ES.chi[j_];                                                           \
+                (void)chi;                                                                          \
+                __VA_ARGS__;                                                                        \
+                ES.act = (ES.act & ~(1u << j_)) | ((act ? 1u : 0u) << j_);                          \
+            }                                                                                       \
+        }                                                                                           \
+    } else {                                                                                        \
+        for (int e = threadIdx.x; e < ne; e += kPT) {                                               \
+            const PoseEdgeRec rec = b.edges[(int64_t)f * b.stride + e];                             \
+            bool act = b.active[(int64_t)f * b.stride + e] != 0;                                    \
+            double& chi = b.chi2[(int64_t)f * b.stride + e];                                        \
+            (void)chi;                                                                              \
+            __VA_ARGS__;                                                                            \
+            b.active[(int64_t)f * b.stride + e] = act ? 1 : 0;                                      \
+        }                                                                                           \
+    }
+
+// computeActiveErrors + activeRobustChi2 at L.s; raw chi2 of active edges -> chi2
+template <int EPT>
 __device__ double active_chi2(PoseLds& L, const PoseBufs& b, const PoseCam& cm, int f, int ne, bool robust,
-                              const double delta[2])
+                              const double delta[2], EdgeSet<EPT>& ES)
 {
     const Se3 s = L.s;
     double acc = 0.0;
-    for (int e = threadIdx.x; e < ne; e += kPT) {
-        if (!b.active[(int64_t)f * b.stride + e]) continue;
-        const PEdge E = load_edge(b, f, e);
-        double er[3];
-        const double c = pq_edge_eval(cm, s, E, er, nullptr);
-        b.chi2[(int64_t)f * b.stride + e] = c;
-        double r = c, r1;
-        if (robust) pq_huber(c, delta[E.stereo], r, r1);
-        acc += r;
-    }
+    COEB_FOR_EDGES(ES, {
+        if (act) {
+            const PEdge E = edge_of(rec);
+            double er[3];
+            const double c = pq_edge_eval(cm, s, E, er, nullptr);
+            chi = c;
+            double r = c, r1;
+            if (robust) pq_huber(c, delta[E.stereo], r, r1);
+            acc += r;
+        }
+    })
     double v[1] = {acc};
     block_reduce(L, v, 1);
     return L.out[0];
 }
 
+template <int EPT>
 __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
 {
+    EdgeSet<EPT> ES;
+    ES.act = 0;
     __shared__ PoseLds L;
     __shared__ int s_ne, s_cnt[4];
     const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -354,6 +403,14 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
         __syncthreads();
     }
     const int ne = s_ne;
+    if constexpr (EPT > 0) {                                       // own edges into registers
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            const int e = tid + j * kPT;
+            if (e < ne) { ES.rec[j] = b.edges[base + e]; ES.act |= 1u << j; }
+            ES.chi[j] = 0.0;
+        }
+    }
     float* Tcw = b.Tcw + (int64_t)f * 16;
     if (ne < 3) {                                                  // :361-362
         if (tid == 0) b.result[f] = 0;
@@ -371,15 +428,15 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
         // ---- optimize(10): OptimizationAlgorithmLevenberg::solve per iteration ----
         double lambda = 0.0, ni = 2.0;                             // thread 0's copies
         for (int iter = 0; iter < 10; iter++) {
-            double currentChi = active_chi2(L, b, cm, f, ne, robust, delta);
+            double currentChi = active_chi2<EPT>(L, b, cm, f, ne, robust, delta, ES);
             // buildSystem
             double acc[27];
             for (int k = 0; k < 27; k++) acc[k] = 0.0;
             {
                 const Se3 s = L.s;
-                for (int e = tid; e < ne; e += kPT) {
-                    if (!b.active[base + e]) continue;
-                    const PEdge E = load_edge(b, f, e);
+                COEB_FOR_EDGES(ES, {
+                    if (act) {
+                    const PEdge E = edge_of(rec);
                     double er[3], J[18];
                     const double c = pq_edge_eval(cm, s, E, er, J);
                     double r0, rho1 = 1.0;
@@ -397,7 +454,8 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
                         if (E.stereo) c1 = c1 + J[12 + a] * er[2];
                         acc[21 + a] += -(wgt * c1);
                     }
-                }
+                    }
+                })
             }
             block_reduce(L, acc, 27);
             double H[36], bv[6];
@@ -431,7 +489,7 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
                     L.s = pq_mul(up, saved);
                 }
                 __syncthreads();
-                double tempChi = active_chi2(L, b, cm, f, ne, robust, delta);
+                double tempChi = active_chi2<EPT>(L, b, cm, f, ne, robust, delta, ES);
                 if (tid == 0) {
                     if (!ok2) tempChi = DBL_MAX;
                     double scale = 0.0;
@@ -467,14 +525,14 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
         // ---- classification (Optimizer.cc:381-437) ----
         const Se3 s = L.s;
         int bad = 0;
-        for (int e = tid; e < ne; e += kPT) {
-            double c = b.chi2[base + e];
-            const PEdge E = load_edge(b, f, e);
-            if (!b.active[base + e]) { double er[3]; c = pq_edge_eval(cm, s, E, er, nullptr); b.chi2[base + e] = c; }
-            const int kp = b.edges[base + e].kp;
-            if (c > chi2th[E.stereo]) { b.outlier[base + kp] = 1; b.active[base + e] = 0; bad++; }
-            else { b.outlier[base + kp] = 0; b.active[base + e] = 1; }
-        }
+        COEB_FOR_EDGES(ES, {
+            const PEdge E = edge_of(rec);
+            if (!act) { double er[3]; chi = pq_edge_eval(cm, s, E, er, nullptr); }
+            const double c = chi;
+            const int kp = rec.kp;
+            if (c > chi2th[E.stereo]) { b.outlier[base + kp] = 1; act = false; bad++; }
+            else { b.outlier[base + kp] = 0; act = true; }
+        })
         for (int off = 32; off >= 1; off >>= 1) bad += __shfl_xor(bad, off, 64);
         if (lane == 0) L.nbad[wv] = bad;
         __syncthreads();
@@ -507,6 +565,8 @@ __global__ __launch_bounds__(kPT) void k_track_prep(TrackPrepBufs t)
     }
     if (!go || i >= n) return;
     const int64_t o = (int64_t)f * t.stride + i;
+    reinterpret_cast<KpRec*>(t.kps_out)[o] = reinterpret_cast<const KpRec*>(t.kps_in)[o];   // k_pose's own copies
+    t.ur_out[o] = t.ur_in[o];
     const int m = t.match[o];
     t.has[o] = m >= 0 ? 1 : 0;
     if (m >= 0) {
@@ -533,7 +593,11 @@ int launch_pose(const PoseBufs& b, int F, double fx, double fy, double cx, doubl
 {
     PoseCam cm{fx, fy, cx, cy, bf};
     prof_begin(prof, "k_pose", s);
-    hipLaunchKernelGGL(k_pose, dim3(F), dim3(kPT), 0, s, b, cm);
+    // edges per thread by the keypoint stride: registers up to 9 x 256 edges, else global scratch
+    const int ept = (b.stride + kPT - 1) / kPT;
+    if (ept <= 5) hipLaunchKernelGGL(k_pose<5>, dim3(F), dim3(kPT), 0, s, b, cm);
+    else if (ept <= 9) hipLaunchKernelGGL(k_pose<9>, dim3(F), dim3(kPT), 0, s, b, cm);
+    else hipLaunchKernelGGL(k_pose<0>, dim3(F), dim3(kPT), 0, s, b, cm);
     prof_end(prof, s);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -27,6 +27,7 @@ for step in "$@"; do
         benchD) run benchD 600 python bench.py --config D --no-cpu-baseline --no-extras ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-e2e ;;
         diag) run diag 600 python tools/diag_parity.py ;;
+        posetime) run posetime 300 python tools/pose_timing.py ;;
         flow) run flow 300 python tools/flow_bench.py ;;
         flowprof) run flowprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/flowprof -o run -- python tools/flow_bench.py ;;
         pmc)
