@@ -363,6 +363,9 @@ struct coeb_ctx {
     // t_* buffers; the next coeb_pose_batch_device, coeb_batch_pose_results, coeb_memcpy_d2h,
     // coeb_synchronize and coeb_destroy join it (join_pose()).
     hipStream_t pose_stream = nullptr;
+    // level-0 blur + FAST beside the pyramid (launch_extract's SideStream); COEB_SIDE_STREAM=0 disables
+    SideStream side{nullptr, nullptr, nullptr, nullptr, 2};
+    bool side_init = false;
     hipEvent_t ev_tprep = nullptr, ev_pose = nullptr;
     bool pose_pending = false;
     // pinned host staging of the host-buffer entry points: their inputs are packed here and
@@ -551,6 +554,27 @@ int upload_dyn(coeb_ctx* c, int F, const coeb_box* boxes, const int32_t* box_off
 
 // The context stream, after it has been made to wait for every chunk stream of the last
 // batch (so work enqueued on it sees the batch's results).
+// The side stream of launch_extract (created on first use), or null when disabled.  Per-kernel
+// profiling (coeb_profile_enable) serialises everything on the context stream, so each event
+// pair brackets one whole-batch launch.
+const SideStream* side_stream(coeb_ctx* c)
+{
+    if (c->prof.enabled) return nullptr;
+    if (!c->side_init) {
+        c->side_init = true;
+        const char* e = getenv("COEB_SIDE_STREAM");
+        if (e && e[0] == '0') return nullptr;
+        const char* sp = getenv("COEB_SIDE_SPLIT");          // first level left to the context stream
+        if (sp) c->side.split = atoi(sp);
+        if (hipStreamCreateWithFlags(&c->side.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->side.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->side.mid, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->side.join, hipEventDisableTiming) != hipSuccess)
+            c->side.s = nullptr;
+    }
+    return c->side.s ? &c->side : nullptr;
+}
+
 // The context stream waits for the last batch pose (k_pose on pose_stream).
 void join_pose(coeb_ctx* c)
 {
@@ -697,6 +721,13 @@ void coeb_destroy(coeb_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(main_stream(c));
+    if (c->side.s) {
+        (void)hipStreamSynchronize(c->side.s);
+        (void)hipStreamDestroy(c->side.s);
+        (void)hipEventDestroy(c->side.fork);
+        (void)hipEventDestroy(c->side.mid);
+        (void)hipEventDestroy(c->side.join);
+    }
     if (c->pose_stream) {
         (void)hipStreamSynchronize(c->pose_stream);
         (void)hipStreamDestroy(c->pose_stream);
@@ -777,7 +808,8 @@ int coeb_extract_batch_device(coeb_ctx* c, const uint8_t* d_gray, int F, int W, 
     c->mdone_valid = false;
     c->extract_chunked = n > 1;
     if (n == 1) {
-        if (launch_extract(c->plan, dplan, b, F, main_stream(c), &c->hook)) return hip_err(c, hipGetLastError(), "launch_extract");
+        if (launch_extract(c->plan, dplan, b, F, main_stream(c), &c->hook, side_stream(c)))
+            return hip_err(c, hipGetLastError(), "launch_extract");
     } else {
         HIP_TRY(c, hipEventRecord(c->ev_main, c->stream));   // no join: steps overlap
         const bool cross = !serial && prev_mdone && prev_chunk == c->chunk;
@@ -842,7 +874,8 @@ int coeb_extract(coeb_ctx* c, const uint8_t* gray, int W, int H, size_t stride, 
                          nbox ? blur.data() : nullptr, b)))
         return rc;
     b.gray = dgray;
-    if (launch_extract(c->plan, static_cast<const Plan*>(c->bufs["plan"].p), b, 1, main_stream(c), &c->hook))
+    if (launch_extract(c->plan, static_cast<const Plan*>(c->bufs["plan"].p), b, 1, main_stream(c), &c->hook,
+                       side_stream(c)))
         return hip_err(c, hipGetLastError(), "launch_extract");
     c->batch_frames = 1;
     c->batch_gray = dgray;

@@ -285,6 +285,7 @@ __device__ __forceinline__ int reflect101(int p, int len)
 
 struct BlurWork {
     int L;
+    int item0, item1;              // this launch's wave items [item0, item1)
     int item_off[COEB_MAXL + 1];   // wave items per level (prefix)
     int nstrips[COEB_MAXL];        // 56-column strips
     int bh[COEB_MAXL];             // rows per band (4 bands per item)
@@ -332,8 +333,8 @@ __global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, E
 {
     const int2 bxy = block_xy();
     const int f = bxy.y;
-    const int item = bxy.x * kWaves + wave_id();
-    if (item >= bw.item_off[bw.L]) return;
+    const int item = bw.item0 + bxy.x * kWaves + wave_id();
+    if (item >= bw.item1) return;
     int l = 0;
     while (l + 1 < bw.L && item >= bw.item_off[l + 1]) l++;
     const int it = item - bw.item_off[l];
@@ -854,7 +855,8 @@ __device__ __forceinline__ CellDesc load_cell(const CellDesc* __restrict__ cells
 // One wave per kFastCellsPerWave consecutive cells, four waves per workgroup, no workgroup
 // barriers.  The next cell's ROI loads are issued before the current cell is processed.
 __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P, ExtractBufs b,
-                                                       const CellDesc* __restrict__ cells)   // read-only: scalar loads
+                                                       const CellDesc* __restrict__ cells,   // read-only: scalar loads
+                                                       int cell0, int cell1)                 // this launch's cells
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // a per-lane wave index here (unlike the other kernels): with the cell geometry in SGPRs the
@@ -871,8 +873,8 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
     uint16_t* corn = surv + kFastSurv;
     const int2 bxy = block_xy<false>();
     const int f = bxy.y;
-    int cidx = (bxy.x * kWaves + wv) * kFastCellsPerWave;
-    if (cidx >= P->ncells) return;
+    int cidx = cell0 + (bxy.x * kWaves + wv) * kFastCellsPerWave;
+    if (cidx >= cell1) return;
     const int area = b.dyn[f].area_flag;
     const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
     CellDesc c = load_cell(cells, cidx);
@@ -884,7 +886,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
         for (int i = lane; i < (kFastRowBytes * c.rh + 15) / 16; i += 64) reinterpret_cast<uint4*>(Ms)[i] = make_uint4(0, 0, 0, 0);
         wave_sync_lds();
         const CellDesc cur = c;
-        const bool more = t + 1 < kFastCellsPerWave && cidx + 1 < P->ncells;
+        const bool more = t + 1 < kFastCellsPerWave && cidx + 1 < cell1;
         if (more) {
             c = load_cell(cells, cidx + 1);
             G = fast_geom(P, b, f, c);
@@ -1818,22 +1820,11 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
 }  // namespace
 
 int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, int F, hipStream_t s,
-                   ProfileHook* prof)
+                   ProfileHook* prof, const SideStream* side)
 {
     prof_begin(prof, "k_dynmask", s);
     hipLaunchKernelGGL(k_dynmask, dim3((F + 63) / 64), dim3(64), 0, s, b, F, plan.W, plan.H);
     prof_end(prof, s);
-    for (int l = 1; l < plan.L; l++) {
-        const LevelGeom& g = plan.lv[l];
-        const LevelGeom& gp = plan.lv[l - 1];
-        const uint8_t* src = l == 1 ? b.gray : b.pyr + gp.pyr_off;
-        const int64_t src_fs = l == 1 ? (int64_t)plan.W * plan.H : plan.pyr_stride;
-        prof_begin(prof, "k_pyr_level", s);
-        hipLaunchKernelGGL(k_pyr_level, dim3((g.w + PT_W - 1) / PT_W, (g.h + PT_H - 1) / PT_H, F), dim3(kThreads), 0, s, src, src_fs,
-                           gp.pitch, gp.w, gp.h, b.pyr + g.pyr_off, plan.pyr_stride, g.pitch, g.w, g.h,
-                           b.rtab + g.rtab_off, g.xmax);
-        prof_end(prof, s);
-    }
     BlurWork bw;
     bw.L = plan.L;
     int items = 0;
@@ -1846,13 +1837,56 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         items += bw.nstrips[l] * (nbands / 4);
     }
     bw.item_off[plan.L] = items;
-    prof_begin(prof, "k_blur", s);
-    hipLaunchKernelGGL(k_blur, dim3((items + kWaves - 1) / kWaves, F), dim3(kThreads), 0, s, d_plan, b, bw);
-    prof_end(prof, s);
-    prof_begin(prof, "k_fast", s);
     const int fast_lds = kWaves * (2 * fast_slab(plan) + 2 * (kFastSurv + kFastCorners));
-    hipLaunchKernelGGL(k_fast, dim3((plan.ncells + kWaves * kFastCellsPerWave - 1) / (kWaves * kFastCellsPerWave), F), dim3(kThreads), fast_lds, s, d_plan, b, b.cells);
-    prof_end(prof, s);
+    constexpr int kFastPerBlock = kWaves * kFastCellsPerWave;
+    auto blur = [&](hipStream_t st, int i0, int i1) {
+        if (i1 <= i0) return;
+        BlurWork w = bw;
+        w.item0 = i0; w.item1 = i1;
+        prof_begin(prof, "k_blur", st);
+        hipLaunchKernelGGL(k_blur, dim3((i1 - i0 + kWaves - 1) / kWaves, F), dim3(kThreads), 0, st, d_plan, b, w);
+        prof_end(prof, st);
+    };
+    auto fast = [&](hipStream_t st, int c0, int c1) {
+        if (c1 <= c0) return;
+        prof_begin(prof, "k_fast", st);
+        hipLaunchKernelGGL(k_fast, dim3((c1 - c0 + kFastPerBlock - 1) / kFastPerBlock, F), dim3(kThreads), fast_lds, st,
+                           d_plan, b, b.cells, c0, c1);
+        prof_end(prof, st);
+    };
+    // level 0 (the input frame itself) needs no pyramid: with a side stream its blur and FAST
+    // overlap the cascaded pyramid launches, whose small late levels leave most CUs idle; levels
+    // 1..m-1 follow on the side stream as soon as the pyramid has built them
+    const bool split = side && side->s && plan.L > 1;
+    const int m = split ? std::min(std::max(side->split, 1), plan.L) : 0;
+    auto cell_at = [&](int l) { return l < plan.L ? plan.lv[l].cell0 : plan.ncells; };
+    if (split) {
+        (void)hipEventRecord(side->fork, s);                 // after k_dynmask (area_flag -> FAST thresholds)
+        (void)hipStreamWaitEvent(side->s, side->fork, 0);
+        blur(side->s, 0, bw.item_off[1]);
+        fast(side->s, 0, cell_at(1));
+    }
+    for (int l = 1; l < plan.L; l++) {
+        const LevelGeom& g = plan.lv[l];
+        const LevelGeom& gp = plan.lv[l - 1];
+        const uint8_t* src = l == 1 ? b.gray : b.pyr + gp.pyr_off;
+        const int64_t src_fs = l == 1 ? (int64_t)plan.W * plan.H : plan.pyr_stride;
+        prof_begin(prof, "k_pyr_level", s);
+        hipLaunchKernelGGL(k_pyr_level, dim3((g.w + PT_W - 1) / PT_W, (g.h + PT_H - 1) / PT_H, F), dim3(kThreads), 0, s, src, src_fs,
+                           gp.pitch, gp.w, gp.h, b.pyr + g.pyr_off, plan.pyr_stride, g.pitch, g.w, g.h,
+                           b.rtab + g.rtab_off, g.xmax);
+        prof_end(prof, s);
+        if (split && m > 1 && l == m - 1) {
+            (void)hipEventRecord(side->mid, s);
+            (void)hipStreamWaitEvent(side->s, side->mid, 0);
+            blur(side->s, bw.item_off[1], bw.item_off[m]);
+            fast(side->s, cell_at(1), cell_at(m));
+        }
+    }
+    if (split) (void)hipEventRecord(side->join, side->s);
+    blur(s, split ? bw.item_off[m] : 0, items);
+    fast(s, split ? cell_at(m) : 0, plan.ncells);
+    if (split) (void)hipStreamWaitEvent(s, side->join, 0);
     prof_begin(prof, "k_octree", s);
     constexpr int kOctThreads = 256;       // 512 / 1024 measured slower
     (void)hipFuncSetAttribute((const void*)k_octree<kOctThreads>, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);

@@ -133,8 +133,12 @@ struct ProfileHook {
 void prof_begin(ProfileHook* p, const char* name, hipStream_t s);
 void prof_end(ProfileHook* p, hipStream_t s);
 
+// side (optional): blur + FAST of level 0 run on side.s while the pyramid builds levels 1..;
+// those of levels 1..split-1 follow there once the pyramid has built them, and s does levels
+// split..L-1 after the pyramid; s joins side.s before the octree.
+struct SideStream { hipStream_t s; hipEvent_t fork, mid, join; int split; };
 int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, int F, hipStream_t s,
-                   ProfileHook* prof);
+                   ProfileHook* prof, const SideStream* side = nullptr);
 
 struct MatchCam {
     float fx, fy, cx, cy, bf, mb;

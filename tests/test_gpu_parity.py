@@ -339,6 +339,13 @@ def test_batch_track_pose_matches_oracle(oracle_mod, ex):
                 tracked += 1
             prev = r
         assert tracked == F - 2 and nin_dev[3] == 0
+        # pipelined: step k's k_pose (own stream) overlaps step k+1's extraction and matching;
+        # three back-to-back steps must leave exactly the single-step results
+        for _ in range(3):
+            bp.run(pose=True)
+        T2, nin2, outl2 = bp.pose_results()
+        assert nin2 == nin_dev and np.array_equal(T2[1:].view(np.uint32), T_dev[1:].view(np.uint32))
+        assert all(np.array_equal(a, b) for a, b in zip(outl2[1:], outl_dev[1:]))
     finally:
         bp.close()
 
