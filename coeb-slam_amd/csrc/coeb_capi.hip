@@ -364,7 +364,7 @@ struct coeb_ctx {
     // coeb_synchronize and coeb_destroy join it (join_pose()).
     hipStream_t pose_stream = nullptr;
     // level-0 blur + FAST beside the pyramid (launch_extract's SideStream); COEB_SIDE_STREAM=0 disables
-    SideStream side{nullptr, nullptr, nullptr, nullptr, 2};
+    SideStream side{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, true, false};
     bool side_init = false;
     hipEvent_t ev_tprep = nullptr, ev_pose = nullptr;
     bool pose_pending = false;
@@ -566,9 +566,15 @@ const SideStream* side_stream(coeb_ctx* c)
         if (e && e[0] == '0') return nullptr;
         const char* sp = getenv("COEB_SIDE_SPLIT");          // first level left to the context stream
         if (sp) c->side.split = atoi(sp);
+        const char* bl = getenv("COEB_SIDE_BLUR");           // 0: late levels' blur on the context stream
+        if (bl) c->side.blur_late = bl[0] == '1';
+        const char* so = getenv("COEB_SIDE_OCTREE");         // 1: early levels' octree on the side stream
+        if (so) c->side.side_octree = so[0] == '1';
         if (hipStreamCreateWithFlags(&c->side.s, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->side.fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->side.mid, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->side.pyr_done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->side.join2, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->side.join, hipEventDisableTiming) != hipSuccess)
             c->side.s = nullptr;
     }
@@ -726,6 +732,8 @@ void coeb_destroy(coeb_ctx* c)
         (void)hipStreamDestroy(c->side.s);
         (void)hipEventDestroy(c->side.fork);
         (void)hipEventDestroy(c->side.mid);
+        (void)hipEventDestroy(c->side.pyr_done);
+        (void)hipEventDestroy(c->side.join2);
         (void)hipEventDestroy(c->side.join);
     }
     if (c->pose_stream) {

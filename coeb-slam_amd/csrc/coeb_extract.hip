@@ -1039,7 +1039,7 @@ __device__ __forceinline__ void child_rect(const int4 p, int q, int4* out, int* 
 }
 
 template <int NT>
-__global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, ExtractBufs b)
+__global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, ExtractBufs b, int level0)
 {
     constexpr int NW = NT / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1055,7 +1055,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
 
     // frame-fastest grid: every frame's level-0 list (the longest) is dispatched in the first
     // wave of workgroups, the cheap upper levels fill in behind them
-    const int f = blockIdx.x, l = blockIdx.y;
+    const int f = blockIdx.x, l = level0 + blockIdx.y;
     const LevelGeom& g = P->lv[l];
     const int tid = threadIdx.x, wv = wave_id(), lane = lane_id();
     const DynMask& dm = b.dyn[f];      // by reference: a local copy is indexed dynamically (scratch)
@@ -1883,15 +1883,37 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
             fast(side->s, cell_at(1), cell_at(m));
         }
     }
-    if (split) (void)hipEventRecord(side->join, side->s);
-    blur(s, split ? bw.item_off[m] : 0, items);
-    fast(s, split ? cell_at(m) : 0, plan.ncells);
-    if (split) (void)hipStreamWaitEvent(s, side->join, 0);
-    prof_begin(prof, "k_octree", s);
     constexpr int kOctThreads = 256;       // 512 / 1024 measured slower
     (void)hipFuncSetAttribute((const void*)k_octree<kOctThreads>, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);
-    hipLaunchKernelGGL(k_octree<kOctThreads>, dim3(F, plan.L), dim3(kOctThreads), plan.oct_lds, s, d_plan, b);
-    prof_end(prof, s);
+    auto octree = [&](hipStream_t st, int l0, int l1) {
+        if (l1 <= l0) return;
+        prof_begin(prof, "k_octree", st);
+        hipLaunchKernelGGL(k_octree<kOctThreads>, dim3(F, l1 - l0), dim3(kOctThreads), plan.oct_lds, st, d_plan, b, l0);
+        prof_end(prof, st);
+    };
+    // the late blur goes to the side stream (beside FAST / octree, which do not read it) and the
+    // octree of the side levels follows their FAST there; s joins before the descriptors
+    const bool late = split && side->blur_late;
+    const bool soct = late && side->side_octree;
+    if (soct) octree(side->s, 0, m);
+    if (split) (void)hipEventRecord(side->join, side->s);
+    if (late) {
+        (void)hipEventRecord(side->pyr_done, s);
+        (void)hipStreamWaitEvent(side->s, side->pyr_done, 0);
+        blur(side->s, bw.item_off[m], items);
+        (void)hipEventRecord(side->join2, side->s);
+    } else {
+        blur(s, split ? bw.item_off[m] : 0, items);
+    }
+    fast(s, split ? cell_at(m) : 0, plan.ncells);
+    if (soct) {
+        octree(s, m, plan.L);
+        (void)hipStreamWaitEvent(s, side->join, 0);
+    } else {
+        if (split) (void)hipStreamWaitEvent(s, side->join, 0);
+        octree(s, 0, plan.L);
+    }
+    if (late) (void)hipStreamWaitEvent(s, side->join2, 0);      // blurred levels ready
     prof_begin(prof, "k_describe", s);
     const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
     hipLaunchKernelGGL(vec0 ? k_describe<true> : k_describe<false>, dim3((plan.kcap + kWaves * kDescKp - 1) / (kWaves * kDescKp), F), dim3(kThreads), 0, s, d_plan, b);

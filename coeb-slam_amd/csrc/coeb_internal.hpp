@@ -136,7 +136,10 @@ void prof_end(ProfileHook* p, hipStream_t s);
 // side (optional): blur + FAST of level 0 run on side.s while the pyramid builds levels 1..;
 // those of levels 1..split-1 follow there once the pyramid has built them, and s does levels
 // split..L-1 after the pyramid; s joins side.s before the octree.
-struct SideStream { hipStream_t s; hipEvent_t fork, mid, join; int split; };
+// With blur_late, the blur of levels split..L-1 also runs on side.s (after the pyramid, beside
+// FAST and the octree on s); s then joins it (join2) only before the descriptors.
+// With side_octree, the octree of levels < split follows their FAST on side.s.
+struct SideStream { hipStream_t s; hipEvent_t fork, mid, join, pyr_done, join2; int split; bool blur_late, side_octree; };
 int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, int F, hipStream_t s,
                    ProfileHook* prof, const SideStream* side = nullptr);
 
