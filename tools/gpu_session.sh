@@ -25,12 +25,15 @@ for step in "$@"; do
         benchB) run benchB 600 python bench.py --config B --batch 64 --no-cpu-baseline ;;
         benchC) run benchC 600 python bench.py --config C --no-cpu-baseline --no-extras ;;
         benchD) run benchD 600 python bench.py --config D --no-cpu-baseline --no-extras ;;
-        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-e2e ;;
+        # per-kernel evidence with the side stream off: every kernel is then one whole-batch launch
+        # per step, the same launches bench.py's HIP-event pass times (it disables the side stream)
+        prof) COEB_SIDE_STREAM=0 run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-e2e ;;
         diag) run diag 600 python tools/diag_parity.py ;;
         posetime) run posetime 300 python tools/pose_timing.py ;;
         flow) run flow 300 python tools/flow_bench.py ;;
         flowprof) run flowprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/flowprof -o run -- python tools/flow_bench.py ;;
         pmc)
+            export COEB_SIDE_STREAM=0
             B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-e2e"
             run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- $B
             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- $B
