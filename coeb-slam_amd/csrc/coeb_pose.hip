@@ -266,7 +266,7 @@ struct PoseLds {
     double run[28][8];     // 32-lane run sums
     double out[28];        // reduced
     double rho;
-    int qmax, ok, nbad[4];
+    int qmax, ok, nbad[4], accepted;
 };
 
 // block-wide canonical reduction of nv per-thread partials (uniform call): each run of 32
@@ -427,8 +427,13 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
         const bool robust = it < 3;
         // ---- optimize(10): OptimizationAlgorithmLevenberg::solve per iteration ----
         double lambda = 0.0, ni = 2.0;                             // thread 0's copies
+        double currentChi = 0.0;
+        bool fresh = false;        // the last trial was accepted: errors and chi2 are already at L.s
         for (int iter = 0; iter < 10; iter++) {
-            double currentChi = active_chi2<EPT>(L, b, cm, f, ne, robust, delta, ES);
+            // computeActiveErrors + activeRobustChi2 at the current estimate.  After an accepted
+            // trial the estimate is that trial's, so the per-edge chi2 and currentChi (= tempChi,
+            // thread 0) computed for it are exactly what this pass would produce: skip it.
+            if (!fresh) currentChi = active_chi2<EPT>(L, b, cm, f, ne, robust, delta, ES);
             // buildSystem
             double acc[27];
             for (int k = 0; k < 27; k++) acc[k] = 0.0;
@@ -503,10 +508,12 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
                         lambda = lambda * sf;
                         ni = 2.0;
                         currentChi = tempChi;
+                        L.accepted = 1;
                     } else {
                         lambda = lambda * ni;
                         ni = ni * 2.0;
                         L.s = saved;
+                        L.accepted = 0;
                     }
                     L.qmax = L.qmax + 1;
                     L.rho = rho;
@@ -520,6 +527,7 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
             const double rho = L.rho;
             const int qmax = L.qmax;
             __syncthreads();
+            fresh = L.accepted != 0;
             if (qmax == 10 || rho == 0) break;                     // Terminate
         }
         // ---- classification (Optimizer.cc:381-437) ----
