@@ -1114,6 +1114,7 @@ int coeb_pose_optimization(coeb_ctx* c, const coeb_camera* cam, const coeb_pose_
     b.n = (const int*)(dbase + o_n); b.has_mp = dbase + o_h; b.xw = (const float*)(dbase + o_x); b.kps = dbase + o_k;
     b.ur = (const float*)(dbase + o_ur); b.inv_sigma2 = (const float*)(dbase + o_is); b.Tcw = (float*)(dbase + o_T);
     b.outlier = dbase + o_out; b.result = (int*)(dbase + o_res); b.edges = dedge; b.active = dact; b.chi2 = dchi;
+    b.timing = nullptr;
     b.stride = cs;
     if (launch_pose(b, 1, cam->fx, cam->fy, cam->cx, cam->cy, cam->bf, s, &c->hook))
         return hip_err(c, hipGetLastError(), "launch_pose");
@@ -1301,6 +1302,13 @@ int coeb_pose_batch_device(coeb_ctx* c, const coeb_camera* cam, int F, const flo
     b.kps = tkp + o; b.ur = tur + o;
     b.inv_sigma2 = isg; b.Tcw = tout + 16; b.outlier = toutl + o; b.result = tres + 1;
     b.edges = tedge + o; b.active = tact + o; b.chi2 = tchi + o; b.stride = K;
+    b.timing = nullptr;
+    if (getenv("COEB_POSE_TIMING")) {               // diagnostic phase clocks, tools/_pose_timing.py
+        long long* tmb;
+        if ((rc = ensure(c, "p_timing", (size_t)F * 8, &tmb))) return rc;
+        HIP_TRY(c, hipMemsetAsync(tmb, 0, (size_t)F * 64, s));
+        b.timing = tmb + 8;
+    }
     HIP_TRY(c, hipEventRecord(c->ev_tprep, s));
     HIP_TRY(c, hipStreamWaitEvent(c->pose_stream, c->ev_tprep, 0));
     if (launch_pose(b, F - 1, cam->fx, cam->fy, cam->cx, cam->cy, cam->bf, c->pose_stream, &c->hook))
@@ -1460,6 +1468,17 @@ int coeb_internal_error(coeb_ctx* c, int code, const char* msg) { return set_err
 int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t bytes, size_t* size_out)
 {
     if (c) join_pose(c);
+    if (c && what && std::string(what) == "pose_timing") {      // [F][8] k_pose phase clocks (COEB_POSE_TIMING)
+        if (!c->bufs.count("p_timing")) return COEB_EINVAL;
+        join_pose(c);
+        const size_t nb = c->bufs["p_timing"].n;
+        if (size_out) *size_out = nb;
+        if (host && bytes) {
+            HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
+            HIP_TRY(c, hipMemcpy(host, c->bufs["p_timing"].p, std::min(bytes, nb), hipMemcpyDeviceToHost));
+        }
+        return COEB_OK;
+    }
     if (c && what && std::string(what) == "match_timing") {     // [F][16] k_match phase clocks (COEB_MATCH_TIMING)
         if (!c->bufs.count("m_timing")) return COEB_EINVAL;
         const size_t nb = c->bufs["m_timing"].n;

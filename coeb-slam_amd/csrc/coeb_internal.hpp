@@ -207,6 +207,7 @@ struct PoseBufs {
     uint8_t* active;              // scratch [F][stride]
     double* chi2;                 // scratch [F][stride]
     int stride;
+    long long* timing;            // optional [F][8] phase clocks (COEB_POSE_TIMING), else null
 };
 int launch_pose(const PoseBufs& b, int F, double fx, double fy, double cx, double cy, double bf, hipStream_t s,
                 ProfileHook* prof);

@@ -25,6 +25,20 @@ struct Se3 { double w, x, y, z, t[3]; };
 struct KpRec { float x, y, size, angle, response; int octave, class_id; };   // coeb_keypoint
 struct PEdge { double X[3], obs[3], w; int stereo; };
 
+// Eigen's Quaternion-from-rotation-matrix, t <= 0 branch with the largest diagonal entry I
+// (compile-time indices: a runtime-indexed R / q would live in scratch memory).
+template <int I>
+__device__ __forceinline__ void pq_from_R_diag(const double R[9], double q[4])
+{
+    constexpr int J = (I + 1) % 3, K = (J + 1) % 3;
+    double t = sqrt(((R[I * 4] - R[J * 4]) - R[K * 4]) + 1.0);
+    q[I] = 0.5 * t;
+    t = 0.5 / t;
+    q[3] = (R[K * 3 + J] - R[J * 3 + K]) * t;
+    q[J] = (R[J * 3 + I] + R[I * 3 + J]) * t;
+    q[K] = (R[K * 3 + I] + R[I * 3 + K]) * t;
+}
+
 __device__ void pq_from_R(const double R[9], Se3& s)
 {
     double t = (R[0] + R[4]) + R[8];
@@ -39,14 +53,10 @@ __device__ void pq_from_R(const double R[9], Se3& s)
     } else {
         int i = 0;
         if (R[4] > R[0]) i = 1;
-        if (R[8] > R[i * 4]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(((R[i * 4] - R[j * 4]) - R[k * 4]) + 1.0);
-        q[i] = 0.5 * t;
-        t = 0.5 / t;
-        q[3] = (R[k * 3 + j] - R[j * 3 + k]) * t;
-        q[j] = (R[j * 3 + i] + R[i * 3 + j]) * t;
-        q[k] = (R[k * 3 + i] + R[i * 3 + k]) * t;
+        if (R[8] > (i ? R[4] : R[0])) i = 2;
+        if (i == 0) pq_from_R_diag<0>(R, q);
+        else if (i == 1) pq_from_R_diag<1>(R, q);
+        else pq_from_R_diag<2>(R, q);
     }
     s.x = q[0]; s.y = q[1]; s.z = q[2]; s.w = q[3];
 }
@@ -362,9 +372,16 @@ __device__ double active_chi2(PoseLds& L, const PoseBufs& b, const PoseCam& cm, 
     return L.out[0];
 }
 
+// phase clocks of thread 0 (diagnostic, COEB_POSE_TIMING): [0] chi2 passes, [1] build passes,
+// [2] thread-0 solve + exp + bookkeeping, [3] classification, [4] total, [5] iterations, [6] trials
+#define PT_MARK(var) long long var = b.timing ? (long long)clock64() : 0
+#define PT_ADD(slot, t0) do { if (b.timing && threadIdx.x == 0) b.timing[(int64_t)blockIdx.x * 8 + (slot)] += (long long)clock64() - (t0); } while (0)
+#define PT_INC(slot) do { if (b.timing && threadIdx.x == 0) b.timing[(int64_t)blockIdx.x * 8 + (slot)] += 1; } while (0)
+
 template <int EPT>
 __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
 {
+    PT_MARK(t_all);
     EdgeSet<EPT> ES;
     ES.act = 0;
     __shared__ PoseLds L;
@@ -433,7 +450,11 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
             // computeActiveErrors + activeRobustChi2 at the current estimate.  After an accepted
             // trial the estimate is that trial's, so the per-edge chi2 and currentChi (= tempChi,
             // thread 0) computed for it are exactly what this pass would produce: skip it.
+            PT_INC(5);
+            PT_MARK(t_c0);
             if (!fresh) currentChi = active_chi2<EPT>(L, b, cm, f, ne, robust, delta, ES);
+            PT_ADD(0, t_c0);
+            PT_MARK(t_b0);
             // buildSystem
             double acc[27];
             for (int k = 0; k < 27; k++) acc[k] = 0.0;
@@ -463,6 +484,8 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
                 })
             }
             block_reduce(L, acc, 27);
+            PT_ADD(1, t_b0);
+            PT_MARK(t_s0);
             double H[36], bv[6];
             if (tid == 0) {
                 int k = 0;
@@ -494,7 +517,12 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
                     L.s = pq_mul(up, saved);
                 }
                 __syncthreads();
+                PT_ADD(2, t_s0);
+                PT_INC(6);
+                PT_MARK(t_c1);
                 double tempChi = active_chi2<EPT>(L, b, cm, f, ne, robust, delta, ES);
+                PT_ADD(0, t_c1);
+                t_s0 = b.timing ? (long long)clock64() : 0;
                 if (tid == 0) {
                     if (!ok2) tempChi = DBL_MAX;
                     double scale = 0.0;
@@ -527,10 +555,12 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
             const double rho = L.rho;
             const int qmax = L.qmax;
             __syncthreads();
+            PT_ADD(2, t_s0);
             fresh = L.accepted != 0;
             if (qmax == 10 || rho == 0) break;                     // Terminate
         }
         // ---- classification (Optimizer.cc:381-437) ----
+        PT_MARK(t_k0);
         const Se3 s = L.s;
         int bad = 0;
         COEB_FOR_EDGES(ES, {
@@ -546,12 +576,14 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
         __syncthreads();
         nBad = (L.nbad[0] + L.nbad[1]) + (L.nbad[2] + L.nbad[3]);
         __syncthreads();
+        PT_ADD(3, t_k0);
         if (ne < 10) break;                                        // optimizer.edges().size() < 10
     }
     if (tid == 0) {
         pq_to_Tcw(L.s, Tcw);
         b.result[f] = ne - nBad;
     }
+    PT_ADD(4, t_all);
 }
 
 // ================================ k_track_prep ================================
