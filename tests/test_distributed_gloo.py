@@ -71,3 +71,19 @@ def test_bench_two_ranks_dry_run():
     # rank 1 sleeps 4 ms per step: the max over ranks must set the time
     assert rec["ms_per_step"] >= 4.0
     assert abs(rec["value"] - 2 * 4 * 3 / (rec["ms_per_step"] * 3 / 1e3)) / rec["value"] < 1e-3
+
+
+@pytest.mark.parametrize("config", ["C", "D"])
+def test_bench_config_dry_run(config):
+    """The other BASELINE configs keep the bench contract (one JSON line, the config's
+    workload named, whole-job frames/s)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", config, "--steps", "2", "--warmup", "1",
+           "--batch", "4", "--dry-run", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    want = {"C": "configs[2]", "D": "configs[4]"}[config]
+    assert want in rec["config"]["workload"] and rec["n_gpus"] == 1 and rec["unit"] == "frames/s"
+    assert abs(rec["value"] - 4 * 2 / (rec["ms_per_step"] * 2 / 1e3)) / rec["value"] < 1e-3
