@@ -547,14 +547,14 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
                     L.rho = rho;
                 }
                 __syncthreads();
+                // no barrier after these reads: thread 0 next writes L.rho / L.qmax / L.accepted
+                // only after barriers every thread reaches after reading them
                 const double rho = L.rho;
                 const int qmax = L.qmax;
-                __syncthreads();
                 if (!(rho < 0 && qmax < 10)) break;
             }
             const double rho = L.rho;
             const int qmax = L.qmax;
-            __syncthreads();
             PT_ADD(2, t_s0);
             fresh = L.accepted != 0;
             if (qmax == 10 || rho == 0) break;                     // Terminate
