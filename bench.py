@@ -126,10 +126,54 @@ def cpu_baseline(cfg, seconds=12.0, min_frames=30):
         prev = r
         i += 1
     med = float(np.median(times))
-    return dict(value=round(1.0 / med, 3), unit="frames/s", cores=1, kind="port",
-                sample="%d consecutive %dx%d synthetic frames, oracle (-O3 -march=native) single thread: "
-                       "extract + ComputeStereoFromRGBD + SearchByProjection(th 15, retry 30); median %.2f ms/frame"
-                       % (len(times), w, h, med * 1e3))
+    out = dict(value=round(1.0 / med, 3), unit="frames/s", cores=1, kind="port",
+               sample="%d consecutive %dx%d synthetic frames, oracle (-O3 -march=native) single thread: "
+                      "extract + ComputeStereoFromRGBD + SearchByProjection(th 15, retry 30); median %.2f ms/frame"
+                      % (len(times), w, h, med * 1e3))
+    out["all_cores"] = cpu_baseline_parallel(O, cfg, frames, depth, cam)
+    return out
+
+
+def cpu_baseline_parallel(O, cfg, frames, depth, cam, seconds=6.0):
+    """SURVEY.md s8(d)'s all-cores frame-parallel CPU run: one oracle extractor per thread, each
+    thread extracting + matching its own run of consecutive frames (ctypes calls release the GIL,
+    and the oracle keeps no global state).  Threads = min(16, os.cpu_count()): the box's CPU share
+    for one GPU."""
+    import threading
+    from coeb_front import synth
+    nthr = max(1, min(16, os.cpu_count() or 1))
+    Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
+    nfr = len(frames)
+    done = [0] * nthr
+    t_end = [0.0]
+
+    def work(t):
+        ex = O.Extractor(cfg["nfeatures"], 1.2, 8, 20, 7)
+        i = (7 * t) % nfr
+        prev = ex.extract(frames[i])
+        while time.perf_counter() < t_end[0]:
+            i = (i + 1) % nfr
+            last = O.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX, synth.TUM_FY,
+                                              synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+            r = ex.extract(frames[i])
+            ur, _ = O.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
+            nm, _ = O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 15.0)
+            if nm < 20:
+                O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 30.0)
+            done[t] += 1
+            prev = r
+    t0 = time.perf_counter()
+    t_end[0] = t0 + seconds
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(nthr)]
+    for x in ths:
+        x.start()
+    for x in ths:
+        x.join()
+    dt = time.perf_counter() - t0
+    return dict(value=round(sum(done) / dt, 3), unit="frames/s", cores=nthr, kind="port",
+                sample="%d threads x %.0f s, one oracle extractor per thread, frame-parallel extract + "
+                       "ComputeStereoFromRGBD + SearchByProjection (LastFrame snapshots inside the timed loop); "
+                       "%d frames" % (nthr, seconds, sum(done)))
 
 
 def cpu_extras(out, w, h, reps=5):
