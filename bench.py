@@ -89,16 +89,41 @@ def kernel_bytes(name, w, h, nkp, nprev, npx, ncand):
     return 0
 
 
+def host_cpu_info():
+    """CPU model (/proc/cpuinfo), the CPUs this process may run on (what `nproc` prints: the
+    affinity mask) and the cgroup CPU quota if one is set (cpu.max), for the baseline record."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    cpus = sorted(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+            if q != "max":
+                quota = round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return dict(cpu_model=model, nproc=len(cpus), cpu_quota=quota, machine_cpus=os.cpu_count()), cpus
+
+
 def cpu_baseline(cfg, seconds=12.0, min_frames=30):
-    """Oracle ('port') timed single-threaded on this host: extract + ComputeStereoFromRGBD +
-    SearchByProjection (retry at 2*th) per frame, on consecutive synthetic frames."""
+    """Oracle ('port') timed on this host: extract + ComputeStereoFromRGBD + SearchByProjection
+    (retry at 2*th) per frame, on consecutive synthetic frames.  The single-thread leg runs
+    pinned to one CPU (os.sched_setaffinity on the timing thread, SURVEY.md s8(d) `taskset -c`)."""
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"])
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import ctypes as C
     import oracle as O
     from coeb_front import synth
     O.LIB = os.path.join(ROOT, "oracle", "liborb_oracle_native.so")
     O._lib = None
+    info, cpus = host_cpu_info()
     w, h = cfg["w"], cfg["h"]
     ex = O.Extractor(cfg["nfeatures"], 1.2, 8, 20, 7)
     cam = O.camera(ex, w, h, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
@@ -106,42 +131,45 @@ def cpu_baseline(cfg, seconds=12.0, min_frames=30):
     nfr = 64
     frames = synth.make_frames(w, h, nfr, seed=5151)
     Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
-    prev = ex.extract(frames[0])
-    for i in range(1, 4):          # warm-up
-        prev = ex.extract(frames[i])
-    times = []
-    t_end = time.perf_counter() + seconds
-    i = 4
-    while (time.perf_counter() < t_end or len(times) < min_frames) and len(times) < 400:
-        f = frames[i % nfr]
-        last = O.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX, synth.TUM_FY,
-                                          synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)   # map snapshot (untimed)
-        t0 = time.perf_counter()
-        r = ex.extract(f)
-        ur, _ = O.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
-        nm, _ = O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 15.0)
-        if nm < 20:
-            O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 30.0)
-        times.append(time.perf_counter() - t0)
-        prev = r
-        i += 1
+    os.sched_setaffinity(0, {cpus[0]})
+    try:
+        prev = ex.extract(frames[0])
+        for i in range(1, 4):          # warm-up
+            prev = ex.extract(frames[i])
+        times = []
+        t_end = time.perf_counter() + seconds
+        i = 4
+        while (time.perf_counter() < t_end or len(times) < min_frames) and len(times) < 400:
+            f = frames[i % nfr]
+            last = O.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX, synth.TUM_FY,
+                                              synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)   # map snapshot (untimed)
+            t0 = time.perf_counter()
+            r = ex.extract(f)
+            ur, _ = O.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
+            nm, _ = O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 15.0)
+            if nm < 20:
+                O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 30.0)
+            times.append(time.perf_counter() - t0)
+            prev = r
+            i += 1
+    finally:
+        os.sched_setaffinity(0, set(cpus))
     med = float(np.median(times))
     out = dict(value=round(1.0 / med, 3), unit="frames/s", cores=1, kind="port",
-               sample="%d consecutive %dx%d synthetic frames, oracle (-O3 -march=native) single thread: "
-                      "extract + ComputeStereoFromRGBD + SearchByProjection(th 15, retry 30); median %.2f ms/frame"
-                      % (len(times), w, h, med * 1e3))
-    out["all_cores"] = cpu_baseline_parallel(O, cfg, frames, depth, cam)
+               sample="%d consecutive %dx%d synthetic frames, oracle (-O3 -march=native) single thread pinned to "
+                      "CPU %d: extract + ComputeStereoFromRGBD + SearchByProjection(th 15, retry 30); median %.2f "
+                      "ms/frame" % (len(times), w, h, cpus[0], med * 1e3))
+    out.update(info)
+    out["all_cores"] = cpu_baseline_parallel(O, cfg, frames, depth, cam, len(cpus))
     return out
 
 
-def cpu_baseline_parallel(O, cfg, frames, depth, cam, seconds=6.0):
+def cpu_baseline_parallel(O, cfg, frames, depth, cam, nthr, seconds=6.0):
     """SURVEY.md s8(d)'s all-cores frame-parallel CPU run: one oracle extractor per thread, each
     thread extracting + matching its own run of consecutive frames (ctypes calls release the GIL,
-    and the oracle keeps no global state).  Threads = min(16, os.cpu_count()): the box's CPU share
-    for one GPU."""
+    and the oracle keeps no global state).  Threads = nproc, the CPUs this process may use."""
     import threading
     from coeb_front import synth
-    nthr = max(1, min(16, os.cpu_count() or 1))
     Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
     nfr = len(frames)
     done = [0] * nthr
@@ -171,7 +199,7 @@ def cpu_baseline_parallel(O, cfg, frames, depth, cam, seconds=6.0):
         x.join()
     dt = time.perf_counter() - t0
     return dict(value=round(sum(done) / dt, 3), unit="frames/s", cores=nthr, kind="port",
-                sample="%d threads x %.0f s, one oracle extractor per thread, frame-parallel extract + "
+                sample="%d threads (nproc) x %.0f s, one oracle extractor per thread, frame-parallel extract + "
                        "ComputeStereoFromRGBD + SearchByProjection (LastFrame snapshots inside the timed loop); "
                        "%d frames" % (nthr, seconds, sum(done)))
 
@@ -216,26 +244,32 @@ def cpu_extras(out, w, h, reps=5):
     return res
 
 
-def pmc_traffic(kernel, frames_per_launch):
+def pmc_traffic(kernel, frames_per_launch, w, h):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by tools/pmc_summary.py --json from separate
-    FETCH_SIZE / WRITE_SIZE passes of this bench), scaled to this run's frames per launch."""
+    FETCH_SIZE / WRITE_SIZE passes of this bench), scaled to this run's frames per launch.
+    None unless the counters were collected at this frame size."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
+        if (d.get("width"), d.get("height")) != (w, h):
+            return None, None
         k = d["kernels"][kernel]
         return int(k["traffic_bytes"] * frames_per_launch / d["frames_per_launch"]), d.get("command", "")
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         return None, None
 
 
-def pmc_valu(kernel):
+def pmc_valu(kernel, w, h):
     """VALU issue utilisation of `kernel` from the committed PMC summary (profiles/pmc_valu.json,
-    tools/pmc_summary.py --valu-json: SQ_INSTS_VALU / (256 CUs x busy cycles))."""
+    tools/pmc_summary.py --valu-json: SQ_INSTS_VALU / (2 x 256 CUs x busy cycles)), if collected
+    at this frame size."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_valu.json")) as f:
             d = json.load(f)
+        if (d.get("width"), d.get("height")) != (w, h):
+            return None
         k = d["kernels"][kernel]
         return dict(valu_issue_frac=k["valu_issue_frac"], valu_insts_per_launch=k["valu_insts"],
                     source="profiles/pmc_valu.json (%s)" % d.get("command", ""))
@@ -379,12 +413,17 @@ def config3_timing(bp, frames, Tcw, w, h, batch, steps=10):
                 note="640x480, 2 boxes + 60 T_M points + blur_flag [0,1] per frame (bench.py --config C for the full line)")
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs to drive.  Under torch.distributed.run this must equal WORLD_SIZE (one process "
+                         "per GPU); started directly, bench drives devices 0..N-1 from N host threads")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="matched frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=256, help="matched frames per step per GPU (weak scaling)")
+    ap.add_argument("--global-frames", type=int, default=None,
+                    help="fixed number of matched frames per step, sharded over the GPUs with one halo frame "
+                         "each (strong scaling; config B defaults to BASELINE configs[3]'s 512)")
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the batch is chunked over (kernels of different chunks overlap)")
@@ -395,17 +434,77 @@ def main():
                     help="skip the per-call timing of the other entry points (local map, relocalisation, pose)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the rank/timing/JSON plumbing with a stand-in pipeline (tests)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    from coeb_front.dist import Ranks
-    ranks = Ranks()
+
+def main():
+    args = parse_args()
+    if args.global_frames is None and args.config == "B":
+        args.global_frames = 512
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world > 1 or "LOCAL_RANK" in os.environ:
+        # one process per GPU under torch.distributed.run
+        if env_world != args.gpus:
+            sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d: refusing to report a run on a different number "
+                     "of GPUs" % (args.gpus, env_world))
+        from coeb_front.dist import Ranks
+        ranks = Ranks()
+        if not args.dry_run:
+            check_devices(ranks.local_rank + 1)
+        rank_main(ranks, args)
+        return
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if not args.dry_run:
+        check_devices(args.gpus)
+    if args.gpus == 1:
+        from coeb_front.dist import Ranks
+        rank_main(Ranks(), args)
+        return
+    # N devices from N host threads of this process (no torch.cuda anywhere)
+    import threading
+    from coeb_front.dist import ThreadRanks
+    grp = ThreadRanks(args.gpus)
+    errors = []
+
+    def body(r):
+        try:
+            rank_main(grp.view(r), args)
+        except BaseException as e:   # noqa: BLE001 - reported below, the process exits non-zero
+            errors.append((r, e))
+            grp.abort()
+    ths = [threading.Thread(target=body, args=(r,), name="rank%d" % r) for r in range(args.gpus)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    if errors:
+        import traceback
+        for r, e in sorted(errors, key=lambda x: x[0]):
+            print("rank %d failed:" % r, file=sys.stderr)
+            traceback.print_exception(type(e), e, e.__traceback__)
+        sys.exit(1)
+
+
+def check_devices(n):
+    import coeb_front
+    have = coeb_front.lib().coeb_device_count()
+    if have < n:
+        sys.exit("bench.py: %d GPU(s) requested but only %d visible" % (n, have))
+
+
+def rank_main(ranks, args):
     world, rank, local_rank = ranks.world, ranks.rank, ranks.local_rank
-
     from coeb_front import synth
+    from coeb_front.dist import shard_frames
     cfg = CONFIGS[args.config]
     w, h = cfg["w"], cfg["h"]
-    F = args.batch + 1
-    frames = synth.make_frames(w, h, F, seed=1000 + 17 * rank)
+    strong = args.global_frames is not None
+    G = args.global_frames if strong else args.batch * world       # matched frames per step, all ranks
+    if G < world:
+        raise SystemExit("bench.py: %d matched frames cannot be split over %d GPUs" % (G, world))
+    first, F, nmatched = shard_frames(G, world, rank)
+    frames = synth.make_frames(w, h, F, seed=1000, first=first)    # global frames first .. first+F-1
     Tcw = np.stack([synth.motion_pose()] * F)
     if args.dry_run:
         bp = DryRunPipeline(rank)
@@ -413,11 +512,14 @@ def main():
         from coeb_front.pipeline import BatchPipeline
         bp = BatchPipeline(w, h, F, nfeatures=cfg["nfeatures"], device=local_rank)
     bp.ctx.set_batch_streams(args.streams)
-    dyn = dyn_batch(w, h, F, 17 * rank) if cfg.get("dyn") else None
+    dyn = dyn_batch(w, h, F, first) if cfg.get("dyn") else None
     bp.load(frames, Tcw=Tcw, dyn=dyn)
-
-    def barrier():
-        ranks.barrier()
+    del frames
+    # every rank states what it covers; the sum must be the whole sequence
+    covered = int(ranks.sum(nmatched))
+    if covered != G:
+        raise RuntimeError("shards cover %d of %d matched frames" % (covered, G))
+    per_rank = [shard_frames(G, world, r)[2] for r in range(world)]
 
     pose = bool(cfg.get("pose"))
     for _ in range(args.warmup):
@@ -429,21 +531,21 @@ def main():
     ncand = int(bp.ctx.debug_read("cand_n", 1).view(np.int32).sum())
 
     # timed region: no instrumentation (HIP event pairs around every launch cost ~10 us each)
-    barrier()
+    ranks.barrier()
     bp.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         bp.run(pose=pose)
     bp.synchronize()
     t1 = time.perf_counter()
-    barrier()
+    ranks.barrier()
     elapsed = ranks.max(t1 - t0)
 
-    # per-kernel device time: a separate pass with HIP events, kernels serialised on one
-    # stream so each event pair brackets exactly one launch
+    # per-kernel device time (rank 0): a separate pass with HIP events, kernels serialised on
+    # one stream so each event pair brackets exactly one launch
     prof = {}
     prof_steps = 0
-    if not args.no_profile:
+    if not args.no_profile and rank == 0:
         prof_steps = max(1, min(args.steps, 10))
         bp.ctx.set_batch_streams(1)
         bp.ctx.profile(True)
@@ -454,26 +556,13 @@ def main():
         prof = bp.ctx.profile_read()
         bp.ctx.profile(False)
         bp.ctx.set_batch_streams(args.streams)
+    ranks.barrier()
 
     e2e = None
     if not args.no_e2e and not args.dry_run:
-        # host buffers in and out (synchronous copies, no overlap): reported, never `value`
-        e2e_steps = max(2, min(5, args.steps))
-        st = bp.run_host(frames)
-        bp.synchronize()
-        barrier()
-        te0 = time.perf_counter()
-        for _ in range(e2e_steps):
-            st = bp.run_host(frames, st)
-        bp.synchronize()
-        te = ranks.max(time.perf_counter() - te0)
-        e2e = dict(value=round(args.batch * e2e_steps * world / te, 2), unit="frames/s",
-                   ms_per_step=round(te / e2e_steps * 1e3, 4), steps=e2e_steps,
-                   note="host gray frames uploaded and keypoints/descriptors/matches downloaded each step "
-                        "(synchronous hipMemcpy on the context stream, pageable host memory)")
+        e2e = e2e_timing(bp, ranks, G, max(2, min(5, args.steps)))
 
-    frames_total = args.batch * args.steps * world
-    value = frames_total / elapsed
+    value = G * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
     if rank == 0:
@@ -484,34 +573,34 @@ def main():
             name, (tot_ms, launches) = dom
             avg_s = tot_ms / launches / 1e3
             frames_per_launch = F if name != "k_match" else F - 1
-            if name == "k_pyr_level":
-                frames_per_launch = F
             bpl = kernel_bytes(name, w, h, nkp, nkp, npx, ncand) * frames_per_launch
             achieved = bpl / avg_s / 1e9
-            traffic, tsrc = pmc_traffic(name, frames_per_launch)
+            traffic, tsrc = pmc_traffic(name, frames_per_launch, w, h)
             roof = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, kernel=name,
                         avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=int(bpl))
             if traffic is not None:
                 roof["traffic_source"] = "profiles/pmc_traffic.json (%s)" % tsrc
-            # the path is integer-VALU bound, not HBM bound: the PMC VALU issue fraction of the
-            # same kernel says how close it runs to the chip's one-VALU-op-per-CU-cycle ceiling
-            valu = pmc_valu(name)
+            # the kernel is bound by integer VALU issue, not HBM: the PMC VALU fraction says how
+            # close it runs to the chip's issue ceiling (2 wave64 VALU instructions per CU per cycle)
+            valu = pmc_valu(name, w, h)
             if valu is not None:
                 roof["valu"] = valu
         pipeline_bytes = w * h + 60 * nkp + 36 * nkp     # B = W*H + 60 N_kp + 36 N_prev
         line = dict(metric=METRIC, value=round(value, 2), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(ms_per_step, 4), higher_is_better=True,
-                    scaling="weak", vs_baseline=None, dtype="u8",
+                    scaling="strong" if strong else "weak", vs_baseline=None, dtype="u8",
                     data="synthetic (TUM-like rectangles + noise, (+2,+1) px/frame, Z=2 m)",
                     config=dict(workload=cfg["workload"], width=w, height=h, nfeatures=cfg["nfeatures"],
-                                nlevels=8, frames_per_step_per_gpu=args.batch, halo_frames_per_step=1,
-                                streams_per_gpu=args.streams,
+                                nlevels=8, matched_frames_per_step=G, frames_per_rank=per_rank,
+                                halo_frames_per_rank=1, streams_per_gpu=args.streams,
+                                ranks="threads" if isinstance(ranks, _thread_rank_type()) else
+                                      ("processes" if world > 1 else "single"),
                                 parallelism="frame-sharded x%d (no collectives)" % world),
                     roofline=roof,
                     pipeline_roofline=dict(bytes_per_frame=int(pipeline_bytes),
                                            achieved_GBps=round(value * pipeline_bytes / 1e9, 3),
-                                           frac=round(value * pipeline_bytes / 1e9 / HBM_PEAK_GBS, 6)),
+                                           frac=round(value * pipeline_bytes / 1e9 / HBM_PEAK_GBS / world, 6)),
                     kernels_ms_per_step={k: round(v[0] / max(1, prof_steps), 4) for k, v in prof.items()},
                     kernels_profiled_steps=prof_steps,
                     keypoints_per_frame=round(nkp, 1), matches_per_frame=round(nmatch, 1),
@@ -519,8 +608,9 @@ def main():
         if not args.no_extras and world == 1 and not args.dry_run:
             line["extras"] = extras_timing(bp.ctx, out, w, h)
             if not cfg.get("dyn") and not cfg.get("pose"):
-                line["extras"]["config5_tracking"] = config5_timing(bp, args.batch)
-                line["extras"]["config3_dynamic_mask"] = config3_timing(bp, frames, Tcw, w, h, args.batch)
+                line["extras"]["config5_tracking"] = config5_timing(bp, nmatched)
+                line["extras"]["config3_dynamic_mask"] = config3_timing(bp, synth.make_frames(w, h, F, seed=1000),
+                                                                        Tcw, w, h, nmatched)
         if not args.no_cpu_baseline and world == 1 and not args.dry_run:
             cb = cpu_baseline(cfg)
             if "extras" in line:
@@ -530,6 +620,28 @@ def main():
         print(json.dumps(line), flush=True)
     bp.close()
     ranks.close()
+
+
+def _thread_rank_type():
+    from coeb_front.dist import _ThreadRank
+    return _ThreadRank
+
+
+def e2e_timing(bp, ranks, G, steps):
+    """Host buffers in and out (reported, never `value`)."""
+    frames = bp.host_frames
+    st = bp.run_host(frames)
+    bp.synchronize()
+    ranks.barrier()
+    te0 = time.perf_counter()
+    for _ in range(steps):
+        st = bp.run_host(frames, st)
+    bp.synchronize()
+    te = ranks.max(time.perf_counter() - te0)
+    return dict(value=round(G * steps / te, 2), unit="frames/s", ms_per_step=round(te / steps * 1e3, 4),
+                steps=steps,
+                note="host gray frames uploaded and keypoints/descriptors/matches downloaded each step "
+                     "(synchronous hipMemcpy on the context stream, pageable host memory)")
 
 
 if __name__ == "__main__":

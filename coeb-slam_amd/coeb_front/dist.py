@@ -1,11 +1,19 @@
 """Multi-GPU plumbing for the frame-sharded front end.
 
 Frames are independent (a frame only needs its predecessor's keypoints, handled by a one-frame
-halo per shard), so ranks never exchange data: torch.distributed (gloo) carries only the
-start/stop barriers and the max-over-ranks of the timed interval.  One process per GPU
-(LOCAL_RANK selects the device); no RCCL collective on the data path.
+halo per shard), so ranks never exchange data.  Two ways to run N ranks:
+
+- `Ranks`: one process per GPU under torch.distributed.run (LOCAL_RANK selects the device);
+  torch.distributed (gloo) carries only the start/stop barriers and the max-over-ranks of the
+  timed interval.
+- `ThreadRanks`: `bench.py --gpus N` started directly: N host threads of one process, thread r
+  driving device r through its own libcoeb_front context (ctypes releases the GIL for every
+  library call, so the threads issue work concurrently).  A threading.Barrier replaces gloo.
+
+No RCCL collective on the data path in either form.
 """
 import os
+import threading
 
 
 class Ranks:
@@ -45,6 +53,58 @@ class Ranks:
         if self.dist is not None:
             self.dist.destroy_process_group()
             self.dist = None
+
+
+class ThreadRanks:
+    """N ranks as N threads of this process (same surface as one rank's `Ranks`: call `view(r)`
+    from thread r).  A rank that raises breaks the barrier, so the others fail instead of
+    waiting forever."""
+
+    def __init__(self, world, timeout=600.0):
+        self.world = world
+        self._bar = threading.Barrier(world, timeout=timeout)
+        self._vals = [0.0] * world
+
+    def view(self, rank):
+        return _ThreadRank(self, rank)
+
+    def abort(self):
+        self._bar.abort()
+
+    def _reduce(self, rank, x, fn):
+        self._vals[rank] = float(x)
+        self._bar.wait()
+        r = fn(self._vals)
+        self._bar.wait()          # nobody overwrites _vals before every rank has read it
+        return r
+
+
+class _ThreadRank:
+    def __init__(self, grp, rank):
+        self.grp, self.world, self.rank, self.local_rank = grp, grp.world, rank, rank
+
+    def barrier(self):
+        self.grp._bar.wait()
+
+    def max(self, x):
+        return self.grp._reduce(self.rank, x, max)
+
+    def sum(self, x):
+        return self.grp._reduce(self.rank, x, sum)
+
+    def close(self):
+        pass
+
+
+def shard_frames(total, world, rank):
+    """Frames of one rank when a sequence of `total` matched frames is split over `world` ranks.
+
+    The sequence has frames 0..total; frame 0 has no predecessor and is not counted, frame j >= 1
+    is matched against frame j-1.  Rank r matches the contiguous chunk [lo+1, hi] (`shard` over
+    the matched frames) and also extracts frame lo, its one-frame halo, so every match is local.
+    Returns (first, nextract, nmatched): the rank extracts frames first .. first+nextract-1."""
+    _, lo, hi = shard(total, world, rank)
+    return lo, hi - lo + 1, hi - lo
 
 
 def shard(total, world, rank):

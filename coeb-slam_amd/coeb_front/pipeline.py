@@ -22,6 +22,7 @@ class BatchPipeline:
         self.dTcw = None
         self.Tcw = np.stack([np.eye(4, dtype=np.float32)] * nframes)
         self.dyn = None
+        self.host_frames = None
 
     def load(self, frames, depth=None, Tcw=None, dyn=None):
         """frames: (F, H, W) uint8; depth: (F, H, W) float32; Tcw: (F, 4, 4) pose of frame f
@@ -29,6 +30,7 @@ class BatchPipeline:
         frames = np.ascontiguousarray(frames, np.uint8)
         assert frames.shape == (self.F, self.H, self.W)
         self.gray = self.ctx.upload(frames)
+        self.host_frames = frames
         if depth is None:
             depth = np.broadcast_to(synth.make_depth(self.W, self.H), (self.F, self.H, self.W))
         self.depth = self.ctx.upload(np.ascontiguousarray(depth, np.float32))

@@ -394,13 +394,19 @@ int hip_err(coeb_ctx* c, hipError_t e, const char* where)
         if (_e != hipSuccess) return hip_err((ctx), _e, #expr);     \
     } while (0)
 
+int quiesce(coeb_ctx* c);
+
 template <typename T>
 int ensure(coeb_ctx* c, const char* name, size_t count, T** out)
 {
     DevBuf& b = c->bufs[name];
     const size_t bytes = std::max<size_t>(count * sizeof(T), 256);
     if (b.n < bytes) {
-        if (b.p) (void)hipFree(b.p);
+        if (b.p) {
+            int rc = quiesce(c);          // work in flight on any of the context's streams may read it
+            if (rc) return rc;
+            (void)hipFree(b.p);
+        }
         b.p = nullptr;
         b.n = 0;
         hipError_t e = hipMalloc(&b.p, bytes);
@@ -468,12 +474,15 @@ int ensure_plan(coeb_ctx* c, int W, int H)
     std::string err;
     Plan P;
     if (!make_plan(c->tab, W, H, P, c->rtab, c->cells, err)) return set_err(c, COEB_EINVAL, err);
+    // the plan, rtab and cells are rewritten in place below: batches still in flight on the
+    // context's streams (pyramid / FAST / octree / describe read them) must finish first
+    int rc;
+    if ((rc = quiesce(c))) return rc;
     c->plan = P;
     Plan* dplan;
     int* drtab;
     CellDesc* dcells;
     int8_t* dpat;
-    int rc;
     if ((rc = ensure(c, "plan", 1, &dplan))) return rc;
     if ((rc = ensure(c, "rtab", std::max<size_t>(c->rtab.size(), 1), &drtab))) return rc;
     if ((rc = ensure(c, "cells", c->cells.size(), &dcells))) return rc;
@@ -600,6 +609,18 @@ hipStream_t main_stream(coeb_ctx* c)
         c->pending_join = false;
     }
     return c->stream;
+}
+
+// Wait until nothing enqueued by this context is still running: the chunk streams and the pose
+// stream are joined into the context stream (the side stream is joined there by every
+// extraction), then the context stream is drained.
+int quiesce(coeb_ctx* c)
+{
+    if (!c->stream) return 0;
+    main_stream(c);
+    join_pose(c);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return 0;
 }
 
 // Chunk boundaries for F frames over the context's batch streams (>= 16 frames per chunk).

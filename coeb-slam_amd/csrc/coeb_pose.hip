@@ -234,6 +234,15 @@ __device__ __forceinline__ void pq_huber(double e2, double delta, double& r0, do
     }
 }
 
+// pow(2*rho - 1, 3) of g2o's LM update, as the oracle's pq_cube: the exact double-double cube
+// rounded once (the correctly rounded value glibc's pow returns)
+__device__ inline double pq_cube(double t)
+{
+    const double h = t * t, l = __builtin_fma(t, t, -h);
+    const double h2 = h * t, l2 = __builtin_fma(h, t, -h2);
+    return h2 + __builtin_fma(l, t, l2);
+}
+
 __device__ bool pq_solve6(const double H[36], const double b[6], double x[6])
 {
     double L[36], d[6], y[6];
@@ -527,10 +536,10 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
                     if (!ok2) tempChi = DBL_MAX;
                     double scale = 0.0;
                     for (int j = 0; j < 6; j++) scale = scale + x[j] * (lambda * x[j] + bv[j]);
+                    scale = scale + 1e-3;   // g2o OptimizationAlgorithmLevenberg::solve: "make sure it's non-zero"
                     const double rho = (currentChi - tempChi) / scale;
                     if (rho > 0 && isfinite(tempChi)) {
-                        const double t2 = 2.0 * rho - 1.0;
-                        double alpha = 1.0 - (t2 * t2) * t2;
+                        double alpha = 1.0 - pq_cube(2.0 * rho - 1.0);
                         alpha = fmin(alpha, 2.0 / 3.0);
                         const double sf = fmax(1.0 / 3.0, alpha);
                         lambda = lambda * sf;

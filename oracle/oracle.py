@@ -242,6 +242,13 @@ def pose_optimization(kps, has_mp, xw, uright, inv_sigma2, fx, fy, cx, cy, bf, T
     return nin, T.reshape(4, 4), out[:n]
 
 
+def pose_last_stats():
+    """(LM iterations, LM trials) of the last pose_optimization call on this thread."""
+    it, tr = C.c_int(0), C.c_int(0)
+    lib().oc_pose_last_stats(C.byref(it), C.byref(tr))
+    return it.value, tr.value
+
+
 def undistort_keypoints(kps, fx, fy, cx, cy, dist):
     """Frame::UndistortKeyPoints (Frame.cc:579-609); dist = (k1, k2, p1, p2, k3)."""
     kps = np.ascontiguousarray(kps)

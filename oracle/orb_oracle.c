@@ -1565,6 +1565,17 @@ static void pq_reduce(double lanes[PQ_LANES][PQ_NV], int nv, double out[PQ_NV])
 }
 
 /* LDL' of the 6x6 (no pivoting; fails unless every pivot > 0), then solve */
+/* g2o OptimizationAlgorithmLevenberg::solve: alpha = 1 - pow(2*rho - 1, 3).  glibc pow is
+   correctly rounded; t^3 is formed exactly as a double-double (t*t = h + l by fma, then
+   (h + l)*t = h2 + l2 + l*t) and rounded once, which equals the correctly rounded cube except
+   in ties closer than 2^-100 relative. */
+static double pq_cube(double t)
+{
+    const double h = t * t, l = fma(t, t, -h);
+    const double h2 = h * t, l2 = fma(h, t, -h2);
+    return h2 + fma(l, t, l2);
+}
+
 static int pq_solve6(const double H[36], const double b[6], double x[6])
 {
     double L[36] = {0}, d[6], y[6];
@@ -1598,7 +1609,7 @@ static int pq_solve6(const double H[36], const double b[6], double x[6])
 static double pq_active_chi2(const oc_pose_frame* fr, const oc_se3* s, const pq_edge* E, int ne, const uint8_t* active,
                              int robust, const double* delta, double* chi2_last)
 {
-    static double lanes[PQ_LANES][PQ_NV];
+    static _Thread_local double lanes[PQ_LANES][PQ_NV];
     memset(lanes, 0, sizeof(lanes));
     for (int i = 0; i < ne; i++) {
         if (!active[i]) continue;
@@ -1614,13 +1625,23 @@ static double pq_active_chi2(const oc_pose_frame* fr, const oc_se3* s, const pq_
     return out[0];
 }
 
+/* LM iterations and trials of the last oc_pose_optimization call on this thread (a KAT hook) */
+static _Thread_local int pq_stat_iters, pq_stat_trials;
+
+void oc_pose_last_stats(int* iterations, int* trials)
+{
+    *iterations = pq_stat_iters;
+    *trials = pq_stat_trials;
+}
+
 /* one SparseOptimizer::optimize(10) with OptimizationAlgorithmLevenberg (g2o 2012) */
 static void pq_optimize(const oc_pose_frame* fr, oc_se3* s, const pq_edge* E, int ne, const uint8_t* active, int robust,
                         const double* delta, double* chi2_last, int iterations)
 {
-    static double lanes[PQ_LANES][PQ_NV];
+    static _Thread_local double lanes[PQ_LANES][PQ_NV];
     double lambda = 0.0, ni = 2.0;
     for (int it = 0; it < iterations; it++) {
+        pq_stat_iters++;
         /* computeActiveErrors, activeRobustChi2, buildSystem (H = sum J' w rho1 J, b = -sum J' w rho1 e) */
         double currentChi = pq_active_chi2(fr, s, E, ne, active, robust, delta, chi2_last);
         memset(lanes, 0, sizeof(lanes));
@@ -1676,10 +1697,10 @@ static void pq_optimize(const oc_pose_frame* fr, oc_se3* s, const pq_edge* E, in
             if (!ok2) tempChi = DBL_MAX;
             double scale = 0.0;                          /* computeScale */
             for (int j = 0; j < 6; j++) scale = scale + x[j] * (lambda * x[j] + b[j]);
+            scale = scale + 1e-3;                        /* g2o: "make sure it's non-zero" */
             rho = (currentChi - tempChi) / scale;
             if (rho > 0 && isfinite(tempChi)) {
-                const double t2 = 2.0 * rho - 1.0;
-                double alpha = 1.0 - (t2 * t2) * t2;
+                double alpha = 1.0 - pq_cube(2.0 * rho - 1.0);
                 alpha = fmin(alpha, 2.0 / 3.0);
                 const double sf = fmax(1.0 / 3.0, alpha);
                 lambda = lambda * sf;
@@ -1691,6 +1712,7 @@ static void pq_optimize(const oc_pose_frame* fr, oc_se3* s, const pq_edge* E, in
                 *s = saved;                              /* pop */
             }
             qmax++;
+            pq_stat_trials++;
         } while (rho < 0 && qmax < 10);
         if (qmax == 10 || rho == 0) break;               /* Terminate */
     }
@@ -1699,6 +1721,7 @@ static void pq_optimize(const oc_pose_frame* fr, oc_se3* s, const pq_edge* E, in
 int oc_pose_optimization(const oc_pose_frame* fr, float Tcw[16], uint8_t* outlier)
 {
     const int n = fr->n;
+    pq_stat_iters = pq_stat_trials = 0;
     pq_edge* E = (pq_edge*)malloc(sizeof(pq_edge) * (n > 0 ? n : 1));
     int* idx = (int*)malloc(sizeof(int) * (n > 0 ? n : 1));
     int ne = 0;

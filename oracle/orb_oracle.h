@@ -203,6 +203,8 @@ typedef struct {
  * (OptimizationAlgorithmLevenberg, 2012 release vendored by ORB-SLAM2) with the per-edge
  * sums reduced over 256 lanes in a fixed tree: parity vs g2o UNPINNED. */
 int oc_pose_optimization(const oc_pose_frame* fr, float Tcw[16], uint8_t* outlier);
+/* LM iterations and trials the last oc_pose_optimization call on this thread ran (test hook). */
+void oc_pose_last_stats(int* iterations, int* trials);
 
 /* Frame::UndistortKeyPoints (Frame.cc:579-609): cv::undistortPoints(mat, mat, mK, mDistCoef,
  * Mat(), mK) of OpenCV 3.4 (cvUndistortPointsInternal, 5 fixed iterations) in double,

@@ -31,6 +31,82 @@ def test_shard_covers_all_frames():
             assert seen == list(range(total))
 
 
+def test_shard_frames_halo():
+    """Each rank extracts its matched chunk plus the frame before it (the halo); the chunks tile
+    frames 1..total of the sequence."""
+    from coeb_front.dist import shard_frames
+    for total in (1, 7, 256, 512, 513):
+        for world in (1, 2, 3, 8):
+            if total < world:
+                continue
+            matched = []
+            for r in range(world):
+                first, nex, nm = shard_frames(total, world, r)
+                assert nex == nm + 1 and nm >= 1
+                matched.extend(range(first + 1, first + nex))
+            assert matched == list(range(1, total + 1))
+
+
+def test_thread_ranks_barrier_and_max():
+    import threading
+    from coeb_front.dist import ThreadRanks
+    g = ThreadRanks(3, timeout=30)
+    res = [None] * 3
+
+    def body(r):
+        v = g.view(r)
+        v.barrier()
+        res[r] = (v.max(r * 10.0 + 1), v.sum(1.0), v.max(-r))
+    ths = [threading.Thread(target=body, args=(r,)) for r in range(3)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert res == [(21.0, 3.0, 0.0)] * 3
+
+
+def _bench(args, env=None, timeout=280):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        e.pop(k, None)
+    e.update(env or {})
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                         timeout=timeout, cwd=ROOT, env=e)
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    return out, lines
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus_without_torchrun():
+    """`bench.py --gpus 2` started directly drives two ranks (threads, one device each): the line
+    says n_gpus 2, the shards cover the whole weak-scaled sequence, the slower rank sets the time."""
+    out, lines = _bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "4", "--dry-run"])
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["scaling"] == "weak" and rec["config"]["ranks"] == "threads"
+    assert rec["config"]["frames_per_rank"] == [4, 4] and rec["config"]["matched_frames_per_step"] == 8
+    assert rec["ms_per_step"] >= 4.0       # rank 1 sleeps 4 ms per step
+    assert abs(rec["value"] - 8 * 3 / (rec["ms_per_step"] * 3 / 1e3)) / rec["value"] < 1e-3
+
+
+@pytest.mark.timeout(300)
+def test_bench_fixed_batch_strong_scaling():
+    """BASELINE configs[3]: a fixed 512-frame batch split over the GPUs (config B default)."""
+    out, lines = _bench(["--gpus", "3", "--config", "B", "--steps", "2", "--warmup", "1", "--dry-run",
+                         "--no-cpu-baseline"])
+    assert out.returncode == 0, out.stderr[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 3 and rec["scaling"] == "strong"
+    assert rec["config"]["frames_per_rank"] == [171, 171, 170] and sum(rec["config"]["frames_per_rank"]) == 512
+
+
+def test_bench_refuses_world_mismatch():
+    out, lines = _bench(["--gpus", "4", "--steps", "1", "--warmup", "0", "--batch", "2", "--dry-run"],
+                        env=dict(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), timeout=120)
+    assert out.returncode != 0 and not lines and "WORLD_SIZE" in out.stderr
+
+
 def _worker(rank, world, port, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))

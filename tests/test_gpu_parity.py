@@ -425,6 +425,59 @@ def test_batch_streams_agree(oracle_mod, ex):
         bp.close()
 
 
+def test_sharded_batch_equals_unsharded():
+    """SURVEY.md s8e partitioning: a 24-frame sequence split over 3 shards (each with its one-frame
+    halo, `dist.shard_frames`), driven concurrently from 3 host threads with one context each (what
+    `bench.py --gpus N` does per device; all on device 0 here), gives per-frame keypoints,
+    descriptors and matches bit-identical to the unsharded batch."""
+    import threading
+    from coeb_front.dist import shard_frames
+    from coeb_front.pipeline import BatchPipeline
+    G, world = 24, 3
+    seq = synth.make_frames(640, 480, G + 1, seed=1000)
+    full = BatchPipeline(640, 480, G + 1)
+    try:
+        full.load(seq, Tcw=np.stack([synth.motion_pose()] * (G + 1)))
+        full.run()
+        full.synchronize()
+        ref_out, ref_m, ref_n = full.results()
+    finally:
+        full.close()
+    got, errs = {}, []
+
+    def rank(r):
+        try:
+            first, F, nm = shard_frames(G, world, r)
+            fr = synth.make_frames(640, 480, F, seed=1000, first=first)
+            assert np.array_equal(fr, seq[first:first + F])
+            bp = BatchPipeline(640, 480, F)
+            try:
+                bp.load(fr, Tcw=np.stack([synth.motion_pose()] * F))
+                for _ in range(2):
+                    bp.run()
+                bp.synchronize()
+                got[r] = (first, bp.results())
+            finally:
+                bp.close()
+        except BaseException as e:    # noqa: BLE001
+            errs.append(e)
+    ths = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    covered = []
+    for r in range(world):
+        first, (out, m, n) = got[r]
+        for i in range(1, len(out)):
+            g = first + i
+            covered.append(g)
+            assert np.array_equal(out[i][0], ref_out[g][0]) and np.array_equal(out[i][1], ref_out[g][1]), g
+            assert n[i] == ref_n[g] and np.array_equal(m[i], ref_m[g]), g
+    assert covered == list(range(1, G + 1))
+
+
 # ------------------------------------------------------------------ local-map projection search
 def localmap_both(ctx, oracle_mod, ex, cur_k, cur_d, cur_ur, cur_obs, mp, th=3.0, nnratio=0.8):
     """coeb_match_localmap vs oracle.search_local_map (ORBmatcher.cc:44-129), bit-exact."""
@@ -624,10 +677,10 @@ def pose_both(ctx, oracle_mod, P, cam=None):
     inlier count identical (same canonical operations and reduction order)."""
     import coeb_front
     isg = np.array(ctx.tables().inv_sigma2[:8], np.float32)
-    nin_ref, T_ref, out_ref = oracle_mod.pose_optimization(P["kps"], P["has_mp"], P["xw"], P["ur"], isg,
-                                                           synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY,
-                                                           synth.TUM_BF, P["Tcw_init"])
-    cam = cam or coeb_front.make_camera(synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF, 640, 480)
+    intr = P.get("cam", (synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF))
+    nin_ref, T_ref, out_ref = oracle_mod.pose_optimization(P["kps"], P["has_mp"], P["xw"], P["ur"], isg, *intr,
+                                                           P["Tcw_init"])
+    cam = cam or coeb_front.make_camera(*intr, 640, 480)
     F = coeb_front.Frame(P["kps"], np.zeros((len(P["kps"]), 32), np.uint8), P["ur"], Tcw=P["Tcw_init"])
     F.mvpMapPoints = np.where(P["has_mp"] > 0, 0, -1).astype(np.int32)
     F.mvMapPointPos = P["xw"]
@@ -654,6 +707,19 @@ def test_pose_optimization_edges(ctx, oracle_mod):
         Q["has_mp"] = np.zeros_like(P["has_mp"])
         Q["has_mp"][:k] = 1
         pose_both(ctx, oracle_mod, Q)
+
+
+def test_pose_optimization_rho_zero(ctx, oracle_mod):
+    """Zero residuals at the entry pose: g2o's scale += 1e-3 gives rho == 0 and Terminate
+    (test_oracle_kat.py::test_pose_optimization_rho_zero_terminates); the kernel agrees, and so
+    it does from a perturbed start."""
+    from test_oracle_kat import exact_pose_problem
+    P = exact_pose_problem()
+    assert pose_both(ctx, oracle_mod, P) == len(P["kps"])
+    Q = dict(P)
+    Q["Tcw_init"] = np.eye(4, dtype=np.float32)
+    Q["Tcw_init"][0, 3] = 0.01
+    assert pose_both(ctx, oracle_mod, Q) == len(P["kps"])
 
 
 # ------------------------------------------------------------------ Frame ingest helpers

@@ -453,6 +453,49 @@ def test_pose_optimization_oracle_edge_cases(oracle_mod):
     assert 0 < nin <= 8
 
 
+def exact_pose_problem(n_side=8):
+    """A PoseOptimization input whose residuals are exactly zero at the entry pose (identity):
+    dyadic 3-D points, fx = fy = 512, integer principal point, depth 1 or 2, so every projection,
+    disparity and error is exact in float and double.  Then b = 0, the LM step is x = 0 and
+    tempChi == currentChi: g2o's `scale += 1e-3` makes rho exactly 0 -> Terminate after one
+    iteration per round (without it rho = 0/0 = NaN and all 10 iterations run)."""
+    from coeb_front import KEYPOINT_DTYPE
+    pts, kps = [], []
+    for i in range(n_side):
+        for j in range(n_side):
+            z = 1.0 if (i + j) % 2 else 2.0
+            X, Y = (i - n_side / 2) / 8.0, (j - n_side / 2) / 16.0
+            pts.append((X, Y, z))
+            kps.append((512.0 * X / z + 320.0, 512.0 * Y / z + 240.0))
+    n = len(pts)
+    k = np.zeros(n, KEYPOINT_DTYPE)
+    k["x"], k["y"] = np.array(kps, np.float32).T
+    k["octave"] = np.arange(n) % 8
+    k["class_id"] = -1
+    xw = np.array(pts, np.float32)
+    ur = (k["x"] - np.float32(40.0) / xw[:, 2]).astype(np.float32)
+    ur[::3] = -1.0                                   # a third monocular
+    return dict(kps=k, has_mp=np.ones(n, np.uint8), xw=xw, ur=ur, Tcw_init=np.eye(4, dtype=np.float32),
+                cam=(512.0, 512.0, 320.0, 240.0, 40.0))
+
+
+def test_pose_optimization_rho_zero_terminates(oracle_mod):
+    """ADVICE r1: g2o's OptimizationAlgorithmLevenberg::solve adds 1e-3 to computeScale() before
+    dividing; at a zero-residual optimum rho == 0 must end each round after one iteration."""
+    P = exact_pose_problem()
+    nin, T, outl = oracle_mod.pose_optimization(P["kps"], P["has_mp"], P["xw"], P["ur"], _inv_sigma2(), *P["cam"],
+                                                P["Tcw_init"])
+    assert nin == len(P["kps"]) and not outl.any()
+    assert np.array_equal(T, np.eye(4, dtype=np.float32))
+    assert oracle_mod.pose_last_stats() == (4, 4)     # 4 rounds x (1 iteration, 1 trial)
+    # a perturbed start converges (rho > 0 steps) and is not cut short
+    T0 = np.eye(4, dtype=np.float32)
+    T0[0, 3] = 0.01
+    nin, T, _ = oracle_mod.pose_optimization(P["kps"], P["has_mp"], P["xw"], P["ur"], _inv_sigma2(), *P["cam"], T0)
+    it, tr = oracle_mod.pose_last_stats()
+    assert nin == len(P["kps"]) and abs(T[0, 3]) < 1e-5 and it > 4 and tr >= it
+
+
 # ---- Frame::UndistortKeyPoints oracle: distort -> undistort round trip ----
 TUM1_DIST = (0.262383, -0.953104, -0.005358, 0.002628, 1.163314)   # Examples/RGB-D/TUM1.yaml
 
