@@ -146,8 +146,59 @@ int resize_tables(int sw, int sh, int dw, int dh, std::vector<int>& tab)
     return xmax;
 }
 
+// Split each cell row of a level into band segments of whole cells for k_fast_band: the fewest
+// segments whose windows fit its LDS rows (64 dwords of 4-pixel groups plus one dword either
+// side from a 16-byte aligned start) and its cell / row limits.
+bool make_segments(Plan& P, const std::vector<CellDesc>& cells, std::vector<FastSeg>& segs, std::string& err)
+{
+    segs.clear();
+    P.band_pw = 0;
+    auto make = [&](int l, int a, int z, FastSeg& S) {
+        S.level = (int16_t)l;
+        S.ncell = (int16_t)(z - a);
+        S.cell = (int16_t)a;
+        S.y0 = cells[a].y0;
+        S.ws = (int16_t)(cells[a].x0 + 3);
+        S.we = (int16_t)(cells[z - 1].x0 + cells[z - 1].rw - 3);
+        S.xs = (int16_t)((S.ws - 4) & ~15);
+        S.pw = (int16_t)((S.we - 1 - S.xs) / 4 + 2);        // dwords the pre-test touches
+        const int gfirst = (S.ws - S.xs) >> 2, glast = (S.we - 1 - S.xs) >> 2;
+        return glast - gfirst < 64 && S.pw <= kBandPW && S.ncell <= kBandCells && cells[a].rh <= kBandRows;
+    };
+    for (int l = 0; l < P.L; l++) {
+        LevelGeom& g = P.lv[l];
+        g.seg0 = (int)segs.size();
+        int k = g.cell0;
+        while (k < g.cell0 + g.ncells) {
+            int e = k;
+            while (e < g.cell0 + g.ncells && cells[e].i == cells[k].i) e++;   // cells of row i: [k, e)
+            const int n = e - k;
+            for (int nseg = 1; ; nseg++) {
+                if (nseg > n) { err = "FAST cell row does not fit the band kernel"; return false; }
+                std::vector<FastSeg> row;
+                bool ok = true;
+                for (int q = 0; q < nseg && ok; q++) {
+                    FastSeg S;
+                    ok = make(l, k + (int)((int64_t)n * q / nseg), k + (int)((int64_t)n * (q + 1) / nseg), S);
+                    row.push_back(S);
+                }
+                if (!ok) continue;
+                for (const FastSeg& S : row) {
+                    P.band_pw = std::max(P.band_pw, (int)S.pw);
+                    segs.push_back(S);
+                }
+                break;
+            }
+            k = e;
+        }
+        g.nseg = (int)segs.size() - g.seg0;
+    }
+    P.nsegs = (int)segs.size();
+    return true;
+}
+
 bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, std::vector<CellDesc>& cells,
-               std::string& err)
+               std::vector<FastSeg>& segs, std::string& err)
 {
     memset(&P, 0, sizeof(P));
     P.W = W; P.H = H; P.L = t.nlevels;
@@ -250,6 +301,10 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
     P.oct_kl = 2048;
     P.oct_lds = P.oct_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * P.oct_kl;
     if (P.oct_lds > 150 * 1024) { err = "octree LDS budget exceeded (features per level too large)"; return false; }
+    {
+        std::string serr;   // a plan the band kernel cannot take runs FAST per cell (k_fast)
+        if (!make_segments(P, cells, segs, serr)) { segs.clear(); P.nsegs = 0; }
+    }
     memcpy(P.umax, t.umax, sizeof(P.umax));
     // k_describe folds the IC_Angle disc (umax for HALF_PATCH_SIZE 15) into constants
     static const int kUmaxDisc[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
@@ -338,6 +393,7 @@ struct coeb_ctx {
     Plan plan{};
     std::vector<int> rtab;
     std::vector<CellDesc> cells;
+    std::vector<FastSeg> segs;
     std::map<std::string, DevBuf> bufs;
     std::string err;
     ProfImpl prof;
@@ -473,7 +529,7 @@ int ensure_plan(coeb_ctx* c, int W, int H)
         return set_err(c, COEB_EINVAL, "image size outside the context limits");
     std::string err;
     Plan P;
-    if (!make_plan(c->tab, W, H, P, c->rtab, c->cells, err)) return set_err(c, COEB_EINVAL, err);
+    if (!make_plan(c->tab, W, H, P, c->rtab, c->cells, c->segs, err)) return set_err(c, COEB_EINVAL, err);
     // the plan, rtab and cells are rewritten in place below: batches still in flight on the
     // context's streams (pyramid / FAST / octree / describe read them) must finish first
     int rc;
@@ -487,6 +543,10 @@ int ensure_plan(coeb_ctx* c, int W, int H)
     if ((rc = ensure(c, "rtab", std::max<size_t>(c->rtab.size(), 1), &drtab))) return rc;
     if ((rc = ensure(c, "cells", c->cells.size(), &dcells))) return rc;
     if ((rc = ensure(c, "pattern", 1024, &dpat))) return rc;
+    FastSeg* dsegs;
+    if ((rc = ensure(c, "segs", std::max<size_t>(c->segs.size(), 1), &dsegs))) return rc;
+    if (!c->segs.empty())
+        HIP_TRY(c, hipMemcpy(dsegs, c->segs.data(), c->segs.size() * sizeof(FastSeg), hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(dplan, &c->plan, sizeof(Plan), hipMemcpyHostToDevice));
     if (!c->rtab.empty()) HIP_TRY(c, hipMemcpy(drtab, c->rtab.data(), c->rtab.size() * sizeof(int), hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(dcells, c->cells.data(), c->cells.size() * sizeof(CellDesc), hipMemcpyHostToDevice));
@@ -524,6 +584,7 @@ int extract_bufs(coeb_ctx* c, int F, ExtractBufs& b)
     b.rtab = static_cast<const int*>(c->bufs["rtab"].p);
     b.cells = static_cast<const CellDesc*>(c->bufs["cells"].p);
     b.pattern = static_cast<const int8_t*>(c->bufs["pattern"].p);
+    b.segs = static_cast<const FastSeg*>(c->bufs["segs"].p);
     return 0;
 }
 
@@ -1489,6 +1550,14 @@ int coeb_internal_error(coeb_ctx* c, int code, const char* msg) { return set_err
 int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t bytes, size_t* size_out)
 {
     if (c) join_pose(c);
+    if (c && what && std::string(what) == "band_timing") {      // [8] k_fast_band phase clocks (COEB_BAND_CLOCK builds)
+        unsigned long long t[8];
+        if (size_out) *size_out = sizeof(t);
+        if (!host) return 0;                         // size query: the read below also clears
+        if (band_timing_read(t)) return COEB_EDEVICE;
+        memcpy(host, t, std::min(bytes, sizeof(t)));
+        return 0;
+    }
     if (c && what && std::string(what) == "pose_timing") {      // [F][8] k_pose phase clocks (COEB_POSE_TIMING)
         if (!c->bufs.count("p_timing")) return COEB_EINVAL;
         join_pose(c);

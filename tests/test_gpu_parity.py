@@ -67,6 +67,30 @@ def test_extract_B_1280x960(ctx, oracle_mod):
         c2.close()
 
 
+def test_fast_band_kernel_matches_oracle(ctx, ex, oracle_mod, monkeypatch):
+    """The band form of FAST (k_fast_band, COEB_FAST_BAND=1: one LDS copy per cell-row segment)
+    gives the same keypoints and descriptors as the per-cell kernel and the oracle, including a
+    size whose ROIs exceed its row limit (falls back to the per-cell kernel) and a noise image
+    (many corners per segment)."""
+    monkeypatch.setenv("COEB_FAST_BAND", "1")
+    for seed in (1000, 7):
+        run_both(ctx, ex, synth.make_frames(640, 480, 1, seed=seed)[0], tag="band %d" % seed)
+    rng = np.random.default_rng(3)
+    run_both(ctx, ex, rng.integers(0, 256, (480, 640), dtype=np.uint8), tag="band noise")
+    for w, h in ((320, 240), (641, 479), (1024, 768)):
+        run_both(ctx, ex, synth.make_frames(w, h, 1, seed=5)[0], tag="band %dx%d" % (w, h))
+    ex2 = oracle_mod.Extractor(2000, 1.2, 8, 20, 7)
+    from coeb_front import Context
+    c2 = Context(2000, 1.2, 8, 20, 7, 0, 1280, 960, 1)
+    try:
+        fr = synth.make_frames(1280, 960, 1, seed=11)[0]
+        k, d = c2.extract(fr)
+        r = ex2.extract(fr)
+        assert_same(k, d, r["kps"], r["desc"], "band B")
+    finally:
+        c2.close()
+
+
 @pytest.mark.parametrize("w,h", [(641, 479), (320, 240), (800, 600), (1024, 768), (720, 405)])
 def test_extract_ragged_sizes(ctx, ex, w, h):
     fr = synth.make_frames(w, h, 1, seed=w * 7 + h)
