@@ -123,7 +123,8 @@ public:
         if (rc != COEB_OK) throw std::runtime_error(coeb_last_error(ctx_));
         _keypoints.resize((size_t)n);
         static_assert(sizeof(coeb_keypoint) == sizeof(cv::KeyPoint), "coeb_keypoint must mirror cv::KeyPoint");
-        if (n) std::memcpy(&_keypoints[0], kps.data(), sizeof(coeb_keypoint) * (size_t)n);
+        // cv::KeyPoint is trivially copyable and layout-identical to coeb_keypoint (static_assert above)
+        if (n) std::memcpy(static_cast<void*>(&_keypoints[0]), kps.data(), sizeof(coeb_keypoint) * (size_t)n);
         if (n == 0) {
             _descriptors.release();
         } else {

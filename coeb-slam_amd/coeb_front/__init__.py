@@ -162,8 +162,8 @@ def lib():
                                       C.c_void_p]
         L.coeb_stereo_from_rgbd.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
                                             C.c_size_t, C.c_float, C.c_void_p, C.c_void_p]
-        L.coeb_rgbd_preprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_size_t,
-                                           C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.coeb_rgbd_preprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_void_p,
+                                           C.c_size_t, C.c_int, C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.coeb_descriptor_distance.argtypes = [C.c_void_p, C.c_void_p]
         L.coeb_profile_enable.argtypes = [C.c_void_p, C.c_int]
         L.coeb_profile_reset.argtypes = [C.c_void_p]
@@ -386,6 +386,30 @@ def UndistortKeyPoints(ctx, keys, camera, dist):
     out = keys.copy()
     ctx.check(lib().coeb_undistort_keypoints(ctx.h, C.byref(camera), _p(d), _p(keys), len(keys), _p(out)))
     return out
+
+
+def GrabImageRGBD(ctx, imRGB, imD=None, mbRGB=True, mDepthMapFactor=1.0):
+    """The input conversions of Tracking::GrabImageRGBD (src/Tracking.cc:212-228) on the device:
+    imRGB (H, W) gray, (H, W, 3) RGB/BGR or (H, W, 4) RGBA/BGRA u8 -> gray u8; imD (H, W) uint16
+    or float32 -> float32 via convertTo(CV_32F, mDepthMapFactor) (a float32 map with factor 1 is
+    kept as is).  mDepthMapFactor is the Tracking member, i.e. 1 / DepthMapFactor of the YAML.
+    Returns (gray, depth or None)."""
+    img = np.ascontiguousarray(imRGB, np.uint8)
+    h, w = img.shape[:2]
+    ch = 1 if img.ndim == 2 else img.shape[2]
+    gray = np.empty((h, w), np.uint8)
+    dep, dtype, dstride = None, 0, 0
+    if imD is not None:
+        d = np.ascontiguousarray(imD)
+        if d.shape != (h, w) or d.dtype not in (np.uint16, np.float32):
+            raise ValueError("imD must be (H, W) uint16 or float32")
+        dtype = 1 if d.dtype == np.float32 else 0
+        dstride = d.strides[0]
+        dep = np.empty((h, w), np.float32)
+    ctx.check(lib().coeb_rgbd_preprocess(ctx.h, _p(img), ch * w, ch, 1 if mbRGB else 0,
+                                         _p(d) if imD is not None else None, dstride, dtype,
+                                         C.c_float(mDepthMapFactor), w, h, _p(gray), _p(dep)))
+    return gray, dep
 
 
 def boxes_from_ros(xyxy):

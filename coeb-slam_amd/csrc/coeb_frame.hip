@@ -57,19 +57,33 @@ __global__ __launch_bounds__(256) void k_blur_flags(const uint8_t* __restrict__ 
     }
 }
 
-__global__ __launch_bounds__(256) void k_rgbd(const uint8_t* __restrict__ rgb, int rgb_stride, int rgb_order,
-                                              const uint16_t* __restrict__ d16, int dstride, float dscale, int W,
-                                              int H, uint8_t* __restrict__ gray, float* __restrict__ depth)
+__global__ __launch_bounds__(256) void k_rgbd(const uint8_t* __restrict__ img, int istride, int channels, int rgb_order,
+                                              const uint8_t* __restrict__ dsrc, int dstride, int dtype, float dscale,
+                                              int dcopy, int W, int H, uint8_t* __restrict__ gray,
+                                              float* __restrict__ depth)
 {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= W || y >= H) return;
-    if (rgb) {
-        const uint8_t* s = rgb + (int64_t)y * rgb_stride + 3 * x;
-        const int R2Y = 4899, G2Y = 9617, B2Y = 1868;
-        const int v = rgb_order ? (s[0] * R2Y + s[1] * G2Y + s[2] * B2Y) : (s[0] * B2Y + s[1] * G2Y + s[2] * R2Y);
-        gray[(int64_t)y * W + x] = (uint8_t)((v + (1 << 13)) >> 14);
+    if (img) {
+        const uint8_t* s = img + (int64_t)y * istride + channels * x;
+        uint8_t g = s[0];
+        if (channels >= 3) {                 // cvtColor RGB2GRAY / RGBA2GRAY (alpha ignored), 14-bit fixed point
+            const int R2Y = 4899, G2Y = 9617, B2Y = 1868;
+            const int v = rgb_order ? (s[0] * R2Y + s[1] * G2Y + s[2] * B2Y) : (s[0] * B2Y + s[1] * G2Y + s[2] * R2Y);
+            g = (uint8_t)((v + (1 << 13)) >> 14);
+        }
+        gray[(int64_t)y * W + x] = g;
     }
-    if (d16) depth[(int64_t)y * W + x] = (float)d16[(int64_t)y * dstride + x] * dscale;
+    if (dsrc) {
+        const uint8_t* row = dsrc + (int64_t)y * dstride;
+        float v;
+        if (dtype == COEB_DEPTH_U16) v = (float)reinterpret_cast<const uint16_t*>(row)[x] * dscale;
+        else {
+            v = reinterpret_cast<const float*>(row)[x];
+            if (!dcopy) v = v * dscale;      // convertTo(CV_32F, scale): float product
+        }
+        depth[(int64_t)y * W + x] = v;
+    }
 }
 
 // Frame::UndistortKeyPoints (Frame.cc:579-609): cv::undistortPoints(.., mK, mDistCoef, Mat(), mK)
@@ -141,37 +155,43 @@ extern "C" int coeb_blur_flags(coeb_ctx* c, const uint8_t* gray, int W, int H, s
     return COEB_OK;
 }
 
-extern "C" int coeb_rgbd_preprocess(coeb_ctx* c, const uint8_t* rgb, size_t rgb_stride, int rgb_order,
-                                    const uint16_t* depth16, size_t depth_stride, float depth_scale, int W, int H,
-                                    uint8_t* gray_out, float* depth_out)
+extern "C" int coeb_rgbd_preprocess(coeb_ctx* c, const uint8_t* img, size_t img_stride, int channels, int rgb_order,
+                                    const void* depth, size_t depth_stride, int depth_type, float depth_scale, int W,
+                                    int H, uint8_t* gray_out, float* depth_out)
 {
-    if (!c || W <= 0 || H <= 0 || (rgb && (!gray_out || rgb_stride < (size_t)3 * W)) ||
-        (depth16 && (!depth_out || depth_stride < (size_t)W)))
+    const size_t dbytes = depth_type == COEB_DEPTH_F32 ? 4 : 2;
+    if (!c || W <= 0 || H <= 0 ||
+        (img && (!gray_out || (channels != 1 && channels != 3 && channels != 4) || img_stride < (size_t)channels * W)) ||
+        (depth && (!depth_out || (depth_type != COEB_DEPTH_U16 && depth_type != COEB_DEPTH_F32) ||
+                   depth_stride < dbytes * W || depth_stride % dbytes)))
         return coeb_internal_error(c, COEB_EINVAL, "coeb_rgbd_preprocess: invalid arguments");
     hipStream_t s;
     int dev;
     if (coeb_internal_stream(c, &s, &dev)) return COEB_EINVAL;
     (void)hipSetDevice(dev);
-    void *drgb = nullptr, *dgray = nullptr, *dd16 = nullptr, *ddep = nullptr;
+    void *dimg = nullptr, *dgray = nullptr, *dd = nullptr, *ddep = nullptr;
     int rc;
-    if (rgb) {
-        if ((rc = coeb_internal_scratch(c, "pp_rgb", (size_t)W * H * 3, &drgb)) ||
+    const size_t rowb = (size_t)channels * W;
+    if (img) {
+        if ((rc = coeb_internal_scratch(c, "pp_img", rowb * H, &dimg)) ||
             (rc = coeb_internal_scratch(c, "pp_gray", (size_t)W * H, &dgray)))
             return rc;
-        FR_TRY(c, hipMemcpy2DAsync(drgb, (size_t)3 * W, rgb, rgb_stride, (size_t)3 * W, H, hipMemcpyHostToDevice, s));
+        FR_TRY(c, hipMemcpy2DAsync(dimg, rowb, img, img_stride, rowb, H, hipMemcpyHostToDevice, s));
     }
-    if (depth16) {
-        if ((rc = coeb_internal_scratch(c, "pp_d16", (size_t)W * H * 2, &dd16)) ||
+    // Tracking.cc:227: convertTo unless the map is already 32F and mDepthMapFactor == 1
+    const int dcopy = depth_type == COEB_DEPTH_F32 && !(fabsf(depth_scale - 1.0f) > 1e-5f);
+    if (depth) {
+        if ((rc = coeb_internal_scratch(c, "pp_dsrc", dbytes * W * H, &dd)) ||
             (rc = coeb_internal_scratch(c, "pp_dep", (size_t)W * H * 4, &ddep)))
             return rc;
-        FR_TRY(c, hipMemcpy2DAsync(dd16, (size_t)2 * W, depth16, depth_stride * 2, (size_t)2 * W, H,
-                                   hipMemcpyHostToDevice, s));
+        FR_TRY(c, hipMemcpy2DAsync(dd, dbytes * W, depth, depth_stride, dbytes * W, H, hipMemcpyHostToDevice, s));
     }
-    hipLaunchKernelGGL(k_rgbd, dim3((W + 63) / 64, (H + 3) / 4), dim3(256), 0, s, (const uint8_t*)drgb, 3 * W, rgb_order,
-                       (const uint16_t*)dd16, W, depth_scale, W, H, (uint8_t*)dgray, (float*)ddep);
+    hipLaunchKernelGGL(k_rgbd, dim3((W + 63) / 64, (H + 3) / 4), dim3(256), 0, s, (const uint8_t*)dimg, (int)rowb, channels,
+                       rgb_order, (const uint8_t*)dd, (int)(dbytes * W), depth_type, depth_scale, dcopy, W, H,
+                       (uint8_t*)dgray, (float*)ddep);
     FR_TRY(c, hipGetLastError());
-    if (rgb) FR_TRY(c, hipMemcpyAsync(gray_out, dgray, (size_t)W * H, hipMemcpyDeviceToHost, s));
-    if (depth16) FR_TRY(c, hipMemcpyAsync(depth_out, ddep, (size_t)W * H * 4, hipMemcpyDeviceToHost, s));
+    if (img) FR_TRY(c, hipMemcpyAsync(gray_out, dgray, (size_t)W * H, hipMemcpyDeviceToHost, s));
+    if (depth) FR_TRY(c, hipMemcpyAsync(depth_out, ddep, (size_t)W * H * 4, hipMemcpyDeviceToHost, s));
     FR_TRY(c, hipStreamSynchronize(s));
     return COEB_OK;
 }

@@ -275,10 +275,17 @@ int coeb_blur_flags(coeb_ctx* ctx, const uint8_t* gray, int width, int height, s
 int coeb_stereo_from_rgbd(coeb_ctx* ctx, const coeb_keypoint* kps, int n, const float* depth,
                           int width, int height, size_t depth_stride_floats, float bf,
                           float* u_right_out, float* depth_out);
-/* rgb: 8UC3 (rgb_order=1: RGB as Camera.RGB=1; 0: BGR); depth16: 16UC1 scaled by depth_scale
- * (= 1/DepthMapFactor) to float.  Either input may be NULL. */
-int coeb_rgbd_preprocess(coeb_ctx* ctx, const uint8_t* rgb, size_t rgb_stride, int rgb_order,
-                         const uint16_t* depth16, size_t depth_stride, float depth_scale,
+/* Tracking::GrabImageRGBD's input conversions (src/Tracking.cc:212-228).
+ * img: `channels` = 1 (8UC1, copied), 3 (8UC3: RGB2GRAY when rgb_order = 1, as Camera.RGB = 1,
+ * else BGR2GRAY) or 4 (8UC4: RGBA2GRAY / BGRA2GRAY, alpha ignored); img_stride in bytes.
+ * depth: depth_type COEB_DEPTH_U16 (16UC1) or COEB_DEPTH_F32 (32FC1), depth_stride in bytes;
+ * imDepth.convertTo(CV_32F, depth_scale) with depth_scale = mDepthMapFactor (= 1/DepthMapFactor),
+ * except that a 32F map with |depth_scale - 1| <= 1e-5 is passed through unchanged (:227).
+ * Either input may be NULL. */
+#define COEB_DEPTH_U16 0
+#define COEB_DEPTH_F32 1
+int coeb_rgbd_preprocess(coeb_ctx* ctx, const uint8_t* img, size_t img_stride, int channels, int rgb_order,
+                         const void* depth, size_t depth_stride, int depth_type, float depth_scale,
                          int width, int height, uint8_t* gray_out, float* depth_out);
 
 /* mvKeysUn from mvKeys: cv::undistortPoints(.., mK, mDistCoef, Mat(), mK) (OpenCV 3.4, 5

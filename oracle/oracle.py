@@ -291,6 +291,28 @@ def gauss_kernel7():
     return list(k)
 
 
+def image_to_gray(img, rgb_order=1):
+    """Tracking::GrabImageRGBD gray conversion (Tracking.cc:212-225): (h, w) gray, (h, w, 3) or
+    (h, w, 4) images."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape[:2]
+    ch = 1 if img.ndim == 2 else img.shape[2]
+    out = np.zeros((h, w), np.uint8)
+    lib().oc_image_to_gray(ptr(img), w, h, ch * w, ch, rgb_order, ptr(out))
+    return out
+
+
+def depth_to_float(depth, factor):
+    """Tracking.cc:227-228: uint16 or float32 depth map -> float32 (convertTo with mDepthMapFactor;
+    a float32 map with factor 1 is returned unchanged)."""
+    depth = np.ascontiguousarray(depth)
+    h, w = depth.shape
+    dt = {np.dtype(np.uint16): 0, np.dtype(np.float32): 1}[depth.dtype]
+    out = np.zeros((h, w), np.float32)
+    lib().oc_depth_to_float(ptr(depth), w, h, C.c_size_t(depth.strides[0]), dt, C.c_float(factor), ptr(out))
+    return out
+
+
 def rgb2gray(rgb, rgb_order=1):
     rgb = np.ascontiguousarray(rgb, np.uint8)
     h, w, _ = rgb.shape

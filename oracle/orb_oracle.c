@@ -928,15 +928,42 @@ int oc_blur_flags(const uint8_t* gray, int w, int h, int stride,
 }
 
 /* cvtColor RGB2GRAY / BGR2GRAY 8U, 14-bit fixed point (imgproc color.cpp RGB2Gray<uchar>) */
-void oc_rgb2gray(const uint8_t* rgb, int w, int h, int stride, int rgb_order, uint8_t* out)
+/* Tracking::GrabImageRGBD (Tracking.cc:212-225): cvtColor RGB2GRAY / BGR2GRAY (3 channels),
+   RGBA2GRAY / BGRA2GRAY (4 channels, alpha ignored); a 1-channel image is used as is.  OpenCV
+   3.4 8U fixed point: R 4899, G 9617, B 1868, 14-bit shift with rounding. */
+void oc_image_to_gray(const uint8_t* img, int w, int h, int stride, int channels, int rgb_order, uint8_t* out)
 {
     const int R2Y = 4899, G2Y = 9617, B2Y = 1868;
     for (int y = 0; y < h; y++) {
-        const uint8_t* s = rgb + (size_t)y * stride;
+        const uint8_t* s = img + (size_t)y * stride;
         for (int x = 0; x < w; x++) {
-            int c0 = s[3 * x], c1 = s[3 * x + 1], c2 = s[3 * x + 2];
-            int v = rgb_order ? (c0 * R2Y + c1 * G2Y + c2 * B2Y) : (c0 * B2Y + c1 * G2Y + c2 * R2Y);
+            const uint8_t* p = s + (size_t)channels * x;
+            if (channels == 1) { out[(size_t)y * w + x] = p[0]; continue; }
+            const int c0 = p[0], c1 = p[1], c2 = p[2];
+            const int v = rgb_order ? (c0 * R2Y + c1 * G2Y + c2 * B2Y) : (c0 * B2Y + c1 * G2Y + c2 * R2Y);
             out[(size_t)y * w + x] = (uint8_t)((v + (1 << 13)) >> 14);
+        }
+    }
+}
+
+void oc_rgb2gray(const uint8_t* rgb, int w, int h, int stride, int rgb_order, uint8_t* out)
+{
+    oc_image_to_gray(rgb, w, h, stride, 3, rgb_order, out);
+}
+
+/* Tracking.cc:227-228: if (fabs(mDepthMapFactor - 1) > 1e-5 || type != CV_32F)
+   imDepth.convertTo(imDepth, CV_32F, mDepthMapFactor) -- float product (cvtScale, WT = float);
+   otherwise the 32F map is used unchanged.  depth_type 0 = 16UC1, 1 = 32FC1; stride in bytes. */
+void oc_depth_to_float(const void* depth, int w, int h, size_t stride, int depth_type, float factor, float* out)
+{
+    const int copy = depth_type == 1 && !(fabsf(factor - 1.0f) > 1e-5f);
+    for (int y = 0; y < h; y++) {
+        const uint8_t* row = (const uint8_t*)depth + (size_t)y * stride;
+        for (int x = 0; x < w; x++) {
+            float v;
+            if (depth_type == 0) v = (float)((const uint16_t*)row)[x] * factor;
+            else v = copy ? ((const float*)row)[x] : ((const float*)row)[x] * factor;
+            out[(size_t)y * w + x] = v;
         }
     }
 }

@@ -17,6 +17,7 @@
  */
 #ifndef ORB_ORACLE_H
 #define ORB_ORACLE_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -97,6 +98,10 @@ int oc_blur_flags(const uint8_t* gray, int w, int h, int stride,
                   const oc_box* boxes, int nbox, int32_t* out, double* mean_out);
 /* Tracking::GrabImageRGBD cvtColor RGB->GRAY 8U (src/Tracking.cc:212-225) */
 void oc_rgb2gray(const uint8_t* rgb, int w, int h, int stride, int rgb_order, uint8_t* out);
+/* Tracking::GrabImageRGBD image and depth conversions (Tracking.cc:212-228); channels 1/3/4,
+   depth_type 0 = 16UC1, 1 = 32FC1 (stride in bytes). */
+void oc_image_to_gray(const uint8_t* img, int w, int h, int stride, int channels, int rgb_order, uint8_t* out);
+void oc_depth_to_float(const void* depth, int w, int h, size_t stride, int depth_type, float factor, float* out);
 
 /* ---- matcher side ---- */
 typedef struct {

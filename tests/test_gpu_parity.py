@@ -155,17 +155,65 @@ def test_blur_flags(ctx, oracle_mod):
     assert np.array_equal(out, ref) and ref[0] == 1
 
 
+@pytest.mark.parametrize("channels,mbrgb", [(3, True), (3, False), (4, True), (4, False), (1, True)])
+def test_rgbd_preprocess_formats(ctx, oracle_mod, channels, mbrgb):
+    """Tracking::GrabImageRGBD (Tracking.cc:212-228): RGB / BGR / RGBA / BGRA / gray images, with
+    a ragged row stride, against the oracle; 16UC1 depth scaled, 32FC1 depth scaled or (factor 1)
+    passed through bit-for-bit."""
+    import coeb_front
+    rng = np.random.default_rng(channels * 10 + mbrgb)
+    h, w = 121, 203
+    shape = (h, w) if channels == 1 else (h, w, channels)
+    img = rng.integers(0, 256, shape, dtype=np.uint8)
+    d16 = rng.integers(0, 65535, (h, w), dtype=np.uint16)
+    gray, dep = coeb_front.GrabImageRGBD(ctx, img, d16, mbrgb, np.float32(1 / 5000.0))
+    assert np.array_equal(gray, oracle_mod.image_to_gray(img, 1 if mbrgb else 0))
+    assert np.array_equal(dep, oracle_mod.depth_to_float(d16, np.float32(1 / 5000.0)))
+    assert np.array_equal(dep, d16.astype(np.float32) * np.float32(1 / 5000.0))
+    d32 = (rng.random((h, w)) * 8).astype(np.float32)
+    d32[0, :4] = [np.nan, np.inf, -0.0, 0.0]
+    for factor in (1.0, 1.0 + 5e-6, 0.5, 1 / 5000.0):
+        _, dep = coeb_front.GrabImageRGBD(ctx, img, d32, mbrgb, np.float32(factor))
+        ref = oracle_mod.depth_to_float(d32, np.float32(factor))
+        assert np.array_equal(dep.view(np.uint32), ref.view(np.uint32)), factor
+        if abs(np.float32(factor) - 1) <= 1e-5:
+            assert np.array_equal(dep.view(np.uint32), d32.view(np.uint32))     # :227 passthrough
+    # a sub-view with a row stride larger than the row (ctypes sees the parent's pitch)
+    big = rng.integers(0, 256, (h, w + 9) + (() if channels == 1 else (channels,)), dtype=np.uint8)
+    view = big[:, :w]
+    from coeb_front import lib
+    import ctypes as C
+    out = np.zeros((h, w), np.uint8)
+    ctx.check(lib().coeb_rgbd_preprocess(ctx.h, big.ctypes.data_as(C.c_void_p), big.strides[0], channels,
+                                         1 if mbrgb else 0, None, 0, 0, C.c_float(1.0), w, h,
+                                         out.ctypes.data_as(C.c_void_p), None))
+    assert np.array_equal(out, oracle_mod.image_to_gray(np.ascontiguousarray(view), 1 if mbrgb else 0))
+
+
+def test_rgbd_preprocess_rejects_bad_arguments(ctx):
+    from coeb_front import CoebError, lib
+    import ctypes as C
+    img = np.zeros((8, 8, 2), np.uint8)
+    out = np.zeros((8, 8), np.uint8)
+    for ch in (0, 2, 5):
+        rc = lib().coeb_rgbd_preprocess(ctx.h, img.ctypes.data_as(C.c_void_p), 16, ch, 1, None, 0, 0,
+                                        C.c_float(1.0), 8, 8, out.ctypes.data_as(C.c_void_p), None)
+        assert rc == -22
+    d = np.zeros((8, 8), np.uint16)
+    rc = lib().coeb_rgbd_preprocess(ctx.h, None, 0, 3, 1, d.ctypes.data_as(C.c_void_p), 16, 7, C.c_float(1.0), 8, 8,
+                                    None, out.ctypes.data_as(C.c_void_p))
+    assert rc == -22
+    assert CoebError
+
+
 def test_rgbd_preprocess_and_stereo(ctx, oracle_mod):
+    import coeb_front
     from coeb_front import lib
     import ctypes as C
     rng = np.random.default_rng(3)
     rgb = rng.integers(0, 256, (480, 640, 3), dtype=np.uint8)
     d16 = rng.integers(0, 6000, (480, 640), dtype=np.uint16)
-    gray = np.zeros((480, 640), np.uint8)
-    dep = np.zeros((480, 640), np.float32)
-    ctx.check(lib().coeb_rgbd_preprocess(ctx.h, rgb.ctypes.data_as(C.c_void_p), 640 * 3, 1,
-                                         d16.ctypes.data_as(C.c_void_p), 640, C.c_float(1 / 5000.0), 640, 480,
-                                         gray.ctypes.data_as(C.c_void_p), dep.ctypes.data_as(C.c_void_p)))
+    gray, dep = coeb_front.GrabImageRGBD(ctx, rgb, d16, True, np.float32(1 / 5000.0))
     assert np.array_equal(gray, oracle_mod.rgb2gray(rgb, 1))
     assert np.array_equal(dep, d16.astype(np.float32) * np.float32(1 / 5000.0))
     k, d = ctx.extract(gray)

@@ -533,3 +533,23 @@ def test_tum_association_golden():
                             c["max_difference"])
         assert [list(x) for x in got] == c["matches"]
         assert len(got) > 20
+
+
+def test_grab_image_rgbd_conversions_kat(oracle_mod):
+    """GrabImageRGBD's cvtColor (Tracking.cc:212-225): the OpenCV 3.4 8U coefficients give the
+    well-known gray levels of the primaries (R -> 76, G -> 150, B -> 29); RGB vs BGR swap R and
+    B; the 4-channel forms ignore alpha; a gray image is used as is.  Depth (:227-228): 16UC1
+    scaled in float; 32FC1 with factor 1 unchanged (NaN and -0 included)."""
+    px = np.array([[[255, 0, 0], [0, 255, 0], [0, 0, 255], [255, 255, 255]]], np.uint8)
+    assert oracle_mod.image_to_gray(px, 1).tolist() == [[76, 150, 29, 255]]
+    assert oracle_mod.image_to_gray(px, 0).tolist() == [[29, 150, 76, 255]]
+    rgba = np.concatenate([px, np.array([[[0], [17], [128], [255]]], np.uint8)], axis=2)
+    assert oracle_mod.image_to_gray(rgba, 1).tolist() == [[76, 150, 29, 255]]
+    g = np.arange(12, dtype=np.uint8).reshape(3, 4)
+    assert np.array_equal(oracle_mod.image_to_gray(g), g)
+    d16 = np.array([[0, 1, 5000, 65535]], np.uint16)
+    f = np.float32(1 / 5000.0)
+    assert np.array_equal(oracle_mod.depth_to_float(d16, f), d16.astype(np.float32) * f)
+    d32 = np.array([[np.nan, -0.0, 1.5, 3e38]], np.float32)
+    assert np.array_equal(oracle_mod.depth_to_float(d32, 1.0).view(np.uint32), d32.view(np.uint32))
+    assert np.array_equal(oracle_mod.depth_to_float(d32, 2.0)[0, 2:], np.float32([3.0, np.inf]))
