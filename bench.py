@@ -22,6 +22,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "coeb-slam_amd"))
+# hardware queues per process (HIP default 4): the PCIe-inclusive leg runs two contexts and three
+# copy queues whose streams must not share queues; read when the HIP runtime starts
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 import numpy as np  # noqa: E402
 
@@ -558,9 +561,6 @@ def rank_main(ranks, args):
         bp.ctx.set_batch_streams(args.streams)
     ranks.barrier()
 
-    e2e = None
-    if not args.no_e2e and not args.dry_run:
-        e2e = e2e_timing(bp, ranks, G, max(2, min(5, args.steps)))
 
     value = G * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -604,9 +604,10 @@ def rank_main(ranks, args):
                     kernels_ms_per_step={k: round(v[0] / max(1, prof_steps), 4) for k, v in prof.items()},
                     kernels_profiled_steps=prof_steps,
                     keypoints_per_frame=round(nkp, 1), matches_per_frame=round(nmatch, 1),
-                    pcie_inclusive=e2e)
+                    pcie_inclusive=None)
         if not args.no_extras and world == 1 and not args.dry_run:
             line["extras"] = extras_timing(bp.ctx, out, w, h)
+            line["extras"]["single_frame"] = single_frame_timing(w, h)
             if not cfg.get("dyn") and not cfg.get("pose"):
                 line["extras"]["config5_tracking"] = config5_timing(bp, nmatched)
                 line["extras"]["config3_dynamic_mask"] = config3_timing(bp, synth.make_frames(w, h, F, seed=1000),
@@ -617,8 +618,16 @@ def rank_main(ranks, args):
                 cb["extras_ms_per_call"] = cpu_extras(out, w, h)
             line["cpu_baseline"] = cb
             line["speedup_vs_cpu_baseline"] = round(value / cb["value"], 1)
-        print(json.dumps(line), flush=True)
+    # PCIe-inclusive leg last, with the device-resident pipeline closed: its two contexts and copy
+    # queue then have hardware queues of their own
+    host_frames, host_tcw = getattr(bp, "host_frames", None), getattr(bp, "Tcw", None)
     bp.close()
+    e2e = None
+    if not args.no_e2e and not args.dry_run:
+        e2e = e2e_timing(host_frames, host_tcw, ranks, G, 30, cfg, local_rank)
+    if rank == 0:
+        line["pcie_inclusive"] = e2e
+        print(json.dumps(line), flush=True)
     ranks.close()
 
 
@@ -627,21 +636,85 @@ def _thread_rank_type():
     return _ThreadRank
 
 
-def e2e_timing(bp, ranks, G, steps):
-    """Host buffers in and out (reported, never `value`)."""
-    frames = bp.host_frames
-    st = bp.run_host(frames)
-    bp.synchronize()
-    ranks.barrier()
-    te0 = time.perf_counter()
-    for _ in range(steps):
-        st = bp.run_host(frames, st)
-    bp.synchronize()
-    te = ranks.max(time.perf_counter() - te0)
-    return dict(value=round(G * steps / te, 2), unit="frames/s", ms_per_step=round(te / steps * 1e3, 4),
-                steps=steps,
-                note="host gray frames uploaded and keypoints/descriptors/matches downloaded each step "
-                     "(synchronous hipMemcpy on the context stream, pageable host memory)")
+def e2e_timing(frames, Tcw, ranks, G, steps, cfg, device):
+    """PCIe-inclusive rate (reported, never `value`): gray frames start in page-locked host
+    memory, keypoints / descriptors / counts / matches end in page-locked host memory.  Two batch
+    slots (HostStream, two contexts) so one batch's uploads and downloads overlap the other's
+    kernels."""
+    from coeb_front import HostBuffer
+    from coeb_front.pipeline import HostStream
+    F, H, W = frames.shape
+    hs = HostStream(W, H, F, nfeatures=cfg["nfeatures"], device=device, Tcw=Tcw)
+    src = HostBuffer(F * H * W)
+    src.view(np.uint8, (F, H, W))[:] = frames
+    try:
+        for i in range(4):                    # warm-up: both slots twice
+            hs.submit(i, src)
+        hs.wait(2)
+        hs.wait(3)
+        ranks.barrier()
+        te0 = time.perf_counter()
+        for i in range(steps):               # device-side ordering only: the host never blocks here
+            hs.submit(i, src)
+        hs.wait(steps - 2)
+        hs.wait(steps - 1)
+        te = ranks.max(time.perf_counter() - te0)
+        out, _, nms = hs.results(steps - 1)
+        ok = len(out) == F and sum(len(o[0]) for o in out) > 0
+    finally:
+        hs.close()
+        src.free()
+    return dict(value=round(G * steps / te, 2), unit="frames/s", ms_per_step=round(te / steps * 1e3, 4), steps=steps,
+                results_nonempty=bool(ok),
+                note="gray frames uploaded from page-locked host memory and keypoints/descriptors/counts/matches "
+                     "downloaded to page-locked host memory every step; two batch slots (contexts) and one copy "
+                     "queue: batch i+1's upload runs while batch i computes, batch i's results follow it")
+
+
+def single_frame_timing(w, h, reps=50):
+    """Drop-in latency of one frame from host buffers, as the sequential Tracking thread calls it
+    (Tracking.cc:229 -> Frame ctor -> ExtractORB; ComputeStereoFromRGBD; TrackWithMotionModel's
+    SearchByProjection): coeb_extract + coeb_stereo_from_rgbd + coeb_match_lastframe, mean ms."""
+    import ctypes as C
+    import coeb_front as cf
+    from coeb_front import synth
+    ctx = cf.Context(max_width=w, max_height=h, max_batch=1)
+    try:
+        fr = synth.make_frames(w, h, reps + 1, seed=77)
+        depth = synth.make_depth(w, h)
+        cam = cf.make_camera(synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF, w, h)
+        m = cf.ORBmatcher(0.9, True, ctx=ctx)
+        Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
+
+        def frame(img):
+            k, d = ctx.extract(img)
+            ur = np.empty(len(k), np.float32)
+            dep = np.empty(len(k), np.float32)
+            ctx.check(cf.lib().coeb_stereo_from_rgbd(ctx.h, k.ctypes.data_as(C.c_void_p), len(k),
+                                                     depth.ctypes.data_as(C.c_void_p), w, h, w, C.c_float(synth.TUM_BF),
+                                                     ur.ctypes.data_as(C.c_void_p), dep.ctypes.data_as(C.c_void_p)))
+            return k, d, ur, dep
+        k0, d0, _, dep0 = frame(fr[0])
+        z = dep0
+        xw = np.stack([(k0["x"] - np.float32(synth.TUM_CX)) * z / np.float32(synth.TUM_FX),
+                       (k0["y"] - np.float32(synth.TUM_CY)) * z / np.float32(synth.TUM_FY), z], 1).astype(np.float32)
+        last = cf.Frame(k0, d0, Tcw=Tl, map_points=dict(world_pos=xw, descriptor=d0,
+                                                        observations=np.full(len(k0), 2, np.int32),
+                                                        valid=(z > 0).astype(np.uint8)))
+        times, nms = [], []
+        for i in range(1, reps + 1):
+            t0 = time.perf_counter()
+            k, d, ur, _ = frame(fr[i])
+            cur = cf.Frame(k, d, ur, Tcw=Tc)
+            nm = m.SearchByProjection(cur, last, 15.0, False, cam)
+            times.append(time.perf_counter() - t0)
+            nms.append(nm)
+        return dict(ms_per_frame=round(float(np.median(times)) * 1e3, 4), reps=reps,
+                    matches=int(np.median(nms)),
+                    note="median over %d frames of coeb_extract + coeb_stereo_from_rgbd + coeb_match_lastframe "
+                         "from host buffers (one frame at a time, synchronous, as the Tracking thread)" % reps)
+    finally:
+        ctx.close()
 
 
 if __name__ == "__main__":

@@ -49,6 +49,9 @@ ABI_SYMBOLS = [
     "coeb_boxes_from_int64", "coeb_good_features", "coeb_corner_subpix", "coeb_optical_flow_pyr_lk",
     "coeb_moving_tail", "coeb_moving_object_points", "coeb_moving_object_points_device",
     "coeb_pose_batch_device", "coeb_batch_pose_results",
+    "coeb_host_alloc", "coeb_host_free", "coeb_memcpy_h2d_async", "coeb_memcpy_d2h_async",
+    "coeb_copyq_create", "coeb_copyq_destroy", "coeb_copyq_h2d", "coeb_copyq_d2h", "coeb_copyq_after_ctx",
+    "coeb_ctx_after_copyq", "coeb_copyq_synchronize",
 ]
 
 
@@ -175,6 +178,18 @@ def lib():
         L.coeb_device_free.argtypes = [C.c_void_p, C.c_void_p]
         L.coeb_memcpy_h2d.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
         L.coeb_memcpy_d2h.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        L.coeb_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p)]
+        L.coeb_host_free.argtypes = [C.c_void_p]
+        L.coeb_memcpy_h2d_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        L.coeb_memcpy_d2h_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        L.coeb_copyq_create.restype = C.c_void_p
+        L.coeb_copyq_create.argtypes = [C.c_void_p]
+        L.coeb_copyq_destroy.argtypes = [C.c_void_p]
+        L.coeb_copyq_h2d.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        L.coeb_copyq_d2h.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        L.coeb_copyq_after_ctx.argtypes = [C.c_void_p, C.c_void_p]
+        L.coeb_ctx_after_copyq.argtypes = [C.c_void_p, C.c_void_p]
+        L.coeb_copyq_synchronize.argtypes = [C.c_void_p]
         L.coeb_debug_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_size_t,
                                       C.POINTER(C.c_size_t)]
         _lib = L
@@ -368,6 +383,36 @@ class DeviceBuffer:
     def free(self):
         if self.ptr is not None and self.ctx.h is not None:
             lib().coeb_device_free(self.ctx.h, C.c_void_p(self.ptr))
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class HostBuffer:
+    """Page-locked host memory (coeb_host_alloc) viewed as a numpy array: copies between it and
+    the device run asynchronously on the DMA engines (coeb_memcpy_*_async)."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        rc = lib().coeb_host_alloc(self.nbytes, C.byref(p))
+        if rc != 0:
+            raise CoebError("coeb_host_alloc rc=%d: %s" % (rc, lib().coeb_last_error(None).decode()))
+        self.ptr = p.value
+        self.array = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def view(self, dtype, shape=None):
+        a = self.array.view(dtype)
+        return a if shape is None else a[:int(np.prod(shape))].reshape(shape)
+
+    def free(self):
+        if self.ptr is not None:
+            self.array = None
+            lib().coeb_host_free(C.c_void_p(self.ptr))
         self.ptr = None
 
     def __del__(self):

@@ -7,7 +7,9 @@ extracted so frame 1 can be matched, and is not counted as a processed frame.
 """
 import numpy as np
 
-from . import Context, KEYPOINT_DTYPE, make_camera, synth
+import ctypes as C
+
+from . import Context, HostBuffer, KEYPOINT_DTYPE, lib, make_camera, synth
 
 
 class BatchPipeline:
@@ -124,3 +126,119 @@ class BatchPipeline:
             if b is not None:
                 b.free()
         self.ctx.close()
+
+
+class HostStream:
+    """Host buffers in, host buffers out, with copy / kernel overlap (the PCIe-inclusive rate,
+    DESIGN.md s5).  Two batch slots, each a BatchPipeline with its own context (streams and device
+    buffers) on the same device, and one copy queue (coeb_copyq; shared_queue=False gives each
+    slot a download queue of its own: measured no faster).  Batch i (slot k = i % 2):
+      copy queue: waits for slot k's earlier kernels (its gray buffer is free), uploads the frames
+                  from page-locked host memory;
+      slot k:     waits for the upload (and, with per-slot download queues, for slot k's previous
+                  download: its result buffers are free), extracts + matches;
+      copy queue: after batch i + 1's upload, waits for those kernels and downloads keypoints /
+                  descriptors / counts / matches into slot k's page-locked output buffers.
+    Uploads run back to back (concurrent uploads only split the PCIe bandwidth) while the
+    previous batch computes; the 17 MB of results per 257 frames follow each upload.  Every
+    ordering is a device-side event wait, so
+    submit() never blocks the host: results of batch i are readable after wait(i) and stay so
+    until batch i + 2's kernels finish (its download reuses slot i % 2's host buffers), so read
+    them before submitting batch i + 2.  The process needs more than 4 hardware queues
+    (GPU_MAX_HW_QUEUES = 16 in bench.py): with HIP's default of 4 the streams of two contexts and the
+    copy queue share queues, and an upload queued behind the other slot's kernels loses the
+    overlap; queues of contexts closed earlier in the process stay taken, measured."""
+
+    def __init__(self, width, height, nframes, nfeatures=1000, device=0, depth=None, Tcw=None, shared_queue=True):
+        self.W, self.H, self.F = width, height, nframes
+        self.slots = [BatchPipeline(width, height, nframes, nfeatures=nfeatures, device=device) for _ in range(2)]
+        zero = np.zeros((nframes, height, width), np.uint8)
+        for sl in self.slots:
+            sl.load(zero, depth=depth, Tcw=Tcw)
+            sl.run()                                   # sizes every device buffer once
+            sl.synchronize()
+        kp_ptr, desc_ptr, cnt_ptr, kcap = self.slots[0].ctx.batch_results()
+        self.kcap = kcap
+        F = nframes
+        self.sizes = dict(kps=28 * kcap * F, desc=32 * kcap * F, counts=4 * F, match=4 * kcap * F, nmatch=4 * F)
+        self.out = [{k: HostBuffer(n) for k, n in self.sizes.items()} for _ in range(2)]
+        L = lib()
+        self.up = L.coeb_copyq_create(self.slots[0].ctx.h)
+        self.down = [self.up, self.up] if shared_queue else [L.coeb_copyq_create(sl.ctx.h) for sl in self.slots]
+        if not self.up or not all(self.down):
+            raise RuntimeError("coeb_copyq_create failed: %s" % L.coeb_last_error(None).decode())
+        self.inflight = []
+        self.pending_dl = None              # batch whose download is not enqueued yet
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise RuntimeError("coeb rc=%d: %s" % (rc, lib().coeb_last_error(None).decode()))
+
+    def submit(self, i, host_frames):
+        """Enqueue batch i (host_frames: a HostBuffer of F*H*W gray bytes) on slot i % 2 and the
+        download of batch i - 1; returns at once (the device orders it after batch i - 2 on the
+        same slot).  Batch i's upload is queued before batch i - 1's download, so on a shared
+        copy queue the upload does not wait behind batch i - 1's kernels."""
+        k = i % 2
+        L = lib()
+        sl, c = self.slots[k], self.slots[k].ctx
+        self._chk(L.coeb_copyq_after_ctx(self.up, c.h))
+        self._chk(L.coeb_copyq_h2d(self.up, C.c_void_p(sl.gray.ptr), C.c_void_p(host_frames.ptr),
+                                   self.F * self.H * self.W))
+        self._chk(L.coeb_ctx_after_copyq(c.h, self.up))
+        if self.down[k] != self.up:
+            self._chk(L.coeb_ctx_after_copyq(c.h, self.down[k]))
+        sl.run()
+        self._flush_download()
+        self.pending_dl = i
+        self.inflight.append(i)
+
+    def _flush_download(self):
+        i = self.pending_dl
+        if i is None:
+            return
+        self.pending_dl = None
+        k = i % 2
+        L = lib()
+        c = self.slots[k].ctx
+        self._chk(L.coeb_copyq_after_ctx(self.down[k], c.h))
+        kp_ptr, desc_ptr, cnt_ptr, _ = c.batch_results()
+        m_ptr, n_ptr = c.batch_match_results()
+        o = self.out[k]
+        for name, dptr in (("counts", cnt_ptr), ("kps", kp_ptr), ("desc", desc_ptr), ("match", m_ptr),
+                           ("nmatch", n_ptr)):
+            self._chk(L.coeb_copyq_d2h(self.down[k], C.c_void_p(o[name].ptr), C.c_void_p(dptr), self.sizes[name]))
+
+    def wait(self, i):
+        """Block until batch i's results are in its slot's host buffers (with later batches of
+        the same slot submitted, this also waits for their downloads)."""
+        if self.pending_dl is not None and self.pending_dl <= i:
+            self._flush_download()
+        if i in self.inflight:
+            self._chk(lib().coeb_copyq_synchronize(self.down[i % 2]))
+            self.inflight = [j for j in self.inflight if j % 2 != i % 2 or j > i]
+        return self.out[i % 2]
+
+    def results(self, i):
+        """Per-frame (keypoints, descriptors), matches and nmatches of batch i (after wait(i))."""
+        o = self.out[i % 2]
+        counts = o["counts"].view(np.int32)
+        kps = o["kps"].view(np.uint8).view(KEYPOINT_DTYPE).reshape(self.F, self.kcap)
+        desc = o["desc"].view(np.uint8).reshape(self.F, self.kcap, 32)
+        mm = o["match"].view(np.int32).reshape(self.F, self.kcap)
+        nm = o["nmatch"].view(np.int32)
+        out = [(kps[f, :counts[f]].copy(), desc[f, :counts[f]].copy()) for f in range(self.F)]
+        return out, [None] + [mm[f, :counts[f]].copy() for f in range(1, self.F)], [None] + [int(x) for x in nm[1:]]
+
+    def close(self):
+        L = lib()
+        for q in set([self.up] + self.down):
+            if q:
+                L.coeb_copyq_destroy(q)
+        self.up, self.down = None, []
+        for sl in self.slots:
+            sl.synchronize()
+            sl.close()
+        for o in self.out:
+            for b in o.values():
+                b.free()

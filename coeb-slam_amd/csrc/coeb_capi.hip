@@ -1008,55 +1008,62 @@ int coeb_match_lastframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curfram
     *nmatches = 0;
     if (cur->n < 0 || last->n < 0) return set_err(c, COEB_EINVAL, "negative frame size");
     if (cur->n > kCurMax) return set_err(c, COEB_EINVAL, "more than 4095 current keypoints");
-    (void)hipSetDevice(c->device);
     const int n = cur->n, nl = last->n;
+    if (n && (!cur->keys_un || !cur->descriptors || !cur->u_right))
+        return set_err(c, COEB_EINVAL, "coeb_match_lastframe: missing current-frame arrays");
+    if (nl && (!last->has_mappoint || !last->outlier || !last->world_pos || !last->mp_descriptor ||
+               !last->mp_observations || !last->keys_un))
+        return set_err(c, COEB_EINVAL, "coeb_match_lastframe: missing LastFrame arrays");
+    // the kernel indexes mvScaleFactors[octave] of every LastFrame point with a MapPoint
+    for (int i = 0; i < nl; i++)
+        if (last->has_mappoint[i] && (last->keys_un[i].octave < 0 || last->keys_un[i].octave >= c->params.nlevels))
+            return set_err(c, COEB_EINVAL, "coeb_match_lastframe: LastFrame keypoint octave outside the pyramid");
+    (void)hipSetDevice(c->device);
     const int cs = std::max(n, 1), ls = std::max(nl, 1);
     int rc;
-    coeb_keypoint *dck, *dlk;
-    uint8_t *dcd, *dld, *dhas, *dout;
-    float *dur, *dxw, *dT;
-    int32_t *dcn, *dnobs, *dmatch, *dnm, *dscr, *derr;
-    if ((rc = ensure(c, "m_ck", cs, &dck)) || (rc = ensure(c, "m_lk", ls, &dlk)) || (rc = ensure(c, "m_cd", (size_t)cs * 32, &dcd)) ||
-        (rc = ensure(c, "m_ld", (size_t)ls * 32, &dld)) || (rc = ensure(c, "m_has", ls, &dhas)) ||
-        (rc = ensure(c, "m_out", ls, &dout)) || (rc = ensure(c, "m_ur", cs, &dur)) ||
-        (rc = ensure(c, "m_xw", (size_t)ls * 3, &dxw)) || (rc = ensure(c, "m_T", 32, &dT)) ||
-        (rc = ensure(c, "m_cn", 2, &dcn)) || (rc = ensure(c, "m_nobs", ls, &dnobs)) ||
-        (rc = ensure(c, "m_match", cs, &dmatch)) || (rc = ensure(c, "m_nm", 1, &dnm)) ||
-        (rc = ensure(c, "m_scr", (size_t)ls * kMatchCQ, &dscr)) || (rc = ensure(c, "err", 4, &derr)))
+    int32_t *dout, *dscr, *derr;
+    uint8_t* dbase;
+    if ((rc = ensure(c, "m_out2", (size_t)cs + 1, &dout)) || (rc = ensure(c, "m_scr", (size_t)ls * kMatchCQ, &dscr)) ||
+        (rc = ensure(c, "err", 4, &derr)))
         return rc;
     hipStream_t s = main_stream(c);
-    int32_t cnts[2] = {n, nl};
-    HIP_TRY(c, hipMemcpyAsync(dcn, cnts, 8, hipMemcpyHostToDevice, s));
-    if (n) {
-        HIP_TRY(c, hipMemcpyAsync(dck, cur->keys_un, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dcd, cur->descriptors, (size_t)n * 32, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dur, cur->u_right, (size_t)n * 4, hipMemcpyHostToDevice, s));
-    }
-    if (nl) {
-        HIP_TRY(c, hipMemcpyAsync(dlk, last->keys_un, (size_t)nl * sizeof(coeb_keypoint), hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dld, last->mp_descriptor, (size_t)nl * 32, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dhas, last->has_mappoint, (size_t)nl, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dout, last->outlier, (size_t)nl, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dxw, last->world_pos, (size_t)nl * 12, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(dnobs, last->mp_observations, (size_t)nl * 4, hipMemcpyHostToDevice, s));
-    }
-    HIP_TRY(c, hipMemcpyAsync(dT, Tcw_cur, 64, hipMemcpyHostToDevice, s));
-    HIP_TRY(c, hipMemcpyAsync(dT + 16, Tcw_last, 64, hipMemcpyHostToDevice, s));
+    // every input in one pinned staged copy (ten small pageable copies cost more than the kernel)
+    const int32_t cnts[2] = {n, nl};
+    Pack pk;
+    const size_t o_cn = pk.add(cnts, 8), o_T = pk.add(Tcw_cur, 64), o_Tl = pk.add(Tcw_last, 64);
+    const size_t o_ck = pk.add(cur->keys_un, (size_t)n * sizeof(coeb_keypoint)), o_cd = pk.add(cur->descriptors, (size_t)n * 32);
+    const size_t o_ur = pk.add(cur->u_right, (size_t)n * 4);
+    const size_t o_lk = pk.add(last->keys_un, (size_t)nl * sizeof(coeb_keypoint));
+    const size_t o_ld = pk.add(last->mp_descriptor, (size_t)nl * 32), o_h = pk.add(last->has_mappoint, (size_t)nl);
+    const size_t o_o = pk.add(last->outlier, (size_t)nl), o_xw = pk.add(last->world_pos, (size_t)nl * 12);
+    const size_t o_nb = pk.add(last->mp_observations, (size_t)nl * 4);
+    if ((rc = stage_in(c, pk, &dbase, s))) return rc;
     MatchBufs mb;
     memset(&mb, 0, sizeof(mb));
-    mb.cur_kps = dck; mb.cur_desc = dcd; mb.cur_n = dcn; mb.cur_ur = dur; mb.cur_stride = cs;
-    mb.last_kps = dlk; mb.last_desc = dld; mb.last_n = dcn + 1; mb.last_has = dhas; mb.last_out = dout;
-    mb.last_xw = dxw; mb.last_nobs = dnobs; mb.last_stride = ls;
-    mb.Tcw_cur = dT; mb.Tcw_last = dT + 16;
-    mb.match = dmatch; mb.nmatch = dnm; mb.scratch = dscr; mb.scratch_stride = ls * kMatchCQ; mb.err = derr;
+    mb.cur_kps = reinterpret_cast<const coeb_keypoint*>(dbase + o_ck);
+    mb.cur_desc = dbase + o_cd;
+    mb.cur_n = reinterpret_cast<const int32_t*>(dbase + o_cn);
+    mb.cur_ur = reinterpret_cast<const float*>(dbase + o_ur);
+    mb.cur_stride = cs;
+    mb.last_kps = reinterpret_cast<const coeb_keypoint*>(dbase + o_lk);
+    mb.last_desc = dbase + o_ld;
+    mb.last_n = reinterpret_cast<const int32_t*>(dbase + o_cn) + 1;
+    mb.last_has = dbase + o_h;
+    mb.last_out = dbase + o_o;
+    mb.last_xw = reinterpret_cast<const float*>(dbase + o_xw);
+    mb.last_nobs = reinterpret_cast<const int32_t*>(dbase + o_nb);
+    mb.last_stride = ls;
+    mb.Tcw_cur = reinterpret_cast<const float*>(dbase + o_T);
+    mb.Tcw_last = reinterpret_cast<const float*>(dbase + o_Tl);
+    mb.match = dout; mb.nmatch = dout + cs; mb.scratch = dscr; mb.scratch_stride = ls * kMatchCQ; mb.err = derr;
     if (launch_match(make_cam(c, cam), mb, 1, th, bmono, check_ori, 0, s, &c->hook))
         return hip_err(c, hipGetLastError(), "launch_match");
-    int nm = 0;
-    HIP_TRY(c, hipMemcpyAsync(&nm, dnm, 4, hipMemcpyDeviceToHost, s));
-    if (n && match_out) HIP_TRY(c, hipMemcpyAsync(match_out, dmatch, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    int32_t* hout = reinterpret_cast<int32_t*>(c->pin);          // one copy back: match[cs], nmatch
+    HIP_TRY(c, hipMemcpyAsync(hout, dout, ((size_t)cs + 1) * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
     if ((rc = check_err_word(c))) return rc;
-    *nmatches = nm;
+    if (n && match_out) memcpy(match_out, hout, (size_t)n * 4);
+    *nmatches = hout[cs];
     return COEB_OK;
 }
 
@@ -1524,6 +1531,127 @@ int coeb_memcpy_d2h(coeb_ctx* c, void* dst, const void* src, size_t bytes)
     join_pose(c);
     HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, main_stream(c)));
     HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
+    return COEB_OK;
+}
+
+int coeb_host_alloc(size_t bytes, void** ptr)
+{
+    if (!ptr) return COEB_EINVAL;
+    hipError_t e = hipHostMalloc(ptr, std::max<size_t>(bytes, 1), hipHostMallocDefault);
+    if (e != hipSuccess) return set_err(nullptr, COEB_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    return COEB_OK;
+}
+
+int coeb_host_free(void* ptr)
+{
+    if (ptr && hipHostFree(ptr) != hipSuccess) return set_err(nullptr, COEB_EDEVICE, "hipHostFree failed");
+    return COEB_OK;
+}
+
+int coeb_memcpy_h2d_async(coeb_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c || (bytes && (!dst || !src))) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, main_stream(c)));
+    return COEB_OK;
+}
+
+int coeb_memcpy_d2h_async(coeb_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c || (bytes && (!dst || !src))) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    join_pose(c);
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, main_stream(c)));
+    return COEB_OK;
+}
+
+// ---- copy queues: a stream of their own beside a context's stream (coeb_front.h) ----
+// Each ordering call records a fresh event of a small ring: re-recording one event object while
+// another stream still waits on its earlier record measured as a false dependency.
+constexpr int kCopyqEvents = 16;
+struct coeb_copyq {
+    int device = 0;
+    hipStream_t s = nullptr;
+    hipEvent_t ev[kCopyqEvents] = {};
+    int next = 0;
+    hipEvent_t take() { hipEvent_t e = ev[next]; next = (next + 1) % kCopyqEvents; return e; }
+};
+
+coeb_copyq* coeb_copyq_create(coeb_ctx* c)
+{
+    if (!c) return nullptr;
+    (void)hipSetDevice(c->device);
+    coeb_copyq* q = new coeb_copyq;
+    q->device = c->device;
+    bool ok = hipStreamCreateWithFlags(&q->s, hipStreamNonBlocking) == hipSuccess;
+    for (int i = 0; ok && i < kCopyqEvents; i++) ok = hipEventCreateWithFlags(&q->ev[i], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        set_err(c, COEB_EDEVICE, "coeb_copyq_create: stream / event creation failed");
+        for (hipEvent_t e : q->ev)
+            if (e) (void)hipEventDestroy(e);
+        if (q->s) (void)hipStreamDestroy(q->s);
+        delete q;
+        return nullptr;
+    }
+    return q;
+}
+
+int coeb_copyq_destroy(coeb_copyq* q)
+{
+    if (!q) return COEB_OK;
+    (void)hipSetDevice(q->device);
+    (void)hipStreamSynchronize(q->s);
+    for (hipEvent_t e : q->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(q->s);
+    delete q;
+    return COEB_OK;
+}
+
+int coeb_copyq_h2d(coeb_copyq* q, void* dst, const void* src, size_t bytes)
+{
+    if (!q || (bytes && (!dst || !src))) return COEB_EINVAL;
+    (void)hipSetDevice(q->device);
+    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, q->s) != hipSuccess)
+        return set_err(nullptr, COEB_EDEVICE, "coeb_copyq_h2d: hipMemcpyAsync failed");
+    return COEB_OK;
+}
+
+int coeb_copyq_d2h(coeb_copyq* q, void* dst, const void* src, size_t bytes)
+{
+    if (!q || (bytes && (!dst || !src))) return COEB_EINVAL;
+    (void)hipSetDevice(q->device);
+    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, q->s) != hipSuccess)
+        return set_err(nullptr, COEB_EDEVICE, "coeb_copyq_d2h: hipMemcpyAsync failed");
+    return COEB_OK;
+}
+
+int coeb_copyq_after_ctx(coeb_copyq* q, coeb_ctx* c)
+{
+    if (!q || !c || q->device != c->device) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    hipStream_t s = main_stream(c);
+    join_pose(c);
+    hipEvent_t e = q->take();
+    HIP_TRY(c, hipEventRecord(e, s));
+    HIP_TRY(c, hipStreamWaitEvent(q->s, e, 0));
+    return COEB_OK;
+}
+
+int coeb_ctx_after_copyq(coeb_ctx* c, coeb_copyq* q)
+{
+    if (!q || !c || q->device != c->device) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    hipEvent_t e = q->take();
+    HIP_TRY(c, hipEventRecord(e, q->s));
+    HIP_TRY(c, hipStreamWaitEvent(main_stream(c), e, 0));
+    return COEB_OK;
+}
+
+int coeb_copyq_synchronize(coeb_copyq* q)
+{
+    if (!q) return COEB_EINVAL;
+    (void)hipSetDevice(q->device);
+    if (hipStreamSynchronize(q->s) != hipSuccess) return set_err(nullptr, COEB_EDEVICE, "coeb_copyq_synchronize failed");
     return COEB_OK;
 }
 

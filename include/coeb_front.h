@@ -347,6 +347,30 @@ int coeb_device_alloc(coeb_ctx* ctx, size_t bytes, void** dptr);
 int coeb_device_free(coeb_ctx* ctx, void* dptr);
 int coeb_memcpy_h2d(coeb_ctx* ctx, void* dst, const void* src, size_t bytes);
 int coeb_memcpy_d2h(coeb_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* Host-resident batches with copy / kernel overlap: page-locked host memory, and copies
+ * enqueued on the context stream behind the work already there (returning at once; the data
+ * is in place after coeb_synchronize).  From page-locked memory the copies run on the DMA
+ * engines beside the kernels of other contexts' streams. */
+int coeb_host_alloc(size_t bytes, void** ptr);
+int coeb_host_free(void* ptr);
+int coeb_memcpy_h2d_async(coeb_ctx* ctx, void* dst, const void* src, size_t bytes);
+int coeb_memcpy_d2h_async(coeb_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* Copy queues: a HIP stream of their own on a context's device, for pipelines whose uploads
+ * must run back to back (one upload queue for all batches: concurrent uploads only split the
+ * PCIe bandwidth) while earlier batches compute on the contexts' streams.  Copies are
+ * asynchronous (page-locked host memory); ordering against a context is explicit:
+ *   coeb_copyq_after_ctx(q, ctx)  work enqueued on q from now on waits for everything enqueued
+ *                                 on ctx so far (e.g. the kernels reading the buffer to refill);
+ *   coeb_ctx_after_copyq(ctx, q)  work enqueued on ctx from now on waits for everything
+ *                                 enqueued on q so far (e.g. the upload of the next batch). */
+typedef struct coeb_copyq coeb_copyq;
+coeb_copyq* coeb_copyq_create(coeb_ctx* ctx);
+int coeb_copyq_destroy(coeb_copyq* q);
+int coeb_copyq_h2d(coeb_copyq* q, void* dst, const void* src, size_t bytes);
+int coeb_copyq_d2h(coeb_copyq* q, void* dst, const void* src, size_t bytes);
+int coeb_copyq_after_ctx(coeb_copyq* q, coeb_ctx* ctx);
+int coeb_ctx_after_copyq(coeb_ctx* ctx, coeb_copyq* q);
+int coeb_copyq_synchronize(coeb_copyq* q);
 
 /* ---- measurement ---- */
 /* Per-kernel device time accumulated with HIP events on the context stream while profiling

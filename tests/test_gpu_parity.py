@@ -550,6 +550,59 @@ def test_sharded_batch_equals_unsharded():
     assert covered == list(range(1, G + 1))
 
 
+def test_host_stream_overlapped_equals_device_batch():
+    """The PCIe-inclusive pipeline (HostStream: page-locked host frames in, host results out, two
+    slots whose copies overlap each other's kernels) returns per-frame keypoints, descriptors and
+    matches bit-identical to the device-resident batch, for several batches in flight."""
+    from coeb_front import HostBuffer
+    from coeb_front.pipeline import BatchPipeline, HostStream
+    F = 9
+    seqs = [synth.make_frames(640, 480, F, seed=s) for s in (11, 12, 13)]
+    Tcw = np.stack([synth.motion_pose()] * F)
+    ref = []
+    bp = BatchPipeline(640, 480, F)
+    try:
+        for fr in seqs:
+            bp.load(fr, Tcw=Tcw)
+            bp.run()
+            bp.synchronize()
+            ref.append(bp.results())
+    finally:
+        bp.close()
+    hs = HostStream(640, 480, F, Tcw=Tcw)
+    bufs = [HostBuffer(F * 480 * 640) for _ in seqs]
+    try:
+        for b, fr in zip(bufs, seqs):
+            b.view(np.uint8, (F, 480, 640))[:] = fr
+        got = []
+        for i in range(4):                      # batches 0,1,2,0 with two in flight
+            hs.submit(i, bufs[i % 3])
+            if i:
+                hs.wait(i - 1)
+                got.append(hs.results(i - 1))
+        hs.wait(3)
+        got.append(hs.results(3))
+        # submit-only loop (device-side ordering): the last two results
+        for i in range(4, 9):
+            hs.submit(i, bufs[i % 3])
+        hs.wait(7)
+        last7 = hs.results(7)
+        hs.wait(8)
+        got += [last7, hs.results(8)]
+        for j, (out, m, n) in enumerate(got):
+            i = j if j < 4 else j + 3             # batch index (7, 8 for the last two)
+            r_out, r_m, r_n = ref[i % 3]
+            assert n == r_n, i
+            for f in range(F):
+                assert np.array_equal(out[f][0], r_out[f][0]) and np.array_equal(out[f][1], r_out[f][1]), (i, f)
+                if f:
+                    assert np.array_equal(m[f], r_m[f]), (i, f)
+    finally:
+        hs.close()
+        for b in bufs:
+            b.free()
+
+
 # ------------------------------------------------------------------ local-map projection search
 def localmap_both(ctx, oracle_mod, ex, cur_k, cur_d, cur_ur, cur_obs, mp, th=3.0, nnratio=0.8):
     """coeb_match_localmap vs oracle.search_local_map (ORBmatcher.cc:44-129), bit-exact."""
