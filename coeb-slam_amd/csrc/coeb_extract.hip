@@ -172,9 +172,27 @@ __device__ __forceinline__ uint32_t vresize_g(uint32_t g0, uint32_t g1, uint32_t
 // store per output row).
 constexpr int PT_W = 128, PT_H = 32, PT_SW = 288, PT_SH = 72;   // LDS source tile (scale <= 2)
 
+// First column of VResizeLinear's scalar tail for a row of w outputs (oracle oc_resize_simd_end):
+// the SSE2 loops run 16 columns while x <= w - 16, then 4 while x < w - 4.
+int resize_simd_end(int w)
+{
+    int x = w >= 16 ? (w / 16) * 16 : 0;
+    while (x < w - 4) x += 4;
+    return x;
+}
+
+// Columns >= xs (VResizeLinear's scalar tail on x86-64: the SIMD loops stop at xs, DESIGN.md
+// s2.1) round exactly: (h0*b0 + h1*b1 + 2^21) >> 22 (FixedPtCast<int, uchar, 22>).
+__device__ __forceinline__ uint32_t vresize_exact(uint32_t g0, uint32_t g1, uint32_t b0s, uint32_t b1s)
+{
+    const uint32_t v = (g0 >> 4) * (b0s >> 8) + (g1 >> 4) * (b1s >> 8) + (1u << 21);   // < 2^31
+    return min(v >> 22, 255u);
+}
+
 __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
                                                         int sw, int sh, uint8_t* __restrict__ dst, int64_t dst_fs,
-                                                        int dp, int dw, int dh, const int* __restrict__ tab, int xmax)
+                                                        int dp, int dw, int dh, const int* __restrict__ tab, int xmax,
+                                                        int xs)
 {
     __shared__ __attribute__((aligned(16))) uint8_t s_src[PT_SH * PT_SW];
     const int f = blockIdx.z;
@@ -255,7 +273,9 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
         for (int k = 0; k < 4; k++) {
             const int g0 = __mul24((int)R0[lx[k]], a0[k]) + __mul24((int)R0[lx[k] + 1], a1[k]);
             const int g1 = __mul24((int)R1[lx[k]], a0[k]) + __mul24((int)R1[lx[k] + 1], a1[k]);
-            word |= vresize_g((uint32_t)g0, (uint32_t)g1, b0s, b1s) << (8 * k);
+            const uint32_t v = cx + k < xs ? vresize_g((uint32_t)g0, (uint32_t)g1, b0s, b1s)
+                                           : vresize_exact((uint32_t)g0, (uint32_t)g1, b0s, b1s);
+            word |= v << (8 * k);
         }
         uint8_t* D = dst + (int64_t)f * dst_fs + (int64_t)dy * dp + cx;
         if (nk == 4 && (dp & 3) == 0) *reinterpret_cast<uint32_t*>(D) = word;
@@ -2339,7 +2359,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         prof_begin(prof, "k_pyr_level", s);
         hipLaunchKernelGGL(k_pyr_level, dim3((g.w + PT_W - 1) / PT_W, (g.h + PT_H - 1) / PT_H, F), dim3(kThreads), 0, s, src, src_fs,
                            gp.pitch, gp.w, gp.h, b.pyr + g.pyr_off, plan.pyr_stride, g.pitch, g.w, g.h,
-                           b.rtab + g.rtab_off, g.xmax);
+                           b.rtab + g.rtab_off, g.xmax, resize_simd_end(g.w));
         prof_end(prof, s);
         if (split && m > 1 && l == m - 1) {
             (void)hipEventRecord(side->mid, s);

@@ -92,9 +92,20 @@ void oc_level_size(const oc_params* p, int w, int h, int level, int* lw, int* lh
 
 /* ============ cv::resize INTER_LINEAR, CV_8U (imgproc resize.cpp, OpenCV 3.4) ============
  * Coefficients: 11-bit fixed point, computed exactly as resize()'s table setup.
- * Horizontal pass: exact int (HResizeLinear).  Vertical pass: the SIMD rounding
- * (VResizeLinearVec_32s8u: ((S0>>4)*b0>>16) + ((S1>>4)*b1>>16), +2 >> 2), applied to
- * every column -- canonical definition, DESIGN.md s3.1. */
+ * Horizontal pass: exact int (HResizeLinear).  Vertical pass as VResizeLinear::operator() runs
+ * it on x86-64 (SSE2 always present): VResizeLinearVec_32s8u takes 16 columns at a time while
+ * x <= width - 16, then 4 at a time while x < width - 4, with the SIMD rounding
+ * ((S0>>4)*b0>>16) + ((S1>>4)*b1>>16), +2 >> 2 (_mm_mulhi_epi16 / _mm_adds_epi16); the columns
+ * left over use the scalar FixedPtCast<int, uchar, 22>: (S0*b0 + S1*b1 + 2^21) >> 22.  This is
+ * the OpenCV 3.4.0/3.4.1 SSE2 loop structure; the reference's minor version is unknown
+ * (DESIGN.md s2.1). */
+int oc_resize_simd_end(int width)
+{
+    int x = width >= 16 ? (width / 16) * 16 : 0;      /* for (; x <= width - 16; x += 16) */
+    while (x < width - 4) x += 4;                     /* for (; x < width - 4; x += 4) */
+    return x;
+}
+
 void oc_resize_linear(const uint8_t* src, int sw, int sh, int sstride,
                       uint8_t* dst, int dw, int dh, int dstride)
 {
@@ -153,13 +164,16 @@ void oc_resize_linear(const uint8_t* src, int sw, int sh, int sstride,
         }
         int b0 = ibeta[2 * dy], b1 = ibeta[2 * dy + 1];
         uint8_t* D = dst + (size_t)dy * dstride;
-        for (int dx = 0; dx < dw; dx++) {
+        const int xs = oc_resize_simd_end(dw);
+        for (int dx = 0; dx < xs; dx++) {
             int v0 = sat_short(h0[dx] >> 4), v1 = sat_short(h1[dx] >> 4);
             int m0 = (v0 * b0) >> 16, m1 = (v1 * b1) >> 16;   /* _mm_mulhi_epi16 */
             int s = sat_short(m0 + m1);                         /* _mm_adds_epi16 */
             s = sat_short(s + 2) >> 2;
             D[dx] = sat_u8(s);
         }
+        for (int dx = xs; dx < dw; dx++)                        /* scalar tail: FixedPtCast */
+            D[dx] = sat_u8((h0[dx] * b0 + h1[dx] * b1 + (1 << 21)) >> 22);
     }
     free(h0); free(h1); free(xofs); free(ialpha); free(yofs); free(ibeta);
 }

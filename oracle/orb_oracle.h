@@ -47,6 +47,8 @@ int oc_init(oc_params* p, int nfeatures, float scale_factor, int nlevels, int in
 void oc_level_size(const oc_params* p, int w, int h, int level, int* lw, int* lh);
 
 /* cv::resize INTER_LINEAR 8U (canonical) used by ComputePyramid :1356 */
+/* first column of VResizeLinear's scalar tail for a row of `width` outputs (OpenCV 3.4 SSE2) */
+int oc_resize_simd_end(int width);
 void oc_resize_linear(const uint8_t* src, int sw, int sh, int sstride,
                       uint8_t* dst, int dw, int dh, int dstride);
 /* ComputePyramid (src/ORBextractor.cc:1344-1367); levels packed, level l stride = lw */

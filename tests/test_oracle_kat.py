@@ -553,3 +553,83 @@ def test_grab_image_rgbd_conversions_kat(oracle_mod):
     d32 = np.array([[np.nan, -0.0, 1.5, 3e38]], np.float32)
     assert np.array_equal(oracle_mod.depth_to_float(d32, 1.0).view(np.uint32), d32.view(np.uint32))
     assert np.array_equal(oracle_mod.depth_to_float(d32, 2.0)[0, 2:], np.float32([3.0, np.inf]))
+
+
+@pytest.mark.timeout(300)
+def test_oracle_clean_under_asan_ubsan():
+    """The oracle built with AddressSanitizer + UndefinedBehaviorSanitizer (no recovery) runs every
+    public entry point on synthetic frames without a finding (`make -C oracle asan`, kat_main.c)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle"), "asan"], capture_output=True, text=True,
+                       timeout=280)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "kat_main: clean" in r.stdout
+
+
+def _py_resize_linear(src, dw, dh):
+    """numpy restatement of OpenCV 3.4 resize INTER_LINEAR 8U on x86-64 (imgproc resize.cpp):
+    11-bit coefficient tables, exact horizontal pass, vertical pass with the SSE2 rounding of
+    VResizeLinearVec_32s8u up to its last column and FixedPtCast<int,uchar,22> after it."""
+    sh, sw = src.shape
+    sx_scale, sy_scale = 1.0 / (dw / sw), 1.0 / (dh / sh)
+
+    def tab(n, scale, limit):
+        ofs, c0, c1, xmax = [], [], [], n
+        for d in range(n):
+            f = np.float32((d + 0.5) * scale - 0.5)
+            s = int(np.floor(f))
+            f = np.float32(f - np.float32(s))
+            if limit:
+                if s < 0:
+                    f, s = np.float32(0), 0
+                if s + 1 >= sw:
+                    xmax = min(xmax, d)
+                    if s >= sw - 1:
+                        f, s = np.float32(0), sw - 1
+            ofs.append(s)
+            c0.append(int(np.rint(np.float32(np.float32(1) - f) * np.float32(2048))))     # cvRound, half even
+            c1.append(int(np.rint(np.float32(f) * np.float32(2048))))
+        return np.array(ofs), np.array(c0), np.array(c1), xmax
+    xofs, a0, a1, xmax = tab(dw, sx_scale, True)
+    yofs, b0, b1, _ = tab(dh, sy_scale, False)
+    x = (dw // 16) * 16 if dw >= 16 else 0
+    while x < dw - 4:
+        x += 4
+    out = np.zeros((dh, dw), np.uint8)
+    s = src.astype(np.int64)
+    for dy in range(dh):
+        r0 = min(max(yofs[dy], 0), sh - 1)
+        r1 = min(max(yofs[dy] + 1, 0), sh - 1)
+        h = []
+        for r in (r0, r1):
+            row = s[r]
+            hx = np.where(np.arange(dw) < xmax, row[xofs] * a0 + row[np.minimum(xofs + 1, sw - 1)] * a1, row[xofs] * 2048)
+            h.append(hx)
+        simd = (((h[0] >> 4) * b0[dy]) >> 16) + (((h[1] >> 4) * b1[dy]) >> 16)
+        simd = (simd + 2) >> 2
+        exact = (h[0] * b0[dy] + h[1] * b1[dy] + (1 << 21)) >> 22
+        v = np.where(np.arange(dw) < x, simd, exact)
+        out[dy] = np.clip(v, 0, 255)
+    return out
+
+
+def test_resize_linear_simd_prefix_scalar_tail(oracle_mod):
+    """The oracle's resize matches the numpy restatement on every ORB level size of configs A and
+    B, including the columns after the SSE2 loops (1 to 4 per row: 533 -> 1, 444 -> 4, ...)."""
+    import ctypes as C
+    rng = np.random.default_rng(5)
+    src = rng.integers(0, 256, (480, 640), dtype=np.uint8)
+    for dw, dh in ((533, 400), (444, 333), (370, 278), (309, 231), (179, 134), (641 // 2, 479 // 2)):
+        ref = _py_resize_linear(src, dw, dh)
+        out = np.zeros((dh, dw), np.uint8)
+        oracle_mod.lib().oc_resize_linear(src.ctypes.data_as(C.c_void_p), 640, 480, 640, out.ctypes.data_as(C.c_void_p),
+                                          dw, dh, dw)
+        assert np.array_equal(out, ref), (dw, dh)
+        tail = oracle_mod.lib().oc_resize_simd_end(dw)
+        assert dw - 4 <= tail <= dw
+    # the scalar tail rounds differently from the SIMD form on some inputs
+    assert any(oracle_mod.lib().oc_resize_simd_end(w) < w for w in (533, 444, 370, 309))
