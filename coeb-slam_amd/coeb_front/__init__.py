@@ -51,7 +51,7 @@ ABI_SYMBOLS = [
     "coeb_pose_batch_device", "coeb_batch_pose_results",
     "coeb_host_alloc", "coeb_host_free", "coeb_memcpy_h2d_async", "coeb_memcpy_d2h_async",
     "coeb_copyq_create", "coeb_copyq_destroy", "coeb_copyq_h2d", "coeb_copyq_d2h", "coeb_copyq_after_ctx",
-    "coeb_ctx_after_copyq", "coeb_copyq_synchronize",
+    "coeb_ctx_after_copyq", "coeb_copyq_synchronize", "coeb_frame_batch_device", "coeb_batch_frame_results",
 ]
 
 
@@ -123,6 +123,10 @@ def lib():
                                    C.POINTER(C.c_int)]
         L.coeb_extract_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.coeb_frame_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                              C.c_void_p]
+        L.coeb_batch_frame_results.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                               C.POINTER(C.c_int), C.POINTER(C.c_void_p)]
         L.coeb_batch_results.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                          C.POINTER(C.c_void_p), C.POINTER(C.c_int)]
         L.coeb_match_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(Camera),
@@ -273,6 +277,24 @@ class Context:
                 keep.append(a)
                 args.append(_p(a))
         self.check(lib().coeb_extract_batch_device(self.h, C.c_void_p(d_gray_ptr), nframes, w, h, *args))
+
+    def frame_batch_device(self, d_gray_ptr, nframes, w, h, boxes=None, box_off=None):
+        """The RGB-D Frame constructor on the batch (coeb_frame_batch_device): T_M from the previous
+        frame, box blur flags and the masked extraction, all on the device."""
+        b = None if boxes is None else np.ascontiguousarray(boxes, np.float32)
+        o = None if box_off is None else np.ascontiguousarray(box_off, np.int32)
+        self.check(lib().coeb_frame_batch_device(self.h, C.c_void_p(d_gray_ptr), nframes, w, h, _p(b), _p(o)))
+
+    def batch_frame_results(self, nframes, nbox=0):
+        """Host copies of the last frame batch's T_M (list of (n, 2) arrays, None where F was
+        empty) and blur flags (nbox,)."""
+        tm, ntm, cap, blur = C.c_void_p(), C.c_void_p(), C.c_int(), C.c_void_p()
+        self.check(lib().coeb_batch_frame_results(self.h, C.byref(tm), C.byref(ntm), C.byref(cap), C.byref(blur)))
+        n = self.download(ntm.value, 4 * nframes, np.int32)
+        pts = self.download(tm.value, 8 * cap.value * nframes, np.float32).reshape(nframes, cap.value, 2)
+        tms = [None if n[f] < 0 else pts[f, :n[f]].copy() for f in range(nframes)]
+        flags = self.download(blur.value, 4 * nbox, np.int32) if nbox and blur.value else np.zeros(0, np.int32)
+        return tms, flags
 
     def batch_results(self):
         k, d, n = C.c_void_p(), C.c_void_p(), C.c_void_p()

@@ -25,6 +25,7 @@ class BatchPipeline:
         self.Tcw = np.stack([np.eye(4, dtype=np.float32)] * nframes)
         self.dyn = None
         self.host_frames = None
+        self.frame_boxes = None      # (boxes, box_off) for run(frame=True)
 
     def load(self, frames, depth=None, Tcw=None, dyn=None):
         """frames: (F, H, W) uint8; depth: (F, H, W) float32; Tcw: (F, 4, 4) pose of frame f
@@ -57,10 +58,16 @@ class BatchPipeline:
                         np.asarray(tm_off, np.int32), np.concatenate(blurs))
         self.ctx.synchronize()
 
-    def run(self, match=True, th=15.0, nobs=2, pose=False):
+    def run(self, match=True, th=15.0, nobs=2, pose=False, frame=False):
         """Enqueue one step (extraction of F frames + F-1 matches, and with pose=True the
-        motion-model PoseOptimization of every matched frame); does not synchronise."""
-        if self.dyn is not None:
+        motion-model PoseOptimization of every matched frame); does not synchronise.  frame=True
+        runs the whole RGB-D Frame constructor instead of the extraction alone: T_M from the
+        previous frame (ProcessMovingObject), blur flags of the boxes set by set_frame_boxes(),
+        masked extraction (coeb_frame_batch_device)."""
+        if frame:
+            b, o = self.frame_boxes if self.frame_boxes is not None else (None, None)
+            self.ctx.frame_batch_device(self.gray.ptr, self.F, self.W, self.H, b, o)
+        elif self.dyn is not None:
             b, bo, t, to, bl = self.dyn
             self.ctx.extract_batch_device(self.gray.ptr, self.F, self.W, self.H, b, bo, t, to, bl)
         else:
@@ -69,6 +76,14 @@ class BatchPipeline:
             self.ctx.match_batch_device_tcw(self.depth.ptr, self.F, self.W, self.H, self.cam, self.dTcw.ptr, th, nobs)
             if pose:
                 self.ctx.pose_batch_device(self.cam, self.F, self.dTcw.ptr)
+
+    def set_frame_boxes(self, boxes_per_frame):
+        """YOLO boxes of every frame (list of (n_f, 4) xyxy) for run(frame=True)."""
+        bl = [np.zeros((0, 4), np.float32) if b is None else np.asarray(b, np.float32).reshape(-1, 4)
+              for b in boxes_per_frame]
+        off = np.zeros(len(bl) + 1, np.int32)
+        off[1:] = np.cumsum([len(b) for b in bl])
+        self.frame_boxes = (np.concatenate(bl) if off[-1] else np.zeros((0, 4), np.float32), off)
 
     def synchronize(self):
         self.ctx.synchronize()

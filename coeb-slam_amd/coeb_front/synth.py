@@ -248,6 +248,15 @@ def moving_object_pair(w, h, seed=0, n_small=600, obj=(200, 120, 160, 200), obj_
     three nearer textured panels by 2x and 3x SHIFT, and an object rectangle obj = (x, y, w, h)
     moves by obj_shift, off the epipolar direction.  Returns (prev, cur, object box
     (xmin, ymin, xmax, ymax) in cur)."""
+    frames, boxes = moving_object_sequence(w, h, 2, seed, n_small, obj, obj_shift, noise)
+    return frames[0], frames[1], boxes[1]
+
+
+def moving_object_sequence(w, h, n, seed=0, n_small=600, obj=(200, 120, 160, 200), obj_shift=(-5, 4), noise=True):
+    """n frames of moving_object_pair's scene (frame k: background and panels k steps of the
+    camera motion on, the object k steps of obj_shift); returns (frames (n, h, w) u8, object box
+    (xmin, ymin, xmax, ymax) per frame as float32 (n, 4)).  The object must stay inside the
+    frame: n * |obj_shift| is limited by obj's margins."""
     rng = np.random.default_rng(seed + 31337)
     canvas = make_canvas(w, h, seed).astype(np.int16)
     for _ in range(n_small):
@@ -260,15 +269,19 @@ def moving_object_pair(w, h, seed=0, n_small=600, obj=(200, 120, 160, 200), obj_
         layers.append((_texture(rng, pw, ph), px, py, (m * SHIFT[0], m * SHIFT[1])))
     ox, oy, ow, oh = obj
     layers.append((_texture(rng, ow, oh), ox, oy, obj_shift))
-    frames = []
-    for k in range(2):
+    frames = np.empty((n, h, w), np.uint8)
+    boxes = np.empty((n, 4), np.float32)
+    for k in range(n):
         img = np.roll(canvas, (k * SHIFT[1], k * SHIFT[0]), axis=(0, 1)).copy()
         for tex, px, py, sh in layers:
             x, y = px + k * sh[0], py + k * sh[1]
             th, tw = tex.shape
-            img[y:y + th, x:x + tw] = tex
+            x0, y0, x1, y1 = max(x, 0), max(y, 0), min(x + tw, w), min(y + th, h)
+            if x1 > x0 and y1 > y0:
+                img[y0:y1, x0:x1] = tex[y0 - y:y1 - y, x0 - x:x1 - x]
         if noise:
             img = img + np.random.default_rng(seed * 7919 + k + 1).integers(-3, 4, size=(h, w), dtype=np.int16)
-        frames.append(np.clip(img, 0, 255).astype(np.uint8))
-    x, y = ox + obj_shift[0], oy + obj_shift[1]
-    return frames[0], frames[1], (x, y, x + ow, y + oh)
+        frames[k] = np.clip(img, 0, 255).astype(np.uint8)
+        x, y = ox + k * obj_shift[0], oy + k * obj_shift[1]
+        boxes[k] = (x, y, x + ow, y + oh)
+    return frames, boxes

@@ -26,6 +26,7 @@ namespace {
 
 enum { PATCH_SIZE = 31, HALF_PATCH_SIZE = 15, EDGE_THRESHOLD = 19 };
 constexpr int kRoiMax = 64;
+constexpr int kFrameTmCap = 1024;     // T_M points per frame kept on the device (coeb_frame_batch_device)
 constexpr int kCurMax = 4095;
 constexpr int kMatchCQ = 64;   // candidate list entries per LastFrame point (coeb_match.hip kCQ)
 
@@ -916,6 +917,74 @@ int coeb_extract_batch_device(coeb_ctx* c, const uint8_t* d_gray, int F, int W, 
     }
     c->batch_frames = F;
     c->batch_gray = d_gray;
+    return COEB_OK;
+}
+
+extern "C" int coeb_internal_pmo_batch(coeb_ctx* c, const uint8_t* d_gray, int F, int w, int h, float* tm_out,
+                                       int* ntm_out, int tm_cap);
+extern "C" int coeb_internal_blur_flags_batch(const uint8_t* d_gray, int W, int H, const float* d_boxes,
+                                              const int* d_box_frame, int nbox, int* d_out, hipStream_t s);
+
+int coeb_frame_batch_device(coeb_ctx* c, const uint8_t* d_gray, int F, int W, int H, const coeb_box* boxes,
+                            const int32_t* box_off)
+{
+    if (!c || !d_gray || F <= 0 || (boxes && !box_off))
+        return set_err(c, COEB_EINVAL, "coeb_frame_batch_device: invalid arguments");
+    if (F > c->max_batch) return set_err(c, COEB_EINVAL, "batch larger than max_batch");
+    (void)hipSetDevice(c->device);
+    int rc;
+    if ((rc = ensure_plan(c, W, H))) return rc;
+    quiesce(c);                                  // single stream: the flow scratch and T_M are rewritten
+    hipStream_t s = main_stream(c);
+    const int nbox = boxes ? box_off[F] : 0;
+    float* tm;
+    int32_t *ntm, *bframe = nullptr, *blur = nullptr;
+    if ((rc = ensure(c, "f_tm", (size_t)F * kFrameTmCap * 2, &tm)) || (rc = ensure(c, "f_ntm", (size_t)F, &ntm)))
+        return rc;
+    // ProcessMovingObject(frame f-1, frame f) -> T_M of frame f (Frame.cc:164-166)
+    if ((rc = coeb_internal_pmo_batch(c, d_gray, F, W, H, tm, ntm, kFrameTmCap))) return rc;
+    ExtractBufs b;
+    if ((rc = extract_bufs(c, F, b))) return rc;
+    if ((rc = upload_dyn(c, F, boxes, box_off, nullptr, nullptr, nullptr, b))) return rc;
+    if (nbox > 0) {
+        // detect_laplacian blur flag of every box (Frame.cc:171-202); frame 0 = the first frame
+        std::vector<int32_t> bf((size_t)nbox);
+        for (int f = 0; f < F; f++)
+            for (int i = box_off[f]; i < box_off[f + 1]; i++) bf[(size_t)i] = f;
+        if ((rc = ensure(c, "f_bframe", (size_t)nbox, &bframe)) || (rc = ensure(c, "f_blur", (size_t)nbox, &blur)))
+            return rc;
+        Pack pk;
+        const size_t o = pk.add(bf.data(), (size_t)nbox * 4);
+        uint8_t* dbase;
+        if ((rc = stage_in(c, pk, &dbase, s))) return rc;
+        HIP_TRY(c, hipMemcpyAsync(bframe, dbase + o, (size_t)nbox * 4, hipMemcpyDeviceToDevice, s));
+        if (coeb_internal_blur_flags_batch(d_gray, W, H, b.boxes, bframe, nbox, blur, s))
+            return hip_err(c, hipGetLastError(), "blur flags");
+        b.blurf = blur;
+    }
+    b.tmd = tm;
+    b.ntmd = ntm;
+    b.tmd_cap = kFrameTmCap;
+    b.gray = d_gray;
+    c->mdone_valid = false;
+    c->extract_chunked = false;
+    c->chunk.assign(2, 0);
+    c->chunk[1] = F;
+    if (launch_extract(c->plan, static_cast<const Plan*>(c->bufs["plan"].p), b, F, s, &c->hook, side_stream(c)))
+        return hip_err(c, hipGetLastError(), "launch_extract");
+    c->batch_frames = F;
+    c->batch_gray = d_gray;
+    return COEB_OK;
+}
+
+int coeb_batch_frame_results(coeb_ctx* c, const float** d_tm, const int32_t** d_ntm, int* tm_cap,
+                             const int32_t** d_blur)
+{
+    if (!c || !c->bufs.count("f_ntm")) return set_err(c, COEB_EINVAL, "no frame batch yet");
+    if (d_tm) *d_tm = static_cast<const float*>(c->bufs["f_tm"].p);
+    if (d_ntm) *d_ntm = static_cast<const int32_t*>(c->bufs["f_ntm"].p);
+    if (tm_cap) *tm_cap = kFrameTmCap;
+    if (d_blur) *d_blur = c->bufs.count("f_blur") ? static_cast<const int32_t*>(c->bufs["f_blur"].p) : nullptr;
     return COEB_OK;
 }
 

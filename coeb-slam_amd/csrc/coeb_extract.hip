@@ -107,7 +107,13 @@ __global__ void k_dynmask(ExtractBufs b, int F, int W, int H)
     m.nrect = 0;
     float area = 0.f;
     const int b0 = b.box_off ? b.box_off[f] : 0, b1 = b.box_off ? b.box_off[f + 1] : 0;
-    const int t0 = b.tm_off ? b.tm_off[f] : 0, t1 = b.tm_off ? b.tm_off[f + 1] : 0;
+    const float* tm = b.tm;
+    int t0 = b.tm_off ? b.tm_off[f] : 0, t1 = b.tm_off ? b.tm_off[f + 1] : 0;
+    if (b.tmd) {                                  // T_M left on the device by ProcessMovingObject
+        tm = b.tmd + (int64_t)f * b.tmd_cap * 2;
+        t0 = 0;
+        t1 = min(max(b.ntmd[f], 0), b.tmd_cap);
+    }
     for (int bi = b0; bi < b1; bi++) {
         const float xmin = b.boxes[4 * bi + 0], ymin = b.boxes[4 * bi + 1];
         const float xmax = b.boxes[4 * bi + 2], ymax = b.boxes[4 * bi + 3];
@@ -116,7 +122,7 @@ __global__ void k_dynmask(ExtractBufs b, int F, int W, int H)
         bool mark = false;
         unsigned long long nin = 0;
         for (int t = t0; t < t1; t++) {
-            const int px = (int)b.tm[2 * t], py = (int)b.tm[2 * t + 1];
+            const int px = (int)tm[2 * t], py = (int)tm[2 * t + 1];
             const bool in = px >= 0 && px < W && py >= 0 && py < H && px >= rx && px < rx + rw &&
                             py >= ry && py < ry + rh;
             if (in) nin++;

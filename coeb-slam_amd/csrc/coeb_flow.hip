@@ -73,10 +73,24 @@ __device__ __forceinline__ int cv_floor(float v)
     return i - (i > v);
 }
 
+// Batched calls (coeb_moving_object_points_batch_device): blockIdx.z = frame pair.  Every
+// per-pair buffer lives in one block of `pz` bytes per pair, so a kernel reaches its pair's
+// buffers by one byte offset; pair z's frames are the batch's frames z and z + 1, `iz` bytes
+// apart.  Single calls pass iz = pz = 0 and one z-slice.
+template <class T>
+__device__ __forceinline__ T* at_pair(T* p, int64_t stride)
+{
+    return p ? reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(p) + (uint64_t)blockIdx.z * (uint64_t)stride) : p;
+}
+
 // ============================== goodFeaturesToTrack ==============================
 __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__ img, int w, int h, int stride, double k,
-                                                     float* __restrict__ R, uint32_t* __restrict__ rmax)
+                                                     float* __restrict__ R, uint32_t* __restrict__ rmax, int64_t iz,
+                                                     int64_t pz)
 {
+    img = at_pair(img, iz);
+    R = at_pair(R, pz);
+    rmax = at_pair(rmax, pz);
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
     float r = -FLT_MAX;
     if (x < w && y < h) {
@@ -117,8 +131,12 @@ __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__
 
 __global__ __launch_bounds__(256) void k_gf_candidates(const float* __restrict__ R, int w, int h, double quality,
                                                        const uint32_t* __restrict__ rmax, uint64_t* __restrict__ keys,
-                                                       int* __restrict__ nkeys, int cap)
+                                                       int* __restrict__ nkeys, int cap, int64_t pz)
 {
+    R = at_pair(R, pz);
+    rmax = at_pair(rmax, pz);
+    keys = at_pair(keys, pz);
+    nkeys = at_pair(nkeys, pz);
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x < 1 || y < 1 || x >= w - 1 || y >= h - 1) return;
     const float thr = (float)((double)ord2f(*rmax) * quality);
@@ -159,8 +177,13 @@ __device__ int block_scan_1024(int flag, int* s_w, int& excl)
 __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __restrict__ keys, const int* __restrict__ nkeys,
                                                          int w, int h, int max_corners, float md2, int cell,
                                                          uint16_t* __restrict__ cell_list, float* __restrict__ out_xy,
-                                                         int* __restrict__ nout, int cap)
+                                                         int* __restrict__ nout, int cap, int64_t pz)
 {
+    keys = at_pair(keys, pz);
+    nkeys = at_pair(nkeys, pz);
+    cell_list = at_pair(cell_list, pz);
+    out_xy = at_pair(out_xy, pz);
+    nout = at_pair(nout, pz);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t* K = reinterpret_cast<uint64_t*>(smem);
     __shared__ int s_w[16];
@@ -276,8 +299,12 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
 template <int WIN>
 __global__ __launch_bounds__(256) void k_subpix(const uint8_t* __restrict__ img, int w, int h, int stride,
                                                 float* __restrict__ xy, const int* __restrict__ d_n, int nmax,
-                                                const float* __restrict__ mask, int iters, double eps2)
+                                                const float* __restrict__ mask, int iters, double eps2, int64_t iz,
+                                                int64_t pz)
 {
+    img = at_pair(img, iz);
+    xy = at_pair(xy, pz);
+    d_n = at_pair(d_n, pz);
     constexpr int WW = 2 * WIN + 1, BW = WW + 2, NB = BW * BW, NK = WW * WW;
     __shared__ float s_buf[4][NB];
     __shared__ double s_t[4][5][NK];
@@ -388,14 +415,18 @@ struct PyrDownArgs {
     const uint8_t* src[2];
     uint8_t* dst[2];
     int sw, sh, spitch, dw, dh;
+    int src_img;                        // src = the input frames (pair stride iz), else pyramid levels (pz)
 };
 
-// pyrDown 8U (5x5 [1 4 6 4 1]^2, (sum + 128) >> 8, REFLECT_101); blockIdx.z = frame
-__global__ __launch_bounds__(256) void k_pyr_down(PyrDownArgs a)
+// pyrDown 8U (5x5 [1 4 6 4 1]^2, (sum + 128) >> 8, REFLECT_101); blockIdx.z = 2 * pair + frame
+__global__ __launch_bounds__(256) void k_pyr_down(PyrDownArgs a, int64_t iz, int64_t pz)
 {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= a.dw || y >= a.dh) return;
-    const uint8_t* src = a.src[blockIdx.z];
+    const int fr = blockIdx.z & 1;
+    const uint64_t pair = blockIdx.z >> 1;
+    const uint8_t* src = a.src[fr] + pair * (uint64_t)(a.src_img ? iz : pz);
+    uint8_t* dst = a.dst[fr] + pair * (uint64_t)pz;
     int cols[5];
     for (int j = 0; j < 5; j++) cols[j] = reflect101(2 * x + j - 2, a.sw);
     const int k[5] = {1, 4, 6, 4, 1};
@@ -406,16 +437,17 @@ __global__ __launch_bounds__(256) void k_pyr_down(PyrDownArgs a)
         for (int j = 0; j < 5; j++) hs += k[j] * row[cols[j]];
         acc += k[i] * hs;
     }
-    a.dst[blockIdx.z][(size_t)y * a.dw + x] = (uint8_t)((acc + 128) >> 8);
+    dst[(size_t)y * a.dw + x] = (uint8_t)((acc + 128) >> 8);
 }
 
-// calcSharrDeriv of every previous-frame level; blockIdx.y = level, grid-stride over pixels
-__global__ __launch_bounds__(256) void k_sharr(LkPyr pyr)
+// calcSharrDeriv of every previous-frame level; blockIdx.y = level, blockIdx.z = pair,
+// grid-stride over pixels
+__global__ __launch_bounds__(256) void k_sharr(LkPyr pyr, int64_t iz, int64_t pz)
 {
     const int l = blockIdx.y;
     const int w = pyr.w[l], h = pyr.h[l], pitch = pyr.pitch[l];
-    const uint8_t* img = pyr.P[l];
-    short2* d = const_cast<short2*>(pyr.D[l]);
+    const uint8_t* img = at_pair(pyr.P[l], l == 0 ? iz : pz);
+    short2* d = at_pair(const_cast<short2*>(pyr.D[l]), pz);
     for (int e = blockIdx.x * 256 + threadIdx.x; e < w * h; e += gridDim.x * 256) {
         const int y = e / w, x = e - y * w;
         const uint8_t* s0 = img + (size_t)(y > 0 ? y - 1 : (h > 1 ? 1 : 0)) * pitch;
@@ -444,8 +476,12 @@ __device__ __forceinline__ int refl1(int p, int n) { return p < 0 ? -p : (p >= n
 // one wave per point; every lane carries up to 8 window pixels (win*win <= 512)
 __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__ pxy, const int* __restrict__ d_n, int nmax,
                                             float* __restrict__ nxy, uint8_t* __restrict__ status, int win, int max_count,
-                                            double eps2)
+                                            double eps2, int64_t iz, int64_t pz)
 {
+    pxy = at_pair(pxy, pz);
+    d_n = at_pair(d_n, pz);
+    nxy = at_pair(nxy, pz);
+    status = at_pair(status, pz);
     constexpr int PPL = 8;
     const int lane = threadIdx.x & 63;
     const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -461,9 +497,9 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
     int iv[PPL], gxv[PPL], gyv[PPL];
     for (int level = pyr.L - 1; level >= 0; level--) {
         const int lw = pyr.w[level], lh = pyr.h[level], pitch = pyr.pitch[level];
-        const uint8_t* I = pyr.P[level];
-        const uint8_t* J = pyr.N[level];
-        const short2* D = pyr.D[level];
+        const uint8_t* I = at_pair(pyr.P[level], level == 0 ? iz : pz);
+        const uint8_t* J = at_pair(pyr.N[level], level == 0 ? iz : pz);
+        const short2* D = at_pair(pyr.D[level], pz);
         const float sc = (float)(1. / (1 << level));
         float px = px0 * sc, py = py0 * sc;
         if (level == pyr.L - 1) { nx = px; ny = py; }
@@ -919,14 +955,26 @@ struct FmOut {
     double* F;          // 9 (optional)
     int* nf;            // |F_prepoint| (optional)
     int tm_cap;
+    int64_t tm_z;       // batch: pair stride of tm / ntm in bytes when they are caller buffers (0: the pair block)
 };
 
 __global__ __launch_bounds__(kFmThreads) void k_fm(const uint8_t* __restrict__ prev, const uint8_t* __restrict__ cur,
                                                   int w, int h, int stride, const float* __restrict__ pxy,
                                                   const float* __restrict__ nxy, const uint8_t* __restrict__ status,
                                                   const int* __restrict__ d_n, int nmax, int edge, double limit,
-                                                  double thr, double conf, FmOut out)
+                                                  double thr, double conf, FmOut out, int64_t iz, int64_t pz)
 {
+    prev = at_pair(prev, iz);
+    cur = at_pair(cur, iz);
+    pxy = at_pair(pxy, pz);
+    nxy = at_pair(nxy, pz);
+    status = at_pair(status, pz);
+    d_n = at_pair(d_n, pz);
+    out.tm = at_pair(out.tm, out.tm_z ? out.tm_z : pz);
+    out.ntm = at_pair(out.ntm, out.tm_z ? 4 : pz);
+    out.state = at_pair(out.state, pz);
+    out.F = at_pair(out.F, pz);
+    out.nf = at_pair(out.nf, pz);
     __shared__ float2 s_m1[kMaxPts], s_m2[kMaxPts];
     __shared__ uint16_t s_map[kMaxPts];
     __shared__ int s_w[16];
@@ -1152,6 +1200,10 @@ struct FlowDev {
     int* ntm;
     double* F;
     int* nf;
+    // batch layout: every pointer above but prev / cur / mask is pair 0's; pair z's copy is
+    // pz * z bytes further on
+    int npairs;
+    int64_t pz;
 };
 
 int lk_levels(int w, int h, int win, int max_level)
@@ -1165,7 +1217,7 @@ int lk_levels(int w, int h, int win, int max_level)
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d)
+int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
 {
     const int gw = (w + 7) / 8, gh = (h + 7) / 8;
     size_t pyr_bytes = 0, der_px = 0;
@@ -1178,25 +1230,32 @@ int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d)
             der_px += (size_t)lw * lh;
         }
     }
-    const size_t sizes[] = {align256((size_t)w * h), align256((size_t)w * h), align256((size_t)w * h * 4), 256, 256,
-                            align256((size_t)kGfSortMax * 8), align256((size_t)gw * gh * kGfCellCap * 2),
-                            align256((size_t)kMaxPts * 8), align256((size_t)kMaxPts * 8), 256, align256(kMaxPts),
-                            align256(kMaxPts), align256(sizeof(float) * 23 * 23), align256(pyr_bytes),
+    // shared: the two frame copies of the host entry points, the subpix weights; then one block
+    // per pair
+    const size_t shared[] = {align256((size_t)w * h), align256((size_t)w * h), align256(sizeof(float) * 23 * 23)};
+    const size_t sizes[] = {align256((size_t)w * h * 4), 256, 256, align256((size_t)kGfSortMax * 8),
+                            align256((size_t)gw * gh * kGfCellCap * 2), align256((size_t)kMaxPts * 8),
+                            align256((size_t)kMaxPts * 8), 256, align256(kMaxPts), align256(kMaxPts), align256(pyr_bytes),
                             align256(der_px * 4 + 64 * kLkMaxLevels), align256((size_t)kMaxPts * 8), 256, 256, 256};
-    size_t total = 0;
-    for (size_t s : sizes) total += s;
+    size_t pair_bytes = 0, shared_bytes = 0;
+    for (size_t v : sizes) pair_bytes += v;
+    for (size_t v : shared) shared_bytes += v;
     void* base;
-    const int rc = coeb_internal_scratch(c, "flow", total, &base);
+    const int rc = coeb_internal_scratch(c, "flow", shared_bytes + pair_bytes * (size_t)npairs, &base);
     if (rc) return rc;
     uint8_t* p = (uint8_t*)base;
     size_t o = 0;
-    auto take = [&](int i) { void* r = p + o; o += sizes[i]; return r; };
-    d->prev = (uint8_t*)take(0); d->cur = (uint8_t*)take(1); d->R = (float*)take(2);
-    d->rmax = (uint32_t*)take(3); d->nkeys = (int*)take(4); d->keys = (uint64_t*)take(5);
-    d->cells = (uint16_t*)take(6); d->pts = (float*)take(7); d->nxt = (float*)take(8); d->npts = (int*)take(9);
-    d->status = (uint8_t*)take(10); d->state = (uint8_t*)take(11); d->mask = (float*)take(12);
-    d->pyr = (uint8_t*)take(13); d->der = (short2*)take(14); d->tm = (float*)take(15); d->ntm = (int*)take(16);
-    d->F = (double*)take(17); d->nf = (int*)take(18);
+    d->prev = p + o; o += shared[0];
+    d->cur = p + o; o += shared[1];
+    d->mask = (float*)(p + o); o += shared[2];
+    int i = 0;
+    auto take = [&]() { void* r = p + o; o += sizes[i++]; return r; };
+    d->R = (float*)take(); d->rmax = (uint32_t*)take(); d->nkeys = (int*)take(); d->keys = (uint64_t*)take();
+    d->cells = (uint16_t*)take(); d->pts = (float*)take(); d->nxt = (float*)take(); d->npts = (int*)take();
+    d->status = (uint8_t*)take(); d->state = (uint8_t*)take(); d->pyr = (uint8_t*)take(); d->der = (short2*)take();
+    d->tm = (float*)take(); d->ntm = (int*)take(); d->F = (double*)take(); d->nf = (int*)take();
+    d->npairs = npairs;
+    d->pz = (int64_t)pair_bytes;
     return COEB_OK;
 }
 
@@ -1208,21 +1267,22 @@ size_t gf_select_lds(int w, int h, int cell, int np)
 
 // goodFeaturesToTrack into d->pts / d->npts (device count: -1 sort capacity, -3 cell capacity)
 int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, int max_corners, double quality,
-              double min_distance, double k, hipStream_t s)
+              double min_distance, double k, hipStream_t s, int64_t iz = 0)
 {
+    const int P = d->npairs;
     const int cell = (int)lrint(min_distance);
     if (cell < 1) return -2;
     const size_t lds = gf_select_lds(w, h, cell, kGfSortMax);
     if (lds > 160 * 1024) return -2;
-    (void)hipMemsetAsync(d->rmax, 0, 4, s);
-    (void)hipMemsetAsync(d->nkeys, 0, 4, s);
-    const dim3 grid((w + 15) / 16, (h + 15) / 16);
-    hipLaunchKernelGGL(k_gf_response, grid, dim3(256), 0, s, img, w, h, stride, k, d->R, d->rmax);
+    (void)hipMemset2DAsync(d->rmax, (size_t)d->pz, 0, 4, P, s);      // one word per pair
+    (void)hipMemset2DAsync(d->nkeys, (size_t)d->pz, 0, 4, P, s);
+    const dim3 grid((w + 15) / 16, (h + 15) / 16, P);
+    hipLaunchKernelGGL(k_gf_response, grid, dim3(256), 0, s, img, w, h, stride, k, d->R, d->rmax, iz, d->pz);
     hipLaunchKernelGGL(k_gf_candidates, grid, dim3(256), 0, s, d->R, w, h, quality, d->rmax, d->keys, d->nkeys,
-                       kGfSortMax);
+                       kGfSortMax, d->pz);
     (void)hipFuncSetAttribute((const void*)k_gf_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_gf_select, dim3(1), dim3(kGfThreads), lds, s, d->keys, d->nkeys, w, h, max_corners,
-                       (float)(min_distance * min_distance), cell, d->cells, d->pts, d->npts, kMaxPts);
+    hipLaunchKernelGGL(k_gf_select, dim3(1, 1, P), dim3(kGfThreads), lds, s, d->keys, d->nkeys, w, h, max_corners,
+                       (float)(min_distance * min_distance), cell, d->cells, d->pts, d->npts, kMaxPts, d->pz);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1240,18 +1300,19 @@ void subpix_mask(int win, float* mask)
 }
 
 int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride, int max_iter, double eps,
-                  hipStream_t s)
+                  hipStream_t s, int64_t iz = 0)
 {
     const int iters = max_iter < 1 ? 1 : max_iter > 100 ? 100 : max_iter;
     const double e = eps > 0 ? eps : 0.;
-    hipLaunchKernelGGL(k_subpix<10>, dim3((kMaxPts + 3) / 4), dim3(256), 0, s, img, w, h, stride, d->pts, d->npts,
-                       kMaxPts, d->mask, iters, e * e);
+    hipLaunchKernelGGL(k_subpix<10>, dim3((kMaxPts + 3) / 4, 1, d->npairs), dim3(256), 0, s, img, w, h, stride, d->pts,
+                       d->npts, kMaxPts, d->mask, iters, e * e, iz, d->pz);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, int win,
-              int max_level, int max_count, double eps, hipStream_t s)
+              int max_level, int max_count, double eps, hipStream_t s, int64_t iz = 0)
 {
+    const int P = d->npairs;
     LkPyr pyr;
     memset(&pyr, 0, sizeof(pyr));
     const int L = lk_levels(w, h, win, max_level);
@@ -1272,21 +1333,23 @@ int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, 
         a.src[0] = pyr.P[l - 1]; a.src[1] = pyr.N[l - 1];
         a.dst[0] = const_cast<uint8_t*>(pyr.P[l]); a.dst[1] = const_cast<uint8_t*>(pyr.N[l]);
         a.sw = pyr.w[l - 1]; a.sh = pyr.h[l - 1]; a.spitch = pyr.pitch[l - 1]; a.dw = pyr.w[l]; a.dh = pyr.h[l];
-        hipLaunchKernelGGL(k_pyr_down, dim3((a.dw + 63) / 64, (a.dh + 3) / 4, 2), dim3(256), 0, s, a);
+        a.src_img = l == 1;
+        hipLaunchKernelGGL(k_pyr_down, dim3((a.dw + 63) / 64, (a.dh + 3) / 4, 2 * P), dim3(256), 0, s, a, iz, d->pz);
     }
-    hipLaunchKernelGGL(k_sharr, dim3(64, L), dim3(256), 0, s, pyr);
-    hipLaunchKernelGGL(k_lk, dim3((kMaxPts + 3) / 4), dim3(256), 0, s, pyr, d->pts, d->npts, kMaxPts, d->nxt,
-                       d->status, win, max_count, eps * eps);
+    hipLaunchKernelGGL(k_sharr, dim3(64, L, P), dim3(256), 0, s, pyr, iz, d->pz);
+    hipLaunchKernelGGL(k_lk, dim3((kMaxPts + 3) / 4, 1, P), dim3(256), 0, s, pyr, d->pts, d->npts, kMaxPts, d->nxt,
+                       d->status, win, max_count, eps * eps, iz, d->pz);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_fm(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, int edge, double limit,
-              hipStream_t s, int tm_cap)
+              hipStream_t s, int tm_cap, int64_t iz = 0, float* tm_out = nullptr, int* ntm_out = nullptr)
 {
     FmOut o;
-    o.tm = d->tm; o.ntm = d->ntm; o.state = d->state; o.F = d->F; o.nf = d->nf; o.tm_cap = tm_cap;
-    hipLaunchKernelGGL(k_fm, dim3(1), dim3(kFmThreads), 0, s, prev, cur, w, h, stride, d->pts, d->nxt, d->status,
-                       d->npts, kMaxPts, edge, limit, 0.1, 0.99, o);
+    o.tm = d->tm; o.ntm = d->ntm; o.state = d->state; o.F = d->F; o.nf = d->nf; o.tm_cap = tm_cap; o.tm_z = 0;
+    hipLaunchKernelGGL(k_fm, dim3(1, 1, d->npairs), dim3(kFmThreads), 0, s, prev, cur, w, h, stride, d->pts, d->nxt,
+                       d->status, d->npts, kMaxPts, edge, limit, 0.1, 0.99,
+                       tm_out ? FmOut{tm_out, ntm_out, o.state, o.F, o.nf, tm_cap, (int64_t)tm_cap * 8} : o, iz, d->pz);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1446,6 +1509,38 @@ extern "C" int coeb_moving_object_points(coeb_ctx* c, const uint8_t* prev, const
         return rc;
     FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
     return coeb_moving_object_points_device(c, fc.d.prev, fc.d.cur, w, h, w, tm_xy, tm_cap, n_tm, dbg);
+}
+
+// Frame::ProcessMovingObject for every consecutive pair of a device-resident batch (the Frame
+// constructor's T_M, Frame.cc:164-166): pair f-1 = frames (f-1, f) of d_gray (packed, w x h),
+// T_M of frame f into tm_out + f * tm_cap * 2 floats, |T_M| (or -1: F empty) into ntm_out[f];
+// ntm_out[0] = 0 (no previous frame).  Enqueued on the context stream, no synchronisation.
+extern "C" int coeb_internal_pmo_batch(coeb_ctx* c, const uint8_t* d_gray, int F, int w, int h, float* tm_out,
+                                       int* ntm_out, int tm_cap)
+{
+    if (F < 1 || !d_gray || !tm_out || !ntm_out || tm_cap < 1 || tm_cap > kMaxPts)
+        return coeb_internal_error(c, COEB_EINVAL, "moving-object batch: invalid arguments");
+    FlowCall fc;
+    int dev;
+    if (coeb_internal_stream(c, &fc.s, &dev)) return COEB_EINVAL;
+    (void)hipSetDevice(dev);
+    FL_TRY(c, hipMemsetAsync(ntm_out, 0, 4, fc.s));
+    if (F < 2) return COEB_OK;
+    if (w < 32 || h < 32 || lk_levels(w, h, 22, 5) > kLkMaxLevels)
+        return coeb_internal_error(c, COEB_EINVAL, "moving-object batch: frame size");
+    int rc = flow_alloc(c, w, h, &fc.d, F - 1);
+    if (rc) return rc;
+    float mask[21 * 21];
+    subpix_mask(10, mask);
+    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
+    const int64_t iz = (int64_t)w * h;
+    if (launch_gf(&fc.d, d_gray, w, h, w, 1000, 0.01, 8.0, 0.04, fc.s, iz) ||
+        launch_subpix(&fc.d, d_gray, w, h, w, 20, 0.03, fc.s, iz) ||
+        launch_lk(&fc.d, d_gray, d_gray + iz, w, h, w, 22, 5, 20, 0.01, fc.s, iz) ||
+        launch_fm(&fc.d, d_gray, d_gray + iz, w, h, w, 5, 2120.0, fc.s, tm_cap, iz, tm_out + (size_t)tm_cap * 2,
+                  ntm_out + 1))
+        return coeb_internal_error(c, COEB_EDEVICE, "moving-object batch: launch failed");
+    return COEB_OK;
 }
 
 // device-resident frames (pitch `stride`); the subpix weight table is uploaded on first use

@@ -24,12 +24,23 @@ __device__ __forceinline__ int reflect101(int p, int len)
 // one workgroup per box: Laplacian [0 1 0; 1 -4 1; 0 1 0] on the cloned crop (REFLECT_101 at
 // the crop edge), negatives saturate to 0 (saturate_cast<ushort>), exact integer sum,
 // cv::mean = sum * (1./count).
+// box_frame (batch form): frame of box bi in a packed batch of frames fstride bytes apart; boxes
+// of frame 0 get flag 0 (the RGB-D Frame constructor's first frame, Frame.cc:205-208).
 __global__ __launch_bounds__(256) void k_blur_flags(const uint8_t* __restrict__ img, int W, int H, int stride,
                                                     const float* __restrict__ boxes, int* __restrict__ out,
-                                                    double* __restrict__ mean_out)
+                                                    double* __restrict__ mean_out, const int* __restrict__ box_frame,
+                                                    int64_t fstride)
 {
     __shared__ unsigned long long s_part[4];
     const int bi = blockIdx.x;
+    if (box_frame) {
+        const int f = box_frame[bi];
+        if (f == 0) {
+            if (threadIdx.x == 0) { out[bi] = 0; if (mean_out) mean_out[bi] = -1.0; }
+            return;
+        }
+        img += (int64_t)f * fstride;
+    }
     const float x0f = boxes[4 * bi], y0f = boxes[4 * bi + 1], x1f = boxes[4 * bi + 2], y1f = boxes[4 * bi + 3];
     const int rx = (int)x0f, ry = (int)y0f, rw = (int)(x1f - x0f), rh = (int)(y1f - y0f);
     if (rx < 0 || ry < 0 || rw <= 0 || rh <= 0 || rx + rw > W || ry + rh > H) {
@@ -129,6 +140,17 @@ extern "C" int coeb_internal_error(coeb_ctx* c, int code, const char* msg);
         if (_e != hipSuccess) return coeb_internal_error((c), COEB_EDEVICE, hipGetErrorString(_e)); \
     } while (0)
 
+// The blur flags of every box of a device-resident batch (packed W x H frames): d_box_frame[bi]
+// = frame of box bi; frame 0's boxes get 0.  Enqueued on stream s.
+extern "C" int coeb_internal_blur_flags_batch(const uint8_t* d_gray, int W, int H, const float* d_boxes,
+                                              const int* d_box_frame, int nbox, int* d_out, hipStream_t s)
+{
+    if (nbox <= 0) return COEB_OK;
+    hipLaunchKernelGGL(k_blur_flags, dim3(nbox), dim3(256), 0, s, d_gray, W, H, W, d_boxes, d_out, (double*)nullptr,
+                       d_box_frame, (int64_t)W * H);
+    return hipGetLastError() == hipSuccess ? COEB_OK : COEB_EDEVICE;
+}
+
 extern "C" int coeb_blur_flags(coeb_ctx* c, const uint8_t* gray, int W, int H, size_t stride, const coeb_box* boxes,
                                int nbox, int32_t* flags_out)
 {
@@ -148,7 +170,7 @@ extern "C" int coeb_blur_flags(coeb_ctx* c, const uint8_t* gray, int W, int H, s
     FR_TRY(c, hipMemcpy2DAsync(dimg, W, gray, stride, W, H, hipMemcpyHostToDevice, s));
     FR_TRY(c, hipMemcpyAsync(dbox, boxes, (size_t)nbox * 16, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_blur_flags, dim3(nbox), dim3(256), 0, s, (const uint8_t*)dimg, W, H, W, (const float*)dbox,
-                       (int*)dout, (double*)nullptr);
+                       (int*)dout, (double*)nullptr, (const int*)nullptr, (int64_t)0);
     FR_TRY(c, hipGetLastError());
     FR_TRY(c, hipMemcpyAsync(flags_out, dout, (size_t)nbox * 4, hipMemcpyDeviceToHost, s));
     FR_TRY(c, hipStreamSynchronize(s));

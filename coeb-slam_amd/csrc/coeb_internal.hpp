@@ -146,6 +146,11 @@ struct ExtractBufs {
     const float* tm;       // [ntm_total][2]
     const int* tm_off;     // [F+1]
     const int* blurf;      // [nbox_total]
+    // T_M computed on the device (coeb_frame_batch_device): frame f's points at
+    // tmd + f * tmd_cap * 2, count ntmd[f] (-1: none); used instead of tm / tm_off when set
+    const float* tmd;
+    const int* ntmd;
+    int tmd_cap;
     int* err;              // device error word (capacity overflows)
 };
 

@@ -161,6 +161,21 @@ int coeb_extract_batch_device(coeb_ctx* ctx, const uint8_t* d_gray, int nframes,
                               const coeb_box* boxes, const int32_t* box_off,
                               const float* tm_xy, const int32_t* tm_off,
                               const int32_t* blur_flag);
+/* The RGB-D Frame constructor on a device-resident batch (src/Frame.cc:157-214): for frame f,
+ * ProcessMovingObject(frame f-1, frame f) -> T_M (:164-166, coeb_moving_object_points), the
+ * detect_laplacian blur flag of every box (:171-202; frame 0 is the sequence's first frame: no
+ * T_M, flags 0, :205-208), then ORBextractor::operator() with those boxes, T_M and flags (:214).
+ * T_M and the flags never leave the device (coeb_batch_frame_results exposes them).  Boxes are
+ * host arrays as in coeb_extract_batch_device (NULL: none).  Runs on the context stream only;
+ * results as coeb_extract_batch_device's (coeb_batch_results), and the batch matcher / pose
+ * entry points follow it. */
+int coeb_frame_batch_device(coeb_ctx* ctx, const uint8_t* d_gray, int nframes, int width, int height,
+                            const coeb_box* boxes, const int32_t* box_off);
+/* Device pointers of the last coeb_frame_batch_device: T_M of frame f at d_tm + f * tm_cap * 2
+ * (x, y floats), |T_M| in d_ntm[f] (-1: the fundamental matrix was empty), blur flags per box
+ * (NULL without boxes). */
+int coeb_batch_frame_results(coeb_ctx* ctx, const float** d_tm, const int32_t** d_ntm, int* tm_cap,
+                             const int32_t** d_blur);
 /* Device pointers to the batch outputs: keypoints [nframes][kcap], descriptors
  * [nframes][kcap][32], counts [nframes]. */
 int coeb_batch_results(coeb_ctx* ctx, const coeb_keypoint** d_kps, const uint8_t** d_desc,

@@ -150,3 +150,46 @@ def test_process_moving_object_flags_object(ctx):
         assert tm is not None and len(tm) >= 20
         inb = (tm[:, 0] >= x0 - 2) & (tm[:, 0] < x1 + 2) & (tm[:, 1] >= y0 - 2) & (tm[:, 1] < y1 + 2)
         assert inb.mean() > 0.8, (seed, inb.mean())
+
+
+def test_frame_batch_matches_oracle_frame_by_frame(oracle_mod):
+    """The RGB-D Frame constructor on a device batch (coeb_frame_batch_device, Frame.cc:157-214):
+    for every frame f, ProcessMovingObject(frame f-1, frame f) -> T_M, the boxes' blur flags
+    (frame 0: the sequence's first frame, no T_M and flags 0) and the masked extraction, against
+    the oracle run frame by frame; then the batch matcher follows on those keypoints."""
+    from coeb_front.pipeline import BatchPipeline
+    F = 6
+    frames, obj = synth.moving_object_sequence(640, 480, F, seed=3)
+    boxes = [np.stack([obj[f], np.float32([420, 60, 600, 200])]) for f in range(F)]   # object + a static panel
+    bp = BatchPipeline(640, 480, F)
+    try:
+        bp.load(frames, Tcw=np.stack([synth.motion_pose()] * F))
+        bp.set_frame_boxes(boxes)
+        bp.run(frame=True)
+        bp.synchronize()
+        out, matches, nms = bp.results()
+        tms, flags = bp.ctx.batch_frame_results(F, 2 * F)
+        ex = oracle_mod.Extractor()
+        ntm_total = 0
+        for f in range(F):
+            if f == 0:
+                tm_ref, blur_ref = np.zeros((0, 2), np.float32), np.zeros(2, np.int32)
+                assert tms[0] is not None and len(tms[0]) == 0
+            else:
+                tm_ref = oracle_mod.process_moving_object(frames[f - 1], frames[f])
+                blur_ref, _ = oracle_mod.blur_flags(frames[f], boxes[f])
+                if tm_ref is None:
+                    assert tms[f] is None, f
+                    tm_ref = np.zeros((0, 2), np.float32)
+                else:
+                    assert np.array_equal(tms[f], tm_ref), f
+                    ntm_total += len(tm_ref)
+            assert np.array_equal(flags[2 * f:2 * f + 2], blur_ref), f
+            r = ex.extract(frames[f], boxes[f], tm_ref, blur_ref)
+            for name in r["kps"].dtype.names:
+                assert np.array_equal(out[f][0][name], r["kps"][name]), (f, name)
+            assert np.array_equal(out[f][1], r["desc"]), f
+        assert ntm_total > 0                       # the mask path is exercised
+        assert all(n is None or n > 0 for n in nms)
+    finally:
+        bp.close()
