@@ -52,6 +52,7 @@ ABI_SYMBOLS = [
     "coeb_host_alloc", "coeb_host_free", "coeb_memcpy_h2d_async", "coeb_memcpy_d2h_async",
     "coeb_copyq_create", "coeb_copyq_destroy", "coeb_copyq_h2d", "coeb_copyq_d2h", "coeb_copyq_after_ctx",
     "coeb_ctx_after_copyq", "coeb_copyq_synchronize", "coeb_frame_batch_device", "coeb_batch_frame_results",
+    "coeb_track_local_map_batch_device", "coeb_batch_track_results",
 ]
 
 
@@ -137,6 +138,9 @@ def lib():
         L.coeb_pose_batch_device.argtypes = [C.c_void_p, C.POINTER(Camera), C.c_int, C.c_void_p, C.c_int32]
         L.coeb_batch_pose_results.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                               C.POINTER(C.c_void_p)]
+        L.coeb_track_local_map_batch_device.argtypes = [C.c_void_p, C.POINTER(Camera), C.c_int, C.c_int32, C.c_float,
+                                                        C.c_float]
+        L.coeb_batch_track_results.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 6
         L.coeb_match_lastframe.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(CurFrameC),
                                            C.POINTER(LastFrameC), C.c_void_p, C.c_void_p, C.c_float, C.c_int,
                                            C.c_int, C.c_void_p, C.POINTER(C.c_int)]
@@ -325,6 +329,19 @@ class Context:
         t, n, o = C.c_void_p(), C.c_void_p(), C.c_void_p()
         self.check(lib().coeb_batch_pose_results(self.h, C.byref(t), C.byref(n), C.byref(o)))
         return t.value, n.value, o.value
+
+    def track_local_map_batch_device(self, cam, nframes, nkf=2, th=3.0, nnratio=0.8):
+        """Tracking::TrackLocalMap over the batch posed last (coeb_track_local_map_batch_device):
+        outlier discard, local map of KeyFrames f-1 / f-2 through isInFrustum, the local-map
+        SearchByProjection(th = 3 for RGB-D, Tracking.cc:1264-1270), second PoseOptimization."""
+        self.check(lib().coeb_track_local_map_batch_device(self.h, C.byref(cam), nframes, int(nkf), float(th),
+                                                           float(nnratio)))
+
+    def batch_track_results(self):
+        """Device pointers (Tcw, ninliers, nmatches_map, nlocal, local_match, outlier)."""
+        ps = [C.c_void_p() for _ in range(6)]
+        self.check(lib().coeb_batch_track_results(self.h, *[C.byref(p) for p in ps]))
+        return tuple(p.value for p in ps)
 
     def synchronize(self):
         self.check(lib().coeb_synchronize(self.h))

@@ -58,9 +58,11 @@ class BatchPipeline:
                         np.asarray(tm_off, np.int32), np.concatenate(blurs))
         self.ctx.synchronize()
 
-    def run(self, match=True, th=15.0, nobs=2, pose=False, frame=False):
+    def run(self, match=True, th=15.0, nobs=2, pose=False, frame=False, track=False, nkf=2):
         """Enqueue one step (extraction of F frames + F-1 matches, and with pose=True the
-        motion-model PoseOptimization of every matched frame); does not synchronise.  frame=True
+        motion-model PoseOptimization of every matched frame, with track=True also TrackLocalMap:
+        local map of KeyFrames f-1, f-2 -> SearchByProjection -> PoseOptimization, BASELINE
+        configs[4]); does not synchronise.  frame=True
         runs the whole RGB-D Frame constructor instead of the extraction alone: T_M from the
         previous frame (ProcessMovingObject), blur flags of the boxes set by set_frame_boxes(),
         masked extraction (coeb_frame_batch_device)."""
@@ -74,8 +76,10 @@ class BatchPipeline:
             self.ctx.extract_batch_device(self.gray.ptr, self.F, self.W, self.H)
         if match:
             self.ctx.match_batch_device_tcw(self.depth.ptr, self.F, self.W, self.H, self.cam, self.dTcw.ptr, th, nobs)
-            if pose:
+            if pose or track:
                 self.ctx.pose_batch_device(self.cam, self.F, self.dTcw.ptr)
+            if track:
+                self.ctx.track_local_map_batch_device(self.cam, self.F, nkf)
 
     def set_frame_boxes(self, boxes_per_frame):
         """YOLO boxes of every frame (list of (n_f, 4) xyxy) for run(frame=True)."""
@@ -135,6 +139,32 @@ class BatchPipeline:
         nin = self.ctx.download(n_ptr, 4 * self.F, np.int32)
         outl = self.ctx.download(o_ptr, kcap * self.F, np.uint8).reshape(self.F, kcap)
         return T, [int(x) for x in nin], [None] + [outl[f, :counts[f]].copy() for f in range(1, self.F)]
+
+    def track_results(self):
+        """Host copies after run(track=True), per frame (index 0 = halo, unused): Tcw (F, 4, 4)
+        after TrackLocalMap, second-PoseOptimization inliers, nmatchesMap, local-map matches
+        (count and per-keypoint local index), outlier flags, and the tracking state (0: the
+        motion model failed, 1: TrackLocalMap failed (< 30 inliers, Tracking.cc:1040-1046),
+        2: tracked)."""
+        _, _, cnt_ptr, kcap = self.ctx.batch_results()
+        counts = self.ctx.download(cnt_ptr, 4 * self.F, np.int32)
+        t_ptr, n_ptr, m_ptr, nl_ptr, lm_ptr, o_ptr = self.ctx.batch_track_results()
+        T = self.ctx.download(t_ptr, 64 * self.F, np.float32).reshape(self.F, 4, 4)
+        nin = self.ctx.download(n_ptr, 4 * self.F, np.int32)
+        nmap = self.ctx.download(m_ptr, 4 * self.F, np.int32)
+        nloc = self.ctx.download(nl_ptr, 4 * self.F, np.int32)
+        lm = self.ctx.download(lm_ptr, 4 * kcap * self.F, np.int32).reshape(self.F, kcap)
+        outl = self.ctx.download(o_ptr, kcap * self.F, np.uint8).reshape(self.F, kcap)
+        _, _, nms = self.results()
+        state = [None]
+        for f in range(1, self.F):
+            if nms[f] < 20 or nmap[f] < 10:
+                state.append(0)
+            else:
+                state.append(2 if nin[f] >= 30 else 1)
+        return dict(T=T, ninliers=[int(x) for x in nin], nmatches_map=[int(x) for x in nmap],
+                    nlocal=[int(x) for x in nloc], local_match=[None] + [lm[f, :counts[f]].copy() for f in range(1, self.F)],
+                    outlier=[None] + [outl[f, :counts[f]].copy() for f in range(1, self.F)], state=state, stride=kcap)
 
     def close(self):
         for b in (self.gray, self.depth, self.dTcw):

@@ -425,6 +425,11 @@ struct coeb_ctx {
     bool side_init = false;
     hipEvent_t ev_tprep = nullptr, ev_pose = nullptr;
     bool pose_pending = false;
+    // batch tracking state: Observations() the matcher gave the LastFrame points, the frames and
+    // min_matches of the last coeb_pose_batch_device (TrackLocalMap continues that batch)
+    int batch_nobs = 2, pose_frames = 0, pose_min_matches = 20;
+    hipEvent_t ev_tlm = nullptr;
+    int tlm_frames = 0;
     // pinned host staging of the host-buffer entry points: their inputs are packed here and
     // moved in one copy (a dozen small pageable copies cost more than the kernels)
     uint8_t* pin = nullptr;
@@ -824,6 +829,7 @@ void coeb_destroy(coeb_ctx* c)
         (void)hipStreamDestroy(c->pose_stream);
         (void)hipEventDestroy(c->ev_tprep);
         (void)hipEventDestroy(c->ev_pose);
+        if (c->ev_tlm) (void)hipEventDestroy(c->ev_tlm);
     }
     for (auto& kv : c->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
@@ -1366,6 +1372,7 @@ int match_batch_impl(coeb_ctx* c, const float* d_depth, int F, int W, int H, con
     }
     c->mdone_valid = chunked;
     if (chunked) c->pending_join = true;
+    c->batch_nobs = nobs;
     return COEB_OK;
 }
 
@@ -1473,6 +1480,9 @@ int coeb_pose_batch_device(coeb_ctx* c, const coeb_camera* cam, int F, const flo
         return hip_err(c, hipGetLastError(), "launch_pose");
     HIP_TRY(c, hipEventRecord(c->ev_pose, c->pose_stream));
     c->pose_pending = true;
+    c->pose_frames = F;
+    c->pose_min_matches = min_matches;
+    c->tlm_frames = 0;
     return COEB_OK;
 }
 
@@ -1483,6 +1493,108 @@ int coeb_batch_pose_results(coeb_ctx* c, const float** d_Tcw, const int32_t** d_
     if (d_Tcw) *d_Tcw = static_cast<const float*>(c->bufs["t_T"].p);
     if (d_ninliers) *d_ninliers = static_cast<const int32_t*>(c->bufs["t_res"].p);
     if (d_outlier) *d_outlier = static_cast<const uint8_t*>(c->bufs["t_outl"].p);
+    return COEB_OK;
+}
+
+int coeb_track_local_map_batch_device(coeb_ctx* c, const coeb_camera* cam, int F, int32_t nkf, float th, float nnratio)
+{
+    if (!c || !cam || F <= 0 || nkf < 1 || nkf > 2 || !(th > 0) || !(nnratio > 0))
+        return set_err(c, COEB_EINVAL, "coeb_track_local_map_batch_device: invalid arguments");
+    if (!c->has_plan || c->batch_frames != F || c->pose_frames != F || !c->bufs.count("t_T"))
+        return set_err(c, COEB_EINVAL, "coeb_track_local_map_batch_device: must follow coeb_pose_batch_device on the same batch");
+    if (c->tlm_frames) return set_err(c, COEB_EINVAL, "coeb_track_local_map_batch_device: already run on this batch");
+    (void)hipSetDevice(c->device);
+    const int K = c->plan.kcap;
+    const int64_t FK = (int64_t)F * K, FM = 2 * FK;
+    int rc;
+    TlmBufs t;
+    memset(&t, 0, sizeof(t));
+    uint8_t *s_desc, *s_has, *seen, *act, *inv, *has2, *outl2;
+    int8_t* s_oct;
+    float *s_xw, *px, *py, *pxr, *vc, *lxw, *xw2, *T2;
+    int32_t *s_m1, *s_cnt, *s_nm1, *cobs, *nmap, *lvl, *lno, *lmatch, *nloc, *lpath, *n2, *res2, *derr;
+    uint32_t* lists;
+    if ((rc = ensure(c, "tl_sdesc", (size_t)(FK + K) * 32, &s_desc)) || (rc = ensure(c, "tl_soct", (size_t)FK, &s_oct)) ||
+        (rc = ensure(c, "tl_shas", (size_t)FK, &s_has)) || (rc = ensure(c, "tl_sxw", (size_t)FK * 3, &s_xw)) ||
+        (rc = ensure(c, "tl_sm1", (size_t)FK, &s_m1)) || (rc = ensure(c, "tl_scnt", (size_t)F, &s_cnt)) ||
+        (rc = ensure(c, "tl_snm1", (size_t)F, &s_nm1)) || (rc = ensure(c, "tl_seen", (size_t)FK, &seen)) ||
+        (rc = ensure(c, "tl_cobs", (size_t)FK, &cobs)) || (rc = ensure(c, "tl_nmap", (size_t)F, &nmap)) ||
+        (rc = ensure(c, "tl_active", (size_t)F, &act)) || (rc = ensure(c, "tl_inview", (size_t)FM, &inv)) ||
+        (rc = ensure(c, "tl_px", (size_t)FM, &px)) || (rc = ensure(c, "tl_py", (size_t)FM, &py)) ||
+        (rc = ensure(c, "tl_pxr", (size_t)FM, &pxr)) || (rc = ensure(c, "tl_level", (size_t)FM, &lvl)) ||
+        (rc = ensure(c, "tl_vcos", (size_t)FM, &vc)) || (rc = ensure(c, "tl_lnobs", (size_t)FM, &lno)) ||
+        (rc = ensure(c, "tl_lxw", (size_t)FM * 3, &lxw)) || (rc = ensure(c, "tl_lmatch", (size_t)FK, &lmatch)) ||
+        (rc = ensure(c, "tl_nlocal", (size_t)F, &nloc)) || (rc = ensure(c, "tl_path", (size_t)F * 2, &lpath)) ||
+        (rc = ensure(c, "tl_lists", (size_t)FM * match_list_cap(), &lists)) ||
+        (rc = ensure(c, "tl_has2", (size_t)FK, &has2)) || (rc = ensure(c, "tl_xw2", (size_t)FK * 3, &xw2)) ||
+        (rc = ensure(c, "tl_T2", (size_t)F * 16, &T2)) || (rc = ensure(c, "tl_outl2", (size_t)FK, &outl2)) ||
+        (rc = ensure(c, "tl_n2", (size_t)F, &n2)) || (rc = ensure(c, "tl_res2", (size_t)F, &res2)) ||
+        (rc = ensure(c, "err", 4, &derr)))
+        return rc;
+    t.K = K; t.nkf = nkf; t.nobs = c->batch_nobs; t.min_matches = c->pose_min_matches; t.min_map = 10;
+    t.kps = c->bufs["kps"].p; t.desc = static_cast<const uint8_t*>(c->bufs["desc"].p);
+    t.counts = static_cast<const int32_t*>(c->bufs["counts"].p);
+    t.match1 = static_cast<const int32_t*>(c->bufs["b_match"].p); t.nmatch1 = static_cast<const int32_t*>(c->bufs["b_nm"].p);
+    t.has = static_cast<const uint8_t*>(c->bufs["b_has"].p); t.xw = static_cast<const float*>(c->bufs["b_xw"].p);
+    t.s_desc = s_desc; t.s_oct = s_oct; t.s_has = s_has; t.s_xw = s_xw; t.s_m1 = s_m1; t.s_cnt = s_cnt; t.s_nm1 = s_nm1;
+    t.T1 = static_cast<const float*>(c->bufs["t_T"].p); t.has1 = static_cast<const uint8_t*>(c->bufs["t_has"].p);
+    t.outl1 = static_cast<const uint8_t*>(c->bufs["t_outl"].p); t.xw1 = static_cast<const float*>(c->bufs["t_xw"].p);
+    t.seen = seen; t.cur_obs = cobs; t.nmap = nmap; t.active = act;
+    t.in_view = inv; t.px = px; t.py = py; t.pxr = pxr; t.level = lvl; t.vcos = vc; t.lm_nobs = lno; t.lm_xw = lxw;
+    t.lmatch = lmatch; t.has2 = has2; t.xw2 = xw2; t.T2 = T2; t.outl2 = outl2; t.n2 = n2;
+    // the snapshot runs on the context stream, after this batch's matcher and before the next
+    // batch's extraction; coeb_pose_batch_device already joined the previous pose-stream work
+    hipStream_t s = main_stream(c);
+    if (launch_tlm_snapshot(t, F, s, &c->hook)) return hip_err(c, hipGetLastError(), "launch_tlm_snapshot");
+    if (F < 2) { c->tlm_frames = F; return COEB_OK; }
+    if (!c->ev_tlm) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_tlm, hipEventDisableTiming));
+    HIP_TRY(c, hipEventRecord(c->ev_tlm, s));
+    hipStream_t ps = c->pose_stream;                // after the first k_pose
+    HIP_TRY(c, hipStreamWaitEvent(ps, c->ev_tlm, 0));
+    const MatchCam mcam = make_cam(c, cam);
+    if (launch_tlm_frustum(mcam, t, F, ps, &c->hook)) return hip_err(c, hipGetLastError(), "launch_tlm_frustum");
+    LocalBufsHost lb;
+    lb.cur_kps = static_cast<const coeb_keypoint*>(c->bufs["t_kp"].p) + K;
+    lb.cur_desc = s_desc + (int64_t)2 * K * 32;      // frame 1 = row 2
+    lb.cur_ur = static_cast<const float*>(c->bufs["t_ur"].p) + K;
+    lb.cur_obs = cobs + K; lb.cur_n = K;
+    const int64_t M = 2 * (int64_t)K;
+    lb.in_view = inv + M; lb.proj_x = px + M; lb.proj_y = py + M; lb.proj_xr = pxr + M; lb.level = lvl + M;
+    lb.view_cos = vc + M; lb.nobs = lno + M; lb.mp_n = (int)M;
+    lb.desc = s_desc;                                // frame 1's local map: KF2 = frame -1 (row 0), KF1 = frame 0
+    lb.match = lmatch + K; lb.nmatch = nloc + 1; lb.lists = lists; lb.err = derr; lb.path = lpath + 2;
+    lb.cur_n_arr = s_cnt + 1; lb.active = act + 1; lb.npairs = F - 1; lb.cur_stride = K; lb.mp_desc_stride = K;
+    rc = launch_match_local(mcam, lb, th, nnratio, ps, &c->hook);
+    if (rc == -2) return set_err(c, COEB_ERANGE, "coeb_track_local_map_batch_device: frame and local map exceed the LDS budget");
+    if (rc) return hip_err(c, hipGetLastError(), "launch_match_local");
+    if (launch_tlm_pose_prep(t, F, ps, &c->hook)) return hip_err(c, hipGetLastError(), "launch_tlm_pose_prep");
+    PoseBufs b;
+    const int64_t o = K;
+    b.n = n2 + 1; b.has_mp = has2 + o; b.xw = xw2 + 3 * o;
+    b.kps = static_cast<const coeb_keypoint*>(c->bufs["t_kp"].p) + o; b.ur = static_cast<const float*>(c->bufs["t_ur"].p) + o;
+    b.inv_sigma2 = static_cast<const float*>(c->bufs["t_isg"].p); b.Tcw = T2 + 16; b.outlier = outl2 + o;
+    b.result = res2 + 1;
+    b.edges = static_cast<PoseEdgeRec*>(c->bufs["t_edge"].p) + o; b.active = static_cast<uint8_t*>(c->bufs["t_act"].p) + o;
+    b.chi2 = static_cast<double*>(c->bufs["t_chi"].p) + o; b.stride = K; b.timing = nullptr;
+    if (launch_pose(b, F - 1, cam->fx, cam->fy, cam->cx, cam->cy, cam->bf, ps, &c->hook))
+        return hip_err(c, hipGetLastError(), "launch_pose");
+    HIP_TRY(c, hipEventRecord(c->ev_pose, ps));
+    c->pose_pending = true;
+    c->tlm_frames = F;
+    return COEB_OK;
+}
+
+int coeb_batch_track_results(coeb_ctx* c, const float** d_Tcw, const int32_t** d_ninliers, const int32_t** d_nmatches_map,
+                             const int32_t** d_nlocal, const int32_t** d_local_match, const uint8_t** d_outlier)
+{
+    if (!c || !c->tlm_frames) return set_err(c, COEB_EINVAL, "coeb_batch_track_results: no batch TrackLocalMap yet");
+    join_pose(c);
+    if (d_Tcw) *d_Tcw = static_cast<const float*>(c->bufs["tl_T2"].p);
+    if (d_ninliers) *d_ninliers = static_cast<const int32_t*>(c->bufs["tl_res2"].p);
+    if (d_nmatches_map) *d_nmatches_map = static_cast<const int32_t*>(c->bufs["tl_nmap"].p);
+    if (d_nlocal) *d_nlocal = static_cast<const int32_t*>(c->bufs["tl_nlocal"].p);
+    if (d_local_match) *d_local_match = static_cast<const int32_t*>(c->bufs["tl_lmatch"].p);
+    if (d_outlier) *d_outlier = static_cast<const uint8_t*>(c->bufs["tl_outl2"].p);
     return COEB_OK;
 }
 

@@ -213,6 +213,12 @@ struct LocalBufsHost {
     const int* level; const float* view_cos; const uint8_t* desc; const int* nobs; int mp_n;
     int* match; int* nmatch; uint32_t* lists; int* err;
     int* path;   // [0]: 0 parallel claims, 1 forced sequential, 2 list overflow, 3 no convergence; [1]: iterations
+    // batch form: npairs workgroups, pair p reads cur_* + p*cur_stride (keypoint count
+    // cur_n_arr[p]), the local-map arrays + p*mp_n, desc + p*mp_desc_stride*32, lists + p*mp_n*kCQ,
+    // and writes match + p*cur_stride, nmatch[p], path[2p..]; active[p] == 0 skips the pair
+    // (no matches).  cur_n_arr == null: the single search above.
+    const int* cur_n_arr = nullptr; const uint8_t* active = nullptr;
+    int npairs = 1, cur_stride = 0, mp_desc_stride = 0;
 };
 int launch_match_local(const MatchCam& cam, const LocalBufsHost& b, float th, float nnratio, hipStream_t s,
                        ProfileHook* prof);
@@ -260,6 +266,33 @@ struct TrackPrepBufs {
     int stride, min_matches;
 };
 int launch_track_prep(const TrackPrepBufs& t, int F, hipStream_t s, ProfileHook* prof);
+
+// Tracking::TrackLocalMap on a device batch (coeb_track.hip), after the TrackWithMotionModel
+// tail: current frame f = 1..F-1, KF1 = frame f-1 (the world frame of pair f), KF2 = frame f-2.
+// Every [F][K] array is indexed from frame 0; the local map of frame f is [f][2K]: slots [0, K)
+// = KF2's keypoint slots, [K, 2K) = KF1's.
+struct TlmBufs {
+    int K, nkf, nobs, min_matches, min_map;
+    // batch outputs of the extraction / matcher (main stream), read by k_tlm_snapshot only
+    const void* kps; const uint8_t* desc; const int* counts; const int* match1; const int* nmatch1;
+    const uint8_t* has; const float* xw;
+    // snapshot (main stream): s_desc holds frame g at row g + 1 (row 0: KF2 of frame 1, never read)
+    uint8_t* s_desc; int8_t* s_oct; uint8_t* s_has; float* s_xw; int* s_m1; int* s_cnt; int* s_nm1;
+    // TrackWithMotionModel's PoseOptimization (t_* of coeb_pose_batch_device)
+    const float* T1; const uint8_t* has1; const uint8_t* outl1; const float* xw1;
+    // discard + SearchLocalPoints state
+    uint8_t* seen;       // [F][K] KF1 slot matched by the motion model (mnLastFrameSeen)
+    int* cur_obs;        // [F][K] Observations() of the MapPoint a keypoint keeps, -1: none
+    int* nmap;           // [F] nmatchesMap (Tracking.cc:967-985)
+    uint8_t* active;     // [F] TrackWithMotionModel returned true -> TrackLocalMap runs
+    uint8_t* in_view; float* px; float* py; float* pxr; int* level; float* vcos; int* lm_nobs; float* lm_xw;
+    const int* lmatch;   // [F][K] SearchByProjection(F, vpLocalMapPoints) assignments
+    // second PoseOptimization's inputs
+    uint8_t* has2; float* xw2; float* T2; uint8_t* outl2; int* n2;
+};
+int launch_tlm_snapshot(const TlmBufs& t, int F, hipStream_t s, ProfileHook* prof);
+int launch_tlm_frustum(const MatchCam& cam, const TlmBufs& t, int F, hipStream_t s, ProfileHook* prof);
+int launch_tlm_pose_prep(const TlmBufs& t, int F, hipStream_t s, ProfileHook* prof);
 
 // relocalisation projection search (ORBmatcher::SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist))
 struct KfBufsHost {

@@ -693,7 +693,23 @@ struct LocalBufs {
     const uint8_t* in_view; const float* proj_x; const float* proj_y; const float* proj_xr;
     const int* level; const float* view_cos; const uint8_t* desc; const int* nobs; int mp_n;
     int* match; int* nmatch; uint32_t* lists; int* err; int* path;
+    // batch form (cur_n_arr != null): workgroup p searches frame p's arrays (LocalBufsHost)
+    const int* cur_n_arr; const uint8_t* active; int cur_stride, mp_stride, mp_desc_stride;
 };
+
+// workgroup p's view of a batch launch
+__device__ __forceinline__ LocalBufs local_at_pair(LocalBufs b, int p)
+{
+    if (!b.cur_n_arr) return b;
+    const int64_t c = (int64_t)p * b.cur_stride, m = (int64_t)p * b.mp_stride;
+    b.cur_n = b.cur_n_arr[p];
+    b.cur_kps = reinterpret_cast<const Kp*>(b.cur_kps) + c;
+    b.cur_desc += c * 32; b.cur_ur += c; b.cur_obs += c;
+    b.in_view += m; b.proj_x += m; b.proj_y += m; b.proj_xr += m; b.level += m; b.view_cos += m; b.nobs += m;
+    b.desc += (int64_t)p * b.mp_desc_stride * 32;
+    b.match += c; b.nmatch += p; b.lists += m * kCQ; b.path += 2 * p;
+    return b;
+}
 
 __device__ __forceinline__ float radius_by_viewing_cos(float c) { return c > 0.998f ? 2.5f : 4.0f; }   // ORBmatcher.cc:131-137
 
@@ -717,12 +733,18 @@ __device__ __forceinline__ QueryWin local_window(const MatchCam& cam, const Loca
 constexpr int kLocKeyDist = 16, kLocKeyOct = 12;    // list entry: dist << 16 | octave << 12 | index
 
 template <bool kLds>
-__global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBufs b, float th, float nnratio,
+__global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBufs b0, float th, float nnratio,
                                                            int force_seq)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int s_flag[8];
     const int tid = threadIdx.x;
+    const LocalBufs b = local_at_pair(b0, blockIdx.x);
+    if (b0.active && !b0.active[blockIdx.x]) {                 // frame not handed to TrackLocalMap
+        for (int c = tid; c < b.cur_n; c += kMThreads) b.match[c] = -1;
+        if (tid == 0) *b.nmatch = 0;
+        return;
+    }
     const int n = b.cur_n, nq = b.mp_n;
     size_t off[7];
     match_lds_bytes(n, nq, kLds, off);
@@ -1135,17 +1157,22 @@ int launch_match_local(const MatchCam& cam, const LocalBufsHost& h, float th, fl
     b.in_view = h.in_view; b.proj_x = h.proj_x; b.proj_y = h.proj_y; b.proj_xr = h.proj_xr; b.level = h.level;
     b.view_cos = h.view_cos; b.desc = h.desc; b.nobs = h.nobs; b.mp_n = h.mp_n;
     b.match = h.match; b.nmatch = h.nmatch; b.lists = h.lists; b.err = h.err; b.path = h.path;
+    b.cur_n_arr = h.cur_n_arr; b.active = h.active;
+    b.cur_stride = h.cur_stride; b.mp_stride = h.mp_n; b.mp_desc_stride = h.mp_desc_stride;
+    const int P = h.cur_n_arr ? h.npairs : 1;
+    if (P <= 0) return 0;
+    if (h.cur_n_arr && h.cur_stride >= (1 << kIdxBits)) return -2;
     const int force_seq = getenv("COEB_MATCH_SEQUENTIAL") ? 1 : 0;
-    const int cs = std::max(h.cur_n, 1), qs = std::max(h.mp_n, 1);
+    const int cs = std::max(h.cur_n_arr ? h.cur_stride : h.cur_n, 1), qs = std::max(h.mp_n, 1);
     const size_t lds_full = match_lds_bytes(cs, qs, true, nullptr) + 256;
     const size_t lds_min = match_lds_bytes(cs, qs, false, nullptr) + 256;
     prof_begin(prof, "k_match_local", s);
     if (lds_full <= 160 * 1024) {
         (void)hipFuncSetAttribute((const void*)k_match_local<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_full);
-        hipLaunchKernelGGL(k_match_local<true>, dim3(1), dim3(kMThreads), lds_full - 256, s, cam, b, th, nnratio, force_seq);
+        hipLaunchKernelGGL(k_match_local<true>, dim3(P), dim3(kMThreads), lds_full - 256, s, cam, b, th, nnratio, force_seq);
     } else if (lds_min <= 160 * 1024) {
         (void)hipFuncSetAttribute((const void*)k_match_local<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_min);
-        hipLaunchKernelGGL(k_match_local<false>, dim3(1), dim3(kMThreads), lds_min - 256, s, cam, b, th, nnratio, force_seq);
+        hipLaunchKernelGGL(k_match_local<false>, dim3(P), dim3(kMThreads), lds_min - 256, s, cam, b, th, nnratio, force_seq);
     } else {
         prof_end(prof, s);
         return -2;

@@ -211,6 +211,30 @@ int coeb_pose_batch_device(coeb_ctx* ctx, const coeb_camera* cam, int nframes, c
 int coeb_batch_pose_results(coeb_ctx* ctx, const float** d_Tcw, const int32_t** d_ninliers,
                             const uint8_t** d_outlier);
 
+/* ---- Tracking::TrackLocalMap on the batch (Tracking.cc:966-993, 996-1047, 1222-1272) ----
+ * After coeb_pose_batch_device on the same batch, for every frame f >= 1:
+ *   - TrackWithMotionModel's tail: matched keypoints the first PoseOptimization flagged outlier
+ *     lose their MapPoint; nmatchesMap = kept MapPoints with Observations() > 0; the frame goes
+ *     on only if the motion model ran (>= min_matches) and nmatchesMap >= 10 (:993);
+ *   - the local map: the MapPoints of KeyFrames f-1 (KF1, the pair's world frame) and, with
+ *     nkf = 2, f-2 (KF2, placed by frame f-1's motion-model pose), one MapPoint per keypoint with
+ *     depth > 0; points matched by the motion model are skipped (mnLastFrameSeen),
+ *     the rest go through Frame::isInFrustum(pMP, 0.5) with the first pose;
+ *   - ORBmatcher(nnratio).SearchByProjection(F, vpLocalMapPoints, th) (3 for RGB-D, :1264-1270);
+ *   - Optimizer::PoseOptimization from the first pose over the kept and the new MapPoints.
+ * Observations() of every MapPoint = the nobs of coeb_match_batch_device.  Work is enqueued
+ * behind the first k_pose on the pose stream.  Results (device, frame 0 = halo):
+ * coeb_batch_track_results -> Tcw nframes x 16 (the first pose where TrackLocalMap did not run),
+ * ninliers per frame (the second PoseOptimization's return = mnMatchesInliers when nobs > 0;
+ * 0: not run), nmatches_map per frame, nlocal = SearchByProjection's return, local_match
+ * nframes x capacity (local-map index per keypoint: [0, capacity) KF2 slot, [capacity,
+ * 2 capacity) KF1 slot, -1), outlier flags nframes x capacity (mvbOutlier of the second run). */
+int coeb_track_local_map_batch_device(coeb_ctx* ctx, const coeb_camera* cam, int nframes, int32_t nkf, float th,
+                                      float nnratio);
+int coeb_batch_track_results(coeb_ctx* ctx, const float** d_Tcw, const int32_t** d_ninliers,
+                             const int32_t** d_nmatches_map, const int32_t** d_nlocal,
+                             const int32_t** d_local_match, const uint8_t** d_outlier);
+
 /* ---- ORBmatcher::SearchByProjection(CurrentFrame, LastFrame, th, bMono) ----
  * match_out[i2] (length cur->n) = index of the LastFrame slot whose MapPoint was assigned to
  * current keypoint i2 (CurrentFrame.mvpMapPoints[i2]), or -1; *nmatches = the return value.

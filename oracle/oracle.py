@@ -242,6 +242,88 @@ def pose_optimization(kps, has_mp, xw, uright, inv_sigma2, fx, fy, cx, cy, bf, T
     return nin, T.reshape(4, 4), out[:n]
 
 
+class KfView(C.Structure):
+    _fields_ = [("n", C.c_int), ("keys", C.c_void_p), ("has", C.c_void_p), ("xw", C.c_void_p)]
+
+
+def local_map_build(cam, kf1, kf2, T_kf1_kf2, seen1, nobs, stride, Tcw_cur, cos_limit=0.5):
+    """The batch chain's local map of a current frame (oc_local_map_build).
+    kf1 / kf2: mapframe_from_extraction dicts of frames f-1 / f-2 (kf2 may be None).  Returns the
+    LOCALMAP_FIELDS arrays over 2*stride slots ([0, stride) KF2, [stride, 2 stride) KF1) plus
+    "xw" (2*stride, 3) world positions (valid where in view)."""
+    M = 2 * stride
+    arrs = {}
+    views = []
+    for kf in (kf1, kf2):
+        if kf is None:
+            views.append(None)
+            continue
+        keys = np.ascontiguousarray(kf["keys_un"])
+        has = np.ascontiguousarray(kf["has_mp"], np.uint8)
+        xw = np.ascontiguousarray(kf["xw"], np.float32)
+        arrs[id(kf)] = (keys, has, xw)
+        views.append(KfView(len(keys), keys.ctypes.data, has.ctypes.data, xw.ctypes.data))
+    v1, v2 = views
+    out = dict(in_view=np.zeros(M, np.uint8), proj_x=np.zeros(M, np.float32), proj_y=np.zeros(M, np.float32),
+               proj_xr=np.zeros(M, np.float32), level=np.zeros(M, np.int32), view_cos=np.zeros(M, np.float32),
+               observations=np.zeros(M, np.int32), xw=np.zeros((M, 3), np.float32))
+    seen = np.zeros(stride, np.uint8) if seen1 is None else np.ascontiguousarray(seen1, np.uint8)
+    T21 = np.ascontiguousarray(T_kf1_kf2 if T_kf1_kf2 is not None else np.eye(4), np.float32)
+    Tc = np.ascontiguousarray(Tcw_cur, np.float32)
+    nin = lib().oc_local_map_build(C.byref(cam), C.byref(v2) if v2 is not None else None, ptr(T21), C.byref(v1),
+                                   ptr(seen), int(nobs), int(stride), ptr(Tc), C.c_float(cos_limit),
+                                   ptr(out["in_view"]), ptr(out["proj_x"]), ptr(out["proj_y"]), ptr(out["proj_xr"]),
+                                   ptr(out["level"]), ptr(out["view_cos"]), ptr(out["observations"]), ptr(out["xw"]))
+    desc = np.zeros((M, 32), np.uint8)
+    if kf2 is not None:
+        desc[:len(kf2["mp_desc"])] = kf2["mp_desc"]
+    desc[stride:stride + len(kf1["mp_desc"])] = kf1["mp_desc"]
+    out["descriptor"] = desc
+    out["n_in_view"] = nin
+    return out
+
+
+def track_frame(cam, isg, cur, ur, last, prev2, T_pred, T_last, stride, nobs=2, th=15.0, lth=3.0, nnratio=0.8,
+                fx=0.0, fy=0.0, cx=0.0, cy=0.0, bf=0.0):
+    """Tracking::Track for one RGB-D frame as the batch chain runs it (BASELINE configs[4]):
+    TrackWithMotionModel (SearchByProjection th, retry 2 th below 20 matches, PoseOptimization,
+    outlier discard, nmatchesMap >= 10; Tracking.cc:933-994) then TrackLocalMap (local map of
+    KeyFrames f-1 = `last` and f-2 = `prev2`, SearchLocalPoints, PoseOptimization, inliers >= 30;
+    :996-1047, 1222-1272).  last / prev2: mapframe_from_extraction dicts (world = last's camera;
+    prev2 placed by T_last, frame f-1's pose relative to f-2).  cur: dict(kps, desc), ur its
+    mvuRight.  Returns a dict of every intermediate result."""
+    I4 = np.eye(4, dtype=np.float32)
+    kps, desc = cur["kps"], cur["desc"]
+    nm, m = search_by_projection(cam, kps, desc, ur, last, T_pred, I4, th)
+    if nm < 20:
+        nm, m = search_by_projection(cam, kps, desc, ur, last, T_pred, I4, 2 * th)
+    res = dict(nmatches=nm, match=m, T1=np.asarray(T_pred, np.float32).copy(), nin1=0, nmatches_map=0,
+               T=np.asarray(T_pred, np.float32).copy(), ninliers=0, nlocal=0, local_match=np.full(len(kps), -1, np.int32),
+               state=0)
+    if nm < 20:
+        return res
+    has = (m >= 0).astype(np.uint8)
+    xw = np.zeros((len(m), 3), np.float32)
+    xw[m >= 0] = last["xw"][m[m >= 0]]
+    nin1, T1, o1 = pose_optimization(kps, has, xw, ur, isg, fx, fy, cx, cy, bf, T_pred)
+    inlier = (has > 0) & (o1 == 0)
+    nmap = int(inlier.sum()) if nobs > 0 else 0
+    res.update(T1=T1, nin1=nin1, outlier1=o1, nmatches_map=nmap, T=T1.copy())
+    if nmap < 10:
+        return res
+    seen = np.zeros(stride, np.uint8)
+    seen[m[m >= 0]] = 1
+    lm = local_map_build(cam, last, prev2, T_last, seen, nobs, stride, T1)
+    cur_obs = np.where(inlier, nobs, -1).astype(np.int32)
+    nl, lmatch = search_local_map(cam, kps, desc, ur, cur_obs, lm, lth, nnratio)
+    has2 = ((lmatch >= 0) | inlier).astype(np.uint8)
+    xw2 = np.where((lmatch >= 0)[:, None], lm["xw"][np.maximum(lmatch, 0)], xw).astype(np.float32)
+    nin2, T2, o2 = pose_optimization(kps, has2, xw2, ur, isg, fx, fy, cx, cy, bf, T1)
+    res.update(local_map=lm, nlocal=nl, local_match=lmatch, has2=has2, T=T2, ninliers=nin2, outlier=o2,
+               state=2 if (nin2 if nobs > 0 else 0) >= 30 else 1)
+    return res
+
+
 def pose_last_stats():
     """(LM iterations, LM trials) of the last pose_optimization call on this thread."""
     it, tr = C.c_int(0), C.c_int(0)

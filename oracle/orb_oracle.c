@@ -1372,6 +1372,119 @@ int oc_search_keyframe(const oc_camera* cam, const oc_curframe* cur, const uint8
     return nmatches;
 }
 
+/* ======================= TrackLocalMap's local map (batch chain) ======================= */
+/* x = R*X + t for a row-major 4x4 T, as the cv::Mat expression R*X + t evaluates it (one gemm
+ * with the addend: small-matrix float products, the addend added in double), the form
+ * oc_search_by_projection uses for Rcw*x3Dw+tcw. */
+static void small_gemm_add(const float* T, const float* X, float* out)
+{
+    for (int k = 0; k < 3; k++) {
+        float t = T[k * 4 + 0] * X[0] + T[k * 4 + 1] * X[1];
+        t = t + T[k * 4 + 2] * X[2];
+        out[k] = (float)((double)t + (double)T[k * 4 + 3]);
+    }
+}
+
+/* cv::norm of a float 3-vector: float components squared and summed in double */
+static double norm3(const float* d)
+{
+    double ss = 0.0;
+    ss += (double)d[0] * (double)d[0];
+    ss += (double)d[1] * (double)d[1];
+    ss += (double)d[2] * (double)d[2];
+    return sqrt(ss);
+}
+
+void oc_mappoint_normal_depth(const oc_camera* cam, const float P[3], const float Ow[3], int octave,
+                              float normal[3], float* max_dist, float* min_dist)
+{
+    const float d[3] = {P[0] - Ow[0], P[1] - Ow[1], P[2] - Ow[2]};
+    const double nd = norm3(d);
+    for (int k = 0; k < 3; k++) normal[k] = (float)((double)d[k] / nd);
+    const float dist = (float)nd;
+    *max_dist = dist * cam->scale[octave];                           /* MapPoint.cc:367 */
+    *min_dist = *max_dist / cam->scale[cam->nlevels - 1];            /* :368 */
+}
+
+int oc_is_in_frustum(const oc_camera* cam, const float Tcw[16], const float P[3], const float Pn[3],
+                     float max_dist, float min_dist, float cos_limit,
+                     float* proj_x, float* proj_y, float* proj_xr, int32_t* level, float* view_cos)
+{
+    const float* T = Tcw;
+    float Pc[3];
+    small_gemm_add(T, P, Pc);                                        /* Pc = mRcw*P + mtcw (:453) */
+    if (Pc[2] < 0.0f) return 0;                                      /* :459-460 */
+    const float invz = 1.0f / Pc[2];                                 /* :463 */
+    const float u = fmaf(cam->fx * Pc[0], invz, cam->cx);            /* :464-465, fused */
+    const float v = fmaf(cam->fy * Pc[1], invz, cam->cy);
+    if (u < cam->min_x || u > cam->max_x) return 0;                  /* :467-470 */
+    if (v < cam->min_y || v > cam->max_y) return 0;
+    /* mOw = -mRcw.t()*mtcw (Frame.cc:442; GEMM_1_T, double accumulation) */
+    float Ow[3];
+    for (int k = 0; k < 3; k++) {
+        double s = (double)T[0 * 4 + k] * T[3] + (double)T[1 * 4 + k] * T[7];
+        s = s + (double)T[2 * 4 + k] * T[11];
+        Ow[k] = (float)(s * -1.0);
+    }
+    const float maxDistance = 1.2f * max_dist;                       /* :473-474, MapPoint.cc:373-383 */
+    const float minDistance = 0.8f * min_dist;
+    const float PO[3] = {P[0] - Ow[0], P[1] - Ow[1], P[2] - Ow[2]};  /* :475 */
+    const float dist = (float)norm3(PO);                             /* :476 */
+    if (dist < minDistance || dist > maxDistance) return 0;          /* :478-479 */
+    /* PO.dot(Pn) / dist: Mat::dot of floats accumulates in double (:484) */
+    double dot = 0.0;
+    dot += (double)PO[0] * (double)Pn[0];
+    dot += (double)PO[1] * (double)Pn[1];
+    dot += (double)PO[2] * (double)Pn[2];
+    const float viewCos = (float)(dot / (double)dist);
+    if (viewCos < cos_limit) return 0;                               /* :486-487 */
+    const float log_sf = cam->nlevels > 1 ? canon_logf(cam->scale[1]) : 1.0f;
+    *level = predict_scale(max_dist, dist, log_sf, cam->nlevels);   /* :490 */
+    *proj_x = u;                                                     /* :493-498 */
+    *proj_xr = fmaf(-cam->bf, invz, u);                              /* u - mbf*invz, fused */
+    *proj_y = v;
+    *view_cos = viewCos;
+    return 1;
+}
+
+int oc_local_map_build(const oc_camera* cam, const oc_kfview* kf2, const float T_kf1_kf2[16], const oc_kfview* kf1,
+                       const uint8_t* seen1, int32_t nobs, int stride, const float Tcw_cur[16], float cos_limit,
+                       uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr, int32_t* level,
+                       float* view_cos, int32_t* nobs_out, float* xw_out)
+{
+    int nin = 0;
+    for (int q = 0; q < 2 * stride; q++) {
+        in_view[q] = 0;
+        level[q] = 0;
+        nobs_out[q] = nobs;
+        const int second = q >= stride;
+        const int j = second ? q - stride : q;
+        const oc_kfview* kf = second ? kf1 : kf2;
+        if (!kf || j >= kf->n || !kf->has[j]) continue;
+        if (second && seen1 && seen1[j]) continue;                   /* Tracking.cc:1249-1250 */
+        float P[3], Ow[3];
+        const float* X = &kf->xw[3 * j];
+        if (second) {                                                /* KF1 is the world frame */
+            P[0] = X[0]; P[1] = X[1]; P[2] = X[2];
+            Ow[0] = Ow[1] = Ow[2] = 0.0f;
+        } else {                                                     /* UnprojectStereo with KF2's Twc */
+            small_gemm_add(T_kf1_kf2, X, P);
+            Ow[0] = T_kf1_kf2[3]; Ow[1] = T_kf1_kf2[7]; Ow[2] = T_kf1_kf2[11];
+        }
+        float Pn[3], maxd, mind;
+        oc_mappoint_normal_depth(cam, P, Ow, kf->keys[j].octave, Pn, &maxd, &mind);
+        xw_out[3 * q + 0] = P[0]; xw_out[3 * q + 1] = P[1]; xw_out[3 * q + 2] = P[2];
+        int32_t lvl;
+        float px, py, pxr, vc;
+        if (oc_is_in_frustum(cam, Tcw_cur, P, Pn, maxd, mind, cos_limit, &px, &py, &pxr, &lvl, &vc)) {
+            in_view[q] = 1;
+            proj_x[q] = px; proj_y[q] = py; proj_xr[q] = pxr; level[q] = lvl; view_cos[q] = vc;
+            nin++;
+        }
+    }
+    return nin;
+}
+
 /* ======================= Optimizer::PoseOptimization (canonical g2o) ======================= */
 /* SE3Quat as g2o holds it: unit quaternion (w, x, y, z) and translation, doubles.  Every
  * operation below has a fixed evaluation order; the HIP kernel (csrc/coeb_pose.hip) performs

@@ -192,6 +192,34 @@ int oc_search_keyframe(const oc_camera* cam, const oc_curframe* cur, const uint8
                        const oc_kfpoints* kf, const float Tcw[16], float th, int orb_dist, int check_ori,
                        int32_t* match_out);
 
+/* ---- Tracking::TrackLocalMap's local map in the batch chain ----
+ * A MapPoint observed by one KeyFrame with camera centre Ow, from a keypoint of that octave
+ * (MapPoint::UpdateNormalAndDepth with one observation, MapPoint.cc:330-371). */
+void oc_mappoint_normal_depth(const oc_camera* cam, const float P[3], const float Ow[3], int octave,
+                              float normal[3], float* max_dist, float* min_dist);
+/* Frame::isInFrustum(pMP, viewingCosLimit) (Frame.cc:445-501) with MapPoint::PredictScale
+ * (MapPoint.cc:402-417): returns mbTrackInView and, when 1, the mTrack* fields. */
+int oc_is_in_frustum(const oc_camera* cam, const float Tcw[16], const float P[3], const float Pn[3],
+                     float max_dist, float min_dist, float cos_limit,
+                     float* proj_x, float* proj_y, float* proj_xr, int32_t* level, float* view_cos);
+/* A KeyFrame's keypoint slots as the local map reads them */
+typedef struct {
+    int n;
+    const oc_kp* keys;             /* octave of each slot */
+    const uint8_t* has;            /* depth > 0: the slot holds a MapPoint */
+    const float* xw;               /* n x 3, UnprojectStereo in the KeyFrame's own camera frame */
+} oc_kfview;
+/* Local map of the current frame f: slots [0, stride) = KF2 (frame f-2, may be NULL), whose
+ * points are placed in KF1's frame by T_kf1_kf2 (KF1's pose with KF2 as world), slots
+ * [stride, 2 stride) = KF1 (frame f-1, the world frame).  seen1[j]: KF1 slot j was matched by
+ * the motion-model search (mnLastFrameSeen == current, Tracking.cc:979,1237,1249).  Every point
+ * gets Observations() = nobs and goes through isInFrustum(cos_limit) with Tcw_cur; writes the
+ * coeb_localmap arrays (2 stride entries) and each point's world position; returns #in view. */
+int oc_local_map_build(const oc_camera* cam, const oc_kfview* kf2, const float T_kf1_kf2[16], const oc_kfview* kf1,
+                       const uint8_t* seen1, int32_t nobs, int stride, const float Tcw_cur[16], float cos_limit,
+                       uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr, int32_t* level,
+                       float* view_cos, int32_t* nobs_out, float* xw_out);
+
 /* Optimizer::PoseOptimization(Frame*) (Optimizer.cc:239-451): the frame's matched keypoints
  * and their map points.  fx..bf are the Frame's intrinsics. */
 typedef struct {

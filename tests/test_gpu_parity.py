@@ -860,3 +860,123 @@ def test_undistort_keypoints(ctx, oracle_mod, ex, pair):
         assert got.tobytes() == ref.tobytes(), dist
     assert len(coeb_front.UndistortKeyPoints(ctx, k[:0], cam, (0.1, 0, 0, 0, 0))) == 0
 
+
+
+def _chain_oracle(oracle_mod, ex, frames, boxes, Tpred, stride, isg, nkf=2):
+    """The configs[4] loop frame by frame on the oracle: Frame ctor (T_M from the previous frame,
+    blur flags, masked extraction) when boxes is given, else the plain extraction; then
+    track_frame (motion model + TrackLocalMap)."""
+    F, H, W = frames.shape
+    depth = synth.make_depth(W, H)
+    cam_o = oracle_mod.camera(ex, W, H, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    ext, res = [], [None]
+    for f in range(F):
+        if boxes is None:
+            ext.append(ex.extract(frames[f]))
+            continue
+        if f == 0:
+            tm, bl = np.zeros((0, 2), np.float32), np.zeros(len(boxes[0]), np.int32)
+        else:
+            tm = oracle_mod.process_moving_object(frames[f - 1], frames[f])
+            tm = np.zeros((0, 2), np.float32) if tm is None else tm
+            bl, _ = oracle_mod.blur_flags(frames[f], boxes[f])
+        ext.append(ex.extract(frames[f], boxes[f], tm, bl))
+    mfs = [oracle_mod.mapframe_from_extraction(e["kps"], e["desc"], depth, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX,
+                                               synth.TUM_CY, synth.TUM_BF) for e in ext]
+    for f in range(1, F):
+        ur, _ = oracle_mod.stereo_from_rgbd(ext[f]["kps"], depth, synth.TUM_BF)
+        prev2 = mfs[f - 2] if (nkf >= 2 and f >= 2) else None
+        T_last = res[f - 1]["T1"] if f >= 2 else np.eye(4, dtype=np.float32)
+        res.append(oracle_mod.track_frame(cam_o, isg, ext[f], ur, mfs[f - 1], prev2, Tpred[f], T_last, stride,
+                                          fx=synth.TUM_FX, fy=synth.TUM_FY, cx=synth.TUM_CX, cy=synth.TUM_CY,
+                                          bf=synth.TUM_BF))
+    return ext, res
+
+
+def _check_chain(bp, ext, res, F):
+    out, matches, nms = bp.results()
+    T1, nin1, _ = bp.pose_results()
+    tr = bp.track_results()
+    states = []
+    for f in range(1, F):
+        r = res[f]
+        assert np.array_equal(out[f][1], ext[f]["desc"]), f
+        assert nms[f] == r["nmatches"] and np.array_equal(matches[f], r["match"]), f
+        assert np.array_equal(T1[f].view(np.uint32), r["T1"].view(np.uint32)), f
+        assert nin1[f] == r["nin1"], f
+        assert tr["state"][f] == r["state"], (f, tr["state"][f], r["state"])
+        states.append(r["state"])
+        if r["nmatches"] >= 20:
+            assert tr["nmatches_map"][f] == r["nmatches_map"], f
+        if r["state"] == 0:
+            assert tr["ninliers"][f] == 0 and np.array_equal(tr["T"][f].view(np.uint32), r["T1"].view(np.uint32)), f
+            continue
+        assert tr["nlocal"][f] == r["nlocal"], (f, tr["nlocal"][f], r["nlocal"])
+        assert np.array_equal(tr["local_match"][f], r["local_match"]), f
+        assert tr["ninliers"][f] == r["ninliers"], (f, tr["ninliers"][f], r["ninliers"])
+        assert np.array_equal(tr["T"][f].view(np.uint32), r["T"].view(np.uint32)), f
+        h2 = r["has2"] > 0
+        assert np.array_equal(tr["outlier"][f][h2], r["outlier"][h2]), f
+    return states, tr
+
+
+def test_batch_track_local_map_matches_oracle(oracle_mod, ex):
+    """BASELINE configs[4] as the loop: TrackWithMotionModel (match + retry + PoseOptimization +
+    outlier discard) then TrackLocalMap (local map of KeyFrames f-1, f-2 through isInFrustum,
+    SearchByProjection th 3, second PoseOptimization) for every frame of the device batch,
+    against the oracle frame by frame (Tracking.cc:933-1047, 1222-1272).  Frame 3's prediction
+    is 180 degrees off: the motion model fails there, and frame 4's local map still uses frame
+    3's (unoptimised) pose for KeyFrame 2."""
+    from coeb_front.pipeline import BatchPipeline
+    F = 7
+    fr = synth.make_frames(640, 480, F, seed=4242)
+    Tcw = np.stack([synth.motion_pose()] * F)
+    Tcw[3] = synth.rotated_pose(180.0, axis=1, t=(0, 0, 0))
+    bp = BatchPipeline(640, 480, F)
+    try:
+        bp.load(fr, Tcw=Tcw)
+        bp.run(track=True)
+        bp.synchronize()
+        stride = bp.ctx.batch_results()[3]
+        isg = np.array(bp.ctx.tables().inv_sigma2[:8], np.float32)
+        ext, res = _chain_oracle(oracle_mod, ex, fr, None, Tcw, stride, isg)
+        states, tr = _check_chain(bp, ext, res, F)
+        assert states.count(2) >= F - 3 and states[2] == 0                  # frame 3 lost
+        assert sum(tr["nlocal"][f] for f in range(1, F) if states[f - 1] == 2) > 0
+        # pipelined: three back-to-back steps leave the single-step results
+        for _ in range(3):
+            bp.run(track=True)
+        tr2 = bp.track_results()
+        assert tr2["ninliers"] == tr["ninliers"] and tr2["nlocal"] == tr["nlocal"]
+        assert np.array_equal(tr2["T"][1:].view(np.uint32), tr["T"][1:].view(np.uint32))
+    finally:
+        bp.close()
+
+
+def test_batch_grab_rgbd_loop_matches_oracle(oracle_mod, ex):
+    """The whole configs[4] loop on a moving-object sequence: Frame ctor on the device (T_M from
+    ProcessMovingObject of the previous frame, blur flags, masked extraction), then the motion
+    model and TrackLocalMap, each frame against the oracle.  The nearer panels move 2-3x the
+    camera prediction, so the optimisations see real outliers.  nkf = 1 (local map = KeyFrame
+    f-1 only) is checked on the same batch."""
+    from coeb_front.pipeline import BatchPipeline
+    F = 6
+    frames, obj = synth.moving_object_sequence(640, 480, F, seed=8)
+    boxes = [obj[f][None, :] for f in range(F)]
+    Tcw = np.stack([synth.motion_pose()] * F)
+    bp = BatchPipeline(640, 480, F)
+    try:
+        bp.load(frames, Tcw=Tcw)
+        bp.set_frame_boxes(boxes)
+        for nkf in (2, 1):
+            bp.run(frame=True, track=True, nkf=nkf)
+            bp.synchronize()
+            stride = bp.ctx.batch_results()[3]
+            isg = np.array(bp.ctx.tables().inv_sigma2[:8], np.float32)
+            ext, res = _chain_oracle(oracle_mod, ex, frames, boxes, Tcw, stride, isg, nkf=nkf)
+            states, tr = _check_chain(bp, ext, res, F)
+            assert states.count(2) >= F - 2, states
+            assert any(r["nlocal"] > 0 for r in res[1:])
+            assert any(((r["outlier"] > 0) & (r["has2"] > 0)).any() for r in res[1:] if r["state"] > 0)
+    finally:
+        bp.close()

@@ -633,3 +633,89 @@ def test_resize_linear_simd_prefix_scalar_tail(oracle_mod):
         assert dw - 4 <= tail <= dw
     # the scalar tail rounds differently from the SIMD form on some inputs
     assert any(oracle_mod.lib().oc_resize_simd_end(w) < w for w in (533, 444, 370, 309))
+
+
+def _frustum(O, cam, T, P, Pn, maxd, mind):
+    import ctypes as C
+    px, py, pxr, vc = C.c_float(), C.c_float(), C.c_float(), C.c_float()
+    lvl = C.c_int32()
+    f3 = lambda v: np.ascontiguousarray(v, np.float32)   # noqa: E731
+    P, Pn, T = f3(P), f3(Pn), f3(T)
+    ok = O.lib().oc_is_in_frustum(C.byref(cam), O.ptr(T), O.ptr(P), O.ptr(Pn), C.c_float(maxd), C.c_float(mind),
+                                  C.c_float(0.5), C.byref(px), C.byref(py), C.byref(pxr), C.byref(lvl), C.byref(vc))
+    return ok, px.value, py.value, pxr.value, lvl.value, vc.value
+
+
+def test_is_in_frustum_kat(oracle_mod):
+    """Frame::isInFrustum(pMP, 0.5) (Frame.cc:445-501) + MapPoint::PredictScale (MapPoint.cc:
+    402-417) on hand-built cases: each rejection branch, and the projection / level / view
+    cosine of an accepted point against float64 arithmetic."""
+    from coeb_front import synth
+    O = oracle_mod
+    ex = O.Extractor()
+    cam = O.camera(ex, 640, 480, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    T = np.eye(4, dtype=np.float32)
+    T[:3, 3] = (0.01, -0.02, 0.05)
+    P = np.array([0.1, -0.05, 2.0], np.float32)
+    Oc = -T[:3, :3].T @ T[:3, 3]
+    d = np.linalg.norm(P.astype(np.float64) - Oc)
+    Pn = (P - Oc) / d
+    ok, u, v, ur, lvl, vc = _frustum(O, cam, T, P, Pn, d * 1.3, d * 1.3 / 3.58)
+    Pc = P.astype(np.float64) + T[:3, 3]
+    assert ok == 1
+    assert abs(u - (synth.TUM_FX * Pc[0] / Pc[2] + synth.TUM_CX)) < 1e-3
+    assert abs(v - (synth.TUM_FY * Pc[1] / Pc[2] + synth.TUM_CY)) < 1e-3
+    assert abs(ur - (u - synth.TUM_BF / Pc[2])) < 1e-3
+    assert lvl == math.ceil(math.log(1.3) / math.log(1.2)) == 2
+    assert abs(vc - 1.0) < 1e-6
+    assert _frustum(O, cam, T, P, Pn, d * 1.3 * 1.2 ** 6, d)[4] == 7          # clamped to the pyramid
+    assert _frustum(O, cam, T, P, Pn, d * 0.9, d * 0.5)[4] == 0                # ratio < 1 -> level 0
+    assert _frustum(O, cam, T, P * np.float32(-1), -Pn, d * 1.3, d * 0.5)[0] == 0    # behind the camera
+    assert _frustum(O, cam, T, np.float32([5, 0, 2]), Pn, 10, 0.1)[0] == 0           # outside the image
+    side = np.cross(Pn, [0, 1, 0]).astype(np.float32)
+    side /= np.linalg.norm(side)
+    assert _frustum(O, cam, T, P, side, d * 1.3, d * 0.5)[0] == 0                    # view angle > 60 deg
+    tilt = (np.cos(np.radians(55)) * Pn + np.sin(np.radians(55)) * side).astype(np.float32)
+    assert _frustum(O, cam, T, P, tilt, d * 1.3, d * 0.5)[0] == 1                    # 55 deg still seen
+    assert _frustum(O, cam, T, P, Pn, d / 1.25, d / 4)[0] == 0                       # beyond 1.2 * maxd
+    assert _frustum(O, cam, T, P, Pn, d * 3, d * 1.3)[0] == 0                        # inside 0.8 * mind
+
+
+def test_oracle_track_chain_properties(oracle_mod):
+    """The configs[4] loop on the oracle (track_frame: motion model + TrackLocalMap) over a
+    plain synthetic sequence: every frame tracked, the local map contributes matches, the
+    second optimisation keeps more inliers than the first, and a 180-degree prediction loses
+    the frame (state 0) without disturbing the next one."""
+    from coeb_front import synth
+    O = oracle_mod
+    ex = O.Extractor()
+    isg = np.array(ex.p.inv_sigma2[:8], np.float32)
+    F, stride = 6, 1256
+    fr = synth.make_frames(640, 480, F, seed=4242)
+    depth = synth.make_depth(640, 480)
+    cam = O.camera(ex, 640, 480, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    Tcw = np.stack([synth.motion_pose()] * F)
+    Tcw[3] = synth.rotated_pose(180.0, axis=1, t=(0, 0, 0))
+    ext = [ex.extract(f) for f in fr]
+    mfs = [O.mapframe_from_extraction(e["kps"], e["desc"], depth, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX,
+                                      synth.TUM_CY, synth.TUM_BF) for e in ext]
+    res = [None]
+    for f in range(1, F):
+        ur, _ = O.stereo_from_rgbd(ext[f]["kps"], depth, synth.TUM_BF)
+        res.append(O.track_frame(cam, isg, ext[f], ur, mfs[f - 1], mfs[f - 2] if f >= 2 else None, Tcw[f],
+                                 res[f - 1]["T1"] if f >= 2 else np.eye(4, dtype=np.float32), stride,
+                                 fx=synth.TUM_FX, fy=synth.TUM_FY, cx=synth.TUM_CX, cy=synth.TUM_CY, bf=synth.TUM_BF))
+    assert [r["state"] for r in res[1:]] == [2, 2, 0, 2, 2]
+    for f in (1, 2, 4, 5):
+        r = res[f]
+        lm = r["local_map"]
+        assert lm["n_in_view"] == int(lm["in_view"].sum()) > 0
+        assert r["nlocal"] > 0 and r["ninliers"] > r["nin1"]
+        # local matches land on keypoints without a kept motion-model MapPoint (Observations() > 0)
+        kept = (r["match"] >= 0) & (r["outlier1"] == 0)
+        assert not ((r["local_match"] >= 0) & kept).any()
+        # KF1 points the motion model matched are not in the local map (mnLastFrameSeen)
+        assert not lm["in_view"][stride + r["match"][r["match"] >= 0]].any()
+        assert np.all(lm["level"][lm["in_view"] > 0] < 8)
+    assert res[1]["local_map"]["in_view"][:stride].sum() == 0          # frame 1 has no KeyFrame f-2
+    assert res[3]["nlocal"] == 0 and res[3]["ninliers"] == 0
