@@ -36,10 +36,40 @@ CONFIGS = {
     "C": dict(w=640, h=480, nfeatures=1000, dyn=True,
               workload="640x480, 1000 kp, YOLO-bbox dynamic mask (2 boxes, 60 T_M points, blur_flag [0,1]) + "
                        "depth association (ComputeStereoFromRGBD) + match to prev frame (BASELINE configs[2])"),
-    "D": dict(w=640, h=480, nfeatures=1000, pose=True,
-              workload="640x480, 1000 kp, TrackWithMotionModel step: extract + match to prev frame + "
-                       "Optimizer::PoseOptimization (4 x 10 LM iterations) per frame (BASELINE configs[4])"),
+    "D": dict(w=640, h=480, nfeatures=1000, chain=True,
+              workload="640x480, 1000 kp, the full Tracking::GrabImageRGBD loop per frame (BASELINE configs[4]): "
+                       "RGB + 16U depth conversion, Frame ctor (ProcessMovingObject T_M from the previous frame, "
+                       "YOLO-box blur flags, dynamic mask, ORB extraction), TrackWithMotionModel (SearchByProjection "
+                       "th 15 + retry, PoseOptimization, outlier discard), TrackLocalMap (local map of KeyFrames f-1 "
+                       "and f-2 through isInFrustum, SearchByProjection th 3, PoseOptimization)",
+              data="synthetic tracking sequence (TUM-like rectangles + noise, (+2,+1) px/frame camera motion, a "
+                   "bouncing 120x160 textured object with its YOLO box; RGB = gray x 3, 16U depth 10000 = 2 m)"),
 }
+DEPTH_MAP_FACTOR = 1.0 / 5000.0     # mDepthMapFactor = 1 / DepthMapFactor (TUM yaml: 5000)
+
+
+def step_kwargs(cfg):
+    """BatchPipeline.run() arguments of one step of `cfg`."""
+    if cfg.get("chain"):
+        return dict(rgbd=True, frame=True, track=True)
+    return dict(pose=bool(cfg.get("pose")))
+
+
+def load_batch(bp, cfg, w, h, F, first):
+    """Synthetic input of `cfg` for global frames first .. first+F-1, resident on the device."""
+    from coeb_front import synth
+    Tcw = np.stack([synth.motion_pose()] * F)
+    if cfg.get("chain"):
+        gray, boxes = synth.tracking_sequence(w, h, F, first=first)
+        rgb, dep = synth.rgbd_from_gray(gray)
+        bp.load_rgbd(rgb, dep, DEPTH_MAP_FACTOR, Tcw=Tcw)
+        bp.set_frame_boxes(boxes[:, None, :])
+        bp.host_frames = gray
+        return gray, Tcw
+    frames = synth.make_frames(w, h, F, seed=1000, first=first)    # global frames first .. first+F-1
+    dyn = dyn_batch(w, h, F, first) if cfg.get("dyn") else None
+    bp.load(frames, Tcw=Tcw, dyn=dyn)
+    return frames, Tcw
 
 
 def dyn_batch(w, h, F, seed0=0):
@@ -164,6 +194,113 @@ def cpu_baseline(cfg, seconds=12.0, min_frames=30):
                       "ms/frame" % (len(times), w, h, cpus[0], med * 1e3))
     out.update(info)
     out["all_cores"] = cpu_baseline_parallel(O, cfg, frames, depth, cam, len(cpus))
+    return out
+
+
+class ChainCpu:
+    """The configs[4] loop on the oracle for one frame sequence (the CPU baseline of config D):
+    per frame GrabImageRGBD's conversions, the Frame ctor (ProcessMovingObject against the
+    previous gray frame, blur flags, masked extraction), ComputeStereoFromRGBD and track_frame
+    (motion model + TrackLocalMap), and the frame's map snapshot for the next one."""
+
+    def __init__(self, O, cfg, rgb, dep, boxes):
+        from coeb_front import synth
+        self.O, self.rgb, self.dep, self.boxes = O, rgb, dep, boxes
+        self.ex = O.Extractor(cfg["nfeatures"], 1.2, 8, 20, 7)
+        w, h = cfg["w"], cfg["h"]
+        self.cam = O.camera(self.ex, w, h, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+        self.isg = np.array(self.ex.p.inv_sigma2[:8], np.float32)
+        self.stride = 8 * cfg["nfeatures"] + 256
+        self.Tp = synth.motion_pose()
+        self.state = None
+
+    def step(self, i):
+        from coeb_front import synth
+        O = self.O
+        g = O.image_to_gray(self.rgb[i])
+        d = O.depth_to_float(self.dep[i], np.float32(DEPTH_MAP_FACTOR))
+        b = self.boxes[i][None, :]
+        if self.state is None:
+            tm, bl = np.zeros((0, 2), np.float32), np.zeros(1, np.int32)
+        else:
+            tm = O.process_moving_object(self.state["gray"], g)
+            tm = np.zeros((0, 2), np.float32) if tm is None else tm
+            bl, _ = O.blur_flags(g, b)
+        r = self.ex.extract(g, b, tm, bl)
+        mf = O.mapframe_from_extraction(r["kps"], r["desc"], d, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX,
+                                        synth.TUM_CY, synth.TUM_BF)
+        T1 = np.eye(4, dtype=np.float32)
+        if self.state is not None:
+            ur, _ = O.stereo_from_rgbd(r["kps"], d, synth.TUM_BF)
+            res = O.track_frame(self.cam, self.isg, r, ur, self.state["mf"], self.state["mf_prev"], self.Tp,
+                                self.state["T1"], self.stride, fx=synth.TUM_FX, fy=synth.TUM_FY, cx=synth.TUM_CX,
+                                cy=synth.TUM_CY, bf=synth.TUM_BF)
+            T1 = res["T1"]
+        self.state = dict(gray=g, mf=mf, mf_prev=self.state["mf"] if self.state else None, T1=T1)
+
+
+def cpu_chain_baseline(cfg, seconds=15.0, min_frames=20):
+    """Config D's CPU baseline: ChainCpu (the oracle's full GrabImageRGBD loop) on consecutive
+    frames of the same synthetic sequence, single thread pinned to one CPU, and all host cores
+    frame-sequence-parallel (one sequence slice per thread)."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"])
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from coeb_front import synth
+    O.LIB = os.path.join(ROOT, "oracle", "liborb_oracle_native.so")
+    O._lib = None
+    info, cpus = host_cpu_info()
+    w, h = cfg["w"], cfg["h"]
+    nfr = 48
+    gray, boxes = synth.tracking_sequence(w, h, nfr, first=0)
+    rgb, dep = synth.rgbd_from_gray(gray)
+    os.sched_setaffinity(0, {cpus[0]})
+    try:
+        cl = ChainCpu(O, cfg, rgb, dep, boxes)
+        for i in range(3):
+            cl.step(i)
+        times = []
+        t_end = time.perf_counter() + seconds
+        i = 3
+        while (time.perf_counter() < t_end or len(times) < min_frames) and i < nfr:
+            t0 = time.perf_counter()
+            cl.step(i)
+            times.append(time.perf_counter() - t0)
+            i += 1
+    finally:
+        os.sched_setaffinity(0, set(cpus))
+    med = float(np.median(times))
+    out = dict(value=round(1.0 / med, 3), unit="frames/s", cores=1, kind="port",
+               sample="%d consecutive %dx%d frames of the synthetic tracking sequence, oracle (-O3 -march=native) "
+                      "single thread pinned to CPU %d: the full GrabImageRGBD loop per frame (conversions, "
+                      "ProcessMovingObject, blur flags, masked extract, stereo, motion model, TrackLocalMap); median "
+                      "%.2f ms/frame" % (len(times), w, h, cpus[0], med * 1e3))
+    out.update(info)
+    nthr = len(cpus)
+    import threading
+    done = [0] * nthr
+    t_stop = [0.0]
+
+    def work(t):
+        cl = ChainCpu(O, cfg, rgb, dep, boxes)
+        j = (5 * t) % nfr
+        while time.perf_counter() < t_stop[0]:
+            cl.step(j)
+            done[t] += 1
+            j = (j + 1) % nfr
+            if j == 0:
+                cl.state = None                       # a new sequence: no predecessor
+    t0 = time.perf_counter()
+    t_stop[0] = t0 + 8.0
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(nthr)]
+    for x in ths:
+        x.start()
+    for x in ths:
+        x.join()
+    dt = time.perf_counter() - t0
+    out["all_cores"] = dict(value=round(sum(done) / dt, 3), unit="frames/s", cores=nthr, kind="port",
+                            sample="%d threads (nproc) x 8 s, one oracle chain per thread on its own slice of the "
+                                   "sequence; %d frames" % (nthr, sum(done)))
     return out
 
 
@@ -309,7 +446,13 @@ class DryRunPipeline:
     def load(self, frames, **kw):
         self.F = len(frames)
 
-    def run(self, pose=False):
+    def load_rgbd(self, images, depth, factor, **kw):
+        self.F = len(images)
+
+    def set_frame_boxes(self, boxes):
+        pass
+
+    def run(self, **kw):
         time.sleep(0.002 * (1 + self.rank))   # ranks finish at different times: max must win
 
     def synchronize(self):
@@ -506,39 +649,47 @@ def rank_main(ranks, args):
     G = args.global_frames if strong else args.batch * world       # matched frames per step, all ranks
     if G < world:
         raise SystemExit("bench.py: %d matched frames cannot be split over %d GPUs" % (G, world))
-    first, F, nmatched = shard_frames(G, world, rank)
-    frames = synth.make_frames(w, h, F, seed=1000, first=first)    # global frames first .. first+F-1
-    Tcw = np.stack([synth.motion_pose()] * F)
+    chain = bool(cfg.get("chain"))
+    halo = 3 if chain else 1
+    first, F, nmatched = shard_frames(G, world, rank, halo=halo)
     if args.dry_run:
         bp = DryRunPipeline(rank)
     else:
         from coeb_front.pipeline import BatchPipeline
         bp = BatchPipeline(w, h, F, nfeatures=cfg["nfeatures"], device=local_rank)
     bp.ctx.set_batch_streams(args.streams)
-    dyn = dyn_batch(w, h, F, first) if cfg.get("dyn") else None
-    bp.load(frames, Tcw=Tcw, dyn=dyn)
+    frames, Tcw = load_batch(bp, cfg, w, h, F, first)
     del frames
     # every rank states what it covers; the sum must be the whole sequence
     covered = int(ranks.sum(nmatched))
     if covered != G:
         raise RuntimeError("shards cover %d of %d matched frames" % (covered, G))
-    per_rank = [shard_frames(G, world, r)[2] for r in range(world)]
+    per_rank = [shard_frames(G, world, r, halo=halo)[2] for r in range(world)]
 
-    pose = bool(cfg.get("pose"))
+    kw = step_kwargs(cfg)
     for _ in range(args.warmup):
-        bp.run(pose=pose)
+        bp.run(**kw)
     bp.synchronize()
     out, matches, nms = bp.results()
-    nkp = float(np.mean([len(o[0]) for o in out[1:]]))
-    nmatch = float(np.mean(nms[1:]))
+    c0 = F - nmatched                                               # first counted frame of the batch
+    nkp = float(np.mean([len(o[0]) for o in out[c0:]]))
+    nmatch = float(np.mean(nms[c0:]))
     ncand = int(bp.ctx.debug_read("cand_n", 1).view(np.int32).sum())
+    tracking = None
+    if chain and not args.dry_run:
+        tr = bp.track_results()
+        st = tr["state"][c0:]
+        tracking = dict(frames=len(st), tracked=st.count(2), local_map_failed=st.count(1), motion_model_failed=st.count(0),
+                        inliers_per_frame=round(float(np.mean(tr["ninliers"][c0:])), 1),
+                        local_map_matches_per_frame=round(float(np.mean(tr["nlocal"][c0:])), 1),
+                        motion_model_matches_map_per_frame=round(float(np.mean(tr["nmatches_map"][c0:])), 1))
 
     # timed region: no instrumentation (HIP event pairs around every launch cost ~10 us each)
     ranks.barrier()
     bp.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        bp.run(pose=pose)
+        bp.run(**kw)
     bp.synchronize()
     t1 = time.perf_counter()
     ranks.barrier()
@@ -554,7 +705,7 @@ def rank_main(ranks, args):
         bp.ctx.profile(True)
         bp.ctx.profile_reset()
         for _ in range(prof_steps):
-            bp.run(pose=pose)
+            bp.run(**kw)
         bp.synchronize()
         prof = bp.ctx.profile_read()
         bp.ctx.profile(False)
@@ -590,10 +741,10 @@ def rank_main(ranks, args):
         line = dict(metric=METRIC, value=round(value, 2), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(ms_per_step, 4), higher_is_better=True,
                     scaling="strong" if strong else "weak", vs_baseline=None, dtype="u8",
-                    data="synthetic (TUM-like rectangles + noise, (+2,+1) px/frame, Z=2 m)",
+                    data=cfg.get("data", "synthetic (TUM-like rectangles + noise, (+2,+1) px/frame, Z=2 m)"),
                     config=dict(workload=cfg["workload"], width=w, height=h, nfeatures=cfg["nfeatures"],
                                 nlevels=8, matched_frames_per_step=G, frames_per_rank=per_rank,
-                                halo_frames_per_rank=1, streams_per_gpu=args.streams,
+                                halo_frames_per_rank=halo, streams_per_gpu=args.streams,
                                 ranks="threads" if isinstance(ranks, _thread_rank_type()) else
                                       ("processes" if world > 1 else "single"),
                                 parallelism="frame-sharded x%d (no collectives)" % world),
@@ -605,15 +756,17 @@ def rank_main(ranks, args):
                     kernels_profiled_steps=prof_steps,
                     keypoints_per_frame=round(nkp, 1), matches_per_frame=round(nmatch, 1),
                     pcie_inclusive=None)
+        if tracking is not None:
+            line["tracking"] = tracking
         if not args.no_extras and world == 1 and not args.dry_run:
             line["extras"] = extras_timing(bp.ctx, out, w, h)
             line["extras"]["single_frame"] = single_frame_timing(w, h)
-            if not cfg.get("dyn") and not cfg.get("pose"):
+            if not cfg.get("dyn") and not cfg.get("pose") and not chain:
                 line["extras"]["config5_tracking"] = config5_timing(bp, nmatched)
                 line["extras"]["config3_dynamic_mask"] = config3_timing(bp, synth.make_frames(w, h, F, seed=1000),
                                                                         Tcw, w, h, nmatched)
         if not args.no_cpu_baseline and world == 1 and not args.dry_run:
-            cb = cpu_baseline(cfg)
+            cb = cpu_chain_baseline(cfg) if chain else cpu_baseline(cfg)
             if "extras" in line:
                 cb["extras_ms_per_call"] = cpu_extras(out, w, h)
             line["cpu_baseline"] = cb
@@ -623,7 +776,7 @@ def rank_main(ranks, args):
     host_frames, host_tcw = getattr(bp, "host_frames", None), getattr(bp, "Tcw", None)
     bp.close()
     e2e = None
-    if not args.no_e2e and not args.dry_run:
+    if not args.no_e2e and not args.dry_run and not chain:
         e2e = e2e_timing(host_frames, host_tcw, ranks, G, 30, cfg, local_rank)
     if rank == 0:
         line["pcie_inclusive"] = e2e

@@ -35,6 +35,7 @@ KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle"
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 assert KEYPOINT_DTYPE.itemsize == 28
 MAX_LEVELS = 16
+DEPTH_U16, DEPTH_F32 = 0, 1          # COEB_DEPTH_U16 / COEB_DEPTH_F32
 
 # exported symbols of include/coeb_front.h (checked by tests/test_capi_symbols.py)
 ABI_SYMBOLS = [
@@ -52,7 +53,7 @@ ABI_SYMBOLS = [
     "coeb_host_alloc", "coeb_host_free", "coeb_memcpy_h2d_async", "coeb_memcpy_d2h_async",
     "coeb_copyq_create", "coeb_copyq_destroy", "coeb_copyq_h2d", "coeb_copyq_d2h", "coeb_copyq_after_ctx",
     "coeb_ctx_after_copyq", "coeb_copyq_synchronize", "coeb_frame_batch_device", "coeb_batch_frame_results",
-    "coeb_track_local_map_batch_device", "coeb_batch_track_results",
+    "coeb_track_local_map_batch_device", "coeb_batch_track_results", "coeb_rgbd_preprocess_batch_device",
 ]
 
 
@@ -141,6 +142,8 @@ def lib():
         L.coeb_track_local_map_batch_device.argtypes = [C.c_void_p, C.POINTER(Camera), C.c_int, C.c_int32, C.c_float,
                                                         C.c_float]
         L.coeb_batch_track_results.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 6
+        L.coeb_rgbd_preprocess_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                                        C.c_float, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.coeb_match_lastframe.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(CurFrameC),
                                            C.POINTER(LastFrameC), C.c_void_p, C.c_void_p, C.c_float, C.c_int,
                                            C.c_int, C.c_void_p, C.POINTER(C.c_int)]
@@ -336,6 +339,13 @@ class Context:
         SearchByProjection(th = 3 for RGB-D, Tracking.cc:1264-1270), second PoseOptimization."""
         self.check(lib().coeb_track_local_map_batch_device(self.h, C.byref(cam), nframes, int(nkf), float(th),
                                                            float(nnratio)))
+
+    def rgbd_preprocess_batch_device(self, d_img, channels, rgb_order, d_depth, depth_type, depth_scale, nframes, w, h,
+                                     d_gray, d_depth_out):
+        """GrabImageRGBD's cvtColor + depth convertTo over a packed device batch."""
+        self.check(lib().coeb_rgbd_preprocess_batch_device(self.h, C.c_void_p(d_img), channels, rgb_order,
+                                                           C.c_void_p(d_depth), depth_type, float(depth_scale), nframes,
+                                                           w, h, C.c_void_p(d_gray), C.c_void_p(d_depth_out)))
 
     def batch_track_results(self):
         """Device pointers (Tcw, ninliers, nmatches_map, nlocal, local_match, outlier)."""

@@ -96,15 +96,22 @@ class _ThreadRank:
         pass
 
 
-def shard_frames(total, world, rank):
+def shard_frames(total, world, rank, halo=1):
     """Frames of one rank when a sequence of `total` matched frames is split over `world` ranks.
 
     The sequence has frames 0..total; frame 0 has no predecessor and is not counted, frame j >= 1
     is matched against frame j-1.  Rank r matches the contiguous chunk [lo+1, hi] (`shard` over
-    the matched frames) and also extracts frame lo, its one-frame halo, so every match is local.
-    Returns (first, nextract, nmatched): the rank extracts frames first .. first+nextract-1."""
+    the matched frames) and also extracts the `halo` frames before it, so every dependency is
+    local: 1 for extract + match (frame lo, the LastFrame); the full GrabImageRGBD loop needs 3
+    (the Frame ctor's T_M of frame lo comes from frame lo-1, and TrackLocalMap's KeyFrame f-2 of
+    frame lo+1 is frame lo-1, itself built from frame lo-2).  The counted frames are the last
+    nmatched of the rank's batch.  Returns (first, nextract, nmatched): the rank extracts frames
+    first .. first+nextract-1."""
+    if halo < 1:
+        raise ValueError("halo must be >= 1")
     _, lo, hi = shard(total, world, rank)
-    return lo, hi - lo + 1, hi - lo
+    first = max(lo - (halo - 1), 0)
+    return first, hi - first + 1, hi - lo
 
 
 def shard(total, world, rank):

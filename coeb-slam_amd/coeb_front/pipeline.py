@@ -26,6 +26,7 @@ class BatchPipeline:
         self.dyn = None
         self.host_frames = None
         self.frame_boxes = None      # (boxes, box_off) for run(frame=True)
+        self.raw = None              # (image, channels, rgb_order, depth, depth_type, factor) for run(rgbd=True)
 
     def load(self, frames, depth=None, Tcw=None, dyn=None):
         """frames: (F, H, W) uint8; depth: (F, H, W) float32; Tcw: (F, 4, 4) pose of frame f
@@ -58,7 +59,30 @@ class BatchPipeline:
                         np.asarray(tm_off, np.int32), np.concatenate(blurs))
         self.ctx.synchronize()
 
-    def run(self, match=True, th=15.0, nobs=2, pose=False, frame=False, track=False, nkf=2):
+    def load_rgbd(self, images, depth, depth_factor, rgb_order=1, Tcw=None):
+        """Raw GrabImageRGBD input resident on the device: images (F, H, W[, C]) u8 with C = 1, 3
+        or 4, depth (F, H, W) u16 or f32, mDepthMapFactor = depth_factor (1 / DepthMapFactor);
+        run(rgbd=True) converts them into the batch's gray frames and float depth first."""
+        images = np.ascontiguousarray(images, np.uint8)
+        ch = 1 if images.ndim == 3 else images.shape[3]
+        assert images.shape[:3] == (self.F, self.H, self.W)
+        depth = np.ascontiguousarray(depth)
+        assert depth.shape == (self.F, self.H, self.W) and depth.dtype in (np.uint16, np.float32)
+        from . import DEPTH_U16, DEPTH_F32
+        for b in (self.raw[0], self.raw[3]) if self.raw else ():
+            b.free()
+        self.raw = (self.ctx.upload(images), ch, rgb_order, self.ctx.upload(depth),
+                    DEPTH_U16 if depth.dtype == np.uint16 else DEPTH_F32, float(np.float32(depth_factor)))
+        if self.gray is None:
+            self.gray = self.ctx.alloc(self.F * self.H * self.W)
+            self.depth = self.ctx.alloc(4 * self.F * self.H * self.W)
+        if Tcw is not None:
+            self.Tcw = np.ascontiguousarray(Tcw, np.float32)
+        if self.dTcw is None or Tcw is not None:
+            self.dTcw = self.ctx.upload(self.Tcw.reshape(self.F, 16))
+        self.ctx.synchronize()
+
+    def run(self, match=True, th=15.0, nobs=2, pose=False, frame=False, track=False, nkf=2, rgbd=False):
         """Enqueue one step (extraction of F frames + F-1 matches, and with pose=True the
         motion-model PoseOptimization of every matched frame, with track=True also TrackLocalMap:
         local map of KeyFrames f-1, f-2 -> SearchByProjection -> PoseOptimization, BASELINE
@@ -66,6 +90,10 @@ class BatchPipeline:
         runs the whole RGB-D Frame constructor instead of the extraction alone: T_M from the
         previous frame (ProcessMovingObject), blur flags of the boxes set by set_frame_boxes(),
         masked extraction (coeb_frame_batch_device)."""
+        if rgbd:
+            img, ch, order, dep, dt, fac = self.raw
+            self.ctx.rgbd_preprocess_batch_device(img.ptr, ch, order, dep.ptr, dt, fac, self.F, self.W, self.H,
+                                                  self.gray.ptr, self.depth.ptr)
         if frame:
             b, o = self.frame_boxes if self.frame_boxes is not None else (None, None)
             self.ctx.frame_batch_device(self.gray.ptr, self.F, self.W, self.H, b, o)
@@ -167,7 +195,7 @@ class BatchPipeline:
                     outlier=[None] + [outl[f, :counts[f]].copy() for f in range(1, self.F)], state=state, stride=kcap)
 
     def close(self):
-        for b in (self.gray, self.depth, self.dTcw):
+        for b in (self.gray, self.depth, self.dTcw) + ((self.raw[0], self.raw[3]) if self.raw else ()):
             if b is not None:
                 b.free()
         self.ctx.close()

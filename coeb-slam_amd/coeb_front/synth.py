@@ -285,3 +285,45 @@ def moving_object_sequence(w, h, n, seed=0, n_small=600, obj=(200, 120, 160, 200
         x, y = ox + k * obj_shift[0], oy + k * obj_shift[1]
         boxes[k] = (x, y, x + ow, y + oh)
     return frames, boxes
+
+
+def _bounce(t, lo, hi):
+    """Triangle wave: position t folded into [lo, hi] (an object bouncing between two walls)."""
+    span = hi - lo
+    if span <= 0:
+        return lo
+    m = t % (2 * span)
+    return lo + (m if m <= span else 2 * span - m)
+
+
+def tracking_sequence(w, h, n, first=0, seed=1000, obj_size=(120, 160), obj_speed=(-5, 4)):
+    """Frames first .. first+n-1 of an endless RGB-D tracking sequence (BASELINE configs[4]):
+    make_frames' background (the camera motion of motion_pose at depth DEPTH_Z) with a textured
+    object bouncing around the image at obj_speed px/frame, off the epipolar direction (the
+    YOLO box is its bounding box).  Frame k depends on k only, so shards of the sequence agree
+    with the whole.  Returns (gray (n, h, w) u8, boxes (n, 4) f32 xyxy)."""
+    canvas = make_canvas(w, h, seed)
+    rng = np.random.default_rng(seed + 4711)
+    ow, oh = obj_size
+    tex = _texture(rng, ow, oh, density=150)
+    x0, y0 = w // 3, h // 4
+    frames = np.empty((n, h, w), np.uint8)
+    boxes = np.empty((n, 4), np.float32)
+    for i in range(n):
+        k = first + i
+        img = np.roll(canvas, (k * SHIFT[1], k * SHIFT[0]), axis=(0, 1)).copy()
+        x = _bounce(x0 + k * obj_speed[0], 8, w - ow - 8)
+        y = _bounce(y0 + k * obj_speed[1], 8, h - oh - 8)
+        img[y:y + oh, x:x + ow] = tex
+        noise = np.random.default_rng(seed * 7919 + k + 1).integers(-6, 7, size=(h, w), dtype=np.int16)
+        frames[i] = np.clip(img + noise, 0, 255).astype(np.uint8)
+        boxes[i] = (x, y, x + ow, y + oh)
+    return frames, boxes
+
+
+def rgbd_from_gray(gray, z=DEPTH_Z, depth_factor=5000.0):
+    """TUM-style raw input for GrabImageRGBD: 8UC3 RGB with R = G = B = gray (RGB2GRAY gives
+    gray back exactly: the 14-bit weights sum to 2^14) and 16UC1 depth in 1/depth_factor m."""
+    rgb = np.repeat(np.asarray(gray, np.uint8)[..., None], 3, axis=-1)
+    d = np.full(gray.shape, int(round(z * depth_factor)), np.uint16)
+    return np.ascontiguousarray(rgb), d

@@ -97,6 +97,52 @@ __global__ __launch_bounds__(256) void k_rgbd(const uint8_t* __restrict__ img, i
     }
 }
 
+// The same conversions over a packed device batch (frame f of the batch at f * W*H pixels), four
+// pixels per thread: one 4/12/16-byte image load, one 8/16-byte depth load, a 4-byte gray and a
+// 16-byte depth store (W % 4 == 0; HBM-bound: 3 + 2 bytes in, 1 + 4 out per pixel for RGB + 16U).
+__global__ __launch_bounds__(256) void k_rgbd_batch(const uint8_t* __restrict__ img, int channels, int rgb_order,
+                                                    const uint8_t* __restrict__ dsrc, int dtype, float dscale, int dcopy,
+                                                    int64_t npix, uint8_t* __restrict__ gray, float* __restrict__ depth)
+{
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (4 * q >= npix) return;
+    const int64_t p0 = (int64_t)blockIdx.y * npix + 4 * q;
+    if (img) {
+        uint32_t w[4];
+        const uint32_t* s = reinterpret_cast<const uint32_t*>(img + p0 * channels);
+        for (int k = 0; k < channels; k++) w[k] = s[k];
+        uint32_t out = 0;
+        for (int k = 0; k < 4; k++) {
+            uint32_t g;
+            if (channels == 1) {
+                g = (w[0] >> (8 * k)) & 0xffu;
+            } else {
+                const int b0 = k * channels;                       // byte offset of pixel k
+                auto byte = [&](int b) { return (int)((w[b >> 2] >> (8 * (b & 3))) & 0xffu); };
+                const int c0 = byte(b0), c1 = byte(b0 + 1), c2 = byte(b0 + 2);
+                const int R2Y = 4899, G2Y = 9617, B2Y = 1868;
+                const int v = rgb_order ? (c0 * R2Y + c1 * G2Y + c2 * B2Y) : (c0 * B2Y + c1 * G2Y + c2 * R2Y);
+                g = (uint32_t)((v + (1 << 13)) >> 14);
+            }
+            out |= g << (8 * k);
+        }
+        reinterpret_cast<uint32_t*>(gray + p0)[0] = out;
+    }
+    if (dsrc) {
+        float v[4];
+        if (dtype == COEB_DEPTH_U16) {
+            const uint2 r = *reinterpret_cast<const uint2*>(dsrc + 2 * p0);
+            v[0] = (float)(r.x & 0xffffu) * dscale; v[1] = (float)(r.x >> 16) * dscale;
+            v[2] = (float)(r.y & 0xffffu) * dscale; v[3] = (float)(r.y >> 16) * dscale;
+        } else {
+            const float4 r = *reinterpret_cast<const float4*>(dsrc + 4 * p0);
+            v[0] = r.x; v[1] = r.y; v[2] = r.z; v[3] = r.w;
+            if (!dcopy) for (int k = 0; k < 4; k++) v[k] = v[k] * dscale;
+        }
+        reinterpret_cast<float4*>(depth + p0)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+}
+
 // Frame::UndistortKeyPoints (Frame.cc:579-609): cv::undistortPoints(.., mK, mDistCoef, Mat(), mK)
 // of OpenCV 3.4 (cvUndistortPointsInternal, 5 fixed iterations), one thread per keypoint, in
 // double with the oracle's operation order.  k = (k1, k2, p1, p2, k3); the remaining rational /
@@ -215,6 +261,30 @@ extern "C" int coeb_rgbd_preprocess(coeb_ctx* c, const uint8_t* img, size_t img_
     if (img) FR_TRY(c, hipMemcpyAsync(gray_out, dgray, (size_t)W * H, hipMemcpyDeviceToHost, s));
     if (depth) FR_TRY(c, hipMemcpyAsync(depth_out, ddep, (size_t)W * H * 4, hipMemcpyDeviceToHost, s));
     FR_TRY(c, hipStreamSynchronize(s));
+    return COEB_OK;
+}
+
+extern "C" int coeb_rgbd_preprocess_batch_device(coeb_ctx* c, const uint8_t* d_img, int channels, int rgb_order,
+                                                 const void* d_depth, int depth_type, float depth_scale, int F, int W,
+                                                 int H, uint8_t* d_gray, float* d_depth_out)
+{
+    if (!c || F <= 0 || W <= 0 || H <= 0 || (!d_img && !d_depth) ||
+        (d_img && (!d_gray || (channels != 1 && channels != 3 && channels != 4))) ||
+        (d_depth && (!d_depth_out || (depth_type != COEB_DEPTH_U16 && depth_type != COEB_DEPTH_F32))))
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_rgbd_preprocess_batch_device: invalid arguments");
+    if (W % 4) return coeb_internal_error(c, COEB_EINVAL, "coeb_rgbd_preprocess_batch_device: width must be a multiple of 4");
+    if ((d_img && (reinterpret_cast<uintptr_t>(d_img) | reinterpret_cast<uintptr_t>(d_gray)) % 4) ||
+        (d_depth && (reinterpret_cast<uintptr_t>(d_depth) | reinterpret_cast<uintptr_t>(d_depth_out)) % 16))
+        return coeb_internal_error(c, COEB_EINVAL, "coeb_rgbd_preprocess_batch_device: misaligned device buffers");
+    hipStream_t s;
+    int dev;
+    if (coeb_internal_stream(c, &s, &dev)) return COEB_EINVAL;
+    (void)hipSetDevice(dev);
+    const int dcopy = depth_type == COEB_DEPTH_F32 && !(fabsf(depth_scale - 1.0f) > 1e-5f);   // Tracking.cc:227
+    const int64_t npix = (int64_t)W * H;
+    hipLaunchKernelGGL(k_rgbd_batch, dim3((unsigned)((npix / 4 + 255) / 256), F), dim3(256), 0, s, d_img, channels,
+                       rgb_order, (const uint8_t*)d_depth, depth_type, depth_scale, dcopy, npix, d_gray, d_depth_out);
+    FR_TRY(c, hipGetLastError());
     return COEB_OK;
 }
 

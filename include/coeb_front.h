@@ -327,6 +327,13 @@ int coeb_rgbd_preprocess(coeb_ctx* ctx, const uint8_t* img, size_t img_stride, i
                          const void* depth, size_t depth_stride, int depth_type, float depth_scale,
                          int width, int height, uint8_t* gray_out, float* depth_out);
 
+/* The same conversions over a packed device batch: d_img nframes x height x width x channels,
+ * d_depth nframes x height x width (16UC1 or 32FC1), outputs packed gray / float depth; width a
+ * multiple of 4, image buffers 4-byte and depth buffers 16-byte aligned.  Enqueued on the
+ * context stream (the batch pipeline's first step, BASELINE configs[4]). */
+int coeb_rgbd_preprocess_batch_device(coeb_ctx* ctx, const uint8_t* d_img, int channels, int rgb_order,
+                                      const void* d_depth, int depth_type, float depth_scale, int nframes, int width,
+                                      int height, uint8_t* d_gray, float* d_depth_out);
 /* mvKeysUn from mvKeys: cv::undistortPoints(.., mK, mDistCoef, Mat(), mK) (OpenCV 3.4, 5
  * iterations) with dist = (k1, k2, p1, p2, k3) (k3 = 0 for a 4-coefficient mDistCoef);
  * dist[0] == 0 copies (Frame.cc:581-585).  out may equal kps. */

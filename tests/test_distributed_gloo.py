@@ -45,6 +45,17 @@ def test_shard_frames_halo():
                 assert nex == nm + 1 and nm >= 1
                 matched.extend(range(first + 1, first + nex))
             assert matched == list(range(1, total + 1))
+            # deeper halos (the full GrabImageRGBD loop: 3): the counted frames are the last nm of
+            # each rank's batch, every rank sees `halo` frames before its first counted one
+            # (fewer at the sequence start), and the counted frames still tile 1..total
+            for halo in (2, 3):
+                matched = []
+                for r in range(world):
+                    first, nex, nm = shard_frames(total, world, r, halo=halo)
+                    c0 = first + nex - nm
+                    assert c0 - first == min(halo, c0)
+                    matched.extend(range(c0, first + nex))
+                assert matched == list(range(1, total + 1))
 
 
 def test_thread_ranks_barrier_and_max():

@@ -980,3 +980,75 @@ def test_batch_grab_rgbd_loop_matches_oracle(oracle_mod, ex):
             assert any(((r["outlier"] > 0) & (r["has2"] > 0)).any() for r in res[1:] if r["state"] > 0)
     finally:
         bp.close()
+
+
+@pytest.mark.parametrize("ch,order,dt", [(3, 1, np.uint16), (3, 0, np.uint16), (4, 1, np.float32), (1, 1, np.float32),
+                                         (4, 0, np.uint16)])
+def test_rgbd_preprocess_batch_matches_oracle(oracle_mod, ch, order, dt):
+    """GrabImageRGBD's conversions over a device batch (coeb_rgbd_preprocess_batch_device) vs
+    the oracle frame by frame: RGB/BGR/RGBA/BGRA/gray images, 16U depth with 1/5000 and 32F
+    depth with factor 1 (passthrough, Tracking.cc:227) or 1/5000."""
+    import coeb_front as cf
+    from coeb_front.pipeline import BatchPipeline
+    F, W, H = 3, 320, 240
+    rng = np.random.default_rng(ch * 10 + order)
+    img = rng.integers(0, 256, (F, H, W, ch) if ch > 1 else (F, H, W), dtype=np.uint8)
+    if dt == np.uint16:
+        dep, fac = rng.integers(0, 65536, (F, H, W), dtype=np.uint16), 1.0 / 5000.0
+    else:
+        dep = rng.uniform(0, 8, (F, H, W)).astype(np.float32)
+        fac = 1.0 if ch == 1 else 1.0 / 5000.0
+    bp = BatchPipeline(W, H, F)
+    try:
+        bp.load_rgbd(img, dep, fac, rgb_order=order)
+        bp.run(rgbd=True, match=False)
+        bp.synchronize()
+        gray = bp.ctx.download(bp.gray.ptr, F * H * W, np.uint8).reshape(F, H, W)
+        depth = bp.ctx.download(bp.depth.ptr, 4 * F * H * W, np.float32).reshape(F, H, W)
+        for f in range(F):
+            assert np.array_equal(gray[f], oracle_mod.image_to_gray(img[f], order)), f
+            assert np.array_equal(depth[f].view(np.uint32), oracle_mod.depth_to_float(dep[f], np.float32(fac)).view(np.uint32)), f
+        # bad arguments fail loudly
+        with pytest.raises(RuntimeError):
+            bp.ctx.rgbd_preprocess_batch_device(bp.raw[0].ptr, 2, 1, 0, 0, 1.0, F, W, H, bp.gray.ptr, 0)
+        with pytest.raises(RuntimeError):
+            bp.ctx.rgbd_preprocess_batch_device(bp.raw[0].ptr, ch, 1, 0, 0, 1.0, F, W - 2, H, bp.gray.ptr, 0)
+        assert cf.DEPTH_F32 == 1
+    finally:
+        bp.close()
+
+
+def test_batch_grab_rgbd_loop_sharded_equals_unsharded():
+    """bench --config D shards the sequence with a 3-frame halo (dist.shard_frames(halo=3)):
+    the counted frames of a shard must come out bit-identical to the same frames of the
+    unsharded batch through the whole loop (RGB-D conversion, Frame ctor, motion model,
+    TrackLocalMap)."""
+    from coeb_front.dist import shard_frames
+    from coeb_front.pipeline import BatchPipeline
+    import bench
+    G = 8
+    full = None
+    for world, rank in ((1, 0), (2, 1)):
+        first, F, nm = shard_frames(G, world, rank, halo=3)
+        bp = BatchPipeline(640, 480, F)
+        try:
+            bench.load_batch(bp, bench.CONFIGS["D"], 640, 480, F, first)
+            bp.run(**bench.step_kwargs(bench.CONFIGS["D"]))
+            bp.synchronize()
+            out, _, nms = bp.results()
+            tr = bp.track_results()
+            res = {first + f: (out[f][0], out[f][1], nms[f], tr["T"][f].copy(), tr["ninliers"][f], tr["nlocal"][f],
+                               tr["local_match"][f], tr["state"][f]) for f in range(F - nm, F)}
+        finally:
+            bp.close()
+        if full is None:
+            full = res
+            assert sorted(res) == list(range(1, G + 1))
+            assert sum(1 for v in res.values() if v[7] == 2) >= G - 1
+            continue
+        assert first == 2 and sorted(res) == list(range(5, G + 1))
+        for g, v in res.items():
+            w = full[g]
+            assert np.array_equal(v[0], w[0]) and np.array_equal(v[1], w[1]) and v[2] == w[2], g
+            assert np.array_equal(v[3].view(np.uint32), w[3].view(np.uint32)), g
+            assert v[4:6] == w[4:6] and np.array_equal(v[6], w[6]) and v[7] == w[7], g
