@@ -1024,6 +1024,7 @@ int coeb_extract(coeb_ctx* c, const uint8_t* gray, int W, int H, size_t stride, 
     if (!gray || W <= 0 || H <= 0) return COEB_OK;          // _image.empty() -> return (:1096-1097)
     if (stride < (size_t)W) return set_err(c, COEB_EINVAL, "stride < width");
     if (nbox < 0 || nbox > COEB_MAXBOX || ntm < 0 || nblur < 0) return set_err(c, COEB_EINVAL, "bad box/T_M counts");
+    if ((nbox && !boxes) || (ntm && !tm_xy)) return set_err(c, COEB_EINVAL, "coeb_extract: null box / T_M array");
     (void)hipSetDevice(c->device);
     int rc;
     if ((rc = ensure_plan(c, W, H))) return rc;
@@ -1032,7 +1033,8 @@ int coeb_extract(coeb_ctx* c, const uint8_t* gray, int W, int H, size_t stride, 
     HIP_TRY(c, hipMemcpy2DAsync(dgray, W, gray, stride, W, H, hipMemcpyHostToDevice, main_stream(c)));
     int32_t box_off[2] = {0, nbox}, tm_off[2] = {0, ntm};
     std::vector<int32_t> blur(nbox, 0);
-    for (int i = 0; i < nbox && i < nblur; i++) blur[i] = blur_flag[i];   // missing flags read as 0
+    if (blur_flag)                                      // missing flags (or a null array) read as 0
+        for (int i = 0; i < nbox && i < nblur; i++) blur[i] = blur_flag[i];
     ExtractBufs b;
     if ((rc = extract_bufs(c, 1, b))) return rc;
     if ((rc = upload_dyn(c, 1, nbox ? boxes : nullptr, box_off, ntm ? tm_xy : nullptr, tm_off,

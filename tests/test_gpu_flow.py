@@ -193,3 +193,24 @@ def test_frame_batch_matches_oracle_frame_by_frame(oracle_mod):
         assert all(n is None or n > 0 for n in nms)
     finally:
         bp.close()
+
+
+def test_good_features_beyond_16384_maxima(ctx, oracle_mod):
+    """A noise frame has more Harris local maxima than the 16384 sorted in LDS: the kernel keeps
+    the 16384 largest (radix select) and the greedy selection over them is exact because it
+    accepts maxCorners = 1000 corners first -- the result equals the uncapped oracle, and the
+    whole ProcessMovingObject on such frames runs instead of failing."""
+    rng = np.random.default_rng(11)
+    noise = rng.integers(0, 256, (480, 640), dtype=np.uint8)
+    with pytest.raises(RuntimeError):                 # the frame does exceed 16384 maxima
+        oracle_mod.good_features(noise, max_cand=16384)
+    ref = oracle_mod.good_features(noise)
+    assert len(ref) == 1000
+    eq(cf.GoodFeaturesToTrack(ctx, noise), ref, "noise")
+    cur = np.roll(noise, (1, 2), axis=(0, 1))
+    tm = cf.ProcessMovingObject(ctx, noise, cur)
+    tm_ref = oracle_mod.process_moving_object(noise, cur)
+    if tm_ref is None:
+        assert tm is None
+    else:
+        eq(tm, tm_ref, "noise T_M")

@@ -1052,3 +1052,26 @@ def test_batch_grab_rgbd_loop_sharded_equals_unsharded():
             assert np.array_equal(v[0], w[0]) and np.array_equal(v[1], w[1]) and v[2] == w[2], g
             assert np.array_equal(v[3].view(np.uint32), w[3].view(np.uint32)), g
             assert v[4:6] == w[4:6] and np.array_equal(v[6], w[6]) and v[7] == w[7], g
+
+
+def test_extract_null_arrays(ctx, oracle_mod, ex):
+    """coeb_extract's array arguments: a null blur_flag with nblur > 0 reads as all-zero flags
+    (the reference's missing flags), null boxes / T_M with a nonzero count fail loudly."""
+    import ctypes as C
+    import coeb_front as cf
+    img = synth.make_frames(640, 480, 1, seed=31)[0]
+    boxes, tm, _ = synth.dynamic_inputs(640, 480, seed=3)
+    cap = ctx.max_keypoints(640, 480)
+    kps = np.zeros(cap, cf.KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int()
+    L = cf.lib()
+    rc = L.coeb_extract(ctx.h, img.ctypes.data, 640, 480, 640, boxes.ctypes.data, len(boxes), tm.ctypes.data, len(tm),
+                        None, 2, kps.ctypes.data, desc.ctypes.data, cap, C.byref(n))
+    assert rc == 0
+    r = ex.extract(img, boxes, tm, np.zeros(len(boxes), np.int32))
+    assert n.value == len(r["kps"]) and np.array_equal(desc[:n.value], r["desc"])
+    for bad in ((None, len(boxes), tm.ctypes.data, len(tm)), (boxes.ctypes.data, len(boxes), None, len(tm))):
+        rc = L.coeb_extract(ctx.h, img.ctypes.data, 640, 480, 640, bad[0], bad[1], bad[2], bad[3], None, 0,
+                            kps.ctypes.data, desc.ctypes.data, cap, C.byref(n))
+        assert rc == cf.COEB_EINVAL if hasattr(cf, "COEB_EINVAL") else rc != 0
