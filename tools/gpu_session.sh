@@ -35,7 +35,7 @@ for step in "$@"; do
         flowprof) run flowprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/flowprof -o run -- python tools/flow_bench.py ;;
         pmc)
             export COEB_SIDE_STREAM=0
-            B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-e2e"
+            B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-e2e --no-extras"
             run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- $B
             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- $B
             python tools/pmc_summary.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv \
