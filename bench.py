@@ -384,19 +384,33 @@ def cpu_extras(out, w, h, reps=5):
     return res
 
 
+def _pmc_file(stem, w, h):
+    """The committed PMC summary collected at frame size w x h: profiles/<stem>.json (config A's
+    640x480) or profiles/<stem>_<w>x<h>.json; None when neither matches the size."""
+    for name in ("%s.json" % stem, "%s_%dx%d.json" % (stem, w, h)):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if (d.get("width"), d.get("height")) == (w, h):
+            d["_file"] = "profiles/" + name
+            return d
+    return None
+
+
 def pmc_traffic(kernel, frames_per_launch, w, h):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by tools/pmc_summary.py --json from separate
     FETCH_SIZE / WRITE_SIZE passes of this bench), scaled to this run's frames per launch.
     None unless the counters were collected at this frame size."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        with open(path) as f:
-            d = json.load(f)
-        if (d.get("width"), d.get("height")) != (w, h):
+        d = _pmc_file("pmc_traffic", w, h)
+        if d is None:
             return None, None
         k = d["kernels"][kernel]
-        return int(k["traffic_bytes"] * frames_per_launch / d["frames_per_launch"]), d.get("command", "")
+        return (int(k["traffic_bytes"] * frames_per_launch / d["frames_per_launch"]),
+                "%s (%s)" % (d["_file"], d.get("command", "")))
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         return None, None
 
@@ -406,13 +420,12 @@ def pmc_valu(kernel, w, h):
     tools/pmc_summary.py --valu-json: SQ_INSTS_VALU / (2 x 256 CUs x busy cycles)), if collected
     at this frame size."""
     try:
-        with open(os.path.join(ROOT, "profiles", "pmc_valu.json")) as f:
-            d = json.load(f)
-        if (d.get("width"), d.get("height")) != (w, h):
+        d = _pmc_file("pmc_valu", w, h)
+        if d is None:
             return None
         k = d["kernels"][kernel]
         return dict(valu_issue_frac=k["valu_issue_frac"], valu_insts_per_launch=k["valu_insts"],
-                    source="profiles/pmc_valu.json (%s)" % d.get("command", ""))
+                    source="%s (%s)" % (d["_file"], d.get("command", "")))
     except (OSError, KeyError, ValueError):
         return None
 
@@ -731,7 +744,7 @@ def rank_main(ranks, args):
                         frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, kernel=name,
                         avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=int(bpl))
             if traffic is not None:
-                roof["traffic_source"] = "profiles/pmc_traffic.json (%s)" % tsrc
+                roof["traffic_source"] = tsrc
             # the kernel is bound by integer VALU issue, not HBM: the PMC VALU fraction says how
             # close it runs to the chip's issue ceiling (2 wave64 VALU instructions per CU per cycle)
             valu = pmc_valu(name, w, h)
