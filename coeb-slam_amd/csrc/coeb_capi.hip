@@ -1861,11 +1861,12 @@ int coeb_internal_error(coeb_ctx* c, int code, const char* msg) { return set_err
 int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t bytes, size_t* size_out)
 {
     if (c) join_pose(c);
-    if (c && what && std::string(what) == "band_timing") {      // [8] k_fast_band phase clocks (COEB_BAND_CLOCK builds)
+    if (c && what && (std::string(what) == "band_timing" || std::string(what) == "fast_timing")) {
+        // [8] k_fast_band / k_fast phase clocks (COEB_BAND_CLOCK / COEB_FAST_CLOCK builds)
         unsigned long long t[8];
         if (size_out) *size_out = sizeof(t);
         if (!host) return 0;                         // size query: the read below also clears
-        if (band_timing_read(t)) return COEB_EDEVICE;
+        if ((std::string(what) == "band_timing" ? band_timing_read(t) : fast_timing_read(t))) return COEB_EDEVICE;
         memcpy(host, t, std::min(bytes, sizeof(t)));
         return 0;
     }

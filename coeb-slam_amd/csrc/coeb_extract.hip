@@ -758,6 +758,21 @@ __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs
 // Bytes of one per-wave ROI (or M) slab: 16-byte multiple so every slab starts 16-aligned.
 __host__ __device__ inline int fast_slab(const Plan& P) { return (kFastRowBytes * P.max_roi_h + 15) & ~15; }
 
+#ifndef COEB_BAND_CLOCK
+#define COEB_BAND_CLOCK 0      // experiment builds: phase clocks of wave 0 (band_timing_read)
+#endif
+__device__ unsigned long long g_band_clk[8];
+#define BC_MARK(v) long long v = COEB_BAND_CLOCK ? (long long)clock64() : 0
+#define BC_ADD(slot, t0) do { if (COEB_BAND_CLOCK && threadIdx.x == 0) atomicAdd(&g_band_clk[slot], (unsigned long long)((long long)clock64() - (t0))); } while (0)
+#ifndef COEB_FAST_CLOCK
+#define COEB_FAST_CLOCK 0      // experiment builds: per-cell k_fast phase clocks (fast_timing)
+#endif
+#define FC_MARK(v) long long v = COEB_FAST_CLOCK ? (long long)clock64() : 0
+// per-cell slots spread over 256 copies (blockIdx.x & 255) so the counters do not contend
+__device__ unsigned long long g_fast_clk[256 * 8];
+#define FC_SLOT(slot) g_fast_clk[(blockIdx.x & 255) * 8 + (slot)]
+#define FC_ADD(slot, t0) do { if (COEB_FAST_CLOCK && lane_id() == 0) atomicAdd(&FC_SLOT(slot), (unsigned long long)((long long)clock64() - (t0))); } while (0)
+
 // Pre-test, exact strength, NMS and ordered output of one staged cell.
 __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, int f, int cidx, const CellDesc& c,
                                           int th_ini, int th_min, const uint8_t* roi, uint8_t* Ms, uint16_t* surv,
@@ -780,6 +795,11 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
     const uint64_t vm0 = __ballot(cg < ngrp && 4 * cg + 0 < ww), vm1 = __ballot(cg < ngrp && 4 * cg + 1 < ww);
     const uint64_t vm2 = __ballot(cg < ngrp && 4 * cg + 2 < ww), vm3 = __ballot(cg < ngrp && 4 * cg + 3 < ww);
     int o = (rsub + 3) * kFastRowBytes + 4 + 4 * cg;
+    FC_MARK(t_scan);
+    long long t_str = 0;
+    // (reading pass k+1's slab words before evaluating pass k, pre_load / pre_eval, measured
+    // 0.330 vs 0.318 ms; a lane-per-group mapping that keeps all 64 lanes busy on 30-37-px
+    // windows measured 0.338: the scan is not the bound, `tools/_fast_timing.py`)
     for (int r0 = 0; npix > 0 && r0 < wh; r0 += rpi, o += rpi * kFastRowBytes) {
         // every lane runs the test (rows past the window read slab bytes that are masked off)
         uint32_t lo, hi;
@@ -798,6 +818,7 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
         }
         ns = uniform(ns + __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
         if (ns > kFastSurv - 256 || r0 + rpi >= wh) {
+            FC_MARK(t_s0);
             wave_sync_lds();
             for (int e0 = 0; e0 < ns; e0 += 64) {
                 const int e = e0 + lane;
@@ -817,8 +838,12 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
             }
             wave_sync_lds();
             ns = 0;
+            if (COEB_FAST_CLOCK) t_str += (long long)clock64() - t_s0;
         }
     }
+    FC_ADD(1, t_scan + t_str);                        // pre-test passes (strength flushes excluded)
+    if (COEB_FAST_CLOCK && lane_id() == 0) atomicAdd(&FC_SLOT(2), (unsigned long long)t_str);
+    FC_MARK(t_nms);
     // ---- 4: NMS + ordered compaction
     uint32_t* out = b.cand + ((int64_t)f * P->ncells + cidx) * P->cell_cap;
     int nkept = 0;
@@ -865,6 +890,8 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
         if (nkept > 0) break;
     }
     if (lane == 0) b.cand_n[(int64_t)f * P->ncells + cidx] = min(nkept, P->cell_cap);
+    FC_ADD(3, t_nms);
+    if (COEB_FAST_CLOCK && lane == 0) { atomicAdd(&FC_SLOT(5), 1ull); atomicAdd(&FC_SLOT(6), (unsigned long long)nc); }
 }
 
 // Cell descriptor as one 16-byte scalar load (16-bit fields would become vector loads).
@@ -908,10 +935,13 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
     FastCellGeom G = fast_geom(P, b, f, c);
     FastRegs R;
     fast_prefetch(G, R);
+    FC_MARK(t_all);
     for (int t = 0; t < kFastCellsPerWave; t++, cidx++) {
+        FC_MARK(t_st);
         fast_stage(G, R, roi);
         for (int i = lane; i < (kFastRowBytes * c.rh + 15) / 16; i += 64) reinterpret_cast<uint4*>(Ms)[i] = make_uint4(0, 0, 0, 0);
         wave_sync_lds();
+        FC_ADD(0, t_st);                              // wait for the ROI loads + stage + M clear
         const CellDesc cur = c;
         const bool more = t + 1 < kFastCellsPerWave && cidx + 1 < cell1;
         if (more) {
@@ -923,6 +953,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
         if (!more) break;
         wave_sync_lds();
     }
+    FC_ADD(4, t_all);
 }
 
 // ================================ k_fast (band form) ================================
@@ -1035,12 +1066,6 @@ __device__ __forceinline__ BandGeom band_geom(const Plan* P, const ExtractBufs& 
 #define COEB_BAND_UNROLL 2
 #endif
 constexpr int kBandUnroll = COEB_BAND_UNROLL;   // window rows per wave per pre-test step
-#ifndef COEB_BAND_CLOCK
-#define COEB_BAND_CLOCK 0      // experiment builds: phase clocks of wave 0 (band_timing_read)
-#endif
-__device__ unsigned long long g_band_clk[8];
-#define BC_MARK(v) long long v = COEB_BAND_CLOCK ? (long long)clock64() : 0
-#define BC_ADD(slot, t0) do { if (COEB_BAND_CLOCK && threadIdx.x == 0) atomicAdd(&g_band_clk[slot], (unsigned long long)((long long)clock64() - (t0))); } while (0)
 
 // Pre-test of the 4 pixels at columns x0 .. x0+3 of the row 3 below `top` (the 7 rows from top
 // are the ring rows): bit q set <=> pixel q passes OpenCV's pair test at t and is in vmask.
@@ -2291,6 +2316,18 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
 // Phase clocks of k_fast_band (COEB_BAND_CLOCK builds): [0] stage, [1] pre-test + strengths +
 // barrier, [2] NMS, [3] keep, [4] output, [5] wave 0's flushes, [6] wave 0's phase 2 before
 // the barrier; read and cleared.
+int fast_timing_read(unsigned long long* out)
+{
+    static unsigned long long h[256 * 8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fast_clk), sizeof(h)) != hipSuccess) return -1;
+    for (int k = 0; k < 8; k++) {
+        out[k] = 0;
+        for (int i = 0; i < 256; i++) out[k] += h[i * 8 + k];
+    }
+    static const unsigned long long z[256 * 8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_fast_clk), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+
 int band_timing_read(unsigned long long* out)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_band_clk), sizeof(unsigned long long) * 8) != hipSuccess) return -1;

@@ -18,8 +18,8 @@
 //   calcOpticalFlowPyrLK(imGrayPre, imgray, .., Size(22,22), 5, (ITER|EPS, 20, 0.01))   (:335)
 //     k_pyr_down       pyrDown 5x5 [1 4 6 4 1]^2 per level, both frames in one launch
 //     k_sharr          calcSharrDeriv of every level of the previous frame in one launch
-//     k_lk             one wave per point, levels coarse to fine; 484-pixel window sums exact in
-//                      int64 (8 pixels per lane, wave reduction)
+//     k_lk             one wave per point, levels coarse to fine; 484-pixel window sums exact
+//                      (8 pixels per lane in int32, DPP wave reduction of the 16-bit halves)
 //   SAD check (:337-365), findFundamentalMat(.., FM_RANSAC, 0.1, 0.99) (:373), epipolar
 //   distance > 1 -> T_M (:375-384)
 //     k_fm             one workgroup: SAD filter + ordered compaction into LDS, RANSAC in
@@ -93,10 +93,13 @@ __device__ __forceinline__ T* at_pair(T* p, int64_t stride)
 }
 
 // ============================== goodFeaturesToTrack ==============================
-// One 16 x 16 tile per workgroup.  The Sobel products (dx^2, dx dy, dy^2) are computed once per
-// position of the 18 x 18 box-filter footprint (positions reflected at the border, Sobel taps
-// reflected again, as boxFilter / Sobel with BORDER_REFLECT_101 read them) into LDS, then each
-// pixel sums its 3 x 3 box from LDS in the reference's order.
+// One 32 x 32 tile per workgroup (thread = one column, four rows).  The Sobel products
+// (dx^2, dx dy, dy^2) are computed once per position of the 34 x 34 box-filter footprint
+// (positions reflected at the border, Sobel taps reflected again, as boxFilter / Sobel with
+// BORDER_REFLECT_101 read them) into LDS -- interior tiles from a staged 36 x 36 pixel tile --
+// then each pixel sums its 3 x 3 box from LDS in the reference's order, the three row sums of
+// a row shared by the outputs that use it.  One atomicMax per 1024 pixels.
+constexpr int kGfT = 32;
 __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__ img, int w, int h, int stride, double k,
                                                      float* __restrict__ R, uint32_t* __restrict__ rmax, int64_t iz,
                                                      int64_t pz)
@@ -104,9 +107,10 @@ __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__
     img = at_pair(img, iz);
     R = at_pair(R, pz);
     rmax = at_pair(rmax, pz);
-    __shared__ float sA[18][19], sB[18][19], sC[18][19];
-    __shared__ uint8_t sT[20][20];
-    const int x0 = blockIdx.x * 16, y0 = blockIdx.y * 16;
+    constexpr int TP = kGfT + 2, PP = TP + 1;        // products footprint, LDS pitch
+    __shared__ float sA[TP][PP], sB[TP][PP], sC[TP][PP];
+    __shared__ uint8_t sT[TP + 2][TP + 2 + 4];
+    const int x0 = blockIdx.x * kGfT, y0 = blockIdx.y * kGfT;
     const double scale = 1.0 / (4.0 * 3.0 * 255.0);
     auto put = [&](int tx, int ty, int gx, int gy) {
         const float dx = (float)((double)gx * scale), dy = (float)((double)gy * scale);
@@ -114,15 +118,15 @@ __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__
         sB[ty][tx] = dx * dy;
         sC[ty][tx] = dy * dy;
     };
-    if (x0 >= 2 && y0 >= 2 && x0 + 18 <= w && y0 + 18 <= h) {
-        // interior tile: no reflection; the 20 x 20 pixel footprint staged once
-        for (int e = threadIdx.x; e < 400; e += 256) {
-            const int ty = e / 20, tx = e - ty * 20;
+    if (x0 >= 2 && y0 >= 2 && x0 + TP <= w && y0 + TP <= h) {
+        // interior tile: no reflection; the 36 x 36 pixel footprint staged once
+        for (int e = threadIdx.x; e < (TP + 2) * (TP + 2); e += 256) {
+            const int ty = e / (TP + 2), tx = e - ty * (TP + 2);
             sT[ty][tx] = img[(size_t)(y0 - 2 + ty) * stride + x0 - 2 + tx];
         }
         __syncthreads();
-        for (int e = threadIdx.x; e < 18 * 18; e += 256) {
-            const int ty = e / 18, tx = e - ty * 18;
+        for (int e = threadIdx.x; e < TP * TP; e += 256) {
+            const int ty = e / TP, tx = e - ty * TP;
             const uint8_t* r0 = &sT[ty][tx];
             const uint8_t* r1 = &sT[ty + 1][tx];
             const uint8_t* r2 = &sT[ty + 2][tx];
@@ -132,8 +136,8 @@ __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__
         }
     } else {
         // border tile: box positions reflected, then the Sobel taps of each position reflected
-        for (int e = threadIdx.x; e < 18 * 18; e += 256) {
-            const int ty = e / 18, tx = e - ty * 18;
+        for (int e = threadIdx.x; e < TP * TP; e += 256) {
+            const int ty = e / TP, tx = e - ty * TP;
             const int xx = reflect101(x0 + tx - 1, w), yy = reflect101(y0 + ty - 1, h);
             const int xm = reflect101(xx - 1, w), xp = reflect101(xx + 1, w);
             const uint8_t* r0 = img + (size_t)reflect101(yy - 1, h) * stride;
@@ -145,23 +149,31 @@ __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__
         }
     }
     __syncthreads();
-    const int lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
-    const int x = x0 + lx, y = y0 + ly;
-    float r = -FLT_MAX;
-    if (x < w && y < h) {
-        float sa[3], sb[3], sc[3];
-        for (int j = 0; j < 3; j++) {
-            sa[j] = (sA[ly + j][lx] + sA[ly + j][lx + 1]) + sA[ly + j][lx + 2];
-            sb[j] = (sB[ly + j][lx] + sB[ly + j][lx + 1]) + sB[ly + j][lx + 2];
-            sc[j] = (sC[ly + j][lx] + sC[ly + j][lx + 1]) + sC[ly + j][lx + 2];
+    const int lx = threadIdx.x & 31, ly = (threadIdx.x >> 5) * 4;
+    const int x = x0 + lx;
+    // row sums of footprint rows ly .. ly+5 at column lx (the reference's left-to-right order)
+    float ra[6], rb[6], rc[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        ra[j] = (sA[ly + j][lx] + sA[ly + j][lx + 1]) + sA[ly + j][lx + 2];
+        rb[j] = (sB[ly + j][lx] + sB[ly + j][lx + 1]) + sB[ly + j][lx + 2];
+        rc[j] = (sC[ly + j][lx] + sC[ly + j][lx + 1]) + sC[ly + j][lx + 2];
+    }
+    float r4 = -FLT_MAX;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int y = y0 + ly + q;
+        if (x < w && y < h) {
+            const float a = (ra[q] + ra[q + 1]) + ra[q + 2], b = (rb[q] + rb[q + 1]) + rb[q + 2];
+            const float c = (rc[q] + rc[q + 1]) + rc[q + 2];
+            const float ac = a * c - b * b, apc = a + c;
+            const float r = (float)((double)ac - (k * (double)apc) * (double)apc);
+            R[(size_t)y * w + x] = r;
+            r4 = fmaxf(r4, r);
         }
-        const float a = (sa[0] + sa[1]) + sa[2], b = (sb[0] + sb[1]) + sb[2], c = (sc[0] + sc[1]) + sc[2];
-        const float ac = a * c - b * b, apc = a + c;
-        r = (float)((double)ac - (k * (double)apc) * (double)apc);
-        R[(size_t)y * w + x] = r;
     }
     __shared__ uint32_t s_m[4];
-    uint32_t o = f2ord(r);
+    uint32_t o = f2ord(r4);
     for (int off = 32; off >= 1; off >>= 1) o = max(o, (uint32_t)__shfl_xor((int)o, off, 64));
     if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = o;
     __syncthreads();
@@ -570,10 +582,25 @@ __global__ __launch_bounds__(256) void k_sharr(LkPyr pyr, int64_t iz, int64_t pz
     }
 }
 
-__device__ __forceinline__ int64_t wave_sum64(int64_t v)
+// Wave sum of an int32 whose total may need 34 bits: the 16-bit halves are summed separately
+// (|hi| < 2^15 and lo < 2^16 per lane keep both sums inside int32 over 64 lanes) with DPP row
+// shifts and row broadcasts -- no LDS round trips (an int64 __shfl_xor tree costs 12
+// ds_bpermute) -- and joined in int64.  Exact: the per-lane partial sums fit int32 (<= 8
+// products of < 2^27).
+__device__ __forceinline__ int dpp_sum_to63(int v)
 {
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return v;                                                          // lane 63: the total
+}
+__device__ __forceinline__ int64_t wave_sum_i32x(int v)
+{
+    const int hi = dpp_sum_to63(v >> 16), lo = dpp_sum_to63(v & 0xffff);
+    return (int64_t)__builtin_amdgcn_readlane(hi, 63) * 65536 + (int64_t)__builtin_amdgcn_readlane(lo, 63);
 }
 
 __device__ __forceinline__ int refl1(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
@@ -620,7 +647,7 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
         int iw01 = (int)rintf(a * (1.f - b) * 16384.f);
         int iw10 = (int)rintf((1.f - a) * b * 16384.f);
         int iw11 = 16384 - iw00 - iw01 - iw10;
-        int64_t sA11 = 0, sA12 = 0, sA22 = 0;
+        int sA11 = 0, sA12 = 0, sA22 = 0;                 // per lane: 8 products of < 2^27
 #pragma unroll
         for (int q = 0; q < PPL; q++) {
             const int e = lane + 64 * q;
@@ -638,13 +665,13 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
                 const short2 d00 = dv(X, Y), d01 = dv(X + 1, Y), d10 = dv(X, Y + 1), d11 = dv(X + 1, Y + 1);
                 gxv[q] = (d00.x * iw00 + d01.x * iw01 + d10.x * iw10 + d11.x * iw11 + (1 << 13)) >> 14;
                 gyv[q] = (d00.y * iw00 + d01.y * iw01 + d10.y * iw10 + d11.y * iw11 + (1 << 13)) >> 14;
-                sA11 += (int64_t)gxv[q] * gxv[q];
-                sA12 += (int64_t)gxv[q] * gyv[q];
-                sA22 += (int64_t)gyv[q] * gyv[q];
+                sA11 += gxv[q] * gxv[q];
+                sA12 += gxv[q] * gyv[q];
+                sA22 += gyv[q] * gyv[q];
             }
         }
-        sA11 = wave_sum64(sA11); sA12 = wave_sum64(sA12); sA22 = wave_sum64(sA22);
-        const float A11 = (float)sA11 * FLT_SCALE, A12 = (float)sA12 * FLT_SCALE, A22 = (float)sA22 * FLT_SCALE;
+        const int64_t tA11 = wave_sum_i32x(sA11), tA12 = wave_sum_i32x(sA12), tA22 = wave_sum_i32x(sA22);
+        const float A11 = (float)tA11 * FLT_SCALE, A12 = (float)tA12 * FLT_SCALE, A22 = (float)tA22 * FLT_SCALE;
         float D2 = A11 * A22 - A12 * A12;
         const float minEig = ((A22 + A11) - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
         if (minEig < 1e-4f || D2 < FLT_EPSILON) {
@@ -665,7 +692,7 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
             iw01 = (int)rintf(a * (1.f - b) * 16384.f);
             iw10 = (int)rintf((1.f - a) * b * 16384.f);
             iw11 = 16384 - iw00 - iw01 - iw10;
-            int64_t ib1 = 0, ib2 = 0;
+            int ib1 = 0, ib2 = 0;                     // per lane: 8 products of < 2^26
 #pragma unroll
             for (int q = 0; q < PPL; q++) {
                 const int e = lane + 64 * q;
@@ -676,12 +703,12 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
                     const uint8_t* r0 = J + (size_t)refl1(Y, lh) * pitch;
                     const uint8_t* r1 = J + (size_t)refl1(Y + 1, lh) * pitch;
                     const int diff = ((r0[x0] * iw00 + r0[x1] * iw01 + r1[x0] * iw10 + r1[x1] * iw11 + (1 << 8)) >> 9) - iv[q];
-                    ib1 += (int64_t)diff * gxv[q];
-                    ib2 += (int64_t)diff * gyv[q];
+                    ib1 += diff * gxv[q];
+                    ib2 += diff * gyv[q];
                 }
             }
-            ib1 = wave_sum64(ib1); ib2 = wave_sum64(ib2);
-            const float b1 = (float)ib1 * FLT_SCALE, b2 = (float)ib2 * FLT_SCALE;
+            const int64_t tb1 = wave_sum_i32x(ib1), tb2 = wave_sum_i32x(ib2);
+            const float b1 = (float)tb1 * FLT_SCALE, b2 = (float)tb2 * FLT_SCALE;
             const float dx = (A12 * b2 - A22 * b1) * D2, dy = (A12 * b1 - A11 * b2) * D2;
             lx += dx; ly += dy;
             nx = lx + hw; ny = ly + hw;
@@ -1384,7 +1411,8 @@ int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, in
     (void)hipMemset2DAsync(d->rmax, (size_t)d->pz, 0, 4, P, s);      // one word per pair
     (void)hipMemset2DAsync(d->nkeys, (size_t)d->pz, 0, 4, P, s);
     const dim3 grid((w + 15) / 16, (h + 15) / 16, P);
-    hipLaunchKernelGGL(k_gf_response, grid, dim3(256), 0, s, img, w, h, stride, k, d->R, d->rmax, iz, d->pz);
+    hipLaunchKernelGGL(k_gf_response, dim3((w + kGfT - 1) / kGfT, (h + kGfT - 1) / kGfT, P), dim3(256), 0, s, img, w, h,
+                       stride, k, d->R, d->rmax, iz, d->pz);
     hipLaunchKernelGGL(k_gf_candidates, grid, dim3(256), 0, s, d->R, w, h, quality, d->rmax, d->keys, d->nkeys,
                        gf_key_cap(w, h), d->pz);
     (void)hipFuncSetAttribute((const void*)k_gf_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

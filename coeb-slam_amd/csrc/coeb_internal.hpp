@@ -121,7 +121,8 @@ constexpr int kBandCornW = 256;          // corners per wave list before the who
 constexpr int kBandCells = 16;           // cells per segment
 
 // ---- launch wrappers (coeb_extract.hip / coeb_match.hip) ----
-int band_timing_read(unsigned long long* out);   // k_fast_band phase clocks (diagnostic builds)
+int band_timing_read(unsigned long long* out);
+int fast_timing_read(unsigned long long* out);   // COEB_FAST_CLOCK builds: per-cell k_fast phase sums   // k_fast_band phase clocks (diagnostic builds)
 struct ExtractBufs {
     const uint8_t* gray;   // [F][H][W]
     uint8_t* pyr;
