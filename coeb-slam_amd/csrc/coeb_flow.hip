@@ -396,6 +396,13 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
 // (10.5 iterations per corner): 1.97 ms per batch vs 4.08 ms for four corners per 256-thread
 // workgroup with unpipelined sums; forming the linear terms in the summing lanes (three product
 // arrays, selects) cost 5x.  itcount (COEB_SUBPIX_COUNT): {iterations, corners} for tools.
+#ifndef COEB_SUBPIX_CLOCK
+#define COEB_SUBPIX_CLOCK 0    // experiment builds: phase clocks of k_subpix (coeb_internal_subpix_clock)
+#endif
+__device__ unsigned long long g_sp_clk[256 * 8];
+#define SP_MARK(v) long long v = COEB_SUBPIX_CLOCK ? (long long)clock64() : 0
+#define SP_ADD(slot, t0) do { if (COEB_SUBPIX_CLOCK && lane == 0) atomicAdd(&g_sp_clk[(blockIdx.x & 255) * 8 + (slot)], (unsigned long long)((long long)clock64() - (t0))); } while (0)
+
 template <int WIN, int CPB>
 __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__ img, int w, int h, int stride,
                                                       float* __restrict__ xy, const int* __restrict__ d_n, int nmax,
@@ -407,40 +414,71 @@ __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__
     d_n = at_pair(d_n, pz);
     constexpr int WW = 2 * WIN + 1, BW = WW + 2, NB = BW * BW, NK = WW * WW;
     constexpr int NKP = (NK + 7) & ~7;
+    constexpr int KPL = (NK + 63) / 64;                // terms per lane
+    // Pixels around the corner staged once (the window may drift kSpM px before a refetch):
+    // the per-iteration window then samples LDS instead of re-reading the image.
+    constexpr int kSpM = 8, SS = BW + 1 + 2 * kSpM;
     __shared__ float s_buf[CPB][NB];
     __shared__ double s_tt[CPB][5][NKP];
+    __shared__ uint8_t s_px[CPB][SS * SS];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int p = blockIdx.x * CPB + wv;
     float* buf = s_buf[wv];
     double (*s_t)[NKP] = s_tt[wv];
+    uint8_t* px8 = s_px[wv];
     int n = *d_n;
     n = n < nmax ? n : nmax;
     if (p >= n) return;
     for (int k = NK + lane; k < NKP; k += 64) for (int q = 0; q < 5; q++) s_t[q][k] = 0.0;
+    double mreg[KPL];                                  // this lane's weights, k = lane + 64 q
+#pragma unroll
+    for (int q = 0; q < KPL; q++) mreg[q] = lane + 64 * q < NK ? (double)mask[lane + 64 * q] : 0.0;
     const float tx = xy[2 * p], ty = xy[2 * p + 1];
+    const int R0x = cv_floor(tx - (float)(BW - 1) * 0.5f) - kSpM, R0y = cv_floor(ty - (float)(BW - 1) * 0.5f) - kSpM;
+    const bool staged = R0x >= 0 && R0y >= 0 && R0x + SS <= w && R0y + SS <= h;
+    if (staged) {
+        const uint8_t* g = img + (size_t)R0y * stride + R0x;
+#pragma unroll
+        for (int q = 0; q < (SS * SS + 63) / 64; q++) {
+            const int e = lane + 64 * q;
+            if (e < SS * SS) { const int r = e / SS; px8[e] = g[(size_t)r * stride + (e - r * SS)]; }
+        }
+    }
     float cx = tx, cy = ty;
     int it = 0;
     double err = 0;
+    SP_MARK(t_all);
+    // getRectSubPix_8u32f's in-image window from rows of `src` (image or staged pixels)
+    auto fill_in = [&](const uint8_t* src0, int sst, float a, float b) {
+        a = a < 0.0001f ? 0.0001f : a;
+        const float a12 = a * (1.f - b), a22 = a * b, b1 = 1.f - b, b2 = b;
+        const double sd = (1. - (double)a) / (double)a;
+        for (int e = lane; e < NB; e += 64) {
+            const int r = e / BW, j = e - r * BW;
+            const uint8_t* src = src0 + r * sst;
+            const float t = a12 * (float)src[j + 1] + a22 * (float)src[j + 1 + sst];
+            float prev;
+            if (j == 0) prev = (1.f - a) * (b1 * (float)src[0] + b2 * (float)src[sst]);
+            else {
+                const float tp = a12 * (float)src[j] + a22 * (float)src[j + sst];
+                prev = (float)((double)tp * sd);
+            }
+            buf[e] = prev + t;
+        }
+    };
     do {
+        SP_MARK(t0);
         const float ctrx = cx - (float)(BW - 1) * 0.5f, ctry = cy - (float)(BW - 1) * 0.5f;
         const int ipx = cv_floor(ctrx), ipy = cv_floor(ctry);
         if (ipx >= 0 && ipx + BW < w && ipy >= 0 && ipy + BW < h) {
-            float a = ctrx - (float)ipx;
-            const float b = ctry - (float)ipy;
-            a = a < 0.0001f ? 0.0001f : a;
-            const float a12 = a * (1.f - b), a22 = a * b, b1 = 1.f - b, b2 = b;
-            const double sd = (1. - (double)a) / (double)a;
-            for (int e = lane; e < NB; e += 64) {
-                const int r = e / BW, j = e - r * BW;
-                const uint8_t* src = img + (size_t)(ipy + r) * stride + ipx;
-                const float t = a12 * (float)src[j + 1] + a22 * (float)src[j + 1 + stride];
-                float prev;
-                if (j == 0) prev = (1.f - a) * (b1 * (float)src[0] + b2 * (float)src[stride]);
-                else {
-                    const float tp = a12 * (float)src[j] + a22 * (float)src[j + stride];
-                    prev = (float)((double)tp * sd);
-                }
-                buf[e] = prev + t;
+            const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
+            if (staged && ipx >= R0x && ipy >= R0y && ipx + BW < R0x + SS && ipy + BW < R0y + SS) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // staged pixels visible
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                fill_in(px8 + (ipy - R0y) * SS + (ipx - R0x), SS, a, b);
+            } else {
+                fill_in(img + (size_t)ipy * stride + ipx, stride, a, b);
             }
         } else {
             const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
@@ -462,10 +500,15 @@ __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (int k = lane; k < NK; k += 64) {
+        SP_ADD(0, t0);
+        SP_MARK(t1);
+#pragma unroll
+        for (int q = 0; q < KPL; q++) {
+            const int k = lane + 64 * q;
+            if (k >= NK) break;
             const int i = k / WW, j = k - i * WW;
             const float* sp = buf + (i + 1) * BW + 1;
-            const double m = mask[k];
+            const double m = mreg[q];
             const double tgx = (double)(sp[j + 1] - sp[j - 1]);
             const double tgy = (double)(sp[j + BW] - sp[j - BW]);
             const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
@@ -479,6 +522,8 @@ __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        SP_ADD(1, t1);
+        SP_MARK(t2);
         double acc = 0;
         if (lane < 5) {
             const double* t = s_t[lane];
@@ -498,6 +543,8 @@ __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__
         }
         const double sa = __shfl(acc, 0, 64), sb = __shfl(acc, 1, 64), sc = __shfl(acc, 2, 64);
         const double bb1 = __shfl(acc, 3, 64), bb2 = __shfl(acc, 4, 64);
+        SP_ADD(2, t2);
+        if (COEB_SUBPIX_CLOCK && lane == 0) atomicAdd(&g_sp_clk[(blockIdx.x & 255) * 8 + 4], 1ull);
         const double det = sa * sc - sb * sb;
         if (fabs(det) <= DBL_EPSILON * DBL_EPSILON) break;
         const double scale = 1.0 / det;
@@ -515,6 +562,7 @@ __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__
         xy[2 * p] = cx; xy[2 * p + 1] = cy;
         if (itcount) { atomicAdd(itcount, it + 1); atomicAdd(itcount + 1, 1); }
     }
+    SP_ADD(3, t_all);
 }
 
 // ============================== pyramidal Lucas-Kanade ==============================
@@ -1663,6 +1711,20 @@ extern "C" int coeb_moving_object_points(coeb_ctx* c, const uint8_t* prev, const
 // ntm_out[0] = 0 (no previous frame).  Enqueued on the context stream, no synchronisation.
 // A/B tool hook: {iterations, corners} counted by the cornerSubPix variants under
 // COEB_SUBPIX_COUNT since the last read (then reset)
+// {fill, terms, sums, whole corner, iterations} cycles of k_subpix summed over corners
+// (COEB_SUBPIX_CLOCK builds), then reset
+extern "C" int coeb_internal_subpix_clock(unsigned long long* out)
+{
+    static unsigned long long h[256 * 8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sp_clk), sizeof(h)) != hipSuccess) return COEB_EDEVICE;
+    for (int k = 0; k < 8; k++) {
+        out[k] = 0;
+        for (int i = 0; i < 256; i++) out[k] += h[i * 8 + k];
+    }
+    static const unsigned long long z[256 * 8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_sp_clk), z, sizeof(z)) == hipSuccess ? COEB_OK : COEB_EDEVICE;
+}
+
 extern "C" int coeb_internal_subpix_count(int* out)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_subpix_count_dev), 8) != hipSuccess) return COEB_EDEVICE;

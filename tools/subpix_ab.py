@@ -37,6 +37,14 @@ def main():
     bp.synchronize()
     L.coeb_internal_subpix_count(cnt.ctypes.data)
     tms, _ = bp.ctx.batch_frame_results(F, F)
+    clk = np.zeros(8, np.uint64)
+    L.coeb_internal_subpix_clock.argtypes = [C.c_void_p]
+    L.coeb_internal_subpix_clock(clk.ctypes.data)       # zeros unless built with COEB_SUBPIX_CLOCK
+    if clk[4]:
+        n = float(clk[4])
+        print(json.dumps(dict(per_iteration_cycles=dict(fill=round(clk[0] / n), terms=round(clk[1] / n),
+                                                        sums=round(clk[2] / n)),
+                              per_corner_cycles=round(float(clk[3]) / max(1, cnt[1])))))
     print(json.dumps(dict(variant=os.environ.get("COEB_SUBPIX_VARIANT", "1"), iterations=int(cnt[0]),
                           corners=int(cnt[1]), iters_per_corner=round(float(cnt[0]) / max(1, cnt[1]), 3),
                           tm_points=int(sum(len(t) for t in tms if t is not None)))))
