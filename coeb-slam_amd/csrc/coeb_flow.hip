@@ -413,23 +413,23 @@ __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__
     xy = at_pair(xy, pz);
     d_n = at_pair(d_n, pz);
     constexpr int WW = 2 * WIN + 1, BW = WW + 2, NB = BW * BW, NK = WW * WW;
-    constexpr int NKP = (NK + 7) & ~7;
     constexpr int KPL = (NK + 63) / 64;                // terms per lane
     // Pixels around the corner staged once (the window may drift kSpM px before a refetch):
     // the per-iteration window then samples LDS instead of re-reading the image.
     constexpr int kSpM = 8, SS = BW + 1 + 2 * kSpM;
+    // the five terms of 64 window pixels at a time: produced by all lanes, summed by lanes 0..4
+    // before the next 64 are written (6.2 KB of LDS per wave instead of 20 with all 441 held)
     __shared__ float s_buf[CPB][NB];
-    __shared__ double s_tt[CPB][5][NKP];
+    __shared__ double s_tt[CPB][5][64];
     __shared__ uint8_t s_px[CPB][SS * SS];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int p = blockIdx.x * CPB + wv;
     float* buf = s_buf[wv];
-    double (*s_t)[NKP] = s_tt[wv];
+    double (*s_t)[64] = s_tt[wv];
     uint8_t* px8 = s_px[wv];
     int n = *d_n;
     n = n < nmax ? n : nmax;
     if (p >= n) return;
-    for (int k = NK + lane; k < NKP; k += 64) for (int q = 0; q < 5; q++) s_t[q][k] = 0.0;
     double mreg[KPL];                                  // this lane's weights, k = lane + 64 q
 #pragma unroll
     for (int q = 0; q < KPL; q++) mreg[q] = lane + 64 * q < NK ? (double)mask[lane + 64 * q] : 0.0;
@@ -501,45 +501,47 @@ __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         SP_ADD(0, t0);
-        SP_MARK(t1);
+        SP_MARK(t2);
+        double acc = 0;
 #pragma unroll
         for (int q = 0; q < KPL; q++) {
             const int k = lane + 64 * q;
-            if (k >= NK) break;
-            const int i = k / WW, j = k - i * WW;
-            const float* sp = buf + (i + 1) * BW + 1;
-            const double m = mreg[q];
-            const double tgx = (double)(sp[j + 1] - sp[j - 1]);
-            const double tgy = (double)(sp[j + BW] - sp[j - BW]);
-            const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
-            const double px = j - WIN, py = i - WIN;
-            s_t[0][k] = gxx;
-            s_t[1][k] = gxy;
-            s_t[2][k] = gyy;
-            s_t[3][k] = gxx * px + gxy * py;
-            s_t[4][k] = gxy * px + gyy * py;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        SP_ADD(1, t1);
-        SP_MARK(t2);
-        double acc = 0;
-        if (lane < 5) {
-            const double* t = s_t[lane];
-            double cur[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) cur[q] = t[q];
-            for (int k0 = 8; k0 <= NKP; k0 += 8) {
-                double nx8[8];
-                const int k1 = k0 < NKP ? k0 : 0;
-#pragma unroll
-                for (int q = 0; q < 8; q++) nx8[q] = t[k1 + q];
-#pragma unroll
-                for (int q = 0; q < 8; q++) acc += cur[q];
-#pragma unroll
-                for (int q = 0; q < 8; q++) cur[q] = nx8[q];
+            double gxx = 0.0, gxy = 0.0, gyy = 0.0, t3 = 0.0, t4 = 0.0;    // +0.0 past the window
+            if (k < NK) {
+                const int i = k / WW, j = k - i * WW;
+                const float* sp = buf + (i + 1) * BW + 1;
+                const double m = mreg[q];
+                const double tgx = (double)(sp[j + 1] - sp[j - 1]);
+                const double tgy = (double)(sp[j + BW] - sp[j - BW]);
+                gxx = tgx * tgx * m; gxy = tgx * tgy * m; gyy = tgy * tgy * m;
+                const double px = j - WIN, py = i - WIN;
+                t3 = gxx * px + gxy * py;
+                t4 = gxy * px + gyy * py;
             }
+            s_t[0][lane] = gxx; s_t[1][lane] = gxy; s_t[2][lane] = gyy; s_t[3][lane] = t3; s_t[4][lane] = t4;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (lane < 5) {
+                const double* t = s_t[lane];
+                double cur[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) cur[u] = t[u];
+#pragma unroll
+                for (int k0 = 8; k0 <= 64; k0 += 8) {
+                    double nx8[8];
+                    const int k1 = k0 < 64 ? k0 : 0;
+#pragma unroll
+                    for (int u = 0; u < 8; u++) nx8[u] = t[k1 + u];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) acc += cur[u];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) cur[u] = nx8[u];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");     // the next 64 overwrite these
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
         const double sa = __shfl(acc, 0, 64), sb = __shfl(acc, 1, 64), sc = __shfl(acc, 2, 64);
         const double bb1 = __shfl(acc, 3, 64), bb2 = __shfl(acc, 4, 64);
