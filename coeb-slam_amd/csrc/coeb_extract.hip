@@ -10,6 +10,7 @@
 //   k_fast       per 30-px cell FAST-9/16 + NMS + iniTh/minTh     (:811-850)
 //   k_octree     per (frame, level) DistributeOctTree emulation   (:546-769, 852-890, 1204-1207)
 //   k_describe   IC_Angle + rBRIEF + output assembly              (:80-156, 902-903, 1291-1337)
+#include <type_traits>
 #include <hip/hip_runtime.h>
 
 #include "coeb_internal.hpp"
@@ -509,7 +510,7 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
 //     :834-838) with ordered (ballot) stores of the kept keys.  A cell with more corners than
 //     the list holds walks the whole window instead.
 constexpr int kFastRowBytes = 72;          // >= 1 + 64 + 7 (slab byte = ROI column + 1)
-constexpr int kFastSurv = 512;             // survivor list (flushed when one more pass could overflow it)
+constexpr int kFastSurv = 384;             // survivor list (flushed when one more pass could overflow it)
 constexpr int kFastCorners = 512;          // corner list
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -609,9 +610,20 @@ __device__ __forceinline__ void fast_pretest4_raw(const uint8_t* c, int t, uint3
         as_us2(win_hi(b0, c0, 3)), as_us2(win_hi(a0, b0, 1)), as_us2(win_hi(bm, cm, 2)), as_us2(win_hi(ap, bp, 2)), T);
 }
 
-__device__ __forceinline__ int nms_keep(const uint8_t* Ms, int o, int t, int* sc_out)
+// M of the detection window is kept in its own compact slab (pitch mp = window width + 2,
+// one zero row / column around the window for the NMS neighbours) instead of a second copy of
+// the 72-byte ROI slab: 6.3 KB of LDS per wave instead of 8.3 KB, so six workgroups (24 waves)
+// fit a CU instead of four.  Detection pixel (row r, col c) sits at (r + 1) * mp + c + 1; the
+// ROI slab offset o of that pixel is (r + 3) * kFastRowBytes + c + 4.
+__device__ __forceinline__ int fast_mi(int o, int mp)
 {
-    const int M = Ms[o];
+    const int yy = (int)((unsigned)o / (unsigned)kFastRowBytes);
+    return (yy - 2) * mp + (o - yy * kFastRowBytes) - 3;
+}
+
+__device__ __forceinline__ int nms_keep(const uint8_t* Ms, int mi, int mp, int t, int* sc_out)
+{
+    const int M = Ms[mi];
     if (M <= t) return 0;
     const int sc = M - 1;
     bool kept = true;
@@ -620,7 +632,7 @@ __device__ __forceinline__ int nms_keep(const uint8_t* Ms, int o, int t, int* sc
 #pragma unroll
         for (int dx = -1; dx <= 1; dx++) {
             if (dx == 0 && dy == 0) continue;
-            const int Mn = Ms[o + dy * kFastRowBytes + dx];
+            const int Mn = Ms[mi + dy * mp + dx];
             const int ns = Mn > t ? Mn - 1 : 0;
             kept = kept && (sc > ns);
         }
@@ -635,7 +647,10 @@ __device__ __forceinline__ int mbcnt(uint64_t m)
 }
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-constexpr int kFastCellsPerWave = 1;
+#ifndef COEB_FAST_CPW
+#define COEB_FAST_CPW 1        // cells per wave (experiment builds: 2 = next cell's ROI loads behind this cell)
+#endif
+constexpr int kFastCellsPerWave = COEB_FAST_CPW;
 constexpr int kFastPass = 12;            // prefetched ROI rows / 4 (cells up to 48 rows)
 
 // Staging of a cell ROI into the wave's slab (slab byte = ROI column + 1, so detection
@@ -757,6 +772,10 @@ __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs
 
 // Bytes of one per-wave ROI (or M) slab: 16-byte multiple so every slab starts 16-aligned.
 __host__ __device__ inline int fast_slab(const Plan& P) { return (kFastRowBytes * P.max_roi_h + 15) & ~15; }
+// compact M slab: pitch = widest detection window + 2 (4-aligned), rows = tallest window + 2
+__host__ __device__ inline int fast_mp(const Plan& P) { return (P.max_roi_w - 6 + 2 + 3) & ~3; }
+__host__ __device__ inline int fast_ms_slab(const Plan& P) { return (fast_mp(P) * (P.max_roi_h - 4) + 15) & ~15; }
+__host__ __device__ inline int fast_wave_lds(const Plan& P) { return fast_slab(P) + fast_ms_slab(P) + 2 * (kFastSurv + kFastCorners); }
 
 #ifndef COEB_BAND_CLOCK
 #define COEB_BAND_CLOCK 0      // experiment builds: phase clocks of wave 0 (band_timing_read)
@@ -783,6 +802,7 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
     const LevelGeom& g = P->lv[c.level];
     const int rw = c.rw, rh = c.rh;
     const int ww = rw - 6, wh = rh - 6;
+    const int mp = fast_mp(*P);
     const int npix = ww > 0 && wh > 0 ? ww * wh : 0;
     // ---- 2 + 3: pre-test 4 pixels per lane (8 or 16 lanes per row), survivors in row-major
     //      order -> exact strength -> corners
@@ -828,7 +848,7 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
                     M = corner_strength(&roi[oo], kFastRowBytes);
                 }
                 const bool isc = e < ns && M > th_min;
-                if (isc) Ms[oo] = (uint8_t)M;
+                if (isc) Ms[fast_mi(oo, mp)] = (uint8_t)M;
                 const uint64_t mc = __ballot(isc);
                 if (isc) {
                     const int qq = nc + mbcnt(mc);
@@ -856,7 +876,7 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
                 int oo = 0, sc = 0, kept = 0;
                 if (e < nc) {
                     oo = corn[e];
-                    kept = nms_keep(Ms, oo, t, &sc);
+                    kept = nms_keep(Ms, fast_mi(oo, mp), mp, t, &sc);
                 }
                 const uint64_t m = __ballot(kept);
                 if (kept) {
@@ -872,9 +892,8 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
             for (int base = 0; base < npix; base += 64) {
                 int col = col0 + lane, row = row0;
                 while (col >= ww) { col -= ww; row++; }
-                const int o = (row + 3) * kFastRowBytes + sh + col + 3;   // == + 4 + col
                 int sc = 0, kept = 0;
-                if (base + lane < npix) kept = nms_keep(Ms, o, t, &sc);
+                if (base + lane < npix) kept = nms_keep(Ms, (row + 1) * mp + col + 1, mp, t, &sc);
                 const uint64_t m = __ballot(kept);
                 if (kept) {
                     const int q = running + mbcnt(m);
@@ -908,7 +927,7 @@ __device__ __forceinline__ CellDesc load_cell(const CellDesc* __restrict__ cells
 
 // One wave per kFastCellsPerWave consecutive cells, four waves per workgroup, no workgroup
 // barriers.  The next cell's ROI loads are issued before the current cell is processed.
-__global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P, ExtractBufs b,
+__global__ __launch_bounds__(kThreads, 6) void k_fast(const Plan* __restrict__ P, ExtractBufs b,
                                                        const CellDesc* __restrict__ cells,   // read-only: scalar loads
                                                        int cell0, int cell1)                 // this launch's cells
 {
@@ -919,11 +938,11 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
     // pairs, no byte gathers; 11 ds_read_b64 per 4-pixel group) cut VALU 7 % but ran 5 % slower
     // (twice the staging stores): the byte slab stays.
     const int wv = threadIdx.x >> 6, lane = lane_id();
-    const int slab = fast_slab(*P);                          // per-wave LDS: roi, M, lists
-    uint8_t* wbase = smem + (size_t)wv * (2 * slab + 2 * (kFastSurv + kFastCorners));
+    const int slab = fast_slab(*P), ms_slab = fast_ms_slab(*P);   // per-wave LDS: roi, M, lists
+    uint8_t* wbase = smem + (size_t)wv * fast_wave_lds(*P);
     uint8_t* roi = wbase;
     uint8_t* Ms = wbase + slab;
-    uint16_t* surv = reinterpret_cast<uint16_t*>(wbase + 2 * slab);
+    uint16_t* surv = reinterpret_cast<uint16_t*>(wbase + slab + ms_slab);
     uint16_t* corn = surv + kFastSurv;
     const int2 bxy = block_xy<false>();
     const int f = bxy.y;
@@ -939,7 +958,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_fast(const Plan* __restrict__ P
     for (int t = 0; t < kFastCellsPerWave; t++, cidx++) {
         FC_MARK(t_st);
         fast_stage(G, R, roi);
-        for (int i = lane; i < (kFastRowBytes * c.rh + 15) / 16; i += 64) reinterpret_cast<uint4*>(Ms)[i] = make_uint4(0, 0, 0, 0);
+        for (int i = lane; i < ms_slab / 16; i += 64) reinterpret_cast<uint4*>(Ms)[i] = make_uint4(0, 0, 0, 0);
         wave_sync_lds();
         FC_ADD(0, t_st);                              // wait for the ROI loads + stage + M clear
         const CellDesc cur = c;
@@ -2037,16 +2056,22 @@ __device__ void sincos_canon(float af, float* s, float* c)
 
 struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
 
-// kDescKp (32) keypoints of one frame per wave, in three phases:
-//   A  lanes k and k+32 = keypoint k: IC_Angle from 16-byte row loads of the unblurred level,
-//      the two halves taking rows -|v| and +|v| (the disc weights depend on |v| only, so they
-//      are compile-time constants for both), realigned in registers so byte j of a row is
-//      patch column j-15; each 4-pixel group costs two v_dot4_u32_u8.  fastAtan2 and the
-//      canonical sincosf run once per keypoint; the cv::KeyPoint record is written here.
+// KP keypoints of one frame per wave (KP = 8 by default), in three phases:
+//   A  kDescLpk = 64/KP lanes per keypoint: IC_Angle from 16-byte row loads of the unblurred
+//      level, half of the lanes taking rows -|v| and half +|v|, each lane KP/2 rows; every row is
+//      realigned in registers so byte j is patch column j-15, masked with the disc row |v| (a
+//      17 x 32 B table in LDS: the rows differ across lanes) and summed by two v_dot4_u32_u8
+//      per 4-pixel group, then reduced over the keypoint's lanes.  fastAtan2 and the canonical
+//      sincosf run on every lane of the keypoint; the cv::KeyPoint record is written here.
 //   B  kDescGroup keypoints per step: their 37 x 64 B blurred patches are staged in the wave's
 //      LDS slab (the next group's are loaded into registers meanwhile); lane = 4 of the 256
 //      tests of each; the nibbles are OR-combined by DPP into the descriptor dwords (LDS).
-//   C  the wave's descriptors (32 x 32 B) are written out with 16-byte stores.
+//   C  the wave's descriptors (KP x 32 B) are written out with 16-byte stores.
+// Few keypoints per wave so that one XCD's resident waves cover few frames: a frame's level and
+// blur images (~1.4 MB of patch rows) then stay in that XCD's 4 MB L2 while its neighbouring
+// patches are read.  With 32 keypoints per wave an XCD had ~20 frames in flight and refetched
+// every patch row (4.6 MB per frame past L2 vs 0.95 MB when only ~2 frames were in flight,
+// tools/_exp_l2.sh).
 // Few wide loads per keypoint: with one byte per lane per load (lane = patch column) the
 // texture-address path, not the VALU, bounded this kernel.
 // The rotated pattern offsets are cvRound of |(px, py)| <= 13*sqrt(2), so |offset| <= 18.
@@ -2054,20 +2079,18 @@ struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
 // different banks, so the 64 lanes' scattered test samples rarely conflict (a 64-byte pitch put
 // every other row on the same 16 banks).
 constexpr int kBlRow = 72, kBlRows = 37, kBlChunks = kBlRows * 4;   // 148 16-byte chunks
-constexpr int kDescKp = 32;                                          // keypoints per wave
 constexpr int kDescGroup = 2;                                        // patches staged per step
-constexpr int kDescSlab = kBlRow * kBlRows * kDescGroup + 32 * kDescKp;   // 6352 B per wave
+template <int KP> constexpr int desc_slab() { return kBlRow * kBlRows * kDescGroup + 32 * KP; }
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};   // ORBextractor.cc:461-476
 
-// Weights of aligned row dword d (patch columns j = 4d..4d+3, u = j - 15) in row |v| = av:
-// W1 = bytes (j * in), W0 = bytes (in), in = |u| <= umax[av].
-__device__ __forceinline__ constexpr uint32_t ic_w(int av, int d, bool with_j)
+// Disc mask of row |v| = av (av 16: all zero), dword d of the realigned row (patch columns
+// j = 4d..4d+3, u = j - 15): byte 0xFF where |u| <= umax[av].
+__device__ __forceinline__ uint32_t ic_mask(int av, int d)
 {
     uint32_t w = 0;
     for (int i = 0; i < 4; i++) {
-        const int j = 4 * d + i, u = j - 15;
-        const bool in = (u < 0 ? -u : u) <= kUmax[av];
-        w |= (uint32_t)(in ? (with_j ? j : 1) : 0) << (8 * i);
+        const int u = 4 * d + i - 15;
+        if (av < 16 && (u < 0 ? -u : u) <= kUmax[av]) w |= 0xFFu << (8 * i);
     }
     return w;
 }
@@ -2105,58 +2128,19 @@ __device__ __forceinline__ void ic_row_load(const uint8_t* rp, uint4& c0, uint4&
     }
 }
 
-// Disc sums of row |v| = av from its 48-byte window (byte a = patch column 0): A += sum j*p,
-// returns the row sum.
-template <int av>
-__device__ __forceinline__ uint32_t ic_row_acc(uint4 c0, uint4 c1, uint4 c2, int a, uint32_t m8, uint32_t m4, uint32_t& A)
-{
-    const uint32_t q[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
-    // realign by a: bit selects (ternaries become a scratch-indexed array), then alignbyte
-    uint32_t r1[10], r2[9];
-#pragma unroll
-    for (int k = 0; k < 10; k++) r1[k] = (m8 & q[k + 2]) | (~m8 & q[k]);
-#pragma unroll
-    for (int k = 0; k < 9; k++) r2[k] = (m4 & r1[k + 1]) | (~m4 & r1[k]);
-    uint32_t rs = 0;
-#pragma unroll
-    for (int d = 0; d < 8; d++) {
-        const uint32_t w1 = ic_w(av, d, true), w0 = ic_w(av, d, false);
-        if (w0 == 0) continue;
-        const uint32_t o = __builtin_amdgcn_alignbyte(r2[d + 1], r2[d], (uint32_t)(a & 3));
-        A = __builtin_amdgcn_udot4(o, w1, A, false);
-        rs = __builtin_amdgcn_udot4(o, w0, rs, false);
-    }
-    return rs;
-}
-
-// Rows |v| = av0 .. av0+3 at row offsets sgn*|v| from `rowp` (4 rows of loads in flight).
-template <bool kVec, int av0>
-__device__ __forceinline__ void ic_rows4(const uint8_t* rowp, int64_t spitch, int a, uint32_t m8, uint32_t m4,
-                                         uint32_t& A, uint32_t& S, int& m01, uint32_t& A0, uint32_t& S0)
-{
-    uint4 c[4][3];
-#pragma unroll
-    for (int r = 0; r < 4; r++) ic_row_load<kVec>(rowp + (av0 + r) * spitch, c[r][0], c[r][1], c[r][2]);
-#define COEB_IC_ACC(r)                                                                   \
-    {                                                                                    \
-        constexpr int av = av0 + r;                                                      \
-        if constexpr (av == 0) {                                                         \
-            S0 += ic_row_acc<0>(c[r][0], c[r][1], c[r][2], a, m8, m4, A0);               \
-        } else {                                                                         \
-            const uint32_t rs = ic_row_acc<av>(c[r][0], c[r][1], c[r][2], a, m8, m4, A); \
-            S += rs;                                                                     \
-            m01 += av * (int)rs;                                                         \
-        }                                                                                \
-    }
-    COEB_IC_ACC(0) COEB_IC_ACC(1) COEB_IC_ACC(2) COEB_IC_ACC(3)
-#undef COEB_IC_ACC
-}
-
-template <bool kVec0>
+template <bool kVec0, int KP>
 // 24 waves per CU (launch bound 6 blocks: 80 VGPRs, 3 spilled) measured 0.253 vs 0.212 ms/step
 __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ P, ExtractBufs b)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t s_slab[kWaves][kDescSlab];
+    constexpr int kLpk = 64 / KP;          // lanes per keypoint in phase A
+    constexpr int kHl = kLpk / 2;          // lanes per half (rows -|v| / +|v|)
+    constexpr int kNr = 16 / kHl;          // IC rows per lane
+    constexpr int kNb = kNr < 4 ? kNr : 4; // rows whose loads are in flight together
+    static_assert(KP >= 2 && KP <= 32 && (KP & (KP - 1)) == 0, "KP: power of two in [2, 32]");
+    __shared__ __attribute__((aligned(16))) uint8_t s_slab[kWaves][desc_slab<KP>()];
+    __shared__ __attribute__((aligned(16))) uint32_t s_msk[17][8];
+    if (threadIdx.x < 17 * 8) s_msk[threadIdx.x >> 3][threadIdx.x & 7] = ic_mask(threadIdx.x >> 3, threadIdx.x & 7);
+    __syncthreads();
     const int2 bxy = block_xy();
     const int f = bxy.y;
     const int L = P->L;
@@ -2170,11 +2154,11 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
     }
     const int total = __builtin_amdgcn_readlane(incl, L - 1);
     if (bxy.x == 0 && threadIdx.x == 0) b.counts[f] = total;
-    const int idx0 = (bxy.x * kWaves + wv) * kDescKp;
+    const int idx0 = (bxy.x * kWaves + wv) * KP;
     if (idx0 >= total) return;
-    const int nk = min(kDescKp, total - idx0);
-    // ---- phase A: lanes k, k+32 = keypoint idx0 + k (excess repeat the last one, no writes)
-    const int kq = lane & 31, half = lane >> 5;
+    const int nk = min(KP, total - idx0);
+    // ---- phase A: lanes kq*kLpk .. +kLpk-1 = keypoint idx0 + kq (excess repeat the last one, no writes)
+    const int kq = lane / kLpk, half = (lane / kHl) & 1, qi = lane % kHl;
     const int id = idx0 + min(kq, nk - 1);
     int l = 0, start = 0;
     for (int q = 0; q < L - 1; q++) {
@@ -2185,38 +2169,60 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
     const uint32_t key = b.lvl_kp[(int64_t)f * P->lvl_stride + g.out_off + (id - start)];
     const int x = key_x(key), y = key_y(key), sc = key_s(key);
     const uint8_t* img = level_ptr(P, b, f, l);
-    // IC_Angle (ORBextractor.cc:80-107): A = sum j*p, S = sum p over the disc, m01 = sum v*rowsum
-    uint32_t A = 0, S = 0, A0 = 0, S0 = 0;
+    // IC_Angle (ORBextractor.cc:80-107): A = sum j*p, S = sum p over the disc, m01 = sum v*rowsum;
+    // lane (half, qi) takes rows |v| = qi + kHl*i, i < kNr (row 0 in the lower half only)
+    uint32_t A = 0, S = 0;
     int m01 = 0;
     const int a = (x - 15) & 15;
     const uint32_t m8 = (a & 8) ? 0xFFFFFFFFu : 0u, m4 = (a & 4) ? 0xFFFFFFFFu : 0u;
     const uint8_t* rowp = img + (int64_t)y * g.pitch + (x - 15 - a);         // row v = 0
     const int64_t spitch = half ? (int64_t)g.pitch : -(int64_t)g.pitch;      // rows +|v| / -|v|
-    if (kVec0 || l != 0) {
-        ic_rows4<true, 0>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
-        ic_rows4<true, 4>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
-        ic_rows4<true, 8>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
-        ic_rows4<true, 12>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
-    } else {
-        ic_rows4<false, 0>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
-        ic_rows4<false, 4>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
-        ic_rows4<false, 8>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
-        ic_rows4<false, 12>(rowp, spitch, a, m8, m4, A, S, m01, A0, S0);
+    const bool vec = kVec0 || l != 0;
+#pragma unroll
+    for (int i0 = 0; i0 < kNr; i0 += kNb) {
+        uint4 c[kNb][3];
+#pragma unroll
+        for (int r = 0; r < kNb; r++) {
+            const uint8_t* rp = rowp + (qi + kHl * (i0 + r)) * spitch;
+            if (vec) ic_row_load<true>(rp, c[r][0], c[r][1], c[r][2]);
+            else ic_row_load<false>(rp, c[r][0], c[r][1], c[r][2]);
+        }
+#pragma unroll
+        for (int r = 0; r < kNb; r++) {
+            const int av = qi + kHl * (i0 + r);
+            const uint32_t* msk = s_msk[(av == 0 && half) ? 16 : av];
+            const uint32_t q[12] = {c[r][0].x, c[r][0].y, c[r][0].z, c[r][0].w, c[r][1].x, c[r][1].y,
+                                    c[r][1].z, c[r][1].w, c[r][2].x, c[r][2].y, c[r][2].z, c[r][2].w};
+            // realign by a: bit selects, then alignbyte
+            uint32_t r1[10], r2[9];
+#pragma unroll
+            for (int k = 0; k < 10; k++) r1[k] = (m8 & q[k + 2]) | (~m8 & q[k]);
+#pragma unroll
+            for (int k = 0; k < 9; k++) r2[k] = (m4 & r1[k + 1]) | (~m4 & r1[k]);
+            uint32_t rs = 0;
+#pragma unroll
+            for (int d = 0; d < 8; d++) {
+                const uint32_t pm = __builtin_amdgcn_alignbyte(r2[d + 1], r2[d], (uint32_t)(a & 3)) & msk[d];
+                A = __builtin_amdgcn_udot4(pm, 0x03020100u + 0x04040404u * (uint32_t)d, A, false);
+                rs = __builtin_amdgcn_udot4(pm, 0x01010101u, rs, false);
+            }
+            S += rs;
+            m01 += av * (int)rs;
+        }
     }
-    if (half == 0) {                   // lower half: rows -|v| (and row 0, counted once)
-        m01 = -m01;
-        A += A0;
-        S += S0;
+    if (half == 0) m01 = -m01;                 // lower half: rows -|v|
+#pragma unroll
+    for (int o = 1; o < kLpk; o <<= 1) {
+        A += __shfl_xor(A, o, 64);
+        S += __shfl_xor(S, o, 64);
+        m01 += __shfl_xor(m01, o, 64);
     }
-    A += __shfl_xor(A, 32, 64);
-    S += __shfl_xor(S, 32, 64);
-    m01 += __shfl_xor(m01, 32, 64);
     const int m10 = (int)A - 15 * (int)S;
     const float angle = fast_atan2_dev((float)m01, (float)m10);
     const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
     float bs, ac;
     sincos_canon(angle * factorPI, &bs, &ac);
-    if (half == 0 && kq < nk) {        // cv::KeyPoint {x, y, size, angle, response, octave, class_id}
+    if (lane % kLpk == 0 && kq < nk) {   // cv::KeyPoint {x, y, size, angle, response, octave, class_id}
         float fx = (float)x, fy = (float)y;
         if (l != 0) { fx *= g.scale; fy *= g.scale; }          // :1327-1334
         KeyPointOut o;
@@ -2248,8 +2254,8 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
 #define COEB_LOAD_PATCH(t, q0, q1, q2)                                                          \
     {                                                                                           \
         const int tt_ = min((t), nk - 1);                                                       \
-        const uint8_t* o_ = blur_f + __builtin_amdgcn_readlane(porg, tt_);                      \
-        const int bpt_ = __builtin_amdgcn_readlane(bpitch, tt_);                                \
+        const uint8_t* o_ = blur_f + __builtin_amdgcn_readlane(porg, tt_ * kLpk);               \
+        const int bpt_ = __builtin_amdgcn_readlane(bpitch, tt_ * kLpk);                         \
         q0 = *reinterpret_cast<const uint4*>(o_ + eo0 * bpt_ + ec0);                            \
         q1 = *reinterpret_cast<const uint4*>(o_ + eo1 * bpt_ + ec1);                            \
         q2 = *reinterpret_cast<const uint4*>(o_ + eo2 * bpt_ + ec2);                            \
@@ -2281,9 +2287,9 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         for (int k = 0; k < kDescGroup; k++) {
             const int t = t0 + k;
             if (t >= nk) break;
-            const float tb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bs), t));
-            const float ta = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ac), t));
-            const uint8_t* bc = slab + k * kBlRow * kBlRows + 18 * kBlRow + __builtin_amdgcn_readlane(xoff, t);
+            const float tb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bs), t * kLpk));
+            const float ta = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ac), t * kLpk));
+            const uint8_t* bc = slab + k * kBlRow * kBlRows + 18 * kBlRow + __builtin_amdgcn_readlane(xoff, t * kLpk);
             // (row, col) = (fma(px, b, py*a), fma(px, a, -(py*b))) as packed-f32 pairs: the same
             // two roundings per component as the reference's fused forms, half the instructions
             const f32x2 AB = {ta, tb}, BA = {tb, ta};
@@ -2353,7 +2359,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         items += bw.nstrips[l] * (nbands / 4);
     }
     bw.item_off[plan.L] = items;
-    const int fast_lds = kWaves * (2 * fast_slab(plan) + 2 * (kFastSurv + kFastCorners));
+    const int fast_lds = kWaves * fast_wave_lds(plan);
     constexpr int kFastPerBlock = kWaves * kFastCellsPerWave;
     auto blur = [&](hipStream_t st, int i0, int i1) {
         if (i1 <= i0) return;
@@ -2444,7 +2450,22 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     if (late) (void)hipStreamWaitEvent(s, side->join2, 0);      // blurred levels ready
     prof_begin(prof, "k_describe", s);
     const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
-    hipLaunchKernelGGL(vec0 ? k_describe<true> : k_describe<false>, dim3((plan.kcap + kWaves * kDescKp - 1) / (kWaves * kDescKp), F), dim3(kThreads), 0, s, d_plan, b);
+    // keypoints per wave: 8 (COEB_DESC_KP = 4 / 16 / 32 for experiments; 32 was round 1's form)
+    static const int kp = [] { const char* e = getenv("COEB_DESC_KP"); const int v = e ? atoi(e) : 8;
+                               return v == 4 || v == 16 || v == 32 ? v : 8; }();
+    auto describe = [&](auto kv, auto kpc) {
+        constexpr int KP = decltype(kpc)::value;
+        hipLaunchKernelGGL((k_describe<decltype(kv)::value, KP>), dim3((plan.kcap + kWaves * KP - 1) / (kWaves * KP), F),
+                           dim3(kThreads), 0, s, d_plan, b);
+    };
+    using T = std::true_type;
+    using Fl = std::false_type;
+    switch (kp) {
+        case 4: vec0 ? describe(T{}, std::integral_constant<int, 4>{}) : describe(Fl{}, std::integral_constant<int, 4>{}); break;
+        case 16: vec0 ? describe(T{}, std::integral_constant<int, 16>{}) : describe(Fl{}, std::integral_constant<int, 16>{}); break;
+        case 32: vec0 ? describe(T{}, std::integral_constant<int, 32>{}) : describe(Fl{}, std::integral_constant<int, 32>{}); break;
+        default: vec0 ? describe(T{}, std::integral_constant<int, 8>{}) : describe(Fl{}, std::integral_constant<int, 8>{}); break;
+    }
     prof_end(prof, s);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
