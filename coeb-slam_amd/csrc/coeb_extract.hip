@@ -509,9 +509,11 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
 //  4. NMS over the corner list at iniThFAST (fallback minThFAST if the cell came out empty,
 //     :834-838) with ordered (ballot) stores of the kept keys.  A cell with more corners than
 //     the list holds walks the whole window instead.
-constexpr int kFastRowBytes = 72;          // >= 1 + 64 + 7 (slab byte = ROI column + 1)
+constexpr int kFastRowBytes = 72;          // >= 1 + 64 + 7 (slab byte = ROI column + 1): any ROI up to 64 wide
+constexpr int kFastRowBytesM = 96;         // ROIs up to 46 wide: pixels in bytes 0..47, M in bytes 48..95
+// (24 dwords: the four rows a half-wave's pre-test reads land on disjoint banks, (a/4) mod 32)
 constexpr int kFastSurv = 384;             // survivor list (flushed when one more pass could overflow it)
-constexpr int kFastCorners = 512;          // corner list
+constexpr int kFastCorners = 384;          // corner list (more corners: NMS walks the whole window)
 
 __device__ __forceinline__ void wave_sync_lds()
 {
@@ -562,35 +564,11 @@ __device__ __forceinline__ uint32_t pretest_half(us2 v, us2 p0, us2 p8, us2 p2, 
     return as_u32(pk_subs(lo, md)) | as_u32(pk_subs(mb, hi));
 }
 
-__device__ __forceinline__ uint32_t fast_pretest4(const uint8_t* c, int t)
-{
-    constexpr int st = kFastRowBytes;
-    const uint32_t* r0 = reinterpret_cast<const uint32_t*>(c);
-    const uint32_t* rp2 = reinterpret_cast<const uint32_t*>(c + 2 * st);
-    const uint32_t* rm2 = reinterpret_cast<const uint32_t*>(c - 2 * st);
-    const uint32_t a0 = r0[-1], b0 = r0[0], c0 = r0[1];
-    const uint32_t ap = rp2[-1], bp = rp2[0], cp = rp2[1];
-    const uint32_t am = rm2[-1], bm = rm2[0], cm = rm2[1];
-    const uint32_t u3 = *reinterpret_cast<const uint32_t*>(c + 3 * st);
-    const uint32_t d3 = *reinterpret_cast<const uint32_t*>(c - 3 * st);
-    const us2 T = pk2(t, t);
-    // low pair = pixels 0,1; high pair = pixels 2,3
-    const uint32_t sl = __builtin_amdgcn_perm(0u, b0, 0x0c010c00u), sh2 = __builtin_amdgcn_perm(0u, b0, 0x0c030c02u);
-    const uint32_t lo = pretest_half(
-        as_us2(sl), as_us2(__builtin_amdgcn_perm(0u, u3, 0x0c010c00u)), as_us2(__builtin_amdgcn_perm(0u, d3, 0x0c010c00u)),
-        as_us2(win_lo(bp, cp, 2)), as_us2(win_lo(am, bm, 2)), as_us2(win_lo(b0, c0, 3)), as_us2(win_lo(a0, b0, 1)),
-        as_us2(win_lo(bm, cm, 2)), as_us2(win_lo(ap, bp, 2)), T);
-    const uint32_t hi = pretest_half(
-        as_us2(sh2), as_us2(__builtin_amdgcn_perm(0u, u3, 0x0c030c02u)), as_us2(__builtin_amdgcn_perm(0u, d3, 0x0c030c02u)),
-        as_us2(win_hi(bp, cp, 2)), as_us2(win_hi(am, bm, 2)), as_us2(win_hi(b0, c0, 3)), as_us2(win_hi(a0, b0, 1)),
-        as_us2(win_hi(bm, cm, 2)), as_us2(win_hi(ap, bp, 2)), T);
-    return ((lo & 0xffffu) ? 1u : 0u) | ((lo >> 16) ? 2u : 0u) | ((hi & 0xffffu) ? 4u : 0u) | ((hi >> 16) ? 8u : 0u);
-}
-
 // Same test, raw packed results: pixel q survives iff 16-bit half q of (lo, hi) is nonzero.
+template <int RB>
 __device__ __forceinline__ void fast_pretest4_raw(const uint8_t* c, int t, uint32_t& lo, uint32_t& hi)
 {
-    constexpr int st = kFastRowBytes;
+    constexpr int st = RB;
     const uint32_t* r0 = reinterpret_cast<const uint32_t*>(c);
     const uint32_t* rp2 = reinterpret_cast<const uint32_t*>(c + 2 * st);
     const uint32_t* rm2 = reinterpret_cast<const uint32_t*>(c - 2 * st);
@@ -610,15 +588,23 @@ __device__ __forceinline__ void fast_pretest4_raw(const uint8_t* c, int t, uint3
         as_us2(win_hi(b0, c0, 3)), as_us2(win_hi(a0, b0, 1)), as_us2(win_hi(bm, cm, 2)), as_us2(win_hi(ap, bp, 2)), T);
 }
 
-// M of the detection window is kept in its own compact slab (pitch mp = window width + 2,
-// one zero row / column around the window for the NMS neighbours) instead of a second copy of
-// the 72-byte ROI slab: 6.3 KB of LDS per wave instead of 8.3 KB, so six workgroups (24 waves)
-// fit a CU instead of four.  Detection pixel (row r, col c) sits at (r + 1) * mp + c + 1; the
-// ROI slab offset o of that pixel is (r + 3) * kFastRowBytes + c + 4.
+// M of the detection window (zero around it, for the NMS neighbours):
+//  * RB = kFastRowBytesM: in the right half of the pixel slab's own rows, M of the pixel at slab
+//    offset o at o + 45 (columns 48.., rows 2..rh-3), pitch RB;
+//  * RB = kFastRowBytes: a compact slab of its own (pitch mp = window width + 2, one zero row /
+//    column around the window): detection pixel (r, c) at (r + 1) * mp + c + 1.
+// Either way 5.8-6.6 KB of LDS per wave instead of 8.3 KB for two 72-byte slabs, so 6-7
+// workgroups fit a CU instead of four.  The ROI slab offset o of detection pixel (r, c) is
+// (r + 3) * RB + c + 4.
+template <int RB>
 __device__ __forceinline__ int fast_mi(int o, int mp)
 {
-    const int yy = (int)((unsigned)o / (unsigned)kFastRowBytes);
-    return (yy - 2) * mp + (o - yy * kFastRowBytes) - 3;
+    if constexpr (RB == kFastRowBytesM) {
+        return o + 45;
+    } else {
+        const int yy = (int)((unsigned)o / (unsigned)RB);
+        return (yy - 2) * mp + (o - yy * RB) - 3;
+    }
 }
 
 __device__ __forceinline__ int nms_keep(const uint8_t* Ms, int mi, int mp, int t, int* sc_out)
@@ -647,10 +633,6 @@ __device__ __forceinline__ int mbcnt(uint64_t m)
 }
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-#ifndef COEB_FAST_CPW
-#define COEB_FAST_CPW 1        // cells per wave (experiment builds: 2 = next cell's ROI loads behind this cell)
-#endif
-constexpr int kFastCellsPerWave = COEB_FAST_CPW;
 constexpr int kFastPass = 12;            // prefetched ROI rows / 4 (cells up to 48 rows)
 
 // Staging of a cell ROI into the wave's slab (slab byte = ROI column + 1, so detection
@@ -665,9 +647,9 @@ struct FastCellGeom {
 
 // ROI prefetch registers: 16-byte path (lane = row (lane >> 2) + 16 i, chunk lane & 3) or
 // word path (lane = row (lane >> 4) + 4 i, word lane & 15).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // native vector: stays in VGPRs
 struct FastRegs {
-    uint4 v0, v1, v2;
-    uint32_t q0[kFastPass];
+    u32x4 v0, v1, v2;                  // 16-byte path only: the word path loads when it stages
 };
 
 __device__ __forceinline__ FastCellGeom fast_geom(const Plan* P, const ExtractBufs& b, int f, const CellDesc& c)
@@ -690,26 +672,16 @@ __device__ __forceinline__ void fast_prefetch(const FastCellGeom& G, FastRegs& R
         // three 16-byte loads per lane cover 48 rows x 64 bytes from (x0 - 1) & ~15
         const uint8_t* base = G.img + (int64_t)G.y0 * G.pitch + ((G.x0 - 1) & ~15) + 16 * (lane & 3);
         const int r = lane >> 2;
-        R.v0 = *reinterpret_cast<const uint4*>(base + (int64_t)min(r, G.rh - 1) * G.pitch);
-        R.v1 = *reinterpret_cast<const uint4*>(base + (int64_t)min(r + 16, G.rh - 1) * G.pitch);
-        R.v2 = *reinterpret_cast<const uint4*>(base + (int64_t)min(r + 32, G.rh - 1) * G.pitch);
-        return;
+        R.v0 = *reinterpret_cast<const u32x4*>(base + (int64_t)min(r, G.rh - 1) * G.pitch);
+        R.v1 = *reinterpret_cast<const u32x4*>(base + (int64_t)min(r + 16, G.rh - 1) * G.pitch);
+        R.v2 = *reinterpret_cast<const u32x4*>(base + (int64_t)min(r + 32, G.rh - 1) * G.pitch);
     }
-    if (!G.words) return;
-    const int gx = G.x0 - 1;
-    const int k = min(lane & 15, G.nwords);
-    const uint32_t* base = reinterpret_cast<const uint32_t*>(G.img + (int64_t)G.y0 * G.pitch + (gx & ~3)) + k;
-    const int pw = G.pitch >> 2;
-    const int npass = (G.rh + 3) >> 2;
-#pragma unroll
-    for (int i = 0; i < kFastPass; i++)
-        if (i < npass) R.q0[i] = base[min((lane >> 4) + 4 * i, G.rh - 1) * pw];
 }
 
 // One 16-byte chunk of the vec path realigned by sh = (x0 - 1) & 15 (wave-uniform): slab
 // dwords 4c .. 4c+3 of the lane's row = source bytes sh + 16c .. sh + 16c + 15, taken from this
 // lane's chunk and the next lane's (DPP; chunk 3 is never stored, so its neighbour is moot).
-__device__ __forceinline__ void fast_stage_chunk(uint4 q, uint32_t m2, uint32_t m1, uint32_t bsh, uint8_t* dst,
+__device__ __forceinline__ void fast_stage_chunk(u32x4 q, uint32_t m2, uint32_t m1, uint32_t bsh, uint8_t* dst,
                                                  bool store)
 {
     const uint32_t w[8] = {q.x, q.y, q.z, q.w, dpp_shl1(q.x), dpp_shl1(q.y), dpp_shl1(q.z), dpp_shl1(q.w)};
@@ -725,6 +697,7 @@ __device__ __forceinline__ void fast_stage_chunk(uint4 q, uint32_t m2, uint32_t 
     }
 }
 
+template <int RB>
 __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs& R, uint8_t* roi)
 {
     const int lane = lane_id();
@@ -733,23 +706,30 @@ __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs
         const uint32_t m2 = (sh & 8) ? 0xFFFFFFFFu : 0u, m1 = (sh & 4) ? 0xFFFFFFFFu : 0u;
         const uint32_t bsh = (uint32_t)(sh & 3);
         const int r = lane >> 2, c = lane & 3;
-        uint8_t* d = roi + r * kFastRowBytes + 16 * c;
+        uint8_t* d = roi + r * RB + 16 * c;
         fast_stage_chunk(R.v0, m2, m1, bsh, d, c < 3 && r < G.rh);
-        fast_stage_chunk(R.v1, m2, m1, bsh, d + 16 * kFastRowBytes, c < 3 && r + 16 < G.rh);
-        fast_stage_chunk(R.v2, m2, m1, bsh, d + 32 * kFastRowBytes, c < 3 && r + 32 < G.rh);
+        fast_stage_chunk(R.v1, m2, m1, bsh, d + 16 * RB, c < 3 && r + 16 < G.rh);
+        fast_stage_chunk(R.v2, m2, m1, bsh, d + 32 * RB, c < 3 && r + 32 < G.rh);
     } else if (G.words) {
-        const uint32_t* q0 = R.q0;
+        const int gx = G.x0 - 1;
+        const int kw = min(lane & 15, G.nwords);
+        const uint32_t* wbase = reinterpret_cast<const uint32_t*>(G.img + (int64_t)G.y0 * G.pitch + (gx & ~3)) + kw;
+        const int pw = G.pitch >> 2;
+        const int npass = (G.rh + 3) >> 2;
+        uint32_t q0[kFastPass];
+#pragma unroll
+        for (int i = 0; i < kFastPass; i++)
+            if (i < npass) q0[i] = wbase[min((lane >> 4) + 4 * i, G.rh - 1) * pw];
         // word k of slab row = ROI columns 4k-1 .. 4k+2 = this lane's aligned word joined
         // with the next lane's (DPP row shift; one slab row = one 16-lane DPP row)
         const int al = (G.x0 - 1) & 3;
-        const int npass = (G.rh + 3) >> 2;
 #pragma unroll
         for (int i = 0; i < kFastPass; i++) {
             if (i < npass) {
                 const uint32_t q1 = dpp_shl1(q0[i]);
                 const int yy = (lane >> 4) + 4 * i;
                 if (yy < G.rh && (lane & 15) < G.nwords)
-                    *reinterpret_cast<uint32_t*>(roi + yy * kFastRowBytes + 4 * (lane & 15)) =
+                    *reinterpret_cast<uint32_t*>(roi + yy * RB + 4 * (lane & 15)) =
                         __builtin_amdgcn_alignbyte(q1, q0[i], (uint32_t)al);
             }
         }
@@ -760,22 +740,30 @@ __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs
         for (int yy = lane >> 4; yy < G.rh; yy += 4)
             for (int k = lane & 15; k < G.nwords; k += 16) {
                 const uint32_t* q = reinterpret_cast<const uint32_t*>(base + (int64_t)yy * G.pitch) + k;
-                *reinterpret_cast<uint32_t*>(roi + yy * kFastRowBytes + 4 * k) =
+                *reinterpret_cast<uint32_t*>(roi + yy * RB + 4 * k) =
                     __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)al);
             }
     } else {
         for (int yy = lane >> 4; yy < G.rh; yy += 4)
             for (int xx = lane & 15; xx < G.rw; xx += 16)
-                roi[yy * kFastRowBytes + 1 + xx] = G.img[(int64_t)(G.y0 + yy) * G.pitch + G.x0 + xx];
+                roi[yy * RB + 1 + xx] = G.img[(int64_t)(G.y0 + yy) * G.pitch + G.x0 + xx];
     }
 }
 
 // Bytes of one per-wave ROI (or M) slab: 16-byte multiple so every slab starts 16-aligned.
-__host__ __device__ inline int fast_slab(const Plan& P) { return (kFastRowBytes * P.max_roi_h + 15) & ~15; }
-// compact M slab: pitch = widest detection window + 2 (4-aligned), rows = tallest window + 2
+// Per-wave LDS of k_fast<RB>: pixel slab (+ M slab for RB = kFastRowBytes), survivor list with
+// one scratch slot per lane, corner list.  RB = kFastRowBytesM when every ROI is <= 46 wide.
+__host__ __device__ inline int fast_rb(const Plan& P) { return P.max_roi_w <= 46 ? kFastRowBytesM : kFastRowBytes; }
+__host__ __device__ inline int fast_slab(const Plan& P, int rb) { return (rb * P.max_roi_h + 15) & ~15; }
 __host__ __device__ inline int fast_mp(const Plan& P) { return (P.max_roi_w - 6 + 2 + 3) & ~3; }
-__host__ __device__ inline int fast_ms_slab(const Plan& P) { return (fast_mp(P) * (P.max_roi_h - 4) + 15) & ~15; }
-__host__ __device__ inline int fast_wave_lds(const Plan& P) { return fast_slab(P) + fast_ms_slab(P) + 2 * (kFastSurv + kFastCorners); }
+__host__ __device__ inline int fast_ms_slab(const Plan& P, int rb)
+{
+    return rb == kFastRowBytesM ? 0 : (fast_mp(P) * (P.max_roi_h - 4) + 15) & ~15;
+}
+__host__ __device__ inline int fast_wave_lds(const Plan& P, int rb)
+{
+    return fast_slab(P, rb) + fast_ms_slab(P, rb) + 2 * (kFastSurv + 64 + kFastCorners);
+}
 
 #ifndef COEB_BAND_CLOCK
 #define COEB_BAND_CLOCK 0      // experiment builds: phase clocks of wave 0 (band_timing_read)
@@ -793,6 +781,7 @@ __device__ unsigned long long g_fast_clk[256 * 8];
 #define FC_ADD(slot, t0) do { if (COEB_FAST_CLOCK && lane_id() == 0) atomicAdd(&FC_SLOT(slot), (unsigned long long)((long long)clock64() - (t0))); } while (0)
 
 // Pre-test, exact strength, NMS and ordered output of one staged cell.
+template <int RB>
 __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, int f, int cidx, const CellDesc& c,
                                           int th_ini, int th_min, const uint8_t* roi, uint8_t* Ms, uint16_t* surv,
                                           uint16_t* corn)
@@ -802,7 +791,7 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
     const LevelGeom& g = P->lv[c.level];
     const int rw = c.rw, rh = c.rh;
     const int ww = rw - 6, wh = rh - 6;
-    const int mp = fast_mp(*P);
+    const int mp = RB == kFastRowBytesM ? RB : fast_mp(*P);   // M pitch
     const int npix = ww > 0 && wh > 0 ? ww * wh : 0;
     // ---- 2 + 3: pre-test 4 pixels per lane (8 or 16 lanes per row), survivors in row-major
     //      order -> exact strength -> corners
@@ -812,31 +801,36 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
     const int cg = lane & ((1 << lpr_log) - 1), rsub = lane >> lpr_log;
     const int rpi = 64 >> lpr_log;
     // lanes' pixel columns inside the window (fixed for the cell): one wave mask per pixel slot
-    const uint64_t vm0 = __ballot(cg < ngrp && 4 * cg + 0 < ww), vm1 = __ballot(cg < ngrp && 4 * cg + 1 < ww);
-    const uint64_t vm2 = __ballot(cg < ngrp && 4 * cg + 2 < ww), vm3 = __ballot(cg < ngrp && 4 * cg + 3 < ww);
-    int o = (rsub + 3) * kFastRowBytes + 4 + 4 * cg;
+    const bool vm0 = cg < ngrp && 4 * cg + 0 < ww, vm1 = cg < ngrp && 4 * cg + 1 < ww;
+    const bool vm2 = cg < ngrp && 4 * cg + 2 < ww, vm3 = cg < ngrp && 4 * cg + 3 < ww;
+    const int dmy = kFastSurv + lane;     // this lane's scratch slot for pixels that did not survive
+    int o = (rsub + 3) * RB + 4 + 4 * cg;
     FC_MARK(t_scan);
     long long t_str = 0;
     // (reading pass k+1's slab words before evaluating pass k, pre_load / pre_eval, measured
     // 0.330 vs 0.318 ms; a lane-per-group mapping that keeps all 64 lanes busy on 30-37-px
     // windows measured 0.338: the scan is not the bound, `tools/_fast_timing.py`)
-    for (int r0 = 0; npix > 0 && r0 < wh; r0 += rpi, o += rpi * kFastRowBytes) {
+    for (int r0 = 0; npix > 0 && r0 < wh; r0 += rpi, o += rpi * RB) {
         // every lane runs the test (rows past the window read slab bytes that are masked off)
         uint32_t lo, hi;
-        fast_pretest4_raw(&roi[o], th_min, lo, hi);
-        const uint64_t rm = __ballot(r0 + rsub < wh);
-        const uint64_t m0 = __ballot((lo & 0xffffu) != 0u) & vm0 & rm, m1 = __ballot((lo >> 16) != 0u) & vm1 & rm;
-        const uint64_t m2 = __ballot((hi & 0xffffu) != 0u) & vm2 & rm, m3 = __ballot((hi >> 16) != 0u) & vm3 & rm;
-        const uint64_t any = m0 | m1 | m2 | m3;
-        if ((any >> lane) & 1u) {
-            const uint64_t me = 1ull << lane;
+        fast_pretest4_raw<RB>(&roi[o], th_min, lo, hi);
+        const bool rv = r0 + rsub < wh;
+        const bool f0 = rv && vm0 && (lo & 0xffffu) != 0u, f1 = rv && vm1 && (lo >> 16) != 0u;
+        const bool f2 = rv && vm2 && (hi & 0xffffu) != 0u, f3 = rv && vm3 && (hi >> 16) != 0u;
+        const uint64_t m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2), m3 = __ballot(f3);
+        if (m0 | m1 | m2 | m3) {
+            // row-major order: pixel q of this lane after every survivor of the lanes below; stores
+            // without branches (a pixel that did not survive goes to the lane's scratch slot)
             int q = ns + mbcnt(m0) + mbcnt(m1) + mbcnt(m2) + mbcnt(m3);
-            if (m0 & me) surv[q++] = (uint16_t)o;
-            if (m1 & me) surv[q++] = (uint16_t)(o + 1);
-            if (m2 & me) surv[q++] = (uint16_t)(o + 2);
-            if (m3 & me) surv[q] = (uint16_t)(o + 3);
+            surv[f0 ? q : dmy] = (uint16_t)o;
+            q += f0 ? 1 : 0;
+            surv[f1 ? q : dmy] = (uint16_t)(o + 1);
+            q += f1 ? 1 : 0;
+            surv[f2 ? q : dmy] = (uint16_t)(o + 2);
+            q += f2 ? 1 : 0;
+            surv[f3 ? q : dmy] = (uint16_t)(o + 3);
+            ns = uniform(ns + __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
         }
-        ns = uniform(ns + __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
         if (ns > kFastSurv - 256 || r0 + rpi >= wh) {
             FC_MARK(t_s0);
             wave_sync_lds();
@@ -845,10 +839,10 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
                 int oo = 0, M = 0;
                 if (e < ns) {
                     oo = surv[e];
-                    M = corner_strength(&roi[oo], kFastRowBytes);
+                    M = corner_strength(&roi[oo], RB);
                 }
                 const bool isc = e < ns && M > th_min;
-                if (isc) Ms[fast_mi(oo, mp)] = (uint8_t)M;
+                if (isc) Ms[fast_mi<RB>(oo, mp)] = (uint8_t)M;
                 const uint64_t mc = __ballot(isc);
                 if (isc) {
                     const int qq = nc + mbcnt(mc);
@@ -876,12 +870,12 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
                 int oo = 0, sc = 0, kept = 0;
                 if (e < nc) {
                     oo = corn[e];
-                    kept = nms_keep(Ms, fast_mi(oo, mp), mp, t, &sc);
+                    kept = nms_keep(Ms, fast_mi<RB>(oo, mp), mp, t, &sc);
                 }
                 const uint64_t m = __ballot(kept);
                 if (kept) {
                     const int q = running + mbcnt(m);
-                    const int yy = oo / kFastRowBytes, xx = oo - yy * kFastRowBytes - sh;
+                    const int yy = oo / RB, xx = oo - yy * RB - sh;
                     if (q < P->cell_cap) out[q] = pack_key(xx + c.j * g.wcell, yy + c.i * g.hcell, sc);
                     else atomicOr(b.err, 2);
                 }
@@ -893,7 +887,8 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
                 int col = col0 + lane, row = row0;
                 while (col >= ww) { col -= ww; row++; }
                 int sc = 0, kept = 0;
-                if (base + lane < npix) kept = nms_keep(Ms, (row + 1) * mp + col + 1, mp, t, &sc);
+                const int mi = RB == kFastRowBytesM ? (row + 3) * RB + col + 4 + 45 : (row + 1) * mp + col + 1;
+                if (base + lane < npix) kept = nms_keep(Ms, mi, mp, t, &sc);
                 const uint64_t m = __ballot(kept);
                 if (kept) {
                     const int q = running + mbcnt(m);
@@ -925,8 +920,10 @@ __device__ __forceinline__ CellDesc load_cell(const CellDesc* __restrict__ cells
     return c;
 }
 
-// One wave per kFastCellsPerWave consecutive cells, four waves per workgroup, no workgroup
-// barriers.  The next cell's ROI loads are issued before the current cell is processed.
+// One wave per cell, four waves per workgroup, no workgroup barriers.  (Two cells per wave with
+// the second cell's ROI loads issued before the first is processed spilled 240 B per lane and
+// ran 2.7x slower.)
+template <int RB>
 __global__ __launch_bounds__(kThreads, 6) void k_fast(const Plan* __restrict__ P, ExtractBufs b,
                                                        const CellDesc* __restrict__ cells,   // read-only: scalar loads
                                                        int cell0, int cell1)                 // this launch's cells
@@ -938,40 +935,37 @@ __global__ __launch_bounds__(kThreads, 6) void k_fast(const Plan* __restrict__ P
     // pairs, no byte gathers; 11 ds_read_b64 per 4-pixel group) cut VALU 7 % but ran 5 % slower
     // (twice the staging stores): the byte slab stays.
     const int wv = threadIdx.x >> 6, lane = lane_id();
-    const int slab = fast_slab(*P), ms_slab = fast_ms_slab(*P);   // per-wave LDS: roi, M, lists
-    uint8_t* wbase = smem + (size_t)wv * fast_wave_lds(*P);
+    const int slab = fast_slab(*P, RB), ms_slab = fast_ms_slab(*P, RB);   // per-wave LDS: roi, M, lists
+    uint8_t* wbase = smem + (size_t)wv * fast_wave_lds(*P, RB);
     uint8_t* roi = wbase;
-    uint8_t* Ms = wbase + slab;
+    uint8_t* Ms = RB == kFastRowBytesM ? wbase : wbase + slab;
     uint16_t* surv = reinterpret_cast<uint16_t*>(wbase + slab + ms_slab);
-    uint16_t* corn = surv + kFastSurv;
+    uint16_t* corn = surv + kFastSurv + 64;     // surv: kFastSurv entries + one scratch slot per lane
     const int2 bxy = block_xy<false>();
     const int f = bxy.y;
-    int cidx = cell0 + (bxy.x * kWaves + wv) * kFastCellsPerWave;
+    const int cidx = cell0 + bxy.x * kWaves + wv;
     if (cidx >= cell1) return;
     const int area = b.dyn[f].area_flag;
     const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
-    CellDesc c = load_cell(cells, cidx);
-    FastCellGeom G = fast_geom(P, b, f, c);
+    const CellDesc c = load_cell(cells, cidx);
+    const FastCellGeom G = fast_geom(P, b, f, c);
     FastRegs R;
     fast_prefetch(G, R);
     FC_MARK(t_all);
-    for (int t = 0; t < kFastCellsPerWave; t++, cidx++) {
-        FC_MARK(t_st);
-        fast_stage(G, R, roi);
-        for (int i = lane; i < ms_slab / 16; i += 64) reinterpret_cast<uint4*>(Ms)[i] = make_uint4(0, 0, 0, 0);
-        wave_sync_lds();
-        FC_ADD(0, t_st);                              // wait for the ROI loads + stage + M clear
-        const CellDesc cur = c;
-        const bool more = t + 1 < kFastCellsPerWave && cidx + 1 < cell1;
-        if (more) {
-            c = load_cell(cells, cidx + 1);
-            G = fast_geom(P, b, f, c);
-            fast_prefetch(G, R);
+    FC_MARK(t_st);
+    fast_stage<RB>(G, R, roi);
+    if (RB == kFastRowBytesM) {
+        // M columns 48..95 of rows 2 .. rh-3 (the staging writes columns 0..47 only)
+        for (int i = lane; i < 3 * (c.rh - 4); i += 64) {
+            const int row = 2 + i / 3;
+            reinterpret_cast<uint4*>(Ms + row * RB + 48)[i - 3 * (row - 2)] = make_uint4(0, 0, 0, 0);
         }
-        fast_cell(P, b, f, cidx, cur, th_ini, th_min, roi, Ms, surv, corn);
-        if (!more) break;
-        wave_sync_lds();
+    } else {
+        for (int i = lane; i < ms_slab / 16; i += 64) reinterpret_cast<uint4*>(Ms)[i] = make_uint4(0, 0, 0, 0);
     }
+    wave_sync_lds();
+    FC_ADD(0, t_st);                              // wait for the ROI loads + stage + M clear
+    fast_cell<RB>(P, b, f, cidx, c, th_ini, th_min, roi, Ms, surv, corn);
     FC_ADD(4, t_all);
 }
 
@@ -1017,7 +1011,6 @@ __device__ __forceinline__ FastSeg load_seg(const FastSeg* __restrict__ segs, in
 
 // Staging registers of one segment: chunk q of thread t = flat 16-byte chunk t + 256 q of the
 // segment's rows (named registers: an array here was demoted to scratch)
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // native vector: stays in VGPRs
 struct BandStage {
     u32x4 v0, v1, v2, v3;
 };
@@ -2359,8 +2352,11 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         items += bw.nstrips[l] * (nbands / 4);
     }
     bw.item_off[plan.L] = items;
-    const int fast_lds = kWaves * fast_wave_lds(plan);
-    constexpr int kFastPerBlock = kWaves * kFastCellsPerWave;
+    // COEB_FAST_RB=72 forces the general slab layout (tests run both layouts)
+    const char* frb = getenv("COEB_FAST_RB");
+    const int fast_rbytes = frb && atoi(frb) == kFastRowBytes ? kFastRowBytes : fast_rb(plan);
+    const int fast_lds = kWaves * fast_wave_lds(plan, fast_rbytes);
+    constexpr int kFastPerBlock = kWaves;
     auto blur = [&](hipStream_t st, int i0, int i1) {
         if (i1 <= i0) return;
         BlurWork w = bw;
@@ -2380,7 +2376,8 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         prof_begin(prof, "k_fast", st);
         if (per_cell || plan.nsegs == 0) {
             const int c0 = plan.lv[l0].cell0, c1 = l1 < plan.L ? plan.lv[l1].cell0 : plan.ncells;
-            hipLaunchKernelGGL(k_fast, dim3((c1 - c0 + kFastPerBlock - 1) / kFastPerBlock, F), dim3(kThreads), fast_lds,
+            hipLaunchKernelGGL(fast_rbytes == kFastRowBytesM ? k_fast<kFastRowBytesM> : k_fast<kFastRowBytes>,
+                               dim3((c1 - c0 + kFastPerBlock - 1) / kFastPerBlock, F), dim3(kThreads), fast_lds,
                                st, d_plan, b, b.cells, c0, c1);
         } else {
             const int s0 = plan.lv[l0].seg0, s1 = l1 < plan.L ? plan.lv[l1].seg0 : plan.nsegs;

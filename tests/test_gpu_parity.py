@@ -91,6 +91,21 @@ def test_fast_band_kernel_matches_oracle(ctx, ex, oracle_mod, monkeypatch):
         c2.close()
 
 
+def test_fast_general_slab_layout_matches_oracle(ctx, ex, monkeypatch):
+    """k_fast keeps the ROI pixels and the corner strengths M in one 96-byte slab row when every
+    ROI is at most 46 wide (the 640x480 plans) and in a 72-byte slab plus a compact M slab
+    otherwise (320x240: its top level has one 57-px cell).  COEB_FAST_RB=72 forces the general
+    layout on the 640x480 plan too; both must equal the oracle, including a noise image whose
+    cells overflow the corner list (whole-window NMS)."""
+    monkeypatch.setenv("COEB_FAST_RB", "72")
+    for seed in (1000, 7):
+        run_both(ctx, ex, synth.make_frames(640, 480, 1, seed=seed)[0], tag="rb72 %d" % seed)
+    rng = np.random.default_rng(5)
+    run_both(ctx, ex, rng.integers(0, 256, (480, 640), dtype=np.uint8), tag="rb72 noise")
+    monkeypatch.delenv("COEB_FAST_RB")
+    run_both(ctx, ex, rng.integers(0, 256, (480, 640), dtype=np.uint8), tag="rb96 noise")
+
+
 @pytest.mark.parametrize("w,h", [(641, 479), (320, 240), (800, 600), (1024, 768), (720, 405)])
 def test_extract_ragged_sizes(ctx, ex, w, h):
     fr = synth.make_frames(w, h, 1, seed=w * 7 + h)
