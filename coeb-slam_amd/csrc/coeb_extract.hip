@@ -11,6 +11,7 @@
 //   k_octree     per (frame, level) DistributeOctTree emulation   (:546-769, 852-890, 1204-1207)
 //   k_describe   IC_Angle + rBRIEF + output assembly              (:80-156, 902-903, 1291-1337)
 #include <type_traits>
+#include <cmath>
 #include <hip/hip_runtime.h>
 
 #include "coeb_internal.hpp"
@@ -176,11 +177,23 @@ __device__ __forceinline__ uint32_t vresize_g(uint32_t g0, uint32_t g1, uint32_t
 // Output tile 128 x 32 per workgroup; the source rows/columns it touches (<= 32*scale+2 rows,
 // <= 128*scale+2 columns) are staged in LDS -- 16-byte loads, each thread issuing all of its
 // loads before its first LDS store -- then each thread produces 4 x 4 outputs (one 32-bit
-// store per output row).
-constexpr int PT_W = 128, PT_H = 32, PT_SW = 288, PT_SH = 72;   // LDS source tile (scale <= 2)
+// store per output row).  The LDS tile (pitch tsw, tsh rows) is sized per level from the
+// level's scale (pyr_tile_lds): 7.2 KB at scale 1.2 instead of a fixed 20.7 KB for scale 2, so
+// 12 workgroups fit a CU instead of 7.
+constexpr int PT_W = 128, PT_H = 32;
 
 // First column of VResizeLinear's scalar tail for a row of w outputs (oracle oc_resize_simd_end):
 // the SSE2 loops run 16 columns while x <= w - 16, then 4 while x < w - 4.
+// LDS source tile of a 128 x 32 output tile resized from sw x sh to dw x dh: columns
+// xofs[ox] & ~15 .. xofs[ox + 127] + 1 (<= ceil(127 * sw / dw) + 2 + 15 bytes), rows
+// yofs[oy] .. yofs[oy + 31] + 1 (<= ceil(31 * sh / dh) + 2), with a margin of one chunk / row.
+void pyr_tile_lds(int sw, int sh, int dw, int dh, int* tsw, int* tsh)
+{
+    const int span = (int)std::ceil(127.0 * sw / dw) + 2 + 15;
+    *tsw = 16 * ((span + 15) / 16 + 1);
+    *tsh = (int)std::ceil(31.0 * sh / dh) + 4;
+}
+
 int resize_simd_end(int w)
 {
     int x = w >= 16 ? (w / 16) * 16 : 0;
@@ -199,9 +212,9 @@ __device__ __forceinline__ uint32_t vresize_exact(uint32_t g0, uint32_t g1, uint
 __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
                                                         int sw, int sh, uint8_t* __restrict__ dst, int64_t dst_fs,
                                                         int dp, int dw, int dh, const int* __restrict__ tab, int xmax,
-                                                        int xs)
+                                                        int xs, int tsw, int tsh)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t s_src[PT_SH * PT_SW];
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_src[];   // tsh x tsw
     const int f = blockIdx.z;
     const int ox = blockIdx.x * PT_W, oy = blockIdx.y * PT_H;
     const int* xofs = tab;
@@ -216,7 +229,7 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
     const int tid = threadIdx.x;
     int sx0;                                      // source column of LDS tile column 0
     const bool vec = ((sp | (int)reinterpret_cast<uintptr_t>(S)) & 15) == 0;
-    if (vec && ((sx1 - (xofs[ox] & ~15)) >> 4) + 1 <= PT_SW / 16 && nrows <= PT_SH) {
+    if (vec && ((sx1 - (xofs[ox] & ~15)) >> 4) + 1 <= tsw / 16 && nrows <= tsh) {
         sx0 = xofs[ox] & ~15;
         const int nch = ((sx1 - sx0) >> 4) + 1;   // 16-byte chunks per row
         const int rstep = kThreads / nch;         // rows per pass; thread = (row, chunk)
@@ -227,18 +240,18 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
             uint4 q0 = base[min(r, nrows - 1) * pw];
             uint4 q1 = base[min(r + rstep, nrows - 1) * pw];
             uint4 q2 = base[min(r + 2 * rstep, nrows - 1) * pw];
-            if (r < nrows) *reinterpret_cast<uint4*>(s_src + r * PT_SW + 16 * k) = q0;
-            if (r + rstep < nrows) *reinterpret_cast<uint4*>(s_src + (r + rstep) * PT_SW + 16 * k) = q1;
-            if (r + 2 * rstep < nrows) *reinterpret_cast<uint4*>(s_src + (r + 2 * rstep) * PT_SW + 16 * k) = q2;
+            if (r < nrows) *reinterpret_cast<uint4*>(s_src + r * tsw + 16 * k) = q0;
+            if (r + rstep < nrows) *reinterpret_cast<uint4*>(s_src + (r + rstep) * tsw + 16 * k) = q1;
+            if (r + 2 * rstep < nrows) *reinterpret_cast<uint4*>(s_src + (r + 2 * rstep) * tsw + 16 * k) = q2;
             for (int rr = r + 3 * rstep; rr < nrows; rr += rstep)     // tall tiles (scale > 1.5)
-                *reinterpret_cast<uint4*>(s_src + rr * PT_SW + 16 * k) = base[rr * pw];
+                *reinterpret_cast<uint4*>(s_src + rr * tsw + 16 * k) = base[rr * pw];
         }
     } else if ((sp & 3) == 0) {
         sx0 = xofs[ox] & ~3;
         const int nwords = (sx1 - sx0) / 4 + 1;
         for (int i = tid; i < nwords * nrows; i += kThreads) {
             const int r = i / nwords, k = i - r * nwords;
-            *reinterpret_cast<uint32_t*>(s_src + r * PT_SW + 4 * k) =
+            *reinterpret_cast<uint32_t*>(s_src + r * tsw + 4 * k) =
                 *reinterpret_cast<const uint32_t*>(S + (int64_t)(sy0 + r) * sp + sx0 + 4 * k);
         }
     } else {
@@ -246,7 +259,7 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
         const int nb = sx1 - sx0 + 1;
         for (int i = tid; i < nb * nrows; i += kThreads) {
             const int r = i / nb, k = i - r * nb;
-            s_src[r * PT_SW + k] = S[(int64_t)(sy0 + r) * sp + sx0 + k];
+            s_src[r * tsw + k] = S[(int64_t)(sy0 + r) * sp + sx0 + k];
         }
     }
     __syncthreads();
@@ -273,8 +286,8 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
         const int r1 = (q0 + 1 >= 0 ? (q0 + 1 < sh ? q0 + 1 : sh - 1) : 0) - sy0;
         const int bb = beta[dy];
         const uint32_t b0s = (uint32_t)((int)(short)(bb & 0xFFFF)) << 8, b1s = (uint32_t)(bb >> 16) << 8;
-        const uint8_t* R0 = s_src + __mul24(r0, PT_SW);
-        const uint8_t* R1 = s_src + __mul24(r1, PT_SW);
+        const uint8_t* R0 = s_src + __mul24(r0, tsw);
+        const uint8_t* R1 = s_src + __mul24(r1, tsw);
         uint32_t word = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -2346,7 +2359,9 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     for (int l = 0; l < plan.L; l++) {
         const LevelGeom& g = plan.lv[l];
         bw.nstrips[l] = (g.w + kBlurCols - 1) / kBlurCols;
-        const int nbands = 4 * ((g.h + 63) / 64);     // 256- and 128-row bands measured slower
+        // 64 rows per wave item (4 bands): 32-, 128- and 256-row items measured slower, also with
+        // the next row block's loads issued before the current one is filtered (0.190 ms either way)
+        const int nbands = 4 * ((g.h + 63) / 64);
         bw.bh[l] = (g.h + nbands - 1) / nbands;
         bw.item_off[l] = items;
         items += bw.nstrips[l] * (nbands / 4);
@@ -2403,9 +2418,11 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         const uint8_t* src = l == 1 ? b.gray : b.pyr + gp.pyr_off;
         const int64_t src_fs = l == 1 ? (int64_t)plan.W * plan.H : plan.pyr_stride;
         prof_begin(prof, "k_pyr_level", s);
-        hipLaunchKernelGGL(k_pyr_level, dim3((g.w + PT_W - 1) / PT_W, (g.h + PT_H - 1) / PT_H, F), dim3(kThreads), 0, s, src, src_fs,
-                           gp.pitch, gp.w, gp.h, b.pyr + g.pyr_off, plan.pyr_stride, g.pitch, g.w, g.h,
-                           b.rtab + g.rtab_off, g.xmax, resize_simd_end(g.w));
+        int tsw, tsh;
+        pyr_tile_lds(gp.w, gp.h, g.w, g.h, &tsw, &tsh);
+        hipLaunchKernelGGL(k_pyr_level, dim3((g.w + PT_W - 1) / PT_W, (g.h + PT_H - 1) / PT_H, F), dim3(kThreads),
+                           tsw * tsh, s, src, src_fs, gp.pitch, gp.w, gp.h, b.pyr + g.pyr_off, plan.pyr_stride, g.pitch,
+                           g.w, g.h, b.rtab + g.rtab_off, g.xmax, resize_simd_end(g.w), tsw, tsh);
         prof_end(prof, s);
         if (split && m > 1 && l == m - 1) {
             (void)hipEventRecord(side->mid, s);
