@@ -822,7 +822,9 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
     long long t_str = 0;
     // (reading pass k+1's slab words before evaluating pass k, pre_load / pre_eval, measured
     // 0.330 vs 0.318 ms; a lane-per-group mapping that keeps all 64 lanes busy on 30-37-px
-    // windows measured 0.338: the scan is not the bound, `tools/_fast_timing.py`)
+    // windows measured 0.338: the scan is not the bound, `tools/_fast_timing.py`; storing a
+    // 4-bit survivor mask per lane and pass and compacting all passes after the loop with one
+    // wave scan measured 0.324 vs 0.288 ms)
     for (int r0 = 0; npix > 0 && r0 < wh; r0 += rpi, o += rpi * RB) {
         // every lane runs the test (rows past the window read slab bytes that are masked off)
         uint32_t lo, hi;
@@ -2454,14 +2456,16 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         blur(s, split ? bw.item_off[m] : 0, items);
     }
     fast(s, split ? m : 0, plan.L);
+    // one cross-stream wait on the critical path instead of two: each costs a ~6 us gap between
+    // the launches it separates (rocprofv3 timeline), and the late blur ends well before FAST
+    // does, so waiting for all of the side stream (join2) before the octree delays nothing
     if (soct) {
         octree(s, m, plan.L);
-        (void)hipStreamWaitEvent(s, side->join, 0);
+        (void)hipStreamWaitEvent(s, late ? side->join2 : side->join, 0);
     } else {
-        if (split) (void)hipStreamWaitEvent(s, side->join, 0);
+        if (split) (void)hipStreamWaitEvent(s, late ? side->join2 : side->join, 0);
         octree(s, 0, plan.L);
     }
-    if (late) (void)hipStreamWaitEvent(s, side->join2, 0);      // blurred levels ready
     prof_begin(prof, "k_describe", s);
     const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
     // keypoints per wave: 8 (COEB_DESC_KP = 4 / 16 / 32 for experiments; 32 was round 1's form)
