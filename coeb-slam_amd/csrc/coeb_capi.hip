@@ -299,7 +299,16 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
     P.oct_w = 0;
     for (int l = 0; l < t.nlevels; l++) P.oct_w = std::max(P.oct_w, P.lv[l].ncap);
     P.oct_w = (P.oct_w + 15) & ~15;
-    P.oct_kl = 2048;
+    // keys kept in LDS per level (more candidates: global ping-pong buffers, slower but exact):
+    // the power of two >= 4.5 x the largest level's features (FAST leaves ~3.8 candidates per
+    // level-0 feature on the config-A frames: 818 median, 934 max for 217), so that config A's
+    // octree needs 31 KB of LDS and five workgroups share a CU (0.091 -> 0.075 ms per step; 768
+    // keys pushed level 0 to the global buffers, 0.102 ms); COEB_OCT_KL overrides
+    int nmax = 0;
+    for (int l = 0; l < t.nlevels; l++) nmax = std::max(nmax, P.lv[l].nfeat);
+    P.oct_kl = 512;
+    while (P.oct_kl < 4096 && P.oct_kl < (9 * nmax + 1) / 2) P.oct_kl *= 2;
+    if (const char* e = getenv("COEB_OCT_KL")) P.oct_kl = std::max(256, std::min(8192, atoi(e)));
     P.oct_lds = P.oct_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * P.oct_kl;
     if (P.oct_lds > 150 * 1024) { err = "octree LDS budget exceeded (features per level too large)"; return false; }
     {
@@ -1867,6 +1876,15 @@ int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t byt
         if (size_out) *size_out = sizeof(t);
         if (!host) return 0;                         // size query: the read below also clears
         if ((std::string(what) == "band_timing" ? band_timing_read(t) : fast_timing_read(t))) return COEB_EDEVICE;
+        memcpy(host, t, std::min(bytes, sizeof(t)));
+        return 0;
+    }
+    if (c && what && std::string(what) == "oct_timing") {       // [4096][6] k_octree clocks (COEB_OCT_CLOCK)
+        static long long t[4096 * 6];
+        if (size_out) *size_out = sizeof(t);
+        if (!host) return 0;
+        HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
+        if (oct_timing_read(t)) return COEB_EDEVICE;
         memcpy(host, t, std::min(bytes, sizeof(t)));
         return 0;
     }

@@ -1559,9 +1559,18 @@ __device__ __forceinline__ void child_rect(const int4 p, int q, int4* out, int* 
     else *out = make_int4(mx, my, p.z, p.w);
 }
 
+#ifndef COEB_OCT_CLOCK
+#define COEB_OCT_CLOCK 0       // experiment builds: per-workgroup k_octree clocks (oct_timing)
+#endif
+// [wg][6]: level, K (candidates), start (wall clock), cycles: total, gather + initial nodes, main loop
+__device__ long long g_oct_clk[4096 * 6];
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, ExtractBufs b, int level0)
 {
+    const long long oc_t0 = COEB_OCT_CLOCK ? (long long)clock64() : 0;
+    const long long oc_w0 = COEB_OCT_CLOCK ? (long long)wall_clock64() : 0;
+    long long oc_t1 = 0, oc_t2 = 0;
     constexpr int NW = NT / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int sbuf[(NW + 2 + 3) & ~3];   // 16-byte multiple: keeps the dynamic LDS base aligned
@@ -1710,6 +1719,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
     }
     lds_barrier();
 
+    if (COEB_OCT_CLOCK) oc_t1 = (long long)clock64();
     // ---- 3. main loop (:601-745) ----
     bool finish = false;
     bool final_phase = false;
@@ -1968,6 +1978,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
         cs ^= 1;
         if (n >= N || n == prevSize) finish = true;
     }
+    if (COEB_OCT_CLOCK) oc_t2 = (long long)clock64();
 
     // ---- 4. retain the best response per node (:747-766), border, final cull ----
     NodeRef S = nref(O, cs);
@@ -2001,6 +2012,14 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
         carry += tot;
     }
     if (tid == 0) b.lvl_n[(int64_t)f * P->L + l] = min(carry, g.out_cap);
+    if (COEB_OCT_CLOCK && tid == 0) {
+        const int wg = blockIdx.x + gridDim.x * blockIdx.y;
+        if (wg < 4096) {
+            long long* r = g_oct_clk + 6 * wg;
+            r[0] = l; r[1] = K; r[2] = oc_w0;
+            r[3] = (long long)clock64() - oc_t0; r[4] = oc_t1 - oc_t0; r[5] = oc_t2 - oc_t1;
+        }
+    }
 }
 
 // ================================ k_describe ================================
@@ -2340,6 +2359,12 @@ int fast_timing_read(unsigned long long* out)
     }
     static const unsigned long long z[256 * 8] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_fast_clk), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+
+// k_octree per-workgroup clocks (COEB_OCT_CLOCK builds): 4096 x 6 long long, see g_oct_clk
+int oct_timing_read(long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oct_clk), sizeof(long long) * 4096 * 6) == hipSuccess ? 0 : -1;
 }
 
 int band_timing_read(unsigned long long* out)

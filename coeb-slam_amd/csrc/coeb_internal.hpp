@@ -122,6 +122,7 @@ constexpr int kBandCells = 16;           // cells per segment
 
 // ---- launch wrappers (coeb_extract.hip / coeb_match.hip) ----
 int band_timing_read(unsigned long long* out);
+int oct_timing_read(long long* out);   // COEB_OCT_CLOCK builds: [4096][6] per-workgroup k_octree clocks
 int fast_timing_read(unsigned long long* out);   // COEB_FAST_CLOCK builds: per-cell k_fast phase sums   // k_fast_band phase clocks (diagnostic builds)
 struct ExtractBufs {
     const uint8_t* gray;   // [F][H][W]

@@ -1,0 +1,25 @@
+"""k_octree per-workgroup clocks over one 257-frame config-A extraction (library built with
+-DCOEB_OCT_CLOCK=1, loaded through COEB_LIB_PATH; COEB_SIDE_STREAM=0).  Diagnostic only."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "coeb-slam_amd"))
+from coeb_front import synth  # noqa: E402
+from coeb_front.pipeline import BatchPipeline  # noqa: E402
+
+F = 257
+fr = synth.make_frames(640, 480, F, seed=1)
+bp = BatchPipeline(640, 480, F)
+bp.load(fr, Tcw=np.stack([synth.motion_pose()] * F))
+for _ in range(3):
+    bp.run(match=False)
+bp.synchronize()
+t = bp.ctx.debug_read("oct_timing").view(np.int64).reshape(4096, 6)[:F * 8]
+w0 = t[:, 2].min()
+for l in range(8):
+    r = t[t[:, 0] == l]
+    print("level %d: WGs %d  K median %d max %d  cycles median %d max %d  (gather+init %d, main loop %d)  start %.1f..%.1f us"
+          % (l, len(r), np.median(r[:, 1]), r[:, 1].max(), np.median(r[:, 3]), r[:, 3].max(), np.median(r[:, 4]),
+             np.median(r[:, 5]), (r[:, 2].min() - w0) / 100.0, (r[:, 2].max() - w0) / 100.0))
