@@ -396,6 +396,9 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
 // (10.5 iterations per corner): 1.97 ms per batch vs 4.08 ms for four corners per 256-thread
 // workgroup with unpipelined sums; forming the linear terms in the summing lanes (three product
 // arrays, selects) cost 5x.  itcount (COEB_SUBPIX_COUNT): {iterations, corners} for tools.
+#ifndef COEB_SUBPIX_RA
+#define COEB_SUBPIX_RA 8       // sum operands read ahead of the adds
+#endif
 #ifndef COEB_SUBPIX_CLOCK
 #define COEB_SUBPIX_CLOCK 0    // experiment builds: phase clocks of k_subpix (coeb_internal_subpix_clock)
 #endif
@@ -503,6 +506,9 @@ __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__
         SP_ADD(0, t0);
         SP_MARK(t2);
         double acc = 0;
+        // (rolled, with the weights read from the cached mask, this takes 58 VGPRs instead of 120
+        // and 7 waves per SIMD instead of 4, but measured 1.59 vs 1.57 ms: the five dependent
+        // double-add chains, issued with 5 of 64 lanes active, bound it, not the occupancy)
 #pragma unroll
         for (int q = 0; q < KPL; q++) {
             const int k = lane + 64 * q;
@@ -524,19 +530,20 @@ __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             if (lane < 5) {
                 const double* t = s_t[lane];
-                double cur[8];
+                constexpr int RA = COEB_SUBPIX_RA;         // operands read ahead of the adds
+                double cur[RA];
 #pragma unroll
-                for (int u = 0; u < 8; u++) cur[u] = t[u];
+                for (int u = 0; u < RA; u++) cur[u] = t[u];
 #pragma unroll
-                for (int k0 = 8; k0 <= 64; k0 += 8) {
-                    double nx8[8];
+                for (int k0 = RA; k0 <= 64; k0 += RA) {
+                    double nx8[RA];
                     const int k1 = k0 < 64 ? k0 : 0;
 #pragma unroll
-                    for (int u = 0; u < 8; u++) nx8[u] = t[k1 + u];
+                    for (int u = 0; u < RA; u++) nx8[u] = t[k1 + u];
 #pragma unroll
-                    for (int u = 0; u < 8; u++) acc += cur[u];
+                    for (int u = 0; u < RA; u++) acc += cur[u];
 #pragma unroll
-                    for (int u = 0; u < 8; u++) cur[u] = nx8[u];
+                    for (int u = 0; u < RA; u++) cur[u] = nx8[u];
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");     // the next 64 overwrite these
@@ -677,6 +684,15 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
     float nx = 0.f, ny = 0.f;
     const float px0 = pxy[2 * p], py0 = pxy[2 * p + 1];
     int iv[PPL], gxv[PPL], gyv[PPL];
+    // window position of this lane's pixel q (e = lane + 64 q): (row << 16) | column, computed once
+    // (a division by win per pixel and iteration was a large share of the sampling loop's VALU)
+    int wxy[PPL];
+#pragma unroll
+    for (int q = 0; q < PPL; q++) {
+        const int e = lane + 64 * q;
+        const int yy = e / win;
+        wxy[q] = e < npx ? (yy << 16) | (e - yy * win) : 0;
+    }
     for (int level = pyr.L - 1; level >= 0; level--) {
         const int lw = pyr.w[level], lh = pyr.h[level], pitch = pyr.pitch[level];
         const uint8_t* I = at_pair(pyr.P[level], level == 0 ? iz : pz);
@@ -703,7 +719,7 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
             const int e = lane + 64 * q;
             iv[q] = 0; gxv[q] = 0; gyv[q] = 0;
             if (e < npx) {
-                const int yy = e / win, xx = e - yy * win;
+                const int yy = wxy[q] >> 16, xx = wxy[q] & 0xffff;
                 const int X = ipx + xx, Y = ipy + yy;
                 const int x0 = refl1(X, lw), x1 = refl1(X + 1, lw);
                 const uint8_t* r0 = I + (size_t)refl1(Y, lh) * pitch;
@@ -743,18 +759,33 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
             iw10 = (int)rintf((1.f - a) * b * 16384.f);
             iw11 = 16384 - iw00 - iw01 - iw10;
             int ib1 = 0, ib2 = 0;                     // per lane: 8 products of < 2^26
+            if (inx >= 0 && iny >= 0 && inx + win < lw && iny + win < lh) {
+                // the window and its +1 neighbours inside the level: no reflection, rows from one
+                // wave-uniform base (the common case)
+                const uint8_t* Jw = J + (size_t)iny * pitch + inx;
 #pragma unroll
-            for (int q = 0; q < PPL; q++) {
-                const int e = lane + 64 * q;
-                if (e < npx) {
-                    const int yy = e / win, xx = e - yy * win;
-                    const int X = inx + xx, Y = iny + yy;
-                    const int x0 = refl1(X, lw), x1 = refl1(X + 1, lw);
-                    const uint8_t* r0 = J + (size_t)refl1(Y, lh) * pitch;
-                    const uint8_t* r1 = J + (size_t)refl1(Y + 1, lh) * pitch;
-                    const int diff = ((r0[x0] * iw00 + r0[x1] * iw01 + r1[x0] * iw10 + r1[x1] * iw11 + (1 << 8)) >> 9) - iv[q];
-                    ib1 += diff * gxv[q];
-                    ib2 += diff * gyv[q];
+                for (int q = 0; q < PPL; q++) {
+                    if (lane + 64 * q < npx) {
+                        const uint8_t* r0 = Jw + (wxy[q] >> 16) * pitch + (wxy[q] & 0xffff);
+                        const uint8_t* r1 = r0 + pitch;
+                        const int diff = ((r0[0] * iw00 + r0[1] * iw01 + r1[0] * iw10 + r1[1] * iw11 + (1 << 8)) >> 9) - iv[q];
+                        ib1 += diff * gxv[q];
+                        ib2 += diff * gyv[q];
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < PPL; q++) {
+                    if (lane + 64 * q < npx) {
+                        const int yy = wxy[q] >> 16, xx = wxy[q] & 0xffff;
+                        const int X = inx + xx, Y = iny + yy;
+                        const int x0 = refl1(X, lw), x1 = refl1(X + 1, lw);
+                        const uint8_t* r0 = J + (size_t)refl1(Y, lh) * pitch;
+                        const uint8_t* r1 = J + (size_t)refl1(Y + 1, lh) * pitch;
+                        const int diff = ((r0[x0] * iw00 + r0[x1] * iw01 + r1[x0] * iw10 + r1[x1] * iw11 + (1 << 8)) >> 9) - iv[q];
+                        ib1 += diff * gxv[q];
+                        ib2 += diff * gyv[q];
+                    }
                 }
             }
             const int64_t tb1 = wave_sum_i32x(ib1), tb2 = wave_sum_i32x(ib2);
