@@ -27,7 +27,7 @@ for step in "$@"; do
         benchD) run benchD 600 python bench.py --config D --no-cpu-baseline --no-extras ;;
         # per-kernel evidence with the side stream off: every kernel is then one whole-batch launch
         # per step, the same launches bench.py's HIP-event pass times (it disables the side stream)
-        prof) COEB_SIDE_STREAM=0 run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-e2e ;;
+        prof) COEB_SIDE_STREAM=0 run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-e2e --no-extras ;;
         profD) COEB_SIDE_STREAM=0 run profD 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profD -o run -- python bench.py --config D --no-cpu-baseline --no-e2e --no-extras --steps 5 --warmup 2 ;;
         diag) run diag 600 python tools/diag_parity.py ;;
         posetime) run posetime 300 python tools/pose_timing.py ;;
