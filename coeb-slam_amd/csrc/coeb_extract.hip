@@ -205,7 +205,7 @@ int resize_simd_end(int w)
 // s2.1) round exactly: (h0*b0 + h1*b1 + 2^21) >> 22 (FixedPtCast<int, uchar, 22>).
 __device__ __forceinline__ uint32_t vresize_exact(uint32_t g0, uint32_t g1, uint32_t b0s, uint32_t b1s)
 {
-    const uint32_t v = (g0 >> 4) * (b0s >> 8) + (g1 >> 4) * (b1s >> 8) + (1u << 21);   // < 2^31
+    const uint32_t v = __umul24(g0 >> 4, b0s >> 8) + __umul24(g1 >> 4, b1s >> 8) + (1u << 21);   // < 2^31
     return min(v >> 22, 255u);
 }
 
