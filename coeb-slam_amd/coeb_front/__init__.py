@@ -54,6 +54,8 @@ ABI_SYMBOLS = [
     "coeb_copyq_create", "coeb_copyq_destroy", "coeb_copyq_h2d", "coeb_copyq_d2h", "coeb_copyq_after_ctx",
     "coeb_ctx_after_copyq", "coeb_copyq_synchronize", "coeb_frame_batch_device", "coeb_batch_frame_results",
     "coeb_track_local_map_batch_device", "coeb_batch_track_results", "coeb_rgbd_preprocess_batch_device",
+    "coeb_marker_create", "coeb_marker_destroy", "coeb_marker_record_ctx", "coeb_marker_record_copyq",
+    "coeb_ctx_wait_marker", "coeb_copyq_wait_marker", "coeb_marker_synchronize",
 ]
 
 
@@ -201,6 +203,13 @@ def lib():
         L.coeb_copyq_after_ctx.argtypes = [C.c_void_p, C.c_void_p]
         L.coeb_ctx_after_copyq.argtypes = [C.c_void_p, C.c_void_p]
         L.coeb_copyq_synchronize.argtypes = [C.c_void_p]
+        L.coeb_marker_create.restype = C.c_void_p
+        L.coeb_marker_create.argtypes = [C.c_void_p]
+        for nm in ("coeb_marker_destroy", "coeb_marker_synchronize"):
+            getattr(L, nm).argtypes = [C.c_void_p]
+        for nm in ("coeb_marker_record_ctx", "coeb_marker_record_copyq", "coeb_ctx_wait_marker",
+                   "coeb_copyq_wait_marker"):
+            getattr(L, nm).argtypes = [C.c_void_p, C.c_void_p]
         L.coeb_debug_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_size_t,
                                       C.POINTER(C.c_size_t)]
         _lib = L

@@ -9,7 +9,7 @@ import numpy as np
 
 import ctypes as C
 
-from . import Context, HostBuffer, KEYPOINT_DTYPE, lib, make_camera, synth
+from . import Context, DeviceBuffer, HostBuffer, KEYPOINT_DTYPE, lib, make_camera, synth
 
 
 class BatchPipeline:
@@ -203,28 +203,37 @@ class BatchPipeline:
 
 class HostStream:
     """Host buffers in, host buffers out, with copy / kernel overlap (the PCIe-inclusive rate,
-    DESIGN.md s5).  Two batch slots, each a BatchPipeline with its own context (streams and device
-    buffers) on the same device, and one copy queue (coeb_copyq; shared_queue=False gives each
-    slot a download queue of its own: measured no faster).  Batch i (slot k = i % 2):
-      copy queue: waits for slot k's earlier kernels (its gray buffer is free), uploads the frames
-                  from page-locked host memory;
-      slot k:     waits for the upload (and, with per-slot download queues, for slot k's previous
-                  download: its result buffers are free), extracts + matches;
-      copy queue: after batch i + 1's upload, waits for those kernels and downloads keypoints /
-                  descriptors / counts / matches into slot k's page-locked output buffers.
-    Uploads run back to back (concurrent uploads only split the PCIe bandwidth) while the
-    previous batch computes; the 17 MB of results per 257 frames follow each upload.  Every
-    ordering is a device-side event wait, so
-    submit() never blocks the host: results of batch i are readable after wait(i) and stay so
-    until batch i + 2's kernels finish (its download reuses slot i % 2's host buffers), so read
-    them before submitting batch i + 2.  The process needs more than 4 hardware queues
-    (GPU_MAX_HW_QUEUES = 16 in bench.py): with HIP's default of 4 the streams of two contexts and the
-    copy queue share queues, and an upload queued behind the other slot's kernels loses the
-    overlap; queues of contexts closed earlier in the process stay taken, measured."""
+    DESIGN.md s6).  Two batch slots, each a BatchPipeline with its own context (streams and device
+    buffers) on the same device.
 
-    def __init__(self, width, height, nframes, nfeatures=1000, device=0, depth=None, Tcw=None, shared_queue=True):
+    mode="slot" (default): batch i (slot k = i % 2) is, in order on slot k's own stream, the
+    upload of its gray frames from page-locked host memory, its kernels, and the download of
+    keypoints / descriptors / counts / matches into slot k's page-locked output buffers.  Batch
+    i's upload also waits for batch i - 1's upload (one event through an idle "gate" queue): left
+    free, the two slots fall into phase (both upload at half rate, both compute at once) and a
+    batch took 2.7 ms.  Staggered, batch i + 1 uploads while batch i computes and downloads.
+    Uploads are the bound (79 MB per 257 frames at ~57 GB/s = 1.38 ms vs 1.07 ms of kernels +
+    0.31 ms of download), and a slot's next upload starts as its own download ends: one upload
+    per batch in steady state.
+
+    mode="copyq": one copy queue (coeb_copyq) carries every upload and download, ordered against
+    the slots by device-side events (shared_queue=False gives each slot a download queue of its
+    own).  Measured slower: the upload of batch i + 1 waited for batch i's kernels
+    (profiles/r02/v3/hoststream_copyq_timeline.txt).
+
+    Either way submit() never blocks the host.  Results of batch i are readable after wait(i) and
+    stay so until batch i + 2 is submitted (its download reuses slot i % 2's host buffers).  The
+    process needs more than 4 hardware queues (GPU_MAX_HW_QUEUES = 16 in bench.py): with HIP's
+    default of 4 the streams of two contexts share queues and the overlap disappears."""
+
+    def __init__(self, width, height, nframes, nfeatures=1000, device=0, depth=None, Tcw=None, shared_queue=True,
+                 mode="slot"):
+        if mode not in ("ring", "slot", "copyq"):
+            raise ValueError("HostStream mode must be 'ring', 'slot' or 'copyq'")
+        self.mode = mode
         self.W, self.H, self.F = width, height, nframes
-        self.slots = [BatchPipeline(width, height, nframes, nfeatures=nfeatures, device=device) for _ in range(2)]
+        nslots = 1 if mode == "ring" else 2
+        self.slots = [BatchPipeline(width, height, nframes, nfeatures=nfeatures, device=device) for _ in range(nslots)]
         zero = np.zeros((nframes, height, width), np.uint8)
         for sl in self.slots:
             sl.load(zero, depth=depth, Tcw=Tcw)
@@ -235,29 +244,89 @@ class HostStream:
         F = nframes
         self.sizes = dict(kps=28 * kcap * F, desc=32 * kcap * F, counts=4 * F, match=4 * kcap * F, nmatch=4 * F)
         self.out = [{k: HostBuffer(n) for k, n in self.sizes.items()} for _ in range(2)]
+        self.inflight = []
+        self.pending_dl = None              # batch whose download is not enqueued yet (copyq mode)
+        self.up, self.down = None, []
+        self.markers, self.ring = [], []
         L = lib()
+        if mode == "ring":
+            sl = self.slots[0]
+            nb = nframes * height * width
+            self.ring = [sl.gray] + [DeviceBuffer(sl.ctx, nb) for _ in range(self.NRING - 1)]
+            self.up = L.coeb_copyq_create(sl.ctx.h)
+            self.markers = [[L.coeb_marker_create(sl.ctx.h) for _ in range(self.NMARK)] for _ in range(3)]
+            if not self.up or not all(all(m) for m in self.markers):
+                raise RuntimeError("HostStream: copy queue / marker creation failed: %s" %
+                                   L.coeb_last_error(None).decode())
+            self.updone, self.kdone, self.dldone = self.markers
+            return
+        if mode == "slot":
+            # gate: an otherwise idle copy queue that only carries event waits, so slot k's
+            # upload can wait for the other slot's upload (and nothing after it) to finish
+            self.gate = L.coeb_copyq_create(self.slots[0].ctx.h)
+            if not self.gate:
+                raise RuntimeError("coeb_copyq_create failed: %s" % L.coeb_last_error(None).decode())
+            self.down = [self.gate]
+            return
         self.up = L.coeb_copyq_create(self.slots[0].ctx.h)
         self.down = [self.up, self.up] if shared_queue else [L.coeb_copyq_create(sl.ctx.h) for sl in self.slots]
         if not self.up or not all(self.down):
             raise RuntimeError("coeb_copyq_create failed: %s" % L.coeb_last_error(None).decode())
-        self.inflight = []
-        self.pending_dl = None              # batch whose download is not enqueued yet
 
     def _chk(self, rc):
         if rc != 0:
             raise RuntimeError("coeb rc=%d: %s" % (rc, lib().coeb_last_error(None).decode()))
 
+    def _downloads(self, k, slot=None):
+        """(host, device, bytes) of the result copies into output set k from slot `slot` (k)."""
+        c = self.slots[k if slot is None else slot].ctx
+        kp_ptr, desc_ptr, cnt_ptr, _ = c.batch_results()
+        m_ptr, n_ptr = c.batch_match_results()
+        o = self.out[k]
+        return [(o[name].ptr, dptr, self.sizes[name]) for name, dptr in
+                (("counts", cnt_ptr), ("kps", kp_ptr), ("desc", desc_ptr), ("match", m_ptr), ("nmatch", n_ptr))]
+
+    NRING = 3          # device input buffers of the ring mode
+    NMARK = 8          # markers per kind (a marker is re-recorded NMARK batches later)
+
     def submit(self, i, host_frames):
-        """Enqueue batch i (host_frames: a HostBuffer of F*H*W gray bytes) on slot i % 2 and the
-        download of batch i - 1; returns at once (the device orders it after batch i - 2 on the
-        same slot).  Batch i's upload is queued before batch i - 1's download, so on a shared
-        copy queue the upload does not wait behind batch i - 1's kernels."""
-        k = i % 2
+        """Enqueue batch i (host_frames: a HostBuffer of F*H*W gray bytes); returns at once (the
+        device orders it after the batches before it)."""
         L = lib()
+        nb = self.F * self.H * self.W
+        if self.mode == "ring":
+            sl, c = self.slots[0], self.slots[0].ctx
+            buf, r = self.ring[i % self.NRING], i % self.NMARK
+            if i >= self.NRING:        # the kernels that read this input buffer last are done
+                self._chk(L.coeb_copyq_wait_marker(self.up, self.kdone[(i - self.NRING) % self.NMARK]))
+            self._chk(L.coeb_copyq_h2d(self.up, C.c_void_p(buf.ptr), C.c_void_p(host_frames.ptr), nb))
+            self._chk(L.coeb_marker_record_copyq(self.updone[r], self.up))
+            self._chk(L.coeb_ctx_wait_marker(c.h, self.updone[r]))
+            sl.gray = buf
+            sl.run()
+            self._chk(L.coeb_marker_record_ctx(self.kdone[r], c.h))
+            for hptr, dptr, n in self._downloads(i % 2, 0):
+                self._chk(L.coeb_memcpy_d2h_async(c.h, C.c_void_p(hptr), C.c_void_p(dptr), n))
+            self._chk(L.coeb_marker_record_ctx(self.dldone[r], c.h))
+            self.inflight.append(i)
+            return
+        k = i % 2
         sl, c = self.slots[k], self.slots[k].ctx
+        if self.mode == "slot":
+            # uploads one after another (each at the full link rate) instead of two at once: the
+            # slots then stay half a period apart and batch i + 1 uploads while batch i computes
+            self._chk(L.coeb_ctx_after_copyq(c.h, self.gate))
+            self._chk(L.coeb_memcpy_h2d_async(c.h, C.c_void_p(sl.gray.ptr), C.c_void_p(host_frames.ptr), nb))
+            self._chk(L.coeb_copyq_after_ctx(self.gate, c.h))
+            sl.run()
+            for hptr, dptr, n in self._downloads(k):
+                self._chk(L.coeb_memcpy_d2h_async(c.h, C.c_void_p(hptr), C.c_void_p(dptr), n))
+            self.inflight.append(i)
+            return
+        # copyq: batch i's upload is queued before batch i - 1's download, so on a shared copy
+        # queue the upload does not wait behind batch i - 1's kernels
         self._chk(L.coeb_copyq_after_ctx(self.up, c.h))
-        self._chk(L.coeb_copyq_h2d(self.up, C.c_void_p(sl.gray.ptr), C.c_void_p(host_frames.ptr),
-                                   self.F * self.H * self.W))
+        self._chk(L.coeb_copyq_h2d(self.up, C.c_void_p(sl.gray.ptr), C.c_void_p(host_frames.ptr), nb))
         self._chk(L.coeb_ctx_after_copyq(c.h, self.up))
         if self.down[k] != self.up:
             self._chk(L.coeb_ctx_after_copyq(c.h, self.down[k]))
@@ -273,22 +342,22 @@ class HostStream:
         self.pending_dl = None
         k = i % 2
         L = lib()
-        c = self.slots[k].ctx
-        self._chk(L.coeb_copyq_after_ctx(self.down[k], c.h))
-        kp_ptr, desc_ptr, cnt_ptr, _ = c.batch_results()
-        m_ptr, n_ptr = c.batch_match_results()
-        o = self.out[k]
-        for name, dptr in (("counts", cnt_ptr), ("kps", kp_ptr), ("desc", desc_ptr), ("match", m_ptr),
-                           ("nmatch", n_ptr)):
-            self._chk(L.coeb_copyq_d2h(self.down[k], C.c_void_p(o[name].ptr), C.c_void_p(dptr), self.sizes[name]))
+        self._chk(L.coeb_copyq_after_ctx(self.down[k], self.slots[k].ctx.h))
+        for hptr, dptr, n in self._downloads(k):
+            self._chk(L.coeb_copyq_d2h(self.down[k], C.c_void_p(hptr), C.c_void_p(dptr), n))
 
     def wait(self, i):
         """Block until batch i's results are in its slot's host buffers (with later batches of
-        the same slot submitted, this also waits for their downloads)."""
-        if self.pending_dl is not None and self.pending_dl <= i:
+        the same slot submitted, this also waits for them)."""
+        if self.mode == "copyq" and self.pending_dl is not None and self.pending_dl <= i:
             self._flush_download()
         if i in self.inflight:
-            self._chk(lib().coeb_copyq_synchronize(self.down[i % 2]))
+            if self.mode == "ring":
+                self._chk(lib().coeb_marker_synchronize(self.dldone[i % self.NMARK]))
+            elif self.mode == "slot":
+                self.slots[i % 2].synchronize()
+            else:
+                self._chk(lib().coeb_copyq_synchronize(self.down[i % 2]))
             self.inflight = [j for j in self.inflight if j % 2 != i % 2 or j > i]
         return self.out[i % 2]
 
@@ -311,6 +380,17 @@ class HostStream:
         self.up, self.down = None, []
         for sl in self.slots:
             sl.synchronize()
+        for kind in self.markers:
+            for m in kind:
+                if m:
+                    L.coeb_marker_destroy(m)
+        self.markers = []
+        for b in self.ring[1:]:
+            b.free()
+        if self.ring:
+            self.slots[0].gray = self.ring[0]
+        self.ring = []
+        for sl in self.slots:
             sl.close()
         for o in self.out:
             for b in o.values():

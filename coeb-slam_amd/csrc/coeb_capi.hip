@@ -1847,6 +1847,78 @@ int coeb_copyq_synchronize(coeb_copyq* q)
     return COEB_OK;
 }
 
+// ---- markers (coeb_front.h): one HIP event, recorded on a context's or queue's stream ----
+struct coeb_marker {
+    int device = 0;
+    hipEvent_t ev = nullptr;
+};
+
+coeb_marker* coeb_marker_create(coeb_ctx* c)
+{
+    if (!c) return nullptr;
+    (void)hipSetDevice(c->device);
+    coeb_marker* m = new coeb_marker;
+    m->device = c->device;
+    if (hipEventCreateWithFlags(&m->ev, hipEventDisableTiming) != hipSuccess) {
+        set_err(c, COEB_EDEVICE, "coeb_marker_create: event creation failed");
+        delete m;
+        return nullptr;
+    }
+    return m;
+}
+
+int coeb_marker_destroy(coeb_marker* m)
+{
+    if (!m) return COEB_OK;
+    (void)hipSetDevice(m->device);
+    (void)hipEventSynchronize(m->ev);
+    (void)hipEventDestroy(m->ev);
+    delete m;
+    return COEB_OK;
+}
+
+int coeb_marker_record_ctx(coeb_marker* m, coeb_ctx* c)
+{
+    if (!m || !c || m->device != c->device) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    hipStream_t s = main_stream(c);          // joins pending side-stream work first
+    join_pose(c);
+    HIP_TRY(c, hipEventRecord(m->ev, s));
+    return COEB_OK;
+}
+
+int coeb_marker_record_copyq(coeb_marker* m, coeb_copyq* q)
+{
+    if (!m || !q || m->device != q->device) return COEB_EINVAL;
+    (void)hipSetDevice(q->device);
+    if (hipEventRecord(m->ev, q->s) != hipSuccess) return set_err(nullptr, COEB_EDEVICE, "coeb_marker_record_copyq failed");
+    return COEB_OK;
+}
+
+int coeb_ctx_wait_marker(coeb_ctx* c, coeb_marker* m)
+{
+    if (!m || !c || m->device != c->device) return COEB_EINVAL;
+    (void)hipSetDevice(c->device);
+    HIP_TRY(c, hipStreamWaitEvent(main_stream(c), m->ev, 0));
+    return COEB_OK;
+}
+
+int coeb_copyq_wait_marker(coeb_copyq* q, coeb_marker* m)
+{
+    if (!m || !q || m->device != q->device) return COEB_EINVAL;
+    (void)hipSetDevice(q->device);
+    if (hipStreamWaitEvent(q->s, m->ev, 0) != hipSuccess) return set_err(nullptr, COEB_EDEVICE, "coeb_copyq_wait_marker failed");
+    return COEB_OK;
+}
+
+int coeb_marker_synchronize(coeb_marker* m)
+{
+    if (!m) return COEB_EINVAL;
+    (void)hipSetDevice(m->device);
+    if (hipEventSynchronize(m->ev) != hipSuccess) return set_err(nullptr, COEB_EDEVICE, "coeb_marker_synchronize failed");
+    return COEB_OK;
+}
+
 int coeb_internal_stream(coeb_ctx* c, hipStream_t* s, int* device)
 {
     if (!c) return COEB_EINVAL;

@@ -525,6 +525,10 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
 constexpr int kFastRowBytes = 72;          // >= 1 + 64 + 7 (slab byte = ROI column + 1): any ROI up to 64 wide
 constexpr int kFastRowBytesM = 96;         // ROIs up to 46 wide: pixels in bytes 0..47, M in bytes 48..95
 // (24 dwords: the four rows a half-wave's pre-test reads land on disjoint banks, (a/4) mod 32)
+#ifndef COEB_FAST_UNALIGNED
+#define COEB_FAST_UNALIGNED 1  // 0: realign the staged ROI rows in registers (DPP + selects + alignbyte)
+#endif
+constexpr int kFastGuard = COEB_FAST_UNALIGNED ? 16 : 0;   // bytes before each wave's slab
 constexpr int kFastSurv = 384;             // survivor list (flushed when one more pass could overflow it)
 constexpr int kFastCorners = 384;          // corner list (more corners: NMS walks the whole window)
 
@@ -715,6 +719,20 @@ __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs
 {
     const int lane = lane_id();
     if (G.vec) {
+#if COEB_FAST_UNALIGNED
+        // the 64-byte window's chunks stored as loaded, each at its own slab offset - sh
+        // (unaligned ds_write_b128: gfx950 LDS takes any byte address), so slab byte j = ROI
+        // column j - 1 with no realignment in registers.  Row r's first chunk spills sh bytes
+        // into the tail of row r - 1 (its M columns 81..95, zeroed by the M clear that follows)
+        // and row 0's into the 16-byte guard before the slab; the last chunk's bytes past
+        // column 47 land in the row's own M columns, also cleared after.
+        const int sh = (G.x0 - 1) & 15;
+        const int r = lane >> 2, c = lane & 3;
+        uint8_t* d = roi + r * RB + 16 * c - sh;
+        if (r < G.rh) __builtin_memcpy(d, &R.v0, 16);
+        if (r + 16 < G.rh) __builtin_memcpy(d + 16 * RB, &R.v1, 16);
+        if (r + 32 < G.rh) __builtin_memcpy(d + 32 * RB, &R.v2, 16);
+#else
         const int sh = (G.x0 - 1) & 15;
         const uint32_t m2 = (sh & 8) ? 0xFFFFFFFFu : 0u, m1 = (sh & 4) ? 0xFFFFFFFFu : 0u;
         const uint32_t bsh = (uint32_t)(sh & 3);
@@ -723,6 +741,7 @@ __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs
         fast_stage_chunk(R.v0, m2, m1, bsh, d, c < 3 && r < G.rh);
         fast_stage_chunk(R.v1, m2, m1, bsh, d + 16 * RB, c < 3 && r + 16 < G.rh);
         fast_stage_chunk(R.v2, m2, m1, bsh, d + 32 * RB, c < 3 && r + 32 < G.rh);
+#endif
     } else if (G.words) {
         const int gx = G.x0 - 1;
         const int kw = min(lane & 15, G.nwords);
@@ -775,7 +794,7 @@ __host__ __device__ inline int fast_ms_slab(const Plan& P, int rb)
 }
 __host__ __device__ inline int fast_wave_lds(const Plan& P, int rb)
 {
-    return fast_slab(P, rb) + fast_ms_slab(P, rb) + 2 * (kFastSurv + 64 + kFastCorners);
+    return kFastGuard + fast_slab(P, rb) + fast_ms_slab(P, rb) + 2 * (kFastSurv + 64 + kFastCorners);
 }
 
 #ifndef COEB_BAND_CLOCK
@@ -951,7 +970,7 @@ __global__ __launch_bounds__(kThreads, 6) void k_fast(const Plan* __restrict__ P
     // (twice the staging stores): the byte slab stays.
     const int wv = threadIdx.x >> 6, lane = lane_id();
     const int slab = fast_slab(*P, RB), ms_slab = fast_ms_slab(*P, RB);   // per-wave LDS: roi, M, lists
-    uint8_t* wbase = smem + (size_t)wv * fast_wave_lds(*P, RB);
+    uint8_t* wbase = smem + (size_t)wv * fast_wave_lds(*P, RB) + kFastGuard;
     uint8_t* roi = wbase;
     uint8_t* Ms = RB == kFastRowBytesM ? wbase : wbase + slab;
     uint16_t* surv = reinterpret_cast<uint16_t*>(wbase + slab + ms_slab);

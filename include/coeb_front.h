@@ -417,6 +417,17 @@ int coeb_copyq_d2h(coeb_copyq* q, void* dst, const void* src, size_t bytes);
 int coeb_copyq_after_ctx(coeb_copyq* q, coeb_ctx* ctx);
 int coeb_ctx_after_copyq(coeb_ctx* ctx, coeb_copyq* q);
 int coeb_copyq_synchronize(coeb_copyq* q);
+/* Markers: a point recorded on a context or copy queue now and waited for later (by another
+ * context or queue, or by the host), for pipelines whose waits refer to work enqueued several
+ * steps earlier (e.g. "the kernels of batch i - 3 are done with this input buffer"). */
+typedef struct coeb_marker coeb_marker;
+coeb_marker* coeb_marker_create(coeb_ctx* ctx);
+int coeb_marker_destroy(coeb_marker* m);
+int coeb_marker_record_ctx(coeb_marker* m, coeb_ctx* ctx);       /* after all work enqueued on ctx */
+int coeb_marker_record_copyq(coeb_marker* m, coeb_copyq* q);     /* after all work enqueued on q */
+int coeb_ctx_wait_marker(coeb_ctx* ctx, coeb_marker* m);         /* later work on ctx waits for m */
+int coeb_copyq_wait_marker(coeb_copyq* q, coeb_marker* m);       /* later work on q waits for m */
+int coeb_marker_synchronize(coeb_marker* m);                     /* host waits for m */
 
 /* ---- measurement ---- */
 /* Per-kernel device time accumulated with HIP events on the context stream while profiling

@@ -565,10 +565,12 @@ def test_sharded_batch_equals_unsharded():
     assert covered == list(range(1, G + 1))
 
 
-def test_host_stream_overlapped_equals_device_batch():
+@pytest.mark.parametrize("mode,shared", [("ring", True), ("slot", True), ("copyq", True), ("copyq", False)])
+def test_host_stream_overlapped_equals_device_batch(mode, shared):
     """The PCIe-inclusive pipeline (HostStream: page-locked host frames in, host results out, two
     slots whose copies overlap each other's kernels) returns per-frame keypoints, descriptors and
-    matches bit-identical to the device-resident batch, for several batches in flight."""
+    matches bit-identical to the device-resident batch, for several batches in flight, with the
+    copies on each slot's own stream or on copy queues."""
     from coeb_front import HostBuffer
     from coeb_front.pipeline import BatchPipeline, HostStream
     F = 9
@@ -584,7 +586,7 @@ def test_host_stream_overlapped_equals_device_batch():
             ref.append(bp.results())
     finally:
         bp.close()
-    hs = HostStream(640, 480, F, Tcw=Tcw)
+    hs = HostStream(640, 480, F, Tcw=Tcw, mode=mode, shared_queue=shared)
     bufs = [HostBuffer(F * 480 * 640) for _ in seqs]
     try:
         for b, fr in zip(bufs, seqs):
