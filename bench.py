@@ -804,9 +804,9 @@ def _thread_rank_type():
 
 def e2e_timing(frames, Tcw, ranks, G, steps, cfg, device):
     """PCIe-inclusive rate (reported, never `value`): gray frames start in page-locked host
-    memory, keypoints / descriptors / counts / matches end in page-locked host memory.  Two batch
-    slots (HostStream, two contexts) so one batch's uploads and downloads overlap the other's
-    kernels."""
+    memory, keypoints / descriptors / counts / matches end in page-locked host memory.
+    HostStream's ring mode: uploads of later batches overlap the current batch's kernels and
+    downloads."""
     from coeb_front import HostBuffer
     from coeb_front.pipeline import HostStream
     F, H, W = frames.shape
@@ -833,8 +833,9 @@ def e2e_timing(frames, Tcw, ranks, G, steps, cfg, device):
     return dict(value=round(G * steps / te, 2), unit="frames/s", ms_per_step=round(te / steps * 1e3, 4), steps=steps,
                 results_nonempty=bool(ok),
                 note="gray frames uploaded from page-locked host memory and keypoints/descriptors/counts/matches "
-                     "downloaded to page-locked host memory every step; two batch slots (contexts) and one copy "
-                     "queue: batch i+1's upload runs while batch i computes, batch i's results follow it")
+                     "downloaded to page-locked host memory every step (HostStream ring mode: an upload queue "
+                     "filling three device input buffers back to back beside the kernels; results downloaded "
+                     "on the compute stream)")
 
 
 def single_frame_timing(w, h, reps=50):

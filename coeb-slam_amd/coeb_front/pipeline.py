@@ -203,10 +203,21 @@ class BatchPipeline:
 
 class HostStream:
     """Host buffers in, host buffers out, with copy / kernel overlap (the PCIe-inclusive rate,
-    DESIGN.md s6).  Two batch slots, each a BatchPipeline with its own context (streams and device
-    buffers) on the same device.
+    DESIGN.md s6).
 
-    mode="slot" (default): batch i (slot k = i % 2) is, in order on slot k's own stream, the
+    mode="ring" (default): one context computes the batches in order; an upload queue
+    (coeb_copyq) fills a ring of three device input buffers.  Batch i: the queue waits for the
+    marker "kernels of batch i - 3 done" (its buffer is free), uploads, records "upload i done";
+    the context waits for that marker, runs the kernels on buffer i % 3, records "kernels i
+    done", downloads keypoints / descriptors / counts / matches into output set i % 2 on its own
+    stream and records "results i in host memory" (what wait(i) waits for).  The upload queue
+    never waits for the batch just before it, so uploads run back to back at the link rate
+    beside the kernels and downloads (79 MB per 257 frames at ~57 GB/s = 1.38 ms; kernels 1.07 ms
+    + download 0.31 ms on the context stream): one upload per batch in steady state.
+
+    The two-context forms, kept for comparison (profiles/r02/v3/hoststream_modes.txt):
+
+    mode="slot": batch i (slot k = i % 2) is, in order on slot k's own stream, the
     upload of its gray frames from page-locked host memory, its kernels, and the download of
     keypoints / descriptors / counts / matches into slot k's page-locked output buffers.  Batch
     i's upload also waits for batch i - 1's upload (one event through an idle "gate" queue): left
@@ -218,8 +229,8 @@ class HostStream:
 
     mode="copyq": one copy queue (coeb_copyq) carries every upload and download, ordered against
     the slots by device-side events (shared_queue=False gives each slot a download queue of its
-    own).  Measured slower: the upload of batch i + 1 waited for batch i's kernels
-    (profiles/r02/v3/hoststream_copyq_timeline.txt).
+    own): the upload of batch i + 1 queued behind batch i - 1's download, which waits for its
+    kernels (profiles/r02/v3/hoststream_copyq_timeline.txt).
 
     Either way submit() never blocks the host.  Results of batch i are readable after wait(i) and
     stay so until batch i + 2 is submitted (its download reuses slot i % 2's host buffers).  The
@@ -227,7 +238,7 @@ class HostStream:
     default of 4 the streams of two contexts share queues and the overlap disappears."""
 
     def __init__(self, width, height, nframes, nfeatures=1000, device=0, depth=None, Tcw=None, shared_queue=True,
-                 mode="slot"):
+                 mode="ring"):
         if mode not in ("ring", "slot", "copyq"):
             raise ValueError("HostStream mode must be 'ring', 'slot' or 'copyq'")
         self.mode = mode

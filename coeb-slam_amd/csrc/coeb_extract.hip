@@ -531,6 +531,7 @@ constexpr int kFastRowBytesM = 96;         // ROIs up to 46 wide: pixels in byte
 constexpr int kFastGuard = COEB_FAST_UNALIGNED ? 16 : 0;   // bytes before each wave's slab
 constexpr int kFastSurv = 384;             // survivor list (flushed when one more pass could overflow it)
 constexpr int kFastCorners = 384;          // corner list (more corners: NMS walks the whole window)
+constexpr int kFastLists = kFastSurv + 64;   // u16 entries before the corner list
 
 __device__ __forceinline__ void wave_sync_lds()
 {
@@ -794,7 +795,7 @@ __host__ __device__ inline int fast_ms_slab(const Plan& P, int rb)
 }
 __host__ __device__ inline int fast_wave_lds(const Plan& P, int rb)
 {
-    return kFastGuard + fast_slab(P, rb) + fast_ms_slab(P, rb) + 2 * (kFastSurv + 64 + kFastCorners);
+    return kFastGuard + fast_slab(P, rb) + fast_ms_slab(P, rb) + 2 * (kFastLists + kFastCorners);
 }
 
 #ifndef COEB_BAND_CLOCK
@@ -974,7 +975,7 @@ __global__ __launch_bounds__(kThreads, 6) void k_fast(const Plan* __restrict__ P
     uint8_t* roi = wbase;
     uint8_t* Ms = RB == kFastRowBytesM ? wbase : wbase + slab;
     uint16_t* surv = reinterpret_cast<uint16_t*>(wbase + slab + ms_slab);
-    uint16_t* corn = surv + kFastSurv + 64;     // surv: kFastSurv entries + one scratch slot per lane
+    uint16_t* corn = surv + kFastLists;         // surv: kFastSurv entries + one scratch slot per lane
     const int2 bxy = block_xy<false>();
     const int f = bxy.y;
     const int cidx = cell0 + bxy.x * kWaves + wv;
