@@ -31,9 +31,13 @@ import numpy as np  # noqa: E402
 METRIC = "frames/sec ORB extract+match @640x480/1000 kp; 1/2/4/8 GPU + %HBM roofline"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
 CONFIGS = {
-    "A": dict(w=640, h=480, nfeatures=1000, workload="640x480, 8-level pyramid, 1000 kp, extract + Hamming match to prev frame (BASELINE configs[1])"),
+    # batch = matched frames per step per GPU.  A and C: 1024 (measured 208 / 250 / 257 / 269 / 265 k
+    # frames/s at 128 / 256 / 512 / 1024 / 2048, profiles/r02/v3/batch_sweep.txt: 1024 frames give every
+    # launch >= 4 workgroups per CU, including the small pyramid levels and the matcher); D: 256.
+    "A": dict(w=640, h=480, nfeatures=1000, batch=1024,
+              workload="640x480, 8-level pyramid, 1000 kp, extract + Hamming match to prev frame (BASELINE configs[1])"),
     "B": dict(w=1280, h=960, nfeatures=2000, workload="1280x960, 8-level pyramid, 2000 kp, extract + match (BASELINE configs[3] shape)"),
-    "C": dict(w=640, h=480, nfeatures=1000, dyn=True,
+    "C": dict(w=640, h=480, nfeatures=1000, dyn=True, batch=1024,
               workload="640x480, 1000 kp, YOLO-bbox dynamic mask (2 boxes, 60 T_M points, blur_flag [0,1]) + "
                        "depth association (ComputeStereoFromRGBD) + match to prev frame (BASELINE configs[2])"),
     "D": dict(w=640, h=480, nfeatures=1000, chain=True,
@@ -579,7 +583,8 @@ def parse_args(argv=None):
                          "per GPU); started directly, bench drives devices 0..N-1 from N host threads")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="matched frames per step per GPU (weak scaling)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="matched frames per step per GPU (weak scaling; default: the config's batch)")
     ap.add_argument("--global-frames", type=int, default=None,
                     help="fixed number of matched frames per step, sharded over the GPUs with one halo frame "
                          "each (strong scaling; config B defaults to BASELINE configs[3]'s 512)")
@@ -600,6 +605,8 @@ def main():
     args = parse_args()
     if args.global_frames is None and args.config == "B":
         args.global_frames = 512
+    if args.batch is None:
+        args.batch = CONFIGS[args.config].get("batch", 256)
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     if env_world > 1 or "LOCAL_RANK" in os.environ:
         # one process per GPU under torch.distributed.run

@@ -39,11 +39,11 @@ for step in "$@"; do
             run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- $B
             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- $B
             python tools/pmc_summary.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv \
-                --json gpurun_out/pmc_traffic.json --frames 257 --command "$B" > gpurun_out/pmc_traffic.log 2>&1
+                --json gpurun_out/pmc_traffic.json --frames 1025 --command "$B" > gpurun_out/pmc_traffic.log 2>&1
             run pmc_sq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace --output-format csv -d gpurun_out/pmc_sq -o run -- $B
             run pmc_sq2 600 rocprofv3 --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_sq2 -o run -- $B
             python tools/pmc_summary.py gpurun_out/pmc_sq/run_counter_collection.csv gpurun_out/pmc_sq2/run_counter_collection.csv \
-                --valu-json gpurun_out/pmc_valu.json --frames 257 --command "$B" > gpurun_out/pmc_valu.log 2>&1
+                --valu-json gpurun_out/pmc_valu.json --frames 1025 --command "$B" > gpurun_out/pmc_valu.log 2>&1
             ;;
         pmcB)
             export COEB_SIDE_STREAM=0
