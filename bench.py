@@ -49,6 +49,9 @@ CONFIGS = {
               data="synthetic tracking sequence (TUM-like rectangles + noise, (+2,+1) px/frame camera motion, a "
                    "bouncing 120x160 textured object with its YOLO box; RGB = gray x 3, 16U depth 10000 = 2 m)"),
 }
+# COEB_BENCH_ONE_DEVICE=1 rehearses --gpus N (threads, shards, barriers, max over ranks) with every
+# rank on device 0 of a one-GPU box; its lines carry "rehearsal_one_device" and measure nothing.
+ONE_DEVICE = os.environ.get("COEB_BENCH_ONE_DEVICE") == "1"
 DEPTH_MAP_FACTOR = 1.0 / 5000.0     # mDepthMapFactor = 1 / DepthMapFactor (TUM yaml: 5000)
 
 
@@ -622,7 +625,7 @@ def main():
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
     if not args.dry_run:
-        check_devices(args.gpus)
+        check_devices(1 if ONE_DEVICE else args.gpus)
     if args.gpus == 1:
         from coeb_front.dist import Ranks
         rank_main(Ranks(), args)
@@ -661,6 +664,8 @@ def check_devices(n):
 
 def rank_main(ranks, args):
     world, rank, local_rank = ranks.world, ranks.rank, ranks.local_rank
+    if ONE_DEVICE:
+        local_rank = 0          # rehearsal: every rank's context on device 0
     from coeb_front import synth
     from coeb_front.dist import shard_frames
     cfg = CONFIGS[args.config]
@@ -778,6 +783,8 @@ def rank_main(ranks, args):
                     pcie_inclusive=None)
         if tracking is not None:
             line["tracking"] = tracking
+        if ONE_DEVICE and world > 1:
+            line["rehearsal_one_device"] = True
         if not args.no_extras and world == 1 and not args.dry_run:
             line["extras"] = extras_timing(bp.ctx, out, w, h)
             line["extras"]["single_frame"] = single_frame_timing(w, h)
