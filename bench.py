@@ -31,13 +31,15 @@ import numpy as np  # noqa: E402
 METRIC = "frames/sec ORB extract+match @640x480/1000 kp; 1/2/4/8 GPU + %HBM roofline"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
 CONFIGS = {
-    # batch = matched frames per step per GPU.  A and C: 1024 (measured 208 / 250 / 257 / 269 / 265 k
-    # frames/s at 128 / 256 / 512 / 1024 / 2048, profiles/r02/v3/batch_sweep.txt: 1024 frames give every
-    # launch >= 4 workgroups per CU, including the small pyramid levels and the matcher); D: 256.
-    "A": dict(w=640, h=480, nfeatures=1000, batch=1024,
+    # batch = matched frames per step per GPU, split over `pipelines` contexts whose kernels overlap.
+    # A and C: 2048 as 2 x 1024.  One pipeline measured 208 / 250 / 257 / 269 / 265 k frames/s at
+    # 128 / 256 / 512 / 1024 / 2048 frames (profiles/r02/v3/batch_sweep.txt: 1024 frames give every
+    # launch >= 4 workgroups per CU, including the small pyramid levels and the matcher); two 1024-frame
+    # pipelines 275 k (profiles/r02/v4/pipelines_ab.txt).  D: 256, one pipeline.
+    "A": dict(w=640, h=480, nfeatures=1000, batch=2048, pipelines=2,
               workload="640x480, 8-level pyramid, 1000 kp, extract + Hamming match to prev frame (BASELINE configs[1])"),
     "B": dict(w=1280, h=960, nfeatures=2000, workload="1280x960, 8-level pyramid, 2000 kp, extract + match (BASELINE configs[3] shape)"),
-    "C": dict(w=640, h=480, nfeatures=1000, dyn=True, batch=1024,
+    "C": dict(w=640, h=480, nfeatures=1000, dyn=True, batch=2048, pipelines=2,
               workload="640x480, 1000 kp, YOLO-bbox dynamic mask (2 boxes, 60 T_M points, blur_flag [0,1]) + "
                        "depth association (ComputeStereoFromRGBD) + match to prev frame (BASELINE configs[2])"),
     "D": dict(w=640, h=480, nfeatures=1000, chain=True,
@@ -591,6 +593,9 @@ def parse_args(argv=None):
     ap.add_argument("--global-frames", type=int, default=None,
                     help="fixed number of matched frames per step, sharded over the GPUs with one halo frame "
                          "each (strong scaling; config B defaults to BASELINE configs[3]'s 512)")
+    ap.add_argument("--pipelines", type=int, default=None,
+                    help="independent batch pipelines (contexts) per GPU whose kernels overlap (default: the "
+                         "config's); the GPU's batch is split between them, each with its own halo frame")
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the batch is chunked over (kernels of different chunks overlap)")
@@ -610,6 +615,8 @@ def main():
         args.global_frames = 512
     if args.batch is None:
         args.batch = CONFIGS[args.config].get("batch", 256)
+    if args.pipelines is None:
+        args.pipelines = CONFIGS[args.config].get("pipelines", 1)
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     if env_world > 1 or "LOCAL_RANK" in os.environ:
         # one process per GPU under torch.distributed.run
@@ -667,7 +674,7 @@ def rank_main(ranks, args):
     if ONE_DEVICE:
         local_rank = 0          # rehearsal: every rank's context on device 0
     from coeb_front import synth
-    from coeb_front.dist import shard_frames
+    from coeb_front.dist import shard, shard_frames
     cfg = CONFIGS[args.config]
     w, h = cfg["w"], cfg["h"]
     strong = args.global_frames is not None
@@ -676,15 +683,28 @@ def rank_main(ranks, args):
         raise SystemExit("bench.py: %d matched frames cannot be split over %d GPUs" % (G, world))
     chain = bool(cfg.get("chain"))
     halo = 3 if chain else 1
-    first, F, nmatched = shard_frames(G, world, rank, halo=halo)
-    if args.dry_run:
-        bp = DryRunPipeline(rank)
-    else:
-        from coeb_front.pipeline import BatchPipeline
-        bp = BatchPipeline(w, h, F, nfeatures=cfg["nfeatures"], device=local_rank)
-    bp.ctx.set_batch_streams(args.streams)
-    frames, Tcw = load_batch(bp, cfg, w, h, F, first)
-    del frames
+    _, nmatched = shard_frames(G, world, rank, halo=halo)[1:]
+    # the rank's matched chunk [lo, hi) split over its pipelines, each extracting its own halo
+    _, lo, hi = shard(G, world, rank)
+    npipe = max(1, min(args.pipelines, hi - lo))
+    subs = []
+    for p in range(npipe):
+        _, a, b = shard(hi - lo, npipe, p)
+        f0 = max(lo + a - (halo - 1), 0)
+        subs.append((f0, lo + b - f0 + 1, b - a))
+    bps = []
+    for first_p, F_p, _ in subs:
+        if args.dry_run:
+            bpp = DryRunPipeline(rank)
+        else:
+            from coeb_front.pipeline import BatchPipeline
+            bpp = BatchPipeline(w, h, F_p, nfeatures=cfg["nfeatures"], device=local_rank)
+        bpp.ctx.set_batch_streams(args.streams)
+        frames, Tcw = load_batch(bpp, cfg, w, h, F_p, first_p)
+        del frames
+        bps.append(bpp)
+    bp = bps[0]                          # results, roofline pass, extras and the PCIe leg use pipeline 0
+    first, F, nmatched0 = subs[0]
     # every rank states what it covers; the sum must be the whole sequence
     covered = int(ranks.sum(nmatched))
     if covered != G:
@@ -693,10 +713,12 @@ def rank_main(ranks, args):
 
     kw = step_kwargs(cfg)
     for _ in range(args.warmup):
-        bp.run(**kw)
-    bp.synchronize()
+        for bpp in bps:
+            bpp.run(**kw)
+    for bpp in bps:
+        bpp.synchronize()
     out, matches, nms = bp.results()
-    c0 = F - nmatched                                               # first counted frame of the batch
+    c0 = F - nmatched0                                              # first counted frame of the batch
     nkp = float(np.mean([len(o[0]) for o in out[c0:]]))
     nmatch = float(np.mean(nms[c0:]))
     ncand = int(bp.ctx.debug_read("cand_n", 1).view(np.int32).sum())
@@ -711,11 +733,14 @@ def rank_main(ranks, args):
 
     # timed region: no instrumentation (HIP event pairs around every launch cost ~10 us each)
     ranks.barrier()
-    bp.synchronize()
+    for bpp in bps:
+        bpp.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        bp.run(**kw)
-    bp.synchronize()
+        for bpp in bps:                  # enqueue only: the pipelines' kernels overlap on the device
+            bpp.run(**kw)
+    for bpp in bps:
+        bpp.synchronize()
     t1 = time.perf_counter()
     ranks.barrier()
     elapsed = ranks.max(t1 - t0)
@@ -769,7 +794,8 @@ def rank_main(ranks, args):
                     data=cfg.get("data", "synthetic (TUM-like rectangles + noise, (+2,+1) px/frame, Z=2 m)"),
                     config=dict(workload=cfg["workload"], width=w, height=h, nfeatures=cfg["nfeatures"],
                                 nlevels=8, matched_frames_per_step=G, frames_per_rank=per_rank,
-                                halo_frames_per_rank=halo, streams_per_gpu=args.streams,
+                                halo_frames_per_rank=halo, pipelines_per_gpu=npipe,
+                                frames_per_pipeline=[sp[2] for sp in subs], streams_per_gpu=args.streams,
                                 ranks="threads" if isinstance(ranks, _thread_rank_type()) else
                                       ("processes" if world > 1 else "single"),
                                 parallelism="frame-sharded x%d (no collectives)" % world),
@@ -789,9 +815,9 @@ def rank_main(ranks, args):
             line["extras"] = extras_timing(bp.ctx, out, w, h)
             line["extras"]["single_frame"] = single_frame_timing(w, h)
             if not cfg.get("dyn") and not cfg.get("pose") and not chain:
-                line["extras"]["config5_tracking"] = config5_timing(bp, nmatched)
+                line["extras"]["config5_tracking"] = config5_timing(bp, nmatched0)
                 line["extras"]["config3_dynamic_mask"] = config3_timing(bp, synth.make_frames(w, h, F, seed=1000),
-                                                                        Tcw, w, h, nmatched)
+                                                                        Tcw, w, h, nmatched0)
         if not args.no_cpu_baseline and world == 1 and not args.dry_run:
             cb = cpu_chain_baseline(cfg) if chain else cpu_baseline(cfg)
             if "extras" in line:
@@ -801,10 +827,12 @@ def rank_main(ranks, args):
     # PCIe-inclusive leg last, with the device-resident pipeline closed: its two contexts and copy
     # queue then have hardware queues of their own
     host_frames, host_tcw = getattr(bp, "host_frames", None), getattr(bp, "Tcw", None)
-    bp.close()
+    for bpp in bps:
+        bpp.close()
     e2e = None
+    g0 = int(ranks.sum(nmatched0))      # the PCIe leg streams pipeline 0's batch on every rank
     if not args.no_e2e and not args.dry_run and not chain:
-        e2e = e2e_timing(host_frames, host_tcw, ranks, G, 30, cfg, local_rank)
+        e2e = e2e_timing(host_frames, host_tcw, ranks, g0, 30, cfg, local_rank)
     if rank == 0:
         line["pcie_inclusive"] = e2e
         print(json.dumps(line), flush=True)
