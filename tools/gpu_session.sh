@@ -25,9 +25,10 @@ for step in "$@"; do
         benchB) run benchB 600 python bench.py --config B --batch 64 --no-cpu-baseline ;;
         benchC) run benchC 600 python bench.py --config C --no-cpu-baseline --no-extras ;;
         benchD) run benchD 600 python bench.py --config D --no-cpu-baseline --no-extras ;;
-        # per-kernel evidence with the side stream off: every kernel is then one whole-batch launch
-        # per step, the same launches bench.py's HIP-event pass times (it disables the side stream)
-        prof) COEB_SIDE_STREAM=0 run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-e2e --no-extras ;;
+        # per-kernel evidence with the side stream off and one pipeline: every kernel is then one
+        # whole-batch launch running alone, the same launches bench.py's HIP-event pass times (it
+        # disables the side stream and profiles pipeline 0 by itself)
+        prof) COEB_SIDE_STREAM=0 run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --pipelines 1 --batch 1024 --no-cpu-baseline --no-e2e --no-extras ;;
         profD) COEB_SIDE_STREAM=0 run profD 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profD -o run -- python bench.py --config D --no-cpu-baseline --no-e2e --no-extras --steps 5 --warmup 2 ;;
         diag) run diag 600 python tools/diag_parity.py ;;
         posetime) run posetime 300 python tools/pose_timing.py ;;
@@ -35,7 +36,7 @@ for step in "$@"; do
         flowprof) run flowprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/flowprof -o run -- python tools/flow_bench.py ;;
         pmc)
             export COEB_SIDE_STREAM=0
-            B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-e2e --no-extras"
+            B="python bench.py --pipelines 1 --batch 1024 --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-e2e --no-extras"
             run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- $B
             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- $B
             python tools/pmc_summary.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv \
