@@ -89,6 +89,7 @@ __global__ __launch_bounds__(kThreads) void k_prep(PrepBufs b)
 // iterations, runs the literal sequential loop instead (exact, slower).
 constexpr int kMThreads = 1024;
 constexpr int kCQ = 64;
+
 constexpr int kMaxIter = 64;
 constexpr int kIdxBits = 12;
 // Lanes per LastFrame query in the candidate phase: a grid column range holds a few
@@ -97,6 +98,59 @@ constexpr int kIdxBits = 12;
 #define COEB_MATCH_QL 8
 #endif
 constexpr int kQL = COEB_MATCH_QL;
+#ifndef COEB_MATCH_FLAT
+#define COEB_MATCH_FLAT 1      // 0: k_match walks a query's window one grid column at a time
+#endif
+
+// Up to kQL window columns, one per lane of a kQL-lane group (lane j: CSR range [lo_j, lo_j +
+// len_j)), as one concatenated range in column-major order: its length, and the CSR index of
+// concatenated position f.  A group scan (DPP row shifts, masked to the group) gives each
+// column's end; ds_swizzle broadcasts (groups of kQL within each 32-lane half) hand every lane
+// all of them.
+struct GroupCols {
+    int total;
+    uint32_t pk[kQL];                  // column j: end in the concatenation << 16 | (lo_j - start_j + 0x8000)
+    __device__ __forceinline__ int index(int f) const
+    {
+        uint32_t sel = pk[0];
+#pragma unroll
+        for (int j = 1; j < kQL; j++)
+            if (f >= (int)(pk[j - 1] >> 16)) sel = pk[j];
+        return f + (int)(sel & 0xFFFFu) - 0x8000;
+    }
+};
+
+template <int K>
+__device__ __forceinline__ void group_bcast(uint32_t v, GroupCols& g)
+{
+    constexpr int pat = (0x1F & ~(kQL - 1)) | (K << 5);   // lane = (lane & and_mask) | K
+    g.pk[K] = (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, pat);
+    if constexpr (K + 1 < kQL) group_bcast<K + 1>(v, g);
+}
+
+__device__ __forceinline__ GroupCols group_cols(int lo, int len, int gl)
+{
+    static_assert(kQL <= 16 && (kQL & (kQL - 1)) == 0, "group scan within one 16-lane DPP row");
+    int inc = len;
+    int t = __builtin_amdgcn_mov_dpp(inc, 0x111, 0xf, 0xf, true);          // row_shr:1
+    if (gl >= 1) inc += t;
+    if constexpr (kQL > 2) {
+        t = __builtin_amdgcn_mov_dpp(inc, 0x112, 0xf, 0xf, true);          // row_shr:2
+        if (gl >= 2) inc += t;
+    }
+    if constexpr (kQL > 4) {
+        t = __builtin_amdgcn_mov_dpp(inc, 0x114, 0xf, 0xf, true);          // row_shr:4
+        if (gl >= 4) inc += t;
+    }
+    if constexpr (kQL > 8) {
+        t = __builtin_amdgcn_mov_dpp(inc, 0x118, 0xf, 0xf, true);          // row_shr:8
+        if (gl >= 8) inc += t;
+    }
+    GroupCols g;   // candidate counts < 2^16 and |lo - start| < 2^15 (kIdxBits = 12: <= 4096 keypoints)
+    group_bcast<0>(((uint32_t)inc << 16) | (uint32_t)(lo - (inc - len) + 0x8000), g);
+    g.total = (int)(g.pk[kQL - 1] >> 16);
+    return g;
+}
 #ifndef COEB_MATCH_REGLIST
 #define COEB_MATCH_REGLIST 16
 #endif
@@ -579,11 +633,29 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
                     qd[4] = qi.d1.x; qd[5] = qi.d1.y; qd[6] = qi.d1.z; qd[7] = qi.d1.w;
                     cnt = 0;
                     uint32_t* lst = lists + (int64_t)q * kCQ;
+#if COEB_MATCH_FLAT
+                    // the window's columns kQL at a time: lane gl holds column gx + gl's CSR range, a
+                    // group scan gives each column's offset in the concatenated (column-major) order,
+                    // and the group walks that concatenation kQL candidates at a time -- one pass per
+                    // column group instead of one per column, same enumeration order
+                    for (int gx = w.x0; gx <= w.x1; gx += kQL) {
+                        int clo = 0, clen = 0;
+                        if (gx + gl <= w.x1) {
+                            clo = L.cell[(gx + gl) * COEB_GRID_ROWS + w.y0];
+                            clen = L.cell[(gx + gl) * COEB_GRID_ROWS + w.y1 + 1] - clo;
+                        }
+                        const GroupCols gc = group_cols(clo, clen, gl);
+                        for (int base = 0; base < gc.total; base += kQL) {
+                            const int fi = base + gl;
+                            const int e = gc.index(fi);
+                            const int c1 = fi < gc.total ? e + 1 : e;      // e < c1 <=> fi < total
+#else
                     for (int ix = w.x0; ix <= w.x1; ix++) {
                         const int c0 = L.cell[ix * COEB_GRID_ROWS + w.y0];
                         const int c1 = L.cell[ix * COEB_GRID_ROWS + w.y1 + 1];
                         for (int base = c0; base < c1; base += kQL) {
                             const int e = base + gl;
+#endif
                             bool ok = false;
                             uint32_t ent = 0;
                             if (e < c1) {
@@ -784,11 +856,25 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
                 qd[4] = d1.x; qd[5] = d1.y; qd[6] = d1.z; qd[7] = d1.w;
                 cnt = 0;
                 uint32_t* lst = b.lists + (int64_t)q * kCQ;
+#if COEB_MATCH_FLAT
+                for (int gx = w.x0; gx <= w.x1; gx += kQL) {        // column groups, as in k_match
+                    int clo = 0, clen = 0;
+                    if (gx + gl <= w.x1) {
+                        clo = L.cell[(gx + gl) * COEB_GRID_ROWS + w.y0];
+                        clen = L.cell[(gx + gl) * COEB_GRID_ROWS + w.y1 + 1] - clo;
+                    }
+                    const GroupCols gc = group_cols(clo, clen, gl);
+                    for (int base = 0; base < gc.total; base += kQL) {
+                        const int fi = base + gl;
+                        const int e = gc.index(fi);
+                        const int c1 = fi < gc.total ? e + 1 : e;
+#else
                 for (int ix = w.x0; ix <= w.x1; ix++) {
                     const int c0 = L.cell[ix * COEB_GRID_ROWS + w.y0];
                     const int c1 = L.cell[ix * COEB_GRID_ROWS + w.y1 + 1];
                     for (int base = c0; base < c1; base += kQL) {
                         const int e = base + gl;
+#endif
                         bool ok = false;
                         uint32_t ent = 0;
                         if (e < c1) {
@@ -1041,11 +1127,25 @@ __global__ __launch_bounds__(kMThreads) void k_match_kf(MatchCam cam, KfBufs b, 
                 qd[4] = d1.x; qd[5] = d1.y; qd[6] = d1.z; qd[7] = d1.w;
                 cnt = 0;
                 uint32_t* lst = b.lists + (int64_t)q * kCQ;
+#if COEB_MATCH_FLAT
+                for (int gx = w.x0; gx <= w.x1; gx += kQL) {        // column groups, as in k_match
+                    int clo = 0, clen = 0;
+                    if (gx + gl <= w.x1) {
+                        clo = L.cell[(gx + gl) * COEB_GRID_ROWS + w.y0];
+                        clen = L.cell[(gx + gl) * COEB_GRID_ROWS + w.y1 + 1] - clo;
+                    }
+                    const GroupCols gc = group_cols(clo, clen, gl);
+                    for (int base = 0; base < gc.total; base += kQL) {
+                        const int fi = base + gl;
+                        const int e = gc.index(fi);
+                        const int c1 = fi < gc.total ? e + 1 : e;
+#else
                 for (int ix = w.x0; ix <= w.x1; ix++) {
                     const int c0 = L.cell[ix * COEB_GRID_ROWS + w.y0];
                     const int c1 = L.cell[ix * COEB_GRID_ROWS + w.y1 + 1];
                     for (int base = c0; base < c1; base += kQL) {
                         const int e = base + gl;
+#endif
                         bool ok = false;
                         uint32_t ent = 0;
                         if (e < c1) {
