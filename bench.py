@@ -805,6 +805,8 @@ def rank_main(ranks, args):
                                            frac=round(value * pipeline_bytes / 1e9 / HBM_PEAK_GBS / world, 6)),
                     kernels_ms_per_step={k: round(v[0] / max(1, prof_steps), 4) for k, v in prof.items()},
                     kernels_profiled_steps=prof_steps,
+                    kernels_note="ms per launch set of pipeline 0 alone (%d frames), side stream off, HIP events on "
+                                 "the context stream; the step runs %d such pipelines concurrently" % (F, npipe),
                     keypoints_per_frame=round(nkp, 1), matches_per_frame=round(nmatch, 1),
                     pcie_inclusive=None)
         if tracking is not None:
