@@ -55,6 +55,10 @@ CONFIGS = {
 # rank on device 0 of a one-GPU box; its lines carry "rehearsal_one_device" and measure nothing.
 ONE_DEVICE = os.environ.get("COEB_BENCH_ONE_DEVICE") == "1"
 DEPTH_MAP_FACTOR = 1.0 / 5000.0     # mDepthMapFactor = 1 / DepthMapFactor (TUM yaml: 5000)
+CPU_CAVEAT = ("the oracle is a scalar C restatement of ORBextractor/ORBmatcher with the OpenCV primitives "
+              "(FAST, resize, GaussianBlur, LK, ...) restated without SIMD: real OpenCV 3.4 vectorises them, so the "
+              "reference binary runs faster than this port (SURVEY.md s8(d)); the reference itself is unbuildable here "
+              "(no OpenCV/g2o/DBoW2 in the image)")
 
 
 def step_kwargs(cfg):
@@ -111,9 +115,49 @@ def fast_roi_pixels(w, h, nlevels=8, scale=1.2):
     return tot
 
 
-def kernel_bytes(name, w, h, nkp, nprev, npx, ncand):
-    """Algorithmic bytes of one launch per frame (each byte the algorithm must read or write,
-    touched once), DESIGN.md s4."""
+# launches over the F - 1 consecutive frame pairs of a batch (the rest cover F frames)
+PAIR_KERNELS = ("k_match", "k_gf_response", "k_gf_candidates", "k_gf_select", "k_subpix", "k_sharr", "k_lk", "k_fm",
+                "k_pose", "k_track_prep", "k_tlm_pose_prep")
+LK_WIN, LK_LEVELS = 22, 5          # calcOpticalFlowPyrLK(winSize 22x22, maxLevel 4), Frame.cc:335
+
+
+def lk_level_sizes(w, h, levels=LK_LEVELS):
+    out = [(w, h)]
+    for _ in range(levels - 1):
+        w, h = (w + 1) // 2, (h + 1) // 2
+        out.append((w, h))
+    return out
+
+
+def kernel_bytes(name, w, h, nkp, nprev, npx, ncand, flow=None):
+    """Algorithmic bytes of one launch per unit (each byte the algorithm must read or write,
+    touched once), DESIGN.md s4.  The unit is a frame for the extraction / matching kernels and a
+    frame pair for the ProcessMovingObject kernels (flow = per-pair means {keys, corners})."""
+    flow = flow or {}
+    corners, keys = flow.get("corners", 0.0), flow.get("keys", 0.0)
+    lv = lk_level_sizes(w, h)
+    if name == "k_rgbd_batch":  # RGB8 + 16U depth in, gray + 32F depth out
+        return (3 + 2 + 1 + 4) * w * h
+    if name == "k_gf_response":  # gray in, float Harris response out
+        return 5 * w * h
+    if name == "k_gf_candidates":  # response in, (value, index) keys out
+        return 4 * w * h + 8 * keys
+    if name == "k_gf_select":   # keys in, corners out
+        return 8 * keys + 8 * corners
+    if name == "k_subpix":      # per corner: the 24x24 source of the 23x23 interpolated window, point in/out
+        return (24 * 24 + 16) * corners
+    if name == "k_pyr_down":    # 4 launches: each frame's level l-1 in, level l out (mean per launch)
+        return sum(a[0] * a[1] + b[0] * b[1] for a, b in zip(lv[:-1], lv[1:])) / (len(lv) - 1)
+    if name == "k_sharr":       # every level of the previous frame in, short2 derivatives out
+        return sum(x * y for x, y in lv) * (1 + 4)
+    if name == "k_lk":          # per point and level: prev window, its derivatives, next window ((win+1)^2 px each)
+        return corners * (LK_LEVELS * (LK_WIN + 1) ** 2 * (1 + 4 + 1) + 17)
+    if name == "k_fm":          # points + status in, 3x3 SAD patches of both frames, T_M out
+        return corners * (8 + 8 + 1 + 18 + 8)
+    if name == "k_blur_flags":  # the box crop (120 x 160 px in config D)
+        return 120 * 160
+    if name in ("k_pose", "k_track_prep", "k_tlm_pose_prep"):   # per keypoint: MapPoint + keypoint + flags
+        return (12 + 28 + 4 + 2) * nkp
     if name == "k_fast":        # read the FAST ROIs of every level, write candidate keys
         return fast_roi_pixels(w, h) + 4 * ncand
     if name == "k_blur":        # read + write every level
@@ -202,6 +246,7 @@ def cpu_baseline(cfg, seconds=12.0, min_frames=30):
                       "CPU %d: extract + ComputeStereoFromRGBD + SearchByProjection(th 15, retry 30); median %.2f "
                       "ms/frame" % (len(times), w, h, cpus[0], med * 1e3))
     out.update(info)
+    out["caveat"] = CPU_CAVEAT
     out["all_cores"] = cpu_baseline_parallel(O, cfg, frames, depth, cam, len(cpus))
     return out
 
@@ -285,6 +330,7 @@ def cpu_chain_baseline(cfg, seconds=15.0, min_frames=20):
                       "ProcessMovingObject, blur flags, masked extract, stereo, motion model, TrackLocalMap); median "
                       "%.2f ms/frame" % (len(times), w, h, cpus[0], med * 1e3))
     out.update(info)
+    out["caveat"] = CPU_CAVEAT
     nthr = len(cpus)
     import threading
     done = [0] * nthr
@@ -393,10 +439,12 @@ def cpu_extras(out, w, h, reps=5):
     return res
 
 
-def _pmc_file(stem, w, h):
-    """The committed PMC summary collected at frame size w x h: profiles/<stem>.json (config A's
-    640x480) or profiles/<stem>_<w>x<h>.json; None when neither matches the size."""
-    for name in ("%s.json" % stem, "%s_%dx%d.json" % (stem, w, h)):
+def _pmc_file(stem, w, h, tag=None):
+    """The committed PMC summary collected at frame size w x h: profiles/<stem>_<tag>.json for a
+    config with its own kernels (tag "D": the configs[4] loop), else profiles/<stem>.json (config
+    A's 640x480) or profiles/<stem>_<w>x<h>.json; None when none matches the size."""
+    names = ("%s_%s.json" % (stem, tag),) if tag else ("%s.json" % stem, "%s_%dx%d.json" % (stem, w, h))
+    for name in names:
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 d = json.load(f)
@@ -408,13 +456,13 @@ def _pmc_file(stem, w, h):
     return None
 
 
-def pmc_traffic(kernel, frames_per_launch, w, h):
+def pmc_traffic(kernel, frames_per_launch, w, h, tag=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by tools/pmc_summary.py --json from separate
     FETCH_SIZE / WRITE_SIZE passes of this bench), scaled to this run's frames per launch.
     None unless the counters were collected at this frame size."""
     try:
-        d = _pmc_file("pmc_traffic", w, h)
+        d = _pmc_file("pmc_traffic", w, h, tag)
         if d is None:
             return None, None
         k = d["kernels"][kernel]
@@ -424,17 +472,21 @@ def pmc_traffic(kernel, frames_per_launch, w, h):
         return None, None
 
 
-def pmc_valu(kernel, w, h):
+def pmc_valu(kernel, w, h, tag=None):
     """VALU issue utilisation of `kernel` from the committed PMC summary (profiles/pmc_valu.json,
     tools/pmc_summary.py --valu-json: SQ_INSTS_VALU / (2 x 256 CUs x busy cycles)), if collected
     at this frame size."""
     try:
-        d = _pmc_file("pmc_valu", w, h)
+        d = _pmc_file("pmc_valu", w, h, tag)
         if d is None:
             return None
         k = d["kernels"][kernel]
-        return dict(valu_issue_frac=k["valu_issue_frac"], valu_insts_per_launch=k["valu_insts"],
-                    source="%s (%s)" % (d["_file"], d.get("command", "")))
+        out = dict(valu_issue_frac=k["valu_issue_frac"], valu_insts_per_launch=k["valu_insts"],
+                   source="%s (%s)" % (d["_file"], d.get("command", "")))
+        for key in ("wait_inst_frac", "wait_any_frac", "lds_conflict_per_lds_inst"):
+            if key in k:
+                out[key] = k[key]
+        return out
     except (OSError, KeyError, ValueError):
         return None
 
@@ -722,6 +774,10 @@ def rank_main(ranks, args):
     nkp = float(np.mean([len(o[0]) for o in out[c0:]]))
     nmatch = float(np.mean(nms[c0:]))
     ncand = int(bp.ctx.debug_read("cand_n", 1).view(np.int32).sum())
+    flow = None
+    if chain and not args.dry_run:        # per-pair Harris keys / corners of ProcessMovingObject
+        fc = bp.ctx.debug_read("flow_counts").view(np.int32).reshape(-1, 2)[c0 - 1:]
+        flow = dict(keys=float(fc[:, 0].mean()), corners=float(fc[:, 1].mean()))
     tracking = None
     if chain and not args.dry_run:
         tr = bp.track_results()
@@ -769,14 +825,15 @@ def rank_main(ranks, args):
     if rank == 0:
         npx = level_pixels(w, h)
         roof = None
+        tag = "D" if chain else None
         if prof:
             dom = max(prof.items(), key=lambda kv: kv[1][0])
             name, (tot_ms, launches) = dom
             avg_s = tot_ms / launches / 1e3
-            frames_per_launch = F if name != "k_match" else F - 1
-            bpl = kernel_bytes(name, w, h, nkp, nkp, npx, ncand) * frames_per_launch
+            frames_per_launch = F - 1 if name in PAIR_KERNELS else F
+            bpl = kernel_bytes(name, w, h, nkp, nkp, npx, ncand, flow) * frames_per_launch
             achieved = bpl / avg_s / 1e9
-            traffic, tsrc = pmc_traffic(name, frames_per_launch, w, h)
+            traffic, tsrc = pmc_traffic(name, frames_per_launch, w, h, tag)
             roof = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, kernel=name,
                         avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=int(bpl))
@@ -784,7 +841,7 @@ def rank_main(ranks, args):
                 roof["traffic_source"] = tsrc
             # the kernel is bound by integer VALU issue, not HBM: the PMC VALU fraction says how
             # close it runs to the chip's issue ceiling (2 wave64 VALU instructions per CU per cycle)
-            valu = pmc_valu(name, w, h)
+            valu = pmc_valu(name, w, h, tag)
             if valu is not None:
                 roof["valu"] = valu
         pipeline_bytes = w * h + 60 * nkp + 36 * nkp     # B = W*H + 60 N_kp + 36 N_prev
@@ -811,6 +868,8 @@ def rank_main(ranks, args):
                     pcie_inclusive=None)
         if tracking is not None:
             line["tracking"] = tracking
+        if flow is not None:
+            line["flow_per_pair"] = dict(harris_keys=round(flow["keys"], 1), corners=round(flow["corners"], 1))
         if ONE_DEVICE and world > 1:
             line["rehearsal_one_device"] = True
         if not args.no_extras and world == 1 and not args.dry_run:

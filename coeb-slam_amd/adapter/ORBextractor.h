@@ -63,6 +63,9 @@ inline coeb_ctx* pooled_context(const coeb_orb_params& p, int device, int max_w,
     std::lock_guard<std::mutex> lk(mu);
     auto it = pool.find(key);
     if (it != pool.end()) return it->second;
+    if (coeb_abi_version() != COEB_ABI_VERSION)      // header and loaded library must agree
+        throw std::runtime_error("libcoeb_front ABI " + std::to_string(coeb_abi_version()) + ", header " +
+                                 std::to_string(COEB_ABI_VERSION));
     coeb_ctx* c = coeb_create(&p, device, max_w, max_h, 1);
     if (!c) throw std::runtime_error(std::string("coeb_create: ") + coeb_last_error(nullptr));
     pool[key] = c;

@@ -69,6 +69,7 @@ inline coeb_ctx* matcher_ctx(int nlevels, float scale_factor)
     for (const Entry& e : pool)
         if (e.nlevels == nlevels && e.scale == scale_factor) return e.ctx;
     coeb_orb_params p{1000, scale_factor, nlevels, 20, 7};
+    if (coeb_abi_version() != COEB_ABI_VERSION) throw std::runtime_error("libcoeb_front ABI differs from the header");
     coeb_ctx* c = coeb_create(&p, 0, 640, 480, 1);
     if (!c) throw std::runtime_error(coeb_last_error(nullptr));
     pool.push_back(Entry{nlevels, scale_factor, c});

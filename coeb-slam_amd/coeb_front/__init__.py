@@ -39,7 +39,7 @@ DEPTH_U16, DEPTH_F32 = 0, 1          # COEB_DEPTH_U16 / COEB_DEPTH_F32
 
 # exported symbols of include/coeb_front.h (checked by tests/test_capi_symbols.py)
 ABI_SYMBOLS = [
-    "coeb_create", "coeb_destroy", "coeb_last_error", "coeb_orb_tables_get", "coeb_max_keypoints",
+    "coeb_abi_version", "coeb_create", "coeb_destroy", "coeb_last_error", "coeb_orb_tables_get", "coeb_max_keypoints",
     "coeb_extract", "coeb_extract_batch_device", "coeb_batch_results", "coeb_match_batch_device",
     "coeb_match_batch_device_tcw",
     "coeb_batch_match_results", "coeb_match_lastframe", "coeb_blur_flags", "coeb_stereo_from_rgbd",

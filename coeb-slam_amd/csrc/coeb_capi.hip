@@ -20,7 +20,13 @@ static const int8_t kPattern[1024] = {
 #include "../../data/orb_bit_pattern_31.inc"
 };
 
-static std::string g_last_error;
+// per host thread: ranks of `bench.py --gpus N` (one thread per device) and threaded adapters call
+// the library concurrently; coeb_last_error(NULL) returns the calling thread's last message
+static thread_local std::string g_last_error;
+
+// coeb_flow.hip
+extern "C" int coeb_internal_flow_counts(coeb_ctx* c, int* out, int cap, int* npairs);
+extern "C" void coeb_internal_flow_forget(const coeb_ctx* c);
 
 namespace {
 
@@ -147,59 +153,8 @@ int resize_tables(int sw, int sh, int dw, int dh, std::vector<int>& tab)
     return xmax;
 }
 
-// Split each cell row of a level into band segments of whole cells for k_fast_band: the fewest
-// segments whose windows fit its LDS rows (64 dwords of 4-pixel groups plus one dword either
-// side from a 16-byte aligned start) and its cell / row limits.
-bool make_segments(Plan& P, const std::vector<CellDesc>& cells, std::vector<FastSeg>& segs, std::string& err)
-{
-    segs.clear();
-    P.band_pw = 0;
-    auto make = [&](int l, int a, int z, FastSeg& S) {
-        S.level = (int16_t)l;
-        S.ncell = (int16_t)(z - a);
-        S.cell = (int16_t)a;
-        S.y0 = cells[a].y0;
-        S.ws = (int16_t)(cells[a].x0 + 3);
-        S.we = (int16_t)(cells[z - 1].x0 + cells[z - 1].rw - 3);
-        S.xs = (int16_t)((S.ws - 4) & ~15);
-        S.pw = (int16_t)((S.we - 1 - S.xs) / 4 + 2);        // dwords the pre-test touches
-        const int gfirst = (S.ws - S.xs) >> 2, glast = (S.we - 1 - S.xs) >> 2;
-        return glast - gfirst < 64 && S.pw <= kBandPW && S.ncell <= kBandCells && cells[a].rh <= kBandRows;
-    };
-    for (int l = 0; l < P.L; l++) {
-        LevelGeom& g = P.lv[l];
-        g.seg0 = (int)segs.size();
-        int k = g.cell0;
-        while (k < g.cell0 + g.ncells) {
-            int e = k;
-            while (e < g.cell0 + g.ncells && cells[e].i == cells[k].i) e++;   // cells of row i: [k, e)
-            const int n = e - k;
-            for (int nseg = 1; ; nseg++) {
-                if (nseg > n) { err = "FAST cell row does not fit the band kernel"; return false; }
-                std::vector<FastSeg> row;
-                bool ok = true;
-                for (int q = 0; q < nseg && ok; q++) {
-                    FastSeg S;
-                    ok = make(l, k + (int)((int64_t)n * q / nseg), k + (int)((int64_t)n * (q + 1) / nseg), S);
-                    row.push_back(S);
-                }
-                if (!ok) continue;
-                for (const FastSeg& S : row) {
-                    P.band_pw = std::max(P.band_pw, (int)S.pw);
-                    segs.push_back(S);
-                }
-                break;
-            }
-            k = e;
-        }
-        g.nseg = (int)segs.size() - g.seg0;
-    }
-    P.nsegs = (int)segs.size();
-    return true;
-}
-
 bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, std::vector<CellDesc>& cells,
-               std::vector<FastSeg>& segs, std::string& err)
+               std::string& err)
 {
     memset(&P, 0, sizeof(P));
     P.W = W; P.H = H; P.L = t.nlevels;
@@ -311,10 +266,6 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
     if (const char* e = getenv("COEB_OCT_KL")) P.oct_kl = std::max(256, std::min(8192, atoi(e)));
     P.oct_lds = P.oct_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * P.oct_kl;
     if (P.oct_lds > 150 * 1024) { err = "octree LDS budget exceeded (features per level too large)"; return false; }
-    {
-        std::string serr;   // a plan the band kernel cannot take runs FAST per cell (k_fast)
-        if (!make_segments(P, cells, segs, serr)) { segs.clear(); P.nsegs = 0; }
-    }
     memcpy(P.umax, t.umax, sizeof(P.umax));
     // k_describe folds the IC_Angle disc (umax for HALF_PATCH_SIZE 15) into constants
     static const int kUmaxDisc[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
@@ -403,7 +354,6 @@ struct coeb_ctx {
     Plan plan{};
     std::vector<int> rtab;
     std::vector<CellDesc> cells;
-    std::vector<FastSeg> segs;
     std::map<std::string, DevBuf> bufs;
     std::string err;
     ProfImpl prof;
@@ -544,7 +494,7 @@ int ensure_plan(coeb_ctx* c, int W, int H)
         return set_err(c, COEB_EINVAL, "image size outside the context limits");
     std::string err;
     Plan P;
-    if (!make_plan(c->tab, W, H, P, c->rtab, c->cells, c->segs, err)) return set_err(c, COEB_EINVAL, err);
+    if (!make_plan(c->tab, W, H, P, c->rtab, c->cells, err)) return set_err(c, COEB_EINVAL, err);
     // the plan, rtab and cells are rewritten in place below: batches still in flight on the
     // context's streams (pyramid / FAST / octree / describe read them) must finish first
     int rc;
@@ -558,10 +508,6 @@ int ensure_plan(coeb_ctx* c, int W, int H)
     if ((rc = ensure(c, "rtab", std::max<size_t>(c->rtab.size(), 1), &drtab))) return rc;
     if ((rc = ensure(c, "cells", c->cells.size(), &dcells))) return rc;
     if ((rc = ensure(c, "pattern", 1024, &dpat))) return rc;
-    FastSeg* dsegs;
-    if ((rc = ensure(c, "segs", std::max<size_t>(c->segs.size(), 1), &dsegs))) return rc;
-    if (!c->segs.empty())
-        HIP_TRY(c, hipMemcpy(dsegs, c->segs.data(), c->segs.size() * sizeof(FastSeg), hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(dplan, &c->plan, sizeof(Plan), hipMemcpyHostToDevice));
     if (!c->rtab.empty()) HIP_TRY(c, hipMemcpy(drtab, c->rtab.data(), c->rtab.size() * sizeof(int), hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(dcells, c->cells.data(), c->cells.size() * sizeof(CellDesc), hipMemcpyHostToDevice));
@@ -599,7 +545,6 @@ int extract_bufs(coeb_ctx* c, int F, ExtractBufs& b)
     b.rtab = static_cast<const int*>(c->bufs["rtab"].p);
     b.cells = static_cast<const CellDesc*>(c->bufs["cells"].p);
     b.pattern = static_cast<const int8_t*>(c->bufs["pattern"].p);
-    b.segs = static_cast<const FastSeg*>(c->bufs["segs"].p);
     return 0;
 }
 
@@ -764,6 +709,8 @@ int check_err_word(coeb_ctx* c)
 
 extern "C" {
 
+int coeb_abi_version(void) { return COEB_ABI_VERSION; }
+
 int coeb_device_count(void)
 {
     int n = 0;
@@ -853,6 +800,7 @@ void coeb_destroy(coeb_ctx* c)
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    coeb_internal_flow_forget(c);
     delete c;
 }
 
@@ -937,8 +885,9 @@ int coeb_extract_batch_device(coeb_ctx* c, const uint8_t* d_gray, int F, int W, 
 
 extern "C" int coeb_internal_pmo_batch(coeb_ctx* c, const uint8_t* d_gray, int F, int w, int h, float* tm_out,
                                        int* ntm_out, int tm_cap);
-extern "C" int coeb_internal_blur_flags_batch(const uint8_t* d_gray, int W, int H, const float* d_boxes,
-                                              const int* d_box_frame, int nbox, int* d_out, hipStream_t s);
+extern "C" int coeb_internal_blur_flags_batch(coeb_ctx* c, const uint8_t* d_gray, int W, int H, const float* d_boxes,
+                                              const int* d_box_off, int F, int* d_box_frame, int nbox, int* d_out,
+                                              hipStream_t s);
 
 int coeb_frame_batch_device(coeb_ctx* c, const uint8_t* d_gray, int F, int W, int H, const coeb_box* boxes,
                             const int32_t* box_off)
@@ -949,7 +898,9 @@ int coeb_frame_batch_device(coeb_ctx* c, const uint8_t* d_gray, int F, int W, in
     (void)hipSetDevice(c->device);
     int rc;
     if ((rc = ensure_plan(c, W, H))) return rc;
-    quiesce(c);                                  // single stream: the flow scratch and T_M are rewritten
+    // Everything below runs on the context stream, so stream order protects the flow scratch,
+    // T_M and the box staging of the previous batch (ensure() quiesces before it reallocates);
+    // the pose stream reads only its own snapshots (k_track_prep / k_tlm_snapshot).
     hipStream_t s = main_stream(c);
     const int nbox = boxes ? box_off[F] : 0;
     float* tm;
@@ -962,18 +913,11 @@ int coeb_frame_batch_device(coeb_ctx* c, const uint8_t* d_gray, int F, int W, in
     if ((rc = extract_bufs(c, F, b))) return rc;
     if ((rc = upload_dyn(c, F, boxes, box_off, nullptr, nullptr, nullptr, b))) return rc;
     if (nbox > 0) {
-        // detect_laplacian blur flag of every box (Frame.cc:171-202); frame 0 = the first frame
-        std::vector<int32_t> bf((size_t)nbox);
-        for (int f = 0; f < F; f++)
-            for (int i = box_off[f]; i < box_off[f + 1]; i++) bf[(size_t)i] = f;
+        // detect_laplacian blur flag of every box (Frame.cc:171-202); frame 0 = the first frame.
+        // The box -> frame map is built on the device from the box offsets upload_dyn staged.
         if ((rc = ensure(c, "f_bframe", (size_t)nbox, &bframe)) || (rc = ensure(c, "f_blur", (size_t)nbox, &blur)))
             return rc;
-        Pack pk;
-        const size_t o = pk.add(bf.data(), (size_t)nbox * 4);
-        uint8_t* dbase;
-        if ((rc = stage_in(c, pk, &dbase, s))) return rc;
-        HIP_TRY(c, hipMemcpyAsync(bframe, dbase + o, (size_t)nbox * 4, hipMemcpyDeviceToDevice, s));
-        if (coeb_internal_blur_flags_batch(d_gray, W, H, b.boxes, bframe, nbox, blur, s))
+        if (coeb_internal_blur_flags_batch(c, d_gray, W, H, b.boxes, b.box_off, F, bframe, nbox, blur, s))
             return hip_err(c, hipGetLastError(), "blur flags");
         b.blurf = blur;
     }
@@ -1937,19 +1881,31 @@ int coeb_internal_scratch(coeb_ctx* c, const char* name, size_t bytes, void** p)
 
 int coeb_internal_error(coeb_ctx* c, int code, const char* msg) { return set_err(c, code, msg); }
 
+ProfileHook* coeb_internal_prof(coeb_ctx* c) { return c ? &c->hook : nullptr; }
+
 /* Debug readback of intermediate buffers of frame f of the last batch (test support):
  * what = "pyr" | "blur" | "cand_n" | "lvl_n" | "lvl_kp" | "dyn"; copies min(bytes, size). */
 int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t bytes, size_t* size_out)
 {
     if (c) join_pose(c);
-    if (c && what && (std::string(what) == "band_timing" || std::string(what) == "fast_timing")) {
-        // [8] k_fast_band / k_fast phase clocks (COEB_BAND_CLOCK / COEB_FAST_CLOCK builds)
+    if (c && what && std::string(what) == "fast_timing") {
+        // [8] k_fast phase clocks (COEB_FAST_CLOCK builds)
         unsigned long long t[8];
         if (size_out) *size_out = sizeof(t);
         if (!host) return 0;                         // size query: the read below also clears
-        if ((std::string(what) == "band_timing" ? band_timing_read(t) : fast_timing_read(t))) return COEB_EDEVICE;
+        if (fast_timing_read(t)) return COEB_EDEVICE;
         memcpy(host, t, std::min(bytes, sizeof(t)));
         return 0;
+    }
+    if (c && what && std::string(what) == "flow_counts") {     // [pairs][2] {Harris keys, corners}
+        static thread_local int t[2 * 8192];
+        int np = 0;
+        int rc = coeb_internal_flow_counts(c, t, 2 * 8192, &np);
+        if (rc) return rc;
+        const size_t n = (size_t)std::min(np, 8192) * 8;
+        if (size_out) *size_out = n;
+        if (host) memcpy(host, t, std::min(bytes, n));
+        return COEB_OK;
     }
     if (c && what && std::string(what) == "oct_timing") {       // [4096][6] k_octree clocks (COEB_OCT_CLOCK)
         static long long t[4096 * 6];

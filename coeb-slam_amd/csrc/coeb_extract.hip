@@ -525,10 +525,7 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
 constexpr int kFastRowBytes = 72;          // >= 1 + 64 + 7 (slab byte = ROI column + 1): any ROI up to 64 wide
 constexpr int kFastRowBytesM = 96;         // ROIs up to 46 wide: pixels in bytes 0..47, M in bytes 48..95
 // (24 dwords: the four rows a half-wave's pre-test reads land on disjoint banks, (a/4) mod 32)
-#ifndef COEB_FAST_UNALIGNED
-#define COEB_FAST_UNALIGNED 1  // 0: realign the staged ROI rows in registers (DPP + selects + alignbyte)
-#endif
-constexpr int kFastGuard = COEB_FAST_UNALIGNED ? 16 : 0;   // bytes before each wave's slab
+constexpr int kFastGuard = 16;             // bytes before each wave's slab (unaligned staging spill)
 constexpr int kFastSurv = 384;             // survivor list (flushed when one more pass could overflow it)
 constexpr int kFastCorners = 384;          // corner list (more corners: NMS walks the whole window)
 constexpr int kFastLists = kFastSurv + 64;   // u16 entries before the corner list
@@ -696,31 +693,11 @@ __device__ __forceinline__ void fast_prefetch(const FastCellGeom& G, FastRegs& R
     }
 }
 
-// One 16-byte chunk of the vec path realigned by sh = (x0 - 1) & 15 (wave-uniform): slab
-// dwords 4c .. 4c+3 of the lane's row = source bytes sh + 16c .. sh + 16c + 15, taken from this
-// lane's chunk and the next lane's (DPP; chunk 3 is never stored, so its neighbour is moot).
-__device__ __forceinline__ void fast_stage_chunk(u32x4 q, uint32_t m2, uint32_t m1, uint32_t bsh, uint8_t* dst,
-                                                 bool store)
-{
-    const uint32_t w[8] = {q.x, q.y, q.z, q.w, dpp_shl1(q.x), dpp_shl1(q.y), dpp_shl1(q.z), dpp_shl1(q.w)};
-    uint32_t w2[6], w1[5];
-#pragma unroll
-    for (int k = 0; k < 6; k++) w2[k] = (m2 & w[k + 2]) | (~m2 & w[k]);
-#pragma unroll
-    for (int k = 0; k < 5; k++) w1[k] = (m1 & w2[k + 1]) | (~m1 & w2[k]);
-    if (store) {
-        uint2* d = reinterpret_cast<uint2*>(dst);
-        d[0] = make_uint2(__builtin_amdgcn_alignbyte(w1[1], w1[0], bsh), __builtin_amdgcn_alignbyte(w1[2], w1[1], bsh));
-        d[1] = make_uint2(__builtin_amdgcn_alignbyte(w1[3], w1[2], bsh), __builtin_amdgcn_alignbyte(w1[4], w1[3], bsh));
-    }
-}
-
 template <int RB>
 __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs& R, uint8_t* roi)
 {
     const int lane = lane_id();
     if (G.vec) {
-#if COEB_FAST_UNALIGNED
         // the 64-byte window's chunks stored as loaded, each at its own slab offset - sh
         // (unaligned ds_write_b128: gfx950 LDS takes any byte address), so slab byte j = ROI
         // column j - 1 with no realignment in registers.  Row r's first chunk spills sh bytes
@@ -733,16 +710,6 @@ __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs
         if (r < G.rh) __builtin_memcpy(d, &R.v0, 16);
         if (r + 16 < G.rh) __builtin_memcpy(d + 16 * RB, &R.v1, 16);
         if (r + 32 < G.rh) __builtin_memcpy(d + 32 * RB, &R.v2, 16);
-#else
-        const int sh = (G.x0 - 1) & 15;
-        const uint32_t m2 = (sh & 8) ? 0xFFFFFFFFu : 0u, m1 = (sh & 4) ? 0xFFFFFFFFu : 0u;
-        const uint32_t bsh = (uint32_t)(sh & 3);
-        const int r = lane >> 2, c = lane & 3;
-        uint8_t* d = roi + r * RB + 16 * c;
-        fast_stage_chunk(R.v0, m2, m1, bsh, d, c < 3 && r < G.rh);
-        fast_stage_chunk(R.v1, m2, m1, bsh, d + 16 * RB, c < 3 && r + 16 < G.rh);
-        fast_stage_chunk(R.v2, m2, m1, bsh, d + 32 * RB, c < 3 && r + 32 < G.rh);
-#endif
     } else if (G.words) {
         const int gx = G.x0 - 1;
         const int kw = min(lane & 15, G.nwords);
@@ -798,12 +765,6 @@ __host__ __device__ inline int fast_wave_lds(const Plan& P, int rb)
     return kFastGuard + fast_slab(P, rb) + fast_ms_slab(P, rb) + 2 * (kFastLists + kFastCorners);
 }
 
-#ifndef COEB_BAND_CLOCK
-#define COEB_BAND_CLOCK 0      // experiment builds: phase clocks of wave 0 (band_timing_read)
-#endif
-__device__ unsigned long long g_band_clk[8];
-#define BC_MARK(v) long long v = COEB_BAND_CLOCK ? (long long)clock64() : 0
-#define BC_ADD(slot, t0) do { if (COEB_BAND_CLOCK && threadIdx.x == 0) atomicAdd(&g_band_clk[slot], (unsigned long long)((long long)clock64() - (t0))); } while (0)
 #ifndef COEB_FAST_CLOCK
 #define COEB_FAST_CLOCK 0      // experiment builds: per-cell k_fast phase clocks (fast_timing)
 #endif
@@ -1004,439 +965,13 @@ __global__ __launch_bounds__(kThreads, 6) void k_fast(const Plan* __restrict__ P
     FC_ADD(4, t_all);
 }
 
-// ================================ k_fast (band form) ================================
-// One workgroup per run of band segments of one frame.  A segment (FastSeg) is the consecutive
-// cells of one cell row of a level; their detection windows tile the segment's window without
-// overlap (ORBextractor.cc:795-829), so every window pixel is tested exactly once and image rows
-// are fetched once per segment instead of once per cell ROI.
-//  1. stage rows y0 .. y0+rh-1, image columns [xs, xs + 4*kBandPW) into LDS rows of kBandPitch
-//     bytes (16-byte loads / ds_write_b128; the next segment's loads are issued before this
-//     segment is processed, so their latency hides behind the pre-test);
-//  2. pre-test at minThFAST, one window row per wave instruction: lane = dword column (4 pixels),
-//     so every LDS read of a wave is 64 consecutive dwords (no bank conflicts) at immediate
-//     offsets; groups with survivors go to the wave's list as (offset, 4-bit mask); a flush
-//     expands them, computes the exact strength M of each survivor and writes the corners
-//     (M > minThFAST) to the strength map and the block's corner list;
-//  3. NMS of every corner against its in-cell neighbours (a neighbour in another cell's window
-//     is outside that cell's FAST ROI: FAST_t scores it 0) at both thresholds; a cell with a kept
-//     corner at iniThFAST uses that result, otherwise minThFAST (:834-838);
-//  4. per cell (one wave, lane = window row) the kept pixels leave in row-major order from a
-//     keep bitmap.
-// Output: the same packed keys and counts as the per-cell form (k_octree input).
-constexpr int kBandPitch = 4 * kBandPW;              // LDS row pitch (bytes), 16-byte multiple
-constexpr int kBandKW = (kBandPitch + 31) / 32;      // keep bitmap dwords per row
-constexpr int kBandEnt = 256;                        // survivor groups per wave list
-constexpr int kBandChunks = (kBandRows * (kBandPitch / 16) + kThreads - 1) / kThreads;   // staging loads per thread
-
-// floor(i / n) for 0 <= i < 2^14, 1 <= n <= 128 from inv = 1.0f / n: (i + 0.5) / n lies at least
-// 0.5 / n from an integer and the float product is within 2^-9 of it.
-__device__ __forceinline__ int div_small(int i, float inv) { return (int)(((float)i + 0.5f) * inv); }
-
-// Segment descriptor as one 16-byte scalar load.
-__device__ __forceinline__ FastSeg load_seg(const FastSeg* __restrict__ segs, int i)
-{
-    const int4 r = reinterpret_cast<const int4*>(segs)[i];
-    FastSeg S;
-    S.level = (int16_t)(r.x & 0xFFFF); S.ncell = (int16_t)(r.x >> 16);
-    S.cell = (int16_t)(r.y & 0xFFFF); S.y0 = (int16_t)(r.y >> 16);
-    S.xs = (int16_t)(r.z & 0xFFFF); S.pw = (int16_t)(r.z >> 16);
-    S.ws = (int16_t)(r.w & 0xFFFF); S.we = (int16_t)(r.w >> 16);
-    return S;
-}
-
-// Staging registers of one segment: chunk q of thread t = flat 16-byte chunk t + 256 q of the
-// segment's rows (named registers: an array here was demoted to scratch)
-struct BandStage {
-    u32x4 v0, v1, v2, v3;
-};
-static_assert(kBandChunks <= 4, "BandStage holds four chunks per thread");
-
-__device__ __forceinline__ void band_load1(const uint8_t* src, int pitch, int rh, int nch, float inv_nch, int q, u32x4& v)
-{
-    const int i = (int)threadIdx.x + q * kThreads;
-    const int r = div_small(i, inv_nch), k = i - r * nch;
-    const int rr = min(r, rh - 1);                        // past the last row: a harmless re-read
-    v = *reinterpret_cast<const u32x4*>(src + (int64_t)rr * pitch + 16 * (r < rh ? k : 0));
-}
-
-__device__ __forceinline__ void band_store1(uint8_t* img, int rh, int nch, float inv_nch, int q, const u32x4& v)
-{
-    const int i = (int)threadIdx.x + q * kThreads;
-    const int r = div_small(i, inv_nch), k = i - r * nch;
-    if (r < rh) *reinterpret_cast<u32x4*>(img + r * kBandPitch + 16 * k) = v;
-}
-
-// Issue the 16-byte row loads of a segment (vec path: rows and the level pitch 16-byte aligned).
-__device__ __forceinline__ void band_load(const uint8_t* src, int pitch, int rh, int nch, float inv_nch, BandStage& R)
-{
-    band_load1(src, pitch, rh, nch, inv_nch, 0, R.v0);
-    if (kBandChunks > 1) band_load1(src, pitch, rh, nch, inv_nch, 1, R.v1);
-    if (kBandChunks > 2) band_load1(src, pitch, rh, nch, inv_nch, 2, R.v2);
-    if (kBandChunks > 3) band_load1(src, pitch, rh, nch, inv_nch, 3, R.v3);
-}
-
-__device__ __forceinline__ void band_store(uint8_t* img, int rh, int nch, float inv_nch, const BandStage& R)
-{
-    band_store1(img, rh, nch, inv_nch, 0, R.v0);
-    if (kBandChunks > 1) band_store1(img, rh, nch, inv_nch, 1, R.v1);
-    if (kBandChunks > 2) band_store1(img, rh, nch, inv_nch, 2, R.v2);
-    if (kBandChunks > 3) band_store1(img, rh, nch, inv_nch, 3, R.v3);
-}
-
-struct BandGeom {
-    const uint8_t* src;   // row y0, column xs of the level image
-    int pitch, rh, nch;
-    float inv_nch;
-    bool vec;
-};
-
-__device__ __forceinline__ BandGeom band_geom(const Plan* P, const ExtractBufs& b, int f, const FastSeg& S)
-{
-    BandGeom G;
-    const LevelGeom& g = P->lv[S.level];
-    G.src = level_ptr(P, b, f, S.level) + (int64_t)S.y0 * g.pitch + S.xs;
-    G.pitch = g.pitch;
-    G.rh = load_cell(b.cells, S.cell).rh;
-    G.nch = (4 * S.pw + 15) >> 4;
-    G.inv_nch = 1.0f / (float)G.nch;
-    G.vec = ((g.pitch | (int)reinterpret_cast<uintptr_t>(G.src)) & 15) == 0;
-    return G;
-}
-
-#ifndef COEB_BAND_STOP
-#define COEB_BAND_STOP 99      // experiment builds (tools/_build_var.sh): end a segment after phase N
-#endif
-#ifndef COEB_BAND_NOFLUSH
-#define COEB_BAND_NOFLUSH 0    // experiment builds: pre-test only (no survivor strengths)
-#endif
-#ifndef COEB_BAND_UNROLL
-#define COEB_BAND_UNROLL 2
-#endif
-constexpr int kBandUnroll = COEB_BAND_UNROLL;   // window rows per wave per pre-test step
-
-// Pre-test of the 4 pixels at columns x0 .. x0+3 of the row 3 below `top` (the 7 rows from top
-// are the ring rows): bit q set <=> pixel q passes OpenCV's pair test at t and is in vmask.
-__device__ __forceinline__ uint32_t band_nib(const uint8_t* top, int t, uint32_t vmask)
-{
-    const uint32_t* rw = reinterpret_cast<const uint32_t*>(top);
-    const uint32_t d3 = rw[0];
-    const uint32_t am = rw[kBandPW - 1], bm = rw[kBandPW], cm = rw[kBandPW + 1];
-    const uint32_t a0 = rw[3 * kBandPW - 1], b0 = rw[3 * kBandPW], c0 = rw[3 * kBandPW + 1];
-    const uint32_t ap = rw[5 * kBandPW - 1], bp = rw[5 * kBandPW], cp = rw[5 * kBandPW + 1];
-    const uint32_t u3 = rw[6 * kBandPW];
-    const us2 T = pk2(t, t);
-    const uint32_t lo = pretest_half(
-        as_us2(__builtin_amdgcn_perm(0u, b0, 0x0c010c00u)), as_us2(__builtin_amdgcn_perm(0u, u3, 0x0c010c00u)),
-        as_us2(__builtin_amdgcn_perm(0u, d3, 0x0c010c00u)), as_us2(win_lo(bp, cp, 2)), as_us2(win_lo(am, bm, 2)),
-        as_us2(win_lo(b0, c0, 3)), as_us2(win_lo(a0, b0, 1)), as_us2(win_lo(bm, cm, 2)), as_us2(win_lo(ap, bp, 2)), T);
-    const uint32_t hi = pretest_half(
-        as_us2(__builtin_amdgcn_perm(0u, b0, 0x0c030c02u)), as_us2(__builtin_amdgcn_perm(0u, u3, 0x0c030c02u)),
-        as_us2(__builtin_amdgcn_perm(0u, d3, 0x0c030c02u)), as_us2(win_hi(bp, cp, 2)), as_us2(win_hi(am, bm, 2)),
-        as_us2(win_hi(b0, c0, 3)), as_us2(win_hi(a0, b0, 1)), as_us2(win_hi(bm, cm, 2)), as_us2(win_hi(ap, bp, 2)), T);
-    // halves are < 256: min(h, 1) per half gives the survivor bits
-    const uint32_t l1 = as_u32(pk_min(as_us2(lo), pk2(1, 1))), h1 = as_u32(pk_min(as_us2(hi), pk2(1, 1)));
-    return (l1 | (l1 >> 15) | (h1 << 2) | (h1 >> 13)) & vmask;
-}
-
 // Workgroup barrier ordering LDS only: __syncthreads() also waits for every outstanding global
-// load and store (vmcnt), which would wait for the next segment's prefetched rows right after
-// issuing them.  k_fast_band shares nothing through global memory between its waves.
+// load and store (vmcnt).  Used where waves share nothing through global memory.
 __device__ __forceinline__ void lds_barrier()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// Exclusive prefix over the wave of a small non-negative count (< 2^nb) from bit-plane ballots:
-// no cross-lane shuffles (each would be an LDS round trip).
-template <int nb>
-__device__ __forceinline__ int wave_prefix_small(int n, int* total)
-{
-    int pre = 0, tot = 0;
-#pragma unroll
-    for (int bt = 0; bt < nb; bt++) {
-        const uint64_t m = __ballot((n >> bt) & 1);
-        pre += mbcnt(m) << bt;
-        tot += __popcll(m) << bt;
-    }
-    *total = tot;
-    return pre;
-}
-
-// Cell of window column col (LDS coordinates) and its window [cs, ce).
-struct BandCells {
-    int ws, we, wcell, ncell;
-    float inv_wcell;
-    __device__ __forceinline__ int cell(int col) const { return min(div_small(col - ws, inv_wcell), ncell - 1); }
-    __device__ __forceinline__ int start(int cc) const { return ws + cc * wcell; }
-    __device__ __forceinline__ int end(int cc) const { return cc == ncell - 1 ? we : ws + (cc + 1) * wcell; }
-};
-
-// NMS of the corner at LDS offset o, column col, at both thresholds: kept(t) <=> (M - t) >
-// max(0, max over in-cell neighbours of (Mn - t)); that is FAST_t's "score > every neighbour's
-// score" with non-corners (M <= t) scoring 0.  A neighbour in another cell's window is outside
-// that cell's FAST ROI and is not a neighbour.  Bit 0 = kept at t_ini, bit 1 = kept at t_min.
-__device__ __forceinline__ int band_nms(const uint8_t* Ms, int o, bool l_ok, bool r_ok, int t_ini, int t_min)
-{
-    constexpr int st = kBandPitch;
-    const int M = Ms[o];
-    const int up = max(max(l_ok ? Ms[o - st - 1] : 0, Ms[o - st]), r_ok ? Ms[o - st + 1] : 0);
-    const int mid = max(l_ok ? Ms[o - 1] : 0, r_ok ? Ms[o + 1] : 0);
-    const int dn = max(max(l_ok ? Ms[o + st - 1] : 0, Ms[o + st]), r_ok ? Ms[o + st + 1] : 0);
-    const int mx = max(max(up, mid), dn);
-    // the maximum over neighbours of (Mn - t) is (max Mn) - t: one maximum serves both thresholds
-    return (M - t_ini > max(mx - t_ini, 0) ? 1 : 0) | (M - t_min > max(mx - t_min, 0) ? 2 : 0);
-}
-
-__global__ __launch_bounds__(kThreads) void k_fast_band(const Plan* __restrict__ P, ExtractBufs b, int seg0, int seg1,
-                                                         int per_block)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t img[kBandRows * kBandPitch];
-    __shared__ __attribute__((aligned(16))) uint8_t Ms[kBandRows * kBandPitch];
-    __shared__ uint32_t ents[kWaves][kBandEnt];          // survivor groups: offset | nibble << 16
-    __shared__ uint16_t pxb[kWaves][4 * 64];             // survivors of 64 groups
-    __shared__ uint32_t corn[kWaves][kBandCornW];        // corners: offset | NMS bits << 16
-    __shared__ uint32_t keep[kBandRows * kBandKW];
-    __shared__ int wcnt[kWaves];                         // corners per wave list (-1: overflow)
-    __shared__ int cellmask;                             // cells with a kept corner at iniThFAST
-    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const int f = blockIdx.y;
-    const int area = b.dyn[f].area_flag;
-    const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
-    const int sfirst = seg0 + blockIdx.x * per_block;
-    const int slast = min(seg1, sfirst + per_block);
-    BandStage R;
-    BandGeom Gn{};
-    FastSeg Sn{};
-    if (sfirst < slast) {
-        Sn = load_seg(b.segs, sfirst);
-        Gn = band_geom(P, b, f, Sn);
-        if (Gn.vec) band_load(Gn.src, Gn.pitch, Gn.rh, Gn.nch, Gn.inv_nch, R);
-    }
-    for (int sg = sfirst; sg < slast; sg++) {
-        const FastSeg S = Sn;
-        const BandGeom G = Gn;
-        const LevelGeom& g = P->lv[S.level];
-        const int rh = G.rh, wh = rh - 6;
-        BandCells C;
-        C.ws = S.ws - S.xs; C.we = S.we - S.xs;                 // window columns in the LDS row
-        C.wcell = g.wcell; C.ncell = S.ncell; C.inv_wcell = 1.0f / (float)g.wcell;
-        BC_MARK(tc0);
-        lds_barrier();                                        // the previous segment is done with LDS
-        // ---- 1. stage (+ issue the next segment's loads) and clear
-        if (G.vec) {
-            band_store(img, rh, G.nch, G.inv_nch, R);
-        } else if (((G.pitch | (int)reinterpret_cast<uintptr_t>(G.src)) & 3) == 0) {
-            const float inv = 1.0f / (float)S.pw;
-            for (int i = tid; i < rh * S.pw; i += kThreads) {
-                const int r = div_small(i, inv), k = i - r * S.pw;
-                reinterpret_cast<uint32_t*>(img + r * kBandPitch)[k] =
-                    reinterpret_cast<const uint32_t*>(G.src + (int64_t)r * G.pitch)[k];
-            }
-        } else {
-            for (int r = 0; r < rh; r++)
-                for (int k = tid; k < 4 * S.pw; k += kThreads)
-                    img[r * kBandPitch + k] = S.xs + k < g.w ? G.src[(int64_t)r * G.pitch + k] : 0;
-        }
-        if (sg + 1 < slast) {
-            Sn = load_seg(b.segs, sg + 1);
-            Gn = band_geom(P, b, f, Sn);
-            if (Gn.vec) band_load(Gn.src, Gn.pitch, Gn.rh, Gn.nch, Gn.inv_nch, R);
-        }
-        for (int i = tid; i < rh * kBandKW; i += kThreads) keep[i] = 0u;
-        // rows 2 and wh + 3 of the strength map: the NMS reads them, the pre-test never writes them
-        if (tid < 2 * kBandPW) reinterpret_cast<uint32_t*>(Ms + (tid < kBandPW ? 2 : wh + 3) * kBandPitch)[tid % kBandPW] = 0u;
-        if (tid == 0) cellmask = 0;
-        lds_barrier();
-        BC_ADD(0, tc0);
-        BC_MARK(tc1);
-
-        // ---- 2. pre-test (4 pixels per lane, one row per wave step) -> survivors -> strength
-        int nc = 0;                                             // this wave's corners
-        if (COEB_BAND_STOP > 1) {
-            const int cw = (C.ws >> 2) + lane;                  // this lane's dword column
-            const int x0 = 4 * cw;
-            const int lo_b = min(max(C.ws - x0, 0), 4), hi_b = min(max(C.we - x0, 0), 4);
-            const uint32_t vmask = ((1u << hi_b) - 1u) & ~((1u << lo_b) - 1u);   // pixels inside the window
-            uint32_t* ent = ents[wv];
-            uint16_t* px = pxb[wv];
-            uint32_t* cl = corn[wv];
-            int ne = 0;
-            for (int r = wv; r < wh; r += kBandUnroll * kWaves) {
-                uint32_t nibs[kBandUnroll];
-#pragma unroll
-                for (int u = 0; u < kBandUnroll; u++) {
-                    const int o = (r + u * kWaves + 3) * kBandPitch + x0;
-                    nibs[u] = r + u * kWaves < wh ? band_nib(img + o - 3 * kBandPitch, th_min, vmask) : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < kBandUnroll; u++) {
-                    const int o = (r + u * kWaves + 3) * kBandPitch + x0;
-                    if (r + u * kWaves < wh) *reinterpret_cast<uint32_t*>(Ms + o) = 0u;   // strength map: 0 = not a corner
-                    const uint64_t m = __ballot(nibs[u] != 0u);
-                    if (nibs[u]) ent[ne + mbcnt(m)] = (uint32_t)o | (nibs[u] << 16);
-                    ne = uniform(ne + __popcll(m));
-                }
-                if (COEB_BAND_NOFLUSH) ne = 0;
-                if (ne > kBandEnt - 64 * kBandUnroll || r + kBandUnroll * kWaves >= wh) {
-                    BC_MARK(tf0);
-                    wave_sync_lds();
-                    for (int e0 = 0; e0 < ne; e0 += 64) {
-                        const int e = e0 + lane;
-                        const uint32_t en = e < ne ? ent[e] : 0u;
-                        const int o = (int)(en & 0xFFFFu);
-                        // survivors of these 64 groups, bit-plane major (order is irrelevant here)
-                        int tot = 0;
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            const uint64_t m = __ballot((en >> (16 + q)) & 1u);
-                            if ((en >> (16 + q)) & 1u) px[tot + mbcnt(m)] = (uint16_t)(o + q);
-                            tot += __popcll(m);
-                        }
-                        wave_sync_lds();
-                        // two survivors per lane per step: both strengths' LDS reads in flight together
-                        for (int p0 = 0; p0 < tot; p0 += 128) {
-                            const int pa = p0 + lane, pb = p0 + 64 + lane;
-                            const int oa = px[min(pa, tot - 1)], ob = px[min(pb, tot - 1)];
-                            const int Ma = corner_strength(img + oa, kBandPitch);
-                            const int Mb = corner_strength(img + ob, kBandPitch);
-                            const bool ca = pa < tot && Ma > th_min, cb = pb < tot && Mb > th_min;
-                            if (ca) Ms[oa] = (uint8_t)Ma;
-                            if (cb) Ms[ob] = (uint8_t)Mb;
-                            const uint64_t ma = __ballot(ca), mb = __ballot(cb);
-                            const int qa = nc + mbcnt(ma), qb = nc + __popcll(ma) + mbcnt(mb);
-                            if (ca && qa < kBandCornW) cl[qa] = (uint32_t)oa;
-                            if (cb && qb < kBandCornW) cl[qb] = (uint32_t)ob;
-                            nc = uniform(nc + __popcll(ma) + __popcll(mb));
-                        }
-                        wave_sync_lds();
-                    }
-                    ne = 0;
-                    BC_ADD(5, tf0);
-                }
-            }
-        }
-        if (lane == 0) wcnt[wv] = nc > kBandCornW ? -1 : nc;
-        BC_ADD(6, tc1);
-        lds_barrier();
-        BC_ADD(1, tc1);
-        BC_MARK(tc2);
-
-        // ---- 3. NMS at both thresholds; per-cell choice of threshold; keep bitmap
-        int n4[kWaves];
-        bool overflow = false;
-#pragma unroll
-        for (int w = 0; w < kWaves; w++) {
-            n4[w] = wcnt[w];
-            overflow = overflow || n4[w] < 0;
-        }
-        if (COEB_BAND_STOP > 2) {
-            if (!overflow) {
-                // the four wave lists as one index space; two corners per thread per step
-                const int n01 = n4[0] + n4[1], n012 = n01 + n4[2], ntot = n012 + n4[3];
-                auto entry = [&](int i) -> uint32_t* {
-                    const int w = (i >= n4[0]) + (i >= n01) + (i >= n012);
-                    const int base = w == 0 ? 0 : w == 1 ? n4[0] : w == 2 ? n01 : n012;
-                    return &corn[w][i - base];
-                };
-                for (int i0 = tid; i0 < ntot; i0 += 2 * kThreads) {
-                    const int i1 = i0 + kThreads;
-                    uint32_t* ea = entry(i0);
-                    uint32_t* eb = entry(min(i1, ntot - 1));
-                    const uint32_t oa = *ea, ob = *eb;
-                    const int ca = (int)(oa % kBandPitch), cb = (int)(ob % kBandPitch);
-                    const int cca = C.cell(ca), ccb = C.cell(cb);
-                    const int ka = band_nms(Ms, (int)oa, ca > C.start(cca), ca + 1 < C.end(cca), th_ini, th_min);
-                    const int kb = band_nms(Ms, (int)ob, cb > C.start(ccb), cb + 1 < C.end(ccb), th_ini, th_min);
-                    *ea = oa | ((uint32_t)ka << 16) | ((uint32_t)cca << 20);
-                    if (i1 < ntot) *eb = ob | ((uint32_t)kb << 16) | ((uint32_t)ccb << 20);
-                    const int bits = ((ka & 1) ? 1 << cca : 0) | ((i1 < ntot && (kb & 1)) ? 1 << ccb : 0);
-                    if (bits) atomicOr(&cellmask, bits);
-                }
-            } else {
-                // more corners than the lists hold: walk the window (the image bytes are free now
-                // and take the NMS results)
-                const int ww = C.we - C.ws, npx = wh * ww;
-                const float inv = 1.0f / (float)ww;
-                for (int i = tid; i < npx; i += kThreads) {
-                    const int r = div_small(i, inv), col = C.ws + i - r * ww;
-                    const int o = (r + 3) * kBandPitch + col;
-                    if (Ms[o] > th_min) {
-                        const int cc = C.cell(col);
-                        const int k = band_nms(Ms, o, col > C.start(cc), col + 1 < C.end(cc), th_ini, th_min);
-                        img[o] = (uint8_t)k;
-                        if (k & 1) atomicOr(&cellmask, 1 << cc);
-                    }
-                }
-            }
-        }
-        lds_barrier();
-        BC_ADD(2, tc2);
-        BC_MARK(tc3);
-        const int cm = cellmask;
-        if (COEB_BAND_STOP > 2) {
-            if (!overflow) {
-#pragma unroll
-                for (int w = 0; w < kWaves; w++)
-                    for (int e = tid; e < n4[w]; e += kThreads) {
-                        const uint32_t en = corn[w][e];
-                        const int oo = (int)(en & 0xFFFFu);
-                        const int k = (int)((en >> 16) & 3u), cc = (int)(en >> 20);
-                        if (((cm >> cc) & 1) ? (k & 1) : (k & 2)) {
-                            const int row = oo / kBandPitch, col = oo - row * kBandPitch;
-                            atomicOr(&keep[row * kBandKW + (col >> 5)], 1u << (col & 31));
-                        }
-                    }
-            } else {
-                const int ww = C.we - C.ws, npx = wh * ww;
-                const float inv = 1.0f / (float)ww;
-                for (int i = tid; i < npx; i += kThreads) {
-                    const int r = div_small(i, inv), col = C.ws + i - r * ww;
-                    const int o = (r + 3) * kBandPitch + col;
-                    if (Ms[o] > th_min) {
-                        const int k = img[o];
-                        if (((cm >> C.cell(col)) & 1) ? (k & 1) : (k & 2))
-                            atomicOr(&keep[(r + 3) * kBandKW + (col >> 5)], 1u << (col & 31));
-                    }
-                }
-            }
-        }
-        lds_barrier();
-        BC_ADD(3, tc3);
-        BC_MARK(tc4);
-
-        // ---- 4. ordered output, one wave per cell, lane = window row
-        for (int k = wv; k < S.ncell; k += kWaves) {
-            const int cs = C.start(k), ce = C.end(k);
-            const int row = lane + 3;
-            uint64_t bits = 0;
-            if (lane < wh && COEB_BAND_STOP > 3) {
-                const uint32_t* kr = keep + row * kBandKW;
-                const int w0 = cs >> 5, sh = cs & 31;
-                const uint32_t a = kr[w0], bb = w0 + 1 < kBandKW ? kr[w0 + 1] : 0u, c2 = w0 + 2 < kBandKW ? kr[w0 + 2] : 0u;
-                const uint64_t lo64 = ((uint64_t)bb << 32) | a;
-                bits = (lo64 >> sh) | (sh ? ((uint64_t)c2 << (64 - sh)) : 0ull);
-                const int wd = ce - cs;
-                if (wd < 64) bits &= (1ull << wd) - 1ull;
-            }
-            int total;
-            int q = wave_prefix_small<7>(__popcll(bits), &total);
-            const int cidx = S.cell + k;
-            uint32_t* out = b.cand + ((int64_t)f * P->ncells + cidx) * P->cell_cap;
-            while (bits) {
-                const int col = cs + __builtin_ctzll(bits);
-                bits &= bits - 1;
-                const int sc = Ms[row * kBandPitch + col] - 1;
-                // keys are relative to minBorder = EDGE_THRESHOLD - 3 (:840-842)
-                if (q < P->cell_cap) out[q] = pack_key(S.xs + col - (EDGE_THRESHOLD_DEV - 3), S.y0 + row - (EDGE_THRESHOLD_DEV - 3), sc);
-                else atomicOr(b.err, 2);
-                q++;
-            }
-            if (lane == 0) b.cand_n[(int64_t)f * P->ncells + cidx] = min(total, P->cell_cap);
-        }
-        BC_ADD(4, tc4);
-    }
 }
 
 // ================================ k_octree ================================
@@ -2366,9 +1901,8 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
 
 }  // namespace
 
-// Phase clocks of k_fast_band (COEB_BAND_CLOCK builds): [0] stage, [1] pre-test + strengths +
-// barrier, [2] NMS, [3] keep, [4] output, [5] wave 0's flushes, [6] wave 0's phase 2 before
-// the barrier; read and cleared.
+// Per-cell phase clocks of k_fast (COEB_FAST_CLOCK builds), summed over the 256 slot copies;
+// read and cleared.
 int fast_timing_read(unsigned long long* out)
 {
     static unsigned long long h[256 * 8];
@@ -2385,13 +1919,6 @@ int fast_timing_read(unsigned long long* out)
 int oct_timing_read(long long* out)
 {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oct_clk), sizeof(long long) * 4096 * 6) == hipSuccess ? 0 : -1;
-}
-
-int band_timing_read(unsigned long long* out)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_band_clk), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_band_clk), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 
 int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, int F, hipStream_t s,
@@ -2427,25 +1954,16 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         hipLaunchKernelGGL(k_blur, dim3((i1 - i0 + kWaves - 1) / kWaves, F), dim3(kThreads), 0, st, d_plan, b, w);
         prof_end(prof, st);
     };
-    // FAST over levels [l0, l1): one wave per cell (k_fast), or band segments (k_fast_band,
-    // COEB_FAST_BAND=1): the band form fetches each image row once instead of once per cell ROI
-    // but measured slower (0.374 vs 0.317 ms per 257-frame launch)
-    const char* fb = getenv("COEB_FAST_BAND");        // read per launch: tests switch it in-process
-    const bool per_cell = !(fb && fb[0] == '1');
+    // FAST over levels [l0, l1): one wave per cell.  A band form (one LDS copy per cell-row
+    // segment, each image row fetched once) measured slower and was removed.
     auto fast = [&](hipStream_t st, int l0, int l1) {
         l1 = std::min(l1, plan.L);
         if (l1 <= l0) return;
         prof_begin(prof, "k_fast", st);
-        if (per_cell || plan.nsegs == 0) {
-            const int c0 = plan.lv[l0].cell0, c1 = l1 < plan.L ? plan.lv[l1].cell0 : plan.ncells;
-            hipLaunchKernelGGL(fast_rbytes == kFastRowBytesM ? k_fast<kFastRowBytesM> : k_fast<kFastRowBytes>,
-                               dim3((c1 - c0 + kFastPerBlock - 1) / kFastPerBlock, F), dim3(kThreads), fast_lds,
-                               st, d_plan, b, b.cells, c0, c1);
-        } else {
-            const int s0 = plan.lv[l0].seg0, s1 = l1 < plan.L ? plan.lv[l1].seg0 : plan.nsegs;
-            static const int per = [] { const char* e = getenv("COEB_BAND_PER_BLOCK"); return e ? std::max(1, atoi(e)) : 1; }();
-            hipLaunchKernelGGL(k_fast_band, dim3((s1 - s0 + per - 1) / per, F), dim3(kThreads), 0, st, d_plan, b, s0, s1, per);
-        }
+        const int c0 = plan.lv[l0].cell0, c1 = l1 < plan.L ? plan.lv[l1].cell0 : plan.ncells;
+        hipLaunchKernelGGL(fast_rbytes == kFastRowBytesM ? k_fast<kFastRowBytesM> : k_fast<kFastRowBytes>,
+                           dim3((c1 - c0 + kFastPerBlock - 1) / kFastPerBlock, F), dim3(kThreads), fast_lds,
+                           st, d_plan, b, b.cells, c0, c1);
         prof_end(prof, st);
     };
     // level 0 (the input frame itself) needs no pyramid: with a side stream its blur and FAST

@@ -34,6 +34,9 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <array>
+#include <map>
+#include <mutex>
 
 #include "../../include/coeb_front.h"
 #include "coeb_internal.hpp"
@@ -41,6 +44,7 @@
 extern "C" int coeb_internal_stream(coeb_ctx* c, hipStream_t* s, int* device);
 extern "C" int coeb_internal_scratch(coeb_ctx* c, const char* name, size_t bytes, void** p);
 extern "C" int coeb_internal_error(coeb_ctx* c, int code, const char* msg);
+extern "C" ProfileHook* coeb_internal_prof(coeb_ctx* c);
 
 namespace {
 
@@ -1417,7 +1421,16 @@ struct FlowDev {
     // pz * z bytes further on
     int npairs;
     int64_t pz;
+    ProfileHook* prof = nullptr;        // the context's HIP-event profiler (coeb_profile_enable)
 };
+
+// one launch bracketed by the context profiler's event pair (a no-op unless profiling is on)
+#define FLOW_LAUNCH(d, name, s, ...)                 \
+    do {                                             \
+        prof_begin((d)->prof, name, s);              \
+        hipLaunchKernelGGL(__VA_ARGS__);             \
+        prof_end((d)->prof, s);                      \
+    } while (0)
 
 int lk_levels(int w, int h, int win, int max_level)
 {
@@ -1471,6 +1484,7 @@ int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
     d->tm = (float*)take(); d->ntm = (int*)take(); d->F = (double*)take(); d->nf = (int*)take();
     d->npairs = npairs;
     d->pz = (int64_t)pair_bytes;
+    d->prof = coeb_internal_prof(c);
     return COEB_OK;
 }
 
@@ -1492,12 +1506,12 @@ int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, in
     (void)hipMemset2DAsync(d->rmax, (size_t)d->pz, 0, 4, P, s);      // one word per pair
     (void)hipMemset2DAsync(d->nkeys, (size_t)d->pz, 0, 4, P, s);
     const dim3 grid((w + 15) / 16, (h + 15) / 16, P);
-    hipLaunchKernelGGL(k_gf_response, dim3((w + kGfT - 1) / kGfT, (h + kGfT - 1) / kGfT, P), dim3(256), 0, s, img, w, h,
+    FLOW_LAUNCH(d, "k_gf_response", s, k_gf_response, dim3((w + kGfT - 1) / kGfT, (h + kGfT - 1) / kGfT, P), dim3(256), 0, s, img, w, h,
                        stride, k, d->R, d->rmax, iz, d->pz);
-    hipLaunchKernelGGL(k_gf_candidates, grid, dim3(256), 0, s, d->R, w, h, quality, d->rmax, d->keys, d->nkeys,
+    FLOW_LAUNCH(d, "k_gf_candidates", s, k_gf_candidates, grid, dim3(256), 0, s, d->R, w, h, quality, d->rmax, d->keys, d->nkeys,
                        gf_key_cap(w, h), d->pz);
     (void)hipFuncSetAttribute((const void*)k_gf_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_gf_select, dim3(1, 1, P), dim3(kGfThreads), lds, s, d->keys, d->nkeys, w, h, max_corners,
+    FLOW_LAUNCH(d, "k_gf_select", s, k_gf_select, dim3(1, 1, P), dim3(kGfThreads), lds, s, d->keys, d->nkeys, w, h, max_corners,
                        (float)(min_distance * min_distance), cell, d->cells, d->pts, d->npts, kMaxPts, gf_key_cap(w, h),
                        d->pz);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1526,7 +1540,7 @@ int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride
         if (!g_subpix_count) (void)hipGetSymbolAddress((void**)&g_subpix_count, HIP_SYMBOL(g_subpix_count_dev));
         itc = g_subpix_count;
     }
-    hipLaunchKernelGGL((k_subpix<10, 1>), dim3(kMaxPts, 1, d->npairs), dim3(64), 0, s, img, w, h, stride, d->pts,
+    FLOW_LAUNCH(d, "k_subpix", s, (k_subpix<10, 1>), dim3(kMaxPts, 1, d->npairs), dim3(64), 0, s, img, w, h, stride, d->pts,
                        d->npts, kMaxPts, d->mask, iters, e * e, iz, d->pz, itc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -1560,11 +1574,11 @@ int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, 
         a.sw = pyr.w[l - 1]; a.sh = pyr.h[l - 1]; a.spitch = pyr.pitch[l - 1]; a.dw = pyr.w[l]; a.dh = pyr.h[l];
         a.src_img = l == 1;
         a.nfr = chained ? 1 : 2;
-        hipLaunchKernelGGL(k_pyr_down, dim3((a.dw + 63) / 64, (a.dh + 3) / 4, chained ? P + 1 : 2 * P), dim3(256), 0, s, a,
+        FLOW_LAUNCH(d, "k_pyr_down", s, k_pyr_down, dim3((a.dw + 63) / 64, (a.dh + 3) / 4, chained ? P + 1 : 2 * P), dim3(256), 0, s, a,
                            iz, d->pz);
     }
-    hipLaunchKernelGGL(k_sharr, dim3(64, L, P), dim3(256), 0, s, pyr, iz, d->pz);
-    hipLaunchKernelGGL(k_lk, dim3((kMaxPts + 3) / 4, 1, P), dim3(256), 0, s, pyr, d->pts, d->npts, kMaxPts, d->nxt,
+    FLOW_LAUNCH(d, "k_sharr", s, k_sharr, dim3(64, L, P), dim3(256), 0, s, pyr, iz, d->pz);
+    FLOW_LAUNCH(d, "k_lk", s, k_lk, dim3((kMaxPts + 3) / 4, 1, P), dim3(256), 0, s, pyr, d->pts, d->npts, kMaxPts, d->nxt,
                        d->status, win, max_count, eps * eps, iz, d->pz);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -1574,7 +1588,7 @@ int launch_fm(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, 
 {
     FmOut o;
     o.tm = d->tm; o.ntm = d->ntm; o.state = d->state; o.F = d->F; o.nf = d->nf; o.tm_cap = tm_cap; o.tm_z = 0;
-    hipLaunchKernelGGL(k_fm, dim3(1, 1, d->npairs), dim3(kFmThreads), 0, s, prev, cur, w, h, stride, d->pts, d->nxt,
+    FLOW_LAUNCH(d, "k_fm", s, k_fm, dim3(1, 1, d->npairs), dim3(kFmThreads), 0, s, prev, cur, w, h, stride, d->pts, d->nxt,
                        d->status, d->npts, kMaxPts, edge, limit, 0.1, 0.99,
                        tm_out ? FmOut{tm_out, ntm_out, o.state, o.F, o.nf, tm_cap, (int64_t)tm_cap * 8} : o, iz, d->pz);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1765,6 +1779,42 @@ extern "C" int coeb_internal_subpix_count(int* out)
     return hipMemcpyToSymbol(HIP_SYMBOL(g_subpix_count_dev), z, 8) == hipSuccess ? COEB_OK : COEB_EDEVICE;
 }
 
+// geometry of each context's last moving-object batch, for coeb_internal_flow_counts
+static std::mutex g_pmo_mu;
+static std::map<const coeb_ctx*, std::array<int, 3>> g_pmo_last;
+
+extern "C" void coeb_internal_flow_forget(const coeb_ctx* c)   // coeb_destroy
+{
+    std::lock_guard<std::mutex> lk(g_pmo_mu);
+    g_pmo_last.erase(c);
+}
+
+// Per pair of the context's last moving-object batch: {Harris candidate keys, corners} (bench.py's
+// algorithmic bytes of k_gf_select / k_subpix / k_lk / k_fm).  Synchronises the context stream.
+extern "C" int coeb_internal_flow_counts(coeb_ctx* c, int* out, int cap, int* npairs)
+{
+    std::array<int, 3> g;
+    {
+        std::lock_guard<std::mutex> lk(g_pmo_mu);
+        auto it = g_pmo_last.find(c);
+        if (it == g_pmo_last.end()) return COEB_EINVAL;
+        g = it->second;
+    }
+    FlowCall fc;
+    int dev;
+    if (coeb_internal_stream(c, &fc.s, &dev)) return COEB_EINVAL;
+    (void)hipSetDevice(dev);
+    int rc = flow_alloc(c, g[0], g[1], &fc.d, g[2]);
+    if (rc) return rc;
+    *npairs = g[2];
+    FL_TRY(c, hipStreamSynchronize(fc.s));
+    for (int z = 0; z < g[2] && 2 * z + 1 < cap; z++) {
+        FL_TRY(c, hipMemcpy(out + 2 * z, (const uint8_t*)fc.d.nkeys + (size_t)z * fc.d.pz, 4, hipMemcpyDeviceToHost));
+        FL_TRY(c, hipMemcpy(out + 2 * z + 1, (const uint8_t*)fc.d.npts + (size_t)z * fc.d.pz, 4, hipMemcpyDeviceToHost));
+    }
+    return COEB_OK;
+}
+
 extern "C" int coeb_internal_pmo_batch(coeb_ctx* c, const uint8_t* d_gray, int F, int w, int h, float* tm_out,
                                        int* ntm_out, int tm_cap)
 {
@@ -1780,6 +1830,10 @@ extern "C" int coeb_internal_pmo_batch(coeb_ctx* c, const uint8_t* d_gray, int F
         return coeb_internal_error(c, COEB_EINVAL, "moving-object batch: frame size");
     int rc = flow_alloc(c, w, h, &fc.d, F - 1);
     if (rc) return rc;
+    {
+        std::lock_guard<std::mutex> lk(g_pmo_mu);
+        g_pmo_last[c] = {w, h, F - 1};
+    }
     float mask[21 * 21];
     subpix_mask(10, mask);
     FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));

@@ -179,6 +179,7 @@ __global__ __launch_bounds__(256) void k_undistort(const KpRec* __restrict__ in,
 extern "C" int coeb_internal_stream(coeb_ctx* c, hipStream_t* s, int* device);
 extern "C" int coeb_internal_scratch(coeb_ctx* c, const char* name, size_t bytes, void** p);
 extern "C" int coeb_internal_error(coeb_ctx* c, int code, const char* msg);
+extern "C" ProfileHook* coeb_internal_prof(coeb_ctx* c);
 
 #define FR_TRY(c, expr)                                                                         \
     do {                                                                                        \
@@ -186,14 +187,28 @@ extern "C" int coeb_internal_error(coeb_ctx* c, int code, const char* msg);
         if (_e != hipSuccess) return coeb_internal_error((c), COEB_EDEVICE, hipGetErrorString(_e)); \
     } while (0)
 
-// The blur flags of every box of a device-resident batch (packed W x H frames): d_box_frame[bi]
-// = frame of box bi; frame 0's boxes get 0.  Enqueued on stream s.
-extern "C" int coeb_internal_blur_flags_batch(const uint8_t* d_gray, int W, int H, const float* d_boxes,
-                                              const int* d_box_frame, int nbox, int* d_out, hipStream_t s)
+// box -> frame map of a batch from its box offsets (frame f owns boxes [box_off[f], box_off[f+1]))
+__global__ __launch_bounds__(256) void k_box_frame(const int* __restrict__ box_off, int F, int* __restrict__ box_frame)
+{
+    const int f = blockIdx.x * 256 + threadIdx.x;
+    if (f >= F) return;
+    for (int i = box_off[f]; i < box_off[f + 1]; i++) box_frame[i] = f;
+}
+
+// The blur flags of every box of a device-resident batch (packed W x H frames): frame f's boxes
+// are [d_box_off[f], d_box_off[f+1]) of d_boxes (device arrays); d_box_frame is scratch for nbox
+// ints; frame 0's boxes get 0.  Enqueued on stream s, nothing staged from the host.
+extern "C" int coeb_internal_blur_flags_batch(coeb_ctx* c, const uint8_t* d_gray, int W, int H, const float* d_boxes,
+                                              const int* d_box_off, int F, int* d_box_frame, int nbox, int* d_out,
+                                              hipStream_t s)
 {
     if (nbox <= 0) return COEB_OK;
+    hipLaunchKernelGGL(k_box_frame, dim3((F + 255) / 256), dim3(256), 0, s, d_box_off, F, d_box_frame);
+    ProfileHook* prof = coeb_internal_prof(c);
+    prof_begin(prof, "k_blur_flags", s);
     hipLaunchKernelGGL(k_blur_flags, dim3(nbox), dim3(256), 0, s, d_gray, W, H, W, d_boxes, d_out, (double*)nullptr,
-                       d_box_frame, (int64_t)W * H);
+                       (const int*)d_box_frame, (int64_t)W * H);
+    prof_end(prof, s);
     return hipGetLastError() == hipSuccess ? COEB_OK : COEB_EDEVICE;
 }
 
@@ -282,8 +297,11 @@ extern "C" int coeb_rgbd_preprocess_batch_device(coeb_ctx* c, const uint8_t* d_i
     (void)hipSetDevice(dev);
     const int dcopy = depth_type == COEB_DEPTH_F32 && !(fabsf(depth_scale - 1.0f) > 1e-5f);   // Tracking.cc:227
     const int64_t npix = (int64_t)W * H;
+    ProfileHook* prof = coeb_internal_prof(c);
+    prof_begin(prof, "k_rgbd_batch", s);
     hipLaunchKernelGGL(k_rgbd_batch, dim3((unsigned)((npix / 4 + 255) / 256), F), dim3(256), 0, s, d_img, channels,
                        rgb_order, (const uint8_t*)d_depth, depth_type, depth_scale, dcopy, npix, d_gray, d_depth_out);
+    prof_end(prof, s);
     FR_TRY(c, hipGetLastError());
     return COEB_OK;
 }

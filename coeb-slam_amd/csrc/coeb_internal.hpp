@@ -46,7 +46,6 @@ struct LevelGeom {
     float scale;           // mvScaleFactor[l]
     int size_i;            // (int)(PATCH_SIZE * scale)
     int maxX, maxY;        // octree box: maxBorderX - minBorderX, maxBorderY - minBorderY
-    int seg0, nseg;        // k_fast band segments of this level (range in the segment table)
 };
 
 struct Plan {
@@ -66,8 +65,6 @@ struct Plan {
     int oct_w;             // k_octree: node records per set / work-list entries (max ncap)
     int oct_kl;            // k_octree: keys kept in LDS when a level has <= oct_kl candidates
     int oct_lds;           // k_octree dynamic LDS bytes
-    int nsegs;             // k_fast band segments (all levels)
-    int band_pw;           // k_fast: widest segment's LDS row in dwords
 };
 
 // FAST cell descriptor (ORBextractor.cc:811-829): ROI in level coordinates
@@ -76,17 +73,6 @@ struct CellDesc {
     int16_t x0, y0;        // iniX, iniY
     int16_t rw, rh;        // maxX-iniX, maxY-iniY (ROI; detection window = inset 3)
     int16_t i, j;          // cell row / column (for x_rel/y_rel offsets)
-};
-
-// k_fast band segment: cells [cell, cell + ncell) of one cell row of one level (consecutive in
-// the cell table, same y0 / rh), detected together from one LDS copy of their rows.  The LDS row
-// holds image columns [xs, xs + 4*pw) (xs 16-aligned); the cells' detection windows tile the
-// image columns [ws, we) and the rows [y0 + 3, y0 + rh - 3).
-struct FastSeg {
-    int16_t level, ncell;
-    int16_t cell, y0;
-    int16_t xs, pw;
-    int16_t ws, we;
 };
 
 // Dynamic-object mask of one frame (ORBextractor.cc:1101-1195): the mask is the complement of
@@ -114,16 +100,9 @@ static inline __host__ __device__ int key_x(uint32_t k) { return (int)(k & 0xFFF
 static inline __host__ __device__ int key_y(uint32_t k) { return (int)((k >> 12) & 0xFFFu); }
 static inline __host__ __device__ int key_s(uint32_t k) { return (int)(k >> 24); }
 
-// k_fast band kernel (coeb_extract.hip): segment limits the host guarantees (make_segments)
-constexpr int kBandPW = 68;              // LDS row dwords: window dwords + the pre-test's one either side
-constexpr int kBandRows = 44;            // rows per segment (ROI height; hcell + 6, hcell < 40 from 3 cell rows up)
-constexpr int kBandCornW = 256;          // corners per wave list before the whole-window fallback
-constexpr int kBandCells = 16;           // cells per segment
-
 // ---- launch wrappers (coeb_extract.hip / coeb_match.hip) ----
-int band_timing_read(unsigned long long* out);
 int oct_timing_read(long long* out);   // COEB_OCT_CLOCK builds: [4096][6] per-workgroup k_octree clocks
-int fast_timing_read(unsigned long long* out);   // COEB_FAST_CLOCK builds: per-cell k_fast phase sums   // k_fast_band phase clocks (diagnostic builds)
+int fast_timing_read(unsigned long long* out);   // COEB_FAST_CLOCK builds: per-cell k_fast phase sums
 struct ExtractBufs {
     const uint8_t* gray;   // [F][H][W]
     uint8_t* pyr;
@@ -140,7 +119,6 @@ struct ExtractBufs {
     DynMask* dyn;
     const int* rtab;
     const CellDesc* cells;
-    const FastSeg* segs;   // k_fast band segments
     const int8_t* pattern; // 512 x (x, y)
     // dynamic-mask inputs
     const float* boxes;    // [nbox_total][4]

@@ -98,9 +98,6 @@ constexpr int kIdxBits = 12;
 #define COEB_MATCH_QL 8
 #endif
 constexpr int kQL = COEB_MATCH_QL;
-#ifndef COEB_MATCH_FLAT
-#define COEB_MATCH_FLAT 1      // 0: k_match walks a query's window one grid column at a time
-#endif
 
 // Up to kQL window columns, one per lane of a kQL-lane group (lane j: CSR range [lo_j, lo_j +
 // len_j)), as one concatenated range in column-major order: its length, and the CSR index of
@@ -633,7 +630,6 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
                     qd[4] = qi.d1.x; qd[5] = qi.d1.y; qd[6] = qi.d1.z; qd[7] = qi.d1.w;
                     cnt = 0;
                     uint32_t* lst = lists + (int64_t)q * kCQ;
-#if COEB_MATCH_FLAT
                     // the window's columns kQL at a time: lane gl holds column gx + gl's CSR range, a
                     // group scan gives each column's offset in the concatenated (column-major) order,
                     // and the group walks that concatenation kQL candidates at a time -- one pass per
@@ -649,13 +645,6 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
                             const int fi = base + gl;
                             const int e = gc.index(fi);
                             const int c1 = fi < gc.total ? e + 1 : e;      // e < c1 <=> fi < total
-#else
-                    for (int ix = w.x0; ix <= w.x1; ix++) {
-                        const int c0 = L.cell[ix * COEB_GRID_ROWS + w.y0];
-                        const int c1 = L.cell[ix * COEB_GRID_ROWS + w.y1 + 1];
-                        for (int base = c0; base < c1; base += kQL) {
-                            const int e = base + gl;
-#endif
                             bool ok = false;
                             uint32_t ent = 0;
                             if (e < c1) {
@@ -856,7 +845,6 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
                 qd[4] = d1.x; qd[5] = d1.y; qd[6] = d1.z; qd[7] = d1.w;
                 cnt = 0;
                 uint32_t* lst = b.lists + (int64_t)q * kCQ;
-#if COEB_MATCH_FLAT
                 for (int gx = w.x0; gx <= w.x1; gx += kQL) {        // column groups, as in k_match
                     int clo = 0, clen = 0;
                     if (gx + gl <= w.x1) {
@@ -868,13 +856,6 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
                         const int fi = base + gl;
                         const int e = gc.index(fi);
                         const int c1 = fi < gc.total ? e + 1 : e;
-#else
-                for (int ix = w.x0; ix <= w.x1; ix++) {
-                    const int c0 = L.cell[ix * COEB_GRID_ROWS + w.y0];
-                    const int c1 = L.cell[ix * COEB_GRID_ROWS + w.y1 + 1];
-                    for (int base = c0; base < c1; base += kQL) {
-                        const int e = base + gl;
-#endif
                         bool ok = false;
                         uint32_t ent = 0;
                         if (e < c1) {
@@ -1127,7 +1108,6 @@ __global__ __launch_bounds__(kMThreads) void k_match_kf(MatchCam cam, KfBufs b, 
                 qd[4] = d1.x; qd[5] = d1.y; qd[6] = d1.z; qd[7] = d1.w;
                 cnt = 0;
                 uint32_t* lst = b.lists + (int64_t)q * kCQ;
-#if COEB_MATCH_FLAT
                 for (int gx = w.x0; gx <= w.x1; gx += kQL) {        // column groups, as in k_match
                     int clo = 0, clen = 0;
                     if (gx + gl <= w.x1) {
@@ -1139,13 +1119,6 @@ __global__ __launch_bounds__(kMThreads) void k_match_kf(MatchCam cam, KfBufs b, 
                         const int fi = base + gl;
                         const int e = gc.index(fi);
                         const int c1 = fi < gc.total ? e + 1 : e;
-#else
-                for (int ix = w.x0; ix <= w.x1; ix++) {
-                    const int c0 = L.cell[ix * COEB_GRID_ROWS + w.y0];
-                    const int c1 = L.cell[ix * COEB_GRID_ROWS + w.y1 + 1];
-                    for (int base = c0; base < c1; base += kQL) {
-                        const int e = base + gl;
-#endif
                         bool ok = false;
                         uint32_t ent = 0;
                         if (e < c1) {

@@ -203,8 +203,13 @@ __global__ __launch_bounds__(kT) void k_tlm_pose_prep(TlmBufs t)
         if (threadIdx.x < 16) t.T2[(int64_t)f * 16 + threadIdx.x] = t.T1[(int64_t)f * 16 + threadIdx.x];
         if (threadIdx.x == 16) t.n2[f] = ok ? n : 0;
     }
-    if (!ok || i >= n) return;
+    if (i >= n) return;
     const int64_t o = f * K + i;
+    if (!ok) {          // TrackLocalMap does not run: no second optimisation, nothing is an outlier
+        t.has2[o] = 0;
+        t.outl2[o] = 0;
+        return;
+    }
     const int lm = t.lmatch[o];
     t.outl2[o] = 0;
     if (lm >= 0) {

@@ -66,6 +66,12 @@ extern "C" {
 #define COEB_ERANGE (-34)    /* an internal capacity was exceeded (see coeb_last_error) */
 #define COEB_ENODEV (-19)    /* no usable gfx950 device */
 
+/* ABI revision of this header.  Bumped whenever an entry point's signature or a struct layout
+ * changes (3: coeb_rgbd_preprocess gained channels/depth_type and a byte depth stride); the
+ * adapters compare it with coeb_abi_version() of the loaded library and refuse a mismatch. */
+#define COEB_ABI_VERSION 3
+int coeb_abi_version(void);
+
 #define COEB_MAX_LEVELS 16
 #define COEB_MAX_BOXES 16
 

@@ -63,3 +63,46 @@ def test_boxes_from_int64_host_only():
     import coeb_front
     b = np.array([[10, 20, 300, 400], [-5, 0, 2 ** 40, 7]], np.int64)
     assert np.array_equal(coeb_front.boxes_from_ros(b), b.astype(np.float32))
+
+
+def test_abi_version_matches_header(lib):
+    txt = open(os.path.join(ROOT, "include", "coeb_front.h")).read()
+    want = int(re.search(r"#define COEB_ABI_VERSION (\d+)", txt).group(1))
+    assert lib.coeb_abi_version() == want
+
+
+def test_last_error_is_per_thread(lib):
+    """coeb_last_error(NULL) is thread-local: ranks of `bench.py --gpus N` (one host thread per
+    device) fail concurrently without racing on one std::string.  Here every thread alternates two
+    coeb_create failures that need no GPU (bad arguments / no usable device) and must read back
+    exactly its own message each time."""
+    import threading
+
+    class Params(ctypes.Structure):
+        _fields_ = [("nfeatures", ctypes.c_int), ("scale_factor", ctypes.c_float), ("nlevels", ctypes.c_int),
+                    ("ini_th", ctypes.c_int), ("min_th", ctypes.c_int)]
+
+    lib.coeb_create.restype = ctypes.c_void_p
+    lib.coeb_create.argtypes = [ctypes.POINTER(Params), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.coeb_last_error.restype = ctypes.c_char_p
+    lib.coeb_last_error.argtypes = [ctypes.c_void_p]
+    prm = Params(1000, 1.2, 8, 20, 7)
+    if lib.coeb_create(ctypes.byref(prm), 0, 640, 480, 1):
+        pytest.skip("a usable device is present: the no-device failure cannot be provoked")
+    bad = []
+
+    def body(t):
+        for i in range(300):
+            invalid = (i + t) % 2 == 0
+            h = lib.coeb_create(ctypes.byref(prm), 0, 0 if invalid else 640, 480, 1)
+            assert not h
+            msg = lib.coeb_last_error(None).decode()
+            if invalid != ("invalid arguments" in msg):
+                bad.append((t, i, msg))
+
+    ths = [threading.Thread(target=body, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not bad, bad[:3]

@@ -67,30 +67,6 @@ def test_extract_B_1280x960(ctx, oracle_mod):
         c2.close()
 
 
-def test_fast_band_kernel_matches_oracle(ctx, ex, oracle_mod, monkeypatch):
-    """The band form of FAST (k_fast_band, COEB_FAST_BAND=1: one LDS copy per cell-row segment)
-    gives the same keypoints and descriptors as the per-cell kernel and the oracle, including a
-    size whose ROIs exceed its row limit (falls back to the per-cell kernel) and a noise image
-    (many corners per segment)."""
-    monkeypatch.setenv("COEB_FAST_BAND", "1")
-    for seed in (1000, 7):
-        run_both(ctx, ex, synth.make_frames(640, 480, 1, seed=seed)[0], tag="band %d" % seed)
-    rng = np.random.default_rng(3)
-    run_both(ctx, ex, rng.integers(0, 256, (480, 640), dtype=np.uint8), tag="band noise")
-    for w, h in ((320, 240), (641, 479), (1024, 768)):
-        run_both(ctx, ex, synth.make_frames(w, h, 1, seed=5)[0], tag="band %dx%d" % (w, h))
-    ex2 = oracle_mod.Extractor(2000, 1.2, 8, 20, 7)
-    from coeb_front import Context
-    c2 = Context(2000, 1.2, 8, 20, 7, 0, 1280, 960, 1)
-    try:
-        fr = synth.make_frames(1280, 960, 1, seed=11)[0]
-        k, d = c2.extract(fr)
-        r = ex2.extract(fr)
-        assert_same(k, d, r["kps"], r["desc"], "band B")
-    finally:
-        c2.close()
-
-
 def test_fast_general_slab_layout_matches_oracle(ctx, ex, monkeypatch):
     """k_fast keeps the ROI pixels and the corner strengths M in one 96-byte slab row when every
     ROI is at most 46 wide (the 640x480 plans) and in a 72-byte slab plus a compact M slab
@@ -124,6 +100,24 @@ def test_extract_params(oracle_mod, nfeat, scale, nlev):
         run_both(c2, ex2, fr[0], tag="params")
         b, t, bl = synth.dynamic_inputs(640, 480)
         run_both(c2, ex2, fr[0], b, t, bl, tag="params dyn")
+    finally:
+        c2.close()
+
+
+@pytest.mark.parametrize("scale,nlev", [(2.0, 5), (4.0, 3)])
+def test_extract_params_reference_ub_rejected(oracle_mod, scale, nlev):
+    """A pyramid level narrower than one 30-px FAST cell gives nCols = 0 and a division by zero
+    in the reference (ORBextractor.cc:806-808, UB): 640x480 at scale 2.0 / 5 levels has a 40x30
+    level 4.  The oracle refuses it (rc -1 from oc_extract) and the HIP path returns COEB_EINVAL
+    with a message instead of launching."""
+    from coeb_front import CoebError, Context
+    fr = synth.make_frames(640, 480, 1, seed=3)[0]
+    with pytest.raises(RuntimeError, match=r"oc_extract rc=-"):
+        oracle_mod.Extractor(1000, scale, nlev, 20, 7).extract(fr)
+    c2 = Context(1000, scale, nlev, 20, 7, max_width=640, max_height=480)
+    try:
+        with pytest.raises(CoebError, match=r"rc=-22: pyramid level too small"):
+            c2.extract(fr)
     finally:
         c2.close()
 

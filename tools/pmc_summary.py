@@ -62,8 +62,17 @@ def valu_json(merged, nd, frames, command, n_cu=256, n_xcd=8, rate=VALU_PER_CU_C
         if "SQ_INSTS_VALU" not in cv or not cv.get("GRBM_GUI_ACTIVE"):
             continue
         cycles = cv["GRBM_GUI_ACTIVE"] / n_xcd
-        out["kernels"][k] = dict(valu_insts=int(cv["SQ_INSTS_VALU"]), busy_cycles=int(cycles),
-                                 valu_issue_frac=round(cv["SQ_INSTS_VALU"] / (rate * n_cu * cycles), 4), dispatches=nd[k])
+        e = out["kernels"][k] = dict(valu_insts=int(cv["SQ_INSTS_VALU"]), busy_cycles=int(cycles),
+                                     valu_issue_frac=round(cv["SQ_INSTS_VALU"] / (rate * n_cu * cycles), 4),
+                                     dispatches=nd[k])
+        # stall fractions of the resident wave-cycles and LDS bank conflicts per LDS instruction
+        if cv.get("SQ_WAVE_CYCLES"):
+            for key, cnt in (("wait_inst_frac", "SQ_WAIT_INST_ANY"), ("wait_any_frac", "SQ_WAIT_ANY"),
+                             ("active_inst_frac", "SQ_ACTIVE_INST_ANY")):
+                if cnt in cv:
+                    e[key] = round(cv[cnt] / cv["SQ_WAVE_CYCLES"], 4)
+        if cv.get("SQ_INSTS_LDS") and "SQ_LDS_BANK_CONFLICT" in cv:
+            e["lds_conflict_per_lds_inst"] = round(cv["SQ_LDS_BANK_CONFLICT"] / cv["SQ_INSTS_LDS"], 3)
     return out
 
 
