@@ -54,7 +54,6 @@ int* g_subpix_count = nullptr;    // device address of g_subpix_count_dev (COEB_
 constexpr int kMaxPts = 1024;        // corners / tracked points per call (reference: 1000)
 constexpr int kGfThreads = 1024;
 constexpr int kGfSortMax = 16384;    // local maxima sorted in LDS (128 KB)
-constexpr int kGfCellCap = 64;       // an 8x8 cell holds at most 64 maxima
 // local-maximum keys kept per frame: a quarter of the pixels (a 3 x 3 maximum needs its
 // neighbours below it unless the response plateaus); more is reported as -1
 inline int gf_key_cap(int w, int h) { return std::max(kGfSortMax, w * h / 4); }
@@ -91,9 +90,66 @@ __device__ __forceinline__ int cv_floor(float v)
 // buffers by one byte offset; pair z's frames are the batch's frames z and z + 1, `iz` bytes
 // apart.  Single calls pass iz = pz = 0 and one z-slice.
 template <class T>
+__device__ __forceinline__ T* at_pair(T* p, int64_t stride, uint32_t z)
+{
+    return p ? reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(p) + (uint64_t)z * (uint64_t)stride) : p;
+}
+template <class T>
 __device__ __forceinline__ T* at_pair(T* p, int64_t stride)
 {
-    return p ? reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(p) + (uint64_t)blockIdx.z * (uint64_t)stride) : p;
+    return at_pair(p, stride, blockIdx.z);
+}
+
+// Per-point kernels of a batch (cornerSubPix, LK) run over one flattened work list instead of a
+// grid of kMaxPts slots per pair: offs[z] = points before pair z (k_flow_index), offs[P] = all.
+// A grid of P x 1024 one-wave slots of which ~150 per pair hold a point was bound by the rate
+// at which the dispatcher retires empty waves (262,144 waves in ~1.5 ms for both kernels).
+// item -> (pair, point) by a binary search over offs.
+__device__ __forceinline__ int2 flow_item(const int* __restrict__ offs, int P, int item)
+{
+    int lo = 0, hi = P;                        // offs[lo] <= item < offs[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (offs[mid] <= item) lo = mid;
+        else hi = mid;
+    }
+    return make_int2(lo, item - offs[lo]);
+}
+
+// offs[z] = sum over pairs < z of clamp(n_z, 0, nmax) (n_z at d_n + z * pz bytes), offs[P] = total
+__global__ __launch_bounds__(1024) void k_flow_index(const int* __restrict__ d_n, int64_t pz, int P, int nmax,
+                                                      int* __restrict__ offs)
+{
+    __shared__ int s_w[16];
+    __shared__ int s_base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_base = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < P; c0 += 1024) {
+        const int z = c0 + (int)threadIdx.x;
+        int v = 0;
+        if (z < P) {
+            v = *at_pair(d_n, pz, (uint32_t)z);
+            v = v < 0 ? 0 : v > nmax ? nmax : v;
+        }
+        int incl = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) s_w[wv] = incl;
+        __syncthreads();
+        int before = s_base, total = s_base;
+        for (int i = 0; i < 16; i++) {
+            before += i < wv ? s_w[i] : 0;
+            total += s_w[i];
+        }
+        if (z < P) offs[z] = before + incl - v;
+        __syncthreads();
+        if (threadIdx.x == 0) s_base = total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) offs[P] = s_base;
 }
 
 // ============================== goodFeaturesToTrack ==============================
@@ -227,22 +283,27 @@ __device__ int block_scan_1024(int flag, int* s_w, int& excl)
     return total;
 }
 
-// K[i] after the sort: low 32 bits pixel index; the selection reuses the high word as the state
-// (0 undecided, 1 accepted, 2 rejected).
+// Greedy minDistance selection (featureselect.cpp): candidates in sorted order (value desc,
+// address desc); a candidate is accepted unless an accepted corner in one of the 3 x 3 grid
+// cells around it lies closer than minDistance; stop at maxCorners.  The accepted corners are
+// kept as per-cell linked lists in LDS.  One wave walks the sorted list 64 candidates at a time:
+// each lane first tests its candidate against the corners accepted before the chunk, then
+// against the earlier candidates of the chunk (a 64-bit conflict mask), and a scalar pass over
+// the chunk's lanes resolves the in-chunk dependencies in order -- the sequential result.
+// (A block-wide Jacobi fixpoint over the whole list, round 2's form, needed one block pass per
+// link of the longest conflict chain: 0.5-0.7 ms per 256 pairs.)
+constexpr uint16_t kGfNone = 0xFFFF;
 __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __restrict__ keys, const int* __restrict__ nkeys,
                                                          int w, int h, int max_corners, float md2, int cell,
-                                                         uint16_t* __restrict__ cell_list, float* __restrict__ out_xy,
-                                                         int* __restrict__ nout, int cap, int key_cap, int64_t pz)
+                                                         float* __restrict__ out_xy, int* __restrict__ nout, int cap,
+                                                         int key_cap, int64_t pz)
 {
     keys = at_pair(keys, pz);
     nkeys = at_pair(nkeys, pz);
-    cell_list = at_pair(cell_list, pz);
     out_xy = at_pair(out_xy, pz);
     nout = at_pair(nout, pz);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t* K = reinterpret_cast<uint64_t*>(smem);
-    __shared__ int s_w[16];
-    __shared__ int s_changed, s_undecided;
     __shared__ uint32_t s_hist[256];
     __shared__ uint64_t s_prefix;
     __shared__ int s_need, s_cnt;
@@ -294,8 +355,10 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
         for (int i = tid; i < np; i += kGfThreads) K[i] = i < n ? keys[i] : 0ull;
     }
     const int gw = (w + cell - 1) / cell, gh = (h + cell - 1) / cell;
-    uint32_t* gcnt = reinterpret_cast<uint32_t*>(K + (np > 1 ? np : 2));
-    for (int g = tid; g < gw * gh; g += kGfThreads) gcnt[g] = 0;
+    uint16_t* head = reinterpret_cast<uint16_t*>(K + (np > 1 ? np : 2));     // [gw * gh] first accepted in the cell
+    uint16_t* next = head + ((gw * gh + 1) & ~1);                               // [kMaxPts] next accepted in its cell
+    uint32_t* axy = reinterpret_cast<uint32_t*>(next + kMaxPts);                // [kMaxPts] accepted x | y << 16
+    for (int g = tid; g < gw * gh; g += kGfThreads) head[g] = kGfNone;
     __syncthreads();
     for (int size = 2; size <= np; size <<= 1)
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -309,85 +372,72 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
             }
             __syncthreads();
         }
-    // cell lists of ranks (order inside a list is irrelevant: ranks are compared)
-    for (int i = tid; i < n; i += kGfThreads) {
-        const int idx = (int)(uint32_t)K[i];
+    if (tid >= 64) return;                         // the selection is one wave's
+    const int lane = tid;
+    const int limit = min(max_corners > 0 ? max_corners : kMaxPts, min(cap, kMaxPts));
+    int nacc = 0;
+    bool full = false;
+    for (int c0 = 0; c0 < n && !full; c0 += 64) {
+        const int i = c0 + lane;
+        const bool valid = i < n;
+        const int idx = valid ? (int)(uint32_t)K[i] : 0;
         const int y = idx / w, x = idx - y * w;
-        const int g = (y / cell) * gw + x / cell;
-        const uint32_t pos = atomicAdd(&gcnt[g], 1u);
-        if (pos < (uint32_t)kGfCellCap) cell_list[(size_t)g * kGfCellCap + pos] = (uint16_t)i;
-        K[i] = (uint64_t)(uint32_t)idx;
-    }
-    __syncthreads();
-    // fixpoint: accept when every earlier conflicting candidate is rejected, reject when one is
-    // accepted; the lowest undecided rank is decided in every round
-    for (;;) {
-        if (tid == 0) { s_changed = 0; s_undecided = 0; }
-        __syncthreads();
-        for (int i = tid; i < n; i += kGfThreads) {
-            const uint64_t ki = K[i];
-            if ((ki >> 32) != 0) continue;
-            const int idx = (int)(uint32_t)ki;
-            const int y = idx / w, x = idx - y * w;
-            const int xc = x / cell, yc = y / cell;
-            bool pending = false, hit = false;
+        const int xc = x / cell, yc = y / cell;
+        const float fx = (float)x, fy = (float)y;
+        bool hit = false;
+        if (valid) {
             for (int yy = max(yc - 1, 0); yy <= min(yc + 1, gh - 1) && !hit; yy++)
-                for (int xx = max(xc - 1, 0); xx <= min(xc + 1, gw - 1) && !hit; xx++) {
-                    const int g = yy * gw + xx;
-                    const int m = min((int)gcnt[g], kGfCellCap);
-                    for (int q = 0; q < m; q++) {
-                        const int j = cell_list[(size_t)g * kGfCellCap + q];
-                        if (j >= i) continue;
-                        const uint64_t kj = K[j];
-                        const uint32_t st = (uint32_t)(kj >> 32);
-                        if (st == 2) continue;
-                        const int jdx = (int)(uint32_t)kj;
-                        const int jy = jdx / w, jx = jdx - jy * w;
-                        const float ddx = (float)x - (float)jx, ddy = (float)y - (float)jy;
-                        if (!(ddx * ddx + ddy * ddy < md2)) continue;
-                        if (st == 1) { hit = true; break; }
-                        pending = true;
+                for (int xx = max(xc - 1, 0); xx <= min(xc + 1, gw - 1) && !hit; xx++)
+                    for (int a = head[yy * gw + xx]; a != kGfNone; a = next[a]) {
+                        const uint32_t q = axy[a];
+                        const float ddx = fx - (float)(int)(q & 0xFFFFu), ddy = fy - (float)(int)(q >> 16);
+                        if (ddx * ddx + ddy * ddy < md2) { hit = true; break; }
                     }
-                }
-            if (hit) { K[i] = ki | (2ull << 32); s_changed = 1; }
-            else if (!pending) { K[i] = ki | (1ull << 32); s_changed = 1; }
-            else s_undecided = 1;
         }
-        __syncthreads();
-        const bool again = s_changed && s_undecided;
-        const bool stuck = !s_changed && s_undecided;
-        __syncthreads();
-        if (stuck) {                   // cannot happen (see above); fail loudly rather than spin
-            if (tid == 0) *nout = -2;
-            return;
+        // earlier candidates of this chunk that would suppress this one once accepted
+        uint64_t conf = 0;
+        const int nc = min(64, n - c0);
+        for (int j = 0; j < nc; j++) {
+            const int xj = __builtin_amdgcn_readlane(x, j), yj = __builtin_amdgcn_readlane(y, j);
+            const int dxc = __builtin_amdgcn_readlane(xc, j) - xc, dyc = __builtin_amdgcn_readlane(yc, j) - yc;
+            const float ddx = fx - (float)xj, ddy = fy - (float)yj;
+            if (j < lane && dxc >= -1 && dxc <= 1 && dyc >= -1 && dyc <= 1 && ddx * ddx + ddy * ddy < md2)
+                conf |= 1ull << j;
         }
-        if (!again) break;
-    }
-    // accepted candidates in rank order, the first max_corners
-    int base = 0;
-    for (int c0 = 0; c0 < n; c0 += kGfThreads) {
-        const int i = c0 + tid;
-        const int acc = i < n && (uint32_t)(K[i] >> 32) == 1u;
-        int excl;
-        const int tot = block_scan_1024(acc, s_w, excl);
-        if (acc) {
-            const int pos = base + excl;
-            if ((max_corners <= 0 || pos < max_corners) && pos < cap) {
-                const int idx = (int)(uint32_t)K[i];
-                const int y = idx / w, x = idx - y * w;
-                out_xy[2 * pos] = (float)x;
-                out_xy[2 * pos + 1] = (float)y;
+        const uint64_t open = __ballot(valid && !hit);
+        const int g = yc * gw + xc;
+        uint64_t acc = 0;
+        const uint32_t conf_lo = (uint32_t)conf, conf_hi = (uint32_t)(conf >> 32);
+        // in order over the chunk (scalar loop): accept j unless an accepted earlier lane conflicts;
+        // lane 0 links each accepted corner into its cell's list
+        for (int j = 0; j < nc; j++) {
+            if (!((open >> j) & 1ull)) continue;
+            const uint64_t cj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)conf_hi, j) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)conf_lo, j);
+            if (cj & acc) continue;
+            const int r = nacc + __popcll(acc);
+            acc |= 1ull << j;
+            if (lane == 0) {
+                const int gj = __builtin_amdgcn_readlane(g, j);
+                next[r] = head[gj];
+                head[gj] = (uint16_t)r;
             }
+            if (r + 1 == limit) { full = true; break; }
         }
-        base += tot;
-        __syncthreads();
+        if ((acc >> lane) & 1ull) {
+            const int r = nacc + __popcll(acc & ((1ull << lane) - 1ull));
+            axy[r] = (uint32_t)x | ((uint32_t)y << 16);
+            out_xy[2 * r] = fx;
+            out_xy[2 * r + 1] = fy;
+        }
+        nacc += __popcll(acc);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");     // lists visible to the next chunk
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
-    if (tid == 0) {
-        int cnt = max_corners > 0 ? min(base, max_corners) : base;
-        bool overflow = false;
-        for (int g = 0; g < gw * gh; g++) overflow |= gcnt[g] > (uint32_t)kGfCellCap;
-        const bool inexact = truncated && (max_corners <= 0 || base < max_corners);
-        *nout = overflow ? -3 : inexact ? -1 : min(cnt, cap);
+    if (lane == 0) {
+        const bool inexact = truncated && (max_corners <= 0 || nacc < max_corners);
+        *nout = inexact ? -1 : nacc;
     }
 }
 
@@ -411,14 +461,11 @@ __device__ unsigned long long g_sp_clk[256 * 8];
 #define SP_ADD(slot, t0) do { if (COEB_SUBPIX_CLOCK && lane == 0) atomicAdd(&g_sp_clk[(blockIdx.x & 255) * 8 + (slot)], (unsigned long long)((long long)clock64() - (t0))); } while (0)
 
 template <int WIN, int CPB>
-__global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__ img, int w, int h, int stride,
-                                                      float* __restrict__ xy, const int* __restrict__ d_n, int nmax,
+__global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__ img0, int w, int h, int stride,
+                                                      float* __restrict__ xy0, const int* __restrict__ offs, int P,
                                                       const float* __restrict__ mask, int iters, double eps2, int64_t iz,
                                                       int64_t pz, int* __restrict__ itcount)
 {
-    img = at_pair(img, iz);
-    xy = at_pair(xy, pz);
-    d_n = at_pair(d_n, pz);
     constexpr int WW = 2 * WIN + 1, BW = WW + 2, NB = BW * BW, NK = WW * WW;
     constexpr int KPL = (NK + 63) / 64;                // terms per lane
     // Pixels around the corner staged once (the window may drift kSpM px before a refetch):
@@ -430,16 +477,22 @@ __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__
     __shared__ double s_tt[CPB][5][64];
     __shared__ uint8_t s_px[CPB][SS * SS];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int p = blockIdx.x * CPB + wv;
     float* buf = s_buf[wv];
     double (*s_t)[64] = s_tt[wv];
     uint8_t* px8 = s_px[wv];
-    int n = *d_n;
-    n = n < nmax ? n : nmax;
-    if (p >= n) return;
     double mreg[KPL];                                  // this lane's weights, k = lane + 64 q
 #pragma unroll
     for (int q = 0; q < KPL; q++) mreg[q] = lane + 64 * q < NK ? (double)mask[lane + 64 * q] : 0.0;
+    const int total = offs[P];
+    for (int item = blockIdx.x * CPB + wv; item < total; item += gridDim.x * CPB) {
+    const int2 zp = flow_item(offs, P, item);
+    const uint8_t* img = at_pair(img0, iz, (uint32_t)zp.x);
+    float* xy = at_pair(xy0, pz, (uint32_t)zp.x);
+    const int p = zp.y;
+    // the previous point's last reads of px8 / buf / s_t are done before they are rewritten
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const float tx = xy[2 * p], ty = xy[2 * p + 1];
     const int R0x = cv_floor(tx - (float)(BW - 1) * 0.5f) - kSpM, R0y = cv_floor(ty - (float)(BW - 1) * 0.5f) - kSpM;
     const bool staged = R0x >= 0 && R0y >= 0 && R0x + SS <= w && R0y + SS <= h;
@@ -576,6 +629,7 @@ __global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__
         if (itcount) { atomicAdd(itcount, it + 1); atomicAdd(itcount + 1, 1); }
     }
     SP_ADD(3, t_all);
+    }
 }
 
 // ============================== pyramidal Lucas-Kanade ==============================
@@ -667,20 +721,20 @@ __device__ __forceinline__ int64_t wave_sum_i32x(int v)
 __device__ __forceinline__ int refl1(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
 
 // one wave per point; every lane carries up to 8 window pixels (win*win <= 512)
-__global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__ pxy, const int* __restrict__ d_n, int nmax,
-                                            float* __restrict__ nxy, uint8_t* __restrict__ status, int win, int max_count,
+__global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__ pxy0, const int* __restrict__ offs, int P,
+                                            float* __restrict__ nxy0, uint8_t* __restrict__ status0, int win, int max_count,
                                             double eps2, int64_t iz, int64_t pz)
 {
-    pxy = at_pair(pxy, pz);
-    d_n = at_pair(d_n, pz);
-    nxy = at_pair(nxy, pz);
-    status = at_pair(status, pz);
     constexpr int PPL = 8;
     const int lane = threadIdx.x & 63;
-    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
-    int n = *d_n;
-    n = n < nmax ? n : nmax;
-    if (p >= n) return;
+    const int total = offs[P];
+    for (int item = blockIdx.x * 4 + (threadIdx.x >> 6); item < total; item += gridDim.x * 4) {
+    const int2 zp = flow_item(offs, P, item);
+    const uint32_t z = (uint32_t)zp.x;
+    const float* pxy = at_pair(pxy0, pz, z);
+    float* nxy = at_pair(nxy0, pz, z);
+    uint8_t* status = at_pair(status0, pz, z);
+    const int p = zp.y;
     const int npx = win * win;
     const float hw = (float)(win - 1) * 0.5f;
     const float FLT_SCALE = 1.f / (1 << 20);
@@ -699,9 +753,9 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
     }
     for (int level = pyr.L - 1; level >= 0; level--) {
         const int lw = pyr.w[level], lh = pyr.h[level], pitch = pyr.pitch[level];
-        const uint8_t* I = at_pair(pyr.P[level], level == 0 ? iz : pz);
-        const uint8_t* J = at_pair(pyr.N[level], level == 0 ? iz : pz);
-        const short2* D = at_pair(pyr.D[level], pz);
+        const uint8_t* I = at_pair(pyr.P[level], level == 0 ? iz : pz, z);
+        const uint8_t* J = at_pair(pyr.N[level], level == 0 ? iz : pz, z);
+        const short2* D = at_pair(pyr.D[level], pz, z);
         const float sc = (float)(1. / (1 << level));
         float px = px0 * sc, py = py0 * sc;
         if (level == pyr.L - 1) { nx = px; ny = py; }
@@ -814,6 +868,7 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
         nxy[2 * p] = nx;
         nxy[2 * p + 1] = ny;
         status[p] = (uint8_t)st;
+    }
     }
 }
 
@@ -1406,7 +1461,6 @@ struct FlowDev {
     uint32_t* rmax;
     int* nkeys;
     uint64_t* keys;
-    uint16_t* cells;
     float *pts, *nxt;
     int* npts;
     uint8_t *status, *state;
@@ -1421,6 +1475,7 @@ struct FlowDev {
     // pz * z bytes further on
     int npairs;
     int64_t pz;
+    int* offs;                          // k_flow_index: points before each pair, [npairs] = all
     ProfileHook* prof = nullptr;        // the context's HIP-event profiler (coeb_profile_enable)
 };
 
@@ -1445,7 +1500,6 @@ size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
 {
-    const int gw = (w + 7) / 8, gh = (h + 7) / 8;
     size_t pyr_bytes = 0, der_px = 0;
     {
         int lw = w, lh = h;
@@ -1458,9 +1512,10 @@ int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
     }
     // shared: the two frame copies of the host entry points, the subpix weights; then one block
     // per pair
-    const size_t shared[] = {align256((size_t)w * h), align256((size_t)w * h), align256(sizeof(float) * 23 * 23)};
+    const size_t shared[] = {align256((size_t)w * h), align256((size_t)w * h), align256(sizeof(float) * 23 * 23),
+                             align256(sizeof(int) * ((size_t)npairs + 1))};
     const size_t sizes[] = {align256((size_t)w * h * 4), 256, 256, align256((size_t)gf_key_cap(w, h) * 8),
-                            align256((size_t)gw * gh * kGfCellCap * 2), align256((size_t)kMaxPts * 8),
+                            align256((size_t)kMaxPts * 8),
                             align256((size_t)kMaxPts * 8), 256, align256(kMaxPts), align256(kMaxPts), align256(pyr_bytes),
                             align256(der_px * 4 + 64 * kLkMaxLevels), align256((size_t)kMaxPts * 8), 256, 256, 256};
     size_t pair_bytes = 0, shared_bytes = 0;
@@ -1476,10 +1531,11 @@ int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
     d->prev = p + o; o += shared[0];
     d->cur = p + o; o += shared[1];
     d->mask = (float*)(p + o); o += shared[2];
+    d->offs = (int*)(p + o); o += shared[3];
     int i = 0;
     auto take = [&]() { void* r = p + o; o += sizes[i++]; return r; };
     d->R = (float*)take(); d->rmax = (uint32_t*)take(); d->nkeys = (int*)take(); d->keys = (uint64_t*)take();
-    d->cells = (uint16_t*)take(); d->pts = (float*)take(); d->nxt = (float*)take(); d->npts = (int*)take();
+    d->pts = (float*)take(); d->nxt = (float*)take(); d->npts = (int*)take();
     d->status = (uint8_t*)take(); d->state = (uint8_t*)take(); d->pyr = (uint8_t*)take(); d->der = (short2*)take();
     d->tm = (float*)take(); d->ntm = (int*)take(); d->F = (double*)take(); d->nf = (int*)take();
     d->npairs = npairs;
@@ -1491,7 +1547,8 @@ int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
 size_t gf_select_lds(int w, int h, int cell, int np)
 {
     const int gw = (w + cell - 1) / cell, gh = (h + cell - 1) / cell;
-    return (size_t)(np > 1 ? np : 2) * 8 + (size_t)gw * gh * 4;
+    // sorted keys, per-cell list heads (u16), per accepted corner: next (u16) and x | y << 16
+    return (size_t)(np > 1 ? np : 2) * 8 + (size_t)((gw * gh + 1) & ~1) * 2 + (size_t)kMaxPts * (2 + 4);
 }
 
 // goodFeaturesToTrack into d->pts / d->npts (device count: -1 sort capacity, -3 cell capacity)
@@ -1512,9 +1569,25 @@ int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, in
                        gf_key_cap(w, h), d->pz);
     (void)hipFuncSetAttribute((const void*)k_gf_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     FLOW_LAUNCH(d, "k_gf_select", s, k_gf_select, dim3(1, 1, P), dim3(kGfThreads), lds, s, d->keys, d->nkeys, w, h, max_corners,
-                       (float)(min_distance * min_distance), cell, d->cells, d->pts, d->npts, kMaxPts, gf_key_cap(w, h),
+                       (float)(min_distance * min_distance), cell, d->pts, d->npts, kMaxPts, gf_key_cap(w, h),
                        d->pz);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// the flattened point list of every pair (k_flow_index) for k_subpix / k_lk: the corners of
+// goodFeaturesToTrack, which both consume unchanged (cornerSubPix refines them in place)
+void launch_flow_index(const FlowDev* d, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_flow_index, dim3(1), dim3(1024), 0, s, d->npts, d->pz, d->npairs, kMaxPts, d->offs);
+}
+
+// workgroups of a persistent per-point launch (wpb waves each): enough waves to fill the chip
+// several times over, never more than there can be points
+int flow_grid(const FlowDev* d, int wpb)
+{
+    const int64_t most = (int64_t)d->npairs * kMaxPts;
+    const int64_t want = 256 * 32 / wpb;             // 32 waves per CU
+    return (int)std::max<int64_t>(1, std::min<int64_t>((most + wpb - 1) / wpb, want));
 }
 
 void subpix_mask(int win, float* mask)
@@ -1540,8 +1613,9 @@ int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride
         if (!g_subpix_count) (void)hipGetSymbolAddress((void**)&g_subpix_count, HIP_SYMBOL(g_subpix_count_dev));
         itc = g_subpix_count;
     }
-    FLOW_LAUNCH(d, "k_subpix", s, (k_subpix<10, 1>), dim3(kMaxPts, 1, d->npairs), dim3(64), 0, s, img, w, h, stride, d->pts,
-                       d->npts, kMaxPts, d->mask, iters, e * e, iz, d->pz, itc);
+    launch_flow_index(d, s);
+    FLOW_LAUNCH(d, "k_subpix", s, (k_subpix<10, 1>), dim3(flow_grid(d, 1)), dim3(64), 0, s, img, w, h, stride, d->pts,
+                d->offs, d->npairs, d->mask, iters, e * e, iz, d->pz, itc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1578,8 +1652,9 @@ int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, 
                            iz, d->pz);
     }
     FLOW_LAUNCH(d, "k_sharr", s, k_sharr, dim3(64, L, P), dim3(256), 0, s, pyr, iz, d->pz);
-    FLOW_LAUNCH(d, "k_lk", s, k_lk, dim3((kMaxPts + 3) / 4, 1, P), dim3(256), 0, s, pyr, d->pts, d->npts, kMaxPts, d->nxt,
-                       d->status, win, max_count, eps * eps, iz, d->pz);
+    launch_flow_index(d, s);            // the host LK entry point sets npts without cornerSubPix
+    FLOW_LAUNCH(d, "k_lk", s, k_lk, dim3(flow_grid(d, 4)), dim3(256), 0, s, pyr, d->pts, d->offs, P, d->nxt,
+                d->status, win, max_count, eps * eps, iz, d->pz);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
