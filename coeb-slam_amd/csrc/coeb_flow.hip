@@ -53,10 +53,9 @@ int* g_subpix_count = nullptr;    // device address of g_subpix_count_dev (COEB_
 
 constexpr int kMaxPts = 1024;        // corners / tracked points per call (reference: 1000)
 constexpr int kGfThreads = 1024;
-constexpr int kGfSortMax = 16384;    // local maxima sorted in LDS (128 KB)
 // local-maximum keys kept per frame: a quarter of the pixels (a 3 x 3 maximum needs its
 // neighbours below it unless the response plateaus); more is reported as -1
-inline int gf_key_cap(int w, int h) { return std::max(kGfSortMax, w * h / 4); }
+inline int gf_key_cap(int w, int h) { return std::max(16384, w * h / 4); }
 constexpr int kLkMaxLevels = 8;
 constexpr int kFmThreads = 1024;
 constexpr int kFmChunk = 32;         // RANSAC hypotheses per chunk
@@ -285,14 +284,21 @@ __device__ int block_scan_1024(int flag, int* s_w, int& excl)
 
 // Greedy minDistance selection (featureselect.cpp): candidates in sorted order (value desc,
 // address desc); a candidate is accepted unless an accepted corner in one of the 3 x 3 grid
-// cells around it lies closer than minDistance; stop at maxCorners.  The accepted corners are
-// kept as per-cell linked lists in LDS.  One wave walks the sorted list 64 candidates at a time:
-// each lane first tests its candidate against the corners accepted before the chunk, then
-// against the earlier candidates of the chunk (a 64-bit conflict mask), and a scalar pass over
-// the chunk's lanes resolves the in-chunk dependencies in order -- the sequential result.
-// (A block-wide Jacobi fixpoint over the whole list, round 2's form, needed one block pass per
-// link of the longest conflict chain: 0.5-0.7 ms per 256 pairs.)
+// cells around it lies closer than minDistance; stop at maxCorners.
+//   * The keys are taken kGfBatch at a time in rank order: when more remain, an 8-bit MSB
+//     radix select over the global key list finds the batch's smallest key (the kGfBatch-th
+//     largest key below the previous batch's); the batch is gathered, bitonic-sorted in LDS and
+//     walked before the next is taken, so any number of maxima is selected exactly with 48 KB of
+//     LDS.  (Round 2 sorted up to 16384 keys in 150 KB of LDS: such a workgroup cannot share a
+//     CU with the pose stream's k_pose and waited for it, 0.6-0.7 ms per 256 pairs.)
+//   * The accepted corners are per-cell linked lists in LDS.  One wave walks a sorted batch 64
+//     candidates at a time: each lane tests its candidate against the corners accepted before the
+//     chunk, then against the earlier candidates of the chunk (a 64-bit conflict mask), and a
+//     scalar pass over the chunk's lanes resolves the in-chunk dependencies in order -- the
+//     sequential result.  (A block-wide Jacobi fixpoint over the whole list needed one block
+//     pass per link of the longest conflict chain.)
 constexpr uint16_t kGfNone = 0xFFFF;
+constexpr int kGfBatch = 4096;
 __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __restrict__ keys, const int* __restrict__ nkeys,
                                                          int w, int h, int max_corners, float md2, int cell,
                                                          float* __restrict__ out_xy, int* __restrict__ nout, int cap,
@@ -303,332 +309,283 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
     out_xy = at_pair(out_xy, pz);
     nout = at_pair(nout, pz);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint64_t* K = reinterpret_cast<uint64_t*>(smem);
+    uint64_t* K = reinterpret_cast<uint64_t*>(smem);                                  // [kGfBatch]
+    const int gw = (w + cell - 1) / cell, gh = (h + cell - 1) / cell;
+    uint16_t* head = reinterpret_cast<uint16_t*>(K + kGfBatch);    // [gw * gh] first accepted corner of the cell
+    uint16_t* next = head + ((gw * gh + 1) & ~1);                   // [kMaxPts] next accepted corner of its cell
+    uint32_t* axy = reinterpret_cast<uint32_t*>(next + kMaxPts);    // [kMaxPts] accepted x | y << 16
     __shared__ uint32_t s_hist[256];
     __shared__ uint64_t s_prefix;
-    __shared__ int s_need, s_cnt;
-    const int tid = threadIdx.x;
+    __shared__ int s_need, s_cnt, s_nacc, s_full;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int nall = *nkeys;
     if (nall > key_cap) {                          // more local maxima than the key buffer holds
         if (tid == 0) *nout = -1;
         return;
     }
-    // More than kGfSortMax maxima: keep the kGfSortMax largest keys (value desc, index desc; keys
-    // are unique), found by an 8-bit MSB radix select over the global key list.  The greedy
-    // selection over that prefix is exact when it accepts max_corners corners before the prefix
-    // ends -- no later candidate can change an earlier decision -- and reported as -1 otherwise.
-    const bool truncated = nall > kGfSortMax;
-    const int n = truncated ? kGfSortMax : nall;
-    if (truncated) {
-        if (tid == 0) { s_prefix = 0; s_need = kGfSortMax; }
-        for (int shift = 56; shift >= 0; shift -= 8) {
-            for (int b = tid; b < 256; b += kGfThreads) s_hist[b] = 0;
-            __syncthreads();
-            const uint64_t pre = s_prefix;
-            for (int i = tid; i < nall; i += kGfThreads) {
-                const uint64_t k = keys[i];
-                if (shift == 56 || (k >> (shift + 8)) == (pre >> (shift + 8))) atomicAdd(&s_hist[(k >> shift) & 255u], 1u);
+    for (int g = tid; g < gw * gh; g += kGfThreads) head[g] = kGfNone;
+    if (tid == 0) { s_nacc = 0; s_full = 0; }
+    const int limit = min(max_corners > 0 ? max_corners : kMaxPts, min(cap, kMaxPts));
+    uint64_t U = ~0ull;                            // keys of later batches are < U (keys are unique)
+    bool first = true;
+    __syncthreads();
+    for (int done = 0; done < nall && !s_full; ) {
+        const int m = min(kGfBatch, nall - done);
+        uint64_t T = 0;                            // this batch: keys in [T, U)
+        if (nall - done > kGfBatch) {
+            if (tid == 0) { s_prefix = 0; s_need = kGfBatch; }
+            for (int shift = 56; shift >= 0; shift -= 8) {
+                for (int b = tid; b < 256; b += kGfThreads) s_hist[b] = 0;
+                __syncthreads();
+                const uint64_t pre = s_prefix;
+                for (int i = tid; i < nall; i += kGfThreads) {
+                    const uint64_t k = keys[i];
+                    if ((first || k < U) && (shift == 56 || (k >> (shift + 8)) == (pre >> (shift + 8))))
+                        atomicAdd(&s_hist[(k >> shift) & 255u], 1u);
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    int need = s_need, b = 255;
+                    while (b > 0 && (int)s_hist[b] < need) need -= (int)s_hist[b--];
+                    s_need = need;
+                    s_prefix = pre | ((uint64_t)b << shift);
+                }
+                __syncthreads();
             }
-            __syncthreads();
-            if (tid == 0) {
-                int need = s_need, b = 255;
-                while (b > 0 && (int)s_hist[b] < need) need -= (int)s_hist[b--];
-                s_need = need;
-                s_prefix = pre | ((uint64_t)b << shift);
-            }
-            __syncthreads();
+            T = s_prefix;                          // the kGfBatch-th largest key below U
         }
-        const uint64_t T = s_prefix;               // the kGfSortMax-th largest key
         if (tid == 0) s_cnt = 0;
         __syncthreads();
-        for (int i = tid; i < nall; i += kGfThreads) {
-            const uint64_t k = keys[i];
-            if (k >= T) K[atomicAdd(&s_cnt, 1)] = k;
+        if (first && m == nall) {
+            for (int i = tid; i < nall; i += kGfThreads) K[i] = keys[i];
+        } else {
+            for (int i = tid; i < nall; i += kGfThreads) {
+                const uint64_t k = keys[i];
+                if ((first || k < U) && k >= T) K[atomicAdd(&s_cnt, 1)] = k;
+            }
+        }
+        int np = 1;
+        while (np < m) np <<= 1;
+        for (int i = m + tid; i < np; i += kGfThreads) K[i] = 0ull;
+        __syncthreads();
+        for (int size = 2; size <= np; size <<= 1)
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int i = tid; i < np; i += kGfThreads) {
+                    const int j = i ^ stride;
+                    if (j > i) {
+                        const uint64_t a = K[i], b = K[j];
+                        const bool desc = (i & size) == 0;
+                        if (desc ? (a < b) : (a > b)) { K[i] = b; K[j] = a; }
+                    }
+                }
+                __syncthreads();
+            }
+        if (tid < 64) {                            // the selection is one wave's
+            int nacc = s_nacc;
+            bool full = false;
+            for (int c0 = 0; c0 < m && !full; c0 += 64) {
+                const int i = c0 + lane;
+                const bool valid = i < m;
+                const int idx = valid ? (int)(uint32_t)K[i] : 0;
+                const int y = idx / w, x = idx - y * w;
+                const int xc = x / cell, yc = y / cell;
+                const float fx = (float)x, fy = (float)y;
+                bool hit = false;
+                if (valid) {
+                    for (int yy = max(yc - 1, 0); yy <= min(yc + 1, gh - 1) && !hit; yy++)
+                        for (int xx = max(xc - 1, 0); xx <= min(xc + 1, gw - 1) && !hit; xx++)
+                            for (int a = head[yy * gw + xx]; a != kGfNone; a = next[a]) {
+                                const uint32_t q = axy[a];
+                                const float ddx = fx - (float)(int)(q & 0xFFFFu), ddy = fy - (float)(int)(q >> 16);
+                                if (ddx * ddx + ddy * ddy < md2) { hit = true; break; }
+                            }
+                }
+                // earlier candidates of this chunk that would suppress this one once accepted
+                uint64_t conf = 0;
+                const int nc = min(64, m - c0);
+                for (int j = 0; j < nc; j++) {
+                    const int xj = __builtin_amdgcn_readlane(x, j), yj = __builtin_amdgcn_readlane(y, j);
+                    const int dxc = __builtin_amdgcn_readlane(xc, j) - xc, dyc = __builtin_amdgcn_readlane(yc, j) - yc;
+                    const float ddx = fx - (float)xj, ddy = fy - (float)yj;
+                    if (j < lane && dxc >= -1 && dxc <= 1 && dyc >= -1 && dyc <= 1 && ddx * ddx + ddy * ddy < md2)
+                        conf |= 1ull << j;
+                }
+                const uint64_t open = __ballot(valid && !hit);
+                const int g = yc * gw + xc;
+                uint64_t acc = 0;
+                const uint32_t conf_lo = (uint32_t)conf, conf_hi = (uint32_t)(conf >> 32);
+                // in order over the chunk (scalar loop): accept j unless an accepted earlier lane
+                // conflicts; lane 0 links each accepted corner into its cell's list
+                for (int j = 0; j < nc; j++) {
+                    if (!((open >> j) & 1ull)) continue;
+                    const uint64_t cj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)conf_hi, j) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)conf_lo, j);
+                    if (cj & acc) continue;
+                    const int r = nacc + __popcll(acc);
+                    acc |= 1ull << j;
+                    if (lane == 0) {
+                        const int gj = __builtin_amdgcn_readlane(g, j);
+                        next[r] = head[gj];
+                        head[gj] = (uint16_t)r;
+                    }
+                    if (r + 1 == limit) { full = true; break; }
+                }
+                if ((acc >> lane) & 1ull) {
+                    const int r = nacc + __popcll(acc & ((1ull << lane) - 1ull));
+                    axy[r] = (uint32_t)x | ((uint32_t)y << 16);
+                    out_xy[2 * r] = fx;
+                    out_xy[2 * r + 1] = fy;
+                }
+                nacc += __popcll(acc);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");     // lists visible to the next chunk
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
+            if (lane == 0) { s_nacc = nacc; s_full = full; }
         }
         __syncthreads();
+        done += m;
+        U = T;
+        first = false;
     }
-    int np = 1;
-    while (np < n) np <<= 1;
-    if (truncated) {
-        for (int i = n + tid; i < np; i += kGfThreads) K[i] = 0ull;
-    } else {
-        for (int i = tid; i < np; i += kGfThreads) K[i] = i < n ? keys[i] : 0ull;
-    }
-    const int gw = (w + cell - 1) / cell, gh = (h + cell - 1) / cell;
-    uint16_t* head = reinterpret_cast<uint16_t*>(K + (np > 1 ? np : 2));     // [gw * gh] first accepted in the cell
-    uint16_t* next = head + ((gw * gh + 1) & ~1);                               // [kMaxPts] next accepted in its cell
-    uint32_t* axy = reinterpret_cast<uint32_t*>(next + kMaxPts);                // [kMaxPts] accepted x | y << 16
-    for (int g = tid; g < gw * gh; g += kGfThreads) head[g] = kGfNone;
-    __syncthreads();
-    for (int size = 2; size <= np; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = tid; i < np; i += kGfThreads) {
-                const int j = i ^ stride;
-                if (j > i) {
-                    const uint64_t a = K[i], b = K[j];
-                    const bool desc = (i & size) == 0;
-                    if (desc ? (a < b) : (a > b)) { K[i] = b; K[j] = a; }
-                }
-            }
-            __syncthreads();
-        }
-    if (tid >= 64) return;                         // the selection is one wave's
-    const int lane = tid;
-    const int limit = min(max_corners > 0 ? max_corners : kMaxPts, min(cap, kMaxPts));
-    int nacc = 0;
-    bool full = false;
-    for (int c0 = 0; c0 < n && !full; c0 += 64) {
-        const int i = c0 + lane;
-        const bool valid = i < n;
-        const int idx = valid ? (int)(uint32_t)K[i] : 0;
-        const int y = idx / w, x = idx - y * w;
-        const int xc = x / cell, yc = y / cell;
-        const float fx = (float)x, fy = (float)y;
-        bool hit = false;
-        if (valid) {
-            for (int yy = max(yc - 1, 0); yy <= min(yc + 1, gh - 1) && !hit; yy++)
-                for (int xx = max(xc - 1, 0); xx <= min(xc + 1, gw - 1) && !hit; xx++)
-                    for (int a = head[yy * gw + xx]; a != kGfNone; a = next[a]) {
-                        const uint32_t q = axy[a];
-                        const float ddx = fx - (float)(int)(q & 0xFFFFu), ddy = fy - (float)(int)(q >> 16);
-                        if (ddx * ddx + ddy * ddy < md2) { hit = true; break; }
-                    }
-        }
-        // earlier candidates of this chunk that would suppress this one once accepted
-        uint64_t conf = 0;
-        const int nc = min(64, n - c0);
-        for (int j = 0; j < nc; j++) {
-            const int xj = __builtin_amdgcn_readlane(x, j), yj = __builtin_amdgcn_readlane(y, j);
-            const int dxc = __builtin_amdgcn_readlane(xc, j) - xc, dyc = __builtin_amdgcn_readlane(yc, j) - yc;
-            const float ddx = fx - (float)xj, ddy = fy - (float)yj;
-            if (j < lane && dxc >= -1 && dxc <= 1 && dyc >= -1 && dyc <= 1 && ddx * ddx + ddy * ddy < md2)
-                conf |= 1ull << j;
-        }
-        const uint64_t open = __ballot(valid && !hit);
-        const int g = yc * gw + xc;
-        uint64_t acc = 0;
-        const uint32_t conf_lo = (uint32_t)conf, conf_hi = (uint32_t)(conf >> 32);
-        // in order over the chunk (scalar loop): accept j unless an accepted earlier lane conflicts;
-        // lane 0 links each accepted corner into its cell's list
-        for (int j = 0; j < nc; j++) {
-            if (!((open >> j) & 1ull)) continue;
-            const uint64_t cj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)conf_hi, j) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)conf_lo, j);
-            if (cj & acc) continue;
-            const int r = nacc + __popcll(acc);
-            acc |= 1ull << j;
-            if (lane == 0) {
-                const int gj = __builtin_amdgcn_readlane(g, j);
-                next[r] = head[gj];
-                head[gj] = (uint16_t)r;
-            }
-            if (r + 1 == limit) { full = true; break; }
-        }
-        if ((acc >> lane) & 1ull) {
-            const int r = nacc + __popcll(acc & ((1ull << lane) - 1ull));
-            axy[r] = (uint32_t)x | ((uint32_t)y << 16);
-            out_xy[2 * r] = fx;
-            out_xy[2 * r + 1] = fy;
-        }
-        nacc += __popcll(acc);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");     // lists visible to the next chunk
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    }
-    if (lane == 0) {
-        const bool inexact = truncated && (max_corners <= 0 || nacc < max_corners);
-        *nout = inexact ? -1 : nacc;
-    }
+    if (tid == 0) *nout = s_nacc;
 }
 
 // ============================== cornerSubPix ==============================
-// One wave per corner (CPB corners per workgroup; 1 measured best: 20 KB of LDS per wave, the
-// next corner's wave starts as soon as a slot frees).  Per iteration all 64 lanes fill the
-// 23 x 23 getRectSubPix window and the five per-pixel terms of the 441 window pixels into LDS;
-// lanes 0..4 then run the five sums in double in the reference's order, the critical path (441
-// dependent adds each), with their operands read 8 ahead of the adds.  Measured on 257 frames
-// (10.5 iterations per corner): 1.97 ms per batch vs 4.08 ms for four corners per 256-thread
-// workgroup with unpipelined sums; forming the linear terms in the summing lanes (three product
-// arrays, selects) cost 5x.  itcount (COEB_SUBPIX_COUNT): {iterations, corners} for tools.
-#ifndef COEB_SUBPIX_RA
-#define COEB_SUBPIX_RA 8       // sum operands read ahead of the adds
-#endif
-#ifndef COEB_SUBPIX_CLOCK
-#define COEB_SUBPIX_CLOCK 0    // experiment builds: phase clocks of k_subpix (coeb_internal_subpix_clock)
-#endif
-__device__ unsigned long long g_sp_clk[256 * 8];
-#define SP_MARK(v) long long v = COEB_SUBPIX_CLOCK ? (long long)clock64() : 0
-#define SP_ADD(slot, t0) do { if (COEB_SUBPIX_CLOCK && lane == 0) atomicAdd(&g_sp_clk[(blockIdx.x & 255) * 8 + (slot)], (unsigned long long)((long long)clock64() - (t0))); } while (0)
-
-template <int WIN, int CPB>
-__global__ __launch_bounds__(64 * CPB) void k_subpix(const uint8_t* __restrict__ img0, int w, int h, int stride,
-                                                      float* __restrict__ xy0, const int* __restrict__ offs, int P,
-                                                      const float* __restrict__ mask, int iters, double eps2, int64_t iz,
-                                                      int64_t pz, int* __restrict__ itcount)
+// One lane per corner, 64 corners per wave.  The five window sums (cornersubpix.cpp) are
+// double-precision running sums in row-major order over the 21 x 21 window, so each corner's
+// sums are inherently sequential; with a lane per corner every lane runs its own five chains
+// (independent of each other, so the adds of one element overlap) and all 64 lanes do useful
+// work.  The 23 x 23 getRectSubPix window is never stored: it is produced one row at a time
+// into registers (rows r-2, r-1, r rotate through R0 / R1 / R2) from the two pixel rows it
+// interpolates, loaded as dwords per lane one row ahead of use, and sum row r - 2 consumes the
+// three rows as soon as row r exists.  The weights are a double table read with scalar loads
+// (the element index is wave-uniform).
+// (Round 2 used one wave per corner: all lanes formed the five terms of 64 window pixels into
+// LDS and lanes 0..4 summed them, so every add of the 2205-long chain per iteration issued a
+// whole wave instruction for 5 lanes: 1.5-1.7 ms per 256 pairs of ~150 corners.)
+// itcount (COEB_SUBPIX_COUNT): {iterations, corners} for tools.
+__device__ __forceinline__ float ubyte_f(uint32_t q, int k)      // byte k of q as float (v_cvt_f32_ubyteN)
 {
-    constexpr int WW = 2 * WIN + 1, BW = WW + 2, NB = BW * BW, NK = WW * WW;
-    constexpr int KPL = (NK + 63) / 64;                // terms per lane
-    // Pixels around the corner staged once (the window may drift kSpM px before a refetch):
-    // the per-iteration window then samples LDS instead of re-reading the image.
-    constexpr int kSpM = 8, SS = BW + 1 + 2 * kSpM;
-    // the five terms of 64 window pixels at a time: produced by all lanes, summed by lanes 0..4
-    // before the next 64 are written (6.2 KB of LDS per wave instead of 20 with all 441 held)
-    __shared__ float s_buf[CPB][NB];
-    __shared__ double s_tt[CPB][5][64];
-    __shared__ uint8_t s_px[CPB][SS * SS];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    float* buf = s_buf[wv];
-    double (*s_t)[64] = s_tt[wv];
-    uint8_t* px8 = s_px[wv];
-    double mreg[KPL];                                  // this lane's weights, k = lane + 64 q
-#pragma unroll
-    for (int q = 0; q < KPL; q++) mreg[q] = lane + 64 * q < NK ? (double)mask[lane + 64 * q] : 0.0;
+    return (float)((q >> (8 * k)) & 0xFFu);
+}
+
+template <int WIN>
+__global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0, int w, int h, int stride,
+                                               float* __restrict__ xy0, const int* __restrict__ offs, int P,
+                                               const double* __restrict__ maskd, int iters, double eps2, int64_t iz,
+                                               int64_t pz, int* __restrict__ itcount)
+{
+    constexpr int WW = 2 * WIN + 1, BW = WW + 2;          // 21 x 21 window, 23 x 23 interpolated
+    constexpr int NQ = (BW + 1 + 3) / 4;                   // dwords of a 24-pixel row
+    const int lane = threadIdx.x;
     const int total = offs[P];
-    for (int item = blockIdx.x * CPB + wv; item < total; item += gridDim.x * CPB) {
-    const int2 zp = flow_item(offs, P, item);
-    const uint8_t* img = at_pair(img0, iz, (uint32_t)zp.x);
-    float* xy = at_pair(xy0, pz, (uint32_t)zp.x);
-    const int p = zp.y;
-    // the previous point's last reads of px8 / buf / s_t are done before they are rewritten
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const float tx = xy[2 * p], ty = xy[2 * p + 1];
-    const int R0x = cv_floor(tx - (float)(BW - 1) * 0.5f) - kSpM, R0y = cv_floor(ty - (float)(BW - 1) * 0.5f) - kSpM;
-    const bool staged = R0x >= 0 && R0y >= 0 && R0x + SS <= w && R0y + SS <= h;
-    if (staged) {
-        const uint8_t* g = img + (size_t)R0y * stride + R0x;
-#pragma unroll
-        for (int q = 0; q < (SS * SS + 63) / 64; q++) {
-            const int e = lane + 64 * q;
-            if (e < SS * SS) { const int r = e / SS; px8[e] = g[(size_t)r * stride + (e - r * SS)]; }
-        }
-    }
-    float cx = tx, cy = ty;
-    int it = 0;
-    double err = 0;
-    SP_MARK(t_all);
-    // getRectSubPix_8u32f's in-image window from rows of `src` (image or staged pixels)
-    auto fill_in = [&](const uint8_t* src0, int sst, float a, float b) {
-        a = a < 0.0001f ? 0.0001f : a;
-        const float a12 = a * (1.f - b), a22 = a * b, b1 = 1.f - b, b2 = b;
-        const double sd = (1. - (double)a) / (double)a;
-        for (int e = lane; e < NB; e += 64) {
-            const int r = e / BW, j = e - r * BW;
-            const uint8_t* src = src0 + r * sst;
-            const float t = a12 * (float)src[j + 1] + a22 * (float)src[j + 1 + sst];
-            float prev;
-            if (j == 0) prev = (1.f - a) * (b1 * (float)src[0] + b2 * (float)src[sst]);
-            else {
-                const float tp = a12 * (float)src[j] + a22 * (float)src[j + sst];
-                prev = (float)((double)tp * sd);
-            }
-            buf[e] = prev + t;
-        }
-    };
-    do {
-        SP_MARK(t0);
-        const float ctrx = cx - (float)(BW - 1) * 0.5f, ctry = cy - (float)(BW - 1) * 0.5f;
-        const int ipx = cv_floor(ctrx), ipy = cv_floor(ctry);
-        if (ipx >= 0 && ipx + BW < w && ipy >= 0 && ipy + BW < h) {
+    const int step = gridDim.x * 64;
+    for (int base = blockIdx.x * 64; base < total; base += step) {
+        const int item = base + lane;
+        if (item >= total) break;
+        const int2 zp = flow_item(offs, P, item);
+        const uint8_t* img = at_pair(img0, iz, (uint32_t)zp.x);
+        float* xy = at_pair(xy0, pz, (uint32_t)zp.x);
+        const int p = zp.y;
+        const float tx = xy[2 * p], ty = xy[2 * p + 1];
+        float cx = tx, cy = ty;
+        int it = 0;
+        double err = 0;
+        do {
+            const float ctrx = cx - (float)(BW - 1) * 0.5f, ctry = cy - (float)(BW - 1) * 0.5f;
+            const int ipx = cv_floor(ctrx), ipy = cv_floor(ctry);
+            const bool inimg = ipx >= 0 && ipx + BW < w && ipy >= 0 && ipy + BW < h;
             const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
-            if (staged && ipx >= R0x && ipy >= R0y && ipx + BW < R0x + SS && ipy + BW < R0y + SS) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // staged pixels visible
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                fill_in(px8 + (ipy - R0y) * SS + (ipx - R0x), SS, a, b);
-            } else {
-                fill_in(img + (size_t)ipy * stride + ipx, stride, a, b);
-            }
-        } else {
-            const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
-            const float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
-            const float b1 = 1.f - b, b2 = b;
-            for (int e = lane; e < NB; e += 64) {
-                const int r = e / BW, j = e - r * BW;
-                const int y0 = min(max(ipy + r, 0), h - 1), y1 = min(max(ipy + r + 1, 0), h - 1);
-                const uint8_t* r0 = img + (size_t)y0 * stride;
-                const uint8_t* r1 = img + (size_t)y1 * stride;
-                const int c = ipx + j;
-                float v;
-                if (c < 0) v = (float)r0[0] * b1 + (float)r1[0] * b2;
-                else if (c >= w - 1) v = (float)r0[w - 1] * b1 + (float)r1[w - 1] * b2;
-                else v = (float)r0[c] * a11 + (float)r0[c + 1] * a12 + (float)r1[c] * a21 + (float)r1[c + 1] * a22;
-                buf[e] = v;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        SP_ADD(0, t0);
-        SP_MARK(t2);
-        double acc = 0;
-        // (rolled, with the weights read from the cached mask, this takes 58 VGPRs instead of 120
-        // and 7 waves per SIMD instead of 4, but measured 1.59 vs 1.57 ms: the five dependent
-        // double-add chains, issued with 5 of 64 lanes active, bound it, not the occupancy)
+            // getRectSubPix_8u32f (in-image): a clamped to 1e-4, prev(j) = (float)(t(j-1) * s)
+            const float ai = a < 0.0001f ? 0.0001f : a;
+            const float a12 = ai * (1.f - b), a22 = ai * b, b1 = 1.f - b, b2 = b, pa = 1.f - ai;
+            const double sd = (1. - (double)ai) / (double)ai;
+            // getRectSubPix_Cn_ (the window leaves the image): clamped rows, 2-term edge columns
+            const float c11 = (1.f - a) * (1.f - b), c12 = a * (1.f - b), c21 = (1.f - a) * b, c22 = a * b;
+            // pixel row y (24 px from ipx) as dwords; the last dword read is the one holding the
+            // row's pixel ipx + 23, so nothing past the row's last needed pixel is touched
+            const uint8_t* rbase = img + ipx;
+            auto load_row = [&](int y, uint32_t* q) {
+                const uint8_t* pr = rbase + (int64_t)y * stride;
+                const uintptr_t pa4 = reinterpret_cast<uintptr_t>(pr) & ~(uintptr_t)3;
+                const uint32_t* a4 = reinterpret_cast<const uint32_t*>(pa4);
+                const uint32_t* last = reinterpret_cast<const uint32_t*>((reinterpret_cast<uintptr_t>(pr) + BW) & ~(uintptr_t)3);
+                const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(pr) & 3);
+                uint32_t d[NQ + 1];
 #pragma unroll
-        for (int q = 0; q < KPL; q++) {
-            const int k = lane + 64 * q;
-            double gxx = 0.0, gxy = 0.0, gyy = 0.0, t3 = 0.0, t4 = 0.0;    // +0.0 past the window
-            if (k < NK) {
-                const int i = k / WW, j = k - i * WW;
-                const float* sp = buf + (i + 1) * BW + 1;
-                const double m = mreg[q];
-                const double tgx = (double)(sp[j + 1] - sp[j - 1]);
-                const double tgy = (double)(sp[j + BW] - sp[j - BW]);
-                gxx = tgx * tgx * m; gxy = tgx * tgy * m; gyy = tgy * tgy * m;
-                const double px = j - WIN, py = i - WIN;
-                t3 = gxx * px + gxy * py;
-                t4 = gxy * px + gyy * py;
-            }
-            s_t[0][lane] = gxx; s_t[1][lane] = gxy; s_t[2][lane] = gyy; s_t[3][lane] = t3; s_t[4][lane] = t4;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if (lane < 5) {
-                const double* t = s_t[lane];
-                constexpr int RA = COEB_SUBPIX_RA;         // operands read ahead of the adds
-                double cur[RA];
+                for (int k = 0; k <= NQ; k++) d[k] = *(a4 + k < last ? a4 + k : last);
 #pragma unroll
-                for (int u = 0; u < RA; u++) cur[u] = t[u];
+                for (int k = 0; k < NQ; k++) q[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+            };
+            auto fill_border = [&](int r, float* R) {
+                const uint8_t* r0 = img + (int64_t)min(max(ipy + r, 0), h - 1) * stride;
+                const uint8_t* r1 = img + (int64_t)min(max(ipy + r + 1, 0), h - 1) * stride;
 #pragma unroll
-                for (int k0 = RA; k0 <= 64; k0 += RA) {
-                    double nx8[RA];
-                    const int k1 = k0 < 64 ? k0 : 0;
-#pragma unroll
-                    for (int u = 0; u < RA; u++) nx8[u] = t[k1 + u];
-#pragma unroll
-                    for (int u = 0; u < RA; u++) acc += cur[u];
-#pragma unroll
-                    for (int u = 0; u < RA; u++) cur[u] = nx8[u];
+                for (int j = 0; j < BW; j++) {
+                    const int c = ipx + j;
+                    float v;
+                    if (c < 0) v = (float)r0[0] * b1 + (float)r1[0] * b2;
+                    else if (c >= w - 1) v = (float)r0[w - 1] * b1 + (float)r1[w - 1] * b2;
+                    else v = (float)r0[c] * c11 + (float)r0[c + 1] * c12 + (float)r1[c] * c21 + (float)r1[c + 1] * c22;
+                    R[j] = v;
                 }
+            };
+            uint32_t qa[NQ], qb[NQ];                       // pixel rows ipy + r, ipy + r + 1
+            if (inimg) { load_row(ipy, qa); load_row(ipy + 1, qb); }
+            auto fill_in = [&](float* R) {
+                float prev = pa * (b1 * ubyte_f(qa[0], 0) + b2 * ubyte_f(qb[0], 0));
+#pragma unroll
+                for (int j = 0; j < BW; j++) {
+                    const float t = a12 * ubyte_f(qa[(j + 1) >> 2], (j + 1) & 3) + a22 * ubyte_f(qb[(j + 1) >> 2], (j + 1) & 3);
+                    R[j] = prev + t;
+                    prev = (float)((double)t * sd);
+                }
+            };
+            float R0[BW], R1[BW], R2[BW];
+            double sa = 0, sb = 0, sc = 0, sb1 = 0, sb2 = 0;
+            for (int r = 0; r < BW; r++) {
+                if (inimg) {
+                    fill_in(R2);
+                    if (r + 1 < BW) {                      // next pixel row pair: rows ipy + r + 1, + 2
+#pragma unroll
+                        for (int k = 0; k < NQ; k++) qa[k] = qb[k];
+                        load_row(ipy + r + 2, qb);
+                    }
+                } else {
+                    fill_border(r, R2);
+                }
+                if (r >= 2) {
+                    const int i = r - 2;
+                    const double py = (double)(i - WIN);
+                    const double* mrow = maskd + i * WW;
+#pragma unroll
+                    for (int j = 0; j < WW; j++) {
+                        const double m = mrow[j];
+                        const double tgx = (double)(R1[j + 2] - R1[j]);
+                        const double tgy = (double)(R2[j + 1] - R0[j + 1]);
+                        const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
+                        const double px = (double)(j - WIN);
+                        sa += gxx; sb += gxy; sc += gyy;
+                        sb1 += gxx * px + gxy * py;
+                        sb2 += gxy * px + gyy * py;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < BW; j++) { R0[j] = R1[j]; R1[j] = R2[j]; }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");     // the next 64 overwrite these
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        }
-        const double sa = __shfl(acc, 0, 64), sb = __shfl(acc, 1, 64), sc = __shfl(acc, 2, 64);
-        const double bb1 = __shfl(acc, 3, 64), bb2 = __shfl(acc, 4, 64);
-        SP_ADD(2, t2);
-        if (COEB_SUBPIX_CLOCK && lane == 0) atomicAdd(&g_sp_clk[(blockIdx.x & 255) * 8 + 4], 1ull);
-        const double det = sa * sc - sb * sb;
-        if (fabs(det) <= DBL_EPSILON * DBL_EPSILON) break;
-        const double scale = 1.0 / det;
-        const float nx = (float)((double)cx + sc * scale * bb1 - sb * scale * bb2);
-        const float ny = (float)((double)cy - sb * scale * bb1 + sa * scale * bb2);
-        err = (double)((nx - cx) * (nx - cx) + (ny - cy) * (ny - cy));
-        cx = nx; cy = ny;
-        if (cx < 0 || cx >= (float)w || cy < 0 || cy >= (float)h) break;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    } while (++it < iters && err > eps2);
-    if (fabsf(cx - tx) > (float)WIN || fabsf(cy - ty) > (float)WIN) { cx = tx; cy = ty; }
-    if (lane == 0) {
+            const double det = sa * sc - sb * sb;
+            if (fabs(det) <= DBL_EPSILON * DBL_EPSILON) break;
+            const double scale = 1.0 / det;
+            const float nx = (float)((double)cx + sc * scale * sb1 - sb * scale * sb2);
+            const float ny = (float)((double)cy - sb * scale * sb1 + sa * scale * sb2);
+            err = (double)((nx - cx) * (nx - cx) + (ny - cy) * (ny - cy));
+            cx = nx; cy = ny;
+            if (cx < 0 || cx >= (float)w || cy < 0 || cy >= (float)h) break;
+        } while (++it < iters && err > eps2);
+        if (fabsf(cx - tx) > (float)WIN || fabsf(cy - ty) > (float)WIN) { cx = tx; cy = ty; }
         xy[2 * p] = cx; xy[2 * p + 1] = cy;
         if (itcount) { atomicAdd(itcount, it + 1); atomicAdd(itcount + 1, 1); }
-    }
-    SP_ADD(3, t_all);
     }
 }
 
@@ -1464,7 +1421,7 @@ struct FlowDev {
     float *pts, *nxt;
     int* npts;
     uint8_t *status, *state;
-    float* mask;
+    double* mask;                       // cornerSubPix weights (21 x 21, double)
     uint8_t* pyr;                       // levels 1.. of both frames
     short2* der;                        // Scharr of every previous-frame level
     float* tm;
@@ -1512,7 +1469,7 @@ int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
     }
     // shared: the two frame copies of the host entry points, the subpix weights; then one block
     // per pair
-    const size_t shared[] = {align256((size_t)w * h), align256((size_t)w * h), align256(sizeof(float) * 23 * 23),
+    const size_t shared[] = {align256((size_t)w * h), align256((size_t)w * h), align256(sizeof(double) * 21 * 21),
                              align256(sizeof(int) * ((size_t)npairs + 1))};
     const size_t sizes[] = {align256((size_t)w * h * 4), 256, 256, align256((size_t)gf_key_cap(w, h) * 8),
                             align256((size_t)kMaxPts * 8),
@@ -1530,7 +1487,7 @@ int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
     size_t o = 0;
     d->prev = p + o; o += shared[0];
     d->cur = p + o; o += shared[1];
-    d->mask = (float*)(p + o); o += shared[2];
+    d->mask = (double*)(p + o); o += shared[2];
     d->offs = (int*)(p + o); o += shared[3];
     int i = 0;
     auto take = [&]() { void* r = p + o; o += sizes[i++]; return r; };
@@ -1558,7 +1515,7 @@ int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, in
     const int P = d->npairs;
     const int cell = (int)lrint(min_distance);
     if (cell < 1) return -2;
-    const size_t lds = gf_select_lds(w, h, cell, kGfSortMax);
+    const size_t lds = gf_select_lds(w, h, cell, kGfBatch);
     if (lds > 160 * 1024) return -2;
     (void)hipMemset2DAsync(d->rmax, (size_t)d->pz, 0, 4, P, s);      // one word per pair
     (void)hipMemset2DAsync(d->nkeys, (size_t)d->pz, 0, 4, P, s);
@@ -1581,16 +1538,16 @@ void launch_flow_index(const FlowDev* d, hipStream_t s)
     hipLaunchKernelGGL(k_flow_index, dim3(1), dim3(1024), 0, s, d->npts, d->pz, d->npairs, kMaxPts, d->offs);
 }
 
-// workgroups of a persistent per-point launch (wpb waves each): enough waves to fill the chip
-// several times over, never more than there can be points
-int flow_grid(const FlowDev* d, int wpb)
+// workgroups of a persistent per-point launch (ipw points per workgroup and pass): enough to
+// fill the chip several times over, never more than there can be points
+int flow_grid(const FlowDev* d, int ipw)
 {
     const int64_t most = (int64_t)d->npairs * kMaxPts;
-    const int64_t want = 256 * 32 / wpb;             // 32 waves per CU
-    return (int)std::max<int64_t>(1, std::min<int64_t>((most + wpb - 1) / wpb, want));
+    const int64_t want = 256 * 32;                   // workgroups: 32 per CU
+    return (int)std::max<int64_t>(1, std::min<int64_t>((most + ipw - 1) / ipw, want));
 }
 
-void subpix_mask(int win, float* mask)
+void subpix_mask(int win, double* mask)
 {
     const int n = 2 * win + 1;
     for (int i = 0; i < n; i++) {
@@ -1614,7 +1571,7 @@ int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride
         itc = g_subpix_count;
     }
     launch_flow_index(d, s);
-    FLOW_LAUNCH(d, "k_subpix", s, (k_subpix<10, 1>), dim3(flow_grid(d, 1)), dim3(64), 0, s, img, w, h, stride, d->pts,
+    FLOW_LAUNCH(d, "k_subpix", s, k_subpix<10>, dim3(flow_grid(d, 64)), dim3(64), 0, s, img, w, h, stride, d->pts,
                 d->offs, d->npairs, d->mask, iters, e * e, iz, d->pz, itc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -1732,7 +1689,7 @@ extern "C" int coeb_corner_subpix(coeb_ctx* c, const uint8_t* img, int w, int h,
     FlowCall fc;
     int rc = flow_begin(c, w, h, &fc, "coeb_corner_subpix: invalid arguments");
     if (rc) return rc;
-    float mask[21 * 21];
+    double mask[21 * 21];
     subpix_mask(win, mask);
     if ((rc = upload_gray(c, fc.s, fc.d.prev, img, w, h, stride))) return rc;
     FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
@@ -1819,7 +1776,7 @@ extern "C" int coeb_moving_object_points(coeb_ctx* c, const uint8_t* prev, const
     if (rc) return rc;
     if (lk_levels(w, h, 22, 5) > kLkMaxLevels)
         return coeb_internal_error(c, COEB_EINVAL, "coeb_moving_object_points: image too large");
-    float mask[21 * 21];
+    double mask[21 * 21];
     subpix_mask(10, mask);
     if ((rc = upload_gray(c, fc.s, fc.d.prev, prev, w, h, stride)) || (rc = upload_gray(c, fc.s, fc.d.cur, cur, w, h, stride)))
         return rc;
@@ -1833,20 +1790,6 @@ extern "C" int coeb_moving_object_points(coeb_ctx* c, const uint8_t* prev, const
 // ntm_out[0] = 0 (no previous frame).  Enqueued on the context stream, no synchronisation.
 // A/B tool hook: {iterations, corners} counted by the cornerSubPix variants under
 // COEB_SUBPIX_COUNT since the last read (then reset)
-// {fill, terms, sums, whole corner, iterations} cycles of k_subpix summed over corners
-// (COEB_SUBPIX_CLOCK builds), then reset
-extern "C" int coeb_internal_subpix_clock(unsigned long long* out)
-{
-    static unsigned long long h[256 * 8];
-    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sp_clk), sizeof(h)) != hipSuccess) return COEB_EDEVICE;
-    for (int k = 0; k < 8; k++) {
-        out[k] = 0;
-        for (int i = 0; i < 256; i++) out[k] += h[i * 8 + k];
-    }
-    static const unsigned long long z[256 * 8] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_sp_clk), z, sizeof(z)) == hipSuccess ? COEB_OK : COEB_EDEVICE;
-}
-
 extern "C" int coeb_internal_subpix_count(int* out)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_subpix_count_dev), 8) != hipSuccess) return COEB_EDEVICE;
@@ -1909,7 +1852,7 @@ extern "C" int coeb_internal_pmo_batch(coeb_ctx* c, const uint8_t* d_gray, int F
         std::lock_guard<std::mutex> lk(g_pmo_mu);
         g_pmo_last[c] = {w, h, F - 1};
     }
-    float mask[21 * 21];
+    double mask[21 * 21];
     subpix_mask(10, mask);
     FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
     const int64_t iz = (int64_t)w * h;
@@ -1934,7 +1877,7 @@ extern "C" int coeb_moving_object_points_device(coeb_ctx* c, const uint8_t* d_pr
     if (rc) return rc;
     if (lk_levels(w, h, 22, 5) > kLkMaxLevels)
         return coeb_internal_error(c, COEB_EINVAL, "coeb_moving_object_points_device: image too large");
-    float mask[21 * 21];
+    double mask[21 * 21];
     subpix_mask(10, mask);
     FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
     const int sp = (int)stride;

@@ -196,10 +196,11 @@ def test_frame_batch_matches_oracle_frame_by_frame(oracle_mod):
 
 
 def test_good_features_beyond_16384_maxima(ctx, oracle_mod):
-    """A noise frame has more Harris local maxima than the 16384 sorted in LDS: the kernel keeps
-    the 16384 largest (radix select) and the greedy selection over them is exact because it
-    accepts maxCorners = 1000 corners first -- the result equals the uncapped oracle, and the
-    whole ProcessMovingObject on such frames runs instead of failing."""
+    """A noise frame has more Harris local maxima than 16384: k_gf_select takes the sorted keys
+    4096 at a time (radix select of each batch's lower bound), so the greedy selection stays the
+    sequential one however many maxima there are -- the result equals the uncapped oracle, with
+    maxCorners reached inside the first batch and, at minDistance 20 (fewer than 1000 corners fit),
+    only after every batch; the whole ProcessMovingObject on such frames runs instead of failing."""
     rng = np.random.default_rng(11)
     noise = rng.integers(0, 256, (480, 640), dtype=np.uint8)
     with pytest.raises(RuntimeError):                 # the frame does exceed 16384 maxima
@@ -207,6 +208,9 @@ def test_good_features_beyond_16384_maxima(ctx, oracle_mod):
     ref = oracle_mod.good_features(noise)
     assert len(ref) == 1000
     eq(cf.GoodFeaturesToTrack(ctx, noise), ref, "noise")
+    ref20 = oracle_mod.good_features(noise, min_distance=20.0)
+    assert 0 < len(ref20) < 1000
+    eq(cf.GoodFeaturesToTrack(ctx, noise, min_distance=20.0), ref20, "noise md20")
     cur = np.roll(noise, (1, 2), axis=(0, 1))
     tm = cf.ProcessMovingObject(ctx, noise, cur)
     tm_ref = oracle_mod.process_moving_object(noise, cur)
