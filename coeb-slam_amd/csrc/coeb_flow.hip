@@ -470,11 +470,45 @@ __device__ __forceinline__ float ubyte_f(uint32_t q, int k)      // byte k of q 
     return (float)((q >> (8 * k)) & 0xFFu);
 }
 
+// cornerSubPix work order: the corners whose window may leave the image (getRectSubPix's
+// clamped path) last, so the waves that take the in-image path (nearly all) never execute the
+// other; lane order within a wave is kept (wave-aggregated atomics), so a wave's corners stay
+// mostly one frame's.  ocnt = {interior, border} counters, zeroed before the launch.
+__global__ __launch_bounds__(256) void k_subpix_order(const float* __restrict__ xy0, const int* __restrict__ offs,
+                                                      int P, int w, int h, int margin, int64_t pz,
+                                                      int* __restrict__ order, int* __restrict__ ocnt)
+{
+    const int total = offs[P];
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int base = blockIdx.x * 256 + (threadIdx.x & ~63); base < total; base += gridDim.x * 256) {
+        const int item = base + lane;
+        bool in = false, bd = false;
+        if (item < total) {
+            const int2 zp = flow_item(offs, P, item);
+            const float* xy = at_pair(xy0, pz, (uint32_t)zp.x);
+            const float x = xy[2 * zp.y], y = xy[2 * zp.y + 1];
+            in = x >= (float)margin && x <= (float)(w - 1 - margin) && y >= (float)margin && y <= (float)(h - 1 - margin);
+            bd = !in;
+        }
+        const uint64_t mi = __ballot(in), mb = __ballot(bd);
+        int bi = 0, bb = 0;
+        if (lane == 0) {
+            bi = atomicAdd(&ocnt[0], __popcll(mi));
+            bb = atomicAdd(&ocnt[1], __popcll(mb));
+        }
+        bi = __builtin_amdgcn_readfirstlane(bi);
+        bb = __builtin_amdgcn_readfirstlane(bb);
+        if (in) order[bi + __popcll(mi & lt)] = item;
+        if (bd) order[total - 1 - (bb + __popcll(mb & lt))] = item;
+    }
+}
+
 template <int WIN>
 __global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0, int w, int h, int stride,
                                                float* __restrict__ xy0, const int* __restrict__ offs, int P,
-                                               const double* __restrict__ maskd, int iters, double eps2, int64_t iz,
-                                               int64_t pz, int* __restrict__ itcount)
+                                               const int* __restrict__ order, const double* __restrict__ maskd,
+                                               int iters, double eps2, int64_t iz, int64_t pz, int* __restrict__ itcount)
 {
     constexpr int WW = 2 * WIN + 1, BW = WW + 2;          // 21 x 21 window, 23 x 23 interpolated
     constexpr int NQ = (BW + 1 + 3) / 4;                   // dwords of a 24-pixel row
@@ -482,8 +516,8 @@ __global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0,
     const int total = offs[P];
     const int step = gridDim.x * 64;
     for (int base = blockIdx.x * 64; base < total; base += step) {
-        const int item = base + lane;
-        if (item >= total) break;
+        if (base + lane >= total) break;
+        const int item = order[base + lane];
         const int2 zp = flow_item(offs, P, item);
         const uint8_t* img = at_pair(img0, iz, (uint32_t)zp.x);
         float* xy = at_pair(xy0, pz, (uint32_t)zp.x);
@@ -518,17 +552,24 @@ __global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0,
 #pragma unroll
                 for (int k = 0; k < NQ; k++) q[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
             };
+            // branch-free: all four taps from clamped addresses (every load issued up front), the
+            // edge columns' two-term value selected
             auto fill_border = [&](int r, float* R) {
                 const uint8_t* r0 = img + (int64_t)min(max(ipy + r, 0), h - 1) * stride;
                 const uint8_t* r1 = img + (int64_t)min(max(ipy + r + 1, 0), h - 1) * stride;
+                uint8_t p0[BW + 1], p1[BW + 1];
+#pragma unroll
+                for (int j = 0; j <= BW; j++) {
+                    const int c = min(max(ipx + j, 0), w - 1);
+                    p0[j] = r0[c];
+                    p1[j] = r1[c];
+                }
 #pragma unroll
                 for (int j = 0; j < BW; j++) {
                     const int c = ipx + j;
-                    float v;
-                    if (c < 0) v = (float)r0[0] * b1 + (float)r1[0] * b2;
-                    else if (c >= w - 1) v = (float)r0[w - 1] * b1 + (float)r1[w - 1] * b2;
-                    else v = (float)r0[c] * c11 + (float)r0[c + 1] * c12 + (float)r1[c] * c21 + (float)r1[c + 1] * c22;
-                    R[j] = v;
+                    const float e = (float)p0[j] * b1 + (float)p1[j] * b2;
+                    const float v = (float)p0[j] * c11 + (float)p0[j + 1] * c12 + (float)p1[j] * c21 + (float)p1[j + 1] * c22;
+                    R[j] = (c < 0 || c >= w - 1) ? e : v;
                 }
             };
             uint32_t qa[NQ], qb[NQ];                       // pixel rows ipy + r, ipy + r + 1
@@ -1433,6 +1474,8 @@ struct FlowDev {
     int npairs;
     int64_t pz;
     int* offs;                          // k_flow_index: points before each pair, [npairs] = all
+    int* order;                         // k_subpix_order: corner work order (interior first)
+    int* ocnt;                          // its two counters
     ProfileHook* prof = nullptr;        // the context's HIP-event profiler (coeb_profile_enable)
 };
 
@@ -1470,7 +1513,8 @@ int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
     // shared: the two frame copies of the host entry points, the subpix weights; then one block
     // per pair
     const size_t shared[] = {align256((size_t)w * h), align256((size_t)w * h), align256(sizeof(double) * 21 * 21),
-                             align256(sizeof(int) * ((size_t)npairs + 1))};
+                             align256(sizeof(int) * ((size_t)npairs + 1)), align256(sizeof(int) * (size_t)npairs * kMaxPts),
+                             256};
     const size_t sizes[] = {align256((size_t)w * h * 4), 256, 256, align256((size_t)gf_key_cap(w, h) * 8),
                             align256((size_t)kMaxPts * 8),
                             align256((size_t)kMaxPts * 8), 256, align256(kMaxPts), align256(kMaxPts), align256(pyr_bytes),
@@ -1489,6 +1533,8 @@ int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
     d->cur = p + o; o += shared[1];
     d->mask = (double*)(p + o); o += shared[2];
     d->offs = (int*)(p + o); o += shared[3];
+    d->order = (int*)(p + o); o += shared[4];
+    d->ocnt = (int*)(p + o); o += shared[5];
     int i = 0;
     auto take = [&]() { void* r = p + o; o += sizes[i++]; return r; };
     d->R = (float*)take(); d->rmax = (uint32_t*)take(); d->nkeys = (int*)take(); d->keys = (uint64_t*)take();
@@ -1571,8 +1617,13 @@ int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride
         itc = g_subpix_count;
     }
     launch_flow_index(d, s);
+    (void)hipMemsetAsync(d->ocnt, 0, 8, s);
+    // interior: the window (23 x 23 around the corner, +1 for the interpolation) stays inside the
+    // image with 2 px of drift to spare
+    hipLaunchKernelGGL(k_subpix_order, dim3(flow_grid(d, 256)), dim3(256), 0, s, d->pts, d->offs, d->npairs, w, h, 14,
+                       d->pz, d->order, d->ocnt);
     FLOW_LAUNCH(d, "k_subpix", s, k_subpix<10>, dim3(flow_grid(d, 64)), dim3(64), 0, s, img, w, h, stride, d->pts,
-                d->offs, d->npairs, d->mask, iters, e * e, iz, d->pz, itc);
+                d->offs, d->npairs, d->order, d->mask, iters, e * e, iz, d->pz, itc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
