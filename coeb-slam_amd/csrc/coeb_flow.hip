@@ -718,13 +718,37 @@ __device__ __forceinline__ int64_t wave_sum_i32x(int v)
 
 __device__ __forceinline__ int refl1(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
 
-// one wave per point; every lane carries up to 8 window pixels (win*win <= 512)
+// One wave per point.  Lane (row r = lane >> 1, half h = lane & 1) carries window row r's
+// pixels [h * hw, min(win, (h + 1) * hw)), hw = ceil(win / 2) <= 11 (win <= 22): a row segment,
+// so a window's I, J and derivative samples come from a few dword loads per lane and row (bytes
+// taken out with v_bfe) instead of four byte gathers per pixel; lanes past 2 * win carry none.
+// Window sums stay exact in int32 per lane (at most 11 products of < 2^27) and are joined by
+// DPP wave reductions of their 16-bit halves.  Windows that reach past the level edge take the
+// per-pixel reflected path of calcOpticalFlowPyrLK (REFLECT_101 images, zero derivatives).
+constexpr int kLkHP = 11;                     // pixels per lane
+__device__ __forceinline__ uint32_t byte_at(const uint32_t* q, int k) { return (q[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
+
+// n <= 12 bytes from p (any alignment) as 3 dwords; no dword past the one holding p[n - 1] is read
+__device__ __forceinline__ void load12(const uint8_t* p, int n, uint32_t* q)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* a4 = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t* last = reinterpret_cast<const uint32_t*>((a + n - 1) & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t d0 = a4[0], d1 = *min(a4 + 1, last), d2 = *min(a4 + 2, last), d3 = *min(a4 + 3, last);
+    q[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    q[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    q[2] = __builtin_amdgcn_alignbyte(d3, d2, sh);
+}
+
 __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__ pxy0, const int* __restrict__ offs, int P,
                                             float* __restrict__ nxy0, uint8_t* __restrict__ status0, int win, int max_count,
                                             double eps2, int64_t iz, int64_t pz)
 {
-    constexpr int PPL = 8;
     const int lane = threadIdx.x & 63;
+    const int hwid = (win + 1) >> 1;
+    const int wr = lane >> 1, c0 = (lane & 1) * hwid;
+    const int ncol = wr < win ? min(hwid, win - c0) : 0;     // this lane's pixels
     const int total = offs[P];
     for (int item = blockIdx.x * 4 + (threadIdx.x >> 6); item < total; item += gridDim.x * 4) {
     const int2 zp = flow_item(offs, P, item);
@@ -733,22 +757,12 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
     float* nxy = at_pair(nxy0, pz, z);
     uint8_t* status = at_pair(status0, pz, z);
     const int p = zp.y;
-    const int npx = win * win;
     const float hw = (float)(win - 1) * 0.5f;
     const float FLT_SCALE = 1.f / (1 << 20);
     int st = 1;
     float nx = 0.f, ny = 0.f;
     const float px0 = pxy[2 * p], py0 = pxy[2 * p + 1];
-    int iv[PPL], gxv[PPL], gyv[PPL];
-    // window position of this lane's pixel q (e = lane + 64 q): (row << 16) | column, computed once
-    // (a division by win per pixel and iteration was a large share of the sampling loop's VALU)
-    int wxy[PPL];
-#pragma unroll
-    for (int q = 0; q < PPL; q++) {
-        const int e = lane + 64 * q;
-        const int yy = e / win;
-        wxy[q] = e < npx ? (yy << 16) | (e - yy * win) : 0;
-    }
+    int iv[kLkHP], gxv[kLkHP], gyv[kLkHP];
     for (int level = pyr.L - 1; level >= 0; level--) {
         const int lw = pyr.w[level], lh = pyr.h[level], pitch = pyr.pitch[level];
         const uint8_t* I = at_pair(pyr.P[level], level == 0 ? iz : pz, z);
@@ -769,27 +783,50 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
         int iw01 = (int)rintf(a * (1.f - b) * 16384.f);
         int iw10 = (int)rintf((1.f - a) * b * 16384.f);
         int iw11 = 16384 - iw00 - iw01 - iw10;
-        int sA11 = 0, sA12 = 0, sA22 = 0;                 // per lane: 8 products of < 2^27
+        int sA11 = 0, sA12 = 0, sA22 = 0;                 // per lane: <= 11 products of < 2^27
+        const int X0 = ipx + c0, Y = ipy + wr;
+        if (ipx >= 0 && ipy >= 0 && ipx + win < lw && ipy + win < lh) {
+            uint32_t q0[3] = {0, 0, 0}, q1[3] = {0, 0, 0};
+            if (ncol > 0) {
+                load12(I + (size_t)Y * pitch + X0, ncol + 1, q0);
+                load12(I + (size_t)(Y + 1) * pitch + X0, ncol + 1, q1);
+            }
+            const short2* d0 = D + (size_t)Y * lw + X0;
+            const short2* d1 = d0 + lw;
 #pragma unroll
-        for (int q = 0; q < PPL; q++) {
-            const int e = lane + 64 * q;
-            iv[q] = 0; gxv[q] = 0; gyv[q] = 0;
-            if (e < npx) {
-                const int yy = wxy[q] >> 16, xx = wxy[q] & 0xffff;
-                const int X = ipx + xx, Y = ipy + yy;
-                const int x0 = refl1(X, lw), x1 = refl1(X + 1, lw);
-                const uint8_t* r0 = I + (size_t)refl1(Y, lh) * pitch;
-                const uint8_t* r1 = I + (size_t)refl1(Y + 1, lh) * pitch;
-                iv[q] = (r0[x0] * iw00 + r0[x1] * iw01 + r1[x0] * iw10 + r1[x1] * iw11 + (1 << 8)) >> 9;
-                auto dv = [&](int xq, int yq) {
-                    return (xq < 0 || yq < 0 || xq >= lw || yq >= lh) ? make_short2(0, 0) : D[(size_t)yq * lw + xq];
-                };
-                const short2 d00 = dv(X, Y), d01 = dv(X + 1, Y), d10 = dv(X, Y + 1), d11 = dv(X + 1, Y + 1);
-                gxv[q] = (d00.x * iw00 + d01.x * iw01 + d10.x * iw10 + d11.x * iw11 + (1 << 13)) >> 14;
-                gyv[q] = (d00.y * iw00 + d01.y * iw01 + d10.y * iw10 + d11.y * iw11 + (1 << 13)) >> 14;
-                sA11 += gxv[q] * gxv[q];
-                sA12 += gxv[q] * gyv[q];
-                sA22 += gyv[q] * gyv[q];
+            for (int k = 0; k < kLkHP; k++) {
+                iv[k] = 0; gxv[k] = 0; gyv[k] = 0;
+                if (k < ncol) {
+                    iv[k] = ((int)byte_at(q0, k) * iw00 + (int)byte_at(q0, k + 1) * iw01 + (int)byte_at(q1, k) * iw10 +
+                             (int)byte_at(q1, k + 1) * iw11 + (1 << 8)) >> 9;
+                    const short2 e00 = d0[k], e01 = d0[k + 1], e10 = d1[k], e11 = d1[k + 1];
+                    gxv[k] = (e00.x * iw00 + e01.x * iw01 + e10.x * iw10 + e11.x * iw11 + (1 << 13)) >> 14;
+                    gyv[k] = (e00.y * iw00 + e01.y * iw01 + e10.y * iw10 + e11.y * iw11 + (1 << 13)) >> 14;
+                    sA11 += gxv[k] * gxv[k];
+                    sA12 += gxv[k] * gyv[k];
+                    sA22 += gyv[k] * gyv[k];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kLkHP; k++) {
+                iv[k] = 0; gxv[k] = 0; gyv[k] = 0;
+                if (k < ncol) {
+                    const int X = X0 + k;
+                    const int x0 = refl1(X, lw), x1 = refl1(X + 1, lw);
+                    const uint8_t* r0 = I + (size_t)refl1(Y, lh) * pitch;
+                    const uint8_t* r1 = I + (size_t)refl1(Y + 1, lh) * pitch;
+                    iv[k] = (r0[x0] * iw00 + r0[x1] * iw01 + r1[x0] * iw10 + r1[x1] * iw11 + (1 << 8)) >> 9;
+                    auto dv = [&](int xq, int yq) {
+                        return (xq < 0 || yq < 0 || xq >= lw || yq >= lh) ? make_short2(0, 0) : D[(size_t)yq * lw + xq];
+                    };
+                    const short2 e00 = dv(X, Y), e01 = dv(X + 1, Y), e10 = dv(X, Y + 1), e11 = dv(X + 1, Y + 1);
+                    gxv[k] = (e00.x * iw00 + e01.x * iw01 + e10.x * iw10 + e11.x * iw11 + (1 << 13)) >> 14;
+                    gyv[k] = (e00.y * iw00 + e01.y * iw01 + e10.y * iw10 + e11.y * iw11 + (1 << 13)) >> 14;
+                    sA11 += gxv[k] * gxv[k];
+                    sA12 += gxv[k] * gyv[k];
+                    sA22 += gyv[k] * gyv[k];
+                }
             }
         }
         const int64_t tA11 = wave_sum_i32x(sA11), tA12 = wave_sum_i32x(sA12), tA22 = wave_sum_i32x(sA22);
@@ -814,33 +851,35 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
             iw01 = (int)rintf(a * (1.f - b) * 16384.f);
             iw10 = (int)rintf((1.f - a) * b * 16384.f);
             iw11 = 16384 - iw00 - iw01 - iw10;
-            int ib1 = 0, ib2 = 0;                     // per lane: 8 products of < 2^26
+            int ib1 = 0, ib2 = 0;                     // per lane: <= 11 products of < 2^26
+            const int JX0 = inx + c0, JY = iny + wr;
             if (inx >= 0 && iny >= 0 && inx + win < lw && iny + win < lh) {
-                // the window and its +1 neighbours inside the level: no reflection, rows from one
-                // wave-uniform base (the common case)
-                const uint8_t* Jw = J + (size_t)iny * pitch + inx;
+                // the window and its +1 neighbours inside the level: one 12-byte segment per row
+                uint32_t q0[3] = {0, 0, 0}, q1[3] = {0, 0, 0};
+                if (ncol > 0) {
+                    load12(J + (size_t)JY * pitch + JX0, ncol + 1, q0);
+                    load12(J + (size_t)(JY + 1) * pitch + JX0, ncol + 1, q1);
+                }
 #pragma unroll
-                for (int q = 0; q < PPL; q++) {
-                    if (lane + 64 * q < npx) {
-                        const uint8_t* r0 = Jw + (wxy[q] >> 16) * pitch + (wxy[q] & 0xffff);
-                        const uint8_t* r1 = r0 + pitch;
-                        const int diff = ((r0[0] * iw00 + r0[1] * iw01 + r1[0] * iw10 + r1[1] * iw11 + (1 << 8)) >> 9) - iv[q];
-                        ib1 += diff * gxv[q];
-                        ib2 += diff * gyv[q];
+                for (int k = 0; k < kLkHP; k++) {
+                    if (k < ncol) {
+                        const int diff = (((int)byte_at(q0, k) * iw00 + (int)byte_at(q0, k + 1) * iw01 +
+                                           (int)byte_at(q1, k) * iw10 + (int)byte_at(q1, k + 1) * iw11 + (1 << 8)) >> 9) - iv[k];
+                        ib1 += diff * gxv[k];
+                        ib2 += diff * gyv[k];
                     }
                 }
             } else {
 #pragma unroll
-                for (int q = 0; q < PPL; q++) {
-                    if (lane + 64 * q < npx) {
-                        const int yy = wxy[q] >> 16, xx = wxy[q] & 0xffff;
-                        const int X = inx + xx, Y = iny + yy;
+                for (int k = 0; k < kLkHP; k++) {
+                    if (k < ncol) {
+                        const int X = JX0 + k;
                         const int x0 = refl1(X, lw), x1 = refl1(X + 1, lw);
-                        const uint8_t* r0 = J + (size_t)refl1(Y, lh) * pitch;
-                        const uint8_t* r1 = J + (size_t)refl1(Y + 1, lh) * pitch;
-                        const int diff = ((r0[x0] * iw00 + r0[x1] * iw01 + r1[x0] * iw10 + r1[x1] * iw11 + (1 << 8)) >> 9) - iv[q];
-                        ib1 += diff * gxv[q];
-                        ib2 += diff * gyv[q];
+                        const uint8_t* r0 = J + (size_t)refl1(JY, lh) * pitch;
+                        const uint8_t* r1 = J + (size_t)refl1(JY + 1, lh) * pitch;
+                        const int diff = ((r0[x0] * iw00 + r0[x1] * iw01 + r1[x0] * iw10 + r1[x1] * iw11 + (1 << 8)) >> 9) - iv[k];
+                        ib1 += diff * gxv[k];
+                        ib2 += diff * gyv[k];
                     }
                 }
             }
