@@ -152,13 +152,24 @@ __global__ __launch_bounds__(1024) void k_flow_index(const int* __restrict__ d_n
 }
 
 // ============================== goodFeaturesToTrack ==============================
-// One 32 x 32 tile per workgroup (thread = one column, four rows).  The Sobel products
-// (dx^2, dx dy, dy^2) are computed once per position of the 34 x 34 box-filter footprint
-// (positions reflected at the border, Sobel taps reflected again, as boxFilter / Sobel with
-// BORDER_REFLECT_101 read them) into LDS -- interior tiles from a staged 36 x 36 pixel tile --
-// then each pixel sums its 3 x 3 box from LDS in the reference's order, the three row sums of
-// a row shared by the outputs that use it.  One atomicMax per 1024 pixels.
-constexpr int kGfT = 32;
+// Harris response, one wave per strip of 60 output columns x kGfRows rows, lane = column
+// (x0 - 2 + lane; lanes 2..61 produce).  Each lane slides down its column: a new pixel row
+// enters, its left / right neighbours come from the adjacent lanes (DPP wave shifts), the Sobel
+// products of the row above are formed, their 3-wide row sums take the neighbours' products the
+// same way, and three row sums down give the box sum -- in the reference's order (left to right,
+// then top to bottom).  Nothing goes through LDS.  (Round 2 staged Sobel products of 32 x 32
+// tiles in LDS: ~130 VALU lane-operations per pixel, 0.47 ms per 256 pairs.)
+// Borders (REFLECT_101, boxFilter over Sobel products that are themselves computed with
+// reflected taps): a lane / row outside the image loads the reflected pixel, so its Sobel is the
+// mirror image of the reflected position's -- gx (column -1, w) or gy (row -1, h) negated
+// exactly -- and only the cross product dx*dy changes sign; it is negated back.
+constexpr int kGfRows = 32;
+constexpr int kGfCols = 60;
+__device__ __forceinline__ int wave_shr1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, false); }  // lane i <- i-1
+__device__ __forceinline__ int wave_shl1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, false); }  // lane i <- i+1
+__device__ __forceinline__ float wave_shr1f(float v) { return __int_as_float(wave_shr1(__float_as_int(v))); }
+__device__ __forceinline__ float wave_shl1f(float v) { return __int_as_float(wave_shl1(__float_as_int(v))); }
+
 __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__ img, int w, int h, int stride, double k,
                                                      float* __restrict__ R, uint32_t* __restrict__ rmax, int64_t iz,
                                                      int64_t pz)
@@ -166,77 +177,54 @@ __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__
     img = at_pair(img, iz);
     R = at_pair(R, pz);
     rmax = at_pair(rmax, pz);
-    constexpr int TP = kGfT + 2, PP = TP + 1;        // products footprint, LDS pitch
-    __shared__ float sA[TP][PP], sB[TP][PP], sC[TP][PP];
-    __shared__ uint8_t sT[TP + 2][TP + 2 + 4];
-    const int x0 = blockIdx.x * kGfT, y0 = blockIdx.y * kGfT;
+    const int lane = threadIdx.x & 63;
+    const int strip = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int x0 = strip * kGfCols, y0 = blockIdx.y * kGfRows;
+    if (x0 >= w) return;
+    const int c = x0 - 2 + lane;                       // this lane's column
+    const int cr = reflect101(c, w);
+    const bool produce = lane >= 2 && lane < 2 + kGfCols && c < w;
+    const float xsgn = (c == -1 || c == w) ? -1.f : 1.f;
     const double scale = 1.0 / (4.0 * 3.0 * 255.0);
-    auto put = [&](int tx, int ty, int gx, int gy) {
-        const float dx = (float)((double)gx * scale), dy = (float)((double)gy * scale);
-        sA[ty][tx] = dx * dx;
-        sB[ty][tx] = dx * dy;
-        sC[ty][tx] = dy * dy;
-    };
-    if (x0 >= 2 && y0 >= 2 && x0 + TP <= w && y0 + TP <= h) {
-        // interior tile: no reflection; the 36 x 36 pixel footprint staged once
-        for (int e = threadIdx.x; e < (TP + 2) * (TP + 2); e += 256) {
-            const int ty = e / (TP + 2), tx = e - ty * (TP + 2);
-            sT[ty][tx] = img[(size_t)(y0 - 2 + ty) * stride + x0 - 2 + tx];
+    const uint8_t* col = img + cr;
+    // pixel rows y-1, y of the Sobel being formed (own column, left, right)
+    int pm = 0, pl_m = 0, pr_m = 0, p0 = 0, pl_0 = 0, pr_0 = 0;
+    // row sums of the products of the last two product rows
+    float ra0 = 0, rb0 = 0, rc0 = 0, ra1 = 0, rb1 = 0, rc1 = 0;
+    float rmx = -FLT_MAX;
+    const int y1 = min(h, y0 + kGfRows);
+    // pixel rows y0-2 .. y1+1: product rows y0-1 .. y1, output rows y0 .. y1-1
+    for (int yy = y0 - 2; yy <= y1 + 1; yy++) {
+        const int pv = col[(int64_t)reflect101(yy, h) * stride];
+        const int pl = wave_shr1(pv), pr = wave_shl1(pv);
+        if (yy >= y0) {                                 // Sobel / products of row yy - 1
+            const int gx = (pr_m - pl_m) + 2 * (pr_0 - pl_0) + (pr - pl);
+            const int gy = (pl - pl_m) + 2 * (pv - pm) + (pr - pr_m);
+            const float dx = (float)((double)gx * scale), dy = (float)((double)gy * scale);
+            const int yp = yy - 1;
+            const float sgn = (yp == -1 || yp == h) ? -xsgn : xsgn;
+            const float A = dx * dx, B = (dx * dy) * sgn, C = dy * dy;
+            const float ra = (wave_shr1f(A) + A) + wave_shl1f(A);
+            const float rb = (wave_shr1f(B) + B) + wave_shl1f(B);
+            const float rc = (wave_shr1f(C) + C) + wave_shl1f(C);
+            if (yy >= y0 + 2) {                         // output row yy - 2
+                const float a = (ra0 + ra1) + ra, b = (rb0 + rb1) + rb, cc = (rc0 + rc1) + rc;
+                const float ac = a * cc - b * b, apc = a + cc;
+                const float r = (float)((double)ac - (k * (double)apc) * (double)apc);
+                if (produce) {
+                    R[(size_t)(yy - 2) * w + c] = r;
+                    rmx = fmaxf(rmx, r);
+                }
+            }
+            ra0 = ra1; rb0 = rb1; rc0 = rc1;
+            ra1 = ra; rb1 = rb; rc1 = rc;
         }
-        __syncthreads();
-        for (int e = threadIdx.x; e < TP * TP; e += 256) {
-            const int ty = e / TP, tx = e - ty * TP;
-            const uint8_t* r0 = &sT[ty][tx];
-            const uint8_t* r1 = &sT[ty + 1][tx];
-            const uint8_t* r2 = &sT[ty + 2][tx];
-            const int gx = (r0[2] - r0[0]) + 2 * (r1[2] - r1[0]) + (r2[2] - r2[0]);
-            const int gy = (r2[0] - r0[0]) + 2 * (r2[1] - r0[1]) + (r2[2] - r0[2]);
-            put(tx, ty, gx, gy);
-        }
-    } else {
-        // border tile: box positions reflected, then the Sobel taps of each position reflected
-        for (int e = threadIdx.x; e < TP * TP; e += 256) {
-            const int ty = e / TP, tx = e - ty * TP;
-            const int xx = reflect101(x0 + tx - 1, w), yy = reflect101(y0 + ty - 1, h);
-            const int xm = reflect101(xx - 1, w), xp = reflect101(xx + 1, w);
-            const uint8_t* r0 = img + (size_t)reflect101(yy - 1, h) * stride;
-            const uint8_t* r1 = img + (size_t)yy * stride;
-            const uint8_t* r2 = img + (size_t)reflect101(yy + 1, h) * stride;
-            const int gx = (r0[xp] - r0[xm]) + 2 * (r1[xp] - r1[xm]) + (r2[xp] - r2[xm]);
-            const int gy = (r2[xm] - r0[xm]) + 2 * (r2[xx] - r0[xx]) + (r2[xp] - r0[xp]);
-            put(tx, ty, gx, gy);
-        }
+        pm = p0; pl_m = pl_0; pr_m = pr_0;
+        p0 = pv; pl_0 = pl; pr_0 = pr;
     }
-    __syncthreads();
-    const int lx = threadIdx.x & 31, ly = (threadIdx.x >> 5) * 4;
-    const int x = x0 + lx;
-    // row sums of footprint rows ly .. ly+5 at column lx (the reference's left-to-right order)
-    float ra[6], rb[6], rc[6];
-#pragma unroll
-    for (int j = 0; j < 6; j++) {
-        ra[j] = (sA[ly + j][lx] + sA[ly + j][lx + 1]) + sA[ly + j][lx + 2];
-        rb[j] = (sB[ly + j][lx] + sB[ly + j][lx + 1]) + sB[ly + j][lx + 2];
-        rc[j] = (sC[ly + j][lx] + sC[ly + j][lx + 1]) + sC[ly + j][lx + 2];
-    }
-    float r4 = -FLT_MAX;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int y = y0 + ly + q;
-        if (x < w && y < h) {
-            const float a = (ra[q] + ra[q + 1]) + ra[q + 2], b = (rb[q] + rb[q + 1]) + rb[q + 2];
-            const float c = (rc[q] + rc[q + 1]) + rc[q + 2];
-            const float ac = a * c - b * b, apc = a + c;
-            const float r = (float)((double)ac - (k * (double)apc) * (double)apc);
-            R[(size_t)y * w + x] = r;
-            r4 = fmaxf(r4, r);
-        }
-    }
-    __shared__ uint32_t s_m[4];
-    uint32_t o = f2ord(r4);
+    uint32_t o = f2ord(rmx);
     for (int off = 32; off >= 1; off >>= 1) o = max(o, (uint32_t)__shfl_xor((int)o, off, 64));
-    if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = o;
-    __syncthreads();
-    if (threadIdx.x == 0) atomicMax(rmax, max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3])));
+    if (lane == 0) atomicMax(rmax, o);
 }
 
 __global__ __launch_bounds__(256) void k_gf_candidates(const float* __restrict__ R, int w, int h, double quality,
@@ -1605,7 +1593,8 @@ int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, in
     (void)hipMemset2DAsync(d->rmax, (size_t)d->pz, 0, 4, P, s);      // one word per pair
     (void)hipMemset2DAsync(d->nkeys, (size_t)d->pz, 0, 4, P, s);
     const dim3 grid((w + 15) / 16, (h + 15) / 16, P);
-    FLOW_LAUNCH(d, "k_gf_response", s, k_gf_response, dim3((w + kGfT - 1) / kGfT, (h + kGfT - 1) / kGfT, P), dim3(256), 0, s, img, w, h,
+    FLOW_LAUNCH(d, "k_gf_response", s, k_gf_response, dim3((w + 4 * kGfCols - 1) / (4 * kGfCols), (h + kGfRows - 1) / kGfRows, P),
+                dim3(256), 0, s, img, w, h,
                        stride, k, d->R, d->rmax, iz, d->pz);
     FLOW_LAUNCH(d, "k_gf_candidates", s, k_gf_candidates, grid, dim3(256), 0, s, d->R, w, h, quality, d->rmax, d->keys, d->nkeys,
                        gf_key_cap(w, h), d->pz);
