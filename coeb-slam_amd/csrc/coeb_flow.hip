@@ -636,26 +636,42 @@ struct PyrDownArgs {
     int nfr;                            // frames per pair block: 2 (prev, next) or 1 (one pyramid per frame)
 };
 
-// pyrDown 8U (5x5 [1 4 6 4 1]^2, (sum + 128) >> 8, REFLECT_101); blockIdx.z = nfr * pair + frame
+// pyrDown 8U (5x5 [1 4 6 4 1]^2, (sum + 128) >> 8, REFLECT_101); blockIdx.z = nfr * pair + frame.
+// One wave per strip of 62 output columns x kPdRows rows, lane = output column x0 - 1 + lane
+// (lanes 1..62 produce): a lane loads source columns 2x and 2x + 1 of each source row (reflected
+// indices), the taps 2x - 2, 2x - 1 and 2x + 2 come from the neighbouring lanes (DPP wave shifts),
+// and the five horizontal sums of an output row slide down the strip two source rows at a time.
+// (Round 2 gathered all 25 taps per output pixel with a reflection per tap.)
+constexpr int kPdRows = 16;
+constexpr int kPdCols = 62;
 __global__ __launch_bounds__(256) void k_pyr_down(PyrDownArgs a, int64_t iz, int64_t pz)
 {
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= a.dw || y >= a.dh) return;
+    const int lane = threadIdx.x & 63;
+    const int strip = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int x0 = strip * kPdCols, y0 = blockIdx.y * kPdRows;
+    if (x0 >= a.dw) return;
     const int fr = a.nfr == 2 ? (int)(blockIdx.z & 1) : 0;
     const uint64_t pair = a.nfr == 2 ? blockIdx.z >> 1 : blockIdx.z;
     const uint8_t* src = a.src[fr] + pair * (uint64_t)(a.src_img ? iz : pz);
     uint8_t* dst = a.dst[fr] + pair * (uint64_t)pz;
-    int cols[5];
-    for (int j = 0; j < 5; j++) cols[j] = reflect101(2 * x + j - 2, a.sw);
-    const int k[5] = {1, 4, 6, 4, 1};
-    int acc = 0;
-    for (int i = 0; i < 5; i++) {
-        const uint8_t* row = src + (size_t)reflect101(2 * y + i - 2, a.sh) * a.spitch;
-        int hs = 0;
-        for (int j = 0; j < 5; j++) hs += k[j] * row[cols[j]];
-        acc += k[i] * hs;
+    const int c = x0 - 1 + lane;
+    const int s0 = reflect101(2 * c, a.sw), s1 = reflect101(2 * c + 1, a.sw);
+    const bool produce = lane >= 1 && lane <= kPdCols && c < a.dw;
+    auto hsum = [&](int sr) {
+        const uint8_t* row = src + (size_t)reflect101(sr, a.sh) * a.spitch;
+        const int e0 = row[s0], e1 = row[s1];
+        const int l0 = wave_shr1(e0), l1 = wave_shr1(e1), r0 = wave_shl1(e0);
+        return l0 + 4 * l1 + 6 * e0 + 4 * e1 + r0;
+    };
+    const int y1 = min(a.dh, y0 + kPdRows);
+    // source rows 2y - 2 .. 2y + 2 of output row y
+    int h0 = hsum(2 * y0 - 2), h1 = hsum(2 * y0 - 1), h2 = hsum(2 * y0);
+    for (int y = y0; y < y1; y++) {
+        const int h3 = hsum(2 * y + 1), h4 = hsum(2 * y + 2);
+        const int acc = h0 + 4 * h1 + 6 * h2 + 4 * h3 + h4;
+        if (produce) dst[(size_t)y * a.dw + c] = (uint8_t)((acc + 128) >> 8);
+        h0 = h2; h1 = h3; h2 = h4;
     }
-    dst[(size_t)y * a.dw + x] = (uint8_t)((acc + 128) >> 8);
 }
 
 // calcSharrDeriv of every previous-frame level; blockIdx.y = level, blockIdx.z = pair,
@@ -1684,7 +1700,8 @@ int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, 
         a.sw = pyr.w[l - 1]; a.sh = pyr.h[l - 1]; a.spitch = pyr.pitch[l - 1]; a.dw = pyr.w[l]; a.dh = pyr.h[l];
         a.src_img = l == 1;
         a.nfr = chained ? 1 : 2;
-        FLOW_LAUNCH(d, "k_pyr_down", s, k_pyr_down, dim3((a.dw + 63) / 64, (a.dh + 3) / 4, chained ? P + 1 : 2 * P), dim3(256), 0, s, a,
+        FLOW_LAUNCH(d, "k_pyr_down", s, k_pyr_down, dim3((a.dw + 4 * kPdCols - 1) / (4 * kPdCols), (a.dh + kPdRows - 1) / kPdRows,
+                                                         chained ? P + 1 : 2 * P), dim3(256), 0, s, a,
                            iz, d->pz);
     }
     FLOW_LAUNCH(d, "k_sharr", s, k_sharr, dim3(64, L, P), dim3(256), 0, s, pyr, iz, d->pz);
