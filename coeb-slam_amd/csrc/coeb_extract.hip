@@ -1516,30 +1516,34 @@ __device__ void sincos_canon(float af, float* s, float* c)
 
 struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
 
-// KP keypoints of one frame per wave (KP = 8), two at a time:
-//   1  stage: the two keypoints' UNBLURRED patches, rows y-21 .. y+21 x 64 bytes from
-//      (x-21) & ~15, go to the wave's LDS slab (rows past the level edge reflected, REFLECT_101;
-//      a patch whose columns leave the level or the row takes a byte path with reflected
-//      columns).  The next pair's 16-byte loads are in flight while this pair is processed.
-//   2  IC_Angle (ORBextractor.cc:80-107) from LDS: lanes 0..30 take rows v = -15..15 of the
-//      first keypoint, lanes 32..62 those of the second; each reads its 32 row bytes, masks them
-//      with the disc row |v| (umax) and sums u*p and p with v_dot4_u32_u8; a 32-lane reduction
-//      gives m10, m01.  fastAtan2 and the canonical sincosf run on every lane of the half; the
-//      cv::KeyPoint record is written here.
+// KP keypoints of one frame per wave (KP = 8), one at a time:
+//   1  stage: the keypoint's UNBLURRED patch, rows y-21 .. y+21 x 64 bytes from (x-21) & ~15,
+//      goes to the wave's LDS slab as four copies shifted by 0..3 bytes (copy k byte j = patch
+//      byte j + k), so every later read of any byte offset o is a dword-aligned read of copy
+//      o & 3 -- misaligned ds_read_b64 / b128 stall the LDS pipe (SQ_LDS_UNALIGNED_STALL: 9e8
+//      per launch in the first form of this kernel, 10x its time).  The shifted dwords are built
+//      in registers (v_alignbyte with the next lane's chunk) and stored aligned.  Rows past the
+//      level edge are reflected (REFLECT_101); a patch whose columns leave the level or the row
+//      takes a byte path with reflected columns.  The next keypoint's 16-byte loads are in flight
+//      while this one is processed.
+//   2  IC_Angle (ORBextractor.cc:80-107) from LDS: lane (row v = -15..15, half) reads 16 row
+//      bytes, masks them with the disc row |v| (umax) and sums u*p and p with v_dot4_u32_u8; a
+//      wave reduction gives m10, m01; fastAtan2 and the canonical sincosf follow; the
+//      cv::KeyPoint record is written.
 //   3  tests (ORBextractor.cc:109-156): lane = 4 of the 256 tests; each sample is the 7x7
 //      GaussianBlur (sigma 2, Q8 kernel k) of the patch evaluated at that point:
 //      (sum_i k_i H_i + 2^15) >> 16, H_i = sum_j k_j p(r + i - 3, c + j - 3) as two
-//      v_dot4_u32_u8 on the 8 bytes from column c - 3 of row r + i - 3 -- the same integer the
-//      separable blur of the whole level produces, so the blurred pyramid is never written.
-//      Nibbles are OR-combined by DPP into the descriptor dwords (LDS).
+//      v_dot4_u32_u8 on the 8 bytes from column c - 3 of row r + i - 3 (one ds_read2_b32) --
+//      the same integer the separable blur of the whole level produces, so the blurred pyramid
+//      is never written.  Nibbles are OR-combined by DPP into the descriptor dwords (LDS).
 // Then the wave's descriptors leave with 16-byte stores.
 // The rotated pattern offsets are cvRound of |(px, py)| <= 13*sqrt(2), so |offset| <= 18 and the
 // blur taps reach 21 from the keypoint.  Patch rows are 72 bytes apart (18 dwords): consecutive
 // rows land on different banks.
 constexpr int kPRow = 72, kPRows = 43, kPChunks = kPRows * 4;   // 172 16-byte chunks per patch
-constexpr int kPBytes = kPRow * kPRows;
+constexpr int kPBytes = kPRow * kPRows;                         // one copy
 constexpr int kPHalf = 21;                                        // patch row / column radius
-template <int KP> constexpr int desc_slab() { return 2 * kPBytes + 32 * KP; }
+template <int KP> constexpr int desc_slab() { return 4 * kPBytes + 32 * KP; }
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};   // ORBextractor.cc:461-476
 
 // Disc mask of row |v| = av (av 16: all zero), dword d of a row read from patch column
@@ -1565,6 +1569,10 @@ __device__ __forceinline__ uint32_t dpp_or_xor2(uint32_t v)   // quad_perm [2,3,
 __device__ __forceinline__ uint32_t dpp_or_shl4(uint32_t v)   // lane i |= lane i+4 (row_shl:4)
 {
     return v | (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_next(uint32_t v)      // lane i <- lane i+1 (wave_shl:1)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, false);
 }
 
 struct DescKey {
@@ -1609,33 +1617,35 @@ __device__ __forceinline__ u32x4 patch_chunk_slow(const uint8_t* img, int pitch,
     }
     return u32x4{q[0], q[1], q[2], q[3]};
 }
-__device__ __forceinline__ void patch_put(uint8_t* pb, int e, u32x4 v)
+// chunk v (this lane's, chunk index e) into the four shifted copies; nx = the next chunk's first
+// dword (the next lane's: chunk e + 1; past a row's end its bytes are never read)
+__device__ __forceinline__ void patch_put4(uint8_t* slab, int e, u32x4 v, uint32_t nx, bool st)
 {
-    uint2* d = reinterpret_cast<uint2*>(pb + (e >> 2) * kPRow + 16 * (e & 3));   // 8-byte aligned rows
-    d[0] = make_uint2(v.x, v.y);
-    d[1] = make_uint2(v.z, v.w);
-}
-
-// blurred patch value at (r, c) from the keypoint (|r|, |c| <= 18): 7 rows of 8 bytes
-__device__ __forceinline__ uint32_t blur_at(const uint8_t* ctr, int r, int c, uint32_t k0123, uint32_t k4560,
-                                            const int* kv)
-{
-    const uint8_t* p = ctr + (r - 3) * kPRow + (c - 3);
-    uint32_t acc = 1u << 15;
+    const uint32_t w[5] = {v.x, v.y, v.z, v.w, nx};
+    const int off = (e >> 2) * kPRow + 16 * (e & 3);
 #pragma unroll
-    for (int i = 0; i < 7; i++) {
-        uint32_t q[2];
-        __builtin_memcpy(q, p + i * kPRow, 8);
-        const uint32_t hsum = __builtin_amdgcn_udot4(q[0], k0123, __builtin_amdgcn_udot4(q[1], k4560, 0u, false), false);
-        acc += __umul24((uint32_t)kv[i], hsum);            // v_mad_u32_u24
+    for (int k = 0; k < 4; k++) {
+        uint32_t s[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) s[i] = k ? __builtin_amdgcn_alignbyte(w[i + 1], w[i], (uint32_t)k) : w[i];
+        if (st) {
+            uint2* d = reinterpret_cast<uint2*>(slab + k * kPBytes + off);       // 8-byte aligned
+            d[0] = make_uint2(s[0], s[1]);
+            d[1] = make_uint2(s[2], s[3]);
+        }
     }
-    return acc >> 16;
+}
+// two dwords = patch bytes o .. o + 7 (o >= 0), as one aligned ds_read2_b32 of copy o & 3
+__device__ __forceinline__ void patch_read8(const uint8_t* slab, int o, uint32_t& lo, uint32_t& hi)
+{
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(slab + (o & 3) * kPBytes + (o & ~3));
+    lo = p[0];
+    hi = p[1];
 }
 
 template <bool kVec0, int KP>
 __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ P, ExtractBufs b)
 {
-    static_assert(KP % 2 == 0, "keypoints are taken in pairs");
     __shared__ __attribute__((aligned(16))) uint8_t s_slab[kWaves][desc_slab<KP>()];
     __shared__ __attribute__((aligned(16))) uint32_t s_msk[17][8];
     if (threadIdx.x < 17 * 8) s_msk[threadIdx.x >> 3][threadIdx.x & 7] = ic_mask(threadIdx.x >> 3, threadIdx.x & 7);
@@ -1670,14 +1680,15 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         px1[t] = (float)(int8_t)((pw >> 16) & 0xff); py1[t] = (float)(int8_t)(pw >> 24);
     }
     uint8_t* slab = s_slab[wv];
-    uint32_t* dsl = reinterpret_cast<uint32_t*>(slab + 2 * kPBytes);
-    const int half = lane >> 5, hl = lane & 31;
+    uint32_t* dsl = reinterpret_cast<uint32_t*>(slab + 4 * kPBytes);
     const int e0 = lane, e1 = lane + 64, e2 = min(lane + 128, kPChunks - 1);
-    // the two keypoints of pair t (the second repeats the first when nk is odd)
-    auto pair_key = [&](int t, int k) { return desc_key<kVec0>(P, b, f, idx0 + min(t + k, nk - 1), incl); };
-    DescKey ka = pair_key(0, 0), kb = pair_key(0, 1);
-    u32x4 qa0, qa1, qa2, qb0, qb1, qb2;
-    auto load_fast = [&](const DescKey& k, u32x4& q0, u32x4& q1, u32x4& q2) {
+    // IC lane roles: row v = (lane >> 1) - 15 (lanes 0..61), half = lane & 1 (16 bytes each)
+    const int icv = (lane >> 1) - 15, ich = lane & 1;
+    const bool icl = lane < 62;
+    const uint32_t* icm = s_msk[icv < 0 ? -icv : (icv > 15 ? 16 : icv)];
+    DescKey kn = desc_key<kVec0>(P, b, f, idx0, incl);
+    u32x4 q0, q1, q2;
+    auto load_fast = [&](const DescKey& k) {
         if (!k.fast) return;
         const LevelGeom& g = P->lv[k.l];
         const uint8_t* img = level_ptr(P, b, f, k.l);
@@ -1685,98 +1696,96 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         q1 = patch_chunk_fast(img, g.pitch, g.h, k.c0, k.y, e1);
         q2 = patch_chunk_fast(img, g.pitch, g.h, k.c0, k.y, e2);
     };
-    auto stage = [&](const DescKey& k, uint8_t* pb, u32x4 q0, u32x4 q1, u32x4 q2) {
-        if (!k.fast) {
-            const LevelGeom& g = P->lv[k.l];
-            const uint8_t* img = level_ptr(P, b, f, k.l);
-            q0 = patch_chunk_slow(img, g.pitch, g.w, g.h, k.c0, k.y, e0);
-            q1 = patch_chunk_slow(img, g.pitch, g.w, g.h, k.c0, k.y, e1);
-            q2 = patch_chunk_slow(img, g.pitch, g.w, g.h, k.c0, k.y, e2);
-        }
-        patch_put(pb, e0, q0);
-        patch_put(pb, e1, q1);
-        if (lane + 128 < kPChunks) patch_put(pb, e2, q2);
-    };
-    load_fast(ka, qa0, qa1, qa2);
-    load_fast(kb, qb0, qb1, qb2);
+    load_fast(kn);
     const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
-    for (int t0 = 0; t0 < nk; t0 += 2) {
-        uint8_t* pa_ = slab;
-        uint8_t* pb_ = slab + kPBytes;
-        stage(ka, pa_, qa0, qa1, qa2);
-        stage(kb, pb_, qb0, qb1, qb2);
-        const DescKey ca = ka, cb = kb;
-        wave_sync_lds();
-        if (t0 + 2 < nk) {                   // next pair's rows in flight during this pair
-            ka = pair_key(t0 + 2, 0);
-            kb = pair_key(t0 + 2, 1);
-            load_fast(ka, qa0, qa1, qa2);
-            load_fast(kb, qb0, qb1, qb2);
+    for (int t = 0; t < nk; t++) {
+        const DescKey ck = kn;
+        if (!ck.fast) {
+            const LevelGeom& g = P->lv[ck.l];
+            const uint8_t* img = level_ptr(P, b, f, ck.l);
+            q0 = patch_chunk_slow(img, g.pitch, g.w, g.h, ck.c0, ck.y, e0);
+            q1 = patch_chunk_slow(img, g.pitch, g.w, g.h, ck.c0, ck.y, e1);
+            q2 = patch_chunk_slow(img, g.pitch, g.w, g.h, ck.c0, ck.y, e2);
         }
-        // ---- IC_Angle: half h = keypoint t0 + h, lane hl = row v = hl - 15
-        const DescKey& ck = half ? cb : ca;
-        const uint8_t* ctr = (half ? pb_ : pa_) + kPHalf * kPRow + (ck.x - ck.c0);
+        // next lane's first dwords: chunks e + 1 (lane 63's successor is chunk 64 = lane 0's q1)
+        const uint32_t n0 = wave_next(q0.x), n1 = wave_next(q1.x), n2 = wave_next(q2.x);
+        const uint32_t n0f = lane == 63 ? __builtin_amdgcn_readlane(q1.x, 0) : n0;
+        const uint32_t n1f = lane == 63 ? __builtin_amdgcn_readlane(q2.x, 0) : n1;
+        patch_put4(slab, e0, q0, n0f, true);
+        patch_put4(slab, e1, q1, n1f, true);
+        patch_put4(slab, e2, q2, n2, lane + 128 < kPChunks);
+        wave_sync_lds();
+        if (t + 1 < nk) {                        // the next keypoint's rows in flight during this one
+            kn = desc_key<kVec0>(P, b, f, idx0 + t + 1, incl);
+            load_fast(kn);
+        }
+        const int xo = ck.x - ck.c0;             // patch column of the keypoint (21..36)
+        const int ctr = kPHalf * kPRow + xo;     // patch byte offset of the keypoint
+        // ---- IC_Angle
         uint32_t A = 0, S = 0;
         int m01 = 0;
-        if (hl < 31) {
-            const int v = hl - 15, av = v < 0 ? -v : v;
-            uint32_t q[8];
-            __builtin_memcpy(q, ctr + v * kPRow - 15, 32);
-            const uint32_t* msk = s_msk[av];
+        if (icl) {
+            const int o = ctr + icv * kPRow - 15 + 16 * ich;
+            uint32_t q[4];
+            patch_read8(slab, o, q[0], q[1]);
+            patch_read8(slab, o + 8, q[2], q[3]);
 #pragma unroll
-            for (int d = 0; d < 8; d++) {
-                const uint32_t pm = q[d] & msk[d];
-                A = __builtin_amdgcn_udot4(pm, 0x03020100u + 0x04040404u * (uint32_t)d, A, false);
+            for (int d = 0; d < 4; d++) {
+                const int dd = 4 * ich + d;
+                const uint32_t pm = q[d] & icm[dd];
+                A = __builtin_amdgcn_udot4(pm, 0x03020100u + 0x04040404u * (uint32_t)dd, A, false);
                 S = __builtin_amdgcn_udot4(pm, 0x01010101u, S, false);
             }
-            m01 = v * (int)S;
+            m01 = icv * (int)S;
         }
 #pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
+        for (int o = 1; o < 64; o <<= 1) {
             A += __shfl_xor(A, o, 64);
             S += __shfl_xor(S, o, 64);
             m01 += __shfl_xor(m01, o, 64);
         }
         const int m10 = (int)A - 15 * (int)S;
         const float angle = fast_atan2_dev((float)m01, (float)m10);
-        float bs, ac;
-        sincos_canon(angle * factorPI, &bs, &ac);
-        if (hl == 0 && t0 + half < nk) {     // cv::KeyPoint {x, y, size, angle, response, octave, class_id}
+        float tb, ta;
+        sincos_canon(angle * factorPI, &tb, &ta);
+        if (lane == 0) {                          // cv::KeyPoint {x, y, size, angle, response, octave, class_id}
             const LevelGeom& g = P->lv[ck.l];
             float fx = (float)ck.x, fy = (float)ck.y;
             if (ck.l != 0) { fx *= g.scale; fy *= g.scale; }          // :1327-1334
             KeyPointOut o;
             o.x = fx; o.y = fy; o.size = (float)g.size_i; o.angle = angle; o.response = (float)ck.sc;
             o.octave = ck.l; o.class_id = -1;
-            reinterpret_cast<KeyPointOut*>(b.kps)[(int64_t)f * P->kcap + idx0 + t0 + half] = o;
+            reinterpret_cast<KeyPointOut*>(b.kps)[(int64_t)f * P->kcap + idx0 + t] = o;
         }
-        // ---- tests of the two keypoints
+        // ---- tests: (row, col) = (fma(px, b, py*a), fma(px, a, -(py*b))) as packed-f32 pairs,
+        // the same two roundings per component as the reference's fused forms
+        const f32x2 AB = {ta, tb}, BA = {tb, ta};
+        auto blur_at = [&](int r, int c) {
+            const int o = ctr + (r - 3) * kPRow + (c - 3);
+            uint32_t acc = 1u << 15;
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const int t = t0 + k;
-            if (t >= nk) break;
-            const float tb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bs), 32 * k));
-            const float ta = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ac), 32 * k));
-            const DescKey& kk = k ? cb : ca;
-            const uint8_t* c = (k ? pb_ : pa_) + kPHalf * kPRow + (kk.x - kk.c0);
-            // (row, col) = (fma(px, b, py*a), fma(px, a, -(py*b))) as packed-f32 pairs: the same
-            // two roundings per component as the reference's fused forms
-            const f32x2 AB = {ta, tb}, BA = {tb, ta};
-            uint32_t nib = 0;
-#pragma unroll
-            for (int tt = 0; tt < 4; tt++) {
-                const f32x2 u0 = f32x2{py0[tt], py0[tt]} * AB, u1 = f32x2{py1[tt], py1[tt]} * AB;
-                const f32x2 rc0 = __builtin_elementwise_fma(f32x2{px0[tt], px0[tt]}, BA, f32x2{u0.x, -u0.y});
-                const f32x2 rc1 = __builtin_elementwise_fma(f32x2{px1[tt], px1[tt]}, BA, f32x2{u1.x, -u1.y});
-                const uint32_t v0 = blur_at(c, (int)rintf(rc0.x), (int)rintf(rc0.y), k0123, k4560, kv);
-                const uint32_t v1 = blur_at(c, (int)rintf(rc1.x), (int)rintf(rc1.y), k0123, k4560, kv);
-                nib |= (uint32_t)(v0 < v1) << tt;
+            for (int i = 0; i < 7; i++) {
+                uint32_t lo, hi;
+                patch_read8(slab, o + i * kPRow, lo, hi);
+                const uint32_t hs = __builtin_amdgcn_udot4(lo, k0123, __builtin_amdgcn_udot4(hi, k4560, 0u, false), false);
+                acc += __umul24((uint32_t)kv[i], hs);            // v_mad_u32_u24
             }
-            // bit k of byte i = test 8i+k: dword d = nibbles of lanes 8d .. 8d+7
-            uint32_t dw = nib << (4 * (lane & 7));
-            dw = dpp_or_shl4(dpp_or_xor2(dpp_or_xor1(dw)));
-            if ((lane & 7) == 0) dsl[8 * t + (lane >> 3)] = dw;
+            return acc >> 16;
+        };
+        uint32_t nib = 0;
+#pragma unroll
+        for (int tt = 0; tt < 4; tt++) {
+            const f32x2 u0 = f32x2{py0[tt], py0[tt]} * AB, u1 = f32x2{py1[tt], py1[tt]} * AB;
+            const f32x2 rc0 = __builtin_elementwise_fma(f32x2{px0[tt], px0[tt]}, BA, f32x2{u0.x, -u0.y});
+            const f32x2 rc1 = __builtin_elementwise_fma(f32x2{px1[tt], px1[tt]}, BA, f32x2{u1.x, -u1.y});
+            const uint32_t v0 = blur_at((int)rintf(rc0.x), (int)rintf(rc0.y));
+            const uint32_t v1 = blur_at((int)rintf(rc1.x), (int)rintf(rc1.y));
+            nib |= (uint32_t)(v0 < v1) << tt;
         }
+        // bit k of byte i = test 8i+k: dword d = nibbles of lanes 8d .. 8d+7
+        uint32_t dw = nib << (4 * (lane & 7));
+        dw = dpp_or_shl4(dpp_or_xor2(dpp_or_xor1(dw)));
+        if ((lane & 7) == 0) dsl[8 * t + (lane >> 3)] = dw;
         wave_sync_lds();                         // patch reads done before the next staging
     }
     // ---- descriptors out
