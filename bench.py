@@ -160,12 +160,14 @@ def kernel_bytes(name, w, h, nkp, nprev, npx, ncand, flow=None):
         return (12 + 28 + 4 + 2) * nkp
     if name == "k_fast":        # read the FAST ROIs of every level, write candidate keys
         return fast_roi_pixels(w, h) + 4 * ncand
+    if name == "k_blur":        # read + write every level
+        return 2 * npx
     if name == "k_pyr_level":   # 7 launches: read level l-1, write level l (sum over launches / 7)
         return 2 * (npx - w * h) / 7.0 + w * h / 7.0
     if name == "k_octree":      # read candidates, write level keypoints
         return 4 * ncand + 4 * nkp
-    if name == "k_describe":    # per keypoint: the 43 x 43 unblurred patch the IC_Angle disc and the 7x7
-        return (43 * 43 + 4 + 60) * nkp     # Gaussian at the 512 samples read, key in, 28-B record + 32-B descriptor out
+    if name == "k_describe":    # per keypoint: 749-px IC_Angle disc + 512 blurred samples in,
+        return (749 + 512 + 4 + 60) * nkp   # key in, 28-B record + 32-B descriptor out
     if name == "k_match":       # read current kps+descs and LastFrame snapshot, write matches
         return 60 * nkp + (32 + 28 + 12 + 4) * nprev + 4 * nkp
     if name == "k_prep":

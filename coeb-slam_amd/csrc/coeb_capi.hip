@@ -161,7 +161,7 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
     rtab.clear();
     cells.clear();
     if (W > 4096 || H > 4096) { err = "image larger than 4096 px is not supported (12-bit key packing)"; return false; }
-    int64_t pyr = 0, node = 0;
+    int64_t pyr = 0, blur = 0, node = 0;
     int kcap_total = 0, out_total = 0, cell_cap = 1;
     for (int l = 0; l < t.nlevels; l++) {
         LevelGeom& g = P.lv[l];
@@ -170,8 +170,11 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
         g.scale = t.scale[l];
         g.size_i = (int)(PATCH_SIZE * t.scale[l]);
         g.pitch = l == 0 ? W : (g.w + 63) & ~63;
+        g.bpitch = (g.w + 63) & ~63;
         if (l == 0) g.pyr_off = -1;
         else { g.pyr_off = pyr; pyr = align256(pyr + (int64_t)g.pitch * g.h); }
+        g.blur_off = blur;
+        blur = align256(blur + (int64_t)g.bpitch * g.h);
         if (l > 0) {
             while (rtab.size() % 4) rtab.push_back(0);     // 16-byte aligned table rows
             g.rtab_off = (int)rtab.size();
@@ -242,6 +245,7 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
         kcap_total += P.lv[l].kcap;
     }
     P.pyr_stride = std::max<int64_t>(pyr, 256);
+    P.blur_stride = blur;
     P.kbuf_stride = kcap_total;
     P.node_stride = node;
     P.lvl_stride = out_total;
@@ -375,8 +379,8 @@ struct coeb_ctx {
     // t_* buffers; the next coeb_pose_batch_device, coeb_batch_pose_results, coeb_memcpy_d2h,
     // coeb_synchronize and coeb_destroy join it (join_pose()).
     hipStream_t pose_stream = nullptr;
-    // level-0 FAST beside the pyramid (launch_extract's SideStream); COEB_SIDE_STREAM=0 disables
-    SideStream side{nullptr, nullptr, nullptr, nullptr, 2, false};
+    // level-0 blur + FAST beside the pyramid (launch_extract's SideStream); COEB_SIDE_STREAM=0 disables
+    SideStream side{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, true, false};
     bool side_init = false;
     hipEvent_t ev_tprep = nullptr, ev_pose = nullptr;
     bool pose_pending = false;
@@ -518,12 +522,13 @@ int extract_bufs(coeb_ctx* c, int F, ExtractBufs& b)
     const Plan& P = c->plan;
     memset(&b, 0, sizeof(b));
     int rc;
-    uint8_t *pyr, *nodes, *desc;
+    uint8_t *pyr, *blur, *nodes, *desc;
     int *cand_n, *lvl_n, *counts, *err;
     uint32_t *cand, *keys, *lvl_kp;
     coeb_keypoint* kps;
     DynMask* dyn;
     if ((rc = ensure(c, "pyr", (size_t)F * P.pyr_stride, &pyr))) return rc;
+    if ((rc = ensure(c, "blur", (size_t)F * P.blur_stride, &blur))) return rc;
     if ((rc = ensure(c, "cand_n", (size_t)F * P.ncells, &cand_n))) return rc;
     if ((rc = ensure(c, "cand", (size_t)F * P.ncells * P.cell_cap, &cand))) return rc;
     if ((rc = ensure(c, "keys", (size_t)F * 2 * P.kbuf_stride, &keys))) return rc;
@@ -535,7 +540,7 @@ int extract_bufs(coeb_ctx* c, int F, ExtractBufs& b)
     if ((rc = ensure(c, "counts", (size_t)F, &counts))) return rc;
     if ((rc = ensure(c, "dyn", (size_t)F, &dyn))) return rc;
     if ((rc = ensure(c, "err", 4, &err))) return rc;
-    b.pyr = pyr; b.cand_n = cand_n; b.cand = cand; b.keys = keys; b.nodes = nodes;
+    b.pyr = pyr; b.blur = blur; b.cand_n = cand_n; b.cand = cand; b.keys = keys; b.nodes = nodes;
     b.lvl_n = lvl_n; b.lvl_kp = lvl_kp; b.kps = kps; b.desc = desc; b.counts = counts; b.dyn = dyn; b.err = err;
     b.rtab = static_cast<const int*>(c->bufs["rtab"].p);
     b.cells = static_cast<const CellDesc*>(c->bufs["cells"].p);
@@ -591,11 +596,15 @@ const SideStream* side_stream(coeb_ctx* c)
         if (e && e[0] == '0') return nullptr;
         const char* sp = getenv("COEB_SIDE_SPLIT");          // first level left to the context stream
         if (sp) c->side.split = atoi(sp);
+        const char* bl = getenv("COEB_SIDE_BLUR");           // 0: late levels' blur on the context stream
+        if (bl) c->side.blur_late = bl[0] == '1';
         const char* so = getenv("COEB_SIDE_OCTREE");         // 1: early levels' octree on the side stream
         if (so) c->side.side_octree = so[0] == '1';
         if (hipStreamCreateWithFlags(&c->side.s, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->side.fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->side.mid, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->side.pyr_done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->side.join2, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->side.join, hipEventDisableTiming) != hipSuccess)
             c->side.s = nullptr;
     }
@@ -663,6 +672,7 @@ ExtractBufs offset_bufs(const Plan& P, const ExtractBufs& b, int f0)
     ExtractBufs o = b;
     o.gray = b.gray + (int64_t)f0 * P.W * P.H;
     o.pyr = b.pyr + (int64_t)f0 * P.pyr_stride;
+    o.blur = b.blur + (int64_t)f0 * P.blur_stride;
     o.cand_n = b.cand_n + (int64_t)f0 * P.ncells;
     o.cand = b.cand + (int64_t)f0 * P.ncells * P.cell_cap;
     o.keys = b.keys + (int64_t)f0 * 2 * P.kbuf_stride;
@@ -766,6 +776,8 @@ void coeb_destroy(coeb_ctx* c)
         (void)hipStreamDestroy(c->side.s);
         (void)hipEventDestroy(c->side.fork);
         (void)hipEventDestroy(c->side.mid);
+        (void)hipEventDestroy(c->side.pyr_done);
+        (void)hipEventDestroy(c->side.join2);
         (void)hipEventDestroy(c->side.join);
     }
     if (c->pose_stream) {
@@ -1872,7 +1884,7 @@ int coeb_internal_error(coeb_ctx* c, int code, const char* msg) { return set_err
 ProfileHook* coeb_internal_prof(coeb_ctx* c) { return c ? &c->hook : nullptr; }
 
 /* Debug readback of intermediate buffers of frame f of the last batch (test support):
- * what = "pyr" | "cand_n" | "lvl_n" | "lvl_kp" | "dyn"; copies min(bytes, size). */
+ * what = "pyr" | "blur" | "cand_n" | "lvl_n" | "lvl_kp" | "dyn"; copies min(bytes, size). */
 int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t bytes, size_t* size_out)
 {
     if (c) join_pose(c);
@@ -1942,6 +1954,7 @@ int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t byt
     size_t n = 0;
     std::string w(what);
     if (w == "pyr") { src = (const uint8_t*)c->bufs["pyr"].p + (size_t)f * P.pyr_stride; n = P.pyr_stride; }
+    else if (w == "blur") { src = (const uint8_t*)c->bufs["blur"].p + (size_t)f * P.blur_stride; n = P.blur_stride; }
     else if (w == "cand_n") { src = (const uint8_t*)c->bufs["cand_n"].p + (size_t)f * P.ncells * 4; n = (size_t)P.ncells * 4; }
     else if (w == "lvl_n") { src = (const uint8_t*)c->bufs["lvl_n"].p + (size_t)f * P.L * 4; n = (size_t)P.L * 4; }
     else if (w == "lvl_kp") { src = (const uint8_t*)c->bufs["lvl_kp"].p + (size_t)f * P.lvl_stride * 4; n = (size_t)P.lvl_stride * 4; }

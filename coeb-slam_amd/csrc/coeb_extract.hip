@@ -6,9 +6,10 @@
 // Pipeline for F frames (one launch each, all on the context stream):
 //   k_dynmask    dynamic-object rectangles + area flag           (ORBextractor.cc:1101-1195)
 //   k_pyr_level  cascaded INTER_LINEAR pyramid, level l from l-1  (:1344-1367)
+//   k_blur       7x7 sigma-2 Gaussian of every level, LDS tiled   (:1317-1318)
 //   k_fast       per 30-px cell FAST-9/16 + NMS + iniTh/minTh     (:811-850)
 //   k_octree     per (frame, level) DistributeOctTree emulation   (:546-769, 852-890, 1204-1207)
-//   k_describe   IC_Angle + Gaussian-at-sample rBRIEF + output    (:80-156, 902-903, 1291-1337, 1317-1318)
+//   k_describe   IC_Angle + rBRIEF + output assembly              (:80-156, 902-903, 1291-1337)
 #include <type_traits>
 #include <cmath>
 #include <hip/hip_runtime.h>
@@ -301,13 +302,34 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
     }
 }
 
-// ================================ shared helpers ================================
+// ================================ k_blur ================================
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), Q8 kernel k (symmetric, sum 256), result
+// (sum_ij k_i k_j p_ij + 2^15) >> 16.  OpenCV's horizontal-then-vertical
+// order has no intermediate rounding, so the same integer is computed vertical-first:
+//   * vertical 7-tap on packed u16 column pairs (sums <= 255*256 fit 16 bits): 7 v_pk ops
+//     per 2 columns, the 7 source rows slide through registers (row loop unrolled by 7, so
+//     the ring never moves);
+//   * horizontal 7-tap as four v_dot2_u32_u16 per output on the packed vertical sums, the
+//     3-column halo coming from the neighbouring lanes by DPP row shifts;
+//   * the rounded result is byte 2 of the 24-bit accumulator: v_perm packs 4 outputs.
+// Work item = one wave: 4 row groups of 16 lanes; a group covers 64 source columns (4 per
+// lane) of which lanes 1..14 produce (56 output columns), and one band of rows.
+constexpr int kBlurCols = 56;
+
 __device__ __forceinline__ int reflect101(int p, int len)
 {
     if (len == 1) return 0;
     while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
     return p;
 }
+
+struct BlurWork {
+    int L;
+    int item0, item1;              // this launch's wave items [item0, item1)
+    int item_off[COEB_MAXL + 1];   // wave items per level (prefix)
+    int nstrips[COEB_MAXL];        // 56-column strips
+    int bh[COEB_MAXL];             // rows per band (4 bands per item)
+};
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -345,6 +367,105 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t v)   // lane i <- lane i-1
 __device__ __forceinline__ uint32_t dpp_shl1(uint32_t v)   // lane i <- lane i+1 (16-lane rows)
 {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xf, 0xf, false);
+}
+
+__global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, ExtractBufs b, BlurWork bw)
+{
+    const int2 bxy = block_xy();
+    const int f = bxy.y;
+    const int item = bw.item0 + bxy.x * kWaves + wave_id();
+    if (item >= bw.item1) return;
+    int l = 0;
+    while (l + 1 < bw.L && item >= bw.item_off[l + 1]) l++;
+    const int it = item - bw.item_off[l];
+    const int strip = it % bw.nstrips[l], bq = it / bw.nstrips[l];
+    const LevelGeom& g = P->lv[l];
+    const int w = g.w, h = g.h, sp = g.pitch, dp = g.bpitch;
+    const int lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
+    const int bh = bw.bh[l];
+    const int y0 = (bq * 4 + grp) * bh;
+    const int y1 = min(h, y0 + bh);
+    const int x = strip * kBlurCols - 4 + gl * 4;
+    const uint8_t* src = level_ptr(P, b, f, l);
+    uint8_t* dst = b.blur + (int64_t)f * P->blur_stride + g.blur_off;
+    const bool produce = gl >= 1 && gl <= 14 && x < w && y0 < y1;
+    const bool edge = x < 0 || x + 3 >= w || (sp & 3) != 0;
+    int cx[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) cx[q] = reflect101(min(x + q, w + 2), w);
+    const int k0 = P->gauss[0], k1 = P->gauss[1], k2 = P->gauss[2], k3 = P->gauss[3];
+    const us2 K0 = pk2(k0, k0), K1 = pk2(k1, k1), K2 = pk2(k2, k2), K3 = pk2(k3, k3);
+    // horizontal weights per (output column, source pair), DESIGN.md s4
+    const us2 W_l01_0 = pk2(0, k0), W_l23_0 = pk2(k1, k2), W_c01_0 = pk2(k3, k2), W_c23_0 = pk2(k1, k0);
+    const us2 W_l23_1 = pk2(k0, k1), W_c01_1 = pk2(k2, k3), W_c23_1 = pk2(k2, k1), W_r01_1 = pk2(k0, 0);
+    const us2 W_l23_2 = pk2(0, k0), W_c01_2 = pk2(k1, k2), W_c23_2 = pk2(k3, k2), W_r01_2 = pk2(k1, k0);
+    const us2 W_c01_3 = pk2(k0, k1), W_c23_3 = pk2(k2, k3), W_r01_3 = pk2(k2, k1), W_r23_3 = pk2(k0, 0);
+    const uint32_t rnd = 1u << 15;
+    const int n_iter = bh + 6;
+    const int hm = 2 * h - 2;
+    uint32_t R0[7], R1[7];
+    for (int i0 = 0; i0 < n_iter; i0 += 7) {
+        // issue the block's 7 row loads up front (latency hiding), then filter
+        uint32_t raw[7];
+#pragma unroll
+        for (int ph = 0; ph < 7; ph++) {
+            // source row y0 - 3 + i, REFLECT_101 (|r| <= 3 outside the level), clamped for
+            // idle bands and for the rows past the end of the last block
+            const int r = y0 - 3 + i0 + ph;
+            int rr = r < 0 ? -r : r;
+            rr = min(rr, hm - rr);
+            rr = max(0, min(rr, h - 1));
+            const uint8_t* row = src + (int64_t)rr * sp;
+            if (!edge) {
+                raw[ph] = *reinterpret_cast<const uint32_t*>(row + x);
+            } else {
+                raw[ph] = (uint32_t)row[cx[0]] | ((uint32_t)row[cx[1]] << 8) | ((uint32_t)row[cx[2]] << 16) |
+                          ((uint32_t)row[cx[3]] << 24);
+            }
+        }
+#pragma unroll
+        for (int ph = 0; ph < 7; ph++) {
+            const int i = i0 + ph;
+            if (i >= n_iter) break;
+            const int r = y0 - 3 + i;
+            R0[ph] = __builtin_amdgcn_perm(0u, raw[ph], 0x0c010c00u);
+            R1[ph] = __builtin_amdgcn_perm(0u, raw[ph], 0x0c030c02u);
+            if (i < 6) continue;
+            // rows i-6 .. i are ring slots ph+1 .. ph (mod 7); centre = slot ph+4
+            const int s0 = (ph + 1) % 7, s1 = (ph + 2) % 7, s2 = (ph + 3) % 7, s3 = (ph + 4) % 7,
+                      s4 = (ph + 5) % 7, s5 = (ph + 6) % 7, s6 = ph;
+            const us2 v01 = K3 * as_us2(R0[s3]) + K2 * (as_us2(R0[s2]) + as_us2(R0[s4])) +
+                            K1 * (as_us2(R0[s1]) + as_us2(R0[s5])) + K0 * (as_us2(R0[s0]) + as_us2(R0[s6]));
+            const us2 v23 = K3 * as_us2(R1[s3]) + K2 * (as_us2(R1[s2]) + as_us2(R1[s4])) +
+                            K1 * (as_us2(R1[s1]) + as_us2(R1[s5])) + K0 * (as_us2(R1[s0]) + as_us2(R1[s6]));
+            const uint32_t V01 = as_u32(v01), V23 = as_u32(v23);
+            const us2 L01 = as_us2(dpp_shr1(V01)), L23 = as_us2(dpp_shr1(V23));
+            const us2 R01 = as_us2(dpp_shl1(V01)), R23 = as_us2(dpp_shl1(V23));
+            uint32_t a0 = __builtin_amdgcn_udot2(L01, W_l01_0, rnd, false);
+            a0 = __builtin_amdgcn_udot2(L23, W_l23_0, a0, false);
+            a0 = __builtin_amdgcn_udot2(v01, W_c01_0, a0, false);
+            a0 = __builtin_amdgcn_udot2(v23, W_c23_0, a0, false);
+            uint32_t a1 = __builtin_amdgcn_udot2(L23, W_l23_1, rnd, false);
+            a1 = __builtin_amdgcn_udot2(v01, W_c01_1, a1, false);
+            a1 = __builtin_amdgcn_udot2(v23, W_c23_1, a1, false);
+            a1 = __builtin_amdgcn_udot2(R01, W_r01_1, a1, false);
+            uint32_t a2 = __builtin_amdgcn_udot2(L23, W_l23_2, rnd, false);
+            a2 = __builtin_amdgcn_udot2(v01, W_c01_2, a2, false);
+            a2 = __builtin_amdgcn_udot2(v23, W_c23_2, a2, false);
+            a2 = __builtin_amdgcn_udot2(R01, W_r01_2, a2, false);
+            uint32_t a3 = __builtin_amdgcn_udot2(v01, W_c01_3, rnd, false);
+            a3 = __builtin_amdgcn_udot2(v23, W_c23_3, a3, false);
+            a3 = __builtin_amdgcn_udot2(R01, W_r01_3, a3, false);
+            a3 = __builtin_amdgcn_udot2(R23, W_r23_3, a3, false);
+            const int y = r - 3;
+            if (produce && y < y1) {
+                // byte 2 of each accumulator = (acc + 2^15) >> 16 (acc + 2^15 < 2^24)
+                const uint32_t p01 = __builtin_amdgcn_perm(a1, a0, 0x0c0c0602u);
+                const uint32_t p23 = __builtin_amdgcn_perm(a3, a2, 0x06020c0cu);
+                *reinterpret_cast<uint32_t*>(dst + (int64_t)y * dp + x) = p01 | p23;
+            }
+        }
+    }
 }
 
 // ================================ k_fast ================================
@@ -1516,38 +1637,35 @@ __device__ void sincos_canon(float af, float* s, float* c)
 
 struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
 
-// KP keypoints of one frame per wave (KP = 8), one at a time:
-//   1  stage: the keypoint's UNBLURRED patch, rows y-21 .. y+21 x 64 bytes from (x-21) & ~15,
-//      goes to the wave's LDS slab as four copies shifted by 0..3 bytes (copy k byte j = patch
-//      byte j + k), so every later read of any byte offset o is a dword-aligned read of copy
-//      o & 3 -- misaligned ds_read_b64 / b128 stall the LDS pipe (SQ_LDS_UNALIGNED_STALL: 9e8
-//      per launch in the first form of this kernel, 10x its time).  The shifted dwords are built
-//      in registers (v_alignbyte with the next lane's chunk) and stored aligned.  Rows past the
-//      level edge are reflected (REFLECT_101); a patch whose columns leave the level or the row
-//      takes a byte path with reflected columns.  The next keypoint's 16-byte loads are in flight
-//      while this one is processed.
-//   2  IC_Angle (ORBextractor.cc:80-107) from LDS: lane (row v = -15..15, half) reads 16 row
-//      bytes, masks them with the disc row |v| (umax) and sums u*p and p with v_dot4_u32_u8; a
-//      wave reduction gives m10, m01; fastAtan2 and the canonical sincosf follow; the
-//      cv::KeyPoint record is written.
-//   3  tests (ORBextractor.cc:109-156): lane = 4 of the 256 tests; each sample is the 7x7
-//      GaussianBlur (sigma 2, Q8 kernel k) of the patch evaluated at that point:
-//      (sum_i k_i H_i + 2^15) >> 16, H_i = sum_j k_j p(r + i - 3, c + j - 3) as two
-//      v_dot4_u32_u8 on the 8 bytes from column c - 3 of row r + i - 3 (one ds_read2_b32) --
-//      the same integer the separable blur of the whole level produces, so the blurred pyramid
-//      is never written.  Nibbles are OR-combined by DPP into the descriptor dwords (LDS).
-// Then the wave's descriptors leave with 16-byte stores.
-// The rotated pattern offsets are cvRound of |(px, py)| <= 13*sqrt(2), so |offset| <= 18 and the
-// blur taps reach 21 from the keypoint.  Patch rows are 72 bytes apart (18 dwords): consecutive
-// rows land on different banks.
-constexpr int kPRow = 72, kPRows = 43, kPChunks = kPRows * 4;   // 172 16-byte chunks per patch
-constexpr int kPBytes = kPRow * kPRows;                         // one copy
-constexpr int kPHalf = 21;                                        // patch row / column radius
-template <int KP> constexpr int desc_slab() { return 4 * kPBytes + 32 * KP; }
+// KP keypoints of one frame per wave (KP = 8 by default), in three phases:
+//   A  kDescLpk = 64/KP lanes per keypoint: IC_Angle from 16-byte row loads of the unblurred
+//      level, half of the lanes taking rows -|v| and half +|v|, each lane KP/2 rows; every row is
+//      realigned in registers so byte j is patch column j-15, masked with the disc row |v| (a
+//      17 x 32 B table in LDS: the rows differ across lanes) and summed by two v_dot4_u32_u8
+//      per 4-pixel group, then reduced over the keypoint's lanes.  fastAtan2 and the canonical
+//      sincosf run on every lane of the keypoint; the cv::KeyPoint record is written here.
+//   B  kDescGroup keypoints per step: their 37 x 64 B blurred patches are staged in the wave's
+//      LDS slab (the next group's are loaded into registers meanwhile); lane = 4 of the 256
+//      tests of each; the nibbles are OR-combined by DPP into the descriptor dwords (LDS).
+//   C  the wave's descriptors (KP x 32 B) are written out with 16-byte stores.
+// Few keypoints per wave so that one XCD's resident waves cover few frames: a frame's level and
+// blur images (~1.4 MB of patch rows) then stay in that XCD's 4 MB L2 while its neighbouring
+// patches are read.  With 32 keypoints per wave an XCD had ~20 frames in flight and refetched
+// every patch row (4.6 MB per frame past L2 vs 0.95 MB when only ~2 frames were in flight,
+// tools/_exp_l2.sh).
+// Few wide loads per keypoint: with one byte per lane per load (lane = patch column) the
+// texture-address path, not the VALU, bounded this kernel.
+// The rotated pattern offsets are cvRound of |(px, py)| <= 13*sqrt(2), so |offset| <= 18.
+// Patch rows are 64 source bytes at an LDS pitch of 72 (18 dwords): consecutive rows land on
+// different banks, so the 64 lanes' scattered test samples rarely conflict (a 64-byte pitch put
+// every other row on the same 16 banks).
+constexpr int kBlRow = 72, kBlRows = 37, kBlChunks = kBlRows * 4;   // 148 16-byte chunks
+constexpr int kDescGroup = 2;                                        // patches staged per step
+template <int KP> constexpr int desc_slab() { return kBlRow * kBlRows * kDescGroup + 32 * KP; }
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};   // ORBextractor.cc:461-476
 
-// Disc mask of row |v| = av (av 16: all zero), dword d of a row read from patch column
-// u = -15 (bytes j = 4d..4d+3, u = j - 15): byte 0xFF where |u| <= umax[av].
+// Disc mask of row |v| = av (av 16: all zero), dword d of the realigned row (patch columns
+// j = 4d..4d+3, u = j - 15): byte 0xFF where |u| <= umax[av].
 __device__ __forceinline__ uint32_t ic_mask(int av, int d)
 {
     uint32_t w = 0;
@@ -1570,82 +1688,36 @@ __device__ __forceinline__ uint32_t dpp_or_shl4(uint32_t v)   // lane i |= lane 
 {
     return v | (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xf, 0xf, false);
 }
-__device__ __forceinline__ uint32_t wave_next(uint32_t v)      // lane i <- lane i+1 (wave_shl:1)
-{
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, false);
-}
 
-struct DescKey {
-    int l, x, y, sc;           // level, level coordinates, FAST score
-    int c0;                    // patch column origin (x - 21) & ~15 (may be negative)
-    bool fast;                 // the 64-byte rows lie inside the level row and its pitch
-};
-
-template <bool kVec0>
-__device__ __forceinline__ DescKey desc_key(const Plan* P, const ExtractBufs& b, int f, int id, int incl)
+// One IC row: 48 bytes from 16-byte aligned `rp` (kVec) or byte loads.
+template <bool kVec>
+__device__ __forceinline__ void ic_row_load(const uint8_t* rp, uint4& c0, uint4& c1, uint4& c2)
 {
-    DescKey k;
-    int l = 0, start = 0;
-    for (int q = 0; q < P->L - 1; q++) {
-        const int e = __builtin_amdgcn_readlane(incl, q);      // end of level q
-        if (id >= e) { l = q + 1; start = e; }
+    if (kVec) {
+        c0 = reinterpret_cast<const uint4*>(rp)[0];
+        c1 = reinterpret_cast<const uint4*>(rp)[1];
+        c2 = reinterpret_cast<const uint4*>(rp)[2];
+    } else {
+        uint32_t q[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++)
+            q[k] = (uint32_t)rp[4 * k] | ((uint32_t)rp[4 * k + 1] << 8) | ((uint32_t)rp[4 * k + 2] << 16) |
+                   ((uint32_t)rp[4 * k + 3] << 24);
+        c0 = make_uint4(q[0], q[1], q[2], q[3]);
+        c1 = make_uint4(q[4], q[5], q[6], q[7]);
+        c2 = make_uint4(q[8], q[9], q[10], q[11]);
     }
-    const LevelGeom& g = P->lv[l];
-    const uint32_t key = b.lvl_kp[(int64_t)f * P->lvl_stride + g.out_off + (id - start)];
-    k.l = l; k.x = key_x(key); k.y = key_y(key); k.sc = key_s(key);
-    k.c0 = (k.x - kPHalf) & ~15;
-    k.fast = (kVec0 || l != 0) && k.c0 >= 0 && k.x + kPHalf <= g.w - 1 && k.c0 + 64 <= g.pitch;
-    return k;
-}
-
-// chunk e of a patch: row e >> 2 (image row y - 21 + (e >> 2), reflected), bytes 16 (e & 3)..
-__device__ __forceinline__ u32x4 patch_chunk_fast(const uint8_t* img, int pitch, int h, int x0, int y, int e)
-{
-    const int rr = reflect101(y - kPHalf + (e >> 2), h);
-    return *reinterpret_cast<const u32x4*>(img + (int64_t)rr * pitch + x0 + 16 * (e & 3));
-}
-__device__ __forceinline__ u32x4 patch_chunk_slow(const uint8_t* img, int pitch, int w, int h, int x0, int y, int e)
-{
-    const uint8_t* row = img + (int64_t)reflect101(y - kPHalf + (e >> 2), h) * pitch;
-    uint32_t q[4];
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) v |= (uint32_t)row[reflect101(x0 + 16 * (e & 3) + 4 * d + i, w)] << (8 * i);
-        q[d] = v;
-    }
-    return u32x4{q[0], q[1], q[2], q[3]};
-}
-// chunk v (this lane's, chunk index e) into the four shifted copies; nx = the next chunk's first
-// dword (the next lane's: chunk e + 1; past a row's end its bytes are never read)
-__device__ __forceinline__ void patch_put4(uint8_t* slab, int e, u32x4 v, uint32_t nx, bool st)
-{
-    const uint32_t w[5] = {v.x, v.y, v.z, v.w, nx};
-    const int off = (e >> 2) * kPRow + 16 * (e & 3);
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        uint32_t s[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) s[i] = k ? __builtin_amdgcn_alignbyte(w[i + 1], w[i], (uint32_t)k) : w[i];
-        if (st) {
-            uint2* d = reinterpret_cast<uint2*>(slab + k * kPBytes + off);       // 8-byte aligned
-            d[0] = make_uint2(s[0], s[1]);
-            d[1] = make_uint2(s[2], s[3]);
-        }
-    }
-}
-// two dwords = patch bytes o .. o + 7 (o >= 0), as one aligned ds_read2_b32 of copy o & 3
-__device__ __forceinline__ void patch_read8(const uint8_t* slab, int o, uint32_t& lo, uint32_t& hi)
-{
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(slab + (o & 3) * kPBytes + (o & ~3));
-    lo = p[0];
-    hi = p[1];
 }
 
 template <bool kVec0, int KP>
+// 24 waves per CU (launch bound 6 blocks: 80 VGPRs, 3 spilled) measured 0.253 vs 0.212 ms/step
 __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ P, ExtractBufs b)
 {
+    constexpr int kLpk = 64 / KP;          // lanes per keypoint in phase A
+    constexpr int kHl = kLpk / 2;          // lanes per half (rows -|v| / +|v|)
+    constexpr int kNr = 16 / kHl;          // IC rows per lane
+    constexpr int kNb = kNr < 4 ? kNr : 4; // rows whose loads are in flight together
+    static_assert(KP >= 2 && KP <= 32 && (KP & (KP - 1)) == 0, "KP: power of two in [2, 32]");
     __shared__ __attribute__((aligned(16))) uint8_t s_slab[kWaves][desc_slab<KP>()];
     __shared__ __attribute__((aligned(16))) uint32_t s_msk[17][8];
     if (threadIdx.x < 17 * 8) s_msk[threadIdx.x >> 3][threadIdx.x & 7] = ic_mask(threadIdx.x >> 3, threadIdx.x & 7);
@@ -1666,12 +1738,81 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
     const int idx0 = (bxy.x * kWaves + wv) * KP;
     if (idx0 >= total) return;
     const int nk = min(KP, total - idx0);
-    const int* gk = P->gauss;
-    const int kv[7] = {gk[0], gk[1], gk[2], gk[3], gk[4], gk[5], gk[6]};
-    const uint32_t k0123 = (uint32_t)kv[0] | ((uint32_t)kv[1] << 8) | ((uint32_t)kv[2] << 16) | ((uint32_t)kv[3] << 24);
-    const uint32_t k4560 = (uint32_t)kv[4] | ((uint32_t)kv[5] << 8) | ((uint32_t)kv[6] << 16);
-    // pattern of this lane's tests 4*lane .. 4*lane+3
-    const int4 pa = reinterpret_cast<const int4*>(b.pattern)[lane];
+    // ---- phase A: lanes kq*kLpk .. +kLpk-1 = keypoint idx0 + kq (excess repeat the last one, no writes)
+    const int kq = lane / kLpk, half = (lane / kHl) & 1, qi = lane % kHl;
+    const int id = idx0 + min(kq, nk - 1);
+    int l = 0, start = 0;
+    for (int q = 0; q < L - 1; q++) {
+        const int e = __builtin_amdgcn_readlane(incl, q);      // end of level q
+        if (id >= e) { l = q + 1; start = e; }
+    }
+    const LevelGeom& g = P->lv[l];
+    const uint32_t key = b.lvl_kp[(int64_t)f * P->lvl_stride + g.out_off + (id - start)];
+    const int x = key_x(key), y = key_y(key), sc = key_s(key);
+    const uint8_t* img = level_ptr(P, b, f, l);
+    // IC_Angle (ORBextractor.cc:80-107): A = sum j*p, S = sum p over the disc, m01 = sum v*rowsum;
+    // lane (half, qi) takes rows |v| = qi + kHl*i, i < kNr (row 0 in the lower half only)
+    uint32_t A = 0, S = 0;
+    int m01 = 0;
+    const int a = (x - 15) & 15;
+    const uint32_t m8 = (a & 8) ? 0xFFFFFFFFu : 0u, m4 = (a & 4) ? 0xFFFFFFFFu : 0u;
+    const uint8_t* rowp = img + (int64_t)y * g.pitch + (x - 15 - a);         // row v = 0
+    const int64_t spitch = half ? (int64_t)g.pitch : -(int64_t)g.pitch;      // rows +|v| / -|v|
+    const bool vec = kVec0 || l != 0;
+#pragma unroll
+    for (int i0 = 0; i0 < kNr; i0 += kNb) {
+        uint4 c[kNb][3];
+#pragma unroll
+        for (int r = 0; r < kNb; r++) {
+            const uint8_t* rp = rowp + (qi + kHl * (i0 + r)) * spitch;
+            if (vec) ic_row_load<true>(rp, c[r][0], c[r][1], c[r][2]);
+            else ic_row_load<false>(rp, c[r][0], c[r][1], c[r][2]);
+        }
+#pragma unroll
+        for (int r = 0; r < kNb; r++) {
+            const int av = qi + kHl * (i0 + r);
+            const uint32_t* msk = s_msk[(av == 0 && half) ? 16 : av];
+            const uint32_t q[12] = {c[r][0].x, c[r][0].y, c[r][0].z, c[r][0].w, c[r][1].x, c[r][1].y,
+                                    c[r][1].z, c[r][1].w, c[r][2].x, c[r][2].y, c[r][2].z, c[r][2].w};
+            // realign by a: bit selects, then alignbyte
+            uint32_t r1[10], r2[9];
+#pragma unroll
+            for (int k = 0; k < 10; k++) r1[k] = (m8 & q[k + 2]) | (~m8 & q[k]);
+#pragma unroll
+            for (int k = 0; k < 9; k++) r2[k] = (m4 & r1[k + 1]) | (~m4 & r1[k]);
+            uint32_t rs = 0;
+#pragma unroll
+            for (int d = 0; d < 8; d++) {
+                const uint32_t pm = __builtin_amdgcn_alignbyte(r2[d + 1], r2[d], (uint32_t)(a & 3)) & msk[d];
+                A = __builtin_amdgcn_udot4(pm, 0x03020100u + 0x04040404u * (uint32_t)d, A, false);
+                rs = __builtin_amdgcn_udot4(pm, 0x01010101u, rs, false);
+            }
+            S += rs;
+            m01 += av * (int)rs;
+        }
+    }
+    if (half == 0) m01 = -m01;                 // lower half: rows -|v|
+#pragma unroll
+    for (int o = 1; o < kLpk; o <<= 1) {
+        A += __shfl_xor(A, o, 64);
+        S += __shfl_xor(S, o, 64);
+        m01 += __shfl_xor(m01, o, 64);
+    }
+    const int m10 = (int)A - 15 * (int)S;
+    const float angle = fast_atan2_dev((float)m01, (float)m10);
+    const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
+    float bs, ac;
+    sincos_canon(angle * factorPI, &bs, &ac);
+    if (lane % kLpk == 0 && kq < nk) {   // cv::KeyPoint {x, y, size, angle, response, octave, class_id}
+        float fx = (float)x, fy = (float)y;
+        if (l != 0) { fx *= g.scale; fy *= g.scale; }          // :1327-1334
+        KeyPointOut o;
+        o.x = fx; o.y = fy; o.size = (float)g.size_i; o.angle = angle; o.response = (float)sc;
+        o.octave = l; o.class_id = -1;
+        reinterpret_cast<KeyPointOut*>(b.kps)[(int64_t)f * P->kcap + idx0 + kq] = o;
+    }
+    // ---- phase B: descriptors (ORBextractor.cc:109-156), kDescGroup keypoints per step
+    const int4 pa = reinterpret_cast<const int4*>(b.pattern)[lane];   // tests 4*lane .. 4*lane+3
     float px0[4], py0[4], px1[4], py1[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
@@ -1680,115 +1821,79 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         px1[t] = (float)(int8_t)((pw >> 16) & 0xff); py1[t] = (float)(int8_t)(pw >> 24);
     }
     uint8_t* slab = s_slab[wv];
-    uint32_t* dsl = reinterpret_cast<uint32_t*>(slab + 4 * kPBytes);
-    const int e0 = lane, e1 = lane + 64, e2 = min(lane + 128, kPChunks - 1);
-    // IC lane roles: row v = (lane >> 1) - 15 (lanes 0..61), half = lane & 1 (16 bytes each)
-    const int icv = (lane >> 1) - 15, ich = lane & 1;
-    const bool icl = lane < 62;
-    const uint32_t* icm = s_msk[icv < 0 ? -icv : (icv > 15 ? 16 : icv)];
-    DescKey kn = desc_key<kVec0>(P, b, f, idx0, incl);
-    u32x4 q0, q1, q2;
-    auto load_fast = [&](const DescKey& k) {
-        if (!k.fast) return;
-        const LevelGeom& g = P->lv[k.l];
-        const uint8_t* img = level_ptr(P, b, f, k.l);
-        q0 = patch_chunk_fast(img, g.pitch, g.h, k.c0, k.y, e0);
-        q1 = patch_chunk_fast(img, g.pitch, g.h, k.c0, k.y, e1);
-        q2 = patch_chunk_fast(img, g.pitch, g.h, k.c0, k.y, e2);
-    };
-    load_fast(kn);
-    const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
-    for (int t = 0; t < nk; t++) {
-        const DescKey ck = kn;
-        if (!ck.fast) {
-            const LevelGeom& g = P->lv[ck.l];
-            const uint8_t* img = level_ptr(P, b, f, ck.l);
-            q0 = patch_chunk_slow(img, g.pitch, g.w, g.h, ck.c0, ck.y, e0);
-            q1 = patch_chunk_slow(img, g.pitch, g.w, g.h, ck.c0, ck.y, e1);
-            q2 = patch_chunk_slow(img, g.pitch, g.w, g.h, ck.c0, ck.y, e2);
+    uint32_t* dsl = reinterpret_cast<uint32_t*>(slab + kBlRow * kBlRows * kDescGroup);
+    // per keypoint: blurred patch origin (16-aligned) relative to the frame's blur block
+    const int porg = (int)g.blur_off + (y - 18) * g.bpitch + ((x - 18) & ~15);
+    const int xoff = x - ((x - 18) & ~15);        // patch column of the keypoint
+    const uint8_t* blur_f = b.blur + (int64_t)f * P->blur_stride;
+    const int bpitch = g.bpitch;
+    static_assert(kDescGroup == 2, "staging below is written for 2 patches per step");
+    uint4 qa0, qa1, qa2, qb0, qb1, qb2;
+    const int e0 = lane, e1 = lane + 64, e2 = min(lane + 128, kBlChunks - 1);
+    const int eo0 = (e0 >> 2), eo1 = (e1 >> 2), eo2 = (e2 >> 2);
+    const int ec0 = 16 * (e0 & 3), ec1 = 16 * (e1 & 3), ec2 = 16 * (e2 & 3);
+#define COEB_LOAD_PATCH(t, q0, q1, q2)                                                          \
+    {                                                                                           \
+        const int tt_ = min((t), nk - 1);                                                       \
+        const uint8_t* o_ = blur_f + __builtin_amdgcn_readlane(porg, tt_ * kLpk);               \
+        const int bpt_ = __builtin_amdgcn_readlane(bpitch, tt_ * kLpk);                         \
+        q0 = *reinterpret_cast<const uint4*>(o_ + eo0 * bpt_ + ec0);                            \
+        q1 = *reinterpret_cast<const uint4*>(o_ + eo1 * bpt_ + ec1);                            \
+        q2 = *reinterpret_cast<const uint4*>(o_ + eo2 * bpt_ + ec2);                            \
+    }
+    COEB_LOAD_PATCH(0, qa0, qa1, qa2)
+    COEB_LOAD_PATCH(1, qb0, qb1, qb2)
+    for (int t0 = 0; t0 < nk; t0 += kDescGroup) {
+        {
+            // chunk e -> row e >> 2, bytes 16 (e & 3) .. +15 (two 8-byte stores: the pitch is 8-aligned)
+            auto put = [&](uint8_t* base, int e, uint4 v) {
+                uint2* d = reinterpret_cast<uint2*>(base + (e >> 2) * kBlRow + 16 * (e & 3));
+                d[0] = make_uint2(v.x, v.y);
+                d[1] = make_uint2(v.z, v.w);
+            };
+            uint8_t* pb = slab + kBlRow * kBlRows;
+            put(slab, lane, qa0);
+            put(slab, lane + 64, qa1);
+            if (lane + 128 < kBlChunks) put(slab, lane + 128, qa2);
+            put(pb, lane, qb0);
+            put(pb, lane + 64, qb1);
+            if (lane + 128 < kBlChunks) put(pb, lane + 128, qb2);
         }
-        // next lane's first dwords: chunks e + 1 (lane 63's successor is chunk 64 = lane 0's q1)
-        const uint32_t n0 = wave_next(q0.x), n1 = wave_next(q1.x), n2 = wave_next(q2.x);
-        const uint32_t n0f = lane == 63 ? __builtin_amdgcn_readlane(q1.x, 0) : n0;
-        const uint32_t n1f = lane == 63 ? __builtin_amdgcn_readlane(q2.x, 0) : n1;
-        patch_put4(slab, e0, q0, n0f, true);
-        patch_put4(slab, e1, q1, n1f, true);
-        patch_put4(slab, e2, q2, n2, lane + 128 < kPChunks);
         wave_sync_lds();
-        if (t + 1 < nk) {                        // the next keypoint's rows in flight during this one
-            kn = desc_key<kVec0>(P, b, f, idx0 + t + 1, incl);
-            load_fast(kn);
+        if (t0 + kDescGroup < nk) {
+            COEB_LOAD_PATCH(t0 + 2, qa0, qa1, qa2)
+            COEB_LOAD_PATCH(t0 + 3, qb0, qb1, qb2)
         }
-        const int xo = ck.x - ck.c0;             // patch column of the keypoint (21..36)
-        const int ctr = kPHalf * kPRow + xo;     // patch byte offset of the keypoint
-        // ---- IC_Angle
-        uint32_t A = 0, S = 0;
-        int m01 = 0;
-        if (icl) {
-            const int o = ctr + icv * kPRow - 15 + 16 * ich;
-            uint32_t q[4];
-            patch_read8(slab, o, q[0], q[1]);
-            patch_read8(slab, o + 8, q[2], q[3]);
 #pragma unroll
-            for (int d = 0; d < 4; d++) {
-                const int dd = 4 * ich + d;
-                const uint32_t pm = q[d] & icm[dd];
-                A = __builtin_amdgcn_udot4(pm, 0x03020100u + 0x04040404u * (uint32_t)dd, A, false);
-                S = __builtin_amdgcn_udot4(pm, 0x01010101u, S, false);
+        for (int k = 0; k < kDescGroup; k++) {
+            const int t = t0 + k;
+            if (t >= nk) break;
+            const float tb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bs), t * kLpk));
+            const float ta = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ac), t * kLpk));
+            const uint8_t* bc = slab + k * kBlRow * kBlRows + 18 * kBlRow + __builtin_amdgcn_readlane(xoff, t * kLpk);
+            // (row, col) = (fma(px, b, py*a), fma(px, a, -(py*b))) as packed-f32 pairs: the same
+            // two roundings per component as the reference's fused forms, half the instructions
+            const f32x2 AB = {ta, tb}, BA = {tb, ta};
+            uint32_t nib = 0;
+#pragma unroll
+            for (int tt = 0; tt < 4; tt++) {
+                const f32x2 t0 = f32x2{py0[tt], py0[tt]} * AB, t1 = f32x2{py1[tt], py1[tt]} * AB;
+                const f32x2 rc0 = __builtin_elementwise_fma(f32x2{px0[tt], px0[tt]}, BA, f32x2{t0.x, -t0.y});
+                const f32x2 rc1 = __builtin_elementwise_fma(f32x2{px1[tt], px1[tt]}, BA, f32x2{t1.x, -t1.y});
+                // cvRound, then row * pitch + col exactly in f32 (|row|, |col| <= 18)
+                const int o0 = (int)__builtin_fmaf(rintf(rc0.x), (float)kBlRow, rintf(rc0.y));
+                const int o1 = (int)__builtin_fmaf(rintf(rc1.x), (float)kBlRow, rintf(rc1.y));
+                nib |= (uint32_t)(bc[o0] < bc[o1]) << tt;
             }
-            m01 = icv * (int)S;
+            // bit k of byte i = test 8i+k: dword d = nibbles of lanes 8d .. 8d+7
+            uint32_t dw = nib << (4 * (lane & 7));
+            dw = dpp_or_shl4(dpp_or_xor2(dpp_or_xor1(dw)));
+            if ((lane & 7) == 0) dsl[8 * t + (lane >> 3)] = dw;
         }
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            A += __shfl_xor(A, o, 64);
-            S += __shfl_xor(S, o, 64);
-            m01 += __shfl_xor(m01, o, 64);
-        }
-        const int m10 = (int)A - 15 * (int)S;
-        const float angle = fast_atan2_dev((float)m01, (float)m10);
-        float tb, ta;
-        sincos_canon(angle * factorPI, &tb, &ta);
-        if (lane == 0) {                          // cv::KeyPoint {x, y, size, angle, response, octave, class_id}
-            const LevelGeom& g = P->lv[ck.l];
-            float fx = (float)ck.x, fy = (float)ck.y;
-            if (ck.l != 0) { fx *= g.scale; fy *= g.scale; }          // :1327-1334
-            KeyPointOut o;
-            o.x = fx; o.y = fy; o.size = (float)g.size_i; o.angle = angle; o.response = (float)ck.sc;
-            o.octave = ck.l; o.class_id = -1;
-            reinterpret_cast<KeyPointOut*>(b.kps)[(int64_t)f * P->kcap + idx0 + t] = o;
-        }
-        // ---- tests: (row, col) = (fma(px, b, py*a), fma(px, a, -(py*b))) as packed-f32 pairs,
-        // the same two roundings per component as the reference's fused forms
-        const f32x2 AB = {ta, tb}, BA = {tb, ta};
-        auto blur_at = [&](int r, int c) {
-            const int o = ctr + (r - 3) * kPRow + (c - 3);
-            uint32_t acc = 1u << 15;
-#pragma unroll
-            for (int i = 0; i < 7; i++) {
-                uint32_t lo, hi;
-                patch_read8(slab, o + i * kPRow, lo, hi);
-                const uint32_t hs = __builtin_amdgcn_udot4(lo, k0123, __builtin_amdgcn_udot4(hi, k4560, 0u, false), false);
-                acc += __umul24((uint32_t)kv[i], hs);            // v_mad_u32_u24
-            }
-            return acc >> 16;
-        };
-        uint32_t nib = 0;
-#pragma unroll
-        for (int tt = 0; tt < 4; tt++) {
-            const f32x2 u0 = f32x2{py0[tt], py0[tt]} * AB, u1 = f32x2{py1[tt], py1[tt]} * AB;
-            const f32x2 rc0 = __builtin_elementwise_fma(f32x2{px0[tt], px0[tt]}, BA, f32x2{u0.x, -u0.y});
-            const f32x2 rc1 = __builtin_elementwise_fma(f32x2{px1[tt], px1[tt]}, BA, f32x2{u1.x, -u1.y});
-            const uint32_t v0 = blur_at((int)rintf(rc0.x), (int)rintf(rc0.y));
-            const uint32_t v1 = blur_at((int)rintf(rc1.x), (int)rintf(rc1.y));
-            nib |= (uint32_t)(v0 < v1) << tt;
-        }
-        // bit k of byte i = test 8i+k: dword d = nibbles of lanes 8d .. 8d+7
-        uint32_t dw = nib << (4 * (lane & 7));
-        dw = dpp_or_shl4(dpp_or_xor2(dpp_or_xor1(dw)));
-        if ((lane & 7) == 0) dsl[8 * t + (lane >> 3)] = dw;
         wave_sync_lds();                         // patch reads done before the next staging
     }
-    // ---- descriptors out
+#undef COEB_LOAD_PATCH
+    // ---- phase C: descriptors out
     uint4* gd = reinterpret_cast<uint4*>(b.desc + ((int64_t)f * P->kcap + idx0) * 32);
     if (lane < 2 * nk) gd[lane] = reinterpret_cast<const uint4*>(dsl)[lane];
 }
@@ -1821,11 +1926,33 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     prof_begin(prof, "k_dynmask", s);
     hipLaunchKernelGGL(k_dynmask, dim3((F + 63) / 64), dim3(64), 0, s, b, F, plan.W, plan.H);
     prof_end(prof, s);
+    BlurWork bw;
+    bw.L = plan.L;
+    int items = 0;
+    for (int l = 0; l < plan.L; l++) {
+        const LevelGeom& g = plan.lv[l];
+        bw.nstrips[l] = (g.w + kBlurCols - 1) / kBlurCols;
+        // 64 rows per wave item (4 bands): 32-, 128- and 256-row items measured slower, also with
+        // the next row block's loads issued before the current one is filtered (0.190 ms either way)
+        const int nbands = 4 * ((g.h + 63) / 64);
+        bw.bh[l] = (g.h + nbands - 1) / nbands;
+        bw.item_off[l] = items;
+        items += bw.nstrips[l] * (nbands / 4);
+    }
+    bw.item_off[plan.L] = items;
     // COEB_FAST_RB=72 forces the general slab layout (tests run both layouts)
     const char* frb = getenv("COEB_FAST_RB");
     const int fast_rbytes = frb && atoi(frb) == kFastRowBytes ? kFastRowBytes : fast_rb(plan);
     const int fast_lds = kWaves * fast_wave_lds(plan, fast_rbytes);
     constexpr int kFastPerBlock = kWaves;
+    auto blur = [&](hipStream_t st, int i0, int i1) {
+        if (i1 <= i0) return;
+        BlurWork w = bw;
+        w.item0 = i0; w.item1 = i1;
+        prof_begin(prof, "k_blur", st);
+        hipLaunchKernelGGL(k_blur, dim3((i1 - i0 + kWaves - 1) / kWaves, F), dim3(kThreads), 0, st, d_plan, b, w);
+        prof_end(prof, st);
+    };
     // FAST over levels [l0, l1): one wave per cell.  A band form (one LDS copy per cell-row
     // segment, each image row fetched once) measured slower and was removed.
     auto fast = [&](hipStream_t st, int l0, int l1) {
@@ -1838,14 +1965,15 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
                            st, d_plan, b, b.cells, c0, c1);
         prof_end(prof, st);
     };
-    // level 0 (the input frame itself) needs no pyramid: with a side stream its FAST overlaps the
-    // cascaded pyramid launches, whose small late levels leave most CUs idle; levels 1..m-1
-    // follow on the side stream as soon as the pyramid has built them
+    // level 0 (the input frame itself) needs no pyramid: with a side stream its blur and FAST
+    // overlap the cascaded pyramid launches, whose small late levels leave most CUs idle; levels
+    // 1..m-1 follow on the side stream as soon as the pyramid has built them
     const bool split = side && side->s && plan.L > 1;
     const int m = split ? std::min(std::max(side->split, 1), plan.L) : 0;
     if (split) {
         (void)hipEventRecord(side->fork, s);                 // after k_dynmask (area_flag -> FAST thresholds)
         (void)hipStreamWaitEvent(side->s, side->fork, 0);
+        blur(side->s, 0, bw.item_off[1]);
         fast(side->s, 0, 1);
     }
     for (int l = 1; l < plan.L; l++) {
@@ -1863,6 +1991,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         if (split && m > 1 && l == m - 1) {
             (void)hipEventRecord(side->mid, s);
             (void)hipStreamWaitEvent(side->s, side->mid, 0);
+            blur(side->s, bw.item_off[1], bw.item_off[m]);
             fast(side->s, 1, m);
         }
     }
@@ -1874,24 +2003,49 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         hipLaunchKernelGGL(k_octree<kOctThreads>, dim3(F, l1 - l0), dim3(kOctThreads), plan.oct_lds, st, d_plan, b, l0);
         prof_end(prof, st);
     };
-    // the octree of the side levels may follow their FAST there (COEB_SIDE_OCTREE=1); s joins the
-    // side stream once, before its own octree launch
-    const bool soct = split && side->side_octree;
+    // the late blur goes to the side stream (beside FAST / octree, which do not read it) and the
+    // octree of the side levels follows their FAST there; s joins before the descriptors
+    const bool late = split && side->blur_late;
+    const bool soct = late && side->side_octree;
     if (soct) octree(side->s, 0, m);
     if (split) (void)hipEventRecord(side->join, side->s);
+    if (late) {
+        (void)hipEventRecord(side->pyr_done, s);
+        (void)hipStreamWaitEvent(side->s, side->pyr_done, 0);
+        blur(side->s, bw.item_off[m], items);
+        (void)hipEventRecord(side->join2, side->s);
+    } else {
+        blur(s, split ? bw.item_off[m] : 0, items);
+    }
     fast(s, split ? m : 0, plan.L);
+    // one cross-stream wait on the critical path instead of two: each costs a ~6 us gap between
+    // the launches it separates (rocprofv3 timeline), and the late blur ends well before FAST
+    // does, so waiting for all of the side stream (join2) before the octree delays nothing
     if (soct) {
         octree(s, m, plan.L);
-        (void)hipStreamWaitEvent(s, side->join, 0);
+        (void)hipStreamWaitEvent(s, late ? side->join2 : side->join, 0);
     } else {
-        if (split) (void)hipStreamWaitEvent(s, side->join, 0);
+        if (split) (void)hipStreamWaitEvent(s, late ? side->join2 : side->join, 0);
         octree(s, 0, plan.L);
     }
     prof_begin(prof, "k_describe", s);
     const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
-    constexpr int KP = 8;                  // keypoints per wave (few: a frame's patches stay in one L2)
-    hipLaunchKernelGGL((vec0 ? k_describe<true, KP> : k_describe<false, KP>),
-                       dim3((plan.kcap + kWaves * KP - 1) / (kWaves * KP), F), dim3(kThreads), 0, s, d_plan, b);
+    // keypoints per wave: 8 (COEB_DESC_KP = 4 / 16 / 32 for experiments; 32 was round 1's form)
+    static const int kp = [] { const char* e = getenv("COEB_DESC_KP"); const int v = e ? atoi(e) : 8;
+                               return v == 4 || v == 16 || v == 32 ? v : 8; }();
+    auto describe = [&](auto kv, auto kpc) {
+        constexpr int KP = decltype(kpc)::value;
+        hipLaunchKernelGGL((k_describe<decltype(kv)::value, KP>), dim3((plan.kcap + kWaves * KP - 1) / (kWaves * KP), F),
+                           dim3(kThreads), 0, s, d_plan, b);
+    };
+    using T = std::true_type;
+    using Fl = std::false_type;
+    switch (kp) {
+        case 4: vec0 ? describe(T{}, std::integral_constant<int, 4>{}) : describe(Fl{}, std::integral_constant<int, 4>{}); break;
+        case 16: vec0 ? describe(T{}, std::integral_constant<int, 16>{}) : describe(Fl{}, std::integral_constant<int, 16>{}); break;
+        case 32: vec0 ? describe(T{}, std::integral_constant<int, 32>{}) : describe(Fl{}, std::integral_constant<int, 32>{}); break;
+        default: vec0 ? describe(T{}, std::integral_constant<int, 8>{}) : describe(Fl{}, std::integral_constant<int, 8>{}); break;
+    }
     prof_end(prof, s);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -3,6 +3,7 @@
 // HBM layout (per frame slot f of a context, all packed, byte offsets 256-aligned):
 //   gray      [f][H][W]                 u8   level 0 (caller's device buffer or ctx staging)
 //   pyr       [f][pyr_stride]           u8   levels 1..L-1, level l at pyr_off[l], row stride W_l
+//   blur      [f][blur_stride]          u8   7x7 Gaussian of levels 0..L-1 (descriptor input)
 //   cand_n    [f][ncells]               i32  FAST corners kept per cell
 //   cand      [f][ncells][cell_cap]     u32  packed (x_rel | y_rel<<12 | score<<24), row-major
 //   keys      [f][2][kbuf_stride]       u32  octree key ping-pong buffers (per level kcap_off)
@@ -27,7 +28,9 @@
 struct LevelGeom {
     int w, h;
     int pitch;             // row pitch of the level image (level 0: W; levels >= 1: 64-byte multiple)
+    int bpitch;            // row pitch of the blurred level (64-byte multiple)
     int64_t pyr_off;       // into pyr frame block (-1 for level 0)
+    int64_t blur_off;      // into blur frame block
     int rtab_off;          // into resize table (ints): xofs[w], alpha[w], yofs[h], beta[h]
     int xmax;              // resize: columns >= xmax use S[sx]*2048
     int ncols, nrows, wcell, hcell;
@@ -51,7 +54,7 @@ struct Plan {
     int ncells;            // all levels
     int cell_cap;          // u32 entries per cell slot
     int max_roi_w, max_roi_h;
-    int64_t pyr_stride;
+    int64_t pyr_stride, blur_stride;
     int64_t kbuf_stride;   // u32 entries per key buffer (x2 per frame)
     int64_t node_stride;   // node records per frame (all levels, both sets)
     int lvl_stride;        // u32 entries per frame in lvl_kp
@@ -103,6 +106,7 @@ int fast_timing_read(unsigned long long* out);   // COEB_FAST_CLOCK builds: per-
 struct ExtractBufs {
     const uint8_t* gray;   // [F][H][W]
     uint8_t* pyr;
+    uint8_t* blur;
     int* cand_n;
     uint32_t* cand;
     uint32_t* keys;
@@ -136,11 +140,13 @@ struct ProfileHook {
 void prof_begin(ProfileHook* p, const char* name, hipStream_t s);
 void prof_end(ProfileHook* p, hipStream_t s);
 
-// side (optional): FAST of level 0 runs on side.s while the pyramid builds levels 1..; that of
-// levels 1..split-1 follows there once the pyramid has built them, and s does levels split..L-1
-// after the pyramid; s joins side.s before the octree.  With side_octree, the octree of levels
-// < split follows their FAST on side.s and s joins after its own octree launch.
-struct SideStream { hipStream_t s; hipEvent_t fork, mid, join; int split; bool side_octree; };
+// side (optional): blur + FAST of level 0 run on side.s while the pyramid builds levels 1..;
+// those of levels 1..split-1 follow there once the pyramid has built them, and s does levels
+// split..L-1 after the pyramid; s joins side.s before the octree.
+// With blur_late, the blur of levels split..L-1 also runs on side.s (after the pyramid, beside
+// FAST and the octree on s); s then joins it (join2) only before the descriptors.
+// With side_octree, the octree of levels < split follows their FAST on side.s.
+struct SideStream { hipStream_t s; hipEvent_t fork, mid, join, pyr_done, join2; int split; bool blur_late, side_octree; };
 int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, int F, hipStream_t s,
                    ProfileHook* prof, const SideStream* side = nullptr);
 

@@ -29,9 +29,9 @@ WIDE16 = ("k_pyr_level", "k_fast", "k_describe")
 def traffic_json(merged, nd, frames, command, fetch_scale, wide_scale=2.0, wide=WIDE16):
     """Per kernel, HBM bytes per launch: scale x FETCH_SIZE + WRITE_SIZE (rocprofv3 KB).
     MI355X_MICROARCH.md s HBM: on gfx950 FETCH_SIZE reports 1/2 of the bytes of 16-B-per-lane
-    reads, so kernels in `wide` get wide_scale = 2.  The kernels loading <= 4 B per lane keep
-    fetch_scale = 1 (round 2 calibrated that on its separable-blur kernel: raw FETCH_SIZE matched
-    the bytes it was known to read)."""
+    reads, so kernels in `wide` get wide_scale = 2.  The kernels loading <= 4 B per lane are
+    calibrated on k_blur (each level byte read once plus the 6-row vertical halo, each written
+    once): raw FETCH_SIZE ~ its known read bytes, so fetch_scale = 1 for them."""
     out = dict(frames_per_launch=frames, command=command, fetch_scale=fetch_scale, wide_kernels=list(wide),
                wide_scale=wide_scale,
                correction="bytes = (s * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch, mean over dispatches; "
