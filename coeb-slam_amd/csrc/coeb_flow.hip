@@ -48,7 +48,7 @@ extern "C" ProfileHook* coeb_internal_prof(coeb_ctx* c);
 
 namespace {
 
-__device__ int g_subpix_count_dev[2];
+__device__ int g_subpix_count_dev[4];   // {cornerSubPix iterations, corners, LK iterations, points}
 int* g_subpix_count = nullptr;    // device address of g_subpix_count_dev (COEB_SUBPIX_COUNT, A/B tool)
 
 constexpr int kMaxPts = 1024;        // corners / tracked points per call (reference: 1000)
@@ -440,22 +440,172 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
 }
 
 // ============================== cornerSubPix ==============================
-// One lane per corner, 64 corners per wave.  The five window sums (cornersubpix.cpp) are
-// double-precision running sums in row-major order over the 21 x 21 window, so each corner's
-// sums are inherently sequential; with a lane per corner every lane runs its own five chains
-// (independent of each other, so the adds of one element overlap) and all 64 lanes do useful
-// work.  The 23 x 23 getRectSubPix window is never stored: it is produced one row at a time
-// into registers (rows r-2, r-1, r rotate through R0 / R1 / R2) from the two pixel rows it
-// interpolates, loaded as dwords per lane one row ahead of use, and sum row r - 2 consumes the
-// three rows as soon as row r exists.  The weights are a double table read with scalar loads
-// (the element index is wave-uniform).
-// (Round 2 used one wave per corner: all lanes formed the five terms of 64 window pixels into
-// LDS and lanes 0..4 summed them, so every add of the 2205-long chain per iteration issued a
-// whole wave instruction for 5 lanes: 1.5-1.7 ms per 256 pairs of ~150 corners.)
-// itcount (COEB_SUBPIX_COUNT): {iterations, corners} for tools.
-__device__ __forceinline__ float ubyte_f(uint32_t q, int k)      // byte k of q as float (v_cvt_f32_ubyteN)
+// One wave per corner.  Per iteration all 64 lanes fill the 23 x 23 getRectSubPix window into
+// LDS (from the corner's 40 x 40 pixels, staged once; the window may drift 8 px before the image
+// is read directly) and form the five per-pixel terms of 64 window pixels at a time; lanes 0..4
+// then run the five double sums in the reference's row-major order -- each a chain of 441
+// dependent adds per iteration, the kernel's critical path.  The terms of an element pair sit
+// together per term ([pair][term][2] doubles), so the five summing lanes read 80 consecutive
+// bytes with one ds_read_b128 each: no bank conflicts, and one LDS read per two adds.  (Round 2
+// stored them term-major, [term][64]: the five lanes' addresses 512 B apart hit one bank, 2.6e8
+// conflict cycles per launch, 1.5-1.7 ms per 256 pairs; one lane per corner with all five sums
+// in its own registers issued ~12 k instructions per iteration on one lane's worth of corners:
+// 1.9 ms.)  itcount (COEB_SUBPIX_COUNT): {iterations, corners} for tools.
+constexpr int kSpRA = 4;                 // term pairs read ahead of the adds
+template <int WIN>
+__global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0, int w, int h, int stride,
+                                               float* __restrict__ xy0, const int* __restrict__ offs, int P,
+                                               const int* __restrict__ order, const double* __restrict__ maskd,
+                                               int iters, double eps2, int64_t iz, int64_t pz, int* __restrict__ itcount)
 {
-    return (float)((q >> (8 * k)) & 0xFFu);
+    constexpr int WW = 2 * WIN + 1, BW = WW + 2, NB = BW * BW, NK = WW * WW;
+    constexpr int KPL = (NK + 63) / 64;                // terms per lane
+    constexpr int kSpM = 8, SS = BW + 1 + 2 * kSpM;    // staged pixels: window + drift margin
+    __shared__ float buf[NB];
+    __shared__ __attribute__((aligned(16))) double s_t[32][5][2];   // [element pair][term][element]
+    __shared__ uint8_t px8[SS * SS];
+    const int lane = threadIdx.x;
+    const int total = offs[P];
+    for (int it_ = blockIdx.x; it_ < total; it_ += gridDim.x) {
+    const int item = order[it_];
+    const int2 zp = flow_item(offs, P, item);
+    const uint8_t* img = at_pair(img0, iz, (uint32_t)zp.x);
+    float* xy = at_pair(xy0, pz, (uint32_t)zp.x);
+    const int p = zp.y;
+    // the previous corner's last reads of px8 / buf / s_t are done before they are rewritten
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const float tx = xy[2 * p], ty = xy[2 * p + 1];
+    const int R0x = cv_floor(tx - (float)(BW - 1) * 0.5f) - kSpM, R0y = cv_floor(ty - (float)(BW - 1) * 0.5f) - kSpM;
+    const bool staged = R0x >= 0 && R0y >= 0 && R0x + SS <= w && R0y + SS <= h;
+    if (staged) {
+        const uint8_t* g = img + (size_t)R0y * stride + R0x;
+#pragma unroll 5
+        for (int q = 0; q < (SS * SS + 63) / 64; q++) {
+            const int e = lane + 64 * q;
+            if (e < SS * SS) { const int r = e / SS; px8[e] = g[(size_t)r * stride + (e - r * SS)]; }
+        }
+    }
+    float cx = tx, cy = ty;
+    int it = 0;
+    double err = 0;
+    // getRectSubPix_8u32f's in-image window from rows of `src` (image or staged pixels)
+    auto fill_in = [&](const uint8_t* src0, int sst, float a, float b) {
+        a = a < 0.0001f ? 0.0001f : a;
+        const float a12 = a * (1.f - b), a22 = a * b, b1 = 1.f - b, b2 = b;
+        const double sd = (1. - (double)a) / (double)a;
+#pragma unroll 3
+        for (int e = lane; e < NB; e += 64) {
+            const int r = e / BW, j = e - r * BW;
+            const uint8_t* src = src0 + r * sst;
+            const float t = a12 * (float)src[j + 1] + a22 * (float)src[j + 1 + sst];
+            float prev;
+            if (j == 0) prev = (1.f - a) * (b1 * (float)src[0] + b2 * (float)src[sst]);
+            else {
+                const float tp = a12 * (float)src[j] + a22 * (float)src[j + sst];
+                prev = (float)((double)tp * sd);
+            }
+            buf[e] = prev + t;
+        }
+    };
+    do {
+        const float ctrx = cx - (float)(BW - 1) * 0.5f, ctry = cy - (float)(BW - 1) * 0.5f;
+        const int ipx = cv_floor(ctrx), ipy = cv_floor(ctry);
+        if (ipx >= 0 && ipx + BW < w && ipy >= 0 && ipy + BW < h) {
+            const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
+            if (staged && ipx >= R0x && ipy >= R0y && ipx + BW < R0x + SS && ipy + BW < R0y + SS) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // staged pixels visible
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                fill_in(px8 + (ipy - R0y) * SS + (ipx - R0x), SS, a, b);
+            } else {
+                fill_in(img + (size_t)ipy * stride + ipx, stride, a, b);
+            }
+        } else {
+            const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
+            const float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
+            const float b1 = 1.f - b, b2 = b;
+#pragma unroll 1
+            for (int e = lane; e < NB; e += 64) {
+                const int r = e / BW, j = e - r * BW;
+                const int y0 = min(max(ipy + r, 0), h - 1), y1 = min(max(ipy + r + 1, 0), h - 1);
+                const uint8_t* r0 = img + (size_t)y0 * stride;
+                const uint8_t* r1 = img + (size_t)y1 * stride;
+                const int c = ipx + j;
+                float v;
+                if (c < 0) v = (float)r0[0] * b1 + (float)r1[0] * b2;
+                else if (c >= w - 1) v = (float)r0[w - 1] * b1 + (float)r1[w - 1] * b2;
+                else v = (float)r0[c] * a11 + (float)r0[c + 1] * a12 + (float)r1[c] * a21 + (float)r1[c + 1] * a22;
+                buf[e] = v;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        double acc = 0;
+#pragma unroll 1
+        for (int q = 0; q < KPL; q++) {
+            const int k = lane + 64 * q;
+            double gxx = 0.0, gxy = 0.0, gyy = 0.0, t3 = 0.0, t4 = 0.0;    // +0.0 past the window
+            if (k < NK) {
+                const int i = k / WW, j = k - i * WW;
+                const float* sp = buf + (i + 1) * BW + 1;
+                const double m = maskd[k];
+                const double tgx = (double)(sp[j + 1] - sp[j - 1]);
+                const double tgy = (double)(sp[j + BW] - sp[j - BW]);
+                gxx = tgx * tgx * m; gxy = tgx * tgy * m; gyy = tgy * tgy * m;
+                const double px = j - WIN, py = i - WIN;
+                t3 = gxx * px + gxy * py;
+                t4 = gxy * px + gyy * py;
+            }
+            double* st = &s_t[lane >> 1][0][lane & 1];
+            st[0] = gxx; st[2] = gxy; st[4] = gyy; st[6] = t3; st[8] = t4;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (lane < 5) {
+                // lane = term; element pairs in order, read kSpRA pairs ahead of the adds
+                const double2* tp = reinterpret_cast<const double2*>(&s_t[0][lane][0]);   // stride 5 per pair
+                double2 cur[kSpRA];
+#pragma unroll
+                for (int u = 0; u < kSpRA; u++) cur[u] = tp[5 * u];
+#pragma unroll 1
+                for (int k0 = kSpRA; k0 <= 32; k0 += kSpRA) {
+                    double2 nx[kSpRA];
+                    const int k1 = k0 < 32 ? k0 : 0;
+#pragma unroll
+                    for (int u = 0; u < kSpRA; u++) nx[u] = tp[5 * (k1 + u)];
+#pragma unroll
+                    for (int u = 0; u < kSpRA; u++) { acc += cur[u].x; acc += cur[u].y; }
+#pragma unroll
+                    for (int u = 0; u < kSpRA; u++) cur[u] = nx[u];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");     // the next 64 overwrite these
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        const double sa = __shfl(acc, 0, 64), sb = __shfl(acc, 1, 64), sc = __shfl(acc, 2, 64);
+        const double bb1 = __shfl(acc, 3, 64), bb2 = __shfl(acc, 4, 64);
+        const double det = sa * sc - sb * sb;
+        if (fabs(det) <= DBL_EPSILON * DBL_EPSILON) break;
+        const double scale = 1.0 / det;
+        const float nx = (float)((double)cx + sc * scale * bb1 - sb * scale * bb2);
+        const float ny = (float)((double)cy - sb * scale * bb1 + sa * scale * bb2);
+        err = (double)((nx - cx) * (nx - cx) + (ny - cy) * (ny - cy));
+        cx = nx; cy = ny;
+        if (cx < 0 || cx >= (float)w || cy < 0 || cy >= (float)h) break;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } while (++it < iters && err > eps2);
+    if (fabsf(cx - tx) > (float)WIN || fabsf(cy - ty) > (float)WIN) { cx = tx; cy = ty; }
+    if (lane == 0) {
+        xy[2 * p] = cx; xy[2 * p + 1] = cy;
+        if (itcount) { atomicAdd(itcount, it + 1); atomicAdd(itcount + 1, 1); }
+    }
+    }
 }
 
 // cornerSubPix work order: the corners whose window may leave the image (getRectSubPix's
@@ -489,132 +639,6 @@ __global__ __launch_bounds__(256) void k_subpix_order(const float* __restrict__ 
         bb = __builtin_amdgcn_readfirstlane(bb);
         if (in) order[bi + __popcll(mi & lt)] = item;
         if (bd) order[total - 1 - (bb + __popcll(mb & lt))] = item;
-    }
-}
-
-template <int WIN>
-__global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0, int w, int h, int stride,
-                                               float* __restrict__ xy0, const int* __restrict__ offs, int P,
-                                               const int* __restrict__ order, const double* __restrict__ maskd,
-                                               int iters, double eps2, int64_t iz, int64_t pz, int* __restrict__ itcount)
-{
-    constexpr int WW = 2 * WIN + 1, BW = WW + 2;          // 21 x 21 window, 23 x 23 interpolated
-    constexpr int NQ = (BW + 1 + 3) / 4;                   // dwords of a 24-pixel row
-    const int lane = threadIdx.x;
-    const int total = offs[P];
-    const int step = gridDim.x * 64;
-    for (int base = blockIdx.x * 64; base < total; base += step) {
-        if (base + lane >= total) break;
-        const int item = order[base + lane];
-        const int2 zp = flow_item(offs, P, item);
-        const uint8_t* img = at_pair(img0, iz, (uint32_t)zp.x);
-        float* xy = at_pair(xy0, pz, (uint32_t)zp.x);
-        const int p = zp.y;
-        const float tx = xy[2 * p], ty = xy[2 * p + 1];
-        float cx = tx, cy = ty;
-        int it = 0;
-        double err = 0;
-        do {
-            const float ctrx = cx - (float)(BW - 1) * 0.5f, ctry = cy - (float)(BW - 1) * 0.5f;
-            const int ipx = cv_floor(ctrx), ipy = cv_floor(ctry);
-            const bool inimg = ipx >= 0 && ipx + BW < w && ipy >= 0 && ipy + BW < h;
-            const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
-            // getRectSubPix_8u32f (in-image): a clamped to 1e-4, prev(j) = (float)(t(j-1) * s)
-            const float ai = a < 0.0001f ? 0.0001f : a;
-            const float a12 = ai * (1.f - b), a22 = ai * b, b1 = 1.f - b, b2 = b, pa = 1.f - ai;
-            const double sd = (1. - (double)ai) / (double)ai;
-            // getRectSubPix_Cn_ (the window leaves the image): clamped rows, 2-term edge columns
-            const float c11 = (1.f - a) * (1.f - b), c12 = a * (1.f - b), c21 = (1.f - a) * b, c22 = a * b;
-            // pixel row y (24 px from ipx) as dwords; the last dword read is the one holding the
-            // row's pixel ipx + 23, so nothing past the row's last needed pixel is touched
-            const uint8_t* rbase = img + ipx;
-            auto load_row = [&](int y, uint32_t* q) {
-                const uint8_t* pr = rbase + (int64_t)y * stride;
-                const uintptr_t pa4 = reinterpret_cast<uintptr_t>(pr) & ~(uintptr_t)3;
-                const uint32_t* a4 = reinterpret_cast<const uint32_t*>(pa4);
-                const uint32_t* last = reinterpret_cast<const uint32_t*>((reinterpret_cast<uintptr_t>(pr) + BW) & ~(uintptr_t)3);
-                const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(pr) & 3);
-                uint32_t d[NQ + 1];
-#pragma unroll
-                for (int k = 0; k <= NQ; k++) d[k] = *(a4 + k < last ? a4 + k : last);
-#pragma unroll
-                for (int k = 0; k < NQ; k++) q[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-            };
-            // branch-free: all four taps from clamped addresses (every load issued up front), the
-            // edge columns' two-term value selected
-            auto fill_border = [&](int r, float* R) {
-                const uint8_t* r0 = img + (int64_t)min(max(ipy + r, 0), h - 1) * stride;
-                const uint8_t* r1 = img + (int64_t)min(max(ipy + r + 1, 0), h - 1) * stride;
-                uint8_t p0[BW + 1], p1[BW + 1];
-#pragma unroll
-                for (int j = 0; j <= BW; j++) {
-                    const int c = min(max(ipx + j, 0), w - 1);
-                    p0[j] = r0[c];
-                    p1[j] = r1[c];
-                }
-#pragma unroll
-                for (int j = 0; j < BW; j++) {
-                    const int c = ipx + j;
-                    const float e = (float)p0[j] * b1 + (float)p1[j] * b2;
-                    const float v = (float)p0[j] * c11 + (float)p0[j + 1] * c12 + (float)p1[j] * c21 + (float)p1[j + 1] * c22;
-                    R[j] = (c < 0 || c >= w - 1) ? e : v;
-                }
-            };
-            uint32_t qa[NQ], qb[NQ];                       // pixel rows ipy + r, ipy + r + 1
-            if (inimg) { load_row(ipy, qa); load_row(ipy + 1, qb); }
-            auto fill_in = [&](float* R) {
-                float prev = pa * (b1 * ubyte_f(qa[0], 0) + b2 * ubyte_f(qb[0], 0));
-#pragma unroll
-                for (int j = 0; j < BW; j++) {
-                    const float t = a12 * ubyte_f(qa[(j + 1) >> 2], (j + 1) & 3) + a22 * ubyte_f(qb[(j + 1) >> 2], (j + 1) & 3);
-                    R[j] = prev + t;
-                    prev = (float)((double)t * sd);
-                }
-            };
-            float R0[BW], R1[BW], R2[BW];
-            double sa = 0, sb = 0, sc = 0, sb1 = 0, sb2 = 0;
-            for (int r = 0; r < BW; r++) {
-                if (inimg) {
-                    fill_in(R2);
-                    if (r + 1 < BW) {                      // next pixel row pair: rows ipy + r + 1, + 2
-#pragma unroll
-                        for (int k = 0; k < NQ; k++) qa[k] = qb[k];
-                        load_row(ipy + r + 2, qb);
-                    }
-                } else {
-                    fill_border(r, R2);
-                }
-                if (r >= 2) {
-                    const int i = r - 2;
-                    const double py = (double)(i - WIN);
-                    const double* mrow = maskd + i * WW;
-#pragma unroll
-                    for (int j = 0; j < WW; j++) {
-                        const double m = mrow[j];
-                        const double tgx = (double)(R1[j + 2] - R1[j]);
-                        const double tgy = (double)(R2[j + 1] - R0[j + 1]);
-                        const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
-                        const double px = (double)(j - WIN);
-                        sa += gxx; sb += gxy; sc += gyy;
-                        sb1 += gxx * px + gxy * py;
-                        sb2 += gxy * px + gyy * py;
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < BW; j++) { R0[j] = R1[j]; R1[j] = R2[j]; }
-            }
-            const double det = sa * sc - sb * sb;
-            if (fabs(det) <= DBL_EPSILON * DBL_EPSILON) break;
-            const double scale = 1.0 / det;
-            const float nx = (float)((double)cx + sc * scale * sb1 - sb * scale * sb2);
-            const float ny = (float)((double)cy - sb * scale * sb1 + sa * scale * sb2);
-            err = (double)((nx - cx) * (nx - cx) + (ny - cy) * (ny - cy));
-            cx = nx; cy = ny;
-            if (cx < 0 || cx >= (float)w || cy < 0 || cy >= (float)h) break;
-        } while (++it < iters && err > eps2);
-        if (fabsf(cx - tx) > (float)WIN || fabsf(cy - ty) > (float)WIN) { cx = tx; cy = ty; }
-        xy[2 * p] = cx; xy[2 * p + 1] = cy;
-        if (itcount) { atomicAdd(itcount, it + 1); atomicAdd(itcount + 1, 1); }
     }
 }
 
@@ -747,7 +771,7 @@ __device__ __forceinline__ void load12(const uint8_t* p, int n, uint32_t* q)
 
 __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__ pxy0, const int* __restrict__ offs, int P,
                                             float* __restrict__ nxy0, uint8_t* __restrict__ status0, int win, int max_count,
-                                            double eps2, int64_t iz, int64_t pz)
+                                            double eps2, int64_t iz, int64_t pz, int* __restrict__ itcount)
 {
     const int lane = threadIdx.x & 63;
     const int hwid = (win + 1) >> 1;
@@ -767,6 +791,7 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
     float nx = 0.f, ny = 0.f;
     const float px0 = pxy[2 * p], py0 = pxy[2 * p + 1];
     int iv[kLkHP], gxv[kLkHP], gyv[kLkHP];
+    int nit = 0;
     for (int level = pyr.L - 1; level >= 0; level--) {
         const int lw = pyr.w[level], lh = pyr.h[level], pitch = pyr.pitch[level];
         const uint8_t* I = at_pair(pyr.P[level], level == 0 ? iz : pz, z);
@@ -845,6 +870,7 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
         float lx = nx - hw, ly = ny - hw;
         float pdx = 0.f, pdy = 0.f;
         for (int j = 0; j < max_count; j++) {
+            nit++;
             const int inx = cv_floor(lx), iny = cv_floor(ly);
             if (inx < -win || inx >= lw || iny < -win || iny >= lh) {
                 if (level == 0) st = 0;
@@ -909,6 +935,7 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
         nxy[2 * p] = nx;
         nxy[2 * p + 1] = ny;
         status[p] = (uint8_t)st;
+        if (itcount) { atomicAdd(itcount + 2, nit); atomicAdd(itcount + 3, 1); }
     }
     }
 }
@@ -1666,7 +1693,7 @@ int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride
     // image with 2 px of drift to spare
     hipLaunchKernelGGL(k_subpix_order, dim3(flow_grid(d, 256)), dim3(256), 0, s, d->pts, d->offs, d->npairs, w, h, 14,
                        d->pz, d->order, d->ocnt);
-    FLOW_LAUNCH(d, "k_subpix", s, k_subpix<10>, dim3(flow_grid(d, 64)), dim3(64), 0, s, img, w, h, stride, d->pts,
+    FLOW_LAUNCH(d, "k_subpix", s, k_subpix<10>, dim3(flow_grid(d, 1)), dim3(64), 0, s, img, w, h, stride, d->pts,
                 d->offs, d->npairs, d->order, d->mask, iters, e * e, iz, d->pz, itc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -1706,8 +1733,13 @@ int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, 
     }
     FLOW_LAUNCH(d, "k_sharr", s, k_sharr, dim3(64, L, P), dim3(256), 0, s, pyr, iz, d->pz);
     launch_flow_index(d, s);            // the host LK entry point sets npts without cornerSubPix
+    int* itc = nullptr;
+    if (getenv("COEB_SUBPIX_COUNT")) {
+        if (!g_subpix_count) (void)hipGetSymbolAddress((void**)&g_subpix_count, HIP_SYMBOL(g_subpix_count_dev));
+        itc = g_subpix_count;
+    }
     FLOW_LAUNCH(d, "k_lk", s, k_lk, dim3(flow_grid(d, 4)), dim3(256), 0, s, pyr, d->pts, d->offs, P, d->nxt,
-                d->status, win, max_count, eps * eps, iz, d->pz);
+                d->status, win, max_count, eps * eps, iz, d->pz, itc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1888,9 +1920,9 @@ extern "C" int coeb_moving_object_points(coeb_ctx* c, const uint8_t* prev, const
 // COEB_SUBPIX_COUNT since the last read (then reset)
 extern "C" int coeb_internal_subpix_count(int* out)
 {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_subpix_count_dev), 8) != hipSuccess) return COEB_EDEVICE;
-    const int z[2] = {0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_subpix_count_dev), z, 8) == hipSuccess ? COEB_OK : COEB_EDEVICE;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_subpix_count_dev), 16) != hipSuccess) return COEB_EDEVICE;
+    const int z[4] = {0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_subpix_count_dev), z, 16) == hipSuccess ? COEB_OK : COEB_EDEVICE;
 }
 
 // geometry of each context's last moving-object batch, for coeb_internal_flow_counts
