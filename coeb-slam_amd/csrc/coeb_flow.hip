@@ -746,27 +746,68 @@ __device__ __forceinline__ int64_t wave_sum_i32x(int v)
 
 __device__ __forceinline__ int refl1(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
 
-// One wave per point.  Lane (row r = lane >> 1, half h = lane & 1) carries window row r's
-// pixels [h * hw, min(win, (h + 1) * hw)), hw = ceil(win / 2) <= 11 (win <= 22): a row segment,
-// so a window's I, J and derivative samples come from a few dword loads per lane and row (bytes
-// taken out with v_bfe) instead of four byte gathers per pixel; lanes past 2 * win carry none.
-// Window sums stay exact in int32 per lane (at most 11 products of < 2^27) and are joined by
-// DPP wave reductions of their 16-bit halves.  Windows that reach past the level edge take the
+// One wave per point.  The window (win <= 24) is tiled 8 x 8 by 3 x 3 pixel tiles, lane
+// (tr, tc) = (lane >> 3, lane & 7) carrying rows 3 tr .. 3 tr + 2 and columns 3 tc .. 3 tc + 2
+// (a 22 x 22 window keeps 484 of the 576 slots busy, every lane has work).  A tile's four image
+// rows (three pixel rows and the +1 neighbour row) are one unaligned 4-byte segment each; each
+// bilinear tap pair (p[k], p[k + 1]) of a row is one v_perm into a u16x2, shared by the pixel rows
+// above and below it, and weighed by v_dot2_i32_i16 against (iw00, iw01) or (iw10, iw11); the
+// products with the derivatives are v_mad_i32_i24 (all operands < 2^23).  sum (J - I) * g is
+// accumulated as sum J * g - sum I * g with the second term fixed per level: every per-lane
+// partial stays exact in int32 (<= 9 products of < 2^26), and the window sums are joined by DPP
+// wave reductions of their 16-bit halves.  Windows that reach past the level edge take the
 // per-pixel reflected path of calcOpticalFlowPyrLK (REFLECT_101 images, zero derivatives).
-constexpr int kLkHP = 11;                     // pixels per lane
-__device__ __forceinline__ uint32_t byte_at(const uint32_t* q, int k) { return (q[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
+// signed: iw11 = 16384 - iw00 - iw01 - iw10 is -1 when the three rounded weights overshoot
+typedef short lk_i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int dot2s(uint32_t a, uint32_t b, int c)
+{
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(lk_i16x2, a), __builtin_bit_cast(lk_i16x2, b), c, false);
+}
 
-// n <= 12 bytes from p (any alignment) as 3 dwords; no dword past the one holding p[n - 1] is read
-__device__ __forceinline__ void load12(const uint8_t* p, int n, uint32_t* q)
+// n <= 4 bytes from p (any alignment) as one dword; no dword past the one holding p[n - 1] is read
+typedef const uint32_t __attribute__((address_space(1)))* lk_gptr;
+__device__ __forceinline__ uint32_t load_seg4(const uint8_t* p, int n)
 {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t* a4 = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-    const uint32_t* last = reinterpret_cast<const uint32_t*>((a + n - 1) & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
-    const uint32_t d0 = a4[0], d1 = *min(a4 + 1, last), d2 = *min(a4 + 2, last), d3 = *min(a4 + 3, last);
-    q[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
-    q[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
-    q[2] = __builtin_amdgcn_alignbyte(d3, d2, sh);
+    const lk_gptr a4 = (lk_gptr)(a & ~(uintptr_t)3);
+    const lk_gptr last = (lk_gptr)((a + n - 1) & ~(uintptr_t)3);
+    const lk_gptr a5 = a4 + 1 < last ? a4 + 1 : last;
+    return __builtin_amdgcn_alignbyte(*a5, *a4, (uint32_t)(a & 3));
+}
+
+// the three tap pairs (p[k], p[k + 1]), k = 0, 1, 2, of a 4-byte row segment as u16x2
+__device__ __forceinline__ void tap_pairs(uint32_t q, uint32_t* t)
+{
+    t[0] = __builtin_amdgcn_perm(0u, q, 0x0c010c00u);
+    t[1] = __builtin_amdgcn_perm(0u, q, 0x0c020c01u);
+    t[2] = __builtin_amdgcn_perm(0u, q, 0x0c030c02u);
+}
+
+// the four row segments of the tile at window offset (C0, R0) of a window whose top-left pixel is
+// org, as tap pairs.  Every lane loads all four (no divergent waits): rows and columns are clamped
+// to the window's +1 row / column, which the caller has checked lie inside the level, and the
+// samples this brings in outside the tile's pixels are weighed by zero derivatives.
+__device__ __forceinline__ void tile_pairs(const uint8_t* org, int pitch, int win, int C0, int R0, int nc, uint32_t (*t)[3])
+{
+    const uint8_t* col = org + min(C0, win);
+#pragma unroll
+    for (int i = 0; i < 4; i++) tap_pairs(load_seg4(col + (size_t)min(R0 + i, win) * pitch, nc + 1), t[i]);
+}
+
+// tile_pairs for a window that reaches past the level edge: byte gathers at REFLECT_101
+// coordinates (the taps of calcOpticalFlowPyrLK's border path), same clamping
+__device__ __forceinline__ void tile_pairs_reflect(const uint8_t* img, int pitch, int lw, int lh, int x0, int y0, int win,
+                                                   int C0, int R0, uint32_t (*t)[3])
+{
+    int cx[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) cx[j] = refl1(x0 + min(C0 + j, win), lw);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint8_t* r = img + (size_t)refl1(y0 + min(R0 + i, win), lh) * pitch;
+        const uint32_t q = (uint32_t)r[cx[0]] | ((uint32_t)r[cx[1]] << 8) | ((uint32_t)r[cx[2]] << 16) | ((uint32_t)r[cx[3]] << 24);
+        tap_pairs(q, t[i]);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__ pxy0, const int* __restrict__ offs, int P,
@@ -774,11 +815,10 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
                                             double eps2, int64_t iz, int64_t pz, int* __restrict__ itcount)
 {
     const int lane = threadIdx.x & 63;
-    const int hwid = (win + 1) >> 1;
-    const int wr = lane >> 1, c0 = (lane & 1) * hwid;
-    const int ncol = wr < win ? min(hwid, win - c0) : 0;     // this lane's pixels
+    const int R0 = (lane >> 3) * 3, C0 = (lane & 7) * 3;
+    const int nr = min(3, max(0, win - R0)), nc = nr > 0 ? min(3, max(0, win - C0)) : 0;   // this lane's pixels
     const int total = offs[P];
-    for (int item = blockIdx.x * 4 + (threadIdx.x >> 6); item < total; item += gridDim.x * 4) {
+    for (int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); item < total; item += gridDim.x * 4) {
     const int2 zp = flow_item(offs, P, item);
     const uint32_t z = (uint32_t)zp.x;
     const float* pxy = at_pair(pxy0, pz, z);
@@ -790,7 +830,7 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
     int st = 1;
     float nx = 0.f, ny = 0.f;
     const float px0 = pxy[2 * p], py0 = pxy[2 * p + 1];
-    int iv[kLkHP], gxv[kLkHP], gyv[kLkHP];
+    int gxv[9], gyv[9];
     int nit = 0;
     for (int level = pyr.L - 1; level >= 0; level--) {
         const int lw = pyr.w[level], lh = pyr.h[level], pitch = pyr.pitch[level];
@@ -812,50 +852,40 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
         int iw01 = (int)rintf(a * (1.f - b) * 16384.f);
         int iw10 = (int)rintf((1.f - a) * b * 16384.f);
         int iw11 = 16384 - iw00 - iw01 - iw10;
-        int sA11 = 0, sA12 = 0, sA22 = 0;                 // per lane: <= 11 products of < 2^27
-        const int X0 = ipx + c0, Y = ipy + wr;
-        if (ipx >= 0 && ipy >= 0 && ipx + win < lw && ipy + win < lh) {
-            uint32_t q0[3] = {0, 0, 0}, q1[3] = {0, 0, 0};
-            if (ncol > 0) {
-                load12(I + (size_t)Y * pitch + X0, ncol + 1, q0);
-                load12(I + (size_t)(Y + 1) * pitch + X0, ncol + 1, q1);
-            }
-            const short2* d0 = D + (size_t)Y * lw + X0;
-            const short2* d1 = d0 + lw;
+        int sA11 = 0, sA12 = 0, sA22 = 0;                 // per lane: <= 9 products of < 2^25
+        int sIx = 0, sIy = 0;                             // per lane sum I * g: <= 9 products of < 2^26
+        const int X0 = ipx + C0, Y0 = ipy + R0;
+        const bool inside = ipx >= 0 && ipy >= 0 && ipx + win < lw && ipy + win < lh;
+        uint32_t t[4][3];
+        if (inside)
+            tile_pairs(I + (size_t)ipy * pitch + ipx, pitch, win, C0, R0, nc, t);
+        else
+            tile_pairs_reflect(I, pitch, lw, lh, ipx, ipy, win, C0, R0, t);
+        const uint32_t W0 = (uint32_t)iw00 | ((uint32_t)iw01 << 16), W1 = (uint32_t)iw10 | ((uint32_t)iw11 << 16);
 #pragma unroll
-            for (int k = 0; k < kLkHP; k++) {
-                iv[k] = 0; gxv[k] = 0; gyv[k] = 0;
-                if (k < ncol) {
-                    iv[k] = ((int)byte_at(q0, k) * iw00 + (int)byte_at(q0, k + 1) * iw01 + (int)byte_at(q1, k) * iw10 +
-                             (int)byte_at(q1, k + 1) * iw11 + (1 << 8)) >> 9;
-                    const short2 e00 = d0[k], e01 = d0[k + 1], e10 = d1[k], e11 = d1[k + 1];
-                    gxv[k] = (e00.x * iw00 + e01.x * iw01 + e10.x * iw10 + e11.x * iw11 + (1 << 13)) >> 14;
-                    gyv[k] = (e00.y * iw00 + e01.y * iw01 + e10.y * iw10 + e11.y * iw11 + (1 << 13)) >> 14;
-                    sA11 += gxv[k] * gxv[k];
-                    sA12 += gxv[k] * gyv[k];
-                    sA22 += gyv[k] * gyv[k];
-                }
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < kLkHP; k++) {
-                iv[k] = 0; gxv[k] = 0; gyv[k] = 0;
-                if (k < ncol) {
-                    const int X = X0 + k;
-                    const int x0 = refl1(X, lw), x1 = refl1(X + 1, lw);
-                    const uint8_t* r0 = I + (size_t)refl1(Y, lh) * pitch;
-                    const uint8_t* r1 = I + (size_t)refl1(Y + 1, lh) * pitch;
-                    iv[k] = (r0[x0] * iw00 + r0[x1] * iw01 + r1[x0] * iw10 + r1[x1] * iw11 + (1 << 8)) >> 9;
+        for (int k = 0; k < 9; k++) {
+            const int i = k / 3, j = k % 3;
+            gxv[k] = 0; gyv[k] = 0;
+            if (i < nr && j < nc) {
+                const int iv = (dot2s(t[i][j], W0, dot2s(t[i + 1][j], W1, 1 << 8)) >> 9);
+                const int X = X0 + j, Y = Y0 + i;
+                short2 e00, e01, e10, e11;
+                if (inside) {
+                    const short2* d0 = D + (size_t)Y * lw + X;
+                    e00 = d0[0]; e01 = d0[1]; e10 = d0[lw]; e11 = d0[lw + 1];
+                } else {
                     auto dv = [&](int xq, int yq) {
                         return (xq < 0 || yq < 0 || xq >= lw || yq >= lh) ? make_short2(0, 0) : D[(size_t)yq * lw + xq];
                     };
-                    const short2 e00 = dv(X, Y), e01 = dv(X + 1, Y), e10 = dv(X, Y + 1), e11 = dv(X + 1, Y + 1);
-                    gxv[k] = (e00.x * iw00 + e01.x * iw01 + e10.x * iw10 + e11.x * iw11 + (1 << 13)) >> 14;
-                    gyv[k] = (e00.y * iw00 + e01.y * iw01 + e10.y * iw10 + e11.y * iw11 + (1 << 13)) >> 14;
-                    sA11 += gxv[k] * gxv[k];
-                    sA12 += gxv[k] * gyv[k];
-                    sA22 += gyv[k] * gyv[k];
+                    e00 = dv(X, Y); e01 = dv(X + 1, Y); e10 = dv(X, Y + 1); e11 = dv(X + 1, Y + 1);
                 }
+                gxv[k] = (__mul24(e00.x, iw00) + __mul24(e01.x, iw01) + __mul24(e10.x, iw10) + __mul24(e11.x, iw11) + (1 << 13)) >> 14;
+                gyv[k] = (__mul24(e00.y, iw00) + __mul24(e01.y, iw01) + __mul24(e10.y, iw10) + __mul24(e11.y, iw11) + (1 << 13)) >> 14;
+                sA11 += __mul24(gxv[k], gxv[k]);
+                sA12 += __mul24(gxv[k], gyv[k]);
+                sA22 += __mul24(gyv[k], gyv[k]);
+                sIx += __mul24(iv, gxv[k]);
+                sIy += __mul24(iv, gyv[k]);
             }
         }
         const int64_t tA11 = wave_sum_i32x(sA11), tA12 = wave_sum_i32x(sA12), tA22 = wave_sum_i32x(sA22);
@@ -881,37 +911,18 @@ __global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__
             iw01 = (int)rintf(a * (1.f - b) * 16384.f);
             iw10 = (int)rintf((1.f - a) * b * 16384.f);
             iw11 = 16384 - iw00 - iw01 - iw10;
-            int ib1 = 0, ib2 = 0;                     // per lane: <= 11 products of < 2^26
-            const int JX0 = inx + c0, JY = iny + wr;
-            if (inx >= 0 && iny >= 0 && inx + win < lw && iny + win < lh) {
-                // the window and its +1 neighbours inside the level: one 12-byte segment per row
-                uint32_t q0[3] = {0, 0, 0}, q1[3] = {0, 0, 0};
-                if (ncol > 0) {
-                    load12(J + (size_t)JY * pitch + JX0, ncol + 1, q0);
-                    load12(J + (size_t)(JY + 1) * pitch + JX0, ncol + 1, q1);
-                }
+            int ib1 = -sIx, ib2 = -sIy;               // per lane: sum (J - I) * g, exact in int32
+            uint32_t t[4][3];
+            if (inx >= 0 && iny >= 0 && inx + win < lw && iny + win < lh)    // the window and its +1 neighbours inside
+                tile_pairs(J + (size_t)iny * pitch + inx, pitch, win, C0, R0, nc, t);
+            else
+                tile_pairs_reflect(J, pitch, lw, lh, inx, iny, win, C0, R0, t);
+            const uint32_t W0 = (uint32_t)iw00 | ((uint32_t)iw01 << 16), W1 = (uint32_t)iw10 | ((uint32_t)iw11 << 16);
 #pragma unroll
-                for (int k = 0; k < kLkHP; k++) {
-                    if (k < ncol) {
-                        const int diff = (((int)byte_at(q0, k) * iw00 + (int)byte_at(q0, k + 1) * iw01 +
-                                           (int)byte_at(q1, k) * iw10 + (int)byte_at(q1, k + 1) * iw11 + (1 << 8)) >> 9) - iv[k];
-                        ib1 += diff * gxv[k];
-                        ib2 += diff * gyv[k];
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < kLkHP; k++) {
-                    if (k < ncol) {
-                        const int X = JX0 + k;
-                        const int x0 = refl1(X, lw), x1 = refl1(X + 1, lw);
-                        const uint8_t* r0 = J + (size_t)refl1(JY, lh) * pitch;
-                        const uint8_t* r1 = J + (size_t)refl1(JY + 1, lh) * pitch;
-                        const int diff = ((r0[x0] * iw00 + r0[x1] * iw01 + r1[x0] * iw10 + r1[x1] * iw11 + (1 << 8)) >> 9) - iv[k];
-                        ib1 += diff * gxv[k];
-                        ib2 += diff * gyv[k];
-                    }
-                }
+            for (int k = 0; k < 9; k++) {                 // gxv = gyv = 0 outside the window
+                const int jv = (dot2s(t[k / 3][k % 3], W0, dot2s(t[k / 3 + 1][k % 3], W1, 1 << 8)) >> 9);
+                ib1 = __mul24(jv, gxv[k]) + ib1;
+                ib2 = __mul24(jv, gyv[k]) + ib2;
             }
             const int64_t tb1 = wave_sum_i32x(ib1), tb2 = wave_sum_i32x(ib2);
             const float b1 = (float)tb1 * FLT_SCALE, b2 = (float)tb2 * FLT_SCALE;

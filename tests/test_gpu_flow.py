@@ -81,8 +81,10 @@ def test_lk(ctx, oracle_mod, tag, prev, cur):
 def test_lk_edges(ctx, oracle_mod):
     prev, cur = PAIRS[1][1], PAIRS[1][2]
     h, w = prev.shape
-    pts = np.array([[0, 0], [w - 1, h - 1], [-3, 10], [w + 40, 20], [2.5, h - 1.5], [320, 240], [11, 470]],
-                   np.float32)
+    # (x.5001, y.5001): at level 0 the window origin sits 1e-4 past a pixel, so the rounded weights
+    # give iw11 = 16384 - 16381 - 2 - 2 = -1 (the taps are signed)
+    pts = np.array([[0, 0], [w - 1, h - 1], [-3, 10], [w + 40, 20], [2.5, h - 1.5], [320, 240], [11, 470],
+                    [100.5001, 200.5001], [320.5001, 240.5001]], np.float32)
     nx, st = cf.CalcOpticalFlowPyrLK(ctx, prev, cur, pts)
     rnx, rst = oracle_mod.lk_pyr(prev, cur, pts)
     eq(st, rst, "status")
