@@ -608,6 +608,222 @@ __global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0,
     }
 }
 
+// ---- cornerSubPix, G corners per wave ----
+// The five double sums of an iteration are chains of 441 dependent adds in the reference's
+// row-major order; one corner per wave (k_subpix) runs them on five lanes, so every add costs a
+// whole wave instruction.  Here a wave carries G corner slots: per window row i (a phase) the
+// fill lanes extend each slot's rolling four-row getRectSubPix patch by one row, the term lanes
+// form the 5 x 21 terms of row i for every slot, and lane 5 g + t then adds row i's 21 terms of
+// term t of slot g -- one add instruction serves G corners.  Slots iterate independently (their
+// own ipx / ipy / weights, rewritten each round by the slot's lane into `par`); a slot whose
+// corner has converged takes the next one from the work queue at the start of the next round.
+// Image rows come straight from global memory (L2-resident windows), one row ahead of use, and
+// each fill lane carries its lower row into the next patch row.
+constexpr int kSpSlots = 6;             // corner slots per wave
+struct SpSlot {
+    const uint8_t* img;
+    double sd;                          // in-image: (1 - a) / a
+    float a12, a22, b1, b2, c4, c5;     // in-image: c4 = 1 - a; clamped: c4 = a11, c5 = a21
+    int ipx, ipy, mode;                 // mode 0: idle, 1: window inside the image, 2: clamped
+};
+
+__device__ __forceinline__ void wave_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+template <int G>
+__global__ __launch_bounds__(64) void k_subpix_ms(const uint8_t* __restrict__ img0, int w, int h, int stride,
+                                                  float* __restrict__ xy0, const int* __restrict__ offs, int P,
+                                                  const int* __restrict__ order, int* __restrict__ queue,
+                                                  const double* __restrict__ maskd, int iters, double eps2, int64_t iz,
+                                                  int64_t pz, int* __restrict__ itcount)
+{
+    constexpr int WIN = 10, WW = 2 * WIN + 1, BW = WW + 2;
+    constexpr int NF = (G * BW + 63) / 64, NT = (G * WW + 63) / 64, NL = 5 * G;
+    static_assert(NL <= 64, "one summing lane per slot and term");
+    __shared__ float pr[G][4][BW + 1];                 // rolling patch rows, row r at r & 3
+    __shared__ double tr[WW][NL];                      // one window row's terms, [j][5 g + t]
+    __shared__ SpSlot par[G];
+    __shared__ double ssum[NL];
+    __shared__ double smask[WW * WW];                  // LDS, so the terms wait on no global load
+    const int lane = threadIdx.x;
+    const int total = offs[P];
+    for (int k = lane; k < WW * WW; k += 64) smask[k] = maskd[k];
+    // slot state on lane g < G
+    int item = -1, it = 0, nit = 0, ncorner = 0, pidx = 0;
+    float tx = 0.f, ty = 0.f, cx = 0.f, cy = 0.f;
+    float* xy = nullptr;
+    const uint8_t* simg = nullptr;
+    bool need = lane < G;
+    for (;;) {
+        // refill the free slots from the queue, one atomic per wave
+        const uint64_t nm = __ballot(need);
+        if (nm) {
+            const int first = __ffsll((unsigned long long)nm) - 1;
+            int base = 0;
+            if (lane == first) base = atomicAdd(queue, __popcll(nm));
+            base = __shfl(base, first, 64);
+            if (need) {
+                const int q = base + __popcll(nm & ((1ull << lane) - 1ull));
+                item = q < total ? q : -1;
+                if (item >= 0) {
+                    const int2 zp = flow_item(offs, P, order[item]);
+                    xy = at_pair(xy0, pz, (uint32_t)zp.x);
+                    simg = at_pair(img0, iz, (uint32_t)zp.x);
+                    pidx = zp.y;
+                    tx = xy[2 * pidx]; ty = xy[2 * pidx + 1];
+                    cx = tx; cy = ty; it = 0;
+                    ncorner++;
+                }
+                need = false;
+            }
+        }
+        if (!__ballot(lane < G && item >= 0)) break;
+        if (lane < G) {
+            SpSlot sl;
+            sl.img = item >= 0 ? simg : img0;           // idle slots: a valid address for the fill loads
+            sl.sd = 0.; sl.a12 = sl.a22 = sl.b1 = sl.b2 = sl.c4 = sl.c5 = 0.f; sl.ipx = sl.ipy = 0; sl.mode = 0;
+            if (item >= 0) {
+                const float ctrx = cx - (float)(BW - 1) * 0.5f, ctry = cy - (float)(BW - 1) * 0.5f;
+                const int ipx = cv_floor(ctrx), ipy = cv_floor(ctry);
+                const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
+                sl.ipx = ipx; sl.ipy = ipy; sl.b1 = 1.f - b; sl.b2 = b;
+                if (ipx >= 0 && ipx + BW < w && ipy >= 0 && ipy + BW < h) {
+                    const float ac = a < 0.0001f ? 0.0001f : a;      // getRectSubPix_8u32f's recurrence
+                    sl.mode = 1;
+                    sl.a12 = ac * (1.f - b); sl.a22 = ac * b; sl.c4 = 1.f - ac;
+                    sl.sd = (1. - (double)ac) / (double)ac;
+                } else {
+                    sl.mode = 2;
+                    sl.c4 = (1.f - a) * (1.f - b); sl.a12 = a * (1.f - b); sl.c5 = (1.f - a) * b; sl.a22 = a * b;
+                }
+            }
+            par[lane] = sl;
+        }
+        wave_order();
+        // fill lanes: task f = q * 64 + lane -> (slot, patch column)
+        int fmode[NF], fcol[NF], frow[NF];
+        const uint8_t* fimg[NF];
+        int fc0[NF], fc1[NF];
+#pragma unroll
+        for (int q = 0; q < NF; q++) {
+            const int f = q * 64 + lane, g = f / BW;
+            fmode[q] = 0; fcol[q] = f - g * BW; frow[q] = 0; fimg[q] = img0; fc0[q] = fc1[q] = 0;
+            if (f < G * BW) {
+                fmode[q] = par[g].mode;
+                fimg[q] = par[g].img;
+                frow[q] = par[g].ipy;
+                const int c = par[g].ipx + fcol[q];
+                fc0[q] = min(max(c, 0), w - 1);
+                fc1[q] = min(max(c + 1, 0), w - 1);
+            }
+        }
+        // every lane loads (idle lanes a valid byte of frame 0): no branch, so the waits for a
+        // prefetched row fall at its use, a phase later
+        auto load_row = [&](int q, int rr, uint32_t& v0, uint32_t& v1) {
+            typedef const uint8_t __attribute__((address_space(1)))* gp8;
+            const gp8 r = (gp8)(fimg[q] + (size_t)min(max(frow[q] + rr, 0), h - 1) * stride);
+            v0 = r[fc0[q]]; v1 = r[fc1[q]];
+        };
+        auto fill = [&](int q, int r, uint32_t u00, uint32_t u01, uint32_t u10, uint32_t u11) {
+            if (!fmode[q]) return;
+            const float b00 = (float)u00, b01 = (float)u01, b10 = (float)u10, b11 = (float)u11;
+            const int f = q * 64 + lane, g = f / BW, j = fcol[q];
+            const SpSlot& sl = par[g];
+            float v;
+            if (fmode[q] == 1) {
+                const float t = sl.a12 * b01 + sl.a22 * b11;
+                const float prev = j == 0 ? sl.c4 * (sl.b1 * b00 + sl.b2 * b10)
+                                          : (float)((double)(sl.a12 * b00 + sl.a22 * b10) * sl.sd);
+                v = prev + t;
+            } else {
+                const int c = sl.ipx + j;
+                v = (c < 0 || c >= w - 1) ? b00 * sl.b1 + b10 * sl.b2 : b00 * sl.c4 + b01 * sl.a12 + b10 * sl.c5 + b11 * sl.a22;
+            }
+            pr[g][r & 3][j] = v;
+        };
+        uint32_t lo0[NF], lo1[NF], nx0[NF], nx1[NF];
+#pragma unroll
+        for (int q = 0; q < NF; q++) {
+            uint32_t a0, a1, b0, b1;
+            load_row(q, 0, a0, a1);
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                load_row(q, r + 1, b0, b1);
+                fill(q, r, a0, a1, b0, b1);
+                a0 = b0; a1 = b1;
+            }
+            lo0[q] = a0; lo1[q] = a1;                   // image row 3
+            load_row(q, 4, nx0[q], nx1[q]);
+        }
+        double acc = 0.0;
+#pragma unroll 1
+        for (int i = 0; i < WW; i++) {
+            uint32_t pf0[NF], pf1[NF];
+#pragma unroll
+            for (int q = 0; q < NF; q++) load_row(q, min(i + 5, BW), pf0[q], pf1[q]);   // image row i + 5, phase i + 1
+            wave_order();
+#pragma unroll
+            for (int q = 0; q < NT; q++) {             // terms of window row i
+                const int e = q * 64 + lane, g = e / WW, j = e - g * WW;
+                if (e < G * WW && par[g].mode) {
+                    const float* r0 = pr[g][i & 3];
+                    const float* r1 = pr[g][(i + 1) & 3];
+                    const float* r2 = pr[g][(i + 2) & 3];
+                    const double m = smask[i * WW + j];
+                    const double tgx = (double)(r1[j + 2] - r1[j]);
+                    const double tgy = (double)(r2[j + 1] - r0[j + 1]);
+                    const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
+                    const double px = j - WIN, py = i - WIN;
+                    double* o = &tr[j][5 * g];
+                    o[0] = gxx; o[1] = gxy; o[2] = gyy;
+                    o[3] = gxx * px + gxy * py;
+                    o[4] = gxy * px + gyy * py;
+                }
+            }
+            wave_order();
+            if (lane < NL) {
+#pragma unroll
+                for (int j = 0; j < WW; j++) acc += tr[j][lane];
+            }
+            wave_order();
+            if (i + 3 < BW) {                          // patch row i + 3 from image rows i + 3, i + 4
+#pragma unroll
+                for (int q = 0; q < NF; q++) {
+                    fill(q, i + 3, lo0[q], lo1[q], nx0[q], nx1[q]);
+                    lo0[q] = nx0[q]; lo1[q] = nx1[q];
+                    nx0[q] = pf0[q]; nx1[q] = pf1[q];
+                }
+            }
+        }
+        if (lane < NL) ssum[lane] = acc;
+        wave_order();
+        if (lane < G && item >= 0) {
+            const double sa = ssum[5 * lane], sb = ssum[5 * lane + 1], sc = ssum[5 * lane + 2];
+            const double bb1 = ssum[5 * lane + 3], bb2 = ssum[5 * lane + 4];
+            bool fin = false;
+            nit++;
+            const double det = sa * sc - sb * sb;
+            if (fabs(det) <= DBL_EPSILON * DBL_EPSILON) fin = true;
+            else {
+                const double scale = 1.0 / det;
+                const float nx = (float)((double)cx + sc * scale * bb1 - sb * scale * bb2);
+                const float ny = (float)((double)cy - sb * scale * bb1 + sa * scale * bb2);
+                const double err = (double)((nx - cx) * (nx - cx) + (ny - cy) * (ny - cy));
+                cx = nx; cy = ny;
+                if (cx < 0 || cx >= (float)w || cy < 0 || cy >= (float)h) fin = true;
+                else if (!(++it < iters && err > eps2)) fin = true;
+            }
+            if (fin) {
+                if (fabsf(cx - tx) > (float)WIN || fabsf(cy - ty) > (float)WIN) { cx = tx; cy = ty; }
+                xy[2 * pidx] = cx; xy[2 * pidx + 1] = cy;
+                item = -1;
+                need = true;
+            }
+        }
+        wave_order();
+    }
+    if (itcount && lane < G && ncorner) { atomicAdd(itcount, nit); atomicAdd(itcount + 1, ncorner); }
+}
+
 // cornerSubPix work order: the corners whose window may leave the image (getRectSubPix's
 // clamped path) last, so the waves that take the in-image path (nearly all) never execute the
 // other; lane order within a wave is kept (wave-aggregated atomics), so a wave's corners stay
@@ -1699,13 +1915,17 @@ int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride
         itc = g_subpix_count;
     }
     launch_flow_index(d, s);
-    (void)hipMemsetAsync(d->ocnt, 0, 8, s);
+    (void)hipMemsetAsync(d->ocnt, 0, 12, s);            // {interior, border, queue}
     // interior: the window (23 x 23 around the corner, +1 for the interpolation) stays inside the
     // image with 2 px of drift to spare
     hipLaunchKernelGGL(k_subpix_order, dim3(flow_grid(d, 256)), dim3(256), 0, s, d->pts, d->offs, d->npairs, w, h, 14,
                        d->pz, d->order, d->ocnt);
-    FLOW_LAUNCH(d, "k_subpix", s, k_subpix<10>, dim3(flow_grid(d, 1)), dim3(64), 0, s, img, w, h, stride, d->pts,
-                d->offs, d->npairs, d->order, d->mask, iters, e * e, iz, d->pz, itc);
+    if (getenv("COEB_SUBPIX_ONE"))
+        FLOW_LAUNCH(d, "k_subpix", s, k_subpix<10>, dim3(flow_grid(d, 1)), dim3(64), 0, s, img, w, h, stride, d->pts,
+                    d->offs, d->npairs, d->order, d->mask, iters, e * e, iz, d->pz, itc);
+    else
+        FLOW_LAUNCH(d, "k_subpix", s, k_subpix_ms<kSpSlots>, dim3(flow_grid(d, 8 * kSpSlots)), dim3(64), 0, s, img, w, h, stride,
+                    d->pts, d->offs, d->npairs, d->order, d->ocnt + 2, d->mask, iters, e * e, iz, d->pz, itc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
