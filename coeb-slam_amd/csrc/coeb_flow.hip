@@ -611,20 +611,24 @@ __global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0,
 // ---- cornerSubPix, G corners per wave ----
 // The five double sums of an iteration are chains of 441 dependent adds in the reference's
 // row-major order; one corner per wave (k_subpix) runs them on five lanes, so every add costs a
-// whole wave instruction.  Here a wave carries G corner slots: per window row i (a phase) the
-// fill lanes extend each slot's rolling four-row getRectSubPix patch by one row, the term lanes
-// form the 5 x 21 terms of row i for every slot, and lane 5 g + t then adds row i's 21 terms of
-// term t of slot g -- one add instruction serves G corners.  Slots iterate independently (their
-// own ipx / ipy / weights, rewritten each round by the slot's lane into `par`); a slot whose
-// corner has converged takes the next one from the work queue at the start of the next round.
-// Image rows come straight from global memory (L2-resident windows), one row ahead of use, and
-// each fill lane carries its lower row into the next patch row.
-constexpr int kSpSlots = 6;             // corner slots per wave
-struct SpSlot {
+// whole wave instruction.  Here a wave carries G corner slots, and an iteration is 21 phases, one
+// per window row i: the fill lanes (slot, column pair) extend each slot's rolling four-row
+// getRectSubPix patch by row i + 3, the term lanes (slot, column) form the five terms of window
+// row i for every slot, and lane 5 g + t adds row i's 21 terms of term t of slot g -- one add
+// instruction serves G corners.  Slots iterate independently (their own ipx / ipy / weights,
+// rewritten each round by the slot's lane into `par`); a slot whose corner has converged takes the
+// next one from the work queue at the start of the next round.  The two image rows a phase's fill
+// needs come straight from global memory (L2-resident windows), issued at the start of the phase
+// and consumed at its end, so no load is in flight across the loop's back edge.
+#ifndef COEB_SP_SLOTS
+#define COEB_SP_SLOTS 9
+#endif
+constexpr int kSpSlots = COEB_SP_SLOTS;   // corner slots per wave (9: 45 summing lanes)
+struct __attribute__((aligned(16))) SpSlot {      // read as three 16-byte words by the fill lanes
     const uint8_t* img;
     double sd;                          // in-image: (1 - a) / a
     float a12, a22, b1, b2, c4, c5;     // in-image: c4 = 1 - a; clamped: c4 = a11, c5 = a21
-    int ipx, ipy, mode;                 // mode 0: idle, 1: window inside the image, 2: clamped
+    int ipx, ipy, mode, pad;            // mode 0: idle, 1: window inside the image, 2: clamped
 };
 
 __device__ __forceinline__ void wave_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
@@ -633,34 +637,54 @@ template <int G>
 __global__ __launch_bounds__(64) void k_subpix_ms(const uint8_t* __restrict__ img0, int w, int h, int stride,
                                                   float* __restrict__ xy0, const int* __restrict__ offs, int P,
                                                   const int* __restrict__ order, int* __restrict__ queue,
-                                                  const double* __restrict__ maskd, int iters, double eps2, int64_t iz,
+                                                  const float* __restrict__ mexp, int iters, double eps2, int64_t iz,
                                                   int64_t pz, int* __restrict__ itcount)
 {
-    constexpr int WIN = 10, WW = 2 * WIN + 1, BW = WW + 2;
-    constexpr int NF = (G * BW + 63) / 64, NT = (G * WW + 63) / 64, NL = 5 * G;
+    constexpr int WIN = 10, WW = 2 * WIN + 1, BW = WW + 2, NJ = (BW + 1) / 2;
+    constexpr int NF = (G * NJ + 63) / 64, NT = (G * WW + 63) / 64, NL = 5 * G;
     static_assert(NL <= 64, "one summing lane per slot and term");
-    __shared__ float pr[G][4][BW + 1];                 // rolling patch rows, row r at r & 3
-    __shared__ double tr[WW][NL];                      // one window row's terms, [j][5 g + t]
-    __shared__ SpSlot par[G];
+    // slot G is a sink: the fill and term lanes past the last slot read and write it, so no
+    // pass needs a branch and the LDS reads of all passes issue together
+    __shared__ __attribute__((aligned(16))) float pr[G + 1][4][BW + 1];   // rolling patch rows, row r at r & 3
+    __shared__ double tr[WW][NL + 5];                  // one window row's terms, [j][5 g + t]
+    __shared__ SpSlot par[G + 1];
     __shared__ double ssum[NL];
-    __shared__ double smask[WW * WW];                  // LDS, so the terms wait on no global load
     const int lane = threadIdx.x;
     const int total = offs[P];
-    for (int k = lane; k < WW * WW; k += 64) smask[k] = maskd[k];
+    // the weights: mask(i, j) = e_i * e_j in float (cornerSubPix's vy * expf(-x * x)); e_lane here,
+    // e_j of each term pass's column, e_i by readlane
+    const float e_lane = mexp[min(lane, WW - 1)];
+    float e_col[NT];
+    int tg[NT], tj[NT];                                // term task (slot, column)
+#pragma unroll
+    for (int q = 0; q < NT; q++) {
+        const int e = q * 64 + lane, g = e / WW;
+        tj[q] = e - g * WW;
+        tg[q] = min(g, G);
+        e_col[q] = mexp[tj[q]];
+    }
+    if (lane == 0) {
+        SpSlot sl;
+        sl.img = img0; sl.sd = 0.; sl.a12 = sl.a22 = sl.b1 = sl.b2 = sl.c4 = sl.c5 = 0.f;
+        sl.ipx = sl.ipy = 0; sl.mode = 0; sl.pad = 0;
+        par[G] = sl;
+    }
     // slot state on lane g < G
-    int item = -1, it = 0, nit = 0, ncorner = 0, pidx = 0;
+    int item = -1, it = 0, pidx = 0;
+    int nit = 0, ncorner = 0;                          // wave totals (COEB_SUBPIX_COUNT)
     float tx = 0.f, ty = 0.f, cx = 0.f, cy = 0.f;
     float* xy = nullptr;
     const uint8_t* simg = nullptr;
-    bool need = lane < G;
+    bool need = lane < G, drained = false;
     for (;;) {
         // refill the free slots from the queue, one atomic per wave
-        const uint64_t nm = __ballot(need);
+        const uint64_t nm = drained ? 0ull : __ballot(need);
         if (nm) {
             const int first = __ffsll((unsigned long long)nm) - 1;
             int base = 0;
             if (lane == first) base = atomicAdd(queue, __popcll(nm));
             base = __shfl(base, first, 64);
+            if (base + __popcll(nm) >= total) drained = true;
             if (need) {
                 const int q = base + __popcll(nm & ((1ull << lane) - 1ull));
                 item = q < total ? q : -1;
@@ -671,16 +695,19 @@ __global__ __launch_bounds__(64) void k_subpix_ms(const uint8_t* __restrict__ im
                     pidx = zp.y;
                     tx = xy[2 * pidx]; ty = xy[2 * pidx + 1];
                     cx = tx; cy = ty; it = 0;
-                    ncorner++;
                 }
                 need = false;
             }
+            ncorner += __popcll(__ballot(lane < G && item >= 0) & nm);
         }
-        if (!__ballot(lane < G && item >= 0)) break;
+        const uint64_t am = __ballot(lane < G && item >= 0);
+        if (!am) break;
+        nit += __popcll(am);
         if (lane < G) {
             SpSlot sl;
             sl.img = item >= 0 ? simg : img0;           // idle slots: a valid address for the fill loads
-            sl.sd = 0.; sl.a12 = sl.a22 = sl.b1 = sl.b2 = sl.c4 = sl.c5 = 0.f; sl.ipx = sl.ipy = 0; sl.mode = 0;
+            sl.sd = 0.;
+            sl.a12 = sl.a22 = sl.b1 = sl.b2 = sl.c4 = sl.c5 = 0.f; sl.ipx = sl.ipy = 0; sl.mode = 0; sl.pad = 0;
             if (item >= 0) {
                 const float ctrx = cx - (float)(BW - 1) * 0.5f, ctry = cy - (float)(BW - 1) * 0.5f;
                 const int ipx = cv_floor(ctrx), ipy = cv_floor(ctry);
@@ -699,85 +726,93 @@ __global__ __launch_bounds__(64) void k_subpix_ms(const uint8_t* __restrict__ im
             par[lane] = sl;
         }
         wave_order();
-        // fill lanes: task f = q * 64 + lane -> (slot, patch column)
-        int fmode[NF], fcol[NF], frow[NF];
-        const uint8_t* fimg[NF];
-        int fc0[NF], fc1[NF];
+        // fill lanes: task f = q * 64 + lane -> (slot f / NJ, patch columns j0, j0 + 1), image
+        // columns c0 .. c0 + 2 clamped (the in-image window needs no clamping); the slot's weights
+        // stay in registers for the round
+        int fipy[NF], fd[NF], fj0[NF], fg[NF], fmode[NF];
+        const uint8_t* fbase[NF];
+        float fa12[NF], fa22[NF], fb1[NF], fb2[NF], fc4[NF], fc5[NF];
+        double fsd[NF];
 #pragma unroll
         for (int q = 0; q < NF; q++) {
-            const int f = q * 64 + lane, g = f / BW;
-            fmode[q] = 0; fcol[q] = f - g * BW; frow[q] = 0; fimg[q] = img0; fc0[q] = fc1[q] = 0;
-            if (f < G * BW) {
-                fmode[q] = par[g].mode;
-                fimg[q] = par[g].img;
-                frow[q] = par[g].ipy;
-                const int c = par[g].ipx + fcol[q];
-                fc0[q] = min(max(c, 0), w - 1);
-                fc1[q] = min(max(c + 1, 0), w - 1);
-            }
+            const int f = q * 64 + lane, g = min(f / NJ, G);
+            fg[q] = g;
+            fj0[q] = 2 * (f - (f / NJ) * NJ);
+            const int4* pw = reinterpret_cast<const int4*>(&par[g]);
+            const int4 w0 = pw[0], w1 = pw[1], w2 = pw[2], w3 = pw[3];
+            fbase[q] = reinterpret_cast<const uint8_t*>((uint64_t)(uint32_t)w0.x | ((uint64_t)(uint32_t)w0.y << 32));
+            fsd[q] = __builtin_bit_cast(double, (int64_t)(uint32_t)w0.z | ((int64_t)w0.w << 32));
+            fa12[q] = __int_as_float(w1.x); fa22[q] = __int_as_float(w1.y); fb1[q] = __int_as_float(w1.z); fb2[q] = __int_as_float(w1.w);
+            fc4[q] = __int_as_float(w2.x); fc5[q] = __int_as_float(w2.y);
+            fipy[q] = w2.w;
+            fmode[q] = w3.x;
+            const int c = w2.z + fj0[q];
+            fbase[q] += min(max(c, 0), w - 1);
+            fd[q] = (min(max(c + 1, 0), w - 1) - min(max(c, 0), w - 1)) | ((min(max(c + 2, 0), w - 1) - min(max(c, 0), w - 1)) << 2) |
+                    ((c < 0 || c >= w - 1) << 4) | ((c + 1 < 0 || c + 1 >= w - 1) << 5);
         }
-        // every lane loads (idle lanes a valid byte of frame 0): no branch, so the waits for a
-        // prefetched row fall at its use, a phase later
-        auto load_row = [&](int q, int rr, uint32_t& v0, uint32_t& v1) {
+        // the three bytes of image row rr (relative to ipy) under a fill task
+        auto load_row = [&](int q, int rr, uint32_t* v) {
             typedef const uint8_t __attribute__((address_space(1)))* gp8;
-            const gp8 r = (gp8)(fimg[q] + (size_t)min(max(frow[q] + rr, 0), h - 1) * stride);
-            v0 = r[fc0[q]]; v1 = r[fc1[q]];
+            const gp8 r = (gp8)(fbase[q] + (size_t)min(max(fipy[q] + rr, 0), h - 1) * stride);
+            v[0] = r[0]; v[1] = r[fd[q] & 3]; v[2] = r[(fd[q] >> 2) & 3];
         };
-        auto fill = [&](int q, int r, uint32_t u00, uint32_t u01, uint32_t u10, uint32_t u11) {
-            if (!fmode[q]) return;
-            const float b00 = (float)u00, b01 = (float)u01, b10 = (float)u10, b11 = (float)u11;
-            const int f = q * 64 + lane, g = f / BW, j = fcol[q];
-            const SpSlot& sl = par[g];
-            float v;
-            if (fmode[q] == 1) {
-                const float t = sl.a12 * b01 + sl.a22 * b11;
-                const float prev = j == 0 ? sl.c4 * (sl.b1 * b00 + sl.b2 * b10)
-                                          : (float)((double)(sl.a12 * b00 + sl.a22 * b10) * sl.sd);
-                v = prev + t;
-            } else {
-                const int c = sl.ipx + j;
-                v = (c < 0 || c >= w - 1) ? b00 * sl.b1 + b10 * sl.b2 : b00 * sl.c4 + b01 * sl.a12 + b10 * sl.c5 + b11 * sl.a22;
+        // patch row r, columns j0 and j0 + 1, from image rows r (lo) and r + 1 (hi); both forms
+        // are evaluated and selected, so the pass has no branch
+        auto fill = [&](int q, int r, const uint32_t* lo, const uint32_t* hi) {
+            const float l0 = (float)lo[0], l1 = (float)lo[1], l2 = (float)lo[2];
+            const float h0 = (float)hi[0], h1 = (float)hi[1], h2 = (float)hi[2];
+            const float a12 = fa12[q], a22 = fa22[q], b1 = fb1[q], b2 = fb2[q], c4 = fc4[q], c5 = fc5[q];
+            // in-image: u_k = a12 src[k] + a22 src[k + sst], element j is prev(u_j) + u_{j + 1}
+            const float u1 = a12 * l1 + a22 * h1, u2 = a12 * l2 + a22 * h2;
+            const float p0 = fj0[q] == 0 ? c4 * (b1 * l0 + b2 * h0) : (float)((double)(a12 * l0 + a22 * h0) * fsd[q]);
+            float v0 = p0 + u1;
+            float v1 = (float)((double)u1 * fsd[q]) + u2;
+            if (fmode[q] == 2) {                        // clamped (wave-uniform in practice: border corners last)
+                v0 = (fd[q] & 16) ? l0 * b1 + h0 * b2 : l0 * c4 + l1 * a12 + h0 * c5 + h1 * a22;
+                v1 = (fd[q] & 32) ? l1 * b1 + h1 * b2 : l1 * c4 + l2 * a12 + h1 * c5 + h2 * a22;
             }
-            pr[g][r & 3][j] = v;
+            *reinterpret_cast<float2*>(&pr[fg[q]][r & 3][fj0[q]]) = make_float2(v0, v1);   // column 23: padding
         };
-        uint32_t lo0[NF], lo1[NF], nx0[NF], nx1[NF];
 #pragma unroll
         for (int q = 0; q < NF; q++) {
-            uint32_t a0, a1, b0, b1;
-            load_row(q, 0, a0, a1);
+            uint32_t ra[3], rb[3];
+            load_row(q, 0, ra);
 #pragma unroll
             for (int r = 0; r < 3; r++) {
-                load_row(q, r + 1, b0, b1);
-                fill(q, r, a0, a1, b0, b1);
-                a0 = b0; a1 = b1;
+                if (r & 1) { load_row(q, r + 1, ra); fill(q, r, rb, ra); }
+                else { load_row(q, r + 1, rb); fill(q, r, ra, rb); }
             }
-            lo0[q] = a0; lo1[q] = a1;                   // image row 3
-            load_row(q, 4, nx0[q], nx1[q]);
         }
         double acc = 0.0;
 #pragma unroll 1
         for (int i = 0; i < WW; i++) {
-            uint32_t pf0[NF], pf1[NF];
+            // image rows i + 3, i + 4 for patch row i + 3 (i + 3 < BW), used at the end of the phase
+            uint32_t lo[NF][3], hi[NF][3];
+            const int rr = min(i + 3, BW - 1);
 #pragma unroll
-            for (int q = 0; q < NF; q++) load_row(q, min(i + 5, BW), pf0[q], pf1[q]);   // image row i + 5, phase i + 1
+            for (int q = 0; q < NF; q++) { load_row(q, rr, lo[q]); load_row(q, rr + 1, hi[q]); }
             wave_order();
+            const float e_row = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, e_lane), i));
+            const double py = i - WIN;
+            float d[NT][4];
 #pragma unroll
-            for (int q = 0; q < NT; q++) {             // terms of window row i
-                const int e = q * 64 + lane, g = e / WW, j = e - g * WW;
-                if (e < G * WW && par[g].mode) {
-                    const float* r0 = pr[g][i & 3];
-                    const float* r1 = pr[g][(i + 1) & 3];
-                    const float* r2 = pr[g][(i + 2) & 3];
-                    const double m = smask[i * WW + j];
-                    const double tgx = (double)(r1[j + 2] - r1[j]);
-                    const double tgy = (double)(r2[j + 1] - r0[j + 1]);
-                    const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
-                    const double px = j - WIN, py = i - WIN;
-                    double* o = &tr[j][5 * g];
-                    o[0] = gxx; o[1] = gxy; o[2] = gyy;
-                    o[3] = gxx * px + gxy * py;
-                    o[4] = gxy * px + gyy * py;
-                }
+            for (int q = 0; q < NT; q++) {             // window row i: all passes' patch reads first
+                const int g = tg[q], j = tj[q];
+                d[q][0] = pr[g][(i + 1) & 3][j + 2]; d[q][1] = pr[g][(i + 1) & 3][j];
+                d[q][2] = pr[g][(i + 2) & 3][j + 1]; d[q][3] = pr[g][i & 3][j + 1];
+            }
+#pragma unroll
+            for (int q = 0; q < NT; q++) {
+                const double m = (double)(e_row * e_col[q]);
+                const double tgx = (double)(d[q][0] - d[q][1]);
+                const double tgy = (double)(d[q][2] - d[q][3]);
+                const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
+                const double px = tj[q] - WIN;
+                double* o = &tr[tj[q]][5 * tg[q]];
+                o[0] = gxx; o[1] = gxy; o[2] = gyy;
+                o[3] = gxx * px + gxy * py;
+                o[4] = gxy * px + gyy * py;
             }
             wave_order();
             if (lane < NL) {
@@ -785,13 +820,9 @@ __global__ __launch_bounds__(64) void k_subpix_ms(const uint8_t* __restrict__ im
                 for (int j = 0; j < WW; j++) acc += tr[j][lane];
             }
             wave_order();
-            if (i + 3 < BW) {                          // patch row i + 3 from image rows i + 3, i + 4
+            if (i + 3 < BW) {
 #pragma unroll
-                for (int q = 0; q < NF; q++) {
-                    fill(q, i + 3, lo0[q], lo1[q], nx0[q], nx1[q]);
-                    lo0[q] = nx0[q]; lo1[q] = nx1[q];
-                    nx0[q] = pf0[q]; nx1[q] = pf1[q];
-                }
+                for (int q = 0; q < NF; q++) fill(q, i + 3, lo[q], hi[q]);
             }
         }
         if (lane < NL) ssum[lane] = acc;
@@ -800,7 +831,6 @@ __global__ __launch_bounds__(64) void k_subpix_ms(const uint8_t* __restrict__ im
             const double sa = ssum[5 * lane], sb = ssum[5 * lane + 1], sc = ssum[5 * lane + 2];
             const double bb1 = ssum[5 * lane + 3], bb2 = ssum[5 * lane + 4];
             bool fin = false;
-            nit++;
             const double det = sa * sc - sb * sb;
             if (fabs(det) <= DBL_EPSILON * DBL_EPSILON) fin = true;
             else {
@@ -821,7 +851,7 @@ __global__ __launch_bounds__(64) void k_subpix_ms(const uint8_t* __restrict__ im
         }
         wave_order();
     }
-    if (itcount && lane < G && ncorner) { atomicAdd(itcount, nit); atomicAdd(itcount + 1, ncorner); }
+    if (itcount && lane == 0) { atomicAdd(itcount, nit); atomicAdd(itcount + 1, ncorner); }
 }
 
 // cornerSubPix work order: the corners whose window may leave the image (getRectSubPix's
@@ -1794,6 +1824,7 @@ int lk_levels(int w, int h, int win, int max_level)
 }
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+constexpr size_t kSubpixMaskBytes = sizeof(double) * 21 * 21 + sizeof(float) * 21;   // subpix_mask
 
 int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
 {
@@ -1809,7 +1840,7 @@ int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
     }
     // shared: the two frame copies of the host entry points, the subpix weights; then one block
     // per pair
-    const size_t shared[] = {align256((size_t)w * h), align256((size_t)w * h), align256(sizeof(double) * 21 * 21),
+    const size_t shared[] = {align256((size_t)w * h), align256((size_t)w * h), align256(kSubpixMaskBytes),
                              align256(sizeof(int) * ((size_t)npairs + 1)), align256(sizeof(int) * (size_t)npairs * kMaxPts),
                              256};
     const size_t sizes[] = {align256((size_t)w * h * 4), 256, 256, align256((size_t)gf_key_cap(w, h) * 8),
@@ -1891,9 +1922,16 @@ int flow_grid(const FlowDev* d, int ipw)
     return (int)std::max<int64_t>(1, std::min<int64_t>((most + ipw - 1) / ipw, want));
 }
 
+// the 21 float factors e_k = expf(-x_k^2) sit after the 441 doubles of the mask
+const float* subpix_exp(const double* mask) { return reinterpret_cast<const float*>(mask + 21 * 21); }
 void subpix_mask(int win, double* mask)
 {
     const int n = 2 * win + 1;
+    float* ex = reinterpret_cast<float*>(mask + 21 * 21);
+    for (int k = 0; k < n; k++) {
+        const float x = (float)(k - win) / (float)win;
+        ex[k] = expf(-x * x);
+    }
     for (int i = 0; i < n; i++) {
         const float y = (float)(i - win) / (float)win;
         const float vy = expf(-y * y);
@@ -1924,8 +1962,8 @@ int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride
         FLOW_LAUNCH(d, "k_subpix", s, k_subpix<10>, dim3(flow_grid(d, 1)), dim3(64), 0, s, img, w, h, stride, d->pts,
                     d->offs, d->npairs, d->order, d->mask, iters, e * e, iz, d->pz, itc);
     else
-        FLOW_LAUNCH(d, "k_subpix", s, k_subpix_ms<kSpSlots>, dim3(flow_grid(d, 8 * kSpSlots)), dim3(64), 0, s, img, w, h, stride,
-                    d->pts, d->offs, d->npairs, d->order, d->ocnt + 2, d->mask, iters, e * e, iz, d->pz, itc);
+        FLOW_LAUNCH(d, "k_subpix", s, k_subpix_ms<kSpSlots>, dim3(getenv("COEB_SP_WAVES") ? atoi(getenv("COEB_SP_WAVES")) : flow_grid(d, 8 * kSpSlots)), dim3(64), 0, s, img, w, h, stride,
+                    d->pts, d->offs, d->npairs, d->order, d->ocnt + 2, subpix_exp(d->mask), iters, e * e, iz, d->pz, itc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2048,10 +2086,10 @@ extern "C" int coeb_corner_subpix(coeb_ctx* c, const uint8_t* img, int w, int h,
     FlowCall fc;
     int rc = flow_begin(c, w, h, &fc, "coeb_corner_subpix: invalid arguments");
     if (rc) return rc;
-    double mask[21 * 21];
+    double mask[21 * 21 + 11];                 // + the 21 float factors
     subpix_mask(win, mask);
     if ((rc = upload_gray(c, fc.s, fc.d.prev, img, w, h, stride))) return rc;
-    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
+    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
     FL_TRY(c, hipMemcpyAsync(fc.d.pts, xy, (size_t)n * 8, hipMemcpyHostToDevice, fc.s));
     FL_TRY(c, hipMemcpyAsync(fc.d.npts, &n, 4, hipMemcpyHostToDevice, fc.s));
     if (launch_subpix(&fc.d, fc.d.prev, w, h, w, max_iter, eps, fc.s))
@@ -2135,11 +2173,11 @@ extern "C" int coeb_moving_object_points(coeb_ctx* c, const uint8_t* prev, const
     if (rc) return rc;
     if (lk_levels(w, h, 22, 5) > kLkMaxLevels)
         return coeb_internal_error(c, COEB_EINVAL, "coeb_moving_object_points: image too large");
-    double mask[21 * 21];
+    double mask[21 * 21 + 11];                 // + the 21 float factors
     subpix_mask(10, mask);
     if ((rc = upload_gray(c, fc.s, fc.d.prev, prev, w, h, stride)) || (rc = upload_gray(c, fc.s, fc.d.cur, cur, w, h, stride)))
         return rc;
-    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
+    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
     return coeb_moving_object_points_device(c, fc.d.prev, fc.d.cur, w, h, w, tm_xy, tm_cap, n_tm, dbg);
 }
 
@@ -2211,9 +2249,9 @@ extern "C" int coeb_internal_pmo_batch(coeb_ctx* c, const uint8_t* d_gray, int F
         std::lock_guard<std::mutex> lk(g_pmo_mu);
         g_pmo_last[c] = {w, h, F - 1};
     }
-    double mask[21 * 21];
+    double mask[21 * 21 + 11];                 // + the 21 float factors
     subpix_mask(10, mask);
-    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
+    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
     const int64_t iz = (int64_t)w * h;
     if (launch_gf(&fc.d, d_gray, w, h, w, 1000, 0.01, 8.0, 0.04, fc.s, iz) ||
         launch_subpix(&fc.d, d_gray, w, h, w, 20, 0.03, fc.s, iz) ||
@@ -2236,9 +2274,9 @@ extern "C" int coeb_moving_object_points_device(coeb_ctx* c, const uint8_t* d_pr
     if (rc) return rc;
     if (lk_levels(w, h, 22, 5) > kLkMaxLevels)
         return coeb_internal_error(c, COEB_EINVAL, "coeb_moving_object_points_device: image too large");
-    double mask[21 * 21];
+    double mask[21 * 21 + 11];                 // + the 21 float factors
     subpix_mask(10, mask);
-    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, sizeof(mask), hipMemcpyHostToDevice, fc.s));
+    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
     const int sp = (int)stride;
     if (launch_gf(&fc.d, d_prev, w, h, sp, 1000, 0.01, 8.0, 0.04, fc.s))
         return coeb_internal_error(c, COEB_EDEVICE, "coeb_moving_object_points: goodFeaturesToTrack launch failed");
