@@ -2030,22 +2030,15 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     }
     prof_begin(prof, "k_describe", s);
     const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
-    // keypoints per wave: 8 (COEB_DESC_KP = 4 / 16 / 32 for experiments; 32 was round 1's form)
-    static const int kp = [] { const char* e = getenv("COEB_DESC_KP"); const int v = e ? atoi(e) : 8;
-                               return v == 4 || v == 16 || v == 32 ? v : 8; }();
-    auto describe = [&](auto kv, auto kpc) {
-        constexpr int KP = decltype(kpc)::value;
-        hipLaunchKernelGGL((k_describe<decltype(kv)::value, KP>), dim3((plan.kcap + kWaves * KP - 1) / (kWaves * KP), F),
-                           dim3(kThreads), 0, s, d_plan, b);
-    };
-    using T = std::true_type;
-    using Fl = std::false_type;
-    switch (kp) {
-        case 4: vec0 ? describe(T{}, std::integral_constant<int, 4>{}) : describe(Fl{}, std::integral_constant<int, 4>{}); break;
-        case 16: vec0 ? describe(T{}, std::integral_constant<int, 16>{}) : describe(Fl{}, std::integral_constant<int, 16>{}); break;
-        case 32: vec0 ? describe(T{}, std::integral_constant<int, 32>{}) : describe(Fl{}, std::integral_constant<int, 32>{}); break;
-        default: vec0 ? describe(T{}, std::integral_constant<int, 8>{}) : describe(Fl{}, std::integral_constant<int, 8>{}); break;
-    }
+    // 8 keypoints per wave (round 1's 32 let one XCD's resident waves span ~20 frames and refetch
+    // every patch row past L2; 4 and 16 measured slower)
+    constexpr int KP = 8;
+    if (vec0)
+        hipLaunchKernelGGL((k_describe<true, KP>), dim3((plan.kcap + kWaves * KP - 1) / (kWaves * KP), F), dim3(kThreads), 0,
+                           s, d_plan, b);
+    else
+        hipLaunchKernelGGL((k_describe<false, KP>), dim3((plan.kcap + kWaves * KP - 1) / (kWaves * KP), F), dim3(kThreads), 0,
+                           s, d_plan, b);
     prof_end(prof, s);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -440,178 +440,10 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
 }
 
 // ============================== cornerSubPix ==============================
-// One wave per corner.  Per iteration all 64 lanes fill the 23 x 23 getRectSubPix window into
-// LDS (from the corner's 40 x 40 pixels, staged once; the window may drift 8 px before the image
-// is read directly) and form the five per-pixel terms of 64 window pixels at a time; lanes 0..4
-// then run the five double sums in the reference's row-major order -- each a chain of 441
-// dependent adds per iteration, the kernel's critical path.  The terms of an element pair sit
-// together per term ([pair][term][2] doubles), so the five summing lanes read 80 consecutive
-// bytes with one ds_read_b128 each: no bank conflicts, and one LDS read per two adds.  (Round 2
-// stored them term-major, [term][64]: the five lanes' addresses 512 B apart hit one bank, 2.6e8
-// conflict cycles per launch, 1.5-1.7 ms per 256 pairs; one lane per corner with all five sums
-// in its own registers issued ~12 k instructions per iteration on one lane's worth of corners:
-// 1.9 ms.)  itcount (COEB_SUBPIX_COUNT): {iterations, corners} for tools.
-constexpr int kSpRA = 4;                 // term pairs read ahead of the adds
-template <int WIN>
-__global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0, int w, int h, int stride,
-                                               float* __restrict__ xy0, const int* __restrict__ offs, int P,
-                                               const int* __restrict__ order, const double* __restrict__ maskd,
-                                               int iters, double eps2, int64_t iz, int64_t pz, int* __restrict__ itcount)
-{
-    constexpr int WW = 2 * WIN + 1, BW = WW + 2, NB = BW * BW, NK = WW * WW;
-    constexpr int KPL = (NK + 63) / 64;                // terms per lane
-    constexpr int kSpM = 8, SS = BW + 1 + 2 * kSpM;    // staged pixels: window + drift margin
-    __shared__ float buf[NB];
-    __shared__ __attribute__((aligned(16))) double s_t[32][5][2];   // [element pair][term][element]
-    __shared__ uint8_t px8[SS * SS];
-    const int lane = threadIdx.x;
-    const int total = offs[P];
-    for (int it_ = blockIdx.x; it_ < total; it_ += gridDim.x) {
-    const int item = order[it_];
-    const int2 zp = flow_item(offs, P, item);
-    const uint8_t* img = at_pair(img0, iz, (uint32_t)zp.x);
-    float* xy = at_pair(xy0, pz, (uint32_t)zp.x);
-    const int p = zp.y;
-    // the previous corner's last reads of px8 / buf / s_t are done before they are rewritten
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const float tx = xy[2 * p], ty = xy[2 * p + 1];
-    const int R0x = cv_floor(tx - (float)(BW - 1) * 0.5f) - kSpM, R0y = cv_floor(ty - (float)(BW - 1) * 0.5f) - kSpM;
-    const bool staged = R0x >= 0 && R0y >= 0 && R0x + SS <= w && R0y + SS <= h;
-    if (staged) {
-        const uint8_t* g = img + (size_t)R0y * stride + R0x;
-#pragma unroll 5
-        for (int q = 0; q < (SS * SS + 63) / 64; q++) {
-            const int e = lane + 64 * q;
-            if (e < SS * SS) { const int r = e / SS; px8[e] = g[(size_t)r * stride + (e - r * SS)]; }
-        }
-    }
-    float cx = tx, cy = ty;
-    int it = 0;
-    double err = 0;
-    // getRectSubPix_8u32f's in-image window from rows of `src` (image or staged pixels)
-    auto fill_in = [&](const uint8_t* src0, int sst, float a, float b) {
-        a = a < 0.0001f ? 0.0001f : a;
-        const float a12 = a * (1.f - b), a22 = a * b, b1 = 1.f - b, b2 = b;
-        const double sd = (1. - (double)a) / (double)a;
-#pragma unroll 3
-        for (int e = lane; e < NB; e += 64) {
-            const int r = e / BW, j = e - r * BW;
-            const uint8_t* src = src0 + r * sst;
-            const float t = a12 * (float)src[j + 1] + a22 * (float)src[j + 1 + sst];
-            float prev;
-            if (j == 0) prev = (1.f - a) * (b1 * (float)src[0] + b2 * (float)src[sst]);
-            else {
-                const float tp = a12 * (float)src[j] + a22 * (float)src[j + sst];
-                prev = (float)((double)tp * sd);
-            }
-            buf[e] = prev + t;
-        }
-    };
-    do {
-        const float ctrx = cx - (float)(BW - 1) * 0.5f, ctry = cy - (float)(BW - 1) * 0.5f;
-        const int ipx = cv_floor(ctrx), ipy = cv_floor(ctry);
-        if (ipx >= 0 && ipx + BW < w && ipy >= 0 && ipy + BW < h) {
-            const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
-            if (staged && ipx >= R0x && ipy >= R0y && ipx + BW < R0x + SS && ipy + BW < R0y + SS) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // staged pixels visible
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                fill_in(px8 + (ipy - R0y) * SS + (ipx - R0x), SS, a, b);
-            } else {
-                fill_in(img + (size_t)ipy * stride + ipx, stride, a, b);
-            }
-        } else {
-            const float a = ctrx - (float)ipx, b = ctry - (float)ipy;
-            const float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
-            const float b1 = 1.f - b, b2 = b;
-#pragma unroll 1
-            for (int e = lane; e < NB; e += 64) {
-                const int r = e / BW, j = e - r * BW;
-                const int y0 = min(max(ipy + r, 0), h - 1), y1 = min(max(ipy + r + 1, 0), h - 1);
-                const uint8_t* r0 = img + (size_t)y0 * stride;
-                const uint8_t* r1 = img + (size_t)y1 * stride;
-                const int c = ipx + j;
-                float v;
-                if (c < 0) v = (float)r0[0] * b1 + (float)r1[0] * b2;
-                else if (c >= w - 1) v = (float)r0[w - 1] * b1 + (float)r1[w - 1] * b2;
-                else v = (float)r0[c] * a11 + (float)r0[c + 1] * a12 + (float)r1[c] * a21 + (float)r1[c + 1] * a22;
-                buf[e] = v;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        double acc = 0;
-#pragma unroll 1
-        for (int q = 0; q < KPL; q++) {
-            const int k = lane + 64 * q;
-            double gxx = 0.0, gxy = 0.0, gyy = 0.0, t3 = 0.0, t4 = 0.0;    // +0.0 past the window
-            if (k < NK) {
-                const int i = k / WW, j = k - i * WW;
-                const float* sp = buf + (i + 1) * BW + 1;
-                const double m = maskd[k];
-                const double tgx = (double)(sp[j + 1] - sp[j - 1]);
-                const double tgy = (double)(sp[j + BW] - sp[j - BW]);
-                gxx = tgx * tgx * m; gxy = tgx * tgy * m; gyy = tgy * tgy * m;
-                const double px = j - WIN, py = i - WIN;
-                t3 = gxx * px + gxy * py;
-                t4 = gxy * px + gyy * py;
-            }
-            double* st = &s_t[lane >> 1][0][lane & 1];
-            st[0] = gxx; st[2] = gxy; st[4] = gyy; st[6] = t3; st[8] = t4;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if (lane < 5) {
-                // lane = term; element pairs in order, read kSpRA pairs ahead of the adds
-                const double2* tp = reinterpret_cast<const double2*>(&s_t[0][lane][0]);   // stride 5 per pair
-                double2 cur[kSpRA];
-#pragma unroll
-                for (int u = 0; u < kSpRA; u++) cur[u] = tp[5 * u];
-#pragma unroll 1
-                for (int k0 = kSpRA; k0 <= 32; k0 += kSpRA) {
-                    double2 nx[kSpRA];
-                    const int k1 = k0 < 32 ? k0 : 0;
-#pragma unroll
-                    for (int u = 0; u < kSpRA; u++) nx[u] = tp[5 * (k1 + u)];
-#pragma unroll
-                    for (int u = 0; u < kSpRA; u++) { acc += cur[u].x; acc += cur[u].y; }
-#pragma unroll
-                    for (int u = 0; u < kSpRA; u++) cur[u] = nx[u];
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");     // the next 64 overwrite these
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        }
-        const double sa = __shfl(acc, 0, 64), sb = __shfl(acc, 1, 64), sc = __shfl(acc, 2, 64);
-        const double bb1 = __shfl(acc, 3, 64), bb2 = __shfl(acc, 4, 64);
-        const double det = sa * sc - sb * sb;
-        if (fabs(det) <= DBL_EPSILON * DBL_EPSILON) break;
-        const double scale = 1.0 / det;
-        const float nx = (float)((double)cx + sc * scale * bb1 - sb * scale * bb2);
-        const float ny = (float)((double)cy - sb * scale * bb1 + sa * scale * bb2);
-        err = (double)((nx - cx) * (nx - cx) + (ny - cy) * (ny - cy));
-        cx = nx; cy = ny;
-        if (cx < 0 || cx >= (float)w || cy < 0 || cy >= (float)h) break;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    } while (++it < iters && err > eps2);
-    if (fabsf(cx - tx) > (float)WIN || fabsf(cy - ty) > (float)WIN) { cx = tx; cy = ty; }
-    if (lane == 0) {
-        xy[2 * p] = cx; xy[2 * p + 1] = cy;
-        if (itcount) { atomicAdd(itcount, it + 1); atomicAdd(itcount + 1, 1); }
-    }
-    }
-}
-
-// ---- cornerSubPix, G corners per wave ----
 // The five double sums of an iteration are chains of 441 dependent adds in the reference's
-// row-major order; one corner per wave (k_subpix) runs them on five lanes, so every add costs a
-// whole wave instruction.  Here a wave carries G corner slots, and an iteration is 21 phases, one
+// row-major order.  Round 2 ran one corner per wave and the sums on five lanes, so every add cost
+// a whole wave instruction (1.44 ms per 256 pairs).  Here a wave carries G corner slots (0.89 ms),
+// and an iteration is 21 phases, one
 // per window row i: the fill lanes (slot, column pair) extend each slot's rolling four-row
 // getRectSubPix patch by row i + 3, the term lanes (slot, column) form the five terms of window
 // row i for every slot, and lane 5 g + t adds row i's 21 terms of term t of slot g -- one add
@@ -634,7 +466,7 @@ struct __attribute__((aligned(16))) SpSlot {      // read as three 16-byte words
 __device__ __forceinline__ void wave_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 template <int G>
-__global__ __launch_bounds__(64) void k_subpix_ms(const uint8_t* __restrict__ img0, int w, int h, int stride,
+__global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0, int w, int h, int stride,
                                                   float* __restrict__ xy0, const int* __restrict__ offs, int P,
                                                   const int* __restrict__ order, int* __restrict__ queue,
                                                   const float* __restrict__ mexp, int iters, double eps2, int64_t iz,
@@ -1789,14 +1621,14 @@ struct FlowDev {
     float *pts, *nxt;
     int* npts;
     uint8_t *status, *state;
-    double* mask;                       // cornerSubPix weights (21 x 21, double)
+    float* mexp;                        // cornerSubPix weight factors e_k = expf(-x_k^2), k < 21
     uint8_t* pyr;                       // levels 1.. of both frames
     short2* der;                        // Scharr of every previous-frame level
     float* tm;
     int* ntm;
     double* F;
     int* nf;
-    // batch layout: every pointer above but prev / cur / mask is pair 0's; pair z's copy is
+    // batch layout: every pointer above but prev / cur / mexp is pair 0's; pair z's copy is
     // pz * z bytes further on
     int npairs;
     int64_t pz;
@@ -1824,7 +1656,7 @@ int lk_levels(int w, int h, int win, int max_level)
 }
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
-constexpr size_t kSubpixMaskBytes = sizeof(double) * 21 * 21 + sizeof(float) * 21;   // subpix_mask
+constexpr size_t kSubpixMaskBytes = sizeof(float) * 21;   // subpix_mask
 
 int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
 {
@@ -1859,7 +1691,7 @@ int flow_alloc(coeb_ctx* c, int w, int h, FlowDev* d, int npairs = 1)
     size_t o = 0;
     d->prev = p + o; o += shared[0];
     d->cur = p + o; o += shared[1];
-    d->mask = (double*)(p + o); o += shared[2];
+    d->mexp = (float*)(p + o); o += shared[2];
     d->offs = (int*)(p + o); o += shared[3];
     d->order = (int*)(p + o); o += shared[4];
     d->ocnt = (int*)(p + o); o += shared[5];
@@ -1922,23 +1754,14 @@ int flow_grid(const FlowDev* d, int ipw)
     return (int)std::max<int64_t>(1, std::min<int64_t>((most + ipw - 1) / ipw, want));
 }
 
-// the 21 float factors e_k = expf(-x_k^2) sit after the 441 doubles of the mask
-const float* subpix_exp(const double* mask) { return reinterpret_cast<const float*>(mask + 21 * 21); }
-void subpix_mask(int win, double* mask)
+// cornerSubPix's weights (cornerSubPix: mask(i, j) = vy_i * expf(-x_j^2) in float, x = (k - win) /
+// win): the 2 win + 1 float factors e_k, so mask(i, j) = e_i * e_j (k_subpix forms the product)
+void subpix_mask(int win, float* ex)
 {
     const int n = 2 * win + 1;
-    float* ex = reinterpret_cast<float*>(mask + 21 * 21);
     for (int k = 0; k < n; k++) {
         const float x = (float)(k - win) / (float)win;
         ex[k] = expf(-x * x);
-    }
-    for (int i = 0; i < n; i++) {
-        const float y = (float)(i - win) / (float)win;
-        const float vy = expf(-y * y);
-        for (int j = 0; j < n; j++) {
-            const float x = (float)(j - win) / (float)win;
-            mask[i * n + j] = vy * expf(-x * x);
-        }
     }
 }
 
@@ -1958,12 +1781,8 @@ int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride
     // image with 2 px of drift to spare
     hipLaunchKernelGGL(k_subpix_order, dim3(flow_grid(d, 256)), dim3(256), 0, s, d->pts, d->offs, d->npairs, w, h, 14,
                        d->pz, d->order, d->ocnt);
-    if (getenv("COEB_SUBPIX_ONE"))
-        FLOW_LAUNCH(d, "k_subpix", s, k_subpix<10>, dim3(flow_grid(d, 1)), dim3(64), 0, s, img, w, h, stride, d->pts,
-                    d->offs, d->npairs, d->order, d->mask, iters, e * e, iz, d->pz, itc);
-    else
-        FLOW_LAUNCH(d, "k_subpix", s, k_subpix_ms<kSpSlots>, dim3(getenv("COEB_SP_WAVES") ? atoi(getenv("COEB_SP_WAVES")) : flow_grid(d, 8 * kSpSlots)), dim3(64), 0, s, img, w, h, stride,
-                    d->pts, d->offs, d->npairs, d->order, d->ocnt + 2, subpix_exp(d->mask), iters, e * e, iz, d->pz, itc);
+    FLOW_LAUNCH(d, "k_subpix", s, k_subpix<kSpSlots>, dim3(flow_grid(d, 8 * kSpSlots)), dim3(64), 0, s, img, w, h, stride,
+                d->pts, d->offs, d->npairs, d->order, d->ocnt + 2, d->mexp, iters, e * e, iz, d->pz, itc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2086,10 +1905,10 @@ extern "C" int coeb_corner_subpix(coeb_ctx* c, const uint8_t* img, int w, int h,
     FlowCall fc;
     int rc = flow_begin(c, w, h, &fc, "coeb_corner_subpix: invalid arguments");
     if (rc) return rc;
-    double mask[21 * 21 + 11];                 // + the 21 float factors
+    float mask[21];
     subpix_mask(win, mask);
     if ((rc = upload_gray(c, fc.s, fc.d.prev, img, w, h, stride))) return rc;
-    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
+    FL_TRY(c, hipMemcpyAsync(fc.d.mexp, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
     FL_TRY(c, hipMemcpyAsync(fc.d.pts, xy, (size_t)n * 8, hipMemcpyHostToDevice, fc.s));
     FL_TRY(c, hipMemcpyAsync(fc.d.npts, &n, 4, hipMemcpyHostToDevice, fc.s));
     if (launch_subpix(&fc.d, fc.d.prev, w, h, w, max_iter, eps, fc.s))
@@ -2173,11 +1992,11 @@ extern "C" int coeb_moving_object_points(coeb_ctx* c, const uint8_t* prev, const
     if (rc) return rc;
     if (lk_levels(w, h, 22, 5) > kLkMaxLevels)
         return coeb_internal_error(c, COEB_EINVAL, "coeb_moving_object_points: image too large");
-    double mask[21 * 21 + 11];                 // + the 21 float factors
+    float mask[21];
     subpix_mask(10, mask);
     if ((rc = upload_gray(c, fc.s, fc.d.prev, prev, w, h, stride)) || (rc = upload_gray(c, fc.s, fc.d.cur, cur, w, h, stride)))
         return rc;
-    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
+    FL_TRY(c, hipMemcpyAsync(fc.d.mexp, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
     return coeb_moving_object_points_device(c, fc.d.prev, fc.d.cur, w, h, w, tm_xy, tm_cap, n_tm, dbg);
 }
 
@@ -2249,9 +2068,9 @@ extern "C" int coeb_internal_pmo_batch(coeb_ctx* c, const uint8_t* d_gray, int F
         std::lock_guard<std::mutex> lk(g_pmo_mu);
         g_pmo_last[c] = {w, h, F - 1};
     }
-    double mask[21 * 21 + 11];                 // + the 21 float factors
+    float mask[21];
     subpix_mask(10, mask);
-    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
+    FL_TRY(c, hipMemcpyAsync(fc.d.mexp, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
     const int64_t iz = (int64_t)w * h;
     if (launch_gf(&fc.d, d_gray, w, h, w, 1000, 0.01, 8.0, 0.04, fc.s, iz) ||
         launch_subpix(&fc.d, d_gray, w, h, w, 20, 0.03, fc.s, iz) ||
@@ -2274,9 +2093,9 @@ extern "C" int coeb_moving_object_points_device(coeb_ctx* c, const uint8_t* d_pr
     if (rc) return rc;
     if (lk_levels(w, h, 22, 5) > kLkMaxLevels)
         return coeb_internal_error(c, COEB_EINVAL, "coeb_moving_object_points_device: image too large");
-    double mask[21 * 21 + 11];                 // + the 21 float factors
+    float mask[21];
     subpix_mask(10, mask);
-    FL_TRY(c, hipMemcpyAsync(fc.d.mask, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
+    FL_TRY(c, hipMemcpyAsync(fc.d.mexp, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
     const int sp = (int)stride;
     if (launch_gf(&fc.d, d_prev, w, h, sp, 1000, 0.01, 8.0, 0.04, fc.s))
         return coeb_internal_error(c, COEB_EDEVICE, "coeb_moving_object_points: goodFeaturesToTrack launch failed");
