@@ -367,6 +367,15 @@ def sincos(a):
     return s.value, c.value
 
 
+def gaussian_blur7(img):
+    """GaussianBlur(7x7, sigma 2, REFLECT_101) of one pyramid level (ORBextractor.cc:1317-1318)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros_like(img)
+    lib().oc_gaussian_blur7(ptr(img), w, h, w, ptr(out), w)
+    return out
+
+
 def gauss_kernel7():
     k = (C.c_int * 7)()
     lib().oc_gauss_kernel7(k)

@@ -88,6 +88,33 @@ def test_extract_ragged_sizes(ctx, ex, w, h):
     run_both(ctx, ex, fr[0], tag="%dx%d" % (w, h))
 
 
+@pytest.mark.parametrize("w,h", [(640, 480), (641, 479), (533, 400), (1280, 960), (720, 405)])
+def test_blur_pyramid_matches_oracle(ctx, ex, oracle_mod, w, h):
+    """k_blur's whole blurred pyramid (not only the pixels rBRIEF samples) equals the oracle's
+    GaussianBlur of each oracle pyramid level (ORBextractor.cc:1317-1318), every pixel including
+    the REFLECT_101 borders and the partial 64-column strips of ragged widths."""
+    from coeb_front import Context
+    c2 = ctx if (w, h) != (1280, 960) else Context(2000, 1.2, 8, 20, 7, max_width=w, max_height=h)
+    ex2 = ex if c2 is ctx else oracle_mod.Extractor(2000, 1.2, 8, 20, 7)
+    try:
+        gray = synth.make_frames(w, h, 1, seed=w + 3 * h)[0]
+        r = ex2.extract(gray, debug=True)
+        c2.extract(gray)
+        blur = c2.debug_read("blur")
+        off = 0
+        for l, (lw, lh) in enumerate(ex2.level_sizes(w, h)):
+            lvl = gray if l == 0 else r["pyramid"][r["level_off"][l]:r["level_off"][l] + lw * lh].reshape(lh, lw)
+            ref = oracle_mod.gaussian_blur7(lvl)
+            pitch = (lw + 63) // 64 * 64
+            got = blur[off:off + pitch * lh].reshape(lh, pitch)[:, :lw]
+            bad = np.argwhere(got != ref)
+            assert len(bad) == 0, ("level", l, len(bad), bad[:4].tolist())
+            off = (off + pitch * lh + 255) // 256 * 256
+    finally:
+        if c2 is not ctx:
+            c2.close()
+
+
 @pytest.mark.parametrize("nfeat,scale,nlev", [(500, 1.2, 8), (2000, 1.2, 8), (1000, 1.3, 6), (1000, 1.2, 4),
                                               (1000, 1.1, 10)])
 def test_extract_params(oracle_mod, nfeat, scale, nlev):
