@@ -42,7 +42,9 @@ CONFIGS = {
     # (profiles/r03/s4/benchD_batch.txt).
     "A": dict(w=640, h=480, nfeatures=1000, batch=2048, pipelines=2,
               workload="640x480, 8-level pyramid, 1000 kp, extract + Hamming match to prev frame (BASELINE configs[1])"),
-    "B": dict(w=1280, h=960, nfeatures=2000, workload="1280x960, 8-level pyramid, 2000 kp, extract + match (BASELINE configs[3] shape)"),
+    # B: the fixed 512-frame batch of BASELINE configs[3] as 2 pipelines per GPU (per-rank shards of
+    # 64-256 frames ran 5-10 % faster with 2 than with 1, profiles/r03/s5/shardB_pipelines.txt)
+    "B": dict(w=1280, h=960, nfeatures=2000, pipelines=2, workload="1280x960, 8-level pyramid, 2000 kp, extract + match (BASELINE configs[3] shape)"),
     "C": dict(w=640, h=480, nfeatures=1000, dyn=True, batch=2048, pipelines=2,
               workload="640x480, 1000 kp, YOLO-bbox dynamic mask (2 boxes, 60 T_M points, blur_flag [0,1]) + "
                        "depth association (ComputeStereoFromRGBD) + match to prev frame (BASELINE configs[2])"),

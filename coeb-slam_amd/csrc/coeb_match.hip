@@ -284,20 +284,13 @@ struct MatchLds {
     int* cell; uint32_t* sort; int* owner; int* res; int* qn; float4* kp; uint32_t* desc;
 };
 
-__host__ __device__ inline int next_pow2(int n)
-{
-    int p = 64;
-    while (p < n) p <<= 1;
-    return p;
-}
-
 __host__ __device__ inline size_t match_lds_bytes(int nmax, int qmax, bool lds_cur, size_t* offs)
 {
     const size_t n4 = (size_t)((nmax + 3) & ~3), q4 = (size_t)((qmax + 3) & ~3);
     size_t o = 0;
     size_t off[7];
     off[0] = o; o += ((COEB_GRID_CELLS + 1) * 4 + 15) & ~(size_t)15;
-    off[1] = o; o += (size_t)next_pow2(nmax) * 4;
+    off[1] = o; o += n4 * 4;
     off[2] = o; o += n4 * 4;
     off[3] = o; o += q4 * 4;
     off[4] = o; o += q4 * 4;
@@ -311,14 +304,14 @@ __host__ __device__ inline size_t match_lds_bytes(int nmax, int qmax, bool lds_c
 // build its 64 x 48 grid (Frame::AssignFeaturesToGrid, Frame.cc:396-411) as a CSR by a stable
 // counting sort: L.cell[c] = start of cell c in L.sort, L.sort = (cell << kIdxBits | index) in
 // cell order, index order inside a cell.  L.owner is scratch here.
-template <bool kLds>
+template <bool kLds, int NT = kMThreads>
 __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, const float* cur_ur, const uint8_t* cdesc,
                                            int n, const MatchLds& L)
 {
     const int tid = threadIdx.x;
-    for (int c = tid; c <= COEB_GRID_CELLS; c += kMThreads) L.cell[c] = 0;
+    for (int c = tid; c <= COEB_GRID_CELLS; c += NT) L.cell[c] = 0;
     __syncthreads();
-    for (int i = tid; i < n; i += kMThreads) {
+    for (int i = tid; i < n; i += NT) {
         const Kp k = cur[i];
         const int px = (int)roundf((k.x - cam.min_x) * cam.grid_inv_w);   // PosInGrid (Frame.cc:560)
         const int py = (int)roundf((k.y - cam.min_y) * cam.grid_inv_h);
@@ -331,12 +324,15 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
     }
     __syncthreads();
     {                                      // prefix: L.cell[c + 1] = end of cell c (block scan)
-        static_assert(COEB_GRID_CELLS == 3 * kMThreads, "three cells per thread");
-        __shared__ int s_wsum[kMThreads / 64];
+        constexpr int CPT = COEB_GRID_CELLS / NT;
+        static_assert(COEB_GRID_CELLS == CPT * NT, "whole cells per thread");
+        __shared__ int s_wsum[NT / 64];
         const int lane = tid & 63, wv = tid >> 6;
-        const int c0 = 1 + 3 * tid;
-        const int a0 = L.cell[c0], a1 = L.cell[c0 + 1], a2 = L.cell[c0 + 2];
-        int v = a0 + a1 + a2;
+        const int c0 = 1 + CPT * tid;
+        int a[CPT];
+        int v = 0;
+#pragma unroll
+        for (int k = 0; k < CPT; k++) { a[k] = L.cell[c0 + k]; v += a[k]; }
         for (int o = 1; o < 64; o <<= 1) {
             const int y = __shfl_up(v, o, 64);
             if (lane >= o) v += y;
@@ -345,15 +341,14 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
         __syncthreads();
         int off = 0;
         for (int w = 0; w < wv; w++) off += s_wsum[w];
-        const int end2 = off + v;                           // inclusive prefix through cell c0 + 2
-        L.cell[c0 + 2] = end2;
-        L.cell[c0 + 1] = end2 - a2;
-        L.cell[c0] = end2 - a2 - a1;
+        int end = off + v;                                  // inclusive prefix through cell c0 + CPT - 1
+#pragma unroll
+        for (int k = CPT - 1; k >= 0; k--) { L.cell[c0 + k] = end; end -= a[k]; }
         if (tid == 0) L.cell[0] = 0;
     }
     __syncthreads();
     // scatter with a per-cell cursor (L.cell[c] advances to the end of cell c = start of c+1) ...
-    for (int i = tid; i < n; i += kMThreads) {
+    for (int i = tid; i < n; i += NT) {
         const int cell = L.owner[i];
         if (cell >= 0) {
             const int pos = atomicAdd(&L.cell[cell], 1);
@@ -363,16 +358,16 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
     __syncthreads();
     // ... so shift the cursors back by one cell to get the starts again
     {
-        int v[(COEB_GRID_CELLS + kMThreads) / kMThreads];
+        int v[(COEB_GRID_CELLS + NT) / NT];
 #pragma unroll
-        for (int k = 0; k < (COEB_GRID_CELLS + kMThreads) / kMThreads; k++) {
-            const int c = tid + k * kMThreads;
+        for (int k = 0; k < (COEB_GRID_CELLS + NT) / NT; k++) {
+            const int c = tid + k * NT;
             v[k] = (c >= 1 && c <= COEB_GRID_CELLS) ? L.cell[c - 1] : 0;
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < (COEB_GRID_CELLS + kMThreads) / kMThreads; k++) {
-            const int c = tid + k * kMThreads;
+        for (int k = 0; k < (COEB_GRID_CELLS + NT) / NT; k++) {
+            const int c = tid + k * NT;
             if (c >= 1 && c <= COEB_GRID_CELLS) L.cell[c] = v[k];
         }
         if (tid == 0) L.cell[0] = 0;
@@ -380,7 +375,7 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
     __syncthreads();
     // insertion order inside a cell = keypoint index order (Frame.cc:403-410): sort each
     // (short) cell range by index
-    for (int c = tid; c < COEB_GRID_CELLS; c += kMThreads) {
+    for (int c = tid; c < COEB_GRID_CELLS; c += NT) {
         const int a = L.cell[c], e = L.cell[c + 1];
         for (int x = a + 1; x < e; x++) {
             const uint32_t key = L.sort[x];
@@ -392,7 +387,7 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
     __syncthreads();
     if (kLds) {                            // candidates in CSR order (CurView)
         const int ng = L.cell[COEB_GRID_CELLS];
-        for (int e = tid; e < ng; e += kMThreads) {
+        for (int e = tid; e < ng; e += NT) {
             const int i = (int)(L.sort[e] & ((1u << kIdxBits) - 1));
             const Kp k = cur[i];
             L.kp[e] = make_float4(k.x, k.y, cur_ur ? cur_ur[i] : -1.f, __int_as_float(k.octave));
@@ -420,6 +415,7 @@ __device__ __forceinline__ void first_min_step(const MatchLds& L, uint32_t v, in
     if (key < bk) { bk = key; best = i2; }
 }
 
+template <int NT = kMThreads>
 __device__ bool claims_first_min(const MatchLds& L, const uint32_t* lists, int stride, int n, int nq, int* s_flag)
 {
     const int tid = threadIdx.x;
@@ -437,17 +433,17 @@ __device__ bool claims_first_min(const MatchLds& L, const uint32_t* lists, int s
         }
     }
     for (int it = 0;; it++) {
-        for (int c = tid; c < n; c += kMThreads) L.owner[c] = 0x7fffffff;
+        for (int c = tid; c < n; c += NT) L.owner[c] = 0x7fffffff;
         if (tid == 0) s_flag[1] = 0;
         __syncthreads();
         if (it > 0) {
-            for (int q = tid; q < nq; q += kMThreads) {
+            for (int q = tid; q < nq; q += NT) {
                 const int r = L.res[q];
                 if (r >= 0 && (L.qn[q] & 0x10000)) atomicMin(&L.owner[r], q);
             }
             __syncthreads();
         }
-        for (int q = tid; q < nq; q += kMThreads) {
+        for (int q = tid; q < nq; q += NT) {
             int best = -1;
             uint32_t bk = 0xFFFFFFFFu;
             if (q == tid) {
@@ -481,17 +477,17 @@ __device__ bool claims_first_min(const MatchLds& L, const uint32_t* lists, int s
 // wins), then the rotation-histogram filter (ORBmatcher.cc:1446-1466 / :1580-1597) over
 // rot = angle(q) - cur[res_q].angle when check_ori.  Leaves L.owner[c] = assigned query or -1
 // and returns nmatches (assignments minus the ones the filter removed).  Block-uniform.
-template <class AngleFn>
+template <int NT = kMThreads, class AngleFn>
 __device__ int assign_rotation(const MatchLds& L, int n, int nq, const Kp* cur, int check_ori, AngleFn qangle,
                                int* s_hist, int* s_flag)
 {
     const int tid = threadIdx.x;
-    for (int c = tid; c < n; c += kMThreads) L.owner[c] = -1;
+    for (int c = tid; c < n; c += NT) L.owner[c] = -1;
     if (tid < HISTO_LENGTH) s_hist[tid] = 0;
     if (tid == 0) { s_flag[2] = 0; s_flag[3] = 0; }
     __syncthreads();
     int mine = 0;
-    for (int q = tid; q < nq; q += kMThreads) {
+    for (int q = tid; q < nq; q += NT) {
         const int r = L.res[q];
         if (r >= 0) {
             atomicMax(&L.owner[r], q);
@@ -514,7 +510,7 @@ __device__ int assign_rotation(const MatchLds& L, int n, int nq, const Kp* cur, 
         __syncthreads();
         const int i1 = s_flag[4], i2 = s_flag[5], i3 = s_flag[6];
         int rem = 0;
-        for (int q = tid; q < nq; q += kMThreads) {
+        for (int q = tid; q < nq; q += NT) {
             const int r = L.res[q];
             if (r >= 0) {
                 const int bin = L.qn[q];
@@ -530,8 +526,8 @@ __device__ int assign_rotation(const MatchLds& L, int n, int nq, const Kp* cur, 
     return s_flag[2] - s_flag[3];
 }
 
-template <bool kLds>
-__global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, float th0, int bmono, int check_ori,
+template <bool kLds, int NT>
+__global__ __launch_bounds__(NT, 4) void k_match(MatchCam cam, MatchBufs b, float th0, int bmono, int check_ori,
                                                      int retry_below, int force_seq)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -571,7 +567,7 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
     // ---- phase 0: stage CurrentFrame, grid CSR by a stable counting sort ----
     long long* tm = b.timing ? b.timing + (int64_t)p * 16 : nullptr;   // phase clocks (COEB_MATCH_TIMING)
     if (tm && tid == 0) { tm[0] = clock64(); tm[13] = 0; tm[14] = 0x7fffffffffffffffll; tm[15] = 0; }
-    stage_grid<kLds>(cam, cur, cur_ur, cdesc, n, L);
+    stage_grid<kLds, NT>(cam, cur, cur_ur, cdesc, n, L);
     if (tm && tid == 0) tm[1] = clock64();
 
     // pose algebra (ORBmatcher.cc:1339-1350): twc = -Rcw^T tcw (double accumulation), tlc
@@ -616,10 +612,10 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
             QIn nx;
             load_qin(grp, nx);
             const long long tw0 = tm ? clock64() : 0;
-            for (int q0 = 0; q0 < nl; q0 += kMThreads / kQL) {
+            for (int q0 = 0; q0 < nl; q0 += NT / kQL) {
                 const int q = q0 + grp;
                 const QIn qi = nx;
-                load_qin(q + kMThreads / kQL, nx);
+                load_qin(q + NT / kQL, nx);
                 int cnt = -1;
                 QueryWin w;
                 w.ok = false;
@@ -689,11 +685,11 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
         bool seq = force_seq || s_flag[0];
         // ---- phase 2: claims by fixpoint iteration ----
         if (tm && tid == 0) tm[2 + 4 * attempt] = clock64();
-        if (!seq) seq = claims_first_min(L, lists, kCQ, n, nl, s_flag);
+        if (!seq) seq = claims_first_min<NT>(L, lists, kCQ, n, nl, s_flag);
         if (tm && tid == 0) { tm[3 + 4 * attempt] = clock64(); tm[12 + attempt] = s_flag[7]; }
         // ---- sequential path (overflow / no convergence / forced): literal loop, one thread ----
         if (seq) {
-            for (int c = tid; c < n; c += kMThreads) L.owner[c] = -1;
+            for (int c = tid; c < n; c += NT) L.owner[c] = -1;
             __syncthreads();
             if (tid == 0) {
                 for (int q = 0; q < nl; q++) {
@@ -722,14 +718,14 @@ __global__ __launch_bounds__(kMThreads) void k_match(MatchCam cam, MatchBufs b, 
         }
         // ---- phase 3: mvpMapPoints, rotation consistency ----
         if (tm && tid == 0) tm[4 + 4 * attempt] = clock64();
-        nmatches = assign_rotation(L, n, nl, cur, check_ori, [&](int q) { return last[q].angle; }, s_hist, s_flag);
+        nmatches = assign_rotation<NT>(L, n, nl, cur, check_ori, [&](int q) { return last[q].angle; }, s_hist, s_flag);
         if (tm && tid == 0) tm[5 + 4 * attempt] = clock64();
         __syncthreads();
         if (nmatches >= retry_below) break;
         th = 2 * th0;                                  // Tracking.cc:954-958
     }
     int* mo = b.match + (int64_t)p * b.cur_stride;
-    for (int i = tid; i < n; i += kMThreads) mo[i] = L.owner[i];
+    for (int i = tid; i < n; i += NT) mo[i] = L.owner[i];
     if (tid == 0) b.nmatch[p] = nmatches;
     if (tm && tid == 0) tm[10] = clock64();
 }
@@ -1206,15 +1202,21 @@ int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int b
     const int force_seq = getenv("COEB_MATCH_SEQUENTIAL") ? 1 : 0;   // test knob: exact literal path
     const size_t lds_full = match_lds_bytes(b.cur_stride, b.last_stride, true, nullptr) + 256;
     const size_t lds_min = match_lds_bytes(b.cur_stride, b.last_stride, false, nullptr) + 256;
+    // 512-thread workgroups when a pair's LDS fits half a CU (config A: 80.6 KB), so two pairs
+    // share a CU and one pair's barrier waits overlap the other's work (k_match 0.355 -> 0.335 ms
+    // per 1025-frame launch, profiles/r03/s5/match_nt_ab.txt); otherwise 1024 threads per pair
+    const int nt = lds_full <= 80 * 1024 ? 512 : 1024;
+    auto go = [&](auto kern, size_t lds) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3(P), dim3(nt), lds - 256, s, cam, b, th, bmono, check_ori, retry_below, force_seq);
+    };
     prof_begin(prof, "k_match", s);
     if (lds_full <= 160 * 1024) {
-        (void)hipFuncSetAttribute((const void*)k_match<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_full);
-        hipLaunchKernelGGL(k_match<true>, dim3(P), dim3(kMThreads), lds_full - 256, s, cam, b, th, bmono, check_ori,
-                           retry_below, force_seq);
+        if (nt == 512) go(k_match<true, 512>, lds_full);
+        else go(k_match<true, 1024>, lds_full);
     } else if (lds_min <= 160 * 1024) {
-        (void)hipFuncSetAttribute((const void*)k_match<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_min);
-        hipLaunchKernelGGL(k_match<false>, dim3(P), dim3(kMThreads), lds_min - 256, s, cam, b, th, bmono, check_ori,
-                           retry_below, force_seq);
+        if (nt == 512) go(k_match<false, 512>, lds_min);
+        else go(k_match<false, 1024>, lds_min);
     } else {
         prof_end(prof, s);
         return -2;
