@@ -419,17 +419,25 @@ template <int NT = kMThreads>
 __device__ bool claims_first_min(const MatchLds& L, const uint32_t* lists, int stride, int n, int nq, int* s_flag)
 {
     const int tid = threadIdx.x;
-    // the thread's first query keeps the head of its list in registers across iterations
-    // (global list reads per iteration were most of this phase's time)
-    uint32_t rl[kRegList];
-    int rm = -1;
-    if (tid < nq) {
-        const int qn = L.qn[tid];
-        if (qn >= 0) {
-            rm = qn & 0xFFFF;
-            const uint32_t* lst = lists + (int64_t)tid * stride;
+    // the thread's first QPT queries (tid, tid + NT, ...) keep the heads of their lists in
+    // registers across iterations (global list reads per iteration were most of this phase's
+    // time); a 512-thread workgroup splits the same register budget over two queries
+    constexpr int QPT = NT >= 1024 ? 1 : 1024 / NT;
+    constexpr int RL = kRegList / QPT;
+    uint32_t rl[QPT][RL];
+    int rm[QPT];
 #pragma unroll
-            for (int e = 0; e < kRegList; e++) rl[e] = e < rm ? lst[e] : 0u;
+    for (int u = 0; u < QPT; u++) {
+        const int q = tid + u * NT;
+        rm[u] = -1;
+        if (q < nq) {
+            const int qn = L.qn[q];
+            if (qn >= 0) {
+                rm[u] = qn & 0xFFFF;
+                const uint32_t* lst = lists + (int64_t)q * stride;
+#pragma unroll
+                for (int e = 0; e < RL; e++) rl[u][e] = e < rm[u] ? lst[e] : 0u;
+            }
         }
     }
     for (int it = 0;; it++) {
@@ -443,28 +451,37 @@ __device__ bool claims_first_min(const MatchLds& L, const uint32_t* lists, int s
             }
             __syncthreads();
         }
-        for (int q = tid; q < nq; q += NT) {
+        bool changed = false;
+#pragma unroll
+        for (int u = 0; u < QPT; u++) {
+            const int q = tid + u * NT;
+            if (q < nq) {
+                int best = -1;
+                uint32_t bk = 0xFFFFFFFFu;
+                if (rm[u] >= 0) {
+#pragma unroll
+                    for (int e = 0; e < RL; e++)
+                        if (e < rm[u]) first_min_step(L, rl[u][e], e, q, bk, best);
+                    const uint32_t* lst = lists + (int64_t)q * stride;
+                    for (int e = RL; e < rm[u]; e++) first_min_step(L, lst[e], e, q, bk, best);
+                }
+                if (it == 0 || best != L.res[q]) changed = true;
+                L.res[q] = best;
+            }
+        }
+        for (int q = tid + QPT * NT; q < nq; q += NT) {
             int best = -1;
             uint32_t bk = 0xFFFFFFFFu;
-            if (q == tid) {
-                if (rm >= 0) {
-#pragma unroll
-                    for (int e = 0; e < kRegList; e++)
-                        if (e < rm) first_min_step(L, rl[e], e, q, bk, best);
-                    const uint32_t* lst = lists + (int64_t)q * stride;
-                    for (int e = kRegList; e < rm; e++) first_min_step(L, lst[e], e, q, bk, best);
-                }
-            } else {
-                const int qn = L.qn[q];
-                if (qn >= 0) {
-                    const int m = qn & 0xFFFF;
-                    const uint32_t* lst = lists + (int64_t)q * stride;
-                    for (int e = 0; e < m; e++) first_min_step(L, lst[e], e, q, bk, best);
-                }
+            const int qn = L.qn[q];
+            if (qn >= 0) {
+                const int m = qn & 0xFFFF;
+                const uint32_t* lst = lists + (int64_t)q * stride;
+                for (int e = 0; e < m; e++) first_min_step(L, lst[e], e, q, bk, best);
             }
-            if (it == 0 || best != L.res[q]) s_flag[1] = 1;
+            if (it == 0 || best != L.res[q]) changed = true;
             L.res[q] = best;
         }
+        if (changed) s_flag[1] = 1;
         __syncthreads();
         if (threadIdx.x == 0) s_flag[7] = it + 1;
         if (!s_flag[1]) return false;
