@@ -95,7 +95,7 @@ constexpr int kIdxBits = 12;
 // Lanes per LastFrame query in the candidate phase: a grid column range holds a few
 // candidates (10-px cells), so 8 lanes waste fewer than 16 (measured 0.171 -> 0.147 ms/step)
 #ifndef COEB_MATCH_QL
-#define COEB_MATCH_QL 8
+#define COEB_MATCH_QL 4
 #endif
 constexpr int kQL = COEB_MATCH_QL;
 
