@@ -243,32 +243,49 @@ __device__ inline double pq_cube(double t)
     return h2 + __builtin_fma(l, t, l2);
 }
 
-__device__ bool pq_solve6(const double H[36], const double b[6], double x[6])
+// Index of H(a, b), a <= b, in the 21 upper-triangle terms of buildSystem's order (a outer).
+__host__ __device__ constexpr int pq_hu(int a, int b) { return a * 6 - (a * (a - 1)) / 2 + (b - a); }
+
+// LDLT solve of (H + lambda I) x = b with H given by its 21 upper-triangle terms hu (LDS) and b by
+// bv (LDS); the same operations in the same order as a dense copy Hl = H, Hl(j, j) += lambda
+// (the oracle's pq_solve6).  L is kept packed (15 terms) so thread 0 holds ~40 doubles, not
+// three 6x6 matrices: the kernel then fits 128 VGPRs and two workgroups share a CU.
+__device__ bool pq_solve6(const double* hu, double lambda, const double* bv, double x[6])
 {
-    double L[36], d[6], y[6];
-    for (int i = 0; i < 36; i++) L[i] = 0.0;
+    double L[15], d[6], y[6];
+#define PQ_L(i, j) L[((i) * ((i) - 1)) / 2 + (j)]       // i > j
+#pragma unroll
     for (int j = 0; j < 6; j++) {
-        double v = H[j * 6 + j];
-        for (int k = 0; k < j; k++) v = v - (L[j * 6 + k] * L[j * 6 + k]) * d[k];
+        double v = hu[pq_hu(j, j)] + lambda;
+#pragma unroll
+        for (int k = 0; k < j; k++) v = v - (PQ_L(j, k) * PQ_L(j, k)) * d[k];
         if (!(v > 0.0)) return false;
         d[j] = v;
+#pragma unroll
         for (int i = j + 1; i < 6; i++) {
-            double w = H[i * 6 + j];
-            for (int k = 0; k < j; k++) w = w - (L[i * 6 + k] * L[j * 6 + k]) * d[k];
-            L[i * 6 + j] = w / d[j];
+            double w = hu[pq_hu(j, i)];
+#pragma unroll
+            for (int k = 0; k < j; k++) w = w - (PQ_L(i, k) * PQ_L(j, k)) * d[k];
+            PQ_L(i, j) = w / d[j];
         }
     }
+#pragma unroll
     for (int i = 0; i < 6; i++) {
-        double v = b[i];
-        for (int k = 0; k < i; k++) v = v - L[i * 6 + k] * y[k];
+        double v = bv[i];
+#pragma unroll
+        for (int k = 0; k < i; k++) v = v - PQ_L(i, k) * y[k];
         y[i] = v;
     }
+#pragma unroll
     for (int i = 0; i < 6; i++) y[i] = y[i] / d[i];
+#pragma unroll
     for (int i = 5; i >= 0; i--) {
         double v = y[i];
-        for (int k = i + 1; k < 6; k++) v = v - L[k * 6 + i] * x[k];
+#pragma unroll
+        for (int k = i + 1; k < 6; k++) v = v - PQ_L(k, i) * x[k];
         x[i] = v;
     }
+#undef PQ_L
     return true;
 }
 
@@ -284,6 +301,7 @@ struct PoseLds {
     double part[28][kPartRow];  // per-thread partials, skewed (part_slot)
     double run[28][8];     // 32-lane run sums
     double out[28];        // reduced
+    double hb[27];         // this iteration's 21 Hessian + 6 gradient terms (thread 0's system)
     double rho;
     int qmax, ok, nbad[4], accepted;
 };
@@ -388,7 +406,7 @@ __device__ double active_chi2(PoseLds& L, const PoseBufs& b, const PoseCam& cm, 
 #define PT_INC(slot) do { if (b.timing && threadIdx.x == 0) b.timing[(int64_t)blockIdx.x * 8 + (slot)] += 1; } while (0)
 
 template <int EPT>
-__global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
+__global__ __launch_bounds__(kPT, 2) void k_pose(PoseBufs b, PoseCam cm)
 {
     PT_MARK(t_all);
     EdgeSet<EPT> ES;
@@ -495,15 +513,11 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
             block_reduce(L, acc, 27);
             PT_ADD(1, t_b0);
             PT_MARK(t_s0);
-            double H[36], bv[6];
             if (tid == 0) {
-                int k = 0;
-                for (int a = 0; a < 6; a++)
-                    for (int bb = a; bb < 6; bb++) { H[a * 6 + bb] = L.out[k]; H[bb * 6 + a] = L.out[k]; k++; }
-                for (int a = 0; a < 6; a++) bv[a] = L.out[21 + a];
+                for (int k = 0; k < 27; k++) L.hb[k] = L.out[k];
                 if (iter == 0) {
                     double m = 0.0;
-                    for (int j = 0; j < 6; j++) m = fmax(fabs(H[j * 6 + j]), m);
+                    for (int j = 0; j < 6; j++) m = fmax(fabs(L.out[pq_hu(j, j)]), m);
                     lambda = 1e-5 * m;
                     ni = 2.0;
                 }
@@ -516,11 +530,8 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
             for (;;) {
                 if (tid == 0) {
                     saved = L.s;
-                    double Hl[36];
-                    for (int q = 0; q < 36; q++) Hl[q] = H[q];
-                    for (int j = 0; j < 6; j++) Hl[j * 6 + j] = Hl[j * 6 + j] + lambda;
                     for (int j = 0; j < 6; j++) x[j] = 0.0;
-                    ok2 = pq_solve6(Hl, bv, x) ? 1 : 0;
+                    ok2 = pq_solve6(L.hb, lambda, L.hb + 21, x) ? 1 : 0;
                     if (!ok2) for (int j = 0; j < 6; j++) x[j] = 0.0;
                     const Se3 up = pq_exp(x);
                     L.s = pq_mul(up, saved);
@@ -535,7 +546,7 @@ __global__ __launch_bounds__(kPT) void k_pose(PoseBufs b, PoseCam cm)
                 if (tid == 0) {
                     if (!ok2) tempChi = DBL_MAX;
                     double scale = 0.0;
-                    for (int j = 0; j < 6; j++) scale = scale + x[j] * (lambda * x[j] + bv[j]);
+                    for (int j = 0; j < 6; j++) scale = scale + x[j] * (lambda * x[j] + L.hb[21 + j]);
                     scale = scale + 1e-3;   // g2o OptimizationAlgorithmLevenberg::solve: "make sure it's non-zero"
                     const double rho = (currentChi - tempChi) / scale;
                     if (rho > 0 && isfinite(tempChi)) {
