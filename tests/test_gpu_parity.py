@@ -1020,15 +1020,18 @@ def test_batch_grab_rgbd_loop_matches_oracle(oracle_mod, ex):
         bp.close()
 
 
-@pytest.mark.parametrize("ch,order,dt", [(3, 1, np.uint16), (3, 0, np.uint16), (4, 1, np.float32), (1, 1, np.float32),
-                                         (4, 0, np.uint16)])
-def test_rgbd_preprocess_batch_matches_oracle(oracle_mod, ch, order, dt):
+@pytest.mark.parametrize("ch,order,dt,W,H", [(3, 1, np.uint16, 320, 240), (3, 0, np.uint16, 320, 240),
+                                              (4, 1, np.float32, 320, 240), (1, 1, np.float32, 320, 240),
+                                              (4, 0, np.uint16, 320, 240), (3, 1, np.uint16, 324, 242),
+                                              (1, 1, np.float32, 324, 242)])
+def test_rgbd_preprocess_batch_matches_oracle(oracle_mod, ch, order, dt, W, H):
     """GrabImageRGBD's conversions over a device batch (coeb_rgbd_preprocess_batch_device) vs
     the oracle frame by frame: RGB/BGR/RGBA/BGRA/gray images, 16U depth with 1/5000 and 32F
-    depth with factor 1 (passthrough, Tracking.cc:227) or 1/5000."""
+    depth with factor 1 (passthrough, Tracking.cc:227) or 1/5000.  320x240 frames take the
+    16-pixels-per-thread kernel; 324x242 (W*H not a multiple of 16) the 4-pixel one."""
     import coeb_front as cf
     from coeb_front.pipeline import BatchPipeline
-    F, W, H = 3, 320, 240
+    F = 3
     rng = np.random.default_rng(ch * 10 + order)
     img = rng.integers(0, 256, (F, H, W, ch) if ch > 1 else (F, H, W), dtype=np.uint8)
     if dt == np.uint16:
