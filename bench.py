@@ -837,12 +837,19 @@ def rank_main(ranks, args):
             name, (tot_ms, launches) = dom
             avg_s = tot_ms / launches / 1e3
             frames_per_launch = F - 1 if name in PAIR_KERNELS else F
-            bpl = kernel_bytes(name, w, h, nkp, nkp, npx, ncand, flow) * frames_per_launch
+            # achieved = SURVEY.md s8(d)'s algorithmic bytes per frame (W*H + 60 N_kp + 36 N_prev) x
+            # the frames the launch processes / the launch's average duration; the kernel's own
+            # touched-once bytes are reported beside it as `kernel_own`
+            bpl = (w * h + 60 * nkp + 36 * nkp) * frames_per_launch
             achieved = bpl / avg_s / 1e9
+            own = kernel_bytes(name, w, h, nkp, nkp, npx, ncand, flow) * frames_per_launch
             traffic, tsrc = pmc_traffic(name, frames_per_launch, w, h, tag)
             roof = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, kernel=name,
-                        avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=int(bpl))
+                        avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=int(bpl),
+                        bytes_rule="SURVEY.md s8(d): (W*H + 60*N_kp + 36*N_prev) x %d frames" % frames_per_launch,
+                        kernel_own=dict(bytes_per_launch=int(own), achieved=round(own / avg_s / 1e9, 3),
+                                        frac=round(own / avg_s / 1e9 / HBM_PEAK_GBS, 6)))
             if traffic is not None:
                 roof["traffic_source"] = tsrc
             # the kernel is bound by integer VALU issue, not HBM: the PMC VALU fraction says how
