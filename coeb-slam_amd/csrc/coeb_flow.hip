@@ -3,23 +3,23 @@
 // forms the oracle restates (oracle/orb_oracle.c):
 //
 //   goodFeaturesToTrack(imGrayPre, prepoint, 1000, 0.01, 8, Mat(), 3, true, 0.04)     (:333)
-//     k_gf_response    per pixel: Sobel 3x3 (REFLECT_101) / 3060, cov products, unnormalised 3x3
-//                      box, Harris R (k term in double); image max by ordered-int atomicMax
+//     k_gf_response    Sobel 3x3 (REFLECT_101) / 3060, cov products, unnormalised 3x3 box, Harris R
+//                      (k term in double): one wave per 60-column strip, lane = column sliding
+//                      down, neighbours by DPP wave shifts; image max by ordered-int atomicMax
 //     k_gf_candidates  per pixel: TOZERO at (float)(max*quality), 3x3 dilation, local maxima as
 //                      (ordered value, index) keys
-//     k_gf_select      one workgroup: bitonic sort of the keys in LDS (value desc, index desc =
-//                      greaterThanPtr), then the greedy minDistance selection solved as a
-//                      fixpoint (candidate accepted <=> no accepted earlier candidate closer than
-//                      minDistance), which equals the sequential loop; the first maxCorners kept
+//     k_gf_select      one workgroup: the keys in 4096-key batches of rank order (MSB radix select
+//                      + bitonic sort in LDS), walked 64 at a time by one wave against per-cell
+//                      lists of accepted corners -- the sequential greedy minDistance result
 //   cornerSubPix(imGrayPre, prepoint, Size(10,10), Size(-1,-1), (ITER|EPS, 20, 0.03))   (:334)
-//     k_subpix         one wave per corner: getRectSubPix 23x23 (8u32f) and the per-pixel terms
-//                      into LDS in parallel, the five sums in double in the reference's order
-//                      (one lane each, operands read ahead)
+//     k_subpix         nine corner slots per wave: rolling getRectSubPix rows, per-row terms of
+//                      every slot, one add instruction per term serves nine corners; the five sums
+//                      in double in the reference's order
 //   calcOpticalFlowPyrLK(imGrayPre, imgray, .., Size(22,22), 5, (ITER|EPS, 20, 0.01))   (:335)
-//     k_pyr_down       pyrDown 5x5 [1 4 6 4 1]^2 per level, both frames in one launch
+//     k_pyr_down       pyrDown 5x5 [1 4 6 4 1]^2 per level, lane = output column sliding down a strip
 //     k_sharr          calcSharrDeriv of every level of the previous frame in one launch
-//     k_lk             one wave per point, levels coarse to fine; 484-pixel window sums exact
-//                      (8 pixels per lane in int32, DPP wave reduction of the 16-bit halves)
+//     k_lk             one wave per point, levels coarse to fine; a 3x3 pixel tile per lane, window
+//                      sums exact (int32 per lane, DPP wave reduction of the 16-bit halves)
 //   SAD check (:337-365), findFundamentalMat(.., FM_RANSAC, 0.1, 0.99) (:373), epipolar
 //   distance > 1 -> T_M (:375-384)
 //     k_fm             one workgroup: SAD filter + ordered compaction into LDS, RANSAC in
