@@ -684,7 +684,7 @@ def main():
         from coeb_front.dist import Ranks
         ranks = Ranks()
         if not args.dry_run:
-            check_devices(ranks.local_rank + 1)
+            check_devices(1 if ONE_DEVICE else ranks.local_rank + 1)
         rank_main(ranks, args)
         return
     if args.gpus < 1:
