@@ -193,9 +193,20 @@ __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__
     float ra0 = 0, rb0 = 0, rc0 = 0, ra1 = 0, rb1 = 0, rc1 = 0;
     float rmx = -FLT_MAX;
     const int y1 = min(h, y0 + kGfRows);
-    // pixel rows y0-2 .. y1+1: product rows y0-1 .. y1, output rows y0 .. y1-1
-    for (int yy = y0 - 2; yy <= y1 + 1; yy++) {
-        const int pv = col[(int64_t)reflect101(yy, h) * stride];
+    // pixel rows y0-2 .. y1+1: product rows y0-1 .. y1, output rows y0 .. y1-1; all of the band's
+    // pixel loads are issued before the first is used (one byte per lane each: a row-at-a-time
+    // loop waited a memory round trip per row)
+    int pvv[kGfRows + 4];
+#pragma unroll
+    for (int i = 0; i < kGfRows + 4; i++) {
+        const int yy = y0 - 2 + i;
+        pvv[i] = yy <= y1 + 1 ? (int)col[(int64_t)reflect101(yy, h) * stride] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < kGfRows + 4; i++) {
+        const int yy = y0 - 2 + i;
+        if (yy > y1 + 1) break;
+        const int pv = pvv[i];
         const int pl = wave_shr1(pv), pr = wave_shl1(pv);
         if (yy >= y0) {                                 // Sobel / products of row yy - 1
             const int gx = (pr_m - pl_m) + 2 * (pr_0 - pl_0) + (pr - pl);
@@ -227,6 +238,14 @@ __global__ __launch_bounds__(256) void k_gf_response(const uint8_t* __restrict__
     if (lane == 0) atomicMax(rmax, o);
 }
 
+// Candidates: TOZERO at thr, 3x3 dilation, local maxima (v != 0, v == its 3x3 max) appended as
+// keys (append order is free: k_gf_select sorts them).  One wave per strip of kGcCols columns x
+// kGcRows rows, lane = column (x0 - 1 + lane; lanes 1..62 produce): every thresholded value of the
+// band (+1 row above and below) is loaded once, all rows up front, the vertical 3-max slides down
+// the column and the horizontal one takes the neighbours' by DPP wave shifts.  max is exact, so
+// the 9-value order of the per-pixel form does not matter.  (The per-pixel form read each value
+// nine times: 0.44 ms per 513 pairs.)
+constexpr int kGcCols = 62, kGcRows = 32;
 __global__ __launch_bounds__(256) void k_gf_candidates(const float* __restrict__ R, int w, int h, double quality,
                                                        const uint32_t* __restrict__ rmax, uint64_t* __restrict__ keys,
                                                        int* __restrict__ nkeys, int cap, int64_t pz)
@@ -235,21 +254,31 @@ __global__ __launch_bounds__(256) void k_gf_candidates(const float* __restrict__
     rmax = at_pair(rmax, pz);
     keys = at_pair(keys, pz);
     nkeys = at_pair(nkeys, pz);
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x < 1 || y < 1 || x >= w - 1 || y >= h - 1) return;
+    const int lane = threadIdx.x & 63;
+    const int x0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kGcCols, y0 = blockIdx.y * kGcRows;
+    if (x0 >= w) return;
+    const int c = x0 - 1 + lane;
+    const bool incol = c >= 0 && c < w;
+    const bool produce = lane >= 1 && lane <= kGcCols && c >= 1 && c < w - 1;
     const float thr = (float)((double)ord2f(*rmax) * quality);
-    auto eig = [&](int xx, int yy) {
-        const float r = R[(size_t)yy * w + xx];
-        return r > thr ? r : 0.f;
-    };
-    const float v = eig(x, y);
-    if (v == 0.f) return;
-    float m = v;
-    for (int dy = -1; dy <= 1; dy++)
-        for (int dx = -1; dx <= 1; dx++) m = fmaxf(m, eig(x + dx, y + dy));
-    if (v != m) return;
-    const int pos = atomicAdd(nkeys, 1);
-    if (pos < cap) keys[pos] = ((uint64_t)f2ord(v) << 32) | (uint32_t)(y * w + x);   // larger = earlier
+    float e[kGcRows + 2];                              // rows y0 - 1 .. y0 + kGcRows
+#pragma unroll
+    for (int i = 0; i < kGcRows + 2; i++) {
+        const int yy = y0 - 1 + i;
+        const float r = incol && yy >= 0 && yy < h ? R[(size_t)yy * w + c] : 0.f;
+        e[i] = r > thr ? r : 0.f;
+    }
+#pragma unroll
+    for (int i = 1; i <= kGcRows; i++) {
+        const int y = y0 - 1 + i;
+        const float vm = fmaxf(fmaxf(e[i - 1], e[i]), e[i + 1]);
+        const float m = fmaxf(fmaxf(wave_shr1f(vm), vm), wave_shl1f(vm));
+        const float v = e[i];
+        if (produce && y >= 1 && y < h - 1 && v != 0.f && v == m) {
+            const int pos = atomicAdd(nkeys, 1);
+            if (pos < cap) keys[pos] = ((uint64_t)f2ord(v) << 32) | (uint32_t)(y * w + c);   // larger = earlier
+        }
+    }
 }
 
 // block-wide exclusive prefix of one flag per thread (1024 threads); returns the total
@@ -776,28 +805,44 @@ __global__ __launch_bounds__(256) void k_pyr_down(PyrDownArgs a, int64_t iz, int
     }
 }
 
-// calcSharrDeriv of every previous-frame level; blockIdx.y = level, blockIdx.z = pair,
-// grid-stride over pixels
+// calcSharrDeriv of every previous-frame level; blockIdx.y = level, blockIdx.z = pair.  One wave
+// per strip of kShCols columns x kShRows rows of a level, lane = column (x0 - 1 + lane; lanes
+// 1..62 produce): the band's source bytes (+1 row above and below, the trow border rule) are all
+// loaded up front, each lane forms its column's vertical terms t0 = 3 (s0 + s2) + 10 s1 and
+// t1 = s2 - s0, and the neighbours' come by DPP wave shifts -- the same integer expressions as
+// calcSharrDeriv, one byte load per pixel.  (The grid-stride per-pixel form read 9 bytes per pixel
+// with a division per pixel, and its level-0 blocks ran 19 passes while the others idled.)
+constexpr int kShCols = 62, kShRows = 32;
 __global__ __launch_bounds__(256) void k_sharr(LkPyr pyr, int64_t iz, int64_t pz)
 {
     const int l = blockIdx.y;
     const int w = pyr.w[l], h = pyr.h[l], pitch = pyr.pitch[l];
+    const int nstrip = (w + kShCols - 1) / kShCols, nband = (h + kShRows - 1) / kShRows;
+    const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= nstrip * nband) return;
+    const int strip = item % nstrip, band = item / nstrip;
     const uint8_t* img = at_pair(pyr.P[l], l == 0 ? iz : pz);
     short2* d = at_pair(const_cast<short2*>(pyr.D[l]), pz);
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < w * h; e += gridDim.x * 256) {
-        const int y = e / w, x = e - y * w;
-        const uint8_t* s0 = img + (size_t)(y > 0 ? y - 1 : (h > 1 ? 1 : 0)) * pitch;
-        const uint8_t* s1 = img + (size_t)y * pitch;
-        const uint8_t* s2 = img + (size_t)(y < h - 1 ? y + 1 : (h > 1 ? h - 2 : 0)) * pitch;
-        auto col = [&](int c) {             // trow border: trow[-1] = trow[1], trow[w] = trow[w-2]
-            if (c < 0) return w > 1 ? 1 : 0;
-            if (c >= w) return w > 1 ? w - 2 : 0;
-            return c;
-        };
-        const int xl = col(x - 1), xr = col(x + 1);
-        const int t0l = (s0[xl] + s2[xl]) * 3 + s1[xl] * 10, t0r = (s0[xr] + s2[xr]) * 3 + s1[xr] * 10;
-        const int t1l = s2[xl] - s0[xl], t1r = s2[xr] - s0[xr], t1c = s2[x] - s0[x];
-        d[e] = make_short2((short)(t0r - t0l), (short)((t1r + t1l) * 3 + t1c * 10));
+    const int lane = threadIdx.x & 63;
+    const int x0 = strip * kShCols, y0 = band * kShRows, y1 = min(h, y0 + kShRows);
+    const int c = x0 - 1 + lane;
+    // trow border: trow[-1] = trow[1], trow[w] = trow[w-2]; columns past w are never used
+    const int cc = c < 0 ? (w > 1 ? 1 : 0) : (c >= w ? (w > 1 ? w - 2 : 0) : c);
+    const bool produce = lane >= 1 && lane <= kShCols && c < w;
+    int px[kShRows + 2];                               // source rows y0 - 1 .. y0 + kShRows
+#pragma unroll
+    for (int i = 0; i < kShRows + 2; i++) {
+        const int yy = y0 - 1 + i;
+        const int yr = yy < 0 ? (h > 1 ? 1 : 0) : (yy >= h ? (h > 1 ? h - 2 : 0) : yy);
+        px[i] = yy <= y1 ? (int)img[(size_t)yr * pitch + cc] : 0;
+    }
+#pragma unroll
+    for (int i = 1; i <= kShRows; i++) {
+        const int y = y0 - 1 + i;
+        if (y >= y1) break;
+        const int t0 = (px[i - 1] + px[i + 1]) * 3 + px[i] * 10, t1 = px[i + 1] - px[i - 1];
+        const int t0l = wave_shr1(t0), t0r = wave_shl1(t0), t1l = wave_shr1(t1), t1r = wave_shl1(t1);
+        if (produce) d[(size_t)y * w + c] = make_short2((short)(t0r - t0l), (short)((t1r + t1l) * 3 + t1 * 10));
     }
 }
 
@@ -1725,11 +1770,12 @@ int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, in
     if (lds > 160 * 1024) return -2;
     (void)hipMemset2DAsync(d->rmax, (size_t)d->pz, 0, 4, P, s);      // one word per pair
     (void)hipMemset2DAsync(d->nkeys, (size_t)d->pz, 0, 4, P, s);
-    const dim3 grid((w + 15) / 16, (h + 15) / 16, P);
     FLOW_LAUNCH(d, "k_gf_response", s, k_gf_response, dim3((w + 4 * kGfCols - 1) / (4 * kGfCols), (h + kGfRows - 1) / kGfRows, P),
                 dim3(256), 0, s, img, w, h,
                        stride, k, d->R, d->rmax, iz, d->pz);
-    FLOW_LAUNCH(d, "k_gf_candidates", s, k_gf_candidates, grid, dim3(256), 0, s, d->R, w, h, quality, d->rmax, d->keys, d->nkeys,
+    FLOW_LAUNCH(d, "k_gf_candidates", s, k_gf_candidates,
+                dim3((w + 4 * kGcCols - 1) / (4 * kGcCols), (h + kGcRows - 1) / kGcRows, P), dim3(256), 0, s, d->R, w,
+                h, quality, d->rmax, d->keys, d->nkeys,
                        gf_key_cap(w, h), d->pz);
     (void)hipFuncSetAttribute((const void*)k_gf_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     FLOW_LAUNCH(d, "k_gf_select", s, k_gf_select, dim3(1, 1, P), dim3(kGfThreads), lds, s, d->keys, d->nkeys, w, h, max_corners,
@@ -1819,7 +1865,8 @@ int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, 
                                                          chained ? P + 1 : 2 * P), dim3(256), 0, s, a,
                            iz, d->pz);
     }
-    FLOW_LAUNCH(d, "k_sharr", s, k_sharr, dim3(64, L, P), dim3(256), 0, s, pyr, iz, d->pz);
+    const int sh_items = ((w + kShCols - 1) / kShCols) * ((h + kShRows - 1) / kShRows);   // level 0 is the largest
+    FLOW_LAUNCH(d, "k_sharr", s, k_sharr, dim3((sh_items + 3) / 4, L, P), dim3(256), 0, s, pyr, iz, d->pz);
     launch_flow_index(d, s);            // the host LK entry point sets npts without cornerSubPix
     int* itc = nullptr;
     if (getenv("COEB_SUBPIX_COUNT")) {
