@@ -818,6 +818,11 @@ def rank_main(ranks, args):
         bp.ctx.profile_reset()
         for _ in range(prof_steps):
             bp.run(**kw)
+            if chain:
+                # the configs[4] loop runs PoseOptimization / TrackLocalMap on a pose stream that
+                # overlaps the next step's conversion and flow kernels: join it, so every event
+                # pair brackets a launch with nothing else on the device
+                bp.synchronize()
         bp.synchronize()
         prof = bp.ctx.profile_read()
         bp.ctx.profile(False)
