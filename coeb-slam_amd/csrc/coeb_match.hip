@@ -68,10 +68,10 @@ __global__ __launch_bounds__(kThreads) void k_prep(PrepBufs b)
 }
 
 // ================================ k_match ================================
-// One workgroup (1024 threads) per frame pair.
+// One workgroup per frame pair (512 threads when the pair's LDS fits half a CU, else 1024).
 //   phase 0  stage CurrentFrame (x, y, uR, octave, descriptor) in LDS; build the 64 x 48
-//            grid as a CSR by a bitonic sort of (cell << 12 | index): a cell column ix over
-//            rows [iy0, iy1] is one contiguous range, so range order == the reference's
+//            grid as a CSR by a stable counting sort of (cell << 12 | index): a cell column ix
+//            over rows [iy0, iy1] is one contiguous range, so range order == the reference's
 //            (ix outer, iy inner, insertion order) enumeration.
 //   phase 1  one thread per LastFrame point: projection, window, level / window / stereo
 //            filters and Hamming distance; the candidates with dist <= TH_HIGH are kept in
@@ -93,7 +93,9 @@ constexpr int kCQ = 64;
 constexpr int kMaxIter = 64;
 constexpr int kIdxBits = 12;
 // Lanes per LastFrame query in the candidate phase: a grid column range holds a few
-// candidates (10-px cells), so 8 lanes waste fewer than 16 (measured 0.171 -> 0.147 ms/step)
+// candidates (10-px cells), so few lanes per query waste least (round 1: 16 -> 8 lanes, 0.171 ->
+// 0.147 ms/step; round 3: 8 -> 4 lanes, lists 174k -> 160k cycles per pair, k_match 0.314 ->
+// 0.309 ms per 1025-frame launch)
 #ifndef COEB_MATCH_QL
 #define COEB_MATCH_QL 4
 #endif
