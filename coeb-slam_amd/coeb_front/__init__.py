@@ -24,6 +24,7 @@ or without a gfx950 device raises.
 """
 import ctypes as C
 import os
+import re
 
 import numpy as np
 
@@ -56,7 +57,11 @@ ABI_SYMBOLS = [
     "coeb_track_local_map_batch_device", "coeb_batch_track_results", "coeb_rgbd_preprocess_batch_device",
     "coeb_marker_create", "coeb_marker_destroy", "coeb_marker_record_ctx", "coeb_marker_record_copyq",
     "coeb_ctx_wait_marker", "coeb_copyq_wait_marker", "coeb_marker_synchronize",
+    "coeb_tum_read_list", "coeb_tum_associate",
 ]
+# COEB_ABI_VERSION of the include/coeb_front.h these argtypes are written against; lib() refuses
+# a library that reports another (tests/test_capi_symbols.py keeps the two equal)
+ABI_VERSION = 3
 
 
 class OrbParams(C.Structure):
@@ -115,6 +120,10 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise CoebError("libcoeb_front.so not built (run __graft_entry__.build() or make -C coeb-slam_amd/csrc)")
         L = C.CDLL(LIB_PATH)
+        got = L.coeb_abi_version()
+        if got != ABI_VERSION:
+            raise CoebError("%s reports ABI %d, this binding is written for ABI %d (rebuild the library)"
+                            % (LIB_PATH, got, ABI_VERSION))
         L.coeb_create.restype = C.c_void_p
         L.coeb_create.argtypes = [C.POINTER(OrbParams), C.c_int, C.c_int, C.c_int, C.c_int]
         L.coeb_destroy.argtypes = [C.c_void_p]
@@ -181,6 +190,10 @@ def lib():
         L.coeb_rgbd_preprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_void_p,
                                            C.c_size_t, C.c_int, C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.coeb_descriptor_distance.argtypes = [C.c_void_p, C.c_void_p]
+        L.coeb_tum_read_list.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                         C.POINTER(C.c_int)]
+        L.coeb_tum_associate.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_double, C.c_double,
+                                         C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
         L.coeb_profile_enable.argtypes = [C.c_void_p, C.c_int]
         L.coeb_profile_reset.argtypes = [C.c_void_p]
         L.coeb_profile_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
@@ -513,6 +526,43 @@ def GrabImageRGBD(ctx, imRGB, imD=None, mbRGB=True, mDepthMapFactor=1.0):
                                          _p(d) if imD is not None else None, dstride, dtype,
                                          C.c_float(mDepthMapFactor), w, h, _p(gray), _p(dep)))
     return gray, dep
+
+
+def tum_read_file_list(text_or_path):
+    """associate.py read_file_list (associate.py:49-69) through coeb_tum_read_list: a dict
+    {stamp: [data fields]} of a TUM list file (a path, or the file's text if it holds a newline)."""
+    if "\n" not in text_or_path:
+        with open(text_or_path) as f:
+            text_or_path = f.read()
+    raw = text_or_path.encode()
+    cap = raw.count(b"\n") + 1
+    st = np.zeros(cap, np.float64)
+    off = np.zeros(cap, np.int64)
+    ln = np.zeros(cap, np.int32)
+    n = C.c_int(0)
+    rc = lib().coeb_tum_read_list(raw, len(raw), _p(st), _p(off), _p(ln), cap, C.byref(n))
+    if rc != 0:
+        raise CoebError("coeb_tum_read_list: %d (a stamp field is not a float literal)" % rc)
+    sep = re.compile(r"[ ,\t]+")
+    return {float(st[i]): [v.strip() for v in sep.split(raw[off[i]:off[i] + ln[i]].decode()) if v.strip()]
+            for i in range(n.value)}
+
+
+def tum_associate(first, second, offset=0.0, max_difference=0.02):
+    """associate.py associate (associate.py:71-102) through coeb_tum_associate: the matched
+    (stamp_first, stamp_second) pairs ordered by stamp.  first / second: stamp collections (the
+    dicts of tum_read_file_list, or arrays)."""
+    a = np.ascontiguousarray(list(first), np.float64)
+    b = np.ascontiguousarray(list(second), np.float64)
+    cap = max(1, min(len(a), len(b)))
+    ia = np.zeros(cap, np.int32)
+    ib = np.zeros(cap, np.int32)
+    n = C.c_int(0)
+    rc = lib().coeb_tum_associate(_p(a), len(a), _p(b), len(b), float(offset), float(max_difference), _p(ia), _p(ib),
+                                  cap, C.byref(n))
+    if rc != 0:
+        raise CoebError("coeb_tum_associate: %d" % rc)
+    return [(float(a[ia[k]]), float(b[ib[k]])) for k in range(n.value)]
 
 
 def boxes_from_ros(xyxy):

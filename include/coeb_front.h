@@ -44,6 +44,8 @@
  *                                      (OpenCV goodFeaturesToTrack / cornerSubPix / calcOpticalFlowPyrLK /
  *                                      findFundamentalMat as called there)
  *   coeb_descriptor_distance        <- ORBmatcher::DescriptorDistance  src/ORBmatcher.cc:1648-1664
+ *   coeb_tum_read_list              <- associate.py read_file_list  associate.py:49-69
+ *   coeb_tum_associate              <- associate.py associate  associate.py:71-102 (host only)
  *
  * Conventions: 0 on success, negative COEB_E* code on failure (the reference has no error
  * returns: it asserts or is UB).  The caller owns host buffers; the context
@@ -347,6 +349,23 @@ int coeb_undistort_keypoints(coeb_ctx* ctx, const coeb_camera* cam, const float 
                              int n, coeb_keypoint* out);
 /* yolov5_ros_msgs/BoundingBox (int64 xmin, ymin, xmax, ymax) -> coeb_box, as GrabRGBD converts */
 int coeb_boxes_from_int64(const int64_t* xyxy, int nbox, coeb_box* out);
+
+/* ---- TUM RGB-D time-stamp lists (associate.py, the ingest step before GrabImageRGBD) ----
+ * Host-only (no context, no device).  coeb_tum_read_list parses a list file's text
+ * (associate.py:49-69): lines split at '\n'; ',' and TAB separate fields like ' '; a line whose
+ * first byte is '#' is a comment; lines with fewer than two fields are ignored; the first field
+ * must be a decimal float literal (else COEB_EINVAL, where read_file_list raises).  A stamp that
+ * occurs twice keeps its last line at the position of its first (the reference's dict).  Per
+ * entry: the stamp, and the byte offset / length in `text` of its data fields (second field to
+ * the end of the last).  *n_out = entries; COEB_ERANGE when that exceeds cap (nothing written).
+ * coeb_tum_associate (associate.py:71-102): candidates |a - (b + offset)| < max_difference in
+ * double, taken greedily by increasing (difference, a, b), each stamp once, returned as index
+ * pairs into first / second ordered by (a, b); a stamp given twice is its last index, NaN never
+ * matches.  *n_out = matches; COEB_ERANGE when that exceeds cap. */
+int coeb_tum_read_list(const char* text, size_t len, double* stamps, int64_t* data_off, int32_t* data_len, int cap,
+                       int* n_out);
+int coeb_tum_associate(const double* first, int n_first, const double* second, int n_second, double offset,
+                       double max_difference, int32_t* first_idx, int32_t* second_idx, int cap, int* n_out);
 
 /* ---- Frame::ProcessMovingObject (src/Frame.cc:311-393): T_M from imGrayPre and imgray ----
  * Each stage replaces the OpenCV 3.4 call Frame.cc makes, in the canonical forms of DESIGN.md

@@ -69,6 +69,10 @@ def test_abi_version_matches_header(lib):
     txt = open(os.path.join(ROOT, "include", "coeb_front.h")).read()
     want = int(re.search(r"#define COEB_ABI_VERSION (\d+)", txt).group(1))
     assert lib.coeb_abi_version() == want
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "coeb-slam_amd"))
+    import coeb_front
+    assert coeb_front.ABI_VERSION == want      # the ctypes argtypes are written for this header
 
 
 def test_last_error_is_per_thread(lib):

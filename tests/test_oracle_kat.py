@@ -524,15 +524,52 @@ def test_undistort_oracle_round_trip(oracle_mod):
 
 
 def test_tum_association_golden():
-    """coeb_front.tum vs the reference associate.py's own output (tests/golden/make_tum_golden.py)."""
+    """coeb_tum_read_list + coeb_tum_associate (host C++ behind the C-ABI) vs the reference
+    associate.py's own output on the same lists (tests/golden/make_tum_golden.py)."""
     import json
-    from coeb_front import tum
+    import coeb_front
     cases = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tum_assoc.json")))
     for c in cases:
-        got = tum.associate(tum.read_file_list(c["rgb"]), tum.read_file_list(c["depth"]), c["offset"],
-                            c["max_difference"])
+        rgb, depth = coeb_front.tum_read_file_list(c["rgb"]), coeb_front.tum_read_file_list(c["depth"])
+        got = coeb_front.tum_associate(rgb, depth, c["offset"], c["max_difference"])
         assert [list(x) for x in got] == c["matches"]
         assert len(got) > 20
+        assert all(len(v) >= 1 for v in rgb.values())
+
+
+def test_tum_association_edge_cases():
+    """The association's definition on hand cases: greedy by (difference, a, b), each stamp once,
+    the strict < max_difference bound, offset applied to the second list, ties on the difference
+    broken by a then b, duplicates / NaN / comments / short lines in the lists."""
+    import coeb_front
+    A = coeb_front.tum_associate
+    assert A([], [1.0]) == [] and A([1.0], []) == []
+    assert A([1.0, 2.0], [1.01, 1.99]) == [(1.0, 1.01), (2.0, 1.99)]
+    assert A([1.0], [1.02]) == []                                   # |d| == 0.02 is not < 0.02
+    assert A([1.0], [1.015]) == [(1.0, 1.015)]
+    assert A([1.0, 1.02], [1.01]) == [(1.0, 1.01)]                  # equal |d|: smaller a first
+    assert A([1.01], [1.0, 1.02]) == [(1.01, 1.0)]                  # equal |d| and a: smaller b first
+    assert A([1.0, 1.011], [1.01]) == [(1.011, 1.01)]               # greedy: the closer pair wins
+    assert A([5.0], [4.5], offset=0.5) == [(5.0, 4.5)]
+    assert A([1.0, 1.0], [1.0]) == [(1.0, 1.0)]                     # a stamp given twice is one stamp
+    assert A([float("nan"), 1.0], [float("nan"), 1.0]) == [(1.0, 1.0)]
+    rng = np.random.default_rng(7)
+    a = np.sort(rng.uniform(0, 30, 900)).round(6)
+    b = np.sort(a + rng.normal(0, 0.01, a.size)).round(6)
+    got = A(a, b, 0.003, 0.02)
+    # brute force of the definition
+    cand = sorted((abs(x - (y + 0.003)), x, y) for x in set(a.tolist()) for y in set(b.tolist())
+                  if abs(x - (y + 0.003)) < 0.02)
+    ua, ub, want = set(), set(), []
+    for _, x, y in cand:
+        if x not in ua and y not in ub:
+            ua.add(x), ub.add(y), want.append((x, y))
+    assert got == sorted(want) and len(got) > 500
+    text = "# c\n1.5 rgb/a.png\n\n2.5,rgb/b.png x\n3.5\n #x\n".replace(" #x\n", "")
+    lst = coeb_front.tum_read_file_list(text + "2.5\trgb/c.png\n")
+    assert lst == {1.5: ["rgb/a.png"], 2.5: ["rgb/c.png"]}
+    with pytest.raises(coeb_front.CoebError):
+        coeb_front.tum_read_file_list("x.png 1.0\n")               # read_file_list's float() raises
 
 
 def test_grab_image_rgbd_conversions_kat(oracle_mod):
