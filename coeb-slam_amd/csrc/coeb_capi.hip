@@ -179,6 +179,10 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
             while (rtab.size() % 4) rtab.push_back(0);     // 16-byte aligned table rows
             g.rtab_off = (int)rtab.size();
             g.xmax = resize_tables(P.lv[l - 1].w, P.lv[l - 1].h, g.w, g.h, rtab);
+            const int* xofs = rtab.data() + g.rtab_off;
+            g.rows_ok = 1;
+            for (int c = 0; c < g.w; c += 2)
+                if (xofs[std::min(c + 1, g.w - 1)] - (xofs[c] & ~3) > 5) g.rows_ok = 0;
         }
         // FAST cells (ComputeKeyPointsOctTree :795-829)
         const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;

@@ -149,6 +149,13 @@ __global__ void k_dynmask(ExtractBufs b, int F, int W, int H)
     b.dyn[f] = m;
 }
 
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us2, v); }
+__device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ us2 pk2(int lo, int hi) { us2 r; r.x = (unsigned short)lo; r.y = (unsigned short)hi; return r; }
+
 // ================================ k_pyr_level ================================
 // cv::resize INTER_LINEAR 8U, canonical rounding.  Four consecutive output
 // pixels per thread (one 32-bit store); the <= 12 source bytes they need from each of the
@@ -302,6 +309,88 @@ __global__ __launch_bounds__(kThreads) void k_pyr_level(const uint8_t* __restric
     }
 }
 
+// k_pyr_rows: the same resize for the common case (scale <= 2, 4-byte aligned source rows),
+// shaped for VALU issue, which bounds the extraction step:
+//   * a wave owns 128 output columns (2 per lane) of PR_ROWS output rows; the rows are wave-
+//     uniform, so yofs / beta / the row clamps / the row addresses are scalar work;
+//   * each lane loads its 8-byte window of a source row (two dword loads from the row's SGPR
+//     base, the second clamped inside the pitch) for all of its rows before the first use;
+//   * horizontal pass as one v_dot2_u32_u16 per output and source row: a v_perm with a per-column
+//     selector lifts (S[sx], S[sx+1]) into a u16 pair, dotted with the packed (a0, a1);
+//   * vertical pass on h: SIMD columns ((h0 >> 4) * b0 >> 16) + ((h1 >> 4) *
+//     b1 >> 16) + 2 >> 2, each term v_mul_hi_u32_u24(h & ~15, b << 12) (16 * 4096 = 2^16; both
+//     operands < 2^24); tail columns (>= xs) (h0*b0 + h1*b1 + 2^21) >> 22.
+// About 10.5 VALU lane-operations per output pixel against ~38 for k_pyr_level's byte form.
+constexpr int PR_ROWS = 8, PR_COLS = 128;
+
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+
+__global__ __launch_bounds__(kThreads) void k_pyr_rows(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
+                                                       int sh, uint8_t* __restrict__ dst, int64_t dst_fs, int dp,
+                                                       int dw, int dh, const int* __restrict__ tab, int xmax, int xs)
+{
+    const int f = blockIdx.z;
+    const int oy = (blockIdx.y * kWaves + wave_id()) * PR_ROWS;
+    if (oy >= dh) return;
+    const int lane = lane_id();
+    const int ox = blockIdx.x * PR_COLS;
+    const int cx = ox + 2 * lane;
+    const int* xofs = tab;
+    const int* alpha = tab + dw;
+    const int* yofs = tab + 2 * dw;
+    const int* beta = tab + 2 * dw + dh;
+    uint32_t sel[2], coef[2];
+    const int d0 = min(cx, dw - 1);
+    const int wb = xofs[d0] & ~3;                 // the lane's window: source bytes wb .. wb + 7
+    const int wb1 = min(wb + 4, sp - 4);          // (the second word stays inside the row's pitch)
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int d = min(cx + k, dw - 1);
+        const int o = xofs[d] - wb;               // <= 5 for scale <= 2 (host checks)
+        const int a = alpha[d];
+        const uint32_t a0 = d >= xmax ? 2048u : (uint32_t)(a & 0xFFFF), a1 = d >= xmax ? 0u : (uint32_t)a >> 16;
+        coef[k] = a0 | (a1 << 16);
+        sel[k] = (uint32_t)o | 0x0c00u | ((uint32_t)(o + 1) << 16) | 0x0c000000u;
+    }
+    const uint8_t* S = src + (int64_t)f * src_fs;
+    uint32_t w[PR_ROWS][4];
+#pragma unroll
+    for (int r = 0; r < PR_ROWS; r++) {
+        const int dy = min(oy + r, dh - 1);
+        const int q0 = yofs[dy];
+        const int r0 = q0 >= 0 ? (q0 < sh ? q0 : sh - 1) : 0;
+        const int r1 = q0 + 1 >= 0 ? (q0 + 1 < sh ? q0 + 1 : sh - 1) : 0;
+        const uint8_t* R0 = S + (int64_t)r0 * sp;
+        const uint8_t* R1 = S + (int64_t)r1 * sp;
+        w[r][0] = ld_u32(R0 + wb); w[r][1] = ld_u32(R0 + wb1);
+        w[r][2] = ld_u32(R1 + wb); w[r][3] = ld_u32(R1 + wb1);
+    }
+    const bool tail = ox + PR_COLS > xs;          // wave-uniform: some column takes the exact form
+    uint8_t* D = dst + (int64_t)f * dst_fs + cx;
+#pragma unroll
+    for (int r = 0; r < PR_ROWS; r++) {
+        const int dy = oy + r;
+        if (dy >= dh) break;
+        const uint32_t bb = (uint32_t)beta[dy];
+        const uint32_t b0 = bb & 0xFFFFu, b1 = bb >> 16;
+        const uint32_t b0s = (bb << 12) & 0xFFF000u, b1s = (bb >> 4) & 0xFFF000u;
+        uint32_t v[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint32_t h0 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(w[r][1], w[r][0], sel[k])),
+                                                       as_us2(coef[k]), 0u, false);
+            const uint32_t h1 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(w[r][3], w[r][2], sel[k])),
+                                                       as_us2(coef[k]), 0u, false);
+            v[k] = (__umulhi(h0 & 0xFFFF0u, b0s) + __umulhi(h1 & 0xFFFF0u, b1s) + 2u) >> 2;
+            if (tail && cx + k >= xs)             // h < 2^20, b <= 2048: 24-bit multiplies
+                v[k] = min((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22, 255u);
+        }
+        uint8_t* Dr = D + (int64_t)dy * dp;
+        if (cx + 1 < dw) *reinterpret_cast<uint16_t*>(Dr) = (uint16_t)(v[0] | (v[1] << 8));
+        else if (cx < dw) Dr[0] = (uint8_t)v[0];
+    }
+}
+
 // ================================ k_blur ================================
 // GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), Q8 kernel k (symmetric, sum 256), result
 // (sum_ij k_i k_j p_ij + 2^15) >> 16.  OpenCV's horizontal-then-vertical
@@ -331,12 +420,6 @@ struct BlurWork {
     int bh[COEB_MAXL];             // rows per band (4 bands per item)
 };
 
-typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us2, v); }
-__device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
-__device__ __forceinline__ us2 pk2(int lo, int hi) { us2 r; r.x = (unsigned short)lo; r.y = (unsigned short)hi; return r; }
 
 #ifndef COEB_XCD_REMAP
 #define COEB_XCD_REMAP 1
@@ -475,6 +558,10 @@ __global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, E
 // OpenCV's cornerScore<16> = M - 1 (derivation: DESIGN.md s4.2).  Per-cell NMS then
 // compares against neighbours' scores (0 outside the detection window), exactly as
 // FAST_t's 3-row buffers do; an empty cell at iniThFAST is redone at minThFAST (:834-838).
+// LDS pointers kept in their address space (a generic pointer would become flat loads)
+typedef const __attribute__((address_space(3))) uint8_t* lds_cu8;
+typedef const __attribute__((address_space(3))) uint32_t* lds_cu32;
+
 __device__ __forceinline__ void ring16(const uint8_t* c, int st, int p[16])
 {
     p[0] = c[3 * st];      p[1] = c[3 * st + 1];  p[2] = c[2 * st + 2];  p[3] = c[st + 3];
@@ -507,6 +594,54 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
 #pragma unroll
     for (int k = 0; k < 16; k++) Bm = min(Bm, max(max(t[k], t[(k + 3) & 15]), t[(k + 6) & 15]));
     return max(A, -Bm);
+}
+
+// The same M for a pre-test survivor, computing only the arc sign(s) that passed the pre-test at
+// t (the four opposite pairs 0/8, 2/10, 4/12, 6/14).  Every nine-pixel arc holds one pixel of each
+// opposite pair, so a sign whose pre-test fails has arc strength <= t: it can neither make the
+// pixel a corner at t nor at any larger threshold, and M only matters where M > t.  Hence
+//   dark passed:   M = max_k min_arc(v - p) = X - (255 - v),  X = max_k min_arc(255 - p)
+//   bright passed: M = max_k min_arc(p - v) = X - v,          X = max_k min_arc(p)
+// i.e. X over q = p ^ mask (mask = 255 for dark, 0 for bright) and M = X - (v ^ mask): one arc
+// pass of min3/max3 instead of two.  A pixel passing both pre-tests (rare) takes the bright pass
+// as well.  The base pointer sits at the lowest ring byte (p9 = -3 rows - 1 column), so all 17
+// reads take positive immediate offsets (LDS offsets are unsigned).
+template <int st>
+__device__ __forceinline__ int arc_max_min(const int q[16])
+{
+    int m3[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) m3[k] = min(min(q[k], q[(k + 1) & 15]), q[(k + 2) & 15]);
+    int X = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) X = max(X, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]));
+    return X;
+}
+
+template <int st>
+__device__ __forceinline__ int corner_strength_sel(const uint8_t* c, int t)
+{
+    lds_cu8 b = (lds_cu8)c - (3 * st + 1);
+    asm volatile("" : "+v"(b));              // keep the lowered base: offsets below are all >= 0
+    constexpr int o = 3 * st + 1;            // c[x] = b[x + o]
+    int p[16];
+    p[0] = b[o + 3 * st];      p[1] = b[o + 3 * st + 1];  p[2] = b[o + 2 * st + 2]; p[3] = b[o + st + 3];
+    p[4] = b[o + 3];           p[5] = b[o - st + 3];      p[6] = b[o - 2 * st + 2]; p[7] = b[o - 3 * st + 1];
+    p[8] = b[0 + 1];           p[9] = b[0];               p[10] = b[o - 2 * st - 2]; p[11] = b[o - st - 3];
+    p[12] = b[o - 3];          p[13] = b[o + st - 3];     p[14] = b[o + 2 * st - 2]; p[15] = b[o + 3 * st - 1];
+    const int v = b[o];
+    const int md = max(max(min(p[0], p[8]), min(p[2], p[10])), max(min(p[4], p[12]), min(p[6], p[14])));
+    const int mb = min(min(max(p[0], p[8]), max(p[2], p[10])), min(max(p[4], p[12]), max(p[6], p[14])));
+    const bool dark = md < v - t, bright = mb > v + t;
+    const int mask = dark ? 255 : 0;
+    int q[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) q[k] = p[k] ^ mask;
+    int M = arc_max_min<st>(q) - (v ^ mask);
+    if (__builtin_expect(__ballot(dark && bright) != 0, 0)) {
+        if (dark && bright) M = max(M, arc_max_min<st>(p) - v);
+    }
+    return M;
 }
 
 // One wave per cell, four cells per workgroup, no workgroup barriers.
@@ -583,14 +718,15 @@ template <int RB>
 __device__ __forceinline__ void fast_pretest4_raw(const uint8_t* c, int t, uint32_t& lo, uint32_t& hi)
 {
     constexpr int st = RB;
-    const uint32_t* r0 = reinterpret_cast<const uint32_t*>(c);
-    const uint32_t* rp2 = reinterpret_cast<const uint32_t*>(c + 2 * st);
-    const uint32_t* rm2 = reinterpret_cast<const uint32_t*>(c - 2 * st);
-    const uint32_t a0 = r0[-1], b0 = r0[0], c0 = r0[1];
-    const uint32_t ap = rp2[-1], bp = rp2[0], cp = rp2[1];
-    const uint32_t am = rm2[-1], bm = rm2[0], cm = rm2[1];
-    const uint32_t u3 = *reinterpret_cast<const uint32_t*>(c + 3 * st);
-    const uint32_t d3 = *reinterpret_cast<const uint32_t*>(c - 3 * st);
+    // base at the lowest word read (row -3), so every read takes a positive immediate offset
+    lds_cu32 w = (lds_cu32)(c - 3 * st);
+    asm volatile("" : "+v"(w));
+    constexpr int o = 3 * st / 4;            // word index of c
+    const uint32_t a0 = w[o - 1], b0 = w[o], c0 = w[o + 1];
+    const uint32_t ap = w[o + 2 * st / 4 - 1], bp = w[o + 2 * st / 4], cp = w[o + 2 * st / 4 + 1];
+    const uint32_t am = w[o - 2 * st / 4 - 1], bm = w[o - 2 * st / 4], cm = w[o - 2 * st / 4 + 1];
+    const uint32_t u3 = w[o + 3 * st / 4];
+    const uint32_t d3 = w[0];
     const us2 T = pk2(t, t);
     lo = pretest_half(
         as_us2(__builtin_amdgcn_perm(0u, b0, 0x0c010c00u)), as_us2(__builtin_amdgcn_perm(0u, u3, 0x0c010c00u)),
@@ -834,7 +970,7 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
                 int oo = 0, M = 0;
                 if (e < ns) {
                     oo = surv[e];
-                    M = corner_strength(&roi[oo], RB);
+                    M = corner_strength_sel<RB>(&roi[oo], th_min);
                 }
                 const bool isc = e < ns && M > th_min;
                 if (isc) Ms[fast_mi<RB>(oo, mp)] = (uint8_t)M;
@@ -1940,6 +2076,9 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         items += bw.nstrips[l] * (nbands / 4);
     }
     bw.item_off[plan.L] = items;
+    // COEB_PYR_BYTES=1 forces k_pyr_level's byte form for every level (tests run both forms)
+    const char* pb = getenv("COEB_PYR_BYTES");
+    const bool pyr_bytes = pb && atoi(pb) != 0;
     // COEB_FAST_RB=72 forces the general slab layout (tests run both layouts)
     const char* frb = getenv("COEB_FAST_RB");
     const int fast_rbytes = frb && atoi(frb) == kFastRowBytes ? kFastRowBytes : fast_rb(plan);
@@ -1982,11 +2121,20 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         const uint8_t* src = l == 1 ? b.gray : b.pyr + gp.pyr_off;
         const int64_t src_fs = l == 1 ? (int64_t)plan.W * plan.H : plan.pyr_stride;
         prof_begin(prof, "k_pyr_level", s);
-        int tsw, tsh;
-        pyr_tile_lds(gp.w, gp.h, g.w, g.h, &tsw, &tsh);
-        hipLaunchKernelGGL(k_pyr_level, dim3((g.w + PT_W - 1) / PT_W, (g.h + PT_H - 1) / PT_H, F), dim3(kThreads),
-                           tsw * tsh, s, src, src_fs, gp.pitch, gp.w, gp.h, b.pyr + g.pyr_off, plan.pyr_stride, g.pitch,
-                           g.w, g.h, b.rtab + g.rtab_off, g.xmax, resize_simd_end(g.w), tsw, tsh);
+        // k_pyr_rows needs 4-byte aligned source rows and every 2-column window within 8 bytes
+        // (g.rows_ok, make_plan: scale <= 2); otherwise the byte form
+        const bool rows = g.rows_ok && ((gp.pitch | (int)(src_fs & 3) | (int)((uintptr_t)src & 3)) & 3) == 0;
+        if (rows && !pyr_bytes) {
+            hipLaunchKernelGGL(k_pyr_rows, dim3((g.w + PR_COLS - 1) / PR_COLS, (g.h + kWaves * PR_ROWS - 1) / (kWaves * PR_ROWS), F),
+                               dim3(kThreads), 0, s, src, src_fs, gp.pitch, gp.h, b.pyr + g.pyr_off, plan.pyr_stride,
+                               g.pitch, g.w, g.h, b.rtab + g.rtab_off, g.xmax, resize_simd_end(g.w));
+        } else {
+            int tsw, tsh;
+            pyr_tile_lds(gp.w, gp.h, g.w, g.h, &tsw, &tsh);
+            hipLaunchKernelGGL(k_pyr_level, dim3((g.w + PT_W - 1) / PT_W, (g.h + PT_H - 1) / PT_H, F), dim3(kThreads),
+                               tsw * tsh, s, src, src_fs, gp.pitch, gp.w, gp.h, b.pyr + g.pyr_off, plan.pyr_stride,
+                               g.pitch, g.w, g.h, b.rtab + g.rtab_off, g.xmax, resize_simd_end(g.w), tsw, tsh);
+        }
         prof_end(prof, s);
         if (split && m > 1 && l == m - 1) {
             (void)hipEventRecord(side->mid, s);

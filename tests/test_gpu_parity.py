@@ -88,11 +88,16 @@ def test_extract_ragged_sizes(ctx, ex, w, h):
     run_both(ctx, ex, fr[0], tag="%dx%d" % (w, h))
 
 
+@pytest.mark.parametrize("pyr_form", ["rows", "bytes"])
 @pytest.mark.parametrize("w,h", [(640, 480), (641, 479), (533, 400), (1280, 960), (720, 405)])
-def test_blur_pyramid_matches_oracle(ctx, ex, oracle_mod, w, h):
+def test_blur_pyramid_matches_oracle(ctx, ex, oracle_mod, w, h, pyr_form, monkeypatch):
     """k_blur's whole blurred pyramid (not only the pixels rBRIEF samples) equals the oracle's
     GaussianBlur of each oracle pyramid level (ORBextractor.cc:1317-1318), every pixel including
-    the REFLECT_101 borders and the partial 64-column strips of ragged widths."""
+    the REFLECT_101 borders and the partial 64-column strips of ragged widths.  Both pyramid
+    kernels: k_pyr_rows (default where rows are 4-byte aligned) and k_pyr_level's byte form
+    (COEB_PYR_BYTES=1; the only form for odd-pitch inputs such as 641x479's level 0)."""
+    if pyr_form == "bytes":
+        monkeypatch.setenv("COEB_PYR_BYTES", "1")
     from coeb_front import Context
     c2 = ctx if (w, h) != (1280, 960) else Context(2000, 1.2, 8, 20, 7, max_width=w, max_height=h)
     ex2 = ex if c2 is ctx else oracle_mod.Extractor(2000, 1.2, 8, 20, 7)
