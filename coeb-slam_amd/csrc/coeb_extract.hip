@@ -325,6 +325,38 @@ constexpr int PR_ROWS = 8, PR_COLS = 128;
 
 __device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 
+// The output rows of a k_pyr_rows wave; kTail: the wave holds columns >= xs (exact rounding).
+// Addresses are a wave-uniform row pointer plus the lane's 32-bit column offset, so loads and
+// stores take the SGPR-base form (no per-lane 64-bit address arithmetic).
+template <bool kTail>
+__device__ __forceinline__ void pyr_rows_out(const uint32_t (&w)[PR_ROWS][4], const uint32_t (&sel)[2],
+                                             const uint32_t (&coef)[2], const int* __restrict__ beta, uint8_t* Df,
+                                             int dp, int oy, int dh, uint32_t cx, int dw, int xs)
+{
+#pragma unroll
+    for (int r = 0; r < PR_ROWS; r++) {
+        const int dy = oy + r;
+        if (dy >= dh) break;
+        const uint32_t bb = (uint32_t)beta[dy];
+        const uint32_t b0 = bb & 0xFFFFu, b1 = bb >> 16;
+        const uint32_t b0s = (bb << 12) & 0xFFF000u, b1s = (bb >> 4) & 0xFFF000u;
+        uint32_t v[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint32_t h0 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(w[r][1], w[r][0], sel[k])),
+                                                       as_us2(coef[k]), 0u, false);
+            const uint32_t h1 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(w[r][3], w[r][2], sel[k])),
+                                                       as_us2(coef[k]), 0u, false);
+            v[k] = (__umulhi(h0 & 0xFFFF0u, b0s) + __umulhi(h1 & 0xFFFF0u, b1s) + 2u) >> 2;
+            if (kTail && (int)cx + k >= xs)       // h < 2^20, b <= 2048: 24-bit multiplies
+                v[k] = min((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22, 255u);
+        }
+        uint8_t* Dr = Df + (int64_t)dy * dp;
+        if ((int)cx + 1 < dw) *reinterpret_cast<uint16_t*>(Dr + cx) = (uint16_t)(v[0] | (v[1] << 8));
+        else if ((int)cx < dw) Dr[cx] = (uint8_t)v[0];
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void k_pyr_rows(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
                                                        int sh, uint8_t* __restrict__ dst, int64_t dst_fs, int dp,
                                                        int dw, int dh, const int* __restrict__ tab, int xmax, int xs)
@@ -334,19 +366,19 @@ __global__ __launch_bounds__(kThreads) void k_pyr_rows(const uint8_t* __restrict
     if (oy >= dh) return;
     const int lane = lane_id();
     const int ox = blockIdx.x * PR_COLS;
-    const int cx = ox + 2 * lane;
+    const uint32_t cx = (uint32_t)(ox + 2 * lane);
     const int* xofs = tab;
     const int* alpha = tab + dw;
     const int* yofs = tab + 2 * dw;
     const int* beta = tab + 2 * dw + dh;
     uint32_t sel[2], coef[2];
-    const int d0 = min(cx, dw - 1);
-    const int wb = xofs[d0] & ~3;                 // the lane's window: source bytes wb .. wb + 7
-    const int wb1 = min(wb + 4, sp - 4);          // (the second word stays inside the row's pitch)
+    const int d0 = min((int)cx, dw - 1);
+    const uint32_t wb = (uint32_t)(xofs[d0] & ~3);                 // the lane's window: bytes wb .. wb + 7
+    const uint32_t wb1 = (uint32_t)min((int)wb + 4, sp - 4);      // (the second word stays inside the pitch)
 #pragma unroll
     for (int k = 0; k < 2; k++) {
-        const int d = min(cx + k, dw - 1);
-        const int o = xofs[d] - wb;               // <= 5 for scale <= 2 (host checks)
+        const int d = min((int)cx + k, dw - 1);
+        const int o = xofs[d] - (int)wb;          // <= 5 for scale <= 2 (make_plan's rows_ok)
         const int a = alpha[d];
         const uint32_t a0 = d >= xmax ? 2048u : (uint32_t)(a & 0xFFFF), a1 = d >= xmax ? 0u : (uint32_t)a >> 16;
         coef[k] = a0 | (a1 << 16);
@@ -365,30 +397,9 @@ __global__ __launch_bounds__(kThreads) void k_pyr_rows(const uint8_t* __restrict
         w[r][0] = ld_u32(R0 + wb); w[r][1] = ld_u32(R0 + wb1);
         w[r][2] = ld_u32(R1 + wb); w[r][3] = ld_u32(R1 + wb1);
     }
-    const bool tail = ox + PR_COLS > xs;          // wave-uniform: some column takes the exact form
-    uint8_t* D = dst + (int64_t)f * dst_fs + cx;
-#pragma unroll
-    for (int r = 0; r < PR_ROWS; r++) {
-        const int dy = oy + r;
-        if (dy >= dh) break;
-        const uint32_t bb = (uint32_t)beta[dy];
-        const uint32_t b0 = bb & 0xFFFFu, b1 = bb >> 16;
-        const uint32_t b0s = (bb << 12) & 0xFFF000u, b1s = (bb >> 4) & 0xFFF000u;
-        uint32_t v[2];
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const uint32_t h0 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(w[r][1], w[r][0], sel[k])),
-                                                       as_us2(coef[k]), 0u, false);
-            const uint32_t h1 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(w[r][3], w[r][2], sel[k])),
-                                                       as_us2(coef[k]), 0u, false);
-            v[k] = (__umulhi(h0 & 0xFFFF0u, b0s) + __umulhi(h1 & 0xFFFF0u, b1s) + 2u) >> 2;
-            if (tail && cx + k >= xs)             // h < 2^20, b <= 2048: 24-bit multiplies
-                v[k] = min((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22, 255u);
-        }
-        uint8_t* Dr = D + (int64_t)dy * dp;
-        if (cx + 1 < dw) *reinterpret_cast<uint16_t*>(Dr) = (uint16_t)(v[0] | (v[1] << 8));
-        else if (cx < dw) Dr[0] = (uint8_t)v[0];
-    }
+    uint8_t* Df = dst + (int64_t)f * dst_fs;
+    if (ox + PR_COLS > xs) pyr_rows_out<true>(w, sel, coef, beta, Df, dp, oy, dh, cx, dw, xs);
+    else pyr_rows_out<false>(w, sel, coef, beta, Df, dp, oy, dh, cx, dw, xs);
 }
 
 // ================================ k_blur ================================
