@@ -15,6 +15,7 @@ initialised: the torch wheel bundles its own HIP runtime).
 """
 import argparse
 import json
+import math
 import os
 import subprocess
 import sys
@@ -65,6 +66,8 @@ CPU_CAVEAT = ("the oracle is a scalar C restatement of ORBextractor/ORBmatcher w
               "(FAST, resize, GaussianBlur, LK, ...) restated without SIMD: real OpenCV 3.4 vectorises them, so the "
               "reference binary runs faster than this port (SURVEY.md s8(d)); the reference itself is unbuildable here "
               "(no OpenCV/g2o/DBoW2 in the image)")
+
+CHAIN_WARMUP = 20    # 20 warm-up frames before the timed ones
 
 
 def step_kwargs(cfg):
@@ -205,55 +208,85 @@ def host_cpu_info():
     return dict(cpu_model=model, nproc=len(cpus), cpu_quota=quota, machine_cpus=os.cpu_count()), cpus
 
 
-def cpu_baseline(cfg, seconds=12.0, min_frames=30):
+def effective_cpus(info, cpus):
+    """Threads the all-cores legs use: the affinity mask (`nproc`) capped by the cgroup CPU
+    quota when one is set, so `cores` states the CPUs the run actually had."""
+    n = len(cpus)
+    if info.get("cpu_quota"):
+        n = max(1, min(n, int(math.ceil(info["cpu_quota"]))))
+    return n
+
+
+def _single_thread_leg(O, lib_path, cfg, ex_args, frames, depth, cam, cpu, seconds, min_frames, warmup=20):
+    """SURVEY.md s8(d)'s single-thread leg on one oracle build: `warmup` untimed frames, then
+    extract + ComputeStereoFromRGBD + SearchByProjection (retry at 2*th) per frame, median time."""
+    from coeb_front import synth
+    O.LIB = lib_path
+    O._lib = None
+    ex = O.Extractor(*ex_args)
+    nfr = len(frames)
+    Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
+    prev = ex.extract(frames[0])
+    for i in range(1, 1 + warmup):
+        prev = ex.extract(frames[i % nfr])
+    times = []
+    t_end = time.perf_counter() + seconds
+    i = 1 + warmup
+    while (time.perf_counter() < t_end or len(times) < min_frames) and len(times) < 400:
+        f = frames[i % nfr]
+        last = O.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX, synth.TUM_FY,
+                                          synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)   # map snapshot (untimed)
+        t0 = time.perf_counter()
+        r = ex.extract(f)
+        ur, _ = O.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
+        nm, _ = O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 15.0)
+        if nm < 20:
+            O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 30.0)
+        times.append(time.perf_counter() - t0)
+        prev = r
+        i += 1
+    return float(np.median(times)), len(times)
+
+
+def cpu_baseline(cfg, seconds=9.0, min_frames=30):
     """Oracle ('port') timed on this host: extract + ComputeStereoFromRGBD + SearchByProjection
-    (retry at 2*th) per frame, on consecutive synthetic frames.  The single-thread leg runs
-    pinned to one CPU (os.sched_setaffinity on the timing thread, SURVEY.md s8(d) `taskset -c`)."""
-    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"])
+    (retry at 2*th) per frame, on consecutive synthetic frames.  The single-thread legs run
+    pinned to one CPU (os.sched_setaffinity on the timing thread, SURVEY.md s8(d) `taskset -c`),
+    20 warm-up frames each: the -O3 -march=native build (the reference's CMakeLists.txt:15 flags,
+    auto-vectorised; the headline `value`) and a plain scalar build (-O3 -march=x86-64, no
+    vectoriser) beside it.  The all-cores leg uses the -march=native build."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native", "scalar"])
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from coeb_front import synth
-    O.LIB = os.path.join(ROOT, "oracle", "liborb_oracle_native.so")
-    O._lib = None
     info, cpus = host_cpu_info()
     w, h = cfg["w"], cfg["h"]
-    ex = O.Extractor(cfg["nfeatures"], 1.2, 8, 20, 7)
-    cam = O.camera(ex, w, h, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    ex_args = (cfg["nfeatures"], 1.2, 8, 20, 7)
     depth = synth.make_depth(w, h)
-    nfr = 64
-    frames = synth.make_frames(w, h, nfr, seed=5151)
-    Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
+    frames = synth.make_frames(w, h, 64, seed=5151)
+    native = os.path.join(ROOT, "oracle", "liborb_oracle_native.so")
+    scalar = os.path.join(ROOT, "oracle", "liborb_oracle_scalar.so")
     os.sched_setaffinity(0, {cpus[0]})
     try:
-        prev = ex.extract(frames[0])
-        for i in range(1, 4):          # warm-up
-            prev = ex.extract(frames[i])
-        times = []
-        t_end = time.perf_counter() + seconds
-        i = 4
-        while (time.perf_counter() < t_end or len(times) < min_frames) and len(times) < 400:
-            f = frames[i % nfr]
-            last = O.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX, synth.TUM_FY,
-                                              synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)   # map snapshot (untimed)
-            t0 = time.perf_counter()
-            r = ex.extract(f)
-            ur, _ = O.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
-            nm, _ = O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 15.0)
-            if nm < 20:
-                O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 30.0)
-            times.append(time.perf_counter() - t0)
-            prev = r
-            i += 1
+        O.LIB, O._lib = native, None
+        cam = O.camera(O.Extractor(*ex_args), w, h, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY,
+                       synth.TUM_BF)
+        med, n = _single_thread_leg(O, native, cfg, ex_args, frames, depth, cam, cpus[0], seconds, min_frames)
+        med_s, n_s = _single_thread_leg(O, scalar, cfg, ex_args, frames, depth, cam, cpus[0], 0.6 * seconds,
+                                        min_frames)
     finally:
         os.sched_setaffinity(0, set(cpus))
-    med = float(np.median(times))
+        O.LIB, O._lib = native, None
     out = dict(value=round(1.0 / med, 3), unit="frames/s", cores=1, kind="port",
-               sample="%d consecutive %dx%d synthetic frames, oracle (-O3 -march=native) single thread pinned to "
-                      "CPU %d: extract + ComputeStereoFromRGBD + SearchByProjection(th 15, retry 30); median %.2f "
-                      "ms/frame" % (len(times), w, h, cpus[0], med * 1e3))
+               sample="%d consecutive %dx%d synthetic frames after 20 warm-up frames, oracle (-O3 -march=native) "
+                      "single thread pinned to CPU %d: extract + ComputeStereoFromRGBD + SearchByProjection (th 15, "
+                      "retry 30); median %.2f ms/frame" % (n, w, h, cpus[0], med * 1e3))
     out.update(info)
     out["caveat"] = CPU_CAVEAT
-    out["all_cores"] = cpu_baseline_parallel(O, cfg, frames, depth, cam, len(cpus))
+    out["scalar_build"] = dict(value=round(1.0 / med_s, 3), unit="frames/s", cores=1, kind="port",
+                               sample="the same leg on the plain scalar build (-O3 -march=x86-64 -fno-tree-vectorize "
+                                      "-fno-tree-slp-vectorize), %d frames, median %.2f ms/frame" % (n_s, med_s * 1e3))
+    out["all_cores"] = cpu_baseline_parallel(O, cfg, frames, depth, cam, effective_cpus(info, cpus))
     return out
 
 
@@ -311,17 +344,17 @@ def cpu_chain_baseline(cfg, seconds=15.0, min_frames=20):
     O._lib = None
     info, cpus = host_cpu_info()
     w, h = cfg["w"], cfg["h"]
-    nfr = 48
+    nfr = 64
     gray, boxes = synth.tracking_sequence(w, h, nfr, first=0)
     rgb, dep = synth.rgbd_from_gray(gray)
     os.sched_setaffinity(0, {cpus[0]})
     try:
         cl = ChainCpu(O, cfg, rgb, dep, boxes)
-        for i in range(3):
+        for i in range(CHAIN_WARMUP):
             cl.step(i)
         times = []
         t_end = time.perf_counter() + seconds
-        i = 3
+        i = CHAIN_WARMUP
         while (time.perf_counter() < t_end or len(times) < min_frames) and i < nfr:
             t0 = time.perf_counter()
             cl.step(i)
@@ -337,7 +370,7 @@ def cpu_chain_baseline(cfg, seconds=15.0, min_frames=20):
                       "%.2f ms/frame" % (len(times), w, h, cpus[0], med * 1e3))
     out.update(info)
     out["caveat"] = CPU_CAVEAT
-    nthr = len(cpus)
+    nthr = effective_cpus(info, cpus)
     import threading
     done = [0] * nthr
     t_stop = [0.0]
@@ -360,7 +393,7 @@ def cpu_chain_baseline(cfg, seconds=15.0, min_frames=20):
         x.join()
     dt = time.perf_counter() - t0
     out["all_cores"] = dict(value=round(sum(done) / dt, 3), unit="frames/s", cores=nthr, kind="port",
-                            sample="%d threads (nproc) x 8 s, one oracle chain per thread on its own slice of the "
+                            sample="%d threads (nproc capped by the cgroup quota) x 8 s, one oracle chain per thread on its own slice of the "
                                    "sequence; %d frames" % (nthr, sum(done)))
     return out
 
@@ -400,7 +433,7 @@ def cpu_baseline_parallel(O, cfg, frames, depth, cam, nthr, seconds=6.0):
         x.join()
     dt = time.perf_counter() - t0
     return dict(value=round(sum(done) / dt, 3), unit="frames/s", cores=nthr, kind="port",
-                sample="%d threads (nproc) x %.0f s, one oracle extractor per thread, frame-parallel extract + "
+                sample="%d threads (nproc capped by the cgroup quota) x %.0f s, one oracle extractor per thread, frame-parallel extract + "
                        "ComputeStereoFromRGBD + SearchByProjection (LastFrame snapshots inside the timed loop); "
                        "%d frames" % (nthr, seconds, sum(done)))
 

@@ -561,6 +561,14 @@ int upload_dyn(coeb_ctx* c, int F, const coeb_box* boxes, const int32_t* box_off
     int rc;
     float *dbox, *dtm;
     int32_t *dboff, *dtoff, *dblur;
+    // offsets must start at 0 and never decrease: every box then gets its frame from
+    // k_box_frame, and every T_M range lies inside the uploaded array
+    if (box_off && boxes && box_off[0] != 0) return set_err(c, COEB_EINVAL, "box_off[0] != 0");
+    if (tm_off && tm_xy && tm_off[0] != 0) return set_err(c, COEB_EINVAL, "tm_off[0] != 0");
+    for (int f = 0; f < F; f++) {
+        if (box_off && boxes && box_off[f + 1] < box_off[f]) return set_err(c, COEB_EINVAL, "box_off decreases");
+        if (tm_off && tm_xy && tm_off[f + 1] < tm_off[f]) return set_err(c, COEB_EINVAL, "tm_off decreases");
+    }
     if (nbox > 0) {
         for (int f = 0; f < F; f++)
             if (box_off[f + 1] - box_off[f] > COEB_MAXBOX) return set_err(c, COEB_EINVAL, "more than 16 boxes in a frame");

@@ -45,6 +45,7 @@ extern "C" int coeb_internal_stream(coeb_ctx* c, hipStream_t* s, int* device);
 extern "C" int coeb_internal_scratch(coeb_ctx* c, const char* name, size_t bytes, void** p);
 extern "C" int coeb_internal_error(coeb_ctx* c, int code, const char* msg);
 extern "C" ProfileHook* coeb_internal_prof(coeb_ctx* c);
+extern "C" void coeb_internal_flow_forget(const coeb_ctx* c);
 
 namespace {
 
@@ -1759,7 +1760,7 @@ size_t gf_select_lds(int w, int h, int cell, int np)
     return (size_t)(np > 1 ? np : 2) * 8 + (size_t)((gw * gh + 1) & ~1) * 2 + (size_t)kMaxPts * (2 + 4);
 }
 
-// goodFeaturesToTrack into d->pts / d->npts (device count: -1 sort capacity, -3 cell capacity)
+// goodFeaturesToTrack into d->pts / d->npts (device count: -1 when the sort capacity is exceeded)
 int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, int max_corners, double quality,
               double min_distance, double k, hipStream_t s, int64_t iz = 0)
 {
@@ -1906,6 +1907,9 @@ int flow_begin(coeb_ctx* c, int w, int h, FlowCall* fc, const char* who)
     if (coeb_internal_stream(c, &fc->s, &dev)) return coeb_internal_error(c, COEB_EINVAL, who);
     (void)hipSetDevice(dev);
     if (w < 32 || h < 32 || (size_t)w * h > (size_t)1 << 26) return coeb_internal_error(c, COEB_EINVAL, who);
+    // a single-pair call rewrites the flow scratch with npairs = 1: the last batch's geometry
+    // no longer describes it, so coeb_internal_flow_counts must refuse rather than misread
+    coeb_internal_flow_forget(c);
     return flow_alloc(c, w, h, &fc->d);
 }
 
