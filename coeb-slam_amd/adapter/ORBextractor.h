@@ -15,12 +15,14 @@
  * Behaviour kept from the reference: empty image -> return without touching the outputs
  * (:1096-1097); non-8UC1 -> assert (:1099); zero keypoints -> descriptors.release()
  * (:1296-1297); mask / img / imD / mask_result are accepted and unused (SURVEY.md s8a note).
- * Device contexts are pooled per (device, parameters) so Tracking's leak-and-recreate of
- * extractors on tracking failure (Tracking.cc:434-465) stays cheap.
+ * Device contexts are pooled per (host thread, device, parameters) so Tracking's leak-and-recreate
+ * of extractors on tracking failure (Tracking.cc:434-465) stays cheap; a context grows to the
+ * largest image it has seen (no fixed size cap) and is freed when its thread exits.
  */
 #ifndef COEB_ADAPTER_ORBEXTRACTOR_H
 #define COEB_ADAPTER_ORBEXTRACTOR_H
 
+#include <algorithm>
 #include <cassert>
 #include <cstdlib>
 #include <cstring>
@@ -53,22 +55,38 @@ public:
 
 namespace coeb_detail
 {
-// one context per (host thread, device, ORB parameters): coeb_ctx is not reentrant
-inline coeb_ctx* pooled_context(const coeb_orb_params& p, int device, int max_w, int max_h)
+// One context per (host thread, device, ORB parameters): coeb_ctx is not reentrant.  The pool
+// is thread_local and destroys its contexts when the thread exits, so thread churn frees device
+// memory.  A context is created for at least 1280 x 960 and re-created larger when an image
+// exceeds it; extractors therefore look their context up per call instead of caching it.
+struct CtxPool {
+    struct Entry { coeb_ctx* ctx; int max_w, max_h; };
+    std::map<std::tuple<int, int, float, int, int, int>, Entry> m;
+    ~CtxPool()
+    {
+        for (auto& kv : m) coeb_destroy(kv.second.ctx);
+    }
+};
+
+inline coeb_ctx* pooled_context(const coeb_orb_params& p, int device, int w, int h)
 {
-    static std::mutex mu;
-    static std::map<std::tuple<std::thread::id, int, int, float, int, int, int>, coeb_ctx*> pool;
-    const auto key = std::make_tuple(std::this_thread::get_id(), device, p.nfeatures, p.scale_factor, p.nlevels,
-                                     max_w, max_h);
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = pool.find(key);
-    if (it != pool.end()) return it->second;
+    thread_local CtxPool pool;
+    const auto key = std::make_tuple(device, p.nfeatures, p.scale_factor, p.nlevels, p.ini_th_fast, p.min_th_fast);
+    auto it = pool.m.find(key);
+    if (it != pool.m.end() && w <= it->second.max_w && h <= it->second.max_h) return it->second.ctx;
+    int mw = std::max(w, 1280), mh = std::max(h, 960);
+    if (it != pool.m.end()) {               // grow: keep the larger of the old and new bounds
+        mw = std::max(mw, it->second.max_w);
+        mh = std::max(mh, it->second.max_h);
+        coeb_destroy(it->second.ctx);
+        pool.m.erase(it);
+    }
     if (coeb_abi_version() != COEB_ABI_VERSION)      // header and loaded library must agree
         throw std::runtime_error("libcoeb_front ABI " + std::to_string(coeb_abi_version()) + ", header " +
                                  std::to_string(COEB_ABI_VERSION));
-    coeb_ctx* c = coeb_create(&p, device, max_w, max_h, 1);
+    coeb_ctx* c = coeb_create(&p, device, mw, mh, 1);
     if (!c) throw std::runtime_error(std::string("coeb_create: ") + coeb_last_error(nullptr));
-    pool[key] = c;
+    pool.m[key] = CtxPool::Entry{c, mw, mh};
     return c;
 }
 }  // namespace coeb_detail
@@ -87,9 +105,9 @@ public:
         params_.nlevels = nlevels;
         params_.ini_th_fast = iniThFAST;
         params_.min_th_fast = minThFAST;
-        ctx_ = coeb_detail::pooled_context(params_, device(), kMaxW, kMaxH);
+        coeb_ctx* ctx = coeb_detail::pooled_context(params_, device(), 0, 0);
         coeb_orb_tables t;
-        if (coeb_orb_tables_get(ctx_, &t) != COEB_OK) throw std::runtime_error(coeb_last_error(ctx_));
+        if (coeb_orb_tables_get(ctx, &t) != COEB_OK) throw std::runtime_error(coeb_last_error(ctx));
         mvScaleFactor.assign(t.scale, t.scale + nlevels);
         mvInvScaleFactor.assign(t.inv_scale, t.inv_scale + nlevels);
         mvLevelSigma2.assign(t.sigma2, t.sigma2 + nlevels);
@@ -113,6 +131,7 @@ public:
         for (const auto& b : box) boxes.push_back(coeb_box{b[0], b[1], b[2], b[3]});
         std::vector<float> tm;
         for (const auto& p : T_M) { tm.push_back(p.x); tm.push_back(p.y); }
+        coeb_ctx* ctx_ = coeb_detail::pooled_context(params_, device(), image.cols, image.rows);
         const int cap = coeb_max_keypoints(ctx_, image.cols, image.rows);
         if (cap < 0) throw std::runtime_error(coeb_last_error(ctx_));
         std::vector<coeb_keypoint> kps((size_t)cap);
@@ -151,7 +170,6 @@ protected:
         const char* e = std::getenv("COEB_DEVICE");
         return e ? std::atoi(e) : 0;
     }
-    static constexpr int kMaxW = 1280, kMaxH = 960;
     int nfeatures;
     double scaleFactor;
     int nlevels;
@@ -164,7 +182,6 @@ protected:
     std::vector<float> mvLevelSigma2;
     std::vector<float> mvInvLevelSigma2;
     coeb_orb_params params_{};
-    coeb_ctx* ctx_ = nullptr;
 };
 
 }  // namespace ORB_SLAM2

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ORBextractor.h"
@@ -122,6 +123,25 @@ int main(int argc, char** argv)
         cv::Mat dd(2, 32, CV_8U);
         ex2(im, none, im, none, kk, dd, box, tm, mask_result, blur);
         checks << "flat_released " << (kk.empty() && dd.empty()) << "\n";
+    }
+    {   // an image larger than the pooled context's 1280 x 960: the context grows (no size cap);
+        // extracted on a worker thread, whose exit destroys that thread's pooled contexts
+        const std::vector<int32_t> bs = load<int32_t>(d + "size_big.i32");
+        std::vector<uint8_t> fb = load<uint8_t>(d + "frame_big.u8");
+        std::vector<cv::KeyPoint> kb;
+        cv::Mat db;
+        std::thread th([&] {
+            ORB_SLAM2::ORBextractor exb(2000, 1.2f, 8, 20, 7);
+            cv::Mat small(H, W, CV_8U, f0.data());
+            std::vector<cv::KeyPoint> ks;
+            cv::Mat ds;
+            exb(small, none, small, none, ks, ds, box, tm, mask_result, blur);   // context at 1280 x 960
+            cv::Mat imb(bs[1], bs[0], CV_8U, fb.data());
+            exb(imb, none, imb, none, kb, db, box, tm, mask_result, blur);      // grows
+        });
+        th.join();
+        save(d + "kps_big.bin", kb.data(), kb.size());
+        save(d + "desc_big.u8", db.data, (size_t)db.rows * 32);
     }
     ORB_SLAM2::ORBextractor ex3(1000, 1.2f, 8, 20, 7);
     checks << "accessors " << (ex3.GetLevels() == 8 && ex3.GetScaleFactors().size() == 8 &&

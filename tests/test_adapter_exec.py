@@ -4,7 +4,8 @@ frames, coeb::SearchByProjectionLastFrame with the Tracking retry (Tracking.cc:9
 coeb::PoseOptimization (Optimizer.cc:239-451), called from C++ with reference-shaped Frame /
 MapPoint types, compared with the oracle.  Also the reference conventions the adapter keeps:
 an empty image leaves the outputs untouched, no keypoints release the descriptors, and two
-extractors with the same parameters share one pooled context."""
+extractors with the same parameters share one pooled context, and an image larger than the
+pooled context's 1280 x 960 (extracted on a worker thread) grows it instead of failing."""
 import os
 import subprocess
 
@@ -46,6 +47,10 @@ def test_adapters_run_against_library(tmp_path, oracle_mod):
     put("last_xw.f32", last["xw"].astype(np.float32))
     put("last_desc.u8", last["mp_desc"].astype(np.uint8))
     put("cur_ur.f32", ur.astype(np.float32))
+    WB, HB = 1600, 1200                     # beyond the pooled context's initial 1280 x 960
+    fb = synth.make_frames(WB, HB, 1, seed=99)[0]
+    put("size_big.i32", np.array([WB, HB], np.int32))
+    put("frame_big.u8", fb)
     out = subprocess.run([EXE, d], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
 
@@ -58,6 +63,12 @@ def test_adapters_run_against_library(tmp_path, oracle_mod):
         for f in KEYPOINT_DTYPE.names:
             assert np.array_equal(k[f], r["kps"][f]), (i, f)
         assert np.array_equal(desc, r["desc"]), i
+    rb = oracle_mod.Extractor(2000, 1.2, 8, 20, 7).extract(fb)
+    kb = get("kps_big.bin", np.uint8).view(KEYPOINT_DTYPE)
+    assert len(kb) == len(rb["kps"]) > 1500
+    for f in KEYPOINT_DTYPE.names:
+        assert np.array_equal(kb[f], rb["kps"][f]), ("big", f)
+    assert np.array_equal(get("desc_big.u8", np.uint8).reshape(-1, 32), rb["desc"])
     checks = dict(l.split() for l in open(os.path.join(d, "checks.txt")))
     assert checks == {"empty_untouched": "1", "flat_released": "1", "accessors": "1"}, checks
     # SearchByProjection with the retry of Tracking::TrackWithMotionModel

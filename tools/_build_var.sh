@@ -11,5 +11,6 @@ for s in $(sed -n "s/^SRCS = //p" Makefile | sed "s/\.hip//g"); do
   objs="$objs $out/$s.o"
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/var_$name.so $objs
+make -s build/coeb_tum.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/.tmp_var_$name.so $objs build/coeb_tum.o && mv ../lib/.tmp_var_$name.so ../lib/var_$name.so
 echo "built lib/var_$name.so ($defs)"

@@ -15,6 +15,8 @@ for v in "$@"; do
 import json, sys
 l = [x for x in open("gpurun_out/kab.log") if x.startswith("{")]
 d = json.loads(l[0])
-print("%-28s %s=%.4f ms  step=%.4f ms  value=%.0f" % (sys.argv[1], sys.argv[2], d["kernels_ms_per_step"].get(sys.argv[2], -1), d["ms_per_step"], d["value"]))
+k = d["kernels_ms_per_step"]
+print("%-28s %s=%.4f ms  step=%.4f ms  value=%.0f" % (sys.argv[1], sys.argv[2], k.get(sys.argv[2], -1), d["ms_per_step"], d["value"]))
+print("    " + " ".join("%s=%.3f" % (n[2:], v) for n, v in k.items()))
 PY
 done

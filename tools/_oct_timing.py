@@ -1,4 +1,4 @@
-"""k_octree per-workgroup clocks over one 257-frame config-A extraction (library built with
+"""k_octree per-workgroup clocks over one extraction (default 257 frames of config A; args W H F) (library built with
 -DCOEB_OCT_CLOCK=1, loaded through COEB_LIB_PATH; COEB_SIDE_STREAM=0).  Diagnostic only."""
 import os
 import sys
@@ -9,9 +9,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from coeb_front import synth  # noqa: E402
 from coeb_front.pipeline import BatchPipeline  # noqa: E402
 
-F = 257
-fr = synth.make_frames(640, 480, F, seed=1)
-bp = BatchPipeline(640, 480, F)
+W, H, F = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (640, 480, 257)))
+NF = 2000 if W >= 1280 else 1000
+fr = synth.make_frames(W, H, F, seed=1)
+bp = BatchPipeline(W, H, F, nfeatures=NF)
 bp.load(fr, Tcw=np.stack([synth.motion_pose()] * F))
 for _ in range(3):
     bp.run(match=False)
