@@ -179,10 +179,24 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
             while (rtab.size() % 4) rtab.push_back(0);     // 16-byte aligned table rows
             g.rtab_off = (int)rtab.size();
             g.xmax = resize_tables(P.lv[l - 1].w, P.lv[l - 1].h, g.w, g.h, rtab);
-            const int* xofs = rtab.data() + g.rtab_off;
             g.rows_ok = 1;
-            for (int c = 0; c < g.w; c += 2)
+            for (int c = 0; c < g.w; c += 2) {
+                const int* xofs = rtab.data() + g.rtab_off;
                 if (xofs[std::min(c + 1, g.w - 1)] - (xofs[c] & ~3) > 5) g.rows_ok = 0;
+            }
+            // k_pyr_rows' row descriptors: one 16-byte scalar load per output row
+            while (rtab.size() % 4) rtab.push_back(0);
+            g.yrow_off = (int)rtab.size();
+            const int sh = P.lv[l - 1].h, sp = P.lv[l - 1].pitch;
+            for (int dy = 0; dy < g.h; dy++) {
+                const int q0 = rtab[g.rtab_off + 2 * g.w + dy], bb = rtab[g.rtab_off + 2 * g.w + g.h + dy];
+                const int r0 = q0 >= 0 ? (q0 < sh ? q0 : sh - 1) : 0;
+                const int r1 = q0 + 1 >= 0 ? (q0 + 1 < sh ? q0 + 1 : sh - 1) : 0;
+                rtab.push_back(r0 * sp);
+                rtab.push_back(r1 * sp);
+                rtab.push_back(bb);
+                rtab.push_back(dy * g.pitch);
+            }
         }
         // FAST cells (ComputeKeyPointsOctTree :795-829)
         const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;

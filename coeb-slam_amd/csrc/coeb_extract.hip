@@ -325,19 +325,22 @@ constexpr int PR_ROWS = 8, PR_COLS = 128;
 
 __device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 
-// The output rows of a k_pyr_rows wave; kTail: the wave holds columns >= xs (exact rounding).
-// Addresses are a wave-uniform row pointer plus the lane's 32-bit column offset, so loads and
-// stores take the SGPR-base form (no per-lane 64-bit address arithmetic).
-template <bool kTail>
+// The output rows of a k_pyr_rows wave; kTail: the wave holds columns >= xs (exact rounding);
+// kEdge: the wave holds the level's last column (per-lane store guards).  Row descriptors
+// (yrow: clamped source-row offsets, beta, the output row offset) are one scalar 16-byte load
+// each, and loads / stores are buffer operations with the row offset as the scalar soffset, so a
+// row costs no 64-bit address arithmetic and no exec-mask juggling in interior waves.
+template <bool kTail, bool kEdge>
 __device__ __forceinline__ void pyr_rows_out(const uint32_t (&w)[PR_ROWS][4], const uint32_t (&sel)[2],
-                                             const uint32_t (&coef)[2], const int* __restrict__ beta, uint8_t* Df,
-                                             int dp, int oy, int dh, uint32_t cx, int dw, int xs)
+                                             const uint32_t (&coef)[2], const int4* __restrict__ yrow,
+                                             __amdgpu_buffer_rsrc_t rd, int oy, int dh, uint32_t cx, int dw, int xs)
 {
 #pragma unroll
     for (int r = 0; r < PR_ROWS; r++) {
         const int dy = oy + r;
         if (dy >= dh) break;
-        const uint32_t bb = (uint32_t)beta[dy];
+        const int4 yr = yrow[dy];
+        const uint32_t bb = (uint32_t)yr.z;
         const uint32_t b0 = bb & 0xFFFFu, b1 = bb >> 16;
         const uint32_t b0s = (bb << 12) & 0xFFF000u, b1s = (bb >> 4) & 0xFFF000u;
         uint32_t v[2];
@@ -351,15 +354,20 @@ __device__ __forceinline__ void pyr_rows_out(const uint32_t (&w)[PR_ROWS][4], co
             if (kTail && (int)cx + k >= xs)       // h < 2^20, b <= 2048: 24-bit multiplies
                 v[k] = min((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22, 255u);
         }
-        uint8_t* Dr = Df + (int64_t)dy * dp;
-        if ((int)cx + 1 < dw) *reinterpret_cast<uint16_t*>(Dr + cx) = (uint16_t)(v[0] | (v[1] << 8));
-        else if ((int)cx < dw) Dr[cx] = (uint8_t)v[0];
+        const uint32_t pr = v[0] | (v[1] << 8);
+        if (!kEdge) {
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)pr, rd, cx, yr.w, 0);
+        } else {
+            if ((int)cx + 1 < dw) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)pr, rd, cx, yr.w, 0);
+            else if ((int)cx < dw) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)pr, rd, cx, yr.w, 0);
+        }
     }
 }
 
 __global__ __launch_bounds__(kThreads) void k_pyr_rows(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
                                                        int sh, uint8_t* __restrict__ dst, int64_t dst_fs, int dp,
-                                                       int dw, int dh, const int* __restrict__ tab, int xmax, int xs)
+                                                       int dw, int dh, const int* __restrict__ tab, int xmax, int xs,
+                                                       const int4* __restrict__ yrow)
 {
     const int f = blockIdx.z;
     const int oy = (blockIdx.y * kWaves + wave_id()) * PR_ROWS;
@@ -369,8 +377,6 @@ __global__ __launch_bounds__(kThreads) void k_pyr_rows(const uint8_t* __restrict
     const uint32_t cx = (uint32_t)(ox + 2 * lane);
     const int* xofs = tab;
     const int* alpha = tab + dw;
-    const int* yofs = tab + 2 * dw;
-    const int* beta = tab + 2 * dw + dh;
     uint32_t sel[2], coef[2];
     const int d0 = min((int)cx, dw - 1);
     const uint32_t wb = (uint32_t)(xofs[d0] & ~3);                 // the lane's window: bytes wb .. wb + 7
@@ -384,22 +390,28 @@ __global__ __launch_bounds__(kThreads) void k_pyr_rows(const uint8_t* __restrict
         coef[k] = a0 | (a1 << 16);
         sel[k] = (uint32_t)o | 0x0c00u | ((uint32_t)(o + 1) << 16) | 0x0c000000u;
     }
-    const uint8_t* S = src + (int64_t)f * src_fs;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(src + (int64_t)f * src_fs), 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(dst + (int64_t)f * dst_fs), 0, 0x7fffffff, 0x00020000);
     uint32_t w[PR_ROWS][4];
 #pragma unroll
     for (int r = 0; r < PR_ROWS; r++) {
-        const int dy = min(oy + r, dh - 1);
-        const int q0 = yofs[dy];
-        const int r0 = q0 >= 0 ? (q0 < sh ? q0 : sh - 1) : 0;
-        const int r1 = q0 + 1 >= 0 ? (q0 + 1 < sh ? q0 + 1 : sh - 1) : 0;
-        const uint8_t* R0 = S + (int64_t)r0 * sp;
-        const uint8_t* R1 = S + (int64_t)r1 * sp;
-        w[r][0] = ld_u32(R0 + wb); w[r][1] = ld_u32(R0 + wb1);
-        w[r][2] = ld_u32(R1 + wb); w[r][3] = ld_u32(R1 + wb1);
+        const int4 yr = yrow[min(oy + r, dh - 1)];
+        w[r][0] = __builtin_amdgcn_raw_buffer_load_b32(rs, wb, yr.x, 0);
+        w[r][1] = __builtin_amdgcn_raw_buffer_load_b32(rs, wb1, yr.x, 0);
+        w[r][2] = __builtin_amdgcn_raw_buffer_load_b32(rs, wb, yr.y, 0);
+        w[r][3] = __builtin_amdgcn_raw_buffer_load_b32(rs, wb1, yr.y, 0);
     }
-    uint8_t* Df = dst + (int64_t)f * dst_fs;
-    if (ox + PR_COLS > xs) pyr_rows_out<true>(w, sel, coef, beta, Df, dp, oy, dh, cx, dw, xs);
-    else pyr_rows_out<false>(w, sel, coef, beta, Df, dp, oy, dh, cx, dw, xs);
+    (void)dp;
+    const bool edge = ox + PR_COLS > dw - 1;
+    if (ox + PR_COLS > xs) {
+        if (edge) pyr_rows_out<true, true>(w, sel, coef, yrow, rd, oy, dh, cx, dw, xs);
+        else pyr_rows_out<true, false>(w, sel, coef, yrow, rd, oy, dh, cx, dw, xs);
+    } else {
+        if (edge) pyr_rows_out<false, true>(w, sel, coef, yrow, rd, oy, dh, cx, dw, xs);
+        else pyr_rows_out<false, false>(w, sel, coef, yrow, rd, oy, dh, cx, dw, xs);
+    }
 }
 
 // ================================ k_blur ================================
@@ -429,6 +441,8 @@ struct BlurWork {
     int item_off[COEB_MAXL + 1];   // wave items per level (prefix)
     int nstrips[COEB_MAXL];        // 56-column strips
     int bh[COEB_MAXL];             // rows per band (4 bands per item)
+    int nquads[COEB_MAXL];         // k_blur_rows: groups of 4 adjacent strips per level
+    int brows;                     // k_blur_rows: rows per band
 };
 
 
@@ -562,6 +576,119 @@ __global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, E
     }
 }
 
+// The same filter with wave-uniform rows: a wave item is 4 ADJACENT 56-column strips (one per
+// 16-lane group) of one band of brows rows, so every row index, its REFLECT_101 and the row
+// pointers are scalar (SGPR base + the lane's constant column offset, no per-row 64-bit address
+// VALU), the band halo is 6 rows per brows instead of per 16, and the next 7-row block's loads
+// are issued before the current block is filtered.
+__device__ __forceinline__ int reflect_row(int r, int h)
+{
+    // selects, not min/max chains: uniform min3/max3 has no scalar form, and the compiler then
+    // moves the whole row offset into VGPRs
+    int rr = r < 0 ? -r : r;
+    rr = rr >= h ? 2 * h - 2 - rr : rr;
+    return rr < 0 ? 0 : rr;
+}
+
+__global__ __launch_bounds__(kThreads) void k_blur_rows(const Plan* __restrict__ P, ExtractBufs b, BlurWork bw)
+{
+    const int2 bxy = block_xy();
+    const int f = bxy.y;
+    const int item = bw.item0 + bxy.x * kWaves + wave_id();
+    if (item >= bw.item1) return;
+    int l = 0;
+    while (l + 1 < bw.L && item >= bw.item_off[l + 1]) l++;
+    const int it = item - bw.item_off[l];
+    const int nq = bw.nquads[l];
+    const int quad = it % nq, band = it / nq;
+    const LevelGeom& g = P->lv[l];
+    const int w = g.w, h = g.h, sp = g.pitch, dp = g.bpitch;
+    const int lane = lane_id(), grp = lane >> 4, gl = lane & 15;
+    const int y0 = band * bw.brows, y1 = min(h, y0 + bw.brows);
+    const int x = (quad * 4 + grp) * kBlurCols - 4 + gl * 4;
+    const bool produce = gl >= 1 && gl <= 14 && x < w;
+    // Every lane loads one dword at column a and picks its 4 columns' bytes with the u16-pair
+    // perms below: a = x inside the level; at the edges a is moved so that the REFLECT_101
+    // columns reflect101(x + q) all fall in [a, a + 3] (w >= 5), so no lane takes a byte path.
+    int cq[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) cq[q] = reflect101(min(x + q, w + 2), w);
+    const int a = min(min(min(cq[0], cq[1]), min(cq[2], cq[3])), w - 4);
+    const uint32_t sel0 = 0x0c000c00u | (uint32_t)(cq[0] - a) | ((uint32_t)(cq[1] - a) << 16);
+    const uint32_t sel1 = 0x0c000c00u | (uint32_t)(cq[2] - a) | ((uint32_t)(cq[3] - a) << 16);
+    // rows through buffer resources: the row offset is a scalar (soffset), the lane's column
+    // the only vector operand
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)level_ptr(P, b, f, l), 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(b.blur + (int64_t)f * P->blur_stride + g.blur_off), 0, 0x7fffffff,
+                                          0x00020000);
+    const int k0 = P->gauss[0], k1 = P->gauss[1], k2 = P->gauss[2], k3 = P->gauss[3];
+    const us2 K0 = pk2(k0, k0), K1 = pk2(k1, k1), K2 = pk2(k2, k2), K3 = pk2(k3, k3);
+    const us2 W_l01_0 = pk2(0, k0), W_l23_0 = pk2(k1, k2), W_c01_0 = pk2(k3, k2), W_c23_0 = pk2(k1, k0);
+    const us2 W_l23_1 = pk2(k0, k1), W_c01_1 = pk2(k2, k3), W_c23_1 = pk2(k2, k1), W_r01_1 = pk2(k0, 0);
+    const us2 W_l23_2 = pk2(0, k0), W_c01_2 = pk2(k1, k2), W_c23_2 = pk2(k3, k2), W_r01_2 = pk2(k1, k0);
+    const us2 W_c01_3 = pk2(k0, k1), W_c23_3 = pk2(k2, k3), W_r01_3 = pk2(k2, k1), W_r23_3 = pk2(k0, 0);
+    const uint32_t rnd = 1u << 15;
+    const int n_rows = (y1 - y0) + 6;          // source rows y0-3 .. y1+2
+    auto load_row = [&](int i) -> uint32_t {   // source row y0 - 3 + i (uniform), REFLECT_101
+        const int so = __builtin_amdgcn_readfirstlane(reflect_row(y0 - 3 + i, h) * sp);
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, a, so, 0);
+    };
+    uint32_t nxt[7];
+#pragma unroll
+    for (int ph = 0; ph < 7; ph++) nxt[ph] = load_row(ph);
+    uint32_t R0[7], R1[7];
+    for (int i0 = 0; i0 < n_rows; i0 += 7) {
+        uint32_t raw[7];
+#pragma unroll
+        for (int ph = 0; ph < 7; ph++) raw[ph] = nxt[ph];
+        if (i0 + 7 < n_rows) {
+#pragma unroll
+            for (int ph = 0; ph < 7; ph++) nxt[ph] = load_row(i0 + 7 + ph);
+        }
+#pragma unroll
+        for (int ph = 0; ph < 7; ph++) {
+            const int i = i0 + ph;
+            if (i >= n_rows) break;
+            R0[ph] = __builtin_amdgcn_perm(0u, raw[ph], sel0);
+            R1[ph] = __builtin_amdgcn_perm(0u, raw[ph], sel1);
+            if (i < 6) continue;
+            const int s0 = (ph + 1) % 7, s1 = (ph + 2) % 7, s2 = (ph + 3) % 7, s3 = (ph + 4) % 7,
+                      s4 = (ph + 5) % 7, s5 = (ph + 6) % 7, s6 = ph;
+            const us2 v01 = K3 * as_us2(R0[s3]) + K2 * (as_us2(R0[s2]) + as_us2(R0[s4])) +
+                            K1 * (as_us2(R0[s1]) + as_us2(R0[s5])) + K0 * (as_us2(R0[s0]) + as_us2(R0[s6]));
+            const us2 v23 = K3 * as_us2(R1[s3]) + K2 * (as_us2(R1[s2]) + as_us2(R1[s4])) +
+                            K1 * (as_us2(R1[s1]) + as_us2(R1[s5])) + K0 * (as_us2(R1[s0]) + as_us2(R1[s6]));
+            const uint32_t V01 = as_u32(v01), V23 = as_u32(v23);
+            const us2 L01 = as_us2(dpp_shr1(V01)), L23 = as_us2(dpp_shr1(V23));
+            const us2 R01 = as_us2(dpp_shl1(V01)), R23 = as_us2(dpp_shl1(V23));
+            uint32_t a0 = __builtin_amdgcn_udot2(L01, W_l01_0, rnd, false);
+            a0 = __builtin_amdgcn_udot2(L23, W_l23_0, a0, false);
+            a0 = __builtin_amdgcn_udot2(v01, W_c01_0, a0, false);
+            a0 = __builtin_amdgcn_udot2(v23, W_c23_0, a0, false);
+            uint32_t a1 = __builtin_amdgcn_udot2(L23, W_l23_1, rnd, false);
+            a1 = __builtin_amdgcn_udot2(v01, W_c01_1, a1, false);
+            a1 = __builtin_amdgcn_udot2(v23, W_c23_1, a1, false);
+            a1 = __builtin_amdgcn_udot2(R01, W_r01_1, a1, false);
+            uint32_t a2 = __builtin_amdgcn_udot2(L23, W_l23_2, rnd, false);
+            a2 = __builtin_amdgcn_udot2(v01, W_c01_2, a2, false);
+            a2 = __builtin_amdgcn_udot2(v23, W_c23_2, a2, false);
+            a2 = __builtin_amdgcn_udot2(R01, W_r01_2, a2, false);
+            uint32_t a3 = __builtin_amdgcn_udot2(v01, W_c01_3, rnd, false);
+            a3 = __builtin_amdgcn_udot2(v23, W_c23_3, a3, false);
+            a3 = __builtin_amdgcn_udot2(R01, W_r01_3, a3, false);
+            a3 = __builtin_amdgcn_udot2(R23, W_r23_3, a3, false);
+            const int y = y0 - 6 + i;                                  // uniform
+            if (produce) {
+                const uint32_t p01 = __builtin_amdgcn_perm(a1, a0, 0x0c0c0602u);
+                const uint32_t p23 = __builtin_amdgcn_perm(a3, a2, 0x06020c0cu);
+                __builtin_amdgcn_raw_buffer_store_b32(p01 | p23, rd, x, __builtin_amdgcn_readfirstlane(y * dp), 0);
+            }
+        }
+    }
+}
+
 // ================================ k_fast ================================
 // One workgroup per (FAST cell, frame).  The cell ROI (<= 64 x 64) is staged in LDS; each
 // detection pixel gets its corner strength M = max over the 16 nine-pixel arcs of
@@ -671,9 +798,15 @@ constexpr int kFastRowBytes = 72;          // >= 1 + 64 + 7 (slab byte = ROI col
 constexpr int kFastRowBytesM = 96;         // ROIs up to 46 wide: pixels in bytes 0..47, M in bytes 48..95
 // (24 dwords: the four rows a half-wave's pre-test reads land on disjoint banks, (a/4) mod 32)
 constexpr int kFastGuard = 16;             // bytes before each wave's slab (unaligned staging spill)
-constexpr int kFastSurv = 384;             // survivor list (flushed when one more pass could overflow it)
-constexpr int kFastCorners = 384;          // corner list (more corners: NMS walks the whole window)
-constexpr int kFastLists = kFastSurv + 64;   // u16 entries before the corner list
+constexpr int kFastEnt = 128;              // pre-test entries (u16: first pixel's offset / 4 | survivor mask << 12)
+constexpr int kFastSurv = 4 * 64 + 8;      // survivors of one 64-entry expansion, + the odd-count pad
+constexpr int kFastCorners = 256;          // corner list (more corners: NMS walks the whole window)
+constexpr int kFastLists = kFastSurv;      // u16 entries before the corner list
+// entry offsets / 4 fit 12 bits: ROIs are at most 64 rows (coeb_capi.hip kRoiMax)
+static_assert(kFastRowBytesM * 64 <= 4 * 4096 && kFastRowBytes * 64 <= 4 * 4096, "k_fast entry offset field");
+#ifndef COEB_FAST_PK
+#define COEB_FAST_PK 1             // survivors' strengths two per lane (u16 halves); 0: one per lane
+#endif              // pre-test entries (u32: first pixel's offset | survivor mask << 16)
 
 __device__ __forceinline__ void wave_sync_lds()
 {
@@ -722,6 +855,56 @@ __device__ __forceinline__ uint32_t pretest_half(us2 v, us2 p0, us2 p8, us2 p2, 
     const us2 md = pk_max(pk_max(pk_min(p0, p8), pk_min(p2, p10)), pk_max(pk_min(p4, p12), pk_min(p6, p14)));
     const us2 mb = pk_min(pk_min(pk_max(p0, p8), pk_max(p2, p10)), pk_min(pk_max(p4, p12), pk_max(p6, p14)));
     return as_u32(pk_subs(lo, md)) | as_u32(pk_subs(mb, hi));
+}
+
+// corner_strength_sel for TWO survivors at once, one per u16 half (pixel A at slab offset oa in
+// the low halves, pixel B at ob in the high halves): the same min / max / xor steps as packed
+// u16 operations (ring bytes loaded straight into the halves), M as a saturating difference
+// (M <= 0 -> 0: only M > t is ever used).  Returns the packed (M_A, M_B).
+__device__ __forceinline__ uint32_t us2_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+template <int st>
+__device__ __forceinline__ us2 corner_strength_pk(const uint8_t* roi, int oa, int ob, int t)
+{
+    lds_cu8 ba = (lds_cu8)roi + oa - (3 * st + 1);
+    lds_cu8 bb = (lds_cu8)roi + ob - (3 * st + 1);
+    asm volatile("" : "+v"(ba), "+v"(bb));
+    constexpr int o = 3 * st + 1;
+    constexpr int off[16] = {o + 3 * st, o + 3 * st + 1, o + 2 * st + 2, o + st + 3, o + 3, o - st + 3, o - 2 * st + 2,
+                             o - 3 * st + 1, 1, 0, o - 2 * st - 2, o - st - 3, o - 3, o + st - 3, o + 2 * st - 2,
+                             o + 3 * st - 1};
+    us2 p[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) { p[k].x = ba[off[k]]; p[k].y = bb[off[k]]; }
+    us2 v;
+    v.x = ba[o]; v.y = bb[o];
+    const us2 T = pk2(t, t);
+    const us2 md = pk_max(pk_max(pk_min(p[0], p[8]), pk_min(p[2], p[10])), pk_max(pk_min(p[4], p[12]), pk_min(p[6], p[14])));
+    const us2 mb = pk_min(pk_min(pk_max(p[0], p[8]), pk_max(p[2], p[10])), pk_min(pk_max(p[4], p[12]), pk_max(p[6], p[14])));
+    // dark: md < v - t (v - t - md > 0 with saturation); bright: mb > v + t
+    const us2 dk = pk_subs(pk_subs(v, T), md), br = pk_subs(mb, v + T);
+    const us2 one = pk2(1, 1), ff = pk2(255, 255);
+    const us2 dmask = pk_min(dk, one) * ff;            // 0x00FF in the dark halves
+    us2 q[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) q[k] = as_us2(us2_u32(p[k]) ^ us2_u32(dmask));
+    auto arc = [](const us2(&a)[16]) {
+        us2 m3[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) m3[k] = pk_min(pk_min(a[k], a[(k + 1) & 15]), a[(k + 2) & 15]);
+        us2 X = pk2(0, 0);
+#pragma unroll
+        for (int k = 0; k < 16; k++) X = pk_max(X, pk_min(pk_min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]));
+        return X;
+    };
+    us2 M = pk_subs(arc(q), as_us2(us2_u32(v) ^ us2_u32(dmask)));
+    // a half passing both pre-tests (rare) also takes the bright pass
+    const us2 both = pk_min(pk_min(dk, one), pk_min(br, one));
+    if (__builtin_expect(__ballot(us2_u32(both) != 0u) != 0, 0)) {
+        const us2 M2 = pk_subs(arc(p), v);
+        M = pk_max(M, as_us2(us2_u32(M2) & us2_u32(both * pk2(0xFFFF, 0xFFFF))));
+    }
+    return M;
 }
 
 // Same test, raw packed results: pixel q survives iff 16-bit half q of (lo, hi) is nonzero.
@@ -908,7 +1091,7 @@ __host__ __device__ inline int fast_ms_slab(const Plan& P, int rb)
 }
 __host__ __device__ inline int fast_wave_lds(const Plan& P, int rb)
 {
-    return kFastGuard + fast_slab(P, rb) + fast_ms_slab(P, rb) + 2 * (kFastLists + kFastCorners);
+    return kFastGuard + fast_slab(P, rb) + fast_ms_slab(P, rb) + 2 * (kFastLists + kFastCorners + kFastEnt);
 }
 
 #ifndef COEB_FAST_CLOCK
@@ -924,7 +1107,7 @@ __device__ unsigned long long g_fast_clk[256 * 8];
 template <int RB>
 __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, int f, int cidx, const CellDesc& c,
                                           int th_ini, int th_min, const uint8_t* roi, uint8_t* Ms, uint16_t* surv,
-                                          uint16_t* corn)
+                                          uint16_t* corn, uint16_t* ent)
 {
     constexpr int sh = 1;
     const int lane = lane_id();
@@ -933,67 +1116,102 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
     const int ww = rw - 6, wh = rh - 6;
     const int mp = RB == kFastRowBytesM ? RB : fast_mp(*P);   // M pitch
     const int npix = ww > 0 && wh > 0 ? ww * wh : 0;
-    // ---- 2 + 3: pre-test 4 pixels per lane (8 or 16 lanes per row), survivors in row-major
-    //      order -> exact strength -> corners
-    int ns = 0, nc = 0;
+    // ---- 2 + 3: pre-test 4 pixels per lane (8 or 16 lanes per row).  A lane with survivors
+    //      appends ONE entry (slab offset of its first pixel / 4 | 4-bit survivor mask << 12) to the
+    //      wave's entry list, in ballot (= row-major) order: one ballot per pass instead of one
+    //      compaction per pixel slot.  When a pass could overflow the list, and at the end, the
+    //      entries are expanded into the survivor list (a wave scan of their popcounts keeps the
+    //      row-major order) and the survivors' exact strengths taken -> Ms + corner list.
+    int ne = 0, nc = 0;
     const int ngrp = (ww + 3) >> 2;
     const int lpr_log = ngrp > 8 ? 4 : 3;
     const int cg = lane & ((1 << lpr_log) - 1), rsub = lane >> lpr_log;
     const int rpi = 64 >> lpr_log;
-    // lanes' pixel columns inside the window (fixed for the cell): one wave mask per pixel slot
-    const bool vm0 = cg < ngrp && 4 * cg + 0 < ww, vm1 = cg < ngrp && 4 * cg + 1 < ww;
-    const bool vm2 = cg < ngrp && 4 * cg + 2 < ww, vm3 = cg < ngrp && 4 * cg + 3 < ww;
-    const int dmy = kFastSurv + lane;     // this lane's scratch slot for pixels that did not survive
+    // lanes' pixel columns inside the window (fixed for the cell)
+    const uint32_t vmask4 = cg < ngrp ? (4 * cg + 0 < ww ? 1u : 0u) | (4 * cg + 1 < ww ? 2u : 0u) |
+                                            (4 * cg + 2 < ww ? 4u : 0u) | (4 * cg + 3 < ww ? 8u : 0u)
+                                      : 0u;
     int o = (rsub + 3) * RB + 4 + 4 * cg;
+    const uint32_t one2 = 0x00010001u;
     FC_MARK(t_scan);
     long long t_str = 0;
-    // (reading pass k+1's slab words before evaluating pass k, pre_load / pre_eval, measured
-    // 0.330 vs 0.318 ms; a lane-per-group mapping that keeps all 64 lanes busy on 30-37-px
-    // windows measured 0.338: the scan is not the bound, `tools/_fast_timing.py`; storing a
-    // 4-bit survivor mask per lane and pass and compacting all passes after the loop with one
-    // wave scan measured 0.324 vs 0.288 ms)
     for (int r0 = 0; npix > 0 && r0 < wh; r0 += rpi, o += rpi * RB) {
         // every lane runs the test (rows past the window read slab bytes that are masked off)
         uint32_t lo, hi;
         fast_pretest4_raw<RB>(&roi[o], th_min, lo, hi);
-        const bool rv = r0 + rsub < wh;
-        const bool f0 = rv && vm0 && (lo & 0xffffu) != 0u, f1 = rv && vm1 && (lo >> 16) != 0u;
-        const bool f2 = rv && vm2 && (hi & 0xffffu) != 0u, f3 = rv && vm3 && (hi >> 16) != 0u;
-        const uint64_t m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2), m3 = __ballot(f3);
-        if (m0 | m1 | m2 | m3) {
-            // row-major order: pixel q of this lane after every survivor of the lanes below; stores
-            // without branches (a pixel that did not survive goes to the lane's scratch slot)
-            int q = ns + mbcnt(m0) + mbcnt(m1) + mbcnt(m2) + mbcnt(m3);
-            surv[f0 ? q : dmy] = (uint16_t)o;
-            q += f0 ? 1 : 0;
-            surv[f1 ? q : dmy] = (uint16_t)(o + 1);
-            q += f1 ? 1 : 0;
-            surv[f2 ? q : dmy] = (uint16_t)(o + 2);
-            q += f2 ? 1 : 0;
-            surv[f3 ? q : dmy] = (uint16_t)(o + 3);
-            ns = uniform(ns + __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
+        // survivor bits: a packed u16 half is nonzero iff its pixel survives.  min(half, 1) as an
+        // opaque v_pk_min_u16: written in C the compiler turns it into per-half compares and selects
+        uint32_t s01, s23;
+        asm("v_pk_min_u16 %0, %1, %2" : "=v"(s01) : "v"(lo), "v"(one2));
+        asm("v_pk_min_u16 %0, %1, %2" : "=v"(s23) : "v"(hi), "v"(one2));
+        const uint32_t t2 = s01 | (s23 << 2);
+        const uint32_t m4 = (t2 | (t2 >> 15)) & (r0 + rsub < wh ? vmask4 : 0u);
+        const uint64_t mk = __ballot(m4 != 0u);
+        if (mk) {
+            if (m4) ent[ne + mbcnt(mk)] = (uint16_t)(((uint32_t)o >> 2) | (m4 << 12));   // o = 4 mod 4: exact
+            ne = uniform(ne + (int)__popcll(mk));
         }
-        if (ns > kFastSurv - 256 || r0 + rpi >= wh) {
+        if (ne > kFastEnt - 64 || r0 + rpi >= wh) {
             FC_MARK(t_s0);
             wave_sync_lds();
-            for (int e0 = 0; e0 < ns; e0 += 64) {
+            for (int e0 = 0; e0 < ne; e0 += 64) {
                 const int e = e0 + lane;
-                int oo = 0, M = 0;
-                if (e < ns) {
-                    oo = surv[e];
-                    M = corner_strength_sel<RB>(&roi[oo], th_min);
+                const uint32_t en = e < ne ? (uint32_t)ent[e] : 0u;
+                const uint32_t m = en >> 12;
+                const int cnt = __popc(m);
+                // exclusive prefix of cnt (0..4) over the lanes, by bit planes
+                const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
+                int q = mbcnt(b0) + 2 * mbcnt(b1) + 4 * mbcnt(b2);
+                const int ns = uniform((int)__popcll(b0) + 2 * (int)__popcll(b1) + 4 * (int)__popcll(b2));
+                const int ob = (int)(en & 0xFFFu) << 2;
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if ((m >> k) & 1u) surv[q++] = (uint16_t)(ob + k);
+                surv[ns] = surv[ns > 0 ? ns - 1 : 0];      // pad an odd count (the pair's B repeats A's pixel)
+                wave_sync_lds();
+#if !COEB_FAST_PK
+                for (int s0 = 0; s0 < ns; s0 += 64) {
+                    const int si = s0 + lane;
+                    int oo = 0, M = 0;
+                    if (si < ns) {
+                        oo = surv[si];
+                        M = corner_strength_sel<RB>(&roi[oo], th_min);
+                    }
+                    const bool isc = si < ns && M > th_min;
+                    if (isc) Ms[fast_mi<RB>(oo, mp)] = (uint8_t)M;
+                    const uint64_t mc = __ballot(isc);
+                    if (isc) {
+                        const int qq = nc + mbcnt(mc);
+                        if (qq < kFastCorners) corn[qq] = (uint16_t)oo;
+                    }
+                    nc = uniform(nc + (int)__popcll(mc));
                 }
-                const bool isc = e < ns && M > th_min;
-                if (isc) Ms[fast_mi<RB>(oo, mp)] = (uint8_t)M;
-                const uint64_t mc = __ballot(isc);
-                if (isc) {
-                    const int qq = nc + mbcnt(mc);
-                    if (qq < kFastCorners) corn[qq] = (uint16_t)oo;
+#else
+                // two survivors per lane (u16 halves): survivor 2i in the low half, 2i + 1 in the high
+                for (int s0 = 0; s0 < ns; s0 += 128) {
+                    const int si = s0 + 2 * lane;
+                    int oa = 0, ob = 0;
+                    uint32_t Mp = 0;
+                    if (si < ns) {
+                        const uint32_t pr = reinterpret_cast<const uint32_t*>(surv)[si >> 1];
+                        oa = (int)(pr & 0xFFFFu);
+                        ob = (int)(pr >> 16);
+                        Mp = us2_u32(corner_strength_pk<RB>(roi, oa, ob, th_min));
+                    }
+                    const int Ma = (int)(Mp & 0xFFFFu), Mb = (int)(Mp >> 16);
+                    const bool ia = si < ns && Ma > th_min, ib = si + 1 < ns && Mb > th_min;
+                    if (ia) Ms[fast_mi<RB>(oa, mp)] = (uint8_t)Ma;
+                    if (ib) Ms[fast_mi<RB>(ob, mp)] = (uint8_t)Mb;
+                    const uint64_t ma = __ballot(ia), mbl = __ballot(ib);
+                    const int qq = nc + mbcnt(ma) + mbcnt(mbl);
+                    if (ia && qq < kFastCorners) corn[qq] = (uint16_t)oa;
+                    if (ib && qq + (ia ? 1 : 0) < kFastCorners) corn[qq + (ia ? 1 : 0)] = (uint16_t)ob;
+                    nc = uniform(nc + (int)__popcll(ma) + (int)__popcll(mbl));
                 }
-                nc = uniform(nc + __popcll(mc));
+#endif
+                wave_sync_lds();
             }
-            wave_sync_lds();
-            ns = 0;
+            ne = 0;
             if (COEB_FAST_CLOCK) t_str += (long long)clock64() - t_s0;
         }
     }
@@ -1082,7 +1300,8 @@ __global__ __launch_bounds__(kThreads, 6) void k_fast(const Plan* __restrict__ P
     uint8_t* roi = wbase;
     uint8_t* Ms = RB == kFastRowBytesM ? wbase : wbase + slab;
     uint16_t* surv = reinterpret_cast<uint16_t*>(wbase + slab + ms_slab);
-    uint16_t* corn = surv + kFastLists;         // surv: kFastSurv entries + one scratch slot per lane
+    uint16_t* corn = surv + kFastLists;
+    uint16_t* ent = corn + kFastCorners;
     const int2 bxy = block_xy<false>();
     const int f = bxy.y;
     const int cidx = cell0 + bxy.x * kWaves + wv;
@@ -1107,7 +1326,7 @@ __global__ __launch_bounds__(kThreads, 6) void k_fast(const Plan* __restrict__ P
     }
     wave_sync_lds();
     FC_ADD(0, t_st);                              // wait for the ROI loads + stage + M clear
-    fast_cell<RB>(P, b, f, cidx, c, th_ini, th_min, roi, Ms, surv, corn);
+    fast_cell<RB>(P, b, f, cidx, c, th_ini, th_min, roi, Ms, surv, corn, ent);
     FC_ADD(4, t_all);
 }
 
@@ -1267,7 +1486,8 @@ __device__ __forceinline__ void child_rect(const int4 p, int q, int4* out, int* 
 __device__ long long g_oct_clk[4096 * 6];
 
 template <int NT>
-__global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, ExtractBufs b, int level0)
+__global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, ExtractBufs b, int level0, int oct_w,
+                                                int oct_kl)   // this launch's node slots / LDS key capacity
 {
     const long long oc_t0 = COEB_OCT_CLOCK ? (long long)clock64() : 0;
     const long long oc_w0 = COEB_OCT_CLOCK ? (long long)wall_clock64() : 0;
@@ -1275,14 +1495,14 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
     constexpr int NW = NT / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int sbuf[(NW + 2 + 3) & ~3];   // 16-byte multiple: keeps the dynamic LDS base aligned
-    const OctLds O = oct_lds(smem, P->oct_w, P->oct_kl);
+    const OctLds O = oct_lds(smem, oct_w, oct_kl);
     int* const s_work = O.work;      // slot ids of nodes divided this phase (processing order)
     int4* const s_cnt = O.cnt;       // their quadrant counts
     int* const s_base = O.base;      // exclusive prefix of nonempty children (push order)
     int* const s_rank = O.rank;      // final phase: processing rank of vPrev entry
     int* const s_push = O.push;      // final phase: push-order base per rank
     uint8_t* const s_dead = O.dead;  // final phase: slot erased this round
-    const int OCT_LMAX = P->oct_w;
+    const int OCT_LMAX = oct_w;
 
     // frame-fastest grid: every frame's level-0 list (the longest) is dispatched in the first
     // wave of workgroups, the cheap upper levels fill in behind them
@@ -1306,7 +1526,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
     // keys in LDS when they fit, else in the level's global ping-pong buffers (L2-resident)
     uint32_t* KB0;
     int64_t kdelta;
-    if (K <= P->oct_kl) {
+    if (K <= oct_kl) {
         KB0 = O.keys[0];
         kdelta = O.keys[1] - O.keys[0];
     } else {
@@ -1314,7 +1534,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
         kdelta = P->kbuf_stride;
     }
     auto KB = [&](int i) -> uint32_t* { return KB0 + (i ? kdelta : 0); };
-    if (g.ncells < P->oct_kl) {
+    if (g.ncells < oct_kl) {
         // per-cell offsets in LDS (keys[1] is free until the pre-octree cull), then every
         // thread copies keys, finding its cell by binary search: all loads independent
         int* s_coff = reinterpret_cast<int*>(O.keys[1]);
@@ -2045,6 +2265,169 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
     if (lane < 2 * nk) gd[lane] = reinterpret_cast<const uint4*>(dsl)[lane];
 }
 
+// The same three phases with the wave's 8 blurred patches staged straight into LDS by LDS-DMA
+// (global_load_lds_dwordx4, no VGPR round trip), all issued before the IC_Angle rows: the wave
+// then waits on memory once instead of once per patch pair, and phase B reads every patch from
+// LDS.  Patch rows sit at a 64-byte pitch (an LDS-DMA instruction writes 64 x 16 consecutive
+// bytes, so rows cannot be padded); 8 x 2368 B per wave = 77 KB per workgroup, 2 per CU.
+constexpr int kDmaRow = 64, kDmaPatch = kDmaRow * kBlRows;   // 2368 B = 148 chunks
+template <int KP> constexpr int dma_wave_lds() { return KP * kDmaPatch + 32 * KP; }
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+template <bool kVec0, int KP>
+__global__ __launch_bounds__(kThreads) void k_describe_dma(const Plan* __restrict__ P, ExtractBufs b)
+{
+    constexpr int kLpk = 64 / KP, kHl = kLpk / 2, kNr = 16 / kHl, kNb = kNr < 4 ? kNr : 4;
+    constexpr int kDmaWaveLds = dma_wave_lds<KP>();
+    extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+    uint32_t (*s_msk)[8] = reinterpret_cast<uint32_t (*)[8]>(dsm + kWaves * kDmaWaveLds);
+    if (threadIdx.x < 17 * 8) s_msk[threadIdx.x >> 3][threadIdx.x & 7] = ic_mask(threadIdx.x >> 3, threadIdx.x & 7);
+    __syncthreads();
+    const int2 bxy = block_xy();
+    const int f = bxy.y;
+    const int L = P->L;
+    const int lane = lane_id(), wv = wave_id();
+    const int nl = lane < L ? b.lvl_n[(int64_t)f * L + lane] : 0;
+    int incl = nl;
+    for (int o = 1; o < COEB_MAXL; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const int total = __builtin_amdgcn_readlane(incl, L - 1);
+    if (bxy.x == 0 && threadIdx.x == 0) b.counts[f] = total;
+    const int idx0 = (bxy.x * kWaves + wv) * KP;
+    if (idx0 >= total) return;
+    const int nk = min(KP, total - idx0);
+    const int kq = lane / kLpk, half = (lane / kHl) & 1, qi = lane % kHl;
+    const int id = idx0 + min(kq, nk - 1);
+    int l = 0, start = 0;
+    for (int q = 0; q < L - 1; q++) {
+        const int e = __builtin_amdgcn_readlane(incl, q);
+        if (id >= e) { l = q + 1; start = e; }
+    }
+    const LevelGeom& g = P->lv[l];
+    const uint32_t key = b.lvl_kp[(int64_t)f * P->lvl_stride + g.out_off + (id - start)];
+    const int x = key_x(key), y = key_y(key), sc = key_s(key);
+    const uint8_t* img = level_ptr(P, b, f, l);
+    // ---- the nk blurred patches -> the wave's slab (rows y-18..y+18, 64 bytes from (x-18) & ~15)
+    uint8_t* slab = dsm + wv * kDmaWaveLds;
+    const int porg = (int)g.blur_off + (y - 18) * g.bpitch + ((x - 18) & ~15);
+    const int xoff = x - ((x - 18) & ~15);
+    const int bpitch = g.bpitch;
+    {
+        const uint8_t* blur_f = b.blur + (int64_t)f * P->blur_stride;
+        const int r0 = lane >> 2, c16 = 16 * (lane & 3);
+#pragma unroll
+        for (int t = 0; t < KP; t++) {
+            if (t < nk) {
+                const uint8_t* src = blur_f + __builtin_amdgcn_readlane(porg, t * kLpk);
+                const int bpt = __builtin_amdgcn_readlane(bpitch, t * kLpk);
+                uint8_t* dst = slab + t * kDmaPatch;
+                __builtin_amdgcn_global_load_lds((gvoid_t*)(src + r0 * bpt + c16), (lvoid_t*)dst, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gvoid_t*)(src + (r0 + 16) * bpt + c16), (lvoid_t*)(dst + 1024), 16, 0, 0);
+                if (lane < (kBlChunks - 128))
+                    __builtin_amdgcn_global_load_lds((gvoid_t*)(src + (r0 + 32) * bpt + c16), (lvoid_t*)(dst + 2048), 16,
+                                                     0, 0);
+            }
+        }
+    }
+    // ---- phase A: IC_Angle, fastAtan2, sincos, the cv::KeyPoint record (as k_describe)
+    uint32_t A = 0, S = 0;
+    int m01 = 0;
+    const int a = (x - 15) & 15;
+    const uint32_t m8 = (a & 8) ? 0xFFFFFFFFu : 0u, m4 = (a & 4) ? 0xFFFFFFFFu : 0u;
+    const uint8_t* rowp = img + (int64_t)y * g.pitch + (x - 15 - a);
+    const int64_t spitch = half ? (int64_t)g.pitch : -(int64_t)g.pitch;
+    const bool vec = kVec0 || l != 0;
+#pragma unroll
+    for (int i0 = 0; i0 < kNr; i0 += kNb) {
+        uint4 c[kNb][3];
+#pragma unroll
+        for (int r = 0; r < kNb; r++) {
+            const uint8_t* rp = rowp + (qi + kHl * (i0 + r)) * spitch;
+            if (vec) ic_row_load<true>(rp, c[r][0], c[r][1], c[r][2]);
+            else ic_row_load<false>(rp, c[r][0], c[r][1], c[r][2]);
+        }
+#pragma unroll
+        for (int r = 0; r < kNb; r++) {
+            const int av = qi + kHl * (i0 + r);
+            const uint32_t* msk = s_msk[(av == 0 && half) ? 16 : av];
+            const uint32_t q[12] = {c[r][0].x, c[r][0].y, c[r][0].z, c[r][0].w, c[r][1].x, c[r][1].y,
+                                    c[r][1].z, c[r][1].w, c[r][2].x, c[r][2].y, c[r][2].z, c[r][2].w};
+            uint32_t r1[10], r2[9];
+#pragma unroll
+            for (int k = 0; k < 10; k++) r1[k] = (m8 & q[k + 2]) | (~m8 & q[k]);
+#pragma unroll
+            for (int k = 0; k < 9; k++) r2[k] = (m4 & r1[k + 1]) | (~m4 & r1[k]);
+            uint32_t rs = 0;
+#pragma unroll
+            for (int d = 0; d < 8; d++) {
+                const uint32_t pm = __builtin_amdgcn_alignbyte(r2[d + 1], r2[d], (uint32_t)(a & 3)) & msk[d];
+                A = __builtin_amdgcn_udot4(pm, 0x03020100u + 0x04040404u * (uint32_t)d, A, false);
+                rs = __builtin_amdgcn_udot4(pm, 0x01010101u, rs, false);
+            }
+            S += rs;
+            m01 += av * (int)rs;
+        }
+    }
+    if (half == 0) m01 = -m01;
+#pragma unroll
+    for (int o = 1; o < kLpk; o <<= 1) {
+        A += __shfl_xor(A, o, 64);
+        S += __shfl_xor(S, o, 64);
+        m01 += __shfl_xor(m01, o, 64);
+    }
+    const int m10 = (int)A - 15 * (int)S;
+    const float angle = fast_atan2_dev((float)m01, (float)m10);
+    const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
+    float bs, ac;
+    sincos_canon(angle * factorPI, &bs, &ac);
+    if (lane % kLpk == 0 && kq < nk) {
+        float fx = (float)x, fy = (float)y;
+        if (l != 0) { fx *= g.scale; fy *= g.scale; }
+        KeyPointOut o;
+        o.x = fx; o.y = fy; o.size = (float)g.size_i; o.angle = angle; o.response = (float)sc;
+        o.octave = l; o.class_id = -1;
+        reinterpret_cast<KeyPointOut*>(b.kps)[(int64_t)f * P->kcap + idx0 + kq] = o;
+    }
+    // ---- phase B: 256 tests per keypoint from the staged patches
+    const int4 pa = reinterpret_cast<const int4*>(b.pattern)[lane];
+    float px0[4], py0[4], px1[4], py1[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int pw = t == 0 ? pa.x : t == 1 ? pa.y : t == 2 ? pa.z : pa.w;
+        px0[t] = (float)(int8_t)(pw & 0xff); py0[t] = (float)(int8_t)((pw >> 8) & 0xff);
+        px1[t] = (float)(int8_t)((pw >> 16) & 0xff); py1[t] = (float)(int8_t)(pw >> 24);
+    }
+    uint32_t* dsl = reinterpret_cast<uint32_t*>(slab + KP * kDmaPatch);
+    __builtin_amdgcn_s_waitcnt(0);           // every LDS-DMA of this wave has landed
+    wave_sync_lds();
+    for (int t = 0; t < nk; t++) {
+        const float tb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bs), t * kLpk));
+        const float ta = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ac), t * kLpk));
+        const uint8_t* bc = slab + t * kDmaPatch + 18 * kDmaRow + __builtin_amdgcn_readlane(xoff, t * kLpk);
+        const f32x2 AB = {ta, tb}, BA = {tb, ta};
+        uint32_t nib = 0;
+#pragma unroll
+        for (int tt = 0; tt < 4; tt++) {
+            const f32x2 t0 = f32x2{py0[tt], py0[tt]} * AB, t1 = f32x2{py1[tt], py1[tt]} * AB;
+            const f32x2 rc0 = __builtin_elementwise_fma(f32x2{px0[tt], px0[tt]}, BA, f32x2{t0.x, -t0.y});
+            const f32x2 rc1 = __builtin_elementwise_fma(f32x2{px1[tt], px1[tt]}, BA, f32x2{t1.x, -t1.y});
+            const int o0 = (int)__builtin_fmaf(rintf(rc0.x), (float)kDmaRow, rintf(rc0.y));
+            const int o1 = (int)__builtin_fmaf(rintf(rc1.x), (float)kDmaRow, rintf(rc1.y));
+            nib |= (uint32_t)(bc[o0] < bc[o1]) << tt;
+        }
+        uint32_t dw = nib << (4 * (lane & 7));
+        dw = dpp_or_shl4(dpp_or_xor2(dpp_or_xor1(dw)));
+        if ((lane & 7) == 0) dsl[8 * t + (lane >> 3)] = dw;
+    }
+    wave_sync_lds();
+    // ---- phase C: descriptors out
+    uint4* gd = reinterpret_cast<uint4*>(b.desc + ((int64_t)f * P->kcap + idx0) * 32);
+    if (lane < 2 * nk) gd[lane] = reinterpret_cast<const uint4*>(dsl)[lane];
+}
+
 }  // namespace
 
 // Per-cell phase clocks of k_fast (COEB_FAST_CLOCK builds), summed over the 256 slot copies;
@@ -2076,15 +2459,24 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     BlurWork bw;
     bw.L = plan.L;
     int items = 0;
+    const char* brv = getenv("COEB_BLUR_ROWS");            // rows per band of k_blur_rows; 0 = k_blur
+    const int brows = brv ? atoi(brv) : 64;
+    bw.brows = brows;
     for (int l = 0; l < plan.L; l++) {
         const LevelGeom& g = plan.lv[l];
         bw.nstrips[l] = (g.w + kBlurCols - 1) / kBlurCols;
-        // 64 rows per wave item (4 bands): 32-, 128- and 256-row items measured slower, also with
-        // the next row block's loads issued before the current one is filtered (0.190 ms either way)
-        const int nbands = 4 * ((g.h + 63) / 64);
-        bw.bh[l] = (g.h + nbands - 1) / nbands;
         bw.item_off[l] = items;
-        items += bw.nstrips[l] * (nbands / 4);
+        if (brows > 0) {
+            bw.nquads[l] = (bw.nstrips[l] + 3) / 4;
+            bw.bh[l] = 0;
+            items += bw.nquads[l] * ((g.h + brows - 1) / brows);
+        } else {
+            // 64 rows per wave item (4 bands): 32-, 128- and 256-row items measured slower, also with
+            // the next row block's loads issued before the current one is filtered (0.190 ms either way)
+            const int nbands = 4 * ((g.h + 63) / 64);
+            bw.bh[l] = (g.h + nbands - 1) / nbands;
+            items += bw.nstrips[l] * (nbands / 4);
+        }
     }
     bw.item_off[plan.L] = items;
     // COEB_PYR_BYTES=1 forces k_pyr_level's byte form for every level (tests run both forms)
@@ -2100,7 +2492,8 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         BlurWork w = bw;
         w.item0 = i0; w.item1 = i1;
         prof_begin(prof, "k_blur", st);
-        hipLaunchKernelGGL(k_blur, dim3((i1 - i0 + kWaves - 1) / kWaves, F), dim3(kThreads), 0, st, d_plan, b, w);
+        hipLaunchKernelGGL(brows > 0 ? k_blur_rows : k_blur, dim3((i1 - i0 + kWaves - 1) / kWaves, F), dim3(kThreads), 0,
+                           st, d_plan, b, w);
         prof_end(prof, st);
     };
     // FAST over levels [l0, l1): one wave per cell.  A band form (one LDS copy per cell-row
@@ -2138,7 +2531,8 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         if (rows && !pyr_bytes) {
             hipLaunchKernelGGL(k_pyr_rows, dim3((g.w + PR_COLS - 1) / PR_COLS, (g.h + kWaves * PR_ROWS - 1) / (kWaves * PR_ROWS), F),
                                dim3(kThreads), 0, s, src, src_fs, gp.pitch, gp.h, b.pyr + g.pyr_off, plan.pyr_stride,
-                               g.pitch, g.w, g.h, b.rtab + g.rtab_off, g.xmax, resize_simd_end(g.w));
+                               g.pitch, g.w, g.h, b.rtab + g.rtab_off, g.xmax, resize_simd_end(g.w),
+                               reinterpret_cast<const int4*>(b.rtab + g.yrow_off));
         } else {
             int tsw, tsh;
             pyr_tile_lds(gp.w, gp.h, g.w, g.h, &tsw, &tsh);
@@ -2154,12 +2548,41 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
             fast(side->s, 1, m);
         }
     }
-    constexpr int kOctThreads = 256;       // 512 / 1024 measured slower
+    constexpr int kOctThreads = 256;       // 512 / 1024 measured slower on large batches
     (void)hipFuncSetAttribute((const void*)k_octree<kOctThreads>, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);
+    // small batches (per-rank shards): level 0's list -- the longest chain of the step -- gets
+    // 1024 threads in a launch of its own; COEB_OCT_WIDE_F = the largest batch that does so.
+    // COEB_OCT_SPLIT = l: levels >= l (short lists) run as one-wave workgroups with LDS sized for
+    // those levels only (no block barriers; many more workgroups per CU)
+    const char* owf = getenv("COEB_OCT_WIDE_F");
+    const int oct_wide_f = owf ? atoi(owf) : 0;
+    const char* osp = getenv("COEB_OCT_SPLIT");
+    const int oct_split = osp ? atoi(osp) : 0;
+    int sw_w = 0, sw_kl = 512, sw_lds = 0;
+    if (oct_split > 0 && oct_split < plan.L) {
+        int nmax = 0;
+        for (int l = oct_split; l < plan.L; l++) { sw_w = std::max(sw_w, plan.lv[l].ncap); nmax = std::max(nmax, plan.lv[l].nfeat); }
+        while (sw_kl < 4096 && sw_kl < (9 * nmax + 1) / 2) sw_kl *= 2;
+        sw_lds = sw_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * sw_kl;
+        (void)hipFuncSetAttribute((const void*)k_octree<64>, hipFuncAttributeMaxDynamicSharedMemorySize, sw_lds);
+    }
     auto octree = [&](hipStream_t st, int l0, int l1) {
         if (l1 <= l0) return;
         prof_begin(prof, "k_octree", st);
-        hipLaunchKernelGGL(k_octree<kOctThreads>, dim3(F, l1 - l0), dim3(kOctThreads), plan.oct_lds, st, d_plan, b, l0);
+        if (l0 == 0 && F <= oct_wide_f) {
+            (void)hipFuncSetAttribute((const void*)k_octree<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);
+            hipLaunchKernelGGL(k_octree<1024>, dim3(F, 1), dim3(1024), plan.oct_lds, st, d_plan, b, 0, plan.oct_w, plan.oct_kl);
+            l0 = 1;
+        }
+        int lm = l1;
+        if (sw_lds > 0 && l1 > oct_split) {
+            const int ls = std::max(l0, oct_split);
+            hipLaunchKernelGGL(k_octree<64>, dim3(F, l1 - ls), dim3(64), sw_lds, st, d_plan, b, ls, sw_w, sw_kl);
+            lm = ls;
+        }
+        if (lm > l0)
+            hipLaunchKernelGGL(k_octree<kOctThreads>, dim3(F, lm - l0), dim3(kOctThreads), plan.oct_lds, st, d_plan, b, l0,
+                               plan.oct_w, plan.oct_kl);
         prof_end(prof, st);
     };
     // the late blur goes to the side stream (beside FAST / octree, which do not read it) and the
@@ -2189,6 +2612,23 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     }
     prof_begin(prof, "k_describe", s);
     const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
+    const char* ddv = getenv("COEB_DESC_DMA");            // 0: register-staged k_describe; 4 / 8: keypoints per wave
+    const int ddk = ddv ? atoi(ddv) : 0;
+    if (ddk == 4 || ddk == 8) {
+        auto go = [&](auto kern, int kp, size_t lds) {
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(kern, dim3((plan.kcap + kWaves * kp - 1) / (kWaves * kp), F), dim3(kThreads), lds, s, d_plan, b);
+        };
+        if (ddk == 8) {
+            const size_t lds = (size_t)kWaves * dma_wave_lds<8>() + 17 * 8 * 4;
+            if (vec0) go(k_describe_dma<true, 8>, 8, lds); else go(k_describe_dma<false, 8>, 8, lds);
+        } else {
+            const size_t lds = (size_t)kWaves * dma_wave_lds<4>() + 17 * 8 * 4;
+            if (vec0) go(k_describe_dma<true, 4>, 4, lds); else go(k_describe_dma<false, 4>, 4, lds);
+        }
+        prof_end(prof, s);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     // 8 keypoints per wave (round 1's 32 let one XCD's resident waves span ~20 frames and refetch
     // every patch row past L2; 4 and 16 measured slower)
     constexpr int KP = 8;

@@ -35,6 +35,8 @@ struct LevelGeom {
     int xmax;              // resize: columns >= xmax use S[sx]*2048
     int rows_ok;           // k_pyr_rows applies: every even column pair's sources within 6 bytes of
                            // the pair's 4-byte aligned window start (scale <= 2)
+    int yrow_off;          // into resize table (ints): per output row {r0 * sp, r1 * sp, beta, dy * pitch}
+                           // (the clamped source rows' byte offsets; sp = the source level's pitch)
     int ncols, nrows, wcell, hcell;
     int cell0, ncells;     // range in the cell table (row-major over non-skipped cells)
     int kcap_off, kcap;    // octree key buffers: offset / capacity (u32 entries)

@@ -61,11 +61,28 @@ __device__ void pq_from_R(const double R[9], Se3& s)
     s.x = q[0]; s.y = q[1]; s.z = q[2]; s.w = q[3];
 }
 
+__device__ __forceinline__ double rl_d(double v, int j)   // v of lane j (j wave-uniform)
+{
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), j);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// kWave: called by every lane of a wave with the same (uniform) values; the four divisions run
+// as one, component c on lanes c mod 4, and come back by v_readlane (the same quotients).
+template <bool kWave = false>
 __device__ void pq_normalize(Se3& s)
 {
     if (s.w < 0) { s.w = -s.w; s.x = -s.x; s.y = -s.y; s.z = -s.z; }
     const double n = sqrt(((s.x * s.x + s.y * s.y) + s.z * s.z) + s.w * s.w);
-    s.x = s.x / n; s.y = s.y / n; s.z = s.z / n; s.w = s.w / n;
+    if constexpr (kWave) {
+        const int c = __lane_id() & 3;
+        const double q = (c == 0 ? s.x : c == 1 ? s.y : c == 2 ? s.z : s.w) / n;
+        s.x = rl_d(q, 0); s.y = rl_d(q, 1); s.z = rl_d(q, 2); s.w = rl_d(q, 3);
+    } else {
+        s.x = s.x / n; s.y = s.y / n; s.z = s.z / n; s.w = s.w / n;
+    }
 }
 
 __device__ __forceinline__ void pq_rotate(const Se3& s, const double v[3], double o[3])
@@ -76,6 +93,7 @@ __device__ __forceinline__ void pq_rotate(const Se3& s, const double v[3], doubl
     for (int k = 0; k < 3; k++) o[k] = (v[k] + s.w * uv[k]) + c[k];
 }
 
+template <bool kWave = false>
 __device__ Se3 pq_mul(const Se3& a, const Se3& b)
 {
     Se3 r;
@@ -86,7 +104,7 @@ __device__ Se3 pq_mul(const Se3& a, const Se3& b)
     r.x = ((a.w * b.x + a.x * b.w) + a.y * b.z) - a.z * b.y;
     r.y = ((a.w * b.y + a.y * b.w) + a.z * b.x) - a.x * b.z;
     r.z = ((a.w * b.z + a.z * b.w) + a.x * b.y) - a.y * b.x;
-    pq_normalize(r);
+    pq_normalize<kWave>(r);
     return r;
 }
 
@@ -118,7 +136,8 @@ __device__ void pq_sincos(double x, double& sn, double& cs)
     else { sn = -c0; cs = s0; }
 }
 
-// SE3Quat::exp(update)
+// SE3Quat::exp(update); kWave as pq_normalize (A, B, C as one division on lanes 0..2)
+template <bool kWave = false>
 __device__ Se3 pq_exp(const double u[6])
 {
     const double o0 = u[0], o1 = u[1], o2 = u[2];
@@ -136,7 +155,16 @@ __device__ Se3 pq_exp(const double u[6])
         double sn, cs;
         pq_sincos(theta, sn, cs);
         const double th2 = theta * theta;
-        const double A = sn / theta, B = (1.0 - cs) / th2, Cc = (theta - sn) / (th2 * theta);
+        double A, B, Cc;
+        if constexpr (kWave) {
+            const int c = __lane_id() % 3;
+            const double num = c == 0 ? sn : c == 1 ? (1.0 - cs) : (theta - sn);
+            const double den = c == 0 ? theta : c == 1 ? th2 : (th2 * theta);
+            const double q = num / den;
+            A = rl_d(q, 0); B = rl_d(q, 1); Cc = rl_d(q, 2);
+        } else {
+            A = sn / theta; B = (1.0 - cs) / th2; Cc = (theta - sn) / (th2 * theta);
+        }
         for (int i = 0; i < 9; i++) {
             const double I = i % 4 == 0 ? 1.0 : 0.0;
             R[i] = (I + A * Om[i]) + B * Om2[i];
@@ -146,7 +174,7 @@ __device__ Se3 pq_exp(const double u[6])
     Se3 s;
     pq_from_R(R, s);
     for (int i = 0; i < 3; i++) s.t[i] = (V[i * 3] * u[3] + V[i * 3 + 1] * u[4]) + V[i * 3 + 2] * u[5];
-    pq_normalize(s);
+    pq_normalize<kWave>(s);
     return s;
 }
 
@@ -289,6 +317,60 @@ __device__ bool pq_solve6(const double* hu, double lambda, const double* bv, dou
     return true;
 }
 
+// pq_solve6 with the rows on lanes (all 64 lanes of one wave call it; lane i < 6 holds row i of L,
+// the others compute a copy of row 5 that is never read).  Column j of the LDL^T: lane i forms
+// hu(j, i) - sum_k (L(i,k) L(j,k)) d_k in the oracle's k order (lane j's value is d_j, plus
+// lambda on the diagonal), and ONE division serves every row below j; the forward substitution
+// runs by columns (lane i subtracts L(i,k) y_k for k = 0, 1, .. in order), the y_i / d_i
+// divisions are one, and the back substitution -- whose row order (k increasing) has to be kept --
+// runs on uniform values.  Row j's values reach the other lanes by v_readlane (j is a constant).
+// Same operations on the same operands as pq_solve6, so x is bit-identical; x is uniform.
+__device__ bool pq_solve6_wave(const double* hu, double lambda, const double* bv, double x[6])
+{
+    const int lane = __lane_id();
+    const int i = lane < 6 ? lane : 5;
+    double Lr[6];                          // Lr[k] = L(i, k), k < i (lane i's row)
+    double d[6];                           // uniform pivots
+    double dl = 1.0;                       // lane i's own pivot d_i
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        const int ii = i > j ? i : j;      // lanes above row j recompute row j (unused)
+        double v = hu[pq_hu(j, ii)];
+        if (ii == j) v = v + lambda;
+#pragma unroll
+        for (int k = 0; k < j; k++) v = v - (Lr[k] * rl_d(Lr[k], j)) * d[k];
+        const double dj = rl_d(v, j);
+        if (!(dj > 0.0)) return false;
+        d[j] = dj;
+        if (i == j) dl = v;
+        Lr[j] = v / dj;                    // L(i, j) on lanes i > j
+    }
+    // forward substitution by columns; lane i's y_i is final when column i is reached
+    double yv = bv[i], ymine = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        if (i == k) ymine = yv;
+        const double yk = rl_d(yv, k);
+        if (k < 5 && i > k) yv = yv - Lr[k] * yk;
+    }
+    const double yd = ymine / dl;          // y_i / d_i on lane i
+    double y[6], Lu[6][6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) y[k] = rl_d(yd, k);
+#pragma unroll
+    for (int a = 0; a < 6; a++)
+#pragma unroll
+        for (int k = a + 1; k < 6; k++) Lu[k][a] = rl_d(Lr[a], k);     // L(k, a)
+#pragma unroll
+    for (int a = 5; a >= 0; a--) {
+        double v = y[a];
+#pragma unroll
+        for (int k = a + 1; k < 6; k++) v = v - Lu[k][a] * x[k];
+        x[a] = v;
+    }
+    return true;
+}
+
 // Partials of thread t live at slot t + t / 32 of a 264-double row: in block_reduce lane
 // (k, c) walks run c of value k, and without the skew all 64 lanes of a wave would read the
 // same LDS bank (runs 256 B apart, rows 2 KB apart).  With it, runs are 33 doubles apart and
@@ -296,14 +378,31 @@ __device__ bool pq_solve6(const double* hu, double lambda, const double* bv, dou
 constexpr int kPartRow = 264;
 __device__ __forceinline__ int part_slot(int t) { return t + (t >> 5); }
 
+// Trials per round after the first of an iteration (see k_pose): g2o's inner loop retries a
+// rejected step with lambda *= ni, ni *= 2 from the same saved estimate, so the trials that follow
+// a rejection depend only on that lambda sequence and can be solved and scored together.
+#ifndef COEB_POSE_TB
+#define COEB_POSE_TB 4
+#endif
+constexpr int kTB = COEB_POSE_TB;
+
+struct PoseTrial {
+    Se3 s;                 // exp(x) * saved
+    double x[6], lam;      // step and its lambda
+    int ok;                // the LDLT succeeded
+};
+
 struct PoseLds {
     Se3 s;                 // current estimate (broadcast)
+    Se3 last;              // estimate of the last chi2 evaluation (the classification's errors)
     double part[28][kPartRow];  // per-thread partials, skewed (part_slot)
     double run[28][8];     // 32-lane run sums
     double out[28];        // reduced
     double hb[27];         // this iteration's 21 Hessian + 6 gradient terms (thread 0's system)
+    PoseTrial tr[kTB];     // this round's trials
+    double lam, ni;        // lambda and ni at the round's first trial
     double rho;
-    int qmax, ok, nbad[4], accepted;
+    int qmax, stop, nbad[4], accepted;
 };
 
 // block-wide canonical reduction of nv per-thread partials (uniform call): each run of 32
@@ -336,7 +435,6 @@ template <int EPT>
 struct EdgeSet {
     static constexpr int R = EPT > 0 ? EPT : 1;
     PoseEdgeRec rec[R];
-    double chi[R];
     uint32_t act;
 };
 
@@ -350,8 +448,8 @@ __device__ __forceinline__ PEdge edge_of(const PoseEdgeRec& r)
     return E;
 }
 
-// Runs the body over this thread's edges in increasing e with `rec` (the edge record), `act`
-// (its active flag; the body may change it) and `chi` (a reference to its chi2) in scope.
+// Runs the body over this thread's edges in increasing e with `rec` (the edge record) and `act`
+// (its active flag; the body may change it) in scope.
 #define COEB_FOR_EDGES(ES, ...)                                                                   \
     if constexpr (EPT > 0) {                                                                        \
         _Pragma("unroll") for (int j_ = 0; j_ < EPT; j_++) {                                        \
@@ -359,8 +457,6 @@ __device__ __forceinline__ PEdge edge_of(const PoseEdgeRec& r)
             if (e < ne) {                                                                           \
                 const PoseEdgeRec& rec = ES.rec[j_];                                                \
                 bool act = (ES.act >> j_) & 1u;                                                     \
-                double& chi = ES.chi[j_];                                                           \
-                (void)chi;                                                                          \
                 __VA_ARGS__;                                                                        \
                 ES.act = (ES.act & ~(1u << j_)) | ((act ? 1u : 0u) << j_);                          \
             }                                                                                       \
@@ -369,34 +465,39 @@ __device__ __forceinline__ PEdge edge_of(const PoseEdgeRec& r)
         for (int e = threadIdx.x; e < ne; e += kPT) {                                               \
             const PoseEdgeRec rec = b.edges[(int64_t)f * b.stride + e];                             \
             bool act = b.active[(int64_t)f * b.stride + e] != 0;                                    \
-            double& chi = b.chi2[(int64_t)f * b.stride + e];                                        \
-            (void)chi;                                                                              \
             __VA_ARGS__;                                                                            \
             b.active[(int64_t)f * b.stride + e] = act ? 1 : 0;                                      \
         }                                                                                           \
     }
 
-// computeActiveErrors + activeRobustChi2 at L.s; raw chi2 of active edges -> chi2
+// computeActiveErrors + activeRobustChi2 at each of the T poses (LDS): robust chi2 sums of the
+// active edges -> L.out[0..T).  Each sum runs over the thread's edges in increasing e and is
+// reduced in the canonical order, so pose t's sum is what a pass at that pose alone gives.
 template <int EPT>
-__device__ double active_chi2(PoseLds& L, const PoseBufs& b, const PoseCam& cm, int f, int ne, bool robust,
-                              const double delta[2], EdgeSet<EPT>& ES)
+__device__ void active_chi2(PoseLds& L, const PoseBufs& b, const PoseCam& cm, int f, int ne, bool robust,
+                            const double delta[2], EdgeSet<EPT>& ES, const Se3* poses, int pstride, int T)
 {
-    const Se3 s = L.s;
-    double acc = 0.0;
-    COEB_FOR_EDGES(ES, {
-        if (act) {
-            const PEdge E = edge_of(rec);
-            double er[3];
-            const double c = pq_edge_eval(cm, s, E, er, nullptr);
-            chi = c;
-            double r = c, r1;
-            if (robust) pq_huber(c, delta[E.stereo], r, r1);
-            acc += r;
+    double acc[kTB];
+#pragma unroll
+    for (int t = 0; t < kTB; t++) {
+        acc[t] = 0.0;
+        if (t < T) {
+            const Se3 s = *reinterpret_cast<const Se3*>(reinterpret_cast<const uint8_t*>(poses) + t * pstride);
+            double a = 0.0;
+            COEB_FOR_EDGES(ES, {
+                if (act) {
+                    const PEdge E = edge_of(rec);
+                    double er[3];
+                    const double c = pq_edge_eval(cm, s, E, er, nullptr);
+                    double r = c, r1;
+                    if (robust) pq_huber(c, delta[E.stereo], r, r1);
+                    a += r;
+                }
+            })
+            acc[t] = a;
         }
-    })
-    double v[1] = {acc};
-    block_reduce(L, v, 1);
-    return L.out[0];
+    }
+    block_reduce(L, acc, T);
 }
 
 // phase clocks of thread 0 (diagnostic, COEB_POSE_TIMING): [0] chi2 passes, [1] build passes,
@@ -452,7 +553,6 @@ __global__ __launch_bounds__(kPT, 2) void k_pose(PoseBufs b, PoseCam cm)
         for (int j = 0; j < EPT; j++) {
             const int e = tid + j * kPT;
             if (e < ne) { ES.rec[j] = b.edges[base + e]; ES.act |= 1u << j; }
-            ES.chi[j] = 0.0;
         }
     }
     float* Tcw = b.Tcw + (int64_t)f * 16;
@@ -475,11 +575,14 @@ __global__ __launch_bounds__(kPT, 2) void k_pose(PoseBufs b, PoseCam cm)
         bool fresh = false;        // the last trial was accepted: errors and chi2 are already at L.s
         for (int iter = 0; iter < 10; iter++) {
             // computeActiveErrors + activeRobustChi2 at the current estimate.  After an accepted
-            // trial the estimate is that trial's, so the per-edge chi2 and currentChi (= tempChi,
-            // thread 0) computed for it are exactly what this pass would produce: skip it.
+            // trial the estimate is that trial's, so the chi2 computed for it (= tempChi, thread 0)
+            // is exactly what this pass would produce: skip it.
             PT_INC(5);
             PT_MARK(t_c0);
-            if (!fresh) currentChi = active_chi2<EPT>(L, b, cm, f, ne, robust, delta, ES);
+            if (!fresh) {
+                active_chi2<EPT>(L, b, cm, f, ne, robust, delta, ES, &L.s, 0, 1);
+                currentChi = L.out[0];
+            }
             PT_ADD(0, t_c0);
             PT_MARK(t_b0);
             // buildSystem
@@ -523,70 +626,111 @@ __global__ __launch_bounds__(kPT, 2) void k_pose(PoseBufs b, PoseCam cm)
                 }
                 L.qmax = 0;
             }
-            __syncthreads();
-            Se3 saved;
-            double x[6];
-            int ok2 = 0;
+            // The trial loop (do { ... } while (rho < 0 && qmax < 10)) in rounds of T trials: the
+            // first round of an iteration tries one step; after a rejection, a round solves and
+            // scores the next T steps of the rejection sequence (lambda_t+1 = lambda_t * ni_t,
+            // ni_t+1 = 2 ni_t, all from the same saved estimate) at once -- lane t of wave 0 solves
+            // step t, one chi2 pass scores all T, and thread 0 then walks them in order exactly as
+            // the sequential loop would, stopping where it stops.  Steps past that point were never
+            // taken: their results are dropped.
+            int qmax = 0;                                          // uniform copy of L.qmax
             for (;;) {
-                if (tid == 0) {
-                    saved = L.s;
+                const int T = qmax == 0 ? 1 : min(kTB, 10 - qmax);
+                if (tid == 0) { L.lam = lambda; L.ni = ni; }
+                __syncthreads();
+                if (T == 1 && wv == 0) {
+                    // one trial: its LDL^T solve on the lanes of wave 0, the rest on lane 0
+                    double x[6];
                     for (int j = 0; j < 6; j++) x[j] = 0.0;
-                    ok2 = pq_solve6(L.hb, lambda, L.hb + 21, x) ? 1 : 0;
+                    const int ok2 = pq_solve6_wave(L.hb, L.lam, L.hb + 21, x) ? 1 : 0;
+                    if (!ok2) for (int j = 0; j < 6; j++) x[j] = 0.0;
+                    const Se3 saved = L.s;
+                    const Se3 up = pq_exp<true>(x);
+                    const Se3 ns = pq_mul<true>(up, saved);
+                    if (lane == 0) {
+                        PoseTrial& tr = L.tr[0];
+                        tr.s = ns;
+                        for (int j = 0; j < 6; j++) tr.x[j] = x[j];
+                        tr.lam = L.lam;
+                        tr.ok = ok2;
+                    }
+                } else if (T > 1 && tid < T) {
+                    double lam = L.lam, nu = L.ni;
+                    for (int k = 0; k < tid; k++) { lam = lam * nu; nu = nu * 2.0; }
+                    const Se3 saved = L.s;
+                    double x[6];
+                    for (int j = 0; j < 6; j++) x[j] = 0.0;
+                    const int ok2 = pq_solve6(L.hb, lam, L.hb + 21, x) ? 1 : 0;
                     if (!ok2) for (int j = 0; j < 6; j++) x[j] = 0.0;
                     const Se3 up = pq_exp(x);
-                    L.s = pq_mul(up, saved);
+                    PoseTrial& tr = L.tr[tid];
+                    tr.s = pq_mul(up, saved);
+                    for (int j = 0; j < 6; j++) tr.x[j] = x[j];
+                    tr.lam = lam;
+                    tr.ok = ok2;
                 }
                 __syncthreads();
                 PT_ADD(2, t_s0);
                 PT_INC(6);
                 PT_MARK(t_c1);
-                double tempChi = active_chi2<EPT>(L, b, cm, f, ne, robust, delta, ES);
+                active_chi2<EPT>(L, b, cm, f, ne, robust, delta, ES, &L.tr[0].s, (int)sizeof(PoseTrial), T);
                 PT_ADD(0, t_c1);
                 t_s0 = b.timing ? (long long)clock64() : 0;
                 if (tid == 0) {
-                    if (!ok2) tempChi = DBL_MAX;
-                    double scale = 0.0;
-                    for (int j = 0; j < 6; j++) scale = scale + x[j] * (lambda * x[j] + L.hb[21 + j]);
-                    scale = scale + 1e-3;   // g2o OptimizationAlgorithmLevenberg::solve: "make sure it's non-zero"
-                    const double rho = (currentChi - tempChi) / scale;
-                    if (rho > 0 && isfinite(tempChi)) {
-                        double alpha = 1.0 - pq_cube(2.0 * rho - 1.0);
-                        alpha = fmin(alpha, 2.0 / 3.0);
-                        const double sf = fmax(1.0 / 3.0, alpha);
-                        lambda = lambda * sf;
-                        ni = 2.0;
-                        currentChi = tempChi;
-                        L.accepted = 1;
-                    } else {
-                        lambda = lambda * ni;
-                        ni = ni * 2.0;
-                        L.s = saved;
-                        L.accepted = 0;
+                    int q = L.qmax, stop = 0;
+                    double rho = 0.0;
+                    for (int t = 0; t < T; t++) {
+                        const PoseTrial& tr = L.tr[t];
+                        double tempChi = L.out[t];
+                        if (!tr.ok) tempChi = DBL_MAX;
+                        double scale = 0.0;
+                        for (int j = 0; j < 6; j++) scale = scale + tr.x[j] * (lambda * tr.x[j] + L.hb[21 + j]);
+                        scale = scale + 1e-3;   // g2o OptimizationAlgorithmLevenberg::solve: "make sure it's non-zero"
+                        rho = (currentChi - tempChi) / scale;
+                        L.last = tr.s;          // the errors computeActiveErrors left behind
+                        if (rho > 0 && isfinite(tempChi)) {
+                            double alpha = 1.0 - pq_cube(2.0 * rho - 1.0);
+                            alpha = fmin(alpha, 2.0 / 3.0);
+                            const double sf = fmax(1.0 / 3.0, alpha);
+                            lambda = lambda * sf;
+                            ni = 2.0;
+                            currentChi = tempChi;
+                            L.s = tr.s;
+                            L.accepted = 1;
+                        } else {
+                            lambda = lambda * ni;
+                            ni = ni * 2.0;
+                            L.accepted = 0;
+                        }
+                        q = q + 1;
+                        if (!(rho < 0 && q < 10)) { stop = 1; break; }
                     }
-                    L.qmax = L.qmax + 1;
+                    L.qmax = q;
                     L.rho = rho;
+                    L.stop = stop;
                 }
                 __syncthreads();
-                // no barrier after these reads: thread 0 next writes L.rho / L.qmax / L.accepted
-                // only after barriers every thread reaches after reading them
-                const double rho = L.rho;
-                const int qmax = L.qmax;
-                if (!(rho < 0 && qmax < 10)) break;
+                qmax = L.qmax;
+                const int stop = L.stop;
+                // no barrier after these reads: thread 0 next writes L.qmax / L.stop only after
+                // barriers every thread reaches after reading them
+                if (stop) break;
             }
             const double rho = L.rho;
-            const int qmax = L.qmax;
             PT_ADD(2, t_s0);
             fresh = L.accepted != 0;
             if (qmax == 10 || rho == 0) break;                     // Terminate
         }
-        // ---- classification (Optimizer.cc:381-437) ----
+        // ---- classification (Optimizer.cc:381-437): the chi2 of an active edge is the one its
+        //      last computeActiveErrors left (at L.last, possibly a rejected trial's estimate), an
+        //      inactive edge's is computed at the final estimate (e->computeError()) ----
         PT_MARK(t_k0);
-        const Se3 s = L.s;
+        const Se3 s = L.s, sl = L.last;
         int bad = 0;
         COEB_FOR_EDGES(ES, {
             const PEdge E = edge_of(rec);
-            if (!act) { double er[3]; chi = pq_edge_eval(cm, s, E, er, nullptr); }
-            const double c = chi;
+            double er[3];
+            const double c = pq_edge_eval(cm, act ? sl : s, E, er, nullptr);
             const int kp = rec.kp;
             if (c > chi2th[E.stereo]) { b.outlier[base + kp] = 1; act = false; bad++; }
             else { b.outlier[base + kp] = 0; act = true; }

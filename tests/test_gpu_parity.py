@@ -464,21 +464,37 @@ def test_batch_track_pose_matches_oracle(oracle_mod, ex):
 
 
 def test_batch_B_full_size_properties(oracle_mod):
-    """Config B at full size: 1280x960, 2000 kp, batch of 16 -- properties for every frame,
-    exact oracle parity on two of them."""
+    """Config B at full size: 1280x960, 2000 kp, batch of 16 -- every frame's keypoints,
+    descriptors and SearchByProjection result (with the 2*th retry) equal to the oracle's, plus
+    the size-independent properties."""
     from coeb_front.pipeline import BatchPipeline
     F = 16
-    fr = synth.make_frames(1280, 960, F, seed=99)
-    bp = BatchPipeline(1280, 960, F, nfeatures=2000)
+    W, H = 1280, 960
+    fr = synth.make_frames(W, H, F, seed=99)
+    Tcw = np.stack([synth.motion_pose()] * F)
+    bp = BatchPipeline(W, H, F, nfeatures=2000)
     try:
-        bp.load(fr, Tcw=np.stack([synth.motion_pose()] * F))
+        bp.load(fr, Tcw=Tcw)
         bp.run()
         bp.synchronize()
         out, matches, nms = bp.results()
         ex2 = oracle_mod.Extractor(2000, 1.2, 8, 20, 7)
-        for f in (0, F - 1):
+        depth = synth.make_depth(W, H)
+        cam_o = oracle_mod.camera(ex2, W, H, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+        I4 = np.eye(4, dtype=np.float32)
+        prev = None
+        for f in range(F):
             r = ex2.extract(fr[f])
             assert_same(out[f][0], out[f][1], r["kps"], r["desc"], "B batch f%d" % f)
+            if prev is not None:
+                last = oracle_mod.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX, synth.TUM_FY,
+                                                           synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+                ur, _ = oracle_mod.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
+                nm, m = oracle_mod.search_by_projection(cam_o, r["kps"], r["desc"], ur, last, Tcw[f], I4, 15.0)
+                if nm < 20:                                      # Tracking.cc:954-958
+                    nm, m = oracle_mod.search_by_projection(cam_o, r["kps"], r["desc"], ur, last, Tcw[f], I4, 30.0)
+                assert nms[f] == nm and np.array_equal(matches[f], m), (f, nms[f], nm)
+            prev = r
         for f in range(F):
             k = out[f][0]
             assert 0 < len(k) <= 2000 + 8 * 8

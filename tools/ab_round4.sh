@@ -11,6 +11,7 @@ grep -E "^FAILED|^ERROR" gpurun_out/pt.log | head -20
 # 0 = pass, 1 = test failures (keep measuring); anything else (crash, timeout, abort) ends the call
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
 bash tools/_kab.sh k_blur main COEB_BLUR_ROWS=0 main COEB_BLUR_ROWS=64 COEB_DESC_DMA=0 main COEB_DESC_DMA=4 main COEB_DESC_DMA=8 main || exit $?
+bash tools/_kab.sh k_octree COEB_OCT_SPLIT=3 main COEB_OCT_SPLIT=5 main COEB_OCT_SPLIT=0 main || exit $?
 bash tools/_dab.sh lib/var_tb1.so lib/var_tb2.so main || exit $?
 # octree per-level clocks: config A batch and a config-B 32-frame shard
 export COEB_SIDE_STREAM=0 COEB_LIB_PATH=$PWD/coeb-slam_amd/lib/var_octclk.so
@@ -21,7 +22,7 @@ cat gpurun_out/oct_B32.txt
 unset COEB_LIB_PATH COEB_SIDE_STREAM
 # config B 64-frame shard (the 8-rank share of the 512-frame batch): level-0 octree at 1024 threads
 for v in 0 64; do
-  COEB_OCT_WIDE_F=$v timeout -k 10 200 python bench.py --config B --global-frames 64 --no-cpu-baseline --no-extras --no-e2e > gpurun_out/b64_$v.log 2>&1 || { echo "b64 rc=$?"; tail -3 gpurun_out/b64_$v.log; exit 1; }
+  COEB_OCT_WIDE_F=$v COEB_OCT_SPLIT=0 timeout -k 10 200 python bench.py --config B --global-frames 64 --no-cpu-baseline --no-extras --no-e2e > gpurun_out/b64_$v.log 2>&1 || { echo "b64 rc=$?"; tail -3 gpurun_out/b64_$v.log; exit 1; }
   python - $v <<'PY'
 import json, sys
 d = json.loads([x for x in open("gpurun_out/b64_%s.log" % sys.argv[1]) if x.startswith("{")][-1])
