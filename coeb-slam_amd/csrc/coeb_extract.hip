@@ -805,8 +805,10 @@ constexpr int kFastLists = kFastSurv;      // u16 entries before the corner list
 // entry offsets / 4 fit 12 bits: ROIs are at most 64 rows (coeb_capi.hip kRoiMax)
 static_assert(kFastRowBytesM * 64 <= 4 * 4096 && kFastRowBytes * 64 <= 4 * 4096, "k_fast entry offset field");
 #ifndef COEB_FAST_PK
-#define COEB_FAST_PK 1             // survivors' strengths two per lane (u16 halves); 0: one per lane
-#endif              // pre-test entries (u32: first pixel's offset | survivor mask << 16)
+// 1: survivors' strengths two per lane (u16 halves); 0: one per lane (1.061 vs 1.105 ms per
+// 1025-frame launch, profiles/r04/ab3)
+#define COEB_FAST_PK 0
+#endif
 
 __device__ __forceinline__ void wave_sync_lds()
 {
@@ -1284,7 +1286,10 @@ __device__ __forceinline__ CellDesc load_cell(const CellDesc* __restrict__ cells
 // the second cell's ROI loads issued before the first is processed spilled 240 B per lane and
 // ran 2.7x slower.)
 template <int RB>
-__global__ __launch_bounds__(kThreads, 6) void k_fast(const Plan* __restrict__ P, ExtractBufs b,
+#ifndef COEB_FAST_MINWG
+#define COEB_FAST_MINWG 6      // launch bound: workgroups per CU the register budget must allow
+#endif
+__global__ __launch_bounds__(kThreads, COEB_FAST_MINWG) void k_fast(const Plan* __restrict__ P, ExtractBufs b,
                                                        const CellDesc* __restrict__ cells,   // read-only: scalar loads
                                                        int cell0, int cell1)                 // this launch's cells
 {
@@ -1421,11 +1426,12 @@ __device__ __forceinline__ int4 wave_count_quadrants(const uint32_t* src, int s,
     return make_int4(c0, c1, c2, c3);
 }
 
-// Stable scatter of node range [s, s+n) from src into dst at [s, s+n), quadrant order.
-__device__ __forceinline__ void wave_scatter_quadrants(const uint32_t* src, uint32_t* dst, int s, int n,
-                                                       int sx, int sy, int4 c)
+// Stable scatter of keys [s, s+n) of src into dst, quadrant q's keys from position r.q on
+// (one wave).
+__device__ __forceinline__ void wave_scatter_quadrants_at(const uint32_t* src, uint32_t* dst, int s, int n,
+                                                          int sx, int sy, int4 r)
 {
-    int r0 = s, r1 = s + c.x, r2 = s + c.x + c.y, r3 = s + c.x + c.y + c.z;
+    int r0 = r.x, r1 = r.y, r2 = r.z, r3 = r.w;
     const int lane = lane_id();
     const uint64_t lt = lanemask_lt();
     for (int base = 0; base < n; base += 64) {
@@ -1441,6 +1447,14 @@ __device__ __forceinline__ void wave_scatter_quadrants(const uint32_t* src, uint
         }
         r0 += __popcll(m0); r1 += __popcll(m1); r2 += __popcll(m2); r3 += __popcll(m3);
     }
+}
+
+// Stable scatter of node range [s, s+n) from src into dst at [s, s+n), quadrant order.
+__device__ __forceinline__ void wave_scatter_quadrants(const uint32_t* src, uint32_t* dst, int s, int n,
+                                                       int sx, int sy, int4 c)
+{
+    wave_scatter_quadrants_at(src, dst, s, n, sx, sy,
+                              make_int4(s, s + c.x, s + c.x + c.y, s + c.x + c.y + c.z));
 }
 
 // The same two steps for one node by one lane (the final phase and the late passes divide
@@ -1465,6 +1479,64 @@ __device__ __forceinline__ void lane_scatter_quadrants(const uint32_t* src, uint
         const int r = q == 0 ? r0++ : q == 1 ? r1++ : q == 2 ? r2++ : r3++;
         dst[r] = k;
     }
+}
+
+// The same two steps by a team of G lanes of one wave (G = 4 or 16): the team's lanes stay
+// converged (same node, same trip count), so the per-lane counts are summed over the team with
+// xor shuffles and the scatter ranks come from the wave's ballots masked to the team's lanes.
+template <int G>
+__device__ __forceinline__ int4 team_count_quadrants(const uint32_t* src, int s, int n, int sx, int sy)
+{
+    int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    for (int i = lane_id() & (G - 1); i < n; i += G) {
+        const int q = quadrant(src[s + i], sx, sy);
+        c0 += q == 0; c1 += q == 1; c2 += q == 2; c3 += q == 3;
+    }
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) {
+        c0 += __shfl_xor(c0, o, 64); c1 += __shfl_xor(c1, o, 64);
+        c2 += __shfl_xor(c2, o, 64); c3 += __shfl_xor(c3, o, 64);
+    }
+    return make_int4(c0, c1, c2, c3);
+}
+
+template <int G>
+__device__ __forceinline__ void team_scatter_quadrants(const uint32_t* src, uint32_t* dst, int s, int n, int sx,
+                                                       int sy, int4 c)
+{
+    int r0 = s, r1 = s + c.x, r2 = s + c.x + c.y, r3 = s + c.x + c.y + c.z;
+    const int lane = lane_id(), gl = lane & (G - 1);
+    const uint64_t tm = ((1ull << G) - 1ull) << (lane & ~(G - 1));   // this team's lanes
+    for (int base = 0; base < n; base += G) {
+        const int i = base + gl;
+        const bool v = i < n;
+        const uint32_t k = v ? src[s + i] : 0u;
+        const int q = v ? quadrant(k, sx, sy) : -1;
+        const uint64_t m0 = __ballot(q == 0) & tm, m1 = __ballot(q == 1) & tm;
+        const uint64_t m2 = __ballot(q == 2) & tm, m3 = __ballot(q == 3) & tm;
+        if (v) {
+            const uint64_t mq = q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
+            const int rq = q == 0 ? r0 : q == 1 ? r1 : q == 2 ? r2 : r3;
+            dst[rq + mbcnt(mq)] = k;
+        }
+        r0 += __popcll(m0); r1 += __popcll(m1); r2 += __popcll(m2); r3 += __popcll(m3);
+    }
+}
+
+// Lanes per node for dividing nd nodes of about `avg` keys with NT threads: the team size
+// (1, 4, 16 or 64) with the fewest sequential key loads per lane, ceil(nd G / NT) ceil(avg / G)
+// (the key loads are latency-bound, L2 when the keys are global); ties go to the larger team.
+template <int NT>
+__device__ __forceinline__ int oct_team(int nd, int avg)
+{
+    int best = 64, bc = 0x7fffffff;
+#pragma unroll
+    for (int gi = 0; gi < 4; gi++) {
+        const int G = 64 >> (2 * gi);
+        const int c = ((nd * G + NT - 1) / NT) * ((avg + G - 1) / G);
+        if (c < bc) { bc = c; best = G; }
+    }
+    return best;
 }
 
 __device__ __forceinline__ void child_rect(const int4 p, int q, int4* out, int* sx, int* sy)
@@ -1495,6 +1567,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
     constexpr int NW = NT / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int sbuf[(NW + 2 + 3) & ~3];   // 16-byte multiple: keeps the dynamic LDS base aligned
+    __shared__ int4 s_wq[NW];                 // per-wave quadrant counts of a node divided by all waves
     const OctLds O = oct_lds(smem, oct_w, oct_kl);
     int* const s_work = O.work;      // slot ids of nodes divided this phase (processing order)
     int4* const s_cnt = O.cnt;       // their quadrant counts
@@ -1526,6 +1599,9 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
     // keys in LDS when they fit, else in the level's global ping-pong buffers (L2-resident)
     uint32_t* KB0;
     int64_t kdelta;
+    // global keys: barriers also wait for the key stores (an LDS-only fence leaves them in flight)
+    const bool kglob = K > oct_kl;
+    auto obar = [&]() { if (kglob) __syncthreads(); else lds_barrier(); };
     if (K <= oct_kl) {
         KB0 = O.keys[0];
         kdelta = O.keys[1] - O.keys[0];
@@ -1548,7 +1624,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
             carry += tot;
         }
         K = carry;
-        lds_barrier();
+        obar();
         for (int i = tid; i < K; i += NT) {
             int lo = 0, hi = g.ncells - 1;            // last cell with offset <= i
             while (lo < hi) {
@@ -1573,7 +1649,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
         }
         K = carry;
     }
-    lds_barrier();
+    obar();
     int kb = 0;   // buffer currently holding the candidates
     // ---- pre-octree cull (ORBextractor.cc:854-858; coordinates still relative, reference quirk)
     if (area) {
@@ -1594,7 +1670,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
         }
         K = carry;
         kb = 1;
-        lds_barrier();
+        obar();
     }
 
     // ---- 2. initial nodes (:549-592) ----
@@ -1638,7 +1714,41 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
             }
         }
     }
-    lds_barrier();
+    obar();
+
+    // Quadrant work on the nodes s_work[j] of set S with teams of G lanes (oct_team): mode 0
+    // counts (-> s_cnt[j]) and divides (keys KB(buf) -> KB(buf ^ 1)) nodes j < cnt; mode 1 only
+    // counts; mode 2 divides the nodes j = s_base[r], r < cnt, with the counts already in s_cnt.
+    auto divide_nodes = [&](int G, const NodeRef& S, int cnt, int mode) {
+        auto team = [&](auto gc) {
+            constexpr int TG = decltype(gc)::value;
+            for (int r = tid / TG; r < cnt; r += NT / TG) {
+                const int j = mode == 2 ? s_base[r] : r;
+                const int k = s_work[j];
+                const int s = S.start[k], c = S.cnt[k], bf = S.buf[k];
+                int4 tmp; int sx, sy;
+                child_rect(S.rect[k], 0, &tmp, &sx, &sy);
+                int4 qc;
+                if (mode == 2) {
+                    qc = s_cnt[j];
+                } else {
+                    if constexpr (TG == 64) qc = wave_count_quadrants(KB(bf), s, c, sx, sy);
+                    else if constexpr (TG == 1) qc = lane_count_quadrants(KB(bf), s, c, sx, sy);
+                    else qc = team_count_quadrants<TG>(KB(bf), s, c, sx, sy);
+                }
+                if (mode != 1) {
+                    if constexpr (TG == 64) wave_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
+                    else if constexpr (TG == 1) lane_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
+                    else team_scatter_quadrants<TG>(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
+                }
+                if (mode != 2 && (lane & (TG - 1)) == 0) s_cnt[j] = qc;
+            }
+        };
+        if (G == 64) team(std::integral_constant<int, 64>());
+        else if (G == 16) team(std::integral_constant<int, 16>());
+        else if (G == 4) team(std::integral_constant<int, 4>());
+        else team(std::integral_constant<int, 1>());
+    };
 
     if (COEB_OCT_CLOCK) oc_t1 = (long long)clock64();
     // ---- 3. main loop (:601-745) ----
@@ -1658,32 +1768,40 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
             if (dv) s_work[nd + pre] = k;
             nd += tot;
         }
-        lds_barrier();
+        obar();
         // partition: one wave per divided node while the nodes are few and large, one lane per
         // node once there are many (then each holds a few keys)
-        if (nd < 2 * NW) {
-            for (int j = wv; j < nd; j += NW) {
-                const int k = s_work[j];
-                const int s = S.start[k], c = S.cnt[k], bf = S.buf[k];
-                const int4 r = S.rect[k];
-                int4 tmp; int sx, sy;
-                child_rect(r, 0, &tmp, &sx, &sy);
-                const int4 qc = wave_count_quadrants(KB(bf), s, c, sx, sy);
-                wave_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
-                if (lane == 0) s_cnt[j] = qc;
-            }
-        } else {
-            for (int j = tid; j < nd; j += NT) {
+        if (nd < NW) {
+            // fewer nodes than waves: every wave on each node in turn, wave w on the w-th
+            // 64-aligned slice, slices placed by a prefix of the per-wave counts
+            for (int j = 0; j < nd; j++) {
                 const int k = s_work[j];
                 const int s = S.start[k], c = S.cnt[k], bf = S.buf[k];
                 int4 tmp; int sx, sy;
                 child_rect(S.rect[k], 0, &tmp, &sx, &sy);
-                const int4 qc = lane_count_quadrants(KB(bf), s, c, sx, sy);
-                lane_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
-                s_cnt[j] = qc;
+                const int chunk = ((c + NW - 1) / NW + 63) & ~63;
+                const int ws = min(c, wv * chunk), wn = min(c - ws, chunk);
+                const int4 qw = wave_count_quadrants(KB(bf), s + ws, wn, sx, sy);
+                if (lane == 0) s_wq[wv] = qw;
+                obar();
+                int4 tot = make_int4(0, 0, 0, 0), pre = tot;
+                for (int w = 0; w < NW; w++) {
+                    const int4 t = s_wq[w];
+                    tot.x += t.x; tot.y += t.y; tot.z += t.z; tot.w += t.w;
+                    if (w < wv) { pre.x += t.x; pre.y += t.y; pre.z += t.z; pre.w += t.w; }
+                }
+                const int4 r = make_int4(s + pre.x, s + tot.x + pre.y, s + tot.x + tot.y + pre.z,
+                                         s + tot.x + tot.y + tot.z + pre.w);
+                wave_scatter_quadrants_at(KB(bf), KB(bf ^ 1), s + ws, wn, sx, sy, r);
+                if (tid == 0) s_cnt[j] = tot;
+                obar();   // s_wq is rewritten for the next node
             }
+        } else {
+            // divided nodes hold every key but the single-key nodes'
+            const int G = oct_team<NT>(nd, (K - (n - nd) + nd - 1) / nd);
+            divide_nodes(G, S, nd, 0);
         }
-        lds_barrier();
+        obar();
         // children alloc order = divided nodes in list order, n1..n4 nonempty
         int T = 0, nexp = 0;
         for (int base = 0; base < nd; base += NT) {
@@ -1701,7 +1819,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
             T += tot;
             nexp += tot2;
         }
-        lds_barrier();
+        obar();
         const int nnew = T + (n - nd);
         if (nnew > g.ncap) { if (tid == 0) atomicOr(b.err, 4); finish = true; break; }
         // write children (reverse push order at the front)
@@ -1741,7 +1859,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
                 carry += tot;
             }
         }
-        lds_barrier();
+        obar();
         alloc_ctr += T;
         n = nnew;
         cs ^= 1;
@@ -1765,14 +1883,10 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
             m += tot;
         }
         for (int k = tid; k < n; k += NT) s_dead[k] = 0;
-        lds_barrier();
-        // quadrant counts of every vPrev node (one lane per node)
-        for (int j = tid; j < m; j += NT) {
-            const int k = s_work[j];
-            int4 tmp; int sx, sy;
-            child_rect(S.rect[k], 0, &tmp, &sx, &sy);
-            s_cnt[j] = lane_count_quadrants(KB(S.buf[k]), S.start[k], S.cnt[k], sx, sy);
-        }
+        obar();
+        // quadrant counts of every vPrev node (vPrev holds every key but the single-key nodes')
+        const int avg = m > 0 ? (K - (n - m) + m - 1) / m : 0;
+        if (m > 0) divide_nodes(oct_team<NT>(m, avg), S, m, 1);
         // sort(vPrev) by (size, node) ascending and walk from the back: rank 0 = largest size,
         // ties -> later allocation first (pointer order of a monotonic allocator)
         // (cnt, alloc) packed as cnt << 16 | alloc (alloc < 2^16, cnt < 2^15) in s_push,
@@ -1781,7 +1895,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
             const int k = s_work[j];
             s_push[j] = (int)(((uint32_t)S.cnt[k] << 16) | (uint32_t)S.alloc[k]);   // used when K < 2^15
         }
-        lds_barrier();
+        obar();
         if (K < 32768 && alloc_ctr < 65536) {
             for (int j = tid; j < m; j += NT) {
                 const int kj = s_push[j];
@@ -1803,9 +1917,9 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
                 s_rank[j] = rank;
             }
         }
-        lds_barrier();
+        obar();
         for (int j = tid; j < m; j += NT) s_base[s_rank[j]] = j;
-        lds_barrier();
+        obar();
         // list size after processing rank r is n + sum_{r'<=r}(e-1); the first r reaching N breaks
         int nproc = m;
         {
@@ -1825,10 +1939,10 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
             int fr = found;
             for (int o = 32; o > 0; o >>= 1) fr = min(fr, __shfl_xor(fr, o, 64));
             if (lane == 0) sbuf[wv] = fr;
-            lds_barrier();
+            obar();
             int mn = 0x7fffffff;
             for (int i = 0; i < NW; i++) mn = min(mn, sbuf[i]);
-            lds_barrier();
+            obar();
             if (mn != 0x7fffffff) nproc = mn + 1;
         }
         // push order = processing order, children n1..n4 nonempty
@@ -1847,19 +1961,18 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
         }
         for (int j = tid; j < m; j += NT)
             if (s_rank[j] < nproc) s_dead[s_work[j]] = 1;
-        lds_barrier();
+        obar();
         const int nnew = T + n - nproc;
         if (nnew > g.ncap) { if (tid == 0) atomicOr(b.err, 4); break; }
-        // DivideNode of the processed nodes + push_front of their children (one lane per node)
+        // DivideNode of the processed nodes (the largest: teams sized for the mean vPrev node
+        // at least), then push_front of their children (one lane per node)
+        divide_nodes(oct_team<NT>(nproc, avg), S, nproc, 2);
         for (int r = tid; r < nproc; r += NT) {
             const int j = s_base[r];
             const int k = s_work[j];
-            const int s = S.start[k], c = S.cnt[k], bf = S.buf[k];
+            const int s = S.start[k], bf = S.buf[k];
             const int4 pr = S.rect[k];
-            int4 tmp; int sx, sy;
-            child_rect(pr, 0, &tmp, &sx, &sy);
             const int4 qc = s_cnt[j];
-            lane_scatter_quadrants(KB(bf), KB(bf ^ 1), s, c, sx, sy, qc);
             {
                 int a = s_push[r];
                 int off = s;
@@ -1893,7 +2006,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, Extra
                 carry += tot;
             }
         }
-        lds_barrier();
+        obar();
         alloc_ctr += T;
         n = nnew;
         cs ^= 1;
