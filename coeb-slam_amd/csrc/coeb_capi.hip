@@ -1287,8 +1287,9 @@ int match_batch_impl(coeb_ctx* c, const float* d_depth, int F, int W, int H, con
     int rc;
     float *ur, *dep, *xw, *dI;
     uint8_t *has, *outl;
-    int32_t *nobsb, *match, *nm, *scr, *derr;
-    if ((rc = ensure(c, "b_ur", (size_t)F * K, &ur)) || (rc = ensure(c, "b_dep", (size_t)F * K, &dep)) ||
+    int32_t *nobsb, *match, *nm, *scr, *mqn, *derr;
+    const int qs = K + 8;                                   // split-list counts + 8 flags per pair
+    if ((rc = ensure(c, "b_mqn", (size_t)F * qs, &mqn)) || (rc = ensure(c, "b_ur", (size_t)F * K, &ur)) || (rc = ensure(c, "b_dep", (size_t)F * K, &dep)) ||
         (rc = ensure(c, "b_xw", (size_t)F * K * 3, &xw)) || (rc = ensure(c, "b_has", (size_t)F * K, &has)) ||
         (rc = ensure(c, "b_outl", (size_t)F * K, &outl)) || (rc = ensure(c, "b_nobs", (size_t)F * K, &nobsb)) ||
         (rc = ensure(c, "b_match", (size_t)F * K, &match)) || (rc = ensure(c, "b_nm", (size_t)F, &nm)) ||
@@ -1342,6 +1343,7 @@ int match_batch_impl(coeb_ctx* c, const float* d_depth, int F, int W, int H, con
             mb.Tcw_cur = dT_cur + 16 * p0; mb.Tcw_last = dI + 16 * p0;
             mb.match = match + q + K; mb.nmatch = nm + p0 + 1; mb.scratch = scr + q * kMatchCQ;
             mb.scratch_stride = K * kMatchCQ; mb.err = derr;
+            mb.qn = mqn + (int64_t)p0 * qs; mb.qn_stride = qs;
             if (getenv("COEB_MATCH_TIMING")) {
                 long long* tmb;
                 if ((rc = ensure(c, "m_timing", (size_t)F * 16, &tmb))) return rc;

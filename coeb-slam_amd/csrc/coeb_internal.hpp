@@ -184,6 +184,8 @@ struct MatchBufs {
     int* nmatch;               // [P]
     int* scratch;              // [P][scratch_stride]
     int scratch_stride;
+    int* qn;                   // optional [P][qn_stride >= last_stride + 8]: split-list counts + flags
+    int qn_stride;
     long long* timing;         // optional [P][16] phase clocks (COEB_MATCH_TIMING), else nullptr
     int* err;
 };

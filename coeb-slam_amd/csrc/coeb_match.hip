@@ -545,52 +545,33 @@ __device__ int assign_rotation(const MatchLds& L, int n, int nq, const Kp* cur, 
     return s_flag[2] - s_flag[3];
 }
 
-template <bool kLds, int NT>
-__global__ __launch_bounds__(NT, 4) void k_match(MatchCam cam, MatchBufs b, float th0, int bmono, int check_ori,
-                                                     int retry_below, int force_seq)
+// Pair p's view of a batch launch: the current / last frame arrays and the pose algebra of
+// SearchByProjection (ORBmatcher.cc:1339-1350): twc = -Rcw^T tcw (double accumulation), tlc.
+struct PairView {
+    const Kp* cur; const uint8_t* cdesc; const float* cur_ur;
+    const Kp* last; const uint8_t* ldesc; const uint8_t* lhas; const uint8_t* lout; const float* lxw;
+    const int* lnobs; uint32_t* lists; const float* T;
+    int n, nl;
+    bool fwd, bwd;
+};
+
+__device__ __forceinline__ PairView pair_view(const MatchCam& cam, const MatchBufs& b, int p, int bmono)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ int s_hist[HISTO_LENGTH];
-    __shared__ int s_flag[8];
-    const int p = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int n = b.cur_n[p];
-    const int nl = b.last_n[p];
-    size_t off[7];
-    match_lds_bytes(b.cur_stride, b.last_stride, kLds, off);
-    MatchLds L;
-    L.cell = reinterpret_cast<int*>(smem + off[0]);
-    L.sort = reinterpret_cast<uint32_t*>(smem + off[1]);
-    L.owner = reinterpret_cast<int*>(smem + off[2]);
-    L.res = reinterpret_cast<int*>(smem + off[3]);
-    L.qn = reinterpret_cast<int*>(smem + off[4]);
-    L.kp = reinterpret_cast<float4*>(smem + off[5]);
-    L.desc = reinterpret_cast<uint32_t*>(smem + off[6]);
-    const Kp* cur = reinterpret_cast<const Kp*>(b.cur_kps) + (int64_t)p * b.cur_stride;
-    const uint8_t* cdesc = b.cur_desc + (int64_t)p * b.cur_stride * 32;
-    const float* cur_ur = b.cur_ur + (int64_t)p * b.cur_stride;
-    const Kp* last = reinterpret_cast<const Kp*>(b.last_kps) + (int64_t)p * b.last_stride;
-    const uint8_t* ldesc = b.last_desc + (int64_t)p * b.last_stride * 32;
-    const uint8_t* lhas = b.last_has + (int64_t)p * b.last_stride;
-    const uint8_t* lout = b.last_out + (int64_t)p * b.last_stride;
-    const float* lxw = b.last_xw + (int64_t)p * b.last_stride * 3;
-    const int* lnobs = b.last_nobs + (int64_t)p * b.last_stride;
-    uint32_t* lists = reinterpret_cast<uint32_t*>(b.scratch) + (int64_t)p * b.scratch_stride;
-    if (n > b.cur_stride || nl > b.last_stride || n >= (1 << kIdxBits)) {
-        if (tid == 0) { atomicOr(b.err, 16); b.nmatch[p] = 0; }
-        return;
-    }
-    CurView<kLds> cv;
-    cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = cur_ur; cv.gdesc = cdesc;
-
-    // ---- phase 0: stage CurrentFrame, grid CSR by a stable counting sort ----
-    long long* tm = b.timing ? b.timing + (int64_t)p * 16 : nullptr;   // phase clocks (COEB_MATCH_TIMING)
-    if (tm && tid == 0) { tm[0] = clock64(); tm[13] = 0; tm[14] = 0x7fffffffffffffffll; tm[15] = 0; }
-    stage_grid<kLds, NT>(cam, cur, cur_ur, cdesc, n, L);
-    if (tm && tid == 0) tm[1] = clock64();
-
-    // pose algebra (ORBmatcher.cc:1339-1350): twc = -Rcw^T tcw (double accumulation), tlc
-    const float* T = b.Tcw_cur + (int64_t)p * 16;
+    PairView v;
+    v.n = b.cur_n[p];
+    v.nl = b.last_n[p];
+    v.cur = reinterpret_cast<const Kp*>(b.cur_kps) + (int64_t)p * b.cur_stride;
+    v.cdesc = b.cur_desc + (int64_t)p * b.cur_stride * 32;
+    v.cur_ur = b.cur_ur + (int64_t)p * b.cur_stride;
+    v.last = reinterpret_cast<const Kp*>(b.last_kps) + (int64_t)p * b.last_stride;
+    v.ldesc = b.last_desc + (int64_t)p * b.last_stride * 32;
+    v.lhas = b.last_has + (int64_t)p * b.last_stride;
+    v.lout = b.last_out + (int64_t)p * b.last_stride;
+    v.lxw = b.last_xw + (int64_t)p * b.last_stride * 3;
+    v.lnobs = b.last_nobs + (int64_t)p * b.last_stride;
+    v.lists = reinterpret_cast<uint32_t*>(b.scratch) + (int64_t)p * b.scratch_stride;
+    v.T = b.Tcw_cur + (int64_t)p * 16;
+    const float* T = v.T;
     const float* Tl = b.Tcw_last + (int64_t)p * 16;
     float twc[3], tlc[3];
     for (int k = 0; k < 3; k++) {
@@ -603,102 +584,233 @@ __global__ __launch_bounds__(NT, 4) void k_match(MatchCam cam, MatchBufs b, floa
         t = t + Tl[k * 4 + 2] * twc[2];
         tlc[k] = (float)((double)t + (double)Tl[k * 4 + 3]);
     }
-    const bool fwd = tlc[2] > cam.mb && !bmono;
-    const bool bwd = -tlc[2] > cam.mb && !bmono;
+    v.fwd = tlc[2] > cam.mb && !bmono;
+    v.bwd = -tlc[2] > cam.mb && !bmono;
+    return v;
+}
+
+__device__ __forceinline__ bool pair_bad(const MatchBufs& b, const PairView& v)
+{
+    return v.n > b.cur_stride || v.nl > b.last_stride || v.n >= (1 << kIdxBits);
+}
+
+// Phase 1 of k_match for the queries q0 + grp, q0 = qbeg, qbeg + qstep, ...: candidate lists
+// (static filters) -> v.lists, counts -> qn_out[q] (-1: none; 0x10000 set when q blocks later
+// queries); s_flag[0] = 1 when a list overflows kCQ.  The caller zeroes s_flag[0] and syncs after.
+template <bool kLds, int NT>
+__device__ void build_lists(const MatchCam& cam, const PairView& v, const MatchLds& L, const CurView<kLds>& cv,
+                            float th, int qbeg, int qstep, int* qn_out, int* s_flag, long long* tm)
+{
+    const int tid = threadIdx.x;
+    const int nl = v.nl;
+    const Kp* last = v.last;
+    const uint8_t* ldesc = v.ldesc;
+    const uint8_t* lhas = v.lhas;
+    const uint8_t* lout = v.lout;
+    const float* lxw = v.lxw;
+    const int* lnobs = v.lnobs;
+    uint32_t* lists = v.lists;
+    const float* T = v.T;
+    const bool fwd = v.fwd, bwd = v.bwd;
+    // one kQL-lane group per query; lanes take the candidates of a grid column range kQL at a
+    // time and ballot-compact them, so each list stays in enumeration order
+    {
+        const int grp = tid / kQL, gl = tid % kQL, gsh = (tid & 63) & ~(kQL - 1);
+        // a query's inputs (flags, world point, octave, descriptor) are loaded one pass ahead
+        struct QIn { int act, oct; float X[3]; uint4 d0, d1; };
+        auto load_qin = [&](int q, QIn& r) {
+            r.act = 0;
+            if (q < nl) {
+                r.act = lhas[q] && !lout[q];
+                r.oct = last[q].octave;
+                r.X[0] = lxw[3 * q]; r.X[1] = lxw[3 * q + 1]; r.X[2] = lxw[3 * q + 2];
+                const uint4* d = reinterpret_cast<const uint4*>(ldesc + 32 * q);
+                r.d0 = d[0]; r.d1 = d[1];
+            }
+        };
+        QIn nx;
+        load_qin(qbeg + grp, nx);
+        const long long tw0 = tm ? clock64() : 0;
+        for (int q0 = qbeg; q0 < nl; q0 += qstep) {
+            const int q = q0 + grp;
+            const QIn qi = nx;
+            load_qin(q + qstep, nx);
+            int cnt = -1;
+            QueryWin w;
+            w.ok = false;
+            if (qi.act) w = query_window(cam, T, qi.X, qi.oct, th, fwd, bwd);
+            if (w.ok) {
+                uint32_t qd[8];
+                qd[0] = qi.d0.x; qd[1] = qi.d0.y; qd[2] = qi.d0.z; qd[3] = qi.d0.w;
+                qd[4] = qi.d1.x; qd[5] = qi.d1.y; qd[6] = qi.d1.z; qd[7] = qi.d1.w;
+                cnt = 0;
+                uint32_t* lst = lists + (int64_t)q * kCQ;
+                // the window's columns kQL at a time: lane gl holds column gx + gl's CSR range, a
+                // group scan gives each column's offset in the concatenated (column-major) order,
+                // and the group walks that concatenation kQL candidates at a time -- one pass per
+                // column group instead of one per column, same enumeration order
+                for (int gx = w.x0; gx <= w.x1; gx += kQL) {
+                    int clo = 0, clen = 0;
+                    if (gx + gl <= w.x1) {
+                        clo = L.cell[(gx + gl) * COEB_GRID_ROWS + w.y0];
+                        clen = L.cell[(gx + gl) * COEB_GRID_ROWS + w.y1 + 1] - clo;
+                    }
+                    const GroupCols gc = group_cols(clo, clen, gl);
+                    for (int base = 0; base < gc.total; base += kQL) {
+                        const int fi = base + gl;
+                        const int e = gc.index(fi);
+                        const int c1 = fi < gc.total ? e + 1 : e;      // e < c1 <=> fi < total
+                        bool ok = false;
+                        uint32_t ent = 0;
+                        if (e < c1) {
+                            const int i2 = (int)(L.sort[e] & ((1u << kIdxBits) - 1));
+                            float x, y, ur;
+                            int oct;
+                            cv.get(e, i2, x, y, ur, oct);
+                            ok = true;
+                            if (w.chk) {
+                                if (oct < w.minL) ok = false;
+                                if (w.maxL >= 0 && oct > w.maxL) ok = false;
+                            }
+                            const float distx = x - w.u, disty = y - w.v;
+                            if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) ok = false;
+                            if (ur > 0 && fabsf(w.ur_q - ur) > w.radius) ok = false;
+                            if (ok) {
+                                const int dist = cv.dist(e, i2, qd);
+                                ok = dist <= TH_HIGH;
+                                ent = ((uint32_t)dist << kIdxBits) | (uint32_t)i2;
+                            }
+                        }
+                        const uint32_t gb = (uint32_t)(__ballot(ok) >> gsh) & ((1u << kQL) - 1u);
+                        if (ok) {
+                            const int pos = cnt + __popc(gb & ((1u << gl) - 1u));
+                            if (pos < kCQ) lst[pos] = ent;
+                        }
+                        cnt += __popc(gb);
+                    }
+                }
+                if (cnt > kCQ) s_flag[0] = 1;      // overflow -> sequential path
+            }
+            if (q < nl && gl == 0) qn_out[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | (lnobs[q] > 0 ? 0x10000 : 0));
+            if (tm && tid == 0) tm[15] += 1;
+        }
+        if (tm && (tid & 63) == 0) {           // per-wave loop time: slowest / fastest wave
+            const long long dt = clock64() - tw0;
+            atomicMax((unsigned long long*)&tm[13], (unsigned long long)dt);
+            atomicMin((unsigned long long*)&tm[14], (unsigned long long)dt);
+        }
+    }
+}
+
+// Split form of phase 1 for small batches (few pairs: one workgroup per pair leaves most CUs
+// idle): workgroup (p, s) stages pair p's grid and builds the lists of every S-th query group
+// (s, s + S, ...), writing the counts to b.qn (pair p's row; entry last_stride + s = s's
+// overflow flag).  k_match then starts at phase 2 with those lists (its own phases 0-1 run only
+// for the sequential fallback or the retry).
+constexpr int kMaxSplit = 8;
+
+template <bool kLds, int NT>
+__global__ __launch_bounds__(NT) void k_match_lists(MatchCam cam, MatchBufs b, float th0, int bmono)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int s_flag[8];
+    const int p = blockIdx.x, sl = blockIdx.y, S = gridDim.y;
+    const PairView v = pair_view(cam, b, p, bmono);
+    int* qn = b.qn + (int64_t)p * b.qn_stride;
+    if (pair_bad(b, v)) {
+        if (threadIdx.x == 0) qn[b.last_stride + sl] = 1;        // k_match reports the error
+        return;
+    }
+    size_t off[7];
+    match_lds_bytes(b.cur_stride, 0, kLds, off);
+    MatchLds L;
+    L.cell = reinterpret_cast<int*>(smem + off[0]);
+    L.sort = reinterpret_cast<uint32_t*>(smem + off[1]);
+    L.owner = reinterpret_cast<int*>(smem + off[2]);
+    L.res = nullptr;
+    L.qn = nullptr;
+    L.kp = reinterpret_cast<float4*>(smem + off[5]);
+    L.desc = reinterpret_cast<uint32_t*>(smem + off[6]);
+    CurView<kLds> cv;
+    cv.kp = L.kp; cv.desc = L.desc; cv.gkp = v.cur; cv.gur = v.cur_ur; cv.gdesc = v.cdesc;
+    stage_grid<kLds, NT>(cam, v.cur, v.cur_ur, v.cdesc, v.n, L);
+    if (threadIdx.x == 0) s_flag[0] = 0;
+    __syncthreads();
+    build_lists<kLds, NT>(cam, v, L, cv, th0, sl * (NT / kQL), S * (NT / kQL), qn, s_flag, nullptr);
+    __syncthreads();
+    if (threadIdx.x == 0) qn[b.last_stride + sl] = s_flag[0];
+}
+
+template <bool kLds, int NT>
+__global__ __launch_bounds__(NT, 4) void k_match(MatchCam cam, MatchBufs b, float th0, int bmono, int check_ori,
+                                                     int retry_below, int force_seq, int nsplit)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int s_hist[HISTO_LENGTH];
+    __shared__ int s_flag[8];
+    const int p = blockIdx.x;
+    const int tid = threadIdx.x;
+    const PairView v = pair_view(cam, b, p, bmono);
+    const int n = v.n, nl = v.nl;
+    size_t off[7];
+    match_lds_bytes(b.cur_stride, b.last_stride, kLds, off);
+    MatchLds L;
+    L.cell = reinterpret_cast<int*>(smem + off[0]);
+    L.sort = reinterpret_cast<uint32_t*>(smem + off[1]);
+    L.owner = reinterpret_cast<int*>(smem + off[2]);
+    L.res = reinterpret_cast<int*>(smem + off[3]);
+    L.qn = reinterpret_cast<int*>(smem + off[4]);
+    L.kp = reinterpret_cast<float4*>(smem + off[5]);
+    L.desc = reinterpret_cast<uint32_t*>(smem + off[6]);
+    const Kp* cur = v.cur;
+    const uint8_t* cdesc = v.cdesc;
+    const float* cur_ur = v.cur_ur;
+    const Kp* last = v.last;
+    const uint8_t* ldesc = v.ldesc;
+    const float* lxw = v.lxw;
+    const int* lnobs = v.lnobs;
+    uint32_t* lists = v.lists;
+    if (pair_bad(b, v)) {
+        if (tid == 0) { atomicOr(b.err, 16); b.nmatch[p] = 0; }
+        return;
+    }
+    CurView<kLds> cv;
+    cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = cur_ur; cv.gdesc = cdesc;
+
+    // ---- phase 0: stage CurrentFrame, grid CSR by a stable counting sort ----
+    long long* tm = b.timing ? b.timing + (int64_t)p * 16 : nullptr;   // phase clocks (COEB_MATCH_TIMING)
+    if (tm && tid == 0) { tm[0] = clock64(); tm[13] = 0; tm[14] = 0x7fffffffffffffffll; tm[15] = 0; }
+    // with split lists (nsplit > 0) the grid is built only if the sequential path or the retry
+    // needs it
+    bool staged = false;
+    auto ensure_grid = [&]() {
+        if (!staged) stage_grid<kLds, NT>(cam, cur, cur_ur, cdesc, n, L);
+        staged = true;
+    };
+    if (!nsplit) ensure_grid();
+    if (tm && tid == 0) tm[1] = clock64();
+
+    const float* T = v.T;
+    const bool fwd = v.fwd, bwd = v.bwd;
 
     float th = th0;
     int nmatches = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
         // ---- phase 1: candidate lists (static filters) ----
         if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; s_flag[2] = 0; s_flag[3] = 0; }
-        __syncthreads();
-        // one kQL-lane group per query; lanes take the candidates of a grid column range kQL at a
-        // time and ballot-compact them, so each list stays in enumeration order
-        {
-            const int grp = tid / kQL, gl = tid % kQL, gsh = (tid & 63) & ~(kQL - 1);
-            // a query's inputs (flags, world point, octave, descriptor) are loaded one pass ahead
-            struct QIn { int act, oct; float X[3]; uint4 d0, d1; };
-            auto load_qin = [&](int q, QIn& r) {
-                r.act = 0;
-                if (q < nl) {
-                    r.act = lhas[q] && !lout[q];
-                    r.oct = last[q].octave;
-                    r.X[0] = lxw[3 * q]; r.X[1] = lxw[3 * q + 1]; r.X[2] = lxw[3 * q + 2];
-                    const uint4* d = reinterpret_cast<const uint4*>(ldesc + 32 * q);
-                    r.d0 = d[0]; r.d1 = d[1];
-                }
-            };
-            QIn nx;
-            load_qin(grp, nx);
-            const long long tw0 = tm ? clock64() : 0;
-            for (int q0 = 0; q0 < nl; q0 += NT / kQL) {
-                const int q = q0 + grp;
-                const QIn qi = nx;
-                load_qin(q + NT / kQL, nx);
-                int cnt = -1;
-                QueryWin w;
-                w.ok = false;
-                if (qi.act) w = query_window(cam, T, qi.X, qi.oct, th, fwd, bwd);
-                if (w.ok) {
-                    uint32_t qd[8];
-                    qd[0] = qi.d0.x; qd[1] = qi.d0.y; qd[2] = qi.d0.z; qd[3] = qi.d0.w;
-                    qd[4] = qi.d1.x; qd[5] = qi.d1.y; qd[6] = qi.d1.z; qd[7] = qi.d1.w;
-                    cnt = 0;
-                    uint32_t* lst = lists + (int64_t)q * kCQ;
-                    // the window's columns kQL at a time: lane gl holds column gx + gl's CSR range, a
-                    // group scan gives each column's offset in the concatenated (column-major) order,
-                    // and the group walks that concatenation kQL candidates at a time -- one pass per
-                    // column group instead of one per column, same enumeration order
-                    for (int gx = w.x0; gx <= w.x1; gx += kQL) {
-                        int clo = 0, clen = 0;
-                        if (gx + gl <= w.x1) {
-                            clo = L.cell[(gx + gl) * COEB_GRID_ROWS + w.y0];
-                            clen = L.cell[(gx + gl) * COEB_GRID_ROWS + w.y1 + 1] - clo;
-                        }
-                        const GroupCols gc = group_cols(clo, clen, gl);
-                        for (int base = 0; base < gc.total; base += kQL) {
-                            const int fi = base + gl;
-                            const int e = gc.index(fi);
-                            const int c1 = fi < gc.total ? e + 1 : e;      // e < c1 <=> fi < total
-                            bool ok = false;
-                            uint32_t ent = 0;
-                            if (e < c1) {
-                                const int i2 = (int)(L.sort[e] & ((1u << kIdxBits) - 1));
-                                float x, y, ur;
-                                int oct;
-                                cv.get(e, i2, x, y, ur, oct);
-                                ok = true;
-                                if (w.chk) {
-                                    if (oct < w.minL) ok = false;
-                                    if (w.maxL >= 0 && oct > w.maxL) ok = false;
-                                }
-                                const float distx = x - w.u, disty = y - w.v;
-                                if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) ok = false;
-                                if (ur > 0 && fabsf(w.ur_q - ur) > w.radius) ok = false;
-                                if (ok) {
-                                    const int dist = cv.dist(e, i2, qd);
-                                    ok = dist <= TH_HIGH;
-                                    ent = ((uint32_t)dist << kIdxBits) | (uint32_t)i2;
-                                }
-                            }
-                            const uint32_t gb = (uint32_t)(__ballot(ok) >> gsh) & ((1u << kQL) - 1u);
-                            if (ok) {
-                                const int pos = cnt + __popc(gb & ((1u << gl) - 1u));
-                                if (pos < kCQ) lst[pos] = ent;
-                            }
-                            cnt += __popc(gb);
-                        }
-                    }
-                    if (cnt > kCQ) s_flag[0] = 1;      // overflow -> sequential path
-                }
-                if (q < nl && gl == 0) L.qn[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | (lnobs[q] > 0 ? 0x10000 : 0));
-                if (tm && tid == 0) tm[15] += 1;
+        if (attempt == 0 && nsplit) {
+            // lists and counts from k_match_lists
+            const int* qg = b.qn + (int64_t)p * b.qn_stride;
+            for (int q = tid; q < nl; q += NT) L.qn[q] = qg[q];
+            if (tid == 0) {
+                int ov = 0;
+                for (int k = 0; k < nsplit; k++) ov |= qg[b.last_stride + k];
+                s_flag[0] = ov;
             }
-            if (tm && (tid & 63) == 0) {           // per-wave loop time: slowest / fastest wave
-                const long long dt = clock64() - tw0;
-                atomicMax((unsigned long long*)&tm[13], (unsigned long long)dt);
-                atomicMin((unsigned long long*)&tm[14], (unsigned long long)dt);
-            }
+        } else {
+            ensure_grid();
+            __syncthreads();
+            build_lists<kLds, NT>(cam, v, L, cv, th, 0, NT / kQL, L.qn, s_flag, tm);
         }
         __syncthreads();
         bool seq = force_seq || s_flag[0];
@@ -708,6 +820,7 @@ __global__ __launch_bounds__(NT, 4) void k_match(MatchCam cam, MatchBufs b, floa
         if (tm && tid == 0) { tm[3 + 4 * attempt] = clock64(); tm[12 + attempt] = s_flag[7]; }
         // ---- sequential path (overflow / no convergence / forced): literal loop, one thread ----
         if (seq) {
+            ensure_grid();
             for (int c = tid; c < n; c += NT) L.owner[c] = -1;
             __syncthreads();
             if (tid == 0) {
@@ -1225,20 +1338,49 @@ int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int b
     // share a CU and one pair's barrier waits overlap the other's work (k_match 0.355 -> 0.335 ms
     // per 1025-frame launch, profiles/r03/s5/match_nt_ab.txt); otherwise 1024 threads per pair
     const int nt = lds_full <= 80 * 1024 ? 512 : 1024;
+    // Few pairs (a small shard): the candidate lists are built by k_match_lists with nsplit
+    // workgroups per pair, so ~256 workgroups share the work instead of P; COEB_MATCH_SPLIT=0
+    // turns this off, =N forces N
+    int nsplit = 0;
+    if (b.qn && b.qn_stride >= b.last_stride + kMaxSplit) {
+        nsplit = std::min(kMaxSplit, 256 / std::max(P, 1));
+        if (const char* e = getenv("COEB_MATCH_SPLIT")) nsplit = std::max(0, std::min(kMaxSplit, atoi(e)));
+        if (nsplit < 2) nsplit = 0;
+    }
+    bool lds_cur = lds_full <= 160 * 1024;
+    if (!lds_cur && lds_min > 160 * 1024) return -2;
+    if (nsplit) {
+        // the lists kernel stages the current frame in LDS (COEB_MATCH_LISTS_LDS=0: reads it from
+        // global memory); k_match then needs no staged frame (its phases 0-1 run only for the
+        // sequential fallback / the retry, then reading the frame from global memory), so it takes
+        // a fraction of the LDS and leaves the CU to the other pipeline's kernels
+        // (COEB_MATCH_SPLIT_FULL=1 keeps the staged form)
+        const char* le = getenv("COEB_MATCH_LISTS_LDS");
+        const bool lists_lds = lds_cur && !(le && atoi(le) == 0);
+        const size_t lds_l = match_lds_bytes(b.cur_stride, 0, lists_lds, nullptr);
+        auto gl = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l);
+            hipLaunchKernelGGL(kern, dim3(P, nsplit), dim3(1024), lds_l, s, cam, b, th, bmono);
+        };
+        prof_begin(prof, "k_match_lists", s);
+        if (lists_lds) gl(k_match_lists<true, 1024>);
+        else gl(k_match_lists<false, 1024>);
+        prof_end(prof, s);
+        const char* fe = getenv("COEB_MATCH_SPLIT_FULL");
+        if (!(fe && atoi(fe) != 0)) lds_cur = false;
+    }
     auto go = [&](auto kern, size_t lds) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(kern, dim3(P), dim3(nt), lds - 256, s, cam, b, th, bmono, check_ori, retry_below, force_seq);
+        hipLaunchKernelGGL(kern, dim3(P), dim3(nt), lds - 256, s, cam, b, th, bmono, check_ori, retry_below, force_seq,
+                           nsplit);
     };
     prof_begin(prof, "k_match", s);
-    if (lds_full <= 160 * 1024) {
+    if (lds_cur) {
         if (nt == 512) go(k_match<true, 512>, lds_full);
         else go(k_match<true, 1024>, lds_full);
-    } else if (lds_min <= 160 * 1024) {
+    } else {
         if (nt == 512) go(k_match<false, 512>, lds_min);
         else go(k_match<false, 1024>, lds_min);
-    } else {
-        prof_end(prof, s);
-        return -2;
     }
     prof_end(prof, s);
     return hipGetLastError() == hipSuccess ? 0 : -1;

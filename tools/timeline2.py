@@ -20,7 +20,7 @@ def main(path, P=2):
     step = rows[i0:i1]
     iv = []
     for r in step:
-        name = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "").replace("void ", "")
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         name = name.split("<")[0].strip()
         s, e = (int(r["Start_Timestamp"]) - t0) / 1000, (int(r["End_Timestamp"]) - t0) / 1000
         iv.append((s, e, name, r["Queue_Id"]))
