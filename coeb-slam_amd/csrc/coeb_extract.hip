@@ -2573,7 +2573,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     bw.L = plan.L;
     int items = 0;
     const char* brv = getenv("COEB_BLUR_ROWS");            // rows per band of k_blur_rows; 0 = k_blur
-    const int brows = brv ? atoi(brv) : 64;
+    const int brows = brv ? atoi(brv) : 32;
     bw.brows = brows;
     for (int l = 0; l < plan.L; l++) {
         const LevelGeom& g = plan.lv[l];

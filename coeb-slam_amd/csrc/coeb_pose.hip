@@ -385,6 +385,12 @@ __device__ __forceinline__ int part_slot(int t) { return t + (t >> 5); }
 #define COEB_POSE_TB 4
 #endif
 constexpr int kTB = COEB_POSE_TB;
+static_assert(kTB >= 1 && kTB <= kPT / 64, "one wave per trial of a round");
+#ifndef COEB_POSE_T1
+#define COEB_POSE_T1 1         // trials in an iteration's first round (speculative beyond 1)
+#endif
+constexpr int kT1 = COEB_POSE_T1;
+static_assert(kT1 >= 1 && kT1 <= kTB, "first-round trials");
 
 struct PoseTrial {
     Se3 s;                 // exp(x) * saved
@@ -629,45 +635,34 @@ __global__ __launch_bounds__(kPT, 2) void k_pose(PoseBufs b, PoseCam cm)
             // The trial loop (do { ... } while (rho < 0 && qmax < 10)) in rounds of T trials: the
             // first round of an iteration tries one step; after a rejection, a round solves and
             // scores the next T steps of the rejection sequence (lambda_t+1 = lambda_t * ni_t,
-            // ni_t+1 = 2 ni_t, all from the same saved estimate) at once -- lane t of wave 0 solves
-            // step t, one chi2 pass scores all T, and thread 0 then walks them in order exactly as
+            // ni_t+1 = 2 ni_t, all from the same saved estimate) at once -- wave t solves step t,
+            // one chi2 pass scores all T, and thread 0 then walks them in order exactly as
             // the sequential loop would, stopping where it stops.  Steps past that point were never
             // taken: their results are dropped.
             int qmax = 0;                                          // uniform copy of L.qmax
             for (;;) {
-                const int T = qmax == 0 ? 1 : min(kTB, 10 - qmax);
+                const int T = qmax == 0 ? kT1 : min(kTB, 10 - qmax);
                 if (tid == 0) { L.lam = lambda; L.ni = ni; }
                 __syncthreads();
-                if (T == 1 && wv == 0) {
-                    // one trial: its LDL^T solve on the lanes of wave 0, the rest on lane 0
+                if (wv < T) {
+                    // trial wv of the round on wave wv (kTB <= the 4 waves): its LDL^T solve on the
+                    // wave's lanes, the SE3 exponential and product as uniform values
+                    double lam = L.lam, nu = L.ni;
+                    for (int k = 0; k < wv; k++) { lam = lam * nu; nu = nu * 2.0; }
                     double x[6];
                     for (int j = 0; j < 6; j++) x[j] = 0.0;
-                    const int ok2 = pq_solve6_wave(L.hb, L.lam, L.hb + 21, x) ? 1 : 0;
+                    const int ok2 = pq_solve6_wave(L.hb, lam, L.hb + 21, x) ? 1 : 0;
                     if (!ok2) for (int j = 0; j < 6; j++) x[j] = 0.0;
                     const Se3 saved = L.s;
                     const Se3 up = pq_exp<true>(x);
                     const Se3 ns = pq_mul<true>(up, saved);
                     if (lane == 0) {
-                        PoseTrial& tr = L.tr[0];
+                        PoseTrial& tr = L.tr[wv];
                         tr.s = ns;
                         for (int j = 0; j < 6; j++) tr.x[j] = x[j];
-                        tr.lam = L.lam;
+                        tr.lam = lam;
                         tr.ok = ok2;
                     }
-                } else if (T > 1 && tid < T) {
-                    double lam = L.lam, nu = L.ni;
-                    for (int k = 0; k < tid; k++) { lam = lam * nu; nu = nu * 2.0; }
-                    const Se3 saved = L.s;
-                    double x[6];
-                    for (int j = 0; j < 6; j++) x[j] = 0.0;
-                    const int ok2 = pq_solve6(L.hb, lam, L.hb + 21, x) ? 1 : 0;
-                    if (!ok2) for (int j = 0; j < 6; j++) x[j] = 0.0;
-                    const Se3 up = pq_exp(x);
-                    PoseTrial& tr = L.tr[tid];
-                    tr.s = pq_mul(up, saved);
-                    for (int j = 0; j < 6; j++) tr.x[j] = x[j];
-                    tr.lam = lam;
-                    tr.ok = ok2;
                 }
                 __syncthreads();
                 PT_ADD(2, t_s0);
