@@ -2189,6 +2189,9 @@ __device__ __forceinline__ void ic_row_load(const uint8_t* rp, uint4& c0, uint4&
     }
 }
 
+#ifndef COEB_DESC_IC_CHUNK
+#define COEB_DESC_IC_CHUNK 1
+#endif
 template <bool kVec0, int KP>
 // 24 waves per CU (launch bound 6 blocks: 80 VGPRs, 3 spilled) measured 0.253 vs 0.212 ms/step
 __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ P, ExtractBufs b)
@@ -2239,6 +2242,53 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
     const uint8_t* rowp = img + (int64_t)y * g.pitch + (x - 15 - a);         // row v = 0
     const int64_t spitch = half ? (int64_t)g.pitch : -(int64_t)g.pitch;      // rows +|v| / -|v|
     const bool vec = kVec0 || l != 0;
+    int aoff = 15;                             // m10 = A - aoff * S
+#if COEB_DESC_IC_CHUNK
+    if (vec) {
+        // lane (kq, j) takes tasks r = j + kLpk i of its keypoint, r = 3 row + chunk: image row
+        // y + row - 15, 16-byte chunk `chunk` of the 48 bytes from x - 15 - a.  One load
+        // instruction then covers ~kLpk / 3 whole rows of each keypoint rather than one chunk of
+        // kLpk rows: a third of the distinct L1 lines per instruction (the row-per-lane form kept
+        // the address unit busy 77 % of the kernel, stalled on the L1 half of it).  The disc mask
+        // is formed per byte from u = column - x, the column weights are u + 31 (in [1, 63], so
+        // packed bytes never carry) and m01 takes v * (row sum) directly.
+        constexpr int kTasks = (93 + kLpk - 1) / kLpk;
+        constexpr uint64_t kUmaxPk = 0x3689ABCDDEEEFFFFull;     // umax[av] in nibble av (kUmax)
+        const int j = lane % kLpk;
+        const uint8_t* base0 = img + (int64_t)(y - 15) * g.pitch + (x - 15 - a);
+        uint4 cq[kTasks];
+#pragma unroll
+        for (int i = 0; i < kTasks; i++) {
+            const int r = min(j + kLpk * i, 92);
+            const int row = r / 3, ch = r - 3 * row;
+            cq[i] = *reinterpret_cast<const uint4*>(base0 + (int64_t)row * g.pitch + 16 * ch);
+        }
+#pragma unroll
+        for (int i = 0; i < kTasks; i++) {
+            const int r = j + kLpk * i;
+            if (r < 93) {
+                const int row = r / 3, ch = r - 3 * row;
+                const int v = row - 15, av = v < 0 ? -v : v;
+                const int um = (int)((kUmaxPk >> (4 * av)) & 15u);
+                const uint32_t q[4] = {cq[i].x, cq[i].y, cq[i].z, cq[i].w};
+                uint32_t rs = 0;
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    const int u0 = 16 * ch + 4 * d - a - 15;        // u of the dword's first byte
+                    const int s0 = min(max(-um - u0, 0), 4), e0 = min(max(um - u0 + 1, 0), 4);
+                    const uint32_t msk = (uint32_t)((1ull << (8 * e0)) - 1ull) & ~(uint32_t)((1ull << (8 * s0)) - 1ull);
+                    const uint32_t pm = q[d] & msk;
+                    A = __builtin_amdgcn_udot4(pm, (uint32_t)(u0 + 31) * 0x01010101u + 0x03020100u, A, false);
+                    rs = __builtin_amdgcn_udot4(pm, 0x01010101u, rs, false);
+                }
+                S += rs;
+                m01 += v * (int)rs;
+            }
+        }
+        aoff = 31;
+    } else
+#endif
+    {
 #pragma unroll
     for (int i0 = 0; i0 < kNr; i0 += kNb) {
         uint4 c[kNb][3];
@@ -2271,14 +2321,15 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
             m01 += av * (int)rs;
         }
     }
-    if (half == 0) m01 = -m01;                 // lower half: rows -|v|
+        if (half == 0) m01 = -m01;             // lower half: rows -|v|
+    }
 #pragma unroll
     for (int o = 1; o < kLpk; o <<= 1) {
         A += __shfl_xor(A, o, 64);
         S += __shfl_xor(S, o, 64);
         m01 += __shfl_xor(m01, o, 64);
     }
-    const int m10 = (int)A - 15 * (int)S;
+    const int m10 = (int)A - aoff * (int)S;
     const float angle = fast_atan2_dev((float)m01, (float)m10);
     const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
     float bs, ac;
@@ -2373,169 +2424,6 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         wave_sync_lds();                         // patch reads done before the next staging
     }
 #undef COEB_LOAD_PATCH
-    // ---- phase C: descriptors out
-    uint4* gd = reinterpret_cast<uint4*>(b.desc + ((int64_t)f * P->kcap + idx0) * 32);
-    if (lane < 2 * nk) gd[lane] = reinterpret_cast<const uint4*>(dsl)[lane];
-}
-
-// The same three phases with the wave's 8 blurred patches staged straight into LDS by LDS-DMA
-// (global_load_lds_dwordx4, no VGPR round trip), all issued before the IC_Angle rows: the wave
-// then waits on memory once instead of once per patch pair, and phase B reads every patch from
-// LDS.  Patch rows sit at a 64-byte pitch (an LDS-DMA instruction writes 64 x 16 consecutive
-// bytes, so rows cannot be padded); 8 x 2368 B per wave = 77 KB per workgroup, 2 per CU.
-constexpr int kDmaRow = 64, kDmaPatch = kDmaRow * kBlRows;   // 2368 B = 148 chunks
-template <int KP> constexpr int dma_wave_lds() { return KP * kDmaPatch + 32 * KP; }
-typedef __attribute__((address_space(1))) void gvoid_t;
-typedef __attribute__((address_space(3))) void lvoid_t;
-
-template <bool kVec0, int KP>
-__global__ __launch_bounds__(kThreads) void k_describe_dma(const Plan* __restrict__ P, ExtractBufs b)
-{
-    constexpr int kLpk = 64 / KP, kHl = kLpk / 2, kNr = 16 / kHl, kNb = kNr < 4 ? kNr : 4;
-    constexpr int kDmaWaveLds = dma_wave_lds<KP>();
-    extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
-    uint32_t (*s_msk)[8] = reinterpret_cast<uint32_t (*)[8]>(dsm + kWaves * kDmaWaveLds);
-    if (threadIdx.x < 17 * 8) s_msk[threadIdx.x >> 3][threadIdx.x & 7] = ic_mask(threadIdx.x >> 3, threadIdx.x & 7);
-    __syncthreads();
-    const int2 bxy = block_xy();
-    const int f = bxy.y;
-    const int L = P->L;
-    const int lane = lane_id(), wv = wave_id();
-    const int nl = lane < L ? b.lvl_n[(int64_t)f * L + lane] : 0;
-    int incl = nl;
-    for (int o = 1; o < COEB_MAXL; o <<= 1) {
-        const int y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-    }
-    const int total = __builtin_amdgcn_readlane(incl, L - 1);
-    if (bxy.x == 0 && threadIdx.x == 0) b.counts[f] = total;
-    const int idx0 = (bxy.x * kWaves + wv) * KP;
-    if (idx0 >= total) return;
-    const int nk = min(KP, total - idx0);
-    const int kq = lane / kLpk, half = (lane / kHl) & 1, qi = lane % kHl;
-    const int id = idx0 + min(kq, nk - 1);
-    int l = 0, start = 0;
-    for (int q = 0; q < L - 1; q++) {
-        const int e = __builtin_amdgcn_readlane(incl, q);
-        if (id >= e) { l = q + 1; start = e; }
-    }
-    const LevelGeom& g = P->lv[l];
-    const uint32_t key = b.lvl_kp[(int64_t)f * P->lvl_stride + g.out_off + (id - start)];
-    const int x = key_x(key), y = key_y(key), sc = key_s(key);
-    const uint8_t* img = level_ptr(P, b, f, l);
-    // ---- the nk blurred patches -> the wave's slab (rows y-18..y+18, 64 bytes from (x-18) & ~15)
-    uint8_t* slab = dsm + wv * kDmaWaveLds;
-    const int porg = (int)g.blur_off + (y - 18) * g.bpitch + ((x - 18) & ~15);
-    const int xoff = x - ((x - 18) & ~15);
-    const int bpitch = g.bpitch;
-    {
-        const uint8_t* blur_f = b.blur + (int64_t)f * P->blur_stride;
-        const int r0 = lane >> 2, c16 = 16 * (lane & 3);
-#pragma unroll
-        for (int t = 0; t < KP; t++) {
-            if (t < nk) {
-                const uint8_t* src = blur_f + __builtin_amdgcn_readlane(porg, t * kLpk);
-                const int bpt = __builtin_amdgcn_readlane(bpitch, t * kLpk);
-                uint8_t* dst = slab + t * kDmaPatch;
-                __builtin_amdgcn_global_load_lds((gvoid_t*)(src + r0 * bpt + c16), (lvoid_t*)dst, 16, 0, 0);
-                __builtin_amdgcn_global_load_lds((gvoid_t*)(src + (r0 + 16) * bpt + c16), (lvoid_t*)(dst + 1024), 16, 0, 0);
-                if (lane < (kBlChunks - 128))
-                    __builtin_amdgcn_global_load_lds((gvoid_t*)(src + (r0 + 32) * bpt + c16), (lvoid_t*)(dst + 2048), 16,
-                                                     0, 0);
-            }
-        }
-    }
-    // ---- phase A: IC_Angle, fastAtan2, sincos, the cv::KeyPoint record (as k_describe)
-    uint32_t A = 0, S = 0;
-    int m01 = 0;
-    const int a = (x - 15) & 15;
-    const uint32_t m8 = (a & 8) ? 0xFFFFFFFFu : 0u, m4 = (a & 4) ? 0xFFFFFFFFu : 0u;
-    const uint8_t* rowp = img + (int64_t)y * g.pitch + (x - 15 - a);
-    const int64_t spitch = half ? (int64_t)g.pitch : -(int64_t)g.pitch;
-    const bool vec = kVec0 || l != 0;
-#pragma unroll
-    for (int i0 = 0; i0 < kNr; i0 += kNb) {
-        uint4 c[kNb][3];
-#pragma unroll
-        for (int r = 0; r < kNb; r++) {
-            const uint8_t* rp = rowp + (qi + kHl * (i0 + r)) * spitch;
-            if (vec) ic_row_load<true>(rp, c[r][0], c[r][1], c[r][2]);
-            else ic_row_load<false>(rp, c[r][0], c[r][1], c[r][2]);
-        }
-#pragma unroll
-        for (int r = 0; r < kNb; r++) {
-            const int av = qi + kHl * (i0 + r);
-            const uint32_t* msk = s_msk[(av == 0 && half) ? 16 : av];
-            const uint32_t q[12] = {c[r][0].x, c[r][0].y, c[r][0].z, c[r][0].w, c[r][1].x, c[r][1].y,
-                                    c[r][1].z, c[r][1].w, c[r][2].x, c[r][2].y, c[r][2].z, c[r][2].w};
-            uint32_t r1[10], r2[9];
-#pragma unroll
-            for (int k = 0; k < 10; k++) r1[k] = (m8 & q[k + 2]) | (~m8 & q[k]);
-#pragma unroll
-            for (int k = 0; k < 9; k++) r2[k] = (m4 & r1[k + 1]) | (~m4 & r1[k]);
-            uint32_t rs = 0;
-#pragma unroll
-            for (int d = 0; d < 8; d++) {
-                const uint32_t pm = __builtin_amdgcn_alignbyte(r2[d + 1], r2[d], (uint32_t)(a & 3)) & msk[d];
-                A = __builtin_amdgcn_udot4(pm, 0x03020100u + 0x04040404u * (uint32_t)d, A, false);
-                rs = __builtin_amdgcn_udot4(pm, 0x01010101u, rs, false);
-            }
-            S += rs;
-            m01 += av * (int)rs;
-        }
-    }
-    if (half == 0) m01 = -m01;
-#pragma unroll
-    for (int o = 1; o < kLpk; o <<= 1) {
-        A += __shfl_xor(A, o, 64);
-        S += __shfl_xor(S, o, 64);
-        m01 += __shfl_xor(m01, o, 64);
-    }
-    const int m10 = (int)A - 15 * (int)S;
-    const float angle = fast_atan2_dev((float)m01, (float)m10);
-    const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
-    float bs, ac;
-    sincos_canon(angle * factorPI, &bs, &ac);
-    if (lane % kLpk == 0 && kq < nk) {
-        float fx = (float)x, fy = (float)y;
-        if (l != 0) { fx *= g.scale; fy *= g.scale; }
-        KeyPointOut o;
-        o.x = fx; o.y = fy; o.size = (float)g.size_i; o.angle = angle; o.response = (float)sc;
-        o.octave = l; o.class_id = -1;
-        reinterpret_cast<KeyPointOut*>(b.kps)[(int64_t)f * P->kcap + idx0 + kq] = o;
-    }
-    // ---- phase B: 256 tests per keypoint from the staged patches
-    const int4 pa = reinterpret_cast<const int4*>(b.pattern)[lane];
-    float px0[4], py0[4], px1[4], py1[4];
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const int pw = t == 0 ? pa.x : t == 1 ? pa.y : t == 2 ? pa.z : pa.w;
-        px0[t] = (float)(int8_t)(pw & 0xff); py0[t] = (float)(int8_t)((pw >> 8) & 0xff);
-        px1[t] = (float)(int8_t)((pw >> 16) & 0xff); py1[t] = (float)(int8_t)(pw >> 24);
-    }
-    uint32_t* dsl = reinterpret_cast<uint32_t*>(slab + KP * kDmaPatch);
-    __builtin_amdgcn_s_waitcnt(0);           // every LDS-DMA of this wave has landed
-    wave_sync_lds();
-    for (int t = 0; t < nk; t++) {
-        const float tb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bs), t * kLpk));
-        const float ta = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ac), t * kLpk));
-        const uint8_t* bc = slab + t * kDmaPatch + 18 * kDmaRow + __builtin_amdgcn_readlane(xoff, t * kLpk);
-        const f32x2 AB = {ta, tb}, BA = {tb, ta};
-        uint32_t nib = 0;
-#pragma unroll
-        for (int tt = 0; tt < 4; tt++) {
-            const f32x2 t0 = f32x2{py0[tt], py0[tt]} * AB, t1 = f32x2{py1[tt], py1[tt]} * AB;
-            const f32x2 rc0 = __builtin_elementwise_fma(f32x2{px0[tt], px0[tt]}, BA, f32x2{t0.x, -t0.y});
-            const f32x2 rc1 = __builtin_elementwise_fma(f32x2{px1[tt], px1[tt]}, BA, f32x2{t1.x, -t1.y});
-            const int o0 = (int)__builtin_fmaf(rintf(rc0.x), (float)kDmaRow, rintf(rc0.y));
-            const int o1 = (int)__builtin_fmaf(rintf(rc1.x), (float)kDmaRow, rintf(rc1.y));
-            nib |= (uint32_t)(bc[o0] < bc[o1]) << tt;
-        }
-        uint32_t dw = nib << (4 * (lane & 7));
-        dw = dpp_or_shl4(dpp_or_xor2(dpp_or_xor1(dw)));
-        if ((lane & 7) == 0) dsl[8 * t + (lane >> 3)] = dw;
-    }
-    wave_sync_lds();
     // ---- phase C: descriptors out
     uint4* gd = reinterpret_cast<uint4*>(b.desc + ((int64_t)f * P->kcap + idx0) * 32);
     if (lane < 2 * nk) gd[lane] = reinterpret_cast<const uint4*>(dsl)[lane];
@@ -2725,25 +2613,9 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     }
     prof_begin(prof, "k_describe", s);
     const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
-    const char* ddv = getenv("COEB_DESC_DMA");            // 0: register-staged k_describe; 4 / 8: keypoints per wave
-    const int ddk = ddv ? atoi(ddv) : 0;
-    if (ddk == 4 || ddk == 8) {
-        auto go = [&](auto kern, int kp, size_t lds) {
-            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(kern, dim3((plan.kcap + kWaves * kp - 1) / (kWaves * kp), F), dim3(kThreads), lds, s, d_plan, b);
-        };
-        if (ddk == 8) {
-            const size_t lds = (size_t)kWaves * dma_wave_lds<8>() + 17 * 8 * 4;
-            if (vec0) go(k_describe_dma<true, 8>, 8, lds); else go(k_describe_dma<false, 8>, 8, lds);
-        } else {
-            const size_t lds = (size_t)kWaves * dma_wave_lds<4>() + 17 * 8 * 4;
-            if (vec0) go(k_describe_dma<true, 4>, 4, lds); else go(k_describe_dma<false, 4>, 4, lds);
-        }
-        prof_end(prof, s);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
     // 8 keypoints per wave (round 1's 32 let one XCD's resident waves span ~20 frames and refetch
-    // every patch row past L2; 4 and 16 measured slower)
+    // every patch row past L2; 4 and 16 measured slower; 4 again with the
+    // row-chunk IC_Angle loads: 0.667 vs 0.630 ms, profiles/r04/ab6)
     constexpr int KP = 8;
     if (vec0)
         hipLaunchKernelGGL((k_describe<true, KP>), dim3((plan.kcap + kWaves * KP - 1) / (kWaves * KP), F), dim3(kThreads), 0,
