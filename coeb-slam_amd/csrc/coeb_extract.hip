@@ -850,13 +850,39 @@ __device__ __forceinline__ us2 pk_min(us2 a, us2 b) { return __builtin_elementwi
 __device__ __forceinline__ us2 pk_max(us2 a, us2 b) { return __builtin_elementwise_max(a, b); }
 __device__ __forceinline__ us2 pk_subs(us2 a, us2 b) { return __builtin_elementwise_sub_sat(a, b); }
 
+#ifndef COEB_FAST_MAX3
+#define COEB_FAST_MAX3 1
+#endif
+// Three-input packed max / min of u16 pixel pairs (values <= 255) as v_pk_maximum3_f16 /
+// v_pk_minimum3_f16: read as f16 the patterns are positive denormals, ordered like the integers
+// (f16 denormals are not flushed), so one instruction replaces two v_pk_max/min_u16
+__device__ __forceinline__ us2 pk_max3(us2 a, us2 b, us2 c)
+{
+    uint32_t r;
+    asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(as_u32(a)), "v"(as_u32(b)), "v"(as_u32(c)));
+    return as_us2(r);
+}
+__device__ __forceinline__ us2 pk_min3(us2 a, us2 b, us2 c)
+{
+    uint32_t r;
+    asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(as_u32(a)), "v"(as_u32(b)), "v"(as_u32(c)));
+    return as_us2(r);
+}
+
 __device__ __forceinline__ uint32_t pretest_half(us2 v, us2 p0, us2 p8, us2 p2, us2 p10, us2 p4, us2 p12, us2 p6,
                                                  us2 p14, us2 T)
 {
+#if COEB_FAST_MAX3
+    // dark survives <=> v - md > t, bright <=> mb - v > t: one threshold test of their maximum
+    const us2 md = pk_max3(pk_min(p0, p8), pk_min(p2, p10), pk_max(pk_min(p4, p12), pk_min(p6, p14)));
+    const us2 mb = pk_min3(pk_max(p0, p8), pk_max(p2, p10), pk_min(pk_max(p4, p12), pk_max(p6, p14)));
+    return as_u32(pk_subs(pk_max(pk_subs(v, md), pk_subs(mb, v)), T));
+#else
     const us2 lo = pk_subs(v, T), hi = v + T;
     const us2 md = pk_max(pk_max(pk_min(p0, p8), pk_min(p2, p10)), pk_max(pk_min(p4, p12), pk_min(p6, p14)));
     const us2 mb = pk_min(pk_min(pk_max(p0, p8), pk_max(p2, p10)), pk_min(pk_max(p4, p12), pk_max(p6, p14)));
     return as_u32(pk_subs(lo, md)) | as_u32(pk_subs(mb, hi));
+#endif
 }
 
 // corner_strength_sel for TWO survivors at once, one per u16 half (pixel A at slab offset oa in
