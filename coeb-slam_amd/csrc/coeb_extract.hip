@@ -1320,12 +1320,14 @@ __global__ __launch_bounds__(kThreads, COEB_FAST_MINWG) void k_fast(const Plan* 
                                                        int cell0, int cell1)                 // this launch's cells
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    // a per-lane wave index here (unlike the other kernels): with the cell geometry in SGPRs the
-    // compiler moves the per-cell bookkeeping onto the shared scalar unit and the kernel ran
-    // 5 % slower (0.320 vs 0.335 ms/step).  A u16-pixel slab (ring operands as aligned u16
+    // A wave-uniform wave index, so the cell geometry and the per-cell bookkeeping live in
+    // SGPRs on the scalar unit: the kernel is VALU-bound (SQ_INSTS_VALU x 4 cycles = 95 % of the
+    // SIMDs' cycles, profiles/r04/pipes), and moving that work off the VALU took 1.026 -> 0.962 ms
+    // per 1025-frame launch (profiles/r04/ab7).  (Round 2 measured the opposite, 5 % slower, when
+    // the scalar unit was the busier pipe.)  A u16-pixel slab (ring operands as aligned u16
     // pairs, no byte gathers; 11 ds_read_b64 per 4-pixel group) cut VALU 7 % but ran 5 % slower
     // (twice the staging stores): the byte slab stays.
-    const int wv = threadIdx.x >> 6, lane = lane_id();
+    const int wv = wave_id(), lane = lane_id();
     const int slab = fast_slab(*P, RB), ms_slab = fast_ms_slab(*P, RB);   // per-wave LDS: roi, M, lists
     uint8_t* wbase = smem + (size_t)wv * fast_wave_lds(*P, RB) + kFastGuard;
     uint8_t* roi = wbase;
