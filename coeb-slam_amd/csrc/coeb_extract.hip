@@ -1067,6 +1067,15 @@ __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs
         if (r < G.rh) __builtin_memcpy(d, &R.v0, 16);
         if (r + 16 < G.rh) __builtin_memcpy(d + 16 * RB, &R.v1, 16);
         if (r + 32 < G.rh) __builtin_memcpy(d + 32 * RB, &R.v2, 16);
+        if constexpr (RB == kFastRowBytesM) {
+            // then zero the rows' M columns 48..95 (after every row's data: the stores above
+            // spill into them), three lanes per row
+            uint8_t* z = roi + r * RB + 48 + 16 * c;
+            const uint4 zero = make_uint4(0, 0, 0, 0);
+            if (c < 3 && r < G.rh) *reinterpret_cast<uint4*>(z) = zero;
+            if (c < 3 && r + 16 < G.rh) *reinterpret_cast<uint4*>(z + 16 * RB) = zero;
+            if (c < 3 && r + 32 < G.rh) *reinterpret_cast<uint4*>(z + 32 * RB) = zero;
+        }
     } else if (G.words) {
         const int gx = G.x0 - 1;
         const int kw = min(lane & 15, G.nwords);
@@ -1156,9 +1165,7 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
     const int cg = lane & ((1 << lpr_log) - 1), rsub = lane >> lpr_log;
     const int rpi = 64 >> lpr_log;
     // lanes' pixel columns inside the window (fixed for the cell)
-    const uint32_t vmask4 = cg < ngrp ? (4 * cg + 0 < ww ? 1u : 0u) | (4 * cg + 1 < ww ? 2u : 0u) |
-                                            (4 * cg + 2 < ww ? 4u : 0u) | (4 * cg + 3 < ww ? 8u : 0u)
-                                      : 0u;
+    const uint32_t vmask4 = (1u << min(max(ww - 4 * cg, 0), 4)) - 1u;   // columns 4 cg + k < ww
     int o = (rsub + 3) * RB + 4 + 4 * cg;
     const uint32_t one2 = 0x00010001u;
     FC_MARK(t_scan);
@@ -1173,7 +1180,7 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
         asm("v_pk_min_u16 %0, %1, %2" : "=v"(s01) : "v"(lo), "v"(one2));
         asm("v_pk_min_u16 %0, %1, %2" : "=v"(s23) : "v"(hi), "v"(one2));
         const uint32_t t2 = s01 | (s23 << 2);
-        const uint32_t m4 = (t2 | (t2 >> 15)) & (r0 + rsub < wh ? vmask4 : 0u);
+        const uint32_t m4 = (t2 | (t2 >> 15)) & (rsub < wh - r0 ? vmask4 : 0u);   // wh - r0: scalar
         const uint64_t mk = __ballot(m4 != 0u);
         if (mk) {
             if (m4) ent[ne + mbcnt(mk)] = (uint16_t)(((uint32_t)o >> 2) | (m4 << 12));   // o = 4 mod 4: exact
@@ -1349,7 +1356,8 @@ __global__ __launch_bounds__(kThreads, COEB_FAST_MINWG) void k_fast(const Plan* 
     FC_MARK(t_st);
     fast_stage<RB>(G, R, roi);
     if (RB == kFastRowBytesM) {
-        // M columns 48..95 of rows 2 .. rh-3 (the staging writes columns 0..47 only)
+        // M columns 48..95 of rows 2 .. rh-3 (the 16-byte staging zeroes them itself)
+        if (!G.vec)
         for (int i = lane; i < 3 * (c.rh - 4); i += 64) {
             const int row = 2 + i / 3;
             reinterpret_cast<uint4*>(Ms + row * RB + 48)[i - 3 * (row - 2)] = make_uint4(0, 0, 0, 0);
