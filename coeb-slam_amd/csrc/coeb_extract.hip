@@ -885,6 +885,93 @@ __device__ __forceinline__ uint32_t pretest_half(us2 v, us2 p0, us2 p8, us2 p2, 
 #endif
 }
 
+#ifndef COEB_FAST_ARC2
+#define COEB_FAST_ARC2 1
+#endif
+// v_pk_maximum3_f16 / v_pk_minimum3_f16 on u16 patterns (see pk_max3) with the halves of the
+// second (S1) and / or third (S2) operand swapped by op_sel
+template <bool kMax, bool S1, bool S2>
+__device__ __forceinline__ uint32_t pk3(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+#define COEB_PK3(OP, SEL) asm(OP " %0, %1, %2, %3" SEL : "=v"(r) : "v"(a), "v"(b), "v"(c))
+    if constexpr (kMax) {
+        if constexpr (!S1 && !S2) COEB_PK3("v_pk_maximum3_f16", "");
+        else if constexpr (!S1 && S2) COEB_PK3("v_pk_maximum3_f16", " op_sel:[0,0,1] op_sel_hi:[1,1,0]");
+        else if constexpr (S1 && !S2) COEB_PK3("v_pk_maximum3_f16", " op_sel:[0,1,0] op_sel_hi:[1,0,1]");
+        else COEB_PK3("v_pk_maximum3_f16", " op_sel:[0,1,1] op_sel_hi:[1,0,0]");
+    } else {
+        if constexpr (!S1 && !S2) COEB_PK3("v_pk_minimum3_f16", "");
+        else if constexpr (!S1 && S2) COEB_PK3("v_pk_minimum3_f16", " op_sel:[0,0,1] op_sel_hi:[1,1,0]");
+        else if constexpr (S1 && !S2) COEB_PK3("v_pk_minimum3_f16", " op_sel:[0,1,0] op_sel_hi:[1,0,1]");
+        else COEB_PK3("v_pk_minimum3_f16", " op_sel:[0,1,1] op_sel_hi:[1,0,0]");
+    }
+#undef COEB_PK3
+    return r;
+}
+
+// max over the 16 circular nine-pixel arcs of the arc minimum, with ring positions k and k + 8
+// in the two u16 halves of Q[k] (k < 8): three-input packed min / max over both halves at once
+// (8 + 8 + 4 instructions instead of 16 + 16 + 8); the wrap-around operands are the swapped
+// registers (op_sel)
+__device__ __forceinline__ uint32_t arc_max_min_pk(const uint32_t Q[8])
+{
+    uint32_t M3[8], M9[8];
+#pragma unroll
+    for (int k = 0; k < 6; k++) M3[k] = pk3<false, false, false>(Q[k], Q[k + 1], Q[k + 2]);
+    M3[6] = pk3<false, false, true>(Q[6], Q[7], Q[0]);     // (q6, q7, q8) | (q14, q15, q0)
+    M3[7] = pk3<false, true, true>(Q[7], Q[0], Q[1]);      // (q7, q8, q9) | (q15, q0, q1)
+    M9[0] = pk3<false, false, false>(M3[0], M3[3], M3[6]);
+    M9[1] = pk3<false, false, false>(M3[1], M3[4], M3[7]);
+#pragma unroll
+    for (int k = 2; k < 5; k++) M9[k] = pk3<false, false, true>(M3[k], M3[k + 3], M3[k - 2]);
+#pragma unroll
+    for (int k = 5; k < 8; k++) M9[k] = pk3<false, true, true>(M3[k], M3[k - 5], M3[k - 2]);
+    const uint32_t A = pk3<true, false, false>(M9[0], M9[1], M9[2]);
+    const uint32_t B = pk3<true, false, false>(M9[3], M9[4], M9[5]);
+    return pk3<true, false, false>(M9[6], M9[7], pk3<true, false, false>(A, B, A));
+}
+
+// corner_strength_sel with the ring bytes loaded straight into u16 halves (Q[k] = p_k | p_{k+8}
+// << 16) and the arc taken by arc_max_min_pk.  Same result.
+template <int st>
+__device__ __forceinline__ int corner_strength_pos2(const uint8_t* c, int t)
+{
+    lds_cu8 b = (lds_cu8)c - (3 * st + 1);
+    asm volatile("" : "+v"(b));
+    constexpr int o = 3 * st + 1;                          // c[x] = b[x + o]
+    constexpr int off[16] = {o + 3 * st, o + 3 * st + 1, o + 2 * st + 2, o + st + 3, o + 3, o - st + 3, o - 2 * st + 2,
+                             o - 3 * st + 1, 1, 0, o - 2 * st - 2, o - st - 3, o - 3, o + st - 3, o + 2 * st - 2,
+                             o + 3 * st - 1};
+    us2 Qv[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) { Qv[k].x = b[off[k]]; Qv[k].y = b[off[k + 8]]; }
+    const int v = b[o];
+    uint32_t Q[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) Q[k] = as_u32(Qv[k]);
+    auto lo = [](uint32_t x) { return (int)(x & 0xFFFFu); };
+    auto hi = [](uint32_t x) { return (int)(x >> 16); };
+    const int md = max(max(min(lo(Q[0]), hi(Q[0])), min(lo(Q[2]), hi(Q[2]))),
+                       max(min(lo(Q[4]), hi(Q[4])), min(lo(Q[6]), hi(Q[6]))));
+    const int mb = min(min(max(lo(Q[0]), hi(Q[0])), max(lo(Q[2]), hi(Q[2]))),
+                       min(max(lo(Q[4]), hi(Q[4])), max(lo(Q[6]), hi(Q[6]))));
+    const bool dark = md < v - t, bright = mb > v + t;
+    const uint32_t mask = dark ? 0x00FF00FFu : 0u;
+    uint32_t Qx[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) Qx[k] = Q[k] ^ mask;
+    const uint32_t X = arc_max_min_pk(Qx);
+    int M = max(lo(X), hi(X)) - (v ^ (int)(mask & 0xFFu));
+    if (__builtin_expect(__ballot(dark && bright) != 0, 0)) {
+        if (dark && bright) {
+            const uint32_t Y = arc_max_min_pk(Q);
+            M = max(M, max(lo(Y), hi(Y)) - v);
+        }
+    }
+    return M;
+}
+
 // corner_strength_sel for TWO survivors at once, one per u16 half (pixel A at slab offset oa in
 // the low halves, pixel B at ob in the high halves): the same min / max / xor steps as packed
 // u16 operations (ring bytes loaded straight into the halves), M as a saturating difference
@@ -1210,7 +1297,11 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
                     int oo = 0, M = 0;
                     if (si < ns) {
                         oo = surv[si];
+#if COEB_FAST_ARC2
+                        M = corner_strength_pos2<RB>(&roi[oo], th_min);
+#else
                         M = corner_strength_sel<RB>(&roi[oo], th_min);
+#endif
                     }
                     const bool isc = si < ns && M > th_min;
                     if (isc) Ms[fast_mi<RB>(oo, mp)] = (uint8_t)M;
@@ -2586,40 +2677,25 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         }
     }
     constexpr int kOctThreads = 256;       // 512 / 1024 measured slower on large batches
-    (void)hipFuncSetAttribute((const void*)k_octree<kOctThreads>, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);
-    // small batches (per-rank shards): level 0's list -- the longest chain of the step -- gets
-    // 1024 threads in a launch of its own; COEB_OCT_WIDE_F = the largest batch that does so.
-    // COEB_OCT_SPLIT = l: levels >= l (short lists) run as one-wave workgroups with LDS sized for
-    // those levels only (no block barriers; many more workgroups per CU)
-    const char* owf = getenv("COEB_OCT_WIDE_F");
-    const int oct_wide_f = owf ? atoi(owf) : 0;
-    const char* osp = getenv("COEB_OCT_SPLIT");
-    const int oct_split = osp ? atoi(osp) : 0;
-    int sw_w = 0, sw_kl = 512, sw_lds = 0;
-    if (oct_split > 0 && oct_split < plan.L) {
-        int nmax = 0;
-        for (int l = oct_split; l < plan.L; l++) { sw_w = std::max(sw_w, plan.lv[l].ncap); nmax = std::max(nmax, plan.lv[l].nfeat); }
-        while (sw_kl < 4096 && sw_kl < (9 * nmax + 1) / 2) sw_kl *= 2;
-        sw_lds = sw_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * sw_kl;
-        (void)hipFuncSetAttribute((const void*)k_octree<64>, hipFuncAttributeMaxDynamicSharedMemorySize, sw_lds);
+    // Small batches (per-rank shards: fewer workgroups than two per CU): the key capacity in LDS
+    // doubles (up to 4096 keys, within 150 KB), so a 1280x960 level 0 (~2 700 candidates) keeps
+    // its keys in LDS instead of the global ping-pong buffers; large batches keep the plan's
+    // capacity, which leaves more workgroups per CU.  (Level 0 as one 1024-thread workgroup and
+    // the short upper levels as one-wave workgroups were both measured slower)
+    int oct_kl = plan.oct_kl, oct_lds = plan.oct_lds;
+    if (F * plan.L <= 2 * 256) {
+        int kl = oct_kl;
+        while (kl < 4096 && plan.oct_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * (2 * kl) <= 150 * 1024) kl *= 2;
+        oct_kl = kl;
+        oct_lds = plan.oct_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * kl;
     }
+    if (const char* e = getenv("COEB_OCT_KL_SMALL")) if (atoi(e) == 0) { oct_kl = plan.oct_kl; oct_lds = plan.oct_lds; }
+    (void)hipFuncSetAttribute((const void*)k_octree<kOctThreads>, hipFuncAttributeMaxDynamicSharedMemorySize, oct_lds);
     auto octree = [&](hipStream_t st, int l0, int l1) {
         if (l1 <= l0) return;
         prof_begin(prof, "k_octree", st);
-        if (l0 == 0 && F <= oct_wide_f) {
-            (void)hipFuncSetAttribute((const void*)k_octree<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, plan.oct_lds);
-            hipLaunchKernelGGL(k_octree<1024>, dim3(F, 1), dim3(1024), plan.oct_lds, st, d_plan, b, 0, plan.oct_w, plan.oct_kl);
-            l0 = 1;
-        }
-        int lm = l1;
-        if (sw_lds > 0 && l1 > oct_split) {
-            const int ls = std::max(l0, oct_split);
-            hipLaunchKernelGGL(k_octree<64>, dim3(F, l1 - ls), dim3(64), sw_lds, st, d_plan, b, ls, sw_w, sw_kl);
-            lm = ls;
-        }
-        if (lm > l0)
-            hipLaunchKernelGGL(k_octree<kOctThreads>, dim3(F, lm - l0), dim3(kOctThreads), plan.oct_lds, st, d_plan, b, l0,
-                               plan.oct_w, plan.oct_kl);
+        hipLaunchKernelGGL(k_octree<kOctThreads>, dim3(F, l1 - l0), dim3(kOctThreads), oct_lds, st, d_plan, b, l0, plan.oct_w,
+                           oct_kl);
         prof_end(prof, st);
     };
     // the late blur goes to the side stream (beside FAST / octree, which do not read it) and the
