@@ -154,6 +154,12 @@ __device__ __forceinline__ GroupCols group_cols(int lo, int len, int gl)
 #define COEB_MATCH_REGLIST 16
 #endif
 constexpr int kRegList = COEB_MATCH_REGLIST;        // list head kept in registers by the claim fixpoint
+#ifndef COEB_MATCH_QPT1024
+#define COEB_MATCH_QPT1024 2
+#endif
+#ifndef COEB_MATCH_RL1024
+#define COEB_MATCH_RL1024 12
+#endif
 
 struct QueryWin {
     bool ok, chk;
@@ -424,8 +430,8 @@ __device__ bool claims_first_min(const MatchLds& L, const uint32_t* lists, int s
     // the thread's first QPT queries (tid, tid + NT, ...) keep the heads of their lists in
     // registers across iterations (global list reads per iteration were most of this phase's
     // time); a 512-thread workgroup splits the same register budget over two queries
-    constexpr int QPT = NT >= 1024 ? 1 : 1024 / NT;
-    constexpr int RL = kRegList / QPT;
+    constexpr int QPT = NT >= 1024 ? COEB_MATCH_QPT1024 : 1024 / NT;
+    constexpr int RL = NT >= 1024 ? COEB_MATCH_RL1024 : kRegList / QPT;
     uint32_t rl[QPT][RL];
     int rm[QPT];
 #pragma unroll

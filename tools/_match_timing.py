@@ -1,5 +1,6 @@
 """k_match phase clocks over one bench-shaped batch (COEB_MATCH_TIMING=1): median cycles per
-phase across the 256 pairs.  Diagnostic only."""
+phase across the batch's pairs.  Diagnostic only.  Optional arguments: W H F NFEATURES
+(default 640 480 257 1000; 1280 960 33 2000 is one pipeline of config B's 64-frame shard)."""
 import os
 import sys
 
@@ -10,14 +11,14 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from coeb_front import synth  # noqa: E402
 from coeb_front.pipeline import BatchPipeline  # noqa: E402
 
-F = 257
-fr = synth.make_frames(640, 480, F, seed=1)
-bp = BatchPipeline(640, 480, F)
+W, H, F, NF = (int(a) for a in sys.argv[1:5]) if len(sys.argv) > 4 else (640, 480, 257, 1000)
+fr = synth.make_frames(W, H, F, seed=1)
+bp = BatchPipeline(W, H, F, nfeatures=NF)
 bp.load(fr, Tcw=np.stack([synth.motion_pose()] * F))
 for _ in range(3):
     bp.run()
 bp.ctx.synchronize()
-t = bp.ctx.debug_read("match_timing").view(np.int64).reshape(-1, 16)[:256]
+t = bp.ctx.debug_read("match_timing").view(np.int64).reshape(-1, 16)[:F - 1]
 names = ["grid", "lists0", "claims0", "gap0", "assign0", "lists1", "claims1", "gap1", "assign1"]
 d = np.stack([t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2], t[:, 4] - t[:, 3], t[:, 5] - t[:, 4],
               np.where(t[:, 6] > 0, t[:, 6] - t[:, 5], 0), np.where(t[:, 7] > 0, t[:, 7] - t[:, 6], 0),
