@@ -160,6 +160,12 @@ constexpr int kRegList = COEB_MATCH_REGLIST;        // list head kept in registe
 #ifndef COEB_MATCH_RL1024
 #define COEB_MATCH_RL1024 12
 #endif
+#ifndef COEB_LOCAL_QPT
+#define COEB_LOCAL_QPT 2                           // k_match_local: points per thread with register list heads
+#endif
+#ifndef COEB_LOCAL_RL
+#define COEB_LOCAL_RL 8                            // ... and the entries held per point
+#endif
 
 struct QueryWin {
     bool ok, chk;
@@ -1024,7 +1030,42 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
     bool seq = force_seq || s_flag[0];
     int iters = 0;
     // ---- phase 2: claims by fixpoint iteration ----
+    // The thread's first LQ points (tid, tid + 1024, ...) keep the first LR entries of their
+    // lists in registers across the iterations, as k_match's claims do; the rest are read from
+    // the global lists in each iteration
+    constexpr int LQ = COEB_LOCAL_QPT, LR = COEB_LOCAL_RL;
+    auto walk = [&](uint32_t v, int q, int& bestDist, int& bestLevel, int& bestDist2, int& bestLevel2, int& bestIdx) {
+        const int i2 = (int)(v & ((1u << kIdxBits) - 1));
+        if (L.owner[i2] < q) return;                       // taken by an earlier point
+        const int dist = (int)(v >> kLocKeyDist), oct = (int)((v >> kLocKeyOct) & 0xF);
+        if (dist < bestDist) {
+            bestDist2 = bestDist; bestDist = dist;
+            bestLevel2 = bestLevel; bestLevel = oct; bestIdx = i2;
+        } else if (dist < bestDist2) {
+            bestLevel2 = oct; bestDist2 = dist;
+        }
+    };
+    auto decide = [&](int bestDist, int bestLevel, int bestDist2, int bestLevel2, int bestIdx) {
+        return bestDist <= TH_HIGH && !(bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2)
+                   ? bestIdx : -1;
+    };
     if (!seq) {
+        uint32_t rl[LQ][LR];
+        int rm[LQ];
+#pragma unroll
+        for (int u = 0; u < LQ; u++) {
+            const int q = tid + u * kMThreads;
+            rm[u] = -1;
+            if (q < nq) {
+                const int qn = L.qn[q];
+                if (qn >= 0) {
+                    rm[u] = qn & 0xFFFF;
+                    const uint32_t* lst = b.lists + (int64_t)q * kCQ;
+#pragma unroll
+                    for (int e = 0; e < LR; e++) rl[u][e] = e < rm[u] ? lst[e] : 0u;
+                }
+            }
+        }
         for (int it = 0;; it++) {
             iters = it + 1;
             for (int c = tid; c < n; c += kMThreads) L.owner[c] = 0x7fffffff;
@@ -1037,27 +1078,33 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
                 }
                 __syncthreads();
             }
-            for (int q = tid; q < nq; q += kMThreads) {
+#pragma unroll
+            for (int u = 0; u < LQ; u++) {
+                const int q = tid + u * kMThreads;
+                if (q < nq) {
+                    int res = -1;
+                    if (rm[u] >= 0) {
+                        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+#pragma unroll
+                        for (int e = 0; e < LR; e++)
+                            if (e < rm[u]) walk(rl[u][e], q, bestDist, bestLevel, bestDist2, bestLevel2, bestIdx);
+                        const uint32_t* lst = b.lists + (int64_t)q * kCQ;
+                        for (int e = LR; e < rm[u]; e++) walk(lst[e], q, bestDist, bestLevel, bestDist2, bestLevel2, bestIdx);
+                        res = decide(bestDist, bestLevel, bestDist2, bestLevel2, bestIdx);
+                    }
+                    if (it == 0 || res != L.res[q]) s_flag[1] = 1;
+                    L.res[q] = res;
+                }
+            }
+            for (int q = tid + LQ * kMThreads; q < nq; q += kMThreads) {
                 const int qn = L.qn[q];
                 int res = -1;
                 if (qn >= 0) {
                     const int m = qn & 0xFFFF;
                     const uint32_t* lst = b.lists + (int64_t)q * kCQ;
                     int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
-                    for (int e = 0; e < m; e++) {
-                        const uint32_t v = lst[e];
-                        const int i2 = (int)(v & ((1u << kIdxBits) - 1));
-                        if (L.owner[i2] < q) continue;             // taken by an earlier point
-                        const int dist = (int)(v >> kLocKeyDist), oct = (int)((v >> kLocKeyOct) & 0xF);
-                        if (dist < bestDist) {
-                            bestDist2 = bestDist; bestDist = dist;
-                            bestLevel2 = bestLevel; bestLevel = oct; bestIdx = i2;
-                        } else if (dist < bestDist2) {
-                            bestLevel2 = oct; bestDist2 = dist;
-                        }
-                    }
-                    if (bestDist <= TH_HIGH && !(bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2))
-                        res = bestIdx;
+                    for (int e = 0; e < m; e++) walk(lst[e], q, bestDist, bestLevel, bestDist2, bestLevel2, bestIdx);
+                    res = decide(bestDist, bestLevel, bestDist2, bestLevel2, bestIdx);
                 }
                 if (it == 0 || res != L.res[q]) s_flag[1] = 1;
                 L.res[q] = res;

@@ -8,7 +8,7 @@ k=$1; shift
 for v in "$@"; do
   case "$v" in *=*) export "$v"; echo "export $v"; continue;; esac
   if [ "$v" = main ]; then unset COEB_LIB_PATH; else export COEB_LIB_PATH=$PWD/coeb-slam_amd/$v; fi
-  timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras --no-e2e > gpurun_out/kab.log 2>&1
+  timeout -k 10 200 python bench.py --config ${KAB_CONFIG:-A} --steps 10 --warmup 2 --no-cpu-baseline --no-extras --no-e2e > gpurun_out/kab.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "$v rc=$rc"; tail -5 gpurun_out/kab.log; exit $rc; fi
   python - "$v" "$k" <<'PY'
