@@ -217,6 +217,68 @@ def effective_cpus(info, cpus):
     return n
 
 
+def idle_cpus(cpus, k=3, window=0.5):
+    """The k CPUs of the affinity mask that were idlest over `window` seconds (/proc/stat idle +
+    iowait deltas), one per physical core where the topology says so: on a shared host cpus[0]
+    can carry other load (round 4's driver run measured 44 frames/s single-thread where the
+    builder's run on the same box type measured 79), so the single-thread legs run on measured-idle
+    CPUs.  Returns [(cpu, idle_fraction)], idlest first."""
+    def snap():
+        st = {}
+        try:
+            with open("/proc/stat") as f:
+                for ln in f:
+                    if ln.startswith("cpu") and ln[3:4].isdigit():
+                        v = ln.split()
+                        nums = [int(x) for x in v[1:]]
+                        st[int(v[0][3:])] = (nums[3] + (nums[4] if len(nums) > 4 else 0), sum(nums[:8]))
+        except (OSError, ValueError):
+            pass
+        return st
+    a = snap()
+    time.sleep(window)
+    b = snap()
+    idle = []
+    for c in cpus:
+        if c in a and c in b and b[c][1] > a[c][1]:
+            idle.append((c, (b[c][0] - a[c][0]) / (b[c][1] - a[c][1])))
+    if not idle:
+        return [(c, None) for c in cpus[:k]]
+    idle.sort(key=lambda t: -t[1])
+
+    def core_of(c):
+        try:
+            with open("/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list" % c) as f:
+                return f.read().strip()
+        except OSError:
+            return str(c)
+    out, cores = [], set()
+    for c, fr in idle:
+        if core_of(c) in cores:
+            continue
+        cores.add(core_of(c))
+        out.append((c, round(fr, 3)))
+        if len(out) == k:
+            break
+    return out
+
+
+def _pinned_legs(run_leg, cpu_list, seconds):
+    """run_leg(cpu, seconds) -> (median s/frame, frames) on each CPU of cpu_list (the timing thread
+    pinned there); returns the median of the per-CPU medians and the per-CPU records."""
+    per = []
+    mask = os.sched_getaffinity(0)
+    try:
+        for c, fr in cpu_list:
+            os.sched_setaffinity(0, {c})
+            med, n = run_leg(c, seconds)
+            per.append(dict(cpu=c, idle_before=fr, frames_per_s=round(1.0 / med, 3), frames=n))
+    finally:
+        os.sched_setaffinity(0, mask)
+    vals = sorted(p["frames_per_s"] for p in per)
+    return vals[len(vals) // 2], per
+
+
 def _single_thread_leg(O, lib_path, cfg, ex_args, frames, depth, cam, cpu, seconds, min_frames, warmup=20):
     """SURVEY.md s8(d)'s single-thread leg on one oracle build: `warmup` untimed frames, then
     extract + ComputeStereoFromRGBD + SearchByProjection (retry at 2*th) per frame, median time."""
@@ -266,26 +328,32 @@ def cpu_baseline(cfg, seconds=9.0, min_frames=30):
     frames = synth.make_frames(w, h, 64, seed=5151)
     native = os.path.join(ROOT, "oracle", "liborb_oracle_native.so")
     scalar = os.path.join(ROOT, "oracle", "liborb_oracle_scalar.so")
-    os.sched_setaffinity(0, {cpus[0]})
+    pick = idle_cpus(cpus, 3)
     try:
         O.LIB, O._lib = native, None
         cam = O.camera(O.Extractor(*ex_args), w, h, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY,
                        synth.TUM_BF)
-        med, n = _single_thread_leg(O, native, cfg, ex_args, frames, depth, cam, cpus[0], seconds, min_frames)
-        med_s, n_s = _single_thread_leg(O, scalar, cfg, ex_args, frames, depth, cam, cpus[0], 0.6 * seconds,
-                                        min_frames)
+        val, per = _pinned_legs(lambda c, sec: _single_thread_leg(O, native, cfg, ex_args, frames, depth, cam, c, sec,
+                                                                  min_frames), pick, seconds / len(pick))
+        val_s, per_s = _pinned_legs(lambda c, sec: _single_thread_leg(O, scalar, cfg, ex_args, frames, depth, cam, c,
+                                                                      sec, min_frames), pick, 0.6 * seconds / len(pick))
     finally:
-        os.sched_setaffinity(0, set(cpus))
         O.LIB, O._lib = native, None
-    out = dict(value=round(1.0 / med, 3), unit="frames/s", cores=1, kind="port",
-               sample="%d consecutive %dx%d synthetic frames after 20 warm-up frames, oracle (-O3 -march=native) "
-                      "single thread pinned to CPU %d: extract + ComputeStereoFromRGBD + SearchByProjection (th 15, "
-                      "retry 30); median %.2f ms/frame" % (n, w, h, cpus[0], med * 1e3))
+    vals = [p["frames_per_s"] for p in per]
+    out = dict(value=val, unit="frames/s", cores=1, kind="port",
+               sample="single thread pinned to each of the %d idlest CPUs (%s; idle fraction measured over 0.5 s "
+                      "before), per CPU >= %d consecutive %dx%d synthetic frames after 20 warm-up frames, oracle "
+                      "(-O3 -march=native): extract + ComputeStereoFromRGBD + SearchByProjection (th 15, retry 30); "
+                      "value = median of the per-CPU median frame rates" % (len(pick), ", ".join(str(c) for c, _ in pick),
+                                                                           min_frames, w, h),
+               spread=dict(min=min(vals), max=max(vals), per_cpu=per))
     out.update(info)
     out["caveat"] = CPU_CAVEAT
-    out["scalar_build"] = dict(value=round(1.0 / med_s, 3), unit="frames/s", cores=1, kind="port",
-                               sample="the same leg on the plain scalar build (-O3 -march=x86-64 -fno-tree-vectorize "
-                                      "-fno-tree-slp-vectorize), %d frames, median %.2f ms/frame" % (n_s, med_s * 1e3))
+    vals_s = [p["frames_per_s"] for p in per_s]
+    out["scalar_build"] = dict(value=val_s, unit="frames/s", cores=1, kind="port",
+                               sample="the same legs on the plain scalar build (-O3 -march=x86-64 -fno-tree-vectorize "
+                                      "-fno-tree-slp-vectorize), median of the per-CPU medians",
+                               spread=dict(min=min(vals_s), max=max(vals_s), per_cpu=per_s))
     out["all_cores"] = cpu_baseline_parallel(O, cfg, frames, depth, cam, effective_cpus(info, cpus))
     return out
 
@@ -347,27 +415,29 @@ def cpu_chain_baseline(cfg, seconds=15.0, min_frames=20):
     nfr = 64
     gray, boxes = synth.tracking_sequence(w, h, nfr, first=0)
     rgb, dep = synth.rgbd_from_gray(gray)
-    os.sched_setaffinity(0, {cpus[0]})
-    try:
+    def leg(cpu, sec):
         cl = ChainCpu(O, cfg, rgb, dep, boxes)
         for i in range(CHAIN_WARMUP):
             cl.step(i)
         times = []
-        t_end = time.perf_counter() + seconds
+        t_end = time.perf_counter() + sec
         i = CHAIN_WARMUP
         while (time.perf_counter() < t_end or len(times) < min_frames) and i < nfr:
             t0 = time.perf_counter()
             cl.step(i)
             times.append(time.perf_counter() - t0)
             i += 1
-    finally:
-        os.sched_setaffinity(0, set(cpus))
-    med = float(np.median(times))
-    out = dict(value=round(1.0 / med, 3), unit="frames/s", cores=1, kind="port",
-               sample="%d consecutive %dx%d frames of the synthetic tracking sequence, oracle (-O3 -march=native) "
-                      "single thread pinned to CPU %d: the full GrabImageRGBD loop per frame (conversions, "
-                      "ProcessMovingObject, blur flags, masked extract, stereo, motion model, TrackLocalMap); median "
-                      "%.2f ms/frame" % (len(times), w, h, cpus[0], med * 1e3))
+        return float(np.median(times)), len(times)
+    pick = idle_cpus(cpus, 3)
+    val, per = _pinned_legs(leg, pick, seconds / len(pick))
+    vals = [p["frames_per_s"] for p in per]
+    out = dict(value=val, unit="frames/s", cores=1, kind="port",
+               sample="single thread pinned to each of the %d idlest CPUs (%s), per CPU >= %d consecutive %dx%d frames "
+                      "of the synthetic tracking sequence after %d warm-up frames, oracle (-O3 -march=native): the full "
+                      "GrabImageRGBD loop per frame (conversions, ProcessMovingObject, blur flags, masked extract, "
+                      "stereo, motion model, TrackLocalMap); value = median of the per-CPU median frame rates"
+                      % (len(pick), ", ".join(str(c) for c, _ in pick), min_frames, w, h, CHAIN_WARMUP),
+               spread=dict(min=min(vals), max=max(vals), per_cpu=per))
     out.update(info)
     out["caveat"] = CPU_CAVEAT
     nthr = effective_cpus(info, cpus)

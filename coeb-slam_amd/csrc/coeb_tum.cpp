@@ -17,6 +17,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <locale.h>
+#include <stdlib.h>
 #include <unordered_map>
 #include <vector>
 
@@ -47,8 +49,17 @@ void fields(const char* t, size_t b, size_t e, std::vector<Field>& out)
     }
 }
 
+// The "C" numeric locale, created once: Python's float() does not depend on the locale, so a
+// host that called setlocale(LC_NUMERIC, "de_DE") must still read '1305031102.175304'.
+locale_t c_locale()
+{
+    static const locale_t loc = newlocale(LC_ALL_MASK, "C", (locale_t)0);
+    return loc;
+}
+
 // A decimal floating-point literal (optional sign, digits with at most one '.', optional
 // exponent, or inf / infinity / nan), as a stamp field must be.  Hex forms are refused.
+// Parsed in the "C" locale whatever the process locale is.
 bool parse_stamp(const char* t, const Field& f, double* v)
 {
     const size_t n = f.e - f.b;
@@ -59,7 +70,9 @@ bool parse_stamp(const char* t, const Field& f, double* v)
     const char* s = buf + ((buf[0] == '+' || buf[0] == '-') ? 1 : 0);
     if ((s[0] == '0' && (s[1] == 'x' || s[1] == 'X'))) return false;
     char* end = nullptr;
-    *v = std::strtod(buf, &end);
+    const locale_t loc = c_locale();
+    if (loc == (locale_t)0) return false;
+    *v = strtod_l(buf, &end, loc);
     return end == buf + n;
 }
 

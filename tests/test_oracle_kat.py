@@ -537,6 +537,60 @@ def test_tum_association_golden():
         assert all(len(v) >= 1 for v in rgb.values())
 
 
+def test_tum_association_reference_files():
+    """The reference's own association outputs (Examples/RGB-D/associations/*.txt: 11 TUM
+    sequences, 18,520 pairs that associate.py:49-102 produced with offset 0, max_difference 0.02),
+    re-derived through the C-ABI: each file is read with coeb_tum_read_list, split into its rgb
+    and depth stamp lists, and re-associated with coeb_tum_associate.  Greedy selection restricted
+    to the matched stamps takes exactly the original pairs (every candidate among them is a
+    candidate of the full run at the same rank, and the pairs that blocked it there are matched
+    pairs too), so every file must come back identical, in its own order.  Fixture packed by
+    tests/golden/make_tum_assoc_files.py."""
+    import coeb_front
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "tum_assoc_files.npz"))
+    assert len(z.files) == 11
+    total = 0
+    for name in sorted(z.files):
+        text = z[name].tobytes().decode()
+        lines = [ln.split() for ln in text.splitlines() if ln.strip() and not ln.startswith("#")]
+        want = [(float(r[0]), float(r[2])) for r in lines]
+        # the association file itself through the C-ABI reader: stamp = rgb stamp, data = the rest
+        assoc = coeb_front.tum_read_file_list(text)
+        assert list(assoc.keys()) == [a for a, _ in want], name
+        rgb_text = "".join("%s %s\n" % (a, v[0]) for a, v in zip((r[0] for r in lines), assoc.values()))
+        depth_text = "".join("%s %s\n" % (v[1], v[2]) for v in assoc.values())
+        rgb, depth = coeb_front.tum_read_file_list(rgb_text), coeb_front.tum_read_file_list(depth_text)
+        assert len(rgb) == len(depth) == len(lines), name
+        got = coeb_front.tum_associate(rgb, depth, 0.0, 0.02)
+        assert got == want, name
+        total += len(got)
+    assert total == 18520, total
+
+
+def test_tum_stamp_parse_ignores_process_locale():
+    """coeb_tum_read_list parses stamps in the "C" locale, as Python's float() does, even after
+    the host process switched LC_NUMERIC to a comma-decimal locale."""
+    import ctypes as C
+    import ctypes.util
+    import coeb_front
+    libc = C.CDLL(ctypes.util.find_library("c"))
+    libc.setlocale.restype = C.c_char_p
+    LC_NUMERIC = 1
+    old = libc.setlocale(LC_NUMERIC, None)
+    switched = None
+    for loc in (b"de_DE.UTF-8", b"de_DE.utf8", b"fr_FR.UTF-8", b"ru_RU.UTF-8"):
+        switched = libc.setlocale(LC_NUMERIC, loc)
+        if switched:
+            break
+    try:
+        lst = coeb_front.tum_read_file_list("1305031102.175304 rgb/a.png\n1305031102.211214 rgb/b.png\n")
+        assert list(lst.keys()) == [1305031102.175304, 1305031102.211214]
+    finally:
+        libc.setlocale(LC_NUMERIC, old)
+    if not switched:
+        pytest.skip("no comma-decimal locale installed: parsed in the default locale only")
+
+
 def test_tum_association_edge_cases():
     """The association's definition on hand cases: greedy by (difference, a, b), each stamp once,
     the strict < max_difference bound, offset applied to the second list, ties on the difference
