@@ -1137,6 +1137,38 @@ __device__ __forceinline__ void fast_prefetch(const FastCellGeom& G, FastRegs& R
     }
 }
 
+#ifndef COEB_FAST_DMA
+#define COEB_FAST_DMA 1        // 96-B slab rows staged by LDS-DMA (global_load_lds_dwordx4)
+#endif
+// Zero chunks of the LDS-DMA staging (the M columns of a 96-B slab row).
+__device__ __attribute__((aligned(64))) const uint8_t g_fast_zero[64] = {0};
+
+// LDS-DMA staging of a cell ROI into 96-B slab rows (RB = kFastRowBytesM, rh <= 48): slab row r is
+// six 16-byte chunks, chunks 0..2 the image bytes x0 - 1 + 16 k .. of row y0 + r (byte-granular
+// source address, so slab byte j = ROI column j - 1 with no realignment and 16-byte aligned LDS
+// writes), chunks 3..5 zeros from g_fast_zero (the M columns 48..95).  A wave-instruction writes
+// 64 consecutive chunks (1 KiB); chunks past row rh - 1 are masked off.  No VGPR staging, no
+// ds_write: the register-staged form's unaligned ds_write_b128 stores were replayed by the LDS
+// (SQ_LDS_UNALIGNED_STALL, profiles/r04/ab8).  Completion: vmcnt (fast_dma_wait).
+__device__ __forceinline__ void fast_dma(const FastCellGeom& G, uint8_t* roi)
+{
+    typedef __attribute__((address_space(3))) void* lds_vp;
+    const int lane = lane_id();
+    const int nq = 6 * G.rh;
+    const uint8_t* row0 = G.img + (int64_t)G.y0 * G.pitch + (G.x0 - 1);
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        if (64 * i < nq) {
+            const int q = 64 * i + lane;
+            const int r = (q * 171) >> 10;                 // q / 6 for q < 512
+            const int k = q - 6 * r;
+            const uint8_t* src = k < 3 ? row0 + r * G.pitch + 16 * k : g_fast_zero;
+            if (q < nq) __builtin_amdgcn_global_load_lds((const void*)src, (lds_vp)(roi + 1024 * i), 16, 0, 0);
+        }
+    }
+}
+__device__ __forceinline__ void fast_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 template <int RB>
 __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs& R, uint8_t* roi)
 {
@@ -1156,7 +1188,12 @@ __device__ __forceinline__ void fast_stage(const FastCellGeom& G, const FastRegs
         if (r + 32 < G.rh) __builtin_memcpy(d + 32 * RB, &R.v2, 16);
         if constexpr (RB == kFastRowBytesM) {
             // then zero the rows' M columns 48..95 (after every row's data: the stores above
-            // spill into them), three lanes per row
+            // spill into them), three lanes per row.  Per lane the data and zero stores never
+            // overlap, so nothing in the compiler's alias analysis keeps them in this order; the
+            // spill of ANOTHER lane's data store does overlap.  The empty asm with a memory clobber
+            // is a scheduling barrier: the zero stores stay after the data stores (one wave's LDS
+            // instructions execute in issue order).
+            asm volatile("" ::: "memory");
             uint8_t* z = roi + r * RB + 48 + 16 * c;
             const uint4 zero = make_uint4(0, 0, 0, 0);
             if (c < 3 && r < G.rh) *reinterpret_cast<uint4*>(z) = zero;
@@ -1441,14 +1478,17 @@ __global__ __launch_bounds__(kThreads, COEB_FAST_MINWG) void k_fast(const Plan* 
     const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
     const CellDesc c = load_cell(cells, cidx);
     const FastCellGeom G = fast_geom(P, b, f, c);
+    const bool dma = COEB_FAST_DMA && RB == kFastRowBytesM && c.rh <= 48;     // wave-uniform
     FastRegs R;
-    fast_prefetch(G, R);
+    if (dma) fast_dma(G, roi);
+    else fast_prefetch(G, R);
     FC_MARK(t_all);
     FC_MARK(t_st);
-    fast_stage<RB>(G, R, roi);
+    if (dma) fast_dma_wait();
+    else fast_stage<RB>(G, R, roi);
     if (RB == kFastRowBytesM) {
-        // M columns 48..95 of rows 2 .. rh-3 (the 16-byte staging zeroes them itself)
-        if (!G.vec)
+        // M columns 48..95 of rows 2 .. rh-3 (the 16-byte staging and the DMA zero them themselves)
+        if (!G.vec && !dma)
         for (int i = lane; i < 3 * (c.rh - 4); i += 64) {
             const int row = 2 + i / 3;
             reinterpret_cast<uint4*>(Ms + row * RB + 48)[i - 3 * (row - 2)] = make_uint4(0, 0, 0, 0);
@@ -2690,7 +2730,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         oct_lds = plan.oct_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * kl;
     }
     if (const char* e = getenv("COEB_OCT_KL_SMALL")) if (atoi(e) == 0) { oct_kl = plan.oct_kl; oct_lds = plan.oct_lds; }
-    (void)hipFuncSetAttribute((const void*)k_octree<kOctThreads>, hipFuncAttributeMaxDynamicSharedMemorySize, oct_lds);
+    lds_limit_max((const void*)k_octree<kOctThreads>);
     auto octree = [&](hipStream_t st, int l0, int l1) {
         if (l1 <= l0) return;
         prof_begin(prof, "k_octree", st);

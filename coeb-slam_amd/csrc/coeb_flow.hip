@@ -1778,7 +1778,7 @@ int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, in
                 dim3((w + 4 * kGcCols - 1) / (4 * kGcCols), (h + kGcRows - 1) / kGcRows, P), dim3(256), 0, s, d->R, w,
                 h, quality, d->rmax, d->keys, d->nkeys,
                        gf_key_cap(w, h), d->pz);
-    (void)hipFuncSetAttribute((const void*)k_gf_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    lds_limit_max((const void*)k_gf_select);
     FLOW_LAUNCH(d, "k_gf_select", s, k_gf_select, dim3(1, 1, P), dim3(kGfThreads), lds, s, d->keys, d->nkeys, w, h, max_corners,
                        (float)(min_distance * min_distance), cell, d->pts, d->npts, kMaxPts, gf_key_cap(w, h),
                        d->pz);

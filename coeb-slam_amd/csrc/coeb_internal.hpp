@@ -16,6 +16,32 @@
 #pragma once
 #include <stdint.h>
 #include <hip/hip_runtime.h>
+#include <mutex>
+#include <set>
+#include <utility>
+
+// Raise a kernel's dynamic-LDS limit once per (kernel, device), to the most any launch may use
+// (the CU's 160 KB; the launch's own size still sets the occupancy).  The attribute is
+// process-wide: setting it per launch to that launch's size let another host thread's launch of
+// the same kernel with a larger size run under a smaller limit set in between.
+constexpr int kLdsLimit = 160 * 1024;
+inline void lds_limit_max(const void* kern)
+{
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    if (!done.insert({kern, dev}).second) return;
+    // the device's per-workgroup maximum less the kernel's static LDS
+    int lim = kLdsLimit, v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess && v > 0)
+        lim = v < lim ? v : lim;
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, kern) == hipSuccess) lim -= (int)fa.sharedSizeBytes;
+    if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, lim) != hipSuccess)
+        (void)hipGetLastError();        // not sticky: the launch itself reports a size it cannot take
+}
 
 #define COEB_MAXL 16
 #define COEB_MAXBOX 16

@@ -1412,7 +1412,7 @@ int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int b
         const bool lists_lds = lds_cur && !(le && atoi(le) == 0);
         const size_t lds_l = match_lds_bytes(b.cur_stride, 0, lists_lds, nullptr);
         auto gl = [&](auto kern) {
-            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l);
+            lds_limit_max((const void*)kern);
             hipLaunchKernelGGL(kern, dim3(P, nsplit), dim3(1024), lds_l, s, cam, b, th, bmono);
         };
         prof_begin(prof, "k_match_lists", s);
@@ -1423,7 +1423,7 @@ int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int b
         if (!(fe && atoi(fe) != 0)) lds_cur = false;
     }
     auto go = [&](auto kern, size_t lds) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        lds_limit_max((const void*)kern);
         hipLaunchKernelGGL(kern, dim3(P), dim3(nt), lds - 256, s, cam, b, th, bmono, check_ori, retry_below, force_seq,
                            nsplit);
     };
@@ -1457,10 +1457,10 @@ int launch_match_local(const MatchCam& cam, const LocalBufsHost& h, float th, fl
     const size_t lds_min = match_lds_bytes(cs, qs, false, nullptr) + 256;
     prof_begin(prof, "k_match_local", s);
     if (lds_full <= 160 * 1024) {
-        (void)hipFuncSetAttribute((const void*)k_match_local<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_full);
+        lds_limit_max((const void*)k_match_local<true>);
         hipLaunchKernelGGL(k_match_local<true>, dim3(P), dim3(kMThreads), lds_full - 256, s, cam, b, th, nnratio, force_seq);
     } else if (lds_min <= 160 * 1024) {
-        (void)hipFuncSetAttribute((const void*)k_match_local<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_min);
+        lds_limit_max((const void*)k_match_local<false>);
         hipLaunchKernelGGL(k_match_local<false>, dim3(P), dim3(kMThreads), lds_min - 256, s, cam, b, th, nnratio, force_seq);
     } else {
         prof_end(prof, s);
@@ -1486,11 +1486,11 @@ int launch_match_kf(const MatchCam& cam, const KfBufsHost& h, float th, int orb_
     const size_t lds_min = match_lds_bytes(cs, qs, false, nullptr) + 256;
     prof_begin(prof, "k_match_kf", s);
     if (lds_full <= 160 * 1024) {
-        (void)hipFuncSetAttribute((const void*)k_match_kf<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_full);
+        lds_limit_max((const void*)k_match_kf<true>);
         hipLaunchKernelGGL(k_match_kf<true>, dim3(1), dim3(kMThreads), lds_full - 256, s, cam, b, th, orb_dist, check_ori,
                            force_seq);
     } else if (lds_min <= 160 * 1024) {
-        (void)hipFuncSetAttribute((const void*)k_match_kf<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_min);
+        lds_limit_max((const void*)k_match_kf<false>);
         hipLaunchKernelGGL(k_match_kf<false>, dim3(1), dim3(kMThreads), lds_min - 256, s, cam, b, th, orb_dist, check_ori,
                            force_seq);
     } else {

@@ -405,6 +405,55 @@ def test_batch_pipeline_matches_oracle(oracle_mod, ex):
         bp.close()
 
 
+@pytest.mark.parametrize("mode", ["default", "sequential", "nosplit"])
+def test_batch_small_split_lists_matches_oracle(oracle_mod, ex, monkeypatch, mode):
+    """Few pairs per launch (P < 128): the candidate lists come from k_match_lists split over
+    several workgroups per pair, and k_match starts at the claims without the current frame staged
+    in LDS.  Its late paths -- list overflow on repetitive texture (sequential fallback), the
+    literal sequential pass (COEB_MATCH_SEQUENTIAL=1) and the 2*th retry of a frame whose
+    prediction is 180 degrees off -- must equal the oracle frame by frame; COEB_MATCH_SPLIT=0
+    runs the unsplit kernel on the same batch."""
+    from coeb_front.pipeline import BatchPipeline
+    if mode == "sequential":
+        monkeypatch.setenv("COEB_MATCH_SEQUENTIAL", "1")
+    elif mode == "nosplit":
+        monkeypatch.setenv("COEB_MATCH_SPLIT", "0")
+    F = 7
+    yy, xx = np.indices((480, 640))
+    base = (((yy // 12) + (xx // 12)) % 2 * 200 + 30).astype(np.int16)
+    rng = np.random.default_rng(31)
+    fr = np.stack([np.clip(np.roll(base, (f, 2 * f), axis=(0, 1)) + rng.integers(-6, 7, base.shape), 0, 255)
+                   for f in range(4)] + list(synth.make_frames(640, 480, F - 4, seed=313))).astype(np.uint8)
+    Tcw = np.stack([synth.motion_pose()] * F)
+    Tcw[5] = synth.rotated_pose(180.0, axis=1, t=(0, 0, 0))          # < 20 matches: the 2*th retry runs
+    depth = synth.make_depth(640, 480)
+    cam_o = oracle_mod.camera(ex, 640, 480, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    I4 = np.eye(4, dtype=np.float32)
+    ref = [ex.extract(f) for f in fr]
+    bp = BatchPipeline(640, 480, F)
+    try:
+        bp.load(fr, Tcw=Tcw)
+        for th in (15.0, 60.0):
+            bp.run(th=th)
+            bp.synchronize()
+            out, matches, nms = bp.results()
+            for f in range(F):
+                assert_same(out[f][0], out[f][1], ref[f]["kps"], ref[f]["desc"], "split f%d" % f)
+                if f == 0:
+                    continue
+                last = oracle_mod.mapframe_from_extraction(ref[f - 1]["kps"], ref[f - 1]["desc"], depth, synth.TUM_FX,
+                                                           synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+                ur, _ = oracle_mod.stereo_from_rgbd(ref[f]["kps"], depth, synth.TUM_BF)
+                nm, m = oracle_mod.search_by_projection(cam_o, ref[f]["kps"], ref[f]["desc"], ur, last, Tcw[f], I4, th)
+                if nm < 20:                                          # Tracking.cc:954-958
+                    nm, m = oracle_mod.search_by_projection(cam_o, ref[f]["kps"], ref[f]["desc"], ur, last, Tcw[f],
+                                                            I4, 2 * th)
+                assert nms[f] == nm and np.array_equal(matches[f], m), (mode, th, f, nms[f], nm)
+            assert nms[5] < 20
+    finally:
+        bp.close()
+
+
 def test_batch_track_pose_matches_oracle(oracle_mod, ex):
     """BASELINE configs[4] slice on the device batch: extract + SearchByProjection + the
     TrackWithMotionModel PoseOptimization (Tracking.cc:947-964) for every pair, against the
