@@ -174,7 +174,7 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
         if (l == 0) g.pyr_off = -1;
         else { g.pyr_off = pyr; pyr = align256(pyr + (int64_t)g.pitch * g.h); }
         g.blur_off = blur;
-        blur = align256(blur + (int64_t)g.bpitch * g.h);
+        blur = align256(blur + (int64_t)g.bpitch * ((g.h + 7) & ~7));    // whole 8-row tiles
         if (l > 0) {
             while (rtab.size() % 4) rtab.push_back(0);     // 16-byte aligned table rows
             g.rtab_off = (int)rtab.size();
@@ -545,8 +545,8 @@ int extract_bufs(coeb_ctx* c, int F, ExtractBufs& b)
     uint32_t *cand, *keys, *lvl_kp;
     coeb_keypoint* kps;
     DynMask* dyn;
-    if ((rc = ensure(c, "pyr", (size_t)F * P.pyr_stride, &pyr))) return rc;
-    if ((rc = ensure(c, "blur", (size_t)F * P.blur_stride, &blur))) return rc;
+    if ((rc = ensure(c, "pyr", (size_t)F * P.pyr_stride + 4096, &pyr))) return rc;
+    if ((rc = ensure(c, "blur", (size_t)F * P.blur_stride + 4096, &blur))) return rc;
     if ((rc = ensure(c, "cand_n", (size_t)F * P.ncells, &cand_n))) return rc;
     if ((rc = ensure(c, "cand", (size_t)F * P.ncells * P.cell_cap, &cand))) return rc;
     if ((rc = ensure(c, "keys", (size_t)F * 2 * P.kbuf_stride, &keys))) return rc;
@@ -1982,7 +1982,28 @@ int coeb_debug_read(coeb_ctx* c, const char* what, int f, void* host, size_t byt
     size_t n = 0;
     std::string w(what);
     if (w == "pyr") { src = (const uint8_t*)c->bufs["pyr"].p + (size_t)f * P.pyr_stride; n = P.pyr_stride; }
-    else if (w == "blur") { src = (const uint8_t*)c->bufs["blur"].p + (size_t)f * P.blur_stride; n = P.blur_stride; }
+    else if (w == "blur") {
+        // the blurred levels row-major at their pitch, each 256-B aligned (the device copy is tiled,
+        // blur_tile_off)
+        std::vector<uint8_t> raw(P.blur_stride);
+        HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
+        HIP_TRY(c, hipMemcpy(raw.data(), (const uint8_t*)c->bufs["blur"].p + (size_t)f * P.blur_stride, raw.size(),
+                             hipMemcpyDeviceToHost));
+        std::vector<uint8_t> rm;
+        size_t off = 0;
+        for (int l = 0; l < P.L; l++) {
+            const LevelGeom& g = P.lv[l];
+            rm.resize(off + (size_t)g.bpitch * g.h);
+            for (int y = 0; y < g.h; y++)
+                for (int x = 0; x < g.bpitch; x++)
+                    rm[off + (size_t)y * g.bpitch + x] = raw[g.blur_off + blur_tile_off(x, y, g.bpitch)];
+            off = ((off + (size_t)g.bpitch * g.h) + 255) & ~(size_t)255;
+        }
+        rm.resize(off);
+        if (size_out) *size_out = rm.size();
+        if (host && bytes) memcpy(host, rm.data(), std::min(bytes, rm.size()));
+        return COEB_OK;
+    }
     else if (w == "cand_n") { src = (const uint8_t*)c->bufs["cand_n"].p + (size_t)f * P.ncells * 4; n = (size_t)P.ncells * 4; }
     else if (w == "lvl_n") { src = (const uint8_t*)c->bufs["lvl_n"].p + (size_t)f * P.L * 4; n = (size_t)P.L * 4; }
     else if (w == "lvl_kp") { src = (const uint8_t*)c->bufs["lvl_kp"].p + (size_t)f * P.lvl_stride * 4; n = (size_t)P.lvl_stride * 4; }

@@ -26,6 +26,14 @@ __device__ __forceinline__ int lane_id() { return __lane_id(); }
 // compiler treats it as divergent, and everything indexed by it (cell descriptors, level
 // geometry) becomes per-lane vector loads and VGPR arithmetic.
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+// orders one wave's LDS accesses (the compiler and the LDS queue), no workgroup barrier
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // native vector: stays in VGPRs
 
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
@@ -570,7 +578,7 @@ __global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, E
                 // byte 2 of each accumulator = (acc + 2^15) >> 16 (acc + 2^15 < 2^24)
                 const uint32_t p01 = __builtin_amdgcn_perm(a1, a0, 0x0c0c0602u);
                 const uint32_t p23 = __builtin_amdgcn_perm(a3, a2, 0x06020c0cu);
-                *reinterpret_cast<uint32_t*>(dst + (int64_t)y * dp + x) = p01 | p23;
+                *reinterpret_cast<uint32_t*>(dst + blur_tile_off(x, y, dp)) = p01 | p23;
             }
         }
     }
@@ -590,8 +598,15 @@ __device__ __forceinline__ int reflect_row(int r, int h)
     return rr < 0 ? 0 : rr;
 }
 
+constexpr int kBlurQuad = 4 * kBlurCols;     // columns of one k_blur_rows wave item (14 tiles of 16)
+static_assert(kBlurQuad % 16 == 0, "a wave item must cover whole 16-column tiles");
+
 __global__ __launch_bounds__(kThreads) void k_blur_rows(const Plan* __restrict__ P, ExtractBufs b, BlurWork bw)
 {
+#if COEB_BLUR_TILED
+    // 8 output rows of the wave item, transposed through LDS into whole 128-B tile lines
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kWaves][8 * kBlurQuad];
+#endif
     const int2 bxy = block_xy();
     const int f = bxy.y;
     const int item = bw.item0 + bxy.x * kWaves + wave_id();
@@ -607,6 +622,10 @@ __global__ __launch_bounds__(kThreads) void k_blur_rows(const Plan* __restrict__
     const int y0 = band * bw.brows, y1 = min(h, y0 + bw.brows);
     const int x = (quad * 4 + grp) * kBlurCols - 4 + gl * 4;
     const bool produce = gl >= 1 && gl <= 14 && x < w;
+#if COEB_BLUR_TILED
+    const int xbase = quad * kBlurQuad;                            // first column of the item (16-aligned)
+    uint8_t* tl = s_tile[wave_id()];
+#endif
     // Every lane loads one dword at column a and picks its 4 columns' bytes with the u16-pair
     // perms below: a = x inside the level; at the edges a is moved so that the REFLECT_101
     // columns reflect101(x + q) all fall in [a, a + 3] (w >= 5), so no lane takes a byte path.
@@ -680,11 +699,37 @@ __global__ __launch_bounds__(kThreads) void k_blur_rows(const Plan* __restrict__
             a3 = __builtin_amdgcn_udot2(R01, W_r01_3, a3, false);
             a3 = __builtin_amdgcn_udot2(R23, W_r23_3, a3, false);
             const int y = y0 - 6 + i;                                  // uniform
+#if COEB_BLUR_TILED
+            // row y into the item's LDS rows; after every 8th row (tile rows start at multiples of 8:
+            // y0 is) the 8 rows leave as whole tile lines, 16 B per lane, consecutive lanes
+            // consecutive bytes (a tile row's tiles are adjacent), 1.75 KiB in two instructions.
+            // Storing each row straight into the tiles (14 partial lines per instruction) took
+            // k_blur_rows 0.487 -> 0.829 ms per 1025-frame launch (profiles/r05/s4).
+            if (produce) {
+                const uint32_t p01 = __builtin_amdgcn_perm(a1, a0, 0x0c0c0602u);
+                const uint32_t p23 = __builtin_amdgcn_perm(a3, a2, 0x06020c0cu);
+                *reinterpret_cast<uint32_t*>(tl + (y & 7) * kBlurQuad + (x - xbase)) = p01 | p23;
+            }
+            if ((y & 7) == 7 || y == y1 - 1) {
+                wave_sync_lds();
+                const int so = __builtin_amdgcn_readfirstlane((int)blur_tile_off(0, y & ~7, dp));
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    const int c = lane + 64 * k;                           // chunk: tile c >> 3, row c & 7
+                    if (c < kBlurQuad / 2 && xbase + 16 * (c >> 3) < dp) {
+                        const u32x4 v = *reinterpret_cast<const u32x4*>(tl + (c & 7) * kBlurQuad + 16 * (c >> 3));
+                        __builtin_amdgcn_raw_buffer_store_b128(v, rd, (xbase >> 4) * 128 + 16 * c, so, 0);
+                    }
+                }
+                wave_sync_lds();
+            }
+#else
             if (produce) {
                 const uint32_t p01 = __builtin_amdgcn_perm(a1, a0, 0x0c0c0602u);
                 const uint32_t p23 = __builtin_amdgcn_perm(a3, a2, 0x06020c0cu);
                 __builtin_amdgcn_raw_buffer_store_b32(p01 | p23, rd, x, __builtin_amdgcn_readfirstlane(y * dp), 0);
             }
+#endif
         }
     }
 }
@@ -810,12 +855,6 @@ static_assert(kFastRowBytesM * 64 <= 4 * 4096 && kFastRowBytes * 64 <= 4 * 4096,
 #define COEB_FAST_PK 0
 #endif
 
-__device__ __forceinline__ void wave_sync_lds()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // FAST_t's first rejection stage (features2d/fast.cpp): d = tab[p0]|tab[p8]; d &= tab[p2]|tab[p10];
 // d &= tab[p4]|tab[p12]; d &= tab[p6]|tab[p14]; with tab = 1 (darker than v-t) / 2 (brighter).
@@ -1106,7 +1145,6 @@ struct FastCellGeom {
 
 // ROI prefetch registers: 16-byte path (lane = row (lane >> 2) + 16 i, chunk lane & 3) or
 // word path (lane = row (lane >> 4) + 4 i, word lane & 15).
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // native vector: stays in VGPRs
 struct FastRegs {
     u32x4 v0, v1, v2;                  // 16-byte path only: the word path loads when it stages
 };
@@ -2520,13 +2558,35 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
     }
     uint8_t* slab = s_slab[wv];
     uint32_t* dsl = reinterpret_cast<uint32_t*>(slab + kBlRow * kBlRows * kDescGroup);
-    // per keypoint: blurred patch origin (16-aligned) relative to the frame's blur block
-    const int porg = (int)g.blur_off + (y - 18) * g.bpitch + ((x - 18) & ~15);
     const int xoff = x - ((x - 18) & ~15);        // patch column of the keypoint
     const uint8_t* blur_f = b.blur + (int64_t)f * P->blur_stride;
-    const int bpitch = g.bpitch;
     static_assert(kDescGroup == 2, "staging below is written for 2 patches per step");
     uint4 qa0, qa1, qa2, qb0, qb1, qb2;
+#if COEB_BLUR_TILED
+    // Patch = rows y-18 .. y+18 x the 64 bytes from (x-18) & ~15 of the tiled blurred level: 4 tile
+    // columns x (5 or 6) tile rows of 8.  Load e (of 192, three per lane) = tile row e >> 5, tile
+    // column (e >> 3) & 3, row e & 7 inside the tile: 8 consecutive lanes read one whole 128-B
+    // line, so an instruction touches 8 lines (row-major: ~22 half-used ones).  Patch row =
+    // 8 * tile row + (e & 7) - dy; rows outside 0..36 are loaded but not staged.
+    const int ty0 = (y - 18) >> 3, dy = (y - 18) & 7, tymax = ((y + 18) >> 3) - ty0;
+    const int porg = (int)g.blur_off + (int)blur_tile_off((x - 18) & ~15, ty0 * 8, g.bpitch);
+    const int trs = g.bpitch * 8;                 // bytes per tile row
+    const int lo = ((lane >> 3) & 3) * 128 + (lane & 7) * 16;   // the lane's tile column and row
+    const int tr0 = lane >> 5;                    // tile row of load 0 (loads 1, 2: + 2, + 4)
+#define COEB_LOAD_PATCH(t, q0, q1, q2)                                                          \
+    {                                                                                           \
+        const int tt_ = min((t), nk - 1);                                                       \
+        const uint8_t* o_ = blur_f + __builtin_amdgcn_readlane(porg, tt_ * kLpk) + lo;          \
+        const int trs_ = __builtin_amdgcn_readlane(trs, tt_ * kLpk);                            \
+        const int tm_ = __builtin_amdgcn_readlane(tymax, tt_ * kLpk);                           \
+        q0 = *reinterpret_cast<const uint4*>(o_ + min(tr0, tm_) * trs_);                        \
+        q1 = *reinterpret_cast<const uint4*>(o_ + min(tr0 + 2, tm_) * trs_);                    \
+        q2 = *reinterpret_cast<const uint4*>(o_ + min(tr0 + 4, tm_) * trs_);                    \
+    }
+#else
+    // per keypoint: blurred patch origin (16-aligned) relative to the frame's blur block
+    const int porg = (int)g.blur_off + (y - 18) * g.bpitch + ((x - 18) & ~15);
+    const int bpitch = g.bpitch;
     const int e0 = lane, e1 = lane + 64, e2 = min(lane + 128, kBlChunks - 1);
     const int eo0 = (e0 >> 2), eo1 = (e1 >> 2), eo2 = (e2 >> 2);
     const int ec0 = 16 * (e0 & 3), ec1 = 16 * (e1 & 3), ec2 = 16 * (e2 & 3);
@@ -2539,23 +2599,40 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         q1 = *reinterpret_cast<const uint4*>(o_ + eo1 * bpt_ + ec1);                            \
         q2 = *reinterpret_cast<const uint4*>(o_ + eo2 * bpt_ + ec2);                            \
     }
+#endif
     COEB_LOAD_PATCH(0, qa0, qa1, qa2)
     COEB_LOAD_PATCH(1, qb0, qb1, qb2)
     for (int t0 = 0; t0 < nk; t0 += kDescGroup) {
         {
-            // chunk e -> row e >> 2, bytes 16 (e & 3) .. +15 (two 8-byte stores: the pitch is 8-aligned)
-            auto put = [&](uint8_t* base, int e, uint4 v) {
-                uint2* d = reinterpret_cast<uint2*>(base + (e >> 2) * kBlRow + 16 * (e & 3));
+            // a 16-byte chunk into slab row `row`, bytes 16 c .. +15 (two 8-byte stores: the pitch is
+            // 8-aligned)
+            auto put = [&](uint8_t* base, int row, int c, uint4 v) {
+                uint2* d = reinterpret_cast<uint2*>(base + row * kBlRow + 16 * c);
                 d[0] = make_uint2(v.x, v.y);
                 d[1] = make_uint2(v.z, v.w);
             };
             uint8_t* pb = slab + kBlRow * kBlRows;
-            put(slab, lane, qa0);
-            put(slab, lane + 64, qa1);
-            if (lane + 128 < kBlChunks) put(slab, lane + 128, qa2);
-            put(pb, lane, qb0);
-            put(pb, lane + 64, qb1);
-            if (lane + 128 < kBlChunks) put(pb, lane + 128, qb2);
+#if COEB_BLUR_TILED
+            const int dya = __builtin_amdgcn_readlane(dy, min(t0, nk - 1) * kLpk);
+            const int dyb = __builtin_amdgcn_readlane(dy, min(t0 + 1, nk - 1) * kLpk);
+            const int c = (lane >> 3) & 3, r = 8 * tr0 + (lane & 7);
+            auto put_t = [&](uint8_t* base, int row, uint4 v) {
+                if ((unsigned)row < (unsigned)kBlRows) put(base, row, c, v);
+            };
+            put_t(slab, r - dya, qa0);
+            put_t(slab, r + 16 - dya, qa1);
+            put_t(slab, r + 32 - dya, qa2);
+            put_t(pb, r - dyb, qb0);
+            put_t(pb, r + 16 - dyb, qb1);
+            put_t(pb, r + 32 - dyb, qb2);
+#else
+            put(slab, lane >> 2, lane & 3, qa0);
+            put(slab, (lane + 64) >> 2, lane & 3, qa1);
+            if (lane + 128 < kBlChunks) put(slab, (lane + 128) >> 2, lane & 3, qa2);
+            put(pb, lane >> 2, lane & 3, qb0);
+            put(pb, (lane + 64) >> 2, lane & 3, qb1);
+            if (lane + 128 < kBlChunks) put(pb, (lane + 128) >> 2, lane & 3, qb2);
+#endif
         }
         wave_sync_lds();
         if (t0 + kDescGroup < nk) {
@@ -2628,7 +2705,8 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     bw.L = plan.L;
     int items = 0;
     const char* brv = getenv("COEB_BLUR_ROWS");            // rows per band of k_blur_rows; 0 = k_blur
-    const int brows = brv ? atoi(brv) : 32;
+    int brows = brv ? atoi(brv) : 32;
+    if (COEB_BLUR_TILED && brows > 0) brows = (brows + 7) & ~7;   // bands start on tile rows
     bw.brows = brows;
     for (int l = 0; l < plan.L; l++) {
         const LevelGeom& g = plan.lv[l];

@@ -3,7 +3,8 @@
 // HBM layout (per frame slot f of a context, all packed, byte offsets 256-aligned):
 //   gray      [f][H][W]                 u8   level 0 (caller's device buffer or ctx staging)
 //   pyr       [f][pyr_stride]           u8   levels 1..L-1, level l at pyr_off[l], row stride W_l
-//   blur      [f][blur_stride]          u8   7x7 Gaussian of levels 0..L-1 (descriptor input)
+//   blur      [f][blur_stride]          u8   7x7 Gaussian of levels 0..L-1 (descriptor input), each
+//                                            level in 16 x 8 tiles (blur_tile_off; rows padded to 8)
 //   cand_n    [f][ncells]               i32  FAST corners kept per cell
 //   cand      [f][ncells][cell_cap]     u32  packed (x_rel | y_rel<<12 | score<<24), row-major
 //   keys      [f][2][kbuf_stride]       u32  octree key ping-pong buffers (per level kcap_off)
@@ -41,6 +42,20 @@ inline void lds_limit_max(const void* kern)
     if (hipFuncGetAttributes(&fa, kern) == hipSuccess) lim -= (int)fa.sharedSizeBytes;
     if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, lim) != hipSuccess)
         (void)hipGetLastError();        // not sticky: the launch itself reports a size it cannot take
+}
+
+#ifndef COEB_BLUR_TILED
+#define COEB_BLUR_TILED 1
+#endif
+// Byte (x, y) of a blurred level with row pitch bpitch (a 64-byte multiple): COEB_BLUR_TILED
+// stores the level in 128-byte tiles of 16 columns x 8 rows, one tile per cache line, tiles
+// row-major (bpitch / 16 per tile row).  k_describe reads 37-row x 64-byte patches: row-major, every
+// patch row is its own line (37-74 line lookups per patch, half of each 128-B line unused); tiled,
+// a patch is 4 x 5-6 whole lines.
+__host__ __device__ inline int64_t blur_tile_off(int x, int y, int bpitch)
+{
+    if (!COEB_BLUR_TILED) return (int64_t)y * bpitch + x;
+    return ((int64_t)(y >> 3) * (bpitch >> 4) + (x >> 4)) * 128 + (y & 7) * 16 + (x & 15);
 }
 
 #define COEB_MAXL 16
