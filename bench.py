@@ -36,17 +36,19 @@ CONFIGS = {
     # A and C: 2048 as 2 x 1024.  One pipeline measured 208 / 250 / 257 / 269 / 265 k frames/s at
     # 128 / 256 / 512 / 1024 / 2048 frames (profiles/r02/v3/batch_sweep.txt: 1024 frames give every
     # launch >= 4 workgroups per CU, including the small pyramid levels and the matcher); two 1024-frame
-    # pipelines 275 k (profiles/r02/v4/pipelines_ab.txt).  D: 1024 as 2 x 512 -- its flow kernels
+    # pipelines 275 k (profiles/r02/v4/pipelines_ab.txt).  Round 5 (profiles/r05/sched): with the side
+    # stream, pipelines x frames 1 x 2048 356.8 k, 2 x 1024 361.4 k, 3 x 683 365.5 k, 3 x 1024 368.0 k,
+    # 4 x 512 356.1 k, 4 x 1024 363.5 k frames/s; without it 2 x 1024 347-350 k.  D: 1024 as 2 x 512 -- its flow kernels
     # (cornerSubPix, LK, findFundamentalMat, PoseOptimization) are latency bound, one workgroup or wave
     # per corner / pair / frame, so they need many frames in flight: batch x pipelines 256 x 1 measured
     # 51.4 k frames/s, 256 x 2 57.0 k, 512 x 2 61.6 k, 1024 x 2 64.5 k, 2048 x 2 64.5 k, 2048 x 4 58.1 k
     # (profiles/r03/s4/benchD_batch.txt).
-    "A": dict(w=640, h=480, nfeatures=1000, batch=2048, pipelines=2,
+    "A": dict(w=640, h=480, nfeatures=1000, batch=3072, pipelines=3,
               workload="640x480, 8-level pyramid, 1000 kp, extract + Hamming match to prev frame (BASELINE configs[1])"),
     # B: the fixed 512-frame batch of BASELINE configs[3] as 2 pipelines per GPU (per-rank shards of
     # 64-256 frames ran 5-10 % faster with 2 than with 1, profiles/r03/s5/shardB_pipelines.txt)
     "B": dict(w=1280, h=960, nfeatures=2000, pipelines=2, workload="1280x960, 8-level pyramid, 2000 kp, extract + match (BASELINE configs[3] shape)"),
-    "C": dict(w=640, h=480, nfeatures=1000, dyn=True, batch=2048, pipelines=2,
+    "C": dict(w=640, h=480, nfeatures=1000, dyn=True, batch=3072, pipelines=3,
               workload="640x480, 1000 kp, YOLO-bbox dynamic mask (2 boxes, 60 T_M points, blur_flag [0,1]) + "
                        "depth association (ComputeStereoFromRGBD) + match to prev frame (BASELINE configs[2])"),
     "D": dict(w=640, h=480, nfeatures=1000, chain=True, batch=1024, pipelines=2,

@@ -91,13 +91,13 @@ def _bench(args, env=None, timeout=280):
 def test_bench_one_device_rehearsal_is_marked():
     """COEB_BENCH_ONE_DEVICE=1 (every rank on device 0, to rehearse --gpus N on a one-GPU box)
     labels its line, so a rehearsal is never read as an N-GPU measurement; the default batch of
-    config A is 2048 matched frames per GPU in two pipelines of 1024."""
+    config A is 3072 matched frames per GPU in three pipelines of 1024."""
     out, lines = _bench(["--gpus", "2", "--steps", "2", "--warmup", "0", "--dry-run"], env={"COEB_BENCH_ONE_DEVICE": "1"})
     assert out.returncode == 0, out.stderr[-2000:]
     rec = json.loads(lines[0])
     assert rec["rehearsal_one_device"] is True and rec["n_gpus"] == 2
-    assert rec["config"]["frames_per_rank"] == [2048, 2048]
-    assert rec["config"]["pipelines_per_gpu"] == 2 and rec["config"]["frames_per_pipeline"] == [1024, 1024]
+    assert rec["config"]["frames_per_rank"] == [3072, 3072]
+    assert rec["config"]["pipelines_per_gpu"] == 3 and rec["config"]["frames_per_pipeline"] == [1024, 1024, 1024]
     out, lines = _bench(["--gpus", "2", "--steps", "2", "--warmup", "0", "--batch", "4", "--dry-run"])
     assert out.returncode == 0 and "rehearsal_one_device" not in json.loads(lines[0])
 
