@@ -95,7 +95,8 @@ def test_blur_pyramid_matches_oracle(ctx, ex, oracle_mod, w, h, pyr_form, monkey
     GaussianBlur of each oracle pyramid level (ORBextractor.cc:1317-1318), every pixel including
     the REFLECT_101 borders and the partial 64-column strips of ragged widths.  Both pyramid
     kernels: k_pyr_rows (default where rows are 4-byte aligned) and k_pyr_level's byte form
-    (COEB_PYR_BYTES=1; the only form for odd-pitch inputs such as 641x479's level 0)."""
+    (COEB_PYR_BYTES=1; the only form for odd-pitch inputs such as 641x479's level 0).  The raw
+    pyramid levels are compared too."""
     if pyr_form == "bytes":
         monkeypatch.setenv("COEB_PYR_BYTES", "1")
     from coeb_front import Context
@@ -106,9 +107,16 @@ def test_blur_pyramid_matches_oracle(ctx, ex, oracle_mod, w, h, pyr_form, monkey
         r = ex2.extract(gray, debug=True)
         c2.extract(gray)
         blur = c2.debug_read("blur")
-        off = 0
+        pyr = c2.debug_read("pyr")
+        off = poff = 0
         for l, (lw, lh) in enumerate(ex2.level_sizes(w, h)):
             lvl = gray if l == 0 else r["pyramid"][r["level_off"][l]:r["level_off"][l] + lw * lh].reshape(lh, lw)
+            if l > 0:
+                pp = (lw + 63) // 64 * 64
+                gotp = pyr[poff:poff + pp * lh].reshape(lh, pp)[:, :lw]
+                badp = np.argwhere(gotp != lvl)
+                assert len(badp) == 0, ("pyramid level", l, len(badp), badp[:4].tolist())
+                poff = (poff + pp * lh + 255) // 256 * 256
             ref = oracle_mod.gaussian_blur7(lvl)
             pitch = (lw + 63) // 64 * 64
             got = blur[off:off + pitch * lh].reshape(lh, pitch)[:, :lw]

@@ -21,26 +21,31 @@ def load(path):
     return {k: ({c: v / len(disp[k]) for c, v in agg[k].items()}, len(disp[k]), grid[k]) for k in agg}
 
 
-# kernels whose HBM reads are 16-byte-per-lane loads (uint4): k_pyr_level tile staging,
-# k_fast ROI staging, k_describe patch rows
-WIDE16 = ("k_pyr_level", "k_fast", "k_describe")
+# FETCH_SIZE scale, calibrated on this chip (tools/micro/fetch_calib.hip, profiles/r05/s1/calib.log):
+# a 1.2 GB buffer (past the 256 MiB Infinity Cache) read exactly once in each of the product kernels'
+# load shapes -- 16 B per lane streaming, 4 B per lane streaming, k_fast's lane-per-row 3 x 16 B
+# windows (register staging), k_fast's byte-granular 48-B LDS-DMA rows, k_describe's 37 x 64 B patch
+# rows -- reports FETCH_SIZE = 0.500 x the bytes in every shape (the DMA rows: 0.500 x the whole
+# 64-B lines they touch).  So FETCH_SIZE counts half of every line the L2 requests, whatever the
+# access width: one scale of 2 for all kernels (the round-4 summary kept 1 for the <= 4-B-load
+# kernels, from k_blur's fetches matching its byte count; the calibration says those were 2x too).
+FETCH_SCALE = 2.0
 
 
-def traffic_json(merged, nd, frames, command, fetch_scale, wide_scale=2.0, wide=WIDE16):
-    """Per kernel, HBM bytes per launch: scale x FETCH_SIZE + WRITE_SIZE (rocprofv3 KB).
-    MI355X_MICROARCH.md s HBM: on gfx950 FETCH_SIZE reports 1/2 of the bytes of 16-B-per-lane
-    reads, so kernels in `wide` get wide_scale = 2.  The kernels loading <= 4 B per lane are
-    calibrated on k_blur (each level byte read once plus the 6-row vertical halo, each written
-    once): raw FETCH_SIZE ~ its known read bytes, so fetch_scale = 1 for them."""
-    out = dict(frames_per_launch=frames, command=command, fetch_scale=fetch_scale, wide_kernels=list(wide),
-               wide_scale=wide_scale,
-               correction="bytes = (s * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch, mean over dispatches; "
-                          "s = %g for the 16-B-load kernels (wide_kernels), %g otherwise" % (wide_scale, fetch_scale),
+def traffic_json(merged, nd, frames, command, fetch_scale=FETCH_SCALE):
+    """Per kernel, memory-side bytes per launch: fetch_scale x FETCH_SIZE + WRITE_SIZE (rocprofv3
+    KB).  FETCH_SIZE counts L2 requests to the fabric, Infinity-Cache hits included
+    (MI355X_MICROARCH.md HBM), so this is the traffic past L2, an upper bound on HBM bytes."""
+    out = dict(frames_per_launch=frames, command=command, fetch_scale=fetch_scale,
+               calibration="tools/micro/fetch_calib.hip: FETCH_SIZE = 0.500 x the bytes of every load shape "
+                           "(profiles/r05/s1/calib.log)",
+               correction="bytes = (%g * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch, mean over dispatches"
+                          % fetch_scale,
                kernels={})
     for k, cv in sorted(merged.items()):
         if "FETCH_SIZE" not in cv or "WRITE_SIZE" not in cv:
             continue
-        sc = wide_scale if k in wide else fetch_scale
+        sc = fetch_scale
         out["kernels"][k] = dict(fetch_kb=round(cv["FETCH_SIZE"], 3), write_kb=round(cv["WRITE_SIZE"], 3),
                                  fetch_scale=sc, traffic_bytes=int((sc * cv["FETCH_SIZE"] + cv["WRITE_SIZE"]) * 1024),
                                  dispatches=nd[k])
@@ -85,7 +90,7 @@ if __name__ == "__main__":
     ap.add_argument("--frames", type=int, default=0, help="frames per launch of the profiled command")
     ap.add_argument("--command", default="")
     ap.add_argument("--size", default="640x480", help="frame size of the profiled command (WxH)")
-    ap.add_argument("--fetch-scale", type=float, default=1.0)
+    ap.add_argument("--fetch-scale", type=float, default=FETCH_SCALE)
     ap.add_argument("--valu-json", help="write per-kernel VALU issue utilisation (SQ_INSTS_VALU, GRBM_GUI_ACTIVE)")
     a = ap.parse_args()
     merged = collections.defaultdict(dict)
