@@ -23,9 +23,11 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "coeb-slam_amd"))
-# hardware queues per process (HIP default 4): the PCIe-inclusive leg runs two contexts and three
-# copy queues whose streams must not share queues; read when the HIP runtime starts
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# Hardware queues per process: the bench takes the environment's GPU_MAX_HW_QUEUES (the GPU box
+# exports 4, HIP's default) and records it in the line (config.hw_queues).  Measured on this build:
+# with 4 queues the pipelines' side streams share one queue, and that is the fastest setting
+# (8 or 16 queues: 1-2 % slower; DESIGN.md s0, profiles/r05/s1).
+HW_QUEUES = os.environ.get("GPU_MAX_HW_QUEUES")
 
 import numpy as np  # noqa: E402
 
@@ -978,7 +980,9 @@ def rank_main(ranks, args):
                                 frames_per_pipeline=[sp[2] for sp in subs], streams_per_gpu=args.streams,
                                 ranks="threads" if isinstance(ranks, _thread_rank_type()) else
                                       ("processes" if world > 1 else "single"),
-                                parallelism="frame-sharded x%d (no collectives)" % world),
+                                parallelism="frame-sharded x%d (no collectives)" % world,
+                                hw_queues=int(HW_QUEUES) if HW_QUEUES and HW_QUEUES.isdigit() else
+                                          "GPU_MAX_HW_QUEUES unset (HIP default 4)"),
                     roofline=roof,
                     pipeline_roofline=dict(bytes_per_frame=int(pipeline_bytes),
                                            achieved_GBps=round(value * pipeline_bytes / 1e9, 3),

@@ -234,8 +234,10 @@ class HostStream:
 
     Either way submit() never blocks the host.  Results of batch i are readable after wait(i) and
     stay so until batch i + 2 is submitted (its download reuses slot i % 2's host buffers).  The
-    process needs more than 4 hardware queues (GPU_MAX_HW_QUEUES = 16 in bench.py): with HIP's
-    default of 4 the streams of two contexts share queues and the overlap disappears."""
+    ring mode needs three streams (context, copy queue, downloads), which HIP's default of 4
+    hardware queues per process gives each a queue of their own; the slot modes' two contexts
+    need more (GPU_MAX_HW_QUEUES = 16), else their streams share queues and the overlap
+    disappears."""
 
     def __init__(self, width, height, nframes, nfeatures=1000, device=0, depth=None, Tcw=None, shared_queue=True,
                  mode="ring"):

@@ -2346,6 +2346,9 @@ struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
 // every other row on the same 16 banks).
 constexpr int kBlRow = 72, kBlRows = 37, kBlChunks = kBlRows * 4;   // 148 16-byte chunks
 constexpr int kDescGroup = 2;                                        // patches staged per step
+#ifndef COEB_DESC_KP
+#define COEB_DESC_KP 8         // keypoints per wave
+#endif
 template <int KP> constexpr int desc_slab() { return kBlRow * kBlRows * kDescGroup + 32 * KP; }
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};   // ORBextractor.cc:461-476
 
@@ -2846,7 +2849,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     // 8 keypoints per wave (round 1's 32 let one XCD's resident waves span ~20 frames and refetch
     // every patch row past L2; 4 and 16 measured slower; 4 again with the
     // row-chunk IC_Angle loads: 0.667 vs 0.630 ms, profiles/r04/ab6)
-    constexpr int KP = 8;
+    constexpr int KP = COEB_DESC_KP;
     if (vec0)
         hipLaunchKernelGGL((k_describe<true, KP>), dim3((plan.kcap + kWaves * KP - 1) / (kWaves * KP), F), dim3(kThreads), 0,
                            s, d_plan, b);

@@ -8,9 +8,6 @@ import sys
 
 import pytest
 
-# as bench.py: the two-context PCIe pipeline needs more than HIP's default 4 hardware queues
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "coeb-slam_amd"), os.path.join(ROOT, "oracle"), ROOT):
     if p not in sys.path:
