@@ -2346,8 +2346,15 @@ struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
 // every other row on the same 16 banks).
 constexpr int kBlRow = 72, kBlRows = 37, kBlChunks = kBlRows * 4;   // 148 16-byte chunks
 constexpr int kDescGroup = 2;                                        // patches staged per step
+#ifndef COEB_DESC_IC_BATCH
+#define COEB_DESC_IC_BATCH 32     // IC row-chunk loads in flight per lane (>= the tasks per lane: all at once)
+#endif
 #ifndef COEB_DESC_KP
-#define COEB_DESC_KP 8         // keypoints per wave
+// keypoints per wave.  8 is the fastest alone (0.537 vs 0.568 ms per 1025-frame launch), 16 the
+// fastest in the three-pipeline step (374 k vs 370 k frames/s, profiles/r05/s13-s15): at 122 VGPRs
+// (4 waves per SIMD instead of 5) it leaves the other pipelines' kernels more room on the CUs;
+// capping 8 at 4 or 3 workgroups per CU through LDS instead starves k_fast (367-358 k)
+#define COEB_DESC_KP 16
 #endif
 template <int KP> constexpr int desc_slab() { return kBlRow * kBlRows * kDescGroup + 32 * KP; }
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};   // ORBextractor.cc:461-476
@@ -2461,24 +2468,32 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
         // is formed per byte from u = column - x, the column weights are u + 31 (in [1, 63], so
         // packed bytes never carry) and m01 takes v * (row sum) directly.
         constexpr int kTasks = (93 + kLpk - 1) / kLpk;
+        // loads in flight per batch (COEB_DESC_IC_BATCH: all kTasks, or fewer for fewer VGPRs)
+        constexpr int kBatch = COEB_DESC_IC_BATCH < kTasks ? COEB_DESC_IC_BATCH : kTasks;
         constexpr uint64_t kUmaxPk = 0x3689ABCDDEEEFFFFull;     // umax[av] in nibble av (kUmax)
         const int j = lane % kLpk;
         const uint8_t* base0 = img + (int64_t)(y - 15) * g.pitch + (x - 15 - a);
-        uint4 cq[kTasks];
 #pragma unroll
-        for (int i = 0; i < kTasks; i++) {
+        for (int i0 = 0; i0 < kTasks; i0 += kBatch) {
+        uint4 cq[kBatch];
+#pragma unroll
+        for (int ii = 0; ii < kBatch; ii++) {
+            const int i = i0 + ii;
+            if (i >= kTasks) break;
             const int r = min(j + kLpk * i, 92);
             const int row = r / 3, ch = r - 3 * row;
-            cq[i] = *reinterpret_cast<const uint4*>(base0 + (int64_t)row * g.pitch + 16 * ch);
+            cq[ii] = *reinterpret_cast<const uint4*>(base0 + (int64_t)row * g.pitch + 16 * ch);
         }
 #pragma unroll
-        for (int i = 0; i < kTasks; i++) {
+        for (int ii = 0; ii < kBatch; ii++) {
+            const int i = i0 + ii;
+            if (i >= kTasks) break;
             const int r = j + kLpk * i;
             if (r < 93) {
                 const int row = r / 3, ch = r - 3 * row;
                 const int v = row - 15, av = v < 0 ? -v : v;
                 const int um = (int)((kUmaxPk >> (4 * av)) & 15u);
-                const uint32_t q[4] = {cq[i].x, cq[i].y, cq[i].z, cq[i].w};
+                const uint32_t q[4] = {cq[ii].x, cq[ii].y, cq[ii].z, cq[ii].w};
                 uint32_t rs = 0;
 #pragma unroll
                 for (int d = 0; d < 4; d++) {
@@ -2492,6 +2507,7 @@ __global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ 
                 S += rs;
                 m01 += v * (int)rs;
             }
+        }
         }
         aoff = 31;
     } else
@@ -2846,9 +2862,9 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     }
     prof_begin(prof, "k_describe", s);
     const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
-    // 8 keypoints per wave (round 1's 32 let one XCD's resident waves span ~20 frames and refetch
-    // every patch row past L2; 4 and 16 measured slower; 4 again with the
-    // row-chunk IC_Angle loads: 0.667 vs 0.630 ms, profiles/r04/ab6)
+    // COEB_DESC_KP keypoints per wave (round 1's 32 let one XCD's resident waves span ~20 frames
+    // and refetch every patch row past L2; with the tiled blurred pyramid 16 gives the fastest
+    // step, 8 the fastest kernel alone)
     constexpr int KP = COEB_DESC_KP;
     if (vec0)
         hipLaunchKernelGGL((k_describe<true, KP>), dim3((plan.kcap + kWaves * KP - 1) / (kWaves * KP), F), dim3(kThreads), 0,

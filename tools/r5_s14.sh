@@ -1,0 +1,17 @@
+#!/bin/bash
+# round 5 session 14: config A step vs k_describe's workgroups per CU (KP 8 capped by LDS) and KP 16
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/s14
+one() {
+  local tag=$1; shift
+  env "$@" timeout -k 10 180 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-extras --no-e2e --no-profile > gpurun_out/s14/$tag.log 2>&1 || { echo "$tag rc=$?"; tail -5 gpurun_out/s14/$tag.log; exit 1; }
+  python -c "import json; d=json.loads([l for l in open('gpurun_out/s14/$tag.log') if l.startswith('{')][-1]); print('%-12s step=%.4f ms value=%.0f' % ('$tag', d['ms_per_step'], d['value']))"
+}
+for rep in 1 2 3; do
+  one kp8
+  one kp8_wg4 COEB_DESC_WG_PER_CU=4
+  one kp8_wg3 COEB_DESC_WG_PER_CU=3
+  one kp16 COEB_LIB_PATH=$PWD/coeb-slam_amd/lib/var_kp16.so
+  one kp16_wg3 COEB_LIB_PATH=$PWD/coeb-slam_amd/lib/var_kp16.so COEB_DESC_WG_PER_CU=3
+done
