@@ -34,7 +34,7 @@ for step in "$@"; do
         # kernel timeline of the default two-pipeline step (concurrency / idle time per step)
         timeline)
             run timeline 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tl -o run -- python bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-extras --no-e2e --no-profile
-            python tools/timeline2.py gpurun_out/tl/run_kernel_trace.csv 2 > gpurun_out/timeline.txt 2>&1; tail -n 30 gpurun_out/timeline.txt ;;
+            python tools/timeline2.py gpurun_out/tl/run_kernel_trace.csv 3 > gpurun_out/timeline.txt 2>&1; tail -n 30 gpurun_out/timeline.txt ;;
         posetime) run posetime 300 python tools/pose_timing.py ;;
         flow) run flow 300 python tools/flow_bench.py ;;
         flowprof) run flowprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/flowprof -o run -- python tools/flow_bench.py ;;
