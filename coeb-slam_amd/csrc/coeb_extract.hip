@@ -2350,11 +2350,10 @@ constexpr int kDescGroup = 2;                                        // patches 
 #define COEB_DESC_IC_BATCH 32     // IC row-chunk loads in flight per lane (>= the tasks per lane: all at once)
 #endif
 #ifndef COEB_DESC_KP
-// keypoints per wave.  8 is the fastest alone (0.537 vs 0.568 ms per 1025-frame launch), 16 the
-// fastest in the three-pipeline step (374 k vs 370 k frames/s, profiles/r05/s13-s15): at 122 VGPRs
-// (4 waves per SIMD instead of 5) it leaves the other pipelines' kernels more room on the CUs;
-// capping 8 at 4 or 3 workgroups per CU through LDS instead starves k_fast (367-358 k)
-#define COEB_DESC_KP 16
+// keypoints per wave: 8 is the fastest alone (0.537 vs 0.568 ms per 1025-frame launch for 16) and
+// in the steps of configs B, C and D (16: -6 %, -3 %, -1 %); 16 wins only config A's step
+// (+1 %, profiles/r05/s13-s17)
+#define COEB_DESC_KP 8
 #endif
 template <int KP> constexpr int desc_slab() { return kBlRow * kBlRows * kDescGroup + 32 * KP; }
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};   // ORBextractor.cc:461-476
@@ -2863,8 +2862,8 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     prof_begin(prof, "k_describe", s);
     const bool vec0 = plan.W % 16 == 0 && (reinterpret_cast<uintptr_t>(b.gray) & 15) == 0;
     // COEB_DESC_KP keypoints per wave (round 1's 32 let one XCD's resident waves span ~20 frames
-    // and refetch every patch row past L2; with the tiled blurred pyramid 16 gives the fastest
-    // step, 8 the fastest kernel alone)
+    // and refetch every patch row past L2; 4 and 16 are slower alone, and 16 is slower in three of
+    // the four configs' steps)
     constexpr int KP = COEB_DESC_KP;
     if (vec0)
         hipLaunchKernelGGL((k_describe<true, KP>), dim3((plan.kcap + kWaves * KP - 1) / (kWaves * KP), F), dim3(kThreads), 0,
