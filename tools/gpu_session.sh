@@ -16,7 +16,10 @@ run() {
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
     return 0
 }
+SIDE0=${COEB_SIDE_STREAM-unset}
 for step in "$@"; do
+    # the PMC steps export COEB_SIDE_STREAM=0 for their passes: restore the caller's setting per step
+    if [ "$SIDE0" = unset ]; then unset COEB_SIDE_STREAM; else export COEB_SIDE_STREAM=$SIDE0; fi
     case "$step" in
         pytest) run pytest_gpu 900 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread ;;
         pytestall) run pytest_gpu 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread ;;
