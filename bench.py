@@ -74,6 +74,11 @@ CPU_CAVEAT = ("the oracle is a scalar C restatement of ORBextractor/ORBmatcher w
 CHAIN_WARMUP = 20    # 20 warm-up frames before the timed ones
 
 
+# kernels that read the frames' pixels (the s8(d) image-byte rule applies to them)
+IMAGE_KERNELS = ("k_fast", "k_describe", "k_blur", "k_blur_rows", "k_pyr_level", "k_pyr_rows", "k_rgbd_batch",
+                 "k_gf_response", "k_subpix", "k_lk", "k_pyr_down", "k_sharr")
+
+
 def step_kwargs(cfg):
     """BatchPipeline.run() arguments of one step of `cfg`."""
     if cfg.get("chain"):
@@ -962,6 +967,16 @@ def rank_main(ranks, args):
                         bytes_rule="SURVEY.md s8(d): (W*H + 60*N_kp + 36*N_prev) x %d frames" % frames_per_launch,
                         kernel_own=dict(bytes_per_launch=int(own), achieved=round(own / avg_s / 1e9, 3),
                                         frac=round(own / avg_s / 1e9 / HBM_PEAK_GBS, 6)))
+            if name not in IMAGE_KERNELS:
+                # a dominant kernel that reads no image (config D's k_pose): the headline figures are
+                # its own bytes, and the s8(d) image-byte figure moves aside
+                roof.update(achieved=roof["kernel_own"]["achieved"], frac=roof["kernel_own"]["frac"],
+                            bytes_per_launch=int(own),
+                            bytes_rule="%s's own touched-once bytes x %d frames (DESIGN.md s4); the kernel "
+                                       "reads no image, so SURVEY.md s8(d)'s image bytes do not apply"
+                                       % (name, frames_per_launch),
+                            s8d=dict(bytes_per_launch=int(bpl), achieved=round(achieved, 3),
+                                     frac=round(achieved / HBM_PEAK_GBS, 6)))
             if traffic is not None:
                 roof["traffic_source"] = tsrc
             # the kernel is bound by integer VALU issue, not HBM: the PMC VALU fraction says how

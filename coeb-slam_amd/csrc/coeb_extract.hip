@@ -2344,7 +2344,8 @@ struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
 // Patch rows are 64 source bytes at an LDS pitch of 72 (18 dwords): consecutive rows land on
 // different banks, so the 64 lanes' scattered test samples rarely conflict (a 64-byte pitch put
 // every other row on the same 16 banks).
-constexpr int kBlRow = 72, kBlRows = 37, kBlChunks = kBlRows * 4;   // 148 16-byte chunks
+constexpr int kBlRow = 72, kBlRows = 37;
+[[maybe_unused]] constexpr int kBlChunks = kBlRows * 4;              // 148 16-byte chunks (row-major blur)
 constexpr int kDescGroup = 2;                                        // patches staged per step
 #ifndef COEB_DESC_IC_BATCH
 #define COEB_DESC_IC_BATCH 32     // IC row-chunk loads in flight per lane (>= the tasks per lane: all at once)
