@@ -50,7 +50,11 @@ CONFIGS = {
     # B: the fixed 512-frame batch of BASELINE configs[3] as 2 pipelines per GPU (per-rank shards of
     # 64-256 frames ran 5-10 % faster with 2 than with 1, profiles/r03/s5/shardB_pipelines.txt)
     "B": dict(w=1280, h=960, nfeatures=2000, pipelines=2, workload="1280x960, 8-level pyramid, 2000 kp, extract + match (BASELINE configs[3] shape)"),
-    "C": dict(w=640, h=480, nfeatures=1000, dyn=True, batch=3072, pipelines=3,
+    # C: the three pipelines share one extraction side stream (3 context streams + 1 side stream on the
+    # box's 4 hardware queues): 8.65-8.89 ms per step against 9.01-9.15 with a side stream each; for A
+    # and D the shared stream measured slower (8.51-8.54 vs 8.27-8.36 ms, 13.63-13.76 vs 13.15-13.21,
+    # profiles/r05/s19, s20)
+    "C": dict(w=640, h=480, nfeatures=1000, dyn=True, batch=3072, pipelines=3, side_stream="shared",
               workload="640x480, 1000 kp, YOLO-bbox dynamic mask (2 boxes, 60 T_M points, blur_flag [0,1]) + "
                        "depth association (ComputeStereoFromRGBD) + match to prev frame (BASELINE configs[2])"),
     "D": dict(w=640, h=480, nfeatures=1000, chain=True, batch=1024, pipelines=2,
@@ -767,6 +771,9 @@ def parse_args(argv=None):
                     help="independent batch pipelines (contexts) per GPU whose kernels overlap (default: the "
                          "config's); the GPU's batch is split between them, each with its own halo frame")
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
+    ap.add_argument("--side-stream", default=None, choices=("own", "shared", "off"),
+                    help="extraction side stream per pipeline (own), one per GPU shared by the pipelines "
+                         "(shared), or none (off); default: the config's")
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the batch is chunked over (kernels of different chunks overlap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -787,6 +794,13 @@ def main():
         args.batch = CONFIGS[args.config].get("batch", 256)
     if args.pipelines is None:
         args.pipelines = CONFIGS[args.config].get("pipelines", 1)
+    if args.side_stream is None:
+        args.side_stream = CONFIGS[args.config].get("side_stream", "own")
+    # read by each context when it first extracts (csrc/coeb_capi.hip side_stream)
+    if args.side_stream == "shared":
+        os.environ["COEB_SIDE_SHARED"] = "1"
+    elif args.side_stream == "off":
+        os.environ["COEB_SIDE_STREAM"] = "0"
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     if env_world > 1 or "LOCAL_RANK" in os.environ:
         # one process per GPU under torch.distributed.run
@@ -997,7 +1011,10 @@ def rank_main(ranks, args):
                                       ("processes" if world > 1 else "single"),
                                 parallelism="frame-sharded x%d (no collectives)" % world,
                                 hw_queues=int(HW_QUEUES) if HW_QUEUES and HW_QUEUES.isdigit() else
-                                          "GPU_MAX_HW_QUEUES unset (HIP default 4)"),
+                                          "GPU_MAX_HW_QUEUES unset (HIP default 4)",
+                                side_stream="off" if os.environ.get("COEB_SIDE_STREAM", "1")[:1] == "0" else
+                                            ("shared" if os.environ.get("COEB_SIDE_SHARED", "0")[:1] == "1"
+                                             else "own")),
                     roofline=roof,
                     pipeline_roofline=dict(bytes_per_frame=int(pipeline_bytes),
                                            achieved_GBps=round(value * pipeline_bytes / 1e9, 3),

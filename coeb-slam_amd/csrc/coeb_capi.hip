@@ -400,6 +400,7 @@ struct coeb_ctx {
     // level-0 blur + FAST beside the pyramid (launch_extract's SideStream); COEB_SIDE_STREAM=0 disables
     SideStream side{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, true, false};
     bool side_init = false;
+    bool side_shared = false;                 // side.s is the device's shared side stream
     hipEvent_t ev_tprep = nullptr, ev_pose = nullptr;
     bool pose_pending = false;
     // batch tracking state: Observations() the matcher gave the LastFrame points, the frames and
@@ -613,6 +614,49 @@ int upload_dyn(coeb_ctx* c, int F, const coeb_box* boxes, const int32_t* box_off
 // The side stream of launch_extract (created on first use), or null when disabled.  Per-kernel
 // profiling (coeb_profile_enable) serialises everything on the context stream, so each event
 // pair brackets one whole-batch launch.
+// A non-blocking stream whose priority the environment variable `env` may set ("high" / "low":
+// the device's greatest / least stream priority; unset: the default).  Experiment knob for the
+// multi-stream schedules (which queue the dispatcher serves first when CUs free up).
+static hipError_t make_stream(hipStream_t* s, const char* env)
+{
+    const char* e = env ? getenv(env) : nullptr;
+    if (e && (e[0] == 'h' || e[0] == 'l')) {
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+            return hipStreamCreateWithPriority(s, hipStreamNonBlocking, e[0] == 'h' ? greatest : least);
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
+// The device's shared side stream (COEB_SIDE_SHARED=1): with P pipelines the P context streams
+// plus one side stream fill the 4 hardware queues exactly, instead of 2P streams sharing them.
+// Reference-counted over the contexts that use it.
+static std::mutex g_shared_side_mu;
+static std::map<int, std::pair<hipStream_t, int>> g_shared_side;
+
+static hipError_t shared_side_acquire(int device, hipStream_t* out)
+{
+    std::lock_guard<std::mutex> lk(g_shared_side_mu);
+    auto& e = g_shared_side[device];
+    if (!e.first) {
+        hipError_t r = make_stream(&e.first, "COEB_SIDE_PRIO");
+        if (r != hipSuccess) { e.first = nullptr; return r; }
+    }
+    ++e.second;
+    *out = e.first;
+    return hipSuccess;
+}
+
+static void shared_side_release(int device)
+{
+    std::lock_guard<std::mutex> lk(g_shared_side_mu);
+    auto it = g_shared_side.find(device);
+    if (it == g_shared_side.end() || --it->second.second > 0) return;
+    (void)hipStreamSynchronize(it->second.first);
+    (void)hipStreamDestroy(it->second.first);
+    g_shared_side.erase(it);
+}
+
 const SideStream* side_stream(coeb_ctx* c)
 {
     if (c->prof.enabled) return nullptr;
@@ -626,13 +670,19 @@ const SideStream* side_stream(coeb_ctx* c)
         if (bl) c->side.blur_late = bl[0] == '1';
         const char* so = getenv("COEB_SIDE_OCTREE");         // 1: early levels' octree on the side stream
         if (so) c->side.side_octree = so[0] == '1';
-        if (hipStreamCreateWithFlags(&c->side.s, hipStreamNonBlocking) != hipSuccess ||
+        const char* sh = getenv("COEB_SIDE_SHARED");         // 1: one side stream per device
+        c->side_shared = sh && sh[0] == '1';
+        hipError_t se = c->side_shared ? shared_side_acquire(c->device, &c->side.s)
+                                       : make_stream(&c->side.s, "COEB_SIDE_PRIO");
+        if (se != hipSuccess ||
             hipEventCreateWithFlags(&c->side.fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->side.mid, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->side.pyr_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->side.join2, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->side.join, hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&c->side.join, hipEventDisableTiming) != hipSuccess) {
+            if (se == hipSuccess && c->side_shared) shared_side_release(c->device);
             c->side.s = nullptr;
+        }
     }
     return c->side.s ? &c->side : nullptr;
 }
@@ -771,7 +821,7 @@ coeb_ctx* coeb_create(const coeb_orb_params* params, int device, int max_width, 
     c->max_w = max_width;
     c->max_h = max_height;
     c->max_batch = max_batch;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || make_stream(&c->stream, "COEB_MAIN_PRIO") != hipSuccess) {
         g_last_error = "coeb_create: stream creation failed";
         delete c;
         return nullptr;
@@ -799,7 +849,8 @@ void coeb_destroy(coeb_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(main_stream(c));
     if (c->side.s) {
         (void)hipStreamSynchronize(c->side.s);
-        (void)hipStreamDestroy(c->side.s);
+        if (c->side_shared) shared_side_release(c->device);
+        else (void)hipStreamDestroy(c->side.s);
         (void)hipEventDestroy(c->side.fork);
         (void)hipEventDestroy(c->side.mid);
         (void)hipEventDestroy(c->side.pyr_done);
@@ -1422,7 +1473,7 @@ int coeb_pose_batch_device(coeb_ctx* c, const coeb_camera* cam, int F, const flo
         return rc;
     hipStream_t s = main_stream(c);                 // joins the matchers' chunk streams
     if (!c->pose_stream) {
-        HIP_TRY(c, hipStreamCreateWithFlags(&c->pose_stream, hipStreamNonBlocking));
+        HIP_TRY(c, make_stream(&c->pose_stream, "COEB_POSE_PRIO"));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_tprep, hipEventDisableTiming));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_pose, hipEventDisableTiming));
     }

@@ -1456,7 +1456,10 @@ int launch_match_local(const MatchCam& cam, const LocalBufsHost& h, float th, fl
     const size_t lds_full = match_lds_bytes(cs, qs, true, nullptr) + 256;
     const size_t lds_min = match_lds_bytes(cs, qs, false, nullptr) + 256;
     prof_begin(prof, "k_match_local", s);
-    if (lds_full <= 160 * 1024) {
+    // COEB_LOCAL_LDS=0: the current frame read from global memory (a third of the LDS, so the
+    // workgroup finds room beside the pose and flow kernels sooner)
+    const char* le = getenv("COEB_LOCAL_LDS");
+    if (lds_full <= 160 * 1024 && !(le && atoi(le) == 0)) {
         lds_limit_max((const void*)k_match_local<true>);
         hipLaunchKernelGGL(k_match_local<true>, dim3(P), dim3(kMThreads), lds_full - 256, s, cam, b, th, nnratio, force_seq);
     } else if (lds_min <= 160 * 1024) {

@@ -371,12 +371,18 @@ __device__ bool pq_solve6_wave(const double* hu, double lambda, const double* bv
     return true;
 }
 
-// Partials of thread t live at slot t + t / 32 of a 264-double row: in block_reduce lane
-// (k, c) walks run c of value k, and without the skew all 64 lanes of a wave would read the
-// same LDS bank (runs 256 B apart, rows 2 KB apart).  With it, runs are 33 doubles apart and
-// rows 264 (≡ 8 mod 32): at most two lanes of a wave share a bank.
-constexpr int kPartRow = 264;
-__device__ __forceinline__ int part_slot(int t) { return t + (t >> 5); }
+// Reduction staging, per wave: wave w holds threads 64w .. 64w + 63, i.e. the whole of runs 2w and
+// 2w + 1, so each wave sums its own two runs with no workgroup barrier.  The values go through a
+// wave-private LDS area kRC at a time (lane l at slot l + l / 32 of a kWRow-double row: the two runs
+// 33 doubles apart), lane (k, c) of the wave sums run c of value k; one barrier publishes the 8 run
+// sums of every value: two workgroup barriers per reduction instead of three (0.5 % on config D's
+// step; kRC = 27, 57 KB).  Smaller chunks cut the LDS (kRC = 9: 22 KB per frame), so more frames'
+// workgroups would fit a CU, but every variant that used that measured slower (profiles/r05/s22).
+#ifndef COEB_POSE_RCHUNK
+#define COEB_POSE_RCHUNK 27
+#endif
+constexpr int kRC = COEB_POSE_RCHUNK;
+constexpr int kWRow = 66;
 
 // Trials per round after the first of an iteration (see k_pose): g2o's inner loop retries a
 // rejected step with lambda *= ni, ni *= 2 from the same saved estimate, so the trials that follow
@@ -401,7 +407,7 @@ struct PoseTrial {
 struct PoseLds {
     Se3 s;                 // current estimate (broadcast)
     Se3 last;              // estimate of the last chi2 evaluation (the classification's errors)
-    double part[28][kPartRow];  // per-thread partials, skewed (part_slot)
+    double wpart[kPT / 64][kRC][kWRow];   // per-wave staging of kRC values (block_reduce)
     double run[28][8];     // 32-lane run sums
     double out[28];        // reduced
     double hb[27];         // this iteration's 21 Hessian + 6 gradient terms (thread 0's system)
@@ -411,18 +417,37 @@ struct PoseLds {
     int qmax, stop, nbad[4], accepted;
 };
 
-// block-wide canonical reduction of nv per-thread partials (uniform call): each run of 32
-// threads summed in thread order, then the 8 run sums in order (the oracle's pq_reduce)
-__device__ void block_reduce(PoseLds& L, double* v, int nv)
+__device__ __forceinline__ void pose_wave_sync()
 {
-    const int tid = threadIdx.x;
-    for (int k = 0; k < nv; k++) L.part[k][part_slot(tid)] = v[k];
-    __syncthreads();
-    if (tid < nv * 8) {
-        const int k = tid >> 3, c = tid & 7;
-        double p = 0.0;
-        for (int l = 33 * c; l < 33 * c + 32; l++) p = p + L.part[k][l];   // threads 32c .. 32c+31 in order
-        L.run[k][c] = p;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// block-wide canonical reduction of nv <= NV per-thread partials (uniform call): each run of 32
+// threads summed in thread order, then the 8 run sums in order (the oracle's pq_reduce)
+template <int NV>
+__device__ void block_reduce(PoseLds& L, const double (&v)[NV], int nv)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    double* wp = &L.wpart[wv][0][0];
+#pragma unroll
+    for (int k0 = 0; k0 < NV; k0 += kRC) {
+        if (k0 < nv) {
+#pragma unroll
+            for (int k = 0; k < kRC; k++)
+                if (k0 + k < NV && k0 + k < nv) wp[k * kWRow + lane + (lane >> 5)] = v[k0 + k];
+            pose_wave_sync();
+            if (lane < 2 * min(kRC, nv - k0)) {
+                const int k = lane >> 1, c = lane & 1;
+                const double* r = wp + k * kWRow + 33 * c;
+                double p = 0.0;
+#pragma unroll 8
+                for (int l = 0; l < 32; l++) p = p + r[l];       // threads 64 wv + 32 c + l in order
+                L.run[k0 + k][2 * wv + c] = p;
+            }
+            pose_wave_sync();                                   // the next chunk reuses wp
+        }
     }
     __syncthreads();
     if (tid < nv) {
@@ -512,8 +537,14 @@ __device__ void active_chi2(PoseLds& L, const PoseBufs& b, const PoseCam& cm, in
 #define PT_ADD(slot, t0) do { if (b.timing && threadIdx.x == 0) b.timing[(int64_t)blockIdx.x * 8 + (slot)] += (long long)clock64() - (t0); } while (0)
 #define PT_INC(slot) do { if (b.timing && threadIdx.x == 0) b.timing[(int64_t)blockIdx.x * 8 + (slot)] += 1; } while (0)
 
+#ifndef COEB_POSE_MINWG
+#define COEB_POSE_MINWG 2      // launch bound: workgroups per CU the register budget must allow
+#endif
+#ifndef COEB_POSE_MINWG0
+#define COEB_POSE_MINWG0 2     // the same for k_pose<0> (edges in global scratch)
+#endif
 template <int EPT>
-__global__ __launch_bounds__(kPT, 2) void k_pose(PoseBufs b, PoseCam cm)
+__global__ __launch_bounds__(kPT, EPT == 0 ? COEB_POSE_MINWG0 : COEB_POSE_MINWG) void k_pose(PoseBufs b, PoseCam cm)
 {
     PT_MARK(t_all);
     EdgeSet<EPT> ES;
@@ -571,7 +602,10 @@ __global__ __launch_bounds__(kPT, 2) void k_pose(PoseBufs b, PoseCam cm)
     Se3 s0;
     if (tid == 0) s0 = pq_from_Tcw(Tcw);
     int nBad = 0;
-    for (int it = 0; it < 4; it++) {
+#ifndef COEB_POSE_ROUNDS
+#define COEB_POSE_ROUNDS 4     // Optimizer.cc:364 (fewer only in sensitivity experiments; not bit-exact)
+#endif
+    for (int it = 0; it < COEB_POSE_ROUNDS; it++) {
         if (tid == 0) L.s = s0;                                    // setEstimate(toSE3Quat(mTcw))
         __syncthreads();
         const bool robust = it < 3;
@@ -793,7 +827,8 @@ int launch_pose(const PoseBufs& b, int F, double fx, double fy, double cx, doubl
     PoseCam cm{fx, fy, cx, cy, bf};
     prof_begin(prof, "k_pose", s);
     // edges per thread by the keypoint stride: registers up to 9 x 256 edges, else global scratch
-    const int ept = (b.stride + kPT - 1) / kPT;
+    int ept = (b.stride + kPT - 1) / kPT;
+    if (const char* e = getenv("COEB_POSE_EPT")) if (atoi(e) == 0) ept = 1 << 20;   // experiment: force k_pose<0>
     if (ept <= 5) hipLaunchKernelGGL(k_pose<5>, dim3(F), dim3(kPT), 0, s, b, cm);
     else if (ept <= 9) hipLaunchKernelGGL(k_pose<9>, dim3(F), dim3(kPT), 0, s, b, cm);
     else hipLaunchKernelGGL(k_pose<0>, dim3(F), dim3(kPT), 0, s, b, cm);
