@@ -401,6 +401,7 @@ struct coeb_ctx {
     SideStream side{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, true, false};
     bool side_init = false;
     bool side_shared = false;                 // side.s is the device's shared side stream
+    hipEvent_t ev_ffork = nullptr, ev_fjoin = nullptr;   // the moving-object batch's LK-pyramid fork / join
     hipEvent_t ev_tprep = nullptr, ev_pose = nullptr;
     bool pose_pending = false;
     // batch tracking state: Observations() the matcher gave the LastFrame points, the frames and
@@ -857,6 +858,8 @@ void coeb_destroy(coeb_ctx* c)
         (void)hipEventDestroy(c->side.join2);
         (void)hipEventDestroy(c->side.join);
     }
+    if (c->ev_ffork) (void)hipEventDestroy(c->ev_ffork);
+    if (c->ev_fjoin) (void)hipEventDestroy(c->ev_fjoin);
     if (c->pose_stream) {
         (void)hipStreamSynchronize(c->pose_stream);
         (void)hipStreamDestroy(c->pose_stream);
@@ -1948,6 +1951,30 @@ int coeb_internal_stream(coeb_ctx* c, hipStream_t* s, int* device)
     *s = main_stream(c);
     *device = c->device;
     return COEB_OK;
+}
+
+// The side stream for the moving-object batch's LK pyramids, with the context's fork / join events
+// (created on first use), when COEB_FLOW_SIDE=1; nonzero otherwise (also with the side stream off
+// or per-kernel profiling), and then everything stays on the context stream.  Off by default: config
+// D's step measured 13.30-13.37 ms with the fork against 13.10-13.30 without (profiles/r05/s24): the
+// step is bound by the kernels' combined demand for CUs, not by the context stream's chain.
+int coeb_internal_flow_side(coeb_ctx* c, hipStream_t* side, hipEvent_t* fork, hipEvent_t* join)
+{
+    if (!c) return COEB_EINVAL;
+    const char* e = getenv("COEB_FLOW_SIDE");
+    if (!(e && e[0] == '1')) return 1;
+    const SideStream* sd = side_stream(c);
+    if (!sd) return 1;
+    if (!c->ev_ffork && (hipEventCreateWithFlags(&c->ev_ffork, hipEventDisableTiming) != hipSuccess ||
+                         hipEventCreateWithFlags(&c->ev_fjoin, hipEventDisableTiming) != hipSuccess)) {
+        if (c->ev_ffork) (void)hipEventDestroy(c->ev_ffork);
+        c->ev_ffork = c->ev_fjoin = nullptr;
+        return 1;
+    }
+    *side = sd->s;
+    *fork = c->ev_ffork;
+    *join = c->ev_fjoin;
+    return 0;
 }
 
 int coeb_internal_scratch(coeb_ctx* c, const char* name, size_t bytes, void** p)

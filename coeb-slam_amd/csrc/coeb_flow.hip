@@ -46,6 +46,7 @@ extern "C" int coeb_internal_scratch(coeb_ctx* c, const char* name, size_t bytes
 extern "C" int coeb_internal_error(coeb_ctx* c, int code, const char* msg);
 extern "C" ProfileHook* coeb_internal_prof(coeb_ctx* c);
 extern "C" void coeb_internal_flow_forget(const coeb_ctx* c);
+extern "C" int coeb_internal_flow_side(coeb_ctx* c, hipStream_t* side, hipEvent_t* fork, hipEvent_t* join);
 
 namespace {
 
@@ -1833,11 +1834,13 @@ int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, int win,
-              int max_level, int max_count, double eps, hipStream_t s, int64_t iz = 0)
+// LK pyramids of both frames (pyrDown levels and the Scharr derivatives of every level): they read
+// only the images, so a batch builds them on a second stream beside goodFeaturesToTrack and
+// cornerSubPix (coeb_internal_pmo_batch); `pyr` is filled for launch_lk_track.
+int launch_lk_pyramids(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, int win,
+                       int max_level, hipStream_t s, int64_t iz, LkPyr& pyr)
 {
     const int P = d->npairs;
-    LkPyr pyr;
     memset(&pyr, 0, sizeof(pyr));
     const int L = lk_levels(w, h, win, max_level);
     if (L > kLkMaxLevels) return -2;
@@ -1868,6 +1871,14 @@ int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, 
     }
     const int sh_items = ((w + kShCols - 1) / kShCols) * ((h + kShRows - 1) / kShRows);   // level 0 is the largest
     FLOW_LAUNCH(d, "k_sharr", s, k_sharr, dim3((sh_items + 3) / 4, L, P), dim3(256), 0, s, pyr, iz, d->pz);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// The LK iterations on the pyramids launch_lk_pyramids built (ordered before this on `s`).
+int launch_lk_track(const FlowDev* d, const LkPyr& pyr, int win, int max_count, double eps, hipStream_t s,
+                    int64_t iz)
+{
+    const int P = d->npairs;
     launch_flow_index(d, s);            // the host LK entry point sets npts without cornerSubPix
     int* itc = nullptr;
     if (getenv("COEB_SUBPIX_COUNT")) {
@@ -1877,6 +1888,15 @@ int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, 
     FLOW_LAUNCH(d, "k_lk", s, k_lk, dim3(flow_grid(d, 4)), dim3(256), 0, s, pyr, d->pts, d->offs, P, d->nxt,
                 d->status, win, max_count, eps * eps, iz, d->pz, itc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_lk(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, int win,
+              int max_level, int max_count, double eps, hipStream_t s, int64_t iz = 0)
+{
+    LkPyr pyr;
+    const int rc = launch_lk_pyramids(d, prev, cur, w, h, stride, win, max_level, s, iz, pyr);
+    if (rc) return rc;
+    return launch_lk_track(d, pyr, win, max_count, eps, s, iz);
 }
 
 int launch_fm(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, int h, int stride, int edge, double limit,
@@ -2123,9 +2143,25 @@ extern "C" int coeb_internal_pmo_batch(coeb_ctx* c, const uint8_t* d_gray, int F
     subpix_mask(10, mask);
     FL_TRY(c, hipMemcpyAsync(fc.d.mexp, mask, kSubpixMaskBytes, hipMemcpyHostToDevice, fc.s));
     const int64_t iz = (int64_t)w * h;
+    // COEB_FLOW_SIDE=1: the LK pyramids go to the context's side stream (idle until extraction)
+    // beside the corner detection, and the context stream joins them before k_lk (measured slower)
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    const bool split = coeb_internal_flow_side(c, &side, &fork, &join) == 0;
+    LkPyr pyr;
+    if (split) {
+        FL_TRY(c, hipEventRecord(fork, fc.s));
+        FL_TRY(c, hipStreamWaitEvent(side, fork, 0));
+        if (launch_lk_pyramids(&fc.d, d_gray, d_gray + iz, w, h, w, 22, 5, side, iz, pyr))
+            return coeb_internal_error(c, COEB_EDEVICE, "moving-object batch: launch failed");
+        FL_TRY(c, hipEventRecord(join, side));
+    }
     if (launch_gf(&fc.d, d_gray, w, h, w, 1000, 0.01, 8.0, 0.04, fc.s, iz) ||
-        launch_subpix(&fc.d, d_gray, w, h, w, 20, 0.03, fc.s, iz) ||
-        launch_lk(&fc.d, d_gray, d_gray + iz, w, h, w, 22, 5, 20, 0.01, fc.s, iz) ||
+        launch_subpix(&fc.d, d_gray, w, h, w, 20, 0.03, fc.s, iz))
+        return coeb_internal_error(c, COEB_EDEVICE, "moving-object batch: launch failed");
+    if (split) FL_TRY(c, hipStreamWaitEvent(fc.s, join, 0));
+    if ((split ? launch_lk_track(&fc.d, pyr, 22, 20, 0.01, fc.s, iz)
+               : launch_lk(&fc.d, d_gray, d_gray + iz, w, h, w, 22, 5, 20, 0.01, fc.s, iz)) ||
         launch_fm(&fc.d, d_gray, d_gray + iz, w, h, w, 5, 2120.0, fc.s, tm_cap, iz, tm_out + (size_t)tm_cap * 2,
                   ntm_out + 1))
         return coeb_internal_error(c, COEB_EDEVICE, "moving-object batch: launch failed");
