@@ -59,7 +59,7 @@ constexpr int kGfThreads = 1024;
 // neighbours below it unless the response plateaus); more is reported as -1
 inline int gf_key_cap(int w, int h) { return std::max(16384, w * h / 4); }
 constexpr int kLkMaxLevels = 8;
-constexpr int kFmThreads = 1024;
+constexpr int kFmThreads = 128;     // threads per pair of k_fm (COEB_FM_THREADS: 128 / 256 / 512 / 1024)
 constexpr int kFmChunk = 32;         // RANSAC hypotheses per chunk
 
 __device__ __forceinline__ int reflect101(int p, int n)
@@ -283,21 +283,27 @@ __global__ __launch_bounds__(256) void k_gf_candidates(const float* __restrict__
     }
 }
 
-// block-wide exclusive prefix of one flag per thread (1024 threads); returns the total
-__device__ int block_scan_1024(int flag, int* s_w, int& excl)
+// block-wide exclusive prefix of a per-thread count (NT threads, any counts); returns the total
+template <int NT>
+__device__ int block_scan_counts(int cnt, int* s_w, int& excl)
 {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t b = __ballot(flag);
-    const int before = __popcll(b & ((1ull << lane) - 1ull));
+    int x = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
     __syncthreads();
-    if (lane == 0) s_w[wv] = __popcll(b);
+    if (lane == 63) s_w[wv] = x;
     __syncthreads();
     int base = 0, total = 0;
-    for (int i = 0; i < 16; i++) {
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) {
         base += i < wv ? s_w[i] : 0;
         total += s_w[i];
     }
-    excl = base + before;
+    excl = base + x - cnt;
     return total;
 }
 
@@ -1434,7 +1440,24 @@ struct FmOut {
     int64_t tm_z;       // batch: pair stride of tm / ntm in bytes when they are caller buffers (0: the pair block)
 };
 
-__global__ __launch_bounds__(kFmThreads) void k_fm(const uint8_t* __restrict__ prev, const uint8_t* __restrict__ cur,
+// NT threads per pair (COEB_FM_THREADS, default kFmThreads): the (hypothesis, model) scoring runs
+// NT / 64 waves wide, and the pair's latency is mostly the serial draws, 7-point solves and scan.
+// Per 513-pair launch (config D, profiles/r05/s25-s27): 1024 threads 0.81 ms (128 VGPRs and 208 B
+// of spills per lane, one pair per CU), 512 0.78, 256 0.46, 128 0.34 (191-203 VGPRs, no spills,
+// two pairs per CU in one round); config D's step 13.14-13.27 -> 12.35-12.43 ms at 128.
+#ifndef COEB_FM_MINWG
+#define COEB_FM_MINWG 0        // launch bound in waves per SIMD (0: the defaults below)
+#endif
+// The bound steers the register allocator more than the occupancy: k_fm<128> cannot reach 6 waves per
+// SIMD (its 45 KB of LDS allow 3 workgroups per CU) and lands on 203 VGPRs either way, but with a
+// 6-wave bound it spills 17 SGPRs instead of 74 (and 60 B of VGPRs to scratch) and runs 0.336-0.338
+// ms per 513-pair launch against 0.516-0.523 at 2-4 (profiles/r05/s30).
+template <int NT>
+constexpr int fm_bound() { return COEB_FM_MINWG ? COEB_FM_MINWG : NT == 1024 ? 4 : NT == 128 ? 6 : 2; }
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wpass-failed"
+template <int NT>
+__global__ __launch_bounds__(NT, fm_bound<NT>()) void k_fm(const uint8_t* __restrict__ prev, const uint8_t* __restrict__ cur,
                                                   int w, int h, int stride, const float* __restrict__ pxy,
                                                   const float* __restrict__ nxy, const uint8_t* __restrict__ status,
                                                   const int* __restrict__ d_n, int nmax, int edge, double limit,
@@ -1465,38 +1488,51 @@ __global__ __launch_bounds__(kFmThreads) void k_fm(const uint8_t* __restrict__ p
     __shared__ double s_F[9];
     __shared__ int s_ok, s_done, s_niters, s_base;
     __shared__ uint64_t s_rng;
+    constexpr int E = kMaxPts / NT;     // points per thread in the ordered compactions
+    static_assert(E * NT == kMaxPts && NT >= 128 && NT <= 1024, "k_fm thread count");
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int n = *d_n;
     n = n < nmax ? n : nmax;
     n = n < kMaxPts ? n : kMaxPts;
-    // ---- SAD check (Frame.cc:337-365) and the ordered F_ sets ----
-    int keep = 0;
-    float2 p1 = make_float2(0.f, 0.f), p2 = p1;
-    if (tid < n) {
-        uint8_t st = status[tid];
-        p1 = make_float2(pxy[2 * tid], pxy[2 * tid + 1]);
-        p2 = make_float2(nxy[2 * tid], nxy[2 * tid + 1]);
-        if (st) {
-            const int x1 = (int)p1.x, y1 = (int)p1.y, x2 = (int)p2.x, y2 = (int)p2.y;
-            if (x1 < edge || x1 >= w - edge || x2 < edge || x2 >= w - edge || y1 < edge || y1 >= h - edge ||
-                y2 < edge || y2 >= h - edge) {
-                st = 0;
-            } else {
-                double sum = 0;
-                for (int j = 0; j < 9; j++) {
-                    const int dx = j % 3 - 1, dy = j / 3 - 1;
-                    sum += (double)abs((int)prev[(size_t)(y1 + dy) * stride + x1 + dx] -
-                                       (int)cur[(size_t)(y2 + dy) * stride + x2 + dx]);
+    // ---- SAD check (Frame.cc:337-365) and the ordered F_ sets: thread t takes points E t .. E t + E - 1
+    //      (the E loads of a thread are independent; rounds of NT points with a block scan each
+    //      measured slower, 0.38 vs 0.34 ms per 513-pair launch at 128 threads) ----
+    int keep[E], cnt = 0;
+    float2 p1[E], p2[E];
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+        const int i = E * tid + j;
+        keep[j] = 0;
+        p1[j] = make_float2(0.f, 0.f); p2[j] = p1[j];
+        if (i < n) {
+            uint8_t st = status[i];
+            p1[j] = make_float2(pxy[2 * i], pxy[2 * i + 1]);
+            p2[j] = make_float2(nxy[2 * i], nxy[2 * i + 1]);
+            if (st) {
+                const int x1 = (int)p1[j].x, y1 = (int)p1[j].y, x2 = (int)p2[j].x, y2 = (int)p2[j].y;
+                if (x1 < edge || x1 >= w - edge || x2 < edge || x2 >= w - edge || y1 < edge || y1 >= h - edge ||
+                    y2 < edge || y2 >= h - edge) {
+                    st = 0;
+                } else {
+                    double sum = 0;
+                    for (int k = 0; k < 9; k++) {
+                        const int dx = k % 3 - 1, dy = k / 3 - 1;
+                        sum += (double)abs((int)prev[(size_t)(y1 + dy) * stride + x1 + dx] -
+                                           (int)cur[(size_t)(y2 + dy) * stride + x2 + dx]);
+                    }
+                    if (sum > limit) st = 0;
                 }
-                if (sum > limit) st = 0;
             }
+            keep[j] = st != 0;
+            if (out.state) out.state[i] = (uint8_t)keep[j];
         }
-        keep = st != 0;
-        if (out.state) out.state[tid] = (uint8_t)keep;
+        cnt += keep[j];
     }
     int pos;
-    const int nf = block_scan_1024(keep, s_w, pos);
-    if (keep) { s_m1[pos] = p1; s_m2[pos] = p2; s_map[pos] = (uint16_t)tid; }
+    const int nf = block_scan_counts<NT>(cnt, s_w, pos);
+#pragma unroll
+    for (int j = 0; j < E; j++)
+        if (keep[j]) { s_m1[pos] = p1[j]; s_m2[pos] = p2[j]; s_map[pos] = (uint16_t)(E * tid + j); pos++; }
     if (tid == 0) {
         s_ok = 0; s_done = 0; s_base = 0; s_rng = ~0ull;
         if (out.nf) *out.nf = nf;
@@ -1560,7 +1596,7 @@ __global__ __launch_bounds__(kFmThreads) void k_fm(const uint8_t* __restrict__ p
             if (tid < kFmChunk) s_nm[tid] = s_found[tid] ? run7point(s_sub1[tid], s_sub2[tid], s_A[tid], s_perm[tid], s_models[tid]) : 0;
             __syncthreads();
             // score every (hypothesis, model): one wave each
-            for (int pr = wv; pr < kFmChunk * 3; pr += kFmThreads / 64) {
+            for (int pr = wv; pr < kFmChunk * 3; pr += NT / 64) {
                 const int hh = pr / 3, m = pr - hh * 3;
                 if (m >= s_nm[hh]) continue;
                 const double* F = s_models[hh] + 9 * m;
@@ -1637,26 +1673,40 @@ __global__ __launch_bounds__(kFmThreads) void k_fm(const uint8_t* __restrict__ p
         return;
     }
     if (tid < 9 && out.F) out.F[tid] = s_F[tid];
-    int flag = 0;
-    float2 q2 = make_float2(0.f, 0.f);
-    if (tid < nf) {
-        const float2 q1 = s_m1[tid];
-        q2 = s_m2[tid];
-        const double px = q1.x, py = q1.y;
-        const double A = s_F[0] * px + s_F[1] * py + s_F[2];
-        const double B = s_F[3] * px + s_F[4] * py + s_F[5];
-        const double Cc = s_F[6] * px + s_F[7] * py + s_F[8];
-        const double dd = fabs(A * q2.x + B * q2.y + Cc) / sqrt(A * A + B * B);
-        flag = !(dd <= 1);
+    int flag[E], fcnt = 0;
+    float2 q2[E];
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+        const int i = E * tid + j;
+        flag[j] = 0;
+        q2[j] = make_float2(0.f, 0.f);
+        if (i < nf) {
+            const float2 q1 = s_m1[i];
+            q2[j] = s_m2[i];
+            const double px = q1.x, py = q1.y;
+            const double A = s_F[0] * px + s_F[1] * py + s_F[2];
+            const double B = s_F[3] * px + s_F[4] * py + s_F[5];
+            const double Cc = s_F[6] * px + s_F[7] * py + s_F[8];
+            const double dd = fabs(A * q2[j].x + B * q2[j].y + Cc) / sqrt(A * A + B * B);
+            flag[j] = !(dd <= 1);
+        }
+        fcnt += flag[j];
     }
     int tpos;
-    const int nt = block_scan_1024(flag, s_w, tpos);
-    if (flag && tpos < out.tm_cap) {
-        out.tm[2 * tpos] = q2.x;
-        out.tm[2 * tpos + 1] = q2.y;
-    }
+    const int nt = block_scan_counts<NT>(fcnt, s_w, tpos);
+#pragma unroll
+    for (int j = 0; j < E; j++)
+        if (flag[j]) {
+            if (tpos < out.tm_cap) {
+                out.tm[2 * tpos] = q2[j].x;
+                out.tm[2 * tpos + 1] = q2[j].y;
+            }
+            tpos++;
+        }
     if (tid == 0) *out.ntm = nt;
 }
+
+#pragma clang diagnostic pop
 
 // ============================== host side ==============================
 struct FlowDev {
@@ -1904,9 +1954,17 @@ int launch_fm(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, 
 {
     FmOut o;
     o.tm = d->tm; o.ntm = d->ntm; o.state = d->state; o.F = d->F; o.nf = d->nf; o.tm_cap = tm_cap; o.tm_z = 0;
-    FLOW_LAUNCH(d, "k_fm", s, k_fm, dim3(1, 1, d->npairs), dim3(kFmThreads), 0, s, prev, cur, w, h, stride, d->pts, d->nxt,
-                       d->status, d->npts, kMaxPts, edge, limit, 0.1, 0.99,
-                       tm_out ? FmOut{tm_out, ntm_out, o.state, o.F, o.nf, tm_cap, (int64_t)tm_cap * 8} : o, iz, d->pz);
+    const FmOut oo = tm_out ? FmOut{tm_out, ntm_out, o.state, o.F, o.nf, tm_cap, (int64_t)tm_cap * 8} : o;
+    int nt = kFmThreads;
+    if (const char* e = getenv("COEB_FM_THREADS")) nt = atoi(e);
+#define COEB_FM_GO(NT_)                                                                                          \
+    FLOW_LAUNCH(d, "k_fm", s, k_fm<NT_>, dim3(1, 1, d->npairs), dim3(NT_), 0, s, prev, cur, w, h, stride, d->pts, \
+                d->nxt, d->status, d->npts, kMaxPts, edge, limit, 0.1, 0.99, oo, iz, d->pz)
+    if (nt == 128) COEB_FM_GO(128);
+    else if (nt == 256) COEB_FM_GO(256);
+    else if (nt == 512) COEB_FM_GO(512);
+    else COEB_FM_GO(1024);
+#undef COEB_FM_GO
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -754,7 +754,10 @@ __global__ __launch_bounds__(NT) void k_match_lists(MatchCam cam, MatchBufs b, f
 }
 
 template <bool kLds, int NT>
-__global__ __launch_bounds__(NT, 4) void k_match(MatchCam cam, MatchBufs b, float th0, int bmono, int check_ori,
+#ifndef COEB_MATCH_MINWG
+#define COEB_MATCH_MINWG 4     // launch bound in waves per SIMD (4: two 512-thread pairs per CU)
+#endif
+__global__ __launch_bounds__(NT, COEB_MATCH_MINWG) void k_match(MatchCam cam, MatchBufs b, float th0, int bmono, int check_ori,
                                                      int retry_below, int force_seq, int nsplit)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
