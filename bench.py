@@ -57,7 +57,9 @@ CONFIGS = {
     "C": dict(w=640, h=480, nfeatures=1000, dyn=True, batch=3072, pipelines=3, side_stream="shared",
               workload="640x480, 1000 kp, YOLO-bbox dynamic mask (2 boxes, 60 T_M points, blur_flag [0,1]) + "
                        "depth association (ComputeStereoFromRGBD) + match to prev frame (BASELINE configs[2])"),
-    "D": dict(w=640, h=480, nfeatures=1000, chain=True, batch=1024, pipelines=2,
+    # D: two pipelines (three or four: 68.7-73.9 k); per-GPU batch 1024 / 1536 / 2048 / 3072 frames:
+    # 81.9-82.6 / 82.6-83.4 / 83.0-83.8 / 83.9-84.4 k frames/s (profiles/r05/s31, s31b): 3072 as for A and C
+    "D": dict(w=640, h=480, nfeatures=1000, chain=True, batch=3072, pipelines=2,
               workload="640x480, 1000 kp, the full Tracking::GrabImageRGBD loop per frame (BASELINE configs[4]): "
                        "RGB + 16U depth conversion, Frame ctor (ProcessMovingObject T_M from the previous frame, "
                        "YOLO-box blur flags, dynamic mask, ORB extraction), TrackWithMotionModel (SearchByProjection "
