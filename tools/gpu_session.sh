@@ -55,29 +55,32 @@ for step in "$@"; do
             ;;
         pmcB)
             export COEB_SIDE_STREAM=0
+            # config B: 512 frames as two pipelines, launches of 257 frames (256 + the halo frame)
             B="python bench.py --config B --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-e2e --no-extras"
             run pmcB_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcB_fetch -o run -- $B
             run pmcB_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcB_write -o run -- $B
             python tools/pmc_summary.py gpurun_out/pmcB_fetch/run_counter_collection.csv gpurun_out/pmcB_write/run_counter_collection.csv \
-                --json gpurun_out/pmc_traffic_1280x960.json --frames 513 --size 1280x960 --command "$B" > gpurun_out/pmcB_traffic.log 2>&1
+                --json gpurun_out/pmc_traffic_1280x960.json --frames 257 --size 1280x960 --command "$B" > gpurun_out/pmcB_traffic.log 2>&1
             run pmcB_sq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace --output-format csv -d gpurun_out/pmcB_sq -o run -- $B
             run pmcB_sq2 600 rocprofv3 --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmcB_sq2 -o run -- $B
             python tools/pmc_summary.py gpurun_out/pmcB_sq/run_counter_collection.csv gpurun_out/pmcB_sq2/run_counter_collection.csv \
-                --valu-json gpurun_out/pmc_valu_1280x960.json --frames 513 --size 1280x960 --command "$B" > gpurun_out/pmcB_valu.log 2>&1
+                --valu-json gpurun_out/pmc_valu_1280x960.json --frames 257 --size 1280x960 --command "$B" > gpurun_out/pmcB_valu.log 2>&1
             ;;
         benchB512) run benchB512 600 python bench.py --config B ;;
         pmcD)
             # the configs[4] loop's kernels (flow, pose, TrackLocalMap) with their own traffic / VALU passes
             export COEB_SIDE_STREAM=0
-            B="python bench.py --config D --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-e2e --no-extras"
+            # two 512-frame pipelines: launches of 515 frames (512 + the 3-frame halo; round 5 fixed the
+            # stale 259 that scaled the D line's traffic)
+            B="python bench.py --config D --pipelines 2 --batch 1024 --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-e2e --no-extras"
             run pmcD_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcD_fetch -o run -- $B
             run pmcD_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcD_write -o run -- $B
             python tools/pmc_summary.py gpurun_out/pmcD_fetch/run_counter_collection.csv gpurun_out/pmcD_write/run_counter_collection.csv \
-                --json gpurun_out/pmc_traffic_D.json --frames 259 --command "$B" > gpurun_out/pmcD_traffic.log 2>&1
+                --json gpurun_out/pmc_traffic_D.json --frames 515 --command "$B" > gpurun_out/pmcD_traffic.log 2>&1
             run pmcD_sq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace --output-format csv -d gpurun_out/pmcD_sq -o run -- $B
             run pmcD_sq2 600 rocprofv3 --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmcD_sq2 -o run -- $B
             python tools/pmc_summary.py gpurun_out/pmcD_sq/run_counter_collection.csv gpurun_out/pmcD_sq2/run_counter_collection.csv \
-                --valu-json gpurun_out/pmc_valu_D.json --frames 259 --command "$B" > gpurun_out/pmcD_valu.log 2>&1
+                --valu-json gpurun_out/pmc_valu_D.json --frames 515 --command "$B" > gpurun_out/pmcD_valu.log 2>&1
             ;;
         *) echo "unknown step $step" ;;
     esac

@@ -15,6 +15,8 @@ step() {   # name timeout cmd...
     echo "[$name] rc=$rc $(( $(date +%s) - t0 ))s"
     if [ $rc -ne 0 ]; then tail -n 5 "$O/$name.log"; exit $rc; fi
 }
+PART=${1:-all}
+if [ "$PART" = all ] || [ "$PART" = 1 ]; then
 step pytest_gpu 800 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread
 tail -n 2 $O/pytest_gpu.log
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
@@ -30,7 +32,10 @@ for t in ("bench", "benchB512", "benchC", "benchD"):
     print(t, "value", d["value"], "ms/step", d["ms_per_step"], "cpu", cb.get("value"), cb.get("spread", {}).get("min"),
           cb.get("spread", {}).get("max"), "roof", d["roofline"].get("kernel"), d["roofline"].get("frac"))
 PY
-bash tools/gpu_session.sh prof pmc pmcB pmcD timeline || exit $?
+fi
+if [ "$PART" = all ] || [ "$PART" = 2 ]; then
+bash tools/gpu_session.sh prof profD pmc pmcB pmcD timeline || exit $?
 bash tools/pipes.sh final_pipes > $O/pipes.txt 2>&1 || { tail -5 $O/pipes.txt; exit 1; }
 bash tools/pipes_mem.sh final_mem > $O/pipes_mem.txt 2>&1 || { tail -5 $O/pipes_mem.txt; exit 1; }
+fi
 echo done
