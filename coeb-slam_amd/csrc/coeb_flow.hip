@@ -941,7 +941,10 @@ __device__ __forceinline__ void tile_pairs_reflect(const uint8_t* img, int pitch
     }
 }
 
-__global__ __launch_bounds__(256) void k_lk(LkPyr pyr, const float* __restrict__ pxy0, const int* __restrict__ offs, int P,
+#ifndef COEB_LK_MINW
+#define COEB_LK_MINW 1         // launch bound of k_lk in waves per SIMD
+#endif
+__global__ __launch_bounds__(256, COEB_LK_MINW) void k_lk(LkPyr pyr, const float* __restrict__ pxy0, const int* __restrict__ offs, int P,
                                             float* __restrict__ nxy0, uint8_t* __restrict__ status0, int win, int max_count,
                                             double eps2, int64_t iz, int64_t pz, int* __restrict__ itcount)
 {
