@@ -533,9 +533,20 @@ __device__ void active_chi2(PoseLds& L, const PoseBufs& b, const PoseCam& cm, in
 
 // phase clocks of thread 0 (diagnostic, COEB_POSE_TIMING): [0] chi2 passes, [1] build passes,
 // [2] thread-0 solve + exp + bookkeeping, [3] classification, [4] total, [5] iterations, [6] trials
-#define PT_MARK(var) long long var = b.timing ? (long long)clock64() : 0
-#define PT_ADD(slot, t0) do { if (b.timing && threadIdx.x == 0) b.timing[(int64_t)blockIdx.x * 8 + (slot)] += (long long)clock64() - (t0); } while (0)
-#define PT_INC(slot) do { if (b.timing && threadIdx.x == 0) b.timing[(int64_t)blockIdx.x * 8 + (slot)] += 1; } while (0)
+// Compiled in only with -DCOEB_POSE_CLOCK=1 (tools/_pose_timing.py's builds): the runtime checks of
+// b.timing alone cost 19 SGPR and 2 VGPR spills in k_pose<5> (3.91 -> 3.85 ms per config-D step
+// without them, profiles/r05/s34).
+#ifndef COEB_POSE_CLOCK
+#define COEB_POSE_CLOCK 0
+#endif
+#if COEB_POSE_CLOCK
+#define PT_ON(b) ((b).timing)
+#else
+#define PT_ON(b) false
+#endif
+#define PT_MARK(var) long long var = PT_ON(b) ? (long long)clock64() : 0
+#define PT_ADD(slot, t0) do { if (PT_ON(b) && threadIdx.x == 0) b.timing[(int64_t)blockIdx.x * 8 + (slot)] += (long long)clock64() - (t0); } while (0)
+#define PT_INC(slot) do { if (PT_ON(b) && threadIdx.x == 0) b.timing[(int64_t)blockIdx.x * 8 + (slot)] += 1; } while (0)
 
 #ifndef COEB_POSE_MINWG
 #define COEB_POSE_MINWG 2      // launch bound: workgroups per CU the register budget must allow
@@ -704,7 +715,7 @@ __global__ __launch_bounds__(kPT, EPT == 0 ? COEB_POSE_MINWG0 : COEB_POSE_MINWG)
                 PT_MARK(t_c1);
                 active_chi2<EPT>(L, b, cm, f, ne, robust, delta, ES, &L.tr[0].s, (int)sizeof(PoseTrial), T);
                 PT_ADD(0, t_c1);
-                t_s0 = b.timing ? (long long)clock64() : 0;
+                t_s0 = PT_ON(b) ? (long long)clock64() : 0;
                 if (tid == 0) {
                     int q = L.qmax, stop = 0;
                     double rho = 0.0;

@@ -1,5 +1,6 @@
 """k_pose phase clocks over one config-D batch (COEB_POSE_TIMING=1): median clock64 cycles
-per phase across the 256 frames.  Diagnostic only."""
+per phase across the 256 frames.  Diagnostic only; needs a library built with the clocks compiled in:
+tools/_build_var.sh clock "-DCOEB_POSE_CLOCK=1" and COEB_LIB_PATH=coeb-slam_amd/lib/var_clock.so."""
 import os
 import sys
 
