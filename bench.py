@@ -796,13 +796,21 @@ def main():
         args.batch = CONFIGS[args.config].get("batch", 256)
     if args.pipelines is None:
         args.pipelines = CONFIGS[args.config].get("pipelines", 1)
-    if args.side_stream is None:
+    # read by each context when it first extracts (csrc/coeb_capi.hip side_stream).  The config's
+    # default only adds the shared stream; an explicit --side-stream also overrides the environment
+    # (the PMC / profiling passes export COEB_SIDE_STREAM=0 and pass no --side-stream)
+    explicit = args.side_stream is not None
+    if not explicit:
         args.side_stream = CONFIGS[args.config].get("side_stream", "own")
-    # read by each context when it first extracts (csrc/coeb_capi.hip side_stream)
     if args.side_stream == "shared":
         os.environ["COEB_SIDE_SHARED"] = "1"
+        if explicit:
+            os.environ["COEB_SIDE_STREAM"] = "1"
     elif args.side_stream == "off":
         os.environ["COEB_SIDE_STREAM"] = "0"
+    elif explicit:
+        os.environ["COEB_SIDE_SHARED"] = "0"
+        os.environ["COEB_SIDE_STREAM"] = "1"
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     if env_world > 1 or "LOCAL_RANK" in os.environ:
         # one process per GPU under torch.distributed.run

@@ -189,3 +189,18 @@ def test_bench_config_dry_run(config):
     want = {"C": "configs[2]", "D": "configs[4]"}[config]
     assert want in rec["config"]["workload"] and rec["n_gpus"] == 1 and rec["unit"] == "frames/s"
     assert abs(rec["value"] - 4 * 2 / (rec["ms_per_step"] * 2 / 1e3)) / rec["value"] < 1e-3
+    # config C runs its pipelines on one shared side stream, D a side stream each (bench.py CONFIGS)
+    assert rec["config"]["side_stream"] == {"C": "shared", "D": "own"}[config]
+
+
+def test_bench_side_stream_option():
+    """--side-stream overrides the config's choice and the environment (set here to the opposite),
+    and the line reports what ran."""
+    for opt, want in (("off", "off"), ("shared", "shared"), ("own", "own")):
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--side-stream", opt, "--steps", "1", "--warmup", "0",
+               "--batch", "2", "--dry-run", "--no-cpu-baseline"]
+        env = dict(os.environ, COEB_SIDE_STREAM="0" if opt != "off" else "1", COEB_SIDE_SHARED="1" if opt == "own" else "0")
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+        assert out.returncode == 0, out.stderr[-2000:]
+        rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+        assert rec["config"]["side_stream"] == want
