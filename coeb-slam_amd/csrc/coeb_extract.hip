@@ -372,7 +372,15 @@ __device__ __forceinline__ void pyr_rows_out(const uint32_t (&w)[PR_ROWS][4], co
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_pyr_rows(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
+#ifndef COEB_PYR_MINW
+#define COEB_PYR_MINW 0         // experiment knob: a min-waves-per-SIMD launch bound for k_pyr_rows (0: none)
+#endif
+#if COEB_PYR_MINW
+#define COEB_PYR_LB __launch_bounds__(kThreads, COEB_PYR_MINW)
+#else
+#define COEB_PYR_LB __launch_bounds__(kThreads)
+#endif
+__global__ COEB_PYR_LB void k_pyr_rows(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
                                                        int sh, uint8_t* __restrict__ dst, int64_t dst_fs, int dp,
                                                        int dw, int dh, const int* __restrict__ tab, int xmax, int xs,
                                                        const int4* __restrict__ yrow)
@@ -601,7 +609,15 @@ __device__ __forceinline__ int reflect_row(int r, int h)
 constexpr int kBlurQuad = 4 * kBlurCols;     // columns of one k_blur_rows wave item (14 tiles of 16)
 static_assert(kBlurQuad % 16 == 0, "a wave item must cover whole 16-column tiles");
 
-__global__ __launch_bounds__(kThreads) void k_blur_rows(const Plan* __restrict__ P, ExtractBufs b, BlurWork bw)
+#ifndef COEB_BLUR_MINW
+#define COEB_BLUR_MINW 0         // experiment knob: a min-waves-per-SIMD launch bound for k_blur_rows (0: none)
+#endif
+#if COEB_BLUR_MINW
+#define COEB_BLUR_LB __launch_bounds__(kThreads, COEB_BLUR_MINW)
+#else
+#define COEB_BLUR_LB __launch_bounds__(kThreads)
+#endif
+__global__ COEB_BLUR_LB void k_blur_rows(const Plan* __restrict__ P, ExtractBufs b, BlurWork bw)
 {
 #if COEB_BLUR_TILED
     // 8 output rows of the wave item, transposed through LDS into whole 128-B tile lines
@@ -1763,7 +1779,15 @@ __device__ __forceinline__ void child_rect(const int4 p, int q, int4* out, int* 
 __device__ long long g_oct_clk[4096 * 6];
 
 template <int NT>
-__global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, ExtractBufs b, int level0, int oct_w,
+#ifndef COEB_OCT_MINW
+#define COEB_OCT_MINW 0         // experiment knob: a min-waves-per-SIMD launch bound for k_octree (0: none)
+#endif
+#if COEB_OCT_MINW
+#define COEB_OCT_LB __launch_bounds__(NT, COEB_OCT_MINW)
+#else
+#define COEB_OCT_LB __launch_bounds__(NT)
+#endif
+__global__ COEB_OCT_LB void k_octree(const Plan* __restrict__ P, ExtractBufs b, int level0, int oct_w,
                                                 int oct_kl)   // this launch's node slots / LDS key capacity
 {
     const long long oc_t0 = COEB_OCT_CLOCK ? (long long)clock64() : 0;
@@ -2409,7 +2433,15 @@ __device__ __forceinline__ void ic_row_load(const uint8_t* rp, uint4& c0, uint4&
 #endif
 template <bool kVec0, int KP>
 // 24 waves per CU (launch bound 6 blocks: 80 VGPRs, 3 spilled) measured 0.253 vs 0.212 ms/step
-__global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ P, ExtractBufs b)
+#ifndef COEB_DESC_MINW
+#define COEB_DESC_MINW 0         // experiment knob: a min-waves-per-SIMD launch bound for k_describe (0: none)
+#endif
+#if COEB_DESC_MINW
+#define COEB_DESC_LB __launch_bounds__(kThreads, COEB_DESC_MINW)
+#else
+#define COEB_DESC_LB __launch_bounds__(kThreads)
+#endif
+__global__ COEB_DESC_LB void k_describe(const Plan* __restrict__ P, ExtractBufs b)
 {
     constexpr int kLpk = 64 / KP;          // lanes per keypoint in phase A
     constexpr int kHl = kLpk / 2;          // lanes per half (rows -|v| / +|v|)
