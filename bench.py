@@ -45,7 +45,10 @@ CONFIGS = {
     # per corner / pair / frame, so they need many frames in flight: batch x pipelines 256 x 1 measured
     # 51.4 k frames/s, 256 x 2 57.0 k, 512 x 2 61.6 k, 1024 x 2 64.5 k, 2048 x 2 64.5 k, 2048 x 4 58.1 k
     # (profiles/r03/s4/benchD_batch.txt).
-    "A": dict(w=640, h=480, nfeatures=1000, batch=3072, pipelines=3,
+    # A: each pipeline's side stream created with its context (COEB_SIDE_EAGER=1), so the six streams
+    # take the box's 4 hardware queues in (context, side) pairs: 8.27-8.31 ms per step against
+    # 8.33-8.38 when they are created at the first extraction (profiles/r05/s38, s38b; C and D: no gain)
+    "A": dict(w=640, h=480, nfeatures=1000, batch=3072, pipelines=3, side_eager=True,
               workload="640x480, 8-level pyramid, 1000 kp, extract + Hamming match to prev frame (BASELINE configs[1])"),
     # B: the fixed 512-frame batch of BASELINE configs[3] as 2 pipelines per GPU (per-rank shards of
     # 64-256 frames ran 5-10 % faster with 2 than with 1, profiles/r03/s5/shardB_pipelines.txt)
@@ -811,6 +814,8 @@ def main():
     elif explicit:
         os.environ["COEB_SIDE_SHARED"] = "0"
         os.environ["COEB_SIDE_STREAM"] = "1"
+    if CONFIGS[args.config].get("side_eager") and "COEB_SIDE_EAGER" not in os.environ:
+        os.environ["COEB_SIDE_EAGER"] = "1"      # read by coeb_create
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     if env_world > 1 or "LOCAL_RANK" in os.environ:
         # one process per GPU under torch.distributed.run
@@ -1024,7 +1029,9 @@ def rank_main(ranks, args):
                                           "GPU_MAX_HW_QUEUES unset (HIP default 4)",
                                 side_stream="off" if os.environ.get("COEB_SIDE_STREAM", "1")[:1] == "0" else
                                             ("shared" if os.environ.get("COEB_SIDE_SHARED", "0")[:1] == "1"
-                                             else "own")),
+                                             else "own"),
+                                side_stream_created="with the context" if os.environ.get("COEB_SIDE_EAGER", "0")[:1] == "1"
+                                                    else "at the first extraction"),
                     roofline=roof,
                     pipeline_roofline=dict(bytes_per_frame=int(pipeline_bytes),
                                            achieved_GBps=round(value * pipeline_bytes / 1e9, 3),

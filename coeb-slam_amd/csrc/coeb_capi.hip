@@ -828,6 +828,11 @@ coeb_ctx* coeb_create(const coeb_orb_params* params, int device, int max_width, 
         return nullptr;
     }
     c->hook.impl = &c->prof;
+    // COEB_SIDE_EAGER=1: create the side stream now, right after the context stream, so the
+    // contexts' streams take the hardware queues in (context, side) pairs (experiment knob; by
+    // default it is created at the first extraction, after every context stream of the process)
+    if (const char* e = getenv("COEB_SIDE_EAGER"))
+        if (e[0] == '1') (void)side_stream(c);
     if (hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         g_last_error = "coeb_create: event creation failed";
