@@ -129,6 +129,31 @@ def test_moving_tail_small_sets(ctx, oracle_mod, npts):
         eq(tm, rtm, "T_M")
 
 
+@pytest.mark.parametrize("threads", [256, 512, 1024])
+def test_moving_tail_fm_thread_counts(ctx, oracle_mod, monkeypatch, threads):
+    """k_fm with 256 / 512 / 1024 threads per pair (COEB_FM_THREADS; the default is 128): every
+    pair's SAD states, F and T_M against the oracle, and the LMeDS (9, 12 points) and RANSAC (15,
+    40) branches on the small sets."""
+    monkeypatch.setenv("COEB_FM_THREADS", str(threads))
+    for tag, prev, cur in PAIRS:
+        pts = oracle_mod.corner_subpix(prev, oracle_mod.good_features(prev))
+        nx, st = oracle_mod.lk_pyr(prev, cur, pts)
+        cases = [(pts, nx, st)]
+        if tag == PAIRS[2][0]:
+            for npts in (9, 12, 15, 40):
+                keep = np.nonzero(st)[0][:npts]
+                cases.append((pts[keep], nx[keep], st[keep]))
+        for p, q, s_ in cases:
+            tm, st2, F, nf = cf.MovingTail(ctx, prev, cur, p, q, s_)
+            rtm, rst2, rF, rnf = oracle_mod.moving_tail(prev, cur, p, q, s_)
+            eq(st2, rst2, tag + " state")
+            assert nf == rnf
+            assert (F is None) == (rF is None)
+            if F is not None:
+                assert np.array_equal(F, rF), (tag, len(p))
+                eq(tm, rtm, tag + " T_M")
+
+
 @pytest.mark.parametrize("tag,prev,cur", PAIRS, ids=[p[0] for p in PAIRS])
 def test_process_moving_object(ctx, oracle_mod, tag, prev, cur):
     tm, d = cf.ProcessMovingObject(ctx, prev, cur, debug=True)
