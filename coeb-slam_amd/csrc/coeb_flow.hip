@@ -492,6 +492,13 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
 #ifndef COEB_SP_SLOTS
 #define COEB_SP_SLOTS 9
 #endif
+#ifndef COEB_SP_PRPAD
+#define COEB_SP_PRPAD 1        // row padding of the rolling patch (floats)
+#endif
+#ifndef COEB_SP_TRPAD
+#define COEB_SP_TRPAD 5        // row padding of the term rows (doubles; >= 5: the sink slot G's terms)
+#endif
+static_assert(COEB_SP_TRPAD >= 5, "the term rows hold the sink slot's five terms");
 constexpr int kSpSlots = COEB_SP_SLOTS;   // corner slots per wave (9: 45 summing lanes)
 struct __attribute__((aligned(16))) SpSlot {      // read as three 16-byte words by the fill lanes
     const uint8_t* img;
@@ -514,8 +521,8 @@ __global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0,
     static_assert(NL <= 64, "one summing lane per slot and term");
     // slot G is a sink: the fill and term lanes past the last slot read and write it, so no
     // pass needs a branch and the LDS reads of all passes issue together
-    __shared__ __attribute__((aligned(16))) float pr[G + 1][4][BW + 1];   // rolling patch rows, row r at r & 3
-    __shared__ double tr[WW][NL + 5];                  // one window row's terms, [j][5 g + t]
+    __shared__ __attribute__((aligned(16))) float pr[G + 1][4][BW + COEB_SP_PRPAD];   // rolling patch rows, row r at r & 3
+    __shared__ double tr[WW][NL + COEB_SP_TRPAD];      // one window row's terms, [j][5 g + t]
     __shared__ SpSlot par[G + 1];
     __shared__ double ssum[NL];
     const int lane = threadIdx.x;
