@@ -119,7 +119,7 @@ __device__ __forceinline__ int2 flow_item(const int* __restrict__ offs, int P, i
 
 // offs[z] = sum over pairs < z of clamp(n_z, 0, nmax) (n_z at d_n + z * pz bytes), offs[P] = total
 __global__ __launch_bounds__(1024) void k_flow_index(const int* __restrict__ d_n, int64_t pz, int P, int nmax,
-                                                      int* __restrict__ offs)
+                                                      int* __restrict__ offs, int* __restrict__ lkq)
 {
     __shared__ int s_w[16];
     __shared__ int s_base;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(1024) void k_flow_index(const int* __restrict__ d_n
         if (threadIdx.x == 0) s_base = total;
         __syncthreads();
     }
-    if (threadIdx.x == 0) offs[P] = s_base;
+    if (threadIdx.x == 0) { offs[P] = s_base; *lkq = 0; }     // k_lk's point queue, for the launch after this
 }
 
 // ============================== goodFeaturesToTrack ==============================
@@ -951,15 +951,33 @@ __device__ __forceinline__ void tile_pairs_reflect(const uint8_t* img, int pitch
 #ifndef COEB_LK_MINW
 #define COEB_LK_MINW 1         // launch bound of k_lk in waves per SIMD
 #endif
+#ifndef COEB_LK_QUEUE
+#define COEB_LK_QUEUE 0        // points from a queue (1: 3.53 vs 3.29 ms per config-D step, profiles/r05/s43) or in grid-stride order (0)
+#endif
+// the next point of the queue for this wave (wave-uniform)
+__device__ __forceinline__ int lk_next(int* q)
+{
+    int v = 0;
+    if (__lane_id() == 0) v = atomicAdd(q, 1);
+    return __builtin_amdgcn_readfirstlane(v);
+}
 __global__ __launch_bounds__(256, COEB_LK_MINW) void k_lk(LkPyr pyr, const float* __restrict__ pxy0, const int* __restrict__ offs, int P,
                                             float* __restrict__ nxy0, uint8_t* __restrict__ status0, int win, int max_count,
-                                            double eps2, int64_t iz, int64_t pz, int* __restrict__ itcount)
+                                            double eps2, int64_t iz, int64_t pz, int* __restrict__ itcount,
+                                            int* __restrict__ lkq)
 {
     const int lane = threadIdx.x & 63;
     const int R0 = (lane >> 3) * 3, C0 = (lane & 7) * 3;
     const int nr = min(3, max(0, win - R0)), nc = nr > 0 ? min(3, max(0, win - C0)) : 0;   // this lane's pixels
     const int total = offs[P];
+#if COEB_LK_QUEUE
+    // points from a queue: a wave that drew fast-converging points takes more (measured slower than
+    // the grid-stride order: one atomic per point on one counter)
+    for (int item = lk_next(lkq); item < total; item = lk_next(lkq)) {
+#else
+    (void)lkq;
     for (int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); item < total; item += gridDim.x * 4) {
+#endif
     const int2 zp = flow_item(offs, P, item);
     const uint32_t z = (uint32_t)zp.x;
     const float* pxy = at_pair(pxy0, pz, z);
@@ -1850,7 +1868,8 @@ int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, in
 // goodFeaturesToTrack, which both consume unchanged (cornerSubPix refines them in place)
 void launch_flow_index(const FlowDev* d, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_flow_index, dim3(1), dim3(1024), 0, s, d->npts, d->pz, d->npairs, kMaxPts, d->offs);
+    hipLaunchKernelGGL(k_flow_index, dim3(1), dim3(1024), 0, s, d->npts, d->pz, d->npairs, kMaxPts, d->offs,
+                       d->ocnt + 3);
 }
 
 // workgroups of a persistent per-point launch (ipw points per workgroup and pass): enough to
@@ -1946,7 +1965,7 @@ int launch_lk_track(const FlowDev* d, const LkPyr& pyr, int win, int max_count, 
         itc = g_subpix_count;
     }
     FLOW_LAUNCH(d, "k_lk", s, k_lk, dim3(flow_grid(d, 4)), dim3(256), 0, s, pyr, d->pts, d->offs, P, d->nxt,
-                d->status, win, max_count, eps * eps, iz, d->pz, itc);
+                d->status, win, max_count, eps * eps, iz, d->pz, itc, d->ocnt + 3);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
