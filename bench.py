@@ -105,11 +105,179 @@ def load_batch(bp, cfg, w, h, F, first):
         bp.load_rgbd(rgb, dep, DEPTH_MAP_FACTOR, Tcw=Tcw)
         bp.set_frame_boxes(boxes[:, None, :])
         bp.host_frames = gray
+        # what parity_check hands the oracle: the raw RGB-D input the device converted itself
+        bp.bench_inputs = dict(first=first, rgb=rgb, dep=dep, boxes=boxes)
         return gray, Tcw
     frames = synth.make_frames(w, h, F, seed=1000, first=first)    # global frames first .. first+F-1
     dyn = dyn_batch(w, h, F, first) if cfg.get("dyn") else None
     bp.load(frames, Tcw=Tcw, dyn=dyn)
+    bp.bench_inputs = dict(first=first, frames=frames, dyn=dyn)
     return frames, Tcw
+
+
+def plan_pipelines(G, world, rank, pipelines, halo):
+    """The bench's per-rank schedule: rank `rank`'s matched chunk of the G-frame sequence
+    (dist.shard) split over up to `pipelines` contexts, each extracting the `halo` frames before
+    its part.  Returns [(first global frame, frames extracted, frames counted)] per pipeline."""
+    from coeb_front.dist import shard
+    _, lo, hi = shard(G, world, rank)
+    npipe = max(1, min(pipelines, hi - lo))
+    subs = []
+    for p in range(npipe):
+        _, a, b = shard(hi - lo, npipe, p)
+        f0 = max(lo + a - (halo - 1), 0)
+        subs.append((f0, lo + b - f0 + 1, b - a))
+    return subs
+
+
+def make_pipelines(cfg, subs, device, streams=1, dry_run=False, rank=0):
+    """One BatchPipeline per entry of plan_pipelines(), its synthetic input resident on the device
+    (what rank_main times, and what tests/test_gpu_bench_scale.py checks against the oracle)."""
+    bps = []
+    try:
+        for first_p, F_p, _ in subs:
+            if dry_run:
+                bpp = DryRunPipeline(rank)
+            else:
+                from coeb_front.pipeline import BatchPipeline
+                bpp = BatchPipeline(cfg["w"], cfg["h"], F_p, nfeatures=cfg["nfeatures"], device=device)
+            bps.append(bpp)
+            bpp.ctx.set_batch_streams(streams)
+            load_batch(bpp, cfg, cfg["w"], cfg["h"], F_p, first_p)
+    except BaseException:
+        for bpp in bps:
+            bpp.close()
+        raise
+    return bps
+
+
+def parity_picks(F, every=128):
+    """Frames of a pipeline's batch that parity_check samples: the first three, both sides of the
+    middle and of 1024, the last two, and every `every`-th frame."""
+    picks = {0, 1, 2, F // 2 - 1, F // 2, F - 2, F - 1} | set(range(0, F, every))
+    if F > 1024:
+        picks |= {1023, 1024}
+    return sorted(f for f in picks if 0 <= f < F)
+
+
+def _oracle_checker():
+    """The oracle module on its checker build (liborb_oracle.so, the build the tests use; the
+    CPU-baseline legs switch the module to their timed builds and back)."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.LIB, O._lib = os.path.join(ROOT, "oracle", "liborb_oracle.so"), None
+    return O
+
+
+def _diff_kps(got, ref_kps, ref_desc):
+    """Names of the fields in which a frame's device keypoints / descriptors differ from the oracle's."""
+    if len(got["kps"]) != len(ref_kps):
+        return ["count %d vs %d" % (len(got["kps"]), len(ref_kps))]
+    bad = [f for f in got["kps"].dtype.names if not np.array_equal(got["kps"][f].view(np.uint32),
+                                                                    ref_kps[f].view(np.uint32))]
+    if len(ref_kps) and not np.array_equal(got["desc"], ref_desc):
+        bad.append("descriptors (%d rows)" % int((got["desc"] != ref_desc).any(axis=1).sum()))
+    return bad
+
+
+def parity_check(bps, cfg, picks):
+    """The oracle on sampled frames of the bench's own pipelines, after their last step (it runs
+    after the timed region, in the CPU-baseline leg, and in tests/test_gpu_bench_scale.py).
+
+    picks[p] lists pipeline p's batch-local frames.  Every field is compared bit for bit: the
+    keypoint records (angles included) and descriptors, for f >= 1 the SearchByProjection count
+    and match indices (th 15, 2*th retry below 20 matches, Tracking.cc:947-958), and for config D
+    the whole configs[4] loop's per-frame records (bench.ChainCpu on frames f-3..f of the same
+    pipeline, which is every dependency of frame f: dist.shard_frames).  Returns a summary dict."""
+    O = _oracle_checker()
+    from coeb_front import synth
+    t0 = time.perf_counter()
+    w, h, nf = cfg["w"], cfg["h"], cfg["nfeatures"]
+    chain = bool(cfg.get("chain"))
+    ex = O.Extractor(nf, 1.2, 8, 20, 7)
+    cam = O.camera(ex, w, h, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+    depth = synth.make_depth(w, h)
+    I4 = np.eye(4, dtype=np.float32)
+    Tc = synth.motion_pose()
+    bad, nframes, nmatched = [], 0, 0
+    for p, (bp, fl) in enumerate(zip(bps, picks)):
+        inp = bp.bench_inputs
+        cache = {}
+
+        def extract(f):
+            if f not in cache:
+                fr = inp["frames"][f]
+                cache[f] = ex.extract(fr, *inp["dyn"][f]) if inp["dyn"] is not None else ex.extract(fr)
+            return cache[f]
+        for f in fl:
+            got = bp.frame(f, track=chain)
+            nframes += 1
+            tag = "pipeline %d frame %d (global %d)" % (p, f, inp["first"] + f)
+            if chain:
+                lo = max(0, f - 3)
+                cl = ChainCpu(O, cfg, inp["rgb"][lo:f + 1], inp["dep"][lo:f + 1], inp["boxes"][lo:f + 1])
+                cl.stride = bp.ctx.batch_results()[3]
+                for i in range(f + 1 - lo):
+                    cl.step(i)
+                r, res = cl.last
+            else:
+                r, res = extract(f), None
+            diff = _diff_kps(got, r["kps"], r["desc"])
+            if f and not chain:
+                prev = extract(f - 1)
+                last = O.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX, synth.TUM_FY,
+                                                  synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
+                ur, _ = O.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
+                nm, m = O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, I4, 15.0)
+                if nm < 20:
+                    nm, m = O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, I4, 30.0)
+                res = dict(nmatches=nm, match=m)
+            if f:
+                nmatched += 1
+                if got["nmatch"] != res["nmatches"] or not np.array_equal(got["match"], res["match"]):
+                    diff.append("matches %d vs %d" % (got["nmatch"], res["nmatches"]))
+            if f and chain:
+                diff += _diff_track(got, res)
+            if diff:
+                bad.append("%s: %s" % (tag, ", ".join(diff)))
+            if len(cache) > 8:
+                for k in sorted(cache)[:-2]:
+                    del cache[k]
+    return dict(bit_exact=not bad, frames=nframes, matched_frames=nmatched, pipelines=len(bps),
+                frames_per_pipeline=[len(fl) for fl in picks], mismatches=bad[:10], seconds=round(time.perf_counter() - t0, 2),
+                compared="keypoint records (every field, angles bitwise), 256-bit descriptors, SearchByProjection "
+                         "count + indices (th 15, retry 30)" + (", the configs[4] loop's T1 / nin1 / nmatchesMap / "
+                                                                 "local matches / T / inliers / outliers / state"
+                                                                 if chain else "") + " vs the oracle")
+
+
+def _diff_track(got, res):
+    """configs[4] per-frame records that differ (tests/test_gpu_parity.py::_check_chain's rules)."""
+    d = []
+    if not np.array_equal(got["T1"].view(np.uint32), np.asarray(res["T1"], np.float32).view(np.uint32)):
+        d.append("T1")
+    if got["nin1"] != res["nin1"]:
+        d.append("nin1 %d vs %d" % (got["nin1"], res["nin1"]))
+    if got["state"] != res["state"]:
+        d.append("state %d vs %d" % (got["state"], res["state"]))
+    if res["nmatches"] >= 20 and got["nmatches_map"] != res["nmatches_map"]:
+        d.append("nmatchesMap")
+    if res["state"] == 0:
+        if got["ninliers"] != 0 or not np.array_equal(got["T"].view(np.uint32),
+                                                       np.asarray(res["T1"], np.float32).view(np.uint32)):
+            d.append("pose / inliers of an untracked frame")
+        return d
+    if got["nlocal"] != res["nlocal"] or not np.array_equal(got["local_match"], res["local_match"]):
+        d.append("local matches %d vs %d" % (got["nlocal"], res["nlocal"]))
+    if got["ninliers"] != res["ninliers"]:
+        d.append("ninliers %d vs %d" % (got["ninliers"], res["ninliers"]))
+    if not np.array_equal(got["T"].view(np.uint32), res["T"].view(np.uint32)):
+        d.append("T")
+    h2 = res["has2"] > 0
+    if not np.array_equal(got["outlier"][h2], res["outlier"][h2]):
+        d.append("outliers")
+    return d
 
 
 def dyn_batch(w, h, F, seed0=0):
@@ -408,7 +576,7 @@ class ChainCpu:
         r = self.ex.extract(g, b, tm, bl)
         mf = O.mapframe_from_extraction(r["kps"], r["desc"], d, synth.TUM_FX, synth.TUM_FY, synth.TUM_CX,
                                         synth.TUM_CY, synth.TUM_BF)
-        T1 = np.eye(4, dtype=np.float32)
+        T1, res = np.eye(4, dtype=np.float32), None
         if self.state is not None:
             ur, _ = O.stereo_from_rgbd(r["kps"], d, synth.TUM_BF)
             res = O.track_frame(self.cam, self.isg, r, ur, self.state["mf"], self.state["mf_prev"], self.Tp,
@@ -416,6 +584,7 @@ class ChainCpu:
                                 cy=synth.TUM_CY, bf=synth.TUM_BF)
             T1 = res["T1"]
         self.state = dict(gray=g, mf=mf, mf_prev=self.state["mf"] if self.state else None, T1=T1)
+        self.last = (r, res)            # frame i's extraction and track_frame records (parity_check)
 
 
 def cpu_chain_baseline(cfg, seconds=15.0, min_frames=20):
@@ -873,7 +1042,7 @@ def rank_main(ranks, args):
     if ONE_DEVICE:
         local_rank = 0          # rehearsal: every rank's context on device 0
     from coeb_front import synth
-    from coeb_front.dist import shard, shard_frames
+    from coeb_front.dist import shard_frames
     cfg = CONFIGS[args.config]
     w, h = cfg["w"], cfg["h"]
     strong = args.global_frames is not None
@@ -883,26 +1052,12 @@ def rank_main(ranks, args):
     chain = bool(cfg.get("chain"))
     halo = 3 if chain else 1
     _, nmatched = shard_frames(G, world, rank, halo=halo)[1:]
-    # the rank's matched chunk [lo, hi) split over its pipelines, each extracting its own halo
-    _, lo, hi = shard(G, world, rank)
-    npipe = max(1, min(args.pipelines, hi - lo))
-    subs = []
-    for p in range(npipe):
-        _, a, b = shard(hi - lo, npipe, p)
-        f0 = max(lo + a - (halo - 1), 0)
-        subs.append((f0, lo + b - f0 + 1, b - a))
-    bps = []
-    for first_p, F_p, _ in subs:
-        if args.dry_run:
-            bpp = DryRunPipeline(rank)
-        else:
-            from coeb_front.pipeline import BatchPipeline
-            bpp = BatchPipeline(w, h, F_p, nfeatures=cfg["nfeatures"], device=local_rank)
-        bpp.ctx.set_batch_streams(args.streams)
-        frames, Tcw = load_batch(bpp, cfg, w, h, F_p, first_p)
-        del frames
-        bps.append(bpp)
-    bp = bps[0]                          # results, roofline pass, extras and the PCIe leg use pipeline 0
+    # the rank's matched chunk split over its pipelines, each extracting its own halo
+    subs = plan_pipelines(G, world, rank, args.pipelines, halo)
+    npipe = len(subs)
+    bps = make_pipelines(cfg, subs, local_rank, args.streams, args.dry_run, rank)
+    Tcw = np.stack([synth.motion_pose()] * subs[0][1])
+    bp = bps[0]                         # results, roofline pass, extras and the PCIe leg use pipeline 0
     first, F, nmatched0 = subs[0]
     # every rank states what it covers; the sum must be the whole sequence
     covered = int(ranks.sum(nmatched))
@@ -1048,6 +1203,10 @@ def rank_main(ranks, args):
             line["flow_per_pair"] = dict(harris_keys=round(flow["keys"], 1), corners=round(flow["corners"], 1))
         if ONE_DEVICE and world > 1:
             line["rehearsal_one_device"] = True
+        if not args.no_cpu_baseline and world == 1 and not args.dry_run:
+            # the timed pipelines' own outputs (their last step) against the oracle, before the
+            # extras below reload pipeline 0: 4 frames of pipeline 0, every field bit for bit
+            line["parity_sample"] = parity_check([bp], cfg, [[1, 2, F // 2, F - 1]])
         if not args.no_extras and world == 1 and not args.dry_run:
             line["extras"] = extras_timing(bp.ctx, out, w, h)
             line["extras"]["single_frame"] = single_frame_timing(w, h)

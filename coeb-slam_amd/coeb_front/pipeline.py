@@ -157,6 +157,42 @@ class BatchPipeline:
             nm = [None] + [int(x) for x in nm[1:]]
         return out, matches, nm
 
+    def frame(self, f, track=False):
+        """Host copies of frame f's results alone (a few KB instead of the whole batch): its
+        keypoints and descriptors, and for f >= 1 its SearchByProjection count and match indices;
+        with track=True also the configs[4] loop's per-frame records as track_results() gives
+        them (motion-model pose T1 / inliers nin1, TrackLocalMap pose T / inliers, nmatchesMap,
+        local-map matches, outlier flags, state)."""
+        if not 0 <= f < self.F:
+            raise IndexError("frame %d outside the batch of %d" % (f, self.F))
+        c = self.ctx
+        kp_ptr, desc_ptr, cnt_ptr, kcap = c.batch_results()
+        n = int(c.download(cnt_ptr + 4 * f, 4, np.int32)[0])
+        out = dict(kps=c.download(kp_ptr + 28 * kcap * f, 28 * n).view(KEYPOINT_DTYPE),
+                   desc=c.download(desc_ptr + 32 * kcap * f, 32 * n).reshape(n, 32))
+        if f == 0:
+            return out
+        m_ptr, n_ptr = c.batch_match_results()
+        out["nmatch"] = int(c.download(n_ptr + 4 * f, 4, np.int32)[0])
+        out["match"] = c.download(m_ptr + 4 * kcap * f, 4 * n, np.int32)
+        if not track:
+            return out
+        t_ptr, ni_ptr, _ = c.batch_pose_results()
+        out["T1"] = c.download(t_ptr + 64 * f, 64, np.float32).reshape(4, 4)
+        out["nin1"] = int(c.download(ni_ptr + 4 * f, 4, np.int32)[0])
+        t_ptr, ni_ptr, nm_ptr, nl_ptr, lm_ptr, o_ptr = c.batch_track_results()
+        out["T"] = c.download(t_ptr + 64 * f, 64, np.float32).reshape(4, 4)
+        out["ninliers"] = int(c.download(ni_ptr + 4 * f, 4, np.int32)[0])
+        out["nmatches_map"] = int(c.download(nm_ptr + 4 * f, 4, np.int32)[0])
+        out["nlocal"] = int(c.download(nl_ptr + 4 * f, 4, np.int32)[0])
+        out["local_match"] = c.download(lm_ptr + 4 * kcap * f, 4 * n, np.int32)
+        out["outlier"] = c.download(o_ptr + kcap * f, n, np.uint8)
+        if out["nmatch"] < 20 or out["nmatches_map"] < 10:           # the rule of track_results()
+            out["state"] = 0
+        else:
+            out["state"] = 2 if out["ninliers"] >= 30 else 1
+        return out
+
     def pose_results(self):
         """Host copies after run(pose=True): Tcw (F, 4, 4) (frame 0 unused), inliers per frame
         (0: not tracked), outlier flags per frame (frame 0: None)."""

@@ -22,6 +22,7 @@ for step in "$@"; do
     if [ "$SIDE0" = unset ]; then unset COEB_SIDE_STREAM; else export COEB_SIDE_STREAM=$SIDE0; fi
     case "$step" in
         pytest) run pytest_gpu 900 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread ;;
+        scale) run scale 900 python -u -m pytest tests/test_gpu_bench_scale.py -v -s -m gpu --timeout 300 --timeout-method thread ;;
         pytestall) run pytest_gpu 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
