@@ -1210,6 +1210,7 @@ def rank_main(ranks, args):
         if not args.no_extras and world == 1 and not args.dry_run:
             line["extras"] = extras_timing(bp.ctx, out, w, h)
             line["extras"]["single_frame"] = single_frame_timing(w, h)
+            line["extras"]["single_frame_cpp"] = single_frame_cpp(w, h)
             if not cfg.get("dyn") and not cfg.get("pose") and not chain:
                 line["extras"]["config5_tracking"] = config5_timing(bp, nmatched0)
                 line["extras"]["config3_dynamic_mask"] = config3_timing(bp, synth.make_frames(w, h, F, seed=1000),
@@ -1276,50 +1277,93 @@ def e2e_timing(frames, Tcw, ranks, G, steps, cfg, device):
                      "on the compute stream)")
 
 
-def single_frame_timing(w, h, reps=50):
+def single_frame_timing(w, h, reps=50, warm=5):
     """Drop-in latency of one frame from host buffers, as the sequential Tracking thread calls it
     (Tracking.cc:229 -> Frame ctor -> ExtractORB; ComputeStereoFromRGBD; TrackWithMotionModel's
-    SearchByProjection): coeb_extract + coeb_stereo_from_rgbd + coeb_match_lastframe, mean ms."""
+    SearchByProjection, Tracking.cc:947-958): coeb_extract + coeb_stereo_from_rgbd +
+    coeb_match_lastframe (th 15, retry 30 below 20 matches), frame i matched against frame i-1's
+    extraction (its MapPoint snapshot -- world positions from its depth, its descriptors -- is the
+    Tracking state the adapter packs, built before the timer starts).  Median ms per frame, and
+    the median of each call."""
     import ctypes as C
     import coeb_front as cf
     from coeb_front import synth
     ctx = cf.Context(max_width=w, max_height=h, max_batch=1)
     try:
-        fr = synth.make_frames(w, h, reps + 1, seed=77)
+        fr = synth.make_frames(w, h, reps + warm + 1, seed=77)
         depth = synth.make_depth(w, h)
         cam = cf.make_camera(synth.TUM_FX, synth.TUM_FY, synth.TUM_CX, synth.TUM_CY, synth.TUM_BF, w, h)
         m = cf.ORBmatcher(0.9, True, ctx=ctx)
         Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
 
-        def frame(img):
-            k, d = ctx.extract(img)
+        def stereo(k):
             ur = np.empty(len(k), np.float32)
             dep = np.empty(len(k), np.float32)
             ctx.check(cf.lib().coeb_stereo_from_rgbd(ctx.h, k.ctypes.data_as(C.c_void_p), len(k),
                                                      depth.ctypes.data_as(C.c_void_p), w, h, w, C.c_float(synth.TUM_BF),
                                                      ur.ctypes.data_as(C.c_void_p), dep.ctypes.data_as(C.c_void_p)))
-            return k, d, ur, dep
-        k0, d0, _, dep0 = frame(fr[0])
-        z = dep0
-        xw = np.stack([(k0["x"] - np.float32(synth.TUM_CX)) * z / np.float32(synth.TUM_FX),
-                       (k0["y"] - np.float32(synth.TUM_CY)) * z / np.float32(synth.TUM_FY), z], 1).astype(np.float32)
-        last = cf.Frame(k0, d0, Tcw=Tl, map_points=dict(world_pos=xw, descriptor=d0,
-                                                        observations=np.full(len(k0), 2, np.int32),
-                                                        valid=(z > 0).astype(np.uint8)))
-        times, nms = [], []
-        for i in range(1, reps + 1):
+            return ur, dep
+
+        def snapshot(k, d, z):
+            xw = np.stack([(k["x"] - np.float32(synth.TUM_CX)) * z / np.float32(synth.TUM_FX),
+                           (k["y"] - np.float32(synth.TUM_CY)) * z / np.float32(synth.TUM_FY), z], 1).astype(np.float32)
+            return cf.Frame(k, d, Tcw=Tl, map_points=dict(world_pos=xw, descriptor=d,
+                                                          observations=np.full(len(k), 2, np.int32),
+                                                          valid=(z > 0).astype(np.uint8)))
+        k, d = ctx.extract(fr[0])
+        last = snapshot(k, d, stereo(k)[1])
+        times, parts, nms = [], [], []
+        for i in range(1, reps + warm + 1):
             t0 = time.perf_counter()
-            k, d, ur, _ = frame(fr[i])
+            k, d = ctx.extract(fr[i])
+            t1 = time.perf_counter()
+            ur, dep = stereo(k)
+            t2 = time.perf_counter()
             cur = cf.Frame(k, d, ur, Tcw=Tc)
             nm = m.SearchByProjection(cur, last, 15.0, False, cam)
-            times.append(time.perf_counter() - t0)
-            nms.append(nm)
+            if nm < 20:                                                # Tracking.cc:954-958
+                cur = cf.Frame(k, d, ur, Tcw=Tc)
+                nm = m.SearchByProjection(cur, last, 30.0, False, cam)
+            t3 = time.perf_counter()
+            if i > warm:
+                times.append(t3 - t0)
+                parts.append((t1 - t0, t2 - t1, t3 - t2))
+                nms.append(nm)
+            last = snapshot(k, d, dep)                                  # untimed: the Tracking state
+        med = np.median(np.array(parts), axis=0) * 1e3
         return dict(ms_per_frame=round(float(np.median(times)) * 1e3, 4), reps=reps,
-                    matches=int(np.median(nms)),
-                    note="median over %d frames of coeb_extract + coeb_stereo_from_rgbd + coeb_match_lastframe "
-                         "from host buffers (one frame at a time, synchronous, as the Tracking thread)" % reps)
+                    matches=int(np.median(nms)), min_matches=int(min(nms)),
+                    ms_extract=round(float(med[0]), 4), ms_stereo=round(float(med[1]), 4),
+                    ms_match=round(float(med[2]), 4),
+                    note="median over %d consecutive frames (after %d warm-up frames) of coeb_extract + "
+                         "coeb_stereo_from_rgbd + coeb_match_lastframe (th 15, retry 30) from host buffers, frame i "
+                         "matched against frame i-1's extraction (one frame at a time, synchronous, as the Tracking "
+                         "thread)" % (reps, warm))
     finally:
         ctx.close()
+
+
+def single_frame_cpp(w, h, reps=50, warm=5):
+    """The same single-frame calls as single_frame_timing, driven from C++ (tools/single_frame_c,
+    built by __graft_entry__.build()) as the reference's Tracking thread drives them: no Python
+    between the calls.  Runs as a child process on the same frames."""
+    import tempfile
+    from coeb_front import synth
+    exe = os.path.join(ROOT, "tools", "single_frame_c")
+    if not os.path.exists(exe):
+        return dict(skipped="tools/single_frame_c not built (make -C tools)")
+    fr = synth.make_frames(w, h, reps + warm + 1, seed=77)
+    with tempfile.NamedTemporaryFile(suffix=".u8") as f:
+        f.write(fr.tobytes())
+        f.flush()
+        out = subprocess.run([exe, f.name, str(w), str(h), str(len(fr)), str(warm)], capture_output=True, text=True,
+                             timeout=120)
+    if out.returncode != 0:
+        raise RuntimeError("single_frame_c failed: %s" % out.stderr[-2000:])
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    res["note"] = ("median over %d consecutive frames of coeb_extract + coeb_stereo_from_rgbd + coeb_match_lastframe "
+                   "(th 15, retry 30), frame i against frame i-1, called from C++ (tools/single_frame_c.cpp)" % reps)
+    return res
 
 
 if __name__ == "__main__":

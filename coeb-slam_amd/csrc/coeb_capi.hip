@@ -412,6 +412,7 @@ struct coeb_ctx {
     // pinned host staging of the host-buffer entry points: their inputs are packed here and
     // moved in one copy (a dozen small pageable copies cost more than the kernels)
     uint8_t* pin = nullptr;
+    uint8_t* pin_dev = nullptr;        // the same page-locked bytes as the device addresses them
     size_t pin_n = 0;
 };
 
@@ -458,6 +459,20 @@ int ensure(coeb_ctx* c, const char* name, size_t count, T** out)
     return 0;
 }
 
+// One frame's results written straight into the context's page-locked buffer (its device
+// alias): the keypoint count and the first min(count, guess) records and descriptors, so the
+// host reads them after one synchronisation with no copy operations in between (each D2H copy
+// op of the single-frame path cost 5-25 us plus its launch gap, profiles/r06/sf).
+__global__ __launch_bounds__(256) void k_out_pack(const int* counts, const uint32_t* kps, const uint4* desc, int guess,
+                                                  int* out_n, uint32_t* out_k, uint4* out_d)
+{
+    const int n = min(*counts, guess);
+    const int t = blockIdx.x * 256 + threadIdx.x, T = gridDim.x * 256;
+    if (t == 0) *out_n = *counts;
+    for (int i = t; i < 7 * n; i += T) out_k[i] = kps[i];          // 28-byte records
+    for (int i = t; i < 2 * n; i += T) out_d[i] = desc[i];         // 32-byte rows
+}
+
 // Inputs of one call packed at 16-byte aligned offsets of the pinned staging buffer, moved to
 // the device in one copy; fill() parts are constant bytes (absent optional arrays).
 struct Pack {
@@ -484,6 +499,14 @@ int pinned(coeb_ctx* c, size_t bytes)
     const size_t n = std::max<size_t>(bytes, (size_t)1 << 20);
     hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&c->pin), n, hipHostMallocDefault);
     if (e != hipSuccess) return set_err(c, COEB_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    void* dv = nullptr;
+    e = hipHostGetDevicePointer(&dv, c->pin, 0);
+    if (e != hipSuccess) {
+        (void)hipHostFree(c->pin);
+        c->pin = nullptr;
+        return set_err(c, COEB_ENOMEM, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
+    }
+    c->pin_dev = static_cast<uint8_t*>(dv);
     c->pin_n = n;
     return 0;
 }
@@ -763,6 +786,30 @@ ExtractBufs offset_bufs(const Plan& P, const ExtractBufs& b, int f0)
     if (b.box_off) o.box_off = b.box_off + f0;   // offsets index the shared box / T_M arrays
     if (b.tm_off) o.tm_off = b.tm_off + f0;
     return o;
+}
+
+// The device error word copied behind the work of a host-buffer call into `dst` (page-locked),
+// so the call's one synchronisation also brings the word back; err_word_seen checks the copy.
+int err_word_async(coeb_ctx* c, uint8_t* dst)
+{
+    int* derr = static_cast<int*>(c->bufs["err"].p);
+    if (!derr) {
+        memset(dst, 0, 4);
+        return 0;
+    }
+    HIP_TRY(c, hipMemcpyAsync(dst, derr, 4, hipMemcpyDeviceToHost, main_stream(c)));
+    return 0;
+}
+
+int err_word_seen(coeb_ctx* c, const uint8_t* src)
+{
+    int h = 0;
+    memcpy(&h, src, 4);
+    if (!h) return 0;
+    char msg[160];
+    snprintf(msg, sizeof msg, "internal capacity exceeded (device error bits 0x%x)", h);
+    HIP_TRY(c, hipMemsetAsync(c->bufs["err"].p, 0, 4, main_stream(c)));
+    return set_err(c, COEB_ERANGE, msg);
 }
 
 int check_err_word(coeb_ctx* c)
@@ -1068,32 +1115,69 @@ int coeb_extract(coeb_ctx* c, const uint8_t* gray, int W, int H, size_t stride, 
     if ((rc = ensure_plan(c, W, H))) return rc;
     uint8_t* dgray;
     if ((rc = ensure(c, "gray_stage", (size_t)W * H, &dgray))) return rc;
-    HIP_TRY(c, hipMemcpy2DAsync(dgray, W, gray, stride, W, H, hipMemcpyHostToDevice, main_stream(c)));
-    int32_t box_off[2] = {0, nbox}, tm_off[2] = {0, ntm};
-    std::vector<int32_t> blur(nbox, 0);
-    if (blur_flag)                                      // missing flags (or a null array) read as 0
-        for (int i = 0; i < nbox && i < nblur; i++) blur[i] = blur_flag[i];
+    // pinned staging at both ends: the image rows go through the context's page-locked buffer
+    // (one DMA, no runtime pinning of the caller's pages), and the results come back into it
+    // behind the kernels -- the count and the first `guess` records in one synchronisation
+    // (a pageable round trip each cost 120-170 us on the box, profiles/r06/sf)
+    const size_t img = ((size_t)W * H + 255) & ~(size_t)255;
+    const int kcap = c->plan.kcap;
+    const size_t o_n = img, o_k = img + 256, o_d = o_k + (((size_t)kcap * sizeof(coeb_keypoint) + 255) & ~(size_t)255);
+    // the dynamic-mask inputs (boxes, T_M, blur flags, their offsets) staged behind the results
+    const size_t o_dyn = o_d + (((size_t)kcap * 32 + 255) & ~(size_t)255);
+    const size_t o_bo = o_dyn + (size_t)nbox * sizeof(coeb_box), o_bl = o_bo + 16, o_to = o_bl + (size_t)nbox * 4 + 16,
+                 o_tm = o_to + 16;
+    if ((rc = pinned(c, o_tm + (size_t)ntm * 8))) return rc;
+    if (stride == (size_t)W) memcpy(c->pin, gray, (size_t)W * H);
+    else
+        for (int y = 0; y < H; y++) memcpy(c->pin + (size_t)y * W, gray + (size_t)y * stride, (size_t)W);
+    HIP_TRY(c, hipMemcpyAsync(dgray, c->pin, (size_t)W * H, hipMemcpyHostToDevice, main_stream(c)));
+    int32_t* box_off = reinterpret_cast<int32_t*>(c->pin + o_bo);
+    int32_t* tm_off = reinterpret_cast<int32_t*>(c->pin + o_to);
+    int32_t* blur = reinterpret_cast<int32_t*>(c->pin + o_bl);
+    box_off[0] = 0; box_off[1] = nbox; tm_off[0] = 0; tm_off[1] = ntm;
+    for (int i = 0; i < nbox; i++)                      // missing flags (or a null array) read as 0
+        blur[i] = (blur_flag && i < nblur) ? blur_flag[i] : 0;
+    if (nbox) memcpy(c->pin + o_dyn, boxes, (size_t)nbox * sizeof(coeb_box));
+    if (ntm) memcpy(c->pin + o_tm, tm_xy, (size_t)ntm * 8);
     ExtractBufs b;
     if ((rc = extract_bufs(c, 1, b))) return rc;
-    if ((rc = upload_dyn(c, 1, nbox ? boxes : nullptr, box_off, ntm ? tm_xy : nullptr, tm_off,
-                         nbox ? blur.data() : nullptr, b)))
+    if ((rc = upload_dyn(c, 1, nbox ? reinterpret_cast<const coeb_box*>(c->pin + o_dyn) : nullptr, box_off,
+                         ntm ? reinterpret_cast<const float*>(c->pin + o_tm) : nullptr, tm_off, nbox ? blur : nullptr, b)))
         return rc;
     b.gray = dgray;
-    if (launch_extract(c->plan, static_cast<const Plan*>(c->bufs["plan"].p), b, 1, main_stream(c), &c->hook,
-                       side_stream(c)))
+    // one frame on one stream: the side stream's fork / join cost more than the overlap it buys
+    // at F = 1 (0.389 vs 0.350 ms per single-frame step, profiles/r06/sf)
+    if (launch_extract(c->plan, static_cast<const Plan*>(c->bufs["plan"].p), b, 1, main_stream(c), &c->hook, nullptr))
         return hip_err(c, hipGetLastError(), "launch_extract");
     c->batch_frames = 1;
     c->batch_gray = dgray;
+    // the retained set is nfeatures plus at most a few per level (the final cull, ORBextractor.cc
+    // :1204-1207), so nfeatures + 256 records almost always cover it; a larger count costs a
+    // second round trip for the rest
+    const int guess = (kp_out && desc_out) ? std::min({kcap, std::max(cap, 0), c->params.nfeatures + 256}) : 0;
+    hipStream_t s = main_stream(c);
+    hipLaunchKernelGGL(k_out_pack, dim3(16), dim3(256), 0, s, b.counts, static_cast<const uint32_t*>(b.kps),
+                       reinterpret_cast<const uint4*>(b.desc), guess, reinterpret_cast<int*>(c->pin_dev + o_n),
+                       reinterpret_cast<uint32_t*>(c->pin_dev + o_k), reinterpret_cast<uint4*>(c->pin_dev + o_d));
+    HIP_TRY(c, hipGetLastError());
+    if ((rc = err_word_async(c, c->pin + o_n + 16))) return rc;
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if ((rc = err_word_seen(c, c->pin + o_n + 16))) return rc;
     int n = 0;
-    HIP_TRY(c, hipMemcpyAsync(&n, b.counts, 4, hipMemcpyDeviceToHost, main_stream(c)));
-    HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
-    if ((rc = check_err_word(c))) return rc;
+    memcpy(&n, c->pin + o_n, 4);
     *n_out = n;
     const int m = std::min(n, cap);
-    if (m > 0 && kp_out)
-        HIP_TRY(c, hipMemcpyAsync(kp_out, b.kps, (size_t)m * sizeof(coeb_keypoint), hipMemcpyDeviceToHost, main_stream(c)));
-    if (m > 0 && desc_out) HIP_TRY(c, hipMemcpyAsync(desc_out, b.desc, (size_t)m * 32, hipMemcpyDeviceToHost, main_stream(c)));
-    HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
+    if (m > guess) {                         // past the packed records (or one output array only)
+        const size_t r = (size_t)(m - guess);
+        if (kp_out)
+            HIP_TRY(c, hipMemcpyAsync(c->pin + o_k + (size_t)guess * sizeof(coeb_keypoint), static_cast<const coeb_keypoint*>(b.kps) + guess,
+                                      r * sizeof(coeb_keypoint), hipMemcpyDeviceToHost, s));
+        if (desc_out) HIP_TRY(c, hipMemcpyAsync(c->pin + o_d + (size_t)guess * 32, b.desc + (size_t)guess * 32, r * 32,
+                                                hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipStreamSynchronize(s));
+    }
+    if (m > 0 && kp_out) memcpy(kp_out, c->pin + o_k, (size_t)m * sizeof(coeb_keypoint));
+    if (m > 0 && desc_out) memcpy(desc_out, c->pin + o_d, (size_t)m * 32);
     if (n > cap) return set_err(c, COEB_ERANGE, "keypoint output capacity too small");
     return COEB_OK;
 }
@@ -1136,9 +1220,9 @@ int coeb_match_lastframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curfram
     (void)hipSetDevice(c->device);
     const int cs = std::max(n, 1), ls = std::max(nl, 1);
     int rc;
-    int32_t *dout, *dscr, *derr;
+    int32_t *dscr, *derr, *dqn;
     uint8_t* dbase;
-    if ((rc = ensure(c, "m_out2", (size_t)cs + 1, &dout)) || (rc = ensure(c, "m_scr", (size_t)ls * kMatchCQ, &dscr)) ||
+    if ((rc = ensure(c, "m_scr", (size_t)ls * kMatchCQ, &dscr)) || (rc = ensure(c, "m_qn", (size_t)ls + 8, &dqn)) ||
         (rc = ensure(c, "err", 4, &derr)))
         return rc;
     hipStream_t s = main_stream(c);
@@ -1152,7 +1236,12 @@ int coeb_match_lastframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curfram
     const size_t o_ld = pk.add(last->mp_descriptor, (size_t)nl * 32), o_h = pk.add(last->has_mappoint, (size_t)nl);
     const size_t o_o = pk.add(last->outlier, (size_t)nl), o_xw = pk.add(last->world_pos, (size_t)nl * 12);
     const size_t o_nb = pk.add(last->mp_observations, (size_t)nl * 4);
-    if ((rc = stage_in(c, pk, &dbase, s))) return rc;
+    // k_match writes match[cs] and nmatches straight behind the staged inputs (page-locked, no
+    // copy back)
+    const size_t o_res = (pk.total + 255) & ~(size_t)255;
+    const size_t o_err = (o_res + ((size_t)cs + 1) * 4 + 15) & ~(size_t)15;
+    if ((rc = pinned(c, o_err + 16)) || (rc = stage_in(c, pk, &dbase, s))) return rc;
+    int32_t* dout = reinterpret_cast<int32_t*>(c->pin_dev + o_res);
     MatchBufs mb;
     memset(&mb, 0, sizeof(mb));
     mb.cur_kps = reinterpret_cast<const coeb_keypoint*>(dbase + o_ck);
@@ -1171,12 +1260,15 @@ int coeb_match_lastframe(coeb_ctx* c, const coeb_camera* cam, const coeb_curfram
     mb.Tcw_cur = reinterpret_cast<const float*>(dbase + o_T);
     mb.Tcw_last = reinterpret_cast<const float*>(dbase + o_Tl);
     mb.match = dout; mb.nmatch = dout + cs; mb.scratch = dscr; mb.scratch_stride = ls * kMatchCQ; mb.err = derr;
+    // one pair: its candidate lists are built by 8 workgroups (k_match_lists), as for a small
+    // batch, instead of by the pair's one workgroup
+    mb.qn = dqn; mb.qn_stride = ls + 8;
     if (launch_match(make_cam(c, cam), mb, 1, th, bmono, check_ori, 0, s, &c->hook))
         return hip_err(c, hipGetLastError(), "launch_match");
-    int32_t* hout = reinterpret_cast<int32_t*>(c->pin);          // one copy back: match[cs], nmatch
-    HIP_TRY(c, hipMemcpyAsync(hout, dout, ((size_t)cs + 1) * 4, hipMemcpyDeviceToHost, s));
+    if ((rc = err_word_async(c, c->pin + o_err))) return rc;
     HIP_TRY(c, hipStreamSynchronize(s));
-    if ((rc = check_err_word(c))) return rc;
+    if ((rc = err_word_seen(c, c->pin + o_err))) return rc;
+    const int32_t* hout = reinterpret_cast<const int32_t*>(c->pin + o_res);    // written by k_match in place
     if (n && match_out) memcpy(match_out, hout, (size_t)n * 4);
     *nmatches = hout[cs];
     return COEB_OK;
@@ -1648,23 +1740,32 @@ int coeb_stereo_from_rgbd(coeb_ctx* c, const coeb_keypoint* kps, int n, const fl
     if (n == 0) return COEB_OK;
     (void)hipSetDevice(c->device);
     int rc;
-    coeb_keypoint* dk;
-    float *dd, *dur, *ddep;
-    int32_t* dn;
-    if ((rc = ensure(c, "s_k", n, &dk)) || (rc = ensure(c, "s_d", (size_t)W * H, &dd)) || (rc = ensure(c, "s_ur", n, &dur)) ||
-        (rc = ensure(c, "s_dep", n, &ddep)) || (rc = ensure(c, "s_n", 1, &dn)))
-        return rc;
-    HIP_TRY(c, hipMemcpyAsync(dk, kps, (size_t)n * sizeof(coeb_keypoint), hipMemcpyHostToDevice, main_stream(c)));
-    HIP_TRY(c, hipMemcpy2DAsync(dd, (size_t)W * 4, depth, dstride * 4, (size_t)W * 4, H, hipMemcpyHostToDevice, main_stream(c)));
-    HIP_TRY(c, hipMemcpyAsync(dn, &n, 4, hipMemcpyHostToDevice, main_stream(c)));
+    hipStream_t s = main_stream(c);
+    // everything through the context's page-locked buffer, addressed by k_prep in place: the
+    // keypoints and their count in, the depth rows (it touches ~n of the W*H values, so copying
+    // the whole map to the device -- 1.2 MB at 640x480 -- would cost more than the lookups), and
+    // uR / depth written straight back; one launch and one synchronisation, no copy operations
+    const size_t o_n = 0, o_k = 256, o_dep = (o_k + (size_t)n * sizeof(coeb_keypoint) + 255) & ~(size_t)255;
+    const size_t o_out = (o_dep + (size_t)W * H * 4 + 255) & ~(size_t)255;
+    if ((rc = pinned(c, o_out + (size_t)n * 8))) return rc;
+    memcpy(c->pin + o_n, &n, 4);
+    memcpy(c->pin + o_k, kps, (size_t)n * sizeof(coeb_keypoint));
+    float* hdep = reinterpret_cast<float*>(c->pin + o_dep);
+    if (dstride == (size_t)W) memcpy(hdep, depth, (size_t)W * H * 4);
+    else
+        for (int y = 0; y < H; y++) memcpy(hdep + (size_t)y * W, depth + (size_t)y * dstride, (size_t)W * 4);
     PrepBufs pb;
     memset(&pb, 0, sizeof(pb));
-    pb.kps = dk; pb.n = dn; pb.stride = n; pb.depth = dd; pb.W = W; pb.H = H; pb.bf = bf; pb.fx = 1; pb.fy = 1;
-    pb.ur = dur; pb.dep = ddep;
-    if (launch_prep(pb, 1, main_stream(c), &c->hook)) return hip_err(c, hipGetLastError(), "launch_prep");
-    HIP_TRY(c, hipMemcpyAsync(ur_out, dur, (size_t)n * 4, hipMemcpyDeviceToHost, main_stream(c)));
-    HIP_TRY(c, hipMemcpyAsync(dep_out, ddep, (size_t)n * 4, hipMemcpyDeviceToHost, main_stream(c)));
-    HIP_TRY(c, hipStreamSynchronize(main_stream(c)));
+    pb.kps = c->pin_dev + o_k;
+    pb.n = reinterpret_cast<const int32_t*>(c->pin_dev + o_n);
+    pb.stride = n; pb.depth = reinterpret_cast<const float*>(c->pin_dev + o_dep); pb.W = W; pb.H = H;
+    pb.bf = bf; pb.fx = 1; pb.fy = 1;
+    pb.ur = reinterpret_cast<float*>(c->pin_dev + o_out);
+    pb.dep = reinterpret_cast<float*>(c->pin_dev + o_out) + n;
+    if (launch_prep(pb, 1, s, &c->hook)) return hip_err(c, hipGetLastError(), "launch_prep");
+    HIP_TRY(c, hipStreamSynchronize(s));
+    memcpy(ur_out, c->pin + o_out, (size_t)n * 4);
+    memcpy(dep_out, c->pin + o_out + (size_t)n * 4, (size_t)n * 4);
     return COEB_OK;
 }
 
