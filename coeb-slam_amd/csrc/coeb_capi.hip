@@ -281,7 +281,7 @@ bool make_plan(const Tables& t, int W, int H, Plan& P, std::vector<int>& rtab, s
     for (int l = 0; l < t.nlevels; l++) nmax = std::max(nmax, P.lv[l].nfeat);
     P.oct_kl = 512;
     while (P.oct_kl < 4096 && P.oct_kl < (9 * nmax + 1) / 2) P.oct_kl *= 2;
-    if (const char* e = getenv("COEB_OCT_KL")) P.oct_kl = std::max(256, std::min(8192, atoi(e)));
+    if (const char* e = coeb_experiment("COEB_OCT_KL")) P.oct_kl = std::max(256, std::min(8192, atoi(e)));
     P.oct_lds = P.oct_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * P.oct_kl;
     if (P.oct_lds > 150 * 1024) { err = "octree LDS budget exceeded (features per level too large)"; return false; }
     memcpy(P.umax, t.umax, sizeof(P.umax));
@@ -635,6 +635,38 @@ int upload_dyn(coeb_ctx* c, int F, const coeb_box* boxes, const int32_t* box_off
 
 // The context stream, after it has been made to wait for every chunk stream of the last
 // batch (so work enqueued on it sees the batch's results).
+}  // namespace
+
+// The product switches (coeb_internal.hpp); every one of them is set by a GPU test.
+static const char* const kSwitches[] = {
+    "COEB_SIDE_STREAM",        // 0: no extraction side stream     (test_sharded_batch_equals_unsharded[off])
+    "COEB_SIDE_SHARED",        // 1: one side stream per device     ([shared], bench config C)
+    "COEB_SIDE_EAGER",         // 1: side stream made with the ctx  ([eager], bench config A)
+    "COEB_MATCH_SEQUENTIAL",   // 1: the literal sequential claims  (test_match_paths_agree, ...)
+    "COEB_MATCH_SPLIT",        // N: split-list workgroups per pair (test_batch_small_split_lists...)
+    "COEB_PYR_BYTES",          // 1: k_pyr_level byte form          (test_blur_pyramid_matches_oracle)
+    "COEB_FAST_RB",            // 72: the general FAST slab layout  (test_fast_general_slab_layout...)
+    "COEB_FM_THREADS",         // k_fm threads per pair             (tests/test_gpu_flow.py)
+};
+
+const char* coeb_switch(const char* name)
+{
+    for (const char* k : kSwitches)
+        if (strcmp(k, name) == 0) return getenv(name);
+    return nullptr;            // not a product switch: never read
+}
+
+const char* coeb_experiment(const char* name)
+{
+    static const bool on = [] {
+        const char* e = getenv("COEB_EXPERIMENTS");
+        return e && e[0] == '1';
+    }();
+    return on ? getenv(name) : nullptr;
+}
+
+namespace {
+
 // The side stream of launch_extract (created on first use), or null when disabled.  Per-kernel
 // profiling (coeb_profile_enable) serialises everything on the context stream, so each event
 // pair brackets one whole-batch launch.
@@ -643,7 +675,7 @@ int upload_dyn(coeb_ctx* c, int F, const coeb_box* boxes, const int32_t* box_off
 // multi-stream schedules (which queue the dispatcher serves first when CUs free up).
 static hipError_t make_stream(hipStream_t* s, const char* env)
 {
-    const char* e = env ? getenv(env) : nullptr;
+    const char* e = env ? coeb_experiment(env) : nullptr;
     if (e && (e[0] == 'h' || e[0] == 'l')) {
         int least = 0, greatest = 0;
         if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
@@ -686,26 +718,37 @@ const SideStream* side_stream(coeb_ctx* c)
     if (c->prof.enabled) return nullptr;
     if (!c->side_init) {
         c->side_init = true;
-        const char* e = getenv("COEB_SIDE_STREAM");
+        const char* e = coeb_switch("COEB_SIDE_STREAM");
         if (e && e[0] == '0') return nullptr;
-        const char* sp = getenv("COEB_SIDE_SPLIT");          // first level left to the context stream
+        const char* sp = coeb_experiment("COEB_SIDE_SPLIT");          // first level left to the context stream
         if (sp) c->side.split = atoi(sp);
-        const char* bl = getenv("COEB_SIDE_BLUR");           // 0: late levels' blur on the context stream
+        const char* bl = coeb_experiment("COEB_SIDE_BLUR");           // 0: late levels' blur on the context stream
         if (bl) c->side.blur_late = bl[0] == '1';
-        const char* so = getenv("COEB_SIDE_OCTREE");         // 1: early levels' octree on the side stream
+        const char* so = coeb_experiment("COEB_SIDE_OCTREE");         // 1: early levels' octree on the side stream
         if (so) c->side.side_octree = so[0] == '1';
-        const char* sh = getenv("COEB_SIDE_SHARED");         // 1: one side stream per device
+        const char* sh = coeb_switch("COEB_SIDE_SHARED");         // 1: one side stream per device
         c->side_shared = sh && sh[0] == '1';
         hipError_t se = c->side_shared ? shared_side_acquire(c->device, &c->side.s)
                                        : make_stream(&c->side.s, "COEB_SIDE_PRIO");
-        if (se != hipSuccess ||
-            hipEventCreateWithFlags(&c->side.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->side.mid, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->side.pyr_done, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->side.join2, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->side.join, hipEventDisableTiming) != hipSuccess) {
-            if (se == hipSuccess && c->side_shared) shared_side_release(c->device);
+        hipEvent_t* evs[] = {&c->side.fork, &c->side.mid, &c->side.pyr_done, &c->side.join2, &c->side.join};
+        bool ok = se == hipSuccess;
+        for (hipEvent_t* e : evs) {
+            *e = nullptr;
+            if (ok && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+                *e = nullptr;
+                ok = false;
+            }
+        }
+        if (!ok) {
+            // run without a side stream: release what was made
+            for (hipEvent_t* e : evs)
+                if (*e) (void)hipEventDestroy(*e), *e = nullptr;
+            if (se == hipSuccess) {
+                if (c->side_shared) shared_side_release(c->device);
+                else (void)hipStreamDestroy(c->side.s);
+            }
             c->side.s = nullptr;
+            c->side_shared = false;
         }
     }
     return c->side.s ? &c->side : nullptr;
@@ -878,7 +921,7 @@ coeb_ctx* coeb_create(const coeb_orb_params* params, int device, int max_width, 
     // COEB_SIDE_EAGER=1: create the side stream now, right after the context stream, so the
     // contexts' streams take the hardware queues in (context, side) pairs (experiment knob; by
     // default it is created at the first extraction, after every context stream of the process)
-    if (const char* e = getenv("COEB_SIDE_EAGER"))
+    if (const char* e = coeb_switch("COEB_SIDE_EAGER"))
         if (e[0] == '1') (void)side_stream(c);
     if (hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
@@ -901,9 +944,17 @@ void coeb_destroy(coeb_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(main_stream(c));
     if (c->side.s) {
-        (void)hipStreamSynchronize(c->side.s);
-        if (c->side_shared) shared_side_release(c->device);
-        else (void)hipStreamDestroy(c->side.s);
+        if (c->side_shared) {
+            // this context's side work ends at its join events; the other contexts' work queued on
+            // the shared stream is theirs to wait for (the last release synchronises the stream)
+            (void)hipEventSynchronize(c->side.join);
+            (void)hipEventSynchronize(c->side.join2);
+            if (c->ev_fjoin) (void)hipEventSynchronize(c->ev_fjoin);
+            shared_side_release(c->device);
+        } else {
+            (void)hipStreamSynchronize(c->side.s);
+            (void)hipStreamDestroy(c->side.s);
+        }
         (void)hipEventDestroy(c->side.fork);
         (void)hipEventDestroy(c->side.mid);
         (void)hipEventDestroy(c->side.pyr_done);
@@ -1495,7 +1546,7 @@ int match_batch_impl(coeb_ctx* c, const float* d_depth, int F, int W, int H, con
             mb.match = match + q + K; mb.nmatch = nm + p0 + 1; mb.scratch = scr + q * kMatchCQ;
             mb.scratch_stride = K * kMatchCQ; mb.err = derr;
             mb.qn = mqn + (int64_t)p0 * qs; mb.qn_stride = qs;
-            if (getenv("COEB_MATCH_TIMING")) {
+            if (COEB_MATCH_CLOCK && coeb_experiment("COEB_MATCH_TIMING")) {
                 long long* tmb;
                 if ((rc = ensure(c, "m_timing", (size_t)F * 16, &tmb))) return rc;
                 mb.timing = tmb + (int64_t)p0 * 16;
@@ -1602,7 +1653,7 @@ int coeb_pose_batch_device(coeb_ctx* c, const coeb_camera* cam, int F, const flo
     b.inv_sigma2 = isg; b.Tcw = tout + 16; b.outlier = toutl + o; b.result = tres + 1;
     b.edges = tedge + o; b.active = tact + o; b.chi2 = tchi + o; b.stride = K;
     b.timing = nullptr;
-    if (getenv("COEB_POSE_TIMING")) {               // diagnostic phase clocks, tools/_pose_timing.py
+    if (coeb_experiment("COEB_POSE_TIMING")) {               // diagnostic phase clocks, tools/_pose_timing.py
         long long* tmb;
         if ((rc = ensure(c, "p_timing", (size_t)F * 8, &tmb))) return rc;
         HIP_TRY(c, hipMemsetAsync(tmb, 0, (size_t)F * 64, s));
@@ -2067,7 +2118,7 @@ int coeb_internal_stream(coeb_ctx* c, hipStream_t* s, int* device)
 int coeb_internal_flow_side(coeb_ctx* c, hipStream_t* side, hipEvent_t* fork, hipEvent_t* join)
 {
     if (!c) return COEB_EINVAL;
-    const char* e = getenv("COEB_FLOW_SIDE");
+    const char* e = coeb_experiment("COEB_FLOW_SIDE");
     if (!(e && e[0] == '1')) return 1;
     const SideStream* sd = side_stream(c);
     if (!sd) return 1;

@@ -6,7 +6,7 @@
 // Pipeline for F frames (one launch each, all on the context stream):
 //   k_dynmask    dynamic-object rectangles + area flag           (ORBextractor.cc:1101-1195)
 //   k_pyr_level  cascaded INTER_LINEAR pyramid, level l from l-1  (:1344-1367)
-//   k_blur       7x7 sigma-2 Gaussian of every level, LDS tiled   (:1317-1318)
+//   k_blur_rows  7x7 sigma-2 Gaussian of every level, 16x8 tiles  (:1317-1318)
 //   k_fast       per 30-px cell FAST-9/16 + NMS + iniTh/minTh     (:811-850)
 //   k_octree     per (frame, level) DistributeOctTree emulation   (:546-769, 852-890, 1204-1207)
 //   k_describe   IC_Angle + rBRIEF + output assembly              (:80-156, 902-903, 1291-1337)
@@ -493,107 +493,8 @@ __device__ __forceinline__ uint32_t dpp_shl1(uint32_t v)   // lane i <- lane i+1
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xf, 0xf, false);
 }
 
-__global__ __launch_bounds__(kThreads) void k_blur(const Plan* __restrict__ P, ExtractBufs b, BlurWork bw)
-{
-    const int2 bxy = block_xy();
-    const int f = bxy.y;
-    const int item = bw.item0 + bxy.x * kWaves + wave_id();
-    if (item >= bw.item1) return;
-    int l = 0;
-    while (l + 1 < bw.L && item >= bw.item_off[l + 1]) l++;
-    const int it = item - bw.item_off[l];
-    const int strip = it % bw.nstrips[l], bq = it / bw.nstrips[l];
-    const LevelGeom& g = P->lv[l];
-    const int w = g.w, h = g.h, sp = g.pitch, dp = g.bpitch;
-    const int lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
-    const int bh = bw.bh[l];
-    const int y0 = (bq * 4 + grp) * bh;
-    const int y1 = min(h, y0 + bh);
-    const int x = strip * kBlurCols - 4 + gl * 4;
-    const uint8_t* src = level_ptr(P, b, f, l);
-    uint8_t* dst = b.blur + (int64_t)f * P->blur_stride + g.blur_off;
-    const bool produce = gl >= 1 && gl <= 14 && x < w && y0 < y1;
-    const bool edge = x < 0 || x + 3 >= w || (sp & 3) != 0;
-    int cx[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) cx[q] = reflect101(min(x + q, w + 2), w);
-    const int k0 = P->gauss[0], k1 = P->gauss[1], k2 = P->gauss[2], k3 = P->gauss[3];
-    const us2 K0 = pk2(k0, k0), K1 = pk2(k1, k1), K2 = pk2(k2, k2), K3 = pk2(k3, k3);
-    // horizontal weights per (output column, source pair), DESIGN.md s4
-    const us2 W_l01_0 = pk2(0, k0), W_l23_0 = pk2(k1, k2), W_c01_0 = pk2(k3, k2), W_c23_0 = pk2(k1, k0);
-    const us2 W_l23_1 = pk2(k0, k1), W_c01_1 = pk2(k2, k3), W_c23_1 = pk2(k2, k1), W_r01_1 = pk2(k0, 0);
-    const us2 W_l23_2 = pk2(0, k0), W_c01_2 = pk2(k1, k2), W_c23_2 = pk2(k3, k2), W_r01_2 = pk2(k1, k0);
-    const us2 W_c01_3 = pk2(k0, k1), W_c23_3 = pk2(k2, k3), W_r01_3 = pk2(k2, k1), W_r23_3 = pk2(k0, 0);
-    const uint32_t rnd = 1u << 15;
-    const int n_iter = bh + 6;
-    const int hm = 2 * h - 2;
-    uint32_t R0[7], R1[7];
-    for (int i0 = 0; i0 < n_iter; i0 += 7) {
-        // issue the block's 7 row loads up front (latency hiding), then filter
-        uint32_t raw[7];
-#pragma unroll
-        for (int ph = 0; ph < 7; ph++) {
-            // source row y0 - 3 + i, REFLECT_101 (|r| <= 3 outside the level), clamped for
-            // idle bands and for the rows past the end of the last block
-            const int r = y0 - 3 + i0 + ph;
-            int rr = r < 0 ? -r : r;
-            rr = min(rr, hm - rr);
-            rr = max(0, min(rr, h - 1));
-            const uint8_t* row = src + (int64_t)rr * sp;
-            if (!edge) {
-                raw[ph] = *reinterpret_cast<const uint32_t*>(row + x);
-            } else {
-                raw[ph] = (uint32_t)row[cx[0]] | ((uint32_t)row[cx[1]] << 8) | ((uint32_t)row[cx[2]] << 16) |
-                          ((uint32_t)row[cx[3]] << 24);
-            }
-        }
-#pragma unroll
-        for (int ph = 0; ph < 7; ph++) {
-            const int i = i0 + ph;
-            if (i >= n_iter) break;
-            const int r = y0 - 3 + i;
-            R0[ph] = __builtin_amdgcn_perm(0u, raw[ph], 0x0c010c00u);
-            R1[ph] = __builtin_amdgcn_perm(0u, raw[ph], 0x0c030c02u);
-            if (i < 6) continue;
-            // rows i-6 .. i are ring slots ph+1 .. ph (mod 7); centre = slot ph+4
-            const int s0 = (ph + 1) % 7, s1 = (ph + 2) % 7, s2 = (ph + 3) % 7, s3 = (ph + 4) % 7,
-                      s4 = (ph + 5) % 7, s5 = (ph + 6) % 7, s6 = ph;
-            const us2 v01 = K3 * as_us2(R0[s3]) + K2 * (as_us2(R0[s2]) + as_us2(R0[s4])) +
-                            K1 * (as_us2(R0[s1]) + as_us2(R0[s5])) + K0 * (as_us2(R0[s0]) + as_us2(R0[s6]));
-            const us2 v23 = K3 * as_us2(R1[s3]) + K2 * (as_us2(R1[s2]) + as_us2(R1[s4])) +
-                            K1 * (as_us2(R1[s1]) + as_us2(R1[s5])) + K0 * (as_us2(R1[s0]) + as_us2(R1[s6]));
-            const uint32_t V01 = as_u32(v01), V23 = as_u32(v23);
-            const us2 L01 = as_us2(dpp_shr1(V01)), L23 = as_us2(dpp_shr1(V23));
-            const us2 R01 = as_us2(dpp_shl1(V01)), R23 = as_us2(dpp_shl1(V23));
-            uint32_t a0 = __builtin_amdgcn_udot2(L01, W_l01_0, rnd, false);
-            a0 = __builtin_amdgcn_udot2(L23, W_l23_0, a0, false);
-            a0 = __builtin_amdgcn_udot2(v01, W_c01_0, a0, false);
-            a0 = __builtin_amdgcn_udot2(v23, W_c23_0, a0, false);
-            uint32_t a1 = __builtin_amdgcn_udot2(L23, W_l23_1, rnd, false);
-            a1 = __builtin_amdgcn_udot2(v01, W_c01_1, a1, false);
-            a1 = __builtin_amdgcn_udot2(v23, W_c23_1, a1, false);
-            a1 = __builtin_amdgcn_udot2(R01, W_r01_1, a1, false);
-            uint32_t a2 = __builtin_amdgcn_udot2(L23, W_l23_2, rnd, false);
-            a2 = __builtin_amdgcn_udot2(v01, W_c01_2, a2, false);
-            a2 = __builtin_amdgcn_udot2(v23, W_c23_2, a2, false);
-            a2 = __builtin_amdgcn_udot2(R01, W_r01_2, a2, false);
-            uint32_t a3 = __builtin_amdgcn_udot2(v01, W_c01_3, rnd, false);
-            a3 = __builtin_amdgcn_udot2(v23, W_c23_3, a3, false);
-            a3 = __builtin_amdgcn_udot2(R01, W_r01_3, a3, false);
-            a3 = __builtin_amdgcn_udot2(R23, W_r23_3, a3, false);
-            const int y = r - 3;
-            if (produce && y < y1) {
-                // byte 2 of each accumulator = (acc + 2^15) >> 16 (acc + 2^15 < 2^24)
-                const uint32_t p01 = __builtin_amdgcn_perm(a1, a0, 0x0c0c0602u);
-                const uint32_t p23 = __builtin_amdgcn_perm(a3, a2, 0x06020c0cu);
-                *reinterpret_cast<uint32_t*>(dst + blur_tile_off(x, y, dp)) = p01 | p23;
-            }
-        }
-    }
-}
-
-// The same filter with wave-uniform rows: a wave item is 4 ADJACENT 56-column strips (one per
-// 16-lane group) of one band of brows rows, so every row index, its REFLECT_101 and the row
+// k_blur_rows: a wave item is 4 ADJACENT 56-column strips (one per 16-lane group) of one band of
+// brows rows, so every row index, its REFLECT_101 and the row
 // pointers are scalar (SGPR base + the lane's constant column offset, no per-row 64-bit address
 // VALU), the band halo is 6 rows per brows instead of per 16, and the next 7-row block's loads
 // are issued before the current block is filtered.
@@ -795,54 +696,6 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c, int st)
     return max(A, -Bm);
 }
 
-// The same M for a pre-test survivor, computing only the arc sign(s) that passed the pre-test at
-// t (the four opposite pairs 0/8, 2/10, 4/12, 6/14).  Every nine-pixel arc holds one pixel of each
-// opposite pair, so a sign whose pre-test fails has arc strength <= t: it can neither make the
-// pixel a corner at t nor at any larger threshold, and M only matters where M > t.  Hence
-//   dark passed:   M = max_k min_arc(v - p) = X - (255 - v),  X = max_k min_arc(255 - p)
-//   bright passed: M = max_k min_arc(p - v) = X - v,          X = max_k min_arc(p)
-// i.e. X over q = p ^ mask (mask = 255 for dark, 0 for bright) and M = X - (v ^ mask): one arc
-// pass of min3/max3 instead of two.  A pixel passing both pre-tests (rare) takes the bright pass
-// as well.  The base pointer sits at the lowest ring byte (p9 = -3 rows - 1 column), so all 17
-// reads take positive immediate offsets (LDS offsets are unsigned).
-template <int st>
-__device__ __forceinline__ int arc_max_min(const int q[16])
-{
-    int m3[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) m3[k] = min(min(q[k], q[(k + 1) & 15]), q[(k + 2) & 15]);
-    int X = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) X = max(X, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]));
-    return X;
-}
-
-template <int st>
-__device__ __forceinline__ int corner_strength_sel(const uint8_t* c, int t)
-{
-    lds_cu8 b = (lds_cu8)c - (3 * st + 1);
-    asm volatile("" : "+v"(b));              // keep the lowered base: offsets below are all >= 0
-    constexpr int o = 3 * st + 1;            // c[x] = b[x + o]
-    int p[16];
-    p[0] = b[o + 3 * st];      p[1] = b[o + 3 * st + 1];  p[2] = b[o + 2 * st + 2]; p[3] = b[o + st + 3];
-    p[4] = b[o + 3];           p[5] = b[o - st + 3];      p[6] = b[o - 2 * st + 2]; p[7] = b[o - 3 * st + 1];
-    p[8] = b[0 + 1];           p[9] = b[0];               p[10] = b[o - 2 * st - 2]; p[11] = b[o - st - 3];
-    p[12] = b[o - 3];          p[13] = b[o + st - 3];     p[14] = b[o + 2 * st - 2]; p[15] = b[o + 3 * st - 1];
-    const int v = b[o];
-    const int md = max(max(min(p[0], p[8]), min(p[2], p[10])), max(min(p[4], p[12]), min(p[6], p[14])));
-    const int mb = min(min(max(p[0], p[8]), max(p[2], p[10])), min(max(p[4], p[12]), max(p[6], p[14])));
-    const bool dark = md < v - t, bright = mb > v + t;
-    const int mask = dark ? 255 : 0;
-    int q[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) q[k] = p[k] ^ mask;
-    int M = arc_max_min<st>(q) - (v ^ mask);
-    if (__builtin_expect(__ballot(dark && bright) != 0, 0)) {
-        if (dark && bright) M = max(M, arc_max_min<st>(p) - v);
-    }
-    return M;
-}
-
 // One wave per cell, four cells per workgroup, no workgroup barriers.
 //  1. stage the cell ROI in the wave's LDS slab with aligned 32-bit loads (slab row starts at
 //     the ROI's x0 & 3, so words are stored unshifted);
@@ -865,11 +718,6 @@ constexpr int kFastCorners = 256;          // corner list (more corners: NMS wal
 constexpr int kFastLists = kFastSurv;      // u16 entries before the corner list
 // entry offsets / 4 fit 12 bits: ROIs are at most 64 rows (coeb_capi.hip kRoiMax)
 static_assert(kFastRowBytesM * 64 <= 4 * 4096 && kFastRowBytes * 64 <= 4 * 4096, "k_fast entry offset field");
-#ifndef COEB_FAST_PK
-// 1: survivors' strengths two per lane (u16 halves); 0: one per lane (1.061 vs 1.105 ms per
-// 1025-frame launch, profiles/r04/ab3)
-#define COEB_FAST_PK 0
-#endif
 
 
 // FAST_t's first rejection stage (features2d/fast.cpp): d = tab[p0]|tab[p8]; d &= tab[p2]|tab[p10];
@@ -905,9 +753,6 @@ __device__ __forceinline__ us2 pk_min(us2 a, us2 b) { return __builtin_elementwi
 __device__ __forceinline__ us2 pk_max(us2 a, us2 b) { return __builtin_elementwise_max(a, b); }
 __device__ __forceinline__ us2 pk_subs(us2 a, us2 b) { return __builtin_elementwise_sub_sat(a, b); }
 
-#ifndef COEB_FAST_MAX3
-#define COEB_FAST_MAX3 1
-#endif
 // Three-input packed max / min of u16 pixel pairs (values <= 255) as v_pk_maximum3_f16 /
 // v_pk_minimum3_f16: read as f16 the patterns are positive denormals, ordered like the integers
 // (f16 denormals are not flushed), so one instruction replaces two v_pk_max/min_u16
@@ -927,22 +772,12 @@ __device__ __forceinline__ us2 pk_min3(us2 a, us2 b, us2 c)
 __device__ __forceinline__ uint32_t pretest_half(us2 v, us2 p0, us2 p8, us2 p2, us2 p10, us2 p4, us2 p12, us2 p6,
                                                  us2 p14, us2 T)
 {
-#if COEB_FAST_MAX3
     // dark survives <=> v - md > t, bright <=> mb - v > t: one threshold test of their maximum
     const us2 md = pk_max3(pk_min(p0, p8), pk_min(p2, p10), pk_max(pk_min(p4, p12), pk_min(p6, p14)));
     const us2 mb = pk_min3(pk_max(p0, p8), pk_max(p2, p10), pk_min(pk_max(p4, p12), pk_max(p6, p14)));
     return as_u32(pk_subs(pk_max(pk_subs(v, md), pk_subs(mb, v)), T));
-#else
-    const us2 lo = pk_subs(v, T), hi = v + T;
-    const us2 md = pk_max(pk_max(pk_min(p0, p8), pk_min(p2, p10)), pk_max(pk_min(p4, p12), pk_min(p6, p14)));
-    const us2 mb = pk_min(pk_min(pk_max(p0, p8), pk_max(p2, p10)), pk_min(pk_max(p4, p12), pk_max(p6, p14)));
-    return as_u32(pk_subs(lo, md)) | as_u32(pk_subs(mb, hi));
-#endif
 }
 
-#ifndef COEB_FAST_ARC2
-#define COEB_FAST_ARC2 1
-#endif
 // v_pk_maximum3_f16 / v_pk_minimum3_f16 on u16 patterns (see pk_max3) with the halves of the
 // second (S1) and / or third (S2) operand swapped by op_sel
 template <bool kMax, bool S1, bool S2>
@@ -987,8 +822,18 @@ __device__ __forceinline__ uint32_t arc_max_min_pk(const uint32_t Q[8])
     return pk3<true, false, false>(M9[6], M9[7], pk3<true, false, false>(A, B, A));
 }
 
-// corner_strength_sel with the ring bytes loaded straight into u16 halves (Q[k] = p_k | p_{k+8}
-// << 16) and the arc taken by arc_max_min_pk.  Same result.
+// The same M for a pre-test survivor, computing only the arc sign(s) that passed the pre-test at
+// t (the four opposite pairs 0/8, 2/10, 4/12, 6/14).  Every nine-pixel arc holds one pixel of each
+// opposite pair, so a sign whose pre-test fails has arc strength <= t: it can neither make the
+// pixel a corner at t nor at any larger threshold, and M only matters where M > t.  Hence
+//   dark passed:   M = max_k min_arc(v - p) = X - (255 - v),  X = max_k min_arc(255 - p)
+//   bright passed: M = max_k min_arc(p - v) = X - v,          X = max_k min_arc(p)
+// i.e. X over q = p ^ mask (mask = 255 for dark, 0 for bright) and M = X - (v ^ mask): one arc
+// pass of min3/max3 instead of two.  A pixel passing both pre-tests (rare) takes the bright pass
+// as well.  The base pointer sits at the lowest ring byte (p9 = -3 rows - 1 column), so all 17
+// reads take positive immediate offsets (LDS offsets are unsigned).
+// The ring bytes are loaded straight into u16 halves (Q[k] = p_k | p_{k+8} << 16) and the arc is
+// taken by arc_max_min_pk.
 template <int st>
 __device__ __forceinline__ int corner_strength_pos2(const uint8_t* c, int t)
 {
@@ -1023,56 +868,6 @@ __device__ __forceinline__ int corner_strength_pos2(const uint8_t* c, int t)
             const uint32_t Y = arc_max_min_pk(Q);
             M = max(M, max(lo(Y), hi(Y)) - v);
         }
-    }
-    return M;
-}
-
-// corner_strength_sel for TWO survivors at once, one per u16 half (pixel A at slab offset oa in
-// the low halves, pixel B at ob in the high halves): the same min / max / xor steps as packed
-// u16 operations (ring bytes loaded straight into the halves), M as a saturating difference
-// (M <= 0 -> 0: only M > t is ever used).  Returns the packed (M_A, M_B).
-__device__ __forceinline__ uint32_t us2_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
-
-template <int st>
-__device__ __forceinline__ us2 corner_strength_pk(const uint8_t* roi, int oa, int ob, int t)
-{
-    lds_cu8 ba = (lds_cu8)roi + oa - (3 * st + 1);
-    lds_cu8 bb = (lds_cu8)roi + ob - (3 * st + 1);
-    asm volatile("" : "+v"(ba), "+v"(bb));
-    constexpr int o = 3 * st + 1;
-    constexpr int off[16] = {o + 3 * st, o + 3 * st + 1, o + 2 * st + 2, o + st + 3, o + 3, o - st + 3, o - 2 * st + 2,
-                             o - 3 * st + 1, 1, 0, o - 2 * st - 2, o - st - 3, o - 3, o + st - 3, o + 2 * st - 2,
-                             o + 3 * st - 1};
-    us2 p[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) { p[k].x = ba[off[k]]; p[k].y = bb[off[k]]; }
-    us2 v;
-    v.x = ba[o]; v.y = bb[o];
-    const us2 T = pk2(t, t);
-    const us2 md = pk_max(pk_max(pk_min(p[0], p[8]), pk_min(p[2], p[10])), pk_max(pk_min(p[4], p[12]), pk_min(p[6], p[14])));
-    const us2 mb = pk_min(pk_min(pk_max(p[0], p[8]), pk_max(p[2], p[10])), pk_min(pk_max(p[4], p[12]), pk_max(p[6], p[14])));
-    // dark: md < v - t (v - t - md > 0 with saturation); bright: mb > v + t
-    const us2 dk = pk_subs(pk_subs(v, T), md), br = pk_subs(mb, v + T);
-    const us2 one = pk2(1, 1), ff = pk2(255, 255);
-    const us2 dmask = pk_min(dk, one) * ff;            // 0x00FF in the dark halves
-    us2 q[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) q[k] = as_us2(us2_u32(p[k]) ^ us2_u32(dmask));
-    auto arc = [](const us2(&a)[16]) {
-        us2 m3[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) m3[k] = pk_min(pk_min(a[k], a[(k + 1) & 15]), a[(k + 2) & 15]);
-        us2 X = pk2(0, 0);
-#pragma unroll
-        for (int k = 0; k < 16; k++) X = pk_max(X, pk_min(pk_min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]));
-        return X;
-    };
-    us2 M = pk_subs(arc(q), as_us2(us2_u32(v) ^ us2_u32(dmask)));
-    // a half passing both pre-tests (rare) also takes the bright pass
-    const us2 both = pk_min(pk_min(dk, one), pk_min(br, one));
-    if (__builtin_expect(__ballot(us2_u32(both) != 0u) != 0, 0)) {
-        const us2 M2 = pk_subs(arc(p), v);
-        M = pk_max(M, as_us2(us2_u32(M2) & us2_u32(both * pk2(0xFFFF, 0xFFFF))));
     }
     return M;
 }
@@ -1368,17 +1163,12 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
                 if ((m >> k) & 1u) surv[q++] = (uint16_t)(ob + k);
             surv[ns] = surv[ns > 0 ? ns - 1 : 0];      // pad an odd count (the pair's B repeats A's pixel)
             wave_sync_lds();
-#if !COEB_FAST_PK
             for (int s0 = 0; s0 < ns; s0 += 64) {
                 const int si = s0 + lane;
                 int oo = 0, M = 0;
                 if (si < ns) {
                     oo = surv[si];
-#if COEB_FAST_ARC2
                     M = corner_strength_pos2<RB>(&roi[oo], th_min);
-#else
-                    M = corner_strength_sel<RB>(&roi[oo], th_min);
-#endif
                 }
                 const bool isc = si < ns && M > th_min;
                 if (isc) Ms[fast_mi<RB>(oo, mp)] = (uint8_t)M;
@@ -1389,29 +1179,6 @@ __device__ __forceinline__ void fast_cell(const Plan* P, const ExtractBufs& b, i
                 }
                 nc = uniform(nc + (int)__popcll(mc));
             }
-#else
-            // two survivors per lane (u16 halves): survivor 2i in the low half, 2i + 1 in the high
-            for (int s0 = 0; s0 < ns; s0 += 128) {
-                const int si = s0 + 2 * lane;
-                int oa = 0, ob = 0;
-                uint32_t Mp = 0;
-                if (si < ns) {
-                    const uint32_t pr = reinterpret_cast<const uint32_t*>(surv)[si >> 1];
-                    oa = (int)(pr & 0xFFFFu);
-                    ob = (int)(pr >> 16);
-                    Mp = us2_u32(corner_strength_pk<RB>(roi, oa, ob, th_min));
-                }
-                const int Ma = (int)(Mp & 0xFFFFu), Mb = (int)(Mp >> 16);
-                const bool ia = si < ns && Ma > th_min, ib = si + 1 < ns && Mb > th_min;
-                if (ia) Ms[fast_mi<RB>(oa, mp)] = (uint8_t)Ma;
-                if (ib) Ms[fast_mi<RB>(ob, mp)] = (uint8_t)Mb;
-                const uint64_t ma = __ballot(ia), mbl = __ballot(ib);
-                const int qq = nc + mbcnt(ma) + mbcnt(mbl);
-                if (ia && qq < kFastCorners) corn[qq] = (uint16_t)oa;
-                if (ib && qq + (ia ? 1 : 0) < kFastCorners) corn[qq + (ia ? 1 : 0)] = (uint16_t)ob;
-                nc = uniform(nc + (int)__popcll(ma) + (int)__popcll(mbl));
-            }
-#endif
             wave_sync_lds();
         }
         ne = 0;
@@ -2761,32 +2528,25 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     BlurWork bw;
     bw.L = plan.L;
     int items = 0;
-    const char* brv = getenv("COEB_BLUR_ROWS");            // rows per band of k_blur_rows; 0 = k_blur
-    int brows = brv ? atoi(brv) : 32;
-    if (COEB_BLUR_TILED && brows > 0) brows = (brows + 7) & ~7;   // bands start on tile rows
+    // 32-row bands (round 4: 0.487 ms per 1025-frame launch; the strip-per-lane k_blur it replaced
+    // took 0.759, and was deleted in round 6)
+    const int brows = 32;
+    static_assert(!COEB_BLUR_TILED || brows % 8 == 0, "bands start on tile rows");
     bw.brows = brows;
     for (int l = 0; l < plan.L; l++) {
         const LevelGeom& g = plan.lv[l];
         bw.nstrips[l] = (g.w + kBlurCols - 1) / kBlurCols;
         bw.item_off[l] = items;
-        if (brows > 0) {
-            bw.nquads[l] = (bw.nstrips[l] + 3) / 4;
-            bw.bh[l] = 0;
-            items += bw.nquads[l] * ((g.h + brows - 1) / brows);
-        } else {
-            // 64 rows per wave item (4 bands): 32-, 128- and 256-row items measured slower, also with
-            // the next row block's loads issued before the current one is filtered (0.190 ms either way)
-            const int nbands = 4 * ((g.h + 63) / 64);
-            bw.bh[l] = (g.h + nbands - 1) / nbands;
-            items += bw.nstrips[l] * (nbands / 4);
-        }
+        bw.nquads[l] = (bw.nstrips[l] + 3) / 4;
+        bw.bh[l] = 0;
+        items += bw.nquads[l] * ((g.h + brows - 1) / brows);
     }
     bw.item_off[plan.L] = items;
     // COEB_PYR_BYTES=1 forces k_pyr_level's byte form for every level (tests run both forms)
-    const char* pb = getenv("COEB_PYR_BYTES");
+    const char* pb = coeb_switch("COEB_PYR_BYTES");
     const bool pyr_bytes = pb && atoi(pb) != 0;
     // COEB_FAST_RB=72 forces the general slab layout (tests run both layouts)
-    const char* frb = getenv("COEB_FAST_RB");
+    const char* frb = coeb_switch("COEB_FAST_RB");
     const int fast_rbytes = frb && atoi(frb) == kFastRowBytes ? kFastRowBytes : fast_rb(plan);
     const int fast_lds = kWaves * fast_wave_lds(plan, fast_rbytes);
     constexpr int kFastPerBlock = kWaves;
@@ -2795,7 +2555,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         BlurWork w = bw;
         w.item0 = i0; w.item1 = i1;
         prof_begin(prof, "k_blur", st);
-        hipLaunchKernelGGL(brows > 0 ? k_blur_rows : k_blur, dim3((i1 - i0 + kWaves - 1) / kWaves, F), dim3(kThreads), 0,
+        hipLaunchKernelGGL(k_blur_rows, dim3((i1 - i0 + kWaves - 1) / kWaves, F), dim3(kThreads), 0,
                            st, d_plan, b, w);
         prof_end(prof, st);
     };
@@ -2864,7 +2624,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
         oct_kl = kl;
         oct_lds = plan.oct_w * (4 + 16 + 4 + 4 + 4 + 1 + 64) + 8 * kl;
     }
-    if (const char* e = getenv("COEB_OCT_KL_SMALL")) if (atoi(e) == 0) { oct_kl = plan.oct_kl; oct_lds = plan.oct_lds; }
+    if (const char* e = coeb_experiment("COEB_OCT_KL_SMALL")) if (atoi(e) == 0) { oct_kl = plan.oct_kl; oct_lds = plan.oct_lds; }
     lds_limit_max((const void*)k_octree<kOctThreads>);
     auto octree = [&](hipStream_t st, int l0, int l1) {
         if (l1 <= l0) return;

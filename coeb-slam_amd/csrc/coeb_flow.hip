@@ -119,7 +119,7 @@ __device__ __forceinline__ int2 flow_item(const int* __restrict__ offs, int P, i
 
 // offs[z] = sum over pairs < z of clamp(n_z, 0, nmax) (n_z at d_n + z * pz bytes), offs[P] = total
 __global__ __launch_bounds__(1024) void k_flow_index(const int* __restrict__ d_n, int64_t pz, int P, int nmax,
-                                                      int* __restrict__ offs, int* __restrict__ lkq)
+                                                      int* __restrict__ offs)
 {
     __shared__ int s_w[16];
     __shared__ int s_base;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(1024) void k_flow_index(const int* __restrict__ d_n
         if (threadIdx.x == 0) s_base = total;
         __syncthreads();
     }
-    if (threadIdx.x == 0) { offs[P] = s_base; *lkq = 0; }     // k_lk's point queue, for the launch after this
+    if (threadIdx.x == 0) offs[P] = s_base;
 }
 
 // ============================== goodFeaturesToTrack ==============================
@@ -489,17 +489,10 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
 // next one from the work queue at the start of the next round.  The two image rows a phase's fill
 // needs come straight from global memory (L2-resident windows), issued at the start of the phase
 // and consumed at its end, so no load is in flight across the loop's back edge.
-#ifndef COEB_SP_SLOTS
-#define COEB_SP_SLOTS 9
-#endif
-#ifndef COEB_SP_PRPAD
-#define COEB_SP_PRPAD 1        // row padding of the rolling patch (floats)
-#endif
-#ifndef COEB_SP_TRPAD
-#define COEB_SP_TRPAD 5        // row padding of the term rows (doubles; >= 5: the sink slot G's terms)
-#endif
-static_assert(COEB_SP_TRPAD >= 5, "the term rows hold the sink slot's five terms");
-constexpr int kSpSlots = COEB_SP_SLOTS;   // corner slots per wave (9: 45 summing lanes)
+constexpr int kSpSlots = 9;      // corner slots per wave (9: 45 summing lanes)
+constexpr int kSpPrPad = 1;      // row padding of the rolling patch (floats)
+constexpr int kSpTrPad = 5;      // row padding of the term rows (doubles; >= 5: the sink slot G's terms)
+static_assert(kSpTrPad >= 5, "the term rows hold the sink slot's five terms");
 struct __attribute__((aligned(16))) SpSlot {      // read as three 16-byte words by the fill lanes
     const uint8_t* img;
     double sd;                          // in-image: (1 - a) / a
@@ -521,8 +514,8 @@ __global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0,
     static_assert(NL <= 64, "one summing lane per slot and term");
     // slot G is a sink: the fill and term lanes past the last slot read and write it, so no
     // pass needs a branch and the LDS reads of all passes issue together
-    __shared__ __attribute__((aligned(16))) float pr[G + 1][4][BW + COEB_SP_PRPAD];   // rolling patch rows, row r at r & 3
-    __shared__ double tr[WW][NL + COEB_SP_TRPAD];      // one window row's terms, [j][5 g + t]
+    __shared__ __attribute__((aligned(16))) float pr[G + 1][4][BW + kSpPrPad];   // rolling patch rows, row r at r & 3
+    __shared__ double tr[WW][NL + kSpTrPad];      // one window row's terms, [j][5 g + t]
     __shared__ SpSlot par[G + 1];
     __shared__ double ssum[NL];
     const int lane = threadIdx.x;
@@ -951,33 +944,17 @@ __device__ __forceinline__ void tile_pairs_reflect(const uint8_t* img, int pitch
 #ifndef COEB_LK_MINW
 #define COEB_LK_MINW 1         // launch bound of k_lk in waves per SIMD
 #endif
-#ifndef COEB_LK_QUEUE
-#define COEB_LK_QUEUE 0        // points from a queue (1: 3.53 vs 3.29 ms per config-D step, profiles/r05/s43) or in grid-stride order (0)
-#endif
-// the next point of the queue for this wave (wave-uniform)
-__device__ __forceinline__ int lk_next(int* q)
-{
-    int v = 0;
-    if (__lane_id() == 0) v = atomicAdd(q, 1);
-    return __builtin_amdgcn_readfirstlane(v);
-}
 __global__ __launch_bounds__(256, COEB_LK_MINW) void k_lk(LkPyr pyr, const float* __restrict__ pxy0, const int* __restrict__ offs, int P,
                                             float* __restrict__ nxy0, uint8_t* __restrict__ status0, int win, int max_count,
-                                            double eps2, int64_t iz, int64_t pz, int* __restrict__ itcount,
-                                            int* __restrict__ lkq)
+                                            double eps2, int64_t iz, int64_t pz, int* __restrict__ itcount)
 {
     const int lane = threadIdx.x & 63;
     const int R0 = (lane >> 3) * 3, C0 = (lane & 7) * 3;
     const int nr = min(3, max(0, win - R0)), nc = nr > 0 ? min(3, max(0, win - C0)) : 0;   // this lane's pixels
     const int total = offs[P];
-#if COEB_LK_QUEUE
-    // points from a queue: a wave that drew fast-converging points takes more (measured slower than
-    // the grid-stride order: one atomic per point on one counter)
-    for (int item = lk_next(lkq); item < total; item = lk_next(lkq)) {
-#else
-    (void)lkq;
+    // points in grid-stride order (taking them from a queue, one atomic per point, measured slower:
+    // 3.53 vs 3.29 ms per config-D step, profiles/r05/s43)
     for (int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); item < total; item += gridDim.x * 4) {
-#endif
     const int2 zp = flow_item(offs, P, item);
     const uint32_t z = (uint32_t)zp.x;
     const float* pxy = at_pair(pxy0, pz, z);
@@ -1868,8 +1845,7 @@ int launch_gf(const FlowDev* d, const uint8_t* img, int w, int h, int stride, in
 // goodFeaturesToTrack, which both consume unchanged (cornerSubPix refines them in place)
 void launch_flow_index(const FlowDev* d, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_flow_index, dim3(1), dim3(1024), 0, s, d->npts, d->pz, d->npairs, kMaxPts, d->offs,
-                       d->ocnt + 3);
+    hipLaunchKernelGGL(k_flow_index, dim3(1), dim3(1024), 0, s, d->npts, d->pz, d->npairs, kMaxPts, d->offs);
 }
 
 // workgroups of a persistent per-point launch (ipw points per workgroup and pass): enough to
@@ -1898,12 +1874,12 @@ int launch_subpix(const FlowDev* d, const uint8_t* img, int w, int h, int stride
     const int iters = max_iter < 1 ? 1 : max_iter > 100 ? 100 : max_iter;
     const double e = eps > 0 ? eps : 0.;
     int* itc = nullptr;
-    if (getenv("COEB_SUBPIX_COUNT")) {
+    if (coeb_experiment("COEB_SUBPIX_COUNT")) {
         if (!g_subpix_count) (void)hipGetSymbolAddress((void**)&g_subpix_count, HIP_SYMBOL(g_subpix_count_dev));
         itc = g_subpix_count;
     }
     launch_flow_index(d, s);
-    (void)hipMemsetAsync(d->ocnt, 0, 12, s);            // {interior, border, queue}
+    (void)hipMemsetAsync(d->ocnt, 0, 12, s);            // {interior, border, corner queue}
     // interior: the window (23 x 23 around the corner, +1 for the interpolation) stays inside the
     // image with 2 px of drift to spare
     hipLaunchKernelGGL(k_subpix_order, dim3(flow_grid(d, 256)), dim3(256), 0, s, d->pts, d->offs, d->npairs, w, h, 14,
@@ -1960,12 +1936,12 @@ int launch_lk_track(const FlowDev* d, const LkPyr& pyr, int win, int max_count, 
     const int P = d->npairs;
     launch_flow_index(d, s);            // the host LK entry point sets npts without cornerSubPix
     int* itc = nullptr;
-    if (getenv("COEB_SUBPIX_COUNT")) {
+    if (coeb_experiment("COEB_SUBPIX_COUNT")) {
         if (!g_subpix_count) (void)hipGetSymbolAddress((void**)&g_subpix_count, HIP_SYMBOL(g_subpix_count_dev));
         itc = g_subpix_count;
     }
     FLOW_LAUNCH(d, "k_lk", s, k_lk, dim3(flow_grid(d, 4)), dim3(256), 0, s, pyr, d->pts, d->offs, P, d->nxt,
-                d->status, win, max_count, eps * eps, iz, d->pz, itc, d->ocnt + 3);
+                d->status, win, max_count, eps * eps, iz, d->pz, itc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1985,7 +1961,7 @@ int launch_fm(const FlowDev* d, const uint8_t* prev, const uint8_t* cur, int w, 
     o.tm = d->tm; o.ntm = d->ntm; o.state = d->state; o.F = d->F; o.nf = d->nf; o.tm_cap = tm_cap; o.tm_z = 0;
     const FmOut oo = tm_out ? FmOut{tm_out, ntm_out, o.state, o.F, o.nf, tm_cap, (int64_t)tm_cap * 8} : o;
     int nt = kFmThreads;
-    if (const char* e = getenv("COEB_FM_THREADS")) nt = atoi(e);
+    if (const char* e = coeb_switch("COEB_FM_THREADS")) nt = atoi(e);
 #define COEB_FM_GO(NT_)                                                                                          \
     FLOW_LAUNCH(d, "k_fm", s, k_fm<NT_>, dim3(1, 1, d->npairs), dim3(NT_), 0, s, prev, cur, w, h, stride, d->pts, \
                 d->nxt, d->status, d->npts, kMaxPts, edge, limit, 0.1, 0.99, oo, iz, d->pz)

@@ -21,6 +21,21 @@
 #include <set>
 #include <utility>
 
+// Runtime switches, the only environment reads of the library (coeb_capi.hip):
+//  * coeb_switch(name): a product switch -- one of kSwitches, each run by the GPU test suite
+//    against the oracle (side-stream modes, the matcher's sequential / split forms, the
+//    pyramid's byte form, the general FAST slab layout, k_fm's threads per pair);
+//  * coeb_experiment(name): a measurement-only switch (schedules and kernel forms measured and
+//    not kept, diagnostic clocks), read only when COEB_EXPERIMENTS=1, so a stray variable in a
+//    caller's environment cannot route the shipped library through an untested path.
+// Both return the value or nullptr.
+const char* coeb_switch(const char* name);
+const char* coeb_experiment(const char* name);
+
+#ifndef COEB_MATCH_CLOCK
+#define COEB_MATCH_CLOCK 0     // experiment builds: k_match phase clocks (COEB_MATCH_TIMING, tools/_match_timing.py)
+#endif
+
 // Raise a kernel's dynamic-LDS limit once per (kernel, device), to the most any launch may use
 // (the CU's 160 KB; the launch's own size still sets the occupancy).  The attribute is
 // process-wide: setting it per launch to that launch's size let another host thread's launch of

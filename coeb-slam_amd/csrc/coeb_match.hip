@@ -753,13 +753,33 @@ __global__ __launch_bounds__(NT) void k_match_lists(MatchCam cam, MatchBufs b, f
     if (threadIdx.x == 0) qn[b.last_stride + sl] = s_flag[0];
 }
 
+// k_match's arguments as one struct at offset 0 of the kernarg segment (kernarg<MatchArgs>())
+struct MatchArgs {
+    MatchCam cam;
+    MatchBufs b;
+    float th0;
+    int bmono, check_ori, retry_below, force_seq, nsplit;
+};
+template <class T>
+__device__ __forceinline__ const T& kernarg()
+{
+    return *(const T*)__builtin_amdgcn_kernarg_segment_ptr();
+}
+
 template <bool kLds, int NT>
 #ifndef COEB_MATCH_MINWG
 #define COEB_MATCH_MINWG 4     // launch bound in waves per SIMD (4: two 512-thread pairs per CU)
 #endif
-__global__ __launch_bounds__(NT, COEB_MATCH_MINWG) void k_match(MatchCam cam, MatchBufs b, float th0, int bmono, int check_ori,
-                                                     int retry_below, int force_seq, int nsplit)
+__global__ __launch_bounds__(NT, COEB_MATCH_MINWG) void k_match(MatchArgs args)
 {
+    // the arguments are read where they are used, from the kernarg segment (a by-value struct is
+    // loaded whole at entry and kept in SGPRs for the kernel's life: 140 spilled SGPRs)
+    const MatchArgs& A = kernarg<MatchArgs>();
+    const MatchCam& cam = A.cam;
+    const MatchBufs& b = A.b;
+    const float th0 = A.th0;
+    const int bmono = A.bmono, check_ori = A.check_ori, retry_below = A.retry_below, force_seq = A.force_seq,
+              nsplit = A.nsplit;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int s_hist[HISTO_LENGTH];
     __shared__ int s_flag[8];
@@ -793,7 +813,9 @@ __global__ __launch_bounds__(NT, COEB_MATCH_MINWG) void k_match(MatchCam cam, Ma
     cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = cur_ur; cv.gdesc = cdesc;
 
     // ---- phase 0: stage CurrentFrame, grid CSR by a stable counting sort ----
-    long long* tm = b.timing ? b.timing + (int64_t)p * 16 : nullptr;   // phase clocks (COEB_MATCH_TIMING)
+    // phase clocks: experiment builds only (-DCOEB_MATCH_CLOCK=1 with COEB_MATCH_TIMING set,
+    // tools/_match_timing.py); the product build has no hook (14 SGPRs)
+    long long* tm = COEB_MATCH_CLOCK && b.timing ? b.timing + (int64_t)p * 16 : nullptr;
     if (tm && tid == 0) { tm[0] = clock64(); tm[13] = 0; tm[14] = 0x7fffffffffffffffll; tm[15] = 0; }
     // with split lists (nsplit > 0) the grid is built only if the sequential path or the retry
     // needs it
@@ -1387,7 +1409,7 @@ int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int b
                  int retry_below, hipStream_t s, ProfileHook* prof)
 {
     if (P <= 0) return 0;
-    const int force_seq = getenv("COEB_MATCH_SEQUENTIAL") ? 1 : 0;   // test knob: exact literal path
+    const int force_seq = coeb_switch("COEB_MATCH_SEQUENTIAL") ? 1 : 0;   // test knob: exact literal path
     const size_t lds_full = match_lds_bytes(b.cur_stride, b.last_stride, true, nullptr) + 256;
     const size_t lds_min = match_lds_bytes(b.cur_stride, b.last_stride, false, nullptr) + 256;
     // 512-thread workgroups when a pair's LDS fits half a CU (config A: 80.6 KB), so two pairs
@@ -1400,7 +1422,7 @@ int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int b
     int nsplit = 0;
     if (b.qn && b.qn_stride >= b.last_stride + kMaxSplit) {
         nsplit = std::min(kMaxSplit, 256 / std::max(P, 1));
-        if (const char* e = getenv("COEB_MATCH_SPLIT")) nsplit = std::max(0, std::min(kMaxSplit, atoi(e)));
+        if (const char* e = coeb_switch("COEB_MATCH_SPLIT")) nsplit = std::max(0, std::min(kMaxSplit, atoi(e)));
         if (nsplit < 2) nsplit = 0;
     }
     bool lds_cur = lds_full <= 160 * 1024;
@@ -1411,7 +1433,7 @@ int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int b
         // sequential fallback / the retry, then reading the frame from global memory), so it takes
         // a fraction of the LDS and leaves the CU to the other pipeline's kernels
         // (COEB_MATCH_SPLIT_FULL=1 keeps the staged form)
-        const char* le = getenv("COEB_MATCH_LISTS_LDS");
+        const char* le = coeb_experiment("COEB_MATCH_LISTS_LDS");
         const bool lists_lds = lds_cur && !(le && atoi(le) == 0);
         const size_t lds_l = match_lds_bytes(b.cur_stride, 0, lists_lds, nullptr);
         auto gl = [&](auto kern) {
@@ -1422,13 +1444,13 @@ int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int b
         if (lists_lds) gl(k_match_lists<true, 1024>);
         else gl(k_match_lists<false, 1024>);
         prof_end(prof, s);
-        const char* fe = getenv("COEB_MATCH_SPLIT_FULL");
+        const char* fe = coeb_experiment("COEB_MATCH_SPLIT_FULL");
         if (!(fe && atoi(fe) != 0)) lds_cur = false;
     }
     auto go = [&](auto kern, size_t lds) {
         lds_limit_max((const void*)kern);
-        hipLaunchKernelGGL(kern, dim3(P), dim3(nt), lds - 256, s, cam, b, th, bmono, check_ori, retry_below, force_seq,
-                           nsplit);
+        const MatchArgs a{cam, b, th, bmono, check_ori, retry_below, force_seq, nsplit};
+        hipLaunchKernelGGL(kern, dim3(P), dim3(nt), lds - 256, s, a);
     };
     prof_begin(prof, "k_match", s);
     if (lds_cur) {
@@ -1454,14 +1476,14 @@ int launch_match_local(const MatchCam& cam, const LocalBufsHost& h, float th, fl
     const int P = h.cur_n_arr ? h.npairs : 1;
     if (P <= 0) return 0;
     if (h.cur_n_arr && h.cur_stride >= (1 << kIdxBits)) return -2;
-    const int force_seq = getenv("COEB_MATCH_SEQUENTIAL") ? 1 : 0;
+    const int force_seq = coeb_switch("COEB_MATCH_SEQUENTIAL") ? 1 : 0;
     const int cs = std::max(h.cur_n_arr ? h.cur_stride : h.cur_n, 1), qs = std::max(h.mp_n, 1);
     const size_t lds_full = match_lds_bytes(cs, qs, true, nullptr) + 256;
     const size_t lds_min = match_lds_bytes(cs, qs, false, nullptr) + 256;
     prof_begin(prof, "k_match_local", s);
     // COEB_LOCAL_LDS=0: the current frame read from global memory (a third of the LDS, so the
     // workgroup finds room beside the pose and flow kernels sooner)
-    const char* le = getenv("COEB_LOCAL_LDS");
+    const char* le = coeb_experiment("COEB_LOCAL_LDS");
     if (lds_full <= 160 * 1024 && !(le && atoi(le) == 0)) {
         lds_limit_max((const void*)k_match_local<true>);
         hipLaunchKernelGGL(k_match_local<true>, dim3(P), dim3(kMThreads), lds_full - 256, s, cam, b, th, nnratio, force_seq);
@@ -1486,7 +1508,7 @@ int launch_match_kf(const MatchCam& cam, const KfBufsHost& h, float th, int orb_
     b.valid = h.valid; b.xw = h.xw; b.desc = h.desc; b.maxd = h.maxd; b.mind = h.mind; b.angle = h.angle;
     b.kf_n = h.kf_n; b.Tcw = h.Tcw; b.match = h.match; b.nmatch = h.nmatch; b.lists = h.lists; b.err = h.err;
     b.path = h.path;
-    const int force_seq = getenv("COEB_MATCH_SEQUENTIAL") ? 1 : 0;
+    const int force_seq = coeb_switch("COEB_MATCH_SEQUENTIAL") ? 1 : 0;
     const int cs = std::max(h.cur_n, 1), qs = std::max(h.kf_n, 1);
     const size_t lds_full = match_lds_bytes(cs, qs, true, nullptr) + 256;
     const size_t lds_min = match_lds_bytes(cs, qs, false, nullptr) + 256;

@@ -613,10 +613,7 @@ __global__ __launch_bounds__(kPT, EPT == 0 ? COEB_POSE_MINWG0 : COEB_POSE_MINWG)
     Se3 s0;
     if (tid == 0) s0 = pq_from_Tcw(Tcw);
     int nBad = 0;
-#ifndef COEB_POSE_ROUNDS
-#define COEB_POSE_ROUNDS 4     // Optimizer.cc:364 (fewer only in sensitivity experiments; not bit-exact)
-#endif
-    for (int it = 0; it < COEB_POSE_ROUNDS; it++) {
+    for (int it = 0; it < 4; it++) {                                // its < 4 (Optimizer.cc:364)
         if (tid == 0) L.s = s0;                                    // setEstimate(toSE3Quat(mTcw))
         __syncthreads();
         const bool robust = it < 3;
@@ -839,7 +836,6 @@ int launch_pose(const PoseBufs& b, int F, double fx, double fy, double cx, doubl
     prof_begin(prof, "k_pose", s);
     // edges per thread by the keypoint stride: registers up to 9 x 256 edges, else global scratch
     int ept = (b.stride + kPT - 1) / kPT;
-    if (const char* e = getenv("COEB_POSE_EPT")) if (atoi(e) == 0) ept = 1 << 20;   // experiment: force k_pose<0>
     if (ept <= 5) hipLaunchKernelGGL(k_pose<5>, dim3(F), dim3(kPT), 0, s, b, cm);
     else if (ept <= 9) hipLaunchKernelGGL(k_pose<9>, dim3(F), dim3(kPT), 0, s, b, cm);
     else hipLaunchKernelGGL(k_pose<0>, dim3(F), dim3(kPT), 0, s, b, cm);

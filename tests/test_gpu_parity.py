@@ -611,16 +611,18 @@ def test_batch_streams_agree(oracle_mod, ex):
         bp.close()
 
 
-@pytest.mark.parametrize("side", ["own", "shared", "eager"])
+@pytest.mark.parametrize("side", ["own", "shared", "eager", "off"])
 def test_sharded_batch_equals_unsharded(monkeypatch, side):
     """SURVEY.md s8e partitioning: a 24-frame sequence split over 3 shards (each with its one-frame
     halo, `dist.shard_frames`), driven concurrently from 3 host threads with one context each (what
     `bench.py --gpus N` does per device; all on device 0 here), gives per-frame keypoints,
     descriptors and matches bit-identical to the unsharded batch.  "shared": the three contexts'
     extraction side work goes to one per-device side stream (COEB_SIDE_SHARED=1, bench.py config C);
-    "eager": each context's side stream is created with the context (COEB_SIDE_EAGER=1, config A)."""
+    "eager": each context's side stream is created with the context (COEB_SIDE_EAGER=1, config A);
+    "off": no side stream (COEB_SIDE_STREAM=0, the profiling passes' schedule)."""
     monkeypatch.setenv("COEB_SIDE_SHARED", "1" if side == "shared" else "0")
     monkeypatch.setenv("COEB_SIDE_EAGER", "1" if side == "eager" else "0")
+    monkeypatch.setenv("COEB_SIDE_STREAM", "0" if side == "off" else "1")
     import threading
     from coeb_front.dist import shard_frames
     from coeb_front.pipeline import BatchPipeline
