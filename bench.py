@@ -465,27 +465,35 @@ def _pinned_legs(run_leg, cpu_list, seconds):
     return vals[len(vals) // 2], per
 
 
+def _cpu_dyn(cfg, nfr):
+    """Config C's per-frame dynamic-mask inputs (boxes, T_M, blur flags) for the CPU legs, as the
+    device batch gets them (dyn_batch), or None."""
+    return dyn_batch(cfg["w"], cfg["h"], nfr) if cfg.get("dyn") else None
+
+
 def _single_thread_leg(O, lib_path, cfg, ex_args, frames, depth, cam, cpu, seconds, min_frames, warmup=20):
     """SURVEY.md s8(d)'s single-thread leg on one oracle build: `warmup` untimed frames, then
-    extract + ComputeStereoFromRGBD + SearchByProjection (retry at 2*th) per frame, median time."""
+    extract (with config C's dynamic mask) + ComputeStereoFromRGBD + SearchByProjection (retry at
+    2*th) per frame, median time."""
     from coeb_front import synth
     O.LIB = lib_path
     O._lib = None
     ex = O.Extractor(*ex_args)
     nfr = len(frames)
+    dyn = _cpu_dyn(cfg, nfr)
+    ext = (lambda i: ex.extract(frames[i % nfr], *dyn[i % nfr])) if dyn else (lambda i: ex.extract(frames[i % nfr]))
     Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
-    prev = ex.extract(frames[0])
+    prev = ext(0)
     for i in range(1, 1 + warmup):
-        prev = ex.extract(frames[i % nfr])
+        prev = ext(i)
     times = []
     t_end = time.perf_counter() + seconds
     i = 1 + warmup
     while (time.perf_counter() < t_end or len(times) < min_frames) and len(times) < 400:
-        f = frames[i % nfr]
         last = O.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX, synth.TUM_FY,
                                           synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)   # map snapshot (untimed)
         t0 = time.perf_counter()
-        r = ex.extract(f)
+        r = ext(i)
         ur, _ = O.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
         nm, _ = O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 15.0)
         if nm < 20:
@@ -529,9 +537,10 @@ def cpu_baseline(cfg, seconds=9.0, min_frames=30):
     out = dict(value=val, unit="frames/s", cores=1, kind="port",
                sample="single thread pinned to each of the %d idlest CPUs (%s; idle fraction measured over 0.5 s "
                       "before), per CPU >= %d consecutive %dx%d synthetic frames after 20 warm-up frames, oracle "
-                      "(-O3 -march=native): extract + ComputeStereoFromRGBD + SearchByProjection (th 15, retry 30); "
-                      "value = median of the per-CPU median frame rates" % (len(pick), ", ".join(str(c) for c, _ in pick),
-                                                                           min_frames, w, h),
+                      "(-O3 -march=native): extract%s + ComputeStereoFromRGBD + SearchByProjection (th 15, retry 30); "
+                      "value = median of the per-CPU median frame rates"
+                      % (len(pick), ", ".join(str(c) for c, _ in pick), min_frames, w, h,
+                         " with the dynamic mask (2 boxes, 60 T_M points, blur flags per frame)" if cfg.get("dyn") else ""),
                spread=dict(min=min(vals), max=max(vals), per_cpu=per))
     out.update(info)
     out["caveat"] = CPU_CAVEAT
@@ -666,15 +675,18 @@ def cpu_baseline_parallel(O, cfg, frames, depth, cam, nthr, seconds=6.0):
     done = [0] * nthr
     t_end = [0.0]
 
+    dyn = _cpu_dyn(cfg, nfr)
+
     def work(t):
         ex = O.Extractor(cfg["nfeatures"], 1.2, 8, 20, 7)
+        ext = (lambda i: ex.extract(frames[i], *dyn[i])) if dyn else (lambda i: ex.extract(frames[i]))
         i = (7 * t) % nfr
-        prev = ex.extract(frames[i])
+        prev = ext(i)
         while time.perf_counter() < t_end[0]:
             i = (i + 1) % nfr
             last = O.mapframe_from_extraction(prev["kps"], prev["desc"], depth, synth.TUM_FX, synth.TUM_FY,
                                               synth.TUM_CX, synth.TUM_CY, synth.TUM_BF)
-            r = ex.extract(frames[i])
+            r = ext(i)
             ur, _ = O.stereo_from_rgbd(r["kps"], depth, synth.TUM_BF)
             nm, _ = O.search_by_projection(cam, r["kps"], r["desc"], ur, last, Tc, Tl, 15.0)
             if nm < 20:
