@@ -895,17 +895,6 @@ __device__ __forceinline__ int dot2s(uint32_t a, uint32_t b, int c)
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(lk_i16x2, a), __builtin_bit_cast(lk_i16x2, b), c, false);
 }
 
-// n <= 4 bytes from p (any alignment) as one dword; no dword past the one holding p[n - 1] is read
-typedef const uint32_t __attribute__((address_space(1)))* lk_gptr;
-__device__ __forceinline__ uint32_t load_seg4(const uint8_t* p, int n)
-{
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const lk_gptr a4 = (lk_gptr)(a & ~(uintptr_t)3);
-    const lk_gptr last = (lk_gptr)((a + n - 1) & ~(uintptr_t)3);
-    const lk_gptr a5 = a4 + 1 < last ? a4 + 1 : last;
-    return __builtin_amdgcn_alignbyte(*a5, *a4, (uint32_t)(a & 3));
-}
-
 // the three tap pairs (p[k], p[k + 1]), k = 0, 1, 2, of a 4-byte row segment as u16x2
 __device__ __forceinline__ void tap_pairs(uint32_t q, uint32_t* t)
 {
@@ -914,18 +903,28 @@ __device__ __forceinline__ void tap_pairs(uint32_t q, uint32_t* t)
     t[2] = __builtin_amdgcn_perm(0u, q, 0x0c030c02u);
 }
 
-// the four row segments of the tile at window offset (C0, R0) of a window whose top-left pixel is
-// org, as tap pairs.  Every lane loads all four (no divergent waits): rows and columns are clamped
-// to the window's +1 row / column, which the caller has checked lie inside the level, and the
-// samples this brings in outside the tile's pixels are weighed by zero derivatives.
-__device__ __forceinline__ void tile_pairs(const uint8_t* org, int pitch, int win, int C0, int R0, int nc, uint32_t (*t)[3])
+// The four row segments of the lane's tile as tap pairs, through a buffer resource over the level image (bounds-checked: a dword past the
+// image end reads as 0, so no per-row clamp), the window at scalar byte offset s_off and the
+// lane's four row offsets lofs[i] = min(C0, win) + min(R0 + i, win) * pitch fixed per level:
+// per row one add and two ands, two loads with a scalar base, one alignbyte (round 5's 64-bit
+// addresses with a clamped second dword cost ~30 more VALU per LK iteration: k_lk 3.27 -> 2.95 ms
+// per config-D step, profiles/r06/s3).  Every lane loads all four rows (no divergent waits):
+// rows and columns are clamped to the window's +1 row / column, which the caller has checked lie
+// inside the level, and the samples this brings in outside the tile's pixels are weighed by zero
+// derivatives.
+__device__ __forceinline__ void tile_pairs_buf(__amdgpu_buffer_rsrc_t r, int s_off, const int (&lofs)[4], uint32_t (*t)[3])
 {
-    const uint8_t* col = org + min(C0, win);
+    const int s_al = s_off & ~3, s_mis = s_off & 3;
 #pragma unroll
-    for (int i = 0; i < 4; i++) tap_pairs(load_seg4(col + (size_t)min(R0 + i, win) * pitch, nc + 1), t[i]);
+    for (int i = 0; i < 4; i++) {
+        const uint32_t o = (uint32_t)(lofs[i] + s_mis);
+        const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(r, o & ~3u, s_al, 0);
+        const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(r, (o & ~3u) + 4u, s_al, 0);
+        tap_pairs(__builtin_amdgcn_alignbyte(hi, lo, o & 3u), t[i]);
+    }
 }
 
-// tile_pairs for a window that reaches past the level edge: byte gathers at REFLECT_101
+// The same taps for a window that reaches past the level edge: byte gathers at REFLECT_101
 // coordinates (the taps of calcOpticalFlowPyrLK's border path), same clamping
 __device__ __forceinline__ void tile_pairs_reflect(const uint8_t* img, int pitch, int lw, int lh, int x0, int y0, int win,
                                                    int C0, int R0, uint32_t (*t)[3])
@@ -973,6 +972,11 @@ __global__ __launch_bounds__(256, COEB_LK_MINW) void k_lk(LkPyr pyr, const float
         const uint8_t* I = at_pair(pyr.P[level], level == 0 ? iz : pz, z);
         const uint8_t* J = at_pair(pyr.N[level], level == 0 ? iz : pz, z);
         const short2* D = at_pair(pyr.D[level], pz, z);
+        const __amdgpu_buffer_rsrc_t rI = __builtin_amdgcn_make_buffer_rsrc((void*)I, 0, pitch * lh, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rJ = __builtin_amdgcn_make_buffer_rsrc((void*)J, 0, pitch * lh, 0x00020000);
+        int lofs[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) lofs[i] = min(C0, win) + min(R0 + i, win) * pitch;
         const float sc = (float)(1. / (1 << level));
         float px = px0 * sc, py = py0 * sc;
         if (level == pyr.L - 1) { nx = px; ny = py; }
@@ -994,7 +998,7 @@ __global__ __launch_bounds__(256, COEB_LK_MINW) void k_lk(LkPyr pyr, const float
         const bool inside = ipx >= 0 && ipy >= 0 && ipx + win < lw && ipy + win < lh;
         uint32_t t[4][3];
         if (inside)
-            tile_pairs(I + (size_t)ipy * pitch + ipx, pitch, win, C0, R0, nc, t);
+            tile_pairs_buf(rI, __builtin_amdgcn_readfirstlane(ipy * pitch + ipx), lofs, t);
         else
             tile_pairs_reflect(I, pitch, lw, lh, ipx, ipy, win, C0, R0, t);
         const uint32_t W0 = (uint32_t)iw00 | ((uint32_t)iw01 << 16), W1 = (uint32_t)iw10 | ((uint32_t)iw11 << 16);
@@ -1050,7 +1054,7 @@ __global__ __launch_bounds__(256, COEB_LK_MINW) void k_lk(LkPyr pyr, const float
             int ib1 = -sIx, ib2 = -sIy;               // per lane: sum (J - I) * g, exact in int32
             uint32_t t[4][3];
             if (inx >= 0 && iny >= 0 && inx + win < lw && iny + win < lh)    // the window and its +1 neighbours inside
-                tile_pairs(J + (size_t)iny * pitch + inx, pitch, win, C0, R0, nc, t);
+                tile_pairs_buf(rJ, __builtin_amdgcn_readfirstlane(iny * pitch + inx), lofs, t);
             else
                 tile_pairs_reflect(J, pitch, lw, lh, inx, iny, win, C0, R0, t);
             const uint32_t W0 = (uint32_t)iw00 | ((uint32_t)iw01 << 16), W1 = (uint32_t)iw10 | ((uint32_t)iw11 << 16);
