@@ -68,6 +68,8 @@ for step in "$@"; do
                 --valu-json gpurun_out/pmc_valu_1280x960.json --frames 257 --size 1280x960 --command "$B" > gpurun_out/pmcB_valu.log 2>&1
             ;;
         benchB512) run benchB512 600 python bench.py --config B ;;
+        benchCfull) run benchC 600 python bench.py --config C ;;
+        benchDfull) run benchD 600 python bench.py --config D --no-extras ;;
         pmcD)
             # the configs[4] loop's kernels (flow, pose, TrackLocalMap) with their own traffic / VALU passes
             export COEB_SIDE_STREAM=0
