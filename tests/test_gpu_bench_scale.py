@@ -41,11 +41,13 @@ def test_bench_schedule_matches_oracle(monkeypatch, name):
                 bp.run(**kw)
         for bp in bps:
             bp.synchronize()
-        every = 16 if name == "B" else 128
+        # ~200 frames of A / C (every 16th), ~70 of B (every 8th), ~100 of D (every 32nd): the oracle
+        # takes a few seconds for A / B / C, ~20 s for D's four-frame chains
+        every = {"A": 16, "C": 16, "B": 8, "D": 32}[name]
         picks = [bench.parity_picks(F, every) for _, F, _ in subs]
         r = bench.parity_check(bps, cfg, picks)
         print(name, {k: r[k] for k in ("frames", "matched_frames", "frames_per_pipeline", "seconds")})
-        assert r["frames"] >= 30, r
+        assert r["frames"] >= 60, r
         assert r["bit_exact"], r["mismatches"]
     finally:
         for bp in bps:
