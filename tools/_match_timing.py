@@ -7,6 +7,8 @@ import sys
 import numpy as np
 
 os.environ["COEB_MATCH_TIMING"] = "1"
+os.environ["COEB_EXPERIMENTS"] = "1"     # experiment switches are read only under this gate
+# (and the library must be an experiment build: tools/_build_var.sh clock "-DCOEB_MATCH_CLOCK=1")
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "coeb-slam_amd"))
 from coeb_front import synth  # noqa: E402
 from coeb_front.pipeline import BatchPipeline  # noqa: E402

@@ -7,6 +7,7 @@ import sys
 import numpy as np
 
 os.environ["COEB_POSE_TIMING"] = "1"
+os.environ["COEB_EXPERIMENTS"] = "1"     # experiment switches are read only under this gate
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "coeb-slam_amd"))
 from coeb_front import synth  # noqa: E402
 from coeb_front.pipeline import BatchPipeline  # noqa: E402

@@ -14,6 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "coeb-slam_amd"))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("COEB_SUBPIX_COUNT", "1")
+os.environ["COEB_EXPERIMENTS"] = "1"     # experiment switches are read only under this gate
 
 
 def main():
