@@ -54,7 +54,11 @@ __device__ int g_subpix_count_dev[4];   // {cornerSubPix iterations, corners, LK
 int* g_subpix_count = nullptr;    // device address of g_subpix_count_dev (COEB_SUBPIX_COUNT, A/B tool)
 
 constexpr int kMaxPts = 1024;        // corners / tracked points per call (reference: 1000)
-constexpr int kGfThreads = 1024;
+// k_gf_select's workgroup: 256 threads (a config-D pair has ~270 local maxima: its sort stages and
+// barriers are cheaper with 4 waves than with 16, and four times as many pairs fit the CUs):
+// 0.39 -> 0.25 ms per 1537-pair launch, config-D step 35.8 -> 35.4 ms (512: 0.235 ms, 35.4-35.5;
+// profiles/r06/s7)
+constexpr int kGfThreads = 256;
 // local-maximum keys kept per frame: a quarter of the pixels (a 3 x 3 maximum needs its
 // neighbours below it unless the response plateaus); more is reported as -1
 inline int gf_key_cap(int w, int h) { return std::max(16384, w * h / 4); }

@@ -958,8 +958,8 @@ __device__ __forceinline__ QueryWin local_window(const MatchCam& cam, const Loca
 
 constexpr int kLocKeyDist = 16, kLocKeyOct = 12;    // list entry: dist << 16 | octave << 12 | index
 
-template <bool kLds>
-__global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBufs b0, float th, float nnratio,
+template <bool kLds, int NT>
+__global__ __launch_bounds__(NT) void k_match_local(MatchCam cam, LocalBufs b0, float th, float nnratio,
                                                            int force_seq)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -967,7 +967,7 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
     const int tid = threadIdx.x;
     const LocalBufs b = local_at_pair(b0, blockIdx.x);
     if (b0.active && !b0.active[blockIdx.x]) {                 // frame not handed to TrackLocalMap
-        for (int c = tid; c < b.cur_n; c += kMThreads) b.match[c] = -1;
+        for (int c = tid; c < b.cur_n; c += NT) b.match[c] = -1;
         if (tid == 0) *b.nmatch = 0;
         return;
     }
@@ -989,14 +989,14 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
     }
     CurView<kLds> cv;
     cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = b.cur_ur; cv.gdesc = b.cur_desc;
-    stage_grid<kLds>(cam, cur, b.cur_ur, b.cur_desc, n, L);
+    stage_grid<kLds, NT>(cam, cur, b.cur_ur, b.cur_desc, n, L);
     if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; s_flag[2] = 0; }
     __syncthreads();
 
     // ---- phase 1: candidate lists ----
     {
         const int grp = tid / kQL, gl = tid % kQL, gsh = (tid & 63) & ~(kQL - 1);
-        for (int q0 = 0; q0 < nq; q0 += kMThreads / kQL) {
+        for (int q0 = 0; q0 < nq; q0 += NT / kQL) {
             const int q = q0 + grp;
             int cnt = -1;
             QueryWin w;
@@ -1079,7 +1079,7 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
         int rm[LQ];
 #pragma unroll
         for (int u = 0; u < LQ; u++) {
-            const int q = tid + u * kMThreads;
+            const int q = tid + u * NT;
             rm[u] = -1;
             if (q < nq) {
                 const int qn = L.qn[q];
@@ -1093,11 +1093,11 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
         }
         for (int it = 0;; it++) {
             iters = it + 1;
-            for (int c = tid; c < n; c += kMThreads) L.owner[c] = 0x7fffffff;
+            for (int c = tid; c < n; c += NT) L.owner[c] = 0x7fffffff;
             if (tid == 0) s_flag[1] = 0;
             __syncthreads();
             if (it > 0) {
-                for (int q = tid; q < nq; q += kMThreads) {
+                for (int q = tid; q < nq; q += NT) {
                     const int r = L.res[q];
                     if (r >= 0 && (L.qn[q] & 0x10000)) atomicMin(&L.owner[r], q);
                 }
@@ -1105,7 +1105,7 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
             }
 #pragma unroll
             for (int u = 0; u < LQ; u++) {
-                const int q = tid + u * kMThreads;
+                const int q = tid + u * NT;
                 if (q < nq) {
                     int res = -1;
                     if (rm[u] >= 0) {
@@ -1121,7 +1121,7 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
                     L.res[q] = res;
                 }
             }
-            for (int q = tid + LQ * kMThreads; q < nq; q += kMThreads) {
+            for (int q = tid + LQ * NT; q < nq; q += NT) {
                 const int qn = L.qn[q];
                 int res = -1;
                 if (qn >= 0) {
@@ -1143,7 +1143,7 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
     if (seq) {
         // literal loop (ORBmatcher.cc:48-126), one thread; L.owner = Observations() of each
         // keypoint's holder
-        for (int c = tid; c < n; c += kMThreads) { L.owner[c] = b.cur_obs[c]; }
+        for (int c = tid; c < n; c += NT) { L.owner[c] = b.cur_obs[c]; }
         __syncthreads();
         if (tid == 0) {
             b.path[0] = force_seq ? 1 : s_flag[0] ? 2 : 3;   // forced / list overflow / no convergence
@@ -1182,16 +1182,16 @@ __global__ __launch_bounds__(kMThreads) void k_match_local(MatchCam cam, LocalBu
         return;
     }
     // ---- phase 3: the last assignment to a keypoint wins ----
-    for (int c = tid; c < n; c += kMThreads) L.owner[c] = -1;
+    for (int c = tid; c < n; c += NT) L.owner[c] = -1;
     __syncthreads();
     int mine = 0;
-    for (int q = tid; q < nq; q += kMThreads) {
+    for (int q = tid; q < nq; q += NT) {
         const int r = L.res[q];
         if (r >= 0) { atomicMax(&L.owner[r], q); mine++; }
     }
     if (mine) atomicAdd(&s_flag[2], mine);
     __syncthreads();
-    for (int c = tid; c < n; c += kMThreads) b.match[c] = L.owner[c];
+    for (int c = tid; c < n; c += NT) b.match[c] = L.owner[c];
     if (tid == 0) { *b.nmatch = s_flag[2]; b.path[0] = 0; b.path[1] = iters; }
 }
 
@@ -1484,12 +1484,23 @@ int launch_match_local(const MatchCam& cam, const LocalBufsHost& h, float th, fl
     // COEB_LOCAL_LDS=0: the current frame read from global memory (a third of the LDS, so the
     // workgroup finds room beside the pose and flow kernels sooner)
     const char* le = coeb_experiment("COEB_LOCAL_LDS");
+    // a batch (the configs[4] loop's TrackLocalMap) takes 512 threads per frame: the kernel alone
+    // runs longer (0.78 vs 0.51 ms per 1537 frames) but leaves room to the pose / flow kernels it
+    // overlaps, and the config-D step is shorter (35.11 vs 35.45-35.60 ms, profiles/r06/s8); one
+    // frame from host buffers keeps 1024 (its latency is all there is)
+    auto go = [&](auto k1024, auto k512, size_t lds) {
+        if (P > 1) {
+            lds_limit_max((const void*)k512);
+            hipLaunchKernelGGL(k512, dim3(P), dim3(512), lds - 256, s, cam, b, th, nnratio, force_seq);
+        } else {
+            lds_limit_max((const void*)k1024);
+            hipLaunchKernelGGL(k1024, dim3(P), dim3(1024), lds - 256, s, cam, b, th, nnratio, force_seq);
+        }
+    };
     if (lds_full <= 160 * 1024 && !(le && atoi(le) == 0)) {
-        lds_limit_max((const void*)k_match_local<true>);
-        hipLaunchKernelGGL(k_match_local<true>, dim3(P), dim3(kMThreads), lds_full - 256, s, cam, b, th, nnratio, force_seq);
+        go(k_match_local<true, 1024>, k_match_local<true, 512>, lds_full);
     } else if (lds_min <= 160 * 1024) {
-        lds_limit_max((const void*)k_match_local<false>);
-        hipLaunchKernelGGL(k_match_local<false>, dim3(P), dim3(kMThreads), lds_min - 256, s, cam, b, th, nnratio, force_seq);
+        go(k_match_local<false, 1024>, k_match_local<false, 512>, lds_min);
     } else {
         prof_end(prof, s);
         return -2;
