@@ -2614,7 +2614,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
             fast(side->s, 1, m);
         }
     }
-    constexpr int kOctThreads = 256;       // 512 / 1024 measured slower on large batches
+    constexpr int kOctThreads = 256;       // 512 / 1024 measured slower on large batches, 128 too (r06/s10)
     // Small batches (per-rank shards: fewer workgroups than two per CU): the key capacity in LDS
     // doubles (up to 4096 keys, within 150 KB), so a 1280x960 level 0 (~2 700 candidates) keeps
     // its keys in LDS instead of the global ping-pong buffers; large batches keep the plan's

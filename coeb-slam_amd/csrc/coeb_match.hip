@@ -1415,7 +1415,7 @@ int launch_match(const MatchCam& cam, const MatchBufs& b, int P, float th, int b
     // 512-thread workgroups when a pair's LDS fits half a CU (config A: 80.6 KB), so two pairs
     // share a CU and one pair's barrier waits overlap the other's work (k_match 0.355 -> 0.335 ms
     // per 1025-frame launch, profiles/r03/s5/match_nt_ab.txt); otherwise 1024 threads per pair
-    const int nt = lds_full <= 80 * 1024 ? 512 : 1024;
+    const int nt = lds_full <= 80 * 1024 ? 512 : 1024;     // (1024 always: config A 8.62-8.70 vs 8.35-8.47 ms, r06/s10)
     // Few pairs (a small shard): the candidate lists are built by k_match_lists with nsplit
     // workgroups per pair, so ~256 workgroups share the work instead of P; COEB_MATCH_SPLIT=0
     // turns this off, =N forces N
