@@ -39,6 +39,13 @@ for step in "$@"; do
         timeline)
             run timeline 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tl -o run -- python bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-extras --no-e2e --no-profile
             python tools/timeline2.py gpurun_out/tl/run_kernel_trace.csv 3 > gpurun_out/timeline.txt 2>&1; tail -n 30 gpurun_out/timeline.txt ;;
+        timelineD)
+            run timelineD 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tlD -o run -- python bench.py --config D --steps 4 --warmup 2 --no-cpu-baseline --no-extras --no-e2e --no-profile
+            python tools/timeline2.py gpurun_out/tlD/run_kernel_trace.csv 2 > gpurun_out/timelineD.txt 2>&1; tail -n 30 gpurun_out/timelineD.txt ;;
+        rehearsal)
+            # the process-per-GPU path (torch.distributed.run, gloo barrier / max) with both ranks on
+            # device 0 of this one-GPU box: plumbing only, the line is marked rehearsal_one_device
+            COEB_BENCH_ONE_DEVICE=1 run rehearsal 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline --no-extras --no-e2e ;;
         posetime) run posetime 300 python tools/pose_timing.py ;;
         flow) run flow 300 python tools/flow_bench.py ;;
         flowprof) run flowprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/flowprof -o run -- python tools/flow_bench.py ;;
