@@ -493,7 +493,9 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
 // next one from the work queue at the start of the next round.  The two image rows a phase's fill
 // needs come straight from global memory (L2-resident windows), issued at the start of the phase
 // and consumed at its end, so no load is in flight across the loop's back edge.
-constexpr int kSpSlots = 9;      // corner slots per wave (9: 45 summing lanes)
+// corner slots per wave (9: 45 summing lanes; 6 and 12 measured slower on the config-D step:
+// 36.30 / 35.71-35.83 vs 35.10 ms, profiles/r06/s11)
+constexpr int kSpSlots = 9;
 constexpr int kSpPrPad = 1;      // row padding of the rolling patch (floats)
 constexpr int kSpTrPad = 5;      // row padding of the term rows (doubles; >= 5: the sink slot G's terms)
 static_assert(kSpTrPad >= 5, "the term rows hold the sink slot's five terms");
