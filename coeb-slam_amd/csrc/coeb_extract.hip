@@ -411,7 +411,12 @@ __global__ COEB_PYR_LB void k_pyr_rows(const uint8_t* __restrict__ src, int64_t 
     const __amdgpu_buffer_rsrc_t rd =
         __builtin_amdgcn_make_buffer_rsrc((void*)(dst + (int64_t)f * dst_fs), 0, 0x7fffffff, 0x00020000);
     uint32_t w[PR_ROWS][4];
-    // (round 6: reusing the source row that consecutive output rows share, behind wave-uniform
+    // (round 6: dealing the grid to the XCDs in contiguous runs (block_xy's mapping over
+    // (strip, band, frame)) cuts this kernel's fetch 1.88x -> 1.02x its reads -- round-robin puts
+    // neighbouring strips, which share 2-3 source lines per row, on different L2s -- but runs
+    // 0.583 vs 0.568 ms per 7-launch pyramid, the step unchanged; a frame-major grid (a frame's
+    // blocks on one XCD) fetched 1.06x and ran 0.600 ms.  The pyramid is not bound by these bytes;
+    // profiles/r06/s17..s19.  Reusing the source row that consecutive output rows share, behind wave-uniform
     // branches, ran 0.669 vs 0.569 ms per 7-launch pyramid: the loads no longer issue back to
     // back; profiles/r06/s3)
 #pragma unroll
