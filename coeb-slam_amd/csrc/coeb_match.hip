@@ -190,8 +190,8 @@ __device__ __forceinline__ bool window_cells(const MatchCam& cam, QueryWin& w)
     return true;
 }
 
-__device__ __forceinline__ QueryWin query_window(const MatchCam& cam, const float* T, const float* X, int octave,
-                                                 float th, bool fwd, bool bwd)
+__device__ __forceinline__ QueryWin query_window(const MatchCam& cam, const float* T, const float* scale, const float* X,
+                                                 int octave, float th, bool fwd, bool bwd)
 {
     QueryWin w;
     w.ok = false;
@@ -207,7 +207,7 @@ __device__ __forceinline__ QueryWin query_window(const MatchCam& cam, const floa
     w.v = __builtin_fmaf(cam.fy * p3[1], invzc, cam.cy);
     if (w.u < cam.min_x || w.u > cam.max_x) return w;
     if (w.v < cam.min_y || w.v > cam.max_y) return w;
-    w.radius = th * cam.scale[octave];
+    w.radius = th * scale[octave];
     if (fwd) { w.minL = octave; w.maxL = -1; }
     else if (bwd) { w.minL = 0; w.maxL = octave; }
     else { w.minL = octave - 1; w.maxL = octave + 1; }
@@ -280,19 +280,32 @@ __device__ __forceinline__ int rot_bin(float a_last, float a_cur)
     return bin;
 }
 
+// ORBmatcher::ComputeThreeMaxima (ORBmatcher.cc:1602-1638) as selects.  max1 >= max2 >= max3
+// holds throughout, so s > max1 implies s > max2 implies s > max3, and each branch of the
+// reference's if / else-if chain is one combination of the three tests.  (Written as that chain,
+// the compiler addressed the index variables through scratch memory -- a dependent scratch
+// round trip per bin, ~20 k cycles of k_match's assignment phase per pair.)
 __device__ __forceinline__ void three_maxima(const int* hist, int& ind1, int& ind2, int& ind3)
 {
     int max1 = 0, max2 = 0, max3 = 0;
-    ind1 = ind2 = ind3 = -1;
+    int i1 = -1, i2 = -1, i3 = -1;
+#pragma unroll 6
     for (int i = 0; i < HISTO_LENGTH; i++) {
         const int s = hist[i];
-        if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
-        else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
-        else if (s > max3) { max3 = s; ind3 = i; }
+        const bool g1 = s > max1, g2 = s > max2, g3 = s > max3;
+        max3 = g2 ? max2 : g3 ? s : max3;
+        i3 = g2 ? i2 : g3 ? i : i3;
+        max2 = g1 ? max1 : g2 ? s : max2;
+        i2 = g1 ? i1 : g2 ? i : i2;
+        max1 = g1 ? s : max1;
+        i1 = g1 ? i : i1;
     }
+    ind1 = i1; ind2 = i2; ind3 = i3;
     if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
     else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
 }
+
+constexpr int kHeldOct = 0x100;          // stage_grid's held-keypoint flag (octaves are < 16)
 
 struct MatchLds {
     int* cell; uint32_t* sort; int* owner; int* res; int* qn; float4* kp; uint32_t* desc;
@@ -320,7 +333,7 @@ __host__ __device__ inline size_t match_lds_bytes(int nmax, int qmax, bool lds_c
 // cell order, index order inside a cell.  L.owner is scratch here.
 template <bool kLds, int NT = kMThreads>
 __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, const float* cur_ur, const uint8_t* cdesc,
-                                           int n, const MatchLds& L)
+                                           int n, const MatchLds& L, const int* cur_obs = nullptr)
 {
     const int tid = threadIdx.x;
     for (int c = tid; c <= COEB_GRID_CELLS; c += NT) L.cell[c] = 0;
@@ -404,7 +417,10 @@ __device__ __forceinline__ void stage_grid(const MatchCam& cam, const Kp* cur, c
         for (int e = tid; e < ng; e += NT) {
             const int i = (int)(L.sort[e] & ((1u << kIdxBits) - 1));
             const Kp k = cur[i];
-            L.kp[e] = make_float4(k.x, k.y, cur_ur ? cur_ur[i] : -1.f, __int_as_float(k.octave));
+            // cur_obs (k_match_local): a keypoint whose MapPoint has observations carries kHeldOct in
+            // its staged octave, which puts it above every level window (it is never a candidate)
+            const int oct = cur_obs && cur_obs[i] > 0 ? k.octave | kHeldOct : k.octave;
+            L.kp[e] = make_float4(k.x, k.y, cur_ur ? cur_ur[i] : -1.f, __int_as_float(oct));
             const uint4* d = reinterpret_cast<const uint4*>(cdesc + 32 * i);
             const uint4 d0 = d[0], d1 = d[1];
             uint4* o = reinterpret_cast<uint4*>(L.desc + 8 * e);
@@ -622,18 +638,33 @@ __device__ void build_lists(const MatchCam& cam, const PairView& v, const MatchL
     const float* lxw = v.lxw;
     const int* lnobs = v.lnobs;
     uint32_t* lists = v.lists;
-    const float* T = v.T;
     const bool fwd = v.fwd, bwd = v.bwd;
+    // the pose and the level scales every query's window reads, staged once: read from global
+    // memory the compiler reloads them for every query (the list stores might alias them) and
+    // waits for each load in turn
+    __shared__ float s_geo[12 + COEB_MAXL];
+    if (tid < 12) s_geo[tid] = v.T[tid];
+    else if (tid < 12 + COEB_MAXL) s_geo[tid] = cam.scale[tid - 12];
+    __syncthreads();
+    const float* T = s_geo;
+    const float* scale = s_geo + 12;
     // one kQL-lane group per query; lanes take the candidates of a grid column range kQL at a
     // time and ballot-compact them, so each list stays in enumeration order
     {
         const int grp = tid / kQL, gl = tid % kQL, gsh = (tid & 63) & ~(kQL - 1);
         // a query's inputs (flags, world point, octave, descriptor) are loaded one pass ahead
-        struct QIn { int act, oct; float X[3]; uint4 d0, d1; };
+        // (the flags are kept raw and tested when the query is taken: as lhas[q] && !lout[q] the
+        // second load waited for the first, and testing them here waits for both one pass early;
+        // Observations() rides along for the count word)
+        struct QIn { int has, out, oct, nobs; float X[3]; uint4 d0, d1; };
         auto load_qin = [&](int q, QIn& r) {
-            r.act = 0;
+            r.has = 0;
+            r.out = 1;
+            r.nobs = 0;
             if (q < nl) {
-                r.act = lhas[q] && !lout[q];
+                r.has = lhas[q];
+                r.out = lout[q];
+                r.nobs = lnobs[q];
                 r.oct = last[q].octave;
                 r.X[0] = lxw[3 * q]; r.X[1] = lxw[3 * q + 1]; r.X[2] = lxw[3 * q + 2];
                 const uint4* d = reinterpret_cast<const uint4*>(ldesc + 32 * q);
@@ -650,7 +681,7 @@ __device__ void build_lists(const MatchCam& cam, const PairView& v, const MatchL
             int cnt = -1;
             QueryWin w;
             w.ok = false;
-            if (qi.act) w = query_window(cam, T, qi.X, qi.oct, th, fwd, bwd);
+            if (qi.has && !qi.out) w = query_window(cam, T, scale, qi.X, qi.oct, th, fwd, bwd);
             if (w.ok) {
                 uint32_t qd[8];
                 qd[0] = qi.d0.x; qd[1] = qi.d0.y; qd[2] = qi.d0.z; qd[3] = qi.d0.w;
@@ -703,7 +734,7 @@ __device__ void build_lists(const MatchCam& cam, const PairView& v, const MatchL
                 }
                 if (cnt > kCQ) s_flag[0] = 1;      // overflow -> sequential path
             }
-            if (q < nl && gl == 0) qn_out[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | (lnobs[q] > 0 ? 0x10000 : 0));
+            if (q < nl && gl == 0) qn_out[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | (qi.nobs > 0 ? 0x10000 : 0));
             if (tm && tid == 0) tm[15] += 1;
         }
         if (tm && (tid & 63) == 0) {           // per-wave loop time: slowest / fastest wave
@@ -864,7 +895,7 @@ __global__ __launch_bounds__(NT, COEB_MATCH_MINWG) void k_match(MatchArgs args)
                 for (int q = 0; q < nl; q++) {
                     int best = -1;
                     if (L.qn[q] >= 0) {
-                        const QueryWin w = query_window(cam, T, lxw + 3 * q, last[q].octave, th, fwd, bwd);
+                        const QueryWin w = query_window(cam, T, cam.scale, lxw + 3 * q, last[q].octave, th, fwd, bwd);
                         if (w.ok) {
                             uint32_t qd[8];
                             for (int k = 0; k < 8; k++) qd[k] = reinterpret_cast<const uint32_t*>(ldesc + 32 * q)[k];
@@ -989,25 +1020,58 @@ __global__ __launch_bounds__(NT) void k_match_local(MatchCam cam, LocalBufs b0, 
     }
     CurView<kLds> cv;
     cv.kp = L.kp; cv.desc = L.desc; cv.gkp = cur; cv.gur = b.cur_ur; cv.gdesc = b.cur_desc;
-    stage_grid<kLds, NT>(cam, cur, b.cur_ur, b.cur_desc, n, L);
+    // the level scales, read by every point's window (from the kernel arguments each read is a
+    // dependent global load)
+    __shared__ float s_scale[COEB_MAXL];
+    if (tid < COEB_MAXL) s_scale[tid] = cam.scale[tid];
+    stage_grid<kLds, NT>(cam, cur, b.cur_ur, b.cur_desc, n, L, kLds ? b.cur_obs : nullptr);
     if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; s_flag[2] = 0; }
     __syncthreads();
 
     // ---- phase 1: candidate lists ----
     {
         const int grp = tid / kQL, gl = tid % kQL, gsh = (tid & 63) & ~(kQL - 1);
-        for (int q0 = 0; q0 < nq; q0 += NT / kQL) {
+        constexpr int qstep = NT / kQL;
+        // a point's inputs (isInFrustum's outputs, Observations(), descriptor) are loaded one pass
+        // ahead, as in k_match's lists
+        struct LIn { int view, level, nobs; float vcos, px, py, pxr; uint4 d0, d1; };
+        auto load_lin = [&](int q, LIn& r) {
+            r.view = 0;
+            r.nobs = 0;
+            if (q < nq) {
+                r.view = b.in_view[q];
+                r.level = b.level[q];
+                r.vcos = b.view_cos[q];
+                r.px = b.proj_x[q]; r.py = b.proj_y[q]; r.pxr = b.proj_xr[q];
+                r.nobs = b.nobs[q];
+                const uint4* d = reinterpret_cast<const uint4*>(b.desc + 32 * q);
+                r.d0 = d[0]; r.d1 = d[1];
+            }
+        };
+        LIn nx;
+        load_lin(grp, nx);
+        for (int q0 = 0; q0 < nq; q0 += qstep) {
             const int q = q0 + grp;
+            const LIn qi = nx;
+            load_lin(q + qstep, nx);
             int cnt = -1;
-            QueryWin w;
+            QueryWin w;                               // local_window, from the prefetched inputs
             w.ok = false;
-            if (q < nq) w = local_window(cam, b, q, th);
+            if (q < nq && qi.view) {
+                float r = radius_by_viewing_cos(qi.vcos);
+                if (th != 1.0f) r *= th;
+                w.u = qi.px;
+                w.v = qi.py;
+                w.radius = r * s_scale[qi.level];
+                w.minL = qi.level - 1;
+                w.maxL = qi.level;
+                w.ur_q = qi.pxr;
+                w.ok = window_cells(cam, w);
+            }
             if (w.ok) {
                 uint32_t qd[8];
-                const uint4* d = reinterpret_cast<const uint4*>(b.desc + 32 * q);
-                const uint4 d0 = d[0], d1 = d[1];
-                qd[0] = d0.x; qd[1] = d0.y; qd[2] = d0.z; qd[3] = d0.w;
-                qd[4] = d1.x; qd[5] = d1.y; qd[6] = d1.z; qd[7] = d1.w;
+                qd[0] = qi.d0.x; qd[1] = qi.d0.y; qd[2] = qi.d0.z; qd[3] = qi.d0.w;
+                qd[4] = qi.d1.x; qd[5] = qi.d1.y; qd[6] = qi.d1.z; qd[7] = qi.d1.w;
                 cnt = 0;
                 uint32_t* lst = b.lists + (int64_t)q * kCQ;
                 for (int gx = w.x0; gx <= w.x1; gx += kQL) {        // column groups, as in k_match
@@ -1031,7 +1095,7 @@ __global__ __launch_bounds__(NT) void k_match_local(MatchCam cam, LocalBufs b0, 
                             ok = !(oct < w.minL || oct > w.maxL);              // chk is always set here
                             const float distx = x - w.u, disty = y - w.v;
                             if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) ok = false;
-                            if (b.cur_obs[i2] > 0) ok = false;                    // :86-88, entry holder
+                            if (!kLds && b.cur_obs[i2] > 0) ok = false;  // :86-88, entry holder (LDS: kHeldOct)
                             if (ur > 0 && fabsf(w.ur_q - ur) > w.radius) ok = false;   // :90-95
                             if (ok) {
                                 const int dist = cv.dist(e, i2, qd);
@@ -1048,7 +1112,7 @@ __global__ __launch_bounds__(NT) void k_match_local(MatchCam cam, LocalBufs b0, 
                 }
                 if (cnt > kCQ) s_flag[0] = 1;
             }
-            if (q < nq && gl == 0) L.qn[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | (b.nobs[q] > 0 ? 0x10000 : 0));
+            if (q < nq && gl == 0) L.qn[q] = cnt < 0 ? -1 : (min(cnt, kCQ) | (qi.nobs > 0 ? 0x10000 : 0));
         }
     }
     __syncthreads();
