@@ -110,6 +110,12 @@ __device__ __forceinline__ T* at_pair(T* p, int64_t stride)
 // A grid of P x 1024 one-wave slots of which ~150 per pair hold a point was bound by the rate
 // at which the dispatcher retires empty waves (262,144 waves in ~1.5 ms for both kernels).
 // item -> (pair, point) by a binary search over offs.
+// (pair, index) of a flattened item packed in one int: index < kMaxPts = 2^kFlowIdxBits
+constexpr int kFlowIdxBits = 10;
+static_assert(kMaxPts <= (1 << kFlowIdxBits), "flow_code index field");
+__device__ __forceinline__ int flow_code(int2 zp) { return (zp.x << kFlowIdxBits) | zp.y; }
+__device__ __forceinline__ int2 flow_decode(int c) { return make_int2(c >> kFlowIdxBits, c & ((1 << kFlowIdxBits) - 1)); }
+
 __device__ __forceinline__ int2 flow_item(const int* __restrict__ offs, int P, int item)
 {
     int lo = 0, hi = P;                        // offs[lo] <= item < offs[hi]
@@ -564,7 +570,7 @@ __global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0,
                 const int q = base + __popcll(nm & ((1ull << lane) - 1ull));
                 item = q < total ? q : -1;
                 if (item >= 0) {
-                    const int2 zp = flow_item(offs, P, order[item]);
+                    const int2 zp = flow_decode(order[item]);
                     xy = at_pair(xy0, pz, (uint32_t)zp.x);
                     simg = at_pair(img0, iz, (uint32_t)zp.x);
                     pidx = zp.y;
@@ -743,8 +749,12 @@ __global__ __launch_bounds__(256) void k_subpix_order(const float* __restrict__ 
     for (int base = blockIdx.x * 256 + (threadIdx.x & ~63); base < total; base += gridDim.x * 256) {
         const int item = base + lane;
         bool in = false, bd = false;
+        int code = 0;
         if (item < total) {
             const int2 zp = flow_item(offs, P, item);
+            // the corner as (pair, index) packed (flow_code): k_subpix's slot refill then needs no
+            // binary search over offs (11 dependent global loads per corner)
+            code = flow_code(zp);
             const float* xy = at_pair(xy0, pz, (uint32_t)zp.x);
             const float x = xy[2 * zp.y], y = xy[2 * zp.y + 1];
             in = x >= (float)margin && x <= (float)(w - 1 - margin) && y >= (float)margin && y <= (float)(h - 1 - margin);
@@ -758,8 +768,8 @@ __global__ __launch_bounds__(256) void k_subpix_order(const float* __restrict__ 
         }
         bi = __builtin_amdgcn_readfirstlane(bi);
         bb = __builtin_amdgcn_readfirstlane(bb);
-        if (in) order[bi + __popcll(mi & lt)] = item;
-        if (bd) order[total - 1 - (bb + __popcll(mb & lt))] = item;
+        if (in) order[bi + __popcll(mi & lt)] = code;
+        if (bd) order[total - 1 - (bb + __popcll(mb & lt))] = code;
     }
 }
 
@@ -960,6 +970,9 @@ __global__ __launch_bounds__(256, COEB_LK_MINW) void k_lk(LkPyr pyr, const float
     // points in grid-stride order (taking them from a queue, one atomic per point, measured slower:
     // 3.53 vs 3.29 ms per config-D step, profiles/r05/s43)
     for (int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); item < total; item += gridDim.x * 4) {
+    // (the points in k_subpix_order's order, decoded from its packed codes instead of this binary
+    // search: 3.01-3.04 vs 2.95-3.01 ms per config-D step, the order loses the frames' locality;
+    // profiles/r06/s26)
     const int2 zp = flow_item(offs, P, item);
     const uint32_t z = (uint32_t)zp.x;
     const float* pxy = at_pair(pxy0, pz, z);
