@@ -968,7 +968,8 @@ __global__ __launch_bounds__(256, COEB_LK_MINW) void k_lk(LkPyr pyr, const float
     const int nr = min(3, max(0, win - R0)), nc = nr > 0 ? min(3, max(0, win - C0)) : 0;   // this lane's pixels
     const int total = offs[P];
     // points in grid-stride order (taking them from a queue, one atomic per point, measured slower:
-    // 3.53 vs 3.29 ms per config-D step, profiles/r05/s43)
+    // 3.53 vs 3.29 ms per config-D step, profiles/r05/s43; the blocks dealt to the XCDs in
+    // contiguous runs, so a pair's points share one L2, 2.97-3.00 vs 2.96-2.98 ms, r06/s27)
     for (int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); item < total; item += gridDim.x * 4) {
     // (the points in k_subpix_order's order, decoded from its packed codes instead of this binary
     // search: 3.01-3.04 vs 2.95-3.01 ms per config-D step, the order loses the frames' locality;
