@@ -503,6 +503,16 @@ __global__ __launch_bounds__(kGfThreads) void k_gf_select(const uint64_t* __rest
 // 36.30 / 35.71-35.83 vs 35.10 ms, profiles/r06/s11)
 constexpr int kSpSlots = 9;
 constexpr int kSpPrPad = 1;      // row padding of the rolling patch (floats)
+// Rolling patch of a slot: three rows (window row i reads patch rows i .. i + 2, and row i + 3 is
+// filled into row i's place once they are read), slot stride kSpSS = 21 (mod 64) dwords so the
+// term lanes of a pass -- slots g, g + 1, g + 2 at the same 21 columns -- read 63 distinct banks.
+// The 4-row ring at 96 dwords per slot put slots g and g + 2 on the same banks: 2.74 vs 1.96
+// conflict cycles per LDS instruction, k_subpix 3.26-3.32 vs 3.19-3.23 ms per config-D step
+// (profiles/r06/s30).
+constexpr int kSpRows = 3;
+constexpr int kSpRS = 23 + kSpPrPad;                       // BW + padding
+constexpr int kSpSS = 85;
+static_assert(kSpSS >= kSpRows * kSpRS && kSpSS % 64 == 21, "k_subpix patch layout");
 constexpr int kSpTrPad = 5;      // row padding of the term rows (doubles; >= 5: the sink slot G's terms)
 static_assert(kSpTrPad >= 5, "the term rows hold the sink slot's five terms");
 struct __attribute__((aligned(16))) SpSlot {      // read as three 16-byte words by the fill lanes
@@ -526,7 +536,9 @@ __global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0,
     static_assert(NL <= 64, "one summing lane per slot and term");
     // slot G is a sink: the fill and term lanes past the last slot read and write it, so no
     // pass needs a branch and the LDS reads of all passes issue together
-    __shared__ __attribute__((aligned(16))) float pr[G + 1][4][BW + kSpPrPad];   // rolling patch rows, row r at r & 3
+    static_assert(BW + kSpPrPad == kSpRS, "k_subpix row stride");
+    __shared__ __attribute__((aligned(16))) float pr[(G + 1) * kSpSS];   // rolling patch rows (kSpRows per slot)
+    auto prow = [](int r) { return r % kSpRows; };
     __shared__ double tr[WW][NL + kSpTrPad];      // one window row's terms, [j][5 g + t]
     __shared__ SpSlot par[G + 1];
     __shared__ double ssum[NL];
@@ -653,7 +665,9 @@ __global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0,
                 v0 = (fd[q] & 16) ? l0 * b1 + h0 * b2 : l0 * c4 + l1 * a12 + h0 * c5 + h1 * a22;
                 v1 = (fd[q] & 32) ? l1 * b1 + h1 * b2 : l1 * c4 + l2 * a12 + h1 * c5 + h2 * a22;
             }
-            *reinterpret_cast<float2*>(&pr[fg[q]][r & 3][fj0[q]]) = make_float2(v0, v1);   // column 23: padding
+            float* dst = &pr[fg[q] * kSpSS + prow(r) * kSpRS + fj0[q]];   // column 23: padding
+            dst[0] = v0;
+            dst[1] = v1;
         };
 #pragma unroll
         for (int q = 0; q < NF; q++) {
@@ -680,8 +694,11 @@ __global__ __launch_bounds__(64) void k_subpix(const uint8_t* __restrict__ img0,
 #pragma unroll
             for (int q = 0; q < NT; q++) {             // window row i: all passes' patch reads first
                 const int g = tg[q], j = tj[q];
-                d[q][0] = pr[g][(i + 1) & 3][j + 2]; d[q][1] = pr[g][(i + 1) & 3][j];
-                d[q][2] = pr[g][(i + 2) & 3][j + 1]; d[q][3] = pr[g][i & 3][j + 1];
+                const float* r0 = &pr[g * kSpSS + prow(i) * kSpRS + j];
+                const float* r1 = &pr[g * kSpSS + prow(i + 1) * kSpRS + j];
+                const float* r2 = &pr[g * kSpSS + prow(i + 2) * kSpRS + j];
+                d[q][0] = r1[2]; d[q][1] = r1[0];
+                d[q][2] = r2[1]; d[q][3] = r0[1];
             }
 #pragma unroll
             for (int q = 0; q < NT; q++) {
