@@ -372,15 +372,7 @@ __device__ __forceinline__ void pyr_rows_out(const uint32_t (&w)[PR_ROWS][4], co
     }
 }
 
-#ifndef COEB_PYR_MINW
-#define COEB_PYR_MINW 0         // experiment knob: a min-waves-per-SIMD launch bound for k_pyr_rows (0: none)
-#endif
-#if COEB_PYR_MINW
-#define COEB_PYR_LB __launch_bounds__(kThreads, COEB_PYR_MINW)
-#else
-#define COEB_PYR_LB __launch_bounds__(kThreads)
-#endif
-__global__ COEB_PYR_LB void k_pyr_rows(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
+__global__ __launch_bounds__(kThreads) void k_pyr_rows(const uint8_t* __restrict__ src, int64_t src_fs, int sp,
                                                        int sh, uint8_t* __restrict__ dst, int64_t dst_fs, int dp,
                                                        int dw, int dh, const int* __restrict__ tab, int xmax, int xs,
                                                        const int4* __restrict__ yrow)
@@ -470,9 +462,6 @@ struct BlurWork {
 };
 
 
-#ifndef COEB_XCD_REMAP
-#define COEB_XCD_REMAP 1
-#endif
 // Logical (x, y) block of a 2-D grid with each XCD given a contiguous run of logical blocks.
 // Blocks are observed to be dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, Workgroup
 // dispatch & XCD placement): physical block p lands on XCD p % 8.  Mapping XCD x's k-th block
@@ -485,7 +474,7 @@ template <bool kRemap = true>
 __device__ __forceinline__ int2 block_xy()
 {
     const int gx = gridDim.x;
-    if (!COEB_XCD_REMAP || !kRemap) return make_int2(blockIdx.x, blockIdx.y);
+    if (!kRemap) return make_int2(blockIdx.x, blockIdx.y);
     const int n = gx * gridDim.y, p = blockIdx.x + gx * blockIdx.y;
     const int q = n >> 3, r = n & 7, x = p & 7, k = p >> 3;
     const int lg = x * q + min(x, r) + k;
@@ -518,20 +507,10 @@ __device__ __forceinline__ int reflect_row(int r, int h)
 constexpr int kBlurQuad = 4 * kBlurCols;     // columns of one k_blur_rows wave item (14 tiles of 16)
 static_assert(kBlurQuad % 16 == 0, "a wave item must cover whole 16-column tiles");
 
-#ifndef COEB_BLUR_MINW
-#define COEB_BLUR_MINW 0         // experiment knob: a min-waves-per-SIMD launch bound for k_blur_rows (0: none)
-#endif
-#if COEB_BLUR_MINW
-#define COEB_BLUR_LB __launch_bounds__(kThreads, COEB_BLUR_MINW)
-#else
-#define COEB_BLUR_LB __launch_bounds__(kThreads)
-#endif
-__global__ COEB_BLUR_LB void k_blur_rows(const Plan* __restrict__ P, ExtractBufs b, BlurWork bw)
+__global__ __launch_bounds__(kThreads) void k_blur_rows(const Plan* __restrict__ P, ExtractBufs b, BlurWork bw)
 {
-#if COEB_BLUR_TILED
     // 8 output rows of the wave item, transposed through LDS into whole 128-B tile lines
     __shared__ __attribute__((aligned(16))) uint8_t s_tile[kWaves][8 * kBlurQuad];
-#endif
     const int2 bxy = block_xy();
     const int f = bxy.y;
     const int item = bw.item0 + bxy.x * kWaves + wave_id();
@@ -547,10 +526,8 @@ __global__ COEB_BLUR_LB void k_blur_rows(const Plan* __restrict__ P, ExtractBufs
     const int y0 = band * bw.brows, y1 = min(h, y0 + bw.brows);
     const int x = (quad * 4 + grp) * kBlurCols - 4 + gl * 4;
     const bool produce = gl >= 1 && gl <= 14 && x < w;
-#if COEB_BLUR_TILED
     const int xbase = quad * kBlurQuad;                            // first column of the item (16-aligned)
     uint8_t* tl = s_tile[wave_id()];
-#endif
     // Every lane loads one dword at column a and picks its 4 columns' bytes with the u16-pair
     // perms below: a = x inside the level; at the edges a is moved so that the REFLECT_101
     // columns reflect101(x + q) all fall in [a, a + 3] (w >= 5), so no lane takes a byte path.
@@ -624,7 +601,6 @@ __global__ COEB_BLUR_LB void k_blur_rows(const Plan* __restrict__ P, ExtractBufs
             a3 = __builtin_amdgcn_udot2(R01, W_r01_3, a3, false);
             a3 = __builtin_amdgcn_udot2(R23, W_r23_3, a3, false);
             const int y = y0 - 6 + i;                                  // uniform
-#if COEB_BLUR_TILED
             // row y into the item's LDS rows; after every 8th row (tile rows start at multiples of 8:
             // y0 is) the 8 rows leave as whole tile lines, 16 B per lane, consecutive lanes
             // consecutive bytes (a tile row's tiles are adjacent), 1.75 KiB in two instructions.
@@ -648,13 +624,6 @@ __global__ COEB_BLUR_LB void k_blur_rows(const Plan* __restrict__ P, ExtractBufs
                 }
                 wave_sync_lds();
             }
-#else
-            if (produce) {
-                const uint32_t p01 = __builtin_amdgcn_perm(a1, a0, 0x0c0c0602u);
-                const uint32_t p23 = __builtin_amdgcn_perm(a3, a2, 0x06020c0cu);
-                __builtin_amdgcn_raw_buffer_store_b32(p01 | p23, rd, x, __builtin_amdgcn_readfirstlane(y * dp), 0);
-            }
-#endif
         }
     }
 }
@@ -994,9 +963,6 @@ __device__ __forceinline__ void fast_prefetch(const FastCellGeom& G, FastRegs& R
     }
 }
 
-#ifndef COEB_FAST_DMA
-#define COEB_FAST_DMA 1        // 96-B slab rows staged by LDS-DMA (global_load_lds_dwordx4)
-#endif
 // Zero chunks of the LDS-DMA staging (the M columns of a 96-B slab row).
 __device__ __attribute__((aligned(64))) const uint8_t g_fast_zero[64] = {0};
 
@@ -1313,7 +1279,7 @@ __global__ __launch_bounds__(kThreads, COEB_FAST_MINWG) void k_fast(const Plan* 
     const int th_ini = area ? 30 : 20, th_min = area ? 10 : 7;   // ORBextractor.cc:775-784
     const CellDesc c = load_cell(cells, cidx);
     const FastCellGeom G = fast_geom(P, b, f, c);
-    const bool dma = COEB_FAST_DMA && RB == kFastRowBytesM && c.rh <= 48;     // wave-uniform
+    const bool dma = RB == kFastRowBytesM && c.rh <= 48;     // 96-B slab rows by LDS-DMA (wave-uniform)
     FastRegs R;
     if (dma) fast_dma(G, roi);
     else fast_prefetch(G, R);
@@ -1560,15 +1526,7 @@ __device__ __forceinline__ void child_rect(const int4 p, int q, int4* out, int* 
 __device__ long long g_oct_clk[4096 * 6];
 
 template <int NT>
-#ifndef COEB_OCT_MINW
-#define COEB_OCT_MINW 0         // experiment knob: a min-waves-per-SIMD launch bound for k_octree (0: none)
-#endif
-#if COEB_OCT_MINW
-#define COEB_OCT_LB __launch_bounds__(NT, COEB_OCT_MINW)
-#else
-#define COEB_OCT_LB __launch_bounds__(NT)
-#endif
-__global__ COEB_OCT_LB void k_octree(const Plan* __restrict__ P, ExtractBufs b, int level0, int oct_w,
+__global__ __launch_bounds__(NT) void k_octree(const Plan* __restrict__ P, ExtractBufs b, int level0, int oct_w,
                                                 int oct_kl)   // this launch's node slots / LDS key capacity
 {
     const long long oc_t0 = COEB_OCT_CLOCK ? (long long)clock64() : 0;
@@ -2150,11 +2108,8 @@ struct KeyPointOut { float x, y, size, angle, response; int octave, class_id; };
 // different banks, so the 64 lanes' scattered test samples rarely conflict (a 64-byte pitch put
 // every other row on the same 16 banks).
 constexpr int kBlRow = 72, kBlRows = 37;
-[[maybe_unused]] constexpr int kBlChunks = kBlRows * 4;              // 148 16-byte chunks (row-major blur)
 constexpr int kDescGroup = 2;                                        // patches staged per step
-#ifndef COEB_DESC_IC_BATCH
-#define COEB_DESC_IC_BATCH 32     // IC row-chunk loads in flight per lane (>= the tasks per lane: all at once)
-#endif
+constexpr int kDescIcBatch = 32;   // IC row-chunk loads in flight per lane (>= the tasks per lane: all at once)
 #ifndef COEB_DESC_KP
 // keypoints per wave: 8 is the fastest alone (0.537 vs 0.568 ms per 1025-frame launch for 16) and
 // in the steps of configs B, C and D (16: -6 %, -3 %, -1 %); 16 wins only config A's step
@@ -2209,20 +2164,9 @@ __device__ __forceinline__ void ic_row_load(const uint8_t* rp, uint4& c0, uint4&
     }
 }
 
-#ifndef COEB_DESC_IC_CHUNK
-#define COEB_DESC_IC_CHUNK 1
-#endif
 template <bool kVec0, int KP>
-// 24 waves per CU (launch bound 6 blocks: 80 VGPRs, 3 spilled) measured 0.253 vs 0.212 ms/step
-#ifndef COEB_DESC_MINW
-#define COEB_DESC_MINW 0         // experiment knob: a min-waves-per-SIMD launch bound for k_describe (0: none)
-#endif
-#if COEB_DESC_MINW
-#define COEB_DESC_LB __launch_bounds__(kThreads, COEB_DESC_MINW)
-#else
-#define COEB_DESC_LB __launch_bounds__(kThreads)
-#endif
-__global__ COEB_DESC_LB void k_describe(const Plan* __restrict__ P, ExtractBufs b)
+// (24 waves per CU, a launch bound of 6 blocks: 80 VGPRs, 3 spilled, measured 0.253 vs 0.212 ms/step)
+__global__ __launch_bounds__(kThreads) void k_describe(const Plan* __restrict__ P, ExtractBufs b)
 {
     constexpr int kLpk = 64 / KP;          // lanes per keypoint in phase A
     constexpr int kHl = kLpk / 2;          // lanes per half (rows -|v| / +|v|)
@@ -2271,7 +2215,6 @@ __global__ COEB_DESC_LB void k_describe(const Plan* __restrict__ P, ExtractBufs 
     const int64_t spitch = half ? (int64_t)g.pitch : -(int64_t)g.pitch;      // rows +|v| / -|v|
     const bool vec = kVec0 || l != 0;
     int aoff = 15;                             // m10 = A - aoff * S
-#if COEB_DESC_IC_CHUNK
     if (vec) {
         // lane (kq, j) takes tasks r = j + kLpk i of its keypoint, r = 3 row + chunk: image row
         // y + row - 15, 16-byte chunk `chunk` of the 48 bytes from x - 15 - a.  One load
@@ -2281,8 +2224,8 @@ __global__ COEB_DESC_LB void k_describe(const Plan* __restrict__ P, ExtractBufs 
         // is formed per byte from u = column - x, the column weights are u + 31 (in [1, 63], so
         // packed bytes never carry) and m01 takes v * (row sum) directly.
         constexpr int kTasks = (93 + kLpk - 1) / kLpk;
-        // loads in flight per batch (COEB_DESC_IC_BATCH: all kTasks, or fewer for fewer VGPRs)
-        constexpr int kBatch = COEB_DESC_IC_BATCH < kTasks ? COEB_DESC_IC_BATCH : kTasks;
+        // loads in flight per batch (kDescIcBatch: all kTasks, or fewer for fewer VGPRs)
+        constexpr int kBatch = kDescIcBatch < kTasks ? kDescIcBatch : kTasks;
         constexpr uint64_t kUmaxPk = 0x3689ABCDDEEEFFFFull;     // umax[av] in nibble av (kUmax)
         const int j = lane % kLpk;
         const uint8_t* base0 = img + (int64_t)(y - 15) * g.pitch + (x - 15 - a);
@@ -2323,9 +2266,7 @@ __global__ COEB_DESC_LB void k_describe(const Plan* __restrict__ P, ExtractBufs 
         }
         }
         aoff = 31;
-    } else
-#endif
-    {
+    } else {
 #pragma unroll
     for (int i0 = 0; i0 < kNr; i0 += kNb) {
         uint4 c[kNb][3];
@@ -2394,7 +2335,6 @@ __global__ COEB_DESC_LB void k_describe(const Plan* __restrict__ P, ExtractBufs 
     const uint8_t* blur_f = b.blur + (int64_t)f * P->blur_stride;
     static_assert(kDescGroup == 2, "staging below is written for 2 patches per step");
     uint4 qa0, qa1, qa2, qb0, qb1, qb2;
-#if COEB_BLUR_TILED
     // Patch = rows y-18 .. y+18 x the 64 bytes from (x-18) & ~15 of the tiled blurred level: 4 tile
     // columns x (5 or 6) tile rows of 8.  Load e (of 192, three per lane) = tile row e >> 5, tile
     // column (e >> 3) & 3, row e & 7 inside the tile: 8 consecutive lanes read one whole 128-B
@@ -2415,23 +2355,6 @@ __global__ COEB_DESC_LB void k_describe(const Plan* __restrict__ P, ExtractBufs 
         q1 = *reinterpret_cast<const uint4*>(o_ + min(tr0 + 2, tm_) * trs_);                    \
         q2 = *reinterpret_cast<const uint4*>(o_ + min(tr0 + 4, tm_) * trs_);                    \
     }
-#else
-    // per keypoint: blurred patch origin (16-aligned) relative to the frame's blur block
-    const int porg = (int)g.blur_off + (y - 18) * g.bpitch + ((x - 18) & ~15);
-    const int bpitch = g.bpitch;
-    const int e0 = lane, e1 = lane + 64, e2 = min(lane + 128, kBlChunks - 1);
-    const int eo0 = (e0 >> 2), eo1 = (e1 >> 2), eo2 = (e2 >> 2);
-    const int ec0 = 16 * (e0 & 3), ec1 = 16 * (e1 & 3), ec2 = 16 * (e2 & 3);
-#define COEB_LOAD_PATCH(t, q0, q1, q2)                                                          \
-    {                                                                                           \
-        const int tt_ = min((t), nk - 1);                                                       \
-        const uint8_t* o_ = blur_f + __builtin_amdgcn_readlane(porg, tt_ * kLpk);               \
-        const int bpt_ = __builtin_amdgcn_readlane(bpitch, tt_ * kLpk);                         \
-        q0 = *reinterpret_cast<const uint4*>(o_ + eo0 * bpt_ + ec0);                            \
-        q1 = *reinterpret_cast<const uint4*>(o_ + eo1 * bpt_ + ec1);                            \
-        q2 = *reinterpret_cast<const uint4*>(o_ + eo2 * bpt_ + ec2);                            \
-    }
-#endif
     COEB_LOAD_PATCH(0, qa0, qa1, qa2)
     COEB_LOAD_PATCH(1, qb0, qb1, qb2)
     for (int t0 = 0; t0 < nk; t0 += kDescGroup) {
@@ -2444,7 +2367,6 @@ __global__ COEB_DESC_LB void k_describe(const Plan* __restrict__ P, ExtractBufs 
                 d[1] = make_uint2(v.z, v.w);
             };
             uint8_t* pb = slab + kBlRow * kBlRows;
-#if COEB_BLUR_TILED
             const int dya = __builtin_amdgcn_readlane(dy, min(t0, nk - 1) * kLpk);
             const int dyb = __builtin_amdgcn_readlane(dy, min(t0 + 1, nk - 1) * kLpk);
             const int c = (lane >> 3) & 3, r = 8 * tr0 + (lane & 7);
@@ -2457,14 +2379,6 @@ __global__ COEB_DESC_LB void k_describe(const Plan* __restrict__ P, ExtractBufs 
             put_t(pb, r - dyb, qb0);
             put_t(pb, r + 16 - dyb, qb1);
             put_t(pb, r + 32 - dyb, qb2);
-#else
-            put(slab, lane >> 2, lane & 3, qa0);
-            put(slab, (lane + 64) >> 2, lane & 3, qa1);
-            if (lane + 128 < kBlChunks) put(slab, (lane + 128) >> 2, lane & 3, qa2);
-            put(pb, lane >> 2, lane & 3, qb0);
-            put(pb, (lane + 64) >> 2, lane & 3, qb1);
-            if (lane + 128 < kBlChunks) put(pb, (lane + 128) >> 2, lane & 3, qb2);
-#endif
         }
         wave_sync_lds();
         if (t0 + kDescGroup < nk) {
@@ -2539,7 +2453,7 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     // 32-row bands (round 4: 0.487 ms per 1025-frame launch; the strip-per-lane k_blur it replaced
     // took 0.759, and was deleted in round 6)
     const int brows = 32;
-    static_assert(!COEB_BLUR_TILED || brows % 8 == 0, "bands start on tile rows");
+    static_assert(brows % 8 == 0, "bands start on tile rows");
     bw.brows = brows;
     for (int l = 0; l < plan.L; l++) {
         const LevelGeom& g = plan.lv[l];

@@ -59,17 +59,13 @@ inline void lds_limit_max(const void* kern)
         (void)hipGetLastError();        // not sticky: the launch itself reports a size it cannot take
 }
 
-#ifndef COEB_BLUR_TILED
-#define COEB_BLUR_TILED 1
-#endif
-// Byte (x, y) of a blurred level with row pitch bpitch (a 64-byte multiple): COEB_BLUR_TILED
-// stores the level in 128-byte tiles of 16 columns x 8 rows, one tile per cache line, tiles
-// row-major (bpitch / 16 per tile row).  k_describe reads 37-row x 64-byte patches: row-major, every
-// patch row is its own line (37-74 line lookups per patch, half of each 128-B line unused); tiled,
-// a patch is 4 x 5-6 whole lines.
+// Byte (x, y) of a blurred level with row pitch bpitch (a 64-byte multiple): the level is stored
+// in 128-byte tiles of 16 columns x 8 rows, one tile per cache line, tiles row-major (bpitch / 16
+// per tile row).  k_describe reads 37-row x 64-byte patches: row-major, every patch row would be its
+// own line (37-74 line lookups per patch, half of each 128-B line unused); tiled, a patch is
+// 4 x 5-6 whole lines.
 __host__ __device__ inline int64_t blur_tile_off(int x, int y, int bpitch)
 {
-    if (!COEB_BLUR_TILED) return (int64_t)y * bpitch + x;
     return ((int64_t)(y >> 3) * (bpitch >> 4) + (x >> 4)) * 128 + (y & 7) * 16 + (x & 15);
 }
 
