@@ -508,7 +508,9 @@ constexpr int kSpPrPad = 1;      // row padding of the rolling patch (floats)
 // term lanes of a pass -- slots g, g + 1, g + 2 at the same 21 columns -- read 63 distinct banks.
 // The 4-row ring at 96 dwords per slot put slots g and g + 2 on the same banks: 2.74 vs 1.96
 // conflict cycles per LDS instruction, k_subpix 3.26-3.32 vs 3.19-3.23 ms per config-D step
-// (profiles/r06/s30).
+// (profiles/r06/s30).  Holding the term rows for half a window row at a time (8.8 KB of LDS, 4 waves
+// per SIMD instead of 3) ran 3.70-3.72 vs 3.19-3.22 ms: the extra term passes and syncs cost more than
+// the occupancy gives (s31).
 constexpr int kSpRows = 3;
 constexpr int kSpRS = 23 + kSpPrPad;                       // BW + padding
 constexpr int kSpSS = 85;
