@@ -1308,12 +1308,12 @@ def single_frame_timing(w, h, reps=50, warm=5):
         m = cf.ORBmatcher(0.9, True, ctx=ctx)
         Tc, Tl = synth.motion_pose(), np.eye(4, dtype=np.float32)
 
+        stereo_fn, dptr, bf = cf.lib().coeb_stereo_from_rgbd, depth.ctypes.data, C.c_float(synth.TUM_BF)
+
         def stereo(k):
             ur = np.empty(len(k), np.float32)
             dep = np.empty(len(k), np.float32)
-            ctx.check(cf.lib().coeb_stereo_from_rgbd(ctx.h, k.ctypes.data_as(C.c_void_p), len(k),
-                                                     depth.ctypes.data_as(C.c_void_p), w, h, w, C.c_float(synth.TUM_BF),
-                                                     ur.ctypes.data_as(C.c_void_p), dep.ctypes.data_as(C.c_void_p)))
+            ctx.check(stereo_fn(ctx.h, k.ctypes.data, len(k), dptr, w, h, w, bf, ur.ctypes.data, dep.ctypes.data))
             return ur, dep
 
         def snapshot(k, d, z):

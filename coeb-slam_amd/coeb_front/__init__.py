@@ -268,9 +268,13 @@ class Context:
         return t
 
     def max_keypoints(self, w, h):
-        r = lib().coeb_max_keypoints(self.h, w, h)
-        if r < 0:
-            self.check(r)
+        cache = self.__dict__.setdefault("_kcap", {})
+        r = cache.get((w, h))
+        if r is None:
+            r = lib().coeb_max_keypoints(self.h, w, h)
+            if r < 0:
+                self.check(r)
+            cache[(w, h)] = r
         return r
 
     # ---- single frame (host buffers) ----
@@ -279,18 +283,23 @@ class Context:
         if gray.size == 0:
             return np.zeros(0, KEYPOINT_DTYPE), None
         h, w = gray.shape
-        boxes = np.zeros((0, 4), np.float32) if boxes is None else np.ascontiguousarray(boxes, np.float32)
-        tm = np.zeros((0, 2), np.float32) if tm is None else np.ascontiguousarray(tm, np.float32)
-        blur = np.zeros(0, np.int32) if blur is None else np.ascontiguousarray(blur, np.int32)
+        boxes = None if boxes is None else np.ascontiguousarray(boxes, np.float32)
+        tm = None if tm is None else np.ascontiguousarray(tm, np.float32)
+        blur = None if blur is None else np.ascontiguousarray(blur, np.int32)
+        nb = 0 if boxes is None else len(boxes)
+        nt = 0 if tm is None else len(tm)
+        nf = 0 if blur is None else len(blur)
         cap = self.max_keypoints(w, h)
-        kps = np.zeros(cap, KEYPOINT_DTYPE)
-        desc = np.zeros((cap, 32), np.uint8)
+        # outputs written by the call (no zero fill) and returned as their first n rows (no copy):
+        # the per-call cost of the binding is part of the drop-in latency bench.py measures
+        kps = np.empty(cap, KEYPOINT_DTYPE)
+        desc = np.empty((cap, 32), np.uint8)
         n = C.c_int()
-        self.check(lib().coeb_extract(self.h, _p(gray), w, h, w, _p(boxes) if len(boxes) else None, len(boxes),
-                                      _p(tm) if len(tm) else None, len(tm), _p(blur) if len(blur) else None,
-                                      len(blur), _p(kps), _p(desc), cap, C.byref(n)))
+        self.check(lib().coeb_extract(self.h, _p(gray), w, h, w, _p(boxes) if nb else None, nb,
+                                      _p(tm) if nt else None, nt, _p(blur) if nf else None,
+                                      nf, _p(kps), _p(desc), cap, C.byref(n)))
         n = n.value
-        return kps[:n].copy(), (desc[:n].copy() if n else None)
+        return kps[:n], (desc[:n] if n else None)
 
     # ---- device-resident batch ----
     def extract_batch_device(self, d_gray_ptr, nframes, w, h, boxes=None, box_off=None, tm=None, tm_off=None,
@@ -634,12 +643,44 @@ class Frame:
         self.mTcw = np.eye(4, dtype=np.float32) if Tcw is None else np.ascontiguousarray(Tcw, np.float32)
         # map_points: dict(world_pos [N,3] f32, descriptor [N,32] u8, observations [N] i32, valid [N] u8)
         self.map_points = map_points
-        self.mvbOutlier = np.zeros(self.N, np.uint8) if outlier is None else np.ascontiguousarray(outlier, np.uint8)
+        self._outlier = None if outlier is None else np.ascontiguousarray(outlier, np.uint8)
         self.mvpMapPoints = np.full(self.N, -1, np.int32)
-        # Observations() of the MapPoint in mvpMapPoints[i] (-1 = NULL); read by the local-map search
-        self.mvpMapPointObs = np.full(self.N, -1, np.int32)
-        # GetWorldPos() of the MapPoint in mvpMapPoints[i]; read by Optimizer.PoseOptimization
-        self.mvMapPointPos = np.zeros((self.N, 3), np.float32)
+        self._mp_obs = None
+        self._mp_pos = None
+
+    # the fields below are allocated on first use (a per-frame cost of the Python binding the
+    # drop-in latency in bench.py includes; the C++ Tracking thread owns them already)
+    @property
+    def mvbOutlier(self):
+        if self._outlier is None:
+            self._outlier = np.zeros(self.N, np.uint8)
+        return self._outlier
+
+    @mvbOutlier.setter
+    def mvbOutlier(self, v):
+        self._outlier = v
+
+    @property
+    def mvpMapPointObs(self):
+        """Observations() of the MapPoint in mvpMapPoints[i] (-1 = NULL); read by the local-map search."""
+        if self._mp_obs is None:
+            self._mp_obs = np.full(self.N, -1, np.int32)
+        return self._mp_obs
+
+    @mvpMapPointObs.setter
+    def mvpMapPointObs(self, v):
+        self._mp_obs = v
+
+    @property
+    def mvMapPointPos(self):
+        """GetWorldPos() of the MapPoint in mvpMapPoints[i]; read by Optimizer.PoseOptimization."""
+        if self._mp_pos is None:
+            self._mp_pos = np.zeros((self.N, 3), np.float32)
+        return self._mp_pos
+
+    @mvMapPointPos.setter
+    def mvMapPointPos(self, v):
+        self._mp_pos = v
 
 
 class LocalMap:
@@ -720,22 +761,23 @@ class ORBmatcher:
 
     def _search_last_frame(self, CurrentFrame, LastFrame, th, bMono, camera):
         mp = LastFrame.map_points
-        n = LastFrame.N
-        lf_arrays = dict(has=np.ascontiguousarray(mp["valid"], np.uint8),
-                         out=np.ascontiguousarray(LastFrame.mvbOutlier, np.uint8),
-                         xw=np.ascontiguousarray(mp["world_pos"], np.float32),
-                         desc=np.ascontiguousarray(mp["descriptor"], np.uint8),
-                         nobs=np.ascontiguousarray(mp["observations"], np.int32),
-                         keys=np.ascontiguousarray(LastFrame.mvKeysUn))
-        lf = LastFrameC(n, *[C.c_void_p(lf_arrays[k].ctypes.data) for k in ("has", "out", "xw", "desc", "nobs", "keys")])
-        cf = CurFrameC(CurrentFrame.N, C.c_void_p(CurrentFrame.mvKeysUn.ctypes.data),
-                       C.c_void_p(CurrentFrame.mDescriptors.ctypes.data), C.c_void_p(CurrentFrame.mvuRight.ctypes.data))
-        out = np.full(max(CurrentFrame.N, 1), -1, np.int32)
+        has = np.ascontiguousarray(mp["valid"], np.uint8)
+        outl = np.ascontiguousarray(LastFrame.mvbOutlier, np.uint8)
+        xw = np.ascontiguousarray(mp["world_pos"], np.float32)
+        desc = np.ascontiguousarray(mp["descriptor"], np.uint8)
+        nobs = np.ascontiguousarray(mp["observations"], np.int32)
+        keys = np.ascontiguousarray(LastFrame.mvKeysUn)
+        lf = LastFrameC(LastFrame.N, has.ctypes.data, outl.ctypes.data, xw.ctypes.data, desc.ctypes.data,
+                        nobs.ctypes.data, keys.ctypes.data)
+        cf = CurFrameC(CurrentFrame.N, CurrentFrame.mvKeysUn.ctypes.data, CurrentFrame.mDescriptors.ctypes.data,
+                       CurrentFrame.mvuRight.ctypes.data)
+        # every entry of the result is written by the call (matched index or -1)
+        out = np.empty(max(CurrentFrame.N, 1), np.int32)
         nm = C.c_int()
         self.ctx.check(lib().coeb_match_lastframe(self.ctx.h, C.byref(camera), C.byref(cf), C.byref(lf),
                                                   _p(CurrentFrame.mTcw), _p(LastFrame.mTcw), th, int(bMono),
                                                   int(self.mbCheckOrientation), _p(out), C.byref(nm)))
-        CurrentFrame.mvpMapPoints = out[:CurrentFrame.N].copy()
+        CurrentFrame.mvpMapPoints = out[:CurrentFrame.N]
         return nm.value
 
 

@@ -1,0 +1,7 @@
+#!/bin/bash
+# round 6 session 32: Context.extract without zero-filled outputs / result copies -- GPU tests, smoke, A line
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out/s32
+bash tools/gpu_session.sh pytest smoke bench
+cp gpurun_out/pytest_gpu.log gpurun_out/smoke.log gpurun_out/bench.log gpurun_out/s32/
