@@ -1221,8 +1221,19 @@ def rank_main(ranks, args):
             line["parity_sample"] = parity_check([bp], cfg, [[1, 2, F // 2, F - 1]])
         if not args.no_extras and world == 1 and not args.dry_run:
             line["extras"] = extras_timing(bp.ctx, out, w, h)
-            line["extras"]["single_frame"] = single_frame_timing(w, h)
-            line["extras"]["single_frame_cpp"] = single_frame_cpp(w, h)
+            # the one-frame-at-a-time legs run their calling thread on the idlest CPU, as the CPU
+            # baseline's single-thread legs do: on the shared host a busy core adds tens of us of
+            # jitter to a 0.3 ms call sequence (the C++ child inherits the affinity)
+            sf_cpu = idle_cpus(sorted(os.sched_getaffinity(0)), k=1)[0][0]
+            mask = os.sched_getaffinity(0)
+            try:
+                os.sched_setaffinity(0, {sf_cpu})
+                line["extras"]["single_frame"] = single_frame_timing(w, h)
+                line["extras"]["single_frame_cpp"] = single_frame_cpp(w, h)
+            finally:
+                os.sched_setaffinity(0, mask)
+            for k in ("single_frame", "single_frame_cpp"):
+                line["extras"][k]["cpu"] = sf_cpu
             if not cfg.get("dyn") and not cfg.get("pose") and not chain:
                 line["extras"]["config5_tracking"] = config5_timing(bp, nmatched0)
                 line["extras"]["config3_dynamic_mask"] = config3_timing(bp, synth.make_frames(w, h, F, seed=1000),
