@@ -2539,6 +2539,8 @@ int launch_extract(const Plan& plan, const Plan* d_plan, const ExtractBufs& b, i
     // its keys in LDS instead of the global ping-pong buffers; large batches keep the plan's
     // capacity, which leaves more workgroups per CU.  (Level 0 as one 1024-thread workgroup and
     // the short upper levels as one-wave workgroups were both measured slower)
+    // One frame (the single-frame path) with 1024 / 512 threads per workgroup: 1024 adds 5 us to
+    // the frame's extract, 512 is within noise of 256 (r06/s38), so one size serves every batch.
     int oct_kl = plan.oct_kl, oct_lds = plan.oct_lds;
     if (F * plan.L <= 2 * 256) {
         int kl = oct_kl;
